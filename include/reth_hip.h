@@ -1,0 +1,203 @@
+/*
+ * reth_hip.h -- C ABI of libreth_hip.so, the MI355X (gfx950) hot path of Reth's Ape-X DQN
+ * rollout -> prioritized replay -> update loop.
+ *
+ * Conventions
+ *   - every call returns int: 0 (RTH_OK) or a negative RTH_ERR_*; rth_last_error() gives the
+ *     message of the last failure on the calling thread.
+ *   - pointers named *_dev are device (HBM) pointers; everything else is host memory.
+ *   - `stream` is a hipStream_t passed as void* (NULL = the legacy default stream); all work
+ *     is enqueued asynchronously on it, no call synchronises the device.
+ *   - handles own their device storage; calls on one handle must be serialised by the
+ *     caller (the reference's single-owner sampler process, server/sampler_loop.py:6-42).
+ *   - index arrays are int64 (the reference mixes int32 appends, fifo_policy.py:13, and
+ *     int64 updates; both widen losslessly).
+ *
+ * The reference is pure Python (numba/numpy/torch); each entry point names the Python
+ * interface it replaces (paths relative to the sosp2021/Reth checkout).  The Python
+ * binding (reth_amd/_lib.py, ctypes) re-exposes the reference's own signatures.
+ */
+#ifndef RETH_HIP_H
+#define RETH_HIP_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RTH_OK 0
+#define RTH_ERR_INVALID -1   /* bad argument (the reference's `assert`s) */
+#define RTH_ERR_HIP -2       /* a HIP runtime call failed */
+#define RTH_ERR_NOMEM -3     /* device allocation failed */
+
+/* element types of replay columns */
+#define RTH_U8 0
+#define RTH_I32 1
+#define RTH_I64 2
+#define RTH_F32 3
+#define RTH_F64 4
+#define RTH_MAX_COLS 8
+
+const char *rth_last_error(void);
+/* library build/ABI version (major*10000 + minor*100 + patch) */
+int rth_version(void);
+
+/* ------------------------------------------------------------------------------------
+ * In-order heap sum-tree, fp64, resident in HBM.
+ * Replaces reth_buffer/reth_buffer/utils/sumtree.py:82-113 (NumbaSumTree and the numba
+ * kernels _numba_maintain_node :5-21, _numba_maintain :24-31, _numba_find_index :34-58,
+ * _numba_update :61-67, _numba_sample :70-79).  Bit-exact with the sequential reference.
+ * ---------------------------------------------------------------------------------- */
+typedef struct rth_sumtree rth_sumtree;
+int rth_sumtree_create(int64_t capacity, int device, rth_sumtree **out); /* NumbaSumTree.__init__ :83-87 */
+int rth_sumtree_destroy(rth_sumtree *t);
+int rth_sumtree_clear(rth_sumtree *t, void *stream);                    /* NumbaSumTree.clear :98-101 */
+/* NumbaSumTree.update :103-104 -> _numba_update: val[idx]=w, maintain, in order */
+int rth_sumtree_update(rth_sumtree *t, const int64_t *idx_dev, const double *w_dev, int64_t n,
+                       void *stream);
+/* _numba_find_index :34-58, one target per element */
+int rth_sumtree_find(rth_sumtree *t, const double *targets_dev, int64_t n, int64_t *idx_out_dev,
+                     double *val_out_dev, void *stream);
+/* NumbaSumTree.sample :112-113 -> _numba_sample :70-79.  uniforms_dev (n = batch) replaces
+ * numba's internal np.random stream when non-NULL (the parity hook); when NULL the
+ * uniforms come from Philox4x32-10(seed, counter). */
+int rth_sumtree_sample(rth_sumtree *t, int64_t batch, const double *uniforms_dev, uint64_t seed,
+                       uint64_t counter, int64_t *idx_out_dev, double *val_out_dev, void *stream);
+/* out2_dev[0] = NumbaSumTree.sum() :106-107, out2_dev[1] = NumbaSumTree.min() :109-110 */
+int rth_sumtree_stats(rth_sumtree *t, double *out2_dev, void *stream);
+/* the three fp64 arrays of the reference layout (each [capacity], device) */
+int rth_sumtree_export(rth_sumtree *t, double *sum_dev, double *min_dev, double *val_dev, void *stream);
+int rth_sumtree_import(rth_sumtree *t, const double *sum_dev, const double *min_dev,
+                       const double *val_dev, void *stream);
+int64_t rth_sumtree_capacity(const rth_sumtree *t);
+
+/* ------------------------------------------------------------------------------------
+ * PER sampler on a sum-tree.  Replaces reth_buffer/reth_buffer/sampler/per_sampler.py:5-35.
+ * Schedules (alpha/beta, utils/schedule.py) stay on the host; the current values are args.
+ * ---------------------------------------------------------------------------------- */
+/* PERSampler._normalize_weights :16-17: out = (w + 1e-6) ** alpha  (float32) */
+int rth_per_normalize(const float *w_dev, int64_t n, float alpha, float *out_dev, void *stream);
+/* PERSampler.update :34-35: tree.update(idx, _normalize_weights(td_abs)) fused in one pass.
+ * td_abs_dev is float32 (td_dtype RTH_F32: normalised in f32 with (float)alpha, like numpy
+ * on an f4 array) or float64 (RTH_F64: normalised in f64). */
+int rth_per_update(rth_sumtree *t, const int64_t *idx_dev, const void *td_abs_dev, int32_t td_dtype,
+                   int64_t n, double alpha, void *stream);
+/* PERSampler.sample :24-28: (idx, (p / tree.min()) ** -beta) */
+int rth_per_sample(rth_sumtree *t, int64_t batch, double beta, const double *uniforms_dev,
+                   uint64_t seed, uint64_t counter, int64_t *idx_out_dev, double *isw_out_dev,
+                   void *stream);
+
+/* ------------------------------------------------------------------------------------
+ * Replay shard in HBM: FIFO slot allocation + column storage + PER tree.
+ * Replaces the reth_buffer service: append_loop (server/main_loop.py:21-61: deserialize,
+ * FIFOPolicy.get_indices, LMDB put, forward to sampler), sampler_loop
+ * (server/sampler_loop.py:6-42), Client.append / update_priorities (client/client.py:21-39)
+ * and the loaders' row fetch (client/torch_cuda_loader.py:20-66, numpy_loader.py:27-51).
+ * ---------------------------------------------------------------------------------- */
+typedef struct {
+  int64_t row_elems; /* elements per row (product of the per-row shape) */
+  int32_t in_dtype;  /* storage type == type appended (RTH_U8 ... RTH_F64) */
+  int32_t out_dtype; /* type produced on sample: == in_dtype, or RTH_F32 from RTH_U8 */
+} rth_col_desc;
+
+/* a column source for an append: rows[i] (or i when rows_dev == NULL) of base_dev, rows
+ * row_stride_bytes apart (0 = dense) */
+typedef struct {
+  const void *base_dev;
+  const int64_t *rows_dev;
+  int64_t row_stride_bytes;
+} rth_src;
+
+typedef struct rth_replay rth_replay;
+int rth_replay_create(int64_t capacity, int32_t n_cols, const rth_col_desc *cols, int device,
+                      uint64_t seed, rth_replay **out);
+int rth_replay_destroy(rth_replay *h);
+/* Client.append + append_loop + PERSampler.update: rows go to FIFO slots
+ * tail, tail+1, ... mod capacity (FIFOPolicy :11-18), priorities (td_abs + 1e-6)**alpha
+ * into the tree.  idx_out_dev (nullable) receives the slots. */
+int rth_replay_append(rth_replay *h, const rth_src *srcs, const void *td_abs_dev, int32_t td_dtype,
+                      int64_t n, double alpha, int64_t *idx_out_dev, void *stream);
+/* sampler_loop sample + loader gather: PER-sample `batch` rows (uniforms_dev nullable, see
+ * rth_sumtree_sample), write IS weights, and gather every column into out_cols_dev[c]
+ * ([batch, row] of out_dtype) -- TorchCudaLoader.sample's (data, indices, weights). */
+int rth_replay_sample(rth_replay *h, int64_t batch, double beta, const double *uniforms_dev,
+                      void *const *out_cols_dev, int64_t *idx_out_dev, double *isw_out_dev,
+                      void *stream);
+/* Client.update_priorities :37-39 -> PERSampler.update */
+int rth_replay_update_priorities(rth_replay *h, const int64_t *idx_dev, const void *td_abs_dev,
+                                 int32_t td_dtype, int64_t n, double alpha, void *stream);
+/* NumpyLoader row fetch (numpy_loader.py:381-396) for explicit indices */
+int rth_replay_gather(rth_replay *h, const int64_t *idx_dev, int64_t n, void *const *out_cols_dev,
+                      void *stream);
+/* host-side counters: rows stored, FIFO tail, sampler cnt (appended + re-prioritised,
+ * sampler_loop.py:36), sample calls issued */
+int rth_replay_info(const rth_replay *h, int64_t *size, int64_t *tail, int64_t *cnt,
+                    int64_t *sample_calls);
+rth_sumtree *rth_replay_tree(rth_replay *h);
+/* device pointer of column c's storage ([capacity, row] of in_dtype) */
+void *rth_replay_column(rth_replay *h, int32_t c);
+
+/* ------------------------------------------------------------------------------------
+ * Row copy / gather with optional uint8 -> float32 widening (the loaders' pinned copy +
+ * H2D, torch_cuda_loader.py:43-62, as one HBM->HBM kernel).  src/dst row index arrays are
+ * nullable (identity).  Strides in bytes.
+ * ---------------------------------------------------------------------------------- */
+int rth_copy_rows(void *dst_dev, int64_t dst_stride, const int64_t *dst_rows_dev, const void *src_dev,
+                  int64_t src_stride, const int64_t *src_rows_dev, int64_t n, int64_t row_elems,
+                  int32_t in_dtype, int32_t out_dtype, void *stream);
+
+/* ------------------------------------------------------------------------------------
+ * Actor side.
+ * ---------------------------------------------------------------------------------- */
+/* RandomExploration.act (reth/reth/utils/exploration.py:26-31) over N actors:
+ * u < eps[i] ? rand_action : argmax_a q[i, a] (first maximum, dqn_solver.py:126-131).
+ * u_dev / rand_action_dev nullable -> Philox(seed, counter). */
+int rth_eps_greedy(const float *q_dev, int64_t N, int64_t A, const double *eps_dev,
+                   const double *u_dev, const int64_t *rand_action_dev, uint64_t seed,
+                   uint64_t counter, int64_t *action_out_dev, void *stream);
+
+/* NStepAdder (reth/reth/utils/nstep_adder.py:5-28), one adder per actor, rows referencing
+ * frame handles.  mode 0 = numpy 1.19 promotion (reference pin), 1 = numpy 2 / NEP 50. */
+typedef struct rth_nstep rth_nstep;
+int rth_nstep_create(int64_t n_actors, int32_t n_step, double gamma, int32_t mode, int device,
+                     rth_nstep **out);
+int rth_nstep_destroy(rth_nstep *h);
+int rth_nstep_reset(rth_nstep *h, void *stream);
+/* push one transition per actor; emit_dev[i] = 1 when actor i's oldest row was popped, its
+ * fields in the *_out arrays (row i) */
+int rth_nstep_push(rth_nstep *h, const int64_t *s0_dev, const int64_t *a_dev, const float *r_dev,
+                   const int64_t *s1_dev, const float *done_dev, int32_t *emit_dev,
+                   int64_t *s0_out_dev, int64_t *a_out_dev, float *r_out_dev,
+                   int64_t *s1_out_dev, float *done_out_dev, void *stream);
+
+/* Synthetic Pong-shaped environment (no ALE on the box): uint8 (4,84,84) frame stacks kept
+ * in a per-actor ring of `ring` stacks.  Step t writes the next stack (shift + one fresh
+ * frame) into slot (2t) % ring and, on done, a reset stack (one fresh frame x4, FrameStack
+ * reset) into slot (2t+1) % ring.  reward in {-1,0,+1}, P(+-1) = p_reward/2 each;
+ * done ~ Bernoulli(p_done).  cur_slot_dev is updated in place; s0/s1 handles
+ * (actor*ring + slot) are written for the n-step adder.  Actions do not affect it. */
+int rth_synth_env_step(uint8_t *frames_dev, int64_t n_actors, int32_t ring, int64_t t,
+                       int64_t *cur_slot_dev, const int64_t *action_dev, uint64_t seed,
+                       float p_reward, float p_done, float *r_out_dev, float *done_out_dev,
+                       int64_t *s0_handle_dev, int64_t *s1_handle_dev, void *stream);
+/* initial reset of every actor into slot 1 (t = 0) */
+int rth_synth_env_reset(uint8_t *frames_dev, int64_t n_actors, int32_t ring, uint64_t seed,
+                        int64_t *cur_slot_dev, void *stream);
+
+/* ------------------------------------------------------------------------------------
+ * Learner: DQNSolver TD error + Huber (reth/reth/algorithm/dqn/dqn_solver.py:68-124).
+ * td = q_s0[a] - (r + (gamma_n * q_tgt(s1)[a*]) * (1 - done)),  a* = argmax q_online(s1)
+ * (double_q) or argmax q_tgt(s1); loss = mean(smooth_l1(td) * w); dq = dloss/dq_s0.
+ * Every output pointer is nullable.  isw_dev is the sampler's fp64 IS weight (cast to f32
+ * like ensure_tensor, :105-106), nullable = no weights.
+ * ---------------------------------------------------------------------------------- */
+int rth_td_huber(const float *q_s0_dev, const float *q_s1_online_dev, const float *q_s1_target_dev,
+                 const int64_t *a_dev, const float *r_dev, const float *done_dev,
+                 const double *isw_dev, int64_t B, int64_t A, float gamma_n, int32_t double_q,
+                 float *td_out_dev, float *td_abs_out_dev, float *loss_elem_dev,
+                 float *loss_out_dev, float *dq_out_dev, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

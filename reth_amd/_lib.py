@@ -1,0 +1,138 @@
+"""ctypes binding of libreth_hip.so (the C ABI declared in include/reth_hip.h).
+
+The library is built in-tree by ``__graft_entry__.build()`` (hipcc --offload-arch=gfx950).
+There is no fallback: if the shared object is missing or cannot be loaded, every entry
+point raises ``HipExtensionMissing`` -- the product never silently runs a CPU path.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libreth_hip.so")
+
+# element types (include/reth_hip.h)
+RTH_U8, RTH_I32, RTH_I64, RTH_F32, RTH_F64 = 0, 1, 2, 3, 4
+MAX_COLS = 8
+
+c_i32, c_i64, c_u64, c_f32, c_f64, c_vp = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64,
+                                          ctypes.c_float, ctypes.c_double, ctypes.c_void_p)
+
+
+class HipExtensionMissing(ImportError):
+    pass
+
+
+class RethHipError(RuntimeError):
+    pass
+
+
+class ColDesc(ctypes.Structure):
+    _fields_ = [("row_elems", c_i64), ("in_dtype", c_i32), ("out_dtype", c_i32)]
+
+
+class Src(ctypes.Structure):
+    _fields_ = [("base_dev", c_vp), ("rows_dev", c_vp), ("row_stride_bytes", c_i64)]
+
+
+# name -> (restype, argtypes); must match include/reth_hip.h exactly
+SIGNATURES = {
+    "rth_last_error": (ctypes.c_char_p, []),
+    "rth_version": (c_i32, []),
+    # sum-tree
+    "rth_sumtree_create": (c_i32, [c_i64, c_i32, ctypes.POINTER(c_vp)]),
+    "rth_sumtree_destroy": (c_i32, [c_vp]),
+    "rth_sumtree_clear": (c_i32, [c_vp, c_vp]),
+    "rth_sumtree_update": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "rth_sumtree_find": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
+    "rth_sumtree_sample": (c_i32, [c_vp, c_i64, c_vp, c_u64, c_u64, c_vp, c_vp, c_vp]),
+    "rth_sumtree_stats": (c_i32, [c_vp, c_vp, c_vp]),
+    "rth_sumtree_export": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "rth_sumtree_import": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "rth_sumtree_capacity": (c_i64, [c_vp]),
+    # PER
+    "rth_per_normalize": (c_i32, [c_vp, c_i64, c_f32, c_vp, c_vp]),
+    "rth_per_update": (c_i32, [c_vp, c_vp, c_vp, c_i32, c_i64, c_f64, c_vp]),
+    "rth_per_sample": (c_i32, [c_vp, c_i64, c_f64, c_vp, c_u64, c_u64, c_vp, c_vp, c_vp]),
+    # replay
+    "rth_replay_create": (c_i32, [c_i64, c_i32, ctypes.POINTER(ColDesc), c_i32, c_u64, ctypes.POINTER(c_vp)]),
+    "rth_replay_destroy": (c_i32, [c_vp]),
+    "rth_replay_append": (c_i32, [c_vp, ctypes.POINTER(Src), c_vp, c_i32, c_i64, c_f64, c_vp, c_vp]),
+    "rth_replay_sample": (c_i32, [c_vp, c_i64, c_f64, c_vp, ctypes.POINTER(c_vp), c_vp, c_vp, c_vp]),
+    "rth_replay_update_priorities": (c_i32, [c_vp, c_vp, c_vp, c_i32, c_i64, c_f64, c_vp]),
+    "rth_replay_gather": (c_i32, [c_vp, c_vp, c_i64, ctypes.POINTER(c_vp), c_vp]),
+    "rth_replay_info": (c_i32, [c_vp, ctypes.POINTER(c_i64), ctypes.POINTER(c_i64),
+                                ctypes.POINTER(c_i64), ctypes.POINTER(c_i64)]),
+    "rth_replay_tree": (c_vp, [c_vp]),
+    "rth_replay_column": (c_vp, [c_vp, c_i32]),
+    "rth_copy_rows": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i32, c_vp]),
+    # actors
+    "rth_eps_greedy": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_u64, c_u64, c_vp, c_vp]),
+    "rth_nstep_create": (c_i32, [c_i64, c_i32, c_f64, c_i32, c_i32, ctypes.POINTER(c_vp)]),
+    "rth_nstep_destroy": (c_i32, [c_vp]),
+    "rth_nstep_reset": (c_i32, [c_vp, c_vp]),
+    "rth_nstep_push": (c_i32, [c_vp] + [c_vp] * 11 + [c_vp]),
+    "rth_synth_env_step": (c_i32, [c_vp, c_i64, c_i32, c_i64, c_vp, c_vp, c_u64, c_f32, c_f32,
+                                   c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "rth_synth_env_reset": (c_i32, [c_vp, c_i64, c_i32, c_u64, c_vp, c_vp]),
+    # learner
+    "rth_td_huber": (c_i32, [c_vp] * 7 + [c_i64, c_i64, c_f32, c_i32] + [c_vp] * 5 + [c_vp]),
+}
+
+_lib = None
+_load_error = None
+
+
+def _load():
+    global _lib, _load_error
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        _load_error = f"{LIB_PATH} not built (run __graft_entry__.build())"
+        raise HipExtensionMissing(_load_error)
+    try:
+        lib = ctypes.CDLL(LIB_PATH)
+    except OSError as e:  # pragma: no cover
+        _load_error = str(e)
+        raise HipExtensionMissing(f"cannot load {LIB_PATH}: {e}") from e
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def lib():
+    """The loaded library (raises HipExtensionMissing -- never falls back)."""
+    return _load()
+
+
+def check(rc, what=""):
+    if rc != 0:
+        msg = _load().rth_last_error().decode(errors="replace")
+        raise RethHipError(f"{what or 'libreth_hip'} failed ({rc}): {msg}")
+
+
+def call(name, *args):
+    rc = getattr(_load(), name)(*args)
+    check(rc, name)
+    return rc
+
+
+def ptr(t):
+    """Device pointer of a torch tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_ptr(stream=None):
+    import torch
+
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream
+
+
+def require_device(t, what):
+    if t is not None and not t.is_cuda:
+        raise ValueError(f"{what} must be a device (HIP) tensor, got {t.device}")

@@ -1,0 +1,148 @@
+"""Vectorised Ape-X actors on one GPU.
+
+Reference actor loop: test/apex-dqn/worker.py:21-61 -- per actor process: epsilon-greedy act
+(reth/reth/utils/exploration.py:26-31 -> DQNSolver.act, dqn_solver.py:126-131), env.step,
+cast to f4/i8/f4/f4/f4, NStepAdder.push (reth/reth/utils/nstep_adder.py:11-28), a 64-row
+staging NumpyBuffer, then calc_loss (the actor's stale copy: target == online, because
+load_weights calls update_target, dqn_solver.py:133-137) and Client.append.
+
+Here all N actors of a GPU step together, entirely in HBM:
+  frames   uint8 [N, ring, 4, 84, 84]   per-actor ring of frame stacks (obs, next obs,
+                                         reset obs); rows reference stacks by handle
+                                         actor*ring + slot, never copy them until insert
+  step():  u8->f32 gather of the acting stacks -> Q-net (batch N) -> rth_eps_greedy ->
+           rth_synth_env_step -> rth_nstep_push (emits one row per actor once warm)
+  prioritise(): u8->f32 gather of the emitted rows' s0/s1 -> Q-net (batch 2N) ->
+           rth_td_huber (no grad) = calc_loss
+  append(): rth_replay_append copies the rows' stacks from the ring into FIFO slots and
+           inserts (|td| + 1e-6)^alpha into the tree.
+No host synchronisation anywhere in the loop.
+"""
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import call, ptr, stream_ptr
+from .solver import td_huber_forward
+
+OBS_SHAPE = (4, 84, 84)
+STACK_ELEMS = 4 * 84 * 84
+
+
+def apex_epsilons(n, offset=0, total=None):
+    """eps_i = 0.4 ** (1 + 7 i / (size - 1)) (test/apex-dqn/worker.py:26), float64"""
+    total = n if total is None else total
+    i = np.arange(offset, offset + n, dtype=np.float64)
+    if total <= 1:
+        return np.full(n, 0.4)
+    return 0.4 ** (1 + (i / (total - 1)) * 7)
+
+
+class VecActors:
+    def __init__(self, n_actors, num_actions, n_step=3, gamma=0.99, device=None, seed=0, eps=None,
+                 actor_offset=0, total_actors=None, p_reward=0.02, p_done=1.0 / 2000, nstep_mode=0):
+        self.N = int(n_actors)
+        self.A = int(num_actions)
+        self.n_step, self.gamma = int(n_step), float(gamma)
+        self.gamma_n = float(np.float32(gamma ** n_step))
+        self.device = torch.device(device if device is not None else "cuda")
+        self.seed = int(seed)
+        self.p_reward, self.p_done = float(p_reward), float(p_done)
+        ring = 4
+        while ring < 2 * (self.n_step + 2):  # live stacks span n_step + 2 env steps, 2 per step
+            ring *= 2
+        self.ring = ring
+        dev = self.device
+        N = self.N
+        self.frames = torch.empty((N * ring, *OBS_SHAPE), dtype=torch.uint8, device=dev)
+        self.cur_slot = torch.empty(N, dtype=torch.int64, device=dev)
+        e = apex_epsilons(N, actor_offset, total_actors) if eps is None else np.broadcast_to(np.asarray(eps, np.float64), (N,))
+        self.eps = torch.as_tensor(np.ascontiguousarray(e), dtype=torch.float64, device=dev)
+        self.obs = torch.empty((N, *OBS_SHAPE), dtype=torch.float32, device=dev)
+        self.rows_f32 = torch.empty((2 * N, *OBS_SHAPE), dtype=torch.float32, device=dev)
+        z = lambda dt: torch.zeros(N, dtype=dt, device=dev)
+        self.action, self.s0_h, self.s1_h = z(torch.int64), z(torch.int64), z(torch.int64)
+        self.reward, self.done = z(torch.float32), z(torch.float32)
+        self.emit = z(torch.int32)
+        self.row_s0, self.row_a, self.row_s1 = z(torch.int64), z(torch.int64), z(torch.int64)
+        self.row_r, self.row_done = z(torch.float32), z(torch.float32)
+        self.row_handles = torch.empty(2 * N, dtype=torch.int64, device=dev)
+        h = _lib.c_vp()
+        call("rth_nstep_create", N, self.n_step, self.gamma, int(nstep_mode), dev.index, _lib.ctypes.byref(h))
+        self._nstep = h.value
+        self.t = 0           # env steps taken (per actor)
+        self.pushes = 0
+        call("rth_synth_env_reset", ptr(self.frames), N, ring, self.seed, ptr(self.cur_slot), stream_ptr())
+
+    def __del__(self):
+        if getattr(self, "_nstep", None):
+            try:
+                _lib.lib().rth_nstep_destroy(self._nstep)
+            except Exception:
+                pass
+            self._nstep = None
+
+    @property
+    def warm(self):
+        """every actor emits one n-step row per push once its deque is full"""
+        return self.pushes > self.n_step
+
+    def gather_f32(self, handles, out):
+        call("rth_copy_rows", ptr(out), 0, None, ptr(self.frames), 0, ptr(handles), handles.numel(), STACK_ELEMS,
+             _lib.RTH_U8, _lib.RTH_F32, stream_ptr())
+        return out
+
+    def current_obs_handles(self):
+        if not hasattr(self, "_base"):
+            self._base = torch.arange(self.N, device=self.device, dtype=torch.int64) * self.ring
+            self._cur_h = torch.empty_like(self._base)
+        return torch.add(self.cur_slot, self._base, out=self._cur_h)
+
+    @torch.no_grad()
+    def step(self, q_net):
+        """one environment step for every actor; returns True when rows were emitted"""
+        s = stream_ptr()
+        self.t += 1
+        # acting batch: current stacks -> f32 (Worker.step -> exploration.act -> solver.act)
+        self.gather_f32(self.current_obs_handles(), self.obs)
+        q = q_net(self.obs)
+        if q.dtype != torch.float32 or not q.is_contiguous():
+            q = q.float().contiguous()
+        call("rth_eps_greedy", ptr(q), self.N, self.A, ptr(self.eps), None, None, self.seed, self.t, ptr(self.action), s)
+        call("rth_synth_env_step", ptr(self.frames), self.N, self.ring, self.t, ptr(self.cur_slot), ptr(self.action),
+             self.seed, self.p_reward, self.p_done, ptr(self.reward), ptr(self.done), ptr(self.s0_h), ptr(self.s1_h), s)
+        call("rth_nstep_push", self._nstep, ptr(self.s0_h), ptr(self.action), ptr(self.reward), ptr(self.s1_h),
+             ptr(self.done), ptr(self.emit), ptr(self.row_s0), ptr(self.row_a), ptr(self.row_r), ptr(self.row_s1),
+             ptr(self.row_done), s)
+        self.pushes += 1
+        return self.warm
+
+    @torch.no_grad()
+    def prioritise(self, q_net):
+        """calc_loss on the emitted rows with the actor's network (target == online)"""
+        torch.cat([self.row_s0, self.row_s1], out=self.row_handles)
+        self.gather_f32(self.row_handles, self.rows_f32)
+        q = q_net(self.rows_f32).float().contiguous()
+        q0, q1 = q[: self.N], q[self.N:]
+        _, td_abs, _ = td_huber_forward(q0, q1, q1, self.row_a, self.row_r, self.row_done, None, self.gamma_n,
+                                        True, want_dq=False)
+        return td_abs
+
+    def append(self, replay, td_abs):
+        """Client.append of the emitted rows (stacks copied from the ring into FIFO slots)"""
+        fr = self.frames
+        replay.append([fr, self.row_a, self.row_r, fr, self.row_done], td_abs,
+                      src_rows=[self.row_s0, None, None, self.row_s1, None])
+
+    def rows(self):
+        """emitted rows as (s0 u8, a, r, s1 u8, done) device tensors (tests / inspection)"""
+        return (self.frames[self.row_s0], self.row_a.clone(), self.row_r.clone(), self.frames[self.row_s1],
+                self.row_done.clone())
+
+
+def apex_columns():
+    """replay columns of the apex-dqn rows [s0, a, r, s1, done] (worker.py:47-51): frames are
+    stored uint8 and sampled as float32 (exact), the rest as the reference casts them"""
+    from .replay import Column
+    return [Column(OBS_SHAPE, torch.uint8, torch.float32), Column((), torch.int64), Column((), torch.float32),
+            Column(OBS_SHAPE, torch.uint8, torch.float32), Column((), torch.float32)]

@@ -1,0 +1,249 @@
+// Actor-side kernels: batched epsilon-greedy, per-actor n-step adders, synthetic
+// Pong-shaped environment.
+//
+// Reference: reth/reth/utils/exploration.py:26-31 (RandomExploration.act),
+// reth/reth/algorithm/dqn/dqn_solver.py:126-131 (act = argmax Q),
+// reth/reth/utils/nstep_adder.py:5-28 (NStepAdder), test/apex-dqn/worker.py:21-61.
+#include "common.hpp"
+
+namespace rth {
+
+// ------------------------------------------------------------------ epsilon-greedy
+// One lane per actor: A <= 18 for Atari, so the row argmax is a short in-register loop and
+// the launch is one wave per 64 actors.
+__global__ void k_eps_greedy(const float *__restrict__ q, int64_t N, int A, const double *__restrict__ eps,
+                             const double *__restrict__ u_in, const int64_t *__restrict__ ra_in, uint64_t seed,
+                             uint64_t counter, int64_t *__restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  const double u = u_in ? u_in[i] : philox_uniform(seed, counter, (uint32_t)i, STREAM_EXPLORE);
+  if (u < eps[i]) {
+    int64_t ra;
+    if (ra_in) {
+      ra = ra_in[i];
+    } else {
+      uint32_t c[4] = {(uint32_t)i, (uint32_t)counter, (uint32_t)(counter >> 32), STREAM_RANDACT};
+      philox4x32(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+      ra = (int64_t)(((uint64_t)c[0] * (uint64_t)A) >> 32);  // uniform in [0, A)
+    }
+    out[i] = ra;
+  } else {
+    out[i] = argmax_first(q + i * A, A);
+  }
+}
+
+// ------------------------------------------------------------------ n-step adder
+// Per actor: a deque of up to n pending rows, position 0 = newest (appendleft), SoA in HBM.
+struct NStepState {
+  int32_t *count;
+  int64_t *s0, *a, *s1;
+  float *r, *done;
+};
+
+__global__ void k_nstep_push(NStepState st, int64_t N, int n, double gamma, int mode,
+                             const int64_t *__restrict__ s0, const int64_t *__restrict__ a,
+                             const float *__restrict__ r, const int64_t *__restrict__ s1,
+                             const float *__restrict__ done, int32_t *__restrict__ emit,
+                             int64_t *__restrict__ s0_out, int64_t *__restrict__ a_out,
+                             float *__restrict__ r_out, int64_t *__restrict__ s1_out,
+                             float *__restrict__ done_out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  const int64_t base = i * n;
+  int count = st.count[i];
+  int emitted = 0;
+  if (count == n) {  // deque full: pop the oldest (nstep_adder.py:13-14)
+    const int64_t k = base + count - 1;
+    s0_out[i] = st.s0[k];
+    a_out[i] = st.a[k];
+    r_out[i] = st.r[k];
+    s1_out[i] = st.s1[k];
+    done_out[i] = st.done[k];
+    --count;
+    emitted = 1;
+  }
+  emit[i] = emitted;
+  const float rn = r[i];
+  const int64_t s1n = s1[i];
+  double t_gamma = gamma;
+  for (int k = 0; k < count; ++k) {  // newest -> oldest (nstep_adder.py:16-25)
+    const int64_t p = base + k;
+    if (st.done[p] != 0.0f) break;
+    if (mode == 0)  // numpy 1.19: f64 product, += casts back to the f32 row
+      st.r[p] = (float)__dadd_rn((double)st.r[p], __dmul_rn(t_gamma, (double)rn));
+    else            // numpy 2 / NEP 50: the python float is weak, product stays f32
+      st.r[p] = __fadd_rn(st.r[p], __fmul_rn((float)t_gamma, rn));
+    t_gamma = __dmul_rn(t_gamma, gamma);
+    st.s1[p] = s1n;
+  }
+  for (int k = count; k > 0; --k) {  // appendleft
+    const int64_t p = base + k;
+    st.s0[p] = st.s0[p - 1];
+    st.a[p] = st.a[p - 1];
+    st.r[p] = st.r[p - 1];
+    st.s1[p] = st.s1[p - 1];
+    st.done[p] = st.done[p - 1];
+  }
+  st.s0[base] = s0[i];
+  st.a[base] = a[i];
+  st.r[base] = rn;
+  st.s1[base] = s1n;
+  st.done[base] = done[i];
+  st.count[i] = count + 1;
+}
+
+// ------------------------------------------------------------------ synthetic env
+constexpr int kFrameBytes = 84 * 84;          // 7,056
+constexpr int kFrameVec = kFrameBytes / 16;   // 441 x 16 B
+constexpr int kStackVec = 4 * kFrameVec;      // 1,764 x 16 B = 28,224 B
+constexpr int kEnvThreads = 256;
+
+__device__ __forceinline__ uint4 env_bytes(uint64_t seed, int64_t actor, int64_t t, int kind, int chunk) {
+  uint32_t c[4] = {(uint32_t)chunk | ((uint32_t)kind << 16), (uint32_t)actor, (uint32_t)t,
+                   STREAM_ENV | ((uint32_t)(t >> 32) << 8)};
+  philox4x32(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  return make_uint4(c[0], c[1], c[2], c[3]);
+}
+
+__global__ __launch_bounds__(kEnvThreads) void k_env_step(uint8_t *frames, int ring, int64_t t,
+                                                          int64_t *cur_slot, uint64_t seed, float p_reward,
+                                                          float p_done, float *r_out, float *done_out,
+                                                          int64_t *s0_h, int64_t *s1_h) {
+  const int64_t i = blockIdx.x;
+  const int64_t stack_bytes = 4 * kFrameBytes;
+  // reward / done: one Philox block per (actor, t), identical in every lane
+  const uint4 rd = env_bytes(seed, i, t, 2, 0);
+  const double ur = (double)rd.x * (1.0 / 4294967296.0), ud = (double)rd.y * (1.0 / 4294967296.0);
+  const float reward = ur < 0.5 * p_reward ? -1.0f : (ur < p_reward ? 1.0f : 0.0f);
+  const bool done = ud < (double)p_done;
+  const int64_t cur = cur_slot[i];
+  const int64_t nxt = (2 * t) % ring, rst = (2 * t + 1) % ring;
+  const uint4 *src = reinterpret_cast<const uint4 *>(frames + (i * ring + cur) * stack_bytes);
+  uint4 *dn = reinterpret_cast<uint4 *>(frames + (i * ring + nxt) * stack_bytes);
+  uint4 *dr = reinterpret_cast<uint4 *>(frames + (i * ring + rst) * stack_bytes);
+  for (int v = threadIdx.x; v < kStackVec; v += kEnvThreads) {
+    const int f = v / kFrameVec, c = v - f * kFrameVec;
+    dn[v] = (f < 3) ? src[v + kFrameVec] : env_bytes(seed, i, t, 0, c);  // FrameStack shift
+    if (done) dr[v] = env_bytes(seed, i, t, 1, c);                        // reset: one frame x4
+  }
+  __syncthreads();  // every lane has read cur_slot[i] before lane 0 rewrites it
+  if (threadIdx.x == 0) {
+    r_out[i] = reward;
+    done_out[i] = done ? 1.0f : 0.0f;
+    s0_h[i] = i * ring + cur;
+    s1_h[i] = i * ring + nxt;
+    cur_slot[i] = done ? rst : nxt;
+  }
+}
+
+__global__ __launch_bounds__(kEnvThreads) void k_env_reset(uint8_t *frames, int ring, uint64_t seed,
+                                                           int64_t *cur_slot) {
+  const int64_t i = blockIdx.x;
+  uint4 *dr = reinterpret_cast<uint4 *>(frames + (i * ring + 1) * (int64_t)(4 * kFrameBytes));
+  for (int v = threadIdx.x; v < kStackVec; v += kEnvThreads) dr[v] = env_bytes(seed, i, 0, 1, v % kFrameVec);
+  if (threadIdx.x == 0) cur_slot[i] = 1;
+}
+
+}  // namespace rth
+
+using namespace rth;
+
+struct rth_nstep {
+  int64_t N;
+  int32_t n;
+  double gamma;
+  int32_t mode;
+  int device;
+  void *mem;
+  NStepState st;
+};
+
+extern "C" {
+
+int rth_eps_greedy(const float *q, int64_t N, int64_t A, const double *eps, const double *u,
+                   const int64_t *ra, uint64_t seed, uint64_t counter, int64_t *out, void *stream) {
+  RTH_REQUIRE(N >= 0 && A >= 1 && A < (1 << 20), "rth_eps_greedy: bad shape");
+  if (N == 0) return RTH_OK;
+  RTH_REQUIRE(q && eps && out, "rth_eps_greedy: NULL buffer");
+  const int bs = 256;
+  hipLaunchKernelGGL(k_eps_greedy, dim3((unsigned)((N + bs - 1) / bs)), dim3(bs), 0, as_stream(stream), q, N,
+                     (int)A, eps, u, ra, seed, counter, out);
+  RTH_LAUNCHED();
+  return RTH_OK;
+}
+
+int rth_nstep_create(int64_t N, int32_t n, double gamma, int32_t mode, int device, rth_nstep **out) {
+  RTH_REQUIRE(out && N >= 1 && n >= 1 && n <= 64 && (mode == 0 || mode == 1), "rth_nstep_create: bad arguments");
+  RTH_HIP(hipSetDevice(device));
+  const size_t slots = (size_t)N * n;
+  const size_t bytes = N * sizeof(int32_t) + slots * (3 * sizeof(int64_t) + 2 * sizeof(float)) + 64;
+  void *mem = nullptr;
+  if (hipMalloc(&mem, bytes) != hipSuccess) {
+    set_error("rth_nstep_create: hipMalloc(%zu) failed", bytes);
+    return RTH_ERR_NOMEM;
+  }
+  RTH_HIP(hipMemset(mem, 0, bytes));
+  auto *h = new rth_nstep{N, n, gamma, mode, device, mem, {}};
+  uint8_t *p = (uint8_t *)mem;
+  h->st.s0 = (int64_t *)p;
+  p += slots * 8;
+  h->st.a = (int64_t *)p;
+  p += slots * 8;
+  h->st.s1 = (int64_t *)p;
+  p += slots * 8;
+  h->st.r = (float *)p;
+  p += slots * 4;
+  h->st.done = (float *)p;
+  p += slots * 4;
+  h->st.count = (int32_t *)p;
+  *out = h;
+  return RTH_OK;
+}
+
+int rth_nstep_destroy(rth_nstep *h) {
+  if (!h) return RTH_OK;
+  (void)hipSetDevice(h->device);
+  (void)hipFree(h->mem);
+  delete h;
+  return RTH_OK;
+}
+
+int rth_nstep_reset(rth_nstep *h, void *stream) {
+  RTH_REQUIRE(h, "rth_nstep_reset: NULL handle");
+  RTH_HIP(hipMemsetAsync(h->st.count, 0, h->N * sizeof(int32_t), as_stream(stream)));
+  return RTH_OK;
+}
+
+int rth_nstep_push(rth_nstep *h, const int64_t *s0, const int64_t *a, const float *r, const int64_t *s1,
+                   const float *done, int32_t *emit, int64_t *s0_out, int64_t *a_out, float *r_out, int64_t *s1_out,
+                   float *done_out, void *stream) {
+  RTH_REQUIRE(h && s0 && a && r && s1 && done && emit && s0_out && a_out && r_out && s1_out && done_out,
+              "rth_nstep_push: NULL argument");
+  const int bs = 256;
+  hipLaunchKernelGGL(k_nstep_push, dim3((unsigned)((h->N + bs - 1) / bs)), dim3(bs), 0, as_stream(stream), h->st,
+                     h->N, h->n, h->gamma, h->mode, s0, a, r, s1, done, emit, s0_out, a_out, r_out, s1_out,
+                     done_out);
+  RTH_LAUNCHED();
+  return RTH_OK;
+}
+
+int rth_synth_env_step(uint8_t *frames, int64_t N, int32_t ring, int64_t t, int64_t *cur_slot,
+                       const int64_t * /*action: the synthetic dynamics ignore it*/, uint64_t seed, float p_reward,
+                       float p_done, float *r_out, float *done_out, int64_t *s0_h, int64_t *s1_h, void *stream) {
+  RTH_REQUIRE(frames && cur_slot && r_out && done_out && s0_h && s1_h, "rth_synth_env_step: NULL argument");
+  RTH_REQUIRE(N >= 1 && N < (int64_t(1) << 31) && ring >= 4 && t >= 1, "rth_synth_env_step: bad shape");
+  hipLaunchKernelGGL(k_env_step, dim3((unsigned)N), dim3(kEnvThreads), 0, as_stream(stream), frames, ring, t,
+                     cur_slot, seed, p_reward, p_done, r_out, done_out, s0_h, s1_h);
+  RTH_LAUNCHED();
+  return RTH_OK;
+}
+
+int rth_synth_env_reset(uint8_t *frames, int64_t N, int32_t ring, uint64_t seed, int64_t *cur_slot, void *stream) {
+  RTH_REQUIRE(frames && cur_slot && N >= 1 && ring >= 4, "rth_synth_env_reset: bad arguments");
+  hipLaunchKernelGGL(k_env_reset, dim3((unsigned)N), dim3(kEnvThreads), 0, as_stream(stream), frames, ring, seed,
+                     cur_slot);
+  RTH_LAUNCHED();
+  return RTH_OK;
+}
+
+}  // extern "C"

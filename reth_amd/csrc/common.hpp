@@ -1,0 +1,114 @@
+// Shared helpers for libreth_hip.so (gfx950 / CDNA4).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "../../include/reth_hip.h"
+
+namespace rth {
+
+void set_error(const char *fmt, ...);
+
+#define RTH_REQUIRE(cond, ...)          \
+  do {                                  \
+    if (!(cond)) {                      \
+      ::rth::set_error(__VA_ARGS__);    \
+      return RTH_ERR_INVALID;           \
+    }                                   \
+  } while (0)
+
+#define RTH_HIP(call)                                                                   \
+  do {                                                                                  \
+    hipError_t e_ = (call);                                                             \
+    if (e_ != hipSuccess) {                                                             \
+      ::rth::set_error("%s failed: %s (%s:%d)", #call, hipGetErrorString(e_), __FILE__, \
+                       __LINE__);                                                       \
+      return RTH_ERR_HIP;                                                               \
+    }                                                                                   \
+  } while (0)
+
+// check a kernel launch (no sync)
+#define RTH_LAUNCHED() RTH_HIP(hipGetLastError())
+
+inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline int dtype_size(int32_t t) {
+  switch (t) {
+    case RTH_U8: return 1;
+    case RTH_I32: return 4;
+    case RTH_I64: return 8;
+    case RTH_F32: return 4;
+    case RTH_F64: return 8;
+    default: return 0;
+  }
+}
+
+// ---------------------------------------------------------------- Philox4x32-10
+// Salmon et al., "Parallel random numbers: as easy as 1, 2, 3" (SC'11).  Counter-based, so
+// every lane derives its own stream from (seed, counter, lane, stream id) with no state.
+// Restated bit-for-bit in oracle/reth_oracle.c (orc_philox4x32) for the parity tests.
+constexpr uint32_t STREAM_SAMPLE = 1u, STREAM_EXPLORE = 2u, STREAM_RANDACT = 3u, STREAM_ENV = 4u;
+
+__host__ __device__ inline void philox4x32(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int rnd = 0; rnd < 10; ++rnd) {
+    if (rnd) {
+      k0 += 0x9E3779B9u;
+      k1 += 0xBB67AE85u;
+    }
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0;
+    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
+    c[0] = n0;
+    c[1] = (uint32_t)p1;
+    c[2] = n2;
+    c[3] = (uint32_t)p0;
+  }
+}
+
+// u in [0, 1) with 53 random bits; same mapping as orc_philox_uniform
+__host__ __device__ inline double philox_uniform(uint64_t seed, uint64_t counter, uint32_t lane,
+                                                 uint32_t stream) {
+  uint32_t c[4] = {lane, (uint32_t)counter, (uint32_t)(counter >> 32), stream};
+  philox4x32(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  const uint64_t bits = ((uint64_t)c[0] | ((uint64_t)c[1] << 32)) >> 11;
+  return (double)bits * (1.0 / 9007199254740992.0);
+}
+
+// first-maximum argmax with torch semantics (a NaN is the maximum; the first NaN wins)
+__device__ inline int argmax_first(const float *q, int A) {
+  int best = 0;
+  float bv = q[0];
+  for (int j = 1; j < A; ++j) {
+    const float v = q[j];
+    if (bv != bv) break;
+    if (v != v || v > bv) {
+      bv = v;
+      best = j;
+    }
+  }
+  return best;
+}
+
+// PERSampler._normalize_weights (per_sampler.py:16-17): (w + 1e-6) ** alpha in float32,
+// correctly rounded; numpy's `** 0.5` is sqrt (fast_scalar_power), also correctly rounded.
+__device__ inline float per_normalize(float w, float alpha) {
+  const float x = __fadd_rn(w, 1e-6f);
+  if (alpha == 0.5f) return __fsqrt_rn(x);
+  if (alpha == 1.0f) return x;
+  return (float)pow((double)x, (double)alpha);
+}
+
+// the same in float64 (numpy float64 arrays: `** 0.5` is sqrt, other exponents pow)
+__device__ inline double per_normalize64(double w, double alpha) {
+  const double x = __dadd_rn(w, 1e-6);
+  if (alpha == 0.5) return __dsqrt_rn(x);
+  if (alpha == 1.0) return x;
+  return pow(x, alpha);
+}
+
+}  // namespace rth

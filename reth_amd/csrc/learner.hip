@@ -1,0 +1,95 @@
+// Learner-side kernel: DQN TD error + Huber loss + its gradient w.r.t. Q(s0), fused.
+//
+// Reference: reth/reth/algorithm/dqn/dqn_solver.py:68-124.  The Q-network itself stays in
+// PyTorch-ROCm (MIOpen/hipBLASLt MFMA GEMMs, fp32); this kernel replaces the chain of
+// one_hot / sum / argmax / mul / sub / smooth_l1 / mul / mean / |td|.cpu() ops and their
+// autograd backward with one launch, keeps |td| on the device for the priority update, and
+// hands autograd d(loss)/d(Q(s0)) directly.
+#include <cstdarg>
+#include <mutex>
+
+#include "common.hpp"
+
+namespace rth {
+
+static thread_local std::string g_last_error;
+
+void set_error(const char *fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+}
+
+constexpr int kTdThreads = 512;
+
+// One workgroup: B = 512 rows is one row per lane; larger B loops.  The loss mean is a
+// fixed-order LDS tree (deterministic run to run).
+__global__ __launch_bounds__(kTdThreads) void k_td_huber(
+    const float *__restrict__ q0, const float *__restrict__ q1o, const float *__restrict__ q1t,
+    const int64_t *__restrict__ act, const float *__restrict__ rew, const float *__restrict__ done,
+    const double *__restrict__ isw, int64_t B, int A, float gamma_n, int double_q, float *__restrict__ td_out,
+    float *__restrict__ td_abs_out, float *__restrict__ loss_elem, float *__restrict__ loss_out,
+    float *__restrict__ dq) {
+  __shared__ float part[kTdThreads];
+  const float invB = 1.0f / (float)B;
+  float acc = 0.0f;
+  for (int64_t b = threadIdx.x; b < B; b += kTdThreads) {
+    const int64_t a = act[b];
+    const float q = q0[b * A + a];  // sum(q * one_hot(a)) (:79-81)
+    const int astar = argmax_first((double_q ? q1o : q1t) + b * A, A);  // (:83-94)
+    const float nqb = q1t[b * A + astar];
+    // expected = r + (gamma**n * next_q_best) * (1 - done)  (:96), f32, no contraction
+    float t = __fmul_rn(gamma_n, nqb);
+    t = __fmul_rn(t, __fsub_rn(1.0f, done[b]));
+    const float y = __fadd_rn(rew[b], t);
+    const float td = __fsub_rn(q, y);  // (:97)
+    if (td_out) td_out[b] = td;
+    const float z = fabsf(td);
+    if (td_abs_out) td_abs_out[b] = z;  // td_error.detach().cpu().abs() (:109), kept on device
+    // smooth_l1(beta=1) (:112) * w (:113-114)
+    float l = z < 1.0f ? __fmul_rn(__fmul_rn(0.5f, z), z) : __fsub_rn(z, 0.5f);
+    const float w = isw ? (float)isw[b] : 1.0f;
+    if (isw) l = __fmul_rn(l, w);
+    if (loss_elem) loss_elem[b] = l;
+    acc = __fadd_rn(acc, l);
+    if (dq) {  // autograd: mean -> mul(w) -> smooth_l1' -> one_hot scatter
+      const float g = __fmul_rn(invB, w);
+      const float d = td <= -1.0f ? -g : (td >= 1.0f ? g : __fmul_rn(td, g));
+      for (int j = 0; j < A; ++j) dq[b * A + j] = __fmul_rn(d, j == a ? 1.0f : 0.0f);
+    }
+  }
+  part[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = kTdThreads / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) part[threadIdx.x] = __fadd_rn(part[threadIdx.x], part[threadIdx.x + s]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 && loss_out) loss_out[0] = part[0] * invB;
+}
+
+}  // namespace rth
+
+using namespace rth;
+
+extern "C" {
+
+const char *rth_last_error(void) { return g_last_error.c_str(); }
+
+int rth_version(void) { return 100; }  // 0.1.0
+
+int rth_td_huber(const float *q0, const float *q1o, const float *q1t, const int64_t *a, const float *r,
+                 const float *done, const double *isw, int64_t B, int64_t A, float gamma_n, int32_t double_q,
+                 float *td_out, float *td_abs_out, float *loss_elem, float *loss_out, float *dq, void *stream) {
+  RTH_REQUIRE(B >= 1 && A >= 1 && A < (1 << 20), "rth_td_huber: bad shape B=%lld A=%lld", (long long)B,
+              (long long)A);
+  RTH_REQUIRE(q0 && q1t && a && r && done && (q1o || !double_q), "rth_td_huber: NULL input");
+  hipLaunchKernelGGL(k_td_huber, dim3(1), dim3(kTdThreads), 0, as_stream(stream), q0, q1o, q1t, a, r, done, isw, B,
+                     (int)A, gamma_n, double_q, td_out, td_abs_out, loss_elem, loss_out, dq);
+  RTH_LAUNCHED();
+  return RTH_OK;
+}
+
+}  // extern "C"

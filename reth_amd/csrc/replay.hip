@@ -1,0 +1,298 @@
+// HBM-resident replay shard: FIFO slots + column storage + PER tree, and the row copy /
+// gather kernel that replaces the reference's LMDB put/get + pinned copy + H2D.
+//
+// Reference: reth_buffer/reth_buffer/server/main_loop.py:21-61 (append_loop),
+// server/sampler_loop.py:6-42, cache_policy/fifo_policy.py:11-18, client/client.py:21-39,
+// client/torch_cuda_loader.py:20-66, client/numpy_loader.py:27-51.
+//
+// Storage is one dense [capacity, row] array per column (struct of arrays), so a sampled
+// row of a frame column is one contiguous 28,224-byte run of uint8: the gather streams it
+// with 16-byte loads and widens to float32 on the way out (uint8 -> f32 is exact, so the
+// learner receives exactly the f32 frames the reference's actors stored, 4x fewer bytes
+// resident and read).
+#include <cstring>
+#include <vector>
+
+#include "common.hpp"
+
+struct rth_sumtree;
+
+namespace rth {
+int tree_update_impl(rth_sumtree *t, const int64_t *idx, int64_t fifo_start, const double *w64,
+                     const void *td_abs, int32_t td_dtype, double alpha, int64_t n, hipStream_t s);
+int tree_sample_impl(rth_sumtree *t, int64_t batch, const double *uniforms, uint64_t seed,
+                     uint64_t counter, int is_weights, double beta, int64_t *idx_out, double *out,
+                     hipStream_t s);
+
+enum Conv : int32_t { CONV_COPY = 0, CONV_U8_F32 = 1 };
+
+struct CopyCol {
+  const uint8_t *src;
+  uint8_t *dst;
+  const int64_t *src_rows;  // nullable: identity
+  const int64_t *dst_rows;  // nullable: identity, or FIFO when CopyArgs::dst_fifo
+  int64_t src_stride;       // bytes
+  int64_t dst_stride;       // bytes
+  int64_t in_bytes;         // bytes of one input row
+  int32_t conv;
+  int32_t pad;
+};
+
+struct CopyArgs {
+  CopyCol col[RTH_MAX_COLS];
+  int64_t n;
+  int64_t fifo_start;
+  int64_t fifo_cap;
+  int32_t dst_fifo;
+  int32_t ncols;
+};
+
+constexpr int kCopyThreads = 256;
+
+// grid: x = row, y = column.  One workgroup per (row, column): contiguous 16-byte loads
+// (1 KiB per wave-instruction); uint8 rows become float32 rows (4 x 16-byte stores/lane).
+__global__ __launch_bounds__(kCopyThreads) void k_copy_rows(CopyArgs a) {
+  const int c = blockIdx.y;
+  const int64_t i = blockIdx.x;
+  if (c >= a.ncols || i >= a.n) return;
+  const CopyCol col = a.col[c];
+  const int64_t sr = col.src_rows ? col.src_rows[i] : i;
+  int64_t dr;
+  if (col.dst_rows)
+    dr = col.dst_rows[i];
+  else if (a.dst_fifo)
+    dr = (a.fifo_start + i) % a.fifo_cap;
+  else
+    dr = i;
+  const uint8_t *__restrict__ src = col.src + sr * col.src_stride;
+  uint8_t *__restrict__ dst = col.dst + dr * col.dst_stride;
+  const int64_t nb = col.in_bytes;
+  const int tid = threadIdx.x;
+  const bool aligned16 = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0;
+  if (col.conv == CONV_U8_F32) {
+    const int64_t nvec = aligned16 ? nb / 16 : 0;
+    const uint4 *s4 = reinterpret_cast<const uint4 *>(src);
+    float4 *d4 = reinterpret_cast<float4 *>(dst);
+    for (int64_t v = tid; v < nvec; v += kCopyThreads) {
+      const uint4 x = s4[v];
+      const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float4 f;
+        f.x = (float)(w[q] & 0xffu);
+        f.y = (float)((w[q] >> 8) & 0xffu);
+        f.z = (float)((w[q] >> 16) & 0xffu);
+        f.w = (float)(w[q] >> 24);
+        d4[v * 4 + q] = f;
+      }
+    }
+    float *df = reinterpret_cast<float *>(dst);
+    for (int64_t b = nvec * 16 + tid; b < nb; b += kCopyThreads) df[b] = (float)src[b];
+  } else {
+    const int64_t nvec = aligned16 ? nb / 16 : 0;
+    const uint4 *s4 = reinterpret_cast<const uint4 *>(src);
+    uint4 *d4 = reinterpret_cast<uint4 *>(dst);
+    for (int64_t v = tid; v < nvec; v += kCopyThreads) d4[v] = s4[v];
+    for (int64_t b = nvec * 16 + tid; b < nb; b += kCopyThreads) dst[b] = src[b];
+  }
+}
+
+__global__ void k_fifo_slots(int64_t *out, int64_t n, int64_t start, int64_t cap) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = (start + i) % cap;
+}
+
+int launch_copy(const CopyArgs &a, hipStream_t s) {
+  if (a.n <= 0 || a.ncols <= 0) return RTH_OK;
+  RTH_REQUIRE(a.n < (int64_t(1) << 31), "copy: too many rows (%lld)", (long long)a.n);
+  hipLaunchKernelGGL(k_copy_rows, dim3((unsigned)a.n, (unsigned)a.ncols), dim3(kCopyThreads), 0, s, a);
+  RTH_LAUNCHED();
+  return RTH_OK;
+}
+
+int conv_of(int32_t in_dtype, int32_t out_dtype, int32_t *conv) {
+  if (in_dtype == out_dtype) {
+    *conv = CONV_COPY;
+    return RTH_OK;
+  }
+  if (in_dtype == RTH_U8 && out_dtype == RTH_F32) {
+    *conv = CONV_U8_F32;
+    return RTH_OK;
+  }
+  set_error("unsupported column conversion %d -> %d", in_dtype, out_dtype);
+  return RTH_ERR_INVALID;
+}
+
+}  // namespace rth
+
+using namespace rth;
+
+struct rth_replay {
+  int64_t cap;
+  int device;
+  uint64_t seed;
+  int32_t ncols;
+  rth_col_desc desc[RTH_MAX_COLS];
+  uint8_t *store[RTH_MAX_COLS];
+  rth_sumtree *tree;
+  // host-side service state (append_loop / sampler_loop counters)
+  int64_t tail, size, cnt, sample_calls;
+};
+
+extern "C" {
+int rth_sumtree_create(int64_t capacity, int device, rth_sumtree **out);
+int rth_sumtree_destroy(rth_sumtree *t);
+
+int rth_copy_rows(void *dst, int64_t dst_stride, const int64_t *dst_rows, const void *src, int64_t src_stride,
+                  const int64_t *src_rows, int64_t n, int64_t row_elems, int32_t in_dtype, int32_t out_dtype,
+                  void *stream) {
+  RTH_REQUIRE(n == 0 || (dst && src), "rth_copy_rows: NULL buffer");
+  RTH_REQUIRE(dtype_size(in_dtype) > 0 && dtype_size(out_dtype) > 0, "rth_copy_rows: bad dtype");
+  CopyArgs a{};
+  int32_t conv;
+  int rc = conv_of(in_dtype, out_dtype, &conv);
+  if (rc) return rc;
+  const int64_t in_bytes = row_elems * dtype_size(in_dtype);
+  const int64_t out_bytes = row_elems * dtype_size(out_dtype);
+  a.col[0] = CopyCol{(const uint8_t *)src, (uint8_t *)dst, src_rows, dst_rows,
+                     src_stride ? src_stride : in_bytes, dst_stride ? dst_stride : out_bytes, in_bytes, conv, 0};
+  a.n = n;
+  a.ncols = 1;
+  return launch_copy(a, as_stream(stream));
+}
+
+int rth_replay_create(int64_t capacity, int32_t n_cols, const rth_col_desc *cols, int device, uint64_t seed,
+                      rth_replay **out) {
+  RTH_REQUIRE(out && cols, "rth_replay_create: NULL argument");
+  RTH_REQUIRE(n_cols >= 1 && n_cols <= RTH_MAX_COLS, "rth_replay_create: n_cols=%d not in [1,%d]", n_cols,
+              RTH_MAX_COLS);
+  RTH_REQUIRE(capacity >= 1, "rth_replay_create: capacity must be >= 1");
+  for (int c = 0; c < n_cols; ++c) {
+    int32_t conv;
+    RTH_REQUIRE(cols[c].row_elems >= 1, "rth_replay_create: column %d has no elements", c);
+    int rc = conv_of(cols[c].in_dtype, cols[c].out_dtype, &conv);
+    if (rc) return rc;
+  }
+  RTH_HIP(hipSetDevice(device));
+  auto *h = new rth_replay{};
+  h->cap = capacity;
+  h->device = device;
+  h->seed = seed;
+  h->ncols = n_cols;
+  for (int c = 0; c < n_cols; ++c) {
+    h->desc[c] = cols[c];
+    const size_t bytes = (size_t)capacity * cols[c].row_elems * dtype_size(cols[c].in_dtype);
+    if (hipMalloc(&h->store[c], bytes) != hipSuccess) {
+      set_error("rth_replay_create: hipMalloc(%zu) for column %d failed", bytes, c);
+      for (int k = 0; k < c; ++k) (void)hipFree(h->store[k]);
+      delete h;
+      return RTH_ERR_NOMEM;
+    }
+  }
+  int rc = rth_sumtree_create(capacity, device, &h->tree);
+  if (rc) {
+    for (int k = 0; k < n_cols; ++k) (void)hipFree(h->store[k]);
+    delete h;
+    return rc;
+  }
+  *out = h;
+  return RTH_OK;
+}
+
+int rth_replay_destroy(rth_replay *h) {
+  if (!h) return RTH_OK;
+  (void)hipSetDevice(h->device);
+  for (int c = 0; c < h->ncols; ++c) (void)hipFree(h->store[c]);
+  rth_sumtree_destroy(h->tree);
+  delete h;
+  return RTH_OK;
+}
+
+rth_sumtree *rth_replay_tree(rth_replay *h) { return h ? h->tree : nullptr; }
+
+void *rth_replay_column(rth_replay *h, int32_t c) {
+  return (h && c >= 0 && c < h->ncols) ? (void *)h->store[c] : nullptr;
+}
+
+int rth_replay_info(const rth_replay *h, int64_t *size, int64_t *tail, int64_t *cnt, int64_t *calls) {
+  RTH_REQUIRE(h, "rth_replay_info: NULL handle");
+  if (size) *size = h->size;
+  if (tail) *tail = h->tail;
+  if (cnt) *cnt = h->cnt;
+  if (calls) *calls = h->sample_calls;
+  return RTH_OK;
+}
+
+int rth_replay_append(rth_replay *h, const rth_src *srcs, const void *td_abs, int32_t td_dtype, int64_t n,
+                      double alpha, int64_t *idx_out, void *stream) {
+  RTH_REQUIRE(h && srcs, "rth_replay_append: NULL argument");
+  RTH_REQUIRE(n >= 0 && n <= h->cap, "rth_replay_append: n=%lld exceeds capacity %lld (fifo_policy.py:12)",
+              (long long)n, (long long)h->cap);
+  if (n == 0) return RTH_OK;
+  RTH_REQUIRE(td_abs, "rth_replay_append: NULL priorities");
+  hipStream_t s = as_stream(stream);
+  CopyArgs a{};
+  for (int c = 0; c < h->ncols; ++c) {
+    RTH_REQUIRE(srcs[c].base_dev, "rth_replay_append: column %d source is NULL", c);
+    const int64_t rb = h->desc[c].row_elems * dtype_size(h->desc[c].in_dtype);
+    a.col[c] = CopyCol{(const uint8_t *)srcs[c].base_dev, h->store[c], srcs[c].rows_dev, nullptr,
+                       srcs[c].row_stride_bytes ? srcs[c].row_stride_bytes : rb, rb, rb, CONV_COPY, 0};
+  }
+  a.n = n;
+  a.ncols = h->ncols;
+  a.dst_fifo = 1;
+  a.fifo_start = h->tail;
+  a.fifo_cap = h->cap;
+  int rc = launch_copy(a, s);
+  if (rc) return rc;
+  rc = tree_update_impl(h->tree, nullptr, h->tail, nullptr, td_abs, td_dtype, alpha, n, s);
+  if (rc) return rc;
+  if (idx_out) {  // FIFO slots for the caller (the append_loop's `indices`)
+    hipLaunchKernelGGL(k_fifo_slots, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, idx_out, n, h->tail,
+                       h->cap);
+    RTH_LAUNCHED();
+  }
+  h->tail = (h->tail + n) % h->cap;
+  h->size = h->size + n < h->cap ? h->size + n : h->cap;
+  h->cnt += n;
+  return RTH_OK;
+}
+
+int rth_replay_gather(rth_replay *h, const int64_t *idx, int64_t n, void *const *out_cols, void *stream) {
+  RTH_REQUIRE(h && (n == 0 || (idx && out_cols)), "rth_replay_gather: bad arguments");
+  CopyArgs a{};
+  for (int c = 0; c < h->ncols; ++c) {
+    RTH_REQUIRE(out_cols[c], "rth_replay_gather: output column %d is NULL", c);
+    const rth_col_desc &d = h->desc[c];
+    int32_t conv;
+    conv_of(d.in_dtype, d.out_dtype, &conv);
+    const int64_t ib = d.row_elems * dtype_size(d.in_dtype), ob = d.row_elems * dtype_size(d.out_dtype);
+    a.col[c] = CopyCol{h->store[c], (uint8_t *)out_cols[c], idx, nullptr, ib, ob, ib, conv, 0};
+  }
+  a.n = n;
+  a.ncols = h->ncols;
+  return launch_copy(a, as_stream(stream));
+}
+
+int rth_replay_sample(rth_replay *h, int64_t batch, double beta, const double *uniforms, void *const *out_cols,
+                      int64_t *idx_out, double *isw_out, void *stream) {
+  RTH_REQUIRE(h && batch > 0 && idx_out && isw_out, "rth_replay_sample: bad arguments");
+  hipStream_t s = as_stream(stream);
+  int rc = tree_sample_impl(h->tree, batch, uniforms, h->seed, (uint64_t)h->sample_calls, 1, beta, idx_out,
+                            isw_out, s);
+  if (rc) return rc;
+  h->sample_calls++;
+  if (out_cols) return rth_replay_gather(h, idx_out, batch, out_cols, stream);
+  return RTH_OK;
+}
+
+int rth_replay_update_priorities(rth_replay *h, const int64_t *idx, const void *td_abs, int32_t td_dtype, int64_t n,
+                                 double alpha, void *stream) {
+  RTH_REQUIRE(h && (n == 0 || (idx && td_abs)), "rth_replay_update_priorities: bad arguments");
+  int rc = tree_update_impl(h->tree, idx, 0, nullptr, td_abs, td_dtype, alpha, n, as_stream(stream));
+  if (rc) return rc;
+  h->cnt += n;
+  return RTH_OK;
+}
+
+}  // extern "C"

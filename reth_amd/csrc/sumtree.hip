@@ -1,0 +1,387 @@
+// In-order heap sum-tree + PER sampler on gfx950.
+//
+// Reference semantics: reth_buffer/reth_buffer/utils/sumtree.py (live PER tree) and
+// reth_buffer/reth_buffer/sampler/per_sampler.py.  The tree is a heap of `capacity` nodes in
+// which EVERY node carries a priority; sum[i] = val[i] + sum[l] + sum[r] (in that order);
+// sampling walks left subtree -> node -> right subtree.  All arithmetic is fp64 with the
+// reference's operation order, so results are bit-identical to the sequential numba code.
+//
+// HBM layout: one 32-byte record per node {sum, val, min, pad}, node i at record i + 1, so
+// the two children of node i (2i+1, 2i+2) are records 2i+2, 2i+3: one aligned 64-byte pair.
+// A descent step therefore needs one 64-byte pair (left {sum,val} + right val), and a
+// maintain step reads the pair plus its own record.
+//
+// Batched update (the reference loops val[idx]=w; maintain(idx) per element):
+//   the final state equals "write the last value of every index, then recompute every
+//   touched ancestor once, deepest level first, from final children" -- a touched node's
+//   last maintenance in the sequential loop happens after every change below it.  Untouched
+//   nodes must NOT be recomputed (the min() quirk, sumtree.py:11-19, seeds 1 for a maintained
+//   zero node).  One workgroup sorts each chunk of <= 4096 (index, position) keys in LDS by
+//   the index's left-aligned leaf position, which makes "ancestor at level L" monotone, so
+//   each distinct ancestor is maintained exactly once per level by the first key of its run.
+//   Chunks run in order, which keeps the sequential semantics for any n.
+#include <cmath>
+
+#include "common.hpp"
+
+namespace rth {
+
+struct alignas(32) Node {
+  double sum, val, mn, pad;
+};
+
+constexpr int kUpdThreads = 1024;
+constexpr int kUpdChunk = 4096;  // keys per LDS chunk (32 KiB)
+constexpr int kPosBits = 12;     // log2(kUpdChunk)
+constexpr int kDepthBits = 6;
+constexpr int64_t kMaxCapacity = int64_t(1) << 40;  // aligned(41) + depth(6) + pos(12) <= 64
+
+__host__ __device__ __forceinline__ int node_depth(int64_t i) { return 63 - __builtin_clzll((unsigned long long)(i + 1)); }
+
+// _numba_maintain_node (sumtree.py:5-21)
+__device__ __forceinline__ void maintain_node(Node *nd, int64_t cap, int64_t i) {
+  const int64_t l = 2 * i + 1, r = 2 * i + 2;
+  const double v = nd[i + 1].val;
+  double s = v;
+  double m = (v != 0.0) ? v : 1.0;
+  if (l < cap) {
+    const Node L = nd[l + 1];
+    s = __dadd_rn(s, L.sum);
+    if (L.mn != 0.0) m = (L.mn < m) ? L.mn : m;
+  }
+  if (r < cap) {
+    const Node R = nd[r + 1];
+    s = __dadd_rn(s, R.sum);
+    if (R.mn != 0.0) m = (R.mn < m) ? R.mn : m;
+  }
+  nd[i + 1].sum = s;
+  nd[i + 1].mn = m;
+}
+
+// _numba_find_index (sumtree.py:34-58)
+__device__ __forceinline__ int64_t tree_find(const Node *__restrict__ nd, int64_t cap, double w) {
+  int64_t cur = 0;
+  double cval = nd[1].val;
+  for (;;) {
+    const int64_t l = 2 * cur + 1;
+    double lsum = 0.0, lval = 0.0, rval = 0.0;
+    if (l < cap) {
+      // issue the left {sum,val} and right val of the 64-byte child pair together
+      const double2 L = *reinterpret_cast<const double2 *>(&nd[l + 1]);
+      rval = nd[l + 2].val;  // record cap+1 exists (padding), so no bound check needed
+      lsum = L.x;
+      lval = L.y;
+      if (w < lsum) {
+        cur = l;
+        cval = lval;
+        continue;
+      }
+      w = __dsub_rn(w, lsum);
+    }
+    if (w < __dadd_rn(cval, 1e-5)) return cur;
+    w = __dsub_rn(w, cval);
+    const int64_t r = l + 1;
+    if (r >= cap) return cur;
+    cur = r;
+    cval = (l < cap) ? rval : nd[r + 1].val;
+  }
+}
+
+__device__ __forceinline__ double tree_min(const Node *nd) {  // NumbaSumTree.min :109-110
+  const Node root = nd[1];
+  return root.sum != 0.0 ? root.mn : 1.0;
+}
+
+// ------------------------------------------------------------------ batched update
+struct UpdArgs {
+  Node *nd;
+  int64_t cap;
+  int32_t maxd;
+  const int64_t *idx;   // nullable: FIFO range (fifo_start + i) % cap
+  int64_t fifo_start;
+  const double *w64;     // priority as given (NumbaSumTree.update)
+  const void *td_abs;    // or PERSampler.update: (td_abs + 1e-6) ** alpha ...
+  int32_t td_dtype;      // ... in float32 (RTH_F32) or float64 (RTH_F64), like numpy
+  double alpha;
+  int64_t n;
+};
+
+__device__ __forceinline__ double priority_of(const UpdArgs &a, int64_t src) {
+  if (a.w64) return a.w64[src];
+  if (a.td_dtype == RTH_F64) return per_normalize64(static_cast<const double *>(a.td_abs)[src], a.alpha);
+  return (double)per_normalize(static_cast<const float *>(a.td_abs)[src], (float)a.alpha);
+}
+
+__device__ __forceinline__ int64_t key_index(uint64_t key, int maxd) {
+  const int d = (int)((key >> kPosBits) & ((1u << kDepthBits) - 1));
+  const uint64_t aligned = key >> (kPosBits + kDepthBits);
+  return (int64_t)(aligned >> (maxd - d)) - 1;
+}
+
+__global__ __launch_bounds__(kUpdThreads) void k_tree_update(UpdArgs a) {
+  __shared__ uint64_t keys[kUpdChunk];
+  const int tid = threadIdx.x;
+  const int maxd = a.maxd;
+  for (int64_t cs = 0; cs < a.n; cs += kUpdChunk) {
+    const int m = (int)min<int64_t>(kUpdChunk, a.n - cs);
+    int P = 2;
+    while (P < m) P <<= 1;
+    for (int j = tid; j < P; j += kUpdThreads) {
+      uint64_t key = ~0ull;
+      if (j < m) {
+        const int64_t id = a.idx ? a.idx[cs + j] : (a.fifo_start + cs + j) % a.cap;
+        if (id >= 0 && id < a.cap) {
+          const int d = node_depth(id);
+          const uint64_t aligned = (uint64_t)(id + 1) << (maxd - d);
+          key = (((aligned << kDepthBits) | (uint64_t)d) << kPosBits) | (uint64_t)j;
+        }
+      }
+      keys[j] = key;
+    }
+    __syncthreads();
+    // bitonic sort, ascending
+    for (int k = 2; k <= P; k <<= 1) {
+      for (int jj = k >> 1; jj > 0; jj >>= 1) {
+        for (int i = tid; i < P; i += kUpdThreads) {
+          const int ixj = i ^ jj;
+          if (ixj > i) {
+            const uint64_t x = keys[i], y = keys[ixj];
+            const bool up = (i & k) == 0;
+            if ((x > y) == up) {
+              keys[i] = y;
+              keys[ixj] = x;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    }
+    // last writer of every index sets val (duplicates sort by position)
+    for (int j = tid; j < m; j += kUpdThreads) {
+      const uint64_t key = keys[j];
+      if (key == ~0ull) continue;
+      const int64_t id = key_index(key, maxd);
+      const bool last = (j == m - 1) || keys[j + 1] == ~0ull || key_index(keys[j + 1], maxd) != id;
+      if (last) {
+        const int64_t src = cs + (int64_t)(key & ((1u << kPosBits) - 1));
+        a.nd[id + 1].val = priority_of(a, src);
+      }
+    }
+    __syncthreads();
+    // touched ancestors, deepest level first; first key of each ancestor run maintains it
+    for (int L = maxd; L >= 0; --L) {
+      for (int j = tid; j < m; j += kUpdThreads) {
+        const uint64_t key = keys[j];
+        if (key == ~0ull) continue;
+        const int d = (int)((key >> kPosBits) & ((1u << kDepthBits) - 1));
+        if (d < L) continue;
+        const uint64_t aligned = key >> (kPosBits + kDepthBits);
+        const uint64_t anc = aligned >> (maxd - L);
+        if (j > 0) {
+          const uint64_t pk = keys[j - 1];
+          const int pd = (int)((pk >> kPosBits) & ((1u << kDepthBits) - 1));
+          if (pd >= L && ((pk >> (kPosBits + kDepthBits)) >> (maxd - L)) == anc) continue;
+        }
+        maintain_node(a.nd, a.cap, (int64_t)anc - 1);
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// ------------------------------------------------------------------ find / sample
+__global__ void k_tree_find(const Node *__restrict__ nd, int64_t cap, const double *__restrict__ tg,
+                            int64_t n, int64_t *__restrict__ idx_out, double *__restrict__ val_out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t k = tree_find(nd, cap, tg[i]);
+  if (idx_out) idx_out[i] = k;
+  if (val_out) val_out[i] = nd[k + 1].val;
+}
+
+// _numba_sample (sumtree.py:70-79) and, with is_weights, PERSampler.sample (:24-28)
+__global__ void k_tree_sample(const Node *__restrict__ nd, int64_t cap, int64_t batch,
+                              const double *__restrict__ uniforms, uint64_t seed, uint64_t counter,
+                              int is_weights, double beta, int64_t *__restrict__ idx_out,
+                              double *__restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= batch) return;
+  const double total = nd[1].sum;
+  const double seg = total / (double)batch;
+  const double u = uniforms ? uniforms[i] : philox_uniform(seed, counter, (uint32_t)i, STREAM_SAMPLE);
+  const double t = __dmul_rn(__dadd_rn((double)i, u), seg);
+  const int64_t k = tree_find(nd, cap, t);
+  const double p = nd[k + 1].val;
+  idx_out[i] = k;
+  if (is_weights) {
+    out[i] = pow(p / tree_min(nd), -beta);
+  } else if (out) {
+    out[i] = p;
+  }
+}
+
+__global__ void k_tree_stats(const Node *nd, double *out) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    out[0] = nd[1].sum;
+    out[1] = tree_min(nd);
+  }
+}
+
+__global__ void k_tree_export(const Node *nd, int64_t cap, double *s, double *m, double *v) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= cap) return;
+  const Node x = nd[i + 1];
+  if (s) s[i] = x.sum;
+  if (m) m[i] = x.mn;
+  if (v) v[i] = x.val;
+}
+
+__global__ void k_tree_import(Node *nd, int64_t cap, const double *s, const double *m, const double *v) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= cap) return;
+  nd[i + 1] = Node{s[i], v[i], m[i], 0.0};
+}
+
+__global__ void k_per_normalize(const float *w, int64_t n, float alpha, float *out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = per_normalize(w[i], alpha);
+}
+
+}  // namespace rth
+
+using namespace rth;
+
+struct rth_sumtree {
+  int64_t cap;
+  int device;
+  int maxd;
+  Node *nodes;
+};
+
+namespace rth {
+int tree_update_impl(rth_sumtree *t, const int64_t *idx, int64_t fifo_start, const double *w64,
+                     const void *td_abs, int32_t td_dtype, double alpha, int64_t n, hipStream_t s) {
+  if (n <= 0) return RTH_OK;
+  RTH_REQUIRE(w64 || td_dtype == RTH_F32 || td_dtype == RTH_F64, "priority dtype must be f32 or f64");
+  UpdArgs a{t->nodes, t->cap, t->maxd, idx, fifo_start, w64, td_abs, td_dtype, alpha, n};
+  hipLaunchKernelGGL(k_tree_update, dim3(1), dim3(kUpdThreads), 0, s, a);
+  RTH_LAUNCHED();
+  return RTH_OK;
+}
+int tree_sample_impl(rth_sumtree *t, int64_t batch, const double *uniforms, uint64_t seed,
+                     uint64_t counter, int is_weights, double beta, int64_t *idx_out, double *out,
+                     hipStream_t s) {
+  if (batch <= 0) return RTH_OK;
+  const int bs = 256;
+  hipLaunchKernelGGL(k_tree_sample, dim3((unsigned)((batch + bs - 1) / bs)), dim3(bs), 0, s, t->nodes,
+                     t->cap, batch, uniforms, seed, counter, is_weights, beta, idx_out, out);
+  RTH_LAUNCHED();
+  return RTH_OK;
+}
+}  // namespace rth
+
+extern "C" {
+
+int rth_sumtree_create(int64_t capacity, int device, rth_sumtree **out) {
+  RTH_REQUIRE(out != nullptr, "rth_sumtree_create: out is NULL");
+  RTH_REQUIRE(capacity >= 1 && capacity < kMaxCapacity, "rth_sumtree_create: capacity %lld out of range",
+              (long long)capacity);
+  RTH_HIP(hipSetDevice(device));
+  Node *nodes = nullptr;
+  const size_t bytes = (size_t)(capacity + 2) * sizeof(Node);
+  if (hipMalloc(&nodes, bytes) != hipSuccess) {
+    set_error("rth_sumtree_create: hipMalloc(%zu) failed", bytes);
+    return RTH_ERR_NOMEM;
+  }
+  RTH_HIP(hipMemset(nodes, 0, bytes));
+  auto *t = new rth_sumtree{capacity, device, node_depth(capacity - 1), nodes};
+  *out = t;
+  return RTH_OK;
+}
+
+int rth_sumtree_destroy(rth_sumtree *t) {
+  if (!t) return RTH_OK;
+  (void)hipSetDevice(t->device);
+  (void)hipFree(t->nodes);
+  delete t;
+  return RTH_OK;
+}
+
+int64_t rth_sumtree_capacity(const rth_sumtree *t) { return t ? t->cap : -1; }
+
+int rth_sumtree_clear(rth_sumtree *t, void *stream) {
+  RTH_REQUIRE(t, "rth_sumtree_clear: NULL tree");
+  RTH_HIP(hipMemsetAsync(t->nodes, 0, (size_t)(t->cap + 2) * sizeof(Node), as_stream(stream)));
+  return RTH_OK;
+}
+
+int rth_sumtree_update(rth_sumtree *t, const int64_t *idx, const double *w, int64_t n, void *stream) {
+  RTH_REQUIRE(t && (n == 0 || (idx && w)), "rth_sumtree_update: bad arguments");
+  return tree_update_impl(t, idx, 0, w, nullptr, RTH_F64, 0.0, n, as_stream(stream));
+}
+
+int rth_sumtree_find(rth_sumtree *t, const double *tg, int64_t n, int64_t *idx_out, double *val_out,
+                     void *stream) {
+  RTH_REQUIRE(t && (n == 0 || tg), "rth_sumtree_find: bad arguments");
+  if (n == 0) return RTH_OK;
+  const int bs = 256;
+  hipLaunchKernelGGL(k_tree_find, dim3((unsigned)((n + bs - 1) / bs)), dim3(bs), 0, as_stream(stream),
+                     t->nodes, t->cap, tg, n, idx_out, val_out);
+  RTH_LAUNCHED();
+  return RTH_OK;
+}
+
+int rth_sumtree_sample(rth_sumtree *t, int64_t batch, const double *uniforms, uint64_t seed,
+                       uint64_t counter, int64_t *idx_out, double *val_out, void *stream) {
+  RTH_REQUIRE(t && batch > 0 && idx_out, "rth_sumtree_sample: bad arguments");  // assert batch_size > 0 (:73)
+  return tree_sample_impl(t, batch, uniforms, seed, counter, 0, 0.0, idx_out, val_out, as_stream(stream));
+}
+
+int rth_sumtree_stats(rth_sumtree *t, double *out2, void *stream) {
+  RTH_REQUIRE(t && out2, "rth_sumtree_stats: bad arguments");
+  hipLaunchKernelGGL(k_tree_stats, dim3(1), dim3(64), 0, as_stream(stream), t->nodes, out2);
+  RTH_LAUNCHED();
+  return RTH_OK;
+}
+
+int rth_sumtree_export(rth_sumtree *t, double *s, double *m, double *v, void *stream) {
+  RTH_REQUIRE(t, "rth_sumtree_export: NULL tree");
+  const int bs = 256;
+  hipLaunchKernelGGL(k_tree_export, dim3((unsigned)((t->cap + bs - 1) / bs)), dim3(bs), 0,
+                     as_stream(stream), t->nodes, t->cap, s, m, v);
+  RTH_LAUNCHED();
+  return RTH_OK;
+}
+
+int rth_sumtree_import(rth_sumtree *t, const double *s, const double *m, const double *v, void *stream) {
+  RTH_REQUIRE(t && s && m && v, "rth_sumtree_import: bad arguments");
+  const int bs = 256;
+  hipLaunchKernelGGL(k_tree_import, dim3((unsigned)((t->cap + bs - 1) / bs)), dim3(bs), 0,
+                     as_stream(stream), t->nodes, t->cap, s, m, v);
+  RTH_LAUNCHED();
+  return RTH_OK;
+}
+
+int rth_per_normalize(const float *w, int64_t n, float alpha, float *out, void *stream) {
+  RTH_REQUIRE(n == 0 || (w && out), "rth_per_normalize: bad arguments");
+  if (n == 0) return RTH_OK;
+  const int bs = 256;
+  hipLaunchKernelGGL(k_per_normalize, dim3((unsigned)((n + bs - 1) / bs)), dim3(bs), 0, as_stream(stream),
+                     w, n, alpha, out);
+  RTH_LAUNCHED();
+  return RTH_OK;
+}
+
+int rth_per_update(rth_sumtree *t, const int64_t *idx, const void *td_abs, int32_t td_dtype, int64_t n,
+                   double alpha, void *stream) {
+  RTH_REQUIRE(t && (n == 0 || (idx && td_abs)), "rth_per_update: bad arguments");
+  return tree_update_impl(t, idx, 0, nullptr, td_abs, td_dtype, alpha, n, as_stream(stream));
+}
+
+int rth_per_sample(rth_sumtree *t, int64_t batch, double beta, const double *uniforms, uint64_t seed,
+                   uint64_t counter, int64_t *idx_out, double *isw_out, void *stream) {
+  RTH_REQUIRE(t && batch > 0 && idx_out && isw_out, "rth_per_sample: bad arguments");
+  return tree_sample_impl(t, batch, uniforms, seed, counter, 1, beta, idx_out, isw_out, as_stream(stream));
+}
+
+}  // extern "C"

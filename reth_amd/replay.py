@@ -1,0 +1,318 @@
+"""HBM-resident sum-tree, PER sampler and replay shard (host side of libreth_hip.so).
+
+    SumTree     <- reth_buffer/reth_buffer/utils/sumtree.py:82-113     (NumbaSumTree)
+    PERSampler  <- reth_buffer/reth_buffer/sampler/per_sampler.py:5-35
+    HbmReplay   <- the reth_buffer service: append_loop (server/main_loop.py:21-61),
+                   FIFOPolicy (cache_policy/fifo_policy.py:11-18), sampler_loop
+                   (server/sampler_loop.py:6-42) and the loaders' gather
+                   (client/torch_cuda_loader.py:20-66, numpy_loader.py:27-51)
+
+Everything runs on the device through the C ABI; results stay in HBM unless a caller asks
+for host copies (the numpy-facing reth_buffer API does).  Argument checking mirrors the
+reference's asserts and raises on the host.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import ColDesc, Src, c_i64, c_vp, call, ptr, stream_ptr
+from .schedule import Schedule
+
+_TORCH_TO_RTH = {torch.uint8: _lib.RTH_U8, torch.int32: _lib.RTH_I32, torch.int64: _lib.RTH_I64,
+                 torch.float32: _lib.RTH_F32, torch.float64: _lib.RTH_F64}
+_RTH_TO_TORCH = {v: k for k, v in _TORCH_TO_RTH.items()}
+
+
+def _device(device):
+    dev = torch.device(device if device is not None else "cuda")
+    if dev.type != "cuda":
+        raise ValueError(f"reth_amd runs on the GPU only (got device {dev})")
+    return torch.device("cuda", dev.index if dev.index is not None else torch.cuda.current_device())
+
+
+def as_device(x, dtype, device):
+    """numpy / list / tensor -> contiguous device tensor of `dtype` (no copy if already so)."""
+    if torch.is_tensor(x):
+        return x.to(device=device, dtype=dtype, non_blocking=True).contiguous()
+    return torch.as_tensor(np.asarray(x), dtype=dtype).to(device, non_blocking=True).contiguous()
+
+
+def _prio_tensor(w, device):
+    """priorities keep their precision class: float64 inputs are normalised in f64 (numpy
+    on an f8 array), everything else in f32 (the apex path's `np.asarray(loss, "f4")`)."""
+    is64 = (torch.is_tensor(w) and w.dtype == torch.float64) or (
+        not torch.is_tensor(w) and np.asarray(w).dtype == np.float64)
+    t = as_device(w, torch.float64 if is64 else torch.float32, device)
+    return t, (_lib.RTH_F64 if is64 else _lib.RTH_F32)
+
+
+class SumTree:
+    """Device in-order heap sum-tree with NumbaSumTree's interface (fp64, bit-exact)."""
+
+    def __init__(self, capacity, device=None, _handle=None):
+        self.capacity = int(capacity)
+        self.device = _device(device)
+        self._owned = _handle is None
+        if _handle is None:
+            h = c_vp()
+            with torch.cuda.device(self.device):
+                call("rth_sumtree_create", self.capacity, self.device.index, ctypes.byref(h))
+            _handle = h.value
+        self._h = _handle
+        self._stats = torch.empty(2, dtype=torch.float64, device=self.device)
+
+    def __del__(self):
+        if getattr(self, "_owned", False) and getattr(self, "_h", None):
+            try:
+                _lib.lib().rth_sumtree_destroy(self._h)
+            except Exception:
+                pass
+            self._h = None
+
+    @property
+    def handle(self):
+        return self._h
+
+    def clear(self):
+        call("rth_sumtree_clear", self._h, stream_ptr())
+
+    def update(self, indices, weights):
+        idx = as_device(indices, torch.int64, self.device)
+        w = as_device(weights, torch.float64, self.device)
+        assert idx.numel() == w.numel()  # _numba_update assert (sumtree.py:63)
+        call("rth_sumtree_update", self._h, ptr(idx), ptr(w), idx.numel(), stream_ptr())
+
+    def find(self, targets):
+        tg = as_device(targets, torch.float64, self.device)
+        idx = torch.empty(tg.numel(), dtype=torch.int64, device=self.device)
+        val = torch.empty(tg.numel(), dtype=torch.float64, device=self.device)
+        call("rth_sumtree_find", self._h, ptr(tg), tg.numel(), ptr(idx), ptr(val), stream_ptr())
+        return idx, val
+
+    def sample(self, batch_size, uniforms=None, seed=0, counter=0):
+        assert batch_size > 0
+        u = None if uniforms is None else as_device(uniforms, torch.float64, self.device)
+        idx = torch.empty(batch_size, dtype=torch.int64, device=self.device)
+        val = torch.empty(batch_size, dtype=torch.float64, device=self.device)
+        call("rth_sumtree_sample", self._h, batch_size, ptr(u), seed, counter, ptr(idx), ptr(val),
+             stream_ptr())
+        return idx, val
+
+    def stats(self):
+        """device tensor [sum(), min()] (no sync)"""
+        call("rth_sumtree_stats", self._h, ptr(self._stats), stream_ptr())
+        return self._stats
+
+    def sum(self):
+        return float(self.stats()[0])
+
+    def min(self):
+        return float(self.stats()[1])
+
+    def export(self):
+        s, m, v = (torch.empty(self.capacity, dtype=torch.float64, device=self.device) for _ in range(3))
+        call("rth_sumtree_export", self._h, ptr(s), ptr(m), ptr(v), stream_ptr())
+        return s, m, v
+
+    def load(self, s, m, v):
+        s, m, v = (as_device(x, torch.float64, self.device) for x in (s, m, v))
+        call("rth_sumtree_import", self._h, ptr(s), ptr(m), ptr(v), stream_ptr())
+
+
+class PERSampler:
+    """reth_buffer/reth_buffer/sampler/per_sampler.py:5-35 on the device tree.
+
+    `update` fuses _normalize_weights ((w + 1e-6) ** alpha) into the tree update; `sample`
+    returns device tensors (indices int64, IS weights float64).  Without explicit uniforms
+    the targets come from Philox(seed, call counter) on the device."""
+
+    def __init__(self, capacity, alpha=0.6, beta=0.4, device=None, seed=0):
+        self.sumtree = SumTree(capacity, device)
+        self.device = self.sumtree.device
+        self._alpha_str, self._beta_str = alpha, beta
+        self.alpha = Schedule.from_str(alpha)
+        self.beta = Schedule.from_str(beta)
+        self.seed = seed
+        self.calls = 0
+
+    def ready_sample(self, batch_size):
+        return True
+
+    def clear(self):
+        self.sumtree.clear()
+        self.alpha = Schedule.from_str(self._alpha_str)
+        self.beta = Schedule.from_str(self._beta_str)
+
+    def on_step(self):
+        self.alpha.step()
+        self.beta.step()
+
+    def update(self, indices, weights):
+        idx = as_device(indices, torch.int64, self.device)
+        w, wt = _prio_tensor(weights, self.device)
+        assert idx.numel() == w.numel()
+        call("rth_per_update", self.sumtree.handle, ptr(idx), ptr(w), wt, idx.numel(),
+             float(self.alpha.value()), stream_ptr())
+
+    def sample(self, batch_size, uniforms=None):
+        u = None if uniforms is None else as_device(uniforms, torch.float64, self.device)
+        idx = torch.empty(batch_size, dtype=torch.int64, device=self.device)
+        isw = torch.empty(batch_size, dtype=torch.float64, device=self.device)
+        call("rth_per_sample", self.sumtree.handle, batch_size, float(self.beta.value()), ptr(u), self.seed,
+             self.calls, ptr(idx), ptr(isw), stream_ptr())
+        self.calls += 1
+        return idx, isw
+
+
+class Column:
+    """one replay column: per-row shape, storage dtype, sampled dtype"""
+
+    def __init__(self, shape, dtype, out_dtype=None):
+        self.shape = tuple(int(s) for s in shape)
+        self.dtype = dtype
+        self.out_dtype = out_dtype or dtype
+        self.row_elems = int(np.prod(self.shape)) if self.shape else 1
+        if dtype not in _TORCH_TO_RTH:
+            raise TypeError(f"unsupported replay column dtype {dtype}")
+        if self.out_dtype != dtype and not (dtype == torch.uint8 and self.out_dtype == torch.float32):
+            raise TypeError(f"unsupported column conversion {dtype} -> {self.out_dtype}")
+
+    def desc(self):
+        return ColDesc(self.row_elems, _TORCH_TO_RTH[self.dtype], _TORCH_TO_RTH[self.out_dtype])
+
+
+class HbmReplay:
+    """A prioritized replay shard resident in HBM (one per GPU).
+
+    columns: list of Column.  alpha / beta: schedule specs (numbers or "start,end,steps").
+    sample_start: the sampler_loop gate, max(sample_start, batch_size) (main_loop.py:144-145).
+    """
+
+    def __init__(self, capacity, columns, alpha=0.6, beta=0.4, device=None, seed=0):
+        if not 1 <= len(columns) <= _lib.MAX_COLS:
+            raise ValueError(f"1..{_lib.MAX_COLS} columns supported, got {len(columns)}")
+        self.capacity = int(capacity)
+        self.columns = list(columns)
+        self.device = _device(device)
+        self._alpha_str, self._beta_str = alpha, beta
+        self.alpha = Schedule.from_str(alpha)
+        self.beta = Schedule.from_str(beta)
+        descs = (ColDesc * len(columns))(*[c.desc() for c in columns])
+        h = c_vp()
+        with torch.cuda.device(self.device):
+            call("rth_replay_create", self.capacity, len(columns), descs, self.device.index, int(seed),
+                 ctypes.byref(h))
+        self._h = h.value
+        self.tree = SumTree(self.capacity, self.device, _handle=_lib.lib().rth_replay_tree(self._h))
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            try:
+                _lib.lib().rth_replay_destroy(self._h)
+            except Exception:
+                pass
+            self._h = None
+
+    # ---------------------------------------------------------------- counters
+    def info(self):
+        vals = [c_i64() for _ in range(4)]
+        call("rth_replay_info", self._h, *[ctypes.byref(v) for v in vals])
+        return tuple(v.value for v in vals)  # size, tail, cnt, sample_calls
+
+    @property
+    def size(self):
+        return self.info()[0]
+
+    @property
+    def cnt(self):
+        return self.info()[2]
+
+    def column_storage(self, c):
+        """device tensor view of column c's storage [capacity, *shape]"""
+        col = self.columns[c]
+        p = _lib.lib().rth_replay_column(self._h, c)
+        n = self.capacity * col.row_elems
+        return _wrap_device(p, n, col.dtype, self.device).view(self.capacity, *col.shape)
+
+    # ---------------------------------------------------------------- ops
+    def append(self, cols, td_abs, src_rows=None, row_strides=None, idx_out=None):
+        """Client.append + append_loop: rows of `cols` (device tensors, [n, *shape] or a row
+        source with src_rows) into FIFO slots; priorities (td_abs + 1e-6) ** alpha."""
+        if len(cols) != len(self.columns):
+            raise ValueError(f"expected {len(self.columns)} columns, got {len(cols)}")
+        w, wt = _prio_tensor(td_abs, self.device)
+        n = w.numel()
+        assert n <= self.capacity  # fifo_policy.py:12
+        srcs = (Src * len(cols))()
+        keep = []
+        for c, (col, t) in enumerate(zip(self.columns, cols)):
+            if t.dtype != col.dtype or not t.is_cuda:
+                t = t.to(device=self.device, dtype=col.dtype)
+            t = t if t.is_contiguous() else t.contiguous()
+            rows = None if src_rows is None else src_rows[c]
+            if rows is None and t.shape[0] != n:
+                raise ValueError(f"column {c} has {t.shape[0]} rows, priorities have {n}")
+            keep.append(t)
+            stride = 0 if row_strides is None else int(row_strides[c])
+            srcs[c] = Src(ptr(t), ptr(rows), stride)
+        call("rth_replay_append", self._h, srcs, ptr(w), wt, n, float(self.alpha.value()), ptr(idx_out),
+             stream_ptr())
+        return n
+
+    def sample_into(self, batch_size, out_cols, idx_out, isw_out, uniforms=None):
+        u = None if uniforms is None else as_device(uniforms, torch.float64, self.device)
+        arr = (c_vp * len(out_cols))(*[ptr(t) for t in out_cols])
+        call("rth_replay_sample", self._h, batch_size, float(self.beta.value()), ptr(u), arr, ptr(idx_out),
+             ptr(isw_out), stream_ptr())
+
+    def new_batch(self, batch_size):
+        cols = [torch.empty((batch_size, *c.shape), dtype=c.out_dtype, device=self.device) for c in self.columns]
+        idx = torch.empty(batch_size, dtype=torch.int64, device=self.device)
+        isw = torch.empty(batch_size, dtype=torch.float64, device=self.device)
+        return cols, idx, isw
+
+    def sample(self, batch_size, uniforms=None):
+        cols, idx, isw = self.new_batch(batch_size)
+        self.sample_into(batch_size, cols, idx, isw, uniforms)
+        return cols, idx, isw
+
+    def gather(self, indices, out_cols=None):
+        idx = as_device(indices, torch.int64, self.device)
+        if out_cols is None:
+            out_cols = [torch.empty((idx.numel(), *c.shape), dtype=c.out_dtype, device=self.device)
+                        for c in self.columns]
+        arr = (c_vp * len(out_cols))(*[ptr(t) for t in out_cols])
+        call("rth_replay_gather", self._h, ptr(idx), idx.numel(), arr, stream_ptr())
+        return out_cols
+
+    def on_step(self):
+        self.alpha.step()
+        self.beta.step()
+
+    def update_priorities(self, indices, td_abs, step=False):
+        """Client.update_priorities -> sampler_loop: on_step() first when step (:32-35)."""
+        if step:
+            self.on_step()
+        idx = as_device(indices, torch.int64, self.device)
+        w, wt = _prio_tensor(td_abs, self.device)
+        assert idx.numel() == w.numel()  # client.py:38
+        call("rth_replay_update_priorities", self._h, ptr(idx), ptr(w), wt, idx.numel(),
+             float(self.alpha.value()), stream_ptr())
+
+
+def _wrap_device(p, n, dtype, device):
+    """A torch view of foreign device memory owned by a handle (kept alive by the caller)."""
+    elem = torch.empty((), dtype=dtype).element_size()
+    return _from_dev_ptr(p, n * elem, device).view(dtype)[:n]
+
+
+def _from_dev_ptr(p, nbytes, device):
+    class _Iface:
+        pass
+
+    iface = _Iface()
+    iface.__cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (p, False), "version": 3}
+    with torch.cuda.device(device):
+        return torch.as_tensor(iface, device=device)

@@ -1,0 +1,206 @@
+"""Drop-in replacement for the `reth_buffer` client API, backed by an HBM replay shard.
+
+Reference API kept (paths in the sosp2021/Reth checkout):
+    start_server / start_per            reth_buffer/reth_buffer/__init__.py:11-49
+    Client.append / update_priorities   reth_buffer/reth_buffer/client/client.py:21-39
+    NumpyLoader.sample                  reth_buffer/reth_buffer/client/numpy_loader.py:27-51
+    TorchCudaLoader.sample / iteration  reth_buffer/reth_buffer/client/torch_cuda_loader.py:69-163
+
+What changes underneath: the service processes (ZMQ append/sampler loops, LMDB in /dev/shm,
+CUDA-IPC loader processes) become one replay object resident in the GPU's HBM, owned by the
+process that drives that GPU (one process per GPU).  `start_*` returns a handle standing in
+for the service Process (terminate/join/is_alive) and an address string ("hbm://dev/id")
+that Client and the loaders resolve in-process.  Differences, by design:
+  * a loader asked for a batch before `cnt >= max(sample_start, batch_size)`
+    (sampler_loop.py:23-28) raises instead of blocking forever (nothing else could fill it);
+  * num_sampler_procs / num_procs / compress / host / port are accepted and ignored;
+  * TorchCudaLoader keeps the reference's sample-ahead: batch k+1 is drawn as soon as batch
+    k is handed out, i.e. before k's priority update lands (the sampler's HWM-1 PUSH).
+"""
+import itertools
+
+import numpy as np
+import torch
+
+from .replay import Column, HbmReplay, _device, as_device
+
+_SERVICES = {}
+_ids = itertools.count()
+
+_NP_TO_TORCH = {np.dtype("uint8"): torch.uint8, np.dtype("int32"): torch.int32, np.dtype("int64"): torch.int64,
+                np.dtype("float32"): torch.float32, np.dtype("float64"): torch.float64}
+
+
+class ReplayService:
+    """Stands in for the service Process returned by the reference's start_server."""
+
+    def __init__(self, capacity, batch_size, sampler, device, seed, widen_u8):
+        self.capacity, self.batch_size = int(capacity), int(batch_size)
+        self.alpha = sampler.get("kwargs", {}).get("alpha", 0.6)
+        self.beta = sampler.get("kwargs", {}).get("beta", 0.4)
+        # main_loop.py:144-145: sample_start = max(sample_start, batch_size)
+        self.sample_start = max(int(sampler.get("sample_start", 1000)), self.batch_size)
+        self.device = _device(device)
+        self.seed = seed
+        self.widen_u8 = widen_u8
+        self.replay = None  # created on the first append (the LMDB map is sized from it too)
+        self.alive = True
+
+    def ensure(self, cols):
+        if self.replay is None:
+            columns = []
+            for c in cols:
+                dt = c.dtype if torch.is_tensor(c) else _NP_TO_TORCH.get(np.asarray(c).dtype)
+                if dt is None:
+                    raise TypeError(f"unsupported column dtype {np.asarray(c).dtype}")
+                widen = dt == torch.uint8 and (self.widen_u8 is True or
+                                               (isinstance(self.widen_u8, (set, list, tuple)) and
+                                                len(columns) in self.widen_u8))
+                columns.append(Column(tuple(c.shape[1:]), dt, torch.float32 if widen else None))
+            self.replay = HbmReplay(self.capacity, columns, self.alpha, self.beta, self.device, self.seed)
+        return self.replay
+
+    def ready(self):
+        return self.replay is not None and self.replay.cnt >= self.sample_start
+
+    def check_ready(self):
+        if not self.ready():
+            cnt = 0 if self.replay is None else self.replay.cnt
+            raise RuntimeError(f"replay not ready: cnt={cnt} < sample_start={self.sample_start} "
+                               "(the reference sampler would block here)")
+
+    # Process-like surface used by the reference's launch scripts
+    def terminate(self):
+        self.alive = False
+        self.replay = None
+
+    def join(self, timeout=None):
+        return None
+
+    def is_alive(self):
+        return self.alive
+
+
+def _lookup(addr):
+    try:
+        return _SERVICES[addr]
+    except KeyError:
+        raise ValueError(f"unknown replay address {addr!r} (services live in the process that started them)")
+
+
+def start_server(capacity, batch_size, host=None, port=None, samplers=None, cache_policy=None, *,
+                 device=None, seed=0, widen_u8=False):
+    """reth_buffer.start_server (__init__.py:11-27) -> (service, address)."""
+    if cache_policy is not None and type(cache_policy).__name__ != "FIFOPolicy":
+        raise NotImplementedError("only the FIFO cache policy is implemented (fifo_policy.py)")
+    if samplers is None:
+        samplers = [{"sampler_cls": "PERSampler", "num_procs": 1, "sample_start": 1000}]
+    if len(samplers) != 1:
+        raise NotImplementedError("one sampler topic per shard")
+    s = samplers[0]
+    name = s["sampler_cls"] if isinstance(s["sampler_cls"], str) else s["sampler_cls"].__name__
+    if name != "PERSampler":
+        raise NotImplementedError(f"sampler {name} (only PERSampler is on the Ape-X path)")
+    svc = ReplayService(capacity, batch_size, s, device, seed, widen_u8)
+    addr = f"hbm://{svc.device.index}/{next(_ids)}"
+    _SERVICES[addr] = svc
+    return svc, addr
+
+
+def start_per(capacity, batch_size, alpha=0.6, beta=0.4, sample_start=1000, num_sampler_procs=1, host=None,
+              port=None, cache_policy=None, *, device=None, seed=0, widen_u8=False):
+    """reth_buffer.start_per (__init__.py:30-49) -> (service, address)."""
+    samplers = [{"sampler_cls": "PERSampler", "num_procs": num_sampler_procs, "sample_start": sample_start,
+                 "kwargs": {"alpha": alpha, "beta": beta}}]
+    return start_server(capacity, batch_size, host, port, samplers, cache_policy, device=device, seed=seed,
+                        widen_u8=widen_u8)
+
+
+class Client:
+    """client/client.py:8-39."""
+
+    def __init__(self, meta_addr):
+        self.svc = _lookup(meta_addr)
+
+    def append(self, data, weights, compress=False):
+        assert isinstance(data, (list, tuple))
+        n = len(weights)
+        for col in data:
+            assert isinstance(col, np.ndarray) or torch.is_tensor(col)
+            assert len(col) == n
+        rep = self.svc.ensure(data)
+        dev = rep.device
+        cols = [as_device(c, col.dtype, dev) for c, col in zip(data, rep.columns)]
+        rep.append(cols, weights)
+
+    def update_priorities(self, indices, weights, step=True):
+        assert len(indices) == len(weights)
+        if self.svc.replay is None:
+            raise RuntimeError("update_priorities before any append")
+        self.svc.replay.update_priorities(indices, weights, step=step)
+
+
+class NumpyLoader:
+    """client/numpy_loader.py:8-56: (list of np columns, np.int64 indices, np.float64 weights)."""
+
+    def __init__(self, meta_addr, topic="default"):
+        self.svc = _lookup(meta_addr)
+
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        return self.sample()
+
+    def sample(self):
+        self.svc.check_ready()
+        cols, idx, isw = self.svc.replay.sample(self.svc.batch_size)
+        return [c.cpu().numpy() for c in cols], idx.cpu().numpy(), isw.cpu().numpy()
+
+
+class TorchCudaLoader:
+    """client/torch_cuda_loader.py:69-163: a ring of `buffer_size` pre-allocated device slots;
+    sample() returns views into one slot, valid until the next call (the reference recycles a
+    slot on the next sample(), :153-155)."""
+
+    def __init__(self, meta_addr, topic="default", buffer_size=8, num_procs=6, prefetch=1):
+        self.svc = _lookup(meta_addr)
+        self.prefetch = int(prefetch)
+        self.buffer_size = max(self.prefetch + 1, int(buffer_size))
+        self._slots = None
+        self._next = 0
+        self._pending = []  # slot ids already sampled, oldest first
+
+    def _issue(self):
+        rep = self.svc.replay
+        if self._slots is None:
+            self._slots = [rep.new_batch(self.svc.batch_size) for _ in range(self.buffer_size)]
+        k = self._next
+        self._next = (self._next + 1) % self.buffer_size
+        cols, idx, isw = self._slots[k]
+        rep.sample_into(self.svc.batch_size, cols, idx, isw)
+        self._pending.append(k)
+
+    def sample_device(self):
+        """(data, device int64 indices, device f64 weights) without any host sync."""
+        self.svc.check_ready()
+        if not self._pending:
+            self._issue()
+        k = self._pending.pop(0)
+        while len(self._pending) < self.prefetch:  # sample-ahead: batch k+1 is drawn before
+            self._issue()                          # batch k's priority update is enqueued
+        cols, idx, isw = self._slots[k]
+        return cols, idx, isw
+
+    def sample(self):
+        cols, idx, isw = self.sample_device()
+        return cols, idx.cpu().numpy(), isw
+
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        return self.sample()
+
+    def close(self):
+        self._slots = None

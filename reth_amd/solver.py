@@ -1,0 +1,227 @@
+"""DQN solver on MI355X: reth.algorithm.DQNSolver's interface, fused HIP TD/Huber op.
+
+Reference: reth/reth/algorithm/dqn/dqn_solver.py:14-143 (and algorithm/algorithm.py:6-30).
+
+The Q-network forward/backward is PyTorch-ROCm (fp32, MFMA through MIOpen/hipBLASLt).  The
+TD error, double-Q target, Huber loss, IS weighting, mean, |td| and the gradient with
+respect to Q(s0) are ONE HIP kernel (rth_td_huber) wrapped as an autograd Function, so
+  * the loss' backward starts from the kernel's d(loss)/d(Q(s0)) -- no chain of small torch
+    ops and their backward kernels;
+  * |td| stays in HBM for the priority update (update_device); the reference-compatible
+    update() still returns it as a CPU tensor (`td_error.detach().cpu().abs()`, :109).
+"""
+import io
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import call, ptr, stream_ptr
+from .model import default_models
+from .schedule import Interval
+
+
+class Discrete:
+    """minimal gym.spaces.Discrete (gym is not part of this image)"""
+
+    def __init__(self, n):
+        self.n = int(n)
+
+
+class Box:
+    """minimal gym.spaces.Box"""
+
+    def __init__(self, low, high, shape, dtype=None):
+        self.low, self.high, self.shape = low, high, tuple(shape)
+
+
+def _check_device(device):
+    dev = torch.device(device if device is not None else "cuda")
+    if dev.type != "cuda":
+        raise ValueError(f"reth_amd.DQNSolver runs on the GPU (HIP) only, got device={dev}; "
+                         "actors are vectorised on the device (reth_amd.actors)")
+    if not torch.cuda.is_available():
+        raise RuntimeError("no HIP device visible")
+    return torch.device("cuda", dev.index if dev.index is not None else torch.cuda.current_device())
+
+
+def td_huber_forward(q_s0, q_s1_online, q_s1_target, a, r, done, isw, gamma_n, double_q, want_dq):
+    """One rth_td_huber launch -> (loss[1], td_abs[B], dq[B,A] or None)."""
+    B, A = q_s0.shape
+    for t, name in ((q_s0, "q_s0"), (q_s1_target, "q_s1_target")):
+        if t.dtype != torch.float32 or not t.is_cuda or t.shape != (B, A):
+            raise ValueError(f"{name} must be a float32 device tensor of shape {(B, A)}")
+    if double_q and (q_s1_online is None or q_s1_online.shape != (B, A)):
+        raise ValueError("double_q needs q_s1_online of the same shape")
+    dev = q_s0.device
+    q0 = q_s0.detach().contiguous()
+    q1o = None if q_s1_online is None else q_s1_online.detach().contiguous()
+    q1t = q_s1_target.detach().contiguous()
+    a = a.to(device=dev, dtype=torch.int64).contiguous().view(-1)
+    r = r.to(device=dev, dtype=torch.float32).contiguous().view(-1)
+    done = done.to(device=dev, dtype=torch.float32).contiguous().view(-1)
+    if isw is not None:
+        isw = isw.to(device=dev, dtype=torch.float64).contiguous().view(-1)
+    if a.numel() != B or r.numel() != B or done.numel() != B or (isw is not None and isw.numel() != B):
+        raise ValueError("batch columns disagree in length")
+    td_abs = torch.empty(B, dtype=torch.float32, device=dev)
+    loss = torch.empty(1, dtype=torch.float32, device=dev)
+    dq = torch.empty((B, A), dtype=torch.float32, device=dev) if want_dq else None
+    call("rth_td_huber", ptr(q0), ptr(q1o), ptr(q1t), ptr(a), ptr(r), ptr(done), ptr(isw), B, A,
+         float(gamma_n), int(bool(double_q)), None, ptr(td_abs), None, ptr(loss), ptr(dq), stream_ptr())
+    return loss, td_abs, dq
+
+
+class _TDHuber(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q_s0, q_s1_online, q_s1_target, a, r, done, isw, gamma_n, double_q):
+        loss, td_abs, dq = td_huber_forward(q_s0, q_s1_online, q_s1_target, a, r, done, isw, gamma_n, double_q,
+                                            want_dq=True)
+        ctx.save_for_backward(dq)
+        ctx.mark_non_differentiable(td_abs)
+        return loss.view(()), td_abs
+
+    @staticmethod
+    def backward(ctx, g_loss, g_td):
+        (dq,) = ctx.saved_tensors
+        return dq * g_loss, None, None, None, None, None, None, None, None
+
+
+def td_huber_loss(q_s0, q_s1_online, q_s1_target, a, r, done, isw, gamma_n, double_q=True):
+    """(mean IS-weighted Huber loss [differentiable w.r.t. q_s0], |td| [B])"""
+    return _TDHuber.apply(q_s0, q_s1_online, q_s1_target, a, r, done, isw, gamma_n, double_q)
+
+
+class Algorithm:
+    """reth/reth/algorithm/algorithm.py:6-30 (device defaults to the current GPU)."""
+
+    def __init__(self, device=None):
+        self.device = _check_device(device)
+
+    def update(self, batch, weights=None):
+        raise NotImplementedError
+
+    def act(self, state):
+        raise NotImplementedError
+
+    def load_weights(self, stream):
+        raise NotImplementedError
+
+    def save_weights(self, stream=None):
+        raise NotImplementedError
+
+
+class DQNSolver(Algorithm):
+    """reth/reth/algorithm/dqn/dqn_solver.py:14-143 with the same constructor arguments.
+
+    grad_hook(params) runs between backward and clip/Adam: the data-parallel learner uses it
+    for the RCCL gradient all-reduce (reth_amd/dist.py)."""
+
+    def __init__(self, observation_space, action_space, models=None, gamma=0.99, clip_value=40, double_q=True,
+                 dueling=True, learning_rate=5e-5, adam_epsilon=1e-8, update_target_interval=150, device=None,
+                 n_step=1, fused_adam=True, grad_hook=None):
+        super().__init__(device)
+        obs_shape = tuple(observation_space.shape)
+        self.num_actions = int(action_space.n)
+        if models is None:
+            models = default_models(obs_shape, self.num_actions, dueling, learning_rate, adam_epsilon, fused_adam)
+        assert models["q_network"] is not None and models["target_q_network"] is not None
+        self.q_network = models["q_network"].to(self.device)
+        self.target_q_network = models["target_q_network"].to(self.device)
+        self.target_q_network.requires_grad_(False)
+        if models.get("optimizer") is not None:
+            self.optimizer = models["optimizer"]
+        else:
+            kw = {"fused": True} if models.get("fused_adam", fused_adam) else {}
+            self.optimizer = torch.optim.Adam(self.q_network.parameters(), lr=models.get("learning_rate", learning_rate),
+                                              eps=models.get("adam_epsilon", adam_epsilon), **kw)
+        self._params = [p for p in self.q_network.parameters()]
+        self._tparams = [p for p in self.target_q_network.parameters()]
+        self.update_target()
+        self.clip_value = clip_value
+        self.double_q = double_q
+        self.gamma = gamma
+        self.n_step = n_step
+        self.gamma_n = float(np.float32(gamma ** n_step))  # python float -> f32 scalar (:96)
+        self.grad_hook = grad_hook
+        self._update_target_interval = (Interval(self.update_target, update_target_interval)
+                                        if update_target_interval is not None else None)
+
+    # ------------------------------------------------------------------ target / weights
+    @torch.no_grad()
+    def update_target(self):
+        """target <- online (:65-66), one fused device copy"""
+        torch._foreach_copy_(self._tparams, self._params)
+
+    def load_weights(self, stream):
+        states = torch.load(stream, map_location=self.device, weights_only=True)
+        self.q_network.load_state_dict(states)
+        self.update_target()
+
+    def save_weights(self, stream=None):
+        if stream is None:
+            stream = io.BytesIO()
+        torch.save(self.q_network.state_dict(), stream)
+        return stream
+
+    # ------------------------------------------------------------------ TD
+    def _tensors(self, batch):
+        s0, a, r, s1, done = batch
+        dev = self.device
+        f = lambda x, dt: (x.to(device=dev, dtype=dt, non_blocking=True) if torch.is_tensor(x)
+                           else torch.as_tensor(np.asarray(x), dtype=dt).to(dev, non_blocking=True))
+        return f(s0, torch.float32), f(a, torch.int64), f(r, torch.float32), f(s1, torch.float32), f(done, torch.float32)
+
+    def _forward_targets(self, s1):
+        with torch.no_grad():
+            q1t = self.target_q_network(s1)
+            q1o = self.q_network(s1) if self.double_q else None
+        return q1o, q1t
+
+    def calc_loss_device(self, batch):
+        """|td| on the device without an update (:100-102)"""
+        s0, a, r, s1, done = self._tensors(batch)
+        with torch.no_grad():
+            q0 = self.q_network(s0)
+        q1o, q1t = self._forward_targets(s1)
+        _, td_abs, _ = td_huber_forward(q0, q1o, q1t, a, r, done, None, self.gamma_n, self.double_q, want_dq=False)
+        return td_abs
+
+    def calc_loss(self, batch):
+        return self.calc_loss_device(batch).cpu()
+
+    def update_device(self, batch, weights=None):
+        """DQNSolver.update (:104-124) returning |td| as a device tensor (no host sync)."""
+        s0, a, r, s1, done = self._tensors(batch)
+        q0 = self.q_network(s0)
+        q1o, q1t = self._forward_targets(s1)
+        isw = None if weights is None else (weights if torch.is_tensor(weights) else torch.as_tensor(np.asarray(weights)))
+        loss, td_abs = td_huber_loss(q0, q1o, q1t, a, r, done, isw, self.gamma_n, self.double_q)
+        self.optimizer.zero_grad(set_to_none=False)
+        loss.backward()
+        if self.grad_hook is not None:
+            self.grad_hook(self._params)
+        if self.clip_value >= 0:
+            torch.nn.utils.clip_grad_norm_(self._params, self.clip_value, foreach=True)
+        self.optimizer.step()
+        if self._update_target_interval is not None:
+            self._update_target_interval()
+        self.last_loss = loss.detach()
+        return td_abs
+
+    def update(self, batch, weights=None):
+        return self.update_device(batch, weights).cpu()
+
+    # ------------------------------------------------------------------ acting
+    @torch.no_grad()
+    def act(self, state):
+        x = torch.as_tensor(np.asarray(state), dtype=torch.float32).to(self.device).unsqueeze(0) \
+            if not torch.is_tensor(state) else state.to(self.device, torch.float32).unsqueeze(0)
+        return int(torch.argmax(self.q_network(x), dim=1).item())
+
+
+def get_solver(name, **kwargs):
+    """reth/reth/algorithm/__init__.py:17-21 (only the DQN path is rebuilt)"""
+    if name != "dqn":
+        raise NotImplementedError(f"solver {name!r}: only 'dqn' is on the Ape-X hot path")
+    return DQNSolver(**kwargs)

@@ -1,0 +1,69 @@
+"""Learner wrapper: reth/reth/presets/trainer.py:9-74 (Trainer).
+
+Same surface (step/print/cur_time/save_weights/load_weights/on_step_end).  The mean |td|
+used for the periodic log line is accumulated on the device and only read when a line is
+printed, so step() adds no host synchronisation beyond what the solver call itself does.
+"""
+import logging
+import sys
+import time
+
+import torch
+
+from .schedule import Interval
+
+
+def getLogger(name, level=logging.DEBUG):
+    """reth/reth/utils/__init__.py:8-20"""
+    logger = logging.getLogger(name)
+    logger.setLevel(level)
+    if not logger.handlers:
+        h = logging.StreamHandler(sys.stderr)
+        h.setLevel(level)
+        h.setFormatter(logging.Formatter("[%(asctime)s][%(name)s][%(levelname)s] %(message)s"))
+        logger.addHandler(h)
+    return logger
+
+
+class Trainer:
+    def __init__(self, solver, logger=None, print_interval=300):
+        self.solver = solver
+        self.logger = logger if logger is not None else getLogger("trainer")
+        self.cur_step = 0
+        self.start_time = None
+        self.on_step_end = [Interval(self.print, int(print_interval))]
+        self._err_sum = None
+        self._err_n = 0
+
+    @property
+    def cur_time(self):
+        return 0 if self.start_time is None else time.monotonic() - self.start_time
+
+    def print(self):
+        if self.logger and self._err_n:
+            mean = float(self._err_sum) / self._err_n
+            self.logger.info(f"train_cnt: {self.cur_step}, mean_error: {mean:.3f}, time: {self.cur_time:.2f}")
+        self._err_sum, self._err_n = None, 0
+
+    def load_weights(self, stream):
+        self.solver.load_weights(stream)
+
+    def save_weights(self, stream=None):
+        return self.solver.save_weights(stream)
+
+    def _track(self, td):
+        m = td.float().mean() if torch.is_tensor(td) else torch.tensor(float(td.mean()))
+        self._err_sum = m if self._err_sum is None else self._err_sum + m
+        self._err_n += 1
+
+    def step(self, batch, device_result=False, **kwargs):
+        """one learner update; returns |td| (CPU tensor like the reference, or the device
+        tensor with device_result=True)."""
+        if self.start_time is None:
+            self.start_time = time.monotonic()
+        self.cur_step += 1
+        td = self.solver.update_device(batch, **kwargs)
+        self._track(td)
+        for f in self.on_step_end:
+            f()
+        return td if device_result else td.cpu()

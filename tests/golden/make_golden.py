@@ -1,0 +1,412 @@
+"""Generate the golden vectors under tests/golden/ from the reference itself.
+
+Run ONCE in the build container (where /root/reference exists):
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+
+It loads the reference's own Python modules (read-only, no bytecode written) with the
+import shims described in SURVEY.md Appendix B (numba.njit -> identity, a minimal
+gym.spaces, namespace packages that skip reth/__init__.py), runs them on seeded inputs
+and writes inputs + outputs as small .npz/.json fixtures.  Nothing here is imported by
+the product, by the GPU tests or by bench.py: only the committed fixtures travel.
+
+Reference functions exercised (paths relative to /root/reference):
+  reth_buffer/reth_buffer/utils/sumtree.py:5-113      NumbaSumTree, _numba_*  (live PER tree)
+  reth_buffer/reth_buffer/sampler/per_sampler.py:5-35 PERSampler
+  reth_buffer/reth_buffer/utils/schedule.py:4-52      Schedule
+  reth_buffer/reth_buffer/cache_policy/fifo_policy.py FIFOPolicy
+  reth/reth/utils/nstep_adder.py:5-28                 NStepAdder
+  reth/reth/algorithm/dqn/dqn_solver.py:14-143        DQNSolver (calc_loss / update / act)
+  reth/reth/algorithm/dqn/dqn_model.py:6-99           DQNNetwork / MLP_DQNNetwork
+
+numba's JIT is replaced by plain Python: njit without fastmath is IEEE with the same
+operation order, so the deterministic arithmetic is identical; numba's private RNG stream
+is not reproduced, so every sample fixture records its uniforms explicitly.
+"""
+import hashlib
+import importlib.util
+import json
+import os
+import sys
+import types
+
+sys.dont_write_bytecode = True
+
+import numpy as np
+
+REF = os.environ.get("RETH_REFERENCE", "/root/reference")
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+# ----------------------------------------------------------------------------- shims
+def _install_shims():
+    numba = types.ModuleType("numba")
+    numba.njit = lambda f=None, **kw: (f if f is not None else (lambda g: g))
+    sys.modules["numba"] = numba
+
+    gym = types.ModuleType("gym")
+    spaces = types.ModuleType("gym.spaces")
+
+    class Discrete:
+        def __init__(self, n):
+            self.n = n
+
+    class Box:
+        def __init__(self, low, high, shape, dtype=None):
+            self.low, self.high, self.shape = low, high, tuple(shape)
+
+    spaces.Discrete, spaces.Box = Discrete, Box
+    gym.spaces = spaces
+    gym.Env = object
+    sys.modules["gym"] = gym
+    sys.modules["gym.spaces"] = spaces
+
+
+def _pkg(name):
+    m = types.ModuleType(name)
+    m.__path__ = []
+    sys.modules[name] = m
+    return m
+
+
+def _load(modname, relpath):
+    spec = importlib.util.spec_from_file_location(modname, os.path.join(REF, relpath))
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules[modname] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def load_reference():
+    _install_shims()
+    R = types.SimpleNamespace()
+    # reth_buffer live tree + PER sampler + schedule + FIFO
+    _pkg("rb")
+    rbu = _pkg("rb.utils")
+    R.sumtree = _load("rb.utils.sumtree", "reth_buffer/reth_buffer/utils/sumtree.py")
+    R.schedule = _load("rb.utils.schedule", "reth_buffer/reth_buffer/utils/schedule.py")
+    rbu.NumbaSumTree = R.sumtree.NumbaSumTree
+    rbu.Schedule = R.schedule.Schedule
+    _pkg("rb.sampler")
+    _load("rb.sampler.base_sampler", "reth_buffer/reth_buffer/sampler/base_sampler.py")
+    R.per = _load("rb.sampler.per_sampler", "reth_buffer/reth_buffer/sampler/per_sampler.py")
+    _pkg("rb.cache_policy")
+    _load("rb.cache_policy.base_policy", "reth_buffer/reth_buffer/cache_policy/base_policy.py")
+    R.fifo = _load("rb.cache_policy.fifo_policy", "reth_buffer/reth_buffer/cache_policy/fifo_policy.py")
+    # reth: utils + dqn (skip reth/__init__.py, which imports env -> gym/cv2)
+    _pkg("reth")
+    _pkg("reth.utils").__path__ = [os.path.join(REF, "reth/reth/utils")]
+    R.rutils = _load("reth.utils", "reth/reth/utils/__init__.py")
+    alg = _pkg("reth.algorithm")
+    R.algorithm = _load("reth.algorithm.algorithm", "reth/reth/algorithm/algorithm.py")
+    alg.Algorithm = R.algorithm.Algorithm
+    _load("reth.algorithm.util", "reth/reth/algorithm/util.py")
+    _pkg("reth.algorithm.dqn")
+    R.dqn_model = _load("reth.algorithm.dqn.dqn_model", "reth/reth/algorithm/dqn/dqn_model.py")
+    R.dqn_solver = _load("reth.algorithm.dqn.dqn_solver", "reth/reth/algorithm/dqn/dqn_solver.py")
+    R.gym = sys.modules["gym"]
+    return R
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+# ----------------------------------------------------------------------------- sum-tree
+def tree_state(t):
+    return t._sum.copy(), t._min.copy(), t._val.copy()
+
+
+def gen_sumtree_small(R):
+    out = {}
+    rng = np.random.default_rng(1)
+    NumbaSumTree = R.sumtree.NumbaSumTree
+    find = R.sumtree._numba_find_index
+
+    def record(tag, t, updates, targets, sample_b=None, seed=0):
+        s, m, v = tree_state(t)
+        out[f"{tag}/capacity"] = np.int64(t.capacity)
+        out[f"{tag}/sum"], out[f"{tag}/min"], out[f"{tag}/val"] = s, m, v
+        out[f"{tag}/tree_min"] = np.float64(t.min())
+        out[f"{tag}/targets"] = np.asarray(targets, np.float64)
+        out[f"{tag}/find"] = np.array([find(t._tree, w) for w in targets], np.int64)
+        for k, (idx, w) in enumerate(updates):
+            out[f"{tag}/upd{k}_idx"] = np.asarray(idx, np.int64)
+            out[f"{tag}/upd{k}_w"] = np.asarray(w, np.float64)
+        out[f"{tag}/n_upd"] = np.int64(len(updates))
+        if sample_b:
+            np.random.seed(seed)
+            u = np.random.random_sample(sample_b)
+            np.random.seed(seed)
+            idx, vals = t.sample(sample_b)
+            out[f"{tag}/sample_u"], out[f"{tag}/sample_idx"], out[f"{tag}/sample_val"] = u, idx, vals
+
+    def run(cap, updates):
+        t = NumbaSumTree(cap)
+        for idx, w in updates:
+            t.update(np.asarray(idx), np.asarray(w))
+        return t
+
+    # A: C=10, all ones -> in-order mass mapping [7,3,8,1,9,4,0,5,2,6]
+    ups = [(np.arange(10), np.ones(10))]
+    t = run(10, ups)
+    tg = [k + 0.5 for k in range(10)] + [10.0, 10.5, 100.0, 0.0, 9.999995, 2.99999]
+    record("c10", t, ups, tg, sample_b=10, seed=3)
+    # B: C=5, targets at/after the total (return last in-order node)
+    ups = [(np.arange(5), np.array([0.5, 1.5, 0.25, 2.0, 1.0]))]
+    t = run(5, ups)
+    record("c5", t, ups, [0.0, 0.49, 0.5, 5.25, 5.2499999, 6.0, 1e9], sample_b=5, seed=4)
+    # C: C=1, degenerate
+    ups = [(np.array([0]), np.array([0.7]))]
+    t = run(1, ups)
+    record("c1", t, ups, [0.0, 0.69, 0.7, 5.0], sample_b=3, seed=5)
+    # D: C=1000, partial fill with exact zeros, then duplicate-heavy updates touching
+    #    never-filled slots (exercises the min() seed quirk, sumtree.py:11-19)
+    w0 = rng.random(600)
+    w0[::37] = 0.0
+    up1 = (np.arange(600), w0)
+    idx2 = rng.integers(0, 1000, 300)
+    idx2[:20] = idx2[20:40]  # forced duplicates (last writer wins)
+    w2 = rng.random(300)
+    w2[::11] = 0.0
+    ups = [up1, (idx2, w2)]
+    t = run(1000, ups)
+    tot = t.sum()
+    tg = list(rng.random(50) * tot) + [tot, tot * (1 - 1e-12), tot + 1.0, 0.0]
+    record("c1000", t, ups, tg, sample_b=64, seed=6)
+    # E: C=3000, 1200 filled in FIFO chunks of 64 (append path), then 512 updates with
+    #    duplicates (learner path) -- SURVEY App. A.2 probe shape
+    ups = []
+    for s in range(0, 1200, 64):
+        n = min(64, 1200 - s)
+        ups.append((np.arange(s, s + n), (rng.random(n).astype(np.float32) + np.float32(1e-6)) ** 0.5))
+    idx = rng.integers(0, 1200, 512)
+    ups.append((idx, rng.random(512)))
+    t = run(3000, ups)
+    tg = list(rng.random(100) * t.sum())
+    record("c3000", t, ups, tg, sample_b=512, seed=7)
+    # F: C=4097 (ragged last level), full random then a sparse re-update incl. zeros
+    ups = [(np.arange(4097), rng.random(4097)), (rng.integers(0, 4097, 1000), np.where(rng.random(1000) < 0.1, 0.0, rng.random(1000)))]
+    t = run(4097, ups)
+    record("c4097", t, ups, list(rng.random(200) * t.sum()), sample_b=128, seed=8)
+    np.savez_compressed(os.path.join(OUT, "sumtree_small.npz"), **out)
+
+
+def gen_sumtree_large(R):
+    """Pong-depth tree (C=2^20, 21 levels): FIFO fill in 256-row appends + 40 learner
+    updates of 512 indices.  Inputs are regenerated from the seed by the test
+    (np.random.default_rng is stable); outputs stored as hashes + one sampled batch."""
+    seed, cap, chunk, n_learn, B = 20, 1 << 20, 256, 40, 512
+    rng = np.random.default_rng(seed)
+    t = R.sumtree.NumbaSumTree(cap)
+    per_norm = lambda w: (w + np.float32(1e-6)) ** np.float32(0.5)
+    for s in range(0, cap, chunk):
+        td = rng.random(chunk, dtype=np.float32)
+        t.update(np.arange(s, s + chunk, dtype=np.int64), per_norm(td))
+    for _ in range(n_learn):
+        idx = rng.integers(0, cap, B)
+        td = rng.random(B, dtype=np.float32) * np.float32(3.0)
+        t.update(idx, per_norm(td))
+    np.random.seed(seed)
+    u = np.random.random_sample(B)
+    np.random.seed(seed)
+    sidx, sval = t.sample(B)
+    out = dict(seed=np.int64(seed), capacity=np.int64(cap), chunk=np.int64(chunk),
+               n_learn=np.int64(n_learn), batch=np.int64(B), sample_u=u,
+               sample_idx=sidx, sample_val=sval, total=np.float64(t.sum()),
+               tree_min=np.float64(t.min()))
+    out["sha_sum"], out["sha_min"], out["sha_val"] = sha(t._sum), sha(t._min), sha(t._val)
+    np.savez_compressed(os.path.join(OUT, "sumtree_large.npz"), **out)
+
+
+# ----------------------------------------------------------------------------- PER
+def gen_per(R):
+    out = {}
+    rng = np.random.default_rng(2)
+    for alpha, tag in ((0.5, "a05"), (0.6, "a06")):
+        s = R.per.PERSampler(2000, alpha=alpha, beta="0.4,1,2000000")
+        w = rng.random(4000, dtype=np.float32) * np.float32(4.0)
+        w[:5] = [0.0, 1e-7, 1.0, 3.5, 1e-30]
+        norm = s._normalize_weights(w)
+        out[f"{tag}/w"], out[f"{tag}/norm"] = w, norm
+        # append 1500 rows in 64-row messages, then 8 learner steps (on_step + update)
+        for st in range(0, 1500, 64):
+            n = min(64, 1500 - st)
+            s.update(np.arange(st, st + n, dtype=np.int32), w[st:st + n])
+        betas, samples = [], []
+        for k in range(8):
+            np.random.seed(100 + k)
+            u = np.random.random_sample(64)
+            np.random.seed(100 + k)
+            idx, isw = s.sample(64)
+            out[f"{tag}/s{k}_u"], out[f"{tag}/s{k}_idx"], out[f"{tag}/s{k}_isw"] = u, idx, isw
+            betas.append(s.beta.value())
+            s.on_step()
+            s.update(idx, w[1500 + 64 * k: 1564 + 64 * k])
+        out[f"{tag}/betas"] = np.array(betas)
+        out[f"{tag}/alpha_f32"] = np.float32(alpha)
+        out[f"{tag}/final_sha_sum"] = sha(s.sumtree._sum)
+        out[f"{tag}/final_sha_val"] = sha(s.sumtree._val)
+        out[f"{tag}/final_sum"] = np.float64(s.sumtree.sum())
+        out[f"{tag}/final_min"] = np.float64(s.sumtree.min())
+    np.savez_compressed(os.path.join(OUT, "per.npz"), **out)
+
+
+# ----------------------------------------------------------------------------- schedule / FIFO
+def gen_schedule_fifo(R):
+    S = R.schedule.Schedule
+    steps = [0, 1, 2, 3, 10, 999, 1000, 1001, 123457, 1999999, 2000000, 2000001, 5000000]
+    res = {"steps": steps, "cases": []}
+    for spec in ["0.4,1,2000000", "linear,0.4,1,2000000", "exp,1,0.01,1000", "1,0.01,100000", 0.5, 3]:
+        sch = S.from_str(spec)
+        vals = [sch.value(k) for k in steps]
+        seq = [sch.step() for _ in range(5)]
+        res["cases"].append({"spec": spec, "value": [float(x).hex() for x in vals],
+                             "step_seq": [float(x).hex() for x in seq]})
+    bad = []
+    for spec in ["0.5", "a,b", "cubic,0,1,10"]:
+        try:
+            S.from_str(spec)
+            bad.append({"spec": spec, "raises": False})
+        except Exception:
+            bad.append({"spec": spec, "raises": True})
+    res["invalid"] = bad
+    fifo = R.fifo.FIFOPolicy(10)
+    res["fifo_capacity"] = 10
+    res["fifo_requests"] = [3, 4, 7, 10, 1]
+    res["fifo_indices"] = [fifo.get_indices(n).tolist() for n in res["fifo_requests"]]
+    with open(os.path.join(OUT, "schedule_fifo.json"), "w") as f:
+        json.dump(res, f, indent=1)
+
+
+# ----------------------------------------------------------------------------- n-step
+def gen_nstep(R):
+    """Streams through the reference NStepAdder (numpy-2 / NEP 50 scalar semantics in this
+    container: the f32 product t_gamma*r stays f32)."""
+    out = {"numpy_version": np.array(np.__version__)}
+    rng = np.random.default_rng(3)
+    streams = {
+        "nodone": np.zeros(12),
+        "done_t2": np.array([0, 0, 1, 0, 0, 0, 0, 0]),
+        "done_each3": np.array([0, 0, 1] * 5),
+        "done_adjacent": np.array([0, 1, 1, 0, 1, 0, 0, 1, 0, 0]),
+        "random": (rng.random(300) < 0.08).astype(np.float64),
+    }
+    for n_step in (1, 3, 5):
+        for name, dones in streams.items():
+            tag = f"n{n_step}/{name}"
+            T = len(dones)
+            rewards = np.where(rng.random(T) < 0.5, rng.choice([-1.0, 1.0], T), rng.random(T) * 2 - 1).astype(np.float32)
+            if name == "done_t2":
+                rewards[:] = 1.0
+            actions = rng.integers(0, 6, T)
+            adder = R.rutils.NStepAdder(0.99, n_step)
+            rows = []
+            for t in range(T):
+                row = adder.push(np.asarray(t, "f4"), np.asarray(actions[t], "i8"), np.asarray(rewards[t], "f4"),
+                                 np.asarray(t + 1000, "f4"), np.asarray(dones[t], "f4"))
+                if row is not None:
+                    rows.append((t, float(row[0]), int(row[1]), np.float32(row[2]), float(row[3]), float(row[4])))
+            out[f"{tag}/rewards"], out[f"{tag}/actions"], out[f"{tag}/dones"] = rewards, actions.astype(np.int64), dones.astype(np.float32)
+            arr = np.array([(r[0], r[1], r[2], r[4], r[5]) for r in rows], dtype=np.float64).reshape(-1, 5)
+            out[f"{tag}/emit_t"] = arr[:, 0].astype(np.int64)
+            out[f"{tag}/emit_s0"] = arr[:, 1].astype(np.int64)
+            out[f"{tag}/emit_a"] = arr[:, 2].astype(np.int64)
+            out[f"{tag}/emit_r"] = np.array([r[3] for r in rows], np.float32)
+            out[f"{tag}/emit_s1"] = (arr[:, 3] - 1000).astype(np.int64)
+            out[f"{tag}/emit_done"] = arr[:, 4].astype(np.float32)
+    np.savez_compressed(os.path.join(OUT, "nstep.npz"), **out)
+
+
+# ----------------------------------------------------------------------------- DQN
+def _param_stats(net):
+    names, s1, s2, head = [], [], [], []
+    for k, v in net.state_dict().items():
+        v = v.detach().double().flatten()
+        names.append(k)
+        s1.append(float(v.sum()))
+        s2.append(float((v * v).sum()))
+        h = np.full(16, np.nan, np.float32)
+        x = v[:16].float().numpy()
+        h[: len(x)] = x
+        head.append(h)
+    return names, np.array(s1), np.array(s2), head
+
+
+def gen_dqn(R):
+    import torch
+    torch.set_num_threads(4)
+    gym = R.gym
+    DQNSolver = R.dqn_solver.DQNSolver
+
+    # --- Pong-shaped conv net, A=6, B=8 (apex-dqn config.yaml hyper-parameters)
+    for B, tag in ((8, "pong_b8"), (32, "pong_b32")):
+        seed = 1234 + B
+        torch.manual_seed(seed)
+        solver = DQNSolver(gym.spaces.Box(0, 255, (4, 84, 84)), gym.spaces.Discrete(6), gamma=0.99,
+                           clip_value=40, double_q=True, dueling=True, learning_rate=1e-4,
+                           adam_epsilon=1.5e-4, update_target_interval=100, device="cpu", n_step=3)
+        rng = np.random.default_rng(seed)
+        s0 = rng.integers(0, 256, (B, 4, 84, 84), dtype=np.uint8)
+        s1 = rng.integers(0, 256, (B, 4, 84, 84), dtype=np.uint8)
+        a = rng.integers(0, 6, B).astype(np.int64)
+        r = rng.choice(np.array([-1.0, 0.0, 1.0], np.float32), B).astype(np.float32)
+        done = (rng.random(B) < 0.25).astype(np.float32)
+        isw = rng.random(B) + 0.2  # f64, as the sampler produces
+        batch = [s0.astype("f4"), a, r, s1.astype("f4"), done]
+        out = dict(seed=np.int64(seed), s0=s0, s1=s1, a=a, r=r, done=done, isw=isw)
+        names, p1, p2, head = _param_stats(solver.q_network)
+        out["init_sum"], out["init_sq"] = p1, p2
+        with torch.no_grad():
+            tq = lambda x: torch.as_tensor(x)
+            out["q_s0"] = solver.q_network(tq(batch[0])).numpy()
+            out["q_s1_online"] = solver.q_network(tq(batch[3])).numpy()
+            out["q_s1_target"] = solver.target_q_network(tq(batch[3])).numpy()
+            out["td"] = solver._calc_td_error(batch).numpy()
+        out["calc_loss"] = solver.calc_loss(batch).numpy()
+        out["act0"] = np.int64(solver.act(batch[0][0]))
+        # two updates (second one exercises Adam state); record returned |td| and params
+        for k in range(2):
+            out[f"upd{k}_abs_td"] = solver.update(batch, weights=isw).numpy()
+            names, p1, p2, head = _param_stats(solver.q_network)
+            out[f"upd{k}_sum"], out[f"upd{k}_sq"] = p1, p2
+            out[f"upd{k}_head"] = np.stack(head)
+        out["param_names"] = np.array(names)
+        np.savez_compressed(os.path.join(OUT, f"dqn_{tag}.npz"), **out)
+
+    # --- CartPole MLP, A=2, B=64: full post-update state_dict
+    seed = 77
+    torch.manual_seed(seed)
+    solver = DQNSolver(gym.spaces.Box(-1, 1, (4,)), gym.spaces.Discrete(2), gamma=0.99, clip_value=40,
+                       double_q=True, dueling=True, learning_rate=1e-4, update_target_interval=200,
+                       device="cpu")
+    rng = np.random.default_rng(seed)
+    B = 64
+    s0 = rng.standard_normal((B, 4)).astype(np.float32)
+    s1 = rng.standard_normal((B, 4)).astype(np.float32)
+    a = rng.integers(0, 2, B).astype(np.int64)
+    r = np.ones(B, np.float32)
+    done = (rng.random(B) < 0.1).astype(np.float32)
+    out = dict(seed=np.int64(seed), s0=s0, s1=s1, a=a, r=r, done=done)
+    for k, v in solver.q_network.state_dict().items():
+        out[f"init/{k}"] = v.numpy().copy()
+    batch = [s0, a, r, s1, done]
+    out["td"] = solver._calc_td_error(batch).detach().numpy()
+    for k in range(3):  # no IS weights (uniform replay, examples/dqn/run.py:29)
+        out[f"upd{k}_abs_td"] = solver.update(batch).numpy()
+    for k, v in solver.q_network.state_dict().items():
+        out[f"final/{k}"] = v.numpy().copy()
+    np.savez_compressed(os.path.join(OUT, "dqn_cartpole_b64.npz"), **out)
+
+
+def main():
+    R = load_reference()
+    which = sys.argv[1:] or ["sumtree_small", "sumtree_large", "per", "schedule_fifo", "nstep", "dqn"]
+    for w in which:
+        print("generating", w, flush=True)
+        globals()[f"gen_{w}"](R)
+    print("done")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,276 @@
+"""Ape-X DQN Pong benchmark: env-steps/s + learner updates/s on N MI355X (one process each).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    (N > 1 under: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+
+Workload (BASELINE.json configs[1]): per GPU 256 vectorised actors on a
+synthetic Pong-shaped env (uint8 4x84x84 frame stacks, A = 6; ALE is not on the box), a 1 M
+transition prioritized replay shard in HBM pre-filled to capacity, B = 512, n = 3,
+gamma = 0.99, alpha = 0.5, beta 0.4 -> 1 over 2 M, Adam lr 1e-4 eps 1.5e-4, clip 40, target
+every 100 updates, weights published every 10 (test/apex-dqn/config.yaml).  One step = 256
+env steps (act, env, n-step, priorities, insert) + one learner update (sample, gather, TD,
+backward, Adam, priority write-back), all fp32 / fp64 as in the reference.  N > 1 is weak
+scaling: every GPU runs the same per-GPU workload and the learner gradients are averaged
+with one RCCL all-reduce per update.
+
+The JSON line carries
+  roofline:      the replay gather kernel (dominant HIP kernel by bytes), timed live with
+                 HIP events on its launch stream; achieved = algorithmic bytes / mean launch
+  cpu_baseline:  the same step on the host cores (oracle restatement of the replay/tree/
+                 n-step path + torch-CPU Q-network), bounded sample, rank 0 at N = 1.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+STACK = 4 * 84 * 84
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+FP32_PEAK_TFLOPS = 157.3
+
+
+def gather_bytes_per_row():
+    """algorithmic bytes of one sampled apex row in rth_replay_gather: read s0/s1 uint8
+    stacks + a(8) r(4) done(4); write s0/s1 float32 stacks + a r done; 5 index reads"""
+    read = 2 * STACK + 8 + 4 + 4
+    write = 2 * STACK * 4 + 8 + 4 + 4
+    return read + write + 5 * 8
+
+
+def qnet_flops_per_sample(A=6):
+    """multiply-adds x2 of the Nature-DQN dueling net at 84x84"""
+    macs = 32 * 20 * 20 * 4 * 8 * 8 + 64 * 9 * 9 * 32 * 4 * 4 + 64 * 7 * 7 * 64 * 3 * 3 + 3136 * 256 * 2 + 256 * (A + 1)
+    return 2 * macs
+
+
+def load_traffic(tag):
+    p = os.path.join(ROOT, "profiles", f"traffic_{tag}.json")
+    if os.path.exists(p):
+        with open(p) as f:
+            return json.load(f).get("gather_hbm_bytes_per_launch")
+    return None
+
+
+# ----------------------------------------------------------------------------- CPU baseline
+def cpu_baseline(n_actors=256, batch=512, capacity=20000, iters=6, seed=0):
+    """The same Ape-X step on the host: torch-CPU Q-net (all host threads the job owns),
+    the oracle's C restatement for tree / PER / n-step / eps-greedy, numpy for the env and
+    row storage.  Replay capacity is reduced (host RAM, fill time); the per-step work is
+    the full configuration (256 actors, B = 512)."""
+    from oracle import oracle as orc
+    from reth_amd.model import DQNNetwork
+
+    torch.set_num_threads(min(16, len(os.sched_getaffinity(0))))
+    cores = torch.get_num_threads()
+    rng = np.random.default_rng(seed)
+    torch.manual_seed(seed)
+    qn, tq, an = (DQNNetwork((4, 84, 84), 6) for _ in range(3))
+    tq.load_state_dict(qn.state_dict())
+    an.load_state_dict(qn.state_dict())
+    opt = torch.optim.Adam(qn.parameters(), lr=1e-4, eps=1.5e-4)
+    s0s = rng.integers(0, 256, (capacity, 4, 84, 84), dtype=np.uint8)
+    s1s = rng.integers(0, 256, (capacity, 4, 84, 84), dtype=np.uint8)
+    acol = rng.integers(0, 6, capacity)
+    rcol = np.zeros(capacity, np.float32)
+    dcol = np.zeros(capacity, np.float32)
+    tree = orc.Tree(capacity)
+    tree.update(np.arange(capacity), orc.per_normalize(1.0 - rng.random(capacity, dtype=np.float32), 0.5)
+                .astype(np.float64))
+    tail = 0
+    obs = rng.integers(0, 256, (n_actors, 4, 84, 84), dtype=np.uint8)
+    eps = 0.4 ** (1 + np.arange(n_actors) / (n_actors - 1) * 7)
+    frames = {}  # handle -> stack (the reference's rows reference frames, never copy them)
+    n_handles = n_actors
+    obs_h = np.arange(n_actors, dtype=np.int64)
+    adders = [orc.NStep(3, 0.99, 0) for _ in range(n_actors)]
+    gamma_n = np.float32(0.99 ** 3)
+
+    def step(t):
+        nonlocal tail, obs, n_handles
+        with torch.no_grad():
+            q = an(torch.from_numpy(obs).float()).numpy()
+        act = orc.eps_greedy(q, eps, rng.random(n_actors), rng.integers(0, 6, n_actors))
+        new = rng.integers(0, 256, (n_actors, 1, 84, 84), dtype=np.uint8)
+        nxt = np.concatenate([obs[:, 1:], new], 1)
+        r = np.where(rng.random(n_actors) < 0.02, 1.0, 0.0).astype(np.float32)
+        d = (rng.random(n_actors) < 1 / 2000).astype(np.float32)
+        rows = []
+        for i in range(n_actors):
+            frames[obs_h[i]] = obs[i]
+            h1 = n_handles
+            n_handles += 1
+            frames[h1] = nxt[i]
+            row = adders[i].push(obs_h[i], act[i], r[i], h1, d[i])
+            obs_h[i] = h1
+            if row is not None:
+                rows.append(row)
+        obs = nxt
+        if rows:  # calc_loss on the actor copy (target == online) + Client.append
+            s0 = np.stack([frames[x[0]] for x in rows])
+            s1 = np.stack([frames[x[3]] for x in rows])
+            for h in [k for k in frames if k < n_handles - 6 * n_actors]:
+                del frames[h]
+            with torch.no_grad():
+                qq = an(torch.from_numpy(np.concatenate([s0, s1])).float()).numpy()
+            n = len(rows)
+            a_ = np.array([x[1] for x in rows])
+            r_ = np.array([x[2] for x in rows], np.float32)
+            d_ = np.array([x[4] for x in rows], np.float32)
+            td = orc.td_error(qq[:n], qq[n:], qq[n:], a_, r_, d_, gamma_n)
+            slots, tail = orc.fifo_indices(capacity, tail, n)
+            s0s[slots], s1s[slots], acol[slots], rcol[slots], dcol[slots] = s0, s1, a_, r_, d_
+            tree.update(slots, orc.per_normalize(np.abs(td), 0.5).astype(np.float64))
+        # learner update (DQNSolver.update on the CPU)
+        idx, p = tree.sample(rng.random(batch))
+        isw = orc.per_is_weights(p, tree.min(), 0.4)
+        b0 = torch.from_numpy(s0s[idx]).float()
+        b1 = torch.from_numpy(s1s[idx]).float()
+        qv = qn(b0)
+        with torch.no_grad():
+            nt = tq(b1)
+            no = qn(b1)
+        a_t = torch.from_numpy(acol[idx])
+        tdt = qv.gather(1, a_t[:, None])[:, 0] - (torch.from_numpy(rcol[idx]) + float(gamma_n) *
+                                                  nt.gather(1, no.argmax(1, keepdim=True))[:, 0] *
+                                                  (1 - torch.from_numpy(dcol[idx])))
+        loss = (torch.nn.functional.smooth_l1_loss(tdt, torch.zeros_like(tdt), reduction="none") *
+                torch.from_numpy(isw).float()).mean()
+        opt.zero_grad()
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(qn.parameters(), 40)
+        opt.step()
+        tree.update(idx, orc.per_normalize(tdt.detach().abs().numpy(), 0.5).astype(np.float64))
+
+    for t in range(4):  # warm the n-step deques (rows flow from step 4 on)
+        step(t)
+    t0 = time.perf_counter()
+    for t in range(4, 4 + iters):
+        step(t)
+    dt = time.perf_counter() - t0
+    return {"value": round(n_actors * iters / dt, 2), "unit": "env-steps/s", "cores": cores, "kind": "port",
+            "updates_per_sec": round(iters / dt, 3),
+            "sample": f"{iters} Ape-X steps (256 actors x 1 env step + 1 B=512 update each), replay capacity "
+                      f"{capacity} rows on the host, torch-CPU Q-net + oracle C tree/PER/n-step, "
+                      f"{torch.get_num_threads()} threads, {dt:.1f} s"}
+
+
+# ----------------------------------------------------------------------------- main
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--actors", type=int, default=256)
+    ap.add_argument("--capacity", type=int, default=1_000_000)
+    ap.add_argument("--batch", type=int, default=512)
+    ap.add_argument("--actor-steps-per-update", type=int, default=1)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-iters", type=int, default=20)
+    ap.add_argument("--tag", default="r01")
+    args = ap.parse_args()
+
+    from reth_amd.apex import ApexConfig, ApexDQN
+    from reth_amd.dist import init_from_env
+
+    import torch.distributed as dist
+
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    rank, world = init_from_env()
+    if world != args.gpus and world_env > 1:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    dev = torch.device("cuda", local)
+    cfg = ApexConfig(n_actors=args.actors, capacity=args.capacity, batch_size=args.batch,
+                     actor_steps_per_update=args.actor_steps_per_update, seed=0)
+    ax = ApexDQN(cfg, device=dev, rank=rank, world=world)
+    ax.prefill(cfg.capacity)
+    for _ in range(args.warmup):
+        ax.iteration()
+
+    events = []
+
+    def timer():
+        e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        events.append(e)
+        return e
+
+    ax.loader.gather_timer = timer
+    u0, e0 = ax.updates, ax.env_steps
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ax.iteration()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    ax.loader.gather_timer = None
+    n_upd, n_env = ax.updates - u0, ax.env_steps - e0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t)
+        c = torch.tensor([n_env, n_upd], dtype=torch.float64, device=dev)
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        n_env, n_upd = int(c[0]), int(c[1])
+    gather_ms = [a.elapsed_time(b) for a, b in events]
+    mean_gather_s = float(np.mean(gather_ms)) / 1e3
+    bytes_launch = gather_bytes_per_row() * cfg.batch_size
+    achieved = bytes_launch / mean_gather_s / 1e9
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    cpu = None
+    if not args.no_cpu_baseline and world == 1:
+        cpu = cpu_baseline(n_actors=cfg.n_actors, batch=cfg.batch_size, iters=args.cpu_iters)
+    flops_update = 5 * cfg.batch_size * qnet_flops_per_sample()  # 3 fwd + bwd(~2 fwd)
+    flops_actor = 3 * cfg.n_actors * qnet_flops_per_sample()     # act (N) + priorities (2N)
+    step_s = dt / args.steps
+    traffic = load_traffic(args.tag)
+    out = {
+        "metric": "env-steps/sec + learner updates/sec, Ape-X DQN Pong, 1/2/4/8 MI355X",
+        "value": round(n_env / dt, 1),
+        "unit": "env-steps/s",
+        "learner_updates_per_sec": round(n_upd / dt, 2),
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(step_s * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (Philox uint8 Pong-shaped frames, random-init Q-net; no ALE/checkpoints on the box)",
+        "config": {"workload": "PongNoFrameskip-v4 Ape-X DQN (BASELINE configs[1])", "actors_per_gpu": cfg.n_actors,
+                   "replay_capacity_per_gpu": cfg.capacity, "replay_prefilled": True, "batch_size": cfg.batch_size,
+                   "n_step": cfg.n_step, "alpha": cfg.alpha, "beta": cfg.beta,
+                   "actor_steps_per_update": cfg.actor_steps_per_update,
+                   "parallelism": f"dp{world} learner (RCCL grad all-reduce) + {world} replay shards"},
+        "roofline": {"kernel": "rth_replay_gather (k_copy_rows: PER-sampled rows, u8->f32 frames)",
+                     "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "bytes_per_launch": bytes_launch, "mean_launch_us": round(mean_gather_s * 1e6, 2),
+                     "launches_timed": len(gather_ms)},
+        "qnet_mfma": {"tflops_per_step": round((flops_update + flops_actor) * args.actor_steps_per_update / 1e12, 4),
+                      "achieved_tflops": round((flops_update + flops_actor) / step_s / 1e12, 2),
+                      "peak_fp32_tflops": FP32_PEAK_TFLOPS},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -261,11 +261,23 @@ class HbmReplay:
              stream_ptr())
         return n
 
-    def sample_into(self, batch_size, out_cols, idx_out, isw_out, uniforms=None):
+    def sample_into(self, batch_size, out_cols, idx_out, isw_out, uniforms=None, gather_timer=None):
+        """PER sample + gather into preallocated outputs.  gather_timer (optional) is a
+        callable returning a (start, end) pair of torch.cuda.Event recorded around the
+        gather launch alone (the bench's live roofline measurement)."""
         u = None if uniforms is None else as_device(uniforms, torch.float64, self.device)
         arr = (c_vp * len(out_cols))(*[ptr(t) for t in out_cols])
-        call("rth_replay_sample", self._h, batch_size, float(self.beta.value()), ptr(u), arr, ptr(idx_out),
-             ptr(isw_out), stream_ptr())
+        if gather_timer is None:
+            call("rth_replay_sample", self._h, batch_size, float(self.beta.value()), ptr(u), arr, ptr(idx_out),
+                 ptr(isw_out), stream_ptr())
+            return
+        s = stream_ptr()
+        call("rth_replay_sample", self._h, batch_size, float(self.beta.value()), ptr(u), None, ptr(idx_out),
+             ptr(isw_out), s)
+        ev0, ev1 = gather_timer()
+        ev0.record()
+        call("rth_replay_gather", self._h, ptr(idx_out), batch_size, arr, s)
+        ev1.record()
 
     def new_batch(self, batch_size):
         cols = [torch.empty((batch_size, *c.shape), dtype=c.out_dtype, device=self.device) for c in self.columns]

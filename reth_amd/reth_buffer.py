@@ -170,6 +170,7 @@ class TorchCudaLoader:
         self._slots = None
         self._next = 0
         self._pending = []  # slot ids already sampled, oldest first
+        self.gather_timer = None  # bench hook: events around the gather launch
 
     def _issue(self):
         rep = self.svc.replay
@@ -178,7 +179,7 @@ class TorchCudaLoader:
         k = self._next
         self._next = (self._next + 1) % self.buffer_size
         cols, idx, isw = self._slots[k]
-        rep.sample_into(self.svc.batch_size, cols, idx, isw)
+        rep.sample_into(self.svc.batch_size, cols, idx, isw, gather_timer=self.gather_timer)
         self._pending.append(k)
 
     def sample_device(self):

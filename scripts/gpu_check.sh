@@ -1,0 +1,22 @@
+#!/bin/bash
+# GPU-box check: each step has its own time limit; stop at the first crash/timeout
+# (pytest rc 0/1 = ran to completion, anything else ends the call).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+run() {
+  local name=$1 limit=$2; shift 2
+  echo "== $name ($(date +%T))"
+  timeout -k 10 "$limit" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc"; tail -n 5 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+}
+for step in "$@"; do
+  case "$step" in
+    tests) run pytest_gpu 1200 python -m pytest tests -m gpu -x -q ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 900 python bench.py ;;
+    benchq) run bench_quick 600 python bench.py --steps 50 --warmup 10 --cpu-iters 5 ;;
+  esac
+done

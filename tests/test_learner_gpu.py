@@ -1,0 +1,130 @@
+"""Learner parity: the fused TD/Huber kernel is bit-exact against the oracle given the same
+Q values; the full DQNSolver.update on the GPU matches the reference's torch-CPU update
+(golden vectors) within north_star's fp32 tolerance (conv summation order differs)."""
+import io
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+GAMMA_N = float(np.float32(0.99 ** 3))
+
+
+@pytest.mark.parametrize("B,A", [(1, 2), (8, 6), (512, 6), (512, 18), (700, 4), (2048, 6)])
+def test_td_huber_kernel_bit_exact(dev, orc, B, A):
+    from reth_amd.solver import td_huber_forward
+
+    rng = np.random.default_rng(B + A)
+    q0, q1o, q1t = (rng.standard_normal((B, A)).astype(np.float32) * 3 for _ in range(3))
+    q1o[: B // 4] = np.round(q1o[: B // 4])  # argmax ties
+    a = rng.integers(0, A, B)
+    r = rng.choice(np.array([-1, 0, 1], np.float32), B)
+    done = (rng.random(B) < 0.3).astype(np.float32)
+    isw = rng.random(B) + 0.1
+    T = lambda x: torch.as_tensor(x, device=dev)
+    for double_q in (True, False):
+        loss, td_abs, dq = td_huber_forward(T(q0), T(q1o), T(q1t), T(a), T(r), T(done), T(isw), GAMMA_N, double_q, True)
+        td = orc.td_error(q0, q1o if double_q else None, q1t, a, r, done, GAMMA_N, double_q)
+        assert np.array_equal(td_abs.cpu().numpy(), np.abs(td))
+        ol, _, odq = orc.td_huber(td, isw.astype(np.float32), a, A)
+        assert np.array_equal(dq.cpu().numpy(), odq)
+        assert abs(loss.item() - float(ol)) <= 1e-6 * max(1.0, abs(float(ol)))
+    # no IS weights
+    loss, td_abs, dq = td_huber_forward(T(q0), T(q1o), T(q1t), T(a), T(r), T(done), None, GAMMA_N, True, True)
+    _, _, odq = orc.td_huber(orc.td_error(q0, q1o, q1t, a, r, done, GAMMA_N), None, a, A)
+    assert np.array_equal(dq.cpu().numpy(), odq)
+
+
+def test_td_huber_autograd_matches_torch_reference(dev):
+    """the custom autograd op == the reference's op chain (dqn_solver.py:77-115) on device"""
+    import torch.nn.functional as F
+
+    from reth_amd.solver import td_huber_loss
+
+    B, A = 512, 6
+    g = torch.Generator(device=dev).manual_seed(0)
+    q0 = torch.randn(B, A, device=dev, generator=g, requires_grad=True)
+    q1o, q1t = torch.randn(B, A, device=dev, generator=g), torch.randn(B, A, device=dev, generator=g)
+    a = torch.randint(0, A, (B,), device=dev, generator=g)
+    r = torch.randn(B, device=dev, generator=g)
+    done = (torch.rand(B, device=dev, generator=g) < 0.2).float()
+    w = torch.rand(B, device=dev, generator=g, dtype=torch.float64)
+    loss, td_abs = td_huber_loss(q0, q1o, q1t, a, r, done, w, GAMMA_N, True)
+    loss.backward()
+    ours = q0.grad.clone()
+    q0.grad = None
+    qv = torch.sum(q0 * F.one_hot(a, A).float(), 1)
+    nqb = torch.sum(q1t * F.one_hot(torch.argmax(q1o, 1), A).float(), 1)
+    td = qv - (r + (0.99 ** 3) * nqb * (1 - done)).detach()
+    ref = (F.smooth_l1_loss(td, torch.zeros_like(td), reduction="none") * w.float()).mean()
+    ref.backward()
+    torch.testing.assert_close(td_abs, td.detach().abs(), rtol=0, atol=0)
+    torch.testing.assert_close(ours, q0.grad, rtol=0, atol=0)
+    torch.testing.assert_close(loss, ref, rtol=1e-6, atol=1e-7)
+
+
+def _make_solver(dev, seed, **kw):
+    from reth_amd.solver import Box, DQNSolver, Discrete
+
+    torch.manual_seed(seed)
+    args = dict(gamma=0.99, clip_value=40, double_q=True, dueling=True, learning_rate=1e-4, adam_epsilon=1.5e-4,
+                update_target_interval=100, device=dev, n_step=3)
+    args.update(kw)
+    return DQNSolver(Box(0, 255, (4, 84, 84)), Discrete(6), **args)
+
+
+@pytest.mark.parametrize("name", ["dqn_pong_b8.npz", "dqn_pong_b32.npz"])
+@pytest.mark.parametrize("fused", [True, False])
+def test_dqn_update_vs_reference(golden, dev, name, fused):
+    g = golden(name)
+    solver = _make_solver(dev, int(g["seed"]), fused_adam=fused)
+    batch = [g["s0"].astype(np.float32), g["a"], g["r"], g["s1"].astype(np.float32), g["done"]]
+    with torch.no_grad():
+        q0 = solver.q_network(torch.as_tensor(batch[0], device=dev)).cpu().numpy()
+    np.testing.assert_allclose(q0, g["q_s0"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(solver.calc_loss(batch).numpy(), g["calc_loss"], rtol=1e-5, atol=1e-5)
+    assert solver.act(batch[0][0]) == int(g["act0"])
+    for k in range(2):
+        td = solver.update(batch, weights=g["isw"]).numpy()
+        np.testing.assert_allclose(td, g[f"upd{k}_abs_td"], rtol=1e-5, atol=1e-5)
+        sd = solver.q_network.state_dict()
+        s1 = np.array([float(v.double().sum()) for v in sd.values()])
+        head = np.stack([np.pad(v.flatten()[:16].float().cpu().numpy(), (0, max(0, 16 - v.numel())),
+                                constant_values=np.nan) for v in sd.values()])
+        # one Adam step moves each weight by ~lr = 1e-4: fp32 agreement to ~1e-6 abs
+        np.testing.assert_allclose(head, g[f"upd{k}_head"], rtol=1e-4, atol=2e-6)
+        np.testing.assert_allclose(s1, g[f"upd{k}_sum"], rtol=1e-4, atol=1e-3)
+
+
+def test_cartpole_mlp_three_updates(golden, dev):
+    from reth_amd.solver import Box, DQNSolver, Discrete
+
+    g = golden("dqn_cartpole_b64.npz")
+    torch.manual_seed(int(g["seed"]))
+    solver = DQNSolver(Box(-1, 1, (4,)), Discrete(2), gamma=0.99, clip_value=40, double_q=True, dueling=True,
+                       learning_rate=1e-4, update_target_interval=200, device=dev)
+    batch = [g["s0"], g["a"], g["r"], g["s1"], g["done"]]
+    for k in range(3):
+        td = solver.update(batch).numpy()
+        np.testing.assert_allclose(td, g[f"upd{k}_abs_td"], rtol=1e-5, atol=1e-6)
+    for k, v in solver.q_network.state_dict().items():
+        np.testing.assert_allclose(v.cpu().numpy(), g[f"final/{k}"], rtol=1e-5, atol=1e-6)
+
+
+def test_target_interval_and_weights_stream(dev):
+    s = _make_solver(dev, 0, update_target_interval=2)
+    batch = [np.random.rand(16, 4, 84, 84).astype(np.float32) * 255, np.random.randint(0, 6, 16),
+             np.random.rand(16).astype(np.float32), np.random.rand(16, 4, 84, 84).astype(np.float32) * 255,
+             np.zeros(16, np.float32)]
+    s.update(batch)
+    differs = any(not torch.equal(p, q) for p, q in zip(s.q_network.parameters(), s.target_q_network.parameters()))
+    assert differs
+    s.update(batch)  # interval 2 -> target synced
+    assert all(torch.equal(p, q) for p, q in zip(s.q_network.parameters(), s.target_q_network.parameters()))
+    buf = s.save_weights()
+    s2 = _make_solver(dev, 1)
+    s2.load_weights(io.BytesIO(buf.getvalue()))
+    assert all(torch.equal(p, q) for p, q in zip(s.q_network.parameters(), s2.q_network.parameters()))
+    assert all(torch.equal(p, q) for p, q in zip(s2.q_network.parameters(), s2.target_q_network.parameters()))

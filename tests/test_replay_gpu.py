@@ -1,0 +1,159 @@
+"""HBM replay shard + the reth_buffer-compatible API (start_per / Client / loaders).
+
+Mirrors reth_buffer/test/test_rb.py (identity column pins index <-> row), reth/test/
+test_buffer.py::test_per (rows and IS weights), plus FIFO wrap-around, exact u8 -> f32
+widening, the sample-start gate, and the sample-ahead order, all against the oracle."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def test_rb_basic_identity_column(dev):
+    """reth_buffer/test/test_rb.py:12-35 through the drop-in API"""
+    from reth_amd import reth_buffer
+
+    svc, addr = reth_buffer.start_server(100000, 32, device=dev)
+    client = reth_buffer.Client(addr)
+    loader = reth_buffer.NumpyLoader(addr)
+    data = [np.random.rand(1000, 4, 84), np.random.rand(1000), np.arange(1000)]
+    w = np.random.rand(1000) + 1
+    for start in range(0, 1000, 100):
+        client.append([x[start:start + 100] for x in data], w[start:start + 100])
+    for _ in range(10):
+        batch, indices, weights = loader.sample()
+        assert indices.dtype == np.int64 and weights.dtype == np.float64 and len(indices) == 32
+        for i, idx in enumerate(indices):
+            assert batch[2][i] == idx
+            assert batch[1][i] == data[1][idx]
+            assert np.array_equal(batch[0][i], data[0][idx])
+    client.update_priorities(np.arange(1000), np.random.rand(1000) + 10)
+    svc.terminate()
+    svc.join()
+
+
+def test_per_rows_and_is_weights(dev, orc):
+    """reth/test/test_buffer.py:113-132: sampled rows equal data[idx]; IS weights equal
+    ((w + 1e-6)^alpha / min)^-beta"""
+    from reth_amd.replay import Column, HbmReplay
+
+    cap, B = 1000, 64
+    rng = np.random.default_rng(0)
+    cols = [Column((), torch.int64), Column((4, 84, 84), torch.float32), Column((), torch.int64),
+            Column((), torch.float32), Column((4, 84, 84), torch.float32), Column((), torch.float32)]
+    rep = HbmReplay(cap, cols, alpha=0.6, beta=0.4, device=dev)
+    data = [np.arange(cap), rng.random((cap, 4, 84, 84), dtype=np.float32), rng.integers(0, 10, cap),
+            rng.random(cap, dtype=np.float32), rng.random((cap, 4, 84, 84), dtype=np.float32),
+            rng.integers(0, 2, cap).astype(np.float32)]
+    w = rng.random(cap)
+    rep.append([torch.as_tensor(x, device=dev) for x in data], w)
+    out, idx, isw = rep.sample(B)
+    idx = idx.cpu().numpy()
+    for c, col in enumerate(out):
+        assert np.array_equal(col.cpu().numpy(), data[c][idx])
+    ow = (w + 1e-6) ** 0.6
+    np.testing.assert_allclose(isw.cpu().numpy(), (ow[idx] / ow.min()) ** -0.4, atol=1e-3)  # the reference's bound
+    p = orc.per_normalize(w, 0.6)
+    np.testing.assert_allclose(isw.cpu().numpy(), orc.per_is_weights(p[idx], p.min(), 0.4), rtol=1e-12)
+
+
+def test_fifo_wraparound_and_u8_widening(dev, orc):
+    """FIFO slots wrap (fifo_policy.py:11-18); uint8 frames come back as exact float32"""
+    from reth_amd.replay import Column, HbmReplay
+
+    cap = 300
+    rep = HbmReplay(cap, [Column((4, 84, 84), torch.uint8, torch.float32), Column((), torch.int64)], alpha=0.5,
+                    device=dev)
+    rng = np.random.default_rng(1)
+    tree = orc.Tree(cap)
+    tail = 0
+    written = {}
+    for step in range(7):
+        n = int(rng.integers(1, 130))
+        frames = rng.integers(0, 256, (n, 4, 84, 84), dtype=np.uint8)
+        ids = np.arange(100 * step, 100 * step + n)
+        td = rng.random(n, dtype=np.float32)
+        slots_out = torch.empty(n, dtype=torch.int64, device=dev)
+        rep.append([torch.as_tensor(frames, device=dev), torch.as_tensor(ids, device=dev)], torch.as_tensor(td, device=dev),
+                   idx_out=slots_out)
+        slots, tail = orc.fifo_indices(cap, tail, n)
+        assert np.array_equal(slots_out.cpu().numpy(), slots)
+        tree.update(slots, orc.per_normalize(td, 0.5).astype(np.float64))
+        for k, s in enumerate(slots):
+            written[int(s)] = (frames[k], ids[k])
+    size, gtail, cnt, _ = rep.info()
+    assert gtail == tail and size == min(cap, cnt)
+    s, m, v = rep.tree.export()
+    assert np.array_equal(s.cpu().numpy(), tree.sum) and np.array_equal(v.cpu().numpy(), tree.val)
+    keys = np.array(sorted(written))
+    out = rep.gather(keys)
+    assert out[0].dtype == torch.float32
+    for k, s_ in enumerate(keys):
+        f, i = written[int(s_)]
+        assert out[1][k].item() == i
+        assert torch.equal(out[0][k].cpu(), torch.as_tensor(f).float())
+
+
+def test_append_exact_capacity_and_errors(dev):
+    from reth_amd import reth_buffer
+    from reth_amd.replay import Column, HbmReplay
+
+    rep = HbmReplay(16, [Column((3,), torch.float32)], device=dev)
+    rep.append([torch.ones(16, 3, device=dev)], torch.ones(16, device=dev))
+    assert rep.info()[:2] == (16, 0)
+    with pytest.raises(AssertionError):  # fifo_policy.py:12 assert batch_size <= capacity
+        rep.append([torch.ones(17, 3, device=dev)], torch.ones(17, device=dev))
+    with pytest.raises(ValueError):
+        rep.append([torch.ones(4, 3, device=dev)], torch.ones(5, device=dev))
+    svc, addr = reth_buffer.start_per(1000, 64, sample_start=100, device=dev)
+    client, loader = reth_buffer.Client(addr), reth_buffer.TorchCudaLoader(addr)
+    client.append([np.zeros((50, 2), np.float32)], np.ones(50, np.float32))
+    with pytest.raises(RuntimeError):  # cnt 50 < max(sample_start, batch) = 100
+        loader.sample()
+    client.append([np.zeros((50, 2), np.float32)], np.ones(50, np.float32))
+    data, idx, w = loader.sample()
+    assert data[0].is_cuda and w.dtype == torch.float64 and idx.shape == (64,)
+    with pytest.raises(ValueError):
+        reth_buffer.Client("hbm://0/does-not-exist")
+
+
+def test_torch_cuda_loader_sample_ahead_order(dev, orc):
+    """batch k+1 is drawn before batch k's priorities are written back (the sampler's HWM-1
+    PUSH, sampler_loop.py:13-15/36-39), with beta stepped by each update message"""
+    from reth_amd import reth_buffer
+
+    cap, B = 5000, 128
+    svc, addr = reth_buffer.start_per(cap, B, alpha=0.5, beta="0.4,1,1000", sample_start=B, device=dev, seed=3)
+    client, loader = reth_buffer.Client(addr), reth_buffer.TorchCudaLoader(addr, buffer_size=4)
+    rng = np.random.default_rng(2)
+    ids = np.arange(cap)
+    td0 = rng.random(cap, dtype=np.float32)
+    client.append([ids], td0)
+    tree = orc.Tree(cap)
+    tree.update(ids, orc.per_normalize(td0, 0.5).astype(np.float64))
+    beta_steps = 0
+    pending = None  # oracle's pre-sampled batch
+    calls = 0
+
+    def oracle_sample():
+        nonlocal calls
+        u = np.array([orc.philox_uniform(3, calls, i, orc.STREAM_SAMPLE) for i in range(B)])
+        calls += 1
+        idx, p = tree.sample(u)
+        beta = 0.4 + (1 - 0.4) * beta_steps / 1000
+        return idx, orc.per_is_weights(p, tree.min(), beta)
+
+    for k in range(6):
+        data, idx, w = loader.sample()
+        if pending is None:
+            pending = oracle_sample()
+        want_idx, want_w = pending
+        pending = oracle_sample()  # sample-ahead happens before this batch's update
+        assert np.array_equal(idx, want_idx)
+        assert np.array_equal(data[0].cpu().numpy(), want_idx)
+        np.testing.assert_allclose(w.cpu().numpy(), want_w, rtol=1e-12)
+        new = rng.random(B, dtype=np.float32)
+        client.update_priorities(idx, new)  # step=True: beta.step() then update
+        beta_steps += 1
+        tree.update(idx, orc.per_normalize(new, 0.5).astype(np.float64))

@@ -70,10 +70,10 @@ __global__ void k_nstep_push(NStepState st, int64_t N, int n, double gamma, int 
     const int64_t p = base + k;
     if (st.done[p] != 0.0f) break;
     if (mode == 0)  // numpy 1.19: f64 product, += casts back to the f32 row
-      st.r[p] = (float)__dadd_rn((double)st.r[p], __dmul_rn(t_gamma, (double)rn));
+      st.r[p] = (float)radd((double)st.r[p], rmul(t_gamma, (double)rn));
     else            // numpy 2 / NEP 50: the python float is weak, product stays f32
-      st.r[p] = __fadd_rn(st.r[p], __fmul_rn((float)t_gamma, rn));
-    t_gamma = __dmul_rn(t_gamma, gamma);
+      st.r[p] = radd(st.r[p], rmul((float)t_gamma, rn));
+    t_gamma = rmul(t_gamma, gamma);
     st.s1[p] = s1n;
   }
   for (int k = count; k > 0; --k) {  // appendleft

@@ -8,7 +8,22 @@
 
 #include "../../include/reth_hip.h"
 
+// Reference parity needs every f32/f64 product and sum rounded exactly where the reference
+// (numpy / numba / torch CPU) rounds it, so nothing in this library may be contracted into
+// an FMA.  The pragma covers all code after this point; the build keeps clang's default
+// -ffp-contract=fast-honor-pragmas so the ocml math library (pow, exp) keeps the fused
+// operations its accuracy depends on.  (The clang HIP header's __fmul_rn & co. are plain
+// `x * y` compiled before this pragma, i.e. contractible -- use radd/rsub/rmul instead.)
+#pragma clang fp contract(off)
+
 namespace rth {
+
+__host__ __device__ __forceinline__ float radd(float a, float b) { return a + b; }
+__host__ __device__ __forceinline__ float rsub(float a, float b) { return a - b; }
+__host__ __device__ __forceinline__ float rmul(float a, float b) { return a * b; }
+__host__ __device__ __forceinline__ double radd(double a, double b) { return a + b; }
+__host__ __device__ __forceinline__ double rsub(double a, double b) { return a - b; }
+__host__ __device__ __forceinline__ double rmul(double a, double b) { return a * b; }
 
 void set_error(const char *fmt, ...);
 
@@ -97,16 +112,16 @@ __device__ inline int argmax_first(const float *q, int A) {
 // PERSampler._normalize_weights (per_sampler.py:16-17): (w + 1e-6) ** alpha in float32,
 // correctly rounded; numpy's `** 0.5` is sqrt (fast_scalar_power), also correctly rounded.
 __device__ inline float per_normalize(float w, float alpha) {
-  const float x = __fadd_rn(w, 1e-6f);
-  if (alpha == 0.5f) return __fsqrt_rn(x);
+  const float x = radd(w, 1e-6f);
+  if (alpha == 0.5f) return sqrtf(x);  // NOT __fsqrt_rn: that is __ocml_native_sqrt_f32 (approximate)
   if (alpha == 1.0f) return x;
   return (float)pow((double)x, (double)alpha);
 }
 
 // the same in float64 (numpy float64 arrays: `** 0.5` is sqrt, other exponents pow)
 __device__ inline double per_normalize64(double w, double alpha) {
-  const double x = __dadd_rn(w, 1e-6);
-  if (alpha == 0.5) return __dsqrt_rn(x);
+  const double x = radd(w, 1e-6);
+  if (alpha == 0.5) return sqrt(x);
   if (alpha == 1.0) return x;
   return pow(x, alpha);
 }

@@ -42,29 +42,29 @@ __global__ __launch_bounds__(kTdThreads) void k_td_huber(
     const int astar = argmax_first((double_q ? q1o : q1t) + b * A, A);  // (:83-94)
     const float nqb = q1t[b * A + astar];
     // expected = r + (gamma**n * next_q_best) * (1 - done)  (:96), f32, no contraction
-    float t = __fmul_rn(gamma_n, nqb);
-    t = __fmul_rn(t, __fsub_rn(1.0f, done[b]));
-    const float y = __fadd_rn(rew[b], t);
-    const float td = __fsub_rn(q, y);  // (:97)
+    float t = rmul(gamma_n, nqb);
+    t = rmul(t, rsub(1.0f, done[b]));
+    const float y = radd(rew[b], t);
+    const float td = rsub(q, y);  // (:97)
     if (td_out) td_out[b] = td;
     const float z = fabsf(td);
     if (td_abs_out) td_abs_out[b] = z;  // td_error.detach().cpu().abs() (:109), kept on device
     // smooth_l1(beta=1) (:112) * w (:113-114)
-    float l = z < 1.0f ? __fmul_rn(__fmul_rn(0.5f, z), z) : __fsub_rn(z, 0.5f);
+    float l = z < 1.0f ? rmul(rmul(0.5f, z), z) : rsub(z, 0.5f);
     const float w = isw ? (float)isw[b] : 1.0f;
-    if (isw) l = __fmul_rn(l, w);
+    if (isw) l = rmul(l, w);
     if (loss_elem) loss_elem[b] = l;
-    acc = __fadd_rn(acc, l);
+    acc = radd(acc, l);
     if (dq) {  // autograd: mean -> mul(w) -> smooth_l1' -> one_hot scatter
-      const float g = __fmul_rn(invB, w);
-      const float d = td <= -1.0f ? -g : (td >= 1.0f ? g : __fmul_rn(td, g));
-      for (int j = 0; j < A; ++j) dq[b * A + j] = __fmul_rn(d, j == a ? 1.0f : 0.0f);
+      const float g = rmul(invB, w);
+      const float d = td <= -1.0f ? -g : (td >= 1.0f ? g : rmul(td, g));
+      for (int j = 0; j < A; ++j) dq[b * A + j] = rmul(d, j == a ? 1.0f : 0.0f);
     }
   }
   part[threadIdx.x] = acc;
   __syncthreads();
   for (int s = kTdThreads / 2; s > 0; s >>= 1) {
-    if ((int)threadIdx.x < s) part[threadIdx.x] = __fadd_rn(part[threadIdx.x], part[threadIdx.x + s]);
+    if ((int)threadIdx.x < s) part[threadIdx.x] = radd(part[threadIdx.x], part[threadIdx.x + s]);
     __syncthreads();
   }
   if (threadIdx.x == 0 && loss_out) loss_out[0] = part[0] * invB;

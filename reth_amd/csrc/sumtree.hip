@@ -46,12 +46,12 @@ __device__ __forceinline__ void maintain_node(Node *nd, int64_t cap, int64_t i) 
   double m = (v != 0.0) ? v : 1.0;
   if (l < cap) {
     const Node L = nd[l + 1];
-    s = __dadd_rn(s, L.sum);
+    s = radd(s, L.sum);
     if (L.mn != 0.0) m = (L.mn < m) ? L.mn : m;
   }
   if (r < cap) {
     const Node R = nd[r + 1];
-    s = __dadd_rn(s, R.sum);
+    s = radd(s, R.sum);
     if (R.mn != 0.0) m = (R.mn < m) ? R.mn : m;
   }
   nd[i + 1].sum = s;
@@ -76,10 +76,10 @@ __device__ __forceinline__ int64_t tree_find(const Node *__restrict__ nd, int64_
         cval = lval;
         continue;
       }
-      w = __dsub_rn(w, lsum);
+      w = rsub(w, lsum);
     }
-    if (w < __dadd_rn(cval, 1e-5)) return cur;
-    w = __dsub_rn(w, cval);
+    if (w < radd(cval, 1e-5)) return cur;
+    w = rsub(w, cval);
     const int64_t r = l + 1;
     if (r >= cap) return cur;
     cur = r;
@@ -209,7 +209,7 @@ __global__ void k_tree_sample(const Node *__restrict__ nd, int64_t cap, int64_t 
   const double total = nd[1].sum;
   const double seg = total / (double)batch;
   const double u = uniforms ? uniforms[i] : philox_uniform(seed, counter, (uint32_t)i, STREAM_SAMPLE);
-  const double t = __dmul_rn(__dadd_rn((double)i, u), seg);
+  const double t = rmul(radd((double)i, u), seg);
   const int64_t k = tree_find(nd, cap, t);
   const double p = nd[k + 1].val;
   idx_out[i] = k;

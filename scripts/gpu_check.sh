@@ -14,9 +14,12 @@ run() {
 }
 for step in "$@"; do
   case "$step" in
-    tests) run pytest_gpu 1200 python -m pytest tests -m gpu -x -q ;;
+    tests) run pytest_gpu 1200 python -m pytest tests -m gpu -q -rf ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 900 python bench.py ;;
     benchq) run bench_quick 600 python bench.py --steps 50 --warmup 10 --cpu-iters 5 ;;
+    debug) run debug 300 python scripts/debug_isw.py ;;
+    prof) export TMPDIR=/tmp; run rocprof_stats 900 rocprofv3 --kernel-trace --stats --output-format csv \
+            -d "$PWD/gpurun_out/prof" -o run -- python bench.py --steps 100 --warmup 10 --no-cpu-baseline ;;
   esac
 done

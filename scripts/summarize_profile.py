@@ -1,0 +1,100 @@
+"""Summarise rocprofv3 outputs (gpurun_out/) into profiles/ (committed evidence).
+
+    python scripts/summarize_profile.py TAG [--steps N]
+
+Reads gpurun_out/prof/run_kernel_{stats,trace}.csv (rocprofv3 --kernel-trace --stats) and
+gpurun_out/pmc_{fetch,write}/run_counter_collection.csv (separate --pmc FETCH_SIZE /
+WRITE_SIZE passes), writes
+    profiles/TAG_kernel_stats.csv        rocprofv3's own --stats table
+    profiles/TAG_steady_state.txt        per-iteration kernel breakdown (timed window)
+    profiles/TAG_gather_launches.txt     the learner gather's launches by grid (avg duration)
+    profiles/TAG_pmc.txt                 FETCH/WRITE per kernel and grid, gfx950-corrected
+    profiles/traffic_TAG.json            HBM bytes per learner-gather launch (bench.py reads it)
+FETCH_SIZE on gfx950 reports half the bytes of a wide coalesced read (MI355X_MICROARCH.md
+§HBM): it is doubled; WRITE_SIZE is exact for 16-byte stores.  Both are in KiB.
+"""
+import collections
+import csv
+import json
+import os
+import shutil
+import statistics as st
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, "gpurun_out")
+PROF = os.path.join(ROOT, "profiles")
+LEARNER_GATHER_GRID = 512 * 5 * 256  # B rows x 5 apex columns x 256 threads
+
+
+def main():
+    tag = sys.argv[1]
+    steps = int(sys.argv[sys.argv.index("--steps") + 1]) if "--steps" in sys.argv else 100
+    os.makedirs(PROF, exist_ok=True)
+    stats = os.path.join(OUT, "prof", "run_kernel_stats.csv")
+    if os.path.exists(stats):
+        shutil.copy(stats, os.path.join(PROF, f"{tag}_kernel_stats.csv"))
+    trace = os.path.join(OUT, "prof", "run_kernel_trace.csv")
+    if os.path.exists(trace):
+        rows = sorted(csv.DictReader(open(trace)), key=lambda r: int(r["Start_Timestamp"]))
+        td = [r for r in rows if "k_td_huber" in r["Kernel_Name"]]
+        start = int(td[-2 * steps]["Start_Timestamp"])  # 2 TD launches per iteration
+        end = int(rows[-1]["End_Timestamp"])
+        win = [r for r in rows if int(r["Start_Timestamp"]) >= start]
+        agg = collections.defaultdict(lambda: [0, 0])
+        for r in win:
+            a = agg[r["Kernel_Name"][:100]]
+            a[0] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+            a[1] += 1
+        busy = sum(v[0] for v in agg.values())
+        with open(os.path.join(PROF, f"{tag}_steady_state.txt"), "w") as f:
+            f.write(f"# last {steps} iterations of the profiled bench run\n")
+            f.write(f"window {((end - start) / 1e6):.3f} ms, kernel-busy {busy / 1e6:.3f} ms, "
+                    f"{(end - start) / 1e3 / steps:.1f} us/iter wall, {busy / 1e3 / steps:.1f} us/iter busy, "
+                    f"{len(win) / steps:.1f} kernels/iter\n")
+            f.write(f"{'share':>7} {'us/iter':>9} {'calls/iter':>10}  kernel\n")
+            for k, v in sorted(agg.items(), key=lambda kv: -kv[1][0]):
+                f.write(f"{v[0] / busy * 100:6.2f}% {v[0] / 1e3 / steps:9.2f} {v[1] / steps:10.2f}  {k}\n")
+        by_grid = collections.defaultdict(list)
+        for r in win:
+            if "k_copy_rows" in r["Kernel_Name"]:
+                g = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"])
+                by_grid[(r["Grid_Size_X"], r["Grid_Size_Y"])].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+        with open(os.path.join(PROF, f"{tag}_gather_launches.txt"), "w") as f:
+            f.write("# rth::k_copy_rows launches in the timed window, by grid (threads x, y)\n")
+            f.write("# (512*256, 5) = learner gather (rth_replay_gather, B=512, 5 columns)\n")
+            for k, v in sorted(by_grid.items()):
+                f.write(f"grid={k} launches={len(v)} avg_us={st.mean(v) / 1e3:.2f} min_us={min(v) / 1e3:.2f} "
+                        f"max_us={max(v) / 1e3:.2f}\n")
+    pf = os.path.join(OUT, "pmc_fetch", "run_counter_collection.csv")
+    pw = os.path.join(OUT, "pmc_write", "run_counter_collection.csv")
+    if os.path.exists(pf) and os.path.exists(pw):
+        def load(p, name):
+            d = collections.defaultdict(list)
+            for r in csv.DictReader(open(p)):
+                if r["Counter_Name"] == name:
+                    d[(r["Kernel_Name"].split("(")[0], int(r["Grid_Size"]))].append(float(r["Counter_Value"]))
+            return d
+
+        fe, wr = load(pf, "FETCH_SIZE"), load(pw, "WRITE_SIZE")
+        with open(os.path.join(PROF, f"{tag}_pmc.txt"), "w") as f:
+            f.write("# rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), KiB per dispatch (median)\n")
+            f.write("# hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024  (gfx950: FETCH_SIZE counts half)\n")
+            for k in sorted(set(fe) | set(wr)):
+                fv, wv = st.median(fe.get(k, [0])), st.median(wr.get(k, [0]))
+                f.write(f"{k[0]:24s} grid={k[1]:>9d} n={len(fe.get(k, [])):4d} FETCH_KiB={fv:12.1f} "
+                        f"WRITE_KiB={wv:12.1f} hbm_MB={(2 * fv + wv) * 1024 / 1e6:10.2f}\n")
+        key = ("rth::k_copy_rows", LEARNER_GATHER_GRID)
+        if key in fe and key in wr:
+            hbm = (2 * st.median(fe[key]) + st.median(wr[key])) * 1024
+            with open(os.path.join(PROF, f"traffic_{tag}.json"), "w") as f:
+                json.dump({"kernel": "rth::k_copy_rows (learner gather, B=512, 5 columns)",
+                           "gather_hbm_bytes_per_launch": round(hbm),
+                           "fetch_kib_median": st.median(fe[key]), "write_kib_median": st.median(wr[key]),
+                           "correction": "FETCH_SIZE x2 (gfx950 half-count on wide coalesced reads)",
+                           "dispatches": len(fe[key])}, f, indent=1)
+    print("wrote", sorted(os.listdir(PROF)))
+
+
+if __name__ == "__main__":
+    main()

@@ -174,6 +174,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-iters", type=int, default=20)
     ap.add_argument("--tag", default="r01")
+    ap.add_argument("--nchw", action="store_true", help="contiguous NCHW Q-net tensors (default channels-last)")
+    ap.add_argument("--no-conv-benchmark", action="store_true", help="MIOpen immediate mode instead of find")
+    ap.add_argument("--eager", action="store_true", help="no HIP-graph replay (launch every kernel from Python)")
     args = ap.parse_args()
 
     from reth_amd.apex import ApexConfig, ApexDQN
@@ -189,7 +192,9 @@ def main():
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     dev = torch.device("cuda", local)
     cfg = ApexConfig(n_actors=args.actors, capacity=args.capacity, batch_size=args.batch,
-                     actor_steps_per_update=args.actor_steps_per_update, seed=0)
+                     actor_steps_per_update=args.actor_steps_per_update, seed=0,
+                     channels_last=not args.nchw, conv_benchmark=not args.no_conv_benchmark,
+                     hip_graph=not args.eager)
     ax = ApexDQN(cfg, device=dev, rank=rank, world=world)
     ax.prefill(cfg.capacity)
     for _ in range(args.warmup):
@@ -256,6 +261,8 @@ def main():
                    "replay_capacity_per_gpu": cfg.capacity, "replay_prefilled": True, "batch_size": cfg.batch_size,
                    "n_step": cfg.n_step, "alpha": cfg.alpha, "beta": cfg.beta,
                    "actor_steps_per_update": cfg.actor_steps_per_update,
+                   "qnet_layout": "channels_last" if cfg.channels_last else "nchw",
+                   "conv_benchmark": cfg.conv_benchmark, "hip_graph": cfg.hip_graph,
                    "parallelism": f"dp{world} learner (RCCL grad all-reduce) + {world} replay shards"},
         "roofline": {"kernel": "rth_replay_gather (k_copy_rows: PER-sampled rows, u8->f32 frames)",
                      "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

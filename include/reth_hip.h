@@ -95,9 +95,12 @@ int rth_per_sample(rth_sumtree *t, int64_t batch, double beta, const double *uni
  * and the loaders' row fetch (client/torch_cuda_loader.py:20-66, numpy_loader.py:27-51).
  * ---------------------------------------------------------------------------------- */
 typedef struct {
-  int64_t row_elems; /* elements per row (product of the per-row shape) */
-  int32_t in_dtype;  /* storage type == type appended (RTH_U8 ... RTH_F64) */
-  int32_t out_dtype; /* type produced on sample: == in_dtype, or RTH_F32 from RTH_U8 */
+  int64_t row_elems;  /* elements per row (product of the per-row shape) */
+  int32_t in_dtype;   /* storage type == type appended (RTH_U8 ... RTH_F64) */
+  int32_t out_dtype;  /* type produced on sample: == in_dtype, or RTH_F32 from RTH_U8 */
+  int32_t out_planes; /* 0: same element order; k > 0 (RTH_U8 -> RTH_F32 only): the row is k
+                         planes (C,H,W) and is produced channels-last (H,W,C) */
+  int32_t reserved;
 } rth_col_desc;
 
 /* a column source for an append: rows[i] (or i when rows_dev == NULL) of base_dev, rows
@@ -108,31 +111,51 @@ typedef struct {
   int64_t row_stride_bytes;
 } rth_src;
 
+/* A PERSampler schedule (reth_buffer/reth_buffer/utils/schedule.py:4-52):
+ * const: start; linear: start + (end - start) * k / max_steps;
+ * exp: end - (end - start) * exp(-k / max_steps); k = steps taken, clamped to max_steps. */
+#define RTH_SCHED_CONST 0
+#define RTH_SCHED_LINEAR 1
+#define RTH_SCHED_EXP 2
+typedef struct {
+  int32_t method;
+  int32_t reserved;
+  double start;
+  double end;
+  int64_t max_steps;
+} rth_schedule;
+
 typedef struct rth_replay rth_replay;
-int rth_replay_create(int64_t capacity, int32_t n_cols, const rth_col_desc *cols, int device,
-                      uint64_t seed, rth_replay **out);
+/* The shard owns its PERSampler state (per_sampler.py:5-12): the alpha / beta schedules and
+ * the step count, the FIFO tail and the sample-call counter live in device memory, so every
+ * launch below is argument-invariant from step to step (HIP-graph replayable). */
+int rth_replay_create(int64_t capacity, int32_t n_cols, const rth_col_desc *cols,
+                      const rth_schedule *alpha, const rth_schedule *beta, int device, uint64_t seed,
+                      rth_replay **out);
 int rth_replay_destroy(rth_replay *h);
 /* Client.append + append_loop + PERSampler.update: rows go to FIFO slots
  * tail, tail+1, ... mod capacity (FIFOPolicy :11-18), priorities (td_abs + 1e-6)**alpha
  * into the tree.  idx_out_dev (nullable) receives the slots. */
 int rth_replay_append(rth_replay *h, const rth_src *srcs, const void *td_abs_dev, int32_t td_dtype,
-                      int64_t n, double alpha, int64_t *idx_out_dev, void *stream);
+                      int64_t n, int64_t *idx_out_dev, void *stream);
 /* sampler_loop sample + loader gather: PER-sample `batch` rows (uniforms_dev nullable, see
- * rth_sumtree_sample), write IS weights, and gather every column into out_cols_dev[c]
- * ([batch, row] of out_dtype) -- TorchCudaLoader.sample's (data, indices, weights). */
-int rth_replay_sample(rth_replay *h, int64_t batch, double beta, const double *uniforms_dev,
+ * rth_sumtree_sample) with the current beta, write IS weights, and gather every column into
+ * out_cols_dev[c] ([batch, row] of out_dtype; NULL = no gather) -- TorchCudaLoader.sample's
+ * (data, indices, weights). */
+int rth_replay_sample(rth_replay *h, int64_t batch, const double *uniforms_dev,
                       void *const *out_cols_dev, int64_t *idx_out_dev, double *isw_out_dev,
                       void *stream);
-/* Client.update_priorities :37-39 -> PERSampler.update */
+/* Client.update_priorities :37-39 -> sampler_loop :31-35: step != 0 advances the alpha/beta
+ * schedules first (PERSampler.on_step), then PERSampler.update */
 int rth_replay_update_priorities(rth_replay *h, const int64_t *idx_dev, const void *td_abs_dev,
-                                 int32_t td_dtype, int64_t n, double alpha, void *stream);
+                                 int32_t td_dtype, int64_t n, int32_t step, void *stream);
 /* NumpyLoader row fetch (numpy_loader.py:381-396) for explicit indices */
 int rth_replay_gather(rth_replay *h, const int64_t *idx_dev, int64_t n, void *const *out_cols_dev,
                       void *stream);
-/* host-side counters: rows stored, FIFO tail, sampler cnt (appended + re-prioritised,
- * sampler_loop.py:36), sample calls issued */
+/* host mirrors of the service counters: rows stored, FIFO tail, sampler cnt (appended +
+ * re-prioritised, sampler_loop.py:36), sample calls issued, schedule steps taken */
 int rth_replay_info(const rth_replay *h, int64_t *size, int64_t *tail, int64_t *cnt,
-                    int64_t *sample_calls);
+                    int64_t *sample_calls, int64_t *sched_steps);
 rth_sumtree *rth_replay_tree(rth_replay *h);
 /* device pointer of column c's storage ([capacity, row] of in_dtype) */
 void *rth_replay_column(rth_replay *h, int32_t c);
@@ -140,21 +163,25 @@ void *rth_replay_column(rth_replay *h, int32_t c);
 /* ------------------------------------------------------------------------------------
  * Row copy / gather with optional uint8 -> float32 widening (the loaders' pinned copy +
  * H2D, torch_cuda_loader.py:43-62, as one HBM->HBM kernel).  src/dst row index arrays are
- * nullable (identity).  Strides in bytes.
+ * nullable (identity).  Strides in bytes.  out_planes as in rth_col_desc (channels-last out).
  * ---------------------------------------------------------------------------------- */
 int rth_copy_rows(void *dst_dev, int64_t dst_stride, const int64_t *dst_rows_dev, const void *src_dev,
                   int64_t src_stride, const int64_t *src_rows_dev, int64_t n, int64_t row_elems,
-                  int32_t in_dtype, int32_t out_dtype, void *stream);
+                  int32_t in_dtype, int32_t out_dtype, int32_t out_planes, void *stream);
 
 /* ------------------------------------------------------------------------------------
  * Actor side.
  * ---------------------------------------------------------------------------------- */
 /* RandomExploration.act (reth/reth/utils/exploration.py:26-31) over N actors:
  * u < eps[i] ? rand_action : argmax_a q[i, a] (first maximum, dqn_solver.py:126-131).
- * u_dev / rand_action_dev nullable -> Philox(seed, counter). */
+ * u_dev / rand_action_dev nullable -> Philox(seed, counter); counter_dev (nullable) supplies
+ * the counter from device memory instead (graph replay). */
 int rth_eps_greedy(const float *q_dev, int64_t N, int64_t A, const double *eps_dev,
                    const double *u_dev, const int64_t *rand_action_dev, uint64_t seed,
-                   uint64_t counter, int64_t *action_out_dev, void *stream);
+                   uint64_t counter, const int64_t *counter_dev, int64_t *action_out_dev,
+                   void *stream);
+/* *counter_dev += delta (device-resident step counters) */
+int rth_counter_add(int64_t *counter_dev, int64_t delta, void *stream);
 
 /* NStepAdder (reth/reth/utils/nstep_adder.py:5-28), one adder per actor, rows referencing
  * frame handles.  mode 0 = numpy 1.19 promotion (reference pin), 1 = numpy 2 / NEP 50. */
@@ -175,9 +202,10 @@ int rth_nstep_push(rth_nstep *h, const int64_t *s0_dev, const int64_t *a_dev, co
  * frame) into slot (2t) % ring and, on done, a reset stack (one fresh frame x4, FrameStack
  * reset) into slot (2t+1) % ring.  reward in {-1,0,+1}, P(+-1) = p_reward/2 each;
  * done ~ Bernoulli(p_done).  cur_slot_dev is updated in place; s0/s1 handles
- * (actor*ring + slot) are written for the n-step adder.  Actions do not affect it. */
+ * (actor*ring + slot) are written for the n-step adder.  Actions do not affect it.
+ * t_dev (nullable) supplies t from device memory (graph replay). */
 int rth_synth_env_step(uint8_t *frames_dev, int64_t n_actors, int32_t ring, int64_t t,
-                       int64_t *cur_slot_dev, const int64_t *action_dev, uint64_t seed,
+                       const int64_t *t_dev, int64_t *cur_slot_dev, const int64_t *action_dev, uint64_t seed,
                        float p_reward, float p_done, float *r_out_dev, float *done_out_dev,
                        int64_t *s0_handle_dev, int64_t *s1_handle_dev, void *stream);
 /* initial reset of every actor into slot 1 (t = 0) */

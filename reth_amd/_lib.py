@@ -27,7 +27,16 @@ class RethHipError(RuntimeError):
 
 
 class ColDesc(ctypes.Structure):
-    _fields_ = [("row_elems", c_i64), ("in_dtype", c_i32), ("out_dtype", c_i32)]
+    _fields_ = [("row_elems", c_i64), ("in_dtype", c_i32), ("out_dtype", c_i32), ("out_planes", c_i32),
+                ("reserved", c_i32)]
+
+
+class Sched(ctypes.Structure):
+    """rth_schedule: Schedule (schedule.py) as method/start/end/max_steps"""
+    _fields_ = [("method", c_i32), ("reserved", c_i32), ("start", c_f64), ("end", c_f64), ("max_steps", c_i64)]
+
+
+SCHED_CONST, SCHED_LINEAR, SCHED_EXP = 0, 1, 2
 
 
 class Src(ctypes.Structure):
@@ -54,24 +63,26 @@ SIGNATURES = {
     "rth_per_update": (c_i32, [c_vp, c_vp, c_vp, c_i32, c_i64, c_f64, c_vp]),
     "rth_per_sample": (c_i32, [c_vp, c_i64, c_f64, c_vp, c_u64, c_u64, c_vp, c_vp, c_vp]),
     # replay
-    "rth_replay_create": (c_i32, [c_i64, c_i32, ctypes.POINTER(ColDesc), c_i32, c_u64, ctypes.POINTER(c_vp)]),
+    "rth_replay_create": (c_i32, [c_i64, c_i32, ctypes.POINTER(ColDesc), ctypes.POINTER(Sched),
+                                  ctypes.POINTER(Sched), c_i32, c_u64, ctypes.POINTER(c_vp)]),
     "rth_replay_destroy": (c_i32, [c_vp]),
-    "rth_replay_append": (c_i32, [c_vp, ctypes.POINTER(Src), c_vp, c_i32, c_i64, c_f64, c_vp, c_vp]),
-    "rth_replay_sample": (c_i32, [c_vp, c_i64, c_f64, c_vp, ctypes.POINTER(c_vp), c_vp, c_vp, c_vp]),
-    "rth_replay_update_priorities": (c_i32, [c_vp, c_vp, c_vp, c_i32, c_i64, c_f64, c_vp]),
+    "rth_replay_append": (c_i32, [c_vp, ctypes.POINTER(Src), c_vp, c_i32, c_i64, c_vp, c_vp]),
+    "rth_replay_sample": (c_i32, [c_vp, c_i64, c_vp, ctypes.POINTER(c_vp), c_vp, c_vp, c_vp]),
+    "rth_replay_update_priorities": (c_i32, [c_vp, c_vp, c_vp, c_i32, c_i64, c_i32, c_vp]),
     "rth_replay_gather": (c_i32, [c_vp, c_vp, c_i64, ctypes.POINTER(c_vp), c_vp]),
     "rth_replay_info": (c_i32, [c_vp, ctypes.POINTER(c_i64), ctypes.POINTER(c_i64),
-                                ctypes.POINTER(c_i64), ctypes.POINTER(c_i64)]),
+                                ctypes.POINTER(c_i64), ctypes.POINTER(c_i64), ctypes.POINTER(c_i64)]),
     "rth_replay_tree": (c_vp, [c_vp]),
     "rth_replay_column": (c_vp, [c_vp, c_i32]),
-    "rth_copy_rows": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i32, c_vp]),
+    "rth_copy_rows": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i32, c_i32, c_vp]),
     # actors
-    "rth_eps_greedy": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_u64, c_u64, c_vp, c_vp]),
+    "rth_eps_greedy": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_u64, c_u64, c_vp, c_vp, c_vp]),
+    "rth_counter_add": (c_i32, [c_vp, c_i64, c_vp]),
     "rth_nstep_create": (c_i32, [c_i64, c_i32, c_f64, c_i32, c_i32, ctypes.POINTER(c_vp)]),
     "rth_nstep_destroy": (c_i32, [c_vp]),
     "rth_nstep_reset": (c_i32, [c_vp, c_vp]),
     "rth_nstep_push": (c_i32, [c_vp] + [c_vp] * 11 + [c_vp]),
-    "rth_synth_env_step": (c_i32, [c_vp, c_i64, c_i32, c_i64, c_vp, c_vp, c_u64, c_f32, c_f32,
+    "rth_synth_env_step": (c_i32, [c_vp, c_i64, c_i32, c_i64, c_vp, c_vp, c_vp, c_u64, c_f32, c_f32,
                                    c_vp, c_vp, c_vp, c_vp, c_vp]),
     "rth_synth_env_reset": (c_i32, [c_vp, c_i64, c_i32, c_u64, c_vp, c_vp]),
     # learner

@@ -40,7 +40,8 @@ def apex_epsilons(n, offset=0, total=None):
 
 class VecActors:
     def __init__(self, n_actors, num_actions, n_step=3, gamma=0.99, device=None, seed=0, eps=None,
-                 actor_offset=0, total_actors=None, p_reward=0.02, p_done=1.0 / 2000, nstep_mode=0):
+                 actor_offset=0, total_actors=None, p_reward=0.02, p_done=1.0 / 2000, nstep_mode=0,
+                 channels_last=False):
         self.N = int(n_actors)
         self.A = int(num_actions)
         self.n_step, self.gamma = int(n_step), float(gamma)
@@ -58,8 +59,10 @@ class VecActors:
         self.cur_slot = torch.empty(N, dtype=torch.int64, device=dev)
         e = apex_epsilons(N, actor_offset, total_actors) if eps is None else np.broadcast_to(np.asarray(eps, np.float64), (N,))
         self.eps = torch.as_tensor(np.ascontiguousarray(e), dtype=torch.float64, device=dev)
-        self.obs = torch.empty((N, *OBS_SHAPE), dtype=torch.float32, device=dev)
-        self.rows_f32 = torch.empty((2 * N, *OBS_SHAPE), dtype=torch.float32, device=dev)
+        self.channels_last = bool(channels_last)
+        fmt = torch.channels_last if channels_last else torch.contiguous_format
+        self.obs = torch.empty((N, *OBS_SHAPE), dtype=torch.float32, device=dev, memory_format=fmt)
+        self.rows_f32 = torch.empty((2 * N, *OBS_SHAPE), dtype=torch.float32, device=dev, memory_format=fmt)
         z = lambda dt: torch.zeros(N, dtype=dt, device=dev)
         self.action, self.s0_h, self.s1_h = z(torch.int64), z(torch.int64), z(torch.int64)
         self.reward, self.done = z(torch.float32), z(torch.float32)
@@ -70,7 +73,8 @@ class VecActors:
         h = _lib.c_vp()
         call("rth_nstep_create", N, self.n_step, self.gamma, int(nstep_mode), dev.index, _lib.ctypes.byref(h))
         self._nstep = h.value
-        self.t = 0           # env steps taken (per actor)
+        self.t = 0           # env steps taken (per actor): host mirror of t_dev
+        self.t_dev = torch.zeros(1, dtype=torch.int64, device=dev)  # what the kernels read
         self.pushes = 0
         call("rth_synth_env_reset", ptr(self.frames), N, ring, self.seed, ptr(self.cur_slot), stream_ptr())
 
@@ -89,7 +93,7 @@ class VecActors:
 
     def gather_f32(self, handles, out):
         call("rth_copy_rows", ptr(out), 0, None, ptr(self.frames), 0, ptr(handles), handles.numel(), STACK_ELEMS,
-             _lib.RTH_U8, _lib.RTH_F32, stream_ptr())
+             _lib.RTH_U8, _lib.RTH_F32, OBS_SHAPE[0] if self.channels_last else 0, stream_ptr())
         return out
 
     def current_obs_handles(self):
@@ -103,14 +107,17 @@ class VecActors:
         """one environment step for every actor; returns True when rows were emitted"""
         s = stream_ptr()
         self.t += 1
+        call("rth_counter_add", ptr(self.t_dev), 1, s)
         # acting batch: current stacks -> f32 (Worker.step -> exploration.act -> solver.act)
         self.gather_f32(self.current_obs_handles(), self.obs)
         q = q_net(self.obs)
         if q.dtype != torch.float32 or not q.is_contiguous():
             q = q.float().contiguous()
-        call("rth_eps_greedy", ptr(q), self.N, self.A, ptr(self.eps), None, None, self.seed, self.t, ptr(self.action), s)
-        call("rth_synth_env_step", ptr(self.frames), self.N, self.ring, self.t, ptr(self.cur_slot), ptr(self.action),
-             self.seed, self.p_reward, self.p_done, ptr(self.reward), ptr(self.done), ptr(self.s0_h), ptr(self.s1_h), s)
+        call("rth_eps_greedy", ptr(q), self.N, self.A, ptr(self.eps), None, None, self.seed, 0, ptr(self.t_dev),
+             ptr(self.action), s)
+        call("rth_synth_env_step", ptr(self.frames), self.N, self.ring, 0, ptr(self.t_dev), ptr(self.cur_slot),
+             ptr(self.action), self.seed, self.p_reward, self.p_done, ptr(self.reward), ptr(self.done), ptr(self.s0_h),
+             ptr(self.s1_h), s)
         call("rth_nstep_push", self._nstep, ptr(self.s0_h), ptr(self.action), ptr(self.reward), ptr(self.s1_h),
              ptr(self.done), ptr(self.emit), ptr(self.row_s0), ptr(self.row_a), ptr(self.row_r), ptr(self.row_s1),
              ptr(self.row_done), s)
@@ -140,9 +147,9 @@ class VecActors:
                 self.row_done.clone())
 
 
-def apex_columns():
+def apex_columns(channels_last=False):
     """replay columns of the apex-dqn rows [s0, a, r, s1, done] (worker.py:47-51): frames are
     stored uint8 and sampled as float32 (exact), the rest as the reference casts them"""
     from .replay import Column
-    return [Column(OBS_SHAPE, torch.uint8, torch.float32), Column((), torch.int64), Column((), torch.float32),
-            Column(OBS_SHAPE, torch.uint8, torch.float32), Column((), torch.float32)]
+    fr = lambda: Column(OBS_SHAPE, torch.uint8, torch.float32, channels_last=channels_last)
+    return [fr(), Column((), torch.int64), Column((), torch.float32), fr(), Column((), torch.float32)]

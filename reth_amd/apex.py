@@ -6,10 +6,23 @@ worker.py:21-61 (actor loop), config.yaml (hyper-parameters, defaults below), tr
 52-61 (K replay shards of C // K).
 
 Per GPU, everything lives in HBM: the actors' frame rings and n-step deques, the replay
-shard (storage + sum-tree), the learner's networks and the actors' weight copy.  One
-iteration = `actor_steps_per_update` vectorised actor steps (N env steps each) + one
-learner update.  The stream order reproduces the reference's sampler semantics: the next
-batch is sampled before the current batch's priorities are written back (HWM-1 PUSH).
+shard (storage + sum-tree + its device-resident sampler state), the learner's networks and
+the actors' weight copy.  One iteration = `actor_steps_per_update` vectorised actor steps
+(N env steps each) + one learner update, in this order:
+
+    actor compute (act, env, n-step, priorities)   append(t)
+    learner train on batch k (forward, TD, backward, clip, Adam)
+    sample + gather batch k+1                      update_priorities(k)
+
+The replay/tree operations run in the reference's order: batch k+1 is sampled before batch
+k's priorities land (the sampler's HWM-1 PUSH, server/sampler_loop.py:13-15, 36-39).
+
+With `hip_graph` the two compute blocks are captured once (the learner's in two copies, one
+per batch-slot parity) and replayed every iteration; the handful of replay-tree launches
+between them stay eager, so the tree-op order, the host counters and the HIP-event timing
+of the gather are exactly those of the eager schedule.  All per-step scalars the kernels
+need (FIFO tail, Philox counters, beta schedule step, env step) live in device memory, so
+the captured launches are valid on every replay.
 """
 from dataclasses import dataclass, field
 
@@ -19,7 +32,7 @@ from .actors import OBS_SHAPE, VecActors, apex_columns
 from .dist import GradAllReduce
 from .model import DQNNetwork
 from .replay import HbmReplay
-from .reth_buffer import TorchCudaLoader, start_per, _SERVICES
+from .reth_buffer import TorchCudaLoader, _SERVICES, start_per
 from .solver import Box, DQNSolver, Discrete
 from .trainer import Trainer
 from .weights import WeightsSlot, WeightsSubscriber
@@ -47,8 +60,10 @@ class ApexConfig:
     p_reward: float = 0.02
     p_done: float = 1.0 / 2000
     nstep_mode: int = 0            # 0 = numpy-1.19 promotion (the reference's pin)
-    prefetch: int = 1
     fused_adam: bool = True
+    channels_last: bool = True     # NHWC end to end (gather writes it, MIOpen consumes it)
+    conv_benchmark: bool = False   # torch.backends.cudnn.benchmark (MIOpen find)
+    hip_graph: bool = False        # replay captured HIP graphs of the compute blocks
     extra: dict = field(default_factory=dict)
 
 
@@ -63,32 +78,38 @@ class ApexDQN:
         self.device = torch.device(device if device is not None else "cuda")
         self.rank, self.world = rank, world
         hook = GradAllReduce(group) if world > 1 else None
+        torch.backends.cudnn.benchmark = bool(cfg.conv_benchmark)
+        fmt = torch.channels_last if cfg.channels_last else torch.contiguous_format
         torch.manual_seed(cfg.seed)  # identical initial weights on every rank
         self.solver = DQNSolver(Box(0, 255, OBS_SHAPE), Discrete(cfg.num_actions), gamma=cfg.gamma,
                                 clip_value=cfg.clip_value, double_q=True, dueling=True,
                                 learning_rate=cfg.learning_rate, adam_epsilon=cfg.adam_epsilon,
                                 update_target_interval=cfg.update_target_interval, device=self.device,
-                                n_step=cfg.n_step, fused_adam=cfg.fused_adam, grad_hook=hook)
+                                n_step=cfg.n_step, fused_adam=cfg.fused_adam, grad_hook=hook,
+                                channels_last=cfg.channels_last, capturable=cfg.hip_graph)
         self.trainer = Trainer(self.solver, logger=logger or _Quiet(), print_interval=1000)
-        self.actor_net = DQNNetwork(OBS_SHAPE, cfg.num_actions).to(self.device).requires_grad_(False)
+        self.actor_net = DQNNetwork(OBS_SHAPE, cfg.num_actions).to(self.device, memory_format=fmt)
+        self.actor_net.requires_grad_(False)
         self.slot = WeightsSlot(self.solver.q_network)
         self.slot.acquire(self.actor_net)
         self.subscriber = WeightsSubscriber(self.slot, cfg.recv_weights_interval)
         self.actors = VecActors(cfg.n_actors, cfg.num_actions, cfg.n_step, cfg.gamma, self.device,
                                 seed=cfg.seed * 1000003 + rank, actor_offset=rank * cfg.n_actors,
                                 total_actors=cfg.n_actors * world, p_reward=cfg.p_reward, p_done=cfg.p_done,
-                                nstep_mode=cfg.nstep_mode)
+                                nstep_mode=cfg.nstep_mode, channels_last=cfg.channels_last)
         self.svc, self.addr = start_per(cfg.capacity, cfg.batch_size, alpha=cfg.alpha, beta=cfg.beta,
                                         sample_start=cfg.sample_start, device=self.device, seed=cfg.seed + 7919 * rank)
-        self.svc.replay = HbmReplay(cfg.capacity, apex_columns(), cfg.alpha, cfg.beta, self.device,
+        self.svc.replay = HbmReplay(cfg.capacity, apex_columns(cfg.channels_last), cfg.alpha, cfg.beta, self.device,
                                     seed=cfg.seed + 7919 * rank)
         self.replay = self.svc.replay
-        self.loader = TorchCudaLoader(self.addr, buffer_size=cfg.prefetch + 1, prefetch=cfg.prefetch)
+        self.loader = TorchCudaLoader(self.addr, buffer_size=2, prefetch=1)
         self.env_steps = 0
         self.updates = 0
+        self._graphs = None
 
     def close(self):
         _SERVICES.pop(self.addr, None)
+        self._graphs = None
 
     # ------------------------------------------------------------------ replay prefill
     @torch.no_grad()
@@ -109,24 +130,114 @@ class ApexDQN:
             self.replay.append([s0, a, r, s1, d], td)
             done += m
 
-    # ------------------------------------------------------------------ loop
-    def actor_step(self):
-        self.subscriber.maybe_load(self.actor_net, self.actors.t)
+    # ------------------------------------------------------------------ the blocks
+    def _actor_compute(self):
+        """act + env + n-step (+ priorities once rows flow); returns |td| of the rows or None"""
         if self.actors.step(self.actor_net):
-            td = self.actors.prioritise(self.actor_net)
-            self.actors.append(self.replay, td)
-        self.env_steps += self.actors.N
+            return self.actors.prioritise(self.actor_net)
+        return None
 
-    def learner_step(self):
-        data, idx, isw = self.loader.sample_device()
-        td = self.trainer.step(data, weights=isw, device_result=True)
-        self.replay.update_priorities(idx, td, step=True)
+    def _learner_train(self, slot):
+        data, idx, isw = slot
+        return self.trainer.train(data, weights=isw)
+
+    def _actor_host(self):
+        """host-side actor bookkeeping between steps (weights reload: perwez RecvSocket)"""
+        self.subscriber.maybe_load(self.actor_net, self.actors.t)
+
+    def _learner_host(self):
+        """host-side learner bookkeeping after an update (Trainer / Interval / weights send)"""
+        self.trainer.account()
         self.updates += 1
+        if self.solver._update_target_interval is not None and not self.solver.auto_target_update:
+            self.solver._update_target_interval()
         if self.updates % self.cfg.send_weights_interval == 0:
             self.slot.publish(self.solver.q_network)
 
+    # ------------------------------------------------------------------ iteration
     def iteration(self):
+        """one Ape-X iteration, enqueued on this object's own stream (the stream the graphs
+        are captured from); callers synchronise with torch.cuda.synchronize()"""
+        if not hasattr(self, "_stream"):
+            self._stream = torch.cuda.Stream(self.device)
+            self._stream.wait_stream(torch.cuda.current_stream(self.device))  # init + prefill
+        with torch.cuda.stream(self._stream):
+            self._iteration()
+
+    def _iteration(self):
+        if self._graphs is None and self.cfg.hip_graph and self._graph_ready():
+            self._capture()
+        if self._graphs is not None:
+            return self._iteration_graph()
         for _ in range(self.cfg.actor_steps_per_update):
-            self.actor_step()
-        if self.svc.ready():
-            self.learner_step()
+            self._actor_host()
+            td = self._actor_compute()
+            if td is not None:
+                self.actors.append(self.replay, td)
+            self.env_steps += self.actors.N
+        if not self.svc.ready():
+            return
+        if not self.loader.pending():
+            self.loader.issue()
+        slot = self.loader.take()
+        td = self._learner_train(slot)
+        self.loader.issue()  # sample-ahead: batch k+1 before batch k's priorities land
+        self.replay.update_priorities(slot[1], td, step=True)
+        self._learner_host()
+
+    # ------------------------------------------------------------------ graph replay
+    def _graph_ready(self):
+        # capture once the actors emit rows every step, the learner has run eagerly (optimizer
+        # state exists, MIOpen has chosen its kernels) and a batch is pending
+        return self.actors.warm and self.updates >= 2 and self.loader.pending() == 1
+
+    def _capture(self):
+        """Capture the actor block and the learner block (one per batch-slot parity).  With a
+        process group the learner is captured in two parts and the RCCL all-reduce of the
+        gradients runs eagerly between them."""
+        solver = self.solver
+        solver.auto_target_update = False
+        slots = self.loader._slots
+        host = (self.actors.t, self.actors.pushes)
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        split = solver.grad_hook is not None
+        G = dict(act=torch.cuda.CUDAGraph(), learn=[], learn_td=[], apply=None)
+        with torch.cuda.stream(side):
+            with torch.cuda.graph(G["act"], stream=side):
+                G["act_td"] = self._actor_compute()
+            for p in range(2):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=side):
+                    data, idx, isw = slots[p]
+                    td = solver.compute_grads(data, isw)
+                    self.trainer._track(td)
+                    if not split:
+                        solver.apply_grads()
+                G["learn"].append(g)
+                G["learn_td"].append(td)
+            if split:
+                G["apply"] = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(G["apply"], stream=side):
+                    solver.apply_grads()
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        self.actors.t, self.actors.pushes = host  # capture recorded, did not run, the step
+        self._graphs = G
+
+    def _iteration_graph(self):
+        G = self._graphs
+        for _ in range(self.cfg.actor_steps_per_update):
+            self._actor_host()
+            G["act"].replay()
+            self.actors.t += 1
+            self.actors.pushes += 1
+            self.actors.append(self.replay, G["act_td"])
+            self.env_steps += self.actors.N
+        k = self.loader._pending.pop(0)
+        G["learn"][k].replay()
+        if G["apply"] is not None:
+            self.solver.grad_hook(self.solver._params)  # RCCL all-reduce, eager
+            G["apply"].replay()
+        self.loader.issue()  # sample-ahead into the other slot
+        self.replay.update_priorities(self.loader._slots[k][1], G["learn_td"][k], step=True)
+        self._learner_host()

@@ -13,9 +13,10 @@ namespace rth {
 // the launch is one wave per 64 actors.
 __global__ void k_eps_greedy(const float *__restrict__ q, int64_t N, int A, const double *__restrict__ eps,
                              const double *__restrict__ u_in, const int64_t *__restrict__ ra_in, uint64_t seed,
-                             uint64_t counter, int64_t *__restrict__ out) {
+                             uint64_t counter, const int64_t *__restrict__ counter_dev, int64_t *__restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= N) return;
+  if (counter_dev) counter = (uint64_t)*counter_dev;
   const double u = u_in ? u_in[i] : philox_uniform(seed, counter, (uint32_t)i, STREAM_EXPLORE);
   if (u < eps[i]) {
     int64_t ra;
@@ -106,10 +107,11 @@ __device__ __forceinline__ uint4 env_bytes(uint64_t seed, int64_t actor, int64_t
 }
 
 __global__ __launch_bounds__(kEnvThreads) void k_env_step(uint8_t *frames, int ring, int64_t t,
-                                                          int64_t *cur_slot, uint64_t seed, float p_reward,
-                                                          float p_done, float *r_out, float *done_out,
-                                                          int64_t *s0_h, int64_t *s1_h) {
+                                                          const int64_t *t_dev, int64_t *cur_slot, uint64_t seed,
+                                                          float p_reward, float p_done, float *r_out,
+                                                          float *done_out, int64_t *s0_h, int64_t *s1_h) {
   const int64_t i = blockIdx.x;
+  if (t_dev) t = *t_dev;
   const int64_t stack_bytes = 4 * kFrameBytes;
   // reward / done: one Philox block per (actor, t), identical in every lane
   const uint4 rd = env_bytes(seed, i, t, 2, 0);
@@ -161,13 +163,14 @@ struct rth_nstep {
 extern "C" {
 
 int rth_eps_greedy(const float *q, int64_t N, int64_t A, const double *eps, const double *u,
-                   const int64_t *ra, uint64_t seed, uint64_t counter, int64_t *out, void *stream) {
+                   const int64_t *ra, uint64_t seed, uint64_t counter, const int64_t *counter_dev, int64_t *out,
+                   void *stream) {
   RTH_REQUIRE(N >= 0 && A >= 1 && A < (1 << 20), "rth_eps_greedy: bad shape");
   if (N == 0) return RTH_OK;
   RTH_REQUIRE(q && eps && out, "rth_eps_greedy: NULL buffer");
   const int bs = 256;
   hipLaunchKernelGGL(k_eps_greedy, dim3((unsigned)((N + bs - 1) / bs)), dim3(bs), 0, as_stream(stream), q, N,
-                     (int)A, eps, u, ra, seed, counter, out);
+                     (int)A, eps, u, ra, seed, counter, counter_dev, out);
   RTH_LAUNCHED();
   return RTH_OK;
 }
@@ -227,12 +230,12 @@ int rth_nstep_push(rth_nstep *h, const int64_t *s0, const int64_t *a, const floa
   return RTH_OK;
 }
 
-int rth_synth_env_step(uint8_t *frames, int64_t N, int32_t ring, int64_t t, int64_t *cur_slot,
+int rth_synth_env_step(uint8_t *frames, int64_t N, int32_t ring, int64_t t, const int64_t *t_dev, int64_t *cur_slot,
                        const int64_t * /*action: the synthetic dynamics ignore it*/, uint64_t seed, float p_reward,
                        float p_done, float *r_out, float *done_out, int64_t *s0_h, int64_t *s1_h, void *stream) {
   RTH_REQUIRE(frames && cur_slot && r_out && done_out && s0_h && s1_h, "rth_synth_env_step: NULL argument");
-  RTH_REQUIRE(N >= 1 && N < (int64_t(1) << 31) && ring >= 4 && t >= 1, "rth_synth_env_step: bad shape");
-  hipLaunchKernelGGL(k_env_step, dim3((unsigned)N), dim3(kEnvThreads), 0, as_stream(stream), frames, ring, t,
+  RTH_REQUIRE(N >= 1 && N < (int64_t(1) << 31) && ring >= 4 && (t >= 1 || t_dev), "rth_synth_env_step: bad shape");
+  hipLaunchKernelGGL(k_env_step, dim3((unsigned)N), dim3(kEnvThreads), 0, as_stream(stream), frames, ring, t, t_dev,
                      cur_slot, seed, p_reward, p_done, r_out, done_out, s0_h, s1_h);
   RTH_LAUNCHED();
   return RTH_OK;

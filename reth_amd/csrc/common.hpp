@@ -118,6 +118,23 @@ __device__ inline float per_normalize(float w, float alpha) {
   return (float)pow((double)x, (double)alpha);
 }
 
+// Device-resident service state of a replay shard: every per-step scalar a launch needs is
+// read from here, so launches are argument-invariant and a captured HIP graph replays them.
+struct ReplayState {
+  int64_t tail;        // FIFOPolicy.tail (fifo_policy.py:10)
+  int64_t calls;       // sample calls issued (Philox counter)
+  int64_t sched_step;  // Schedule.cur_step shared by alpha and beta (per_sampler.py:30-32)
+  int64_t pad;
+};
+
+// Schedule.value (schedule.py:29-40, 48-52), python float operation order
+__host__ __device__ inline double sched_value(const rth_schedule &s, int64_t step) {
+  if (s.method == RTH_SCHED_CONST) return s.start;
+  const int64_t k = step < s.max_steps ? step : s.max_steps;
+  if (s.method == RTH_SCHED_LINEAR) return s.start + ((s.end - s.start) * (double)k) / (double)s.max_steps;
+  return s.end - (s.end - s.start) * exp((double)(-k) / (double)s.max_steps);
+}
+
 // the same in float64 (numpy float64 arrays: `** 0.5` is sqrt, other exponents pow)
 __device__ inline double per_normalize64(double w, double alpha) {
   const double x = radd(w, 1e-6);

@@ -19,12 +19,13 @@ struct rth_sumtree;
 
 namespace rth {
 int tree_update_impl(rth_sumtree *t, const int64_t *idx, int64_t fifo_start, const double *w64,
-                     const void *td_abs, int32_t td_dtype, double alpha, int64_t n, hipStream_t s);
+                     const void *td_abs, int32_t td_dtype, double alpha, int64_t n, hipStream_t s,
+                     const ReplayState *st, const rth_schedule *alpha_s);
 int tree_sample_impl(rth_sumtree *t, int64_t batch, const double *uniforms, uint64_t seed,
                      uint64_t counter, int is_weights, double beta, int64_t *idx_out, double *out,
-                     hipStream_t s);
+                     hipStream_t s, const ReplayState *st, const rth_schedule *beta_s);
 
-enum Conv : int32_t { CONV_COPY = 0, CONV_U8_F32 = 1 };
+enum Conv : int32_t { CONV_COPY = 0, CONV_U8_F32 = 1, CONV_U8_F32_HWC = 2 };
 
 struct CopyCol {
   const uint8_t *src;
@@ -35,7 +36,7 @@ struct CopyCol {
   int64_t dst_stride;       // bytes
   int64_t in_bytes;         // bytes of one input row
   int32_t conv;
-  int32_t pad;
+  int32_t planes;           // CONV_U8_F32_HWC: channel planes per row (CHW in, HWC out)
 };
 
 struct CopyArgs {
@@ -43,15 +44,27 @@ struct CopyArgs {
   int64_t n;
   int64_t fifo_start;
   int64_t fifo_cap;
+  const ReplayState *st;  // nullable: FIFO start = st->tail (device-resident)
   int32_t dst_fifo;
   int32_t ncols;
 };
 
 constexpr int kCopyThreads = 256;
+constexpr int kStageBytes = 32768;  // one 4x84x84 stack (28,224 B) fits
 
-// grid: x = row, y = column.  One workgroup per (row, column): contiguous 16-byte loads
-// (1 KiB per wave-instruction); uint8 rows become float32 rows (4 x 16-byte stores/lane).
+__device__ __forceinline__ float4 u8x4_to_f4(uint32_t w) {
+  return make_float4((float)(w & 0xffu), (float)((w >> 8) & 0xffu), (float)((w >> 16) & 0xffu), (float)(w >> 24));
+}
+
+// grid: x = row, y = column; one workgroup per (row, column).
+//   COPY        16-byte loads and stores (1 KiB per wave-instruction).
+//   U8_F32      4 pixels per lane-step: a 4-byte load (256 B per wave-instruction) becomes a
+//               16-byte store (1 KiB contiguous per wave-instruction), four steps in flight.
+//   U8_F32_HWC  the row (C planes of H*W bytes) is staged in LDS with 16-byte loads, then
+//               every lane gathers one pixel's C bytes and writes its C floats contiguously:
+//               channels_last f32 for the Q-net, one coalesced 1 KiB store per instruction.
 __global__ __launch_bounds__(kCopyThreads) void k_copy_rows(CopyArgs a) {
+  __shared__ uint4 stage[kStageBytes / 16];
   const int c = blockIdx.y;
   const int64_t i = blockIdx.x;
   if (c >= a.ncols || i >= a.n) return;
@@ -61,7 +74,7 @@ __global__ __launch_bounds__(kCopyThreads) void k_copy_rows(CopyArgs a) {
   if (col.dst_rows)
     dr = col.dst_rows[i];
   else if (a.dst_fifo)
-    dr = (a.fifo_start + i) % a.fifo_cap;
+    dr = ((a.st ? a.st->tail : a.fifo_start) + i) % a.fifo_cap;
   else
     dr = i;
   const uint8_t *__restrict__ src = col.src + sr * col.src_stride;
@@ -69,25 +82,42 @@ __global__ __launch_bounds__(kCopyThreads) void k_copy_rows(CopyArgs a) {
   const int64_t nb = col.in_bytes;
   const int tid = threadIdx.x;
   const bool aligned16 = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0;
-  if (col.conv == CONV_U8_F32) {
-    const int64_t nvec = aligned16 ? nb / 16 : 0;
-    const uint4 *s4 = reinterpret_cast<const uint4 *>(src);
-    float4 *d4 = reinterpret_cast<float4 *>(dst);
-    for (int64_t v = tid; v < nvec; v += kCopyThreads) {
-      const uint4 x = s4[v];
-      const uint32_t w[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        float4 f;
-        f.x = (float)(w[q] & 0xffu);
-        f.y = (float)((w[q] >> 8) & 0xffu);
-        f.z = (float)((w[q] >> 16) & 0xffu);
-        f.w = (float)(w[q] >> 24);
-        d4[v * 4 + q] = f;
+  float *df = reinterpret_cast<float *>(dst);
+  if (col.conv == CONV_U8_F32_HWC) {
+    const int C = col.planes;
+    const int64_t P = nb / C;
+    if (aligned16 && nb % 16 == 0 && nb <= kStageBytes) {
+      const uint4 *s4 = reinterpret_cast<const uint4 *>(src);
+      for (int v = tid; v < nb / 16; v += kCopyThreads) stage[v] = s4[v];
+      __syncthreads();
+      const uint8_t *sb = reinterpret_cast<const uint8_t *>(stage);
+      if (C == 4) {
+        float4 *d4 = reinterpret_cast<float4 *>(dst);
+        for (int64_t p = tid; p < P; p += kCopyThreads)
+          d4[p] = make_float4((float)sb[p], (float)sb[P + p], (float)sb[2 * P + p], (float)sb[3 * P + p]);
+      } else {
+        for (int64_t p = tid; p < P; p += kCopyThreads)
+          for (int k = 0; k < C; ++k) df[p * C + k] = (float)sb[k * P + p];
       }
+    } else {
+      for (int64_t p = tid; p < P; p += kCopyThreads)
+        for (int k = 0; k < C; ++k) df[p * C + k] = (float)src[k * P + p];
     }
-    float *df = reinterpret_cast<float *>(dst);
-    for (int64_t b = nvec * 16 + tid; b < nb; b += kCopyThreads) df[b] = (float)src[b];
+  } else if (col.conv == CONV_U8_F32) {
+    const int64_t nw = aligned16 ? nb / 4 : 0;
+    const uint32_t *s32 = reinterpret_cast<const uint32_t *>(src);
+    float4 *d4 = reinterpret_cast<float4 *>(dst);
+    int64_t v = tid;
+    for (; v + 3 * kCopyThreads < nw; v += 4 * kCopyThreads) {
+      const uint32_t w0 = s32[v], w1 = s32[v + kCopyThreads], w2 = s32[v + 2 * kCopyThreads],
+                     w3 = s32[v + 3 * kCopyThreads];
+      d4[v] = u8x4_to_f4(w0);
+      d4[v + kCopyThreads] = u8x4_to_f4(w1);
+      d4[v + 2 * kCopyThreads] = u8x4_to_f4(w2);
+      d4[v + 3 * kCopyThreads] = u8x4_to_f4(w3);
+    }
+    for (; v < nw; v += kCopyThreads) d4[v] = u8x4_to_f4(s32[v]);
+    for (int64_t b = nw * 4 + tid; b < nb; b += kCopyThreads) df[b] = (float)src[b];
   } else {
     const int64_t nvec = aligned16 ? nb / 16 : 0;
     const uint4 *s4 = reinterpret_cast<const uint4 *>(src);
@@ -97,9 +127,22 @@ __global__ __launch_bounds__(kCopyThreads) void k_copy_rows(CopyArgs a) {
   }
 }
 
-__global__ void k_fifo_slots(int64_t *out, int64_t n, int64_t start, int64_t cap) {
+__global__ void k_fifo_slots(int64_t *out, int64_t n, const ReplayState *st, int64_t cap) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out[i] = (start + i) % cap;
+  if (i < n) out[i] = (st->tail + i) % cap;
+}
+
+// advance the shard's device state after the launches that read it
+__global__ void k_state_bump(ReplayState *st, int64_t dtail, int64_t cap, int64_t dcalls, int64_t dstep) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    st->tail = (st->tail + dtail) % cap;
+    st->calls += dcalls;
+    st->sched_step += dstep;
+  }
+}
+
+__global__ void k_counter_add(int64_t *c, int64_t d) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) *c += d;
 }
 
 int launch_copy(const CopyArgs &a, hipStream_t s) {
@@ -110,13 +153,17 @@ int launch_copy(const CopyArgs &a, hipStream_t s) {
   return RTH_OK;
 }
 
-int conv_of(int32_t in_dtype, int32_t out_dtype, int32_t *conv) {
-  if (in_dtype == out_dtype) {
+int conv_of(int32_t in_dtype, int32_t out_dtype, int32_t planes, int32_t *conv) {
+  if (planes < 0 || planes > 64) {
+    set_error("out_planes %d out of range", planes);
+    return RTH_ERR_INVALID;
+  }
+  if (in_dtype == out_dtype && planes == 0) {
     *conv = CONV_COPY;
     return RTH_OK;
   }
   if (in_dtype == RTH_U8 && out_dtype == RTH_F32) {
-    *conv = CONV_U8_F32;
+    *conv = planes ? CONV_U8_F32_HWC : CONV_U8_F32;
     return RTH_OK;
   }
   set_error("unsupported column conversion %d -> %d", in_dtype, out_dtype);
@@ -135,9 +182,17 @@ struct rth_replay {
   rth_col_desc desc[RTH_MAX_COLS];
   uint8_t *store[RTH_MAX_COLS];
   rth_sumtree *tree;
-  // host-side service state (append_loop / sampler_loop counters)
-  int64_t tail, size, cnt, sample_calls;
+  rth_schedule alpha, beta;
+  ReplayState *st;  // device-resident service state (authoritative)
+  // host mirrors of the service counters (append_loop / sampler_loop bookkeeping)
+  int64_t tail, size, cnt, sample_calls, sched_steps;
 };
+
+static int bump(rth_replay *h, int64_t dtail, int64_t dcalls, int64_t dstep, hipStream_t s) {
+  hipLaunchKernelGGL(k_state_bump, dim3(1), dim3(64), 0, s, h->st, dtail, h->cap, dcalls, dstep);
+  RTH_LAUNCHED();
+  return RTH_OK;
+}
 
 extern "C" {
 int rth_sumtree_create(int64_t capacity, int device, rth_sumtree **out);
@@ -145,32 +200,46 @@ int rth_sumtree_destroy(rth_sumtree *t);
 
 int rth_copy_rows(void *dst, int64_t dst_stride, const int64_t *dst_rows, const void *src, int64_t src_stride,
                   const int64_t *src_rows, int64_t n, int64_t row_elems, int32_t in_dtype, int32_t out_dtype,
-                  void *stream) {
+                  int32_t out_planes, void *stream) {
   RTH_REQUIRE(n == 0 || (dst && src), "rth_copy_rows: NULL buffer");
   RTH_REQUIRE(dtype_size(in_dtype) > 0 && dtype_size(out_dtype) > 0, "rth_copy_rows: bad dtype");
+  RTH_REQUIRE(out_planes == 0 || row_elems % out_planes == 0, "rth_copy_rows: row not divisible into planes");
   CopyArgs a{};
   int32_t conv;
-  int rc = conv_of(in_dtype, out_dtype, &conv);
+  int rc = conv_of(in_dtype, out_dtype, out_planes, &conv);
   if (rc) return rc;
   const int64_t in_bytes = row_elems * dtype_size(in_dtype);
   const int64_t out_bytes = row_elems * dtype_size(out_dtype);
   a.col[0] = CopyCol{(const uint8_t *)src, (uint8_t *)dst, src_rows, dst_rows,
-                     src_stride ? src_stride : in_bytes, dst_stride ? dst_stride : out_bytes, in_bytes, conv, 0};
+                     src_stride ? src_stride : in_bytes, dst_stride ? dst_stride : out_bytes, in_bytes, conv, out_planes};
   a.n = n;
   a.ncols = 1;
   return launch_copy(a, as_stream(stream));
 }
 
-int rth_replay_create(int64_t capacity, int32_t n_cols, const rth_col_desc *cols, int device, uint64_t seed,
-                      rth_replay **out) {
-  RTH_REQUIRE(out && cols, "rth_replay_create: NULL argument");
+int rth_counter_add(int64_t *c, int64_t d, void *stream) {
+  RTH_REQUIRE(c, "rth_counter_add: NULL counter");
+  hipLaunchKernelGGL(k_counter_add, dim3(1), dim3(64), 0, as_stream(stream), c, d);
+  RTH_LAUNCHED();
+  return RTH_OK;
+}
+
+int rth_replay_create(int64_t capacity, int32_t n_cols, const rth_col_desc *cols, const rth_schedule *alpha,
+                      const rth_schedule *beta, int device, uint64_t seed, rth_replay **out) {
+  RTH_REQUIRE(out && cols && alpha && beta, "rth_replay_create: NULL argument");
+  for (const rth_schedule *sc : {alpha, beta})
+    RTH_REQUIRE(sc->method >= RTH_SCHED_CONST && sc->method <= RTH_SCHED_EXP &&
+                    (sc->method == RTH_SCHED_CONST || sc->max_steps >= 1),
+                "rth_replay_create: bad schedule (method %d, max_steps %lld)", sc->method, (long long)sc->max_steps);
   RTH_REQUIRE(n_cols >= 1 && n_cols <= RTH_MAX_COLS, "rth_replay_create: n_cols=%d not in [1,%d]", n_cols,
               RTH_MAX_COLS);
   RTH_REQUIRE(capacity >= 1, "rth_replay_create: capacity must be >= 1");
   for (int c = 0; c < n_cols; ++c) {
     int32_t conv;
     RTH_REQUIRE(cols[c].row_elems >= 1, "rth_replay_create: column %d has no elements", c);
-    int rc = conv_of(cols[c].in_dtype, cols[c].out_dtype, &conv);
+    RTH_REQUIRE(cols[c].out_planes == 0 || cols[c].row_elems % cols[c].out_planes == 0,
+                "rth_replay_create: column %d not divisible into %d planes", c, cols[c].out_planes);
+    int rc = conv_of(cols[c].in_dtype, cols[c].out_dtype, cols[c].out_planes, &conv);
     if (rc) return rc;
   }
   RTH_HIP(hipSetDevice(device));
@@ -179,6 +248,14 @@ int rth_replay_create(int64_t capacity, int32_t n_cols, const rth_col_desc *cols
   h->device = device;
   h->seed = seed;
   h->ncols = n_cols;
+  h->alpha = *alpha;
+  h->beta = *beta;
+  if (hipMalloc(&h->st, sizeof(ReplayState)) != hipSuccess) {
+    delete h;
+    set_error("rth_replay_create: hipMalloc(state) failed");
+    return RTH_ERR_NOMEM;
+  }
+  RTH_HIP(hipMemset(h->st, 0, sizeof(ReplayState)));
   for (int c = 0; c < n_cols; ++c) {
     h->desc[c] = cols[c];
     const size_t bytes = (size_t)capacity * cols[c].row_elems * dtype_size(cols[c].in_dtype);
@@ -203,6 +280,7 @@ int rth_replay_destroy(rth_replay *h) {
   if (!h) return RTH_OK;
   (void)hipSetDevice(h->device);
   for (int c = 0; c < h->ncols; ++c) (void)hipFree(h->store[c]);
+  (void)hipFree(h->st);
   rth_sumtree_destroy(h->tree);
   delete h;
   return RTH_OK;
@@ -214,17 +292,18 @@ void *rth_replay_column(rth_replay *h, int32_t c) {
   return (h && c >= 0 && c < h->ncols) ? (void *)h->store[c] : nullptr;
 }
 
-int rth_replay_info(const rth_replay *h, int64_t *size, int64_t *tail, int64_t *cnt, int64_t *calls) {
+int rth_replay_info(const rth_replay *h, int64_t *size, int64_t *tail, int64_t *cnt, int64_t *calls, int64_t *steps) {
   RTH_REQUIRE(h, "rth_replay_info: NULL handle");
   if (size) *size = h->size;
   if (tail) *tail = h->tail;
   if (cnt) *cnt = h->cnt;
   if (calls) *calls = h->sample_calls;
+  if (steps) *steps = h->sched_steps;
   return RTH_OK;
 }
 
 int rth_replay_append(rth_replay *h, const rth_src *srcs, const void *td_abs, int32_t td_dtype, int64_t n,
-                      double alpha, int64_t *idx_out, void *stream) {
+                      int64_t *idx_out, void *stream) {
   RTH_REQUIRE(h && srcs, "rth_replay_append: NULL argument");
   RTH_REQUIRE(n >= 0 && n <= h->cap, "rth_replay_append: n=%lld exceeds capacity %lld (fifo_policy.py:12)",
               (long long)n, (long long)h->cap);
@@ -241,17 +320,18 @@ int rth_replay_append(rth_replay *h, const rth_src *srcs, const void *td_abs, in
   a.n = n;
   a.ncols = h->ncols;
   a.dst_fifo = 1;
-  a.fifo_start = h->tail;
+  a.st = h->st;
   a.fifo_cap = h->cap;
   int rc = launch_copy(a, s);
   if (rc) return rc;
-  rc = tree_update_impl(h->tree, nullptr, h->tail, nullptr, td_abs, td_dtype, alpha, n, s);
+  rc = tree_update_impl(h->tree, nullptr, 0, nullptr, td_abs, td_dtype, 0.0, n, s, h->st, &h->alpha);
   if (rc) return rc;
   if (idx_out) {  // FIFO slots for the caller (the append_loop's `indices`)
-    hipLaunchKernelGGL(k_fifo_slots, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, idx_out, n, h->tail,
-                       h->cap);
+    hipLaunchKernelGGL(k_fifo_slots, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, idx_out, n, h->st, h->cap);
     RTH_LAUNCHED();
   }
+  rc = bump(h, n, 0, 0, s);
+  if (rc) return rc;
   h->tail = (h->tail + n) % h->cap;
   h->size = h->size + n < h->cap ? h->size + n : h->cap;
   h->cnt += n;
@@ -265,21 +345,22 @@ int rth_replay_gather(rth_replay *h, const int64_t *idx, int64_t n, void *const 
     RTH_REQUIRE(out_cols[c], "rth_replay_gather: output column %d is NULL", c);
     const rth_col_desc &d = h->desc[c];
     int32_t conv;
-    conv_of(d.in_dtype, d.out_dtype, &conv);
+    conv_of(d.in_dtype, d.out_dtype, d.out_planes, &conv);
     const int64_t ib = d.row_elems * dtype_size(d.in_dtype), ob = d.row_elems * dtype_size(d.out_dtype);
-    a.col[c] = CopyCol{h->store[c], (uint8_t *)out_cols[c], idx, nullptr, ib, ob, ib, conv, 0};
+    a.col[c] = CopyCol{h->store[c], (uint8_t *)out_cols[c], idx, nullptr, ib, ob, ib, conv, d.out_planes};
   }
   a.n = n;
   a.ncols = h->ncols;
   return launch_copy(a, as_stream(stream));
 }
 
-int rth_replay_sample(rth_replay *h, int64_t batch, double beta, const double *uniforms, void *const *out_cols,
+int rth_replay_sample(rth_replay *h, int64_t batch, const double *uniforms, void *const *out_cols,
                       int64_t *idx_out, double *isw_out, void *stream) {
   RTH_REQUIRE(h && batch > 0 && idx_out && isw_out, "rth_replay_sample: bad arguments");
   hipStream_t s = as_stream(stream);
-  int rc = tree_sample_impl(h->tree, batch, uniforms, h->seed, (uint64_t)h->sample_calls, 1, beta, idx_out,
-                            isw_out, s);
+  int rc = tree_sample_impl(h->tree, batch, uniforms, h->seed, 0, 1, 0.0, idx_out, isw_out, s, h->st, &h->beta);
+  if (rc) return rc;
+  rc = bump(h, 0, 1, 0, s);
   if (rc) return rc;
   h->sample_calls++;
   if (out_cols) return rth_replay_gather(h, idx_out, batch, out_cols, stream);
@@ -287,9 +368,16 @@ int rth_replay_sample(rth_replay *h, int64_t batch, double beta, const double *u
 }
 
 int rth_replay_update_priorities(rth_replay *h, const int64_t *idx, const void *td_abs, int32_t td_dtype, int64_t n,
-                                 double alpha, void *stream) {
+                                 int32_t step, void *stream) {
   RTH_REQUIRE(h && (n == 0 || (idx && td_abs)), "rth_replay_update_priorities: bad arguments");
-  int rc = tree_update_impl(h->tree, idx, 0, nullptr, td_abs, td_dtype, alpha, n, as_stream(stream));
+  hipStream_t s = as_stream(stream);
+  int rc;
+  if (step) {  // sampler_loop.py:32-33: on_step() before the update
+    rc = bump(h, 0, 0, 1, s);
+    if (rc) return rc;
+    h->sched_steps++;
+  }
+  rc = tree_update_impl(h->tree, idx, 0, nullptr, td_abs, td_dtype, 0.0, n, s, h->st, &h->alpha);
   if (rc) return rc;
   h->cnt += n;
   return RTH_OK;

@@ -104,12 +104,14 @@ struct UpdArgs {
   int32_t td_dtype;      // ... in float32 (RTH_F32) or float64 (RTH_F64), like numpy
   double alpha;
   int64_t n;
+  const ReplayState *st;  // nullable: a replay shard's device state supplies the FIFO start
+  rth_schedule alpha_s;   // and alpha = alpha_s(st->sched_step)
 };
 
-__device__ __forceinline__ double priority_of(const UpdArgs &a, int64_t src) {
+__device__ __forceinline__ double priority_of(const UpdArgs &a, double alpha, int64_t src) {
   if (a.w64) return a.w64[src];
-  if (a.td_dtype == RTH_F64) return per_normalize64(static_cast<const double *>(a.td_abs)[src], a.alpha);
-  return (double)per_normalize(static_cast<const float *>(a.td_abs)[src], (float)a.alpha);
+  if (a.td_dtype == RTH_F64) return per_normalize64(static_cast<const double *>(a.td_abs)[src], alpha);
+  return (double)per_normalize(static_cast<const float *>(a.td_abs)[src], (float)alpha);
 }
 
 __device__ __forceinline__ int64_t key_index(uint64_t key, int maxd) {
@@ -122,6 +124,8 @@ __global__ __launch_bounds__(kUpdThreads) void k_tree_update(UpdArgs a) {
   __shared__ uint64_t keys[kUpdChunk];
   const int tid = threadIdx.x;
   const int maxd = a.maxd;
+  const int64_t fifo_start = a.st ? a.st->tail : a.fifo_start;
+  const double alpha = a.st ? sched_value(a.alpha_s, a.st->sched_step) : a.alpha;
   for (int64_t cs = 0; cs < a.n; cs += kUpdChunk) {
     const int m = (int)min<int64_t>(kUpdChunk, a.n - cs);
     int P = 2;
@@ -129,7 +133,7 @@ __global__ __launch_bounds__(kUpdThreads) void k_tree_update(UpdArgs a) {
     for (int j = tid; j < P; j += kUpdThreads) {
       uint64_t key = ~0ull;
       if (j < m) {
-        const int64_t id = a.idx ? a.idx[cs + j] : (a.fifo_start + cs + j) % a.cap;
+        const int64_t id = a.idx ? a.idx[cs + j] : (fifo_start + cs + j) % a.cap;
         if (id >= 0 && id < a.cap) {
           const int d = node_depth(id);
           const uint64_t aligned = (uint64_t)(id + 1) << (maxd - d);
@@ -164,7 +168,7 @@ __global__ __launch_bounds__(kUpdThreads) void k_tree_update(UpdArgs a) {
       const bool last = (j == m - 1) || keys[j + 1] == ~0ull || key_index(keys[j + 1], maxd) != id;
       if (last) {
         const int64_t src = cs + (int64_t)(key & ((1u << kPosBits) - 1));
-        a.nd[id + 1].val = priority_of(a, src);
+        a.nd[id + 1].val = priority_of(a, alpha, src);
       }
     }
     __syncthreads();
@@ -202,10 +206,14 @@ __global__ void k_tree_find(const Node *__restrict__ nd, int64_t cap, const doub
 // _numba_sample (sumtree.py:70-79) and, with is_weights, PERSampler.sample (:24-28)
 __global__ void k_tree_sample(const Node *__restrict__ nd, int64_t cap, int64_t batch,
                               const double *__restrict__ uniforms, uint64_t seed, uint64_t counter,
-                              int is_weights, double beta, int64_t *__restrict__ idx_out,
-                              double *__restrict__ out) {
+                              int is_weights, double beta, const ReplayState *st, rth_schedule beta_s,
+                              int64_t *__restrict__ idx_out, double *__restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= batch) return;
+  if (st) {  // a replay shard's device state: call counter and beta_s(sched_step)
+    counter = (uint64_t)st->calls;
+    beta = sched_value(beta_s, st->sched_step);
+  }
   const double total = nd[1].sum;
   const double seg = total / (double)batch;
   const double u = uniforms ? uniforms[i] : philox_uniform(seed, counter, (uint32_t)i, STREAM_SAMPLE);
@@ -260,21 +268,24 @@ struct rth_sumtree {
 
 namespace rth {
 int tree_update_impl(rth_sumtree *t, const int64_t *idx, int64_t fifo_start, const double *w64,
-                     const void *td_abs, int32_t td_dtype, double alpha, int64_t n, hipStream_t s) {
+                     const void *td_abs, int32_t td_dtype, double alpha, int64_t n, hipStream_t s,
+                     const ReplayState *st, const rth_schedule *alpha_s) {
   if (n <= 0) return RTH_OK;
   RTH_REQUIRE(w64 || td_dtype == RTH_F32 || td_dtype == RTH_F64, "priority dtype must be f32 or f64");
-  UpdArgs a{t->nodes, t->cap, t->maxd, idx, fifo_start, w64, td_abs, td_dtype, alpha, n};
+  UpdArgs a{t->nodes, t->cap, t->maxd, idx, fifo_start, w64, td_abs, td_dtype, alpha, n, st,
+            alpha_s ? *alpha_s : rth_schedule{}};
   hipLaunchKernelGGL(k_tree_update, dim3(1), dim3(kUpdThreads), 0, s, a);
   RTH_LAUNCHED();
   return RTH_OK;
 }
 int tree_sample_impl(rth_sumtree *t, int64_t batch, const double *uniforms, uint64_t seed,
                      uint64_t counter, int is_weights, double beta, int64_t *idx_out, double *out,
-                     hipStream_t s) {
+                     hipStream_t s, const ReplayState *st, const rth_schedule *beta_s) {
   if (batch <= 0) return RTH_OK;
   const int bs = 256;
   hipLaunchKernelGGL(k_tree_sample, dim3((unsigned)((batch + bs - 1) / bs)), dim3(bs), 0, s, t->nodes,
-                     t->cap, batch, uniforms, seed, counter, is_weights, beta, idx_out, out);
+                     t->cap, batch, uniforms, seed, counter, is_weights, beta, st,
+                     beta_s ? *beta_s : rth_schedule{}, idx_out, out);
   RTH_LAUNCHED();
   return RTH_OK;
 }
@@ -317,7 +328,7 @@ int rth_sumtree_clear(rth_sumtree *t, void *stream) {
 
 int rth_sumtree_update(rth_sumtree *t, const int64_t *idx, const double *w, int64_t n, void *stream) {
   RTH_REQUIRE(t && (n == 0 || (idx && w)), "rth_sumtree_update: bad arguments");
-  return tree_update_impl(t, idx, 0, w, nullptr, RTH_F64, 0.0, n, as_stream(stream));
+  return tree_update_impl(t, idx, 0, w, nullptr, RTH_F64, 0.0, n, as_stream(stream), nullptr, nullptr);
 }
 
 int rth_sumtree_find(rth_sumtree *t, const double *tg, int64_t n, int64_t *idx_out, double *val_out,
@@ -334,7 +345,8 @@ int rth_sumtree_find(rth_sumtree *t, const double *tg, int64_t n, int64_t *idx_o
 int rth_sumtree_sample(rth_sumtree *t, int64_t batch, const double *uniforms, uint64_t seed,
                        uint64_t counter, int64_t *idx_out, double *val_out, void *stream) {
   RTH_REQUIRE(t && batch > 0 && idx_out, "rth_sumtree_sample: bad arguments");  // assert batch_size > 0 (:73)
-  return tree_sample_impl(t, batch, uniforms, seed, counter, 0, 0.0, idx_out, val_out, as_stream(stream));
+  return tree_sample_impl(t, batch, uniforms, seed, counter, 0, 0.0, idx_out, val_out, as_stream(stream), nullptr,
+                          nullptr);
 }
 
 int rth_sumtree_stats(rth_sumtree *t, double *out2, void *stream) {
@@ -375,13 +387,14 @@ int rth_per_normalize(const float *w, int64_t n, float alpha, float *out, void *
 int rth_per_update(rth_sumtree *t, const int64_t *idx, const void *td_abs, int32_t td_dtype, int64_t n,
                    double alpha, void *stream) {
   RTH_REQUIRE(t && (n == 0 || (idx && td_abs)), "rth_per_update: bad arguments");
-  return tree_update_impl(t, idx, 0, nullptr, td_abs, td_dtype, alpha, n, as_stream(stream));
+  return tree_update_impl(t, idx, 0, nullptr, td_abs, td_dtype, alpha, n, as_stream(stream), nullptr, nullptr);
 }
 
 int rth_per_sample(rth_sumtree *t, int64_t batch, double beta, const double *uniforms, uint64_t seed,
                    uint64_t counter, int64_t *idx_out, double *isw_out, void *stream) {
   RTH_REQUIRE(t && batch > 0 && idx_out && isw_out, "rth_per_sample: bad arguments");
-  return tree_sample_impl(t, batch, uniforms, seed, counter, 1, beta, idx_out, isw_out, as_stream(stream));
+  return tree_sample_impl(t, batch, uniforms, seed, counter, 1, beta, idx_out, isw_out, as_stream(stream), nullptr,
+                          nullptr);
 }
 
 }  // extern "C"

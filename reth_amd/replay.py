@@ -167,20 +167,33 @@ class PERSampler:
 
 
 class Column:
-    """one replay column: per-row shape, storage dtype, sampled dtype"""
+    """one replay column: per-row shape, storage dtype, sampled dtype.  channels_last (uint8
+    (C,H,W) -> float32 only) makes sampled batches channels-last [B,C,H,W] tensors, the
+    memory format the Q-network's NHWC convolutions consume without a transpose."""
 
-    def __init__(self, shape, dtype, out_dtype=None):
+    def __init__(self, shape, dtype, out_dtype=None, channels_last=False):
         self.shape = tuple(int(s) for s in shape)
         self.dtype = dtype
         self.out_dtype = out_dtype or dtype
         self.row_elems = int(np.prod(self.shape)) if self.shape else 1
+        self.channels_last = bool(channels_last)
         if dtype not in _TORCH_TO_RTH:
             raise TypeError(f"unsupported replay column dtype {dtype}")
         if self.out_dtype != dtype and not (dtype == torch.uint8 and self.out_dtype == torch.float32):
             raise TypeError(f"unsupported column conversion {dtype} -> {self.out_dtype}")
+        if self.channels_last and (len(self.shape) != 3 or self.out_dtype != torch.float32 or dtype != torch.uint8):
+            raise TypeError("channels_last needs a uint8 (C,H,W) column sampled as float32")
+
+    @property
+    def out_planes(self):
+        return self.shape[0] if self.channels_last else 0
 
     def desc(self):
-        return ColDesc(self.row_elems, _TORCH_TO_RTH[self.dtype], _TORCH_TO_RTH[self.out_dtype])
+        return ColDesc(self.row_elems, _TORCH_TO_RTH[self.dtype], _TORCH_TO_RTH[self.out_dtype], self.out_planes, 0)
+
+    def empty_out(self, n, device):
+        fmt = torch.channels_last if self.channels_last else torch.contiguous_format
+        return torch.empty((n, *self.shape), dtype=self.out_dtype, device=device, memory_format=fmt)
 
 
 class HbmReplay:
@@ -202,8 +215,8 @@ class HbmReplay:
         descs = (ColDesc * len(columns))(*[c.desc() for c in columns])
         h = c_vp()
         with torch.cuda.device(self.device):
-            call("rth_replay_create", self.capacity, len(columns), descs, self.device.index, int(seed),
-                 ctypes.byref(h))
+            call("rth_replay_create", self.capacity, len(columns), descs, ctypes.byref(sched_struct(self.alpha)),
+                 ctypes.byref(sched_struct(self.beta)), self.device.index, int(seed), ctypes.byref(h))
         self._h = h.value
         self.tree = SumTree(self.capacity, self.device, _handle=_lib.lib().rth_replay_tree(self._h))
 
@@ -217,9 +230,10 @@ class HbmReplay:
 
     # ---------------------------------------------------------------- counters
     def info(self):
-        vals = [c_i64() for _ in range(4)]
+        """host mirrors: (size, tail, cnt, sample_calls, schedule steps)"""
+        vals = [c_i64() for _ in range(5)]
         call("rth_replay_info", self._h, *[ctypes.byref(v) for v in vals])
-        return tuple(v.value for v in vals)  # size, tail, cnt, sample_calls
+        return tuple(v.value for v in vals)
 
     @property
     def size(self):
@@ -257,8 +271,7 @@ class HbmReplay:
             keep.append(t)
             stride = 0 if row_strides is None else int(row_strides[c])
             srcs[c] = Src(ptr(t), ptr(rows), stride)
-        call("rth_replay_append", self._h, srcs, ptr(w), wt, n, float(self.alpha.value()), ptr(idx_out),
-             stream_ptr())
+        call("rth_replay_append", self._h, srcs, ptr(w), wt, n, ptr(idx_out), stream_ptr())
         return n
 
     def sample_into(self, batch_size, out_cols, idx_out, isw_out, uniforms=None, gather_timer=None):
@@ -268,19 +281,17 @@ class HbmReplay:
         u = None if uniforms is None else as_device(uniforms, torch.float64, self.device)
         arr = (c_vp * len(out_cols))(*[ptr(t) for t in out_cols])
         if gather_timer is None:
-            call("rth_replay_sample", self._h, batch_size, float(self.beta.value()), ptr(u), arr, ptr(idx_out),
-                 ptr(isw_out), stream_ptr())
+            call("rth_replay_sample", self._h, batch_size, ptr(u), arr, ptr(idx_out), ptr(isw_out), stream_ptr())
             return
         s = stream_ptr()
-        call("rth_replay_sample", self._h, batch_size, float(self.beta.value()), ptr(u), None, ptr(idx_out),
-             ptr(isw_out), s)
+        call("rth_replay_sample", self._h, batch_size, ptr(u), None, ptr(idx_out), ptr(isw_out), s)
         ev0, ev1 = gather_timer()
         ev0.record()
         call("rth_replay_gather", self._h, ptr(idx_out), batch_size, arr, s)
         ev1.record()
 
     def new_batch(self, batch_size):
-        cols = [torch.empty((batch_size, *c.shape), dtype=c.out_dtype, device=self.device) for c in self.columns]
+        cols = [c.empty_out(batch_size, self.device) for c in self.columns]
         idx = torch.empty(batch_size, dtype=torch.int64, device=self.device)
         isw = torch.empty(batch_size, dtype=torch.float64, device=self.device)
         return cols, idx, isw
@@ -293,25 +304,31 @@ class HbmReplay:
     def gather(self, indices, out_cols=None):
         idx = as_device(indices, torch.int64, self.device)
         if out_cols is None:
-            out_cols = [torch.empty((idx.numel(), *c.shape), dtype=c.out_dtype, device=self.device)
-                        for c in self.columns]
+            out_cols = [c.empty_out(idx.numel(), self.device) for c in self.columns]
         arr = (c_vp * len(out_cols))(*[ptr(t) for t in out_cols])
         call("rth_replay_gather", self._h, ptr(idx), idx.numel(), arr, stream_ptr())
         return out_cols
 
-    def on_step(self):
-        self.alpha.step()
-        self.beta.step()
-
     def update_priorities(self, indices, td_abs, step=False):
-        """Client.update_priorities -> sampler_loop: on_step() first when step (:32-35)."""
+        """Client.update_priorities -> sampler_loop: on_step() first when step (:32-35).
+        The device owns the schedules; the host Schedules mirror them for inspection."""
         if step:
-            self.on_step()
+            self.alpha.step()
+            self.beta.step()
         idx = as_device(indices, torch.int64, self.device)
         w, wt = _prio_tensor(td_abs, self.device)
         assert idx.numel() == w.numel()  # client.py:38
-        call("rth_replay_update_priorities", self._h, ptr(idx), ptr(w), wt, idx.numel(),
-             float(self.alpha.value()), stream_ptr())
+        call("rth_replay_update_priorities", self._h, ptr(idx), ptr(w), wt, idx.numel(), int(bool(step)),
+             stream_ptr())
+
+
+def sched_struct(s):
+    """Schedule -> rth_schedule (the device evaluates it in the same operation order)"""
+    from ._lib import SCHED_CONST, SCHED_EXP, SCHED_LINEAR, Sched
+
+    if s.method == "const":
+        return Sched(SCHED_CONST, 0, float(s.const), float(s.const), 1)
+    return Sched(SCHED_LINEAR if s.method == "linear" else SCHED_EXP, 0, s.start, s.end, s.max_steps)
 
 
 def _wrap_device(p, n, dtype, device):

@@ -172,6 +172,19 @@ class TorchCudaLoader:
         self._pending = []  # slot ids already sampled, oldest first
         self.gather_timer = None  # bench hook: events around the gather launch
 
+    def pending(self):
+        return len(self._pending)
+
+    def take(self):
+        """the oldest already-sampled batch (no replay operation is enqueued)"""
+        k = self._pending.pop(0)
+        return self._slots[k]
+
+    def issue(self):
+        """enqueue the PER sample + gather of the next batch into a free slot"""
+        self.svc.check_ready()
+        self._issue()
+
     def _issue(self):
         rep = self.svc.replay
         if self._slots is None:

@@ -115,24 +115,28 @@ class DQNSolver(Algorithm):
     """reth/reth/algorithm/dqn/dqn_solver.py:14-143 with the same constructor arguments.
 
     grad_hook(params) runs between backward and clip/Adam: the data-parallel learner uses it
-    for the RCCL gradient all-reduce (reth_amd/dist.py)."""
+    for the RCCL gradient all-reduce (reth_amd/dist.py).  channels_last keeps the conv
+    weights NHWC (MIOpen's fp32 implicit-GEMM kernels are NHWC: no transposes)."""
 
     def __init__(self, observation_space, action_space, models=None, gamma=0.99, clip_value=40, double_q=True,
                  dueling=True, learning_rate=5e-5, adam_epsilon=1e-8, update_target_interval=150, device=None,
-                 n_step=1, fused_adam=True, grad_hook=None):
+                 n_step=1, fused_adam=True, grad_hook=None, channels_last=False, capturable=False):
         super().__init__(device)
         obs_shape = tuple(observation_space.shape)
         self.num_actions = int(action_space.n)
         if models is None:
             models = default_models(obs_shape, self.num_actions, dueling, learning_rate, adam_epsilon, fused_adam)
         assert models["q_network"] is not None and models["target_q_network"] is not None
-        self.q_network = models["q_network"].to(self.device)
-        self.target_q_network = models["target_q_network"].to(self.device)
+        fmt = torch.channels_last if channels_last and len(obs_shape) == 3 else torch.preserve_format
+        self.q_network = models["q_network"].to(self.device, memory_format=fmt)
+        self.target_q_network = models["target_q_network"].to(self.device, memory_format=fmt)
         self.target_q_network.requires_grad_(False)
         if models.get("optimizer") is not None:
             self.optimizer = models["optimizer"]
         else:
             kw = {"fused": True} if models.get("fused_adam", fused_adam) else {}
+            if capturable:  # step count on the device: the update can be captured in a HIP graph
+                kw["capturable"] = True
             self.optimizer = torch.optim.Adam(self.q_network.parameters(), lr=models.get("learning_rate", learning_rate),
                                               eps=models.get("adam_epsilon", adam_epsilon), **kw)
         self._params = [p for p in self.q_network.parameters()]
@@ -146,6 +150,8 @@ class DQNSolver(Algorithm):
         self.grad_hook = grad_hook
         self._update_target_interval = (Interval(self.update_target, update_target_interval)
                                         if update_target_interval is not None else None)
+        # graph replay runs the (host-side) target-sync Interval outside the captured step
+        self.auto_target_update = True
 
     # ------------------------------------------------------------------ target / weights
     @torch.no_grad()
@@ -190,8 +196,8 @@ class DQNSolver(Algorithm):
     def calc_loss(self, batch):
         return self.calc_loss_device(batch).cpu()
 
-    def update_device(self, batch, weights=None):
-        """DQNSolver.update (:104-124) returning |td| as a device tensor (no host sync)."""
+    def compute_grads(self, batch, weights=None):
+        """dqn_solver.py:104-117: forward passes, fused TD/Huber, backward -> |td| (device)"""
         s0, a, r, s1, done = self._tensors(batch)
         q0 = self.q_network(s0)
         q1o, q1t = self._forward_targets(s1)
@@ -199,14 +205,23 @@ class DQNSolver(Algorithm):
         loss, td_abs = td_huber_loss(q0, q1o, q1t, a, r, done, isw, self.gamma_n, self.double_q)
         self.optimizer.zero_grad(set_to_none=False)
         loss.backward()
-        if self.grad_hook is not None:
-            self.grad_hook(self._params)
+        self.last_loss = loss.detach()
+        return td_abs
+
+    def apply_grads(self):
+        """dqn_solver.py:118-123: clip_grad_norm_ -> Adam -> target Interval"""
         if self.clip_value >= 0:
             torch.nn.utils.clip_grad_norm_(self._params, self.clip_value, foreach=True)
         self.optimizer.step()
-        if self._update_target_interval is not None:
+        if self.auto_target_update and self._update_target_interval is not None:
             self._update_target_interval()
-        self.last_loss = loss.detach()
+
+    def update_device(self, batch, weights=None):
+        """DQNSolver.update (:104-124) returning |td| as a device tensor (no host sync)."""
+        td_abs = self.compute_grads(batch, weights)
+        if self.grad_hook is not None:
+            self.grad_hook(self._params)
+        self.apply_grads()
         return td_abs
 
     def update(self, batch, weights=None):

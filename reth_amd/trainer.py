@@ -32,7 +32,7 @@ class Trainer:
         self.cur_step = 0
         self.start_time = None
         self.on_step_end = [Interval(self.print, int(print_interval))]
-        self._err_sum = None
+        self._err_acc = None  # persistent device accumulator (in-place: graph-replay safe)
         self._err_n = 0
 
     @property
@@ -41,9 +41,11 @@ class Trainer:
 
     def print(self):
         if self.logger and self._err_n:
-            mean = float(self._err_sum) / self._err_n
+            mean = float(self._err_acc) / self._err_n
             self.logger.info(f"train_cnt: {self.cur_step}, mean_error: {mean:.3f}, time: {self.cur_time:.2f}")
-        self._err_sum, self._err_n = None, 0
+        if self._err_acc is not None:
+            self._err_acc.zero_()
+        self._err_n = 0
 
     def load_weights(self, stream):
         self.solver.load_weights(stream)
@@ -52,18 +54,29 @@ class Trainer:
         return self.solver.save_weights(stream)
 
     def _track(self, td):
-        m = td.float().mean() if torch.is_tensor(td) else torch.tensor(float(td.mean()))
-        self._err_sum = m if self._err_sum is None else self._err_sum + m
-        self._err_n += 1
+        if self._err_acc is None:
+            self._err_acc = torch.zeros((), dtype=torch.float32, device=td.device)
+        self._err_acc.add_(td.float().mean())
+
+    def train(self, batch, **kwargs):
+        """the device work of one step (capturable): update + error accounting"""
+        td = self.solver.update_device(batch, **kwargs)
+        self._track(td)
+        return td
+
+    def account(self, n=1):
+        """host bookkeeping of n steps (eager or graph-replayed)"""
+        if self.start_time is None:
+            self.start_time = time.monotonic()
+        for _ in range(n):
+            self.cur_step += 1
+            self._err_n += 1
+            for f in self.on_step_end:
+                f()
 
     def step(self, batch, device_result=False, **kwargs):
         """one learner update; returns |td| (CPU tensor like the reference, or the device
         tensor with device_result=True)."""
-        if self.start_time is None:
-            self.start_time = time.monotonic()
-        self.cur_step += 1
-        td = self.solver.update_device(batch, **kwargs)
-        self._track(td)
-        for f in self.on_step_end:
-            f()
+        td = self.train(batch, **kwargs)
+        self.account()
         return td if device_result else td.cpu()

@@ -19,11 +19,22 @@ for step in "$@"; do
     bench) run bench 900 python bench.py ;;
     benchq) run bench_quick 600 python bench.py --steps 50 --warmup 10 --cpu-iters 5 ;;
     debug) run debug 300 python scripts/debug_isw.py ;;
+    variants)
+      run bench_nchw 600 python bench.py --steps 100 --warmup 20 --no-cpu-baseline --nchw
+      run bench_cl 600 python bench.py --steps 100 --warmup 20 --no-cpu-baseline
+      run bench_cl_find 900 python bench.py --steps 100 --warmup 20 --no-cpu-baseline --conv-benchmark ;;
+    variants2)
+      run bench_eager 600 python bench.py --steps 100 --warmup 20 --no-cpu-baseline --eager
+      run bench_graph 600 python bench.py --steps 100 --warmup 20 --no-cpu-baseline
+      run bench_graph_nchw 600 python bench.py --steps 100 --warmup 20 --no-cpu-baseline --nchw
+      run bench_graph_nofind 900 python bench.py --steps 100 --warmup 20 --no-cpu-baseline --no-conv-benchmark ;;
     pmc) export TMPDIR=/tmp
          run pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv --kernel-include-regex "rth::" \
             -d "$PWD/gpurun_out/pmc_fetch" -o run -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline
          run pmc_write 900 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv --kernel-include-regex "rth::" \
             -d "$PWD/gpurun_out/pmc_write" -o run -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
+    prof1) export TMPDIR=/tmp; run rocprof_1s 900 rocprofv3 --kernel-trace --stats --output-format csv \
+            -d "$PWD/gpurun_out/prof" -o run -- python bench.py --steps 100 --warmup 20 --no-cpu-baseline ;;
     prof) export TMPDIR=/tmp; run rocprof_stats 900 rocprofv3 --kernel-trace --stats --output-format csv \
             -d "$PWD/gpurun_out/prof" -o run -- python bench.py --steps 100 --warmup 10 --no-cpu-baseline ;;
   esac

@@ -50,7 +50,7 @@ def test_binding_arg_counts_match_header():
 def test_struct_layouts():
     from reth_amd._lib import ColDesc, Src
 
-    assert ctypes.sizeof(ColDesc) == 16
+    assert ctypes.sizeof(ColDesc) == 24
     assert ctypes.sizeof(Src) == 24
 
 

@@ -21,7 +21,7 @@ def test_eps_greedy_explicit_and_philox(dev, orc):
     ra = rng.integers(0, A, N)
     qd, ed, ud, rd = (torch.as_tensor(x, device=dev) for x in (q, eps, u, ra))
     out = torch.empty(N, dtype=torch.int64, device=dev)
-    _lib.call("rth_eps_greedy", qd.data_ptr(), N, A, ed.data_ptr(), ud.data_ptr(), rd.data_ptr(), 0, 0,
+    _lib.call("rth_eps_greedy", qd.data_ptr(), N, A, ed.data_ptr(), ud.data_ptr(), rd.data_ptr(), 0, 0, None,
               out.data_ptr(), _lib.stream_ptr())
     assert np.array_equal(out.cpu().numpy(), orc.eps_greedy(q, eps, u, ra))
     greedy = torch.argmax(torch.as_tensor(q), 1).numpy()
@@ -29,12 +29,18 @@ def test_eps_greedy_explicit_and_philox(dev, orc):
     assert np.array_equal(out.cpu().numpy()[sel], greedy[sel])  # torch.argmax first-max semantics
     # device RNG path: Philox(seed, counter, lane)
     seed, counter = 77, 5
-    _lib.call("rth_eps_greedy", qd.data_ptr(), N, A, ed.data_ptr(), None, None, seed, counter, out.data_ptr(),
-              _lib.stream_ptr())
+    _lib.call("rth_eps_greedy", qd.data_ptr(), N, A, ed.data_ptr(), None, None, seed, counter, None,
+              out.data_ptr(), _lib.stream_ptr())
     pu = np.array([orc.philox_uniform(seed, counter, i, orc.STREAM_EXPLORE) for i in range(N)])
     pra = np.array([(int(orc.philox4x32([i, counter, 0, orc.STREAM_RANDACT], [seed, 0])[0]) * A) >> 32
                     for i in range(N)])
     assert np.array_equal(out.cpu().numpy(), orc.eps_greedy(q, eps, pu, pra))
+    # the counter read from device memory (graph-replay form) gives the same draws
+    cdev = torch.tensor([counter], dtype=torch.int64, device=dev)
+    out2 = torch.empty_like(out)
+    _lib.call("rth_eps_greedy", qd.data_ptr(), N, A, ed.data_ptr(), None, None, seed, 999, cdev.data_ptr(),
+              out2.data_ptr(), _lib.stream_ptr())
+    assert torch.equal(out, out2)
 
 
 @pytest.mark.parametrize("mode", [0, 1])
@@ -89,7 +95,7 @@ def test_synth_env_stack_invariants(dev):
     for t in range(1, 40):
         prev = frames[base + cur].clone()
         prev_cur = cur.clone()
-        _lib.call("rth_synth_env_step", frames.data_ptr(), N, ring, t, cur.data_ptr(), None, 5, 0.5, 0.1,
+        _lib.call("rth_synth_env_step", frames.data_ptr(), N, ring, t, None, cur.data_ptr(), None, 5, 0.5, 0.1,
                   r.data_ptr(), d.data_ptr(), s0.data_ptr(), s1.data_ptr(), _lib.stream_ptr())
         nxt = frames[s1]
         assert torch.equal(s0, base + prev_cur)

@@ -16,7 +16,8 @@ def test_apex_small_end_to_end(dev):
     for _ in range(60):
         ax.iteration()
     torch.cuda.synchronize()
-    size, tail, cnt, calls = ax.replay.info()
+    size, tail, cnt, calls, steps = ax.replay.info()
+    assert steps == ax.updates and calls == ax.updates + 1  # one batch sampled ahead
     assert size == 16 * (60 - cfg.n_step) and ax.env_steps == 16 * 60
     assert ax.updates > 40 and ax.slot.version == ax.updates // 5
     assert ax.subscriber.loaded_version > 0
@@ -27,6 +28,35 @@ def test_apex_small_end_to_end(dev):
     assert torch.equal(out[0], ax.actors.frames[ax.actors.row_s0].float())
     assert torch.equal(out[3], ax.actors.frames[ax.actors.row_s1].float())
     ax.close()
+
+
+def test_graph_replay_matches_eager(dev):
+    """HIP-graph replay of the compute blocks keeps every replay/tree op, counter and Philox
+    stream of the eager schedule: identical replay state (lr = 0 keeps the networks fixed, so
+    MIOpen's atomic weight-gradient reductions cannot make the two runs diverge)"""
+    from reth_amd.apex import ApexConfig, ApexDQN
+
+    def run(graph):
+        cfg = ApexConfig(n_actors=16, capacity=1024, batch_size=32, sample_start=64, learning_rate=0.0,
+                         p_done=0.05, seed=4, hip_graph=graph, send_weights_interval=3,
+                         recv_weights_interval=4, update_target_interval=5)
+        ax = ApexDQN(cfg, device=dev)
+        for _ in range(40):
+            ax.iteration()
+        torch.cuda.synchronize()
+        assert (ax._graphs is not None) == graph
+        s, m, v = ax.replay.tree.export()
+        cols = ax.replay.gather(torch.arange(ax.replay.info()[0], device=dev))
+        out = [s.cpu(), m.cpu(), v.cpu()] + [c.cpu() for c in cols]
+        info = ax.replay.info()
+        ax.close()
+        return out, info
+
+    a, ia = run(False)
+    b, ib = run(True)
+    assert ia == ib
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
 
 
 def test_prefill_then_learn(dev):
@@ -46,3 +76,22 @@ def test_graft_smoke(dev):
     import __graft_entry__
 
     __graft_entry__.smoke()
+
+
+def test_graph_replay_learns(dev):
+    """with learning on, graph replay runs the whole loop: finite weights, target syncs,
+    weights published and reloaded by the actors"""
+    from reth_amd.apex import ApexConfig, ApexDQN
+
+    cfg = ApexConfig(n_actors=32, capacity=4096, batch_size=64, sample_start=128, hip_graph=True, seed=5,
+                     send_weights_interval=4, recv_weights_interval=6, update_target_interval=7)
+    ax = ApexDQN(cfg, device=dev)
+    for _ in range(50):
+        ax.iteration()
+    torch.cuda.synchronize()
+    assert ax._graphs is not None and ax.updates == ax.replay.info()[4]
+    assert ax.trainer.cur_step == ax.updates and ax.slot.version == ax.updates // 4
+    assert ax.subscriber.loaded_version > 0
+    assert all(torch.isfinite(p).all() for p in ax.solver.q_network.parameters())
+    assert int(ax.actors.t_dev.item()) == ax.actors.t == 50
+    ax.close()

@@ -82,7 +82,7 @@ def test_fifo_wraparound_and_u8_widening(dev, orc):
         tree.update(slots, orc.per_normalize(td, 0.5).astype(np.float64))
         for k, s in enumerate(slots):
             written[int(s)] = (frames[k], ids[k])
-    size, gtail, cnt, _ = rep.info()
+    size, gtail, cnt, _, _ = rep.info()
     assert gtail == tail and size == min(cap, cnt)
     s, m, v = rep.tree.export()
     assert np.array_equal(s.cpu().numpy(), tree.sum) and np.array_equal(v.cpu().numpy(), tree.val)
@@ -93,6 +93,34 @@ def test_fifo_wraparound_and_u8_widening(dev, orc):
         f, i = written[int(s_)]
         assert out[1][k].item() == i
         assert torch.equal(out[0][k].cpu(), torch.as_tensor(f).float())
+
+
+@pytest.mark.parametrize("planes,shape", [(4, (4, 84, 84)), (3, (3, 5, 7)), (4, (4, 100, 100))])
+def test_channels_last_gather(dev, planes, shape):
+    """uint8 (C,H,W) rows sampled as channels-last float32 (the NHWC conv input), exact;
+    the 4x100x100 row exceeds the LDS stage and takes the direct path"""
+    from reth_amd import _lib
+    from reth_amd.replay import Column, HbmReplay
+
+    rng = np.random.default_rng(planes)
+    n = 50
+    rows = torch.as_tensor(rng.integers(0, 256, (n, *shape), dtype=np.uint8), device=dev)
+    rep = HbmReplay(64, [Column(shape, torch.uint8, torch.float32, channels_last=True), Column((), torch.int64)],
+                    device=dev)
+    rep.append([rows, torch.arange(n, device=dev)], torch.ones(n, device=dev))
+    idx = torch.as_tensor(rng.integers(0, n, 33), device=dev)
+    out = rep.gather(idx)
+    assert out[0].is_contiguous(memory_format=torch.channels_last)
+    assert torch.equal(out[0], rows[idx].float())
+    # the raw copy kernel in the same mode (actors' acting / priority batches)
+    dst = torch.empty((33, *shape), dtype=torch.float32, device=dev, memory_format=torch.channels_last)
+    _lib.call("rth_copy_rows", dst.data_ptr(), 0, None, rows.data_ptr(), 0, idx.data_ptr(), 33, int(np.prod(shape)),
+              _lib.RTH_U8, _lib.RTH_F32, planes, _lib.stream_ptr())
+    assert torch.equal(dst, rows[idx].float())
+    dst2 = torch.empty((33, *shape), dtype=torch.float32, device=dev)
+    _lib.call("rth_copy_rows", dst2.data_ptr(), 0, None, rows.data_ptr(), 0, idx.data_ptr(), 33, int(np.prod(shape)),
+              _lib.RTH_U8, _lib.RTH_F32, 0, _lib.stream_ptr())
+    assert torch.equal(dst2, rows[idx].float())
 
 
 def test_append_exact_capacity_and_errors(dev):

@@ -172,11 +172,14 @@ int rth_copy_rows(void *dst_dev, int64_t dst_stride, const int64_t *dst_rows_dev
 /* ------------------------------------------------------------------------------------
  * Actor side.
  * ---------------------------------------------------------------------------------- */
+/* dueling (rth_eps_greedy, rth_td_huber): q rows hold the network's raw heads -- A
+ * advantages then the state value -- and Q = (V + A) - mean(A) is formed in-kernel
+ * (dqn_model.py:185-193); rth_td_huber's dq is then d(loss)/d(heads) [B, A+1].  A <= 32. */
 /* RandomExploration.act (reth/reth/utils/exploration.py:26-31) over N actors:
  * u < eps[i] ? rand_action : argmax_a q[i, a] (first maximum, dqn_solver.py:126-131).
  * u_dev / rand_action_dev nullable -> Philox(seed, counter); counter_dev (nullable) supplies
  * the counter from device memory instead (graph replay). */
-int rth_eps_greedy(const float *q_dev, int64_t N, int64_t A, const double *eps_dev,
+int rth_eps_greedy(const float *q_dev, int64_t N, int64_t A, int32_t dueling, const double *eps_dev,
                    const double *u_dev, const int64_t *rand_action_dev, uint64_t seed,
                    uint64_t counter, const int64_t *counter_dev, int64_t *action_out_dev,
                    void *stream);
@@ -222,7 +225,7 @@ int rth_synth_env_reset(uint8_t *frames_dev, int64_t n_actors, int32_t ring, uin
 int rth_td_huber(const float *q_s0_dev, const float *q_s1_online_dev, const float *q_s1_target_dev,
                  const int64_t *a_dev, const float *r_dev, const float *done_dev,
                  const double *isw_dev, int64_t B, int64_t A, float gamma_n, int32_t double_q,
-                 float *td_out_dev, float *td_abs_out_dev, float *loss_elem_dev,
+                 int32_t dueling, float *td_out_dev, float *td_abs_out_dev, float *loss_elem_dev,
                  float *loss_out_dev, float *dq_out_dev, void *stream);
 
 #ifdef __cplusplus

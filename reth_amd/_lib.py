@@ -76,7 +76,7 @@ SIGNATURES = {
     "rth_replay_column": (c_vp, [c_vp, c_i32]),
     "rth_copy_rows": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i32, c_i32, c_vp]),
     # actors
-    "rth_eps_greedy": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_u64, c_u64, c_vp, c_vp, c_vp]),
+    "rth_eps_greedy": (c_i32, [c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_u64, c_u64, c_vp, c_vp, c_vp]),
     "rth_counter_add": (c_i32, [c_vp, c_i64, c_vp]),
     "rth_nstep_create": (c_i32, [c_i64, c_i32, c_f64, c_i32, c_i32, ctypes.POINTER(c_vp)]),
     "rth_nstep_destroy": (c_i32, [c_vp]),
@@ -86,7 +86,7 @@ SIGNATURES = {
                                    c_vp, c_vp, c_vp, c_vp, c_vp]),
     "rth_synth_env_reset": (c_i32, [c_vp, c_i64, c_i32, c_u64, c_vp, c_vp]),
     # learner
-    "rth_td_huber": (c_i32, [c_vp] * 7 + [c_i64, c_i64, c_f32, c_i32] + [c_vp] * 5 + [c_vp]),
+    "rth_td_huber": (c_i32, [c_vp] * 7 + [c_i64, c_i64, c_f32, c_i32, c_i32] + [c_vp] * 5 + [c_vp]),
 }
 
 _lib = None

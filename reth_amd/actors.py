@@ -110,11 +110,9 @@ class VecActors:
         call("rth_counter_add", ptr(self.t_dev), 1, s)
         # acting batch: current stacks -> f32 (Worker.step -> exploration.act -> solver.act)
         self.gather_f32(self.current_obs_handles(), self.obs)
-        q = q_net(self.obs)
-        if q.dtype != torch.float32 or not q.is_contiguous():
-            q = q.float().contiguous()
-        call("rth_eps_greedy", ptr(q), self.N, self.A, ptr(self.eps), None, None, self.seed, 0, ptr(self.t_dev),
-             ptr(self.action), s)
+        q, dueling = _q_forward(q_net, self.obs)
+        call("rth_eps_greedy", ptr(q), self.N, self.A, dueling, ptr(self.eps), None, None, self.seed, 0,
+             ptr(self.t_dev), ptr(self.action), s)
         call("rth_synth_env_step", ptr(self.frames), self.N, self.ring, 0, ptr(self.t_dev), ptr(self.cur_slot),
              ptr(self.action), self.seed, self.p_reward, self.p_done, ptr(self.reward), ptr(self.done), ptr(self.s0_h),
              ptr(self.s1_h), s)
@@ -129,10 +127,10 @@ class VecActors:
         """calc_loss on the emitted rows with the actor's network (target == online)"""
         torch.cat([self.row_s0, self.row_s1], out=self.row_handles)
         self.gather_f32(self.row_handles, self.rows_f32)
-        q = q_net(self.rows_f32).float().contiguous()
+        q, dueling = _q_forward(q_net, self.rows_f32)
         q0, q1 = q[: self.N], q[self.N:]
         _, td_abs, _ = td_huber_forward(q0, q1, q1, self.row_a, self.row_r, self.row_done, None, self.gamma_n,
-                                        True, want_dq=False)
+                                        True, want_dq=False, dueling=bool(dueling))
         return td_abs
 
     def append(self, replay, td_abs):
@@ -145,6 +143,18 @@ class VecActors:
         """emitted rows as (s0 u8, a, r, s1 u8, done) device tensors (tests / inspection)"""
         return (self.frames[self.row_s0], self.row_a.clone(), self.row_r.clone(), self.frames[self.row_s1],
                 self.row_done.clone())
+
+
+def _q_forward(q_net, x):
+    """(f32 contiguous network output, dueling flag): a dueling conv net returns its raw heads
+    [n, A+1] through the merged-heads path and the HIP consumer forms Q (model.py)"""
+    if getattr(q_net, "dueling", False) and hasattr(q_net, "forward_heads"):
+        q, dueling = q_net.forward_heads(x), 1
+    else:
+        q, dueling = q_net(x), 0
+    if q.dtype != torch.float32 or not q.is_contiguous():
+        q = q.float().contiguous()
+    return q, dueling
 
 
 def apex_columns(channels_last=False):

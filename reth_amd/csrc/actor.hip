@@ -11,7 +11,7 @@ namespace rth {
 // ------------------------------------------------------------------ epsilon-greedy
 // One lane per actor: A <= 18 for Atari, so the row argmax is a short in-register loop and
 // the launch is one wave per 64 actors.
-__global__ void k_eps_greedy(const float *__restrict__ q, int64_t N, int A, const double *__restrict__ eps,
+__global__ void k_eps_greedy(const float *__restrict__ q, int64_t N, int A, int dueling, const double *__restrict__ eps,
                              const double *__restrict__ u_in, const int64_t *__restrict__ ra_in, uint64_t seed,
                              uint64_t counter, const int64_t *__restrict__ counter_dev, int64_t *__restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -29,7 +29,9 @@ __global__ void k_eps_greedy(const float *__restrict__ q, int64_t N, int A, cons
     }
     out[i] = ra;
   } else {
-    out[i] = argmax_first(q + i * A, A);
+    float qr[kMaxActions];
+    q_row(q + i * (A + dueling), A, dueling, qr);
+    out[i] = argmax_first(qr, A);
   }
 }
 
@@ -162,15 +164,15 @@ struct rth_nstep {
 
 extern "C" {
 
-int rth_eps_greedy(const float *q, int64_t N, int64_t A, const double *eps, const double *u,
+int rth_eps_greedy(const float *q, int64_t N, int64_t A, int32_t dueling, const double *eps, const double *u,
                    const int64_t *ra, uint64_t seed, uint64_t counter, const int64_t *counter_dev, int64_t *out,
                    void *stream) {
-  RTH_REQUIRE(N >= 0 && A >= 1 && A < (1 << 20), "rth_eps_greedy: bad shape");
+  RTH_REQUIRE(N >= 0 && A >= 1 && A <= kMaxActions && (dueling == 0 || dueling == 1), "rth_eps_greedy: bad shape");
   if (N == 0) return RTH_OK;
   RTH_REQUIRE(q && eps && out, "rth_eps_greedy: NULL buffer");
   const int bs = 256;
   hipLaunchKernelGGL(k_eps_greedy, dim3((unsigned)((N + bs - 1) / bs)), dim3(bs), 0, as_stream(stream), q, N,
-                     (int)A, eps, u, ra, seed, counter, counter_dev, out);
+                     (int)A, (int)dueling, eps, u, ra, seed, counter, counter_dev, out);
   RTH_LAUNCHED();
   return RTH_OK;
 }

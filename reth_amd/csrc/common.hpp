@@ -109,6 +109,22 @@ __device__ inline int argmax_first(const float *q, int A) {
   return best;
 }
 
+// Q values of one row of network output.  Plain: q_j = row[j].  Dueling heads (row = A
+// advantages then the state value, dqn_model.py:185-193): q_j = (v + a_j) - mean(a), with
+// torch's mean = sum * (1/A).  A <= kMaxActions.
+constexpr int kMaxActions = 32;
+__device__ inline void q_row(const float *row, int A, int dueling, float *q) {
+  if (!dueling) {
+    for (int j = 0; j < A; ++j) q[j] = row[j];
+    return;
+  }
+  float s = 0.0f;
+  for (int j = 0; j < A; ++j) s = radd(s, row[j]);
+  const float mean = rmul(s, 1.0f / (float)A);
+  const float v = row[A];
+  for (int j = 0; j < A; ++j) q[j] = rsub(radd(v, row[j]), mean);
+}
+
 // PERSampler._normalize_weights (per_sampler.py:16-17): (w + 1e-6) ** alpha in float32,
 // correctly rounded; numpy's `** 0.5` is sqrt (fast_scalar_power), also correctly rounded.
 __device__ inline float per_normalize(float w, float alpha) {

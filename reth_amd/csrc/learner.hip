@@ -30,17 +30,22 @@ constexpr int kTdThreads = 512;
 __global__ __launch_bounds__(kTdThreads) void k_td_huber(
     const float *__restrict__ q0, const float *__restrict__ q1o, const float *__restrict__ q1t,
     const int64_t *__restrict__ act, const float *__restrict__ rew, const float *__restrict__ done,
-    const double *__restrict__ isw, int64_t B, int A, float gamma_n, int double_q, float *__restrict__ td_out,
+    const double *__restrict__ isw, int64_t B, int A, float gamma_n, int double_q, int dueling, float *__restrict__ td_out,
     float *__restrict__ td_abs_out, float *__restrict__ loss_elem, float *__restrict__ loss_out,
     float *__restrict__ dq) {
   __shared__ float part[kTdThreads];
   const float invB = 1.0f / (float)B;
   float acc = 0.0f;
+  const int ld = A + dueling;  // row length: A values, or A advantages + 1 state value
   for (int64_t b = threadIdx.x; b < B; b += kTdThreads) {
     const int64_t a = act[b];
-    const float q = q0[b * A + a];  // sum(q * one_hot(a)) (:79-81)
-    const int astar = argmax_first((double_q ? q1o : q1t) + b * A, A);  // (:83-94)
-    const float nqb = q1t[b * A + astar];
+    float qa[kMaxActions], qs[kMaxActions];
+    q_row(q0 + b * ld, A, dueling, qa);
+    const float q = qa[a];  // sum(q * one_hot(a)) (:79-81)
+    q_row((double_q ? q1o : q1t) + b * ld, A, dueling, qs);
+    const int astar = argmax_first(qs, A);  // (:83-94)
+    if (double_q) q_row(q1t + b * ld, A, dueling, qs);
+    const float nqb = qs[astar];
     // expected = r + (gamma**n * next_q_best) * (1 - done)  (:96), f32, no contraction
     float t = rmul(gamma_n, nqb);
     t = rmul(t, rsub(1.0f, done[b]));
@@ -58,7 +63,13 @@ __global__ __launch_bounds__(kTdThreads) void k_td_huber(
     if (dq) {  // autograd: mean -> mul(w) -> smooth_l1' -> one_hot scatter
       const float g = rmul(invB, w);
       const float d = td <= -1.0f ? -g : (td >= 1.0f ? g : rmul(td, g));
-      for (int j = 0; j < A; ++j) dq[b * A + j] = rmul(d, j == a ? 1.0f : 0.0f);
+      if (!dueling) {
+        for (int j = 0; j < A; ++j) dq[b * A + j] = rmul(d, j == a ? 1.0f : 0.0f);
+      } else {  // through q = (v + adv) - mean(adv): d adv_j = g_j + (-sum g) / A, d v = sum g
+        const float dm = (-d) / (float)A;
+        for (int j = 0; j < A; ++j) dq[b * ld + j] = radd(j == a ? d : 0.0f, dm);
+        dq[b * ld + A] = d;
+      }
     }
   }
   part[threadIdx.x] = acc;
@@ -82,12 +93,13 @@ int rth_version(void) { return 100; }  // 0.1.0
 
 int rth_td_huber(const float *q0, const float *q1o, const float *q1t, const int64_t *a, const float *r,
                  const float *done, const double *isw, int64_t B, int64_t A, float gamma_n, int32_t double_q,
-                 float *td_out, float *td_abs_out, float *loss_elem, float *loss_out, float *dq, void *stream) {
-  RTH_REQUIRE(B >= 1 && A >= 1 && A < (1 << 20), "rth_td_huber: bad shape B=%lld A=%lld", (long long)B,
-              (long long)A);
+                 int32_t dueling, float *td_out, float *td_abs_out, float *loss_elem, float *loss_out, float *dq,
+                 void *stream) {
+  RTH_REQUIRE(B >= 1 && A >= 1 && A <= kMaxActions && (dueling == 0 || dueling == 1),
+              "rth_td_huber: bad shape B=%lld A=%lld", (long long)B, (long long)A);
   RTH_REQUIRE(q0 && q1t && a && r && done && (q1o || !double_q), "rth_td_huber: NULL input");
   hipLaunchKernelGGL(k_td_huber, dim3(1), dim3(kTdThreads), 0, as_stream(stream), q0, q1o, q1t, a, r, done, isw, B,
-                     (int)A, gamma_n, double_q, td_out, td_abs_out, loss_elem, loss_out, dq);
+                     (int)A, gamma_n, double_q, dueling, td_out, td_abs_out, loss_elem, loss_out, dq);
   RTH_LAUNCHED();
   return RTH_OK;
 }

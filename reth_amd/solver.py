@@ -45,13 +45,15 @@ def _check_device(device):
     return torch.device("cuda", dev.index if dev.index is not None else torch.cuda.current_device())
 
 
-def td_huber_forward(q_s0, q_s1_online, q_s1_target, a, r, done, isw, gamma_n, double_q, want_dq):
-    """One rth_td_huber launch -> (loss[1], td_abs[B], dq[B,A] or None)."""
-    B, A = q_s0.shape
+def td_huber_forward(q_s0, q_s1_online, q_s1_target, a, r, done, isw, gamma_n, double_q, want_dq, dueling=False):
+    """One rth_td_huber launch -> (loss[1], td_abs[B], dq or None).  dueling: the q inputs are
+    raw heads [B, A+1] (advantages, value) and dq is d(loss)/d(heads)."""
+    B, W = q_s0.shape
+    A = W - int(bool(dueling))
     for t, name in ((q_s0, "q_s0"), (q_s1_target, "q_s1_target")):
-        if t.dtype != torch.float32 or not t.is_cuda or t.shape != (B, A):
-            raise ValueError(f"{name} must be a float32 device tensor of shape {(B, A)}")
-    if double_q and (q_s1_online is None or q_s1_online.shape != (B, A)):
+        if t.dtype != torch.float32 or not t.is_cuda or t.shape != (B, W):
+            raise ValueError(f"{name} must be a float32 device tensor of shape {(B, W)}")
+    if double_q and (q_s1_online is None or q_s1_online.shape != (B, W)):
         raise ValueError("double_q needs q_s1_online of the same shape")
     dev = q_s0.device
     q0 = q_s0.detach().contiguous()
@@ -66,17 +68,18 @@ def td_huber_forward(q_s0, q_s1_online, q_s1_target, a, r, done, isw, gamma_n, d
         raise ValueError("batch columns disagree in length")
     td_abs = torch.empty(B, dtype=torch.float32, device=dev)
     loss = torch.empty(1, dtype=torch.float32, device=dev)
-    dq = torch.empty((B, A), dtype=torch.float32, device=dev) if want_dq else None
+    dq = torch.empty((B, W), dtype=torch.float32, device=dev) if want_dq else None
     call("rth_td_huber", ptr(q0), ptr(q1o), ptr(q1t), ptr(a), ptr(r), ptr(done), ptr(isw), B, A,
-         float(gamma_n), int(bool(double_q)), None, ptr(td_abs), None, ptr(loss), ptr(dq), stream_ptr())
+         float(gamma_n), int(bool(double_q)), int(bool(dueling)), None, ptr(td_abs), None, ptr(loss), ptr(dq),
+         stream_ptr())
     return loss, td_abs, dq
 
 
 class _TDHuber(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, q_s0, q_s1_online, q_s1_target, a, r, done, isw, gamma_n, double_q):
+    def forward(ctx, q_s0, q_s1_online, q_s1_target, a, r, done, isw, gamma_n, double_q, dueling):
         loss, td_abs, dq = td_huber_forward(q_s0, q_s1_online, q_s1_target, a, r, done, isw, gamma_n, double_q,
-                                            want_dq=True)
+                                            want_dq=True, dueling=dueling)
         ctx.save_for_backward(dq)
         ctx.mark_non_differentiable(td_abs)
         return loss.view(()), td_abs
@@ -84,12 +87,12 @@ class _TDHuber(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g_loss, g_td):
         (dq,) = ctx.saved_tensors
-        return dq * g_loss, None, None, None, None, None, None, None, None
+        return dq * g_loss, None, None, None, None, None, None, None, None, None
 
 
-def td_huber_loss(q_s0, q_s1_online, q_s1_target, a, r, done, isw, gamma_n, double_q=True):
+def td_huber_loss(q_s0, q_s1_online, q_s1_target, a, r, done, isw, gamma_n, double_q=True, dueling=False):
     """(mean IS-weighted Huber loss [differentiable w.r.t. q_s0], |td| [B])"""
-    return _TDHuber.apply(q_s0, q_s1_online, q_s1_target, a, r, done, isw, gamma_n, double_q)
+    return _TDHuber.apply(q_s0, q_s1_online, q_s1_target, a, r, done, isw, gamma_n, double_q, dueling)
 
 
 class Algorithm:
@@ -141,6 +144,8 @@ class DQNSolver(Algorithm):
                                               eps=models.get("adam_epsilon", adam_epsilon), **kw)
         self._params = [p for p in self.q_network.parameters()]
         self._tparams = [p for p in self.target_q_network.parameters()]
+        # dueling conv net: merged-heads forward, Q formed inside the TD kernel (model.py)
+        self._heads = bool(getattr(self.q_network, "dueling", False) and hasattr(self.q_network, "forward_heads"))
         self.update_target()
         self.clip_value = clip_value
         self.double_q = double_q
@@ -156,8 +161,10 @@ class DQNSolver(Algorithm):
     # ------------------------------------------------------------------ target / weights
     @torch.no_grad()
     def update_target(self):
-        """target <- online (:65-66), one fused device copy"""
+        """target <- online (:65-66), one fused device copy (+ the target's merged heads)"""
         torch._foreach_copy_(self._tparams, self._params)
+        if self._heads:
+            self.target_q_network.freeze_heads()
 
     def load_weights(self, stream):
         states = torch.load(stream, map_location=self.device, weights_only=True)
@@ -178,19 +185,27 @@ class DQNSolver(Algorithm):
                            else torch.as_tensor(np.asarray(x), dtype=dt).to(dev, non_blocking=True))
         return f(s0, torch.float32), f(a, torch.int64), f(r, torch.float32), f(s1, torch.float32), f(done, torch.float32)
 
-    def _forward_targets(self, s1):
+    def _forward_targets(self, s1, merged=None):
         with torch.no_grad():
-            q1t = self.target_q_network(s1)
-            q1o = self.q_network(s1) if self.double_q else None
+            if self._heads:  # raw dueling heads; the TD kernel forms Q
+                q1t = self.target_q_network.forward_heads(s1)
+                q1o = None
+                if self.double_q:
+                    m = [t.detach() for t in merged] if merged is not None else None
+                    q1o = self.q_network.forward_heads(s1, m)
+            else:
+                q1t = self.target_q_network(s1)
+                q1o = self.q_network(s1) if self.double_q else None
         return q1o, q1t
 
     def calc_loss_device(self, batch):
         """|td| on the device without an update (:100-102)"""
         s0, a, r, s1, done = self._tensors(batch)
         with torch.no_grad():
-            q0 = self.q_network(s0)
+            q0 = self.q_network.forward_heads(s0) if self._heads else self.q_network(s0)
         q1o, q1t = self._forward_targets(s1)
-        _, td_abs, _ = td_huber_forward(q0, q1o, q1t, a, r, done, None, self.gamma_n, self.double_q, want_dq=False)
+        _, td_abs, _ = td_huber_forward(q0, q1o, q1t, a, r, done, None, self.gamma_n, self.double_q, want_dq=False,
+                                        dueling=self._heads)
         return td_abs
 
     def calc_loss(self, batch):
@@ -199,10 +214,15 @@ class DQNSolver(Algorithm):
     def compute_grads(self, batch, weights=None):
         """dqn_solver.py:104-117: forward passes, fused TD/Huber, backward -> |td| (device)"""
         s0, a, r, s1, done = self._tensors(batch)
-        q0 = self.q_network(s0)
-        q1o, q1t = self._forward_targets(s1)
+        merged = None
+        if self._heads:  # merged dueling head weights, built once and shared by both online passes
+            merged = self.q_network._merged_head_weights()
+            q0 = self.q_network.forward_heads(s0, merged)
+        else:
+            q0 = self.q_network(s0)
+        q1o, q1t = self._forward_targets(s1, merged)
         isw = None if weights is None else (weights if torch.is_tensor(weights) else torch.as_tensor(np.asarray(weights)))
-        loss, td_abs = td_huber_loss(q0, q1o, q1t, a, r, done, isw, self.gamma_n, self.double_q)
+        loss, td_abs = td_huber_loss(q0, q1o, q1t, a, r, done, isw, self.gamma_n, self.double_q, self._heads)
         self.optimizer.zero_grad(set_to_none=False)
         loss.backward()
         self.last_loss = loss.detach()

@@ -25,6 +25,8 @@ class WeightsSlot:
     @torch.no_grad()
     def acquire(self, module):
         torch._foreach_copy_([p for p in module.parameters()], self._slot)
+        if getattr(module, "dueling", False) and hasattr(module, "freeze_heads"):
+            module.freeze_heads()  # the actor's cached merged heads follow its parameters
         return self.version
 
 

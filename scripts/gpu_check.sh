@@ -23,6 +23,8 @@ for step in "$@"; do
       run bench_nchw 600 python bench.py --steps 100 --warmup 20 --no-cpu-baseline --nchw
       run bench_cl 600 python bench.py --steps 100 --warmup 20 --no-cpu-baseline
       run bench_cl_find 900 python bench.py --steps 100 --warmup 20 --no-cpu-baseline --conv-benchmark ;;
+    bg) run bench_graph 600 python bench.py --steps 100 --warmup 20 --no-cpu-baseline ;;
+    probe) run probe 300 python scripts/probe_qnet.py ;;
     variants2)
       run bench_eager 600 python bench.py --steps 100 --warmup 20 --no-cpu-baseline --eager
       run bench_graph 600 python bench.py --steps 100 --warmup 20 --no-cpu-baseline

@@ -21,7 +21,7 @@ def test_eps_greedy_explicit_and_philox(dev, orc):
     ra = rng.integers(0, A, N)
     qd, ed, ud, rd = (torch.as_tensor(x, device=dev) for x in (q, eps, u, ra))
     out = torch.empty(N, dtype=torch.int64, device=dev)
-    _lib.call("rth_eps_greedy", qd.data_ptr(), N, A, ed.data_ptr(), ud.data_ptr(), rd.data_ptr(), 0, 0, None,
+    _lib.call("rth_eps_greedy", qd.data_ptr(), N, A, 0, ed.data_ptr(), ud.data_ptr(), rd.data_ptr(), 0, 0, None,
               out.data_ptr(), _lib.stream_ptr())
     assert np.array_equal(out.cpu().numpy(), orc.eps_greedy(q, eps, u, ra))
     greedy = torch.argmax(torch.as_tensor(q), 1).numpy()
@@ -29,7 +29,7 @@ def test_eps_greedy_explicit_and_philox(dev, orc):
     assert np.array_equal(out.cpu().numpy()[sel], greedy[sel])  # torch.argmax first-max semantics
     # device RNG path: Philox(seed, counter, lane)
     seed, counter = 77, 5
-    _lib.call("rth_eps_greedy", qd.data_ptr(), N, A, ed.data_ptr(), None, None, seed, counter, None,
+    _lib.call("rth_eps_greedy", qd.data_ptr(), N, A, 0, ed.data_ptr(), None, None, seed, counter, None,
               out.data_ptr(), _lib.stream_ptr())
     pu = np.array([orc.philox_uniform(seed, counter, i, orc.STREAM_EXPLORE) for i in range(N)])
     pra = np.array([(int(orc.philox4x32([i, counter, 0, orc.STREAM_RANDACT], [seed, 0])[0]) * A) >> 32
@@ -38,9 +38,36 @@ def test_eps_greedy_explicit_and_philox(dev, orc):
     # the counter read from device memory (graph-replay form) gives the same draws
     cdev = torch.tensor([counter], dtype=torch.int64, device=dev)
     out2 = torch.empty_like(out)
-    _lib.call("rth_eps_greedy", qd.data_ptr(), N, A, ed.data_ptr(), None, None, seed, 999, cdev.data_ptr(),
+    _lib.call("rth_eps_greedy", qd.data_ptr(), N, A, 0, ed.data_ptr(), None, None, seed, 999, cdev.data_ptr(),
               out2.data_ptr(), _lib.stream_ptr())
     assert torch.equal(out, out2)
+
+
+def dueling_q(h):
+    """Q = (V + adv) - mean(adv) from raw heads [n, A+1] in float32 (dqn_model.py:185-193);
+    mean = sequential sum * (1/A) as torch's reduction computes it for short rows"""
+    A = h.shape[1] - 1
+    s = np.zeros(h.shape[0], np.float32)
+    for j in range(A):
+        s = (s + h[:, j]).astype(np.float32)
+    mean = s * (np.float32(1.0) / np.float32(A))
+    return (h[:, A:A + 1] + h[:, :A]) - mean[:, None]
+
+
+def test_eps_greedy_dueling_heads(dev, orc):
+    from reth_amd import _lib
+
+    rng = np.random.default_rng(3)
+    N, A = 2000, 6
+    h = (rng.standard_normal((N, A + 1)) * 4).astype(np.float32)
+    h[:100, :A] = np.round(h[:100, :A])  # ties survive the dueling combine
+    eps = rng.random(N) * 0.2
+    u, ra = rng.random(N), rng.integers(0, A, N)
+    hd, ed, ud, rd = (torch.as_tensor(x, device=dev) for x in (h, eps, u, ra))
+    out = torch.empty(N, dtype=torch.int64, device=dev)
+    _lib.call("rth_eps_greedy", hd.data_ptr(), N, A, 1, ed.data_ptr(), ud.data_ptr(), rd.data_ptr(), 0, 0, None,
+              out.data_ptr(), _lib.stream_ptr())
+    assert np.array_equal(out.cpu().numpy(), orc.eps_greedy(dueling_q(h), eps, u, ra))
 
 
 @pytest.mark.parametrize("mode", [0, 1])

@@ -65,6 +65,58 @@ def test_td_huber_autograd_matches_torch_reference(dev):
     torch.testing.assert_close(loss, ref, rtol=1e-6, atol=1e-7)
 
 
+@pytest.mark.parametrize("B,A", [(8, 6), (512, 6), (512, 18)])
+def test_td_huber_dueling_heads(dev, orc, B, A):
+    """dueling mode: the kernel forms Q from raw heads [B, A+1]; td bit-exact against the
+    oracle on the f32 restatement of the combine, d(loss)/d(heads) to 1e-6 against torch
+    autograd through the reference's combine (dqn_model.py:192-193)"""
+    from test_actor_gpu import dueling_q
+
+    from reth_amd.solver import td_huber_forward, td_huber_loss
+
+    rng = np.random.default_rng(100 + B + A)
+    h0, h1o, h1t = ((rng.standard_normal((B, A + 1)) * 3).astype(np.float32) for _ in range(3))
+    a = rng.integers(0, A, B)
+    r = rng.choice(np.array([-1, 0, 1], np.float32), B)
+    done = (rng.random(B) < 0.3).astype(np.float32)
+    isw = rng.random(B) + 0.1
+    T = lambda x: torch.as_tensor(x, device=dev)
+    loss, td_abs, dq = td_huber_forward(T(h0), T(h1o), T(h1t), T(a), T(r), T(done), T(isw), GAMMA_N, True, True,
+                                        dueling=True)
+    q0, q1o, q1t = dueling_q(h0), dueling_q(h1o), dueling_q(h1t)
+    td = orc.td_error(q0, q1o, q1t, a, r, done, GAMMA_N, True)
+    assert np.array_equal(td_abs.cpu().numpy(), np.abs(td))
+    ol, _, odq = orc.td_huber(td, isw.astype(np.float32), a, A)
+    assert abs(loss.item() - float(ol)) <= 1e-6 * max(1.0, abs(float(ol)))
+    # gradient through the combine, torch autograd on the same dq
+    hh = torch.as_tensor(h0, device=dev).requires_grad_(True)
+    adv, val = hh[:, :A], hh[:, A:]
+    (val + adv - adv.mean(dim=1, keepdim=True)).backward(T(odq))
+    # the kernel divides by A as CPU torch does (mean_backward); CUDA torch multiplies by 1/A
+    torch.testing.assert_close(dq, hh.grad, rtol=1e-6, atol=0)
+    # the autograd op routes the heads gradient
+    hh2 = torch.as_tensor(h0, device=dev).requires_grad_(True)
+    l2, _ = td_huber_loss(hh2, T(h1o), T(h1t), T(a), T(r), T(done), T(isw), GAMMA_N, True, True)
+    l2.backward()
+    assert torch.equal(hh2.grad, dq)
+
+
+def test_dueling_heads_forward_matches_module(dev):
+    """merged-heads forward (one FC1 GEMM + block-diagonal FC2) == the module's forward"""
+    from reth_amd.model import DQNNetwork
+
+    torch.manual_seed(5)
+    net = DQNNetwork((4, 84, 84), 6).to(dev)
+    x = torch.rand(64, 4, 84, 84, device=dev) * 255
+    with torch.no_grad():
+        ref = net(x)
+        h = net.forward_heads(x)
+        adv, val = h[:, :6], h[:, 6:]
+        torch.testing.assert_close(val + adv - adv.mean(1, keepdim=True), ref, rtol=1e-5, atol=1e-5)
+        net.freeze_heads()
+        torch.testing.assert_close(net.forward_heads(x), h, rtol=1e-6, atol=1e-6)
+
+
 def _make_solver(dev, seed, **kw):
     from reth_amd.solver import Box, DQNSolver, Discrete
 

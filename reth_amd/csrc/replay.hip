@@ -10,6 +10,7 @@
 // with 16-byte loads and widens to float32 on the way out (uint8 -> f32 is exact, so the
 // learner receives exactly the f32 frames the reference's actors stored, 4x fewer bytes
 // resident and read).
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -37,6 +38,13 @@ struct CopyCol {
   int64_t in_bytes;         // bytes of one input row
   int32_t conv;
   int32_t planes;           // CONV_U8_F32_HWC: channel planes per row (CHW in, HWC out)
+  // grid layout, filled by launch_copy
+  int64_t chunk_in;         // input bytes per chunk
+  int64_t chunks;           // chunks per row (0: small column, one lane per row)
+  int64_t chunk_px;         // CONV_U8_F32_HWC: pixels per chunk
+  int64_t blk0;             // first workgroup of this column
+  int32_t vec;              // every row's src/dst 16-byte aligned: vector path
+  int32_t pad;
 };
 
 struct CopyArgs {
@@ -50,25 +58,76 @@ struct CopyArgs {
 };
 
 constexpr int kCopyThreads = 256;
-constexpr int kStageBytes = 32768;  // one 4x84x84 stack (28,224 B) fits
+constexpr int64_t kSmallRow = 64;  // rows up to this many bytes: one lane per row
 
 __device__ __forceinline__ float4 u8x4_to_f4(uint32_t w) {
   return make_float4((float)(w & 0xffu), (float)((w >> 8) & 0xffu), (float)((w >> 16) & 0xffu), (float)(w >> 24));
 }
 
-// grid: x = row, y = column; one workgroup per (row, column).
-//   COPY        16-byte loads and stores (1 KiB per wave-instruction).
-//   U8_F32      4 pixels per lane-step: a 4-byte load (256 B per wave-instruction) becomes a
-//               16-byte store (1 KiB contiguous per wave-instruction), four steps in flight.
-//   U8_F32_HWC  the row (C planes of H*W bytes) is staged in LDS with 16-byte loads, then
-//               every lane gathers one pixel's C bytes and writes its C floats contiguously:
-//               channels_last f32 for the Q-net, one coalesced 1 KiB store per instruction.
+// byte j of each of four words -> one float4 (one pixel's four channel planes)
+__device__ __forceinline__ float4 plane_px(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, int j) {
+  const int s = 8 * j;
+  return make_float4((float)((w0 >> s) & 0xffu), (float)((w1 >> s) & 0xffu), (float)((w2 >> s) & 0xffu),
+                     (float)((w3 >> s) & 0xffu));
+}
+
+// CHW u8 (4 planes of P pixels, P % 4 == 0) -> HWC f32 for pixels [pc, pc + 1024*M): the
+// chunk's 4 planes are staged in LDS with coalesced 4-byte loads (M per plane per lane in
+// flight), then each lane writes whole pixels, one float4 each: every wave store
+// instruction covers 1 KiB of contiguous output.
+template <int M>
+__device__ __forceinline__ void hwc4_chunk(const uint8_t *__restrict__ src, float *__restrict__ df, int64_t P,
+                                           int64_t pc, int tid) {
+  constexpr int W = M * kCopyThreads;  // words per plane in the chunk
+  extern __shared__ uint32_t stage[];  // 4 * W words, sized at launch
+  const int64_t wlim = (P - pc) / 4;   // words of this chunk inside the row
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t *s32 = reinterpret_cast<const uint32_t *>(src + k * P + pc);
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+      const int w = j * kCopyThreads + tid;
+      if (w < wlim) stage[k * W + w] = s32[w];
+    }
+  }
+  __syncthreads();
+  const uint8_t *sb = reinterpret_cast<const uint8_t *>(stage);
+  float4 *d4 = reinterpret_cast<float4 *>(df) + pc;
+  const int64_t plim = P - pc;
+#pragma unroll
+  for (int j = 0; j < 4 * M; ++j) {
+    const int p = j * kCopyThreads + tid;
+    if (p < plim)
+      d4[p] = make_float4((float)sb[p], (float)sb[4 * W + p], (float)sb[8 * W + p], (float)sb[12 * W + p]);
+  }
+}
+
+// Flat 1-D grid.  Column c owns workgroups [blk0, blk0 + nblk); a large column splits each
+// row into `chunks` independent chunks of `chunk_in` input bytes (one per workgroup: no LDS,
+// no barrier, thousands of workgroups in flight so loads and stores of different chunks
+// overlap), a small column (a, r, done: <= 64 B) gives each lane a whole row.
+//   COPY        16-byte loads and stores; chunk = 4 KiB.
+//   U8_F32      4-byte loads of 4 pixels become 16-byte stores (1 KiB contiguous per wave
+//               instruction), four per lane in flight; chunk = 4 KiB in.
+//   U8_F32_HWC  C planes of P pixels (CHW u8) -> P pixels x C floats (HWC f32, channels_last
+//               for the Q-net).  C == 4: the chunk's 4 planes x 1024 pixels are staged in
+//               4 KiB of LDS, then each lane writes whole pixels (one float4 each, 1 KiB
+//               contiguous per wave instruction); chunk = 1024 pixels.
 __global__ __launch_bounds__(kCopyThreads) void k_copy_rows(CopyArgs a) {
-  __shared__ uint4 stage[kStageBytes / 16];
-  const int c = blockIdx.y;
-  const int64_t i = blockIdx.x;
-  if (c >= a.ncols || i >= a.n) return;
-  const CopyCol col = a.col[c];
+  const int64_t b = blockIdx.x;
+  int c = 0;
+  while (c + 1 < a.ncols && b >= a.col[c + 1].blk0) ++c;
+  const CopyCol &col = a.col[c];
+  const int tid = threadIdx.x;
+  int64_t i, chunk = 0;
+  if (col.chunks == 0) {  // small rows
+    i = (b - col.blk0) * kCopyThreads + tid;
+    if (i >= a.n) return;
+  } else {
+    const int64_t r = b - col.blk0;
+    i = r / col.chunks;
+    chunk = r - i * col.chunks;
+  }
   const int64_t sr = col.src_rows ? col.src_rows[i] : i;
   int64_t dr;
   if (col.dst_rows)
@@ -80,50 +139,58 @@ __global__ __launch_bounds__(kCopyThreads) void k_copy_rows(CopyArgs a) {
   const uint8_t *__restrict__ src = col.src + sr * col.src_stride;
   uint8_t *__restrict__ dst = col.dst + dr * col.dst_stride;
   const int64_t nb = col.in_bytes;
-  const int tid = threadIdx.x;
-  const bool aligned16 = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0;
   float *df = reinterpret_cast<float *>(dst);
+  if (col.chunks == 0) {
+    if (col.conv == CONV_COPY) {
+      for (int64_t k = 0; k < nb; ++k) dst[k] = src[k];
+    } else if (col.conv == CONV_U8_F32) {
+      for (int64_t k = 0; k < nb; ++k) df[k] = (float)src[k];
+    } else {
+      const int C = col.planes;
+      const int64_t P = nb / C;
+      for (int64_t p = 0; p < P; ++p)
+        for (int k = 0; k < C; ++k) df[p * C + k] = (float)src[k * P + p];
+    }
+    return;
+  }
+  const bool vec = col.vec != 0;  // alignment checked on the host for every row
   if (col.conv == CONV_U8_F32_HWC) {
     const int C = col.planes;
     const int64_t P = nb / C;
-    if (aligned16 && nb % 16 == 0 && nb <= kStageBytes) {
-      const uint4 *s4 = reinterpret_cast<const uint4 *>(src);
-      for (int v = tid; v < nb / 16; v += kCopyThreads) stage[v] = s4[v];
-      __syncthreads();
-      const uint8_t *sb = reinterpret_cast<const uint8_t *>(stage);
-      if (C == 4) {
-        float4 *d4 = reinterpret_cast<float4 *>(dst);
-        for (int64_t p = tid; p < P; p += kCopyThreads)
-          d4[p] = make_float4((float)sb[p], (float)sb[P + p], (float)sb[2 * P + p], (float)sb[3 * P + p]);
-      } else {
-        for (int64_t p = tid; p < P; p += kCopyThreads)
-          for (int k = 0; k < C; ++k) df[p * C + k] = (float)sb[k * P + p];
+    const int64_t pc = chunk * col.chunk_px;  // first pixel of this chunk
+    if (vec && C == 4) {
+      switch (col.chunk_px / (4 * kCopyThreads)) {
+        case 1: hwc4_chunk<1>(src, df, P, pc, tid); break;
+        case 2: hwc4_chunk<2>(src, df, P, pc, tid); break;
+        case 4: hwc4_chunk<4>(src, df, P, pc, tid); break;
+        default: hwc4_chunk<8>(src, df, P, pc, tid); break;
       }
     } else {
-      for (int64_t p = tid; p < P; p += kCopyThreads)
+      for (int64_t p = pc + tid; p < pc + col.chunk_px && p < P; p += kCopyThreads)
         for (int k = 0; k < C; ++k) df[p * C + k] = (float)src[k * P + p];
     }
-  } else if (col.conv == CONV_U8_F32) {
-    const int64_t nw = aligned16 ? nb / 4 : 0;
-    const uint32_t *s32 = reinterpret_cast<const uint32_t *>(src);
-    float4 *d4 = reinterpret_cast<float4 *>(dst);
-    int64_t v = tid;
-    for (; v + 3 * kCopyThreads < nw; v += 4 * kCopyThreads) {
-      const uint32_t w0 = s32[v], w1 = s32[v + kCopyThreads], w2 = s32[v + 2 * kCopyThreads],
-                     w3 = s32[v + 3 * kCopyThreads];
-      d4[v] = u8x4_to_f4(w0);
-      d4[v + kCopyThreads] = u8x4_to_f4(w1);
-      d4[v + 2 * kCopyThreads] = u8x4_to_f4(w2);
-      d4[v + 3 * kCopyThreads] = u8x4_to_f4(w3);
+    return;
+  }
+  const int64_t o = chunk * col.chunk_in;  // first input byte of this chunk
+  if (vec && o + col.chunk_in <= nb) {
+    if (col.conv == CONV_COPY) {  // lane-contiguous 16-byte loads and stores
+      *reinterpret_cast<uint4 *>(dst + o + 16 * tid) = *reinterpret_cast<const uint4 *>(src + o + 16 * tid);
+    } else {  // 4-byte loads -> 16-byte stores, 1 KiB contiguous per wave store, 4 in flight
+      const uint32_t *s32 = reinterpret_cast<const uint32_t *>(src + o);
+      float4 *d4 = reinterpret_cast<float4 *>(df + o);
+      uint32_t w[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) w[j] = s32[j * kCopyThreads + tid];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) d4[j * kCopyThreads + tid] = u8x4_to_f4(w[j]);
     }
-    for (; v < nw; v += kCopyThreads) d4[v] = u8x4_to_f4(s32[v]);
-    for (int64_t b = nw * 4 + tid; b < nb; b += kCopyThreads) df[b] = (float)src[b];
   } else {
-    const int64_t nvec = aligned16 ? nb / 16 : 0;
-    const uint4 *s4 = reinterpret_cast<const uint4 *>(src);
-    uint4 *d4 = reinterpret_cast<uint4 *>(dst);
-    for (int64_t v = tid; v < nvec; v += kCopyThreads) d4[v] = s4[v];
-    for (int64_t b = nvec * 16 + tid; b < nb; b += kCopyThreads) dst[b] = src[b];
+    for (int64_t k = o + tid; k < o + col.chunk_in && k < nb; k += kCopyThreads) {
+      if (col.conv == CONV_COPY)
+        dst[k] = src[k];
+      else
+        df[k] = (float)src[k];
+    }
   }
 }
 
@@ -145,10 +212,49 @@ __global__ void k_counter_add(int64_t *c, int64_t d) {
   if (threadIdx.x == 0 && blockIdx.x == 0) *c += d;
 }
 
-int launch_copy(const CopyArgs &a, hipStream_t s) {
+// pixels per HWC chunk = 1024 * M (M in 1, 2, 4, 8); RTH_COPY_HWC_M overrides (tuning aid)
+static int hwc_chunk_m() {
+  static const int m = [] {
+    const char *e = getenv("RTH_COPY_HWC_M");
+    const int v = e ? atoi(e) : 1;
+    return (v == 1 || v == 2 || v == 4 || v == 8) ? v : 1;
+  }();
+  return m;
+}
+
+// lay the columns out on the flat grid (see k_copy_rows)
+int launch_copy(CopyArgs &a, hipStream_t s) {
   if (a.n <= 0 || a.ncols <= 0) return RTH_OK;
-  RTH_REQUIRE(a.n < (int64_t(1) << 31), "copy: too many rows (%lld)", (long long)a.n);
-  hipLaunchKernelGGL(k_copy_rows, dim3((unsigned)a.n, (unsigned)a.ncols), dim3(kCopyThreads), 0, s, a);
+  int64_t blocks = 0;
+  for (int c = 0; c < a.ncols; ++c) {
+    CopyCol &col = a.col[c];
+    col.blk0 = blocks;
+    const int64_t nb = col.in_bytes;
+    const uintptr_t al = reinterpret_cast<uintptr_t>(col.src) | reinterpret_cast<uintptr_t>(col.dst) |
+                         (uintptr_t)col.src_stride | (uintptr_t)col.dst_stride;
+    if (nb <= kSmallRow) {
+      col.chunks = 0;
+      blocks += (a.n + kCopyThreads - 1) / kCopyThreads;
+      continue;
+    }
+    if (col.conv == CONV_U8_F32_HWC) {
+      const int64_t P = nb / col.planes;
+      col.chunk_px = 4 * kCopyThreads * hwc_chunk_m();
+      col.chunk_in = col.chunk_px * col.planes;
+      col.chunks = (P + col.chunk_px - 1) / col.chunk_px;
+      col.vec = (al % 16 == 0) && P % 4 == 0;
+    } else {
+      col.chunk_in = 16 * kCopyThreads;
+      col.chunks = (nb + col.chunk_in - 1) / col.chunk_in;
+      col.vec = al % 16 == 0;
+    }
+    blocks += a.n * col.chunks;
+  }
+  RTH_REQUIRE(blocks < (int64_t(1) << 31), "copy: grid too large (%lld workgroups)", (long long)blocks);
+  size_t lds = 0;
+  for (int c = 0; c < a.ncols; ++c)
+    if (a.col[c].conv == CONV_U8_F32_HWC && a.col[c].chunks) lds = (size_t)4 * a.col[c].chunk_px;  // 4 planes x chunk_px bytes
+  hipLaunchKernelGGL(k_copy_rows, dim3((unsigned)blocks), dim3(kCopyThreads), lds, s, a);
   RTH_LAUNCHED();
   return RTH_OK;
 }

@@ -21,6 +21,7 @@
 //   each distinct ancestor is maintained exactly once per level by the first key of its run.
 //   Chunks run in order, which keeps the sequential semantics for any n.
 #include <cmath>
+#include <cstdlib>
 
 #include "common.hpp"
 
@@ -58,33 +59,95 @@ __device__ __forceinline__ void maintain_node(Node *nd, int64_t cap, int64_t i) 
   nd[i + 1].mn = m;
 }
 
-// _numba_find_index (sumtree.py:34-58)
-__device__ __forceinline__ int64_t tree_find(const Node *__restrict__ nd, int64_t cap, double w) {
+// _numba_find_index (sumtree.py:34-58).
+// The walk is a chain of dependent loads (one per level, ~20 for 1M rows), so it runs
+// K levels per memory round trip: at node c it issues the child pairs of c and of its
+// descendants down to depth K-1 together (2^K - 1 pairs, all independent), then takes up
+// to K steps of the reference's exact comparisons/subtractions on registers.
+struct Pair {
+  double ls, lv, rv;  // left child {sum, val}, right child val
+};
+
+__device__ __forceinline__ Pair load_pair(const Node *__restrict__ nd, int64_t cap, int64_t c) {
+  const int64_t l = 2 * c + 1;
+  Pair p{0.0, 0.0, 0.0};
+  if (l < cap) {
+    const double2 L = *reinterpret_cast<const double2 *>(&nd[l + 1]);
+    p.ls = L.x;
+    p.lv = L.y;
+    p.rv = nd[l + 2].val;  // record cap+1 exists (padding), so no bound check needed
+  }
+  return p;
+}
+
+// one level of the reference loop at `cur`; false: `cur` is the answer
+__device__ __forceinline__ bool find_step(int64_t &cur, double &cval, double &w, const Pair &p, int64_t cap) {
+  const int64_t l = 2 * cur + 1;
+  if (l < cap) {
+    if (w < p.ls) {
+      cur = l;
+      cval = p.lv;
+      return true;
+    }
+    w = rsub(w, p.ls);
+  }
+  if (w < radd(cval, 1e-5)) return false;
+  w = rsub(w, cval);
+  if (l + 1 >= cap) return false;
+  cur = l + 1;  // r < cap implies l < cap: its val came with the pair
+  cval = p.rv;
+  return true;
+}
+
+template <int K>
+__device__ __forceinline__ int64_t tree_find_k(const Node *__restrict__ nd, int64_t cap, double w) {
+  constexpr int NP = (1 << K) - 1;  // pairs per round trip: c's subtree down to depth K-1
   int64_t cur = 0;
   double cval = nd[1].val;
   for (;;) {
-    const int64_t l = 2 * cur + 1;
-    double lsum = 0.0, lval = 0.0, rval = 0.0;
-    if (l < cap) {
-      // issue the left {sum,val} and right val of the 64-byte child pair together
-      const double2 L = *reinterpret_cast<const double2 *>(&nd[l + 1]);
-      rval = nd[l + 2].val;  // record cap+1 exists (padding), so no bound check needed
-      lsum = L.x;
-      lval = L.y;
-      if (w < lsum) {
-        cur = l;
-        cval = lval;
-        continue;
-      }
-      w = rsub(w, lsum);
+    Pair p[NP];
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      // q-th node of the depth-(K-1) heap under cur: depth dq = log2(q+1), offset q+1-2^dq
+      const int dq = 31 - __builtin_clz(q + 1);
+      const int64_t node = (cur + 1) * (int64_t(1) << dq) - 1 + (q + 1 - (1 << dq));
+      p[q] = load_pair(nd, cap, node);
     }
-    if (w < radd(cval, 1e-5)) return cur;
-    w = rsub(w, cval);
-    const int64_t r = l + 1;
-    if (r >= cap) return cur;
-    cur = r;
-    cval = (l < cap) ? rval : nd[r + 1].val;
+    int q = 0;  // position of `cur` inside the prefetched subtree (heap order)
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      Pair pk = p[0];
+#pragma unroll
+      for (int j = 1; j < NP; ++j)
+        if (j == q) pk = p[j];
+      const int64_t before = cur;
+      if (!find_step(cur, cval, w, pk, cap)) return cur;
+      q = 2 * q + 1 + (int)(cur - (2 * before + 1));
+    }
   }
+}
+
+__device__ __forceinline__ int64_t tree_find(const Node *__restrict__ nd, int64_t cap, double w, int kspec = 2) {
+  switch (kspec) {
+    case 1: return tree_find_k<1>(nd, cap, w);
+    case 4: return tree_find_k<4>(nd, cap, w);
+    case 3: return tree_find_k<3>(nd, cap, w);
+    default: return tree_find_k<2>(nd, cap, w);
+  }
+}
+
+// tuning aids: levels per round trip and sample workgroup size (RTH_FIND_K, RTH_SAMPLE_BS)
+static int env_int(const char *name, int dflt) {
+  const char *e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+static int find_k() {
+  static const int k = env_int("RTH_FIND_K", 2);
+  return k;
+}
+static int sample_bs() {
+  static const int b = env_int("RTH_SAMPLE_BS", 64);
+  return b;
 }
 
 __device__ __forceinline__ double tree_min(const Node *nd) {  // NumbaSumTree.min :109-110
@@ -128,6 +191,31 @@ __global__ __launch_bounds__(kUpdThreads) void k_tree_update(UpdArgs a) {
   const double alpha = a.st ? sched_value(a.alpha_s, a.st->sched_step) : a.alpha;
   for (int64_t cs = 0; cs < a.n; cs += kUpdChunk) {
     const int m = (int)min<int64_t>(kUpdChunk, a.n - cs);
+    // Warm every 64-byte line the level loop below will touch (for each node on a key's
+    // path: the line holding its children pair), all loads independent, so the ~20
+    // dependent levels then hit L2 instead of paying an HBM miss (and TLB walk) each.
+    {
+      uint64_t acc = 0;
+      for (int j = tid; j < m; j += kUpdThreads) {
+        int64_t x = a.idx ? a.idx[cs + j] : (fifo_start + cs + j) % a.cap;
+        if (x < 0 || x >= a.cap) continue;
+        while (x >= 0) {
+          double v[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            v[u] = 0.0;
+            if (x >= 0) {
+              const int64_t c = 2 * x + 1;
+              v[u] = a.nd[(c < a.cap ? c : x) + 1].sum;
+              x = x ? (x - 1) / 2 : -1;
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u) acc ^= (uint64_t)__double_as_longlong(v[u]);
+        }
+      }
+      if (acc == 0x9E3779B97F4A7C15ull) a.nd[0].pad = 1.0;  // record 0 is padding; keeps the loads
+    }
     int P = 2;
     while (P < m) P <<= 1;
     for (int j = tid; j < P; j += kUpdThreads) {
@@ -195,10 +283,10 @@ __global__ __launch_bounds__(kUpdThreads) void k_tree_update(UpdArgs a) {
 
 // ------------------------------------------------------------------ find / sample
 __global__ void k_tree_find(const Node *__restrict__ nd, int64_t cap, const double *__restrict__ tg,
-                            int64_t n, int64_t *__restrict__ idx_out, double *__restrict__ val_out) {
+                            int64_t n, int64_t *__restrict__ idx_out, double *__restrict__ val_out, int kspec) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const int64_t k = tree_find(nd, cap, tg[i]);
+  const int64_t k = tree_find(nd, cap, tg[i], kspec);
   if (idx_out) idx_out[i] = k;
   if (val_out) val_out[i] = nd[k + 1].val;
 }
@@ -207,7 +295,7 @@ __global__ void k_tree_find(const Node *__restrict__ nd, int64_t cap, const doub
 __global__ void k_tree_sample(const Node *__restrict__ nd, int64_t cap, int64_t batch,
                               const double *__restrict__ uniforms, uint64_t seed, uint64_t counter,
                               int is_weights, double beta, const ReplayState *st, rth_schedule beta_s,
-                              int64_t *__restrict__ idx_out, double *__restrict__ out) {
+                              int64_t *__restrict__ idx_out, double *__restrict__ out, int kspec) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= batch) return;
   if (st) {  // a replay shard's device state: call counter and beta_s(sched_step)
@@ -218,7 +306,7 @@ __global__ void k_tree_sample(const Node *__restrict__ nd, int64_t cap, int64_t 
   const double seg = total / (double)batch;
   const double u = uniforms ? uniforms[i] : philox_uniform(seed, counter, (uint32_t)i, STREAM_SAMPLE);
   const double t = rmul(radd((double)i, u), seg);
-  const int64_t k = tree_find(nd, cap, t);
+  const int64_t k = tree_find(nd, cap, t, kspec);
   const double p = nd[k + 1].val;
   idx_out[i] = k;
   if (is_weights) {
@@ -282,10 +370,10 @@ int tree_sample_impl(rth_sumtree *t, int64_t batch, const double *uniforms, uint
                      uint64_t counter, int is_weights, double beta, int64_t *idx_out, double *out,
                      hipStream_t s, const ReplayState *st, const rth_schedule *beta_s) {
   if (batch <= 0) return RTH_OK;
-  const int bs = 256;
+  const int bs = sample_bs();
   hipLaunchKernelGGL(k_tree_sample, dim3((unsigned)((batch + bs - 1) / bs)), dim3(bs), 0, s, t->nodes,
                      t->cap, batch, uniforms, seed, counter, is_weights, beta, st,
-                     beta_s ? *beta_s : rth_schedule{}, idx_out, out);
+                     beta_s ? *beta_s : rth_schedule{}, idx_out, out, find_k());
   RTH_LAUNCHED();
   return RTH_OK;
 }
@@ -335,9 +423,9 @@ int rth_sumtree_find(rth_sumtree *t, const double *tg, int64_t n, int64_t *idx_o
                      void *stream) {
   RTH_REQUIRE(t && (n == 0 || tg), "rth_sumtree_find: bad arguments");
   if (n == 0) return RTH_OK;
-  const int bs = 256;
+  const int bs = sample_bs();
   hipLaunchKernelGGL(k_tree_find, dim3((unsigned)((n + bs - 1) / bs)), dim3(bs), 0, as_stream(stream),
-                     t->nodes, t->cap, tg, n, idx_out, val_out);
+                     t->nodes, t->cap, tg, n, idx_out, val_out, find_k());
   RTH_LAUNCHED();
   return RTH_OK;
 }

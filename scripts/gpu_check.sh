@@ -24,6 +24,13 @@ for step in "$@"; do
       run bench_cl 600 python bench.py --steps 100 --warmup 20 --no-cpu-baseline
       run bench_cl_find 900 python bench.py --steps 100 --warmup 20 --no-cpu-baseline --conv-benchmark ;;
     bg) run bench_graph 600 python bench.py --steps 100 --warmup 20 --no-cpu-baseline ;;
+    mtune) for m in 1 2 4 8; do RTH_COPY_HWC_M=$m run bench_m$m 600 python bench.py --steps 100 --warmup 20 --no-cpu-baseline; done ;;
+    probetree) export TMPDIR=/tmp; run probe_tree 600 rocprofv3 --kernel-trace --stats --output-format csv \
+            -d "$PWD/gpurun_out/ptree" -o run -- python scripts/probe_tree.py ;;
+    ktune) export TMPDIR=/tmp; for k in 1 2 3 4; do for b in 64 256; do RTH_FIND_K=$k RTH_SAMPLE_BS=$b run probe_tree_k${k}_b$b 300 \
+            rocprofv3 --kernel-trace --output-format csv -d "$PWD/gpurun_out/ktune_k${k}_b$b" -o run -- python scripts/probe_tree.py; done; done ;;
+    kbench) export TMPDIR=/tmp; for kb in ${KB:-2_64}; do k=${kb%_*}; b=${kb#*_}; RTH_FIND_K=$k RTH_SAMPLE_BS=$b run kbench_k${k}_b$b 600 \
+            rocprofv3 --kernel-trace --output-format csv -d "$PWD/gpurun_out/kbench_k${k}_b$b" -o run -- python bench.py --steps 60 --warmup 10 --no-cpu-baseline; done ;;
     probe) run probe 300 python scripts/probe_qnet.py ;;
     variants2)
       run bench_eager 600 python bench.py --steps 100 --warmup 20 --no-cpu-baseline --eager

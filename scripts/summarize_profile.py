@@ -24,7 +24,9 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "gpurun_out")
 PROF = os.path.join(ROOT, "profiles")
-LEARNER_GATHER_GRID = 512 * 5 * 256  # B rows x 5 apex columns x 256 threads
+# learner gather launch (k_copy_rows flat grid): B rows x 2 frame columns x 7 chunks of 1024
+# pixels + 3 small columns x ceil(B/256) workgroups, 256 threads each
+LEARNER_GATHER_GRID = (512 * 2 * 7 + 3 * 2) * 256
 
 
 def main():

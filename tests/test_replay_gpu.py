@@ -95,10 +95,12 @@ def test_fifo_wraparound_and_u8_widening(dev, orc):
         assert torch.equal(out[0][k].cpu(), torch.as_tensor(f).float())
 
 
-@pytest.mark.parametrize("planes,shape", [(4, (4, 84, 84)), (3, (3, 5, 7)), (4, (4, 100, 100))])
+@pytest.mark.parametrize("planes,shape", [(4, (4, 84, 84)), (3, (3, 5, 7)), (4, (4, 100, 100)), (4, (4, 9, 9)),
+                                          (4, (4, 3, 5)), (2, (2, 30, 30))])
 def test_channels_last_gather(dev, planes, shape):
-    """uint8 (C,H,W) rows sampled as channels-last float32 (the NHWC conv input), exact;
-    the 4x100x100 row exceeds the LDS stage and takes the direct path"""
+    """uint8 (C,H,W) rows sampled as channels-last float32 (the NHWC conv input), exact:
+    multi-chunk rows with a partial last chunk (4x84x84: 7 chunks of 1024 pixels), pixel
+    counts not divisible by 4 (scalar lanes), rows small enough for one lane per row"""
     from reth_amd import _lib
     from reth_amd.replay import Column, HbmReplay
 
@@ -121,6 +123,30 @@ def test_channels_last_gather(dev, planes, shape):
     _lib.call("rth_copy_rows", dst2.data_ptr(), 0, None, rows.data_ptr(), 0, idx.data_ptr(), 33, int(np.prod(shape)),
               _lib.RTH_U8, _lib.RTH_F32, 0, _lib.stream_ptr())
     assert torch.equal(dst2, rows[idx].float())
+
+
+@pytest.mark.parametrize("nbytes,stride", [(28224, 28224), (1000, 1003), (4096, 4096), (17, 17), (64, 80), (65, 65)])
+def test_copy_rows_chunked_bytes(dev, nbytes, stride):
+    """raw row copy and u8->f32 widening over the chunked grid: unaligned strides fall back
+    to byte lanes, rows <= 64 B take one lane per row, destination rows scattered"""
+    from reth_amd import _lib
+
+    rng = np.random.default_rng(nbytes + stride)
+    n = 37
+    src = torch.as_tensor(rng.integers(0, 256, n * stride, dtype=np.uint8), device=dev)
+    view = src.as_strided((n, nbytes), (stride, 1))
+    idx = torch.as_tensor(rng.permutation(n), device=dev)
+    drow = torch.as_tensor(rng.permutation(n), device=dev)
+    dst = torch.zeros((n, nbytes), dtype=torch.uint8, device=dev)
+    _lib.call("rth_copy_rows", dst.data_ptr(), 0, drow.data_ptr(), src.data_ptr(), stride, idx.data_ptr(), n, nbytes,
+              _lib.RTH_U8, _lib.RTH_U8, 0, _lib.stream_ptr())
+    ref = torch.zeros_like(dst)
+    ref[drow] = view[idx]
+    assert torch.equal(dst, ref)
+    dstf = torch.zeros((n, nbytes), dtype=torch.float32, device=dev)
+    _lib.call("rth_copy_rows", dstf.data_ptr(), 0, None, src.data_ptr(), stride, idx.data_ptr(), n, nbytes,
+              _lib.RTH_U8, _lib.RTH_F32, 0, _lib.stream_ptr())
+    assert torch.equal(dstf, view[idx].float())
 
 
 def test_append_exact_capacity_and_errors(dev):

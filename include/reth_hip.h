@@ -228,6 +228,19 @@ int rth_td_huber(const float *q_s0_dev, const float *q_s1_online_dev, const floa
                  int32_t dueling, float *td_out_dev, float *td_abs_out_dev, float *loss_elem_dev,
                  float *loss_out_dev, float *dq_out_dev, void *stream);
 
+/* ------------------------------------------------------------------------------------
+ * Q-network conv epilogue (reth/reth/algorithm/dqn/dqn_model.py:14-20: Conv2d -> ReLU),
+ * on channels-last (NHWC) contiguous fp32 activations of `rows` = N*H*W rows x C channels.
+ * rth_bias_relu: y = relu(y + bias[c]) in place (the convolution runs without bias).
+ * rth_relu_bias_grad: gy = (y > 0) ? g : 0 (threshold_backward) and db[c] = sum of gy over
+ * the rows, deterministic; `workspace` holds rth_relu_bias_grad_workspace(C) bytes of
+ * per-block partial sums (scratch, no initialisation).  C a power of 2 in [4, 256].
+ * ---------------------------------------------------------------------------------- */
+int rth_bias_relu(float *y_dev, const float *bias_dev, int64_t rows, int32_t C, void *stream);
+int64_t rth_relu_bias_grad_workspace(int32_t C);
+int rth_relu_bias_grad(const float *g_dev, const float *y_dev, float *gy_dev, float *db_dev, void *workspace_dev,
+                       int64_t rows, int32_t C, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -87,6 +87,9 @@ SIGNATURES = {
     "rth_synth_env_reset": (c_i32, [c_vp, c_i64, c_i32, c_u64, c_vp, c_vp]),
     # learner
     "rth_td_huber": (c_i32, [c_vp] * 7 + [c_i64, c_i64, c_f32, c_i32, c_i32] + [c_vp] * 5 + [c_vp]),
+    "rth_bias_relu": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_vp]),
+    "rth_relu_bias_grad_workspace": (c_i64, [c_i32]),
+    "rth_relu_bias_grad": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_vp]),
 }
 
 _lib = None

@@ -90,6 +90,7 @@ class ApexDQN:
         self.trainer = Trainer(self.solver, logger=logger or _Quiet(), print_interval=1000)
         self.actor_net = DQNNetwork(OBS_SHAPE, cfg.num_actions).to(self.device, memory_format=fmt)
         self.actor_net.requires_grad_(False)
+        self.actor_net.hwc_features = bool(cfg.channels_last)
         self.slot = WeightsSlot(self.solver.q_network)
         self.slot.acquire(self.actor_net)
         self.subscriber = WeightsSubscriber(self.slot, cfg.recv_weights_interval)

@@ -1,0 +1,162 @@
+// Q-network glue on gfx950: the conv epilogue and its backward as single HBM passes.
+//
+// Reference: reth/reth/algorithm/dqn/dqn_model.py:14-20 -- every Conv2d is followed by a
+// ReLU.  PyTorch-ROCm runs MIOpen's convolution without bias, then a broadcast bias add and
+// a separate ReLU (two read+write passes over each activation), and in the backward a
+// threshold pass plus a per-channel reduction for the bias gradient.  Here:
+//   rth_bias_relu      y = relu(y + b[c]) in place, one pass (same fp32 add as torch's, so
+//                      the activations are bit-identical to conv(+bias) -> relu);
+//   rth_relu_bias_grad gy = (y > 0) ? g : 0 and db[c] = sum of gy over N*H*W in one pass;
+//                      the channel sums are deterministic (fixed per-lane order, fixed LDS
+//                      tree, per-block partials combined in block order by a second launch).
+// Activations are channels-last (NHWC) contiguous: element e has channel e % C.
+#include <cstdint>
+
+#include "common.hpp"
+
+namespace rth {
+
+constexpr int kEpiThreads = 256;
+constexpr int kGradBlocks = 2048;  // max partial-sum slabs for the bias gradient
+
+__device__ __forceinline__ float relu_f(float v) { return v < 0.0f ? 0.0f : v; }  // NaN passes, like torch
+
+__global__ __launch_bounds__(kEpiThreads) void k_bias_relu(float4 *__restrict__ y, const float *__restrict__ b,
+                                                            int64_t n4, int C) {
+  const int64_t stride = (int64_t)gridDim.x * kEpiThreads;
+  for (int64_t i = (int64_t)blockIdx.x * kEpiThreads + threadIdx.x; i < n4; i += stride) {
+    const int c = (int)((4 * i) % C);
+    float4 v = y[i];
+    v.x = relu_f(radd(v.x, b[c]));
+    v.y = relu_f(radd(v.y, b[c + 1]));
+    v.z = relu_f(radd(v.z, b[c + 2]));
+    v.w = relu_f(radd(v.w, b[c + 3]));
+    y[i] = v;
+  }
+}
+
+// One lane owns channel quad q = tid % (C/4) and walks rows tid / (C/4), + R, + 2R, ... of
+// its block's row slab (R = 256 / (C/4) rows per sweep), so each lane's partial sums have a
+// fixed order; lanes with the same quad are then summed by a fixed LDS tree.
+__global__ __launch_bounds__(kEpiThreads) void k_relu_bias_grad(const float4 *__restrict__ g,
+                                                                 const float4 *__restrict__ y,
+                                                                 float4 *__restrict__ gy, float *__restrict__ part,
+                                                                 int64_t rows, int C) {
+  __shared__ float4 red[kEpiThreads];
+  const int tid = threadIdx.x;
+  const int Q = C / 4;            // quads per row
+  const int R = kEpiThreads / Q;  // rows per sweep
+  const int q = tid % Q;
+  const int64_t per = (rows + gridDim.x - 1) / gridDim.x;
+  const int64_t r0 = (int64_t)blockIdx.x * per;
+  const int64_t r1 = min<int64_t>(rows, r0 + per);
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int64_t r = r0 + tid / Q; r < r1; r += R) {
+    const int64_t i = r * Q + q;
+    const float4 gv = g[i], yv = y[i];
+    float4 o;
+    o.x = yv.x > 0.0f ? gv.x : 0.0f;  // threshold_backward(g, y, 0): y <= 0 -> 0
+    o.y = yv.y > 0.0f ? gv.y : 0.0f;
+    o.z = yv.z > 0.0f ? gv.z : 0.0f;
+    o.w = yv.w > 0.0f ? gv.w : 0.0f;
+    gy[i] = o;
+    acc.x = radd(acc.x, o.x);
+    acc.y = radd(acc.y, o.y);
+    acc.z = radd(acc.z, o.z);
+    acc.w = radd(acc.w, o.w);
+  }
+  red[tid] = acc;
+  __syncthreads();
+  for (int s = kEpiThreads / 2; s >= Q; s >>= 1) {  // lanes tid and tid+s share a quad
+    if (tid < s) {
+      float4 a = red[tid];
+      const float4 o = red[tid + s];
+      a.x = radd(a.x, o.x);
+      a.y = radd(a.y, o.y);
+      a.z = radd(a.z, o.z);
+      a.w = radd(a.w, o.w);
+      red[tid] = a;
+    }
+    __syncthreads();
+  }
+  if (tid < Q) reinterpret_cast<float4 *>(part)[(int64_t)blockIdx.x * Q + tid] = red[tid];
+}
+
+// db[c] = sum of the slabs' partials in slab order: lane t sums slabs t / C, t / C + G, ...
+// of channel t % C (G = 1024 / C lanes per channel, 8 loads in flight), then the G lane sums
+// of a channel by a fixed LDS tree.  A separate launch: the kernel boundary publishes the
+// partials (a per-block agent-scope fence would write back the XCD's whole L2 each time).
+constexpr int kCombThreads = 1024;
+__global__ __launch_bounds__(kCombThreads) void k_bias_grad_combine(const float *__restrict__ part, int nslabs, int C,
+                                                                     float *__restrict__ db) {
+  __shared__ float red[kCombThreads];
+  const int tid = threadIdx.x;
+  const int G = kCombThreads / C;
+  const int c = tid % C;
+  float s = 0.0f;
+  for (int k = tid / C; k < nslabs; k += 8 * G) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int kk = k + u * G;
+      v[u] = kk < nslabs ? part[(int64_t)kk * C + c] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s = radd(s, v[u]);
+  }
+  red[tid] = s;
+  __syncthreads();
+  for (int st = kCombThreads / 2; st >= C; st >>= 1) {
+    if (tid < st) red[tid] = radd(red[tid], red[tid + st]);
+    __syncthreads();
+  }
+  if (tid < C) db[tid] = red[tid];
+}
+
+}  // namespace rth
+
+using namespace rth;
+
+extern "C" {
+
+int rth_bias_relu(float *y, const float *bias, int64_t rows, int32_t C, void *stream) {
+  RTH_REQUIRE(y && bias, "rth_bias_relu: NULL argument");
+  RTH_REQUIRE(C >= 4 && C % 4 == 0 && C <= 4096, "rth_bias_relu: channels %d must be a multiple of 4", C);
+  RTH_REQUIRE((reinterpret_cast<uintptr_t>(y) & 15) == 0, "rth_bias_relu: activations not 16-byte aligned");
+  if (rows <= 0) return RTH_OK;
+  const int64_t n4 = rows * C / 4;
+  const int64_t want = (n4 + kEpiThreads - 1) / kEpiThreads;
+  const int64_t blocks = want < 8192 ? want : 8192;
+  hipLaunchKernelGGL(k_bias_relu, dim3((unsigned)blocks), dim3(kEpiThreads), 0, as_stream(stream),
+                     reinterpret_cast<float4 *>(y), bias, n4, (int)C);
+  RTH_LAUNCHED();
+  return RTH_OK;
+}
+
+int64_t rth_relu_bias_grad_workspace(int32_t C) { return (int64_t)kGradBlocks * C * 4; }
+
+int rth_relu_bias_grad(const float *g, const float *y, float *gy, float *db, void *workspace, int64_t rows,
+                       int32_t C, void *stream) {
+  RTH_REQUIRE(g && y && gy && db && workspace, "rth_relu_bias_grad: NULL argument");
+  RTH_REQUIRE(C >= 4 && C % 4 == 0 && C <= kEpiThreads * 4 && kEpiThreads % (C / 4) == 0,
+              "rth_relu_bias_grad: channels %d unsupported (multiple of 4 dividing 1024)", C);
+  RTH_REQUIRE((C & (C - 1)) == 0 && C <= kEpiThreads, "rth_relu_bias_grad: channels %d must be a power of 2 <= 256", C);
+  RTH_REQUIRE(((reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(y) | reinterpret_cast<uintptr_t>(gy) |
+                reinterpret_cast<uintptr_t>(workspace)) & 15) == 0,
+              "rth_relu_bias_grad: buffers not 16-byte aligned");
+  if (rows <= 0) return RTH_OK;
+  float *part = static_cast<float *>(workspace);
+  const int64_t R = kEpiThreads / (C / 4);       // rows per block sweep
+  const int64_t want = (rows + 8 * R - 1) / (8 * R);  // ~8 sweeps per block
+  const int64_t blocks = want < kGradBlocks ? want : kGradBlocks;
+  hipLaunchKernelGGL(k_relu_bias_grad, dim3((unsigned)blocks), dim3(kEpiThreads), 0, as_stream(stream),
+                     reinterpret_cast<const float4 *>(g), reinterpret_cast<const float4 *>(y),
+                     reinterpret_cast<float4 *>(gy), part, rows, (int)C);
+  RTH_LAUNCHED();
+  hipLaunchKernelGGL(k_bias_grad_combine, dim3(1), dim3(kCombThreads), 0, as_stream(stream), part, (int)blocks, (int)C,
+                     db);
+  RTH_LAUNCHED();
+  return RTH_OK;
+}
+
+}  // extern "C"

@@ -28,6 +28,9 @@ class DQNNetwork(nn.Module):
         fh = conv_out(conv_out(conv_out(h, 8, 4), 4, 2), 3, 1)
         fw = conv_out(conv_out(conv_out(w, 8, 4), 4, 2), 3, 1)
         nfeat = 64 * fh * fw
+        self._feat_chw = (64, fh, fw)
+        # forward_heads on channels-last input: HIP conv epilogues and NHWC feature order
+        self.hwc_features = False
         if dueling:
             self.fc_adv = nn.Sequential(nn.Linear(nfeat, hidden_unit), nn.ReLU(), nn.Linear(hidden_unit, num_actions))
             self.fc_value = nn.Sequential(nn.Linear(nfeat, hidden_unit), nn.ReLU(), nn.Linear(hidden_unit, 1))
@@ -53,7 +56,12 @@ class DQNNetwork(nn.Module):
     # weights change only at refresh points: target sync, actor weight reload).
     def _merged_head_weights(self):
         a0, v0, a2, v2 = self.fc_adv[0], self.fc_value[0], self.fc_adv[2], self.fc_value[2]
-        w1 = torch.cat([a0.weight, v0.weight])
+        if self.hwc_features:  # FC1 columns permuted (C,H,W) -> (H,W,C): the NHWC flatten is a view
+            c, fh, fw = self._feat_chw
+            hwc = lambda wt: wt.view(wt.shape[0], c, fh, fw).permute(0, 2, 3, 1)
+            w1 = torch.cat([hwc(a0.weight), hwc(v0.weight)]).reshape(2 * a0.weight.shape[0], -1)
+        else:
+            w1 = torch.cat([a0.weight, v0.weight])
         b1 = torch.cat([a0.bias, v0.bias])
         A, H = a2.weight.shape
         w2 = torch.cat([torch.cat([a2.weight, a2.weight.new_zeros(A, H)], 1),
@@ -65,7 +73,7 @@ class DQNNetwork(nn.Module):
     def freeze_heads(self):
         """(re)build the cached merged weights in place (stable storage for graph replay)"""
         merged = self._merged_head_weights()
-        if getattr(self, "_frozen", None) is None:
+        if getattr(self, "_frozen", None) is None or self._frozen[0].shape != merged[0].shape:
             self._frozen = [t.clone() for t in merged]
         else:
             for dst, src in zip(self._frozen, merged):
@@ -77,9 +85,26 @@ class DQNNetwork(nn.Module):
         if merged is None:
             merged = self._frozen if getattr(self, "_frozen", None) is not None else self._merged_head_weights()
         w1, b1, w2, b2 = merged
-        h = self.features(x).flatten(1)
+        if self.hwc_features:
+            h = self._features_nhwc(x)
+            h = h.permute(0, 2, 3, 1).reshape(h.shape[0], -1)  # a view of the NHWC activations
+        else:
+            h = self.features(x).flatten(1)
         h = _LinearReLU.apply(h, w1, b1)
         return torch.addmm(b2, h, w2.t())
+
+    def _features_nhwc(self, x):
+        """the conv torso with each bias+ReLU (and its backward) as one HIP pass"""
+        if not x.is_contiguous(memory_format=torch.channels_last):
+            x = x.contiguous(memory_format=torch.channels_last)
+        if getattr(self, "_ws", None) is None or self._ws[0].device != x.device:
+            from . import _lib
+            self._ws = [torch.zeros(_lib.lib().rth_relu_bias_grad_workspace(m.out_channels), dtype=torch.uint8,
+                                    device=x.device) for m in self.features if isinstance(m, nn.Conv2d)]
+        convs = [m for m in self.features if isinstance(m, nn.Conv2d)]
+        for conv, ws in zip(convs, self._ws):
+            x = _ConvBiasReLU.apply(x, conv.weight, conv.bias, conv.stride, ws)
+        return x
 
 
 class _LinearReLU(torch.autograd.Function):
@@ -101,6 +126,40 @@ class _LinearReLU(torch.autograd.Function):
         gw = g.t().mm(x) if ctx.needs_input_grad[1] else None
         gb = g.sum(0) if ctx.needs_input_grad[2] else None
         return gx, gw, gb
+
+
+class _ConvBiasReLU(torch.autograd.Function):
+    """relu(conv2d(x, w) + b) on channels-last fp32: MIOpen convolution without bias, then
+    rth_bias_relu in place; backward: rth_relu_bias_grad (mask + bias gradient in one pass)
+    and MIOpen's data/weight gradients (dqn_model.py:14-20)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, stride, ws):
+        from ._lib import call, ptr, stream_ptr
+
+        y = torch.ops.aten.convolution(x, w, None, list(stride), [0, 0], [1, 1], False, [0, 0], 1)
+        if not y.is_contiguous(memory_format=torch.channels_last):
+            y = y.contiguous(memory_format=torch.channels_last)
+        n, c, h, wd = y.shape
+        call("rth_bias_relu", ptr(y), ptr(b), n * h * wd, c, stream_ptr())
+        ctx.save_for_backward(x, w, y)
+        ctx.stride, ctx.ws = list(stride), ws
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        from ._lib import call, ptr, stream_ptr
+
+        x, w, y = ctx.saved_tensors
+        if not g.is_contiguous(memory_format=torch.channels_last):
+            g = g.contiguous(memory_format=torch.channels_last)
+        gy = torch.empty_like(y)
+        n, c, h, wd = y.shape
+        db = torch.empty(c, dtype=y.dtype, device=y.device)
+        call("rth_relu_bias_grad", ptr(g), ptr(y), ptr(gy), ptr(db), ptr(ctx.ws), n * h * wd, c, stream_ptr())
+        gx, gw, _ = torch.ops.aten.convolution_backward(gy, x, w, None, ctx.stride, [0, 0], [1, 1], False, [0, 0], 1,
+                                                        [ctx.needs_input_grad[0], ctx.needs_input_grad[1], False])
+        return gx, gw, db, None, None
 
 
 class MLP_DQNNetwork(nn.Module):

@@ -134,6 +134,10 @@ class DQNSolver(Algorithm):
         self.q_network = models["q_network"].to(self.device, memory_format=fmt)
         self.target_q_network = models["target_q_network"].to(self.device, memory_format=fmt)
         self.target_q_network.requires_grad_(False)
+        if channels_last and len(obs_shape) == 3:
+            for net in (self.q_network, self.target_q_network):
+                if hasattr(net, "hwc_features"):
+                    net.hwc_features = True  # HIP conv epilogues, NHWC feature order (model.py)
         if models.get("optimizer") is not None:
             self.optimizer = models["optimizer"]
         else:

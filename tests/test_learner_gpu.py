@@ -117,6 +117,57 @@ def test_dueling_heads_forward_matches_module(dev):
         torch.testing.assert_close(net.forward_heads(x), h, rtol=1e-6, atol=1e-6)
 
 
+@pytest.mark.parametrize("C,hw", [(32, 20), (64, 9), (64, 7), (4, 3)])
+def test_conv_epilogue_kernels(dev, C, hw):
+    """rth_bias_relu == relu(conv + b) bit for bit; rth_relu_bias_grad: the mask bit for bit,
+    the channel sums deterministic and within fp32 summation error of torch's"""
+    from reth_amd import _lib
+
+    g0 = torch.Generator(device=dev).manual_seed(C + hw)
+    n = 37
+    y = torch.randn(n, C, hw, hw, device=dev, generator=g0).contiguous(memory_format=torch.channels_last)
+    b = torch.randn(C, device=dev, generator=g0)
+    ref = torch.relu(y + b.view(1, C, 1, 1))
+    out = y.clone()
+    _lib.call("rth_bias_relu", out.data_ptr(), b.data_ptr(), n * hw * hw, C, _lib.stream_ptr())
+    assert torch.equal(out, ref)
+    g = torch.randn(n, C, hw, hw, device=dev, generator=g0).contiguous(memory_format=torch.channels_last)
+    ws = torch.zeros(_lib.lib().rth_relu_bias_grad_workspace(C), dtype=torch.uint8, device=dev)
+    dbs = []
+    for _ in range(3):  # the workspace re-arms itself
+        gy = torch.empty_like(out)
+        db = torch.empty(C, device=dev)
+        _lib.call("rth_relu_bias_grad", g.data_ptr(), out.data_ptr(), gy.data_ptr(), db.data_ptr(), ws.data_ptr(),
+                  n * hw * hw, C, _lib.stream_ptr())
+        dbs.append(db)
+    assert torch.equal(gy, torch.ops.aten.threshold_backward(g, out, 0))
+    assert torch.equal(dbs[0], dbs[1]) and torch.equal(dbs[0], dbs[2])
+    torch.testing.assert_close(dbs[0], gy.sum((0, 2, 3)), rtol=1e-5, atol=1e-4)  # ~2k-term fp32 sums
+
+
+def test_nhwc_features_forward_backward_match_module(dev):
+    """the HIP-epilogue NHWC torso + permuted FC1 columns == the reference module (values
+    and every parameter gradient, fp32 tolerance)"""
+    from reth_amd.model import DQNNetwork
+
+    torch.manual_seed(11)
+    net = DQNNetwork((4, 84, 84), 6).to(dev, memory_format=torch.channels_last)
+    x = (torch.rand(48, 4, 84, 84, device=dev) * 255).floor().contiguous(memory_format=torch.channels_last)
+    ref = net(x)
+    ref.square().sum().backward()
+    gref = [p.grad.clone() for p in net.parameters()]
+    net.zero_grad()
+    net.hwc_features = True
+    h = net.forward_heads(x)
+    adv, val = h[:, :6], h[:, 6:]
+    q = val + adv - adv.mean(1, keepdim=True)
+    torch.testing.assert_close(q, ref, rtol=1e-5, atol=1e-5)
+    q.square().sum().backward()
+    for (name, p), gr in zip(net.named_parameters(), gref):
+        err = ((p.grad - gr).abs().max() / gr.abs().max()).item()  # relative to the tensor's scale
+        assert err < 1e-5, (name, err)
+
+
 def _make_solver(dev, seed, **kw):
     from reth_amd.solver import Box, DQNSolver, Discrete
 
@@ -128,10 +179,10 @@ def _make_solver(dev, seed, **kw):
 
 
 @pytest.mark.parametrize("name", ["dqn_pong_b8.npz", "dqn_pong_b32.npz"])
-@pytest.mark.parametrize("fused", [True, False])
-def test_dqn_update_vs_reference(golden, dev, name, fused):
+@pytest.mark.parametrize("fused,channels_last", [(True, False), (False, False), (True, True)])
+def test_dqn_update_vs_reference(golden, dev, name, fused, channels_last):
     g = golden(name)
-    solver = _make_solver(dev, int(g["seed"]), fused_adam=fused)
+    solver = _make_solver(dev, int(g["seed"]), fused_adam=fused, channels_last=channels_last)
     batch = [g["s0"].astype(np.float32), g["a"], g["r"], g["s1"].astype(np.float32), g["done"]]
     with torch.no_grad():
         q0 = solver.q_network(torch.as_tensor(batch[0], device=dev)).cpu().numpy()

@@ -227,7 +227,10 @@ class DQNSolver(Algorithm):
         q1o, q1t = self._forward_targets(s1, merged)
         isw = None if weights is None else (weights if torch.is_tensor(weights) else torch.as_tensor(np.asarray(weights)))
         loss, td_abs = td_huber_loss(q0, q1o, q1t, a, r, done, isw, self.gamma_n, self.double_q, self._heads)
-        self.optimizer.zero_grad(set_to_none=False)
+        # grads set to None: backward hands each parameter its gradient buffer directly
+        # (no accumulate-add into a zeroed .grad, no zero fill); inside a captured HIP graph
+        # the buffers come from the graph's pool at fixed addresses
+        self.optimizer.zero_grad(set_to_none=True)
         loss.backward()
         self.last_loss = loss.detach()
         return td_abs

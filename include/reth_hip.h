@@ -241,6 +241,27 @@ int64_t rth_relu_bias_grad_workspace(int32_t C);
 int rth_relu_bias_grad(const float *g_dev, const float *y_dev, float *gy_dev, float *db_dev, void *workspace_dev,
                        int64_t rows, int32_t C, void *stream);
 
+/* ------------------------------------------------------------------------------------
+ * Learner optimizer step (reth/reth/algorithm/dqn/dqn_solver.py:118-121):
+ * torch.nn.utils.clip_grad_norm_(params, max_norm) then torch.optim.Adam.step() over up to
+ * RTH_MAX_PARAM_TENSORS fp32 tensors in three launches (norm partials, scalars, update).
+ * max_norm < 0 skips clipping.  step_dev (int64, device) is Adam's step count, incremented
+ * on the device; workspace_dev holds rth_clip_adam_workspace() bytes of scratch;
+ * total_norm_out_dev (nullable) receives the pre-clip 2-norm (clip_grad_norm_'s return).
+ * ---------------------------------------------------------------------------------- */
+#define RTH_MAX_PARAM_TENSORS 32
+typedef struct rth_param_tensor {
+  float *param;
+  const float *grad;
+  float *exp_avg;    /* Adam state["exp_avg"] */
+  float *exp_avg_sq; /* Adam state["exp_avg_sq"] */
+  int64_t n;
+} rth_param_tensor;
+int64_t rth_clip_adam_workspace(void);
+int rth_clip_adam(const rth_param_tensor *tensors, int32_t n_tensors, double lr, double beta1, double beta2,
+                  double eps, double max_norm, int64_t *step_dev, void *workspace_dev, float *total_norm_out_dev,
+                  void *stream);
+
 #ifdef __cplusplus
 }
 #endif

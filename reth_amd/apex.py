@@ -26,6 +26,8 @@ the captured launches are valid on every replay.
 """
 from dataclasses import dataclass, field
 
+from typing import Optional
+
 import torch
 
 from .actors import OBS_SHAPE, VecActors, apex_columns
@@ -64,6 +66,7 @@ class ApexConfig:
     channels_last: bool = True     # NHWC end to end (gather writes it, MIOpen consumes it)
     conv_benchmark: bool = False   # torch.backends.cudnn.benchmark (MIOpen find)
     hip_graph: bool = False        # replay captured HIP graphs of the compute blocks
+    dp_hook: Optional[bool] = None  # gradient all-reduce hook: None = when world > 1 (tests force it)
     extra: dict = field(default_factory=dict)
 
 
@@ -77,7 +80,8 @@ class ApexDQN:
         self.cfg = cfg
         self.device = torch.device(device if device is not None else "cuda")
         self.rank, self.world = rank, world
-        hook = GradAllReduce(group) if world > 1 else None
+        use_hook = world > 1 if cfg.dp_hook is None else cfg.dp_hook
+        hook = GradAllReduce(group) if use_hook else None
         torch.backends.cudnn.benchmark = bool(cfg.conv_benchmark)
         fmt = torch.channels_last if cfg.channels_last else torch.contiguous_format
         torch.manual_seed(cfg.seed)  # identical initial weights on every rank
@@ -203,7 +207,7 @@ class ApexDQN:
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
         split = solver.grad_hook is not None
-        G = dict(act=torch.cuda.CUDAGraph(), learn=[], learn_td=[], apply=None)
+        G = dict(act=torch.cuda.CUDAGraph(), learn=[], learn_td=[], apply=[], grads=[])
         with torch.cuda.stream(side):
             with torch.cuda.graph(G["act"], stream=side):
                 G["act_td"] = self._actor_compute()
@@ -217,10 +221,12 @@ class ApexDQN:
                         solver.apply_grads()
                 G["learn"].append(g)
                 G["learn_td"].append(td)
-            if split:
-                G["apply"] = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(G["apply"], stream=side):
-                    solver.apply_grads()
+                if split:  # the gradients live in this graph's pool: all-reduce and apply THESE
+                    G["grads"].append([q.grad for q in solver._params])
+                    ga = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(ga, stream=side):
+                        solver.apply_grads()
+                    G["apply"].append(ga)
         torch.cuda.current_stream(self.device).wait_stream(side)
         self.actors.t, self.actors.pushes = host  # capture recorded, did not run, the step
         self._graphs = G
@@ -236,9 +242,9 @@ class ApexDQN:
             self.env_steps += self.actors.N
         k = self.loader._pending.pop(0)
         G["learn"][k].replay()
-        if G["apply"] is not None:
-            self.solver.grad_hook(self.solver._params)  # RCCL all-reduce, eager
-            G["apply"].replay()
+        if G["apply"]:
+            self.solver.grad_hook(self.solver._params, grads=G["grads"][k])  # RCCL all-reduce, eager
+            G["apply"][k].replay()
         self.loader.issue()  # sample-ahead into the other slot
         self.replay.update_priorities(self.loader._slots[k][1], G["learn_td"][k], step=True)
         self._learner_host()

@@ -1,0 +1,171 @@
+// Learner optimizer step on gfx950: clip_grad_norm_ + Adam as three launches over every
+// parameter tensor at once.
+//
+// Reference: reth/reth/algorithm/dqn/dqn_solver.py:118-121 -- torch.nn.utils.clip_grad_norm_
+// (max_norm = clip_value, 2-norm) then torch.optim.Adam.step() (no weight decay, no amsgrad;
+// torch/optim/adam.py single-tensor math):
+//   g       = g * min(max_norm / (||g||_2 + 1e-6), 1)
+//   m       = lerp(m, g, 1 - beta1)            = m + (1 - beta1) * (g - m)
+//   v       = v * beta2 + (1 - beta2) * g * g
+//   p       = p - (lr / (1 - beta1^t)) * m / (sqrt(v) / sqrt(1 - beta2^t) + eps)
+// The step count t lives on the device (graph replay).  The global norm is a deterministic
+// two-stage reduction (per-workgroup fp64 partials, combined in workgroup order); torch's
+// fused/foreach kernels chunk 65,536 elements per workgroup (~30 workgroups for the 1.69 M
+// Q-net parameters), here every workgroup takes 4,096 elements (~420 workgroups).
+#include "common.hpp"
+
+namespace rth {
+
+constexpr int kOptThreads = 256;
+constexpr int kOptChunk = 4096;  // elements per workgroup (16 per lane)
+constexpr int kMaxPartials = 1 << 15;
+
+struct OptSeg {
+  float *param;
+  const float *grad;
+  float *m;
+  float *v;
+  int64_t n;
+  int64_t blk0;  // first workgroup of this tensor
+};
+
+struct OptArgs {
+  OptSeg seg[RTH_MAX_PARAM_TENSORS];
+  int32_t nseg;
+};
+
+// scalars the combine stage hands to the Adam stage (workspace layout after the partials)
+struct OptScalars {
+  float coef;         // clip coefficient (1 when not clipping)
+  float step_size;    // lr / (1 - beta1^t)
+  float bc2_sqrt;     // sqrt(1 - beta2^t)
+  float total_norm;   // ||g||_2 before clipping (clip_grad_norm_'s return value)
+};
+
+__device__ __forceinline__ int seg_of(const OptArgs &a, int64_t b) {
+  int s = 0;
+  while (s + 1 < a.nseg && b >= a.seg[s + 1].blk0) ++s;
+  return s;
+}
+
+__global__ __launch_bounds__(kOptThreads) void k_grad_sqsum(OptArgs a, double *__restrict__ part) {
+  __shared__ double red[kOptThreads];
+  const int64_t b = blockIdx.x;
+  const OptSeg &sg = a.seg[seg_of(a, b)];
+  const int64_t base = (b - sg.blk0) * kOptChunk;
+  double acc = 0.0;
+#pragma unroll 4
+  for (int k = 0; k < kOptChunk / kOptThreads; ++k) {
+    const int64_t i = base + k * kOptThreads + threadIdx.x;
+    if (i < sg.n) {
+      const double g = (double)sg.grad[i];
+      acc = radd(acc, rmul(g, g));
+    }
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = kOptThreads / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] = radd(red[threadIdx.x], red[threadIdx.x + s]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[b] = red[0];
+}
+
+// one workgroup: the norm, the clip coefficient, t += 1 and the bias corrections
+__global__ __launch_bounds__(kOptThreads) void k_opt_scalars(const double *__restrict__ part, int nparts, int clip,
+                                                            float max_norm, double lr, double beta1, double beta2,
+                                                            int64_t *__restrict__ step, OptScalars *__restrict__ out,
+                                                            float *__restrict__ total_out) {
+  __shared__ double red[kOptThreads];
+  double acc = 0.0;
+  for (int k = threadIdx.x; k < nparts; k += kOptThreads) acc = radd(acc, part[k]);
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = kOptThreads / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] = radd(red[threadIdx.x], red[threadIdx.x + s]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float total = (float)sqrt(red[0]);
+    float coef = 1.0f;
+    if (clip) {  // clip_coef = max_norm / (total_norm + 1e-6), clamped to 1 (f32 tensor math)
+      const float c = max_norm / radd(total, 1e-6f);
+      coef = c < 1.0f ? c : 1.0f;
+    }
+    const int64_t t = *step + 1;
+    *step = t;
+    // python-float scalars of adam.py, cast to f32 where they meet the f32 tensors
+    const double bc1 = 1.0 - pow(beta1, (double)t);
+    const double bc2 = 1.0 - pow(beta2, (double)t);
+    out->coef = coef;
+    out->step_size = (float)(lr / bc1);
+    out->bc2_sqrt = (float)sqrt(bc2);
+    out->total_norm = total;
+    if (total_out) *total_out = total;
+  }
+}
+
+__global__ __launch_bounds__(kOptThreads) void k_adam(OptArgs a, const OptScalars *__restrict__ sc, int clip,
+                                                     float w1, float beta2, float w2, float eps) {
+  const int64_t b = blockIdx.x;
+  const OptSeg &sg = a.seg[seg_of(a, b)];
+  const int64_t base = (b - sg.blk0) * kOptChunk;
+  const float coef = sc->coef, step_size = sc->step_size, bc2_sqrt = sc->bc2_sqrt;
+#pragma unroll 4
+  for (int k = 0; k < kOptChunk / kOptThreads; ++k) {
+    const int64_t i = base + k * kOptThreads + threadIdx.x;
+    if (i >= sg.n) break;
+    float g = sg.grad[i];
+    if (clip) g = rmul(g, coef);  // grad.mul_(clip_coef_clamped)
+    float m = sg.m[i], v = sg.v[i];
+    m = radd(m, rmul(w1, rsub(g, m)));        // lerp_(g, 1 - beta1), weight < 0.5 branch
+    v = radd(rmul(v, beta2), rmul(rmul(w2, g), g));  // mul_(beta2).addcmul_(g, g, 1 - beta2)
+    const float denom = radd(sqrtf(v) / bc2_sqrt, eps);
+    sg.param[i] = radd(sg.param[i], rmul(-step_size, m) / denom);  // addcdiv_(m, denom, -step_size)
+    sg.m[i] = m;
+    sg.v[i] = v;
+  }
+}
+
+}  // namespace rth
+
+using namespace rth;
+
+extern "C" {
+
+int64_t rth_clip_adam_workspace(void) { return (int64_t)kMaxPartials * 8 + 64; }
+
+int rth_clip_adam(const rth_param_tensor *tensors, int32_t n_tensors, double lr, double beta1, double beta2,
+                  double eps, double max_norm, int64_t *step_dev, void *workspace_dev, float *total_norm_out,
+                  void *stream) {
+  RTH_REQUIRE(tensors && step_dev && workspace_dev, "rth_clip_adam: NULL argument");
+  RTH_REQUIRE(n_tensors >= 1 && n_tensors <= RTH_MAX_PARAM_TENSORS, "rth_clip_adam: %d tensors not in [1, %d]",
+              n_tensors, RTH_MAX_PARAM_TENSORS);
+  OptArgs a{};
+  int64_t blocks = 0;
+  for (int s = 0; s < n_tensors; ++s) {
+    const rth_param_tensor &t = tensors[s];
+    RTH_REQUIRE(t.param && t.grad && t.exp_avg && t.exp_avg_sq && t.n >= 1, "rth_clip_adam: tensor %d incomplete", s);
+    a.seg[s] = OptSeg{t.param, t.grad, t.exp_avg, t.exp_avg_sq, t.n, blocks};
+    blocks += (t.n + kOptChunk - 1) / kOptChunk;
+  }
+  a.nseg = n_tensors;
+  RTH_REQUIRE(blocks <= kMaxPartials, "rth_clip_adam: %lld elements exceed the workspace",
+              (long long)(blocks * kOptChunk));
+  auto *part = static_cast<double *>(workspace_dev);
+  auto *sc = reinterpret_cast<OptScalars *>(static_cast<uint8_t *>(workspace_dev) + (int64_t)kMaxPartials * 8);
+  const int clip = max_norm >= 0.0;
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(k_grad_sqsum, dim3((unsigned)blocks), dim3(kOptThreads), 0, s, a, part);
+  RTH_LAUNCHED();
+  hipLaunchKernelGGL(k_opt_scalars, dim3(1), dim3(kOptThreads), 0, s, part, (int)blocks, clip, (float)max_norm, lr,
+                     beta1, beta2, step_dev, sc, total_norm_out);
+  RTH_LAUNCHED();
+  // 1 - beta1 and 1 - beta2 are python floats in adam.py, rounded to f32 once
+  hipLaunchKernelGGL(k_adam, dim3((unsigned)blocks), dim3(kOptThreads), 0, s, a, sc, clip, (float)(1.0 - beta1),
+                     (float)beta2, (float)(1.0 - beta2), (float)eps);
+  RTH_LAUNCHED();
+  return RTH_OK;
+}
+
+}  // extern "C"

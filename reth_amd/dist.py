@@ -31,13 +31,16 @@ class GradAllReduce:
             self._views.append(self._flat[off: off + p.numel()].view_as(p))
             off += p.numel()
 
-    def __call__(self, params):
-        world = dist.get_world_size(self.group)
+    def __call__(self, params, grads=None):
+        """grads: the gradient tensors to reduce (default: each parameter's .grad; a replayed
+        HIP graph passes the buffers its captured backward writes)"""
+        world = dist.get_world_size(self.group) if dist.is_initialized() else 1
         if world == 1:
             return
         if self._flat is None:
             self._bind(params)
-        grads = [p.grad for p in params]
+        if grads is None:
+            grads = [p.grad for p in params]
         torch._foreach_copy_(self._views, grads)
         dist.all_reduce(self._flat, op=dist.ReduceOp.SUM, group=self.group)
         self._flat.div_(world)

@@ -18,6 +18,7 @@ import torch
 from . import _lib
 from ._lib import call, ptr, stream_ptr
 from .model import default_models
+from .optim import ClipAdam
 from .schedule import Interval
 
 
@@ -140,10 +141,12 @@ class DQNSolver(Algorithm):
                     net.hwc_features = True  # HIP conv epilogues, NHWC feature order (model.py)
         if models.get("optimizer") is not None:
             self.optimizer = models["optimizer"]
-        else:
-            kw = {"fused": True} if models.get("fused_adam", fused_adam) else {}
-            if capturable:  # step count on the device: the update can be captured in a HIP graph
-                kw["capturable"] = True
+        elif models.get("fused_adam", fused_adam):  # clip_grad_norm_ + Adam in one HIP call (optim.py)
+            self.optimizer = ClipAdam(self.q_network.parameters(), lr=models.get("learning_rate", learning_rate),
+                                      eps=models.get("adam_epsilon", adam_epsilon),
+                                      max_norm=clip_value if clip_value >= 0 else None)
+        else:  # torch's Adam (the reference's optimizer object)
+            kw = {"capturable": True} if capturable else {}  # device step count: graph-capturable
             self.optimizer = torch.optim.Adam(self.q_network.parameters(), lr=models.get("learning_rate", learning_rate),
                                               eps=models.get("adam_epsilon", adam_epsilon), **kw)
         self._params = [p for p in self.q_network.parameters()]
@@ -237,9 +240,12 @@ class DQNSolver(Algorithm):
 
     def apply_grads(self):
         """dqn_solver.py:118-123: clip_grad_norm_ -> Adam -> target Interval"""
-        if self.clip_value >= 0:
-            torch.nn.utils.clip_grad_norm_(self._params, self.clip_value, foreach=True)
-        self.optimizer.step()
+        if isinstance(self.optimizer, ClipAdam):
+            self.optimizer.step()  # clips to optimizer.max_norm (= clip_value) itself
+        else:
+            if self.clip_value >= 0:
+                torch.nn.utils.clip_grad_norm_(self._params, self.clip_value, foreach=True)
+            self.optimizer.step()
         if self.auto_target_update and self._update_target_interval is not None:
             self._update_target_interval()
 

@@ -59,6 +59,34 @@ def test_graph_replay_matches_eager(dev):
         assert torch.equal(x, y)
 
 
+def test_graph_split_learner_applies_its_own_gradients(dev):
+    """with a gradient all-reduce hook the learner is captured as compute + apply per batch
+    parity; each replayed apply must consume the gradients its own compute graph wrote
+    (Adam's exp_avg after one replayed step follows exactly those gradients)"""
+    from reth_amd.apex import ApexConfig, ApexDQN
+
+    cfg = ApexConfig(n_actors=16, capacity=1024, batch_size=32, sample_start=64, seed=4, hip_graph=True,
+                     dp_hook=True)
+    ax = ApexDQN(cfg, device=dev)
+    for _ in range(30):
+        ax.iteration()
+    G = ax._graphs
+    assert G is not None and len(G["apply"]) == 2
+    ptrs = [{t.data_ptr() for t in G["grads"][p]} for p in range(2)]
+    assert not (ptrs[0] & ptrs[1])
+    opt, params = ax.solver.optimizer, ax.solver._params
+    for _ in range(2):  # both parities
+        torch.cuda.synchronize()  # ax runs on its own stream
+        k = ax.loader._pending[0]
+        before = [opt.state[p]["exp_avg"].clone() for p in params]
+        ax.iteration()
+        torch.cuda.synchronize()
+        coef = min(cfg.clip_value / (float(opt.total_norm[0]) + 1e-6), 1.0)
+        for p, mb, g in zip(params, before, G["grads"][k]):
+            torch.testing.assert_close(opt.state[p]["exp_avg"], mb + 0.1 * (g * coef - mb), rtol=1e-5, atol=1e-9)
+    ax.close()
+
+
 def test_prefill_then_learn(dev):
     from reth_amd.apex import ApexConfig, ApexDQN
 

@@ -37,6 +37,9 @@ extern "C" {
 #define RTH_F32 3
 #define RTH_F64 4
 #define RTH_MAX_COLS 8
+/* priority "dtype" for the tree/replay update calls: float64 priorities stored as given,
+ * without (w + 1e-6) ** alpha (NumbaSumTree.update; reth.buffer.PrioritizedBuffer.append) */
+#define RTH_PRIO_RAW 16
 
 const char *rth_last_error(void);
 /* library build/ABI version (major*10000 + minor*100 + patch) */
@@ -126,10 +129,22 @@ typedef struct {
 } rth_schedule;
 
 typedef struct rth_replay rth_replay;
-/* The shard owns its PERSampler state (per_sampler.py:5-12): the alpha / beta schedules and
- * the step count, the FIFO tail and the sample-call counter live in device memory, so every
- * launch below is argument-invariant from step to step (HIP-graph replayable). */
-int rth_replay_create(int64_t capacity, int32_t n_cols, const rth_col_desc *cols,
+/* Samplers of a shard (reth_buffer/reth_buffer/sampler/):
+ *   RTH_SAMPLER_PER      PERSampler (per_sampler.py:5-35): sum-tree, IS weights;
+ *   RTH_SAMPLER_UNIFORM  UniformSampler (uniform_sampler.py:6-25): updates append their
+ *                        indices to a list until it holds `capacity`; a sample draws
+ *                        list[floor(u * len)], weights 1;
+ *   RTH_SAMPLER_FIFO     FIFOSampler (fifo_sampler.py:8-29): updates push (index, weight)
+ *                        into a queue of at most `capacity` (oldest dropped); a sample pops
+ *                        the `batch` oldest, weights as pushed. */
+#define RTH_SAMPLER_PER 0
+#define RTH_SAMPLER_UNIFORM 1
+#define RTH_SAMPLER_FIFO 2
+/* The shard owns its sampler state (per_sampler.py:5-12): the alpha / beta schedules and
+ * the step count, the FIFO tail, the sample-call counter and the uniform list / FIFO queue
+ * live in device memory, so every launch below is argument-invariant from step to step
+ * (HIP-graph replayable). */
+int rth_replay_create(int64_t capacity, int32_t n_cols, const rth_col_desc *cols, int32_t sampler,
                       const rth_schedule *alpha, const rth_schedule *beta, int device, uint64_t seed,
                       rth_replay **out);
 int rth_replay_destroy(rth_replay *h);
@@ -153,9 +168,16 @@ int rth_replay_update_priorities(rth_replay *h, const int64_t *idx_dev, const vo
 int rth_replay_gather(rth_replay *h, const int64_t *idx_dev, int64_t n, void *const *out_cols_dev,
                       void *stream);
 /* host mirrors of the service counters: rows stored, FIFO tail, sampler cnt (appended +
- * re-prioritised, sampler_loop.py:36), sample calls issued, schedule steps taken */
+ * re-prioritised, sampler_loop.py:36), sample calls issued, schedule steps taken, and the
+ * sampler's own length (PER: rows stored; uniform: list length; FIFO: queued entries --
+ * FIFOSampler.ready_sample is len > batch) */
 int rth_replay_info(const rth_replay *h, int64_t *size, int64_t *tail, int64_t *cnt,
-                    int64_t *sample_calls, int64_t *sched_steps);
+                    int64_t *sample_calls, int64_t *sched_steps, int64_t *sampler_len);
+/* uniform row draw of NumpyBuffer.sample (reth/reth/buffer/buffer.py:88-90,
+ * np.random.choice(size, batch)): idx[i] = floor(u_i * size), u_i = uniforms_dev[i] or
+ * Philox(seed, counter (or *counter_dev), i) */
+int rth_uniform_indices(int64_t size, int64_t batch, const double *uniforms_dev, uint64_t seed, uint64_t counter,
+                        const int64_t *counter_dev, int64_t *idx_out_dev, void *stream);
 rth_sumtree *rth_replay_tree(rth_replay *h);
 /* device pointer of column c's storage ([capacity, row] of in_dtype) */
 void *rth_replay_column(rth_replay *h, int32_t c);

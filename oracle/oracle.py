@@ -192,3 +192,122 @@ def philox4x32(ctr, key):
     o = np.empty(4, np.uint32)
     lib().orc_philox4x32(P(c), P(k), P(o))
     return o
+
+
+# ---------------------------------------------------------------------------------------
+# Samplers and in-process buffers (pure-Python restatements; small cases only)
+# ---------------------------------------------------------------------------------------
+class UniformSampler:
+    """reth_buffer/reth_buffer/sampler/uniform_sampler.py:6-25 with the random draw injected:
+    sample() maps uniforms u to positions floor(u * tail) (np.random.choice(tail, B) draws
+    positions uniformly).  update() stops at capacity (the reference writes one entry past
+    a full list and raises IndexError when an update straddles capacity)."""
+
+    def __init__(self, capacity):
+        self.indices = np.zeros(capacity, dtype="i8")
+        self.capacity = capacity
+        self.tail = 0
+
+    def sample(self, uniforms):
+        pos = np.minimum((np.asarray(uniforms, np.float64) * self.tail).astype(np.int64), self.tail - 1)
+        return self.indices[pos], np.ones(len(pos), dtype="i8")
+
+    def update(self, indices, weights=None):
+        for idx in indices:
+            if self.tail == self.capacity:
+                return
+            self.indices[self.tail] = idx
+            self.tail += 1
+
+
+class FIFOSampler:
+    """reth_buffer/reth_buffer/sampler/fifo_sampler.py:8-29 (verbatim semantics)."""
+
+    def __init__(self, capacity):
+        from collections import deque
+
+        self.buffer = deque(maxlen=capacity)
+
+    def ready_sample(self, batch_size):
+        return len(self.buffer) > batch_size
+
+    def sample(self, batch_size):
+        res_i, res_w = [], []
+        for _ in range(batch_size):
+            i, w = self.buffer.pop()
+            res_i.append(i)
+            res_w.append(w)
+        return np.asarray(res_i, np.int64), np.asarray(res_w, np.float64)
+
+    def update(self, indices, weights):
+        for i, idx in enumerate(indices):
+            self.buffer.appendleft((int(idx), float(weights[i])))
+
+
+def numpy_buffer_indices(capacity, tail, size, batch_size):
+    """reth/reth/buffer/buffer.py:55-85 (NumpyBuffer.append_batch): slots written and the new
+    (tail, size); tail starts at -1"""
+    size = min(size + batch_size, capacity)
+    tail = (tail + 1) % capacity
+    len1 = min(batch_size, capacity - tail)
+    len2 = batch_size - len1
+    if len2 == 0:
+        idx = np.arange(tail, tail + len1)
+        tail = tail + len1 - 1
+    else:
+        idx = np.concatenate((np.arange(tail, tail + len1), np.arange(len2)))
+        tail = len2 - 1
+    return idx, tail, size
+
+
+class PrioritizedBuffer:
+    """reth/reth/buffer/prioritized_buffer.py:8-74 on the C tree (indices only, uniforms
+    injected into the tree sample; alpha/beta are Schedule specs)."""
+
+    def __init__(self, capacity, alpha, beta):
+        self.tree = Tree(capacity)
+        self.capacity = capacity
+        self.alpha, self.beta = _Sched(alpha), _Sched(beta)
+        self.tail, self.size = -1, 0
+
+    def _norm(self, w):
+        w = np.asarray(w)
+        return (w + 1e-6) ** self.alpha.value()
+
+    def append_batch(self, n, weights=None):
+        idx, self.tail, self.size = numpy_buffer_indices(self.capacity, self.tail, self.size, n)
+        w = np.ones(n) if weights is None else self._norm(weights)
+        self.tree.update(idx, np.asarray(w, np.float64))
+        return idx
+
+    def sample(self, uniforms):
+        idx, p = self.tree.sample(uniforms)
+        self.alpha.step()
+        self.beta.step()
+        return idx, (p / self.tree.min()) ** (-self.beta.value())
+
+    def update_priorities(self, indices, weights):
+        self.tree.update(np.asarray(indices, np.int64), np.asarray(self._norm(weights), np.float64))
+
+
+class _Sched:
+    """reth/reth/utils/schedule.py:4-52 (const or 'start,end,steps' linear)"""
+
+    def __init__(self, spec):
+        parts = str(spec).split(",")
+        if len(parts) == 1:
+            self.start = self.end = float(parts[0])
+            self.steps = 1
+            self.const = True
+        else:
+            self.start, self.end, self.steps = float(parts[0]), float(parts[1]), int(parts[2])
+            self.const = False
+        self.k = 0
+
+    def step(self):
+        self.k = min(self.k + 1, self.steps)
+
+    def value(self):
+        if self.const:
+            return self.start
+        return self.start + ((self.end - self.start) * self.k) / self.steps

@@ -12,6 +12,8 @@ LIB_PATH = os.path.join(_HERE, "libreth_hip.so")
 
 # element types (include/reth_hip.h)
 RTH_U8, RTH_I32, RTH_I64, RTH_F32, RTH_F64 = 0, 1, 2, 3, 4
+RTH_PRIO_RAW = 16  # priorities stored as given (no (w + 1e-6) ** alpha)
+SAMPLER_PER, SAMPLER_UNIFORM, SAMPLER_FIFO = 0, 1, 2
 MAX_COLS = 8
 
 c_i32, c_i64, c_u64, c_f32, c_f64, c_vp = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64,
@@ -63,7 +65,7 @@ SIGNATURES = {
     "rth_per_update": (c_i32, [c_vp, c_vp, c_vp, c_i32, c_i64, c_f64, c_vp]),
     "rth_per_sample": (c_i32, [c_vp, c_i64, c_f64, c_vp, c_u64, c_u64, c_vp, c_vp, c_vp]),
     # replay
-    "rth_replay_create": (c_i32, [c_i64, c_i32, ctypes.POINTER(ColDesc), ctypes.POINTER(Sched),
+    "rth_replay_create": (c_i32, [c_i64, c_i32, ctypes.POINTER(ColDesc), c_i32, ctypes.POINTER(Sched),
                                   ctypes.POINTER(Sched), c_i32, c_u64, ctypes.POINTER(c_vp)]),
     "rth_replay_destroy": (c_i32, [c_vp]),
     "rth_replay_append": (c_i32, [c_vp, ctypes.POINTER(Src), c_vp, c_i32, c_i64, c_vp, c_vp]),
@@ -71,7 +73,9 @@ SIGNATURES = {
     "rth_replay_update_priorities": (c_i32, [c_vp, c_vp, c_vp, c_i32, c_i64, c_i32, c_vp]),
     "rth_replay_gather": (c_i32, [c_vp, c_vp, c_i64, ctypes.POINTER(c_vp), c_vp]),
     "rth_replay_info": (c_i32, [c_vp, ctypes.POINTER(c_i64), ctypes.POINTER(c_i64),
-                                ctypes.POINTER(c_i64), ctypes.POINTER(c_i64), ctypes.POINTER(c_i64)]),
+                                ctypes.POINTER(c_i64), ctypes.POINTER(c_i64), ctypes.POINTER(c_i64),
+                                ctypes.POINTER(c_i64)]),
+    "rth_uniform_indices": (c_i32, [c_i64, c_i64, c_vp, c_u64, c_u64, c_vp, c_vp, c_vp]),
     "rth_replay_tree": (c_vp, [c_vp]),
     "rth_replay_column": (c_vp, [c_vp, c_i32]),
     "rth_copy_rows": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i32, c_i32, c_vp]),

@@ -212,6 +212,92 @@ __global__ void k_counter_add(int64_t *c, int64_t d) {
   if (threadIdx.x == 0 && blockIdx.x == 0) *c += d;
 }
 
+// ---------------------------------------------------------------- uniform / FIFO samplers
+// Device state of the non-PER samplers (one 32-byte record next to the ReplayState).
+struct SamplerState {
+  int64_t ulen;    // UniformSampler.tail: entries in the index list
+  int64_t fhead;   // FIFOSampler deque: ring position of the oldest entry
+  int64_t fcount;  // entries queued
+  int64_t pad;
+};
+
+constexpr int kSampThreads = 256;
+
+// the i-th index of an update: given, or the i-th FIFO slot of an append (before the bump)
+__device__ __forceinline__ int64_t upd_index(const int64_t *idx, const ReplayState *st, int64_t cap, int64_t i) {
+  return idx ? idx[i] : (st->tail + i) % cap;
+}
+
+// UniformSampler.update (uniform_sampler.py:16-21): append while the list is below capacity
+__global__ __launch_bounds__(kSampThreads) void k_uniform_push(int64_t *list, SamplerState *ss, int64_t cap,
+                                                                const int64_t *idx, const ReplayState *st,
+                                                                int64_t n) {
+  const int64_t l0 = ss->ulen;
+  for (int64_t i = threadIdx.x; i < n && l0 + i < cap; i += kSampThreads) list[l0 + i] = upd_index(idx, st, cap, i);
+  __syncthreads();
+  if (threadIdx.x == 0) ss->ulen = l0 + n < cap ? l0 + n : cap;
+}
+
+// UniformSampler.sample (:12-14): list[choice(len)], weights 1
+__global__ void k_uniform_sample(const int64_t *list, const SamplerState *ss, const ReplayState *st, int64_t batch,
+                                 const double *uniforms, uint64_t seed, int64_t *idx_out, double *w_out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= batch) return;
+  const int64_t L = ss->ulen;
+  const double u = uniforms ? uniforms[i] : philox_uniform(seed, (uint64_t)st->calls, (uint32_t)i, STREAM_SAMPLE);
+  int64_t j = (int64_t)(u * (double)L);
+  if (j >= L) j = L - 1;
+  idx_out[i] = list[j];
+  w_out[i] = 1.0;
+}
+
+// FIFOSampler.update (fifo_sampler.py:27-29): appendleft((idx, w)) on a deque(maxlen=cap)
+__global__ __launch_bounds__(kSampThreads) void k_fifo_push(int64_t *ridx, double *rw, SamplerState *ss, int64_t cap,
+                                                             const int64_t *idx, const ReplayState *st,
+                                                             const void *w, int32_t wdt, int64_t n) {
+  const int64_t head = ss->fhead, cnt = ss->fcount;
+  const int64_t keep0 = n > cap ? n - cap : 0;  // only the newest cap entries survive
+  for (int64_t i = keep0 + threadIdx.x; i < n; i += kSampThreads) {
+    const int64_t pos = (head + cnt + i) % cap;
+    ridx[pos] = upd_index(idx, st, cap, i);
+    rw[pos] = wdt == RTH_F32 ? (double)static_cast<const float *>(w)[i] : static_cast<const double *>(w)[i];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int64_t total = cnt + n, drop = total > cap ? total - cap : 0;
+    ss->fhead = (head + drop) % cap;
+    ss->fcount = total - drop;
+  }
+}
+
+// FIFOSampler.sample (:19-25): pop() the batch oldest entries
+__global__ __launch_bounds__(kSampThreads) void k_fifo_pop(const int64_t *ridx, const double *rw, SamplerState *ss,
+                                                            int64_t cap, int64_t batch, int64_t *idx_out,
+                                                            double *w_out) {
+  const int64_t head = ss->fhead;
+  for (int64_t i = threadIdx.x; i < batch; i += kSampThreads) {
+    const int64_t pos = (head + i) % cap;
+    idx_out[i] = ridx[pos];
+    w_out[i] = rw[pos];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    ss->fhead = (head + batch) % cap;
+    ss->fcount -= batch;
+  }
+}
+
+// NumpyBuffer.sample (buffer.py:88-90): choice(size, batch)
+__global__ void k_uniform_indices(int64_t size, int64_t batch, const double *uniforms, uint64_t seed,
+                                  uint64_t counter, const int64_t *counter_dev, int64_t *idx_out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= batch) return;
+  const uint64_t ctr = counter_dev ? (uint64_t)*counter_dev : counter;
+  const double u = uniforms ? uniforms[i] : philox_uniform(seed, ctr, (uint32_t)i, STREAM_SAMPLE);
+  int64_t j = (int64_t)(u * (double)size);
+  idx_out[i] = j < size ? j : size - 1;
+}
+
 // pixels per HWC chunk = 1024 * M (M in 1, 2, 4, 8); RTH_COPY_HWC_M overrides (tuning aid)
 static int hwc_chunk_m() {
   static const int m = [] {
@@ -285,14 +371,40 @@ struct rth_replay {
   int device;
   uint64_t seed;
   int32_t ncols;
+  int32_t kind;  // RTH_SAMPLER_*
   rth_col_desc desc[RTH_MAX_COLS];
   uint8_t *store[RTH_MAX_COLS];
-  rth_sumtree *tree;
+  rth_sumtree *tree;   // PER
+  int64_t *ulist;      // uniform: index list
+  int64_t *fidx;       // FIFO: queue ring (index, weight)
+  double *fw;
   rth_schedule alpha, beta;
-  ReplayState *st;  // device-resident service state (authoritative)
+  ReplayState *st;     // device-resident service state (authoritative)
+  SamplerState *ss;    // device-resident uniform / FIFO sampler state
   // host mirrors of the service counters (append_loop / sampler_loop bookkeeping)
-  int64_t tail, size, cnt, sample_calls, sched_steps;
+  int64_t tail, size, cnt, sample_calls, sched_steps, slen;
 };
+
+// sampler update for n indices (given, or the FIFO slots of an append when idx == NULL)
+static int sampler_update(rth_replay *h, const int64_t *idx, const void *w, int32_t wdt, int64_t n, hipStream_t s) {
+  if (n <= 0) return RTH_OK;
+  switch (h->kind) {
+    case RTH_SAMPLER_PER:
+      return tree_update_impl(h->tree, idx, 0, nullptr, w, wdt, 0.0, n, s, h->st, &h->alpha);
+    case RTH_SAMPLER_UNIFORM:
+      hipLaunchKernelGGL(k_uniform_push, dim3(1), dim3(kSampThreads), 0, s, h->ulist, h->ss, h->cap, idx, h->st, n);
+      RTH_LAUNCHED();
+      h->slen = h->slen + n < h->cap ? h->slen + n : h->cap;
+      return RTH_OK;
+    default:
+      RTH_REQUIRE(wdt == RTH_F32 || wdt == RTH_F64 || wdt == RTH_PRIO_RAW, "FIFO sampler: weights must be f32/f64");
+      hipLaunchKernelGGL(k_fifo_push, dim3(1), dim3(kSampThreads), 0, s, h->fidx, h->fw, h->ss, h->cap, idx, h->st, w,
+                         wdt == RTH_F32 ? RTH_F32 : RTH_F64, n);
+      RTH_LAUNCHED();
+      h->slen = h->slen + n < h->cap ? h->slen + n : h->cap;
+      return RTH_OK;
+  }
+}
 
 static int bump(rth_replay *h, int64_t dtail, int64_t dcalls, int64_t dstep, hipStream_t s) {
   hipLaunchKernelGGL(k_state_bump, dim3(1), dim3(64), 0, s, h->st, dtail, h->cap, dcalls, dstep);
@@ -330,9 +442,11 @@ int rth_counter_add(int64_t *c, int64_t d, void *stream) {
   return RTH_OK;
 }
 
-int rth_replay_create(int64_t capacity, int32_t n_cols, const rth_col_desc *cols, const rth_schedule *alpha,
-                      const rth_schedule *beta, int device, uint64_t seed, rth_replay **out) {
+int rth_replay_create(int64_t capacity, int32_t n_cols, const rth_col_desc *cols, int32_t sampler,
+                      const rth_schedule *alpha, const rth_schedule *beta, int device, uint64_t seed,
+                      rth_replay **out) {
   RTH_REQUIRE(out && cols && alpha && beta, "rth_replay_create: NULL argument");
+  RTH_REQUIRE(sampler >= RTH_SAMPLER_PER && sampler <= RTH_SAMPLER_FIFO, "rth_replay_create: bad sampler %d", sampler);
   for (const rth_schedule *sc : {alpha, beta})
     RTH_REQUIRE(sc->method >= RTH_SCHED_CONST && sc->method <= RTH_SCHED_EXP &&
                     (sc->method == RTH_SCHED_CONST || sc->max_steps >= 1),
@@ -354,14 +468,18 @@ int rth_replay_create(int64_t capacity, int32_t n_cols, const rth_col_desc *cols
   h->device = device;
   h->seed = seed;
   h->ncols = n_cols;
+  h->kind = sampler;
   h->alpha = *alpha;
   h->beta = *beta;
-  if (hipMalloc(&h->st, sizeof(ReplayState)) != hipSuccess) {
+  void *state = nullptr;
+  if (hipMalloc(&state, sizeof(ReplayState) + sizeof(SamplerState)) != hipSuccess) {
     delete h;
     set_error("rth_replay_create: hipMalloc(state) failed");
     return RTH_ERR_NOMEM;
   }
-  RTH_HIP(hipMemset(h->st, 0, sizeof(ReplayState)));
+  h->st = static_cast<ReplayState *>(state);
+  h->ss = reinterpret_cast<SamplerState *>(h->st + 1);
+  RTH_HIP(hipMemset(state, 0, sizeof(ReplayState) + sizeof(SamplerState)));
   for (int c = 0; c < n_cols; ++c) {
     h->desc[c] = cols[c];
     const size_t bytes = (size_t)capacity * cols[c].row_elems * dtype_size(cols[c].in_dtype);
@@ -372,10 +490,18 @@ int rth_replay_create(int64_t capacity, int32_t n_cols, const rth_col_desc *cols
       return RTH_ERR_NOMEM;
     }
   }
-  int rc = rth_sumtree_create(capacity, device, &h->tree);
+  int rc = RTH_OK;
+  if (sampler == RTH_SAMPLER_PER) {
+    rc = rth_sumtree_create(capacity, device, &h->tree);
+  } else if (sampler == RTH_SAMPLER_UNIFORM) {
+    if (hipMalloc(&h->ulist, (size_t)capacity * 8) != hipSuccess) rc = RTH_ERR_NOMEM;
+  } else if (hipMalloc(&h->fidx, (size_t)capacity * 8) != hipSuccess ||
+             hipMalloc(&h->fw, (size_t)capacity * 8) != hipSuccess) {
+    rc = RTH_ERR_NOMEM;
+  }
   if (rc) {
-    for (int k = 0; k < n_cols; ++k) (void)hipFree(h->store[k]);
-    delete h;
+    if (rc == RTH_ERR_NOMEM) set_error("rth_replay_create: sampler state allocation failed");
+    rth_replay_destroy(h);
     return rc;
   }
   *out = h;
@@ -387,7 +513,9 @@ int rth_replay_destroy(rth_replay *h) {
   (void)hipSetDevice(h->device);
   for (int c = 0; c < h->ncols; ++c) (void)hipFree(h->store[c]);
   (void)hipFree(h->st);
-  rth_sumtree_destroy(h->tree);
+  if (h->tree) rth_sumtree_destroy(h->tree);
+  for (void *p : {(void *)h->ulist, (void *)h->fidx, (void *)h->fw})
+    if (p) (void)hipFree(p);
   delete h;
   return RTH_OK;
 }
@@ -398,8 +526,10 @@ void *rth_replay_column(rth_replay *h, int32_t c) {
   return (h && c >= 0 && c < h->ncols) ? (void *)h->store[c] : nullptr;
 }
 
-int rth_replay_info(const rth_replay *h, int64_t *size, int64_t *tail, int64_t *cnt, int64_t *calls, int64_t *steps) {
+int rth_replay_info(const rth_replay *h, int64_t *size, int64_t *tail, int64_t *cnt, int64_t *calls, int64_t *steps,
+                    int64_t *sampler_len) {
   RTH_REQUIRE(h, "rth_replay_info: NULL handle");
+  if (sampler_len) *sampler_len = h->kind == RTH_SAMPLER_PER ? h->size : h->slen;
   if (size) *size = h->size;
   if (tail) *tail = h->tail;
   if (cnt) *cnt = h->cnt;
@@ -430,7 +560,7 @@ int rth_replay_append(rth_replay *h, const rth_src *srcs, const void *td_abs, in
   a.fifo_cap = h->cap;
   int rc = launch_copy(a, s);
   if (rc) return rc;
-  rc = tree_update_impl(h->tree, nullptr, 0, nullptr, td_abs, td_dtype, 0.0, n, s, h->st, &h->alpha);
+  rc = sampler_update(h, nullptr, td_abs, td_dtype, n, s);
   if (rc) return rc;
   if (idx_out) {  // FIFO slots for the caller (the append_loop's `indices`)
     hipLaunchKernelGGL(k_fifo_slots, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, idx_out, n, h->st, h->cap);
@@ -464,7 +594,22 @@ int rth_replay_sample(rth_replay *h, int64_t batch, const double *uniforms, void
                       int64_t *idx_out, double *isw_out, void *stream) {
   RTH_REQUIRE(h && batch > 0 && idx_out && isw_out, "rth_replay_sample: bad arguments");
   hipStream_t s = as_stream(stream);
-  int rc = tree_sample_impl(h->tree, batch, uniforms, h->seed, 0, 1, 0.0, idx_out, isw_out, s, h->st, &h->beta);
+  int rc = RTH_OK;
+  if (h->kind == RTH_SAMPLER_PER) {
+    rc = tree_sample_impl(h->tree, batch, uniforms, h->seed, 0, 1, 0.0, idx_out, isw_out, s, h->st, &h->beta);
+  } else if (h->kind == RTH_SAMPLER_UNIFORM) {
+    RTH_REQUIRE(h->slen > 0, "rth_replay_sample: uniform sampler is empty (np.random.choice(0, ...))");
+    hipLaunchKernelGGL(k_uniform_sample, dim3((unsigned)((batch + 255) / 256)), dim3(256), 0, s, h->ulist, h->ss, h->st,
+                       batch, uniforms, h->seed, idx_out, isw_out);
+    RTH_LAUNCHED();
+  } else {
+    RTH_REQUIRE(h->slen >= batch, "rth_replay_sample: FIFO sampler holds %lld < batch %lld (deque.pop from empty)",
+                (long long)h->slen, (long long)batch);
+    hipLaunchKernelGGL(k_fifo_pop, dim3(1), dim3(kSampThreads), 0, s, h->fidx, h->fw, h->ss, h->cap, batch, idx_out,
+                       isw_out);
+    RTH_LAUNCHED();
+    h->slen -= batch;
+  }
   if (rc) return rc;
   rc = bump(h, 0, 1, 0, s);
   if (rc) return rc;
@@ -483,9 +628,20 @@ int rth_replay_update_priorities(rth_replay *h, const int64_t *idx, const void *
     if (rc) return rc;
     h->sched_steps++;
   }
-  rc = tree_update_impl(h->tree, idx, 0, nullptr, td_abs, td_dtype, 0.0, n, s, h->st, &h->alpha);
+  rc = sampler_update(h, idx, td_abs, td_dtype, n, s);
   if (rc) return rc;
   h->cnt += n;
+  return RTH_OK;
+}
+
+int rth_uniform_indices(int64_t size, int64_t batch, const double *uniforms, uint64_t seed, uint64_t counter,
+                        const int64_t *counter_dev, int64_t *idx_out, void *stream) {
+  RTH_REQUIRE(size > 0, "rth_uniform_indices: size must be > 0 (np.random.choice(0, ...))");
+  RTH_REQUIRE(batch >= 0 && (batch == 0 || idx_out), "rth_uniform_indices: bad arguments");
+  if (batch == 0) return RTH_OK;
+  hipLaunchKernelGGL(k_uniform_indices, dim3((unsigned)((batch + 255) / 256)), dim3(256), 0, as_stream(stream), size,
+                     batch, uniforms, seed, counter, counter_dev, idx_out);
+  RTH_LAUNCHED();
   return RTH_OK;
 }
 

@@ -359,7 +359,8 @@ int tree_update_impl(rth_sumtree *t, const int64_t *idx, int64_t fifo_start, con
                      const void *td_abs, int32_t td_dtype, double alpha, int64_t n, hipStream_t s,
                      const ReplayState *st, const rth_schedule *alpha_s) {
   if (n <= 0) return RTH_OK;
-  RTH_REQUIRE(w64 || td_dtype == RTH_F32 || td_dtype == RTH_F64, "priority dtype must be f32 or f64");
+  if (!w64 && td_dtype == RTH_PRIO_RAW) w64 = static_cast<const double *>(td_abs);  // stored as given
+  RTH_REQUIRE(w64 || td_dtype == RTH_F32 || td_dtype == RTH_F64, "priority dtype must be f32, f64 or raw f64");
   UpdArgs a{t->nodes, t->cap, t->maxd, idx, fifo_start, w64, td_abs, td_dtype, alpha, n, st,
             alpha_s ? *alpha_s : rth_schedule{}};
   hipLaunchKernelGGL(k_tree_update, dim3(1), dim3(kUpdThreads), 0, s, a);

@@ -23,6 +23,7 @@ from .schedule import Schedule
 _TORCH_TO_RTH = {torch.uint8: _lib.RTH_U8, torch.int32: _lib.RTH_I32, torch.int64: _lib.RTH_I64,
                  torch.float32: _lib.RTH_F32, torch.float64: _lib.RTH_F64}
 _RTH_TO_TORCH = {v: k for k, v in _TORCH_TO_RTH.items()}
+_TORCH_TO_RTH[torch.bool] = _lib.RTH_U8  # bool columns (gym's `done`) are stored as bytes
 
 
 def _device(device):
@@ -39,9 +40,12 @@ def as_device(x, dtype, device):
     return torch.as_tensor(np.asarray(x), dtype=dtype).to(device, non_blocking=True).contiguous()
 
 
-def _prio_tensor(w, device):
+def _prio_tensor(w, device, raw=False):
     """priorities keep their precision class: float64 inputs are normalised in f64 (numpy
-    on an f8 array), everything else in f32 (the apex path's `np.asarray(loss, "f4")`)."""
+    on an f8 array), everything else in f32 (the apex path's `np.asarray(loss, "f4")`);
+    raw: float64 priorities stored without normalisation."""
+    if raw:
+        return as_device(w, torch.float64, device), _lib.RTH_PRIO_RAW
     is64 = (torch.is_tensor(w) and w.dtype == torch.float64) or (
         not torch.is_tensor(w) and np.asarray(w).dtype == np.float64)
     t = as_device(w, torch.float64 if is64 else torch.float32, device)
@@ -196,14 +200,19 @@ class Column:
         return torch.empty((n, *self.shape), dtype=self.out_dtype, device=device, memory_format=fmt)
 
 
+SAMPLERS = {"per": _lib.SAMPLER_PER, "uniform": _lib.SAMPLER_UNIFORM, "fifo": _lib.SAMPLER_FIFO}
+
+
 class HbmReplay:
-    """A prioritized replay shard resident in HBM (one per GPU).
+    """A replay shard resident in HBM (one per GPU).
 
     columns: list of Column.  alpha / beta: schedule specs (numbers or "start,end,steps").
-    sample_start: the sampler_loop gate, max(sample_start, batch_size) (main_loop.py:144-145).
+    sampler: "per" (PERSampler, the Ape-X path), "uniform" (UniformSampler) or "fifo"
+    (FIFOSampler) -- reth_buffer/reth_buffer/sampler/*.py; the non-PER samplers return
+    their weights (ones / the pushed weights) where PER returns IS weights.
     """
 
-    def __init__(self, capacity, columns, alpha=0.6, beta=0.4, device=None, seed=0):
+    def __init__(self, capacity, columns, alpha=0.6, beta=0.4, device=None, seed=0, sampler="per"):
         if not 1 <= len(columns) <= _lib.MAX_COLS:
             raise ValueError(f"1..{_lib.MAX_COLS} columns supported, got {len(columns)}")
         self.capacity = int(capacity)
@@ -212,13 +221,18 @@ class HbmReplay:
         self._alpha_str, self._beta_str = alpha, beta
         self.alpha = Schedule.from_str(alpha)
         self.beta = Schedule.from_str(beta)
+        if sampler not in SAMPLERS:
+            raise ValueError(f"sampler must be one of {sorted(SAMPLERS)}, got {sampler!r}")
+        self.sampler = sampler
         descs = (ColDesc * len(columns))(*[c.desc() for c in columns])
         h = c_vp()
         with torch.cuda.device(self.device):
-            call("rth_replay_create", self.capacity, len(columns), descs, ctypes.byref(sched_struct(self.alpha)),
-                 ctypes.byref(sched_struct(self.beta)), self.device.index, int(seed), ctypes.byref(h))
+            call("rth_replay_create", self.capacity, len(columns), descs, SAMPLERS[sampler],
+                 ctypes.byref(sched_struct(self.alpha)), ctypes.byref(sched_struct(self.beta)), self.device.index,
+                 int(seed), ctypes.byref(h))
         self._h = h.value
-        self.tree = SumTree(self.capacity, self.device, _handle=_lib.lib().rth_replay_tree(self._h))
+        th = _lib.lib().rth_replay_tree(self._h)
+        self.tree = SumTree(self.capacity, self.device, _handle=th) if th else None
 
     def __del__(self):
         if getattr(self, "_h", None):
@@ -229,11 +243,25 @@ class HbmReplay:
             self._h = None
 
     # ---------------------------------------------------------------- counters
-    def info(self):
-        """host mirrors: (size, tail, cnt, sample_calls, schedule steps)"""
-        vals = [c_i64() for _ in range(5)]
+    def _info(self):
+        vals = [c_i64() for _ in range(6)]
         call("rth_replay_info", self._h, *[ctypes.byref(v) for v in vals])
         return tuple(v.value for v in vals)
+
+    def info(self):
+        """host mirrors: (size, tail, cnt, sample_calls, schedule steps)"""
+        return self._info()[:5]
+
+    @property
+    def sampler_len(self):
+        """PER: rows stored; uniform: index-list length; FIFO: queued entries"""
+        return self._info()[5]
+
+    def ready_sample(self, batch_size):
+        """BaseSampler.ready_sample: FIFOSampler needs len > batch (fifo_sampler.py:16-17)"""
+        if self.sampler == "fifo":
+            return self.sampler_len > batch_size
+        return self.sampler_len > 0
 
     @property
     def size(self):
@@ -251,12 +279,13 @@ class HbmReplay:
         return _wrap_device(p, n, col.dtype, self.device).view(self.capacity, *col.shape)
 
     # ---------------------------------------------------------------- ops
-    def append(self, cols, td_abs, src_rows=None, row_strides=None, idx_out=None):
+    def append(self, cols, td_abs, src_rows=None, row_strides=None, idx_out=None, raw=False):
         """Client.append + append_loop: rows of `cols` (device tensors, [n, *shape] or a row
-        source with src_rows) into FIFO slots; priorities (td_abs + 1e-6) ** alpha."""
+        source with src_rows) into FIFO slots; priorities (td_abs + 1e-6) ** alpha, or stored
+        as given (float64) with raw=True."""
         if len(cols) != len(self.columns):
             raise ValueError(f"expected {len(self.columns)} columns, got {len(cols)}")
-        w, wt = _prio_tensor(td_abs, self.device)
+        w, wt = _prio_tensor(td_abs, self.device, raw)
         n = w.numel()
         assert n <= self.capacity  # fifo_policy.py:12
         srcs = (Src * len(cols))()
@@ -309,14 +338,14 @@ class HbmReplay:
         call("rth_replay_gather", self._h, ptr(idx), idx.numel(), arr, stream_ptr())
         return out_cols
 
-    def update_priorities(self, indices, td_abs, step=False):
+    def update_priorities(self, indices, td_abs, step=False, raw=False):
         """Client.update_priorities -> sampler_loop: on_step() first when step (:32-35).
         The device owns the schedules; the host Schedules mirror them for inspection."""
         if step:
             self.alpha.step()
             self.beta.step()
         idx = as_device(indices, torch.int64, self.device)
-        w, wt = _prio_tensor(td_abs, self.device)
+        w, wt = _prio_tensor(td_abs, self.device, raw)
         assert idx.numel() == w.numel()  # client.py:38
         call("rth_replay_update_priorities", self._h, ptr(idx), ptr(w), wt, idx.numel(), int(bool(step)),
              stream_ptr())

@@ -34,8 +34,9 @@ _NP_TO_TORCH = {np.dtype("uint8"): torch.uint8, np.dtype("int32"): torch.int32, 
 class ReplayService:
     """Stands in for the service Process returned by the reference's start_server."""
 
-    def __init__(self, capacity, batch_size, sampler, device, seed, widen_u8):
+    def __init__(self, capacity, batch_size, sampler, device, seed, widen_u8, kind="per"):
         self.capacity, self.batch_size = int(capacity), int(batch_size)
+        self.kind = kind
         self.alpha = sampler.get("kwargs", {}).get("alpha", 0.6)
         self.beta = sampler.get("kwargs", {}).get("beta", 0.4)
         # main_loop.py:144-145: sample_start = max(sample_start, batch_size)
@@ -57,11 +58,19 @@ class ReplayService:
                                                (isinstance(self.widen_u8, (set, list, tuple)) and
                                                 len(columns) in self.widen_u8))
                 columns.append(Column(tuple(c.shape[1:]), dt, torch.float32 if widen else None))
-            self.replay = HbmReplay(self.capacity, columns, self.alpha, self.beta, self.device, self.seed)
+            self.replay = HbmReplay(self.capacity, columns, self.alpha, self.beta, self.device, self.seed,
+                                    sampler=self.kind)
         return self.replay
 
     def ready(self):
-        return self.replay is not None and self.replay.cnt >= self.sample_start
+        """sampler_loop.py:23-28: cnt >= sample_start and sampler.ready_sample(batch_size)"""
+        return (self.replay is not None and self.replay.cnt >= self.sample_start
+                and self.replay.ready_sample(self.batch_size))
+
+    def weights_out(self, w):
+        """the sampler's weight column: IS weights (PER, f64), ones as int64 (UniformSampler
+        returns np.ones(batch, "i8")), or the pushed weights (FIFO, f64)"""
+        return w.to(torch.int64) if self.kind == "uniform" else w
 
     def check_ready(self):
         if not self.ready():
@@ -99,9 +108,10 @@ def start_server(capacity, batch_size, host=None, port=None, samplers=None, cach
         raise NotImplementedError("one sampler topic per shard")
     s = samplers[0]
     name = s["sampler_cls"] if isinstance(s["sampler_cls"], str) else s["sampler_cls"].__name__
-    if name != "PERSampler":
-        raise NotImplementedError(f"sampler {name} (only PERSampler is on the Ape-X path)")
-    svc = ReplayService(capacity, batch_size, s, device, seed, widen_u8)
+    kinds = {"PERSampler": "per", "UniformSampler": "uniform", "FIFOSampler": "fifo"}
+    if name not in kinds:
+        raise NotImplementedError(f"sampler {name} (PERSampler, UniformSampler, FIFOSampler are implemented)")
+    svc = ReplayService(capacity, batch_size, s, device, seed, widen_u8, kind=kinds[name])
     addr = f"hbm://{svc.device.index}/{next(_ids)}"
     _SERVICES[addr] = svc
     return svc, addr
@@ -155,7 +165,7 @@ class NumpyLoader:
     def sample(self):
         self.svc.check_ready()
         cols, idx, isw = self.svc.replay.sample(self.svc.batch_size)
-        return [c.cpu().numpy() for c in cols], idx.cpu().numpy(), isw.cpu().numpy()
+        return [c.cpu().numpy() for c in cols], idx.cpu().numpy(), self.svc.weights_out(isw).cpu().numpy()
 
 
 class TorchCudaLoader:
@@ -201,10 +211,12 @@ class TorchCudaLoader:
         if not self._pending:
             self._issue()
         k = self._pending.pop(0)
-        while len(self._pending) < self.prefetch:  # sample-ahead: batch k+1 is drawn before
-            self._issue()                          # batch k's priority update is enqueued
+        # sample-ahead: batch k+1 is drawn before batch k's priority update is enqueued (when
+        # the sampler can serve it now; a FIFO sampler may have to wait for more rows)
+        while len(self._pending) < self.prefetch and self.svc.ready():
+            self._issue()
         cols, idx, isw = self._slots[k]
-        return cols, idx, isw
+        return cols, idx, self.svc.weights_out(isw)
 
     def sample(self):
         cols, idx, isw = self.sample_device()

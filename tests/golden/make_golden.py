@@ -399,9 +399,138 @@ def gen_dqn(R):
     np.savez_compressed(os.path.join(OUT, "dqn_cartpole_b64.npz"), **out)
 
 
+# ----------------------------------------------------------------------------- samplers / buffers
+def _load_buffers(R):
+    """reth.buffer (NumpyBuffer, PrioritizedBuffer with its own NumbaSumTree) and the
+    Uniform / FIFO samplers; readerwriterlock is absent -> a no-op lock shim"""
+    import contextlib
+
+    rw = types.ModuleType("readerwriterlock")
+
+    class _Lock:
+        def gen_wlock(self):
+            return contextlib.nullcontext()
+
+        def gen_rlock(self):
+            return contextlib.nullcontext()
+
+    rw.rwlock = types.SimpleNamespace(RWLockWrite=_Lock)
+    sys.modules["readerwriterlock"] = rw
+    sys.modules["readerwriterlock.rwlock"] = rw.rwlock
+    _pkg("reth.buffer")
+    R.buf = _load("reth.buffer.buffer", "reth/reth/buffer/buffer.py")
+    R.bsum = _load("reth.buffer.sumtree", "reth/reth/buffer/sumtree.py")
+    R.pbuf = _load("reth.buffer.prioritized_buffer", "reth/reth/buffer/prioritized_buffer.py")
+    R.uni = _load("rb.sampler.uniform_sampler", "reth_buffer/reth_buffer/sampler/uniform_sampler.py")
+    R.fifos = _load("rb.sampler.fifo_sampler", "reth_buffer/reth_buffer/sampler/fifo_sampler.py")
+
+
+def gen_buffers(R):
+    _load_buffers(R)
+    out = {}
+    rng = np.random.default_rng(77)
+    # FIFOSampler (capacity 50): appends (FIFO-policy slots) and explicit updates, samples
+    cap = 50
+    fs, pol = R.fifos.FIFOSampler(cap), R.fifo.FIFOPolicy(cap)
+    ops = [("a", 30), ("s", 10), ("u", 40), ("s", 25), ("a", 45), ("s", 45), ("u", 7), ("s", 3)]
+    for k, (op, n) in enumerate(ops):
+        if op == "s":
+            out[f"fifo{k}_ready"] = np.array(fs.ready_sample(n))
+            i, w = fs.sample(n)
+            out[f"fifo{k}_idx"], out[f"fifo{k}_w"] = np.asarray(i, np.int64), np.asarray(w, np.float64)
+        else:
+            idx = pol.get_indices(n) if op == "a" else rng.integers(0, cap, n)
+            w = rng.random(n).astype(np.float32)
+            out[f"fifo{k}_in_idx"], out[f"fifo{k}_in_w"] = np.asarray(idx, np.int64), w
+            fs.update(idx, w)
+    out["fifo_ops"] = np.array([f"{op}{n}" for op, n in ops])
+    # UniformSampler (capacity 64): the list fills to exactly capacity, then ignores updates;
+    # sample positions recorded by replaying numpy's global stream
+    cap = 64
+    us, pol = R.uni.UniformSampler(cap), R.fifo.FIFOPolicy(cap)
+    np.random.seed(5)
+    ops = [("a", 20), ("u", 30), ("s", 16), ("a", 14), ("s", 32), ("a", 10), ("u", 5), ("s", 40)]
+    for k, (op, n) in enumerate(ops):
+        if op == "s":
+            st = np.random.get_state()
+            pos = np.random.choice(us.tail, n)
+            np.random.set_state(st)
+            i, w = us.sample(n)
+            out[f"uni{k}_pos"], out[f"uni{k}_tail"] = pos.astype(np.int64), np.array(us.tail)
+            out[f"uni{k}_idx"], out[f"uni{k}_w"] = np.asarray(i, np.int64), np.asarray(w)
+        else:
+            idx = pol.get_indices(n) if op == "a" else rng.integers(0, cap, n)
+            out[f"uni{k}_in_idx"] = np.asarray(idx, np.int64)
+            us.update(idx, np.ones(n, np.float32))
+    out["uni_ops"] = np.array([f"{op}{n}" for op, n in ops])
+    # NumpyBuffer (capacity 10, circular) + DynamicSizeBuffer growth
+    nb = R.buf.NumpyBuffer(10)
+    rows = lambda n: [rng.standard_normal((n, 4)), rng.integers(0, 6, n), rng.random(n) < 0.3]
+    k = 0
+    for kind, n in [("one", 1), ("one", 1), ("one", 1), ("batch", 5), ("batch", 6), ("one", 1), ("batch", 10)]:
+        r = rows(n)
+        for c, col in enumerate(r):
+            out[f"nb{k}_in{c}"] = col
+        if kind == "one":
+            ret = np.array([nb.append([col[0] for col in r])])
+        else:
+            ret = np.asarray(nb.append_batch(r))
+        out[f"nb{k}_ret"], out[f"nb{k}_tail"], out[f"nb{k}_size"] = ret.astype(np.int64), np.array(nb._tail), np.array(nb.size)
+        k += 1
+    for c, col in enumerate(nb.data):
+        out[f"nb_data{c}"] = col
+    out["nb_steps"] = np.array(k)
+    dyn = R.buf.DynamicSizeBuffer(4)
+    caps = []
+    for n in (1, 1, 1, 1, 1, 3, 10):
+        r = rows(n)
+        if n == 1:
+            dyn.append([col[0] for col in r])
+        else:
+            dyn.append_batch(r)
+        caps.append((dyn.capacity, dyn.size))
+    out["dyn_caps"] = np.array(caps, np.int64)
+    # PrioritizedBuffer (reth.buffer): alpha 0.6, beta "0.4,1,1000", capacity 100
+    pb = R.pbuf.PrioritizedBuffer(100, alpha=0.6, beta="0.4,1,1000")
+    d = lambda n: [rng.standard_normal((n, 3)).astype(np.float32), rng.integers(0, 4, n)]
+    # (PrioritizedBuffer.append of one row fails in the reference: the 0-d index/weight
+    # arrays it passes to _numba_update have no len(), prioritized_buffer.py:31-35)
+    seq = [("batch_w", 60), ("batch", 50), ("sample", 32), ("sample", 32), ("update", 40), ("sample", 32),
+           ("batch_w", 20), ("sample", 64)]
+    np.random.seed(9)
+    for k, (op, arg) in enumerate(seq):
+        if op == "batch_w":
+            r, w = d(arg), rng.random(arg)
+            out[f"pb{k}_d0"], out[f"pb{k}_d1"], out[f"pb{k}_w"] = r[0], r[1], w
+            pb.append_batch(r, weights=w)
+        elif op == "batch":
+            r = d(arg)
+            out[f"pb{k}_d0"], out[f"pb{k}_d1"] = r[0], r[1]
+            pb.append_batch(r)
+        elif op == "one":
+            r = d(1)
+            out[f"pb{k}_d0"], out[f"pb{k}_d1"] = r[0], r[1]
+            out[f"pb{k}_w"] = np.array(np.nan if arg is None else arg)
+            pb.append([r[0][0], r[1][0]], arg)
+        elif op == "update":
+            idx, w = rng.integers(0, 100, arg), rng.random(arg).astype(np.float32)
+            out[f"pb{k}_idx"], out[f"pb{k}_w"] = idx, w
+            pb.update_priorities(idx, w)
+        else:
+            st = np.random.get_state()
+            u = np.random.random_sample(arg)
+            np.random.set_state(st)
+            data, idx, w = pb.sample(arg)
+            out[f"pb{k}_u"], out[f"pb{k}_idx"], out[f"pb{k}_isw"] = u, np.asarray(idx), np.asarray(w)
+            out[f"pb{k}_rows0"] = data[0]
+        out[f"pb{k}_sum"] = pb.sumtree._sum.copy()
+    out["pb_ops"] = np.array([op for op, _ in seq])
+    np.savez_compressed(os.path.join(OUT, "buffers.npz"), **out)
+
+
 def main():
     R = load_reference()
-    which = sys.argv[1:] or ["sumtree_small", "sumtree_large", "per", "schedule_fifo", "nstep", "dqn"]
+    which = sys.argv[1:] or ["sumtree_small", "sumtree_large", "per", "schedule_fifo", "nstep", "dqn", "buffers"]
     for w in which:
         print("generating", w, flush=True)
         globals()[f"gen_{w}"](R)

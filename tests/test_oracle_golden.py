@@ -219,3 +219,67 @@ def test_philox_known_answer(orc):
                                                                           0x6D5451FD]
     assert orc.philox4x32([0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344], [0xA4093822, 0x299F31D0]).tolist() == [
         0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1]
+
+
+# ---------------------------------------------------------------------------------------
+# samplers / in-process buffers: the oracle restatements against the reference's outputs
+# (tests/golden/buffers.npz, generated from the reference modules by make_golden.py)
+# ---------------------------------------------------------------------------------------
+def _ops(g, key):
+    return [(str(x)[0], int(str(x)[1:])) for x in g[key]]
+
+
+def test_fifo_sampler_restatement(golden, orc):
+    g = golden("buffers.npz")
+    s = orc.FIFOSampler(50)
+    for k, (op, n) in enumerate(_ops(g, "fifo_ops")):
+        if op == "s":
+            assert s.ready_sample(n) == bool(g[f"fifo{k}_ready"])
+            i, w = s.sample(n)
+            assert np.array_equal(i, g[f"fifo{k}_idx"]) and np.array_equal(w, g[f"fifo{k}_w"])
+        else:
+            s.update(g[f"fifo{k}_in_idx"], g[f"fifo{k}_in_w"])
+
+
+def uniforms_for_positions(pos, tail):
+    """u with floor(u * tail) == pos (the reference drew positions with choice(tail, B))"""
+    return (np.asarray(pos, np.float64) + 0.5) / tail
+
+
+def test_uniform_sampler_restatement(golden, orc):
+    g = golden("buffers.npz")
+    s = orc.UniformSampler(64)
+    for k, (op, n) in enumerate(_ops(g, "uni_ops")):
+        if op == "s":
+            assert s.tail == int(g[f"uni{k}_tail"])
+            i, w = s.sample(uniforms_for_positions(g[f"uni{k}_pos"], s.tail))
+            assert np.array_equal(i, g[f"uni{k}_idx"]) and np.array_equal(w, g[f"uni{k}_w"])
+            assert w.dtype == np.int64
+        else:
+            s.update(g[f"uni{k}_in_idx"])
+
+
+def test_numpy_buffer_indices_restatement(golden, orc):
+    g = golden("buffers.npz")
+    tail, size = -1, 0
+    for k in range(int(g["nb_steps"])):
+        n = len(g[f"nb{k}_in0"])
+        idx, tail, size = orc.numpy_buffer_indices(10, tail, size, n)
+        assert np.array_equal(idx, g[f"nb{k}_ret"]) and tail == int(g[f"nb{k}_tail"]) and size == int(g[f"nb{k}_size"])
+
+
+def test_prioritized_buffer_restatement(golden, orc):
+    g = golden("buffers.npz")
+    pb = orc.PrioritizedBuffer(100, 0.6, "0.4,1,1000")
+    for k, op in enumerate(str(x) for x in g["pb_ops"]):
+        if op == "batch_w":
+            pb.append_batch(len(g[f"pb{k}_w"]), g[f"pb{k}_w"])
+        elif op == "batch":
+            pb.append_batch(len(g[f"pb{k}_d1"]))
+        elif op == "update":
+            pb.update_priorities(g[f"pb{k}_idx"], g[f"pb{k}_w"])
+        else:
+            idx, w = pb.sample(g[f"pb{k}_u"])
+            assert np.array_equal(idx, g[f"pb{k}_idx"])
+            np.testing.assert_allclose(w, g[f"pb{k}_isw"], rtol=1e-12, atol=0)
+        assert np.array_equal(pb.tree.sum, g[f"pb{k}_sum"])

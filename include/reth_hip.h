@@ -107,11 +107,15 @@ typedef struct {
 } rth_col_desc;
 
 /* a column source for an append: rows[i] (or i when rows_dev == NULL) of base_dev, rows
- * row_stride_bytes apart (0 = dense) */
+ * row_stride_bytes apart (0 = dense).  src_dtype: element type of the source rows; 0 or the
+ * column's storage type = as stored; RTH_F32 into a RTH_U8 column narrows whole-number
+ * pixels 0..255 (frames the reference's actors send as float32, test/apex-dqn/worker.py:46-50) */
 typedef struct {
   const void *base_dev;
   const int64_t *rows_dev;
   int64_t row_stride_bytes;
+  int32_t src_dtype;
+  int32_t reserved;
 } rth_src;
 
 /* A PERSampler schedule (reth_buffer/reth_buffer/utils/schedule.py:4-52):

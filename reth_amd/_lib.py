@@ -42,7 +42,8 @@ SCHED_CONST, SCHED_LINEAR, SCHED_EXP = 0, 1, 2
 
 
 class Src(ctypes.Structure):
-    _fields_ = [("base_dev", c_vp), ("rows_dev", c_vp), ("row_stride_bytes", c_i64)]
+    _fields_ = [("base_dev", c_vp), ("rows_dev", c_vp), ("row_stride_bytes", c_i64), ("src_dtype", c_i32),
+                ("reserved", c_i32)]
 
 
 # name -> (restype, argtypes); must match include/reth_hip.h exactly

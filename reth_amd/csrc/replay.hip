@@ -26,7 +26,19 @@ int tree_sample_impl(rth_sumtree *t, int64_t batch, const double *uniforms, uint
                      uint64_t counter, int is_weights, double beta, int64_t *idx_out, double *out,
                      hipStream_t s, const ReplayState *st, const rth_schedule *beta_s);
 
-enum Conv : int32_t { CONV_COPY = 0, CONV_U8_F32 = 1, CONV_U8_F32_HWC = 2 };
+enum Conv : int32_t { CONV_COPY = 0, CONV_U8_F32 = 1, CONV_U8_F32_HWC = 2, CONV_F32_U8 = 3 };
+
+// f32 pixel -> u8 (append of frames an actor sends as float32 whole numbers 0..255)
+__device__ __forceinline__ uint32_t f32_u8(float v) {
+  v = rintf(v);
+  return (uint32_t)(v < 0.0f ? 0.0f : (v > 255.0f ? 255.0f : v));
+}
+
+// a float at any byte address (arrays inside a wire-format message body are unaligned)
+__device__ __forceinline__ float ld_f32_bytes(const uint8_t *p) {
+  const uint32_t u = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+  return __uint_as_float(u);
+}
 
 struct CopyCol {
   const uint8_t *src;
@@ -143,6 +155,8 @@ __global__ __launch_bounds__(kCopyThreads) void k_copy_rows(CopyArgs a) {
   if (col.chunks == 0) {
     if (col.conv == CONV_COPY) {
       for (int64_t k = 0; k < nb; ++k) dst[k] = src[k];
+    } else if (col.conv == CONV_F32_U8) {
+      for (int64_t k = 0; k < nb / 4; ++k) dst[k] = (uint8_t)f32_u8(ld_f32_bytes(src + 4 * k));
     } else if (col.conv == CONV_U8_F32) {
       for (int64_t k = 0; k < nb; ++k) df[k] = (float)src[k];
     } else {
@@ -172,6 +186,17 @@ __global__ __launch_bounds__(kCopyThreads) void k_copy_rows(CopyArgs a) {
     return;
   }
   const int64_t o = chunk * col.chunk_in;  // first input byte of this chunk
+  if (col.conv == CONV_F32_U8) {  // 16-byte loads of 4 pixels -> one 4-byte store
+    const float *sf = reinterpret_cast<const float *>(src);
+    const int64_t e = o / 4 + 4 * tid;  // first element of this lane
+    if (vec && o + col.chunk_in <= nb) {
+      const float4 v = *reinterpret_cast<const float4 *>(sf + e);
+      *reinterpret_cast<uint32_t *>(dst + e) = f32_u8(v.x) | (f32_u8(v.y) << 8) | (f32_u8(v.z) << 16) | (f32_u8(v.w) << 24);
+    } else {
+      for (int64_t k = e; k < e + 4 && k < nb / 4; ++k) dst[k] = (uint8_t)f32_u8(ld_f32_bytes(src + 4 * k));
+    }
+    return;
+  }
   if (vec && o + col.chunk_in <= nb) {
     if (col.conv == CONV_COPY) {  // lane-contiguous 16-byte loads and stores
       *reinterpret_cast<uint4 *>(dst + o + 16 * tid) = *reinterpret_cast<const uint4 *>(src + o + 16 * tid);
@@ -549,9 +574,19 @@ int rth_replay_append(rth_replay *h, const rth_src *srcs, const void *td_abs, in
   CopyArgs a{};
   for (int c = 0; c < h->ncols; ++c) {
     RTH_REQUIRE(srcs[c].base_dev, "rth_replay_append: column %d source is NULL", c);
-    const int64_t rb = h->desc[c].row_elems * dtype_size(h->desc[c].in_dtype);
+    const rth_col_desc &d = h->desc[c];
+    const int64_t rb = d.row_elems * dtype_size(d.in_dtype);
+    int32_t conv = CONV_COPY;
+    int64_t ib = rb;  // bytes of one source row
+    if (srcs[c].src_dtype != 0 && srcs[c].src_dtype != d.in_dtype) {
+      RTH_REQUIRE(srcs[c].src_dtype == RTH_F32 && d.in_dtype == RTH_U8,
+                  "rth_replay_append: column %d: source type %d into storage type %d is not supported", c,
+                  srcs[c].src_dtype, d.in_dtype);
+      conv = CONV_F32_U8;
+      ib = d.row_elems * 4;
+    }
     a.col[c] = CopyCol{(const uint8_t *)srcs[c].base_dev, h->store[c], srcs[c].rows_dev, nullptr,
-                       srcs[c].row_stride_bytes ? srcs[c].row_stride_bytes : rb, rb, rb, CONV_COPY, 0};
+                       srcs[c].row_stride_bytes ? srcs[c].row_stride_bytes : ib, rb, ib, conv, 0};
   }
   a.n = n;
   a.ncols = h->ncols;

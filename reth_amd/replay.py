@@ -291,7 +291,12 @@ class HbmReplay:
         srcs = (Src * len(cols))()
         keep = []
         for c, (col, t) in enumerate(zip(self.columns, cols)):
-            if t.dtype != col.dtype or not t.is_cuda:
+            src_dtype = 0  # as stored
+            if t.dtype == torch.float32 and col.dtype == torch.uint8:
+                src_dtype = _lib.RTH_F32  # float32 frames narrowed to bytes by the copy kernel
+                if not t.is_cuda:
+                    t = t.to(self.device)
+            elif t.dtype != col.dtype or not t.is_cuda:
                 t = t.to(device=self.device, dtype=col.dtype)
             t = t if t.is_contiguous() else t.contiguous()
             rows = None if src_rows is None else src_rows[c]
@@ -299,8 +304,25 @@ class HbmReplay:
                 raise ValueError(f"column {c} has {t.shape[0]} rows, priorities have {n}")
             keep.append(t)
             stride = 0 if row_strides is None else int(row_strides[c])
-            srcs[c] = Src(ptr(t), ptr(rows), stride)
+            srcs[c] = Src(ptr(t), ptr(rows), stride, src_dtype, 0)
         call("rth_replay_append", self._h, srcs, ptr(w), wt, n, ptr(idx_out), stream_ptr())
+        return n
+
+    def append_strided(self, cols, td_abs, row_strides, raw=False):
+        """append from columns that live inside a device byte buffer (pack.ingest_append):
+        cols[c].view starts at row 0 of column c, rows row_strides[c] bytes apart;
+        cols[c].dtype is the source element type (float32 narrows into uint8 storage)."""
+        w, wt = _prio_tensor(td_abs, self.device, raw)
+        n = w.numel()
+        assert n <= self.capacity  # fifo_policy.py:12
+        srcs = (Src * len(cols))()
+        for c, (col, bc) in enumerate(zip(self.columns, cols)):
+            if bc.row_elems != col.row_elems:
+                raise ValueError(f"column {c}: message rows hold {bc.row_elems} elements, replay rows {col.row_elems}")
+            if bc.dtype != col.dtype and not (bc.dtype == torch.float32 and col.dtype == torch.uint8):
+                raise TypeError(f"column {c}: {bc.dtype} rows into {col.dtype} storage")
+            srcs[c] = Src(ptr(bc.view), None, int(row_strides[c]), _TORCH_TO_RTH[bc.dtype], 0)
+        call("rth_replay_append", self._h, srcs, ptr(w), wt, n, None, stream_ptr())
         return n
 
     def sample_into(self, batch_size, out_cols, idx_out, isw_out, uniforms=None, gather_timer=None):

@@ -47,17 +47,25 @@ class ReplayService:
         self.replay = None  # created on the first append (the LMDB map is sized from it too)
         self.alive = True
 
-    def ensure(self, cols):
+    def _widen(self, c):
+        return self.widen_u8 is True or (isinstance(self.widen_u8, (set, list, tuple)) and c in self.widen_u8)
+
+    def ensure(self, cols, row_shapes=None):
+        """create the shard from the first append's columns.  widen_u8 (True or a set of
+        column numbers): uint8 columns -- and float32 frame columns of a wire-format
+        message -- are stored as bytes and sampled as float32."""
         if self.replay is None:
             columns = []
-            for c in cols:
+            for k, c in enumerate(cols):
                 dt = c.dtype if torch.is_tensor(c) else _NP_TO_TORCH.get(np.asarray(c).dtype)
                 if dt is None:
                     raise TypeError(f"unsupported column dtype {np.asarray(c).dtype}")
-                widen = dt == torch.uint8 and (self.widen_u8 is True or
-                                               (isinstance(self.widen_u8, (set, list, tuple)) and
-                                                len(columns) in self.widen_u8))
-                columns.append(Column(tuple(c.shape[1:]), dt, torch.float32 if widen else None))
+                shape = tuple(c.shape[1:]) if row_shapes is None else tuple(row_shapes[k])
+                if dt == torch.float32 and row_shapes is not None and self._widen(k):
+                    columns.append(Column(shape, torch.uint8, torch.float32))
+                    continue
+                widen = dt == torch.uint8 and self._widen(k)
+                columns.append(Column(shape, dt, torch.float32 if widen else None))
             self.replay = HbmReplay(self.capacity, columns, self.alpha, self.beta, self.device, self.seed,
                                     sampler=self.kind)
         return self.replay
@@ -142,6 +150,18 @@ class Client:
         dev = rep.device
         cols = [as_device(c, col.dtype, dev) for c, col in zip(data, rep.columns)]
         rep.append(cols, weights)
+
+    def append_message(self, message):
+        """append_loop (server/main_loop.py:21-61) for one wire-format message as
+        Client.append sends it (utils/pack.py): the rows go from the message body to HBM
+        through one host->device copy (reth_amd/pack.py)"""
+        from . import pack
+
+        if self.svc.replay is None:
+            rows, _ = pack.deserialize(message)
+            first = pack.deserialize(rows[0])
+            self.svc.ensure([np.asarray(x)[None] for x in first], row_shapes=[np.shape(x) for x in first])
+        return pack.ingest_append(self.svc.replay, message)
 
     def update_priorities(self, indices, weights, step=True):
         assert len(indices) == len(weights)

@@ -528,9 +528,45 @@ def gen_buffers(R):
     np.savez_compressed(os.path.join(OUT, "buffers.npz"), **out)
 
 
+# ----------------------------------------------------------------------------- wire format
+def gen_pack(R):
+    """reth_buffer/utils/pack.py messages (uncompressed; lz4 and loguru are absent -> stubs),
+    with time.time() pinned so the bytes are reproducible"""
+    lz4 = types.ModuleType("lz4")
+    lz4.frame = types.ModuleType("lz4.frame")
+    sys.modules["lz4"], sys.modules["lz4.frame"] = lz4, lz4.frame
+    loguru = types.ModuleType("loguru")
+    loguru.logger = types.SimpleNamespace(info=lambda *a, **k: None, warning=lambda *a, **k: None)
+    sys.modules["loguru"] = loguru
+    pack = _load("rb.utils.pack", "reth_buffer/reth_buffer/utils/pack.py")
+    pack.time = types.SimpleNamespace(time=lambda: 1234.5)
+    rng = np.random.default_rng(11)
+    out = {}
+    # a Client.append message as test/apex-dqn/worker.py sends it (float32 frames)
+    n = 6
+    s0 = rng.integers(0, 256, (n, 4, 10, 12)).astype("f4")
+    s1 = rng.integers(0, 256, (n, 4, 10, 12)).astype("f4")
+    a = rng.integers(0, 6, n).astype("i8")
+    r = rng.choice(np.array([-1, 0, 1], "f4"), n)
+    done = (rng.random(n) < 0.3).astype("f4")
+    w = rng.random(n).astype("f4")
+    rows = [pack.serialize([c[i, ...] for c in (s0, a, r, s1, done)]) for i in range(n)]  # client.py:27-33
+    msg = pack.serialize([rows, w])
+    out.update(app_s0=s0, app_s1=s1, app_a=a, app_r=r, app_done=done, app_w=w,
+               app_msg=np.frombuffer(bytes(msg), np.uint8))
+    # a generic nested object (dict / list / bytes / scalars / Fortran array / 0-d array)
+    obj = {"x": [np.arange(10, dtype="i4"), b"raw-bytes", 3, "s", 2.5],
+           "f": np.asfortranarray(rng.standard_normal((3, 4))), "z": np.array(7.0, "f8"), "e": [[], {}]}
+    out["obj_msg"] = np.frombuffer(bytes(pack.serialize(obj)), np.uint8)
+    out["obj_x0"], out["obj_f"] = obj["x"][0], obj["f"]
+    # update_priorities message
+    out["upd_msg"] = np.frombuffer(bytes(pack.serialize([np.arange(5), w[:5], True])), np.uint8)
+    np.savez_compressed(os.path.join(OUT, "pack.npz"), **out)
+
+
 def main():
     R = load_reference()
-    which = sys.argv[1:] or ["sumtree_small", "sumtree_large", "per", "schedule_fifo", "nstep", "dqn", "buffers"]
+    which = sys.argv[1:] or ["sumtree_small", "sumtree_large", "per", "schedule_fifo", "nstep", "dqn", "buffers", "pack"]
     for w in which:
         print("generating", w, flush=True)
         globals()[f"gen_{w}"](R)

@@ -51,7 +51,7 @@ def test_struct_layouts():
     from reth_amd._lib import ColDesc, Src
 
     assert ctypes.sizeof(ColDesc) == 24
-    assert ctypes.sizeof(Src) == 24
+    assert ctypes.sizeof(Src) == 32
 
 
 def test_no_cpu_fallback_when_library_missing(monkeypatch, tmp_path):

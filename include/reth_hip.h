@@ -268,6 +268,24 @@ int rth_relu_bias_grad(const float *g_dev, const float *y_dev, float *gy_dev, fl
                        int64_t rows, int32_t C, void *stream);
 
 /* ------------------------------------------------------------------------------------
+ * Atari observation preprocessing (reth/reth/env/util.py:121-209, 281-297): per actor, the
+ * max of the last two raw RGB frames of the skip window (MaxAndSkipEnv), cv2 RGB2GRAY +
+ * INTER_AREA resize to out_h x out_w (WarpFrame; OpenCV's 8-bit algorithms restated, cv2
+ * being absent), pushed onto the actor's frame stack (FrameStack, ImageToPyTorch layout).
+ *   raw_dev    [n, 2, in_h, in_w, 3] uint8 (for a reset: the reset frame twice)
+ *   frames_dev the actors' stack ring [n * ring, stack, out_h, out_w] uint8 (nullable):
+ *              slot new_slot[i] <- slot prev_slot[i] shifted by one frame + the new frame,
+ *              or the new frame `stack` times when reset_dev[i] != 0 (reset_dev nullable)
+ *   out_frame_dev (nullable) [n, out_h, out_w]: the preprocessed frames alone
+ * ---------------------------------------------------------------------------------- */
+typedef struct rth_atari rth_atari;
+int rth_atari_create(int32_t in_h, int32_t in_w, int32_t out_h, int32_t out_w, int device, rth_atari **out);
+int rth_atari_destroy(rth_atari *h);
+int rth_atari_step(rth_atari *h, const uint8_t *raw_dev, int64_t n, uint8_t *frames_dev, int32_t ring, int32_t stack,
+                   const int64_t *prev_slot_dev, const int64_t *new_slot_dev, const uint8_t *reset_dev,
+                   uint8_t *out_frame_dev, void *stream);
+
+/* ------------------------------------------------------------------------------------
  * Learner optimizer step (reth/reth/algorithm/dqn/dqn_solver.py:118-121):
  * torch.nn.utils.clip_grad_norm_(params, max_norm) then torch.optim.Adam.step() over up to
  * RTH_MAX_PARAM_TENSORS fp32 tensors in three launches (norm partials, scalars, update).

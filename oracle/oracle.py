@@ -311,3 +311,63 @@ class _Sched:
         if self.const:
             return self.start
         return self.start + ((self.end - self.start) * self.k) / self.steps
+
+
+# ---------------------------------------------------------------------------------------
+# Atari preprocessing (reth/reth/env/util.py:121-209): MaxAndSkip max, cv2 RGB2GRAY,
+# cv2.resize INTER_AREA (OpenCV's 8-bit algorithms restated; cv2 is absent -> parity with
+# cv2 itself is unpinned), float32 operation order of resizeArea_
+# ---------------------------------------------------------------------------------------
+def area_tab(ssize, dsize, scale):
+    """computeResizeAreaTab: per destination index, [(source index, float32 weight)]"""
+    import math
+
+    out = []
+    for d in range(dsize):
+        f1 = d * scale
+        f2 = f1 + scale
+        cell = min(scale, ssize - f1)
+        s1, s2 = math.ceil(f1), math.floor(f2)
+        s2 = min(s2, ssize - 1)
+        s1 = min(s1, s2)
+        taps = []
+        if s1 - f1 > 1e-3:
+            taps.append((s1 - 1, np.float32((s1 - f1) / cell)))
+        for s in range(s1, s2):
+            taps.append((s, np.float32(1.0 / cell)))
+        if f2 - s2 > 1e-3:
+            taps.append((s2, np.float32(min(min(f2 - s2, 1.0), cell) / cell)))
+        out.append(taps)
+    return out
+
+
+def rgb2gray(rgb):
+    """cv2.cvtColor(RGB2GRAY) on uint8: (R*4899 + G*9617 + B*1868 + 8192) >> 14"""
+    c = rgb.astype(np.uint32)
+    return ((c[..., 0] * 4899 + c[..., 1] * 9617 + c[..., 2] * 1868 + 8192) >> 14).astype(np.uint32)
+
+
+def warp_frame(f0, f1, oh=84, ow=84):
+    """WarpFrame(MaxAndSkip max of two raw frames) -> uint8 [oh, ow]"""
+    H, W, _ = f0.shape
+    gray = rgb2gray(np.maximum(f0, f1)).astype(np.float32)
+    xt = area_tab(W, ow, 1.0 / (ow / W))
+    yt = area_tab(H, oh, 1.0 / (oh / H))
+    K = max(len(t) for t in xt)
+    xs = np.zeros((ow, K), np.int64)
+    xw = np.zeros((ow, K), np.float32)  # padded taps add S * 0 = +0: exact no-ops
+    for d, taps in enumerate(xt):
+        for k, (s, w) in enumerate(taps):
+            xs[d, k], xw[d, k] = s, w
+    out = np.empty((oh, ow), np.uint8)
+    for dy, taps in enumerate(yt):
+        acc = None
+        for sy, beta in taps:
+            row = gray[sy]
+            buf = np.zeros(ow, np.float32)
+            for k in range(K):
+                buf = (buf + row[xs[:, k]] * xw[:, k]).astype(np.float32)
+            term = (np.float32(beta) * buf).astype(np.float32)
+            acc = term if acc is None else (acc + term).astype(np.float32)
+        out[dy] = np.clip(np.rint(acc), 0, 255).astype(np.uint8)
+    return out

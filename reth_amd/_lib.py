@@ -95,6 +95,9 @@ SIGNATURES = {
     "rth_bias_relu": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_vp]),
     "rth_relu_bias_grad_workspace": (c_i64, [c_i32]),
     "rth_relu_bias_grad": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_vp]),
+    "rth_atari_create": (c_i32, [c_i32, c_i32, c_i32, c_i32, c_i32, ctypes.POINTER(c_vp)]),
+    "rth_atari_destroy": (c_i32, [c_vp]),
+    "rth_atari_step": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "rth_clip_adam_workspace": (c_i64, []),
     "rth_clip_adam": (c_i32, [c_vp, c_i32, c_f64, c_f64, c_f64, c_f64, c_f64, c_vp, c_vp, c_vp, c_vp]),
 }

@@ -182,7 +182,7 @@ def ingest_append(replay, message, staging=None):
         view = dbody[start:start + (n - 1) * stride + e["length"]]
         cols.append(_BodyColumn(view, tdt, elems))
         strides.append(stride)
-    w = torch.as_tensor(np.ascontiguousarray(weights)).to(dev)
+    w = torch.as_tensor(np.array(weights)).to(dev)  # (a copy: the message buffer is read-only)
     return replay.append_strided(cols, w, strides)
 
 

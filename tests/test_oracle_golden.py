@@ -283,3 +283,12 @@ def test_prioritized_buffer_restatement(golden, orc):
             assert np.array_equal(idx, g[f"pb{k}_idx"])
             np.testing.assert_allclose(w, g[f"pb{k}_isw"], rtol=1e-12, atol=0)
         assert np.array_equal(pb.tree.sum, g[f"pb{k}_sum"])
+
+
+def test_oracle_gray_known_values(orc):
+    """cv2 RGB2GRAY fixed point on the primaries (OpenCV gives 76 / 150 / 29) and area
+    weights summing to one per output pixel"""
+    px = np.array([[[255, 0, 0], [0, 255, 0], [0, 0, 255], [255, 255, 255], [0, 0, 0]]], np.uint8)
+    assert orc.rgb2gray(px).tolist() == [[76, 150, 29, 255, 0]]  # OpenCV's RGB2GRAY values
+    for tab in (orc.area_tab(160, 84, 1 / (84 / 160)), orc.area_tab(210, 84, 1 / (84 / 210))):
+        assert all(abs(sum(float(w) for _, w in t) - 1) < 1e-6 for t in tab)

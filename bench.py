@@ -186,6 +186,8 @@ def main():
 
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("RTH_SHARE_GPU"):  # rehearsal of N ranks on fewer GPUs (with RTH_DIST_BACKEND=gloo)
+        local %= torch.cuda.device_count()
     torch.cuda.set_device(local)
     rank, world = init_from_env()
     if world != args.gpus and world_env > 1:
@@ -213,8 +215,13 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    debug = os.environ.get("RTH_BENCH_DEBUG")
+    for k in range(args.steps):
         ax.iteration()
+        if debug:
+            torch.cuda.synchronize()
+            print(f"rank {rank} step {k}: {1e3 * (time.perf_counter() - t0):.1f} ms graphs={ax._graphs is not None} "
+                  f"updates={ax.updates} pending={ax.loader.pending()}", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

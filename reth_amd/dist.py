@@ -42,6 +42,10 @@ class GradAllReduce:
         if grads is None:
             grads = [p.grad for p in params]
         torch._foreach_copy_(self._views, grads)
+        if self._flat.is_cuda and dist.get_backend(self.group) != "nccl":
+            # gloo stages CUDA tensors through the host: hand it a finished buffer (its
+            # own stream bookkeeping against a busy non-default stream stalls for seconds)
+            torch.cuda.current_stream(self._flat.device).synchronize()
         dist.all_reduce(self._flat, op=dist.ReduceOp.SUM, group=self.group)
         self._flat.div_(world)
         torch._foreach_copy_(grads, self._views)
@@ -54,6 +58,8 @@ def init_from_env(backend=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world == 1 or dist.is_initialized():
         return (dist.get_rank() if dist.is_initialized() else 0), world
+    if backend is None:
+        backend = os.environ.get("RTH_DIST_BACKEND")  # e.g. gloo for a multi-rank rehearsal on one GPU
     if backend is None:
         backend = "nccl" if torch.cuda.is_available() else "gloo"  # nccl == RCCL on ROCm
     dist.init_process_group(backend=backend)

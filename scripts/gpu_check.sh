@@ -31,6 +31,13 @@ for step in "$@"; do
             rocprofv3 --kernel-trace --output-format csv -d "$PWD/gpurun_out/ktune_k${k}_b$b" -o run -- python scripts/probe_tree.py; done; done ;;
     kbench) export TMPDIR=/tmp; for kb in ${KB:-2_64}; do k=${kb%_*}; b=${kb#*_}; RTH_FIND_K=$k RTH_SAMPLE_BS=$b run kbench_k${k}_b$b 600 \
             rocprofv3 --kernel-trace --output-format csv -d "$PWD/gpurun_out/kbench_k${k}_b$b" -o run -- python bench.py --steps 60 --warmup 10 --no-cpu-baseline; done ;;
+    dp2) RTH_SHARE_GPU=1 RTH_DIST_BACKEND=gloo run bench_dp2 900 python -m torch.distributed.run --nnodes=1 \
+            --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 30 --warmup 10 \
+            --capacity 100000 --no-cpu-baseline ${DP2_ARGS:-} ;;
+    dpprobe) RTH_DIST_BACKEND=gloo run dp_probe2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+            --master-addr 127.0.0.1 --master-port 29518 scripts/dp_probe.py &&
+            RTH_DIST_BACKEND=gloo run dp_probe1 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+            --master-addr 127.0.0.1 --master-port 29519 scripts/dp_probe.py ;;
     probe) run probe 300 python scripts/probe_qnet.py ;;
     variants2)
       run bench_eager 600 python bench.py --steps 100 --warmup 20 --no-cpu-baseline --eager

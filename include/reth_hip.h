@@ -264,6 +264,17 @@ int rth_td_huber(const float *q_s0_dev, const float *q_s1_online_dev, const floa
  * ---------------------------------------------------------------------------------- */
 int rth_bias_relu(float *y_dev, const float *bias_dev, int64_t rows, int32_t C, void *stream);
 int64_t rth_relu_bias_grad_workspace(int32_t C);
+/* Merged dueling heads (dqn_model.py:22-43 fc_adv / fc_value): params = {adv.0.weight [H,F],
+ * value.0.weight [H,F], adv.0.bias, value.0.bias, adv.2.weight [A,H], value.2.weight [1,H],
+ * adv.2.bias [A], value.2.bias [1]} -> w1 [2H,F] (FC1 of both branches; with C > 0 its
+ * columns follow the NHWC flatten of a C x P feature map), b1 [2H], w2 [A+1,2H]
+ * (block diagonal), b2 [A+1].  rth_heads_split_grad maps the four gradients back onto the
+ * eight parameters (grads in the same order). */
+int rth_heads_merge(const float *const *params_dev, int64_t H, int64_t F, int64_t A, int32_t C, int32_t P,
+                    float *w1_dev, float *b1_dev, float *w2_dev, float *b2_dev, void *stream);
+int rth_heads_split_grad(const float *gw1_dev, const float *gb1_dev, const float *gw2_dev, const float *gb2_dev,
+                         int64_t H, int64_t F, int64_t A, int32_t C, int32_t P, float *const *grads_dev,
+                         void *stream);
 int rth_relu_bias_grad(const float *g_dev, const float *y_dev, float *gy_dev, float *db_dev, void *workspace_dev,
                        int64_t rows, int32_t C, void *stream);
 

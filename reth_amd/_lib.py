@@ -94,6 +94,10 @@ SIGNATURES = {
     "rth_td_huber": (c_i32, [c_vp] * 7 + [c_i64, c_i64, c_f32, c_i32, c_i32] + [c_vp] * 5 + [c_vp]),
     "rth_bias_relu": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_vp]),
     "rth_relu_bias_grad_workspace": (c_i64, [c_i32]),
+    "rth_heads_merge": (c_i32, [ctypes.POINTER(c_vp), c_i64, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp,
+                                c_vp]),
+    "rth_heads_split_grad": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i32, c_i32,
+                                     ctypes.POINTER(c_vp), c_vp]),
     "rth_relu_bias_grad": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_vp]),
     "rth_atari_create": (c_i32, [c_i32, c_i32, c_i32, c_i32, c_i32, ctypes.POINTER(c_vp)]),
     "rth_atari_destroy": (c_i32, [c_vp]),

@@ -113,6 +113,87 @@ __global__ __launch_bounds__(kCombThreads) void k_bias_grad_combine(const float 
   if (tid < C) db[tid] = red[tid];
 }
 
+
+// ---------------------------------------------------------------- merged dueling heads
+// model.py's merged-heads forward runs the two dueling branches as one FC1 GEMM (rows: the
+// advantage then the value branch; columns in the NHWC flatten order of the conv features
+// when hwc != 0) and one block-diagonal FC2 GEMM.  One launch builds the merged operands
+// from the reference's eight parameters, one launch splits their gradients back.
+struct HeadsDims {
+  int64_t H, F, A;  // hidden units per branch, features, actions
+  int32_t C, P;     // feature map channels and H*W positions (C = 0: no permutation)
+};
+
+__device__ __forceinline__ int64_t chw_col(const HeadsDims &d, int64_t j) {  // merged column -> reference column
+  if (d.C == 0) return j;
+  const int64_t p = j / d.C, c = j - p * d.C;
+  return c * d.P + p;
+}
+
+__global__ void k_heads_merge(HeadsDims d, const float *__restrict__ wa1, const float *__restrict__ wv1,
+                              const float *__restrict__ ba1, const float *__restrict__ bv1,
+                              const float *__restrict__ wa2, const float *__restrict__ wv2,
+                              const float *__restrict__ ba2, const float *__restrict__ bv2, float *__restrict__ w1,
+                              float *__restrict__ b1, float *__restrict__ w2, float *__restrict__ b2) {
+  const int64_t n1 = 2 * d.H * d.F, n2 = n1 + 2 * d.H, n3 = n2 + (d.A + 1) * 2 * d.H, n4 = n3 + d.A + 1;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n4; e += stride) {
+    if (e < n1) {
+      const int64_t r = e / d.F, j = e - r * d.F;
+      const int64_t src = (r % d.H) * d.F + chw_col(d, j);
+      w1[e] = r < d.H ? wa1[src] : wv1[src];
+    } else if (e < n2) {
+      const int64_t r = e - n1;
+      b1[r] = r < d.H ? ba1[r] : bv1[r - d.H];
+    } else if (e < n3) {
+      const int64_t k = e - n2, r = k / (2 * d.H), j = k - r * 2 * d.H;
+      float v = 0.0f;
+      if (r < d.A && j < d.H) v = wa2[r * d.H + j];
+      if (r == d.A && j >= d.H) v = wv2[j - d.H];
+      w2[k] = v;
+    } else {
+      const int64_t r = e - n3;
+      b2[r] = r < d.A ? ba2[r] : bv2[0];
+    }
+  }
+}
+
+__global__ void k_heads_split_grad(HeadsDims d, const float *__restrict__ gw1, const float *__restrict__ gb1,
+                                   const float *__restrict__ gw2, const float *__restrict__ gb2,
+                                   float *__restrict__ gwa1, float *__restrict__ gwv1, float *__restrict__ gba1,
+                                   float *__restrict__ gbv1, float *__restrict__ gwa2, float *__restrict__ gwv2,
+                                   float *__restrict__ gba2, float *__restrict__ gbv2) {
+  // indexed by the reference layouts (coalesced writes): FC1 weights, FC1 biases, FC2, FC2 bias
+  const int64_t n1 = 2 * d.H * d.F, n2 = n1 + 2 * d.H, n3 = n2 + d.A * d.H + d.H, n4 = n3 + d.A + 1;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n4; e += stride) {
+    if (e < n1) {  // reference column jr of branch row r -> merged column
+      const int64_t r = e / d.F, jr = e - r * d.F;
+      int64_t j = jr;
+      if (d.C) {
+        const int64_t c = jr / d.P, p = jr - c * d.P;
+        j = p * d.C + c;
+      }
+      const float g = gw1[r * d.F + j];
+      if (r < d.H) gwa1[r * d.F + jr] = g; else gwv1[(r - d.H) * d.F + jr] = g;
+    } else if (e < n2) {
+      const int64_t r = e - n1;
+      if (r < d.H) gba1[r] = gb1[r]; else gbv1[r - d.H] = gb1[r];
+    } else if (e < n3) {
+      const int64_t k = e - n2;
+      if (k < d.A * d.H) {
+        const int64_t r = k / d.H, j = k - r * d.H;
+        gwa2[k] = gw2[r * 2 * d.H + j];
+      } else {
+        gwv2[k - d.A * d.H] = gw2[d.A * 2 * d.H + d.H + (k - d.A * d.H)];
+      }
+    } else {
+      const int64_t r = e - n3;
+      if (r < d.A) gba2[r] = gb2[r]; else gbv2[0] = gb2[r];
+    }
+  }
+}
+
 }  // namespace rth
 
 using namespace rth;
@@ -155,6 +236,31 @@ int rth_relu_bias_grad(const float *g, const float *y, float *gy, float *db, voi
   RTH_LAUNCHED();
   hipLaunchKernelGGL(k_bias_grad_combine, dim3(1), dim3(kCombThreads), 0, as_stream(stream), part, (int)blocks, (int)C,
                      db);
+  RTH_LAUNCHED();
+  return RTH_OK;
+}
+
+
+int rth_heads_merge(const float *const *params, int64_t H, int64_t F, int64_t A, int32_t C, int32_t P,
+                    float *w1, float *b1, float *w2, float *b2, void *stream) {
+  RTH_REQUIRE(params && w1 && b1 && w2 && b2 && H >= 1 && F >= 1 && A >= 1, "rth_heads_merge: bad arguments");
+  for (int k = 0; k < 8; ++k) RTH_REQUIRE(params[k], "rth_heads_merge: parameter %d is NULL", k);
+  RTH_REQUIRE(C == 0 || (int64_t)C * P == F, "rth_heads_merge: C*P != F");
+  const HeadsDims d{H, F, A, C, P};
+  hipLaunchKernelGGL(k_heads_merge, dim3(2048), dim3(256), 0, as_stream(stream), d, params[0], params[1], params[2],
+                     params[3], params[4], params[5], params[6], params[7], w1, b1, w2, b2);
+  RTH_LAUNCHED();
+  return RTH_OK;
+}
+
+int rth_heads_split_grad(const float *gw1, const float *gb1, const float *gw2, const float *gb2, int64_t H,
+                         int64_t F, int64_t A, int32_t C, int32_t P, float *const *grads, void *stream) {
+  RTH_REQUIRE(gw1 && gb1 && gw2 && gb2 && grads && H >= 1 && F >= 1 && A >= 1, "rth_heads_split_grad: bad arguments");
+  for (int k = 0; k < 8; ++k) RTH_REQUIRE(grads[k], "rth_heads_split_grad: gradient %d is NULL", k);
+  RTH_REQUIRE(C == 0 || (int64_t)C * P == F, "rth_heads_split_grad: C*P != F");
+  const HeadsDims d{H, F, A, C, P};
+  hipLaunchKernelGGL(k_heads_split_grad, dim3(2048), dim3(256), 0, as_stream(stream), d, gw1, gb1, gw2, gb2, grads[0],
+                     grads[1], grads[2], grads[3], grads[4], grads[5], grads[6], grads[7]);
   RTH_LAUNCHED();
   return RTH_OK;
 }

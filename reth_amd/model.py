@@ -54,7 +54,16 @@ class DQNNetwork(nn.Module):
     # stay the reference's; the merged weights are either built per call (training, autograd
     # flows back into the branch parameters) or cached (`freeze_heads`, inference copies whose
     # weights change only at refresh points: target sync, actor weight reload).
+    def _head_params(self):
+        a0, v0, a2, v2 = self.fc_adv[0], self.fc_value[0], self.fc_adv[2], self.fc_value[2]
+        return [a0.weight, v0.weight, a0.bias, v0.bias, a2.weight, v2.weight, a2.bias, v2.bias]
+
     def _merged_head_weights(self):
+        ps = self._head_params()
+        if ps[0].is_cuda:  # one HIP launch (and one for the gradients), qnet.hip
+            c, fh, fw = self._feat_chw
+            dims = (ps[0].shape[0], ps[0].shape[1], ps[4].shape[0], c if self.hwc_features else 0, fh * fw)
+            return _MergeHeads.apply(dims, *ps)
         a0, v0, a2, v2 = self.fc_adv[0], self.fc_value[0], self.fc_adv[2], self.fc_value[2]
         if self.hwc_features:  # FC1 columns permuted (C,H,W) -> (H,W,C): the NHWC flatten is a view
             c, fh, fw = self._feat_chw
@@ -105,6 +114,41 @@ class DQNNetwork(nn.Module):
         for conv, ws in zip(convs, self._ws):
             x = _ConvBiasReLU.apply(x, conv.weight, conv.bias, conv.stride, ws)
         return x
+
+
+class _MergeHeads(torch.autograd.Function):
+    """(w1, b1, w2, b2) of the merged dueling heads from the eight branch parameters
+    (rth_heads_merge) and their gradients back (rth_heads_split_grad)"""
+
+    @staticmethod
+    def forward(ctx, dims, *ps):
+        from ._lib import c_vp, call, ptr, stream_ptr
+
+        H, F, A, C, P = dims
+        ps = [p.contiguous() for p in ps]
+        o = dict(device=ps[0].device, dtype=torch.float32)
+        w1, b1 = torch.empty(2 * H, F, **o), torch.empty(2 * H, **o)
+        w2, b2 = torch.empty(A + 1, 2 * H, **o), torch.empty(A + 1, **o)
+        arr = (c_vp * 8)(*[p.data_ptr() for p in ps])
+        call("rth_heads_merge", arr, H, F, A, C, P, ptr(w1), ptr(b1), ptr(w2), ptr(b2), stream_ptr())
+        ctx.dims = dims
+        ctx.shapes = [p.shape for p in ps]
+        return w1, b1, w2, b2
+
+    @staticmethod
+    def backward(ctx, gw1, gb1, gw2, gb2):
+        from ._lib import c_vp, call, ptr, stream_ptr
+
+        H, F, A, C, P = ctx.dims
+        outs = [gw1, gb1, gw2, gb2]
+        shapes = [(2 * H, F), (2 * H,), (A + 1, 2 * H), (A + 1,)]
+        ref = next(g for g in outs if g is not None)
+        outs = [torch.zeros(s, device=ref.device) if g is None else g.contiguous() for g, s in zip(outs, shapes)]
+        grads = [torch.empty(s, device=ref.device) for s in ctx.shapes]
+        arr = (c_vp * 8)(*[g.data_ptr() for g in grads])
+        call("rth_heads_split_grad", ptr(outs[0]), ptr(outs[1]), ptr(outs[2]), ptr(outs[3]), H, F, A, C, P, arr,
+             stream_ptr())
+        return (None, *grads)
 
 
 class _LinearReLU(torch.autograd.Function):

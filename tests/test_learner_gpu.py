@@ -231,3 +231,27 @@ def test_target_interval_and_weights_stream(dev):
     s2.load_weights(io.BytesIO(buf.getvalue()))
     assert all(torch.equal(p, q) for p, q in zip(s.q_network.parameters(), s2.q_network.parameters()))
     assert all(torch.equal(p, q) for p, q in zip(s2.q_network.parameters(), s2.target_q_network.parameters()))
+
+
+@pytest.mark.parametrize("hwc", [False, True])
+def test_merged_heads_kernels_match_torch(dev, hwc):
+    """rth_heads_merge / rth_heads_split_grad == the torch cat/permute construction of the
+    merged dueling heads and its autograd, element for element"""
+    from reth_amd.model import DQNNetwork
+
+    torch.manual_seed(3)
+    net = DQNNetwork((4, 84, 84), 6).to(dev)
+    net.hwc_features = hwc
+    ours = net._merged_head_weights()
+    cpu = DQNNetwork((4, 84, 84), 6)
+    cpu.load_state_dict({k: v.cpu() for k, v in net.state_dict().items()})
+    cpu.hwc_features = hwc
+    ref = cpu._merged_head_weights()  # the torch construction (CPU tensors)
+    for a, b in zip(ours, ref):
+        assert torch.equal(a.cpu(), b)
+    g = [torch.randn(t.shape) for t in ref]
+    torch.autograd.backward(ours, [x.to(dev) for x in g])
+    torch.autograd.backward(ref, g)
+    for (name, p), q in zip(net.named_parameters(), cpu.parameters()):
+        if name.startswith("fc_"):
+            assert torch.equal(p.grad.cpu(), q.grad), name

@@ -168,6 +168,15 @@ int rth_replay_sample(rth_replay *h, int64_t batch, const double *uniforms_dev,
  * schedules first (PERSampler.on_step), then PERSampler.update */
 int rth_replay_update_priorities(rth_replay *h, const int64_t *idx_dev, const void *td_abs_dev,
                                  int32_t td_dtype, int64_t n, int32_t step, void *stream);
+/* The same, deferred (PER shards): the update is recorded and applied by the shard's next
+ * tree launch -- merged into the next rth_replay_append's (one launch instead of two), or on
+ * its own before a sample / immediate update / rth_replay_flush -- which is the order the
+ * reference's sampler applies its messages in.  idx_dev / td_abs_dev must stay valid (and
+ * unmodified) until then.  Host counters are updated at once.  Call rth_replay_flush before
+ * reading the tree through rth_replay_tree. */
+int rth_replay_update_priorities_deferred(rth_replay *h, const int64_t *idx_dev, const void *td_abs_dev,
+                                          int32_t td_dtype, int64_t n, int32_t step, void *stream);
+int rth_replay_flush(rth_replay *h, void *stream);
 /* NumpyLoader row fetch (numpy_loader.py:381-396) for explicit indices */
 int rth_replay_gather(rth_replay *h, const int64_t *idx_dev, int64_t n, void *const *out_cols_dev,
                       void *stream);

@@ -72,6 +72,8 @@ SIGNATURES = {
     "rth_replay_append": (c_i32, [c_vp, ctypes.POINTER(Src), c_vp, c_i32, c_i64, c_vp, c_vp]),
     "rth_replay_sample": (c_i32, [c_vp, c_i64, c_vp, ctypes.POINTER(c_vp), c_vp, c_vp, c_vp]),
     "rth_replay_update_priorities": (c_i32, [c_vp, c_vp, c_vp, c_i32, c_i64, c_i32, c_vp]),
+    "rth_replay_update_priorities_deferred": (c_i32, [c_vp, c_vp, c_vp, c_i32, c_i64, c_i32, c_vp]),
+    "rth_replay_flush": (c_i32, [c_vp, c_vp]),
     "rth_replay_gather": (c_i32, [c_vp, c_vp, c_i64, ctypes.POINTER(c_vp), c_vp]),
     "rth_replay_info": (c_i32, [c_vp, ctypes.POINTER(c_i64), ctypes.POINTER(c_i64),
                                 ctypes.POINTER(c_i64), ctypes.POINTER(c_i64), ctypes.POINTER(c_i64),

@@ -187,7 +187,7 @@ class ApexDQN:
         slot = self.loader.take()
         td = self._learner_train(slot)
         self.loader.issue()  # sample-ahead: batch k+1 before batch k's priorities land
-        self.replay.update_priorities(slot[1], td, step=True)
+        self.replay.update_priorities(slot[1], td, step=True, deferred=True)  # merged into the next append
         self._learner_host()
 
     # ------------------------------------------------------------------ graph replay
@@ -246,5 +246,5 @@ class ApexDQN:
             self.solver.grad_hook(self.solver._params, grads=G["grads"][k])  # RCCL all-reduce, eager
             G["apply"][k].replay()
         self.loader.issue()  # sample-ahead into the other slot
-        self.replay.update_priorities(self.loader._slots[k][1], G["learn_td"][k], step=True)
+        self.replay.update_priorities(self.loader._slots[k][1], G["learn_td"][k], step=True, deferred=True)
         self._learner_host()

@@ -143,6 +143,16 @@ struct ReplayState {
   int64_t pad;
 };
 
+// A PER priority update recorded by rth_replay_update_priorities_deferred and applied by the
+// next tree-update launch of the shard (merged with an append's), before its keys.
+struct UpdPending {
+  const int64_t *idx;
+  const void *td;
+  int32_t dtype;
+  int32_t step;  // advance the schedules first (update_priorities(step=True))
+  int64_t n;
+};
+
 // Schedule.value (schedule.py:29-40, 48-52), python float operation order
 __host__ __device__ inline double sched_value(const rth_schedule &s, int64_t step) {
   if (s.method == RTH_SCHED_CONST) return s.start;

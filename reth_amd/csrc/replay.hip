@@ -21,7 +21,8 @@ struct rth_sumtree;
 namespace rth {
 int tree_update_impl(rth_sumtree *t, const int64_t *idx, int64_t fifo_start, const double *w64,
                      const void *td_abs, int32_t td_dtype, double alpha, int64_t n, hipStream_t s,
-                     const ReplayState *st, const rth_schedule *alpha_s);
+                     ReplayState *st, const rth_schedule *alpha_s, const UpdPending *pend = nullptr,
+                     int post_tail = 0);
 int tree_sample_impl(rth_sumtree *t, int64_t batch, const double *uniforms, uint64_t seed,
                      uint64_t counter, int is_weights, double beta, int64_t *idx_out, double *out,
                      hipStream_t s, const ReplayState *st, const rth_schedule *beta_s);
@@ -408,7 +409,16 @@ struct rth_replay {
   SamplerState *ss;    // device-resident uniform / FIFO sampler state
   // host mirrors of the service counters (append_loop / sampler_loop bookkeeping)
   int64_t tail, size, cnt, sample_calls, sched_steps, slen;
+  UpdPending pend;  // a deferred PER update, applied by the next tree launch
+  int has_pend;
 };
+
+// apply a deferred update on its own (before a sample, an immediate update, a flush)
+static int flush_pending(rth_replay *h, hipStream_t s) {
+  if (!h->has_pend) return RTH_OK;
+  h->has_pend = 0;
+  return tree_update_impl(h->tree, nullptr, 0, nullptr, nullptr, RTH_F32, 0.0, 0, s, h->st, &h->alpha, &h->pend, 0);
+}
 
 // sampler update for n indices (given, or the FIFO slots of an append when idx == NULL)
 static int sampler_update(rth_replay *h, const int64_t *idx, const void *w, int32_t wdt, int64_t n, hipStream_t s) {
@@ -595,14 +605,23 @@ int rth_replay_append(rth_replay *h, const rth_src *srcs, const void *td_abs, in
   a.fifo_cap = h->cap;
   int rc = launch_copy(a, s);
   if (rc) return rc;
-  rc = sampler_update(h, nullptr, td_abs, td_dtype, n, s);
-  if (rc) return rc;
   if (idx_out) {  // FIFO slots for the caller (the append_loop's `indices`)
     hipLaunchKernelGGL(k_fifo_slots, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, idx_out, n, h->st, h->cap);
     RTH_LAUNCHED();
   }
-  rc = bump(h, n, 0, 0, s);
-  if (rc) return rc;
+  if (h->kind == RTH_SAMPLER_PER) {
+    // one tree launch: a deferred update_priorities (if any), this append's priorities,
+    // then the FIFO tail advance -- the sequential order of the reference's messages
+    rc = tree_update_impl(h->tree, nullptr, 0, nullptr, td_abs, td_dtype, 0.0, n, s, h->st, &h->alpha,
+                          h->has_pend ? &h->pend : nullptr, 1);
+    h->has_pend = 0;
+    if (rc) return rc;
+  } else {
+    rc = sampler_update(h, nullptr, td_abs, td_dtype, n, s);
+    if (rc) return rc;
+    rc = bump(h, n, 0, 0, s);
+    if (rc) return rc;
+  }
   h->tail = (h->tail + n) % h->cap;
   h->size = h->size + n < h->cap ? h->size + n : h->cap;
   h->cnt += n;
@@ -629,7 +648,8 @@ int rth_replay_sample(rth_replay *h, int64_t batch, const double *uniforms, void
                       int64_t *idx_out, double *isw_out, void *stream) {
   RTH_REQUIRE(h && batch > 0 && idx_out && isw_out, "rth_replay_sample: bad arguments");
   hipStream_t s = as_stream(stream);
-  int rc = RTH_OK;
+  int rc = flush_pending(h, s);
+  if (rc) return rc;
   if (h->kind == RTH_SAMPLER_PER) {
     rc = tree_sample_impl(h->tree, batch, uniforms, h->seed, 0, 1, 0.0, idx_out, isw_out, s, h->st, &h->beta);
   } else if (h->kind == RTH_SAMPLER_UNIFORM) {
@@ -657,7 +677,8 @@ int rth_replay_update_priorities(rth_replay *h, const int64_t *idx, const void *
                                  int32_t step, void *stream) {
   RTH_REQUIRE(h && (n == 0 || (idx && td_abs)), "rth_replay_update_priorities: bad arguments");
   hipStream_t s = as_stream(stream);
-  int rc;
+  int rc = flush_pending(h, s);
+  if (rc) return rc;
   if (step) {  // sampler_loop.py:32-33: on_step() before the update
     rc = bump(h, 0, 0, 1, s);
     if (rc) return rc;
@@ -667,6 +688,26 @@ int rth_replay_update_priorities(rth_replay *h, const int64_t *idx, const void *
   if (rc) return rc;
   h->cnt += n;
   return RTH_OK;
+}
+
+int rth_replay_update_priorities_deferred(rth_replay *h, const int64_t *idx, const void *td_abs, int32_t td_dtype,
+                                          int64_t n, int32_t step, void *stream) {
+  RTH_REQUIRE(h && n >= 0 && (n == 0 || (idx && td_abs)), "rth_replay_update_priorities_deferred: bad arguments");
+  if (h->kind != RTH_SAMPLER_PER) return rth_replay_update_priorities(h, idx, td_abs, td_dtype, n, step, stream);
+  RTH_REQUIRE(n == 0 || td_dtype == RTH_F32 || td_dtype == RTH_F64 || td_dtype == RTH_PRIO_RAW,
+              "rth_replay_update_priorities_deferred: priority dtype must be f32, f64 or raw f64");
+  int rc = flush_pending(h, as_stream(stream));  // at most one update in flight
+  if (rc) return rc;
+  h->pend = UpdPending{idx, td_abs, td_dtype, step ? 1 : 0, n};
+  h->has_pend = 1;
+  if (step) h->sched_steps++;
+  h->cnt += n;
+  return RTH_OK;
+}
+
+int rth_replay_flush(rth_replay *h, void *stream) {
+  RTH_REQUIRE(h, "rth_replay_flush: NULL handle");
+  return flush_pending(h, as_stream(stream));
 }
 
 int rth_uniform_indices(int64_t size, int64_t batch, const double *uniforms, uint64_t seed, uint64_t counter,

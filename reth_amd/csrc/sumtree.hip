@@ -167,14 +167,35 @@ struct UpdArgs {
   int32_t td_dtype;      // ... in float32 (RTH_F32) or float64 (RTH_F64), like numpy
   double alpha;
   int64_t n;
-  const ReplayState *st;  // nullable: a replay shard's device state supplies the FIFO start
+  ReplayState *st;        // nullable: a replay shard's device state supplies the FIFO start
   rth_schedule alpha_s;   // and alpha = alpha_s(st->sched_step)
+  // a deferred update_priorities merged into this launch, applied before the n keys above
+  const int64_t *pidx;
+  const void *ptd;
+  int32_t pdtype;
+  int32_t pre_step;   // st->sched_step += 1 before alpha is read (its step=True on_step)
+  int64_t pn;
+  int32_t post_tail;  // st->tail += n after every read of it (the append's FIFO advance)
 };
 
-__device__ __forceinline__ double priority_of(const UpdArgs &a, double alpha, int64_t src) {
-  if (a.w64) return a.w64[src];
-  if (a.td_dtype == RTH_F64) return per_normalize64(static_cast<const double *>(a.td_abs)[src], alpha);
-  return (double)per_normalize(static_cast<const float *>(a.td_abs)[src], (float)alpha);
+__device__ __forceinline__ double prio_value(const void *td, int32_t dt, double alpha, int64_t i) {
+  if (dt == RTH_PRIO_RAW) return static_cast<const double *>(td)[i];
+  if (dt == RTH_F64) return per_normalize64(static_cast<const double *>(td)[i], alpha);
+  return (double)per_normalize(static_cast<const float *>(td)[i], (float)alpha);
+}
+
+// key g of the launch: the deferred update's g-th index, then the main segment's
+__device__ __forceinline__ int64_t upd_id(const UpdArgs &a, int64_t g, int64_t fifo_start) {
+  if (g < a.pn) return a.pidx[g];
+  g -= a.pn;
+  return a.idx ? a.idx[g] : (fifo_start + g) % a.cap;
+}
+
+__device__ __forceinline__ double priority_of(const UpdArgs &a, double alpha, int64_t g) {
+  if (g < a.pn) return prio_value(a.ptd, a.pdtype, alpha, g);
+  g -= a.pn;
+  if (a.w64) return a.w64[g];
+  return prio_value(a.td_abs, a.td_dtype, alpha, g);
 }
 
 __device__ __forceinline__ int64_t key_index(uint64_t key, int maxd) {
@@ -187,17 +208,20 @@ __global__ __launch_bounds__(kUpdThreads) void k_tree_update(UpdArgs a) {
   __shared__ uint64_t keys[kUpdChunk];
   const int tid = threadIdx.x;
   const int maxd = a.maxd;
+  if (a.pre_step && tid == 0) a.st->sched_step += 1;
+  __syncthreads();
   const int64_t fifo_start = a.st ? a.st->tail : a.fifo_start;
   const double alpha = a.st ? sched_value(a.alpha_s, a.st->sched_step) : a.alpha;
-  for (int64_t cs = 0; cs < a.n; cs += kUpdChunk) {
-    const int m = (int)min<int64_t>(kUpdChunk, a.n - cs);
+  const int64_t N = a.pn + a.n;
+  for (int64_t cs = 0; cs < N; cs += kUpdChunk) {
+    const int m = (int)min<int64_t>(kUpdChunk, N - cs);
     // Warm every 64-byte line the level loop below will touch (for each node on a key's
     // path: the line holding its children pair), all loads independent, so the ~20
     // dependent levels then hit L2 instead of paying an HBM miss (and TLB walk) each.
     {
       uint64_t acc = 0;
       for (int j = tid; j < m; j += kUpdThreads) {
-        int64_t x = a.idx ? a.idx[cs + j] : (fifo_start + cs + j) % a.cap;
+        int64_t x = upd_id(a, cs + j, fifo_start);
         if (x < 0 || x >= a.cap) continue;
         while (x >= 0) {
           double v[8];
@@ -221,7 +245,7 @@ __global__ __launch_bounds__(kUpdThreads) void k_tree_update(UpdArgs a) {
     for (int j = tid; j < P; j += kUpdThreads) {
       uint64_t key = ~0ull;
       if (j < m) {
-        const int64_t id = a.idx ? a.idx[cs + j] : (fifo_start + cs + j) % a.cap;
+        const int64_t id = upd_id(a, cs + j, fifo_start);
         if (id >= 0 && id < a.cap) {
           const int d = node_depth(id);
           const uint64_t aligned = (uint64_t)(id + 1) << (maxd - d);
@@ -279,6 +303,7 @@ __global__ __launch_bounds__(kUpdThreads) void k_tree_update(UpdArgs a) {
       __syncthreads();
     }
   }
+  if (a.post_tail && tid == 0) a.st->tail = (fifo_start + a.n) % a.cap;  // all reads of tail are done
 }
 
 // ------------------------------------------------------------------ find / sample
@@ -357,12 +382,26 @@ struct rth_sumtree {
 namespace rth {
 int tree_update_impl(rth_sumtree *t, const int64_t *idx, int64_t fifo_start, const double *w64,
                      const void *td_abs, int32_t td_dtype, double alpha, int64_t n, hipStream_t s,
-                     const ReplayState *st, const rth_schedule *alpha_s) {
-  if (n <= 0) return RTH_OK;
-  if (!w64 && td_dtype == RTH_PRIO_RAW) w64 = static_cast<const double *>(td_abs);  // stored as given
-  RTH_REQUIRE(w64 || td_dtype == RTH_F32 || td_dtype == RTH_F64, "priority dtype must be f32, f64 or raw f64");
-  UpdArgs a{t->nodes, t->cap, t->maxd, idx, fifo_start, w64, td_abs, td_dtype, alpha, n, st,
+                     ReplayState *st, const rth_schedule *alpha_s, const UpdPending *pend, int post_tail) {
+  const bool has_pend = pend && (pend->n > 0 || pend->step);
+  if (n <= 0 && !has_pend && !post_tail) return RTH_OK;
+  if (n > 0 && !w64 && td_dtype == RTH_PRIO_RAW) w64 = static_cast<const double *>(td_abs);  // stored as given
+  RTH_REQUIRE(n <= 0 || w64 || td_dtype == RTH_F32 || td_dtype == RTH_F64,
+              "priority dtype must be f32, f64 or raw f64");
+  RTH_REQUIRE(!(has_pend || post_tail) || st, "deferred updates and FIFO bumps need a replay state");
+  UpdArgs a{t->nodes, t->cap, t->maxd, idx, fifo_start, w64, td_abs, td_dtype, alpha, n > 0 ? n : 0, st,
             alpha_s ? *alpha_s : rth_schedule{}};
+  if (has_pend) {
+    RTH_REQUIRE(pend->n <= 0 || (pend->idx && pend->td && (pend->dtype == RTH_F32 || pend->dtype == RTH_F64 ||
+                                                          pend->dtype == RTH_PRIO_RAW)),
+                "deferred update: bad arguments");
+    a.pidx = pend->idx;
+    a.ptd = pend->td;
+    a.pdtype = pend->dtype;
+    a.pn = pend->n > 0 ? pend->n : 0;
+    a.pre_step = pend->step ? 1 : 0;
+  }
+  a.post_tail = post_tail;
   hipLaunchKernelGGL(k_tree_update, dim3(1), dim3(kUpdThreads), 0, s, a);
   RTH_LAUNCHED();
   return RTH_OK;
@@ -417,7 +456,7 @@ int rth_sumtree_clear(rth_sumtree *t, void *stream) {
 
 int rth_sumtree_update(rth_sumtree *t, const int64_t *idx, const double *w, int64_t n, void *stream) {
   RTH_REQUIRE(t && (n == 0 || (idx && w)), "rth_sumtree_update: bad arguments");
-  return tree_update_impl(t, idx, 0, w, nullptr, RTH_F64, 0.0, n, as_stream(stream), nullptr, nullptr);
+  return tree_update_impl(t, idx, 0, w, nullptr, RTH_F64, 0.0, n, as_stream(stream), nullptr, nullptr, nullptr, 0);
 }
 
 int rth_sumtree_find(rth_sumtree *t, const double *tg, int64_t n, int64_t *idx_out, double *val_out,
@@ -476,7 +515,8 @@ int rth_per_normalize(const float *w, int64_t n, float alpha, float *out, void *
 int rth_per_update(rth_sumtree *t, const int64_t *idx, const void *td_abs, int32_t td_dtype, int64_t n,
                    double alpha, void *stream) {
   RTH_REQUIRE(t && (n == 0 || (idx && td_abs)), "rth_per_update: bad arguments");
-  return tree_update_impl(t, idx, 0, nullptr, td_abs, td_dtype, alpha, n, as_stream(stream), nullptr, nullptr);
+  return tree_update_impl(t, idx, 0, nullptr, td_abs, td_dtype, alpha, n, as_stream(stream), nullptr, nullptr,
+                          nullptr, 0);
 }
 
 int rth_per_sample(rth_sumtree *t, int64_t batch, double beta, const double *uniforms, uint64_t seed,

@@ -232,7 +232,20 @@ class HbmReplay:
                  int(seed), ctypes.byref(h))
         self._h = h.value
         th = _lib.lib().rth_replay_tree(self._h)
-        self.tree = SumTree(self.capacity, self.device, _handle=th) if th else None
+        self._tree = SumTree(self.capacity, self.device, _handle=th) if th else None
+        self._pending = None  # buffers of a deferred priority update (kept alive until applied)
+
+    @property
+    def tree(self):
+        """the shard's sum-tree (a deferred priority update is applied first)"""
+        self.flush()
+        return self._tree
+
+    def flush(self):
+        """apply a deferred update_priorities now (rth_replay_flush)"""
+        if self._pending is not None:
+            call("rth_replay_flush", self._h, stream_ptr())
+            self._pending = None
 
     def __del__(self):
         if getattr(self, "_h", None):
@@ -306,6 +319,7 @@ class HbmReplay:
             stride = 0 if row_strides is None else int(row_strides[c])
             srcs[c] = Src(ptr(t), ptr(rows), stride, src_dtype, 0)
         call("rth_replay_append", self._h, srcs, ptr(w), wt, n, ptr(idx_out), stream_ptr())
+        self._pending = None  # a deferred update was merged into this launch
         return n
 
     def append_strided(self, cols, td_abs, row_strides, raw=False):
@@ -323,6 +337,7 @@ class HbmReplay:
                 raise TypeError(f"column {c}: {bc.dtype} rows into {col.dtype} storage")
             srcs[c] = Src(ptr(bc.view), None, int(row_strides[c]), _TORCH_TO_RTH[bc.dtype], 0)
         call("rth_replay_append", self._h, srcs, ptr(w), wt, n, None, stream_ptr())
+        self._pending = None
         return n
 
     def sample_into(self, batch_size, out_cols, idx_out, isw_out, uniforms=None, gather_timer=None):
@@ -333,9 +348,11 @@ class HbmReplay:
         arr = (c_vp * len(out_cols))(*[ptr(t) for t in out_cols])
         if gather_timer is None:
             call("rth_replay_sample", self._h, batch_size, ptr(u), arr, ptr(idx_out), ptr(isw_out), stream_ptr())
+            self._pending = None  # the sample applied a deferred update first
             return
         s = stream_ptr()
         call("rth_replay_sample", self._h, batch_size, ptr(u), None, ptr(idx_out), ptr(isw_out), s)
+        self._pending = None
         ev0, ev1 = gather_timer()
         ev0.record()
         call("rth_replay_gather", self._h, ptr(idx_out), batch_size, arr, s)
@@ -360,17 +377,20 @@ class HbmReplay:
         call("rth_replay_gather", self._h, ptr(idx), idx.numel(), arr, stream_ptr())
         return out_cols
 
-    def update_priorities(self, indices, td_abs, step=False, raw=False):
+    def update_priorities(self, indices, td_abs, step=False, raw=False, deferred=False):
         """Client.update_priorities -> sampler_loop: on_step() first when step (:32-35).
-        The device owns the schedules; the host Schedules mirror them for inspection."""
+        The device owns the schedules; the host Schedules mirror them for inspection.
+        deferred: applied by the next tree launch (merged into the next append's), in the
+        same order the reference's sampler applies its messages."""
         if step:
             self.alpha.step()
             self.beta.step()
         idx = as_device(indices, torch.int64, self.device)
         w, wt = _prio_tensor(td_abs, self.device, raw)
         assert idx.numel() == w.numel()  # client.py:38
-        call("rth_replay_update_priorities", self._h, ptr(idx), ptr(w), wt, idx.numel(), int(bool(step)),
-             stream_ptr())
+        fn = "rth_replay_update_priorities_deferred" if deferred else "rth_replay_update_priorities"
+        call(fn, self._h, ptr(idx), ptr(w), wt, idx.numel(), int(bool(step)), stream_ptr())
+        self._pending = (idx, w) if deferred and self.sampler == "per" else None
 
 
 def sched_struct(s):

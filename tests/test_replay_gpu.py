@@ -211,3 +211,36 @@ def test_torch_cuda_loader_sample_ahead_order(dev, orc):
         client.update_priorities(idx, new)  # step=True: beta.step() then update
         beta_steps += 1
         tree.update(idx, orc.per_normalize(new, 0.5).astype(np.float64))
+
+
+def test_deferred_update_merged_into_append(dev, orc):
+    """a deferred update_priorities is applied by the next append's tree launch (before the
+    append's rows), or before a sample / flush: the tree equals the immediate schedule's"""
+    from reth_amd.replay import Column, HbmReplay
+
+    rng = np.random.default_rng(5)
+    cap = 700
+
+    def run(deferred):
+        rep = HbmReplay(cap, [Column((), torch.int64)], alpha=0.6, beta="0.4,1,100", device=dev, seed=3)
+        out = []
+        for step in range(12):
+            n = ns[step]
+            rep.append([torch.arange(n, device=dev)], torch.as_tensor(tds[step], device=dev))
+            if step % 3 == 2:
+                _, idx, isw = rep.sample(64)
+                out += [idx.cpu(), isw.cpu()]
+            rep.update_priorities(torch.as_tensor(upd_idx[step], device=dev),
+                                  torch.as_tensor(upd_w[step], device=dev), step=True, deferred=deferred)
+        s, m, v = rep.tree.export()  # applies a pending update
+        return out + [s.cpu(), m.cpu(), v.cpu()], rep.info()
+
+    ns = [int(x) for x in rng.integers(1, 120, 12)]
+    tds = [rng.random(n).astype(np.float32) for n in ns]
+    upd_idx = [rng.integers(0, min(cap, sum(ns[:k + 1])), 50) for k in range(12)]
+    upd_w = [rng.random(50).astype(np.float32) for _ in range(12)]
+    a, ia = run(False)
+    b, ib = run(True)
+    assert ia == ib
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)

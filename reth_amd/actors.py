@@ -50,8 +50,8 @@ class VecActors:
         self.seed = int(seed)
         self.p_reward, self.p_done = float(p_reward), float(p_done)
         ring = 4
-        while ring < 2 * (self.n_step + 2):  # live stacks span n_step + 2 env steps, 2 per step
-            ring *= 2
+        while ring < 2 * (self.n_step + 3):  # live stacks span n_step + 2 env steps (+1 when the
+            ring *= 2                         # rows are prioritised a step late), 2 per step
         self.ring = ring
         dev = self.device
         N = self.N
@@ -70,6 +70,11 @@ class VecActors:
         self.row_s0, self.row_a, self.row_s1 = z(torch.int64), z(torch.int64), z(torch.int64)
         self.row_r, self.row_done = z(torch.float32), z(torch.float32)
         self.row_handles = torch.empty(2 * N, dtype=torch.int64, device=dev)
+        # step_fused: rows alternate between two sets by push parity (the rows of step t are
+        # prioritised and appended at step t + 1, while step t + 1 emits into the other set)
+        self._sets = [self._rowset_of_attrs(), RowSet(N, dev)]
+        self.handles3 = torch.empty(3 * N, dtype=torch.int64, device=dev)
+        self.obs3 = torch.empty((3 * N, *OBS_SHAPE), dtype=torch.float32, device=dev, memory_format=fmt)
         h = _lib.c_vp()
         call("rth_nstep_create", N, self.n_step, self.gamma, int(nstep_mode), dev.index, _lib.ctypes.byref(h))
         self._nstep = h.value
@@ -122,6 +127,46 @@ class VecActors:
         self.pushes += 1
         return self.warm
 
+    def _rowset_of_attrs(self):
+        rs = RowSet.__new__(RowSet)
+        rs.s0, rs.a, rs.r, rs.s1, rs.done = self.row_s0, self.row_a, self.row_r, self.row_s1, self.row_done
+        return rs
+
+    def _bind_rows(self, rs):
+        self.row_s0, self.row_a, self.row_r, self.row_s1, self.row_done = rs.s0, rs.a, rs.r, rs.s1, rs.done
+
+    @torch.no_grad()
+    def step_fused(self, q_net):
+        """one environment step for every actor with the previous step's rows prioritised in
+        the same forward pass: Q-net over [acting stacks; prev rows' s0; prev rows' s1]
+        (3N) -> rth_eps_greedy on the first N -> rth_td_huber (calc_loss, target == online)
+        on the rest -> env step -> n-step push into the other row set.  The reference's
+        actor runs calc_loss on a 64-row batch well after the rows were emitted
+        (test/apex-dqn/worker.py:55-60); here the delay is one step.
+        Returns (|td|, RowSet) of the previous step's rows, or (None, None) before any."""
+        s = stream_ptr()
+        p = self.pushes
+        prev, cur = self._sets[(p - 1) % 2], self._sets[p % 2]
+        self.t += 1
+        call("rth_counter_add", ptr(self.t_dev), 1, s)
+        N = self.N
+        torch.cat([self.current_obs_handles(), prev.s0, prev.s1], out=self.handles3)
+        self.gather_f32(self.handles3, self.obs3)
+        q, dueling = _q_forward(q_net, self.obs3)
+        call("rth_eps_greedy", ptr(q), N, self.A, dueling, ptr(self.eps), None, None, self.seed, 0,
+             ptr(self.t_dev), ptr(self.action), s)
+        q1 = q[2 * N:]
+        _, td_abs, _ = td_huber_forward(q[N:2 * N], q1, q1, prev.a, prev.r, prev.done, None, self.gamma_n, True,
+                                        want_dq=False, dueling=bool(dueling))
+        call("rth_synth_env_step", ptr(self.frames), N, self.ring, 0, ptr(self.t_dev), ptr(self.cur_slot),
+             ptr(self.action), self.seed, self.p_reward, self.p_done, ptr(self.reward), ptr(self.done), ptr(self.s0_h),
+             ptr(self.s1_h), s)
+        call("rth_nstep_push", self._nstep, ptr(self.s0_h), ptr(self.action), ptr(self.reward), ptr(self.s1_h),
+             ptr(self.done), ptr(self.emit), ptr(cur.s0), ptr(cur.a), ptr(cur.r), ptr(cur.s1), ptr(cur.done), s)
+        self.pushes += 1
+        self._bind_rows(cur)
+        return (td_abs, prev) if p > self.n_step else (None, None)
+
     @torch.no_grad()
     def prioritise(self, q_net):
         """calc_loss on the emitted rows with the actor's network (target == online)"""
@@ -133,16 +178,26 @@ class VecActors:
                                         True, want_dq=False, dueling=bool(dueling))
         return td_abs
 
-    def append(self, replay, td_abs):
-        """Client.append of the emitted rows (stacks copied from the ring into FIFO slots)"""
+    def append(self, replay, td_abs, rows=None):
+        """Client.append of emitted rows (default: the latest; stacks copied from the ring
+        into FIFO slots)"""
+        rs = self._rowset_of_attrs() if rows is None else rows
         fr = self.frames
-        replay.append([fr, self.row_a, self.row_r, fr, self.row_done], td_abs,
-                      src_rows=[self.row_s0, None, None, self.row_s1, None])
+        replay.append([fr, rs.a, rs.r, fr, rs.done], td_abs, src_rows=[rs.s0, None, None, rs.s1, None])
 
     def rows(self):
         """emitted rows as (s0 u8, a, r, s1 u8, done) device tensors (tests / inspection)"""
         return (self.frames[self.row_s0], self.row_a.clone(), self.row_r.clone(), self.frames[self.row_s1],
                 self.row_done.clone())
+
+
+class RowSet:
+    """one set of emitted n-step rows: s0/s1 stack handles, a, r, done"""
+
+    def __init__(self, n, dev):
+        z = lambda dt: torch.zeros(n, dtype=dt, device=dev)
+        self.s0, self.a, self.s1 = z(torch.int64), z(torch.int64), z(torch.int64)
+        self.r, self.done = z(torch.float32), z(torch.float32)
 
 
 def _q_forward(q_net, x):

@@ -66,6 +66,7 @@ class ApexConfig:
     channels_last: bool = True     # NHWC end to end (gather writes it, MIOpen consumes it)
     conv_benchmark: bool = False   # torch.backends.cudnn.benchmark (MIOpen find)
     hip_graph: bool = False        # replay captured HIP graphs of the compute blocks
+    fused_actor: bool = True       # act + previous rows' priorities in one 3N forward (VecActors.step_fused)
     dp_hook: Optional[bool] = None  # gradient all-reduce hook: None = when world > 1 (tests force it)
     extra: dict = field(default_factory=dict)
 
@@ -137,10 +138,13 @@ class ApexDQN:
 
     # ------------------------------------------------------------------ the blocks
     def _actor_compute(self):
-        """act + env + n-step (+ priorities once rows flow); returns |td| of the rows or None"""
+        """act + env + n-step (+ priorities once rows flow); returns (|td|, rows) of the rows
+        to append (the previous step's with fused_actor, this step's otherwise) or (None, None)"""
+        if self.cfg.fused_actor:
+            return self.actors.step_fused(self.actor_net)
         if self.actors.step(self.actor_net):
-            return self.actors.prioritise(self.actor_net)
-        return None
+            return self.actors.prioritise(self.actor_net), None
+        return None, None
 
     def _learner_train(self, slot):
         data, idx, isw = slot
@@ -176,9 +180,9 @@ class ApexDQN:
             return self._iteration_graph()
         for _ in range(self.cfg.actor_steps_per_update):
             self._actor_host()
-            td = self._actor_compute()
+            td, rows = self._actor_compute()
             if td is not None:
-                self.actors.append(self.replay, td)
+                self.actors.append(self.replay, td, rows)
             self.env_steps += self.actors.N
         if not self.svc.ready():
             return
@@ -207,10 +211,19 @@ class ApexDQN:
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
         split = solver.grad_hook is not None
-        G = dict(act=torch.cuda.CUDAGraph(), learn=[], learn_td=[], apply=[], grads=[])
+        G = dict(act=[], act_out=[], learn=[], learn_td=[], apply=[], grads=[])
         with torch.cuda.stream(side):
-            with torch.cuda.graph(G["act"], stream=side):
-                G["act_td"] = self._actor_compute()
+            # the actor block by push parity (fused_actor alternates row sets; both graphs
+            # are identical otherwise)
+            for _ in range(2):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=side):
+                    out = self._actor_compute()
+                G["act"].append(g)
+                G["act_out"].append(out)
+            if host[1] % 2:  # keep G["act"][k] <-> pushes % 2 == k
+                G["act"].reverse()
+                G["act_out"].reverse()
             for p in range(2):
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, stream=side):
@@ -233,13 +246,21 @@ class ApexDQN:
 
     def _iteration_graph(self):
         G = self._graphs
+        act = self.actors
         for _ in range(self.cfg.actor_steps_per_update):
             self._actor_host()
-            G["act"].replay()
-            self.actors.t += 1
-            self.actors.pushes += 1
-            self.actors.append(self.replay, G["act_td"])
-            self.env_steps += self.actors.N
+            k = act.pushes % 2
+            G["act"][k].replay()
+            act.t += 1
+            act.pushes += 1
+            td, rows = G["act_out"][k]
+            if self.cfg.fused_actor:
+                act._bind_rows(act._sets[k])  # this step's rows (appended next step)
+                if act.pushes - 1 > act.n_step:  # the previous step emitted rows
+                    act.append(self.replay, td, rows)
+            else:
+                act.append(self.replay, td)
+            self.env_steps += act.N
         k = self.loader._pending.pop(0)
         G["learn"][k].replay()
         if G["apply"]:

@@ -172,3 +172,29 @@ def test_vec_actors_rows_follow_nstep_semantics(dev, orc):
             want = orc.td_error(q0.cpu().numpy(), q1.cpu().numpy(), q1.cpu().numpy(), got[1], got[2], got[4],
                                 np.float32(0.99 ** 3))
             np.testing.assert_allclose(td.cpu().numpy(), np.abs(want), rtol=1e-5, atol=1e-5)
+
+
+def test_step_fused_matches_step_then_prioritise(dev):
+    """the fused actor step (act + the previous rows' calc_loss in one 3N forward) emits the
+    same rows and the same |td| (one step later) as step() + prioritise()"""
+    from reth_amd.actors import VecActors
+    from reth_amd.model import DQNNetwork
+
+    torch.manual_seed(0)
+    N = 24
+    net = DQNNetwork((4, 84, 84), 6).to(dev, memory_format=torch.channels_last)
+    net.hwc_features = True
+    kw = dict(n_step=3, gamma=0.99, device=dev, seed=9, p_reward=0.3, p_done=0.1, channels_last=True)
+    a, b = VecActors(N, 6, **kw), VecActors(N, 6, **kw)
+    want = []
+    for t in range(10):
+        if a.step(net):
+            want.append((a.row_s0.clone(), a.row_a.clone(), a.row_r.clone(), a.row_done.clone(), a.prioritise(net)))
+        td, rows = b.step_fused(net)
+        assert torch.equal(a.action, b.action)
+        assert torch.equal(a.frames[a.current_obs_handles()], b.frames[b.current_obs_handles()])
+        if td is not None:
+            s0, ra, rr, rd, wtd = want[-2]
+            assert torch.equal(rows.s0, s0) and torch.equal(rows.a, ra) and torch.equal(rows.r, rr)
+            assert torch.equal(rows.done, rd)
+            torch.testing.assert_close(td, wtd, rtol=1e-5, atol=1e-5)  # batch 3N vs 2N GEMM blocking

@@ -7,26 +7,30 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def test_apex_small_end_to_end(dev):
+@pytest.mark.parametrize("fused", [True, False])
+def test_apex_small_end_to_end(dev, fused):
     from reth_amd.apex import ApexConfig, ApexDQN
 
     cfg = ApexConfig(n_actors=16, capacity=4096, batch_size=32, sample_start=64, send_weights_interval=5,
-                     recv_weights_interval=8, update_target_interval=10, p_done=0.05, seed=1)
+                     recv_weights_interval=8, update_target_interval=10, p_done=0.05, seed=1, fused_actor=fused)
     ax = ApexDQN(cfg, device=dev)
     for _ in range(60):
         ax.iteration()
     torch.cuda.synchronize()
     size, tail, cnt, calls, steps = ax.replay.info()
     assert steps == ax.updates and calls == ax.updates + 1  # one batch sampled ahead
-    assert size == 16 * (60 - cfg.n_step) and ax.env_steps == 16 * 60
+    lag = 1 if fused else 0  # fused: a step's rows are prioritised and appended one step later
+    assert size == 16 * (60 - cfg.n_step - lag) and ax.env_steps == 16 * 60
     assert ax.updates > 40 and ax.slot.version == ax.updates // 5
     assert ax.subscriber.loaded_version > 0
     assert all(torch.isfinite(p).all() for p in ax.solver.q_network.parameters())
-    # the replay's a/r/done columns hold what the actors emitted last
+    # the replay's last rows are what the actors emitted (the previous step's, when fused)
+    act = ax.actors
+    rows = act._sets[(act.pushes - 2) % 2] if fused else act._rowset_of_attrs()
     out = ax.replay.gather(torch.arange(tail - 16, tail, device=dev))
-    assert torch.equal(out[1], ax.actors.row_a) and torch.equal(out[2], ax.actors.row_r)
-    assert torch.equal(out[0], ax.actors.frames[ax.actors.row_s0].float())
-    assert torch.equal(out[3], ax.actors.frames[ax.actors.row_s1].float())
+    assert torch.equal(out[1], rows.a) and torch.equal(out[2], rows.r)
+    assert torch.equal(out[0], act.frames[rows.s0].float())
+    assert torch.equal(out[3], act.frames[rows.s1].float())
     ax.close()
 
 

@@ -105,6 +105,7 @@ SIGNATURES = {
     "rth_atari_destroy": (c_i32, [c_vp]),
     "rth_atari_step": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "rth_clip_adam_workspace": (c_i64, []),
+    "rth_debug_tree_timing": (c_i32, [c_vp]),
     "rth_clip_adam": (c_i32, [c_vp, c_i32, c_f64, c_f64, c_f64, c_f64, c_f64, c_vp, c_vp, c_vp, c_vp]),
 }
 

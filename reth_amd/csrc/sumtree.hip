@@ -204,10 +204,23 @@ __device__ __forceinline__ int64_t key_index(uint64_t key, int maxd) {
   return (int64_t)(aligned >> (maxd - d)) - 1;
 }
 
+// phase timestamps of the last k_tree_update (wall clock ticks; development aid, read by
+// rth_debug_tree_timing)
+__device__ long long g_upd_clock[8];
+
+// a workgroup barrier that orders LDS only (global stores are not waited for)
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 __global__ __launch_bounds__(kUpdThreads) void k_tree_update(UpdArgs a) {
   __shared__ uint64_t keys[kUpdChunk];
+  __shared__ double res_sum[kUpdChunk], res_min[kUpdChunk];  // an owner's (sum, min) per level
   const int tid = threadIdx.x;
   const int maxd = a.maxd;
+  if (tid == 0) g_upd_clock[0] = wall_clock64();
   if (a.pre_step && tid == 0) a.st->sched_step += 1;
   __syncthreads();
   const int64_t fifo_start = a.st ? a.st->tail : a.fifo_start;
@@ -215,10 +228,60 @@ __global__ __launch_bounds__(kUpdThreads) void k_tree_update(UpdArgs a) {
   const int64_t N = a.pn + a.n;
   for (int64_t cs = 0; cs < N; cs += kUpdChunk) {
     const int m = (int)min<int64_t>(kUpdChunk, N - cs);
-    // Warm every 64-byte line the level loop below will touch (for each node on a key's
-    // path: the line holding its children pair), all loads independent, so the ~20
-    // dependent levels then hit L2 instead of paying an HBM miss (and TLB walk) each.
-    {
+    int P = 2;
+    while (P < m) P <<= 1;
+    if (P <= kUpdThreads) {
+      // One key per lane.  Issue the loads that warm the lines the level loop will touch
+      // (the children-pair line of the deepest kPre nodes on the key's path; the top of the
+      // tree is hot anyway) and keep them in flight through the sort, which synchronises on
+      // LDS only; consume them afterwards.
+      constexpr int kPre = 16;
+      double pre[kPre];
+      const int64_t id = tid < m ? upd_id(a, cs + tid, fifo_start) : -1;
+      {
+        int64_t x = (id >= 0 && id < a.cap) ? id : -1;
+#pragma unroll
+        for (int u = 0; u < kPre; ++u) {
+          pre[u] = 0.0;
+          if (x >= 0) {
+            const int64_t c = 2 * x + 1;
+            pre[u] = a.nd[(c < a.cap ? c : x) + 1].sum;
+            x = x ? (x - 1) / 2 : -1;
+          }
+        }
+      }
+      if (tid == 0) g_upd_clock[1] = wall_clock64();
+      uint64_t key = ~0ull;
+      if (id >= 0 && id < a.cap) {
+        const int d = node_depth(id);
+        const uint64_t aligned = (uint64_t)(id + 1) << (maxd - d);
+        key = (((aligned << kDepthBits) | (uint64_t)d) << kPosBits) | (uint64_t)tid;
+      }
+      // bitonic sort of the workgroup's 1024 lanes (sentinels sort last): partners within a
+      // wave exchange through cross-lane shuffles, wider strides through LDS
+      for (int k = 2; k <= kUpdThreads; k <<= 1) {
+        for (int jj = k >> 1; jj > 0; jj >>= 1) {
+          uint64_t y;
+          if (jj < 64) {
+            y = __shfl_xor(key, jj, 64);
+          } else {
+            keys[tid] = key;
+            lds_barrier();
+            y = keys[tid ^ jj];
+            lds_barrier();
+          }
+          const bool up = (tid & k) == 0, lower = (tid & jj) == 0;
+          key = (lower == up) ? (key < y ? key : y) : (key < y ? y : key);
+        }
+      }
+      keys[tid] = key;
+      uint64_t acc = 0;
+#pragma unroll
+      for (int u = 0; u < kPre; ++u) acc ^= (uint64_t)__double_as_longlong(pre[u]);
+      if (acc == 0x9E3779B97F4A7C15ull) a.nd[0].pad = 1.0;  // record 0 is padding; keeps the loads
+      lds_barrier();
+    } else {
+      // several keys per lane: warm the lines first, then an LDS bitonic sort
       uint64_t acc = 0;
       for (int j = tid; j < m; j += kUpdThreads) {
         int64_t x = upd_id(a, cs + j, fifo_start);
@@ -238,40 +301,39 @@ __global__ __launch_bounds__(kUpdThreads) void k_tree_update(UpdArgs a) {
           for (int u = 0; u < 8; ++u) acc ^= (uint64_t)__double_as_longlong(v[u]);
         }
       }
-      if (acc == 0x9E3779B97F4A7C15ull) a.nd[0].pad = 1.0;  // record 0 is padding; keeps the loads
-    }
-    int P = 2;
-    while (P < m) P <<= 1;
-    for (int j = tid; j < P; j += kUpdThreads) {
-      uint64_t key = ~0ull;
-      if (j < m) {
-        const int64_t id = upd_id(a, cs + j, fifo_start);
-        if (id >= 0 && id < a.cap) {
-          const int d = node_depth(id);
-          const uint64_t aligned = (uint64_t)(id + 1) << (maxd - d);
-          key = (((aligned << kDepthBits) | (uint64_t)d) << kPosBits) | (uint64_t)j;
-        }
-      }
-      keys[j] = key;
-    }
-    __syncthreads();
-    // bitonic sort, ascending
-    for (int k = 2; k <= P; k <<= 1) {
-      for (int jj = k >> 1; jj > 0; jj >>= 1) {
-        for (int i = tid; i < P; i += kUpdThreads) {
-          const int ixj = i ^ jj;
-          if (ixj > i) {
-            const uint64_t x = keys[i], y = keys[ixj];
-            const bool up = (i & k) == 0;
-            if ((x > y) == up) {
-              keys[i] = y;
-              keys[ixj] = x;
-            }
+      if (acc == 0x9E3779B97F4A7C15ull) a.nd[0].pad = 1.0;
+      if (tid == 0) g_upd_clock[1] = wall_clock64();
+      for (int j = tid; j < P; j += kUpdThreads) {
+        uint64_t key = ~0ull;
+        if (j < m) {
+          const int64_t id = upd_id(a, cs + j, fifo_start);
+          if (id >= 0 && id < a.cap) {
+            const int d = node_depth(id);
+            const uint64_t aligned = (uint64_t)(id + 1) << (maxd - d);
+            key = (((aligned << kDepthBits) | (uint64_t)d) << kPosBits) | (uint64_t)j;
           }
         }
-        __syncthreads();
+        keys[j] = key;
+      }
+      __syncthreads();
+      for (int k = 2; k <= P; k <<= 1) {  // bitonic sort, ascending
+        for (int jj = k >> 1; jj > 0; jj >>= 1) {
+          for (int i = tid; i < P; i += kUpdThreads) {
+            const int ixj = i ^ jj;
+            if (ixj > i) {
+              const uint64_t x = keys[i], y = keys[ixj];
+              const bool up = (i & k) == 0;
+              if ((x > y) == up) {
+                keys[i] = y;
+                keys[ixj] = x;
+              }
+            }
+          }
+          lds_barrier();
+        }
       }
     }
+    if (tid == 0) g_upd_clock[2] = wall_clock64();
     // last writer of every index sets val (duplicates sort by position)
     for (int j = tid; j < m; j += kUpdThreads) {
       const uint64_t key = keys[j];
@@ -284,7 +346,13 @@ __global__ __launch_bounds__(kUpdThreads) void k_tree_update(UpdArgs a) {
       }
     }
     __syncthreads();
-    // touched ancestors, deepest level first; first key of each ancestor run maintains it
+    if (tid == 0) g_upd_clock[3] = wall_clock64();
+    // Touched ancestors, deepest level first; the first key of each ancestor's run maintains
+    // it (_numba_maintain_node).  A touched child's (sum, min) comes from LDS -- its owner
+    // at the level below stored it in res[owner] -- found by binary search in the sorted
+    // keys (the child's subtree is a key range); only untouched children and the node's own
+    // val are read from memory (issued before the search), so a level costs one overlapped
+    // L2 round trip and an LDS-only barrier instead of store -> barrier -> load.
     for (int L = maxd; L >= 0; --L) {
       for (int j = tid; j < m; j += kUpdThreads) {
         const uint64_t key = keys[j];
@@ -292,16 +360,73 @@ __global__ __launch_bounds__(kUpdThreads) void k_tree_update(UpdArgs a) {
         const int d = (int)((key >> kPosBits) & ((1u << kDepthBits) - 1));
         if (d < L) continue;
         const uint64_t aligned = key >> (kPosBits + kDepthBits);
-        const uint64_t anc = aligned >> (maxd - L);
+        const uint64_t anc = aligned >> (maxd - L);  // 1-based heap index
         if (j > 0) {
           const uint64_t pk = keys[j - 1];
           const int pd = (int)((pk >> kPosBits) & ((1u << kDepthBits) - 1));
           if (pd >= L && ((pk >> (kPosBits + kDepthBits)) >> (maxd - L)) == anc) continue;
         }
-        maintain_node(a.nd, a.cap, (int64_t)anc - 1);
+        const int64_t node = (int64_t)anc - 1, l = 2 * node + 1, r = l + 1;
+        const double v = a.nd[node + 1].val;
+        double ls = 0.0, lm = 0.0, rs = 0.0, rm = 0.0;
+        if (l < a.cap) {
+          ls = a.nd[l + 1].sum;
+          lm = a.nd[l + 1].mn;
+        }
+        if (r < a.cap) {
+          rs = a.nd[r + 1].sum;
+          rm = a.nd[r + 1].mn;
+        }
+        if (L < maxd) {
+          // the node's subtree is the key range of aligned values [al, al + 2 half): its own
+          // keys first (depth L), then the left child's range, then the right child's; a
+          // child's owner at level L + 1 is the first key of its range
+          const uint64_t al = anc << (maxd - L), half = uint64_t(1) << (maxd - L - 1);
+          constexpr int kSh = kPosBits + kDepthBits;
+          int k1 = j;  // skip the node's own keys (duplicates of it)
+          while (k1 < m && (keys[k1] >> kSh) == al && (int)((keys[k1] >> kPosBits) & ((1u << kDepthBits) - 1)) == L)
+            ++k1;
+          if (k1 < m && keys[k1] != ~0ull && (keys[k1] >> kSh) < al + half) {
+            ls = res_sum[k1];
+            lm = res_min[k1];
+          }
+          // right child: first key at or after k1 with aligned >= al + half (galloping)
+          const uint64_t rc_al = al + half;
+          int lo = k1, hi = k1, b = 1;
+          while (hi < m && (keys[hi] >> kSh) < rc_al) {
+            lo = hi + 1;
+            hi = k1 + b;
+            b <<= 1;
+          }
+          if (hi > m) hi = m;
+          while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if ((keys[mid] >> kSh) < rc_al) lo = mid + 1; else hi = mid;
+          }
+          if (lo < m && keys[lo] != ~0ull && (keys[lo] >> kSh) < al + 2 * half) {
+            rs = res_sum[lo];
+            rm = res_min[lo];
+          }
+        }
+        double sm = v;  // sum[i] = val[i] + sum[l] + sum[r]; min seeded 1 for a zero val
+        double mn = (v != 0.0) ? v : 1.0;
+        if (l < a.cap) {
+          sm = radd(sm, ls);
+          if (lm != 0.0) mn = (lm < mn) ? lm : mn;
+        }
+        if (r < a.cap) {
+          sm = radd(sm, rs);
+          if (rm != 0.0) mn = (rm < mn) ? rm : mn;
+        }
+        a.nd[node + 1].sum = sm;
+        a.nd[node + 1].mn = mn;
+        res_sum[j] = sm;
+        res_min[j] = mn;
       }
-      __syncthreads();
+      lds_barrier();
     }
+    __syncthreads();  // the next chunk reads this chunk's stores from memory
+    if (tid == 0) g_upd_clock[4] = wall_clock64();
   }
   if (a.post_tail && tid == 0) a.st->tail = (fifo_start + a.n) % a.cap;  // all reads of tail are done
 }
@@ -451,6 +576,12 @@ int64_t rth_sumtree_capacity(const rth_sumtree *t) { return t ? t->cap : -1; }
 int rth_sumtree_clear(rth_sumtree *t, void *stream) {
   RTH_REQUIRE(t, "rth_sumtree_clear: NULL tree");
   RTH_HIP(hipMemsetAsync(t->nodes, 0, (size_t)(t->cap + 2) * sizeof(Node), as_stream(stream)));
+  return RTH_OK;
+}
+
+int rth_debug_tree_timing(long long *out5) {
+  RTH_REQUIRE(out5, "rth_debug_tree_timing: NULL");
+  RTH_HIP(hipMemcpyFromSymbol(out5, HIP_SYMBOL(g_upd_clock), 5 * sizeof(long long)));
   return RTH_OK;
 }
 

@@ -67,6 +67,7 @@ class ApexConfig:
     conv_benchmark: bool = False   # torch.backends.cudnn.benchmark (MIOpen find)
     hip_graph: bool = False        # replay captured HIP graphs of the compute blocks
     fused_actor: bool = True       # act + previous rows' priorities in one 3N forward (VecActors.step_fused)
+    overlap: bool = True           # graph mode: actor block and learner block on two streams, concurrently
     dp_hook: Optional[bool] = None  # gradient all-reduce hook: None = when world > 1 (tests force it)
     extra: dict = field(default_factory=dict)
 
@@ -245,6 +246,8 @@ class ApexDQN:
         self._graphs = G
 
     def _iteration_graph(self):
+        if self.cfg.overlap:
+            return self._iteration_graph_overlap()
         G = self._graphs
         act = self.actors
         for _ in range(self.cfg.actor_steps_per_update):
@@ -269,3 +272,51 @@ class ApexDQN:
         self.loader.issue()  # sample-ahead into the other slot
         self.replay.update_priorities(self.loader._slots[k][1], G["learn_td"][k], step=True, deferred=True)
         self._learner_host()
+
+    def _actor_block_graph(self):
+        G, act = self._graphs, self.actors
+        for _ in range(self.cfg.actor_steps_per_update):
+            self._actor_host()
+            k = act.pushes % 2
+            G["act"][k].replay()
+            act.t += 1
+            act.pushes += 1
+            td, rows = G["act_out"][k]
+            if self.cfg.fused_actor:
+                act._bind_rows(act._sets[k])
+                if act.pushes - 1 > act.n_step:
+                    act.append(self.replay, td, rows)
+            else:
+                act.append(self.replay, td)
+            self.env_steps += act.N
+
+    def _iteration_graph_overlap(self):
+        """The actor block (stream A: act + env + n-step + append, then the sample of batch
+        k+1) runs concurrently with the learner block of batch k (stream B: forward/backward,
+        Adam, target sync, weights publish).  Cross-stream edges, all one iteration apart:
+        A waits for learner k-1 (its |td| merges into this append, its batch slot is
+        resampled, its weights may be loaded by the actors); B waits for sample k.  The
+        replay's operations keep the single-stream order on A."""
+        G = self._graphs
+        A = self._stream
+        if not hasattr(self, "_stream_b"):
+            self._stream_b = torch.cuda.Stream(self.device)
+            self._ev_learn = torch.cuda.Event()
+            self._ev_sample = torch.cuda.Event()
+            self._ev_sample.record(A)  # batch k was sampled on A before the first overlapped step
+            self._ev_learn.record(A)
+        B = self._stream_b
+        A.wait_event(self._ev_learn)
+        self._actor_block_graph()  # on A (the caller's stream)
+        k = self.loader._pending.pop(0)
+        with torch.cuda.stream(B):
+            B.wait_event(self._ev_sample)
+            G["learn"][k].replay()
+            if G["apply"]:
+                self.solver.grad_hook(self.solver._params, grads=G["grads"][k])  # RCCL all-reduce on B
+                G["apply"][k].replay()
+            self._learner_host()  # target sync / weights publish copies: on B
+            self._ev_learn.record(B)
+        self.loader.issue()  # sample-ahead into the other slot (on A, after this step's append)
+        self._ev_sample.record(A)
+        self.replay.update_priorities(self.loader._slots[k][1], G["learn_td"][k], step=True, deferred=True)

@@ -239,6 +239,18 @@ def main():
     mean_gather_s = float(np.mean(gather_ms)) / 1e3
     bytes_launch = gather_bytes_per_row() * cfg.batch_size
     achieved = bytes_launch / mean_gather_s / 1e9
+    # the same gather alone on the GPU (in the timed region it shares the GPU with the
+    # concurrently running learner block): context for the in-loop figure, not `achieved`
+    slot_cols, slot_idx, _ = ax.loader._slots[0]
+    iso = []
+    for _ in range(30):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        ax.replay.gather(slot_idx, out_cols=slot_cols)
+        e1.record()
+        iso.append((e0, e1))
+    torch.cuda.synchronize()
+    iso_s = float(np.median([a.elapsed_time(b) for a, b in iso[5:]])) / 1e3
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
@@ -275,7 +287,10 @@ def main():
                      "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "bytes_per_launch": bytes_launch, "mean_launch_us": round(mean_gather_s * 1e6, 2),
-                     "launches_timed": len(gather_ms)},
+                     "launches_timed": len(gather_ms),
+                     "isolated_launch_us": round(iso_s * 1e6, 2),
+                     "isolated_frac": round(bytes_launch / iso_s / 1e9 / HBM_PEAK_GBS, 4),
+                     "note": "in the timed region the gather overlaps the learner block on a second stream"},
         "qnet_mfma": {"tflops_per_step": round((flops_update + flops_actor) * args.actor_steps_per_update / 1e12, 4),
                       "achieved_tflops": round((flops_update + flops_actor) / step_s / 1e12, 2),
                       "peak_fp32_tflops": FP32_PEAK_TFLOPS},

@@ -196,7 +196,8 @@ def main():
     cfg = ApexConfig(n_actors=args.actors, capacity=args.capacity, batch_size=args.batch,
                      actor_steps_per_update=args.actor_steps_per_update, seed=0,
                      channels_last=not args.nchw, conv_benchmark=not args.no_conv_benchmark,
-                     hip_graph=not args.eager)
+                     hip_graph=not args.eager,
+                     extra={"learner_priority": int(os.environ.get("RTH_LEARNER_PRIORITY", "-1"))})
     ax = ApexDQN(cfg, device=dev, rank=rank, world=world)
     ax.prefill(cfg.capacity)
     for _ in range(args.warmup):

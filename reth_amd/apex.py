@@ -300,7 +300,8 @@ class ApexDQN:
         G = self._graphs
         A = self._stream
         if not hasattr(self, "_stream_b"):
-            self._stream_b = torch.cuda.Stream(self.device)
+            # the learner block is the longer of the two: give its stream the higher priority
+            self._stream_b = torch.cuda.Stream(self.device, priority=self.cfg.extra.get("learner_priority", -1))
             self._ev_learn = torch.cuda.Event()
             self._ev_sample = torch.cuda.Event()
             self._ev_sample.record(A)  # batch k was sampled on A before the first overlapped step

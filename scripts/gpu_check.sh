@@ -39,6 +39,7 @@ for step in "$@"; do
             RTH_DIST_BACKEND=gloo run dp_probe1 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
             --master-addr 127.0.0.1 --master-port 29519 scripts/dp_probe.py ;;
     phases) run tree_phases 300 python scripts/probe_tree_phases.py ;;
+    prio) for pr in 0 -1; do RTH_LEARNER_PRIORITY=$pr run bench_prio$pr 600 python bench.py --steps 200 --warmup 20 --no-cpu-baseline; done ;;
     probe) run probe 300 python scripts/probe_qnet.py ;;
     variants2)
       run bench_eager 600 python bench.py --steps 100 --warmup 20 --no-cpu-baseline --eager

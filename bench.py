@@ -36,11 +36,13 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 FP32_PEAK_TFLOPS = 157.3
 
 
-def gather_bytes_per_row():
+def gather_bytes_per_row(s1_u8=False):
     """algorithmic bytes of one sampled apex row in rth_replay_gather: read s0/s1 uint8
-    stacks + a(8) r(4) done(4); write s0/s1 float32 stacks + a r done; 5 index reads"""
+    stacks + a(8) r(4) done(4); write s0 as a float32 stack (the learner's gradient pass),
+    s1 as float32 too or -- with the HIP conv torso, whose target passes read uint8 -- as the
+    uint8 stack; a r done; 5 index reads"""
     read = 2 * STACK + 8 + 4 + 4
-    write = 2 * STACK * 4 + 8 + 4 + 4
+    write = STACK * 4 + (STACK if s1_u8 else STACK * 4) + 8 + 4 + 4
     return read + write + 5 * 8
 
 
@@ -177,6 +179,8 @@ def main():
     ap.add_argument("--nchw", action="store_true", help="contiguous NCHW Q-net tensors (default channels-last)")
     ap.add_argument("--no-conv-benchmark", action="store_true", help="MIOpen immediate mode instead of find")
     ap.add_argument("--eager", action="store_true", help="no HIP-graph replay (launch every kernel from Python)")
+    ap.add_argument("--miopen-conv", action="store_true", help="conv torso forward in MIOpen (+ rth_bias_relu) "
+                    "instead of rth_conv_bias_relu")
     args = ap.parse_args()
 
     from reth_amd.apex import ApexConfig, ApexDQN
@@ -196,7 +200,7 @@ def main():
     cfg = ApexConfig(n_actors=args.actors, capacity=args.capacity, batch_size=args.batch,
                      actor_steps_per_update=args.actor_steps_per_update, seed=0,
                      channels_last=not args.nchw, conv_benchmark=not args.no_conv_benchmark,
-                     hip_graph=not args.eager,
+                     hip_graph=not args.eager, hip_conv=not args.miopen_conv,
                      extra={"learner_priority": int(os.environ.get("RTH_LEARNER_PRIORITY", "-1"))})
     ax = ApexDQN(cfg, device=dev, rank=rank, world=world)
     ax.prefill(cfg.capacity)
@@ -238,7 +242,7 @@ def main():
         n_env, n_upd = int(c[0]), int(c[1])
     gather_ms = [a.elapsed_time(b) for a, b in events]
     mean_gather_s = float(np.mean(gather_ms)) / 1e3
-    bytes_launch = gather_bytes_per_row() * cfg.batch_size
+    bytes_launch = gather_bytes_per_row(cfg.hip_conv and cfg.channels_last) * cfg.batch_size
     achieved = bytes_launch / mean_gather_s / 1e9
     # the same gather alone on the GPU (in the timed region it shares the GPU with the
     # concurrently running learner block): context for the in-loop figure, not `achieved`
@@ -282,9 +286,10 @@ def main():
                    "n_step": cfg.n_step, "alpha": cfg.alpha, "beta": cfg.beta,
                    "actor_steps_per_update": cfg.actor_steps_per_update,
                    "qnet_layout": "channels_last" if cfg.channels_last else "nchw",
-                   "conv_benchmark": cfg.conv_benchmark, "hip_graph": cfg.hip_graph,
+                   "conv_benchmark": cfg.conv_benchmark, "hip_graph": cfg.hip_graph, "hip_conv": cfg.hip_conv,
                    "parallelism": f"dp{world} learner (RCCL grad all-reduce) + {world} replay shards"},
-        "roofline": {"kernel": "rth_replay_gather (k_copy_rows: PER-sampled rows, u8->f32 frames)",
+        "roofline": {"kernel": "rth_replay_gather (k_copy_rows: PER-sampled rows, s0 u8->f32 NHWC%s)"
+                     % (", s1 u8" if cfg.hip_conv and cfg.channels_last else ", s1 u8->f32 NHWC"),
                      "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "bytes_per_launch": bytes_launch, "mean_launch_us": round(mean_gather_s * 1e6, 2),

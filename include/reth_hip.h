@@ -291,6 +291,30 @@ int rth_relu_bias_grad(const float *g_dev, const float *y_dev, float *gy_dev, fl
                        int64_t rows, int32_t C, void *stream);
 
 /* ------------------------------------------------------------------------------------
+ * Q-network convolution torso forward (reth/reth/algorithm/dqn/dqn_model.py:14-20: each
+ * Conv2d -> ReLU of `features`): y = relu(conv2d(x, w) + bias) in one launch, implicit GEMM
+ * on the fp32 MFMA, output NHWC fp32 [n, hout, wout, cout].  w is the Conv2d weight in OHWI
+ * storage (a channels_last [cout, cin, kh, kw] parameter), 16-byte aligned.
+ *   input RTH_CONV_F32_NHWC: x = [n, hin, win, cin] fp32 (channels-last activations);
+ *   input RTH_CONV_U8_CHW:   x = uint8 frame stacks [cin, hin, win] (the reference's float32
+ *       frames hold exactly these integers); sample i reads stack rows_dev[i] when rows_dev
+ *       is given (replay rows, actor frame-ring handles), else stack i -- no f32 copy of the
+ *       observations is made.
+ * Built geometries: the Nature-DQN torso on 4 x 84 x 84 stacks (conv1 either input form,
+ * conv2 32x20x20 -> 64 k4 s2, conv3 64x9x9 -> 64 k3 s1); rth_conv_supported says whether
+ * a shape is one of them.  Replaces MIOpen's forward + the separate rth_bias_relu pass.
+ * ---------------------------------------------------------------------------------- */
+#define RTH_CONV_F32_NHWC 0
+#define RTH_CONV_U8_CHW 1
+typedef struct rth_conv_shape {
+  int32_t input; /* RTH_CONV_F32_NHWC | RTH_CONV_U8_CHW */
+  int32_t cin, hin, win, cout, kh, kw, stride;
+} rth_conv_shape;
+int rth_conv_supported(const rth_conv_shape *shape);
+int rth_conv_bias_relu(const rth_conv_shape *shape, const void *x_dev, const int64_t *rows_dev, int64_t n,
+                       const float *w_dev, const float *bias_dev, float *y_dev, void *stream);
+
+/* ------------------------------------------------------------------------------------
  * Atari observation preprocessing (reth/reth/env/util.py:121-209, 281-297): per actor, the
  * max of the last two raw RGB frames of the skip window (MaxAndSkipEnv), cv2 RGB2GRAY +
  * INTER_AREA resize to out_h x out_w (WarpFrame; OpenCV's 8-bit algorithms restated, cv2

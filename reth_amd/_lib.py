@@ -46,6 +46,14 @@ class Src(ctypes.Structure):
                 ("reserved", c_i32)]
 
 
+class ConvShape(ctypes.Structure):
+    """rth_conv_shape"""
+    _fields_ = [("input", c_i32), ("cin", c_i32), ("hin", c_i32), ("win", c_i32), ("cout", c_i32), ("kh", c_i32),
+                ("kw", c_i32), ("stride", c_i32)]
+
+
+CONV_F32_NHWC, CONV_U8_CHW = 0, 1
+
 # name -> (restype, argtypes); must match include/reth_hip.h exactly
 SIGNATURES = {
     "rth_last_error": (ctypes.c_char_p, []),
@@ -101,6 +109,8 @@ SIGNATURES = {
     "rth_heads_split_grad": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i32, c_i32,
                                      ctypes.POINTER(c_vp), c_vp]),
     "rth_relu_bias_grad": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_vp]),
+    "rth_conv_supported": (c_i32, [ctypes.POINTER(ConvShape)]),
+    "rth_conv_bias_relu": (c_i32, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "rth_atari_create": (c_i32, [c_i32, c_i32, c_i32, c_i32, c_i32, ctypes.POINTER(c_vp)]),
     "rth_atari_destroy": (c_i32, [c_vp]),
     "rth_atari_step": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),

@@ -10,10 +10,12 @@ Here all N actors of a GPU step together, entirely in HBM:
   frames   uint8 [N, ring, 4, 84, 84]   per-actor ring of frame stacks (obs, next obs,
                                          reset obs); rows reference stacks by handle
                                          actor*ring + slot, never copy them until insert
-  step():  u8->f32 gather of the acting stacks -> Q-net (batch N) -> rth_eps_greedy ->
-           rth_synth_env_step -> rth_nstep_push (emits one row per actor once warm)
-  prioritise(): u8->f32 gather of the emitted rows' s0/s1 -> Q-net (batch 2N) ->
-           rth_td_huber (no grad) = calc_loss
+  step():  Q-net over the acting stacks (batch N; the HIP conv torso reads the uint8 ring
+           through the stack handles) -> rth_eps_greedy -> rth_synth_env_step ->
+           rth_nstep_push (emits one row per actor once warm)
+  prioritise(): Q-net over the emitted rows' s0/s1 stacks (batch 2N) -> rth_td_huber
+           (no grad) = calc_loss
+  step_fused(): both in one 3N forward (acting stacks + the previous step's rows)
   append(): rth_replay_append copies the rows' stacks from the ring into FIFO slots and
            inserts (|td| + 1e-6)^alpha into the tree.
 No host synchronisation anywhere in the loop.
@@ -61,8 +63,8 @@ class VecActors:
         self.eps = torch.as_tensor(np.ascontiguousarray(e), dtype=torch.float64, device=dev)
         self.channels_last = bool(channels_last)
         fmt = torch.channels_last if channels_last else torch.contiguous_format
-        self.obs = torch.empty((N, *OBS_SHAPE), dtype=torch.float32, device=dev, memory_format=fmt)
-        self.rows_f32 = torch.empty((2 * N, *OBS_SHAPE), dtype=torch.float32, device=dev, memory_format=fmt)
+        self._fmt = fmt
+        self._f32 = {}  # f32 observation batches, only for networks that cannot read uint8 stacks
         z = lambda dt: torch.zeros(N, dtype=dt, device=dev)
         self.action, self.s0_h, self.s1_h = z(torch.int64), z(torch.int64), z(torch.int64)
         self.reward, self.done = z(torch.float32), z(torch.float32)
@@ -74,7 +76,6 @@ class VecActors:
         # prioritised and appended at step t + 1, while step t + 1 emits into the other set)
         self._sets = [self._rowset_of_attrs(), RowSet(N, dev)]
         self.handles3 = torch.empty(3 * N, dtype=torch.int64, device=dev)
-        self.obs3 = torch.empty((3 * N, *OBS_SHAPE), dtype=torch.float32, device=dev, memory_format=fmt)
         h = _lib.c_vp()
         call("rth_nstep_create", N, self.n_step, self.gamma, int(nstep_mode), dev.index, _lib.ctypes.byref(h))
         self._nstep = h.value
@@ -101,6 +102,19 @@ class VecActors:
              _lib.RTH_U8, _lib.RTH_F32, OBS_SHAPE[0] if self.channels_last else 0, stream_ptr())
         return out
 
+    def _forward_stacks(self, q_net, handles):
+        """Q-net over the frame-ring stacks `handles`: the HIP torso reads the uint8 ring
+        directly (rth_conv_bias_relu through the handle index, no f32 copy); other networks
+        get a u8 -> f32 gather first"""
+        if getattr(q_net, "hwc_features", False) and getattr(q_net, "dueling", False) and q_net.hip_conv:
+            return q_net.forward_heads(self.frames, rows=handles), 1
+        n = handles.numel()
+        buf = self._f32.get(n)
+        if buf is None:
+            buf = self._f32[n] = torch.empty((n, *OBS_SHAPE), dtype=torch.float32, device=self.device,
+                                             memory_format=self._fmt)
+        return _q_forward(q_net, self.gather_f32(handles, buf))
+
     def current_obs_handles(self):
         if not hasattr(self, "_base"):
             self._base = torch.arange(self.N, device=self.device, dtype=torch.int64) * self.ring
@@ -113,9 +127,8 @@ class VecActors:
         s = stream_ptr()
         self.t += 1
         call("rth_counter_add", ptr(self.t_dev), 1, s)
-        # acting batch: current stacks -> f32 (Worker.step -> exploration.act -> solver.act)
-        self.gather_f32(self.current_obs_handles(), self.obs)
-        q, dueling = _q_forward(q_net, self.obs)
+        # acting batch: the current stacks (Worker.step -> exploration.act -> solver.act)
+        q, dueling = self._forward_stacks(q_net, self.current_obs_handles())
         call("rth_eps_greedy", ptr(q), self.N, self.A, dueling, ptr(self.eps), None, None, self.seed, 0,
              ptr(self.t_dev), ptr(self.action), s)
         call("rth_synth_env_step", ptr(self.frames), self.N, self.ring, 0, ptr(self.t_dev), ptr(self.cur_slot),
@@ -151,8 +164,7 @@ class VecActors:
         call("rth_counter_add", ptr(self.t_dev), 1, s)
         N = self.N
         torch.cat([self.current_obs_handles(), prev.s0, prev.s1], out=self.handles3)
-        self.gather_f32(self.handles3, self.obs3)
-        q, dueling = _q_forward(q_net, self.obs3)
+        q, dueling = self._forward_stacks(q_net, self.handles3)
         call("rth_eps_greedy", ptr(q), N, self.A, dueling, ptr(self.eps), None, None, self.seed, 0,
              ptr(self.t_dev), ptr(self.action), s)
         q1 = q[2 * N:]
@@ -171,8 +183,7 @@ class VecActors:
     def prioritise(self, q_net):
         """calc_loss on the emitted rows with the actor's network (target == online)"""
         torch.cat([self.row_s0, self.row_s1], out=self.row_handles)
-        self.gather_f32(self.row_handles, self.rows_f32)
-        q, dueling = _q_forward(q_net, self.rows_f32)
+        q, dueling = self._forward_stacks(q_net, self.row_handles)
         q0, q1 = q[: self.N], q[self.N:]
         _, td_abs, _ = td_huber_forward(q0, q1, q1, self.row_a, self.row_r, self.row_done, None, self.gamma_n,
                                         True, want_dq=False, dueling=bool(dueling))
@@ -212,9 +223,12 @@ def _q_forward(q_net, x):
     return q, dueling
 
 
-def apex_columns(channels_last=False):
+def apex_columns(channels_last=False, s1_u8=False):
     """replay columns of the apex-dqn rows [s0, a, r, s1, done] (worker.py:47-51): frames are
-    stored uint8 and sampled as float32 (exact), the rest as the reference casts them"""
+    stored uint8 and sampled as float32 (exact), the rest as the reference casts them.
+    s1_u8: s1 is sampled as the stored uint8 stacks -- the learner's no-grad target passes
+    read them in the HIP conv torso, which widens in registers (same values, 4x fewer bytes)"""
     from .replay import Column
     fr = lambda: Column(OBS_SHAPE, torch.uint8, torch.float32, channels_last=channels_last)
-    return [fr(), Column((), torch.int64), Column((), torch.float32), fr(), Column((), torch.float32)]
+    s1 = Column(OBS_SHAPE, torch.uint8) if s1_u8 else fr()
+    return [fr(), Column((), torch.int64), Column((), torch.float32), s1, Column((), torch.float32)]

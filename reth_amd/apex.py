@@ -68,6 +68,7 @@ class ApexConfig:
     hip_graph: bool = False        # replay captured HIP graphs of the compute blocks
     fused_actor: bool = True       # act + previous rows' priorities in one 3N forward (VecActors.step_fused)
     overlap: bool = True           # graph mode: actor block and learner block on two streams, concurrently
+    hip_conv: bool = True          # conv torso forward in rth_conv_bias_relu (actors/targets read uint8 stacks)
     dp_hook: Optional[bool] = None  # gradient all-reduce hook: None = when world > 1 (tests force it)
     extra: dict = field(default_factory=dict)
 
@@ -97,6 +98,8 @@ class ApexDQN:
         self.actor_net = DQNNetwork(OBS_SHAPE, cfg.num_actions).to(self.device, memory_format=fmt)
         self.actor_net.requires_grad_(False)
         self.actor_net.hwc_features = bool(cfg.channels_last)
+        for net in (self.actor_net, self.solver.q_network, self.solver.target_q_network):
+            net.hip_conv = bool(cfg.hip_conv)
         self.slot = WeightsSlot(self.solver.q_network)
         self.slot.acquire(self.actor_net)
         self.subscriber = WeightsSubscriber(self.slot, cfg.recv_weights_interval)
@@ -106,8 +109,9 @@ class ApexDQN:
                                 nstep_mode=cfg.nstep_mode, channels_last=cfg.channels_last)
         self.svc, self.addr = start_per(cfg.capacity, cfg.batch_size, alpha=cfg.alpha, beta=cfg.beta,
                                         sample_start=cfg.sample_start, device=self.device, seed=cfg.seed + 7919 * rank)
-        self.svc.replay = HbmReplay(cfg.capacity, apex_columns(cfg.channels_last), cfg.alpha, cfg.beta, self.device,
-                                    seed=cfg.seed + 7919 * rank)
+        u8 = bool(cfg.hip_conv and cfg.channels_last)
+        self.svc.replay = HbmReplay(cfg.capacity, apex_columns(cfg.channels_last, s1_u8=u8), cfg.alpha, cfg.beta,
+                                    self.device, seed=cfg.seed + 7919 * rank)
         self.replay = self.svc.replay
         self.loader = TorchCudaLoader(self.addr, buffer_size=2, prefetch=1)
         self.env_steps = 0

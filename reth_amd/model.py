@@ -31,6 +31,7 @@ class DQNNetwork(nn.Module):
         self._feat_chw = (64, fh, fw)
         # forward_heads on channels-last input: HIP conv epilogues and NHWC feature order
         self.hwc_features = False
+        self.hip_conv = True  # rth_conv_bias_relu for the built torso geometries (else MIOpen)
         if dueling:
             self.fc_adv = nn.Sequential(nn.Linear(nfeat, hidden_unit), nn.ReLU(), nn.Linear(hidden_unit, num_actions))
             self.fc_value = nn.Sequential(nn.Linear(nfeat, hidden_unit), nn.ReLU(), nn.Linear(hidden_unit, 1))
@@ -88,32 +89,68 @@ class DQNNetwork(nn.Module):
             for dst, src in zip(self._frozen, merged):
                 dst.copy_(src)
 
-    def forward_heads(self, x, merged=None):
+    def forward_heads(self, x, merged=None, rows=None):
+        """raw dueling heads [n, A+1].  x: float32 observations (channels-last with
+        hwc_features), or -- on the HIP torso -- uint8 frame stacks [m, C, H, W], read as
+        stacks `rows` (an int64 device index, n = rows.numel()) or all m of them"""
         if not self.dueling:
             raise ValueError("forward_heads needs the dueling network")
         if merged is None:
             merged = self._frozen if getattr(self, "_frozen", None) is not None else self._merged_head_weights()
         w1, b1, w2, b2 = merged
         if self.hwc_features:
-            h = self._features_nhwc(x)
+            h = self._features_nhwc(x, rows)
             h = h.permute(0, 2, 3, 1).reshape(h.shape[0], -1)  # a view of the NHWC activations
         else:
+            if x.dtype == torch.uint8 or rows is not None:
+                raise ValueError("uint8 / row-indexed observations need the HIP torso (hwc_features)")
             h = self.features(x).flatten(1)
         h = _LinearReLU.apply(h, w1, b1)
         return torch.addmm(b2, h, w2.t())
 
-    def _features_nhwc(self, x):
-        """the conv torso with each bias+ReLU (and its backward) as one HIP pass"""
-        if not x.is_contiguous(memory_format=torch.channels_last):
+    def _features_nhwc(self, x, rows=None):
+        """the conv torso on channels-last activations: each Conv2d -> ReLU is one HIP
+        implicit-GEMM launch with the bias and ReLU fused (rth_conv_bias_relu) where the
+        geometry is built, else MIOpen + the rth_bias_relu pass; backward: rth_relu_bias_grad
+        and MIOpen's data/weight gradients"""
+        from . import _lib
+
+        u8 = x.dtype == torch.uint8
+        if not u8 and not x.is_contiguous(memory_format=torch.channels_last):
             x = x.contiguous(memory_format=torch.channels_last)
-        if getattr(self, "_ws", None) is None or self._ws[0].device != x.device:
-            from . import _lib
-            self._ws = [torch.zeros(_lib.lib().rth_relu_bias_grad_workspace(m.out_channels), dtype=torch.uint8,
-                                    device=x.device) for m in self.features if isinstance(m, nn.Conv2d)]
         convs = [m for m in self.features if isinstance(m, nn.Conv2d)]
-        for conv, ws in zip(convs, self._ws):
-            x = _ConvBiasReLU.apply(x, conv.weight, conv.bias, conv.stride, ws)
+        if getattr(self, "_ws", None) is None or self._ws[0].device != x.device:
+            self._ws = [torch.zeros(_lib.lib().rth_relu_bias_grad_workspace(m.out_channels), dtype=torch.uint8,
+                                    device=x.device) for m in convs]
+        if len(getattr(self, "_shapes", ())) != len(convs) or self._shapes[0][0] != (x.shape[1:], u8):
+            self._shapes = self._conv_shapes(x, u8)
+        for li, (conv, ws) in enumerate(zip(convs, self._ws)):
+            shape = self._shapes[li][1]
+            if shape is not None:
+                x = _HipConvBiasReLU.apply(x, conv.weight, conv.bias, shape, conv.stride, ws, rows if li == 0 else None)
+            else:
+                if x.dtype == torch.uint8 or (li == 0 and rows is not None):
+                    raise ValueError("uint8 / row-indexed observations need rth_conv_bias_relu's conv1 geometry")
+                x = _ConvBiasReLU.apply(x, conv.weight, conv.bias, conv.stride, ws)
         return x
+
+    def _conv_shapes(self, x, u8):
+        """per conv: ((input shape key), rth_conv_shape or None when MIOpen runs it)"""
+        from . import _lib
+
+        out = []
+        c, h, w = x.shape[1:]
+        for li, conv in enumerate(m for m in self.features if isinstance(m, nn.Conv2d)):
+            kind = _lib.CONV_U8_CHW if (u8 and li == 0) else _lib.CONV_F32_NHWC
+            shp = _lib.ConvShape(kind, c, h, w, conv.out_channels, conv.kernel_size[0], conv.kernel_size[1],
+                                 conv.stride[0])
+            ok = (self.hip_conv and conv.stride[0] == conv.stride[1] and conv.padding == (0, 0)
+                  and conv.dilation == (1, 1) and conv.groups == 1
+                  and _lib.lib().rth_conv_supported(_lib.ctypes.byref(shp)) == 1)
+            out.append(((x.shape[1:], u8) if li == 0 else None, shp if ok else None))
+            c, h, w = conv.out_channels, (h - conv.kernel_size[0]) // conv.stride[0] + 1, \
+                (w - conv.kernel_size[1]) // conv.stride[1] + 1
+        return out
 
 
 class _MergeHeads(torch.autograd.Function):
@@ -204,6 +241,47 @@ class _ConvBiasReLU(torch.autograd.Function):
         gx, gw, _ = torch.ops.aten.convolution_backward(gy, x, w, None, ctx.stride, [0, 0], [1, 1], False, [0, 0], 1,
                                                         [ctx.needs_input_grad[0], ctx.needs_input_grad[1], False])
         return gx, gw, db, None, None
+
+
+class _HipConvBiasReLU(torch.autograd.Function):
+    """relu(conv2d(x, w) + b) as one rth_conv_bias_relu launch (conv.hip); x channels-last
+    fp32, or uint8 CHW frame stacks (optionally through a row index) for the first layer.
+    Backward as _ConvBiasReLU: rth_relu_bias_grad + MIOpen data/weight gradients (a uint8
+    input is widened to the f32 channels-last batch it stands for)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, shape, stride, ws, rows):
+        from ._lib import call, ctypes, ptr, stream_ptr
+
+        n = rows.numel() if rows is not None else x.shape[0]
+        ho = (shape.hin - shape.kh) // shape.stride + 1
+        wo = (shape.win - shape.kw) // shape.stride + 1
+        y = torch.empty((n, shape.cout, ho, wo), dtype=torch.float32, device=x.device,
+                        memory_format=torch.channels_last)
+        if not w.is_contiguous(memory_format=torch.channels_last):
+            w = w.contiguous(memory_format=torch.channels_last)
+        call("rth_conv_bias_relu", ctypes.byref(shape), ptr(x), ptr(rows), n, ptr(w), ptr(b), ptr(y), stream_ptr())
+        ctx.save_for_backward(x, w, y, rows)
+        ctx.stride, ctx.ws = list(stride), ws
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        from ._lib import call, ptr, stream_ptr
+
+        x, w, y, rows = ctx.saved_tensors
+        if x.dtype == torch.uint8:
+            x = (x if rows is None else x[rows]).float().contiguous(memory_format=torch.channels_last)
+        if not g.is_contiguous(memory_format=torch.channels_last):
+            g = g.contiguous(memory_format=torch.channels_last)
+        gy = torch.empty_like(y)
+        n, c, h, wd = y.shape
+        db = torch.empty(c, dtype=y.dtype, device=y.device)
+        call("rth_relu_bias_grad", ptr(g), ptr(y), ptr(gy), ptr(db), ptr(ctx.ws), n * h * wd, c, stream_ptr())
+        need_x = ctx.needs_input_grad[0]
+        gx, gw, _ = torch.ops.aten.convolution_backward(gy, x, w, None, ctx.stride, [0, 0], [1, 1], False, [0, 0], 1,
+                                                        [need_x, ctx.needs_input_grad[1], False])
+        return gx, gw, db, None, None, None, None
 
 
 class MLP_DQNNetwork(nn.Module):

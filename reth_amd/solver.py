@@ -190,7 +190,15 @@ class DQNSolver(Algorithm):
         dev = self.device
         f = lambda x, dt: (x.to(device=dev, dtype=dt, non_blocking=True) if torch.is_tensor(x)
                            else torch.as_tensor(np.asarray(x), dtype=dt).to(dev, non_blocking=True))
-        return f(s0, torch.float32), f(a, torch.int64), f(r, torch.float32), f(s1, torch.float32), f(done, torch.float32)
+        # uint8 frame stacks stay uint8 when the HIP conv torso reads them (the f32 frames the
+        # reference feeds hold exactly these integers); anything else is cast as the reference does
+        fr = lambda x: x if self._u8_frames(x) else f(x, torch.float32)
+        return fr(s0), f(a, torch.int64), f(r, torch.float32), fr(s1), f(done, torch.float32)
+
+    def _u8_frames(self, x):
+        net = self.q_network
+        return (torch.is_tensor(x) and x.dtype == torch.uint8 and x.is_cuda and self._heads
+                and getattr(net, "hwc_features", False) and getattr(net, "hip_conv", False))
 
     def _forward_targets(self, s1, merged=None):
         with torch.no_grad():

@@ -40,6 +40,8 @@ for step in "$@"; do
             --master-addr 127.0.0.1 --master-port 29519 scripts/dp_probe.py ;;
     phases) run tree_phases 300 python scripts/probe_tree_phases.py ;;
     prio) for pr in 0 -1; do RTH_LEARNER_PRIORITY=$pr run bench_prio$pr 600 python bench.py --steps 200 --warmup 20 --no-cpu-baseline; done ;;
+    convt) run pytest_conv 600 python -m pytest tests/test_conv_gpu.py -q -rf -x ;;
+    convb) run bench_conv 300 python scripts/bench_conv.py ;;
     probe) run probe 300 python scripts/probe_qnet.py ;;
     variants2)
       run bench_eager 600 python bench.py --steps 100 --warmup 20 --no-cpu-baseline --eager

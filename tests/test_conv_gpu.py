@@ -1,0 +1,133 @@
+"""rth_conv_bias_relu (conv.hip) against a float64 CPU convolution: the three Nature-DQN
+torso geometries (dqn_model.py:14-20) on channels-last fp32 input, conv1 on uint8 CHW
+stacks addressed through a row index, ragged tails and the unsupported-shape error."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+GEOMS = [(4, 84, 84, 32, 8, 4), (32, 20, 20, 64, 4, 2), (64, 9, 9, 64, 3, 1)]
+
+
+def _shape(inp, cin, h, w, cout, k, s):
+    from reth_amd import _lib
+
+    return _lib.ConvShape(inp, cin, h, w, cout, k, k, s)
+
+
+def _run(shape, x, rows, n, w, b, dev):
+    from reth_amd import _lib
+
+    ho = (shape.hin - shape.kh) // shape.stride + 1
+    wo = (shape.win - shape.kw) // shape.stride + 1
+    y = torch.full((n, ho, wo, shape.cout), float("nan"), device=dev)
+    wt = w.to(dev).contiguous(memory_format=torch.channels_last)
+    _lib.call("rth_conv_bias_relu", _lib.ctypes.byref(shape), x.data_ptr(), None if rows is None else rows.data_ptr(),
+              n, wt.data_ptr(), b.to(dev).data_ptr(), y.data_ptr(), _lib.stream_ptr())
+    return y.permute(0, 3, 1, 2).cpu()
+
+
+def _ref(x_nchw, w, b, s):
+    return F.relu(F.conv2d(x_nchw.double(), w.double(), b.double(), stride=s))
+
+
+@pytest.mark.parametrize("geom", GEOMS)
+@pytest.mark.parametrize("n", [1, 3, 37])
+def test_conv_f32_nhwc(dev, geom, n):
+    from reth_amd import _lib
+
+    cin, h, wd, cout, k, s = geom
+    g = torch.Generator().manual_seed(hash((geom, n)) % 2**31)
+    x = torch.rand((n, cin, h, wd), generator=g) * 2 - 1
+    w = (torch.rand((cout, cin, k, k), generator=g) * 2 - 1) / np.sqrt(cin * k * k)
+    b = (torch.rand(cout, generator=g) * 2 - 1) * 0.1
+    xd = x.to(dev).contiguous(memory_format=torch.channels_last)
+    got = _run(_shape(_lib.CONV_F32_NHWC, *geom), xd, None, n, w, b, dev)
+    want = _ref(x, w, b, s)
+    assert not torch.isnan(got).any()
+    torch.testing.assert_close(got.double(), want, rtol=1e-5, atol=1e-5)
+    assert (got == 0).any() and (got > 0).any()  # ReLU active on both sides
+
+
+@pytest.mark.parametrize("n", [1, 5, 64])
+def test_conv1_u8_rows(dev, n):
+    from reth_amd import _lib
+
+    g = torch.Generator().manual_seed(7 + n)
+    stacks = torch.randint(0, 256, (80, 4, 84, 84), dtype=torch.uint8, generator=g)
+    rows = torch.randint(0, 80, (n,), generator=g)
+    rows[0] = 79
+    w = (torch.rand((32, 4, 8, 8), generator=g) * 2 - 1) / 16
+    b = (torch.rand(32, generator=g) * 2 - 1) * 0.1
+    shape = _shape(_lib.CONV_U8_CHW, *GEOMS[0])
+    got = _run(shape, stacks.to(dev), rows.to(dev), n, w, b, dev)
+    want = _ref(stacks[rows].double(), w, b, 4)
+    torch.testing.assert_close(got.double(), want, rtol=1e-5, atol=5e-4)  # |x| <= 255: sums ~ 1e2
+    # without a row index: stacks 0..n-1; the f32 NHWC form of the same data agrees
+    got2 = _run(shape, stacks.to(dev), None, n, w, b, dev)
+    torch.testing.assert_close(got2.double(), _ref(stacks[:n].double(), w, b, 4), rtol=1e-5, atol=5e-4)
+    xf = stacks[:n].float().to(dev).contiguous(memory_format=torch.channels_last)
+    got3 = _run(_shape(_lib.CONV_F32_NHWC, *GEOMS[0]), xf, None, n, w, b, dev)
+    torch.testing.assert_close(got3, got2, rtol=1e-5, atol=5e-4)
+
+
+def test_conv_empty_and_unsupported(dev):
+    from reth_amd import _lib
+
+    shape = _shape(_lib.CONV_F32_NHWC, *GEOMS[1])
+    assert _lib.lib().rth_conv_supported(_lib.ctypes.byref(shape)) == 1
+    x = torch.zeros(16, device=dev)
+    y = torch.zeros(16, device=dev)
+    w = torch.zeros(64 * 32 * 16, device=dev)
+    _lib.call("rth_conv_bias_relu", _lib.ctypes.byref(shape), x.data_ptr(), None, 0, w.data_ptr(), w.data_ptr(),
+              y.data_ptr(), _lib.stream_ptr())
+    bad = _shape(_lib.CONV_F32_NHWC, 3, 84, 84, 32, 8, 4)
+    assert _lib.lib().rth_conv_supported(_lib.ctypes.byref(bad)) == 0
+    with pytest.raises(_lib.RethHipError, match="not built"):
+        _lib.call("rth_conv_bias_relu", _lib.ctypes.byref(bad), x.data_ptr(), None, 1, w.data_ptr(), w.data_ptr(),
+                  y.data_ptr(), _lib.stream_ptr())
+
+
+def _torso_net(dev, seed=0):
+    from reth_amd.model import DQNNetwork
+
+    torch.manual_seed(seed)
+    net = DQNNetwork((4, 84, 84), 6).to(dev, memory_format=torch.channels_last)
+    net.hwc_features = True
+    return net
+
+
+def test_forward_heads_u8_rows_matches_miopen(dev):
+    """the HIP torso on uint8 stacks through a row index == MIOpen on the gathered f32 batch"""
+    net = _torso_net(dev)
+    g = torch.Generator(device=dev).manual_seed(3)
+    frames = torch.randint(0, 256, (40, 4, 84, 84), dtype=torch.uint8, device=dev, generator=g)
+    rows = torch.randint(0, 40, (33,), device=dev, generator=g)
+    with torch.no_grad():
+        q = net.forward_heads(frames, rows=rows)
+        net.hip_conv = False
+        want = net.forward_heads(frames[rows].float().contiguous(memory_format=torch.channels_last))
+        net.hip_conv = True
+        q_all = net.forward_heads(frames)
+    torch.testing.assert_close(q, want, rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(q_all[rows], q, rtol=0, atol=0)  # same kernel, same data
+
+
+def test_hip_torso_gradients_match_miopen(dev):
+    """grad path: rth_conv_bias_relu forward + MIOpen backward == MIOpen forward + backward"""
+    net = _torso_net(dev, seed=1)
+    g = torch.Generator(device=dev).manual_seed(4)
+    x = torch.randint(0, 256, (24, 4, 84, 84), device=dev, generator=g).float()
+    x = x.contiguous(memory_format=torch.channels_last)
+    grads = []
+    for hip in (True, False):
+        net.hip_conv = hip
+        net.zero_grad(set_to_none=True)
+        h = net.forward_heads(x, net._merged_head_weights())
+        (h.square().sum() * 1e-3).backward()
+        grads.append([p.grad.clone() for p in net.parameters()])
+    for a, b in zip(*grads):
+        scale = b.abs().max().clamp_min(1e-12)
+        assert ((a - b).abs().max() / scale) < 1e-4

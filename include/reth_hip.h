@@ -293,8 +293,10 @@ int rth_relu_bias_grad(const float *g_dev, const float *y_dev, float *gy_dev, fl
 /* ------------------------------------------------------------------------------------
  * Q-network convolution torso forward (reth/reth/algorithm/dqn/dqn_model.py:14-20: each
  * Conv2d -> ReLU of `features`): y = relu(conv2d(x, w) + bias) in one launch, implicit GEMM
- * on the fp32 MFMA, output NHWC fp32 [n, hout, wout, cout].  w is the Conv2d weight in OHWI
- * storage (a channels_last [cout, cin, kh, kw] parameter), 16-byte aligned.
+ * on the fp32 MFMA, output NHWC fp32 [n, hout, wout, cout].  `packed` is the Conv2d weight
+ * in the kernel's fragment order, made by rth_conv_pack from the OHWI weight (a channels_last
+ * [cout, cin, kh, kw] parameter) into rth_conv_packed_bytes(shape) bytes -- once per weight
+ * version, so every launch stages it into LDS with one coalesced copy.  16-byte aligned.
  *   input RTH_CONV_F32_NHWC: x = [n, hin, win, cin] fp32 (channels-last activations);
  *   input RTH_CONV_U8_CHW:   x = uint8 frame stacks [cin, hin, win] (the reference's float32
  *       frames hold exactly these integers); sample i reads stack rows_dev[i] when rows_dev
@@ -311,8 +313,10 @@ typedef struct rth_conv_shape {
   int32_t cin, hin, win, cout, kh, kw, stride;
 } rth_conv_shape;
 int rth_conv_supported(const rth_conv_shape *shape);
+int64_t rth_conv_packed_bytes(const rth_conv_shape *shape);
+int rth_conv_pack(const rth_conv_shape *shape, const float *w_ohwi_dev, float *packed_dev, void *stream);
 int rth_conv_bias_relu(const rth_conv_shape *shape, const void *x_dev, const int64_t *rows_dev, int64_t n,
-                       const float *w_dev, const float *bias_dev, float *y_dev, void *stream);
+                       const float *packed_dev, const float *bias_dev, float *y_dev, void *stream);
 
 /* ------------------------------------------------------------------------------------
  * Atari observation preprocessing (reth/reth/env/util.py:121-209, 281-297): per actor, the

@@ -8,7 +8,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libreth_hip.so")
+LIB_PATH = os.environ.get("RTH_LIB_PATH") or os.path.join(_HERE, "libreth_hip.so")  # override: kernel A/B runs
 
 # element types (include/reth_hip.h)
 RTH_U8, RTH_I32, RTH_I64, RTH_F32, RTH_F64 = 0, 1, 2, 3, 4
@@ -110,6 +110,8 @@ SIGNATURES = {
                                      ctypes.POINTER(c_vp), c_vp]),
     "rth_relu_bias_grad": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_vp]),
     "rth_conv_supported": (c_i32, [ctypes.POINTER(ConvShape)]),
+    "rth_conv_packed_bytes": (c_i64, [ctypes.POINTER(ConvShape)]),
+    "rth_conv_pack": (c_i32, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_vp]),
     "rth_conv_bias_relu": (c_i32, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "rth_atari_create": (c_i32, [c_i32, c_i32, c_i32, c_i32, c_i32, ctypes.POINTER(c_vp)]),
     "rth_atari_destroy": (c_i32, [c_vp]),

@@ -27,6 +27,9 @@
 // Numerics: each output is an fp32 fma chain over K in the permuted order above (MFMA f32 is
 // a k-ordered fmaf chain), then + bias, then ReLU -- the same operations as conv -> bias ->
 // relu, summed in a different order than MIOpen's or the reference's CPU convolution.
+#include <cstdlib>
+#include <type_traits>
+
 #include "common.hpp"
 
 namespace rth {
@@ -40,153 +43,255 @@ struct ConvGeom {
   static constexpr int HOUT = (HIN - KH) / S + 1, WOUT = (WIN - KW) / S + 1, PIX = HOUT * WOUT;
   static constexpr int K = KH * KW * CIN, G = K / 16, NB = COUT / 16;
   static constexpr int LDS_F4 = G * NB * 64;  // float4 slots of the staged weights
-  // input chunks in flight per wave (f32 input): a divisor of G, at most 12
-  static constexpr int PREFETCH = G % 8 == 0 ? 8 : (G % 12 == 0 ? 12 : (G % 6 == 0 ? 6 : (G % 4 == 0 ? 4 : 1)));
+  // input chunks in flight per wave (f32 input): a divisor of G, at most 8 / MB
+  static constexpr int prefetch(int mb) {
+    for (int d = 8 / mb; d > 1; --d)
+      if (G % d == 0) return d;
+    return 1;
+  }
   static constexpr int64_t STACK = (int64_t)CIN * HIN * WIN;
   static_assert(K % 16 == 0 && COUT % 16 == 0, "K and COUT must be multiples of 16");
   static_assert(MODE == 0 ? (KW * CIN) % 16 == 0 : (KW == 8 && KH % 2 == 0), "unsupported window");
 
-  // LDS float index of weight W[o][kh][kw][ci] (OHWI storage order)
-  __device__ static int lds_index(int o, int kh, int kw, int ci) {
-    int g, q, t;
+  // the 4 weights of LDS float4 slot sl = (g * NB + nb) * 64 + lane (t = 0..3) from W in
+  // OHWI storage: f32 input -> 4 consecutive ci (one 16-byte read); u8 input -> 4 kw
+  __device__ static f32x4 load_slot(const float *__restrict__ w, int sl) {
+    const int lane = sl % 64, gn = sl / 64, nb = gn % NB, g = gn / NB;
+    const int q = lane >> 4, o = nb * 16 + (lane & 15);
     if (MODE == RTH_CONV_F32_NHWC) {
-      const int r = kw * CIN + ci;  // position inside the kh row
-      g = kh * (KW * CIN / 16) + r / 16;
-      q = (r % 16) / 4;
-      t = r % 4;
+      constexpr int RC = KW * CIN / 16;
+      const int kh = g / RC, r = (g % RC) * 16 + 4 * q;  // r = kw * CIN + ci, ci % 4 == 0
+      const float4 v = *reinterpret_cast<const float4 *>(w + (int64_t)o * K + kh * KW * CIN + r);
+      return f32x4{v.x, v.y, v.z, v.w};
     } else {
-      const int rho = ci * KH + kh;  // (ci, kh) byte run
-      g = rho / 2;
-      q = (rho % 2) * 2 + kw / 4;
-      t = kw % 4;
+      const int rho = 2 * g + (q >> 1), ci = rho / KH, kh = rho % KH, kw = 4 * (q & 1);
+      const float *p = w + (int64_t)o * K + (kh * KW + kw) * CIN + ci;
+      return f32x4{p[0], p[CIN], p[2 * CIN], p[3 * CIN]};
     }
-    const int nb = o / 16, lane = q * 16 + o % 16;
-    return ((g * NB + nb) * 64 + lane) * 4 + t;
   }
 };
 
-template <int MODE, int KH, int KW, int S, int CIN, int COUT, int HIN, int WIN, int WAVES>
+template <int MODE, int KH, int KW, int S, int CIN, int COUT, int HIN, int WIN, int WAVES, int MB>
 __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__restrict__ x,
                                                               const int64_t *__restrict__ rows, int64_t n,
                                                               const float *__restrict__ w,
                                                               const float *__restrict__ bias,
                                                               float *__restrict__ y) {
   using Gm = ConvGeom<MODE, KH, KW, S, CIN, COUT, HIN, WIN>;
-  constexpr int G = Gm::G, NB = Gm::NB, K = Gm::K;
+  constexpr bool F32 = MODE == RTH_CONV_F32_NHWC;
+  constexpr int G = Gm::G, NB = Gm::NB, T = WAVES * 64;
+  constexpr int TP = 16 * MB;                    // output pixels per wave tile
+  constexpr int D = F32 ? Gm::prefetch(MB) : G;  // input chunks in flight per wave
+  using Frag = typename std::conditional<F32, f32x4, uint32_t>::type;
   __shared__ f32x4 wl[Gm::LDS_F4];
-  float *wf = reinterpret_cast<float *>(wl);
-
-  // stage W (OHWI, contiguous) into fragment order: coalesced float4 reads
-  for (int i = threadIdx.x; i < COUT * K / 4; i += WAVES * 64) {
-    const float4 v = reinterpret_cast<const float4 *>(w)[i];
-    const int e = 4 * i, o = e / K, rem = e % K;
-    const int kh = rem / (KW * CIN), r = rem % (KW * CIN), kw = r / CIN, ci = r % CIN;
-    if (MODE == RTH_CONV_F32_NHWC) {  // 4 consecutive ci -> 4 consecutive t: one LDS float4
-      wl[Gm::lds_index(o, kh, kw, ci) / 4] = f32x4{v.x, v.y, v.z, v.w};
-    } else {
-      wf[Gm::lds_index(o, kh, kw, ci)] = v.x;
-      wf[Gm::lds_index(o, kh, kw, ci + 1)] = v.y;
-      wf[Gm::lds_index(o, kh, kw, ci + 2)] = v.z;
-      wf[Gm::lds_index(o, kh, kw, ci + 3)] = v.w;
-    }
-  }
-  __syncthreads();
 
   const int wave = threadIdx.x / 64, lane = threadIdx.x % 64;
   const int q = lane >> 4, mr = lane & 15;
-  const int64_t P = n * Gm::PIX, tiles = (P + 15) / 16;
+  const int64_t P = n * Gm::PIX, tiles = (P + TP - 1) / TP, tstride = (int64_t)gridDim.x * WAVES;
+
+  // this lane's window origin in tile t, per M-block (tail lanes read a duplicate pixel)
+  auto bases = [&](int64_t t, const uint8_t *(&out)[MB]) {
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) {
+      int64_t p = t * TP + mb * 16 + mr;
+      if (p >= P) p = P - 1;
+      const int64_t b = p / Gm::PIX;
+      const int pp = (int)(p % Gm::PIX), oy = pp / Gm::WOUT, ox = pp % Gm::WOUT;
+      if constexpr (F32) {
+        out[mb] = reinterpret_cast<const uint8_t *>(static_cast<const float *>(x) +
+                                                    ((b * HIN + S * oy) * WIN + S * ox) * CIN + 4 * q);
+      } else {
+        const int64_t row = rows ? rows[b] : b;
+        out[mb] = static_cast<const uint8_t *>(x) + row * Gm::STACK + (int64_t)(S * oy + (q >> 1)) * WIN + S * ox +
+                  4 * (q & 1);
+      }
+    }
+  };
+  // byte offset of chunk g inside the window: f32 = kh rows of KW*CIN floats in 16-float
+  // chunks; u8 = runs 2g, 2g+1 = (ci, kh), (ci, kh+1) with ci = 2g / KH, kh = 2g % KH
+  auto chunk_off = [](int g) -> int {
+    if constexpr (F32) {
+      constexpr int RC = KW * CIN / 16;
+      return 4 * ((g / RC) * WIN * CIN + (g % RC) * 16);
+    } else {
+      return ((2 * g) / KH) * HIN * WIN + ((2 * g) % KH) * WIN;
+    }
+  };
+  auto ld = [](const uint8_t *p) { return *reinterpret_cast<const Frag *>(p); };
+
+#ifdef CONV_PROBE_TIMING  // A/B probe only: per-wave timestamps written over y
+  const uint64_t pt0 = wall_clock64(), pc0 = clock64();
+#endif
+  // wave slots are numbered SIMD-major (waves w and w + 4 of a workgroup share a SIMD): the
+  // first gridDim.x * 4 slots put one wave on every SIMD, so a partial last round of tiles
+  // lands on distinct SIMDs and no SIMD runs more than ceil(tiles / SIMDs) tiles
+  const int64_t slot = WAVES % 4 == 0 ? (int64_t)(wave / 4) * gridDim.x * 4 + blockIdx.x * 4 + wave % 4
+                                      : (int64_t)blockIdx.x * WAVES + wave;
+  // the first tile's leading input chunks are requested before the weights are staged
+  int64_t tile = slot;
+  const uint8_t *cur[MB], *nxt[MB];
+  bases(tile < tiles ? tile : tiles - 1, cur);
+  Frag ar[D][MB];
+#pragma unroll
+  for (int d = 0; d < D; ++d)
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) ar[d][mb] = ld(cur[mb] + chunk_off(d));
+
+  // stage the packed weights (rth_conv_pack: already in fragment order): a coalesced copy,
+  // consecutive threads -> consecutive 16-byte LDS slots; all loads first
+#ifndef CONV_PROBE_NOSTAGE  // A/B probe only: LDS weights left uninitialised
+  {
+    constexpr int PER = (Gm::LDS_F4 + T - 1) / T;
+    const f32x4 *wp = reinterpret_cast<const f32x4 *>(w);
+    f32x4 tmp[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int sl = threadIdx.x + j * T;
+      if (sl < Gm::LDS_F4) tmp[j] = wp[sl];
+    }
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int sl = threadIdx.x + j * T;
+      if (sl < Gm::LDS_F4) wl[sl] = tmp[j];
+    }
+  }
+#endif
+  __syncthreads();
+#ifdef CONV_PROBE_TIMING
+  const uint64_t pt1 = wall_clock64();
+  int ptiles = 0;
+#endif
+#ifdef CONV_PROBE_STAGE_ONLY  // A/B probe only: staging cost alone
+  if (tile < tiles) return;
+#endif
+
   float bl[NB];
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb) bl[nb] = bias[nb * 16 + mr];
+  const f32x4 *wlane = wl + lane;
 
-  for (int64_t tile = (int64_t)blockIdx.x * WAVES + wave; tile < tiles; tile += (int64_t)gridDim.x * WAVES) {
-    int64_t p = tile * 16 + mr;
-    if (p >= P) p = P - 1;  // tail lanes compute a duplicate, never stored
-    const int64_t b = p / Gm::PIX;
-    const int pp = (int)(p % Gm::PIX), oy = pp / Gm::WOUT, ox = pp % Gm::WOUT;
-    f32x4 acc[NB];
+  for (; tile < tiles; tile += tstride) {
+    // the chunks past the end of this tile are the next tile's leading chunks
+    bases(tile + tstride < tiles ? tile + tstride : tile, nxt);
+    f32x4 acc[MB][NB];
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb) acc[nb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) acc[mb][nb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    f32x4 bcur[NB], bnxt[NB];  // B fragments, one chunk ahead
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) bcur[nb] = wlane[nb * 64];
 
-    if constexpr (MODE == RTH_CONV_F32_NHWC) {
-      const float *base =
-          static_cast<const float *>(x) + ((b * HIN + S * oy) * WIN + S * ox) * CIN + 4 * q;
-      constexpr int RC = KW * CIN / 16;  // chunks per kh row
-      auto a_at = [&](int g) {
-        return *reinterpret_cast<const f32x4 *>(base + (g / RC) * WIN * CIN + (g % RC) * 16);
-      };
-      // A ring: chunk g + D is requested while chunk g is multiplied (D chunks in flight)
-      constexpr int D = Gm::PREFETCH;
-      f32x4 ar[D];
-#pragma unroll
-      for (int d = 0; d < D; ++d) ar[d] = a_at(d);
 #pragma unroll 1
-      for (int g0 = 0; g0 < G; g0 += D) {
+    for (int g0 = 0; g0 < G; g0 += D) {
 #pragma unroll
-        for (int d = 0; d < D; ++d) {
-          const int g = g0 + d;
-          const f32x4 a = ar[d];
-          if (g + D < G) ar[d] = a_at(g + D);
-          f32x4 bv[NB];
+      for (int d = 0; d < D; ++d) {
+        const int g = g0 + d;
+        const int gb = g + 1 < G ? g + 1 : G - 1;
 #pragma unroll
-          for (int nb = 0; nb < NB; ++nb) bv[nb] = wl[(g * NB + nb) * 64 + lane];
+        for (int nb = 0; nb < NB; ++nb) {
+#ifdef CONV_PROBE_NOB  // A/B probe only: no B reads in the loop (wrong results)
+          bnxt[nb] = bcur[nb] + (float)gb;
+#else
+          bnxt[nb] = wlane[(gb * NB + nb) * 64];
+#endif
+        }
+        // keep the next chunk's B reads here, a whole chunk of MFMAs ahead of their use
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-          for (int t = 0; t < 4; ++t)
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int mb = 0; mb < MB; ++mb) {
+            float a;
+            if constexpr (F32) a = ar[d][mb][t];
+            else a = (float)((ar[d][mb] >> (8 * t)) & 0xffu);
 #pragma unroll
             for (int nb = 0; nb < NB; ++nb)
-              acc[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t], bv[nb][t], acc[nb], 0, 0, 0);
-        }
-      }
-    } else {
-      const int64_t row = rows ? rows[b] : b;
-      const uint8_t *base = static_cast<const uint8_t *>(x) + row * Gm::STACK + (int64_t)(S * oy + (q >> 1)) * WIN +
-                            S * ox + 4 * (q & 1);
+              acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bcur[nb][t], acc[mb][nb], 0, 0, 0);
+          }
+        const int ga = g + D;
+#ifdef CONV_PROBE_NOA  // A/B probe only: no input reads in the loop (wrong results)
+        if (ga >= G)
+#endif
 #pragma unroll
-      for (int g = 0; g < G; ++g) {
-        // runs 2g, 2g+1 = (ci, kh), (ci, kh+1) with ci = 2g / KH, kh = 2g % KH
-        const uint32_t v =
-            *reinterpret_cast<const uint32_t *>(base + ((2 * g) / KH) * HIN * WIN + ((2 * g) % KH) * WIN);
-        f32x4 bv[NB];
+        for (int mb = 0; mb < MB; ++mb)
+          ar[d][mb] = ld(ga < G ? cur[mb] + chunk_off(ga) : nxt[mb] + chunk_off(ga - G));
 #pragma unroll
-        for (int nb = 0; nb < NB; ++nb) bv[nb] = wl[(g * NB + nb) * 64 + lane];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const float a = (float)((v >> (8 * t)) & 0xffu);
-#pragma unroll
-          for (int nb = 0; nb < NB; ++nb) acc[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bv[nb][t], acc[nb], 0, 0, 0);
-        }
+        for (int nb = 0; nb < NB; ++nb) bcur[nb] = bnxt[nb];
       }
     }
-    // C/D: lane holds column mr of rows 4q .. 4q+3
+    // C/D: lane holds column mr of rows 4q .. 4q+3 of each M-block
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int64_t po = tile * 16 + 4 * q + i;
-      if (po < P) {
+    for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
-        for (int nb = 0; nb < NB; ++nb) y[po * COUT + nb * 16 + mr] = relu_c(radd(acc[nb][i], bl[nb]));
+      for (int i = 0; i < 4; ++i) {
+        const int64_t po = tile * TP + mb * 16 + 4 * q + i;
+        if (po < P) {
+#pragma unroll
+          for (int nb = 0; nb < NB; ++nb) y[po * COUT + nb * 16 + mr] = relu_c(radd(acc[mb][nb][i], bl[nb]));
+        }
       }
-    }
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) cur[mb] = nxt[mb];
+#ifdef CONV_PROBE_TIMING
+    ++ptiles;
+#endif
   }
+#ifdef CONV_PROBE_TIMING
+  __syncthreads();  // all outputs of this workgroup are stored
+  if (lane == 0) {
+    uint64_t *rec = reinterpret_cast<uint64_t *>(y + ((P * COUT + 1) & ~(int64_t)1)) +
+                    ((int64_t)blockIdx.x * WAVES + wave) * 6;
+    rec[0] = pt0;
+    rec[1] = pt1;
+    rec[2] = wall_clock64();
+    rec[3] = clock64() - pc0;
+    rec[4] = ptiles;
+    uint32_t hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    rec[5] = hw;
+  }
+#endif
+}
+
+// OHWI weights -> MFMA fragment order (the LDS image the conv kernel copies)
+template <int MODE, int KH, int KW, int S, int CIN, int COUT, int HIN, int WIN>
+__global__ __launch_bounds__(256) void k_conv_pack(const float *__restrict__ w, f32x4 *__restrict__ packed) {
+  using Gm = ConvGeom<MODE, KH, KW, S, CIN, COUT, HIN, WIN>;
+  const int sl = blockIdx.x * 256 + threadIdx.x;
+  if (sl < Gm::LDS_F4) packed[sl] = Gm::load_slot(w, sl);
 }
 
 struct ConvLaunch {
-  const void *fn;
+  const void *fn, *pack;
   int waves;
   int lds_bytes;
   int per_cu;  // resident workgroups per CU (occupancy query, cached)
+  int tile_px;  // output pixels per wave tile
 };
 
-template <int MODE, int KH, int KW, int S, int CIN, int COUT, int HIN, int WIN, int WAVES>
+template <int MODE, int KH, int KW, int S, int CIN, int COUT, int HIN, int WIN, int WAVES, int MB>
 static ConvLaunch conv_launch() {
   using Gm = ConvGeom<MODE, KH, KW, S, CIN, COUT, HIN, WIN>;
-  ConvLaunch l{reinterpret_cast<const void *>(&k_conv_bias_relu<MODE, KH, KW, S, CIN, COUT, HIN, WIN, WAVES>), WAVES,
-               Gm::LDS_F4 * 16, 0};
+  ConvLaunch l{reinterpret_cast<const void *>(&k_conv_bias_relu<MODE, KH, KW, S, CIN, COUT, HIN, WIN, WAVES, MB>),
+               reinterpret_cast<const void *>(&k_conv_pack<MODE, KH, KW, S, CIN, COUT, HIN, WIN>), WAVES,
+               Gm::LDS_F4 * 16, 0, 16 * MB};
   int blocks = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, l.fn, WAVES * 64, 0) != hipSuccess || blocks < 1)
     blocks = 1;
   l.per_cu = blocks;
   return l;
 }
+
+#ifndef CONV1_MB
+#define CONV1_MB 1
+#endif
+#ifndef CONV2_MB
+#define CONV2_MB 1
+#endif
+#ifndef CONV3_MB
+#define CONV3_MB 1
+#endif
 
 // the supported geometries (the Nature-DQN torso on 4 x 84 x 84 stacks)
 static bool find_conv(const rth_conv_shape &s, ConvLaunch *out) {
@@ -195,16 +300,16 @@ static bool find_conv(const rth_conv_shape &s, ConvLaunch *out) {
            s.kw == kw && s.stride == st;
   };
   if (is(RTH_CONV_U8_CHW, 4, 84, 84, 32, 8, 8, 4)) {
-    static const ConvLaunch l = conv_launch<RTH_CONV_U8_CHW, 8, 8, 4, 4, 32, 84, 84, 4>();
+    static const ConvLaunch l = conv_launch<RTH_CONV_U8_CHW, 8, 8, 4, 4, 32, 84, 84, 4, CONV1_MB>();
     *out = l;
   } else if (is(RTH_CONV_F32_NHWC, 4, 84, 84, 32, 8, 8, 4)) {
-    static const ConvLaunch l = conv_launch<RTH_CONV_F32_NHWC, 8, 8, 4, 4, 32, 84, 84, 4>();
+    static const ConvLaunch l = conv_launch<RTH_CONV_F32_NHWC, 8, 8, 4, 4, 32, 84, 84, 4, CONV1_MB>();
     *out = l;
   } else if (is(RTH_CONV_F32_NHWC, 32, 20, 20, 64, 4, 4, 2)) {
-    static const ConvLaunch l = conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8>();
+    static const ConvLaunch l = conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB>();
     *out = l;
   } else if (is(RTH_CONV_F32_NHWC, 64, 9, 9, 64, 3, 3, 1)) {
-    static const ConvLaunch l = conv_launch<RTH_CONV_F32_NHWC, 3, 3, 1, 64, 64, 9, 9, 8>();
+    static const ConvLaunch l = conv_launch<RTH_CONV_F32_NHWC, 3, 3, 1, 64, 64, 9, 9, 8, CONV3_MB>();
     *out = l;
   } else {
     return false;
@@ -223,6 +328,15 @@ static int cu_count() {
   return cus;
 }
 
+static int wg_per_cu() {  // RTH_CONV_WG_PER_CU (tuning), default 2
+  static int v = [] {
+    const char *e = getenv("RTH_CONV_WG_PER_CU");
+    const int x = e ? atoi(e) : 2;
+    return x >= 1 && x <= 8 ? x : 2;
+  }();
+  return v;
+}
+
 }  // namespace rth
 
 using namespace rth;
@@ -232,6 +346,23 @@ extern "C" {
 int rth_conv_supported(const rth_conv_shape *shape) {
   ConvLaunch l;
   return shape && find_conv(*shape, &l) ? 1 : 0;
+}
+
+int64_t rth_conv_packed_bytes(const rth_conv_shape *shape) {
+  ConvLaunch l;
+  return shape && find_conv(*shape, &l) ? (int64_t)l.lds_bytes : 0;
+}
+
+int rth_conv_pack(const rth_conv_shape *shape, const float *w, float *packed, void *stream) {
+  RTH_REQUIRE(shape && w && packed, "rth_conv_pack: NULL argument");
+  ConvLaunch l;
+  RTH_REQUIRE(find_conv(*shape, &l), "rth_conv_pack: geometry not built");
+  RTH_REQUIRE(((reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(packed)) & 15) == 0,
+              "rth_conv_pack: misaligned buffer");
+  void *args[] = {(void *)&w, (void *)&packed};
+  const int slots = l.lds_bytes / 16;
+  RTH_HIP(hipLaunchKernel(l.pack, dim3((unsigned)((slots + 255) / 256)), dim3(256), args, 0, as_stream(stream)));
+  return RTH_OK;
 }
 
 int rth_conv_bias_relu(const rth_conv_shape *shape, const void *x, const int64_t *rows, int64_t n, const float *w,
@@ -248,10 +379,12 @@ int rth_conv_bias_relu(const rth_conv_shape *shape, const void *x, const int64_t
               "rth_conv_bias_relu: misaligned buffer");
   if (n == 0) return RTH_OK;
   const int hout = (shape->hin - shape->kh) / shape->stride + 1, wout = (shape->win - shape->kw) / shape->stride + 1;
-  const int64_t tiles = (n * hout * wout + 15) / 16;
+  const int64_t tiles = (n * hout * wout + l.tile_px - 1) / l.tile_px;
   int64_t grid = (tiles + l.waves - 1) / l.waves;
-  const int64_t resident = (int64_t)cu_count() * l.per_cu;
-  if (grid > resident) grid = resident;  // persistent: each workgroup stages W once
+  // persistent: at most wg_per_cu() workgroups per CU (each stages the weights once)
+  const int cap = wg_per_cu();
+  const int64_t resident = (int64_t)cu_count() * (l.per_cu < cap ? l.per_cu : cap);
+  if (grid > resident) grid = resident;
   void *args[] = {(void *)&x, (void *)&rows, (void *)&n, (void *)&w, (void *)&bias, (void *)&y};
   RTH_HIP(hipLaunchKernel(l.fn, dim3((unsigned)grid), dim3(l.waves * 64), args, 0, as_stream(stream)));
   return RTH_OK;

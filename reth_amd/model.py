@@ -81,25 +81,34 @@ class DQNNetwork(nn.Module):
 
     @torch.no_grad()
     def freeze_heads(self):
-        """(re)build the cached merged weights in place (stable storage for graph replay)"""
+        """(re)build the cached merged head weights and packed conv weights in place (stable
+        storage for graph replay): for copies whose parameters change only at refresh points
+        (target sync, actor weight reload)"""
         merged = self._merged_head_weights()
         if getattr(self, "_frozen", None) is None or self._frozen[0].shape != merged[0].shape:
             self._frozen = [t.clone() for t in merged]
         else:
             for dst, src in zip(self._frozen, merged):
                 dst.copy_(src)
+        if self.hwc_features and merged[0].is_cuda:
+            self._frozen_packed = self.pack_convs(out=getattr(self, "_frozen_packed", None))
 
-    def forward_heads(self, x, merged=None, rows=None):
+    def forward_heads(self, x, merged=None, rows=None, packed=None):
         """raw dueling heads [n, A+1].  x: float32 observations (channels-last with
         hwc_features), or -- on the HIP torso -- uint8 frame stacks [m, C, H, W], read as
-        stacks `rows` (an int64 device index, n = rows.numel()) or all m of them"""
+        stacks `rows` (an int64 device index, n = rows.numel()) or all m of them.  merged /
+        packed: the head weights / packed conv weights of this weight version (pack_convs),
+        default the frozen ones, else built now"""
         if not self.dueling:
             raise ValueError("forward_heads needs the dueling network")
+        frozen = getattr(self, "_frozen", None) is not None
         if merged is None:
-            merged = self._frozen if getattr(self, "_frozen", None) is not None else self._merged_head_weights()
+            merged = self._frozen if frozen else self._merged_head_weights()
         w1, b1, w2, b2 = merged
         if self.hwc_features:
-            h = self._features_nhwc(x, rows)
+            if packed is None and frozen:
+                packed = getattr(self, "_frozen_packed", None)
+            h = self._features_nhwc(x, rows, packed)
             h = h.permute(0, 2, 3, 1).reshape(h.shape[0], -1)  # a view of the NHWC activations
         else:
             if x.dtype == torch.uint8 or rows is not None:
@@ -108,7 +117,58 @@ class DQNNetwork(nn.Module):
         h = _LinearReLU.apply(h, w1, b1)
         return torch.addmm(b2, h, w2.t())
 
-    def _features_nhwc(self, x, rows=None):
+    def _convs(self):
+        return [m for m in self.features if isinstance(m, nn.Conv2d)]
+
+    def _torso_shapes(self, x_shape, u8):
+        """per conv (None, rth_conv_shape or None), cached per (input shape, form, hip_conv)"""
+        cache = self.__dict__.setdefault("_shape_cache", {})
+        key = (tuple(x_shape), bool(u8), self.hip_conv)
+        if key not in cache:
+            cache[key] = self._conv_shapes(x_shape, u8)
+        return cache[key]
+
+    def pack_convs(self, u8=None, out=None):
+        """the HIP torso's packed conv weights (rth_conv_pack, fragment order) for the current
+        parameters: [per conv: a device buffer, or None where MIOpen runs the layer].  Built
+        for both conv1 input forms (f32 channels-last and uint8 stacks share conv2/conv3);
+        `out` (a previous result) is refilled in place."""
+        from . import _lib
+
+        convs = self._convs()
+        dev = convs[0].weight.device
+        res = [] if out is None else out
+        forms = [False, True] if u8 is None else [bool(u8)]
+        k = 0
+        for form in forms:
+            for li, (conv, (_, shape)) in enumerate(zip(convs, self._torso_shapes(self.input_shape, form))):
+                if form and li > 0 and len(forms) == 2:
+                    continue  # conv2 / conv3 are the same for both forms
+                if shape is None:
+                    buf = None
+                else:
+                    w = conv.weight.detach()
+                    if not w.is_contiguous(memory_format=torch.channels_last):
+                        w = w.contiguous(memory_format=torch.channels_last)
+                    buf = res[k] if out is not None else torch.empty(
+                        _lib.lib().rth_conv_packed_bytes(_lib.ctypes.byref(shape)) // 4, dtype=torch.float32,
+                        device=dev)
+                    _lib.call("rth_conv_pack", _lib.ctypes.byref(shape), w.data_ptr(), buf.data_ptr(),
+                              _lib.stream_ptr())
+                if out is None:
+                    res.append(buf)
+                k += 1
+        return res
+
+    @staticmethod
+    def _packed_for(packed, li, u8):
+        """packed buffer of conv li for the given conv1 input form (pack_convs layout: both
+        forms [conv1 f32, conv2, conv3, conv1 u8]; one form [conv1, conv2, conv3])"""
+        if li == 0 and u8 and len(packed) > 3:
+            return packed[3]
+        return packed[li]
+
+    def _features_nhwc(self, x, rows=None, packed=None):
         """the conv torso on channels-last activations: each Conv2d -> ReLU is one HIP
         implicit-GEMM launch with the bias and ReLU fused (rth_conv_bias_relu) where the
         geometry is built, else MIOpen + the rth_bias_relu pass; backward: rth_relu_bias_grad
@@ -118,28 +178,31 @@ class DQNNetwork(nn.Module):
         u8 = x.dtype == torch.uint8
         if not u8 and not x.is_contiguous(memory_format=torch.channels_last):
             x = x.contiguous(memory_format=torch.channels_last)
-        convs = [m for m in self.features if isinstance(m, nn.Conv2d)]
+        convs = self._convs()
         if getattr(self, "_ws", None) is None or self._ws[0].device != x.device:
             self._ws = [torch.zeros(_lib.lib().rth_relu_bias_grad_workspace(m.out_channels), dtype=torch.uint8,
                                     device=x.device) for m in convs]
-        if len(getattr(self, "_shapes", ())) != len(convs) or self._shapes[0][0] != (x.shape[1:], u8):
-            self._shapes = self._conv_shapes(x, u8)
+        shapes = self._torso_shapes(x.shape[1:], u8)
+        if packed is None and any(s is not None for _, s in shapes):
+            packed = self.pack_convs(u8)
         for li, (conv, ws) in enumerate(zip(convs, self._ws)):
-            shape = self._shapes[li][1]
+            shape = shapes[li][1]
             if shape is not None:
-                x = _HipConvBiasReLU.apply(x, conv.weight, conv.bias, shape, conv.stride, ws, rows if li == 0 else None)
+                pk = self._packed_for(packed, li, u8)
+                x = _HipConvBiasReLU.apply(x, conv.weight, conv.bias, pk, shape, conv.stride, ws,
+                                           rows if li == 0 else None)
             else:
                 if x.dtype == torch.uint8 or (li == 0 and rows is not None):
                     raise ValueError("uint8 / row-indexed observations need rth_conv_bias_relu's conv1 geometry")
                 x = _ConvBiasReLU.apply(x, conv.weight, conv.bias, conv.stride, ws)
         return x
 
-    def _conv_shapes(self, x, u8):
-        """per conv: ((input shape key), rth_conv_shape or None when MIOpen runs it)"""
+    def _conv_shapes(self, x_shape, u8):
+        """per conv: (None, rth_conv_shape or None when MIOpen runs it)"""
         from . import _lib
 
         out = []
-        c, h, w = x.shape[1:]
+        c, h, w = x_shape
         for li, conv in enumerate(m for m in self.features if isinstance(m, nn.Conv2d)):
             kind = _lib.CONV_U8_CHW if (u8 and li == 0) else _lib.CONV_F32_NHWC
             shp = _lib.ConvShape(kind, c, h, w, conv.out_channels, conv.kernel_size[0], conv.kernel_size[1],
@@ -147,7 +210,7 @@ class DQNNetwork(nn.Module):
             ok = (self.hip_conv and conv.stride[0] == conv.stride[1] and conv.padding == (0, 0)
                   and conv.dilation == (1, 1) and conv.groups == 1
                   and _lib.lib().rth_conv_supported(_lib.ctypes.byref(shp)) == 1)
-            out.append(((x.shape[1:], u8) if li == 0 else None, shp if ok else None))
+            out.append((None, shp if ok else None))
             c, h, w = conv.out_channels, (h - conv.kernel_size[0]) // conv.stride[0] + 1, \
                 (w - conv.kernel_size[1]) // conv.stride[1] + 1
         return out
@@ -250,7 +313,7 @@ class _HipConvBiasReLU(torch.autograd.Function):
     input is widened to the f32 channels-last batch it stands for)."""
 
     @staticmethod
-    def forward(ctx, x, w, b, shape, stride, ws, rows):
+    def forward(ctx, x, w, b, packed, shape, stride, ws, rows):
         from ._lib import call, ctypes, ptr, stream_ptr
 
         n = rows.numel() if rows is not None else x.shape[0]
@@ -258,9 +321,8 @@ class _HipConvBiasReLU(torch.autograd.Function):
         wo = (shape.win - shape.kw) // shape.stride + 1
         y = torch.empty((n, shape.cout, ho, wo), dtype=torch.float32, device=x.device,
                         memory_format=torch.channels_last)
-        if not w.is_contiguous(memory_format=torch.channels_last):
-            w = w.contiguous(memory_format=torch.channels_last)
-        call("rth_conv_bias_relu", ctypes.byref(shape), ptr(x), ptr(rows), n, ptr(w), ptr(b), ptr(y), stream_ptr())
+        call("rth_conv_bias_relu", ctypes.byref(shape), ptr(x), ptr(rows), n, ptr(packed), ptr(b), ptr(y),
+             stream_ptr())
         ctx.save_for_backward(x, w, y, rows)
         ctx.stride, ctx.ws = list(stride), ws
         return y
@@ -270,6 +332,8 @@ class _HipConvBiasReLU(torch.autograd.Function):
         from ._lib import call, ptr, stream_ptr
 
         x, w, y, rows = ctx.saved_tensors
+        if not w.is_contiguous(memory_format=torch.channels_last):
+            w = w.contiguous(memory_format=torch.channels_last)
         if x.dtype == torch.uint8:
             x = (x if rows is None else x[rows]).float().contiguous(memory_format=torch.channels_last)
         if not g.is_contiguous(memory_format=torch.channels_last):
@@ -281,7 +345,7 @@ class _HipConvBiasReLU(torch.autograd.Function):
         need_x = ctx.needs_input_grad[0]
         gx, gw, _ = torch.ops.aten.convolution_backward(gy, x, w, None, ctx.stride, [0, 0], [1, 1], False, [0, 0], 1,
                                                         [need_x, ctx.needs_input_grad[1], False])
-        return gx, gw, db, None, None, None, None
+        return gx, gw, db, None, None, None, None, None
 
 
 class MLP_DQNNetwork(nn.Module):

@@ -200,14 +200,14 @@ class DQNSolver(Algorithm):
         return (torch.is_tensor(x) and x.dtype == torch.uint8 and x.is_cuda and self._heads
                 and getattr(net, "hwc_features", False) and getattr(net, "hip_conv", False))
 
-    def _forward_targets(self, s1, merged=None):
+    def _forward_targets(self, s1, merged=None, packed=None):
         with torch.no_grad():
             if self._heads:  # raw dueling heads; the TD kernel forms Q
                 q1t = self.target_q_network.forward_heads(s1)
                 q1o = None
                 if self.double_q:
                     m = [t.detach() for t in merged] if merged is not None else None
-                    q1o = self.q_network.forward_heads(s1, m)
+                    q1o = self.q_network.forward_heads(s1, m, packed=packed)
             else:
                 q1t = self.target_q_network(s1)
                 q1o = self.q_network(s1) if self.double_q else None
@@ -229,13 +229,17 @@ class DQNSolver(Algorithm):
     def compute_grads(self, batch, weights=None):
         """dqn_solver.py:104-117: forward passes, fused TD/Huber, backward -> |td| (device)"""
         s0, a, r, s1, done = self._tensors(batch)
-        merged = None
-        if self._heads:  # merged dueling head weights, built once and shared by both online passes
+        merged = packed = None
+        if self._heads:  # merged dueling head weights (and packed conv weights of the HIP torso),
+            # built once per weight version and shared by both online passes
             merged = self.q_network._merged_head_weights()
-            q0 = self.q_network.forward_heads(s0, merged)
+            if getattr(self.q_network, "hwc_features", False) and merged[0].is_cuda:
+                with torch.no_grad():
+                    packed = self.q_network.pack_convs()
+            q0 = self.q_network.forward_heads(s0, merged, packed=packed)
         else:
             q0 = self.q_network(s0)
-        q1o, q1t = self._forward_targets(s1, merged)
+        q1o, q1t = self._forward_targets(s1, merged, packed)
         isw = None if weights is None else (weights if torch.is_tensor(weights) else torch.as_tensor(np.asarray(weights)))
         loss, td_abs = td_huber_loss(q0, q1o, q1t, a, r, done, isw, self.gamma_n, self.double_q, self._heads)
         # grads set to None: backward hands each parameter its gradient buffer directly

@@ -26,7 +26,7 @@ def timeit(fn, iters=50):
     return e0.elapsed_time(e1) / iters * 1000.0
 
 
-for n in (512, 768, 1536):
+for n in [int(v) for v in os.environ.get("CONV_NS", "512,768,1536").split(",")]:
     for li, (cin, h, w, cout, k, s) in enumerate(GEOMS):
         x = torch.randn((n, cin, h, w), device=dev).contiguous(memory_format=torch.channels_last)
         wt = (torch.randn((cout, cin, k, k), device=dev) * 0.05).contiguous(memory_format=torch.channels_last)
@@ -41,8 +41,15 @@ for n in (512, 768, 1536):
 
         shp = _lib.ConvShape(_lib.CONV_F32_NHWC, cin, h, w, cout, k, k, s)
 
+        def packed(shape):
+            pk = torch.empty(_lib.lib().rth_conv_packed_bytes(_lib.ctypes.byref(shape)) // 4, device=dev)
+            _lib.call("rth_conv_pack", _lib.ctypes.byref(shape), wt.data_ptr(), pk.data_ptr(), _lib.stream_ptr())
+            return pk
+
+        pk = packed(shp)
+
         def ours():
-            _lib.call("rth_conv_bias_relu", _lib.ctypes.byref(shp), x.data_ptr(), None, n, wt.data_ptr(), b.data_ptr(),
+            _lib.call("rth_conv_bias_relu", _lib.ctypes.byref(shp), x.data_ptr(), None, n, pk.data_ptr(), b.data_ptr(),
                       y.data_ptr(), _lib.stream_ptr())
 
         tm, to = timeit(miopen), timeit(ours)
@@ -51,10 +58,11 @@ for n in (512, 768, 1536):
             st = torch.randint(0, 256, (n, 4, 84, 84), dtype=torch.uint8, device=dev)
             rows = torch.randperm(n, device=dev)
             shu = _lib.ConvShape(_lib.CONV_U8_CHW, cin, h, w, cout, k, k, s)
+            pku = packed(shu)
 
             def ours_u8():
                 _lib.call("rth_conv_bias_relu", _lib.ctypes.byref(shu), st.data_ptr(), rows.data_ptr(), n,
-                          wt.data_ptr(), b.data_ptr(), y.data_ptr(), _lib.stream_ptr())
+                          pku.data_ptr(), b.data_ptr(), y.data_ptr(), _lib.stream_ptr())
 
             tu = timeit(ours_u8)
             line += f"  ours-u8 {tu:7.1f} us ({flops / tu / 1e6:6.1f} TF)"

@@ -42,6 +42,16 @@ for step in "$@"; do
     prio) for pr in 0 -1; do RTH_LEARNER_PRIORITY=$pr run bench_prio$pr 600 python bench.py --steps 200 --warmup 20 --no-cpu-baseline; done ;;
     convt) run pytest_conv 600 python -m pytest tests/test_conv_gpu.py -q -rf -x ;;
     convb) run bench_conv 300 python scripts/bench_conv.py ;;
+    convv) for v in build/variants/*.so; do b=$(basename $v .so); RTH_LIB_PATH=$PWD/$v run bench_conv_$b 300 python scripts/bench_conv.py; done ;;
+    convprof) export TMPDIR=/tmp; run prof_conv 300 rocprofv3 --kernel-trace --output-format csv \
+            -d "$PWD/gpurun_out/prof_conv" -o run -- python scripts/bench_conv.py ;;
+    convtime) RTH_LIB_PATH=$PWD/build/variants/timing.so run conv_timing 300 python scripts/conv_timing.py ;;
+    convpmc) export TMPDIR=/tmp
+         run pmc_conv_a 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+            SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT --kernel-trace --output-format csv \
+            -d "$PWD/gpurun_out/pmc_conv_a" -o run -- python scripts/conv_pmc.py &&
+         run pmc_conv_b 300 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM \
+            --kernel-trace --output-format csv -d "$PWD/gpurun_out/pmc_conv_b" -o run -- python scripts/conv_pmc.py ;;
     probe) run probe 300 python scripts/probe_qnet.py ;;
     variants2)
       run bench_eager 600 python bench.py --steps 100 --warmup 20 --no-cpu-baseline --eager

@@ -24,8 +24,11 @@ def _run(shape, x, rows, n, w, b, dev):
     wo = (shape.win - shape.kw) // shape.stride + 1
     y = torch.full((n, ho, wo, shape.cout), float("nan"), device=dev)
     wt = w.to(dev).contiguous(memory_format=torch.channels_last)
+    pk = torch.full((_lib.lib().rth_conv_packed_bytes(_lib.ctypes.byref(shape)) // 4,), float("nan"), device=dev)
+    _lib.call("rth_conv_pack", _lib.ctypes.byref(shape), wt.data_ptr(), pk.data_ptr(), _lib.stream_ptr())
+    assert not torch.isnan(pk).any()  # every fragment slot written
     _lib.call("rth_conv_bias_relu", _lib.ctypes.byref(shape), x.data_ptr(), None if rows is None else rows.data_ptr(),
-              n, wt.data_ptr(), b.to(dev).data_ptr(), y.data_ptr(), _lib.stream_ptr())
+              n, pk.data_ptr(), b.to(dev).data_ptr(), y.data_ptr(), _lib.stream_ptr())
     return y.permute(0, 3, 1, 2).cpu()
 
 
@@ -85,6 +88,8 @@ def test_conv_empty_and_unsupported(dev):
               y.data_ptr(), _lib.stream_ptr())
     bad = _shape(_lib.CONV_F32_NHWC, 3, 84, 84, 32, 8, 4)
     assert _lib.lib().rth_conv_supported(_lib.ctypes.byref(bad)) == 0
+    assert _lib.lib().rth_conv_packed_bytes(_lib.ctypes.byref(bad)) == 0
+    assert _lib.lib().rth_conv_packed_bytes(_lib.ctypes.byref(shape)) == 64 * 32 * 16 * 4
     with pytest.raises(_lib.RethHipError, match="not built"):
         _lib.call("rth_conv_bias_relu", _lib.ctypes.byref(bad), x.data_ptr(), None, 1, w.data_ptr(), w.data_ptr(),
                   y.data_ptr(), _lib.stream_ptr())
@@ -97,6 +102,27 @@ def _torso_net(dev, seed=0):
     net = DQNNetwork((4, 84, 84), 6).to(dev, memory_format=torch.channels_last)
     net.hwc_features = True
     return net
+
+
+def test_frozen_packed_weights_follow_refresh(dev):
+    """a frozen copy's packed conv weights (and merged heads) are rebuilt by freeze_heads
+    (target sync / actor reload) and used by default; stale until then (biases of the conv
+    layers are read live)"""
+    net = _torso_net(dev, seed=2)
+    x = torch.randint(0, 256, (8, 4, 84, 84), dtype=torch.uint8, device=dev)
+    with torch.no_grad():
+        net.freeze_heads()
+        q0 = net.forward_heads(x)
+        for name, p in net.named_parameters():
+            if name.endswith("weight"):
+                p.mul_(1.01)
+        q_stale = net.forward_heads(x)
+        net.freeze_heads()
+        q1 = net.forward_heads(x)
+        q_fresh = net.forward_heads(x, net._merged_head_weights(), packed=net.pack_convs())
+    assert torch.equal(q0, q_stale)
+    assert not torch.equal(q0, q1)
+    torch.testing.assert_close(q1, q_fresh, rtol=0, atol=0)
 
 
 def test_forward_heads_u8_rows_matches_miopen(dev):

@@ -216,7 +216,7 @@ class ApexDQN:
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
         split = solver.grad_hook is not None
-        G = dict(act=[], act_out=[], learn=[], learn_td=[], apply=[], grads=[])
+        G = dict(act=[], act_out=[], tgt=[], q1t=[], learn={}, learn_td={}, apply={}, grads={})
         with torch.cuda.stream(side):
             # the actor block by push parity (fused_actor alternates row sets; both graphs
             # are identical otherwise)
@@ -229,22 +229,32 @@ class ApexDQN:
             if host[1] % 2:  # keep G["act"][k] <-> pushes % 2 == k
                 G["act"].reverse()
                 G["act_out"].reverse()
+            # the target network's output on each slot's s1, computed on the actor stream ahead
+            # of the update (target_heads); "pre" learner graphs consume it, "full" ones
+            # compute it themselves (after a target sync, and before any was precomputed)
             for p in range(2):
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, stream=side):
-                    data, idx, isw = slots[p]
-                    td = solver.compute_grads(data, isw)
-                    self.trainer._track(td)
-                    if not split:
-                        solver.apply_grads()
-                G["learn"].append(g)
-                G["learn_td"].append(td)
-                if split:  # the gradients live in this graph's pool: all-reduce and apply THESE
-                    G["grads"].append([q.grad for q in solver._params])
-                    ga = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(ga, stream=side):
-                        solver.apply_grads()
-                    G["apply"].append(ga)
+                    q1t = solver.target_heads(slots[p][0][3])
+                G["tgt"].append(g)
+                G["q1t"].append(q1t)
+            for variant in ("full", "pre"):
+                for p in range(2):
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, stream=side):
+                        data, idx, isw = slots[p]
+                        td = solver.compute_grads(data, isw, q1t=G["q1t"][p] if variant == "pre" else None)
+                        self.trainer._track(td)
+                        if not split:
+                            solver.apply_grads()
+                    G["learn"][variant, p] = g
+                    G["learn_td"][variant, p] = td
+                    if split:  # the gradients live in this graph's pool: all-reduce and apply THESE
+                        G["grads"][variant, p] = [q.grad for q in solver._params]
+                        ga = torch.cuda.CUDAGraph()
+                        with torch.cuda.graph(ga, stream=side):
+                            solver.apply_grads()
+                        G["apply"][variant, p] = ga
         torch.cuda.current_stream(self.device).wait_stream(side)
         self.actors.t, self.actors.pushes = host  # capture recorded, did not run, the step
         self._graphs = G
@@ -269,12 +279,13 @@ class ApexDQN:
                 act.append(self.replay, td)
             self.env_steps += act.N
         k = self.loader._pending.pop(0)
-        G["learn"][k].replay()
+        v = ("full", k)
+        G["learn"][v].replay()
         if G["apply"]:
-            self.solver.grad_hook(self.solver._params, grads=G["grads"][k])  # RCCL all-reduce, eager
-            G["apply"][k].replay()
+            self.solver.grad_hook(self.solver._params, grads=G["grads"][v])  # RCCL all-reduce, eager
+            G["apply"][v].replay()
         self.loader.issue()  # sample-ahead into the other slot
-        self.replay.update_priorities(self.loader._slots[k][1], G["learn_td"][k], step=True, deferred=True)
+        self.replay.update_priorities(self.loader._slots[k][1], G["learn_td"][v], step=True, deferred=True)
         self._learner_host()
 
     def _actor_block_graph(self):
@@ -294,6 +305,12 @@ class ApexDQN:
                 act.append(self.replay, td)
             self.env_steps += act.N
 
+    def _next_learner_variant(self):
+        """graph key of the next replayed learner step: (full | pre, batch slot)"""
+        k = self.loader._pending[0]
+        ready = getattr(self, "_q1t_ready", None)
+        return ("pre" if self.cfg.overlap and ready is not None and ready[k] else "full", k)
+
     def _iteration_graph_overlap(self):
         """The actor block (stream A: act + env + n-step + append, then the sample of batch
         k+1) runs concurrently with the learner block of batch k (stream B: forward/backward,
@@ -310,18 +327,28 @@ class ApexDQN:
             self._ev_sample = torch.cuda.Event()
             self._ev_sample.record(A)  # batch k was sampled on A before the first overlapped step
             self._ev_learn.record(A)
+            self._q1t_ready = [False, False]  # per slot: its target pass was precomputed on A
         B = self._stream_b
         A.wait_event(self._ev_learn)
         self._actor_block_graph()  # on A (the caller's stream)
         k = self.loader._pending.pop(0)
+        v = ("pre" if self._q1t_ready[k] else "full", k)
+        self._q1t_ready[k] = False
+        syncs = self.solver._target_syncs
         with torch.cuda.stream(B):
             B.wait_event(self._ev_sample)
-            G["learn"][k].replay()
+            G["learn"][v].replay()
             if G["apply"]:
-                self.solver.grad_hook(self.solver._params, grads=G["grads"][k])  # RCCL all-reduce on B
-                G["apply"][k].replay()
+                self.solver.grad_hook(self.solver._params, grads=G["grads"][v])  # RCCL all-reduce on B
+                G["apply"][v].replay()
             self._learner_host()  # target sync / weights publish copies: on B
             self._ev_learn.record(B)
         self.loader.issue()  # sample-ahead into the other slot (on A, after this step's append)
+        if self.solver._target_syncs == syncs:
+            # no target sync in this step: the next batch's target pass runs here on A,
+            # concurrently with the learner (the target weights do not change before it is used)
+            kn = self.loader._pending[-1]
+            G["tgt"][kn].replay()
+            self._q1t_ready[kn] = True
         self._ev_sample.record(A)
-        self.replay.update_priorities(self.loader._slots[k][1], G["learn_td"][k], step=True, deferred=True)
+        self.replay.update_priorities(self.loader._slots[k][1], G["learn_td"][v], step=True, deferred=True)

@@ -169,6 +169,7 @@ class DQNSolver(Algorithm):
     @torch.no_grad()
     def update_target(self):
         """target <- online (:65-66), one fused device copy (+ the target's merged heads)"""
+        self._target_syncs = getattr(self, "_target_syncs", 0) + 1
         torch._foreach_copy_(self._tparams, self._params)
         if self._heads:
             self.target_q_network.freeze_heads()
@@ -200,16 +201,27 @@ class DQNSolver(Algorithm):
         return (torch.is_tensor(x) and x.dtype == torch.uint8 and x.is_cuda and self._heads
                 and getattr(net, "hwc_features", False) and getattr(net, "hip_conv", False))
 
-    def _forward_targets(self, s1, merged=None, packed=None):
+    def target_heads(self, s1):
+        """the target network's output on s1 (raw dueling heads with the HIP TD kernel): a
+        function of the target weights only, so it may be computed ahead of the update that
+        consumes it as long as no target sync falls in between (compute_grads(q1t=...))"""
+        if not self._u8_frames(s1):
+            s1 = (s1 if torch.is_tensor(s1) else torch.as_tensor(np.asarray(s1))).to(self.device, torch.float32)
+        with torch.no_grad():
+            return self.target_q_network.forward_heads(s1) if self._heads else self.target_q_network(s1)
+
+    def _forward_targets(self, s1, merged=None, packed=None, q1t=None):
         with torch.no_grad():
             if self._heads:  # raw dueling heads; the TD kernel forms Q
-                q1t = self.target_q_network.forward_heads(s1)
+                if q1t is None:
+                    q1t = self.target_q_network.forward_heads(s1)
                 q1o = None
                 if self.double_q:
                     m = [t.detach() for t in merged] if merged is not None else None
                     q1o = self.q_network.forward_heads(s1, m, packed=packed)
             else:
-                q1t = self.target_q_network(s1)
+                if q1t is None:
+                    q1t = self.target_q_network(s1)
                 q1o = self.q_network(s1) if self.double_q else None
         return q1o, q1t
 
@@ -226,8 +238,10 @@ class DQNSolver(Algorithm):
     def calc_loss(self, batch):
         return self.calc_loss_device(batch).cpu()
 
-    def compute_grads(self, batch, weights=None):
-        """dqn_solver.py:104-117: forward passes, fused TD/Huber, backward -> |td| (device)"""
+    def compute_grads(self, batch, weights=None, q1t=None):
+        """dqn_solver.py:104-117: forward passes, fused TD/Huber, backward -> |td| (device).
+        q1t: the target network's output on this batch's s1 if already computed
+        (target_heads), else it is computed here"""
         s0, a, r, s1, done = self._tensors(batch)
         merged = packed = None
         if self._heads:  # merged dueling head weights (and packed conv weights of the HIP torso),
@@ -239,7 +253,7 @@ class DQNSolver(Algorithm):
             q0 = self.q_network.forward_heads(s0, merged, packed=packed)
         else:
             q0 = self.q_network(s0)
-        q1o, q1t = self._forward_targets(s1, merged, packed)
+        q1o, q1t = self._forward_targets(s1, merged, packed, q1t)
         isw = None if weights is None else (weights if torch.is_tensor(weights) else torch.as_tensor(np.asarray(weights)))
         loss, td_abs = td_huber_loss(q0, q1o, q1t, a, r, done, isw, self.gamma_n, self.double_q, self._heads)
         # grads set to None: backward hands each parameter its gradient buffer directly
@@ -261,9 +275,9 @@ class DQNSolver(Algorithm):
         if self.auto_target_update and self._update_target_interval is not None:
             self._update_target_interval()
 
-    def update_device(self, batch, weights=None):
+    def update_device(self, batch, weights=None, q1t=None):
         """DQNSolver.update (:104-124) returning |td| as a device tensor (no host sync)."""
-        td_abs = self.compute_grads(batch, weights)
+        td_abs = self.compute_grads(batch, weights, q1t)
         if self.grad_hook is not None:
             self.grad_hook(self._params)
         self.apply_grads()

@@ -70,24 +70,27 @@ def test_graph_split_learner_applies_its_own_gradients(dev):
     from reth_amd.apex import ApexConfig, ApexDQN
 
     cfg = ApexConfig(n_actors=16, capacity=1024, batch_size=32, sample_start=64, seed=4, hip_graph=True,
-                     dp_hook=True)
+                     dp_hook=True, update_target_interval=3)
     ax = ApexDQN(cfg, device=dev)
     for _ in range(30):
         ax.iteration()
     G = ax._graphs
-    assert G is not None and len(G["apply"]) == 2
-    ptrs = [{t.data_ptr() for t in G["grads"][p]} for p in range(2)]
-    assert not (ptrs[0] & ptrs[1])
+    assert G is not None and len(G["apply"]) == 4  # (full | pre target pass) x batch parity
+    ptrs = [{t.data_ptr() for t in G["grads"][v]} for v in G["grads"]]
+    assert all(not (ptrs[i] & ptrs[j]) for i in range(4) for j in range(i))
     opt, params = ax.solver.optimizer, ax.solver._params
-    for _ in range(2):  # both parities
+    seen = set()
+    for _ in range(4):  # both parities, both variants
         torch.cuda.synchronize()  # ax runs on its own stream
-        k = ax.loader._pending[0]
+        v = ax._next_learner_variant()
+        seen.add(v)
         before = [opt.state[p]["exp_avg"].clone() for p in params]
         ax.iteration()
         torch.cuda.synchronize()
         coef = min(cfg.clip_value / (float(opt.total_norm[0]) + 1e-6), 1.0)
-        for p, mb, g in zip(params, before, G["grads"][k]):
+        for p, mb, g in zip(params, before, G["grads"][v]):
             torch.testing.assert_close(opt.state[p]["exp_avg"], mb + 0.1 * (g * coef - mb), rtol=1e-5, atol=1e-9)
+    assert {v[1] for v in seen} == {0, 1} and ("pre", 0) in seen or ("pre", 1) in seen
     ax.close()
 
 
@@ -126,4 +129,33 @@ def test_graph_replay_learns(dev):
     assert ax.subscriber.loaded_version > 0
     assert all(torch.isfinite(p).all() for p in ax.solver.q_network.parameters())
     assert int(ax.actors.t_dev.item()) == ax.actors.t == 50
+    ax.close()
+
+
+def test_target_pass_precompute_respects_target_syncs(dev):
+    """overlapped graph mode computes the next batch's target pass on the actor stream
+    ("pre" learner graphs) except right after a target sync, where the learner computes it
+    itself ("full"); a precomputed pass equals the target network's output on that batch"""
+    from reth_amd.apex import ApexConfig, ApexDQN
+
+    cfg = ApexConfig(n_actors=16, capacity=1024, batch_size=32, sample_start=64, seed=5, hip_graph=True,
+                     update_target_interval=4)
+    ax = ApexDQN(cfg, device=dev)
+    while ax._graphs is None:
+        ax.iteration()
+    log = []
+    for _ in range(16):
+        v = ax._next_learner_variant()
+        syncs = ax.solver._target_syncs
+        ax.iteration()
+        torch.cuda.synchronize()
+        synced = ax.solver._target_syncs != syncs
+        if v[0] == "pre" and not synced:  # the target weights are still the ones it used
+            s1 = ax.loader._slots[v[1]][0][3]
+            torch.testing.assert_close(ax._graphs["q1t"][v[1]], ax.solver.target_heads(s1), rtol=0, atol=0)
+        log.append((v[0], synced))
+    assert any(s for _, s in log) and any(v == "pre" for v, _ in log)
+    for (_, synced), (v_next, _) in zip(log, log[1:]):
+        if synced:
+            assert v_next == "full"
     ax.close()

@@ -315,6 +315,9 @@ typedef struct rth_conv_shape {
 int rth_conv_supported(const rth_conv_shape *shape);
 int64_t rth_conv_packed_bytes(const rth_conv_shape *shape);
 int rth_conv_pack(const rth_conv_shape *shape, const float *w_ohwi_dev, float *packed_dev, void *stream);
+/* rth_conv_pack for n <= 4 layers in one launch (a network's torso, both conv1 forms) */
+int rth_conv_pack_many(int32_t n, const rth_conv_shape *shapes, const float *const *w_ohwi_dev,
+                       float *const *packed_dev, void *stream);
 int rth_conv_bias_relu(const rth_conv_shape *shape, const void *x_dev, const int64_t *rows_dev, int64_t n,
                        const float *packed_dev, const float *bias_dev, float *y_dev, void *stream);
 

@@ -262,6 +262,34 @@ __global__ __launch_bounds__(256) void k_conv_pack(const float *__restrict__ w, 
   if (sl < Gm::LDS_F4) packed[sl] = Gm::load_slot(w, sl);
 }
 
+// several layers in one launch (a network's torso): block ranges per layer
+constexpr int kPackMax = 4;
+struct PackJob {
+  int geom[kPackMax];  // index into the built geometries (find_conv order)
+  const float *w[kPackMax];
+  f32x4 *packed[kPackMax];
+  int first_block[kPackMax + 1];
+  int n;
+};
+
+template <int MODE, int KH, int KW, int S, int CIN, int COUT, int HIN, int WIN>
+__device__ __forceinline__ void pack_one(const float *w, f32x4 *packed, int sl) {
+  using Gm = ConvGeom<MODE, KH, KW, S, CIN, COUT, HIN, WIN>;
+  if (sl < Gm::LDS_F4) packed[sl] = Gm::load_slot(w, sl);
+}
+
+__global__ __launch_bounds__(256) void k_conv_pack_many(PackJob job) {
+  int l = 0;
+  while (l + 1 < job.n && (int)blockIdx.x >= job.first_block[l + 1]) ++l;
+  const int sl = ((int)blockIdx.x - job.first_block[l]) * 256 + threadIdx.x;
+  switch (job.geom[l]) {
+    case 0: pack_one<RTH_CONV_U8_CHW, 8, 8, 4, 4, 32, 84, 84>(job.w[l], job.packed[l], sl); break;
+    case 1: pack_one<RTH_CONV_F32_NHWC, 8, 8, 4, 4, 32, 84, 84>(job.w[l], job.packed[l], sl); break;
+    case 2: pack_one<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20>(job.w[l], job.packed[l], sl); break;
+    default: pack_one<RTH_CONV_F32_NHWC, 3, 3, 1, 64, 64, 9, 9>(job.w[l], job.packed[l], sl); break;
+  }
+}
+
 struct ConvLaunch {
   const void *fn, *pack;
   int waves;
@@ -294,7 +322,7 @@ static ConvLaunch conv_launch() {
 #endif
 
 // the supported geometries (the Nature-DQN torso on 4 x 84 x 84 stacks)
-static bool find_conv(const rth_conv_shape &s, ConvLaunch *out) {
+static bool find_conv(const rth_conv_shape &s, ConvLaunch *out, int *geom = nullptr) {
   auto is = [&](int mode, int cin, int hin, int win, int cout, int kh, int kw, int st) {
     return s.input == mode && s.cin == cin && s.hin == hin && s.win == win && s.cout == cout && s.kh == kh &&
            s.kw == kw && s.stride == st;
@@ -302,15 +330,19 @@ static bool find_conv(const rth_conv_shape &s, ConvLaunch *out) {
   if (is(RTH_CONV_U8_CHW, 4, 84, 84, 32, 8, 8, 4)) {
     static const ConvLaunch l = conv_launch<RTH_CONV_U8_CHW, 8, 8, 4, 4, 32, 84, 84, 4, CONV1_MB>();
     *out = l;
+    if (geom) *geom = 0;
   } else if (is(RTH_CONV_F32_NHWC, 4, 84, 84, 32, 8, 8, 4)) {
     static const ConvLaunch l = conv_launch<RTH_CONV_F32_NHWC, 8, 8, 4, 4, 32, 84, 84, 4, CONV1_MB>();
     *out = l;
+    if (geom) *geom = 1;
   } else if (is(RTH_CONV_F32_NHWC, 32, 20, 20, 64, 4, 4, 2)) {
     static const ConvLaunch l = conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB>();
     *out = l;
+    if (geom) *geom = 2;
   } else if (is(RTH_CONV_F32_NHWC, 64, 9, 9, 64, 3, 3, 1)) {
     static const ConvLaunch l = conv_launch<RTH_CONV_F32_NHWC, 3, 3, 1, 64, 64, 9, 9, 8, CONV3_MB>();
     *out = l;
+    if (geom) *geom = 3;
   } else {
     return false;
   }
@@ -362,6 +394,30 @@ int rth_conv_pack(const rth_conv_shape *shape, const float *w, float *packed, vo
   void *args[] = {(void *)&w, (void *)&packed};
   const int slots = l.lds_bytes / 16;
   RTH_HIP(hipLaunchKernel(l.pack, dim3((unsigned)((slots + 255) / 256)), dim3(256), args, 0, as_stream(stream)));
+  return RTH_OK;
+}
+
+int rth_conv_pack_many(int32_t n, const rth_conv_shape *shapes, const float *const *w, float *const *packed,
+                       void *stream) {
+  RTH_REQUIRE(n >= 0 && n <= kPackMax && (n == 0 || (shapes && w && packed)), "rth_conv_pack_many: bad arguments");
+  PackJob job{};
+  job.n = n;
+  int blocks = 0;
+  for (int l = 0; l < n; ++l) {
+    ConvLaunch cl;
+    RTH_REQUIRE(find_conv(shapes[l], &cl, &job.geom[l]), "rth_conv_pack_many: layer %d geometry not built", l);
+    RTH_REQUIRE(w[l] && packed[l] && ((reinterpret_cast<uintptr_t>(w[l]) | reinterpret_cast<uintptr_t>(packed[l])) &
+                                      15) == 0,
+                "rth_conv_pack_many: layer %d buffer NULL or misaligned", l);
+    job.w[l] = w[l];
+    job.packed[l] = reinterpret_cast<f32x4 *>(packed[l]);
+    job.first_block[l] = blocks;
+    blocks += (cl.lds_bytes / 16 + 255) / 256;
+  }
+  job.first_block[n] = blocks;
+  if (n == 0) return RTH_OK;
+  hipLaunchKernelGGL(k_conv_pack_many, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), job);
+  RTH_LAUNCHED();
   return RTH_OK;
 }
 

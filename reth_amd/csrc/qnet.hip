@@ -124,73 +124,89 @@ struct HeadsDims {
   int32_t C, P;     // feature map channels and H*W positions (C = 0: no permutation)
 };
 
-__device__ __forceinline__ int64_t chw_col(const HeadsDims &d, int64_t j) {  // merged column -> reference column
-  if (d.C == 0) return j;
-  const int64_t p = j / d.C, c = j - p * d.C;
-  return c * d.P + p;
+
+// One workgroup per FC1 row (2H rows) + one for the small tail (b1, w2, b2).  A row of the
+// NHWC-permuted FC1 weight is a C x P -> P x C transpose of the reference row, done through
+// LDS so both the HBM reads and the writes are coalesced.
+__global__ __launch_bounds__(256) void k_heads_merge(HeadsDims d, const float *__restrict__ wa1,
+                                                     const float *__restrict__ wv1, const float *__restrict__ ba1,
+                                                     const float *__restrict__ bv1, const float *__restrict__ wa2,
+                                                     const float *__restrict__ wv2, const float *__restrict__ ba2,
+                                                     const float *__restrict__ bv2, float *__restrict__ w1,
+                                                     float *__restrict__ b1, float *__restrict__ w2,
+                                                     float *__restrict__ b2) {
+  extern __shared__ float row[];
+  const int64_t r = blockIdx.x, F = d.F;
+  if (r < 2 * d.H) {
+    const float *src = (r < d.H ? wa1 : wv1) + (r % d.H) * F;
+    float *dst = w1 + r * F;
+    if (d.C == 0) {
+      for (int64_t i = threadIdx.x; i < F; i += blockDim.x) dst[i] = src[i];
+      return;
+    }
+    for (int64_t i = threadIdx.x; i < F; i += blockDim.x) row[i] = src[i];  // reference order c * P + p
+    __syncthreads();
+    for (int64_t j = threadIdx.x; j < F; j += blockDim.x) {  // merged order p * C + c
+      const int p = (int)(j / d.C), c = (int)(j - (int64_t)p * d.C);
+      dst[j] = row[c * d.P + p];
+    }
+    return;
+  }
+  const int64_t H2 = 2 * d.H, A1 = d.A + 1;
+  for (int64_t k = threadIdx.x; k < H2; k += blockDim.x) b1[k] = k < d.H ? ba1[k] : bv1[k - d.H];
+  for (int64_t k = threadIdx.x; k < A1 * H2; k += blockDim.x) {
+    const int64_t rr = k / H2, j = k - rr * H2;
+    float v = 0.0f;
+    if (rr < d.A && j < d.H) v = wa2[rr * d.H + j];
+    if (rr == d.A && j >= d.H) v = wv2[j - d.H];
+    w2[k] = v;
+  }
+  for (int64_t k = threadIdx.x; k < A1; k += blockDim.x) b2[k] = k < d.A ? ba2[k] : bv2[0];
 }
 
-__global__ void k_heads_merge(HeadsDims d, const float *__restrict__ wa1, const float *__restrict__ wv1,
-                              const float *__restrict__ ba1, const float *__restrict__ bv1,
-                              const float *__restrict__ wa2, const float *__restrict__ wv2,
-                              const float *__restrict__ ba2, const float *__restrict__ bv2, float *__restrict__ w1,
-                              float *__restrict__ b1, float *__restrict__ w2, float *__restrict__ b2) {
-  const int64_t n1 = 2 * d.H * d.F, n2 = n1 + 2 * d.H, n3 = n2 + (d.A + 1) * 2 * d.H, n4 = n3 + d.A + 1;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n4; e += stride) {
-    if (e < n1) {
-      const int64_t r = e / d.F, j = e - r * d.F;
-      const int64_t src = (r % d.H) * d.F + chw_col(d, j);
-      w1[e] = r < d.H ? wa1[src] : wv1[src];
-    } else if (e < n2) {
-      const int64_t r = e - n1;
-      b1[r] = r < d.H ? ba1[r] : bv1[r - d.H];
-    } else if (e < n3) {
-      const int64_t k = e - n2, r = k / (2 * d.H), j = k - r * 2 * d.H;
-      float v = 0.0f;
-      if (r < d.A && j < d.H) v = wa2[r * d.H + j];
-      if (r == d.A && j >= d.H) v = wv2[j - d.H];
-      w2[k] = v;
+__global__ __launch_bounds__(256) void k_heads_split_grad(HeadsDims d, const float *__restrict__ gw1,
+                                                          const float *__restrict__ gb1,
+                                                          const float *__restrict__ gw2,
+                                                          const float *__restrict__ gb2, float *__restrict__ gwa1,
+                                                          float *__restrict__ gwv1, float *__restrict__ gba1,
+                                                          float *__restrict__ gbv1, float *__restrict__ gwa2,
+                                                          float *__restrict__ gwv2, float *__restrict__ gba2,
+                                                          float *__restrict__ gbv2) {
+  extern __shared__ float row[];
+  const int64_t r = blockIdx.x, F = d.F;
+  if (r < 2 * d.H) {
+    const float *src = gw1 + r * F;
+    float *dst = (r < d.H ? gwa1 : gwv1) + (r % d.H) * F;
+    if (d.C == 0) {
+      for (int64_t i = threadIdx.x; i < F; i += blockDim.x) dst[i] = src[i];
+      return;
+    }
+    // merged order j = p * C + c, kept at p * (C + 1) + c (padded: conflict-free reads below)
+    for (int64_t j = threadIdx.x; j < F; j += blockDim.x) {
+      const int p = (int)(j / d.C), c = (int)(j - (int64_t)p * d.C);
+      row[p * (d.C + 1) + c] = src[j];
+    }
+    __syncthreads();
+    for (int64_t i = threadIdx.x; i < F; i += blockDim.x) {  // reference order c * P + p
+      const int c = (int)(i / d.P), p = (int)(i - (int64_t)c * d.P);
+      dst[i] = row[p * (d.C + 1) + c];
+    }
+    return;
+  }
+  const int64_t H2 = 2 * d.H;
+  for (int64_t k = threadIdx.x; k < H2; k += blockDim.x) {
+    if (k < d.H) gba1[k] = gb1[k]; else gbv1[k - d.H] = gb1[k];
+  }
+  for (int64_t k = threadIdx.x; k < d.A * d.H + d.H; k += blockDim.x) {
+    if (k < d.A * d.H) {
+      const int64_t rr = k / d.H, j = k - rr * d.H;
+      gwa2[k] = gw2[rr * H2 + j];
     } else {
-      const int64_t r = e - n3;
-      b2[r] = r < d.A ? ba2[r] : bv2[0];
+      gwv2[k - d.A * d.H] = gw2[d.A * H2 + d.H + (k - d.A * d.H)];
     }
   }
-}
-
-__global__ void k_heads_split_grad(HeadsDims d, const float *__restrict__ gw1, const float *__restrict__ gb1,
-                                   const float *__restrict__ gw2, const float *__restrict__ gb2,
-                                   float *__restrict__ gwa1, float *__restrict__ gwv1, float *__restrict__ gba1,
-                                   float *__restrict__ gbv1, float *__restrict__ gwa2, float *__restrict__ gwv2,
-                                   float *__restrict__ gba2, float *__restrict__ gbv2) {
-  // indexed by the reference layouts (coalesced writes): FC1 weights, FC1 biases, FC2, FC2 bias
-  const int64_t n1 = 2 * d.H * d.F, n2 = n1 + 2 * d.H, n3 = n2 + d.A * d.H + d.H, n4 = n3 + d.A + 1;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n4; e += stride) {
-    if (e < n1) {  // reference column jr of branch row r -> merged column
-      const int64_t r = e / d.F, jr = e - r * d.F;
-      int64_t j = jr;
-      if (d.C) {
-        const int64_t c = jr / d.P, p = jr - c * d.P;
-        j = p * d.C + c;
-      }
-      const float g = gw1[r * d.F + j];
-      if (r < d.H) gwa1[r * d.F + jr] = g; else gwv1[(r - d.H) * d.F + jr] = g;
-    } else if (e < n2) {
-      const int64_t r = e - n1;
-      if (r < d.H) gba1[r] = gb1[r]; else gbv1[r - d.H] = gb1[r];
-    } else if (e < n3) {
-      const int64_t k = e - n2;
-      if (k < d.A * d.H) {
-        const int64_t r = k / d.H, j = k - r * d.H;
-        gwa2[k] = gw2[r * 2 * d.H + j];
-      } else {
-        gwv2[k - d.A * d.H] = gw2[d.A * 2 * d.H + d.H + (k - d.A * d.H)];
-      }
-    } else {
-      const int64_t r = e - n3;
-      if (r < d.A) gba2[r] = gb2[r]; else gbv2[0] = gb2[r];
-    }
+  for (int64_t k = threadIdx.x; k <= d.A; k += blockDim.x) {
+    if (k < d.A) gba2[k] = gb2[k]; else gbv2[0] = gb2[k];
   }
 }
 
@@ -247,7 +263,10 @@ int rth_heads_merge(const float *const *params, int64_t H, int64_t F, int64_t A,
   for (int k = 0; k < 8; ++k) RTH_REQUIRE(params[k], "rth_heads_merge: parameter %d is NULL", k);
   RTH_REQUIRE(C == 0 || (int64_t)C * P == F, "rth_heads_merge: C*P != F");
   const HeadsDims d{H, F, A, C, P};
-  hipLaunchKernelGGL(k_heads_merge, dim3(2048), dim3(256), 0, as_stream(stream), d, params[0], params[1], params[2],
+  RTH_REQUIRE(F <= 12288, "rth_heads_merge: F %lld > 12288 (one row in LDS)", (long long)F);
+  const size_t lds = (size_t)(C ? F : 0) * 4;
+  hipLaunchKernelGGL(k_heads_merge, dim3((unsigned)(2 * H + 1)), dim3(256), lds, as_stream(stream), d, params[0],
+                     params[1], params[2],
                      params[3], params[4], params[5], params[6], params[7], w1, b1, w2, b2);
   RTH_LAUNCHED();
   return RTH_OK;
@@ -259,7 +278,10 @@ int rth_heads_split_grad(const float *gw1, const float *gb1, const float *gw2, c
   for (int k = 0; k < 8; ++k) RTH_REQUIRE(grads[k], "rth_heads_split_grad: gradient %d is NULL", k);
   RTH_REQUIRE(C == 0 || (int64_t)C * P == F, "rth_heads_split_grad: C*P != F");
   const HeadsDims d{H, F, A, C, P};
-  hipLaunchKernelGGL(k_heads_split_grad, dim3(2048), dim3(256), 0, as_stream(stream), d, gw1, gb1, gw2, gb2, grads[0],
+  RTH_REQUIRE(F <= 12288, "rth_heads_split_grad: F %lld > 12288 (one row in LDS)", (long long)F);
+  const size_t lds = (size_t)(C ? F + F / C : 0) * 4;
+  hipLaunchKernelGGL(k_heads_split_grad, dim3((unsigned)(2 * H + 1)), dim3(256), lds, as_stream(stream), d, gw1, gb1,
+                     gw2, gb2, grads[0],
                      grads[1], grads[2], grads[3], grads[4], grads[5], grads[6], grads[7]);
   RTH_LAUNCHED();
   return RTH_OK;

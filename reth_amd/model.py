@@ -139,25 +139,30 @@ class DQNNetwork(nn.Module):
         dev = convs[0].weight.device
         res = [] if out is None else out
         forms = [False, True] if u8 is None else [bool(u8)]
-        k = 0
+        jobs, keep, k = [], [], 0
         for form in forms:
             for li, (conv, (_, shape)) in enumerate(zip(convs, self._torso_shapes(self.input_shape, form))):
                 if form and li > 0 and len(forms) == 2:
                     continue  # conv2 / conv3 are the same for both forms
-                if shape is None:
-                    buf = None
-                else:
+                buf = None
+                if shape is not None:
                     w = conv.weight.detach()
                     if not w.is_contiguous(memory_format=torch.channels_last):
                         w = w.contiguous(memory_format=torch.channels_last)
+                        keep.append(w)
                     buf = res[k] if out is not None else torch.empty(
                         _lib.lib().rth_conv_packed_bytes(_lib.ctypes.byref(shape)) // 4, dtype=torch.float32,
                         device=dev)
-                    _lib.call("rth_conv_pack", _lib.ctypes.byref(shape), w.data_ptr(), buf.data_ptr(),
-                              _lib.stream_ptr())
+                    jobs.append((shape, w.data_ptr(), buf.data_ptr()))
                 if out is None:
                     res.append(buf)
                 k += 1
+        if jobs:  # one launch for the whole torso
+            n = len(jobs)
+            shapes = (_lib.ConvShape * n)(*[j[0] for j in jobs])
+            ws = (_lib.c_vp * n)(*[j[1] for j in jobs])
+            pks = (_lib.c_vp * n)(*[j[2] for j in jobs])
+            _lib.call("rth_conv_pack_many", n, shapes, ws, pks, _lib.stream_ptr())
         return res
 
     @staticmethod

@@ -157,3 +157,23 @@ def test_hip_torso_gradients_match_miopen(dev):
     for a, b in zip(*grads):
         scale = b.abs().max().clamp_min(1e-12)
         assert ((a - b).abs().max() / scale) < 1e-4
+
+
+def test_pack_many_matches_single_packs(dev):
+    from reth_amd import _lib
+
+    shapes = [_shape(_lib.CONV_F32_NHWC, *GEOMS[0]), _shape(_lib.CONV_F32_NHWC, *GEOMS[1]),
+              _shape(_lib.CONV_F32_NHWC, *GEOMS[2]), _shape(_lib.CONV_U8_CHW, *GEOMS[0])]
+    ws, singles, many = [], [], []
+    for shp in shapes:
+        cin, cout, k = shp.cin, shp.cout, shp.kh
+        w = torch.randn((cout, cin, k, k), device=dev).contiguous(memory_format=torch.channels_last)
+        nb = _lib.lib().rth_conv_packed_bytes(_lib.ctypes.byref(shp)) // 4
+        a, b = torch.zeros(nb, device=dev), torch.zeros(nb, device=dev)
+        _lib.call("rth_conv_pack", _lib.ctypes.byref(shp), w.data_ptr(), a.data_ptr(), _lib.stream_ptr())
+        ws.append(w), singles.append(a), many.append(b)
+    n = len(shapes)
+    _lib.call("rth_conv_pack_many", n, (_lib.ConvShape * n)(*shapes), (_lib.c_vp * n)(*[w.data_ptr() for w in ws]),
+              (_lib.c_vp * n)(*[b.data_ptr() for b in many]), _lib.stream_ptr())
+    for a, b in zip(singles, many):
+        assert torch.equal(a, b)

@@ -255,3 +255,31 @@ def test_merged_heads_kernels_match_torch(dev, hwc):
     for (name, p), q in zip(net.named_parameters(), cpu.parameters()):
         if name.startswith("fc_"):
             assert torch.equal(p.grad.cpu(), q.grad), name
+
+
+def test_heads_merge_split_roundtrip_nhwc(dev):
+    """rth_heads_merge / rth_heads_split_grad (one LDS row transpose per FC1 row) against the
+    torch construction of the merged NHWC-permuted heads, and split(merge) == identity"""
+    from reth_amd.model import DQNNetwork
+
+    torch.manual_seed(11)
+    net = DQNNetwork((4, 84, 84), 6).to(dev)
+    net.hwc_features = True
+    with torch.no_grad():
+        got = net._merged_head_weights()
+        a0, v0, a2, v2 = net.fc_adv[0], net.fc_value[0], net.fc_adv[2], net.fc_value[2]
+        hwc = lambda wt: wt.view(wt.shape[0], 64, 7, 7).permute(0, 2, 3, 1).reshape(wt.shape[0], -1)
+        want_w1 = torch.cat([hwc(a0.weight), hwc(v0.weight)])
+        assert torch.equal(got[0], want_w1)
+        assert torch.equal(got[1], torch.cat([a0.bias, v0.bias]))
+    # gradient split: d/dparams of sum(merged * R) == the branch slices of R, un-permuted
+    ps = net._head_params()
+    merged = net._merged_head_weights()
+    rs = [torch.randn_like(m) for m in merged]
+    sum((m * r).sum() for m, r in zip(merged, rs)).backward()
+    unperm = lambda g: g.view(g.shape[0], 7, 7, 64).permute(0, 3, 1, 2).reshape(g.shape[0], -1)
+    H = a0.weight.shape[0]
+    assert torch.equal(ps[0].grad, unperm(rs[0][:H])) and torch.equal(ps[1].grad, unperm(rs[0][H:]))
+    assert torch.equal(ps[2].grad, rs[1][:H]) and torch.equal(ps[3].grad, rs[1][H:])
+    assert torch.equal(ps[4].grad, rs[2][:6, :H]) and torch.equal(ps[5].grad, rs[2][6:, H:])
+    assert torch.equal(ps[6].grad, rs[3][:6]) and torch.equal(ps[7].grad, rs[3][6:])

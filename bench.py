@@ -36,13 +36,13 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 FP32_PEAK_TFLOPS = 157.3
 
 
-def gather_bytes_per_row(s1_u8=False):
+def gather_bytes_per_row(frames_u8=False):
     """algorithmic bytes of one sampled apex row in rth_replay_gather: read s0/s1 uint8
-    stacks + a(8) r(4) done(4); write s0 as a float32 stack (the learner's gradient pass),
-    s1 as float32 too or -- with the HIP conv torso, whose target passes read uint8 -- as the
-    uint8 stack; a r done; 5 index reads"""
+    stacks + a(8) r(4) done(4); write s0/s1 as float32 channels-last stacks, or -- with the
+    HIP conv torso, which reads uint8 stacks itself -- as the uint8 stacks; a r done; 5
+    index reads"""
     read = 2 * STACK + 8 + 4 + 4
-    write = STACK * 4 + (STACK if s1_u8 else STACK * 4) + 8 + 4 + 4
+    write = 2 * STACK * (1 if frames_u8 else 4) + 8 + 4 + 4
     return read + write + 5 * 8
 
 
@@ -288,8 +288,8 @@ def main():
                    "qnet_layout": "channels_last" if cfg.channels_last else "nchw",
                    "conv_benchmark": cfg.conv_benchmark, "hip_graph": cfg.hip_graph, "hip_conv": cfg.hip_conv,
                    "parallelism": f"dp{world} learner (RCCL grad all-reduce) + {world} replay shards"},
-        "roofline": {"kernel": "rth_replay_gather (k_copy_rows: PER-sampled rows, s0 u8->f32 NHWC%s)"
-                     % (", s1 u8" if cfg.hip_conv and cfg.channels_last else ", s1 u8->f32 NHWC"),
+        "roofline": {"kernel": "rth_replay_gather (k_copy_rows: PER-sampled rows, frames %s)"
+                     % ("uint8 stacks" if cfg.hip_conv and cfg.channels_last else "u8->f32 NHWC"),
                      "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "bytes_per_launch": bytes_launch, "mean_launch_us": round(mean_gather_s * 1e6, 2),

@@ -320,6 +320,16 @@ int rth_conv_pack_many(int32_t n, const rth_conv_shape *shapes, const float *con
                        float *const *packed_dev, void *stream);
 int rth_conv_bias_relu(const rth_conv_shape *shape, const void *x_dev, const int64_t *rows_dev, int64_t n,
                        const float *packed_dev, const float *bias_dev, float *y_dev, void *stream);
+/* Backward of relu(conv2d(x, w) + b) for the weights and bias, on uint8 stacks (conv1, whose
+ * input needs no gradient): gy = (y > 0) ? g : 0, gw = sum over output pixels of gy times the
+ * input window (OHWI [cout, kh, kw, cin], the layout of a channels_last weight), gb = sum of
+ * gy.  g, y: NHWC fp32 [n, hout, wout, cout] (upstream gradient, forward output).  Summed in
+ * a fixed order (deterministic); workspace = rth_conv_wgrad_workspace(shape) bytes.  Built
+ * for the uint8 conv1 geometry; replaces rth_relu_bias_grad + MIOpen's weight gradient. */
+int64_t rth_conv_wgrad_workspace(const rth_conv_shape *shape);
+int rth_conv_relu_wgrad(const rth_conv_shape *shape, const void *x_dev, const int64_t *rows_dev, int64_t n,
+                        const float *g_dev, const float *y_dev, float *gw_dev, float *gb_dev, void *workspace_dev,
+                        void *stream);
 
 /* ------------------------------------------------------------------------------------
  * Atari observation preprocessing (reth/reth/env/util.py:121-209, 281-297): per actor, the

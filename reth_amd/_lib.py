@@ -112,6 +112,9 @@ SIGNATURES = {
     "rth_conv_supported": (c_i32, [ctypes.POINTER(ConvShape)]),
     "rth_conv_packed_bytes": (c_i64, [ctypes.POINTER(ConvShape)]),
     "rth_conv_pack": (c_i32, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_vp]),
+    "rth_conv_wgrad_workspace": (c_i64, [ctypes.POINTER(ConvShape)]),
+    "rth_conv_relu_wgrad": (c_i32, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                    c_vp]),
     "rth_conv_pack_many": (c_i32, [c_i32, ctypes.POINTER(ConvShape), ctypes.POINTER(c_vp), ctypes.POINTER(c_vp),
                                    c_vp]),
     "rth_conv_bias_relu": (c_i32, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),

@@ -223,12 +223,13 @@ def _q_forward(q_net, x):
     return q, dueling
 
 
-def apex_columns(channels_last=False, s1_u8=False):
+def apex_columns(channels_last=False, frames_u8=False):
     """replay columns of the apex-dqn rows [s0, a, r, s1, done] (worker.py:47-51): frames are
     stored uint8 and sampled as float32 (exact), the rest as the reference casts them.
-    s1_u8: s1 is sampled as the stored uint8 stacks -- the learner's no-grad target passes
-    read them in the HIP conv torso, which widens in registers (same values, 4x fewer bytes)"""
+    frames_u8: s0 / s1 are sampled as the stored uint8 stacks -- the HIP conv torso reads
+    them directly (forward, and conv1's weight gradient), widening in registers (the same
+    values at a quarter of the bytes)"""
     from .replay import Column
-    fr = lambda: Column(OBS_SHAPE, torch.uint8, torch.float32, channels_last=channels_last)
-    s1 = Column(OBS_SHAPE, torch.uint8) if s1_u8 else fr()
-    return [fr(), Column((), torch.int64), Column((), torch.float32), s1, Column((), torch.float32)]
+    fr = lambda: Column(OBS_SHAPE, torch.uint8) if frames_u8 else Column(OBS_SHAPE, torch.uint8, torch.float32,
+                                                                         channels_last=channels_last)
+    return [fr(), Column((), torch.int64), Column((), torch.float32), fr(), Column((), torch.float32)]

@@ -110,7 +110,7 @@ class ApexDQN:
         self.svc, self.addr = start_per(cfg.capacity, cfg.batch_size, alpha=cfg.alpha, beta=cfg.beta,
                                         sample_start=cfg.sample_start, device=self.device, seed=cfg.seed + 7919 * rank)
         u8 = bool(cfg.hip_conv and cfg.channels_last)
-        self.svc.replay = HbmReplay(cfg.capacity, apex_columns(cfg.channels_last, s1_u8=u8), cfg.alpha, cfg.beta,
+        self.svc.replay = HbmReplay(cfg.capacity, apex_columns(cfg.channels_last, frames_u8=u8), cfg.alpha, cfg.beta,
                                     self.device, seed=cfg.seed + 7919 * rank)
         self.replay = self.svc.replay
         self.loader = TorchCudaLoader(self.addr, buffer_size=2, prefetch=1)

@@ -35,6 +35,7 @@
 namespace rth {
 
 using f32x4 = __attribute__((ext_vector_type(4))) float;
+using f32x16 = __attribute__((ext_vector_type(16))) float;
 
 __device__ __forceinline__ float relu_c(float v) { return v < 0.0f ? 0.0f : v; }  // NaN passes, like torch
 
@@ -360,6 +361,139 @@ static int cu_count() {
   return cus;
 }
 
+// ---------------------------------------------------------------------------------------
+// conv1 backward on uint8 stacks: gy = (y > 0) ? g : 0 (ReLU backward), gw = sum over output
+// pixels of gy (x) im2col(x), gb = sum of gy -- one pass over g, y and the stacks, MFMA
+// 32x32x2 f32 with the reduction over pixels (2 per MFMA).  The 32 x 256 weight gradient is
+// held as KW = 8 accumulator tiles per wave: tile kw, column j = (ci, kh) (32 of them), so a
+// lane's 8 B-operand values of one pixel are 8 contiguous bytes of one input row (two dword
+// loads).  Pixel pairs are loaded one group of kWgU pairs ahead.  Workgroup w sums a
+// contiguous pixel range and writes its partial; k_wgrad_reduce adds the partials in
+// workgroup order (deterministic).
+constexpr int kWgWaves = 8, kWgBlocks = 256, kWgU = 4;
+
+template <int KH, int KW, int S, int CIN, int COUT, int HIN, int WIN>
+__global__ __launch_bounds__(kWgWaves * 64) void k_conv_wgrad_u8(const uint8_t *__restrict__ x,
+                                                                const int64_t *__restrict__ rows, int64_t n,
+                                                                const float *__restrict__ g,
+                                                                const float *__restrict__ y,
+                                                                float *__restrict__ partial) {
+  constexpr int HOUT = (HIN - KH) / S + 1, WOUT = (WIN - KW) / S + 1, PIX = HOUT * WOUT;
+  constexpr int K = CIN * KH * KW, STACK = CIN * HIN * WIN;
+  static_assert(COUT == 32 && CIN * KH == 32 && KW == 8 && S % 4 == 0, "conv1 layout");
+  __shared__ float red[kWgWaves][32];
+  __shared__ float tile[kWgWaves][32 * 32];
+  const int wave = threadIdx.x / 64, lane = threadIdx.x % 64, o = lane & 31, h = lane >> 5;
+  const int64_t P = n * PIX;
+  constexpr int STEP = 2 * kWgWaves;  // pixels per round over the workgroup's waves
+  const int64_t chunk = ((P + gridDim.x - 1) / gridDim.x + STEP * kWgU - 1) / (STEP * kWgU) * (STEP * kWgU);
+  const int64_t p_begin = (int64_t)blockIdx.x * chunk, p_end = p_begin + chunk < P ? p_begin + chunk : P;
+  // B column j = o = (ci, kh): its input row inside the window
+  const int row_off = (o / KH) * HIN * WIN + (o % KH) * WIN;
+  struct Pair {
+    float a;
+    uint32_t lo, hi;
+  };
+  auto load = [&](int64_t p0) {  // pixel p0 + h of this wave's pair
+    const int64_t p = p0 + h;
+    const bool live = p < p_end;
+    const int64_t pc = live ? p : (p_begin < P ? p_begin : 0);
+    const int64_t b = pc / PIX;
+    const int pp = (int)(pc % PIX), oy = pp / WOUT, ox = pp % WOUT;
+    const uint8_t *src = x + (rows ? rows[b] : b) * (int64_t)STACK + row_off + (S * oy) * WIN + S * ox;
+    const float gv = g[pc * COUT + o], yv = y[pc * COUT + o];
+    Pair r;
+    r.a = (live && yv > 0.0f) ? gv : 0.0f;
+    r.lo = *reinterpret_cast<const uint32_t *>(src);
+    r.hi = *reinterpret_cast<const uint32_t *>(src + 4);
+    return r;
+  };
+  f32x16 acc[KW];
+#pragma unroll
+  for (int t = 0; t < KW; ++t) acc[t] = f32x16{};
+  float db = 0.0f;
+  Pair cur[kWgU], nxt[kWgU];
+  int64_t p0 = p_begin + 2 * wave;
+#pragma unroll
+  for (int u = 0; u < kWgU; ++u) cur[u] = load(p0 + u * STEP);
+  for (; p0 < p_end; p0 += kWgU * STEP) {
+#pragma unroll
+    for (int u = 0; u < kWgU; ++u) nxt[u] = load(p0 + (kWgU + u) * STEP);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < kWgU; ++u) {
+      db = radd(db, cur[u].a);
+#pragma unroll
+      for (int t = 0; t < KW; ++t) {
+        const uint32_t wv = t < 4 ? cur[u].lo : cur[u].hi;
+        const float bx = (float)((wv >> (8 * (t % 4))) & 0xffu);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[u].a, bx, acc[t], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kWgU; ++u) cur[u] = nxt[u];
+  }
+  // bias: lanes o and o + 32 of every wave
+  db = radd(db, __shfl_down(db, 32));
+  if (h == 0) red[wave][o] = db;
+  // the weight tiles: sum the waves through LDS, tile by tile (C/D: lane -> column o of the
+  // tile, register r -> row i = 8 (r / 4) + 4 h + r % 4 = output channel)
+  float *out = partial + (int64_t)blockIdx.x * (COUT * K + COUT);
+#pragma unroll
+  for (int t = 0; t < KW; ++t) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) tile[wave][(8 * (r / 4) + 4 * h + r % 4) * 32 + o] = acc[t][r];
+    __syncthreads();
+    for (int e = threadIdx.x; e < 32 * 32; e += kWgWaves * 64) {
+      float v = tile[0][e];
+#pragma unroll
+      for (int w = 1; w < kWgWaves; ++w) v = radd(v, tile[w][e]);
+      out[(e / 32) * K + t * 32 + e % 32] = v;  // [o][kk = kw * 32 + (ci, kh)]
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x < 32) {
+    float v = red[0][threadIdx.x];
+    for (int w = 1; w < kWgWaves; ++w) v = radd(v, red[w][threadIdx.x]);
+    out[COUT * K + threadIdx.x] = v;
+  }
+}
+
+// partials [blocks][COUT * K + COUT] (kk = kw * 32 + ci * KH + kh) -> gw OHWI, gb: 64
+// elements per workgroup, 4 groups of 64 lanes each summing a quarter of the partials
+// (coalesced rows), then the 4 group sums in fixed order
+template <int KH, int KW, int CIN, int COUT>
+__global__ __launch_bounds__(256) void k_wgrad_reduce(const float *__restrict__ partial, int blocks,
+                                                      float *__restrict__ gw, float *__restrict__ gb) {
+  constexpr int K = CIN * KH * KW, E = COUT * K + COUT;
+  __shared__ float part[4][64];
+  const int grp = threadIdx.x / 64, l = threadIdx.x % 64;
+  const int e = blockIdx.x * 64 + l;
+  const int per = (blocks + 3) / 4, w0 = grp * per, w1 = w0 + per < blocks ? w0 + per : blocks;
+  float v = 0.0f;
+  if (e < E) {
+    int w = w0;
+    for (; w + 8 <= w1; w += 8) {
+      float t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t[u] = partial[(int64_t)(w + u) * E + e];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v = radd(v, t[u]);
+    }
+    for (; w < w1; ++w) v = radd(v, partial[(int64_t)w * E + e]);
+  }
+  part[grp][l] = v;
+  __syncthreads();
+  if (grp != 0 || e >= E) return;
+  v = radd(radd(radd(part[0][l], part[1][l]), part[2][l]), part[3][l]);
+  if (e >= COUT * K) {
+    gb[e - COUT * K] = v;
+    return;
+  }
+  const int oi = e / K, kk = e % K, kw = kk / 32, ci = (kk % 32) / KH, kh = kk % KH;
+  gw[((oi * KH + kh) * KW + kw) * CIN + ci] = v;
+}
+
 static int wg_per_cu() {  // RTH_CONV_WG_PER_CU (tuning), default 2
   static int v = [] {
     const char *e = getenv("RTH_CONV_WG_PER_CU");
@@ -417,6 +551,34 @@ int rth_conv_pack_many(int32_t n, const rth_conv_shape *shapes, const float *con
   job.first_block[n] = blocks;
   if (n == 0) return RTH_OK;
   hipLaunchKernelGGL(k_conv_pack_many, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), job);
+  RTH_LAUNCHED();
+  return RTH_OK;
+}
+
+static bool is_conv1_u8(const rth_conv_shape *s) {
+  return s && s->input == RTH_CONV_U8_CHW && s->cin == 4 && s->hin == 84 && s->win == 84 && s->cout == 32 &&
+         s->kh == 8 && s->kw == 8 && s->stride == 4;
+}
+
+int64_t rth_conv_wgrad_workspace(const rth_conv_shape *shape) {
+  return is_conv1_u8(shape) ? (int64_t)kWgBlocks * (32 * 256 + 32) * 4 : 0;
+}
+
+int rth_conv_relu_wgrad(const rth_conv_shape *shape, const void *x, const int64_t *rows, int64_t n, const float *g,
+                        const float *y, float *gw, float *gb, void *workspace, void *stream) {
+  RTH_REQUIRE(shape && x && g && y && gw && gb && workspace && n >= 0, "rth_conv_relu_wgrad: NULL argument");
+  RTH_REQUIRE(is_conv1_u8(shape), "rth_conv_relu_wgrad: only the uint8 conv1 geometry (4x84x84 -> 32, k8 s4) is built");
+  float *part = static_cast<float *>(workspace);
+  if (n == 0) {
+    RTH_HIP(hipMemsetAsync(gw, 0, 32 * 256 * 4, as_stream(stream)));
+    RTH_HIP(hipMemsetAsync(gb, 0, 32 * 4, as_stream(stream)));
+    return RTH_OK;
+  }
+  hipLaunchKernelGGL((k_conv_wgrad_u8<8, 8, 4, 4, 32, 84, 84>), dim3(kWgBlocks), dim3(kWgWaves * 64), 0,
+                     as_stream(stream), static_cast<const uint8_t *>(x), rows, n, g, y, part);
+  RTH_LAUNCHED();
+  hipLaunchKernelGGL((k_wgrad_reduce<8, 8, 4, 32>), dim3((32 * 256 + 32 + 63) / 64), dim3(256), 0,
+                     as_stream(stream), part, kWgBlocks, gw, gb);
   RTH_LAUNCHED();
   return RTH_OK;
 }

@@ -125,6 +125,8 @@ struct HeadsDims {
 };
 
 
+constexpr int kRowF4 = 12;  // float4 per thread for one FC1 row in LDS: F <= 12288
+
 // One workgroup per FC1 row (2H rows) + one for the small tail (b1, w2, b2).  A row of the
 // NHWC-permuted FC1 weight is a C x P -> P x C transpose of the reference row, done through
 // LDS so both the HBM reads and the writes are coalesced.
@@ -144,11 +146,27 @@ __global__ __launch_bounds__(256) void k_heads_merge(HeadsDims d, const float *_
       for (int64_t i = threadIdx.x; i < F; i += blockDim.x) dst[i] = src[i];
       return;
     }
-    for (int64_t i = threadIdx.x; i < F; i += blockDim.x) row[i] = src[i];  // reference order c * P + p
+    // reference order c * P + p; float4 loads, all issued before the first LDS write
+    {
+      const int F4 = (int)(F / 4);
+      const float4 *s4 = reinterpret_cast<const float4 *>(src);
+      float4 v[kRowF4];
+#pragma unroll
+      for (int u = 0; u < kRowF4; ++u) {
+        const int i = threadIdx.x + u * 256;
+        if (i < F4) v[u] = s4[i];
+      }
+#pragma unroll
+      for (int u = 0; u < kRowF4; ++u) {
+        const int i = threadIdx.x + u * 256;
+        if (i < F4) reinterpret_cast<float4 *>(row)[i] = v[u];
+      }
+    }
     __syncthreads();
-    for (int64_t j = threadIdx.x; j < F; j += blockDim.x) {  // merged order p * C + c
-      const int p = (int)(j / d.C), c = (int)(j - (int64_t)p * d.C);
-      dst[j] = row[c * d.P + p];
+    for (int j4 = threadIdx.x; j4 < F / 4; j4 += 256) {  // merged order p * C + c, 4 c per thread
+      const int j = 4 * j4, p = j / d.C, c = j - p * d.C;
+      reinterpret_cast<float4 *>(dst)[j4] =
+          float4{row[c * d.P + p], row[(c + 1) * d.P + p], row[(c + 2) * d.P + p], row[(c + 3) * d.P + p]};
     }
     return;
   }
@@ -181,13 +199,29 @@ __global__ __launch_bounds__(256) void k_heads_split_grad(HeadsDims d, const flo
       for (int64_t i = threadIdx.x; i < F; i += blockDim.x) dst[i] = src[i];
       return;
     }
-    // merged order j = p * C + c, kept at p * (C + 1) + c (padded: conflict-free reads below)
-    for (int64_t j = threadIdx.x; j < F; j += blockDim.x) {
-      const int p = (int)(j / d.C), c = (int)(j - (int64_t)p * d.C);
-      row[p * (d.C + 1) + c] = src[j];
+    // merged order j = p * C + c, kept at p * (C + 1) + c (padded: conflict-free reads below);
+    // float4 loads, all issued before the first LDS write
+    {
+      const int F4 = (int)(F / 4);
+      const float4 *s4 = reinterpret_cast<const float4 *>(src);
+      float4 v[kRowF4];
+#pragma unroll
+      for (int u = 0; u < kRowF4; ++u) {
+        const int i = threadIdx.x + u * 256;
+        if (i < F4) v[u] = s4[i];
+      }
+#pragma unroll
+      for (int u = 0; u < kRowF4; ++u) {
+        const int i = threadIdx.x + u * 256;
+        if (i < F4) {
+          const int j = 4 * i, p = j / d.C, c = j - p * d.C;  // C % 4 == 0: same p for all 4
+          float *o = row + p * (d.C + 1) + c;
+          o[0] = v[u].x, o[1] = v[u].y, o[2] = v[u].z, o[3] = v[u].w;
+        }
+      }
     }
     __syncthreads();
-    for (int64_t i = threadIdx.x; i < F; i += blockDim.x) {  // reference order c * P + p
+    for (int64_t i = threadIdx.x; i < F; i += 256) {  // reference order c * P + p
       const int c = (int)(i / d.P), p = (int)(i - (int64_t)c * d.P);
       dst[i] = row[p * (d.C + 1) + c];
     }
@@ -264,6 +298,9 @@ int rth_heads_merge(const float *const *params, int64_t H, int64_t F, int64_t A,
   RTH_REQUIRE(C == 0 || (int64_t)C * P == F, "rth_heads_merge: C*P != F");
   const HeadsDims d{H, F, A, C, P};
   RTH_REQUIRE(F <= 12288, "rth_heads_merge: F %lld > 12288 (one row in LDS)", (long long)F);
+  RTH_REQUIRE(F % 4 == 0 && C % 4 == 0 && ((reinterpret_cast<uintptr_t>(params[0]) | reinterpret_cast<uintptr_t>(params[1]) |
+                                           reinterpret_cast<uintptr_t>(w1)) & 15) == 0,
+              "rth_heads_merge: F and C must be multiples of 4, FC1 weights 16-byte aligned");
   const size_t lds = (size_t)(C ? F : 0) * 4;
   hipLaunchKernelGGL(k_heads_merge, dim3((unsigned)(2 * H + 1)), dim3(256), lds, as_stream(stream), d, params[0],
                      params[1], params[2],
@@ -279,6 +316,8 @@ int rth_heads_split_grad(const float *gw1, const float *gb1, const float *gw2, c
   RTH_REQUIRE(C == 0 || (int64_t)C * P == F, "rth_heads_split_grad: C*P != F");
   const HeadsDims d{H, F, A, C, P};
   RTH_REQUIRE(F <= 12288, "rth_heads_split_grad: F %lld > 12288 (one row in LDS)", (long long)F);
+  RTH_REQUIRE(F % 4 == 0 && C % 4 == 0 && (reinterpret_cast<uintptr_t>(gw1) & 15) == 0,
+              "rth_heads_split_grad: F and C must be multiples of 4, gw1 16-byte aligned");
   const size_t lds = (size_t)(C ? F + F / C : 0) * 4;
   hipLaunchKernelGGL(k_heads_split_grad, dim3((unsigned)(2 * H + 1)), dim3(256), lds, as_stream(stream), d, gw1, gb1,
                      gw2, gb2, grads[0],

@@ -311,6 +311,22 @@ class _ConvBiasReLU(torch.autograd.Function):
         return gx, gw, db, None, None
 
 
+_WGRAD_WS = {}
+
+
+def _wgrad_workspace(shape, device):
+    """rth_conv_relu_wgrad's partial-sum workspace (one per device; backward passes on a
+    device run in stream order)"""
+    from ._lib import ctypes, lib
+
+    key = (device, shape.input, shape.cin, shape.cout)
+    ws = _WGRAD_WS.get(key)
+    if ws is None:
+        nbytes = lib().rth_conv_wgrad_workspace(ctypes.byref(shape))
+        ws = _WGRAD_WS[key] = torch.empty(max(nbytes, 16) // 4, dtype=torch.float32, device=device)
+    return ws
+
+
 class _HipConvBiasReLU(torch.autograd.Function):
     """relu(conv2d(x, w) + b) as one rth_conv_bias_relu launch (conv.hip); x channels-last
     fp32, or uint8 CHW frame stacks (optionally through a row index) for the first layer.
@@ -329,7 +345,10 @@ class _HipConvBiasReLU(torch.autograd.Function):
         call("rth_conv_bias_relu", ctypes.byref(shape), ptr(x), ptr(rows), n, ptr(packed), ptr(b), ptr(y),
              stream_ptr())
         ctx.save_for_backward(x, w, y, rows)
-        ctx.stride, ctx.ws = list(stride), ws
+        ctx.stride, ctx.ws, ctx.shape = list(stride), ws, shape
+        ctx.wgrad_ws = None
+        if x.dtype == torch.uint8 and ctx.needs_input_grad[1]:
+            ctx.wgrad_ws = _wgrad_workspace(shape, x.device)
         return y
 
     @staticmethod
@@ -337,12 +356,23 @@ class _HipConvBiasReLU(torch.autograd.Function):
         from ._lib import call, ptr, stream_ptr
 
         x, w, y, rows = ctx.saved_tensors
+        if not g.is_contiguous(memory_format=torch.channels_last):
+            g = g.contiguous(memory_format=torch.channels_last)
+        if x.dtype == torch.uint8 and ctx.wgrad_ws is not None:
+            # conv1 on uint8 stacks: ReLU mask + weight and bias gradients in one HIP pass
+            # (rth_conv_relu_wgrad), straight from the stacks
+            from ._lib import ctypes
+
+            gw = torch.empty(w.shape, dtype=w.dtype, device=w.device, memory_format=torch.channels_last)
+            db = torch.empty(w.shape[0], dtype=w.dtype, device=w.device)
+            n = y.shape[0]
+            call("rth_conv_relu_wgrad", ctypes.byref(ctx.shape), ptr(x), ptr(rows), n, ptr(g), ptr(y), ptr(gw),
+                 ptr(db), ptr(ctx.wgrad_ws), stream_ptr())
+            return None, gw if ctx.needs_input_grad[1] else None, db, None, None, None, None, None
         if not w.is_contiguous(memory_format=torch.channels_last):
             w = w.contiguous(memory_format=torch.channels_last)
         if x.dtype == torch.uint8:
             x = (x if rows is None else x[rows]).float().contiguous(memory_format=torch.channels_last)
-        if not g.is_contiguous(memory_format=torch.channels_last):
-            g = g.contiguous(memory_format=torch.channels_last)
         gy = torch.empty_like(y)
         n, c, h, wd = y.shape
         db = torch.empty(c, dtype=y.dtype, device=y.device)

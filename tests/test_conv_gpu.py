@@ -177,3 +177,55 @@ def test_pack_many_matches_single_packs(dev):
               (_lib.c_vp * n)(*[b.data_ptr() for b in many]), _lib.stream_ptr())
     for a, b in zip(singles, many):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("n", [1, 7, 40])
+def test_conv1_relu_wgrad_u8(dev, n):
+    """rth_conv_relu_wgrad against a float64 CPU autograd of relu(conv2d(x, w) + b)"""
+    from reth_amd import _lib
+
+    g = torch.Generator().manual_seed(100 + n)
+    stacks = torch.randint(0, 256, (60, 4, 84, 84), dtype=torch.uint8, generator=g)
+    rows = torch.randint(0, 60, (n,), generator=g)
+    w = ((torch.rand((32, 4, 8, 8), generator=g) * 2 - 1) / 16).double().requires_grad_(True)
+    b = ((torch.rand(32, generator=g) * 2 - 1) * 0.5).double().requires_grad_(True)
+    x = stacks[rows].double()
+    y = F.relu(F.conv2d(x, w, b, stride=4))
+    up = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    (y * up).sum().backward()
+    shape = _shape(_lib.CONV_U8_CHW, *GEOMS[0])
+    yd = y.detach().float().permute(0, 2, 3, 1).contiguous().to(dev)   # NHWC
+    gd = up.float().permute(0, 2, 3, 1).contiguous().to(dev)
+    gw = torch.full((32, 8, 8, 4), float("nan"), device=dev)           # OHWI
+    gb = torch.full((32,), float("nan"), device=dev)
+    ws = torch.empty(_lib.lib().rth_conv_wgrad_workspace(_lib.ctypes.byref(shape)) // 4, device=dev)
+    _lib.call("rth_conv_relu_wgrad", _lib.ctypes.byref(shape), stacks.to(dev).data_ptr(), rows.to(dev).data_ptr(), n,
+              gd.data_ptr(), yd.data_ptr(), gw.data_ptr(), gb.data_ptr(), ws.data_ptr(), _lib.stream_ptr())
+    want_w = w.grad.permute(0, 2, 3, 1)
+    scale = want_w.abs().max()
+    assert ((gw.cpu().double() - want_w).abs().max() / scale) < 2e-6
+    torch.testing.assert_close(gb.cpu().double(), b.grad, rtol=1e-5, atol=1e-4)
+    # deterministic: a second call gives the same bits
+    gw2 = torch.empty_like(gw)
+    _lib.call("rth_conv_relu_wgrad", _lib.ctypes.byref(shape), stacks.to(dev).data_ptr(), rows.to(dev).data_ptr(), n,
+              gd.data_ptr(), yd.data_ptr(), gw2.data_ptr(), gb.data_ptr(), ws.data_ptr(), _lib.stream_ptr())
+    assert torch.equal(gw, gw2)
+
+
+def test_hip_torso_gradients_u8_input(dev):
+    """grad path on uint8 stacks (forward + rth_conv_relu_wgrad for conv1) == MIOpen on the
+    float32 batch"""
+    net = _torso_net(dev, seed=3)
+    g = torch.Generator(device=dev).manual_seed(5)
+    xu = torch.randint(0, 256, (24, 4, 84, 84), dtype=torch.uint8, device=dev, generator=g)
+    grads = []
+    for hip in (True, False):
+        net.hip_conv = hip
+        net.zero_grad(set_to_none=True)
+        x = xu if hip else xu.float().contiguous(memory_format=torch.channels_last)
+        h = net.forward_heads(x, net._merged_head_weights())
+        (h.square().sum() * 1e-3).backward()
+        grads.append([p.grad.clone() for p in net.parameters()])
+    for a, b in zip(*grads):
+        scale = b.abs().max().clamp_min(1e-12)
+        assert ((a - b).abs().max() / scale) < 1e-4

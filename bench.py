@@ -174,7 +174,7 @@ def main():
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--actor-steps-per-update", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-iters", type=int, default=20)
+    ap.add_argument("--cpu-iters", type=int, default=72)
     ap.add_argument("--tag", default="r01")
     ap.add_argument("--nchw", action="store_true", help="contiguous NCHW Q-net tensors (default channels-last)")
     ap.add_argument("--no-conv-benchmark", action="store_true", help="MIOpen immediate mode instead of find")

@@ -53,6 +53,7 @@ for step in "$@"; do
          run pmc_conv_b 300 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM \
             --kernel-trace --output-format csv -d "$PWD/gpurun_out/pmc_conv_b" -o run -- python scripts/conv_pmc.py ;;
     probe) run probe 300 python scripts/probe_qnet.py ;;
+    host) run host_probe 300 python scripts/host_probe.py ;;
     variants2)
       run bench_eager 600 python bench.py --steps 100 --warmup 20 --no-cpu-baseline --eager
       run bench_graph 600 python bench.py --steps 100 --warmup 20 --no-cpu-baseline

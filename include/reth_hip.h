@@ -289,6 +289,16 @@ int rth_heads_split_grad(const float *gw1_dev, const float *gb1_dev, const float
                          void *stream);
 int rth_relu_bias_grad(const float *g_dev, const float *y_dev, float *gy_dev, float *db_dev, void *workspace_dev,
                        int64_t rows, int32_t C, void *stream);
+/* Backward of the merged heads' second layer, heads = h @ w2^T + b2 with h = relu(FC1) [B, H2]
+ * (row stride ldh), from d(loss)/d(heads) dq [B, A1] (rth_td_huber, dueling): replaces the
+ * addmm backward (two GEMMs + a column sum) and threshold_backward of torch.autograd at
+ * dqn_solver.py:116 (loss.backward()).  Writes gh = (h > 0) ? dq @ w2 : 0 [B, H2],
+ * gw2 = dq^T @ h [A1, H2], gb2 [A1], gb1 = column sums of gh [H2] (the FC1 bias gradient);
+ * deterministic.  td_abs_dev / td_acc_dev (nullable): td_acc[0] += mean(td_abs[0..B)), the
+ * Trainer's mean_error accumulator (reth/reth/presets/trainer.py:64-69).  H2 % 16 == 0. */
+int rth_heads_backward(const float *dq_dev, const float *h_dev, int64_t ldh, const float *w2_dev, int64_t B,
+                       int32_t H2, int32_t A1, float *gh_dev, float *gw2_dev, float *gb2_dev, float *gb1_dev,
+                       const float *td_abs_dev, float *td_acc_dev, void *stream);
 
 /* ------------------------------------------------------------------------------------
  * Q-network convolution torso forward (reth/reth/algorithm/dqn/dqn_model.py:14-20: each
@@ -352,9 +362,10 @@ int rth_atari_step(rth_atari *h, const uint8_t *raw_dev, int64_t n, uint8_t *fra
 /* ------------------------------------------------------------------------------------
  * Learner optimizer step (reth/reth/algorithm/dqn/dqn_solver.py:118-121):
  * torch.nn.utils.clip_grad_norm_(params, max_norm) then torch.optim.Adam.step() over up to
- * RTH_MAX_PARAM_TENSORS fp32 tensors in three launches (norm partials, scalars, update).
- * max_norm < 0 skips clipping.  step_dev (int64, device) is Adam's step count, incremented
- * on the device; workspace_dev holds rth_clip_adam_workspace() bytes of scratch;
+ * RTH_MAX_PARAM_TENSORS fp32 tensors in two launches (norm partials + scalars by the last
+ * workgroup, update).  max_norm < 0 skips clipping.  step_dev (int64, device) is Adam's step
+ * count, incremented on the device; workspace_dev holds rth_clip_adam_workspace() bytes,
+ * zero-filled once before the first call (it keeps a ticket counter that every call leaves 0);
  * total_norm_out_dev (nullable) receives the pre-clip 2-norm (clip_grad_norm_'s return).
  * ---------------------------------------------------------------------------------- */
 #define RTH_MAX_PARAM_TENSORS 32

@@ -108,6 +108,8 @@ SIGNATURES = {
                                 c_vp]),
     "rth_heads_split_grad": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i32, c_i32,
                                      ctypes.POINTER(c_vp), c_vp]),
+    "rth_heads_backward": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                   c_vp]),
     "rth_relu_bias_grad": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_vp]),
     "rth_conv_supported": (c_i32, [ctypes.POINTER(ConvShape)]),
     "rth_conv_packed_bytes": (c_i64, [ctypes.POINTER(ConvShape)]),

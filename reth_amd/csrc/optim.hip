@@ -1,4 +1,4 @@
-// Learner optimizer step on gfx950: clip_grad_norm_ + Adam as three launches over every
+// Learner optimizer step on gfx950: clip_grad_norm_ + Adam as two launches over every
 // parameter tensor at once.
 //
 // Reference: reth/reth/algorithm/dqn/dqn_solver.py:118-121 -- torch.nn.utils.clip_grad_norm_
@@ -48,35 +48,11 @@ __device__ __forceinline__ int seg_of(const OptArgs &a, int64_t b) {
   return s;
 }
 
-__global__ __launch_bounds__(kOptThreads) void k_grad_sqsum(OptArgs a, double *__restrict__ part) {
-  __shared__ double red[kOptThreads];
-  const int64_t b = blockIdx.x;
-  const OptSeg &sg = a.seg[seg_of(a, b)];
-  const int64_t base = (b - sg.blk0) * kOptChunk;
-  double acc = 0.0;
-#pragma unroll 4
-  for (int k = 0; k < kOptChunk / kOptThreads; ++k) {
-    const int64_t i = base + k * kOptThreads + threadIdx.x;
-    if (i < sg.n) {
-      const double g = (double)sg.grad[i];
-      acc = radd(acc, rmul(g, g));
-    }
-  }
-  red[threadIdx.x] = acc;
-  __syncthreads();
-  for (int s = kOptThreads / 2; s > 0; s >>= 1) {
-    if (threadIdx.x < s) red[threadIdx.x] = radd(red[threadIdx.x], red[threadIdx.x + s]);
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) part[b] = red[0];
-}
-
-// one workgroup: the norm, the clip coefficient, t += 1 and the bias corrections
-__global__ __launch_bounds__(kOptThreads) void k_opt_scalars(const double *__restrict__ part, int nparts, int clip,
-                                                            float max_norm, double lr, double beta1, double beta2,
-                                                            int64_t *__restrict__ step, OptScalars *__restrict__ out,
-                                                            float *__restrict__ total_out) {
-  __shared__ double red[kOptThreads];
+// the norm, the clip coefficient, t += 1 and the bias corrections, by one workgroup from the
+// per-workgroup partials (summed in workgroup order: deterministic)
+__device__ void opt_scalars(const double *__restrict__ part, int nparts, double *red, int clip, float max_norm,
+                            double lr, double beta1, double beta2, int64_t *__restrict__ step,
+                            OptScalars *__restrict__ out, float *__restrict__ total_out) {
   double acc = 0.0;
   for (int k = threadIdx.x; k < nparts; k += kOptThreads) acc = radd(acc, part[k]);
   red[threadIdx.x] = acc;
@@ -103,6 +79,59 @@ __global__ __launch_bounds__(kOptThreads) void k_opt_scalars(const double *__res
     out->total_norm = total;
     if (total_out) *total_out = total;
   }
+}
+
+struct ScalarArgs {
+  int clip;
+  float max_norm;
+  double lr, beta1, beta2;
+  int64_t *step;
+  OptScalars *out;
+  float *total_out;
+};
+
+// per-workgroup sums of squares of the gradients; the workgroup that finishes last (ticket
+// counter, agent-scope release/acquire hand-off of the partials) then computes the scalars,
+// so the Adam launch follows directly (no separate single-workgroup launch in between)
+__global__ __launch_bounds__(kOptThreads) void k_grad_sqsum(OptArgs a, double *__restrict__ part,
+                                                           unsigned *__restrict__ ticket, ScalarArgs sa) {
+  __shared__ double red[kOptThreads];
+  __shared__ int last;
+  const int64_t b = blockIdx.x;
+  const OptSeg &sg = a.seg[seg_of(a, b)];
+  const int64_t base = (b - sg.blk0) * kOptChunk;
+  double acc = 0.0;
+#pragma unroll 4
+  for (int k = 0; k < kOptChunk / kOptThreads; ++k) {
+    const int64_t i = base + k * kOptThreads + threadIdx.x;
+    if (i < sg.n) {
+      const double g = (double)sg.grad[i];
+      acc = radd(acc, rmul(g, g));
+    }
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = kOptThreads / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] = radd(red[threadIdx.x], red[threadIdx.x + s]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    part[b] = red[0];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = t == gridDim.x - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  opt_scalars(part, (int)gridDim.x, red, sa.clip, sa.max_norm, sa.lr, sa.beta1, sa.beta2, sa.step, sa.out,
+              sa.total_out);
+  if (threadIdx.x == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __global__ __launch_bounds__(kOptThreads) void k_adam(OptArgs a, const OptScalars *__restrict__ sc, int clip,
@@ -133,6 +162,7 @@ using namespace rth;
 
 extern "C" {
 
+// [partials: kMaxPartials doubles][OptScalars][ticket counter]; zero-initialised by the caller
 int64_t rth_clip_adam_workspace(void) { return (int64_t)kMaxPartials * 8 + 64; }
 
 int rth_clip_adam(const rth_param_tensor *tensors, int32_t n_tensors, double lr, double beta1, double beta2,
@@ -156,10 +186,9 @@ int rth_clip_adam(const rth_param_tensor *tensors, int32_t n_tensors, double lr,
   auto *sc = reinterpret_cast<OptScalars *>(static_cast<uint8_t *>(workspace_dev) + (int64_t)kMaxPartials * 8);
   const int clip = max_norm >= 0.0;
   hipStream_t s = as_stream(stream);
-  hipLaunchKernelGGL(k_grad_sqsum, dim3((unsigned)blocks), dim3(kOptThreads), 0, s, a, part);
-  RTH_LAUNCHED();
-  hipLaunchKernelGGL(k_opt_scalars, dim3(1), dim3(kOptThreads), 0, s, part, (int)blocks, clip, (float)max_norm, lr,
-                     beta1, beta2, step_dev, sc, total_norm_out);
+  auto *ticket = reinterpret_cast<unsigned *>(static_cast<uint8_t *>(workspace_dev) + (int64_t)kMaxPartials * 8 + 32);
+  const ScalarArgs sa{clip, (float)max_norm, lr, beta1, beta2, step_dev, sc, total_norm_out};
+  hipLaunchKernelGGL(k_grad_sqsum, dim3((unsigned)blocks), dim3(kOptThreads), 0, s, a, part, ticket, sa);
   RTH_LAUNCHED();
   // 1 - beta1 and 1 - beta2 are python floats in adam.py, rounded to f32 once
   hipLaunchKernelGGL(k_adam, dim3((unsigned)blocks), dim3(kOptThreads), 0, s, a, sc, clip, (float)(1.0 - beta1),

@@ -244,6 +244,88 @@ __global__ __launch_bounds__(256) void k_heads_split_grad(HeadsDims d, const flo
   }
 }
 
+
+// ---------------------------------------------------------------- heads backward
+// The merged heads' second layer backward (heads = h @ w2^T + b2, h = relu(FC1)) in one
+// launch, from the TD kernel's d(loss)/d(heads):
+//   gh  = (h > 0) ? dq @ w2 : 0      (addmm backward -> threshold_backward, [B, H2])
+//   gw2 = dq^T @ h  [A1, H2],  gb2 = column sums of dq [A1],  gb1 = column sums of gh [H2]
+// Workgroup k < H2 / 16 owns columns 16k .. 16k+15 over all B rows (lane = column
+// tid % 16, row group tid / 16); the 16 row-group partials are summed in LDS in a fixed
+// order (deterministic).  The last workgroup sums gb2 and, optionally, adds mean(|td|) to a
+// device accumulator (Trainer's mean_error, reth/reth/presets/trainer.py:64-69).
+constexpr int kHbCols = 16, kHbRows = 16, kHbMaxA1 = kMaxActions + 1;
+
+__global__ __launch_bounds__(256) void k_heads_backward(const float *__restrict__ dq, const float *__restrict__ h,
+                                                        int64_t ldh, const float *__restrict__ w2, int64_t B,
+                                                        int H2, int A1, float *__restrict__ gh,
+                                                        float *__restrict__ gw2, float *__restrict__ gb2,
+                                                        float *__restrict__ gb1, const float *__restrict__ td_abs,
+                                                        float *__restrict__ td_acc) {
+  __shared__ float red[kHbRows][kHbCols + 1];
+  const int tid = threadIdx.x;
+  if ((int)blockIdx.x == H2 / kHbCols) {  // gb2 and the |td| mean
+    __shared__ float tr[256];
+    for (int a = 0; a <= A1; ++a) {
+      if (a == A1 && !(td_abs && td_acc)) break;
+      float s = 0.0f;
+      for (int64_t r = tid; r < B; r += 256) s = radd(s, a < A1 ? dq[r * A1 + a] : td_abs[r]);
+      tr[tid] = s;
+      __syncthreads();
+      for (int st = 128; st > 0; st >>= 1) {
+        if (tid < st) tr[tid] = radd(tr[tid], tr[tid + st]);
+        __syncthreads();
+      }
+      if (tid == 0) {
+        if (a < A1) gb2[a] = tr[0];
+        else td_acc[0] = radd(td_acc[0], tr[0] / (float)B);  // _err_acc.add_(td.mean())
+      }
+      __syncthreads();
+    }
+    return;
+  }
+  const int c = tid % kHbCols, rg = tid / kHbCols;
+  const int j = (int)blockIdx.x * kHbCols + c;
+  float wc[kHbMaxA1], aw[kHbMaxA1];
+#pragma unroll
+  for (int a = 0; a < kHbMaxA1; ++a) {
+    wc[a] = a < A1 ? w2[(int64_t)a * H2 + j] : 0.0f;
+    aw[a] = 0.0f;
+  }
+  float ab = 0.0f;
+  for (int64_t r = rg; r < B; r += kHbRows) {
+    const float hv = h[r * ldh + j];
+    const float *d = dq + r * A1;
+    float g = 0.0f;
+#pragma unroll
+    for (int a = 0; a < kHbMaxA1; ++a)
+      if (a < A1) {
+        const float da = d[a];
+        g = radd(g, rmul(da, wc[a]));
+        aw[a] = radd(aw[a], rmul(da, hv));
+      }
+    g = hv > 0.0f ? g : 0.0f;  // threshold_backward(g, h, 0)
+    gh[r * H2 + j] = g;
+    ab = radd(ab, g);
+  }
+  // fixed-order sums over the row groups: gb1, then each row of gw2
+  for (int a = -1; a < A1; ++a) {
+    float v = ab;
+#pragma unroll
+    for (int k = 0; k < kHbMaxA1; ++k)
+      if (k == a) v = aw[k];
+    red[rg][c] = v;
+    __syncthreads();
+    if (rg == 0) {
+      float s = red[0][c];
+      for (int k = 1; k < kHbRows; ++k) s = radd(s, red[k][c]);
+      if (a < 0) gb1[j] = s;
+      else gw2[(int64_t)a * H2 + j] = s;
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace rth
 
 using namespace rth;
@@ -322,6 +404,18 @@ int rth_heads_split_grad(const float *gw1, const float *gb1, const float *gw2, c
   hipLaunchKernelGGL(k_heads_split_grad, dim3((unsigned)(2 * H + 1)), dim3(256), lds, as_stream(stream), d, gw1, gb1,
                      gw2, gb2, grads[0],
                      grads[1], grads[2], grads[3], grads[4], grads[5], grads[6], grads[7]);
+  RTH_LAUNCHED();
+  return RTH_OK;
+}
+
+int rth_heads_backward(const float *dq, const float *h, int64_t ldh, const float *w2, int64_t B, int32_t H2,
+                       int32_t A1, float *gh, float *gw2, float *gb2, float *gb1, const float *td_abs, float *td_acc,
+                       void *stream) {
+  RTH_REQUIRE(dq && h && w2 && gh && gw2 && gb2 && gb1, "rth_heads_backward: NULL argument");
+  RTH_REQUIRE(B >= 1 && A1 >= 1 && A1 <= kHbMaxA1 && H2 >= kHbCols && H2 % kHbCols == 0 && ldh >= H2,
+              "rth_heads_backward: bad shape B=%lld H2=%d A1=%d ldh=%lld", (long long)B, H2, A1, (long long)ldh);
+  hipLaunchKernelGGL(k_heads_backward, dim3((unsigned)(H2 / kHbCols + 1)), dim3(256), 0, as_stream(stream), dq, h, ldh,
+                     w2, B, H2, A1, gh, gw2, gb2, gb1, td_abs, td_acc);
   RTH_LAUNCHED();
   return RTH_OK;
 }

@@ -1,0 +1,141 @@
+"""The learner's gradient pass for the dueling Nature-DQN as an explicit kernel sequence.
+
+Reference: reth/reth/algorithm/dqn/dqn_solver.py:68-117 (_calc_td_error, then
+loss.backward()) on reth/reth/algorithm/dqn/dqn_model.py:6-56.  Same math as the autograd
+path of solver.py (compute_grads with torch.autograd), without the autograd engine's glue:
+
+  forward   Q(s0) and Q(s1) of the online network as ONE pass over 2B stacks (the batch
+            slot keeps s1 right behind s0, replay.HbmReplay.new_batch), each conv one
+            rth_conv_bias_relu launch, FC1 one hipBLASLt GEMM with the bias+ReLU epilogue,
+            the block-diagonal FC2 one GEMM;
+  TD        rth_td_huber on the raw heads -> |td|, loss, d(loss)/d(heads of s0);
+  backward  FC2 + threshold + both bias sums in rth_heads_backward (also the Trainer's
+            mean |td|), FC1 as two GEMMs, conv3 / conv2 as rth_relu_bias_grad + MIOpen's data
+            and weight gradients, conv1 as rth_conv_relu_wgrad straight from the uint8 stacks
+            (f32 input: rth_relu_bias_grad + MIOpen's weight gradient), the merged-head
+            gradients mapped back onto the eight branch parameters by rth_heads_split_grad.
+
+Only the first B rows of the 2B forward are differentiated: they are contiguous views
+(NHWC, batch-major), so the backward reads them in place.
+"""
+import torch
+
+from . import _lib
+from ._lib import call, ctypes, ptr, stream_ptr
+
+
+def eligible(net, s0, s1):
+    """the explicit pass covers the channels-last dueling net whose three convs all run in
+    rth_conv_bias_relu, on uint8 stacks or f32 channels-last observations"""
+    if not (getattr(net, "dueling", False) and getattr(net, "hwc_features", False) and getattr(net, "hip_conv", False)):
+        return False
+    if not (torch.is_tensor(s0) and torch.is_tensor(s1) and s0.is_cuda and s1.is_cuda and s0.dtype == s1.dtype):
+        return False
+    if s0.dtype not in (torch.uint8, torch.float32) or s0.shape != s1.shape or s0.dim() != 4:
+        return False
+    shapes = net._torso_shapes(tuple(s0.shape[1:]), s0.dtype == torch.uint8)
+    return all(sh is not None for _, sh in shapes)
+
+
+def _pair(s0, s1):
+    """[s0; s1] as one [2B, ...] tensor: a view when s1 sits right behind s0 in memory (the
+    apex batch slots), else a copy"""
+    u8 = s0.dtype == torch.uint8
+    fmt = torch.contiguous_format if u8 else torch.channels_last
+    if s0.is_contiguous(memory_format=fmt) and s1.is_contiguous(memory_format=fmt) and s1.stride() == s0.stride() \
+            and s1.data_ptr() == s0.data_ptr() + s0.numel() * s0.element_size():
+        return torch.as_strided(s0, (2 * s0.shape[0], *s0.shape[1:]), s0.stride())
+    return torch.cat([s0, s1]).contiguous(memory_format=fmt)
+
+
+def _nhwc(t):
+    return t if t.is_contiguous(memory_format=torch.channels_last) else t.contiguous(memory_format=torch.channels_last)
+
+
+def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None):
+    """forward + TD + backward of one learner batch; sets .grad of every online parameter
+    and returns (loss [], |td| [B]).  q1t: the target network's heads on s1 if precomputed
+    (DQNSolver.target_heads).  td_acc (nullable f32 device scalar): += mean |td|."""
+    from .solver import td_huber_forward
+
+    net = solver.q_network
+    B = s0.shape[0]
+    u8 = s0.dtype == torch.uint8
+    pair = bool(solver.double_q)
+    x = _pair(s0, s1) if pair else (s0 if u8 else _nhwc(s0))
+    n = x.shape[0]
+    convs = net._convs()
+    shapes = [sh for _, sh in net._torso_shapes(tuple(s0.shape[1:]), u8)]
+    with torch.no_grad():
+        w1, b1, w2, b2 = net._merged_head_weights()
+        packed = net.pack_convs()
+        st = stream_ptr()
+        ys, h = [], x
+        for li, (conv, shape) in enumerate(zip(convs, shapes)):
+            ho = (shape.hin - shape.kh) // shape.stride + 1
+            wo = (shape.win - shape.kw) // shape.stride + 1
+            y = torch.empty((n, shape.cout, ho, wo), dtype=torch.float32, device=x.device,
+                            memory_format=torch.channels_last)
+            call("rth_conv_bias_relu", ctypes.byref(shape), ptr(h), None, n, ptr(net._packed_for(packed, li, u8)),
+                 ptr(conv.bias), ptr(y), st)
+            ys.append(y)
+            h = y
+        feat = h.permute(0, 2, 3, 1).reshape(n, -1)  # NHWC flatten: a view
+        h1 = torch._addmm_activation(b1, feat, w1.t())
+        heads = torch.addmm(b2, h1, w2.t())
+        if q1t is None:
+            q1t = solver.target_heads(s1)
+        q0 = heads[:B]
+        q1o = heads[B:] if pair else None
+        loss, td_abs, dq = td_huber_forward(q0, q1o, q1t, a, r, done, isw, solver.gamma_n, solver.double_q,
+                                            want_dq=True, dueling=True)
+        # FC2 + threshold + bias sums
+        H2, A1 = w1.shape[0], w2.shape[0]
+        gh1 = torch.empty((B, H2), dtype=torch.float32, device=x.device)
+        gw2, gb2, gb1 = torch.empty_like(w2), torch.empty_like(b2), torch.empty_like(b1)
+        call("rth_heads_backward", ptr(dq), ptr(h1), h1.stride(0), ptr(w2), B, H2, A1, ptr(gh1), ptr(gw2), ptr(gb2),
+             ptr(gb1), ptr(td_abs), ptr(td_acc), st)
+        # FC1
+        gfeat = torch.mm(gh1, w1)
+        gw1 = torch.mm(gh1.t(), feat[:B])
+        c3 = convs[-1]
+        g = gfeat.view(B, ys[-1].shape[2], ys[-1].shape[3], c3.out_channels).permute(0, 3, 1, 2)
+        grads = {}
+        if getattr(net, "_ws", None) is None or net._ws[0].device != x.device:
+            net._ws = [torch.zeros(_lib.lib().rth_relu_bias_grad_workspace(m.out_channels), dtype=torch.uint8,
+                                   device=x.device) for m in convs]
+        for li in range(len(convs) - 1, -1, -1):
+            conv, y = convs[li], ys[li][:B]
+            if li == 0 and u8:  # ReLU mask + weight/bias gradients from the stacks
+                from .model import _wgrad_workspace
+
+                gw = torch.empty(conv.weight.shape, dtype=torch.float32, device=x.device,
+                                 memory_format=torch.channels_last)
+                db = torch.empty(conv.out_channels, dtype=torch.float32, device=x.device)
+                call("rth_conv_relu_wgrad", ctypes.byref(shapes[0]), ptr(x), None, B, ptr(_nhwc(g)), ptr(y), ptr(gw),
+                     ptr(db), ptr(_wgrad_workspace(shapes[0], x.device)), st)
+                grads[conv.weight], grads[conv.bias] = gw, db
+                break
+            g = _nhwc(g)
+            gy = torch.empty_like(y)
+            nb, c, hh, ww = y.shape
+            db = torch.empty(c, dtype=torch.float32, device=x.device)
+            call("rth_relu_bias_grad", ptr(g), ptr(y), ptr(gy), ptr(db), ptr(net._ws[li]), nb * hh * ww, c, st)
+            xin = ys[li - 1][:B] if li > 0 else x[:B]
+            w = _nhwc(conv.weight.detach())
+            gx, gw, _ = torch.ops.aten.convolution_backward(gy, xin, w, None, list(conv.stride), [0, 0], [1, 1], False,
+                                                            [0, 0], 1, [li > 0, True, False])
+            grads[conv.weight], grads[conv.bias] = gw, db
+            g = gx
+        # merged heads -> the eight branch parameters
+        hp = net._head_params()
+        hgrads = [torch.empty_like(p) for p in hp]
+        c_, fh, fw = net._feat_chw
+        arr = (_lib.c_vp * 8)(*[t.data_ptr() for t in hgrads])
+        call("rth_heads_split_grad", ptr(gw1), ptr(gb1), ptr(gw2), ptr(gb2), hp[0].shape[0], hp[0].shape[1],
+             hp[4].shape[0], c_, fh * fw, arr, st)
+        for p, gr in zip(hp, hgrads):
+            grads[p] = gr
+    for p in net.parameters():
+        p.grad = grads[p]
+    return loss.view(()), td_abs

@@ -37,7 +37,7 @@ class ClipAdam(torch.optim.Optimizer):
                 raise ValueError("ClipAdam: parameters must be dense float32 tensors on one device")
         self.max_norm = max_norm
         self._step = torch.zeros(1, dtype=torch.int64, device=dev)
-        self._ws = torch.empty(_lib.lib().rth_clip_adam_workspace(), dtype=torch.uint8, device=dev)
+        self._ws = torch.zeros(_lib.lib().rth_clip_adam_workspace(), dtype=torch.uint8, device=dev)  # ticket = 0
         self.total_norm = torch.zeros(1, dtype=torch.float32, device=dev)
         for p in ps:
             st = self.state[p]

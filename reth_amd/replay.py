@@ -359,7 +359,18 @@ class HbmReplay:
         ev1.record()
 
     def new_batch(self, batch_size):
-        cols = [c.empty_out(batch_size, self.device) for c in self.columns]
+        """empty (cols, idx, isw) batch buffers.  Columns of identical row shape and sampled
+        dtype share one allocation, back to back in column order (s1 directly behind s0), so
+        a learner can run one forward over [s0; s1] without a copy (fused_learner._pair)"""
+        groups = {}
+        for i, c in enumerate(self.columns):
+            groups.setdefault((c.shape, c.out_dtype, c.channels_last), []).append(i)
+        cols = [None] * len(self.columns)
+        for members in groups.values():
+            c = self.columns[members[0]]
+            buf = c.empty_out(len(members) * batch_size, self.device)
+            for k, i in enumerate(members):
+                cols[i] = buf[k * batch_size:(k + 1) * batch_size]
         idx = torch.empty(batch_size, dtype=torch.int64, device=self.device)
         isw = torch.empty(batch_size, dtype=torch.float64, device=self.device)
         return cols, idx, isw

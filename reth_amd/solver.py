@@ -15,7 +15,7 @@ import io
 import numpy as np
 import torch
 
-from . import _lib
+from . import _lib, fused_learner
 from ._lib import call, ptr, stream_ptr
 from .model import default_models
 from .optim import ClipAdam
@@ -164,6 +164,10 @@ class DQNSolver(Algorithm):
                                         if update_target_interval is not None else None)
         # graph replay runs the (host-side) target-sync Interval outside the captured step
         self.auto_target_update = True
+        # explicit kernel-sequence gradient pass (fused_learner.py) where it applies; False:
+        # torch.autograd over the same forward (the A/B reference)
+        self.fused_grads = True
+        self.td_mean_acc = None  # Trainer's device mean-|td| accumulator (fused pass adds to it)
 
     # ------------------------------------------------------------------ target / weights
     @torch.no_grad()
@@ -243,6 +247,13 @@ class DQNSolver(Algorithm):
         q1t: the target network's output on this batch's s1 if already computed
         (target_heads), else it is computed here"""
         s0, a, r, s1, done = self._tensors(batch)
+        isw = None if weights is None else (weights if torch.is_tensor(weights) else torch.as_tensor(np.asarray(weights)))
+        if self.fused_grads and self._heads and fused_learner.eligible(self.q_network, s0, s1):
+            loss, td_abs = fused_learner.dueling_grads(self, s0, a, r, s1, done, isw, q1t, td_acc=self.td_mean_acc)
+            if self.td_mean_acc is not None:
+                td_abs._rth_mean_tracked = True
+            self.last_loss = loss.detach()
+            return td_abs
         merged = packed = None
         if self._heads:  # merged dueling head weights (and packed conv weights of the HIP torso),
             # built once per weight version and shared by both online passes
@@ -254,7 +265,6 @@ class DQNSolver(Algorithm):
         else:
             q0 = self.q_network(s0)
         q1o, q1t = self._forward_targets(s1, merged, packed, q1t)
-        isw = None if weights is None else (weights if torch.is_tensor(weights) else torch.as_tensor(np.asarray(weights)))
         loss, td_abs = td_huber_loss(q0, q1o, q1t, a, r, done, isw, self.gamma_n, self.double_q, self._heads)
         # grads set to None: backward hands each parameter its gradient buffer directly
         # (no accumulate-add into a zeroed .grad, no zero fill); inside a captured HIP graph

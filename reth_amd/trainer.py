@@ -34,6 +34,11 @@ class Trainer:
         self.on_step_end = [Interval(self.print, int(print_interval))]
         self._err_acc = None  # persistent device accumulator (in-place: graph-replay safe)
         self._err_n = 0
+        dev = getattr(solver, "device", None)
+        if dev is not None and getattr(dev, "type", None) == "cuda" and hasattr(solver, "td_mean_acc"):
+            # the solver's fused gradient pass adds mean |td| here itself (rth_heads_backward)
+            self._err_acc = torch.zeros((), dtype=torch.float32, device=dev)
+            solver.td_mean_acc = self._err_acc
 
     @property
     def cur_time(self):
@@ -54,6 +59,8 @@ class Trainer:
         return self.solver.save_weights(stream)
 
     def _track(self, td):
+        if getattr(td, "_rth_mean_tracked", False):
+            return
         if self._err_acc is None:
             self._err_acc = torch.zeros((), dtype=torch.float32, device=td.device)
         self._err_acc.add_(td.float().mean())

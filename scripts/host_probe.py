@@ -80,6 +80,28 @@ def main():
     torch.cuda.synchronize()
     t2 = time.perf_counter()
     print(f"pipelined: host {1e6 * (t1 - t0) / n:8.1f} us/iter, wall {1e6 * (t2 - t0) / n:8.1f} us/iter")
+    # each block alone on the GPU (no concurrent work on the other stream)
+    G = ax._graphs
+
+    def alone(label, fn, reps=20):
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1) * 1e3)
+        ts.sort()
+        print(f"alone: {label:40s} median {ts[len(ts) // 2]:8.1f} us  min {ts[0]:8.1f} us")
+
+    k = ax.loader._pending[0]
+    alone("learner graph (pre, slot k)", lambda: G["learn"][("pre", k)].replay())
+    alone("learner graph (full, slot k)", lambda: G["learn"][("full", k)].replay())
+    alone("actor graph", lambda: G["act"][ax.actors.pushes % 2].replay())
+    alone("target pass graph", lambda: G["tgt"][k].replay())
+    alone("sample + gather", lambda: ax.replay.sample_into(512, *ax.loader._slots[1 - k]))
 
 
 if __name__ == "__main__":

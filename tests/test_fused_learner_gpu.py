@@ -1,0 +1,116 @@
+"""The explicit learner gradient pass (reth_amd/fused_learner.py) against torch.autograd over
+the same network: rth_heads_backward against the addmm -> relu autograd chain, and the whole
+pass (one 2B forward, TD, backward) against DQNSolver's autograd path and the reference's
+update (golden vectors, dqn_solver.py:104-124) on uint8 stacks."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("B,H2,A1", [(512, 512, 7), (37, 64, 5), (8, 512, 19)])
+def test_heads_backward_matches_autograd(dev, B, H2, A1):
+    from reth_amd._lib import call, ptr, stream_ptr
+
+    g = torch.Generator(device=dev).manual_seed(B + A1)
+    h = torch.relu(torch.randn(B, H2, device=dev, generator=g))
+    w2 = torch.randn(A1, H2, device=dev, generator=g) * 0.05
+    dq = torch.randn(B, A1, device=dev, generator=g) * 1e-3
+    td = torch.rand(B, device=dev, generator=g)
+    acc = torch.full((), 0.25, device=dev)
+    gh, gw2 = torch.empty(B, H2, device=dev), torch.empty(A1, H2, device=dev)
+    gb2, gb1 = torch.empty(A1, device=dev), torch.empty(H2, device=dev)
+    call("rth_heads_backward", ptr(dq), ptr(h), H2, ptr(w2), B, H2, A1, ptr(gh), ptr(gw2), ptr(gb2), ptr(gb1),
+         ptr(td), ptr(acc), stream_ptr())
+    # autograd of heads = addmm(b2, h, w2^T), h = relu(pre)
+    hh = h.clone().requires_grad_(True)
+    ww = w2.clone().requires_grad_(True)
+    bb = torch.zeros(A1, device=dev, requires_grad=True)
+    torch.addmm(bb, hh, ww.t()).backward(dq)
+    want_gh = torch.ops.aten.threshold_backward(hh.grad, h, 0)
+    torch.testing.assert_close(gh, want_gh, rtol=1e-5, atol=1e-9)
+    torch.testing.assert_close(gw2, ww.grad, rtol=1e-5, atol=1e-8)
+    torch.testing.assert_close(gb2, bb.grad, rtol=1e-5, atol=1e-9)
+    torch.testing.assert_close(gb1, want_gh.sum(0), rtol=1e-5, atol=1e-8)
+    torch.testing.assert_close(acc, 0.25 + td.mean(), rtol=1e-6, atol=0)
+    # deterministic
+    gh2 = torch.empty_like(gh)
+    call("rth_heads_backward", ptr(dq), ptr(h), H2, ptr(w2), B, H2, A1, ptr(gh2), ptr(gw2), ptr(gb2), ptr(gb1),
+         None, None, stream_ptr())
+    assert torch.equal(gh, gh2)
+
+
+def _solver(dev, seed):
+    from reth_amd.solver import Box, DQNSolver, Discrete
+
+    torch.manual_seed(seed)
+    return DQNSolver(Box(0, 255, (4, 84, 84)), Discrete(6), gamma=0.99, clip_value=40, double_q=True, dueling=True,
+                     learning_rate=1e-4, adam_epsilon=1.5e-4, update_target_interval=100, device=dev, n_step=3,
+                     channels_last=True)
+
+
+@pytest.mark.parametrize("u8,adjacent", [(True, True), (True, False), (False, False)])
+def test_fused_grads_match_autograd(dev, u8, adjacent):
+    from reth_amd import fused_learner
+
+    B = 64
+    g = torch.Generator(device=dev).manual_seed(5)
+    frames = torch.randint(0, 256, (2 * B, 4, 84, 84), dtype=torch.uint8, device=dev, generator=g)
+    s0, s1 = frames[:B], frames[B:]
+    if not adjacent:
+        s1 = s1.clone()  # separate allocation -> the pass concatenates
+    if not u8:
+        s0 = s0.float().contiguous(memory_format=torch.channels_last)
+        s1 = s1.float().contiguous(memory_format=torch.channels_last)
+    a = torch.randint(0, 6, (B,), device=dev, generator=g)
+    r = (torch.rand(B, device=dev, generator=g) < 0.3).float()
+    done = (torch.rand(B, device=dev, generator=g) < 0.1).float()
+    isw = torch.rand(B, device=dev, generator=g, dtype=torch.float64) + 0.5
+    solver = _solver(dev, 7)
+    for p in solver.target_q_network.parameters():  # target != online
+        p.data.add_(torch.randn_like(p) * 1e-3)
+    solver.target_q_network.freeze_heads()
+    assert fused_learner.eligible(solver.q_network, s0, s1)
+    res = {}
+    for fused in (True, False):
+        solver.fused_grads = fused
+        td = solver.compute_grads([s0, a, r, s1, done], weights=isw)
+        res[fused] = (td.clone(), float(solver.last_loss), [p.grad.clone() for p in solver.q_network.parameters()])
+    torch.testing.assert_close(res[True][0], res[False][0], rtol=1e-5, atol=1e-6)
+    assert abs(res[True][1] - res[False][1]) <= 1e-5 * max(1.0, abs(res[False][1]))
+    for (name, _), x, y in zip(solver.q_network.named_parameters(), res[True][2], res[False][2]):
+        err = ((x - y).abs().max() / y.abs().max().clamp_min(1e-30)).item()
+        assert err < 1e-4, (name, err)
+
+
+@pytest.mark.parametrize("name", ["dqn_pong_b8.npz", "dqn_pong_b32.npz"])
+def test_fused_update_u8_vs_reference(golden, dev, name):
+    """DQNSolver.update on uint8 stacks (the apex learner's input) through the fused pass
+    vs the reference's torch-CPU update on the same frames as float32"""
+    gd = golden(name)
+    solver = _solver(dev, int(gd["seed"]))
+    assert np.array_equal(gd["s0"], gd["s0"].astype(np.uint8)) and np.array_equal(gd["s1"], gd["s1"].astype(np.uint8))
+    B = gd["s0"].shape[0]
+    frames = torch.as_tensor(np.concatenate([gd["s0"], gd["s1"]]).astype(np.uint8), device=dev)
+    batch = [frames[:B], gd["a"], gd["r"], frames[B:], gd["done"]]
+    for k in range(2):
+        td = solver.update(batch, weights=gd["isw"]).numpy()
+        np.testing.assert_allclose(td, gd[f"upd{k}_abs_td"], rtol=1e-5, atol=1e-5)
+        sd = solver.q_network.state_dict()
+        head = np.stack([np.pad(v.flatten()[:16].float().cpu().numpy(), (0, max(0, 16 - v.numel())),
+                                constant_values=np.nan) for v in sd.values()])
+        np.testing.assert_allclose(head, gd[f"upd{k}_head"], rtol=1e-4, atol=2e-6)
+
+
+def test_batch_slots_keep_s1_behind_s0(dev):
+    from reth_amd.actors import apex_columns
+    from reth_amd.fused_learner import _pair
+    from reth_amd.replay import HbmReplay
+
+    rep = HbmReplay(1024, apex_columns(True, frames_u8=True), 0.5, "0.4,1,100", dev)
+    cols, idx, isw = rep.new_batch(32)
+    s0, s1 = cols[0], cols[3]
+    assert s1.data_ptr() == s0.data_ptr() + s0.numel()
+    x = _pair(s0, s1)
+    assert x.data_ptr() == s0.data_ptr() and x.shape[0] == 64

@@ -252,6 +252,12 @@ int rth_synth_env_step(uint8_t *frames_dev, int64_t n_actors, int32_t ring, int6
 /* initial reset of every actor into slot 1 (t = 0) */
 int rth_synth_env_reset(uint8_t *frames_dev, int64_t n_actors, int32_t ring, uint64_t seed,
                         int64_t *cur_slot_dev, void *stream);
+/* stream compaction for variable-size device batches: out[0..k) = vals[i] for the i < n with
+ * flag[i] != 0, in order of i (at most cap of them), out[k..cap) = fill, *count_out = base + k.
+ * The actors use it to list the terminal stacks of the episodes that just ended (flag = done,
+ * vals = the step's next-observation handles) behind the next acting batch. */
+int rth_compact_flagged(const float *flag_dev, const int64_t *vals_dev, int64_t n, int64_t *out_dev, int64_t cap,
+                        int64_t fill, int64_t base, int64_t *count_out_dev, void *stream);
 
 /* ------------------------------------------------------------------------------------
  * Learner: DQNSolver TD error + Huber (reth/reth/algorithm/dqn/dqn_solver.py:68-124).
@@ -330,6 +336,12 @@ int rth_conv_pack_many(int32_t n, const rth_conv_shape *shapes, const float *con
                        float *const *packed_dev, void *stream);
 int rth_conv_bias_relu(const rth_conv_shape *shape, const void *x_dev, const int64_t *rows_dev, int64_t n,
                        const float *packed_dev, const float *bias_dev, float *y_dev, void *stream);
+/* rth_conv_bias_relu over the first min(n_max, *n_dev) samples, the count read on the device
+ * (graph replay of a variable-size batch: the actors' acting stacks plus the terminal stacks
+ * of the episodes that just ended); outputs past the count are left untouched. */
+int rth_conv_bias_relu_upto(const rth_conv_shape *shape, const void *x_dev, const int64_t *rows_dev, int64_t n_max,
+                            const int64_t *n_dev, const float *packed_dev, const float *bias_dev, float *y_dev,
+                            void *stream);
 /* Backward of relu(conv2d(x, w) + b) for the weights and bias, on uint8 stacks (conv1, whose
  * input needs no gradient): gy = (y > 0) ? g : 0, gw = sum over output pixels of gy times the
  * input window (OHWI [cout, kh, kw, cin], the layout of a channels_last weight), gb = sum of

@@ -93,6 +93,7 @@ SIGNATURES = {
     # actors
     "rth_eps_greedy": (c_i32, [c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_u64, c_u64, c_vp, c_vp, c_vp]),
     "rth_counter_add": (c_i32, [c_vp, c_i64, c_vp]),
+    "rth_compact_flagged": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp]),
     "rth_nstep_create": (c_i32, [c_i64, c_i32, c_f64, c_i32, c_i32, ctypes.POINTER(c_vp)]),
     "rth_nstep_destroy": (c_i32, [c_vp]),
     "rth_nstep_reset": (c_i32, [c_vp, c_vp]),
@@ -120,6 +121,7 @@ SIGNATURES = {
     "rth_conv_pack_many": (c_i32, [c_i32, ctypes.POINTER(ConvShape), ctypes.POINTER(c_vp), ctypes.POINTER(c_vp),
                                    c_vp]),
     "rth_conv_bias_relu": (c_i32, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "rth_conv_bias_relu_upto": (c_i32, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "rth_atari_create": (c_i32, [c_i32, c_i32, c_i32, c_i32, c_i32, ctypes.POINTER(c_vp)]),
     "rth_atari_destroy": (c_i32, [c_vp]),
     "rth_atari_step": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),

@@ -57,7 +57,9 @@ class VecActors:
         self.ring = ring
         dev = self.device
         N = self.N
-        self.frames = torch.empty((N * ring, *OBS_SHAPE), dtype=torch.uint8, device=dev)
+        # one extra all-zero stack at N * ring: the sink handle of unused batch slots
+        self.frames = torch.empty((N * ring + 1, *OBS_SHAPE), dtype=torch.uint8, device=dev)
+        self.frames[N * ring].zero_()
         self.cur_slot = torch.empty(N, dtype=torch.int64, device=dev)
         e = apex_epsilons(N, actor_offset, total_actors) if eps is None else np.broadcast_to(np.asarray(eps, np.float64), (N,))
         self.eps = torch.as_tensor(np.ascontiguousarray(e), dtype=torch.float64, device=dev)
@@ -79,6 +81,19 @@ class VecActors:
         h = _lib.c_vp()
         call("rth_nstep_create", N, self.n_step, self.gamma, int(nstep_mode), dev.index, _lib.ctypes.byref(h))
         self._nstep = h.value
+        # deduplicated prioritisation (step_fused dedup mode): per frame-ring stack, the actor
+        # network's heads from the last forward that covered it; the rows' s0 / s1 are looked
+        # up there instead of being run through the network again.  Row N * ring is a sink for
+        # the unused slots of the variable-size batch.
+        self._sink = N * ring
+        self.qcache = None  # [N * ring + 1, A + 1], allocated at the first forward
+        # forward batch handles [acting | terminal stacks of the last step (sink-padded) |
+        # previous rows' s0 | their s1]: dedup forwards the first 2N (n_ext counted), full all 4N
+        self.hx = torch.full((4 * N,), self._sink, dtype=torch.int64, device=dev)
+        self.n_ext = torch.full((1,), N, dtype=torch.int64, device=dev)  # acting + terminal stacks
+        self._base = torch.arange(N, device=dev, dtype=torch.int64) * ring
+        self.qrows = None
+        self.fresh = 0       # steps since the actor network's weights last changed
         self.t = 0           # env steps taken (per actor): host mirror of t_dev
         self.t_dev = torch.zeros(1, dtype=torch.int64, device=dev)  # what the kernels read
         self.pushes = 0
@@ -116,8 +131,7 @@ class VecActors:
         return _q_forward(q_net, self.gather_f32(handles, buf))
 
     def current_obs_handles(self):
-        if not hasattr(self, "_base"):
-            self._base = torch.arange(self.N, device=self.device, dtype=torch.int64) * self.ring
+        if not hasattr(self, "_cur_h"):
             self._cur_h = torch.empty_like(self._base)
         return torch.add(self.cur_slot, self._base, out=self._cur_h)
 
@@ -148,34 +162,94 @@ class VecActors:
     def _bind_rows(self, rs):
         self.row_s0, self.row_a, self.row_r, self.row_s1, self.row_done = rs.s0, rs.a, rs.r, rs.s1, rs.done
 
+    def weights_changed(self):
+        """the actor network was reloaded: cached heads are stale until n + 2 steps passed"""
+        self.fresh = 0
+
+    @staticmethod
+    def _hip_heads(q_net):
+        return getattr(q_net, "hwc_features", False) and getattr(q_net, "dueling", False) and q_net.hip_conv
+
+    def dedup_ready(self, q_net):
+        """every stack a row prioritised now can reference has cached heads computed with the
+        current weights: its s0 was acted at most n + 1 steps ago, its s1 was acted at most n
+        steps ago or is the terminal stack of an episode that ended in the last n + 1 steps
+        (each forward -- dedup or full -- covers the previous step's terminal stacks)"""
+        return self.qcache is not None and self.fresh >= self.n_step + 2 and self._hip_heads(q_net)
+
+    def _scatter_heads(self, q, handles, n):
+        """qcache[handles[i]] = q[i] for i < n (the sink absorbs unused slots)"""
+        A1 = q.shape[1]
+        if self.qcache is None:
+            self.qcache = torch.zeros((self.N * self.ring + 1, A1), dtype=torch.float32, device=self.device)
+            self.qrows = torch.empty((2 * self.N, A1), dtype=torch.float32, device=self.device)
+        call("rth_copy_rows", ptr(self.qcache), 0, ptr(handles), ptr(q), 0, None, n, A1, _lib.RTH_F32, _lib.RTH_F32, 0,
+             stream_ptr())
+
+    def _terminal_stacks(self):
+        """behind the next acting batch: the terminal stacks of this step's finished episodes
+        (the s1 a done row keeps, which the next acting batch -- reset stacks -- does not cover)"""
+        N = self.N
+        call("rth_compact_flagged", ptr(self.done), ptr(self.s1_h), N, ptr(self.hx[N:2 * N]), N, self._sink, N,
+             ptr(self.n_ext), stream_ptr())
+
     @torch.no_grad()
-    def step_fused(self, q_net):
+    def step_fused(self, q_net, dedup=None):
         """one environment step for every actor with the previous step's rows prioritised in
         the same forward pass: Q-net over [acting stacks; prev rows' s0; prev rows' s1]
         (3N) -> rth_eps_greedy on the first N -> rth_td_huber (calc_loss, target == online)
         on the rest -> env step -> n-step push into the other row set.  The reference's
         actor runs calc_loss on a 64-row batch well after the rows were emitted
         (test/apex-dqn/worker.py:55-60); here the delay is one step.
+        dedup (default: whenever dedup_ready): the forward covers only the acting stacks and
+        the terminal stacks of the episodes that ended in the previous step (a device-side
+        count); the rows' heads come from the per-stack cache -- the same values, about a third
+        of the forward work.
         Returns (|td|, RowSet) of the previous step's rows, or (None, None) before any."""
         s = stream_ptr()
         p = self.pushes
         prev, cur = self._sets[(p - 1) % 2], self._sets[p % 2]
+        if dedup is None:
+            dedup = self.dedup_ready(q_net)
+        elif dedup and not self.dedup_ready(q_net):
+            raise RuntimeError("step_fused(dedup=True): the stack cache is not valid for the current weights")
         self.t += 1
         call("rth_counter_add", ptr(self.t_dev), 1, s)
         N = self.N
-        torch.cat([self.current_obs_handles(), prev.s0, prev.s1], out=self.handles3)
-        q, dueling = self._forward_stacks(q_net, self.handles3)
+        hip = self._hip_heads(q_net)
+        if dedup:
+            torch.add(self.cur_slot, self._base, out=self.hx[:N])
+            q = q_net.forward_heads(self.frames, rows=self.hx[:2 * N], n_dev=self.n_ext)
+            dueling = 1
+            self._scatter_heads(q, self.hx, 2 * N)
+            call("rth_copy_rows", ptr(self.qrows), 0, None, ptr(self.qcache), 0, ptr(prev.s0), N, q.shape[1],
+                 _lib.RTH_F32, _lib.RTH_F32, 0, s)
+            call("rth_copy_rows", ptr(self.qrows[N:]), 0, None, ptr(self.qcache), 0, ptr(prev.s1), N, q.shape[1],
+                 _lib.RTH_F32, _lib.RTH_F32, 0, s)
+            q0, q1 = self.qrows[:N], self.qrows[N:]
+        elif hip:  # everything: acting, last step's terminal stacks, the rows' s0 and s1 -> cache
+            torch.add(self.cur_slot, self._base, out=self.hx[:N])
+            torch.cat([prev.s0, prev.s1], out=self.hx[2 * N:])
+            q = q_net.forward_heads(self.frames, rows=self.hx)
+            dueling = 1
+            self._scatter_heads(q, self.hx, 4 * N)
+            q0, q1 = q[2 * N:3 * N], q[3 * N:]
+        else:
+            torch.cat([self.current_obs_handles(), prev.s0, prev.s1], out=self.handles3)
+            q, dueling = self._forward_stacks(q_net, self.handles3)
+            q0, q1 = q[N:2 * N], q[2 * N:]
         call("rth_eps_greedy", ptr(q), N, self.A, dueling, ptr(self.eps), None, None, self.seed, 0,
              ptr(self.t_dev), ptr(self.action), s)
-        q1 = q[2 * N:]
-        _, td_abs, _ = td_huber_forward(q[N:2 * N], q1, q1, prev.a, prev.r, prev.done, None, self.gamma_n, True,
+        _, td_abs, _ = td_huber_forward(q0, q1, q1, prev.a, prev.r, prev.done, None, self.gamma_n, True,
                                         want_dq=False, dueling=bool(dueling))
         call("rth_synth_env_step", ptr(self.frames), N, self.ring, 0, ptr(self.t_dev), ptr(self.cur_slot),
              ptr(self.action), self.seed, self.p_reward, self.p_done, ptr(self.reward), ptr(self.done), ptr(self.s0_h),
              ptr(self.s1_h), s)
         call("rth_nstep_push", self._nstep, ptr(self.s0_h), ptr(self.action), ptr(self.reward), ptr(self.s1_h),
              ptr(self.done), ptr(self.emit), ptr(cur.s0), ptr(cur.a), ptr(cur.r), ptr(cur.s1), ptr(cur.done), s)
+        self._terminal_stacks()
         self.pushes += 1
+        self.fresh += 1
         self._bind_rows(cur)
         return (td_abs, prev) if p > self.n_step else (None, None)
 

@@ -157,7 +157,8 @@ class ApexDQN:
 
     def _actor_host(self):
         """host-side actor bookkeeping between steps (weights reload: perwez RecvSocket)"""
-        self.subscriber.maybe_load(self.actor_net, self.actors.t)
+        if self.subscriber.maybe_load(self.actor_net, self.actors.t):
+            self.actors.weights_changed()
 
     def _learner_host(self):
         """host-side learner bookkeeping after an update (Trainer / Interval / weights send)"""
@@ -218,17 +219,24 @@ class ApexDQN:
         split = solver.grad_hook is not None
         G = dict(act=[], act_out=[], tgt=[], q1t=[], learn={}, learn_td={}, apply={}, grads={})
         with torch.cuda.stream(side):
-            # the actor block by push parity (fused_actor alternates row sets; both graphs
-            # are identical otherwise)
-            for _ in range(2):
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, stream=side):
-                    out = self._actor_compute()
-                G["act"].append(g)
-                G["act_out"].append(out)
-            if host[1] % 2:  # keep G["act"][k] <-> pushes % 2 == k
-                G["act"].reverse()
-                G["act_out"].reverse()
+            # the actor block by (mode, push parity): fused_actor alternates row sets; mode
+            # "dedup" takes the rows' heads from the per-stack cache (VecActors.step_fused),
+            # "full" runs them through the network (after a weights reload)
+            act = self.actors
+            fresh = act.fresh
+            modes = ["full"] + (["dedup"] if self.cfg.fused_actor and act._hip_heads(self.actor_net) else [])
+            G["act"], G["act_out"] = {}, {}
+            for mode in modes:
+                for _ in range(2):
+                    k = act.pushes % 2
+                    g = torch.cuda.CUDAGraph()
+                    act.fresh = act.n_step + 2 if mode == "dedup" else 0
+                    with torch.cuda.graph(g, stream=side):
+                        out = (act.step_fused(self.actor_net, dedup=mode == "dedup") if self.cfg.fused_actor
+                               else self._actor_compute())
+                    G["act"][mode, k] = g
+                    G["act_out"][mode, k] = out
+            act.fresh = fresh
             # the target network's output on each slot's s1, computed on the actor stream ahead
             # of the update (target_heads); "pre" learner graphs consume it, "full" ones
             # compute it themselves (after a target sync, and before any was precomputed)
@@ -256,7 +264,7 @@ class ApexDQN:
                             solver.apply_grads()
                         G["apply"][variant, p] = ga
         torch.cuda.current_stream(self.device).wait_stream(side)
-        self.actors.t, self.actors.pushes = host  # capture recorded, did not run, the step
+        self.actors.t, self.actors.pushes = host  # capture recorded, did not run, the steps
         self._graphs = G
 
     def _iteration_graph(self):
@@ -264,20 +272,7 @@ class ApexDQN:
             return self._iteration_graph_overlap()
         G = self._graphs
         act = self.actors
-        for _ in range(self.cfg.actor_steps_per_update):
-            self._actor_host()
-            k = act.pushes % 2
-            G["act"][k].replay()
-            act.t += 1
-            act.pushes += 1
-            td, rows = G["act_out"][k]
-            if self.cfg.fused_actor:
-                act._bind_rows(act._sets[k])  # this step's rows (appended next step)
-                if act.pushes - 1 > act.n_step:  # the previous step emitted rows
-                    act.append(self.replay, td, rows)
-            else:
-                act.append(self.replay, td)
-            self.env_steps += act.N
+        self._actor_block_graph()
         k = self.loader._pending.pop(0)
         v = ("full", k)
         G["learn"][v].replay()
@@ -293,10 +288,12 @@ class ApexDQN:
         for _ in range(self.cfg.actor_steps_per_update):
             self._actor_host()
             k = act.pushes % 2
-            G["act"][k].replay()
+            mode = "dedup" if ("dedup", k) in G["act"] and act.dedup_ready(self.actor_net) else "full"
+            G["act"][mode, k].replay()
             act.t += 1
             act.pushes += 1
-            td, rows = G["act_out"][k]
+            act.fresh += 1
+            td, rows = G["act_out"][mode, k]
             if self.cfg.fused_actor:
                 act._bind_rows(act._sets[k])
                 if act.pushes - 1 > act.n_step:

@@ -48,13 +48,13 @@ class AtariPreprocessor:
 
     def step(self, raw, frames, ring, prev_slot, new_slot, reset=None, out_frame=None):
         """push the preprocessed frames onto each actor's stack: frames is the ring
-        [n * ring, stack, 84, 84] uint8; slot new_slot[i] <- slot prev_slot[i] shifted by one
+        [n * ring (+ trailing stacks, e.g. VecActors' sink), stack, 84, 84] uint8; slot new_slot[i] <- slot prev_slot[i] shifted by one
         + the new frame (or the frame `stack` times where reset[i])"""
         raw = self._check_raw(raw)
         n = raw.shape[0]
         if frames.dtype != torch.uint8 or tuple(frames.shape[1:]) != (self.stack, *self.out_hw) or \
-                frames.shape[0] != n * ring or not frames.is_contiguous():
-            raise ValueError("frames must be a contiguous uint8 ring [n * ring, stack, 84, 84]")
+                frames.shape[0] < n * ring or not frames.is_contiguous():
+            raise ValueError("frames must be a contiguous uint8 ring [>= n * ring, stack, 84, 84]")
         for t in (prev_slot, new_slot):
             if t.dtype != torch.int64 or t.numel() != n:
                 raise ValueError("slots must be int64 [n]")

@@ -148,6 +148,38 @@ __global__ __launch_bounds__(kEnvThreads) void k_env_reset(uint8_t *frames, int 
   if (threadIdx.x == 0) cur_slot[i] = 1;
 }
 
+
+// out[0..k) = vals[i] for the i < n with flag[i] != 0, in order of i; out[k..cap) = fill;
+// *count_out = base + k.  One workgroup, a block scan per 1024-entry chunk.
+constexpr int kCompactThreads = 1024;
+__global__ __launch_bounds__(kCompactThreads) void k_compact_flagged(const float *__restrict__ flag,
+                                                                    const int64_t *__restrict__ vals, int64_t n,
+                                                                    int64_t *__restrict__ out, int64_t cap,
+                                                                    int64_t fill, int64_t base,
+                                                                    int64_t *__restrict__ count_out) {
+  __shared__ int scan[kCompactThreads];
+  const int tid = threadIdx.x;
+  int64_t k = 0;
+  for (int64_t c0 = 0; c0 < n; c0 += kCompactThreads) {
+    const int64_t i = c0 + tid;
+    const int f = (i < n && flag[i] != 0.0f) ? 1 : 0;
+    scan[tid] = f;
+    __syncthreads();
+    for (int off = 1; off < kCompactThreads; off <<= 1) {  // inclusive Hillis-Steele scan
+      const int v = tid >= off ? scan[tid - off] : 0;
+      __syncthreads();
+      scan[tid] += v;
+      __syncthreads();
+    }
+    if (f && k + scan[tid] - 1 < cap) out[k + scan[tid] - 1] = vals[i];
+    k += scan[kCompactThreads - 1];
+    __syncthreads();
+  }
+  const int64_t kk = k < cap ? k : cap;
+  for (int64_t j = kk + tid; j < cap; j += kCompactThreads) out[j] = fill;
+  if (tid == 0) *count_out = base + kk;
+}
+
 }  // namespace rth
 
 using namespace rth;
@@ -247,6 +279,15 @@ int rth_synth_env_reset(uint8_t *frames, int64_t N, int32_t ring, uint64_t seed,
   RTH_REQUIRE(frames && cur_slot && N >= 1 && ring >= 4, "rth_synth_env_reset: bad arguments");
   hipLaunchKernelGGL(k_env_reset, dim3((unsigned)N), dim3(kEnvThreads), 0, as_stream(stream), frames, ring, seed,
                      cur_slot);
+  RTH_LAUNCHED();
+  return RTH_OK;
+}
+
+int rth_compact_flagged(const float *flag, const int64_t *vals, int64_t n, int64_t *out, int64_t cap, int64_t fill,
+                        int64_t base, int64_t *count_out, void *stream) {
+  RTH_REQUIRE(flag && vals && out && count_out && n >= 0 && cap >= 0, "rth_compact_flagged: bad arguments");
+  hipLaunchKernelGGL(k_compact_flagged, dim3(1), dim3(kCompactThreads), 0, as_stream(stream), flag, vals, n, out, cap,
+                     fill, base, count_out);
   RTH_LAUNCHED();
   return RTH_OK;
 }

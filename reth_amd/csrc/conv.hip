@@ -75,6 +75,7 @@ struct ConvGeom {
 template <int MODE, int KH, int KW, int S, int CIN, int COUT, int HIN, int WIN, int WAVES, int MB>
 __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__restrict__ x,
                                                               const int64_t *__restrict__ rows, int64_t n,
+                                                              const int64_t *__restrict__ n_dev,
                                                               const float *__restrict__ w,
                                                               const float *__restrict__ bias,
                                                               float *__restrict__ y) {
@@ -88,6 +89,10 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__res
 
   const int wave = threadIdx.x / 64, lane = threadIdx.x % 64;
   const int q = lane >> 4, mr = lane & 15;
+  if (n_dev) {  // a device-side sample count (<= n): rows past it are neither read nor written
+    const int64_t m = *n_dev;
+    n = m < n ? (m > 0 ? m : 0) : n;
+  }
   const int64_t P = n * Gm::PIX, tiles = (P + TP - 1) / TP, tstride = (int64_t)gridDim.x * WAVES;
 
   // this lane's window origin in tile t, per M-block (tail lanes read a duplicate pixel)
@@ -583,8 +588,8 @@ int rth_conv_relu_wgrad(const rth_conv_shape *shape, const void *x, const int64_
   return RTH_OK;
 }
 
-int rth_conv_bias_relu(const rth_conv_shape *shape, const void *x, const int64_t *rows, int64_t n, const float *w,
-                       const float *bias, float *y, void *stream) {
+static int conv_bias_relu(const rth_conv_shape *shape, const void *x, const int64_t *rows, int64_t n,
+                          const int64_t *n_dev, const float *w, const float *bias, float *y, void *stream) {
   RTH_REQUIRE(shape && x && w && bias && y && n >= 0, "rth_conv_bias_relu: NULL argument");
   ConvLaunch l;
   RTH_REQUIRE(find_conv(*shape, &l),
@@ -603,9 +608,20 @@ int rth_conv_bias_relu(const rth_conv_shape *shape, const void *x, const int64_t
   const int cap = wg_per_cu();
   const int64_t resident = (int64_t)cu_count() * (l.per_cu < cap ? l.per_cu : cap);
   if (grid > resident) grid = resident;
-  void *args[] = {(void *)&x, (void *)&rows, (void *)&n, (void *)&w, (void *)&bias, (void *)&y};
+  void *args[] = {(void *)&x, (void *)&rows, (void *)&n, (void *)&n_dev, (void *)&w, (void *)&bias, (void *)&y};
   RTH_HIP(hipLaunchKernel(l.fn, dim3((unsigned)grid), dim3(l.waves * 64), args, 0, as_stream(stream)));
   return RTH_OK;
+}
+
+int rth_conv_bias_relu(const rth_conv_shape *shape, const void *x, const int64_t *rows, int64_t n, const float *w,
+                       const float *bias, float *y, void *stream) {
+  return conv_bias_relu(shape, x, rows, n, nullptr, w, bias, y, stream);
+}
+
+int rth_conv_bias_relu_upto(const rth_conv_shape *shape, const void *x, const int64_t *rows, int64_t n_max,
+                            const int64_t *n_dev, const float *w, const float *bias, float *y, void *stream) {
+  RTH_REQUIRE(n_dev, "rth_conv_bias_relu_upto: NULL count");
+  return conv_bias_relu(shape, x, rows, n_max, n_dev, w, bias, y, stream);
 }
 
 }  // extern "C"

@@ -27,7 +27,33 @@ struct OptSeg {
   float *v;
   int64_t n;
   int64_t blk0;  // first workgroup of this tensor
+  int vec;       // all four pointers 16-byte aligned: float4 accesses
 };
+
+constexpr int kOptV = kOptChunk / kOptThreads / 4;  // float4 groups per lane
+
+// lane's k-th float4 group of the chunk at element base: elements base + 4 (k T + tid) + 0..3,
+// zero past n
+__device__ __forceinline__ float4 ld4(const float *__restrict__ p, int64_t e, int64_t n, int vec) {
+  if (vec && e + 3 < n) return *reinterpret_cast<const float4 *>(p + e);
+  float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (e < n) r.x = p[e];
+  if (e + 1 < n) r.y = p[e + 1];
+  if (e + 2 < n) r.z = p[e + 2];
+  if (e + 3 < n) r.w = p[e + 3];
+  return r;
+}
+
+__device__ __forceinline__ void st4(float *__restrict__ p, int64_t e, int64_t n, int vec, float4 v) {
+  if (vec && e + 3 < n) {
+    *reinterpret_cast<float4 *>(p + e) = v;
+    return;
+  }
+  if (e < n) p[e] = v.x;
+  if (e + 1 < n) p[e + 1] = v.y;
+  if (e + 2 < n) p[e + 2] = v.z;
+  if (e + 3 < n) p[e + 3] = v.w;
+}
 
 struct OptArgs {
   OptSeg seg[RTH_MAX_PARAM_TENSORS];
@@ -100,16 +126,18 @@ __global__ __launch_bounds__(kOptThreads) void k_grad_sqsum(OptArgs a, double *_
   const int64_t b = blockIdx.x;
   const OptSeg &sg = a.seg[seg_of(a, b)];
   const int64_t base = (b - sg.blk0) * kOptChunk;
+  float4 gv[kOptV];  // every load of the chunk in flight before the first use
+#pragma unroll
+  for (int k = 0; k < kOptV; ++k) gv[k] = ld4(sg.grad, base + 4 * (k * kOptThreads + threadIdx.x), sg.n, sg.vec);
   double acc = 0.0;
-#pragma unroll 4
-  for (int k = 0; k < kOptChunk / kOptThreads; ++k) {
-    const int64_t i = base + k * kOptThreads + threadIdx.x;
-    if (i < sg.n) {
-      const double g = (double)sg.grad[i];
-      acc = radd(acc, rmul(g, g));
-    }
-  }
-  red[threadIdx.x] = acc;
+#pragma unroll
+  for (int k = 0; k < kOptV; ++k) {
+    const double x = gv[k].x, y = gv[k].y, z = gv[k].z, w = gv[k].w;
+    acc = radd(acc, rmul(x, x));
+    acc = radd(acc, rmul(y, y));
+    acc = radd(acc, rmul(z, z));
+    acc = radd(acc, rmul(w, w));
+  }  red[threadIdx.x] = acc;
   __syncthreads();
   for (int s = kOptThreads / 2; s > 0; s >>= 1) {
     if (threadIdx.x < s) red[threadIdx.x] = radd(red[threadIdx.x], red[threadIdx.x + s]);
@@ -140,19 +168,33 @@ __global__ __launch_bounds__(kOptThreads) void k_adam(OptArgs a, const OptScalar
   const OptSeg &sg = a.seg[seg_of(a, b)];
   const int64_t base = (b - sg.blk0) * kOptChunk;
   const float coef = sc->coef, step_size = sc->step_size, bc2_sqrt = sc->bc2_sqrt;
-#pragma unroll 4
-  for (int k = 0; k < kOptChunk / kOptThreads; ++k) {
-    const int64_t i = base + k * kOptThreads + threadIdx.x;
-    if (i >= sg.n) break;
-    float g = sg.grad[i];
+  auto adam1 = [&](float g, float &m, float &v, float &p) {
     if (clip) g = rmul(g, coef);  // grad.mul_(clip_coef_clamped)
-    float m = sg.m[i], v = sg.v[i];
-    m = radd(m, rmul(w1, rsub(g, m)));        // lerp_(g, 1 - beta1), weight < 0.5 branch
+    m = radd(m, rmul(w1, rsub(g, m)));               // lerp_(g, 1 - beta1), weight < 0.5 branch
     v = radd(rmul(v, beta2), rmul(rmul(w2, g), g));  // mul_(beta2).addcmul_(g, g, 1 - beta2)
     const float denom = radd(sqrtf(v) / bc2_sqrt, eps);
-    sg.param[i] = radd(sg.param[i], rmul(-step_size, m) / denom);  // addcdiv_(m, denom, -step_size)
-    sg.m[i] = m;
-    sg.v[i] = v;
+    p = radd(p, rmul(-step_size, m) / denom);  // addcdiv_(m, denom, -step_size)
+  };
+  float4 gv[kOptV], mv[kOptV], vv[kOptV], pv[kOptV];
+#pragma unroll
+  for (int k = 0; k < kOptV; ++k) {
+    const int64_t e = base + 4 * (k * kOptThreads + threadIdx.x);
+    gv[k] = ld4(sg.grad, e, sg.n, sg.vec);
+    mv[k] = ld4(sg.m, e, sg.n, sg.vec);
+    vv[k] = ld4(sg.v, e, sg.n, sg.vec);
+    pv[k] = ld4(sg.param, e, sg.n, sg.vec);
+  }
+#pragma unroll
+  for (int k = 0; k < kOptV; ++k) {
+    const int64_t e = base + 4 * (k * kOptThreads + threadIdx.x);
+    if (e >= sg.n) break;
+    adam1(gv[k].x, mv[k].x, vv[k].x, pv[k].x);
+    adam1(gv[k].y, mv[k].y, vv[k].y, pv[k].y);
+    adam1(gv[k].z, mv[k].z, vv[k].z, pv[k].z);
+    adam1(gv[k].w, mv[k].w, vv[k].w, pv[k].w);
+    st4(sg.param, e, sg.n, sg.vec, pv[k]);
+    st4(sg.m, e, sg.n, sg.vec, mv[k]);
+    st4(sg.v, e, sg.n, sg.vec, vv[k]);
   }
 }
 
@@ -176,7 +218,9 @@ int rth_clip_adam(const rth_param_tensor *tensors, int32_t n_tensors, double lr,
   for (int s = 0; s < n_tensors; ++s) {
     const rth_param_tensor &t = tensors[s];
     RTH_REQUIRE(t.param && t.grad && t.exp_avg && t.exp_avg_sq && t.n >= 1, "rth_clip_adam: tensor %d incomplete", s);
-    a.seg[s] = OptSeg{t.param, t.grad, t.exp_avg, t.exp_avg_sq, t.n, blocks};
+    const uintptr_t al = reinterpret_cast<uintptr_t>(t.param) | reinterpret_cast<uintptr_t>(t.grad) |
+                         reinterpret_cast<uintptr_t>(t.exp_avg) | reinterpret_cast<uintptr_t>(t.exp_avg_sq);
+    a.seg[s] = OptSeg{t.param, t.grad, t.exp_avg, t.exp_avg_sq, t.n, blocks, (al & 15) == 0 ? 1 : 0};
     blocks += (t.n + kOptChunk - 1) / kOptChunk;
   }
   a.nseg = n_tensors;

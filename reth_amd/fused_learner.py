@@ -43,6 +43,7 @@ def _pair(s0, s1):
     u8 = s0.dtype == torch.uint8
     fmt = torch.contiguous_format if u8 else torch.channels_last
     if s0.is_contiguous(memory_format=fmt) and s1.is_contiguous(memory_format=fmt) and s1.stride() == s0.stride() \
+            and s1.untyped_storage().data_ptr() == s0.untyped_storage().data_ptr() \
             and s1.data_ptr() == s0.data_ptr() + s0.numel() * s0.element_size():
         return torch.as_strided(s0, (2 * s0.shape[0], *s0.shape[1:]), s0.stride())
     return torch.cat([s0, s1]).contiguous(memory_format=fmt)

@@ -93,12 +93,14 @@ class DQNNetwork(nn.Module):
         if self.hwc_features and merged[0].is_cuda:
             self._frozen_packed = self.pack_convs(out=getattr(self, "_frozen_packed", None))
 
-    def forward_heads(self, x, merged=None, rows=None, packed=None):
+    def forward_heads(self, x, merged=None, rows=None, packed=None, n_dev=None):
         """raw dueling heads [n, A+1].  x: float32 observations (channels-last with
         hwc_features), or -- on the HIP torso -- uint8 frame stacks [m, C, H, W], read as
         stacks `rows` (an int64 device index, n = rows.numel()) or all m of them.  merged /
         packed: the head weights / packed conv weights of this weight version (pack_convs),
-        default the frozen ones, else built now"""
+        default the frozen ones, else built now.  n_dev (int64 device scalar, inference only):
+        only the first *n_dev of the n samples are computed by the torso (rows past it hold
+        whatever the FC layers make of unwritten activations)"""
         if not self.dueling:
             raise ValueError("forward_heads needs the dueling network")
         frozen = getattr(self, "_frozen", None) is not None
@@ -108,11 +110,11 @@ class DQNNetwork(nn.Module):
         if self.hwc_features:
             if packed is None and frozen:
                 packed = getattr(self, "_frozen_packed", None)
-            h = self._features_nhwc(x, rows, packed)
+            h = self._features_nhwc(x, rows, packed, n_dev)
             h = h.permute(0, 2, 3, 1).reshape(h.shape[0], -1)  # a view of the NHWC activations
         else:
-            if x.dtype == torch.uint8 or rows is not None:
-                raise ValueError("uint8 / row-indexed observations need the HIP torso (hwc_features)")
+            if x.dtype == torch.uint8 or rows is not None or n_dev is not None:
+                raise ValueError("uint8 / row-indexed / counted observations need the HIP torso (hwc_features)")
             h = self.features(x).flatten(1)
         h = _LinearReLU.apply(h, w1, b1)
         return torch.addmm(b2, h, w2.t())
@@ -173,7 +175,7 @@ class DQNNetwork(nn.Module):
             return packed[3]
         return packed[li]
 
-    def _features_nhwc(self, x, rows=None, packed=None):
+    def _features_nhwc(self, x, rows=None, packed=None, n_dev=None):
         """the conv torso on channels-last activations: each Conv2d -> ReLU is one HIP
         implicit-GEMM launch with the bias and ReLU fused (rth_conv_bias_relu) where the
         geometry is built, else MIOpen + the rth_bias_relu pass; backward: rth_relu_bias_grad
@@ -190,6 +192,24 @@ class DQNNetwork(nn.Module):
         shapes = self._torso_shapes(x.shape[1:], u8)
         if packed is None and any(s is not None for _, s in shapes):
             packed = self.pack_convs(u8)
+        if n_dev is not None:  # device-counted inference batch: every layer in rth_conv_bias_relu_upto
+            from ._lib import call, ptr, stream_ptr
+
+            if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+                raise RuntimeError("forward_heads(n_dev=...) is inference only (no autograd)")
+            if any(sh is None for _, sh in shapes):
+                raise ValueError("forward_heads(n_dev=...) needs every conv in rth_conv_bias_relu")
+            n = rows.numel() if rows is not None else x.shape[0]
+            for li, conv in enumerate(convs):
+                shape = shapes[li][1]
+                ho = (shape.hin - shape.kh) // shape.stride + 1
+                wo = (shape.win - shape.kw) // shape.stride + 1
+                y = torch.empty((n, shape.cout, ho, wo), dtype=torch.float32, device=x.device,
+                                memory_format=torch.channels_last)
+                call("rth_conv_bias_relu_upto", _lib.ctypes.byref(shape), ptr(x), ptr(rows) if li == 0 else None, n,
+                     ptr(n_dev), ptr(self._packed_for(packed, li, u8)), ptr(conv.bias), ptr(y), stream_ptr())
+                x = y
+            return x
         for li, (conv, ws) in enumerate(zip(convs, self._ws)):
             shape = shapes[li][1]
             if shape is not None:

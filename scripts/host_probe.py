@@ -85,6 +85,7 @@ def main():
 
     def alone(label, fn, reps=20):
         torch.cuda.synchronize()
+        time.sleep(0.05)  # a gap that separates the sections in a kernel trace
         ts = []
         for _ in range(reps):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -99,7 +100,8 @@ def main():
     k = ax.loader._pending[0]
     alone("learner graph (pre, slot k)", lambda: G["learn"][("pre", k)].replay())
     alone("learner graph (full, slot k)", lambda: G["learn"][("full", k)].replay())
-    alone("actor graph", lambda: G["act"][ax.actors.pushes % 2].replay())
+    alone("actor graph (dedup)", lambda: G["act"]["dedup", ax.actors.pushes % 2].replay())
+    alone("actor graph (full)", lambda: G["act"]["full", ax.actors.pushes % 2].replay())
     alone("target pass graph", lambda: G["tgt"][k].replay())
     alone("sample + gather", lambda: ax.replay.sample_into(512, *ax.loader._slots[1 - k]))
 

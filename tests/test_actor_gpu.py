@@ -198,3 +198,55 @@ def test_step_fused_matches_step_then_prioritise(dev):
             assert torch.equal(rows.s0, s0) and torch.equal(rows.a, ra) and torch.equal(rows.r, rr)
             assert torch.equal(rows.done, rd)
             torch.testing.assert_close(td, wtd, rtol=1e-5, atol=1e-5)  # batch 3N vs 2N GEMM blocking
+
+
+def test_step_fused_dedup_matches_full(dev):
+    """dedup mode (forward over the acting + terminal stacks only, rows' heads from the
+    per-stack cache) gives the actions and |td| of the full 3-way forward, through many
+    episode ends (p_done = 0.25) and a weights change (the cache is rebuilt: full mode for
+    n + 2 steps)"""
+    from reth_amd.actors import VecActors
+    from reth_amd.model import DQNNetwork
+
+    torch.manual_seed(1)
+    N = 40
+    net = DQNNetwork((4, 84, 84), 6).to(dev, memory_format=torch.channels_last)
+    net.hwc_features = True
+    net.requires_grad_(False)
+    kw = dict(n_step=3, gamma=0.99, device=dev, seed=21, p_reward=0.3, p_done=0.25, channels_last=True)
+    a, b = VecActors(N, 6, **kw), VecActors(N, 6, **kw)
+    modes = []
+    for t in range(24):
+        if t == 12:  # actor weights reload
+            with torch.no_grad():
+                for p in net.parameters():
+                    p.add_(torch.randn_like(p) * 1e-3)
+            a.weights_changed()
+            b.weights_changed()
+        dedup = b.dedup_ready(net)
+        modes.append(dedup)
+        ta, ra = a.step_fused(net, dedup=False)
+        tb, rb = b.step_fused(net)
+        assert torch.equal(a.action, b.action), t
+        assert torch.equal(a.n_ext, b.n_ext)
+        if ta is not None:
+            assert torch.equal(ra.s0, rb.s0) and torch.equal(ra.s1, rb.s1) and torch.equal(ra.done, rb.done)
+            torch.testing.assert_close(tb, ta, rtol=1e-5, atol=1e-5)
+    assert modes[:5] == [False] * 5 and all(modes[5:12]) and modes[12:17] == [False] * 5 and all(modes[17:])
+    assert int(b.n_ext) > N or bool(b.done.any())  # the episodes did end
+
+
+def test_compact_flagged(dev):
+    from reth_amd._lib import call, ptr, stream_ptr
+
+    g = torch.Generator(device=dev).manual_seed(4)
+    for n, cap in [(1, 1), (37, 37), (2048, 2048), (3000, 100)]:
+        flag = (torch.rand(n, device=dev, generator=g) < 0.3).float()
+        vals = torch.randint(0, 1 << 40, (n,), device=dev, generator=g)
+        out = torch.empty(cap, dtype=torch.int64, device=dev)
+        cnt = torch.empty(1, dtype=torch.int64, device=dev)
+        call("rth_compact_flagged", ptr(flag), ptr(vals), n, ptr(out), cap, -7, 100, ptr(cnt), stream_ptr())
+        want = vals[flag != 0][:cap]
+        k = want.numel()
+        assert int(cnt) == 100 + k
+        assert torch.equal(out[:k], want) and bool((out[k:] == -7).all())

@@ -34,6 +34,12 @@ sys.path.insert(0, ROOT)
 STACK = 4 * 84 * 84
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 FP32_PEAK_TFLOPS = 157.3
+# BASELINE.json configs[1] (the metric's workload) and configs[2] (a scale case, not the bench line)
+WORKLOADS = {
+    "pong": dict(name="PongNoFrameskip-v4 Ape-X DQN (BASELINE configs[1])", actors=256, capacity=1_000_000, actions=6),
+    "breakout": dict(name="BreakoutNoFrameskip-v4 Ape-X (BASELINE configs[2]; full-row uint8 replay, no frame "
+                          "de-duplication)", actors=2048, capacity=4_000_000, actions=4),
+}
 
 
 def gather_bytes_per_row(frames_u8=False):
@@ -169,8 +175,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--actors", type=int, default=256)
-    ap.add_argument("--capacity", type=int, default=1_000_000)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="pong",
+                    help="pong = BASELINE configs[1] (the metric's workload); breakout = configs[2] (2048 actors, "
+                         "4 M replay, A = 4: 225.9 GB of full-row uint8 storage)")
+    ap.add_argument("--actors", type=int, default=None)
+    ap.add_argument("--capacity", type=int, default=None)
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--actor-steps-per-update", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -182,6 +191,9 @@ def main():
     ap.add_argument("--miopen-conv", action="store_true", help="conv torso forward in MIOpen (+ rth_bias_relu) "
                     "instead of rth_conv_bias_relu")
     args = ap.parse_args()
+    wl = WORKLOADS[args.workload]
+    args.actors = wl["actors"] if args.actors is None else args.actors
+    args.capacity = wl["capacity"] if args.capacity is None else args.capacity
 
     from reth_amd.apex import ApexConfig, ApexDQN
     from reth_amd.dist import init_from_env
@@ -197,7 +209,7 @@ def main():
     if world != args.gpus and world_env > 1:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     dev = torch.device("cuda", local)
-    cfg = ApexConfig(n_actors=args.actors, capacity=args.capacity, batch_size=args.batch,
+    cfg = ApexConfig(n_actors=args.actors, capacity=args.capacity, batch_size=args.batch, num_actions=wl["actions"],
                      actor_steps_per_update=args.actor_steps_per_update, seed=0,
                      channels_last=not args.nchw, conv_benchmark=not args.no_conv_benchmark,
                      hip_graph=not args.eager, hip_conv=not args.miopen_conv,
@@ -263,8 +275,13 @@ def main():
     cpu = None
     if not args.no_cpu_baseline and world == 1:
         cpu = cpu_baseline(n_actors=cfg.n_actors, batch=cfg.batch_size, iters=args.cpu_iters)
-    flops_update = 5 * cfg.batch_size * qnet_flops_per_sample()  # 3 fwd + bwd(~2 fwd)
-    flops_actor = 3 * cfg.n_actors * qnet_flops_per_sample()     # act (N) + priorities (2N)
+    f = qnet_flops_per_sample(cfg.num_actions)
+    flops_update = 5 * cfg.batch_size * f  # online fwd on s0 + s1, target fwd on s1, bwd (~2 fwd)
+    # actors: the acting stacks (N) -- the rows' heads come from the per-stack cache
+    # (VecActors.step_fused dedup mode; the terminal stacks of ended episodes, ~N/2000 per
+    # step, and the full passes after a weights reload are not counted)
+    flops_actor = cfg.n_actors * f * args.actor_steps_per_update
+    flops_step = flops_update + flops_actor
     step_s = dt / args.steps
     traffic = load_traffic(args.tag)
     out = {
@@ -281,7 +298,7 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (Philox uint8 Pong-shaped frames, random-init Q-net; no ALE/checkpoints on the box)",
-        "config": {"workload": "PongNoFrameskip-v4 Ape-X DQN (BASELINE configs[1])", "actors_per_gpu": cfg.n_actors,
+        "config": {"workload": wl["name"], "actors_per_gpu": cfg.n_actors, "num_actions": cfg.num_actions,
                    "replay_capacity_per_gpu": cfg.capacity, "replay_prefilled": True, "batch_size": cfg.batch_size,
                    "n_step": cfg.n_step, "alpha": cfg.alpha, "beta": cfg.beta,
                    "actor_steps_per_update": cfg.actor_steps_per_update,
@@ -297,8 +314,8 @@ def main():
                      "isolated_launch_us": round(iso_s * 1e6, 2),
                      "isolated_frac": round(bytes_launch / iso_s / 1e9 / HBM_PEAK_GBS, 4),
                      "note": "in the timed region the gather overlaps the learner block on a second stream"},
-        "qnet_mfma": {"tflops_per_step": round((flops_update + flops_actor) * args.actor_steps_per_update / 1e12, 4),
-                      "achieved_tflops": round((flops_update + flops_actor) / step_s / 1e12, 2),
+        "qnet_mfma": {"tflops_per_step": round(flops_step / 1e12, 4),
+                      "achieved_tflops": round(flops_step / step_s / 1e12, 2),
                       "peak_fp32_tflops": FP32_PEAK_TFLOPS},
         "cpu_baseline": cpu,
     }

@@ -117,6 +117,8 @@ class ApexDQN:
         self.env_steps = 0
         self.updates = 0
         self._graphs = None
+        self._ev_acquired = None
+        self.actor_modes = {}  # graph mode: actor steps replayed per mode ("dedup" / "full")
 
     def close(self):
         _SERVICES.pop(self.addr, None)
@@ -159,6 +161,10 @@ class ApexDQN:
         """host-side actor bookkeeping between steps (weights reload: perwez RecvSocket)"""
         if self.subscriber.maybe_load(self.actor_net, self.actors.t):
             self.actors.weights_changed()
+            # the learner's next publish (another stream in overlapped graph mode) must not
+            # overwrite the slot before this copy out of it has run
+            self._ev_acquired = torch.cuda.Event()
+            self._ev_acquired.record()
 
     def _learner_host(self):
         """host-side learner bookkeeping after an update (Trainer / Interval / weights send)"""
@@ -167,6 +173,8 @@ class ApexDQN:
         if self.solver._update_target_interval is not None and not self.solver.auto_target_update:
             self.solver._update_target_interval()
         if self.updates % self.cfg.send_weights_interval == 0:
+            if self._ev_acquired is not None:
+                torch.cuda.current_stream(self.device).wait_event(self._ev_acquired)
             self.slot.publish(self.solver.q_network)
 
     # ------------------------------------------------------------------ iteration
@@ -290,6 +298,7 @@ class ApexDQN:
             k = act.pushes % 2
             mode = "dedup" if ("dedup", k) in G["act"] and act.dedup_ready(self.actor_net) else "full"
             G["act"][mode, k].replay()
+            self.actor_modes[mode] = self.actor_modes.get(mode, 0) + 1
             act.t += 1
             act.pushes += 1
             act.fresh += 1

@@ -71,6 +71,7 @@ struct CopyArgs {
 };
 
 constexpr int kCopyThreads = 256;
+constexpr int kCopyVec = 1;  // COPY: 16-byte vectors per lane (4 KiB chunks: more, smaller workgroups measured faster than 16 KiB)
 constexpr int64_t kSmallRow = 64;  // rows up to this many bytes: one lane per row
 
 __device__ __forceinline__ float4 u8x4_to_f4(uint32_t w) {
@@ -119,7 +120,8 @@ __device__ __forceinline__ void hwc4_chunk(const uint8_t *__restrict__ src, floa
 // row into `chunks` independent chunks of `chunk_in` input bytes (one per workgroup: no LDS,
 // no barrier, thousands of workgroups in flight so loads and stores of different chunks
 // overlap), a small column (a, r, done: <= 64 B) gives each lane a whole row.
-//   COPY        16-byte loads and stores; chunk = 4 KiB.
+//   COPY        16-byte loads and stores (kCopyVec per lane), the row tail vectorised too;
+//               chunk = 4 KiB.
 //   U8_F32      4-byte loads of 4 pixels become 16-byte stores (1 KiB contiguous per wave
 //               instruction), four per lane in flight; chunk = 4 KiB in.
 //   U8_F32_HWC  C planes of P pixels (CHW u8) -> P pixels x C floats (HWC f32, channels_last
@@ -198,10 +200,25 @@ __global__ __launch_bounds__(kCopyThreads) void k_copy_rows(CopyArgs a) {
     }
     return;
   }
+  if (vec && col.conv == CONV_COPY) {  // lane-contiguous 16-byte loads and stores, kCopyVec in flight
+    uint4 v[kCopyVec];
+#pragma unroll
+    for (int j = 0; j < kCopyVec; ++j) {
+      const int64_t off = o + 16 * (j * kCopyThreads + tid);
+      if (off + 16 <= nb) v[j] = *reinterpret_cast<const uint4 *>(src + off);
+    }
+#pragma unroll
+    for (int j = 0; j < kCopyVec; ++j) {
+      const int64_t off = o + 16 * (j * kCopyThreads + tid);
+      if (off + 16 <= nb) *reinterpret_cast<uint4 *>(dst + off) = v[j];
+    }
+    const int64_t t0 = nb & ~int64_t(15);  // bytes past the row's last whole vector
+    if (t0 < nb && t0 >= o && t0 < o + col.chunk_in)
+      for (int64_t k = t0 + tid; k < nb; k += kCopyThreads) dst[k] = src[k];
+    return;
+  }
   if (vec && o + col.chunk_in <= nb) {
-    if (col.conv == CONV_COPY) {  // lane-contiguous 16-byte loads and stores
-      *reinterpret_cast<uint4 *>(dst + o + 16 * tid) = *reinterpret_cast<const uint4 *>(src + o + 16 * tid);
-    } else {  // 4-byte loads -> 16-byte stores, 1 KiB contiguous per wave store, 4 in flight
+    {  // 4-byte loads -> 16-byte stores, 1 KiB contiguous per wave store, 4 in flight
       const uint32_t *s32 = reinterpret_cast<const uint32_t *>(src + o);
       float4 *d4 = reinterpret_cast<float4 *>(df + o);
       uint32_t w[4];
@@ -356,7 +373,7 @@ int launch_copy(CopyArgs &a, hipStream_t s) {
       col.chunks = (P + col.chunk_px - 1) / col.chunk_px;
       col.vec = (al % 16 == 0) && P % 4 == 0;
     } else {
-      col.chunk_in = 16 * kCopyThreads;
+      col.chunk_in = 16 * kCopyThreads * (col.conv == CONV_COPY ? kCopyVec : 1);
       col.chunks = (nb + col.chunk_in - 1) / col.chunk_in;
       col.vec = al % 16 == 0;
     }

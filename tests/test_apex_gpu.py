@@ -129,6 +129,8 @@ def test_graph_replay_learns(dev):
     assert ax.subscriber.loaded_version > 0
     assert all(torch.isfinite(p).all() for p in ax.solver.q_network.parameters())
     assert int(ax.actors.t_dev.item()) == ax.actors.t == 50
+    # actors: cached-heads (dedup) steps, and full steps after each weights reload
+    assert ax.actor_modes.get("dedup", 0) > 0 and ax.actor_modes.get("full", 0) > 0
     ax.close()
 
 

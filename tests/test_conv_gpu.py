@@ -229,3 +229,29 @@ def test_hip_torso_gradients_u8_input(dev):
     for a, b in zip(*grads):
         scale = b.abs().max().clamp_min(1e-12)
         assert ((a - b).abs().max() / scale) < 1e-4
+
+
+@pytest.mark.parametrize("count", [0, 5, 37, 64])
+def test_conv_upto_device_count(dev, count):
+    """rth_conv_bias_relu_upto computes the first *n_dev samples exactly as the plain launch
+    and leaves the rest of the output untouched"""
+    from reth_amd import _lib
+
+    n = 64
+    g = torch.Generator().manual_seed(31 + count)
+    stacks = torch.randint(0, 256, (n, 4, 84, 84), dtype=torch.uint8, generator=g).to(dev)
+    rows = torch.randperm(n, generator=g).to(dev)
+    w = ((torch.rand((32, 4, 8, 8), generator=g) * 2 - 1) / 16).to(dev).contiguous(memory_format=torch.channels_last)
+    b = ((torch.rand(32, generator=g) * 2 - 1) * 0.1).to(dev)
+    shape = _shape(_lib.CONV_U8_CHW, *GEOMS[0])
+    pk = torch.empty(_lib.lib().rth_conv_packed_bytes(_lib.ctypes.byref(shape)) // 4, device=dev)
+    _lib.call("rth_conv_pack", _lib.ctypes.byref(shape), w.data_ptr(), pk.data_ptr(), _lib.stream_ptr())
+    full = torch.empty((n, 20, 20, 32), device=dev)
+    _lib.call("rth_conv_bias_relu", _lib.ctypes.byref(shape), stacks.data_ptr(), rows.data_ptr(), n, pk.data_ptr(),
+              b.data_ptr(), full.data_ptr(), _lib.stream_ptr())
+    part = torch.full((n, 20, 20, 32), float("nan"), device=dev)
+    cnt = torch.tensor([count], dtype=torch.int64, device=dev)
+    _lib.call("rth_conv_bias_relu_upto", _lib.ctypes.byref(shape), stacks.data_ptr(), rows.data_ptr(), n,
+              cnt.data_ptr(), pk.data_ptr(), b.data_ptr(), part.data_ptr(), _lib.stream_ptr())
+    assert torch.equal(part[:count], full[:count])
+    assert bool(torch.isnan(part[count:]).all())

@@ -119,7 +119,8 @@ __device__ __forceinline__ void hwc4_chunk(const uint8_t *__restrict__ src, floa
 // Flat 1-D grid.  Column c owns workgroups [blk0, blk0 + nblk); a large column splits each
 // row into `chunks` independent chunks of `chunk_in` input bytes (one per workgroup: no LDS,
 // no barrier, thousands of workgroups in flight so loads and stores of different chunks
-// overlap), a small column (a, r, done: <= 64 B) gives each lane a whole row.
+// overlap), a small column (a, r, done: <= 64 B) gives each lane one 4-byte word of a row
+// (plain copies) or a whole row (conversions).
 //   COPY        16-byte loads and stores (kCopyVec per lane), the row tail vectorised too;
 //               chunk = 4 KiB.
 //   U8_F32      4-byte loads of 4 pixels become 16-byte stores (1 KiB contiguous per wave
@@ -135,7 +136,13 @@ __global__ __launch_bounds__(kCopyThreads) void k_copy_rows(CopyArgs a) {
   const CopyCol &col = a.col[c];
   const int tid = threadIdx.x;
   int64_t i, chunk = 0;
-  if (col.chunks == 0) {  // small rows
+  int32_t word = -1;
+  if (col.chunks == 0 && col.vec) {  // small COPY rows of whole words: one lane per 4-byte word
+    const int64_t e = (b - col.blk0) * kCopyThreads + tid, words = col.in_bytes / 4;
+    if (e >= a.n * words) return;
+    i = e / words;
+    word = (int32_t)(e - i * words);
+  } else if (col.chunks == 0) {  // small rows
     i = (b - col.blk0) * kCopyThreads + tid;
     if (i >= a.n) return;
   } else {
@@ -156,7 +163,9 @@ __global__ __launch_bounds__(kCopyThreads) void k_copy_rows(CopyArgs a) {
   const int64_t nb = col.in_bytes;
   float *df = reinterpret_cast<float *>(dst);
   if (col.chunks == 0) {
-    if (col.conv == CONV_COPY) {
+    if (word >= 0) {
+      reinterpret_cast<uint32_t *>(dst)[word] = reinterpret_cast<const uint32_t *>(src)[word];
+    } else if (col.conv == CONV_COPY) {
       for (int64_t k = 0; k < nb; ++k) dst[k] = src[k];
     } else if (col.conv == CONV_F32_U8) {
       for (int64_t k = 0; k < nb / 4; ++k) dst[k] = (uint8_t)f32_u8(ld_f32_bytes(src + 4 * k));
@@ -363,7 +372,9 @@ int launch_copy(CopyArgs &a, hipStream_t s) {
                          (uintptr_t)col.src_stride | (uintptr_t)col.dst_stride;
     if (nb <= kSmallRow) {
       col.chunks = 0;
-      blocks += (a.n + kCopyThreads - 1) / kCopyThreads;
+      // plain copies of whole 4-byte words (a, r, done, Q heads): a lane per word
+      col.vec = col.conv == CONV_COPY && nb % 4 == 0 && al % 4 == 0;
+      blocks += ((col.vec ? a.n * (nb / 4) : a.n) + kCopyThreads - 1) / kCopyThreads;
       continue;
     }
     if (col.conv == CONV_U8_F32_HWC) {

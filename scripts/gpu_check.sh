@@ -54,6 +54,7 @@ for step in "$@"; do
             --kernel-trace --output-format csv -d "$PWD/gpurun_out/pmc_conv_b" -o run -- python scripts/conv_pmc.py ;;
     probe) run probe 300 python scripts/probe_qnet.py ;;
     host) run host_probe 300 python scripts/host_probe.py ;;
+    breakout) run bench_breakout 900 python bench.py --workload breakout --steps 50 --warmup 10 --no-cpu-baseline ;;
     hostprof) export TMPDIR=/tmp; run host_prof 300 rocprofv3 --kernel-trace --output-format csv -d "$PWD/gpurun_out/hp" -o run -- python scripts/host_probe.py ;;
     variants2)
       run bench_eager 600 python bench.py --steps 100 --warmup 20 --no-cpu-baseline --eager

@@ -250,35 +250,38 @@ __global__ __launch_bounds__(256) void k_heads_split_grad(HeadsDims d, const flo
 // launch, from the TD kernel's d(loss)/d(heads):
 //   gh  = (h > 0) ? dq @ w2 : 0      (addmm backward -> threshold_backward, [B, H2])
 //   gw2 = dq^T @ h  [A1, H2],  gb2 = column sums of dq [A1],  gb1 = column sums of gh [H2]
-// Workgroup k < H2 / 16 owns columns 16k .. 16k+15 over all B rows (lane = column
-// tid % 16, row group tid / 16); the 16 row-group partials are summed in LDS in a fixed
-// order (deterministic).  The last workgroup sums gb2 and, optionally, adds mean(|td|) to a
-// device accumulator (Trainer's mean_error, reth/reth/presets/trainer.py:64-69).
-constexpr int kHbCols = 16, kHbRows = 16, kHbMaxA1 = kMaxActions + 1;
+// Workgroup k < H2 / 16 owns columns 16k .. 16k+15 over all B rows: lane = column tid % 16,
+// row group tid / 16 (64 groups), RB rows of h and dq loaded per batch before any use (the
+// loop is load-latency bound otherwise); the 64 row-group partials are summed in LDS in a
+// fixed order (deterministic).  The last workgroup sums gb2 and, optionally, adds
+// mean(|td|) to a device accumulator (Trainer's mean_error, reth/reth/presets/trainer.py:64-69).
+constexpr int kHbCols = 16, kHbGroups = 64, kHbThreads = kHbCols * kHbGroups, kHbMaxA1 = kMaxActions + 1;
 
-__global__ __launch_bounds__(256) void k_heads_backward(const float *__restrict__ dq, const float *__restrict__ h,
-                                                        int64_t ldh, const float *__restrict__ w2, int64_t B,
-                                                        int H2, int A1, float *__restrict__ gh,
-                                                        float *__restrict__ gw2, float *__restrict__ gb2,
-                                                        float *__restrict__ gb1, const float *__restrict__ td_abs,
-                                                        float *__restrict__ td_acc) {
-  __shared__ float red[kHbRows][kHbCols + 1];
+template <int MAXA, int RB>
+__global__ __launch_bounds__(kHbThreads) void k_heads_backward(const float *__restrict__ dq,
+                                                               const float *__restrict__ h, int64_t ldh,
+                                                               const float *__restrict__ w2, int64_t B, int H2,
+                                                               int A1, float *__restrict__ gh,
+                                                               float *__restrict__ gw2, float *__restrict__ gb2,
+                                                               float *__restrict__ gb1,
+                                                               const float *__restrict__ td_abs,
+                                                               float *__restrict__ td_acc) {
+  __shared__ float red[kHbThreads];
   const int tid = threadIdx.x;
   if ((int)blockIdx.x == H2 / kHbCols) {  // gb2 and the |td| mean
-    __shared__ float tr[256];
     for (int a = 0; a <= A1; ++a) {
       if (a == A1 && !(td_abs && td_acc)) break;
       float s = 0.0f;
-      for (int64_t r = tid; r < B; r += 256) s = radd(s, a < A1 ? dq[r * A1 + a] : td_abs[r]);
-      tr[tid] = s;
+      for (int64_t r = tid; r < B; r += kHbThreads) s = radd(s, a < A1 ? dq[r * A1 + a] : td_abs[r]);
+      red[tid] = s;
       __syncthreads();
-      for (int st = 128; st > 0; st >>= 1) {
-        if (tid < st) tr[tid] = radd(tr[tid], tr[tid + st]);
+      for (int st = kHbThreads / 2; st > 0; st >>= 1) {
+        if (tid < st) red[tid] = radd(red[tid], red[tid + st]);
         __syncthreads();
       }
       if (tid == 0) {
-        if (a < A1) gb2[a] = tr[0];
-        else td_acc[0] = radd(td_acc[0], tr[0] / (float)B);  // _err_acc.add_(td.mean())
+        if (a < A1) gb2[a] = red[0];
+        else td_acc[0] = radd(td_acc[0], red[0] / (float)B);  // _err_acc.add_(td.mean())
       }
       __syncthreads();
     }
@@ -286,41 +289,54 @@ __global__ __launch_bounds__(256) void k_heads_backward(const float *__restrict_
   }
   const int c = tid % kHbCols, rg = tid / kHbCols;
   const int j = (int)blockIdx.x * kHbCols + c;
-  float wc[kHbMaxA1], aw[kHbMaxA1];
+  float wc[MAXA], aw[MAXA];
 #pragma unroll
-  for (int a = 0; a < kHbMaxA1; ++a) {
+  for (int a = 0; a < MAXA; ++a) {
     wc[a] = a < A1 ? w2[(int64_t)a * H2 + j] : 0.0f;
     aw[a] = 0.0f;
   }
   float ab = 0.0f;
-  for (int64_t r = rg; r < B; r += kHbRows) {
-    const float hv = h[r * ldh + j];
-    const float *d = dq + r * A1;
-    float g = 0.0f;
+  for (int64_t r0 = rg; r0 < B; r0 += (int64_t)RB * kHbGroups) {
+    float hv[RB], dv[RB][MAXA];
 #pragma unroll
-    for (int a = 0; a < kHbMaxA1; ++a)
-      if (a < A1) {
-        const float da = d[a];
-        g = radd(g, rmul(da, wc[a]));
-        aw[a] = radd(aw[a], rmul(da, hv));
-      }
-    g = hv > 0.0f ? g : 0.0f;  // threshold_backward(g, h, 0)
-    gh[r * H2 + j] = g;
-    ab = radd(ab, g);
+    for (int u = 0; u < RB; ++u) {  // all loads of the batch first
+      const int64_t r = r0 + (int64_t)u * kHbGroups;
+      const bool live = r < B;
+      hv[u] = live ? h[r * ldh + j] : 0.0f;
+#pragma unroll
+      for (int a = 0; a < MAXA; ++a) dv[u][a] = (live && a < A1) ? dq[r * A1 + a] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < RB; ++u) {
+      const int64_t r = r0 + (int64_t)u * kHbGroups;
+      if (r >= B) break;
+      float g = 0.0f;
+#pragma unroll
+      for (int a = 0; a < MAXA; ++a)
+        if (a < A1) {
+          g = radd(g, rmul(dv[u][a], wc[a]));
+          aw[a] = radd(aw[a], rmul(dv[u][a], hv[u]));
+        }
+      g = hv[u] > 0.0f ? g : 0.0f;  // threshold_backward(g, h, 0)
+      gh[r * H2 + j] = g;
+      ab = radd(ab, g);
+    }
   }
   // fixed-order sums over the row groups: gb1, then each row of gw2
   for (int a = -1; a < A1; ++a) {
     float v = ab;
 #pragma unroll
-    for (int k = 0; k < kHbMaxA1; ++k)
+    for (int k = 0; k < MAXA; ++k)
       if (k == a) v = aw[k];
-    red[rg][c] = v;
+    red[tid] = v;
     __syncthreads();
-    if (rg == 0) {
-      float s = red[0][c];
-      for (int k = 1; k < kHbRows; ++k) s = radd(s, red[k][c]);
-      if (a < 0) gb1[j] = s;
-      else gw2[(int64_t)a * H2 + j] = s;
+    for (int st = kHbThreads / 2; st >= kHbCols; st >>= 1) {  // lanes tid, tid + st: same column
+      if (tid < st) red[tid] = radd(red[tid], red[tid + st]);
+      __syncthreads();
+    }
+    if (tid < kHbCols) {
+      if (a < 0) gb1[j] = red[tid];
+      else gw2[(int64_t)a * H2 + j] = red[tid];
     }
     __syncthreads();
   }
@@ -414,8 +430,13 @@ int rth_heads_backward(const float *dq, const float *h, int64_t ldh, const float
   RTH_REQUIRE(dq && h && w2 && gh && gw2 && gb2 && gb1, "rth_heads_backward: NULL argument");
   RTH_REQUIRE(B >= 1 && A1 >= 1 && A1 <= kHbMaxA1 && H2 >= kHbCols && H2 % kHbCols == 0 && ldh >= H2,
               "rth_heads_backward: bad shape B=%lld H2=%d A1=%d ldh=%lld", (long long)B, H2, A1, (long long)ldh);
-  hipLaunchKernelGGL(k_heads_backward, dim3((unsigned)(H2 / kHbCols + 1)), dim3(256), 0, as_stream(stream), dq, h, ldh,
-                     w2, B, H2, A1, gh, gw2, gb2, gb1, td_abs, td_acc);
+  const dim3 grid((unsigned)(H2 / kHbCols + 1)), block(kHbThreads);
+  if (A1 <= 8)  // Atari's minimal action sets (Pong 6, Breakout 4): 4 rows of dq in registers per batch
+    hipLaunchKernelGGL((k_heads_backward<8, 4>), grid, block, 0, as_stream(stream), dq, h, ldh, w2, B, H2, A1, gh, gw2,
+                       gb2, gb1, td_abs, td_acc);
+  else
+    hipLaunchKernelGGL((k_heads_backward<kHbMaxA1, 1>), grid, block, 0, as_stream(stream), dq, h, ldh, w2, B, H2, A1,
+                       gh, gw2, gb2, gb1, td_abs, td_acc);
   RTH_LAUNCHED();
   return RTH_OK;
 }

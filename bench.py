@@ -58,6 +58,38 @@ def qnet_flops_per_sample(A=6):
     return 2 * macs
 
 
+def conv_roofline(ax, slot_cols, reps=30):
+    """The kernel with the most time per step, the conv torso's first layer
+    (k_conv_bias_relu on uint8 stacks), over the learner's 2B stacks of a batch slot, timed
+    alone with HIP events around direct launches on the current stream"""
+    from reth_amd import _lib
+    from reth_amd.fused_learner import _pair
+
+    net = ax.solver.q_network
+    x = _pair(slot_cols[0], slot_cols[3])
+    n = x.shape[0]
+    shape = net._torso_shapes(tuple(x.shape[1:]), True)[0][1]
+    pk = net._packed_for(net.pack_convs(), 0, True)
+    ho = (shape.hin - shape.kh) // shape.stride + 1
+    y = torch.empty((n, shape.cout, ho, ho), device=x.device, memory_format=torch.channels_last)
+    bias = net._convs()[0].bias
+    ev = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        _lib.call("rth_conv_bias_relu", _lib.ctypes.byref(shape), x.data_ptr(), None, n, pk.data_ptr(),
+                  bias.data_ptr(), y.data_ptr(), _lib.stream_ptr())
+        e1.record()
+        ev.append((e0, e1))
+    torch.cuda.synchronize()
+    t = float(np.median([a.elapsed_time(b) for a, b in ev[5:]])) / 1e3
+    flops = 2.0 * n * ho * ho * shape.cout * shape.cin * shape.kh * shape.kw
+    return {"kernel": f"k_conv_bias_relu conv1 (uint8 stacks, {n} samples = the learner's [s0; s1])",
+            "bound": "mfma", "achieved": round(flops / t / 1e12, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(flops / t / 1e12 / FP32_PEAK_TFLOPS, 4), "flops_per_launch": flops,
+            "launch_us": round(t * 1e6, 2), "note": "timed alone after the timed region (HIP events)"}
+
+
 def load_traffic(tag):
     p = os.path.join(ROOT, "profiles", f"traffic_{tag}.json")
     if os.path.exists(p):
@@ -268,6 +300,7 @@ def main():
         iso.append((e0, e1))
     torch.cuda.synchronize()
     iso_s = float(np.median([a.elapsed_time(b) for a, b in iso[5:]])) / 1e3
+    conv = conv_roofline(ax, slot_cols) if cfg.hip_conv and cfg.channels_last else None
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
@@ -317,6 +350,7 @@ def main():
         "qnet_mfma": {"tflops_per_step": round(flops_step / 1e12, 4),
                       "achieved_tflops": round(flops_step / step_s / 1e12, 2),
                       "peak_fp32_tflops": FP32_PEAK_TFLOPS},
+        "roofline_conv": conv,
         "cpu_baseline": cpu,
     }
     print(json.dumps(out), flush=True)

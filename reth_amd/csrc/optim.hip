@@ -117,7 +117,7 @@ struct ScalarArgs {
 };
 
 // per-workgroup sums of squares of the gradients; the workgroup that finishes last (ticket
-// counter, agent-scope release/acquire hand-off of the partials) then computes the scalars,
+// counter; partials stored write-through, read after an agent-scope acquire) then computes the scalars,
 // so the Adam launch follows directly (no separate single-workgroup launch in between)
 __global__ __launch_bounds__(kOptThreads) void k_grad_sqsum(OptArgs a, double *__restrict__ part,
                                                            unsigned *__restrict__ ticket, ScalarArgs sa) {
@@ -144,9 +144,9 @@ __global__ __launch_bounds__(kOptThreads) void k_grad_sqsum(OptArgs a, double *_
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    part[b] = red[0];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    // write-through (sc1) store of the partial, so no L2 write-back (release fence) is needed
+    // before the ticket; the last block invalidates its L1 (acquire) and reads plainly
+    __hip_atomic_store(&part[b], red[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     last = t == gridDim.x - 1;

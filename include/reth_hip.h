@@ -305,6 +305,14 @@ int rth_relu_bias_grad(const float *g_dev, const float *y_dev, float *gy_dev, fl
 int rth_heads_backward(const float *dq_dev, const float *h_dev, int64_t ldh, const float *w2_dev, int64_t B,
                        int32_t H2, int32_t A1, float *gh_dev, float *gw2_dev, float *gb2_dev, float *gb1_dev,
                        const float *td_abs_dev, float *td_acc_dev, void *stream);
+/* rth_td_huber (dueling heads, want dq) + rth_heads_backward in one launch, for
+ * B * (A + 1) <= 16384: writes |td| [B], the loss [1] and the heads' gradients as above;
+ * td_acc_dev (nullable) += mean |td|.  |td| and the gradients equal the two-launch path's. */
+int rth_td_heads_backward(const float *q_s0_dev, const float *q_s1_online_dev, const float *q_s1_target_dev,
+                          const int64_t *a_dev, const float *r_dev, const float *done_dev, const double *isw_dev,
+                          int64_t B, int64_t A, float gamma_n, int32_t double_q, const float *h_dev, int64_t ldh,
+                          const float *w2_dev, int32_t H2, float *td_abs_dev, float *loss_out_dev, float *gh_dev,
+                          float *gw2_dev, float *gb2_dev, float *gb1_dev, float *td_acc_dev, void *stream);
 
 /* ------------------------------------------------------------------------------------
  * Q-network convolution torso forward (reth/reth/algorithm/dqn/dqn_model.py:14-20: each

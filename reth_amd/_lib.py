@@ -111,6 +111,8 @@ SIGNATURES = {
                                      ctypes.POINTER(c_vp), c_vp]),
     "rth_heads_backward": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                    c_vp]),
+    "rth_td_heads_backward": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f32, c_i32, c_vp,
+                                      c_i64, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "rth_relu_bias_grad": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_vp]),
     "rth_conv_supported": (c_i32, [ctypes.POINTER(ConvShape)]),
     "rth_conv_packed_bytes": (c_i64, [ctypes.POINTER(ConvShape)]),

@@ -125,6 +125,48 @@ __device__ inline void q_row(const float *row, int A, int dueling, float *q) {
   for (int j = 0; j < A; ++j) q[j] = rsub(radd(v, row[j]), mean);
 }
 
+// One row of DQNSolver._calc_td_error + the IS-weighted smooth-L1 loss (dqn_solver.py:77-114):
+// returns td; *l_out = smooth_l1(|td|) * w; dq_row (nullable, A + dueling values) = d(mean
+// loss)/d(q row of s0) -- through Q = (V + A) - mean(A) when dueling.  f32, no contraction.
+__device__ inline float td_huber_row(const float *__restrict__ q0, const float *__restrict__ q1o,
+                                     const float *__restrict__ q1t, const int64_t *__restrict__ act,
+                                     const float *__restrict__ rew, const float *__restrict__ done,
+                                     const double *__restrict__ isw, int64_t b, int A, int dueling, float gamma_n,
+                                     int double_q, float invB, float *l_out, float *dq_row) {
+  const int ld = A + dueling;  // row length: A values, or A advantages + 1 state value
+  const int64_t a = act[b];
+  float qa[kMaxActions], qs[kMaxActions];
+  q_row(q0 + b * ld, A, dueling, qa);
+  const float q = qa[a];  // sum(q * one_hot(a)) (:79-81)
+  q_row((double_q ? q1o : q1t) + b * ld, A, dueling, qs);
+  const int astar = argmax_first(qs, A);  // (:83-94)
+  if (double_q) q_row(q1t + b * ld, A, dueling, qs);
+  const float nqb = qs[astar];
+  // expected = r + (gamma**n * next_q_best) * (1 - done)  (:96)
+  float t = rmul(gamma_n, nqb);
+  t = rmul(t, rsub(1.0f, done[b]));
+  const float y = radd(rew[b], t);
+  const float td = rsub(q, y);  // (:97)
+  const float z = fabsf(td);
+  // smooth_l1(beta=1) (:112) * w (:113-114)
+  float l = z < 1.0f ? rmul(rmul(0.5f, z), z) : rsub(z, 0.5f);
+  const float w = isw ? (float)isw[b] : 1.0f;
+  if (isw) l = rmul(l, w);
+  *l_out = l;
+  if (dq_row) {  // autograd: mean -> mul(w) -> smooth_l1' -> one_hot scatter
+    const float g = rmul(invB, w);
+    const float d = td <= -1.0f ? -g : (td >= 1.0f ? g : rmul(td, g));
+    if (!dueling) {
+      for (int j = 0; j < A; ++j) dq_row[j] = rmul(d, j == a ? 1.0f : 0.0f);
+    } else {  // through q = (v + adv) - mean(adv): d adv_j = g_j + (-sum g) / A, d v = sum g
+      const float dm = (-d) / (float)A;
+      for (int j = 0; j < A; ++j) dq_row[j] = radd(j == a ? d : 0.0f, dm);
+      dq_row[A] = d;
+    }
+  }
+  return td;
+}
+
 // PERSampler._normalize_weights (per_sampler.py:16-17): (w + 1e-6) ** alpha in float32,
 // correctly rounded; numpy's `** 0.5` is sqrt (fast_scalar_power), also correctly rounded.
 __device__ inline float per_normalize(float w, float alpha) {

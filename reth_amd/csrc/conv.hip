@@ -375,7 +375,13 @@ static int cu_count() {
 // loads).  Pixel pairs are loaded one group of kWgU pairs ahead.  Workgroup w sums a
 // contiguous pixel range and writes its partial; k_wgrad_reduce adds the partials in
 // workgroup order (deterministic).
-constexpr int kWgWaves = 8, kWgBlocks = 256, kWgU = 4;
+#ifndef CONV_WG_BLOCKS
+#define CONV_WG_BLOCKS 256
+#endif
+#ifndef CONV_WG_U
+#define CONV_WG_U 4
+#endif
+constexpr int kWgWaves = 8, kWgBlocks = CONV_WG_BLOCKS, kWgU = CONV_WG_U;
 
 template <int KH, int KW, int S, int CIN, int COUT, int HIN, int WIN>
 __global__ __launch_bounds__(kWgWaves * 64) void k_conv_wgrad_u8(const uint8_t *__restrict__ x,

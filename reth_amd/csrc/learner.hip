@@ -38,39 +38,13 @@ __global__ __launch_bounds__(kTdThreads) void k_td_huber(
   float acc = 0.0f;
   const int ld = A + dueling;  // row length: A values, or A advantages + 1 state value
   for (int64_t b = threadIdx.x; b < B; b += kTdThreads) {
-    const int64_t a = act[b];
-    float qa[kMaxActions], qs[kMaxActions];
-    q_row(q0 + b * ld, A, dueling, qa);
-    const float q = qa[a];  // sum(q * one_hot(a)) (:79-81)
-    q_row((double_q ? q1o : q1t) + b * ld, A, dueling, qs);
-    const int astar = argmax_first(qs, A);  // (:83-94)
-    if (double_q) q_row(q1t + b * ld, A, dueling, qs);
-    const float nqb = qs[astar];
-    // expected = r + (gamma**n * next_q_best) * (1 - done)  (:96), f32, no contraction
-    float t = rmul(gamma_n, nqb);
-    t = rmul(t, rsub(1.0f, done[b]));
-    const float y = radd(rew[b], t);
-    const float td = rsub(q, y);  // (:97)
+    float l;
+    const float td = td_huber_row(q0, q1o, q1t, act, rew, done, isw, b, A, dueling, gamma_n, double_q, invB, &l,
+                                  dq ? dq + b * ld : nullptr);
     if (td_out) td_out[b] = td;
-    const float z = fabsf(td);
-    if (td_abs_out) td_abs_out[b] = z;  // td_error.detach().cpu().abs() (:109), kept on device
-    // smooth_l1(beta=1) (:112) * w (:113-114)
-    float l = z < 1.0f ? rmul(rmul(0.5f, z), z) : rsub(z, 0.5f);
-    const float w = isw ? (float)isw[b] : 1.0f;
-    if (isw) l = rmul(l, w);
+    if (td_abs_out) td_abs_out[b] = fabsf(td);  // td_error.detach().cpu().abs() (:109), kept on device
     if (loss_elem) loss_elem[b] = l;
     acc = radd(acc, l);
-    if (dq) {  // autograd: mean -> mul(w) -> smooth_l1' -> one_hot scatter
-      const float g = rmul(invB, w);
-      const float d = td <= -1.0f ? -g : (td >= 1.0f ? g : rmul(td, g));
-      if (!dueling) {
-        for (int j = 0; j < A; ++j) dq[b * A + j] = rmul(d, j == a ? 1.0f : 0.0f);
-      } else {  // through q = (v + adv) - mean(adv): d adv_j = g_j + (-sum g) / A, d v = sum g
-        const float dm = (-d) / (float)A;
-        for (int j = 0; j < A; ++j) dq[b * ld + j] = radd(j == a ? d : 0.0f, dm);
-        dq[b * ld + A] = d;
-      }
-    }
   }
   part[threadIdx.x] = acc;
   __syncthreads();

@@ -342,6 +342,111 @@ __global__ __launch_bounds__(kHbThreads) void k_heads_backward(const float *__re
   }
 }
 
+
+// rth_td_huber + k_heads_backward in one launch: every workgroup recomputes the batch's TD rows
+// (td_huber_row, the same arithmetic as k_td_huber) into LDS -- d(loss)/d(heads) of all B
+// rows, <= kTdHbMaxElems values -- instead of reading them back from a separate launch; the
+// last workgroup also writes |td|, the loss (a fixed-order tree) and the |td| mean.
+constexpr int kTdHbMaxElems = 16384;
+
+template <int MAXA, int RB>
+__global__ __launch_bounds__(kHbThreads) void k_td_heads_backward(
+    const float *__restrict__ q0, const float *__restrict__ q1o, const float *__restrict__ q1t,
+    const int64_t *__restrict__ act, const float *__restrict__ rew, const float *__restrict__ done,
+    const double *__restrict__ isw, int64_t B, int A, float gamma_n, int double_q, const float *__restrict__ h,
+    int64_t ldh, const float *__restrict__ w2, int H2, float *__restrict__ td_abs, float *__restrict__ loss_out,
+    float *__restrict__ gh, float *__restrict__ gw2, float *__restrict__ gb2, float *__restrict__ gb1,
+    float *__restrict__ td_acc) {
+  __shared__ float dqs[kTdHbMaxElems];
+  __shared__ float red[kHbThreads];
+  const int tid = threadIdx.x, A1 = A + 1;
+  const bool tail = (int)blockIdx.x == H2 / kHbCols;  // gb2, |td|, loss, |td| mean
+  const float invB = 1.0f / (float)B;
+  float lacc = 0.0f, tacc = 0.0f;
+  for (int64_t b = tid; b < B; b += kHbThreads) {
+    float l;
+    const float td = td_huber_row(q0, q1o, q1t, act, rew, done, isw, b, A, 1, gamma_n, double_q, invB, &l,
+                                  dqs + b * A1);
+    if (tail) {
+      td_abs[b] = fabsf(td);
+      lacc = radd(lacc, l);
+      tacc = radd(tacc, fabsf(td));
+    }
+  }
+  __syncthreads();
+  if (tail) {
+    for (int a = -2; a < A1; ++a) {  // loss, |td| mean, then gb2
+      float v = a == -2 ? lacc : (a == -1 ? tacc : 0.0f);
+      if (a >= 0)
+        for (int64_t r = tid; r < B; r += kHbThreads) v = radd(v, dqs[r * A1 + a]);
+      red[tid] = v;
+      __syncthreads();
+      for (int st = kHbThreads / 2; st > 0; st >>= 1) {
+        if (tid < st) red[tid] = radd(red[tid], red[tid + st]);
+        __syncthreads();
+      }
+      if (tid == 0) {
+        if (a == -2) loss_out[0] = red[0] * invB;
+        else if (a == -1) { if (td_acc) td_acc[0] = radd(td_acc[0], red[0] / (float)B); }
+        else gb2[a] = red[0];
+      }
+      __syncthreads();
+    }
+    return;
+  }
+  const int c = tid % kHbCols, rg = tid / kHbCols;
+  const int j = (int)blockIdx.x * kHbCols + c;
+  float wc[MAXA], aw[MAXA];
+#pragma unroll
+  for (int a = 0; a < MAXA; ++a) {
+    wc[a] = a < A1 ? w2[(int64_t)a * H2 + j] : 0.0f;
+    aw[a] = 0.0f;
+  }
+  float ab = 0.0f;
+  for (int64_t r0 = rg; r0 < B; r0 += (int64_t)RB * kHbGroups) {
+    float hv[RB];
+#pragma unroll
+    for (int u = 0; u < RB; ++u) {
+      const int64_t r = r0 + (int64_t)u * kHbGroups;
+      hv[u] = r < B ? h[r * ldh + j] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < RB; ++u) {
+      const int64_t r = r0 + (int64_t)u * kHbGroups;
+      if (r >= B) break;
+      const float *d = dqs + r * A1;
+      float g = 0.0f;
+#pragma unroll
+      for (int a = 0; a < MAXA; ++a)
+        if (a < A1) {
+          const float da = d[a];
+          g = radd(g, rmul(da, wc[a]));
+          aw[a] = radd(aw[a], rmul(da, hv[u]));
+        }
+      g = hv[u] > 0.0f ? g : 0.0f;  // threshold_backward(g, h, 0)
+      gh[r * H2 + j] = g;
+      ab = radd(ab, g);
+    }
+  }
+  for (int a = -1; a < A1; ++a) {
+    float v = ab;
+#pragma unroll
+    for (int k = 0; k < MAXA; ++k)
+      if (k == a) v = aw[k];
+    red[tid] = v;
+    __syncthreads();
+    for (int st = kHbThreads / 2; st >= kHbCols; st >>= 1) {
+      if (tid < st) red[tid] = radd(red[tid], red[tid + st]);
+      __syncthreads();
+    }
+    if (tid < kHbCols) {
+      if (a < 0) gb1[j] = red[tid];
+      else gw2[(int64_t)a * H2 + j] = red[tid];
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace rth
 
 using namespace rth;
@@ -437,6 +542,28 @@ int rth_heads_backward(const float *dq, const float *h, int64_t ldh, const float
   else
     hipLaunchKernelGGL((k_heads_backward<kHbMaxA1, 1>), grid, block, 0, as_stream(stream), dq, h, ldh, w2, B, H2, A1,
                        gh, gw2, gb2, gb1, td_abs, td_acc);
+  RTH_LAUNCHED();
+  return RTH_OK;
+}
+
+int rth_td_heads_backward(const float *q0, const float *q1o, const float *q1t, const int64_t *a, const float *r,
+                          const float *done, const double *isw, int64_t B, int64_t A, float gamma_n, int32_t double_q,
+                          const float *h, int64_t ldh, const float *w2, int32_t H2, float *td_abs, float *loss_out,
+                          float *gh, float *gw2, float *gb2, float *gb1, float *td_acc, void *stream) {
+  RTH_REQUIRE(q0 && q1t && a && r && done && (q1o || !double_q) && h && w2 && td_abs && loss_out && gh && gw2 && gb2 &&
+                  gb1,
+              "rth_td_heads_backward: NULL argument");
+  RTH_REQUIRE(B >= 1 && A >= 1 && A < kHbMaxA1 && B * (A + 1) <= kTdHbMaxElems && H2 >= kHbCols && H2 % kHbCols == 0 &&
+                  ldh >= H2,
+              "rth_td_heads_backward: bad shape B=%lld A=%lld H2=%d (B * (A + 1) <= %d)", (long long)B, (long long)A,
+              H2, kTdHbMaxElems);
+  const dim3 grid((unsigned)(H2 / kHbCols + 1)), block(kHbThreads);
+  if (A + 1 <= 8)
+    hipLaunchKernelGGL((k_td_heads_backward<8, 4>), grid, block, 0, as_stream(stream), q0, q1o, q1t, a, r, done, isw, B,
+                       (int)A, gamma_n, double_q, h, ldh, w2, H2, td_abs, loss_out, gh, gw2, gb2, gb1, td_acc);
+  else
+    hipLaunchKernelGGL((k_td_heads_backward<kHbMaxA1, 1>), grid, block, 0, as_stream(stream), q0, q1o, q1t, a, r, done,
+                       isw, B, (int)A, gamma_n, double_q, h, ldh, w2, H2, td_abs, loss_out, gh, gw2, gb2, gb1, td_acc);
   RTH_LAUNCHED();
   return RTH_OK;
 }

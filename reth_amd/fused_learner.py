@@ -8,8 +8,8 @@ path of solver.py (compute_grads with torch.autograd), without the autograd engi
             slot keeps s1 right behind s0, replay.HbmReplay.new_batch), each conv one
             rth_conv_bias_relu launch, FC1 one hipBLASLt GEMM with the bias+ReLU epilogue,
             the block-diagonal FC2 one GEMM;
-  TD        rth_td_huber on the raw heads -> |td|, loss, d(loss)/d(heads of s0);
-  backward  FC2 + threshold + both bias sums in rth_heads_backward (also the Trainer's
+  TD        rth_td_huber on the raw heads -> |td|, loss, d(loss)/d(heads of s0), fused with
+  backward  FC2 + threshold + both bias sums (rth_td_heads_backward; also the Trainer's
             mean |td|), FC1 as two GEMMs, conv3 / conv2 as rth_relu_bias_grad + MIOpen's data
             and weight gradients, conv1 as rth_conv_relu_wgrad straight from the uint8 stacks
             (f32 input: rth_relu_bias_grad + MIOpen's weight gradient), the merged-head
@@ -22,6 +22,9 @@ import torch
 
 from . import _lib
 from ._lib import call, ctypes, ptr, stream_ptr
+
+
+TD_HB_MAX = 16384  # rth_td_heads_backward keeps B * (A + 1) TD gradient rows in LDS
 
 
 def eligible(net, s0, s1):
@@ -88,14 +91,32 @@ def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None):
             q1t = solver.target_heads(s1)
         q0 = heads[:B]
         q1o = heads[B:] if pair else None
-        loss, td_abs, dq = td_huber_forward(q0, q1o, q1t, a, r, done, isw, solver.gamma_n, solver.double_q,
-                                            want_dq=True, dueling=True)
-        # FC2 + threshold + bias sums
         H2, A1 = w1.shape[0], w2.shape[0]
         gh1 = torch.empty((B, H2), dtype=torch.float32, device=x.device)
         gw2, gb2, gb1 = torch.empty_like(w2), torch.empty_like(b2), torch.empty_like(b1)
-        call("rth_heads_backward", ptr(dq), ptr(h1), h1.stride(0), ptr(w2), B, H2, A1, ptr(gh1), ptr(gw2), ptr(gb2),
-             ptr(gb1), ptr(td_abs), ptr(td_acc), st)
+        if B * A1 <= TD_HB_MAX:
+            # TD/Huber + FC2 + threshold + bias sums in one launch
+            dev = x.device
+            a = a.to(device=dev, dtype=torch.int64).contiguous().view(-1)
+            r = r.to(device=dev, dtype=torch.float32).contiguous().view(-1)
+            done = done.to(device=dev, dtype=torch.float32).contiguous().view(-1)
+            if isw is not None:
+                isw = isw.to(device=dev, dtype=torch.float64).contiguous().view(-1)
+            q1t = q1t.contiguous()
+            if q1t.shape != q0.shape or a.numel() != B or r.numel() != B or done.numel() != B or \
+                    (isw is not None and isw.numel() != B):
+                raise ValueError("batch columns / target heads disagree with the batch")
+            td_abs = torch.empty(B, dtype=torch.float32, device=dev)
+            loss = torch.empty(1, dtype=torch.float32, device=dev)
+            call("rth_td_heads_backward", ptr(q0), ptr(q1o), ptr(q1t), ptr(a), ptr(r), ptr(done), ptr(isw), B, A1 - 1,
+                 float(solver.gamma_n), int(bool(solver.double_q)), ptr(h1), h1.stride(0), ptr(w2), H2, ptr(td_abs),
+                 ptr(loss), ptr(gh1), ptr(gw2), ptr(gb2), ptr(gb1), ptr(td_acc), st)
+        else:
+            loss, td_abs, dq = td_huber_forward(q0, q1o, q1t, a, r, done, isw, solver.gamma_n, solver.double_q,
+                                                want_dq=True, dueling=True)
+            # FC2 + threshold + bias sums
+            call("rth_heads_backward", ptr(dq), ptr(h1), h1.stride(0), ptr(w2), B, H2, A1, ptr(gh1), ptr(gw2),
+                 ptr(gb2), ptr(gb1), ptr(td_abs), ptr(td_acc), st)
         # FC1
         gfeat = torch.mm(gh1, w1)
         gw1 = torch.mm(gh1.t(), feat[:B])

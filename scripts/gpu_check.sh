@@ -42,6 +42,7 @@ for step in "$@"; do
     prio) for pr in 0 -1; do RTH_LEARNER_PRIORITY=$pr run bench_prio$pr 600 python bench.py --steps 200 --warmup 20 --no-cpu-baseline; done ;;
     convt) run pytest_conv 600 python -m pytest tests/test_conv_gpu.py -q -rf -x ;;
     convb) run bench_conv 300 python scripts/bench_conv.py ;;
+    wgv) for v in build/variants/*.so; do b=$(basename $v .so); RTH_LIB_PATH=$PWD/$v run bench_wgrad_$b 300 python scripts/bench_wgrad.py; done ;;
     convwpc) for w in 1 2 3 4; do RTH_CONV_WG_PER_CU=$w run bench_conv_wpc$w 300 python scripts/bench_conv.py; done ;;
     convv) for v in build/variants/*.so; do b=$(basename $v .so); RTH_LIB_PATH=$PWD/$v run bench_conv_$b 300 python scripts/bench_conv.py; done ;;
     convprof) export TMPDIR=/tmp; run prof_conv 300 rocprofv3 --kernel-trace --output-format csv \

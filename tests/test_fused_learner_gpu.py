@@ -114,3 +114,42 @@ def test_batch_slots_keep_s1_behind_s0(dev):
     assert s1.data_ptr() == s0.data_ptr() + s0.numel()
     x = _pair(s0, s1)
     assert x.data_ptr() == s0.data_ptr() and x.shape[0] == 64
+
+
+@pytest.mark.parametrize("B,A,double_q", [(512, 6, 1), (37, 4, 1), (64, 18, 0)])
+def test_td_heads_backward_equals_two_launches(dev, B, A, double_q):
+    """rth_td_heads_backward (TD rows recomputed per workgroup in LDS) gives exactly the |td|
+    and gradients of rth_td_huber + rth_heads_backward; the loss within fp32 rounding"""
+    from reth_amd._lib import call, ptr, stream_ptr
+
+    g = torch.Generator(device=dev).manual_seed(B + A)
+    A1, H2 = A + 1, 512
+    q0, q1o, q1t = (torch.randn(B, A1, device=dev, generator=g) for _ in range(3))
+    a = torch.randint(0, A, (B,), device=dev, generator=g)
+    r = torch.randn(B, device=dev, generator=g)
+    done = (torch.rand(B, device=dev, generator=g) < 0.2).float()
+    isw = torch.rand(B, device=dev, generator=g, dtype=torch.float64) + 0.5
+    h = torch.relu(torch.randn(B, H2, device=dev, generator=g))
+    w2 = torch.randn(A1, H2, device=dev, generator=g) * 0.05
+    gn = float(np.float32(0.99 ** 3))
+    outs = []
+    for fused in (True, False):
+        td = torch.empty(B, device=dev)
+        loss = torch.empty(1, device=dev)
+        gh, gw2 = torch.empty(B, H2, device=dev), torch.empty(A1, H2, device=dev)
+        gb2, gb1 = torch.empty(A1, device=dev), torch.empty(H2, device=dev)
+        acc = torch.zeros((), device=dev)
+        if fused:
+            call("rth_td_heads_backward", ptr(q0), ptr(q1o), ptr(q1t), ptr(a), ptr(r), ptr(done), ptr(isw), B, A, gn,
+                 double_q, ptr(h), H2, ptr(w2), H2, ptr(td), ptr(loss), ptr(gh), ptr(gw2), ptr(gb2), ptr(gb1),
+                 ptr(acc), stream_ptr())
+        else:
+            dq = torch.empty(B, A1, device=dev)
+            call("rth_td_huber", ptr(q0), ptr(q1o), ptr(q1t), ptr(a), ptr(r), ptr(done), ptr(isw), B, A, gn, double_q,
+                 1, None, ptr(td), None, ptr(loss), ptr(dq), stream_ptr())
+            call("rth_heads_backward", ptr(dq), ptr(h), H2, ptr(w2), B, H2, A1, ptr(gh), ptr(gw2), ptr(gb2), ptr(gb1),
+                 ptr(td), ptr(acc), stream_ptr())
+        outs.append((td, gh, gw2, gb2, gb1, acc, loss))
+    for x, y in zip(outs[0][:6], outs[1][:6]):
+        assert torch.equal(x, y)
+    torch.testing.assert_close(outs[0][6], outs[1][6], rtol=1e-6, atol=0)

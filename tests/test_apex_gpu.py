@@ -161,3 +161,27 @@ def test_target_pass_precompute_respects_target_syncs(dev):
         if synced:
             assert v_next == "full"
     ax.close()
+
+
+def test_breakout_shaped_graph_loop(dev):
+    """BASELINE configs[2]'s shape at a small scale (A = 4, many actors relative to the replay):
+    graph replay with the dedup actor, the fused learner pass and the fused TD + heads kernel;
+    the replay keeps the actors' rows and the weights stay finite"""
+    from reth_amd.apex import ApexConfig, ApexDQN
+
+    cfg = ApexConfig(n_actors=128, num_actions=4, capacity=8192, batch_size=64, sample_start=256, hip_graph=True,
+                     seed=9, p_done=0.01, send_weights_interval=3, recv_weights_interval=5, update_target_interval=6)
+    ax = ApexDQN(cfg, device=dev)
+    for _ in range(40):
+        ax.iteration()
+    torch.cuda.synchronize()
+    assert ax._graphs is not None and ax.updates == ax.replay.info()[4]
+    assert ax.actor_modes.get("dedup", 0) > 0
+    assert all(torch.isfinite(p).all() for p in ax.solver.q_network.parameters())
+    act = ax.actors
+    assert int(act.action.max()) < 4
+    size, tail = ax.replay.info()[:2]
+    out = ax.replay.gather(torch.arange(tail - 128, tail, device=dev))
+    rows = act._sets[(act.pushes - 2) % 2]
+    assert torch.equal(out[1], rows.a) and torch.equal(out[0], act.frames[rows.s0])
+    ax.close()

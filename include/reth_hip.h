@@ -249,6 +249,32 @@ int rth_synth_env_step(uint8_t *frames_dev, int64_t n_actors, int32_t ring, int6
                        const int64_t *t_dev, int64_t *cur_slot_dev, const int64_t *action_dev, uint64_t seed,
                        float p_reward, float p_done, float *r_out_dev, float *done_out_dev,
                        int64_t *s0_handle_dev, int64_t *s1_handle_dev, void *stream);
+/* The tail of one fused actor step, one workgroup per actor: rth_eps_greedy (dueling heads,
+ * Philox draws at counter *t_dev) on q, the previous n-step rows' |td| (rth_td_huber with
+ * target == online, isw = 1) from the per-stack heads cache -- heads of stack h at
+ * qcache[h * (A + 1)] --, rth_synth_env_step at t = *t_dev and rth_nstep_push of the new
+ * transition into the row outputs; every value equals the one of those separate calls.
+ * td_abs (nullable) skips the rows' |td|. */
+typedef struct rth_actor_tail_args {
+  const float *q;          /* acting heads [N, A + 1] */
+  const double *eps;       /* [N] */
+  const int64_t *t_dev;    /* env step / Philox counter */
+  int64_t *action;         /* out [N] */
+  const float *qcache;
+  const int64_t *prev_s0, *prev_a, *prev_s1;
+  const float *prev_r, *prev_done;
+  float *td_abs;           /* out [N] */
+  uint8_t *frames;
+  int64_t *cur_slot;
+  float *r_out, *done_out; /* out [N] */
+  int64_t *s0_h, *s1_h;    /* out [N] */
+  uint64_t seed;           /* exploration and env seed */
+  int64_t N;
+  float gamma_n, p_reward, p_done;
+  int32_t ring, A;
+} rth_actor_tail_args;
+int rth_actor_tail(rth_nstep *h, const rth_actor_tail_args *args, int32_t *emit_dev, int64_t *s0_out_dev,
+                   int64_t *a_out_dev, float *r_out_dev, int64_t *s1_out_dev, float *done_out_dev, void *stream);
 /* initial reset of every actor into slot 1 (t = 0) */
 int rth_synth_env_reset(uint8_t *frames_dev, int64_t n_actors, int32_t ring, uint64_t seed,
                         int64_t *cur_slot_dev, void *stream);

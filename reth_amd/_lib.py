@@ -54,6 +54,15 @@ class ConvShape(ctypes.Structure):
 
 CONV_F32_NHWC, CONV_U8_CHW = 0, 1
 
+
+class ActorTailArgs(ctypes.Structure):
+    """rth_actor_tail_args"""
+    _fields_ = [("q", c_vp), ("eps", c_vp), ("t_dev", c_vp), ("action", c_vp), ("qcache", c_vp),
+                ("prev_s0", c_vp), ("prev_a", c_vp), ("prev_s1", c_vp), ("prev_r", c_vp), ("prev_done", c_vp),
+                ("td_abs", c_vp), ("frames", c_vp), ("cur_slot", c_vp), ("r_out", c_vp), ("done_out", c_vp),
+                ("s0_h", c_vp), ("s1_h", c_vp), ("seed", c_u64), ("N", c_i64), ("gamma_n", c_f32),
+                ("p_reward", c_f32), ("p_done", c_f32), ("ring", c_i32), ("A", c_i32)]
+
 # name -> (restype, argtypes); must match include/reth_hip.h exactly
 SIGNATURES = {
     "rth_last_error": (ctypes.c_char_p, []),
@@ -94,6 +103,7 @@ SIGNATURES = {
     "rth_eps_greedy": (c_i32, [c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_u64, c_u64, c_vp, c_vp, c_vp]),
     "rth_counter_add": (c_i32, [c_vp, c_i64, c_vp]),
     "rth_compact_flagged": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp]),
+    "rth_actor_tail": (c_i32, [c_vp, ctypes.POINTER(ActorTailArgs), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "rth_nstep_create": (c_i32, [c_i64, c_i32, c_f64, c_i32, c_i32, ctypes.POINTER(c_vp)]),
     "rth_nstep_destroy": (c_i32, [c_vp]),
     "rth_nstep_reset": (c_i32, [c_vp, c_vp]),

@@ -15,7 +15,9 @@ Here all N actors of a GPU step together, entirely in HBM:
            rth_nstep_push (emits one row per actor once warm)
   prioritise(): Q-net over the emitted rows' s0/s1 stacks (batch 2N) -> rth_td_huber
            (no grad) = calc_loss
-  step_fused(): both in one 3N forward (acting stacks + the previous step's rows)
+  step_fused(): the acting forward and the previous step's rows' priorities in one step: the
+           rows' heads come from a per-stack cache (dedup) or one 4-way forward, then
+           rth_actor_tail (eps-greedy + |td| + env step + n-step push, one launch)
   append(): rth_replay_append copies the rows' stacks from the ring into FIFO slots and
            inserts (|td| + 1e-6)^alpha into the tree.
 No host synchronisation anywhere in the loop.
@@ -217,23 +219,29 @@ class VecActors:
         call("rth_counter_add", ptr(self.t_dev), 1, s)
         N = self.N
         hip = self._hip_heads(q_net)
-        if dedup:
+        if hip:
             torch.add(self.cur_slot, self._base, out=self.hx[:N])
-            q = q_net.forward_heads(self.frames, rows=self.hx[:2 * N], n_dev=self.n_ext)
-            dueling = 1
-            self._scatter_heads(q, self.hx, 2 * N)
-            call("rth_copy_rows", ptr(self.qrows), 0, None, ptr(self.qcache), 0, ptr(prev.s0), N, q.shape[1],
-                 _lib.RTH_F32, _lib.RTH_F32, 0, s)
-            call("rth_copy_rows", ptr(self.qrows[N:]), 0, None, ptr(self.qcache), 0, ptr(prev.s1), N, q.shape[1],
-                 _lib.RTH_F32, _lib.RTH_F32, 0, s)
-            q0, q1 = self.qrows[:N], self.qrows[N:]
-        elif hip:  # everything: acting, last step's terminal stacks, the rows' s0 and s1 -> cache
-            torch.add(self.cur_slot, self._base, out=self.hx[:N])
-            torch.cat([prev.s0, prev.s1], out=self.hx[2 * N:])
-            q = q_net.forward_heads(self.frames, rows=self.hx)
-            dueling = 1
-            self._scatter_heads(q, self.hx, 4 * N)
-            q0, q1 = q[2 * N:3 * N], q[3 * N:]
+            if dedup:  # acting + terminal stacks (device count); the rows' heads are in the cache
+                q = q_net.forward_heads(self.frames, rows=self.hx[:2 * N], n_dev=self.n_ext)
+                self._scatter_heads(q, self.hx, 2 * N)
+            else:  # everything: acting, last step's terminal stacks, the rows' s0 and s1 -> cache
+                torch.cat([prev.s0, prev.s1], out=self.hx[2 * N:])
+                q = q_net.forward_heads(self.frames, rows=self.hx)
+                self._scatter_heads(q, self.hx, 4 * N)
+            # eps-greedy, the previous rows' |td| from the cache, env step, n-step push: one launch
+            td_abs = torch.empty(N, dtype=torch.float32, device=self.device)
+            args = _lib.ActorTailArgs(ptr(q), ptr(self.eps), ptr(self.t_dev), ptr(self.action), ptr(self.qcache),
+                                      ptr(prev.s0), ptr(prev.a), ptr(prev.s1), ptr(prev.r), ptr(prev.done),
+                                      ptr(td_abs), ptr(self.frames), ptr(self.cur_slot), ptr(self.reward),
+                                      ptr(self.done), ptr(self.s0_h), ptr(self.s1_h), self.seed, N, self.gamma_n,
+                                      self.p_reward, self.p_done, self.ring, self.A)
+            call("rth_actor_tail", self._nstep, _lib.ctypes.byref(args), ptr(self.emit), ptr(cur.s0), ptr(cur.a),
+                 ptr(cur.r), ptr(cur.s1), ptr(cur.done), s)
+            self._terminal_stacks()
+            self.pushes += 1
+            self.fresh += 1
+            self._bind_rows(cur)
+            return (td_abs, prev) if p > self.n_step else (None, None)
         else:
             torch.cat([self.current_obs_handles(), prev.s0, prev.s1], out=self.handles3)
             q, dueling = self._forward_stacks(q_net, self.handles3)

@@ -11,28 +11,28 @@ namespace rth {
 // ------------------------------------------------------------------ epsilon-greedy
 // One lane per actor: A <= 18 for Atari, so the row argmax is a short in-register loop and
 // the launch is one wave per 64 actors.
+__device__ inline int64_t eps_greedy_one(const float *__restrict__ q, int64_t i, int A, int dueling,
+                                         const double *__restrict__ eps, const double *__restrict__ u_in,
+                                         const int64_t *__restrict__ ra_in, uint64_t seed, uint64_t counter) {
+  const double u = u_in ? u_in[i] : philox_uniform(seed, counter, (uint32_t)i, STREAM_EXPLORE);
+  if (u < eps[i]) {
+    if (ra_in) return ra_in[i];
+    uint32_t c[4] = {(uint32_t)i, (uint32_t)counter, (uint32_t)(counter >> 32), STREAM_RANDACT};
+    philox4x32(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    return (int64_t)(((uint64_t)c[0] * (uint64_t)A) >> 32);  // uniform in [0, A)
+  }
+  float qr[kMaxActions];
+  q_row(q + i * (A + dueling), A, dueling, qr);
+  return argmax_first(qr, A);
+}
+
 __global__ void k_eps_greedy(const float *__restrict__ q, int64_t N, int A, int dueling, const double *__restrict__ eps,
                              const double *__restrict__ u_in, const int64_t *__restrict__ ra_in, uint64_t seed,
                              uint64_t counter, const int64_t *__restrict__ counter_dev, int64_t *__restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= N) return;
   if (counter_dev) counter = (uint64_t)*counter_dev;
-  const double u = u_in ? u_in[i] : philox_uniform(seed, counter, (uint32_t)i, STREAM_EXPLORE);
-  if (u < eps[i]) {
-    int64_t ra;
-    if (ra_in) {
-      ra = ra_in[i];
-    } else {
-      uint32_t c[4] = {(uint32_t)i, (uint32_t)counter, (uint32_t)(counter >> 32), STREAM_RANDACT};
-      philox4x32(c, (uint32_t)seed, (uint32_t)(seed >> 32));
-      ra = (int64_t)(((uint64_t)c[0] * (uint64_t)A) >> 32);  // uniform in [0, A)
-    }
-    out[i] = ra;
-  } else {
-    float qr[kMaxActions];
-    q_row(q + i * (A + dueling), A, dueling, qr);
-    out[i] = argmax_first(qr, A);
-  }
+  out[i] = eps_greedy_one(q, i, A, dueling, eps, u_in, ra_in, seed, counter);
 }
 
 // ------------------------------------------------------------------ n-step adder
@@ -43,15 +43,11 @@ struct NStepState {
   float *r, *done;
 };
 
-__global__ void k_nstep_push(NStepState st, int64_t N, int n, double gamma, int mode,
-                             const int64_t *__restrict__ s0, const int64_t *__restrict__ a,
-                             const float *__restrict__ r, const int64_t *__restrict__ s1,
-                             const float *__restrict__ done, int32_t *__restrict__ emit,
-                             int64_t *__restrict__ s0_out, int64_t *__restrict__ a_out,
-                             float *__restrict__ r_out, int64_t *__restrict__ s1_out,
-                             float *__restrict__ done_out) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= N) return;
+__device__ inline void nstep_push_one(const NStepState &st, int64_t i, int n, double gamma, int mode, int64_t s0,
+                                      int64_t a, float rn, int64_t s1n, float done, int32_t *__restrict__ emit,
+                                      int64_t *__restrict__ s0_out, int64_t *__restrict__ a_out,
+                                      float *__restrict__ r_out, int64_t *__restrict__ s1_out,
+                                      float *__restrict__ done_out) {
   const int64_t base = i * n;
   int count = st.count[i];
   int emitted = 0;
@@ -66,8 +62,6 @@ __global__ void k_nstep_push(NStepState st, int64_t N, int n, double gamma, int 
     emitted = 1;
   }
   emit[i] = emitted;
-  const float rn = r[i];
-  const int64_t s1n = s1[i];
   double t_gamma = gamma;
   for (int k = 0; k < count; ++k) {  // newest -> oldest (nstep_adder.py:16-25)
     const int64_t p = base + k;
@@ -87,12 +81,25 @@ __global__ void k_nstep_push(NStepState st, int64_t N, int n, double gamma, int 
     st.s1[p] = st.s1[p - 1];
     st.done[p] = st.done[p - 1];
   }
-  st.s0[base] = s0[i];
-  st.a[base] = a[i];
+  st.s0[base] = s0;
+  st.a[base] = a;
   st.r[base] = rn;
   st.s1[base] = s1n;
-  st.done[base] = done[i];
+  st.done[base] = done;
   st.count[i] = count + 1;
+}
+
+__global__ void k_nstep_push(NStepState st, int64_t N, int n, double gamma, int mode,
+                             const int64_t *__restrict__ s0, const int64_t *__restrict__ a,
+                             const float *__restrict__ r, const int64_t *__restrict__ s1,
+                             const float *__restrict__ done, int32_t *__restrict__ emit,
+                             int64_t *__restrict__ s0_out, int64_t *__restrict__ a_out,
+                             float *__restrict__ r_out, int64_t *__restrict__ s1_out,
+                             float *__restrict__ done_out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  nstep_push_one(st, i, n, gamma, mode, s0[i], a[i], r[i], s1[i], done[i], emit, s0_out, a_out, r_out, s1_out,
+                 done_out);
 }
 
 // ------------------------------------------------------------------ synthetic env
@@ -108,12 +115,17 @@ __device__ __forceinline__ uint4 env_bytes(uint64_t seed, int64_t actor, int64_t
   return make_uint4(c[0], c[1], c[2], c[3]);
 }
 
-__global__ __launch_bounds__(kEnvThreads) void k_env_step(uint8_t *frames, int ring, int64_t t,
-                                                          const int64_t *t_dev, int64_t *cur_slot, uint64_t seed,
-                                                          float p_reward, float p_done, float *r_out,
-                                                          float *done_out, int64_t *s0_h, int64_t *s1_h) {
-  const int64_t i = blockIdx.x;
-  if (t_dev) t = *t_dev;
+// one actor's synthetic env step by a whole workgroup; returns (in every lane) the reward,
+// done flag and the s0 / s1 stack handles; lane 0 writes them and the new cur_slot
+struct EnvOut {
+  float reward;
+  bool done;
+  int64_t s0h, s1h;
+};
+
+__device__ inline EnvOut env_step_one(uint8_t *frames, int ring, int64_t t, int64_t i, int64_t *cur_slot, uint64_t seed,
+                                      float p_reward, float p_done, float *r_out, float *done_out, int64_t *s0_h,
+                                      int64_t *s1_h) {
   const int64_t stack_bytes = 4 * kFrameBytes;
   // reward / done: one Philox block per (actor, t), identical in every lane
   const uint4 rd = env_bytes(seed, i, t, 2, 0);
@@ -131,13 +143,77 @@ __global__ __launch_bounds__(kEnvThreads) void k_env_step(uint8_t *frames, int r
     if (done) dr[v] = env_bytes(seed, i, t, 1, c);                        // reset: one frame x4
   }
   __syncthreads();  // every lane has read cur_slot[i] before lane 0 rewrites it
+  const EnvOut o{reward, done, i * ring + cur, i * ring + nxt};
   if (threadIdx.x == 0) {
     r_out[i] = reward;
     done_out[i] = done ? 1.0f : 0.0f;
-    s0_h[i] = i * ring + cur;
-    s1_h[i] = i * ring + nxt;
+    s0_h[i] = o.s0h;
+    s1_h[i] = o.s1h;
     cur_slot[i] = done ? rst : nxt;
   }
+  return o;
+}
+
+__global__ __launch_bounds__(kEnvThreads) void k_env_step(uint8_t *frames, int ring, int64_t t,
+                                                          const int64_t *t_dev, int64_t *cur_slot, uint64_t seed,
+                                                          float p_reward, float p_done, float *r_out,
+                                                          float *done_out, int64_t *s0_h, int64_t *s1_h) {
+  if (t_dev) t = *t_dev;
+  env_step_one(frames, ring, t, blockIdx.x, cur_slot, seed, p_reward, p_done, r_out, done_out, s0_h, s1_h);
+}
+
+// The tail of a fused actor step (VecActors.step_fused), one workgroup per actor i:
+// epsilon-greedy on its acting heads, |td| of its previous n-step row from the per-stack heads
+// cache (calc_loss, target == online), its env step and its n-step push -- the same device
+// functions as k_eps_greedy / k_td_huber / k_env_step / k_nstep_push, one launch instead of
+// six (the rows' two heads gathers included).
+struct ActorTail {
+  const float *q;  // acting heads [N, A + 1]
+  const double *eps;
+  uint64_t seed;
+  const int64_t *t_dev;
+  int64_t *action;
+  const float *qcache;  // [stacks, A + 1]
+  const int64_t *prev_s0, *prev_a, *prev_s1;
+  const float *prev_r, *prev_done;
+  float gamma_n;
+  float *td_abs;
+  uint8_t *frames;
+  int ring;
+  int64_t *cur_slot;
+  float p_reward, p_done;
+  float *r_out, *done_out;
+  int64_t *s0_h, *s1_h;
+  NStepState ns;
+  int n;
+  double gamma;
+  int mode;
+  int32_t *emit;
+  int64_t *row_s0, *row_a, *row_s1;
+  float *row_r, *row_done;
+  int A;
+};
+
+__global__ __launch_bounds__(kEnvThreads) void k_actor_tail(ActorTail a) {
+  const int64_t i = blockIdx.x;
+  const int64_t t = *a.t_dev;
+  int64_t act = 0;
+  if (threadIdx.x == 0) {
+    act = eps_greedy_one(a.q, i, a.A, 1, a.eps, nullptr, nullptr, a.seed, (uint64_t)t);
+    a.action[i] = act;
+  } else if (threadIdx.x == 64 && a.td_abs) {  // another wave: the previous row's |td|
+    const int A1 = a.A + 1;
+    const float *q0 = a.qcache + a.prev_s0[i] * A1, *q1 = a.qcache + a.prev_s1[i] * A1;
+    float l;
+    const float td = td_huber_row(q0, q1, q1, a.prev_a + i, a.prev_r + i, a.prev_done + i, nullptr, 0, a.A, 1,
+                                  a.gamma_n, 1, 1.0f, &l, nullptr);
+    a.td_abs[i] = fabsf(td);
+  }
+  const EnvOut e = env_step_one(a.frames, a.ring, t, i, a.cur_slot, a.seed, a.p_reward, a.p_done, a.r_out, a.done_out,
+                                a.s0_h, a.s1_h);
+  if (threadIdx.x == 0)
+    nstep_push_one(a.ns, i, a.n, a.gamma, a.mode, e.s0h, act, e.reward, e.s1h, e.done ? 1.0f : 0.0f, a.emit,
+                   a.row_s0, a.row_a, a.row_r, a.row_s1, a.row_done);
 }
 
 __global__ __launch_bounds__(kEnvThreads) void k_env_reset(uint8_t *frames, int ring, uint64_t seed,
@@ -288,6 +364,25 @@ int rth_compact_flagged(const float *flag, const int64_t *vals, int64_t n, int64
   RTH_REQUIRE(flag && vals && out && count_out && n >= 0 && cap >= 0, "rth_compact_flagged: bad arguments");
   hipLaunchKernelGGL(k_compact_flagged, dim3(1), dim3(kCompactThreads), 0, as_stream(stream), flag, vals, n, out, cap,
                      fill, base, count_out);
+  RTH_LAUNCHED();
+  return RTH_OK;
+}
+
+int rth_actor_tail(rth_nstep *h, const rth_actor_tail_args *x, int32_t *emit, int64_t *s0_out, int64_t *a_out,
+                   float *r_out, int64_t *s1_out, float *done_out, void *stream) {
+  RTH_REQUIRE(h && x && emit && s0_out && a_out && r_out && s1_out && done_out, "rth_actor_tail: NULL argument");
+  RTH_REQUIRE(x->q && x->eps && x->t_dev && x->action && x->frames && x->cur_slot && x->r_out && x->done_out &&
+                  x->s0_h && x->s1_h && (!x->td_abs || (x->qcache && x->prev_s0 && x->prev_a && x->prev_s1 &&
+                                                         x->prev_r && x->prev_done)),
+              "rth_actor_tail: NULL field");
+  RTH_REQUIRE(x->N == h->N && x->N < (int64_t(1) << 31) && x->ring >= 4 && x->A >= 1 && x->A <= kMaxActions,
+              "rth_actor_tail: bad shape (N %lld, adder N %lld, ring %d, A %d)", (long long)x->N, (long long)h->N,
+              x->ring, x->A);
+  ActorTail a{x->q, x->eps, x->seed, x->t_dev, x->action, x->qcache, x->prev_s0, x->prev_a, x->prev_s1,
+              x->prev_r, x->prev_done, x->gamma_n, x->td_abs, x->frames, x->ring, x->cur_slot, x->p_reward,
+              x->p_done, x->r_out, x->done_out, x->s0_h, x->s1_h, h->st, h->n, h->gamma, h->mode, emit,
+              s0_out, a_out, s1_out, r_out, done_out, x->A};
+  hipLaunchKernelGGL(k_actor_tail, dim3((unsigned)x->N), dim3(kEnvThreads), 0, as_stream(stream), a);
   RTH_LAUNCHED();
   return RTH_OK;
 }

@@ -24,9 +24,9 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "gpurun_out")
 PROF = os.path.join(ROOT, "profiles")
-# learner gather launch (k_copy_rows flat grid): B rows x 2 frame columns x 7 chunks of 1024
-# pixels + 3 small columns x ceil(B/256) workgroups, 256 threads each
-LEARNER_GATHER_GRID = (512 * 2 * 7 + 3 * 2) * 256
+# learner gather launch (k_copy_rows flat grid): B rows x 2 frame columns x 7 chunks of 4 KiB
+# + the small columns one lane per 4-byte word, 256 threads per workgroup
+LEARNER_GATHER_GRID = (512 * 2 * 7 + 4 + 2 + 2) * 256  # a: 2 words/row, r and done: 1 word/row, 256 lanes/WG
 
 
 def main():
@@ -39,10 +39,11 @@ def main():
     trace = os.path.join(OUT, "prof", "run_kernel_trace.csv")
     if os.path.exists(trace):
         rows = sorted(csv.DictReader(open(trace)), key=lambda r: int(r["Start_Timestamp"]))
-        td = [r for r in rows if "k_td_huber" in r["Kernel_Name"]]
-        start = int(td[-2 * steps]["Start_Timestamp"])  # 2 TD launches per iteration
-        end = int(rows[-1]["End_Timestamp"])
-        win = [r for r in rows if int(r["Start_Timestamp"]) >= start]
+        ts = [r for r in rows if "k_tree_sample" in r["Kernel_Name"]]
+        start = int(ts[-steps]["Start_Timestamp"])  # one PER sample per iteration
+        # ... up to the last learner update (the bench's isolated gather / conv timings follow)
+        end = max(int(r["End_Timestamp"]) for r in rows if "k_adam" in r["Kernel_Name"])
+        win = [r for r in rows if start <= int(r["Start_Timestamp"]) <= end]
         agg = collections.defaultdict(lambda: [0, 0])
         for r in win:
             a = agg[r["Kernel_Name"][:100]]

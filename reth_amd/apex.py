@@ -216,8 +216,8 @@ class ApexDQN:
 
     def _capture(self):
         """Capture the actor block and the learner block (one per batch-slot parity).  With a
-        process group the learner is captured in two parts and the RCCL all-reduce of the
-        gradients runs eagerly between them."""
+        process group the learner is captured in parts cut at each final gradient bucket, and
+        the RCCL all-reduces run eagerly between them (_learner_replay)."""
         solver = self.solver
         solver.auto_target_update = False
         slots = self.loader._slots
@@ -225,7 +225,7 @@ class ApexDQN:
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
         split = solver.grad_hook is not None
-        G = dict(act=[], act_out=[], tgt=[], q1t=[], learn={}, learn_td={}, apply={}, grads={})
+        G = dict(act=[], act_out=[], tgt=[], q1t=[], learn={}, learn_td={}, buckets={}, grads={})
         with torch.cuda.stream(side):
             # the actor block by (mode, push parity): fused_actor alternates row sets; mode
             # "dedup" takes the rows' heads from the per-stack cache (VecActors.step_fused),
@@ -256,21 +256,28 @@ class ApexDQN:
                 G["q1t"].append(q1t)
             for variant in ("full", "pre"):
                 for p in range(2):
-                    g = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g, stream=side):
-                        data, idx, isw = slots[p]
-                        td = solver.compute_grads(data, isw, q1t=G["q1t"][p] if variant == "pre" else None)
-                        self.trainer._track(td)
-                        if not split:
-                            solver.apply_grads()
-                    G["learn"][variant, p] = g
-                    G["learn_td"][variant, p] = td
-                    if split:  # the gradients live in this graph's pool: all-reduce and apply THESE
-                        G["grads"][variant, p] = [q.grad for q in solver._params]
-                        ga = torch.cuda.CUDAGraph()
-                        with torch.cuda.graph(ga, stream=side):
-                            solver.apply_grads()
-                        G["apply"][variant, p] = ga
+                    v = (variant, p)
+                    parts, buckets = [torch.cuda.CUDAGraph()], []
+
+                    def cut(bucket, parts=parts, buckets=buckets):
+                        # end this part of the learner graph at a final gradient bucket: its
+                        # all-reduce runs between the parts (overlapping the next one)
+                        parts[-1].capture_end()
+                        buckets.append(bucket)
+                        parts.append(torch.cuda.CUDAGraph())
+                        parts[-1].capture_begin(pool=parts[0].pool())
+
+                    parts[0].capture_begin()
+                    data, idx, isw = slots[p]
+                    td = solver.compute_grads(data, isw, q1t=G["q1t"][p] if variant == "pre" else None,
+                                              mid=cut if split else None)
+                    self.trainer._track(td)
+                    if split and not buckets:  # autograd path: one bucket, every .grad
+                        cut([q.grad for q in solver._params])
+                    solver.apply_grads()
+                    parts[-1].capture_end()
+                    G["learn"][v], G["buckets"][v], G["learn_td"][v] = parts, buckets, td
+                    G["grads"][v] = [q.grad for q in solver._params]  # what apply_grads consumed
         torch.cuda.current_stream(self.device).wait_stream(side)
         self.actors.t, self.actors.pushes = host  # capture recorded, did not run, the steps
         self._graphs = G
@@ -283,13 +290,36 @@ class ApexDQN:
         self._actor_block_graph()
         k = self.loader._pending.pop(0)
         v = ("full", k)
-        G["learn"][v].replay()
-        if G["apply"]:
-            self.solver.grad_hook(self.solver._params, grads=G["grads"][v])  # RCCL all-reduce, eager
-            G["apply"][v].replay()
+        self._learner_replay(v)
         self.loader.issue()  # sample-ahead into the other slot
         self.replay.update_priorities(self.loader._slots[k][1], G["learn_td"][v], step=True, deferred=True)
         self._learner_host()
+
+    def _learner_replay(self, v):
+        """replay learner graph v on the current stream.  Split (data-parallel) learner: every
+        bucket but the last is all-reduced on a side stream while the following part runs (the
+        merged heads' gradients, 95 % of the bytes, under the conv backward); the last one on
+        this stream; the final part (heads split + clip + Adam) waits for all of them."""
+        G = self._graphs
+        parts, buckets = G["learn"][v], G["buckets"][v]
+        if len(parts) == 1:
+            parts[0].replay()
+            return
+        hook = self.solver.grad_hook
+        cur = torch.cuda.current_stream(self.device)
+        if not hasattr(self, "_stream_comm"):
+            self._stream_comm = torch.cuda.Stream(self.device)
+        comm = self._stream_comm
+        for i, (g, bucket) in enumerate(zip(parts, buckets)):
+            g.replay()
+            if i + 1 < len(buckets):
+                comm.wait_stream(cur)
+                with torch.cuda.stream(comm):
+                    hook.reduce(bucket, key=("bucket", i))
+            else:
+                hook.reduce(bucket, key=("bucket", i))
+        cur.wait_stream(comm)
+        parts[-1].replay()
 
     def _actor_block_graph(self):
         G, act = self._graphs, self.actors
@@ -343,10 +373,7 @@ class ApexDQN:
         syncs = self.solver._target_syncs
         with torch.cuda.stream(B):
             B.wait_event(self._ev_sample)
-            G["learn"][v].replay()
-            if G["apply"]:
-                self.solver.grad_hook(self.solver._params, grads=G["grads"][v])  # RCCL all-reduce on B
-                G["apply"][v].replay()
+            self._learner_replay(v)  # on B
             self._learner_host()  # target sync / weights publish copies: on B
             self._ev_learn.record(B)
         self.loader.issue()  # sample-ahead into the other slot (on A, after this step's append)

@@ -12,43 +12,51 @@ import torch.distributed as dist
 
 
 class GradAllReduce:
-    """grad_hook for DQNSolver: average .grad over the process group in one collective.
+    """grad_hook for DQNSolver: average gradients over the process group, one collective per
+    bucket.
 
-    The flat buffer is allocated once; grads are copied in and out with two fused foreach
-    copies (no per-parameter collectives)."""
+    Each bucket (a fixed list of gradient tensors) gets one flat buffer, allocated once;
+    grads are copied in and out with two fused foreach copies (no per-parameter
+    collectives).  The eager learner reduces everything as one bucket; the captured learner
+    reduces the fully-connected gradients on a side stream while the conv backward runs
+    (ApexDQN._capture)."""
 
     def __init__(self, group=None):
         self.group = group
-        self._flat = None
-        self._views = None
+        self._flat = {}  # bucket key -> (flat buffer, views)
 
-    def _bind(self, params):
-        n = sum(p.numel() for p in params)
-        dev = params[0].device
-        self._flat = torch.empty(n, dtype=torch.float32, device=dev)
-        self._views, off = [], 0
-        for p in params:
-            self._views.append(self._flat[off: off + p.numel()].view_as(p))
-            off += p.numel()
+    def world(self):
+        return dist.get_world_size(self.group) if dist.is_initialized() else 1
 
-    def __call__(self, params, grads=None):
-        """grads: the gradient tensors to reduce (default: each parameter's .grad; a replayed
-        HIP graph passes the buffers its captured backward writes)"""
-        world = dist.get_world_size(self.group) if dist.is_initialized() else 1
+    def reduce(self, grads, key="all"):
+        """all-reduce-average the tensors in `grads` in place, on the current stream"""
+        world = self.world()
         if world == 1:
             return
-        if self._flat is None:
-            self._bind(params)
-        if grads is None:
-            grads = [p.grad for p in params]
-        torch._foreach_copy_(self._views, grads)
-        if self._flat.is_cuda and dist.get_backend(self.group) != "nccl":
+        ent = self._flat.get(key)
+        if ent is None or ent[1][0].shape != grads[0].shape or len(ent[1]) != len(grads):
+            n = sum(g.numel() for g in grads)
+            flat = torch.empty(n, dtype=torch.float32, device=grads[0].device)
+            views, off = [], 0
+            for g in grads:
+                views.append(flat[off: off + g.numel()].view_as(g))
+                off += g.numel()
+            ent = self._flat[key] = (flat, views)
+        flat, views = ent
+        torch._foreach_copy_(views, grads)
+        if flat.is_cuda and dist.get_backend(self.group) != "nccl":
             # gloo stages CUDA tensors through the host: hand it a finished buffer (its
             # own stream bookkeeping against a busy non-default stream stalls for seconds)
-            torch.cuda.current_stream(self._flat.device).synchronize()
-        dist.all_reduce(self._flat, op=dist.ReduceOp.SUM, group=self.group)
-        self._flat.div_(world)
-        torch._foreach_copy_(grads, self._views)
+            torch.cuda.current_stream(flat.device).synchronize()
+        dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
+        flat.div_(world)
+        torch._foreach_copy_(grads, views)
+
+    def __call__(self, params, grads=None):
+        """grads: the gradient tensors to reduce (default: each parameter's .grad)"""
+        if self.world() == 1:
+            return
+        self.reduce([p.grad for p in params] if grads is None else list(grads))
 
 
 def init_from_env(backend=None):

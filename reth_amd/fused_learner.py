@@ -56,10 +56,16 @@ def _nhwc(t):
     return t if t.is_contiguous(memory_format=torch.channels_last) else t.contiguous(memory_format=torch.channels_last)
 
 
-def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None):
+def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None, mid=None):
     """forward + TD + backward of one learner batch; sets .grad of every online parameter
     and returns (loss [], |td| [B]).  q1t: the target network's heads on s1 if precomputed
-    (DQNSolver.target_heads).  td_acc (nullable f32 device scalar): += mean |td|."""
+    (DQNSolver.target_heads).  td_acc (nullable f32 device scalar): += mean |td|.
+
+    mid (optional callable) is handed each gradient bucket as soon as it is final: first the
+    merged heads' [gw1, gb1, gw2, gb2] (before the conv backward), then the conv weights' and
+    biases' (before the heads are split back onto the branch parameters).  The data-parallel
+    capture ends a graph there, so the all-reduce of the first bucket overlaps the conv
+    backward; whatever mid's caller does to a bucket in place is what the parameters get."""
     from .solver import td_huber_forward
 
     net = solver.q_network
@@ -120,6 +126,8 @@ def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None):
         # FC1
         gfeat = torch.mm(gh1, w1)
         gw1 = torch.mm(gh1.t(), feat[:B])
+        if mid is not None:
+            mid([gw1, gb1, gw2, gb2])
         c3 = convs[-1]
         g = gfeat.view(B, ys[-1].shape[2], ys[-1].shape[3], c3.out_channels).permute(0, 3, 1, 2)
         grads = {}
@@ -149,6 +157,8 @@ def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None):
                                                             [0, 0], 1, [li > 0, True, False])
             grads[conv.weight], grads[conv.bias] = gw, db
             g = gx
+        if mid is not None:
+            mid([t for c in convs for t in (grads[c.weight], grads[c.bias])])
         # merged heads -> the eight branch parameters
         hp = net._head_params()
         hgrads = [torch.empty_like(p) for p in hp]

@@ -34,10 +34,8 @@ for step in "$@"; do
     dp2) RTH_SHARE_GPU=1 RTH_DIST_BACKEND=gloo run bench_dp2 900 python -m torch.distributed.run --nnodes=1 \
             --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 30 --warmup 10 \
             --capacity 100000 --no-cpu-baseline ${DP2_ARGS:-} ;;
-    dpprobe) RTH_DIST_BACKEND=gloo run dp_probe2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
-            --master-addr 127.0.0.1 --master-port 29518 scripts/dp_probe.py &&
-            RTH_DIST_BACKEND=gloo run dp_probe1 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
-            --master-addr 127.0.0.1 --master-port 29519 scripts/dp_probe.py ;;
+    dpt) run pytest_dp 900 python -u -m pytest tests/test_dp_gpu.py tests/test_apex_gpu.py tests/test_fused_learner_gpu.py \
+            -v -rf -x --timeout 300 --timeout-method thread ;;
     phases) run tree_phases 300 python scripts/probe_tree_phases.py ;;
     prio) for pr in 0 -1; do RTH_LEARNER_PRIORITY=$pr run bench_prio$pr 600 python bench.py --steps 200 --warmup 20 --no-cpu-baseline; done ;;
     convt) run pytest_conv 600 python -m pytest tests/test_conv_gpu.py -q -rf -x ;;

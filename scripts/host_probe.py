@@ -98,8 +98,8 @@ def main():
         print(f"alone: {label:40s} median {ts[len(ts) // 2]:8.1f} us  min {ts[0]:8.1f} us")
 
     k = ax.loader._pending[0]
-    alone("learner graph (pre, slot k)", lambda: G["learn"][("pre", k)].replay())
-    alone("learner graph (full, slot k)", lambda: G["learn"][("full", k)].replay())
+    alone("learner graph (pre, slot k)", lambda: ax._learner_replay(("pre", k)))
+    alone("learner graph (full, slot k)", lambda: ax._learner_replay(("full", k)))
     alone("actor graph (dedup)", lambda: G["act"]["dedup", ax.actors.pushes % 2].replay())
     alone("actor graph (full)", lambda: G["act"]["full", ax.actors.pushes % 2].replay())
     alone("target pass graph", lambda: G["tgt"][k].replay())

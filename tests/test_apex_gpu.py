@@ -64,9 +64,10 @@ def test_graph_replay_matches_eager(dev):
 
 
 def test_graph_split_learner_applies_its_own_gradients(dev):
-    """with a gradient all-reduce hook the learner is captured as compute + apply per batch
-    parity; each replayed apply must consume the gradients its own compute graph wrote
-    (Adam's exp_avg after one replayed step follows exactly those gradients)"""
+    """with a gradient all-reduce hook the learner is captured in parts cut at the gradient
+    buckets (merged heads | convs | heads split + clip + Adam) per variant and batch parity;
+    each replayed apply must consume the gradients its own compute parts wrote (Adam's
+    exp_avg after one replayed step follows exactly those gradients)"""
     from reth_amd.apex import ApexConfig, ApexDQN
 
     cfg = ApexConfig(n_actors=16, capacity=1024, batch_size=32, sample_start=64, seed=4, hip_graph=True,
@@ -75,7 +76,8 @@ def test_graph_split_learner_applies_its_own_gradients(dev):
     for _ in range(30):
         ax.iteration()
     G = ax._graphs
-    assert G is not None and len(G["apply"]) == 4  # (full | pre target pass) x batch parity
+    assert G is not None and len(G["learn"]) == 4  # (full | pre target pass) x batch parity
+    assert all(len(G["learn"][v]) == 3 and len(G["buckets"][v]) == 2 for v in G["learn"])
     ptrs = [{t.data_ptr() for t in G["grads"][v]} for v in G["grads"]]
     assert all(not (ptrs[i] & ptrs[j]) for i in range(4) for j in range(i))
     opt, params = ax.solver.optimizer, ax.solver._params

@@ -54,6 +54,28 @@ def test_conv_f32_nhwc(dev, geom, n):
     assert (got == 0).any() and (got > 0).any()  # ReLU active on both sides
 
 
+# the learner / target / actor batch sizes, and sizes whose tiles (16 output pixels) leave a
+# short partial last round on 256 CUs (several tiles per wave, the last round ragged)
+@pytest.mark.parametrize("gi,n", [(0, 41), (0, 72), (1, 204), (1, 1024), (2, 340), (2, 1024), (2, 512)])
+def test_conv_partial_rounds(dev, gi, n):
+    from reth_amd import _lib
+
+    geom = GEOMS[gi]
+    cin, h, wd, cout, k, s = geom
+    g = torch.Generator().manual_seed(1000 * gi + n)
+    x = torch.rand((n, cin, h, wd), generator=g) * 2 - 1
+    w = (torch.rand((cout, cin, k, k), generator=g) * 2 - 1) / np.sqrt(cin * k * k)
+    b = (torch.rand(cout, generator=g) * 2 - 1) * 0.1
+    xd = x.to(dev).contiguous(memory_format=torch.channels_last)
+    got = _run(_shape(_lib.CONV_F32_NHWC, *geom), xd, None, n, w, b, dev)
+    assert not torch.isnan(got).any()  # every output written
+    torch.testing.assert_close(got.double(), _ref(x, w, b, s), rtol=1e-5, atol=1e-5)
+    if gi == 0:  # the uint8 form of conv1
+        st = torch.randint(0, 256, (n, 4, 84, 84), dtype=torch.uint8, generator=g)
+        got = _run(_shape(_lib.CONV_U8_CHW, *geom), st.to(dev), None, n, w, b, dev)
+        torch.testing.assert_close(got.double(), _ref(st.double(), w, b, 4), rtol=1e-5, atol=5e-4)
+
+
 @pytest.mark.parametrize("n", [1, 5, 64])
 def test_conv1_u8_rows(dev, n):
     from reth_amd import _lib

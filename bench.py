@@ -259,6 +259,34 @@ def main():
         return e
 
     ax.loader.gather_timer = timer
+    spans = []
+    if os.environ.get("RTH_BENCH_SPAN"):  # diagnostics: the learner block's span on its stream
+        replay = ax._learner_replay
+
+        def timed_replay(v):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            replay(v)
+            b.record()
+            spans.append((a, b))
+        ax._learner_replay = timed_replay
+        ready = []  # when each batch's sample + target pass were done on the actor stream
+
+        class _Ready:  # ApexDQN._ev_sample with a timing twin
+            def __init__(self, ev):
+                self.ev = ev
+
+            def record(self, stream=None):
+                self.ev.record(stream)
+                t = torch.cuda.Event(enable_timing=True)
+                t.record(stream)
+                ready.append(t)
+
+            def wait(self, stream=None):
+                self.ev.wait(stream)
+
+        ax._ev_sample = _Ready(ax._ev_sample)
+    u0, e0 = ax.updates, ax.env_steps
     u0, e0 = ax.updates, ax.env_steps
     if world > 1:
         dist.barrier()
@@ -284,6 +312,16 @@ def main():
         c = torch.tensor([n_env, n_upd], dtype=torch.float64, device=dev)
         dist.all_reduce(c, op=dist.ReduceOp.SUM)
         n_env, n_upd = int(c[0]), int(c[1])
+    if spans:
+        busy = [a.elapsed_time(b) * 1e3 for a, b in spans]
+        gaps = [spans[i][1].elapsed_time(spans[i + 1][0]) * 1e3 for i in range(len(spans) - 1)]
+        print(f"learner block span {np.mean(busy):.1f} us (min {np.min(busy):.1f}), gap to the next "
+              f"{np.mean(gaps):.1f} us (median {np.median(gaps):.1f}), over {len(busy)} updates", file=sys.stderr)
+        if ready:  # actor stream's batch ready vs the learner block's previous end: > 0 = the learner waited
+            m = min(len(ready), len(spans) - 1)
+            late = [spans[i][1].elapsed_time(ready[i]) * 1e3 for i in range(m)]
+            print(f"next batch ready after the learner block ends: mean {np.mean(late):.1f} us, median "
+                  f"{np.median(late):.1f}, > 0 in {np.mean(np.array(late) > 0) * 100:.0f} % of updates", file=sys.stderr)
     gather_ms = [a.elapsed_time(b) for a, b in events]
     mean_gather_s = float(np.mean(gather_ms)) / 1e3
     bytes_launch = gather_bytes_per_row(cfg.hip_conv and cfg.channels_last) * cfg.batch_size

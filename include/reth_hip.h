@@ -376,6 +376,16 @@ int rth_conv_bias_relu(const rth_conv_shape *shape, const void *x_dev, const int
 int rth_conv_bias_relu_upto(const rth_conv_shape *shape, const void *x_dev, const int64_t *rows_dev, int64_t n_max,
                             const int64_t *n_dev, const float *packed_dev, const float *bias_dev, float *y_dev,
                             void *stream);
+/* Data gradient of conv2d(x, w) (the backward through conv3 / conv2 of the learner's torso,
+ * reth/reth/algorithm/dqn/dqn_solver.py:117 loss.backward() on dqn_model.py:14-20; replaces
+ * MIOpen's backward-data solver and its zero fill): gx = [n, hin, win, cin] fp32 NHWC from
+ * gy = [n, hout, wout, cout] fp32 NHWC and w = the OHWI weight (a channels_last Conv2d
+ * parameter, read directly: no packing).  Every element of gx is written exactly once.
+ * `shape` is the FORWARD convolution's (input RTH_CONV_F32_NHWC); built: conv2 and conv3 of
+ * the Nature-DQN torso (rth_conv_dgrad_supported).  16-byte aligned buffers. */
+int rth_conv_dgrad_supported(const rth_conv_shape *shape);
+int rth_conv_dgrad(const rth_conv_shape *shape, const float *gy_dev, int64_t n, const float *w_ohwi_dev,
+                   float *gx_dev, void *stream);
 /* Backward of relu(conv2d(x, w) + b) for the weights and bias, on uint8 stacks (conv1, whose
  * input needs no gradient): gy = (y > 0) ? g : 0, gw = sum over output pixels of gy times the
  * input window (OHWI [cout, kh, kw, cin], the layout of a channels_last weight), gb = sum of

@@ -367,6 +367,144 @@ static int cu_count() {
 }
 
 // ---------------------------------------------------------------------------------------
+// conv data gradient (the learner's backward through conv3 / conv2): gx = the transposed
+// convolution of gy with W, as an implicit GEMM per stride-parity class on the fp32 MFMA.
+// Input pixel (iy, ix) = (S*jy + py, S*jx + px) of class (py, px) only meets the taps
+// kh = py + S*dy, kw = px + S*dx (dy < KH/S, dx < KW/S), at output pixel (jy - dy, jx - dx):
+//   gx[b, iy, ix, ci] = sum_{dy, dx, co} gy[b, jy - dy, jx - dx, co] * W[co, kh, kw, ci]
+// (taps falling outside gy read zero).  Rows = the class's pixels (b, jy, jx), columns = ci,
+// K = (tap, co): every input pixel belongs to exactly one class and is written once, so
+// there is no zero fill and no atomic.  A workgroup serves one class and stages that class's
+// taps of W in LDS in MFMA fragment order (lane (n, q) holds co = 4q .. 4q+3 of column n);
+// the A operand is a float4 of gy's channels-last row, read straight from global memory.
+#ifndef DGRAD_WAVES
+#define DGRAD_WAVES 8
+#endif
+#ifndef DGRAD_D
+#define DGRAD_D 4  // input chunks in flight per wave (divides the chunk count)
+#endif
+
+template <int KH, int KW, int S, int CI, int CO, int HI, int WI>
+struct DgradGeom {
+  static constexpr int HO = (HI - KH) / S + 1, WO = (WI - KW) / S + 1;
+  static constexpr int TH = KH / S, TW = KW / S, TAPS = TH * TW, JH = HI / S, JW = WI / S;
+  static constexpr int CPT = CO / 16, G = TAPS * CPT, NB = CI / 16, LDS_F4 = G * NB * 64;
+  static_assert(KH % S == 0 && KW % S == 0 && HI % S == 0 && WI % S == 0, "stride must tile kernel and input");
+  static_assert(CI % 16 == 0 && CO % 16 == 0, "channels must be multiples of 16");
+  static_assert(G % DGRAD_D == 0, "prefetch depth must divide the chunks");
+};
+
+template <int KH, int KW, int S, int CI, int CO, int HI, int WI, int WAVES>
+__global__ __launch_bounds__(WAVES * 64) void k_conv_dgrad(const float *__restrict__ gy, int64_t n,
+                                                          const float *__restrict__ w, float *__restrict__ gx) {
+  using Gm = DgradGeom<KH, KW, S, CI, CO, HI, WI>;
+  constexpr int HO = Gm::HO, WO = Gm::WO, TW = Gm::TW, CPT = Gm::CPT, NB = Gm::NB;
+  constexpr int T = WAVES * 64, NCLS = S * S;
+  __shared__ f32x4 wl[Gm::LDS_F4];
+  const int wave = threadIdx.x / 64, lane = threadIdx.x % 64, q = lane >> 4, mr = lane & 15;
+  const int cls = blockIdx.x % NCLS, py = cls / S, px = cls % S;
+  const int64_t wg = blockIdx.x / NCLS, nwg = gridDim.x / NCLS;
+
+  // stage this class's taps: slot (g * NB + nb) * 64 + lane, chunk g = (tap, 16 co)
+  for (int sl = threadIdx.x; sl < Gm::LDS_F4; sl += T) {
+    const int ln = sl % 64, gn = sl / 64, nb = gn % NB, g = gn / NB;
+    const int t = g / CPT, co = (g % CPT) * 16 + 4 * (ln >> 4), ci = nb * 16 + (ln & 15);
+    const int kh = py + S * (t / TW), kw = px + S * (t % TW);
+    const float *src = w + ((int64_t)co * KH * KW + kh * KW + kw) * CI + ci;
+    constexpr int CS = KH * KW * CI;  // OHWI stride between consecutive co
+    wl[sl] = f32x4{src[0], src[CS], src[2 * CS], src[3 * CS]};
+  }
+  __syncthreads();
+
+  const int64_t PC = n * Gm::JH * Gm::JW, tiles = (PC + 15) / 16;
+  const f32x4 *wlane = wl + lane;
+  for (int64_t tile = wg * WAVES + wave; tile < tiles; tile += nwg * WAVES) {
+    int64_t p = tile * 16 + mr;
+    if (p >= PC) p = PC - 1;  // tail lanes compute a duplicate pixel, never stored
+    const int64_t b = p / (Gm::JH * Gm::JW);
+    const int r = (int)(p % (Gm::JH * Gm::JW)), jy = r / Gm::JW, jx = r % Gm::JW;
+    const float *gyb = gy + b * (HO * WO * CO) + 4 * q;
+    // chunk g = (tap g / CPT, 16 co from (g % CPT) * 16): this lane's float4 of gy (zero off the edge)
+    auto aload = [&](int g) {
+      const int t = g / CPT, oy = jy - t / TW, ox = jx - t % TW;
+      f32x4 a = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+      if (oy >= 0 && oy < HO && ox >= 0 && ox < WO)
+        a = *reinterpret_cast<const f32x4 *>(gyb + (oy * WO + ox) * CO + (g % CPT) * 16);
+      return a;
+    };
+    f32x4 acc[NB];
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) acc[nb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    f32x4 ar[DGRAD_D];  // input chunks in flight
+#pragma unroll
+    for (int d = 0; d < DGRAD_D; ++d) ar[d] = aload(d);
+#pragma unroll 1
+    for (int g0 = 0; g0 < Gm::G; g0 += DGRAD_D) {
+#pragma unroll
+      for (int d = 0; d < DGRAD_D; ++d) {
+        const int g = g0 + d;
+        f32x4 bf[NB];
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) bf[nb] = wlane[(g * NB + nb) * 64];
+#pragma unroll
+        for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+          for (int nb = 0; nb < NB; ++nb)
+            acc[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(ar[d][tt], bf[nb][tt], acc[nb], 0, 0, 0);
+        if (g + DGRAD_D < Gm::G) ar[d] = aload(g + DGRAD_D);
+      }
+    }
+    // C/D: lane holds column mr of rows 4q .. 4q+3
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t po = tile * 16 + 4 * q + i;
+      if (po < PC) {
+        const int64_t bo = po / (Gm::JH * Gm::JW);
+        const int ro = (int)(po % (Gm::JH * Gm::JW)), iy = S * (ro / Gm::JW) + py, ix = S * (ro % Gm::JW) + px;
+        float *dst = gx + ((bo * HI + iy) * WI + ix) * CI + mr;
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) dst[nb * 16] = acc[nb][i];
+      }
+    }
+  }
+}
+
+struct DgradLaunch {
+  const void *fn;
+  int waves, classes, per_cu, lds_bytes;
+  int jh, jw;
+};
+
+template <int KH, int KW, int S, int CI, int CO, int HI, int WI, int WAVES>
+static DgradLaunch dgrad_launch() {
+  using Gm = DgradGeom<KH, KW, S, CI, CO, HI, WI>;
+  DgradLaunch l{reinterpret_cast<const void *>(&k_conv_dgrad<KH, KW, S, CI, CO, HI, WI, WAVES>), WAVES, S * S, 1,
+                Gm::LDS_F4 * 16, Gm::JH, Gm::JW};
+  int blocks = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, l.fn, WAVES * 64, 0) == hipSuccess && blocks >= 1)
+    l.per_cu = blocks;
+  return l;
+}
+
+
+static bool find_dgrad(const rth_conv_shape &s, DgradLaunch *out) {
+  auto is = [&](int cin, int hin, int win, int cout, int kh, int kw, int st) {
+    return s.input == RTH_CONV_F32_NHWC && s.cin == cin && s.hin == hin && s.win == win && s.cout == cout &&
+           s.kh == kh && s.kw == kw && s.stride == st;
+  };
+  if (is(32, 20, 20, 64, 4, 4, 2)) {
+    static const DgradLaunch l = dgrad_launch<4, 4, 2, 32, 64, 20, 20, DGRAD_WAVES>();
+    *out = l;
+  } else if (is(64, 9, 9, 64, 3, 3, 1)) {
+    static const DgradLaunch l = dgrad_launch<3, 3, 1, 64, 64, 9, 9, DGRAD_WAVES>();
+    *out = l;
+  } else {
+    return false;
+  }
+  return true;
+}
+
+// ---------------------------------------------------------------------------------------
 // conv1 backward on uint8 stacks: gy = (y > 0) ? g : 0 (ReLU backward), gw = sum over output
 // pixels of gy (x) im2col(x), gb = sum of gy -- one pass over g, y and the stacks, MFMA
 // 32x32x2 f32 with the reduction over pixels (2 per MFMA).  The 32 x 256 weight gradient is
@@ -615,6 +753,30 @@ static int conv_bias_relu(const rth_conv_shape *shape, const void *x, const int6
   const int64_t resident = (int64_t)cu_count() * (l.per_cu < cap ? l.per_cu : cap);
   if (grid > resident) grid = resident;
   void *args[] = {(void *)&x, (void *)&rows, (void *)&n, (void *)&n_dev, (void *)&w, (void *)&bias, (void *)&y};
+  RTH_HIP(hipLaunchKernel(l.fn, dim3((unsigned)grid), dim3(l.waves * 64), args, 0, as_stream(stream)));
+  return RTH_OK;
+}
+
+int rth_conv_dgrad_supported(const rth_conv_shape *shape) {
+  DgradLaunch l;
+  return shape && find_dgrad(*shape, &l) ? 1 : 0;
+}
+
+int rth_conv_dgrad(const rth_conv_shape *shape, const float *gy, int64_t n, const float *w, float *gx, void *stream) {
+  RTH_REQUIRE(shape && gy && w && gx && n >= 0, "rth_conv_dgrad: NULL argument");
+  DgradLaunch l;
+  RTH_REQUIRE(find_dgrad(*shape, &l), "rth_conv_dgrad: geometry (%d x %d x %d -> %d, k %dx%d, stride %d) not built",
+              shape->cin, shape->hin, shape->win, shape->cout, shape->kh, shape->kw, shape->stride);
+  RTH_REQUIRE(((reinterpret_cast<uintptr_t>(gy) | reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(gx)) &
+               15) == 0,
+              "rth_conv_dgrad: misaligned buffer");
+  if (n == 0) return RTH_OK;
+  const int64_t tiles = (n * l.jh * l.jw + 15) / 16;
+  int64_t per_class = (tiles + l.waves - 1) / l.waves;
+  const int64_t resident = (int64_t)cu_count() * l.per_cu / l.classes;
+  if (per_class > resident) per_class = resident > 0 ? resident : 1;
+  const int64_t grid = per_class * l.classes;
+  void *args[] = {(void *)&gy, (void *)&n, (void *)&w, (void *)&gx};
   RTH_HIP(hipLaunchKernel(l.fn, dim3((unsigned)grid), dim3(l.waves * 64), args, 0, as_stream(stream)));
   return RTH_OK;
 }

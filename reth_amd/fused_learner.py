@@ -11,13 +11,15 @@ path of solver.py (compute_grads with torch.autograd), without the autograd engi
   TD        rth_td_huber on the raw heads -> |td|, loss, d(loss)/d(heads of s0), fused with
   backward  FC2 + threshold + both bias sums (rth_td_heads_backward; also the Trainer's
             mean |td|), FC1 as two GEMMs, conv3 / conv2 as rth_relu_bias_grad + MIOpen's data
-            and weight gradients, conv1 as rth_conv_relu_wgrad straight from the uint8 stacks
+            and weight gradients (conv2's data gradient optionally rth_conv_dgrad), conv1 as rth_conv_relu_wgrad straight from the uint8 stacks
             (f32 input: rth_relu_bias_grad + MIOpen's weight gradient), the merged-head
             gradients mapped back onto the eight branch parameters by rth_heads_split_grad.
 
 Only the first B rows of the 2B forward are differentiated: they are contiguous views
 (NHWC, batch-major), so the backward reads them in place.
 """
+import os
+
 import torch
 
 from . import _lib
@@ -25,6 +27,9 @@ from ._lib import call, ctypes, ptr, stream_ptr
 
 
 TD_HB_MAX = 16384  # rth_td_heads_backward keeps B * (A + 1) TD gradient rows in LDS
+# conv2's data gradient in rth_conv_dgrad instead of MIOpen: 49 vs 61 us alone, no faster in
+# the overlapped loop, so opt-in
+HIP_DGRAD = os.environ.get("RTH_HIP_DGRAD") is not None
 
 
 def eligible(net, s0, s1):
@@ -153,8 +158,12 @@ def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None, mid=No
             call("rth_relu_bias_grad", ptr(g), ptr(y), ptr(gy), ptr(db), ptr(net._ws[li]), nb * hh * ww, c, st)
             xin = ys[li - 1][:B] if li > 0 else x[:B]
             w = _nhwc(conv.weight.detach())
+            hip_dgrad = li == 1 and HIP_DGRAD and _lib.lib().rth_conv_dgrad_supported(ctypes.byref(shapes[li]))
             gx, gw, _ = torch.ops.aten.convolution_backward(gy, xin, w, None, list(conv.stride), [0, 0], [1, 1], False,
-                                                            [0, 0], 1, [li > 0, True, False])
+                                                            [0, 0], 1, [li > 0 and not hip_dgrad, True, False])
+            if hip_dgrad:  # data gradient in rth_conv_dgrad (no zero fill)
+                gx = torch.empty(xin.shape, dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
+                call("rth_conv_dgrad", ctypes.byref(shapes[li]), ptr(gy), B, ptr(w), ptr(gx), st)
             grads[conv.weight], grads[conv.bias] = gw, db
             g = gx
         if mid is not None:

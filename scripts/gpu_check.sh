@@ -39,6 +39,17 @@ for step in "$@"; do
     phases) run tree_phases 300 python scripts/probe_tree_phases.py ;;
     prio) for pr in 0 -1; do RTH_LEARNER_PRIORITY=$pr run bench_prio$pr 600 python bench.py --steps 200 --warmup 20 --no-cpu-baseline; done ;;
     convt) run pytest_conv 600 python -m pytest tests/test_conv_gpu.py -q -rf -x ;;
+    dgrad) run bench_dgrad 300 python scripts/bench_dgrad.py &&
+           for v in hip miopen hip2 miopen2; do
+             if [ "${v:0:3}" = hip ]; then export RTH_HIP_DGRAD=1; else unset RTH_HIP_DGRAD; fi
+             run bench_dgrad_$v 600 python bench.py --steps 400 --warmup 20 --no-cpu-baseline; done; unset RTH_HIP_DGRAD ;;
+    dgv) for v in build/variants/*.so; do b=$(basename $v .so); RTH_LIB_PATH=$PWD/$v run bench_dgrad_$b 300 python scripts/bench_dgrad.py; done ;;
+    span) for v in miopen; do
+             if [ $v = hip ]; then export RTH_HIP_DGRAD=1; else unset RTH_HIP_DGRAD; fi
+             RTH_BENCH_SPAN=1 run bench_span_$v 600 python bench.py --steps 400 --warmup 20 --no-cpu-baseline; done
+          unset RTH_HIP_DGRAD ;;
+    knobs) for w in 1 3 2; do RTH_CONV_WG_PER_CU=$w run bench_wpc$w 600 python bench.py --steps 400 --warmup 20 --no-cpu-baseline; done
+           for pr in 0 -1; do RTH_LEARNER_PRIORITY=$pr run bench_prio$pr 600 python bench.py --steps 400 --warmup 20 --no-cpu-baseline; done ;;
     convb) run bench_conv 300 python scripts/bench_conv.py ;;
     wgv) for v in build/variants/*.so; do b=$(basename $v .so); RTH_LIB_PATH=$PWD/$v run bench_wgrad_$b 300 python scripts/bench_wgrad.py; done ;;
     convwpc) for w in 1 2 3 4; do RTH_CONV_WG_PER_CU=$w run bench_conv_wpc$w 300 python scripts/bench_conv.py; done ;;

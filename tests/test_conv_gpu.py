@@ -277,3 +277,40 @@ def test_conv_upto_device_count(dev, count):
               cnt.data_ptr(), pk.data_ptr(), b.data_ptr(), part.data_ptr(), _lib.stream_ptr())
     assert torch.equal(part[:count], full[:count])
     assert bool(torch.isnan(part[count:]).all())
+
+
+@pytest.mark.parametrize("gi", [1, 2])
+@pytest.mark.parametrize("n", [1, 3, 37, 512])
+def test_conv_dgrad(dev, gi, n):
+    """rth_conv_dgrad (per stride-parity class implicit GEMM) against the float64 CPU data
+    gradient of conv2d; every element of gx written (no fill: NaN-initialised output)"""
+    from reth_amd import _lib
+
+    cin, h, wd, cout, k, s = GEOMS[gi]
+    shape = _shape(_lib.CONV_F32_NHWC, *GEOMS[gi])
+    assert _lib.lib().rth_conv_dgrad_supported(_lib.ctypes.byref(shape)) == 1
+    g = torch.Generator().manual_seed(31 * gi + n)
+    ho, wo = (h - k) // s + 1, (wd - k) // s + 1
+    gy = torch.rand((n, cout, ho, wo), generator=g) * 2 - 1
+    gy[gy < -0.3] = 0  # ReLU-masked, like the learner's
+    w = (torch.rand((cout, cin, k, k), generator=g) * 2 - 1) / np.sqrt(cin * k * k)
+    gyd = gy.to(dev).contiguous(memory_format=torch.channels_last)
+    wd_ = w.to(dev).contiguous(memory_format=torch.channels_last)
+    gx = torch.full((n, cin, h, wd), float("nan"), device=dev).contiguous(memory_format=torch.channels_last)
+    _lib.call("rth_conv_dgrad", _lib.ctypes.byref(shape), gyd.data_ptr(), n, wd_.data_ptr(), gx.data_ptr(),
+              _lib.stream_ptr())
+    want = torch.nn.grad.conv2d_input((n, cin, h, wd), w.double(), gy.double(), stride=s)
+    got = gx.cpu()
+    assert not torch.isnan(got).any()
+    torch.testing.assert_close(got.double(), want, rtol=1e-5, atol=1e-5)
+
+
+def test_conv_dgrad_unsupported(dev):
+    from reth_amd import _lib
+
+    conv1 = _shape(_lib.CONV_F32_NHWC, *GEOMS[0])
+    assert _lib.lib().rth_conv_dgrad_supported(_lib.ctypes.byref(conv1)) == 0
+    t = torch.zeros(16, device=dev)
+    with pytest.raises(_lib.RethHipError, match="not built"):
+        _lib.call("rth_conv_dgrad", _lib.ctypes.byref(conv1), t.data_ptr(), 1, t.data_ptr(), t.data_ptr(),
+                  _lib.stream_ptr())

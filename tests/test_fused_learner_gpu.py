@@ -50,9 +50,12 @@ def _solver(dev, seed):
                      channels_last=True)
 
 
-@pytest.mark.parametrize("u8,adjacent", [(True, True), (True, False), (False, False)])
-def test_fused_grads_match_autograd(dev, u8, adjacent):
+@pytest.mark.parametrize("u8,adjacent,hip_dgrad", [(True, True, False), (True, False, False), (False, False, False),
+                                                   (True, True, True)])
+def test_fused_grads_match_autograd(dev, u8, adjacent, hip_dgrad, monkeypatch):
     from reth_amd import fused_learner
+
+    monkeypatch.setattr(fused_learner, "HIP_DGRAD", hip_dgrad)  # conv2's data gradient in rth_conv_dgrad
 
     B = 64
     g = torch.Generator(device=dev).manual_seed(5)

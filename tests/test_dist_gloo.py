@@ -37,7 +37,12 @@ def _rank_main(rank, world, port, out_dir):
         opt.zero_grad()
         loss.backward()
         local = [p.grad.clone() for p in params]
-        hook(params)
+        if step == 1:  # the captured learner's form: two buckets (heads | rest), reduced separately
+            grads = [p.grad for p in params]
+            hook.reduce(grads[:2], key=("bucket", 0))
+            hook.reduce(grads[2:], key=("bucket", 1))
+        else:
+            hook(params)
         gathered = [[torch.empty_like(t) for _ in range(world)] for t in local]
         for t, buf in zip(local, gathered):
             dist.all_gather(buf, t)

@@ -125,9 +125,6 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__res
   };
   auto ld = [](const uint8_t *p) { return *reinterpret_cast<const Frag *>(p); };
 
-#ifdef CONV_PROBE_TIMING  // A/B probe only: per-wave timestamps written over y
-  const uint64_t pt0 = wall_clock64(), pc0 = clock64();
-#endif
   // wave slots are numbered SIMD-major (waves w and w + 4 of a workgroup share a SIMD): the
   // first gridDim.x * 4 slots put one wave on every SIMD, so a partial last round of tiles
   // lands on distinct SIMDs and no SIMD runs more than ceil(tiles / SIMDs) tiles
@@ -145,7 +142,6 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__res
 
   // stage the packed weights (rth_conv_pack: already in fragment order): a coalesced copy,
   // consecutive threads -> consecutive 16-byte LDS slots; all loads first
-#ifndef CONV_PROBE_NOSTAGE  // A/B probe only: LDS weights left uninitialised
   {
     constexpr int PER = (Gm::LDS_F4 + T - 1) / T;
     const f32x4 *wp = reinterpret_cast<const f32x4 *>(w);
@@ -161,15 +157,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__res
       if (sl < Gm::LDS_F4) wl[sl] = tmp[j];
     }
   }
-#endif
   __syncthreads();
-#ifdef CONV_PROBE_TIMING
-  const uint64_t pt1 = wall_clock64();
-  int ptiles = 0;
-#endif
-#ifdef CONV_PROBE_STAGE_ONLY  // A/B probe only: staging cost alone
-  if (tile < tiles) return;
-#endif
 
   float bl[NB];
 #pragma unroll
@@ -196,11 +184,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__res
         const int gb = g + 1 < G ? g + 1 : G - 1;
 #pragma unroll
         for (int nb = 0; nb < NB; ++nb) {
-#ifdef CONV_PROBE_NOB  // A/B probe only: no B reads in the loop (wrong results)
-          bnxt[nb] = bcur[nb] + (float)gb;
-#else
           bnxt[nb] = wlane[(gb * NB + nb) * 64];
-#endif
         }
         // keep the next chunk's B reads here, a whole chunk of MFMAs ahead of their use
         __builtin_amdgcn_sched_barrier(0);
@@ -216,9 +200,6 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__res
               acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bcur[nb][t], acc[mb][nb], 0, 0, 0);
           }
         const int ga = g + D;
-#ifdef CONV_PROBE_NOA  // A/B probe only: no input reads in the loop (wrong results)
-        if (ga >= G)
-#endif
 #pragma unroll
         for (int mb = 0; mb < MB; ++mb)
           ar[d][mb] = ld(ga < G ? cur[mb] + chunk_off(ga) : nxt[mb] + chunk_off(ga - G));
@@ -239,25 +220,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__res
       }
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb) cur[mb] = nxt[mb];
-#ifdef CONV_PROBE_TIMING
-    ++ptiles;
-#endif
   }
-#ifdef CONV_PROBE_TIMING
-  __syncthreads();  // all outputs of this workgroup are stored
-  if (lane == 0) {
-    uint64_t *rec = reinterpret_cast<uint64_t *>(y + ((P * COUT + 1) & ~(int64_t)1)) +
-                    ((int64_t)blockIdx.x * WAVES + wave) * 6;
-    rec[0] = pt0;
-    rec[1] = pt1;
-    rec[2] = wall_clock64();
-    rec[3] = clock64() - pc0;
-    rec[4] = ptiles;
-    uint32_t hw;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-    rec[5] = hw;
-  }
-#endif
 }
 
 // OHWI weights -> MFMA fragment order (the LDS image the conv kernel copies)

@@ -18,7 +18,6 @@ for step in "$@"; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 900 python bench.py ;;
     benchq) run bench_quick 600 python bench.py --steps 50 --warmup 10 --cpu-iters 5 ;;
-    debug) run debug 300 python scripts/debug_isw.py ;;
     variants)
       run bench_nchw 600 python bench.py --steps 100 --warmup 20 --no-cpu-baseline --nchw
       run bench_cl 600 python bench.py --steps 100 --warmup 20 --no-cpu-baseline
@@ -56,7 +55,6 @@ for step in "$@"; do
     convv) for v in build/variants/*.so; do b=$(basename $v .so); RTH_LIB_PATH=$PWD/$v run bench_conv_$b 300 python scripts/bench_conv.py; done ;;
     convprof) export TMPDIR=/tmp; run prof_conv 300 rocprofv3 --kernel-trace --output-format csv \
             -d "$PWD/gpurun_out/prof_conv" -o run -- python scripts/bench_conv.py ;;
-    convtime) RTH_LIB_PATH=$PWD/build/variants/timing.so run conv_timing 300 python scripts/conv_timing.py ;;
     convpmc) export TMPDIR=/tmp
          run pmc_conv_a 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
             SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT --kernel-trace --output-format csv \

@@ -305,6 +305,7 @@ int rth_td_huber(const float *q_s0_dev, const float *q_s1_online_dev, const floa
  * rth_relu_bias_grad: gy = (y > 0) ? g : 0 (threshold_backward) and db[c] = sum of gy over
  * the rows, deterministic; `workspace` holds rth_relu_bias_grad_workspace(C) bytes of
  * per-block partial sums (scratch, no initialisation).  C a power of 2 in [4, 256].
+ * db = NULL: only the slabs are written (finished by rth_conv_relu_wgrad_ex).
  * ---------------------------------------------------------------------------------- */
 int rth_bias_relu(float *y_dev, const float *bias_dev, int64_t rows, int32_t C, void *stream);
 int64_t rth_relu_bias_grad_workspace(int32_t C);
@@ -396,6 +397,18 @@ int64_t rth_conv_wgrad_workspace(const rth_conv_shape *shape);
 int rth_conv_relu_wgrad(const rth_conv_shape *shape, const void *x_dev, const int64_t *rows_dev, int64_t n,
                         const float *g_dev, const float *y_dev, float *gw_dev, float *gb_dev, void *workspace_dev,
                         void *stream);
+/* rth_conv_relu_wgrad that also finishes up to 4 deferred bias gradients in its reduce launch
+ * (one launch fewer per layer): each a rth_relu_bias_grad called with db = NULL on
+ * `workspace`, over `rows` rows of C channels, earlier on the same stream. */
+typedef struct rth_bias_deferred {
+  const void *workspace; /* the rth_relu_bias_grad workspace holding the slabs */
+  float *db;             /* [C] output */
+  int64_t rows;
+  int32_t C;
+} rth_bias_deferred;
+int rth_conv_relu_wgrad_ex(const rth_conv_shape *shape, const void *x_dev, const int64_t *rows_dev, int64_t n,
+                           const float *g_dev, const float *y_dev, float *gw_dev, float *gb_dev, void *workspace_dev,
+                           const rth_bias_deferred *deferred, int32_t ndeferred, void *stream);
 
 /* ------------------------------------------------------------------------------------
  * Atari observation preprocessing (reth/reth/env/util.py:121-209, 281-297): per actor, the

@@ -52,6 +52,13 @@ class ConvShape(ctypes.Structure):
                 ("kw", c_i32), ("stride", c_i32)]
 
 
+class BiasDeferred(ctypes.Structure):
+    """rth_bias_deferred (include/reth_hip.h): a bias gradient whose slabs rth_relu_bias_grad
+    wrote with db = NULL, finished by rth_conv_relu_wgrad_ex"""
+    _fields_ = [("workspace", ctypes.c_void_p), ("db", ctypes.c_void_p), ("rows", ctypes.c_int64),
+                ("C", ctypes.c_int32)]
+
+
 CONV_F32_NHWC, CONV_U8_CHW = 0, 1
 
 
@@ -130,6 +137,8 @@ SIGNATURES = {
     "rth_conv_wgrad_workspace": (c_i64, [ctypes.POINTER(ConvShape)]),
     "rth_conv_relu_wgrad": (c_i32, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
                                     c_vp]),
+    "rth_conv_relu_wgrad_ex": (c_i32, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                       c_vp, c_i32, c_vp]),
     "rth_conv_pack_many": (c_i32, [c_i32, ctypes.POINTER(ConvShape), ctypes.POINTER(c_vp), ctypes.POINTER(c_vp),
                                    c_vp]),
     "rth_conv_bias_relu": (c_i32, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),

@@ -25,6 +25,15 @@ __host__ __device__ __forceinline__ double radd(double a, double b) { return a +
 __host__ __device__ __forceinline__ double rsub(double a, double b) { return a - b; }
 __host__ __device__ __forceinline__ double rmul(double a, double b) { return a * b; }
 
+// rth_relu_bias_grad's partial-sum slabs: one per workgroup of kBiasThreads lanes, about 8
+// row sweeps each, at most kBiasSlabs (shared with the deferred combine in conv.hip)
+constexpr int kBiasThreads = 256, kBiasSlabs = 2048;
+__host__ __device__ inline int64_t bias_grad_slabs(int64_t rows, int C) {
+  const int64_t R = kBiasThreads / (C / 4);  // rows per block sweep
+  const int64_t want = (rows + 8 * R - 1) / (8 * R);
+  return want < kBiasSlabs ? want : kBiasSlabs;
+}
+
 void set_error(const char *fmt, ...);
 
 #define RTH_REQUIRE(cond, ...)          \

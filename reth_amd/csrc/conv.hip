@@ -574,11 +574,49 @@ __global__ __launch_bounds__(kWgWaves * 64) void k_conv_wgrad_u8(const uint8_t *
 // partials [blocks][COUT * K + COUT] (kk = kw * 32 + ci * KH + kh) -> gw OHWI, gb: 64
 // elements per workgroup, 4 groups of 64 lanes each summing a quarter of the partials
 // (coalesced rows), then the 4 group sums in fixed order
+// deferred bias gradients (rth_relu_bias_grad with db = NULL) finished by the extra
+// workgroups of this launch: db[c] = sum of the job's slabs in slab order, G = 256 / C lanes
+// per channel striding the slabs, then the G lane sums by a fixed LDS tree
+constexpr int kBiasJobsMax = 4;
+struct BiasJobs {
+  const float *part[kBiasJobsMax];
+  float *db[kBiasJobsMax];
+  int slabs[kBiasJobsMax], C[kBiasJobsMax];
+  int n;
+};
+
+__device__ void bias_job(const BiasJobs &bj, int j, float *red) {
+  const int C = bj.C[j], G = 256 / C, tid = threadIdx.x, c = tid % C;
+  const float *part = bj.part[j];
+  float s = 0.0f;
+  for (int k = tid / C; k < bj.slabs[j]; k += 8 * G) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int kk = k + u * G;
+      v[u] = kk < bj.slabs[j] ? part[(int64_t)kk * C + c] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s = radd(s, v[u]);
+  }
+  red[tid] = s;
+  __syncthreads();
+  for (int st = 128; st >= C; st >>= 1) {
+    if (tid < st) red[tid] = radd(red[tid], red[tid + st]);
+    __syncthreads();
+  }
+  if (tid < C) bj.db[j][tid] = red[tid];
+}
+
 template <int KH, int KW, int CIN, int COUT>
 __global__ __launch_bounds__(256) void k_wgrad_reduce(const float *__restrict__ partial, int blocks,
-                                                      float *__restrict__ gw, float *__restrict__ gb) {
-  constexpr int K = CIN * KH * KW, E = COUT * K + COUT;
+                                                      float *__restrict__ gw, float *__restrict__ gb, BiasJobs bj) {
+  constexpr int K = CIN * KH * KW, E = COUT * K + COUT, RB = (E + 63) / 64;
   __shared__ float part[4][64];
+  if ((int)blockIdx.x >= RB) {  // a deferred bias gradient
+    bias_job(bj, blockIdx.x - RB, &part[0][0]);
+    return;
+  }
   const int grp = threadIdx.x / 64, l = threadIdx.x % 64;
   const int e = blockIdx.x * 64 + l;
   const int per = (blocks + 3) / 4, w0 = grp * per, w1 = w0 + per < blocks ? w0 + per : blocks;
@@ -676,23 +714,44 @@ int64_t rth_conv_wgrad_workspace(const rth_conv_shape *shape) {
   return is_conv1_u8(shape) ? (int64_t)kWgBlocks * (32 * 256 + 32) * 4 : 0;
 }
 
-int rth_conv_relu_wgrad(const rth_conv_shape *shape, const void *x, const int64_t *rows, int64_t n, const float *g,
-                        const float *y, float *gw, float *gb, void *workspace, void *stream) {
+int rth_conv_relu_wgrad_ex(const rth_conv_shape *shape, const void *x, const int64_t *rows, int64_t n, const float *g,
+                           const float *y, float *gw, float *gb, void *workspace, const rth_bias_deferred *deferred,
+                           int32_t ndeferred, void *stream) {
   RTH_REQUIRE(shape && x && g && y && gw && gb && workspace && n >= 0, "rth_conv_relu_wgrad: NULL argument");
+  RTH_REQUIRE(ndeferred >= 0 && ndeferred <= kBiasJobsMax && (ndeferred == 0 || deferred),
+              "rth_conv_relu_wgrad_ex: %d deferred bias gradients (at most %d)", ndeferred, kBiasJobsMax);
+  BiasJobs bj{};
+  bj.n = ndeferred;
+  for (int j = 0; j < ndeferred; ++j) {
+    const rth_bias_deferred &d = deferred[j];
+    RTH_REQUIRE(d.workspace && d.db && d.C >= 4 && d.C <= 256 && (d.C & (d.C - 1)) == 0 && d.rows >= 0,
+                "rth_conv_relu_wgrad_ex: deferred bias gradient %d malformed", j);
+    bj.part[j] = static_cast<const float *>(d.workspace);
+    bj.db[j] = d.db;
+    bj.C[j] = d.C;
+    bj.slabs[j] = (int)bias_grad_slabs(d.rows, d.C);
+  }
   RTH_REQUIRE(is_conv1_u8(shape), "rth_conv_relu_wgrad: only the uint8 conv1 geometry (4x84x84 -> 32, k8 s4) is built");
   float *part = static_cast<float *>(workspace);
   if (n == 0) {
     RTH_HIP(hipMemsetAsync(gw, 0, 32 * 256 * 4, as_stream(stream)));
     RTH_HIP(hipMemsetAsync(gb, 0, 32 * 4, as_stream(stream)));
+    for (int j = 0; j < ndeferred; ++j)  // an empty batch: every layer's slabs are empty too
+      RTH_HIP(hipMemsetAsync(deferred[j].db, 0, deferred[j].C * 4, as_stream(stream)));
     return RTH_OK;
   }
   hipLaunchKernelGGL((k_conv_wgrad_u8<8, 8, 4, 4, 32, 84, 84>), dim3(kWgBlocks), dim3(kWgWaves * 64), 0,
                      as_stream(stream), static_cast<const uint8_t *>(x), rows, n, g, y, part);
   RTH_LAUNCHED();
-  hipLaunchKernelGGL((k_wgrad_reduce<8, 8, 4, 32>), dim3((32 * 256 + 32 + 63) / 64), dim3(256), 0,
-                     as_stream(stream), part, kWgBlocks, gw, gb);
+  hipLaunchKernelGGL((k_wgrad_reduce<8, 8, 4, 32>), dim3((32 * 256 + 32 + 63) / 64 + ndeferred), dim3(256), 0,
+                     as_stream(stream), part, kWgBlocks, gw, gb, bj);
   RTH_LAUNCHED();
   return RTH_OK;
+}
+
+int rth_conv_relu_wgrad(const rth_conv_shape *shape, const void *x, const int64_t *rows, int64_t n, const float *g,
+                        const float *y, float *gw, float *gb, void *workspace, void *stream) {
+  return rth_conv_relu_wgrad_ex(shape, x, rows, n, g, y, gw, gb, workspace, nullptr, 0, stream);
 }
 
 static int conv_bias_relu(const rth_conv_shape *shape, const void *x, const int64_t *rows, int64_t n,

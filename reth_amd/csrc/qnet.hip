@@ -16,8 +16,8 @@
 
 namespace rth {
 
-constexpr int kEpiThreads = 256;
-constexpr int kGradBlocks = 2048;  // max partial-sum slabs for the bias gradient
+constexpr int kEpiThreads = kBiasThreads;
+constexpr int kGradBlocks = kBiasSlabs;  // max partial-sum slabs for the bias gradient
 
 __device__ __forceinline__ float relu_f(float v) { return v < 0.0f ? 0.0f : v; }  // NaN passes, like torch
 
@@ -471,7 +471,7 @@ int64_t rth_relu_bias_grad_workspace(int32_t C) { return (int64_t)kGradBlocks * 
 
 int rth_relu_bias_grad(const float *g, const float *y, float *gy, float *db, void *workspace, int64_t rows,
                        int32_t C, void *stream) {
-  RTH_REQUIRE(g && y && gy && db && workspace, "rth_relu_bias_grad: NULL argument");
+  RTH_REQUIRE(g && y && gy && workspace, "rth_relu_bias_grad: NULL argument");
   RTH_REQUIRE(C >= 4 && C % 4 == 0 && C <= kEpiThreads * 4 && kEpiThreads % (C / 4) == 0,
               "rth_relu_bias_grad: channels %d unsupported (multiple of 4 dividing 1024)", C);
   RTH_REQUIRE((C & (C - 1)) == 0 && C <= kEpiThreads, "rth_relu_bias_grad: channels %d must be a power of 2 <= 256", C);
@@ -480,13 +480,12 @@ int rth_relu_bias_grad(const float *g, const float *y, float *gy, float *db, voi
               "rth_relu_bias_grad: buffers not 16-byte aligned");
   if (rows <= 0) return RTH_OK;
   float *part = static_cast<float *>(workspace);
-  const int64_t R = kEpiThreads / (C / 4);       // rows per block sweep
-  const int64_t want = (rows + 8 * R - 1) / (8 * R);  // ~8 sweeps per block
-  const int64_t blocks = want < kGradBlocks ? want : kGradBlocks;
+  const int64_t blocks = bias_grad_slabs(rows, C);
   hipLaunchKernelGGL(k_relu_bias_grad, dim3((unsigned)blocks), dim3(kEpiThreads), 0, as_stream(stream),
                      reinterpret_cast<const float4 *>(g), reinterpret_cast<const float4 *>(y),
                      reinterpret_cast<float4 *>(gy), part, rows, (int)C);
   RTH_LAUNCHED();
+  if (!db) return RTH_OK;  // deferred: rth_conv_relu_wgrad_ex finishes it
   hipLaunchKernelGGL(k_bias_grad_combine, dim3(1), dim3(kCombThreads), 0, as_stream(stream), part, (int)blocks, (int)C,
                      db);
   RTH_LAUNCHED();

@@ -136,26 +136,33 @@ def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None, mid=No
         c3 = convs[-1]
         g = gfeat.view(B, ys[-1].shape[2], ys[-1].shape[3], c3.out_channels).permute(0, 3, 1, 2)
         grads = {}
+        deferred = []  # bias gradients whose slabs wait for conv1's reduce launch
         if getattr(net, "_ws", None) is None or net._ws[0].device != x.device:
             net._ws = [torch.zeros(_lib.lib().rth_relu_bias_grad_workspace(m.out_channels), dtype=torch.uint8,
                                    device=x.device) for m in convs]
         for li in range(len(convs) - 1, -1, -1):
             conv, y = convs[li], ys[li][:B]
-            if li == 0 and u8:  # ReLU mask + weight/bias gradients from the stacks
+            if li == 0 and u8:  # ReLU mask + weight/bias gradients from the stacks, and the
+                # deferred conv3 / conv2 bias gradients in the same reduce launch
                 from .model import _wgrad_workspace
 
                 gw = torch.empty(conv.weight.shape, dtype=torch.float32, device=x.device,
                                  memory_format=torch.channels_last)
                 db = torch.empty(conv.out_channels, dtype=torch.float32, device=x.device)
-                call("rth_conv_relu_wgrad", ctypes.byref(shapes[0]), ptr(x), None, B, ptr(_nhwc(g)), ptr(y), ptr(gw),
-                     ptr(db), ptr(_wgrad_workspace(shapes[0], x.device)), st)
+                jobs = (_lib.BiasDeferred * max(len(deferred), 1))(*deferred)
+                call("rth_conv_relu_wgrad_ex", ctypes.byref(shapes[0]), ptr(x), None, B, ptr(_nhwc(g)), ptr(y),
+                     ptr(gw), ptr(db), ptr(_wgrad_workspace(shapes[0], x.device)), jobs, len(deferred), st)
                 grads[conv.weight], grads[conv.bias] = gw, db
                 break
             g = _nhwc(g)
             gy = torch.empty_like(y)
             nb, c, hh, ww = y.shape
             db = torch.empty(c, dtype=torch.float32, device=x.device)
-            call("rth_relu_bias_grad", ptr(g), ptr(y), ptr(gy), ptr(db), ptr(net._ws[li]), nb * hh * ww, c, st)
+            defer = u8  # finished by conv1's rth_conv_relu_wgrad_ex
+            call("rth_relu_bias_grad", ptr(g), ptr(y), ptr(gy), None if defer else ptr(db), ptr(net._ws[li]),
+                 nb * hh * ww, c, st)
+            if defer:
+                deferred.append(_lib.BiasDeferred(net._ws[li].data_ptr(), db.data_ptr(), nb * hh * ww, c))
             xin = ys[li - 1][:B] if li > 0 else x[:B]
             w = _nhwc(conv.weight.detach())
             hip_dgrad = li == 1 and HIP_DGRAD and _lib.lib().rth_conv_dgrad_supported(ctypes.byref(shapes[li]))

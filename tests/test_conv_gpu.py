@@ -314,3 +314,45 @@ def test_conv_dgrad_unsupported(dev):
     with pytest.raises(_lib.RethHipError, match="not built"):
         _lib.call("rth_conv_dgrad", _lib.ctypes.byref(conv1), t.data_ptr(), 1, t.data_ptr(), t.data_ptr(),
                   _lib.stream_ptr())
+
+
+def test_deferred_bias_grads_finished_by_conv1_reduce(dev):
+    """rth_relu_bias_grad with db = NULL leaves its slabs; rth_conv_relu_wgrad_ex finishes
+    them in conv1's reduce launch: the same bias gradients as the two-launch form (fixed
+    order, rtol 1e-5), conv1's own gradients unchanged"""
+    from reth_amd import _lib
+
+    g = torch.Generator(device=dev).manual_seed(11)
+    jobs, want, outs, keep = [], [], [], []
+    for rows, C in [(512 * 49, 64), (512 * 81, 64), (37, 64)]:
+        gg = torch.randn((rows, C), device=dev, generator=g)
+        yy = torch.randn((rows, C), device=dev, generator=g)
+        ws = torch.empty(_lib.lib().rth_relu_bias_grad_workspace(C), dtype=torch.uint8, device=dev)
+        gy, db = torch.empty_like(gg), torch.empty(C, device=dev)
+        _lib.call("rth_relu_bias_grad", gg.data_ptr(), yy.data_ptr(), gy.data_ptr(), db.data_ptr(), ws.data_ptr(),
+                  rows, C, _lib.stream_ptr())
+        want.append(db.clone())
+        gy2, db2 = torch.empty_like(gg), torch.full((C,), float("nan"), device=dev)
+        _lib.call("rth_relu_bias_grad", gg.data_ptr(), yy.data_ptr(), gy2.data_ptr(), None, ws.data_ptr(), rows, C,
+                  _lib.stream_ptr())
+        assert torch.equal(gy, gy2)
+        jobs.append(_lib.BiasDeferred(ws.data_ptr(), db2.data_ptr(), rows, C))
+        outs.append(db2)
+        keep += [gg, yy, ws, gy, gy2]
+    n = 5
+    shape = _shape(_lib.CONV_U8_CHW, *GEOMS[0])
+    st = torch.randint(0, 256, (n, 4, 84, 84), dtype=torch.uint8, device=dev, generator=g)
+    gc = torch.randn((n, 20, 20, 32), device=dev, generator=g)
+    yc = torch.randn((n, 20, 20, 32), device=dev, generator=g)
+    wsc = torch.empty(_lib.lib().rth_conv_wgrad_workspace(_lib.ctypes.byref(shape)), dtype=torch.uint8, device=dev)
+    res = []
+    for deferred in (False, True):
+        gw, gb = torch.empty((32, 8, 8, 4), device=dev), torch.empty(32, device=dev)
+        arr = (_lib.BiasDeferred * len(jobs))(*jobs)
+        _lib.call("rth_conv_relu_wgrad_ex", _lib.ctypes.byref(shape), st.data_ptr(), None, n, gc.data_ptr(),
+                  yc.data_ptr(), gw.data_ptr(), gb.data_ptr(), wsc.data_ptr(), arr if deferred else None,
+                  len(jobs) if deferred else 0, _lib.stream_ptr())
+        res.append((gw.clone(), gb.clone()))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    for got, ref in zip(outs, want):
+        torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-5)

@@ -245,7 +245,7 @@ def main():
                      actor_steps_per_update=args.actor_steps_per_update, seed=0,
                      channels_last=not args.nchw, conv_benchmark=not args.no_conv_benchmark,
                      hip_graph=not args.eager, hip_conv=not args.miopen_conv,
-                     extra={"learner_priority": int(os.environ.get("RTH_LEARNER_PRIORITY", "-1"))})
+                     extra={"learner_priority": int(os.environ.get("RTH_LEARNER_PRIORITY", "0"))})
     ax = ApexDQN(cfg, device=dev, rank=rank, world=world)
     ax.prefill(cfg.capacity)
     for _ in range(args.warmup):

@@ -357,8 +357,9 @@ class ApexDQN:
         G = self._graphs
         A = self._stream
         if not hasattr(self, "_stream_b"):
-            # the learner block is the longer of the two: give its stream the higher priority
-            self._stream_b = torch.cuda.Stream(self.device, priority=self.cfg.extra.get("learner_priority", -1))
+            # both streams at normal priority: a high-priority learner stream (-1) gives the same
+            # step time and a slower in-loop gather (40 vs 33-35 us)
+            self._stream_b = torch.cuda.Stream(self.device, priority=self.cfg.extra.get("learner_priority", 0))
             self._ev_learn = torch.cuda.Event()
             self._ev_sample = torch.cuda.Event()
             self._ev_sample.record(A)  # batch k was sampled on A before the first overlapped step

@@ -273,6 +273,11 @@ typedef struct rth_actor_tail_args {
   float gamma_n, p_reward, p_done;
   int32_t ring, A;
 } rth_actor_tail_args;
+/* The fused actor step's first launch (reth_amd/actors.py step_fused): *t_dev += 1 (the
+ * step counter rth_actor_tail's ε-greedy and env step read) and rows_out[i] = i * ring +
+ * cur_slot[i], the acting stacks' frame-ring rows the torso forward reads (i < n). */
+int rth_actor_prologue(int64_t *t_dev, const int64_t *cur_slot_dev, int64_t n, int64_t ring, int64_t *rows_out_dev,
+                       void *stream);
 int rth_actor_tail(rth_nstep *h, const rth_actor_tail_args *args, int32_t *emit_dev, int64_t *s0_out_dev,
                    int64_t *a_out_dev, float *r_out_dev, int64_t *s1_out_dev, float *done_out_dev, void *stream);
 /* initial reset of every actor into slot 1 (t = 0) */

@@ -109,6 +109,7 @@ SIGNATURES = {
     # actors
     "rth_eps_greedy": (c_i32, [c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_u64, c_u64, c_vp, c_vp, c_vp]),
     "rth_counter_add": (c_i32, [c_vp, c_i64, c_vp]),
+    "rth_actor_prologue": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp]),
     "rth_compact_flagged": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp]),
     "rth_actor_tail": (c_i32, [c_vp, ctypes.POINTER(ActorTailArgs), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "rth_nstep_create": (c_i32, [c_i64, c_i32, c_f64, c_i32, c_i32, ctypes.POINTER(c_vp)]),

@@ -216,11 +216,10 @@ class VecActors:
         elif dedup and not self.dedup_ready(q_net):
             raise RuntimeError("step_fused(dedup=True): the stack cache is not valid for the current weights")
         self.t += 1
-        call("rth_counter_add", ptr(self.t_dev), 1, s)
         N = self.N
         hip = self._hip_heads(q_net)
-        if hip:
-            torch.add(self.cur_slot, self._base, out=self.hx[:N])
+        if hip:  # step counter + acting rows (= cur_slot + _base) in one launch
+            call("rth_actor_prologue", ptr(self.t_dev), ptr(self.cur_slot), N, self.ring, ptr(self.hx), s)
             if dedup:  # acting + terminal stacks (device count); the rows' heads are in the cache
                 q = q_net.forward_heads(self.frames, rows=self.hx[:2 * N], n_dev=self.n_ext)
                 self._scatter_heads(q, self.hx, 2 * N)
@@ -243,6 +242,7 @@ class VecActors:
             self._bind_rows(cur)
             return (td_abs, prev) if p > self.n_step else (None, None)
         else:
+            call("rth_counter_add", ptr(self.t_dev), 1, s)
             torch.cat([self.current_obs_handles(), prev.s0, prev.s1], out=self.handles3)
             q, dueling = self._forward_stacks(q_net, self.handles3)
             q0, q1 = q[N:2 * N], q[2 * N:]

@@ -270,6 +270,15 @@ struct rth_nstep {
   NStepState st;
 };
 
+// the actor step's first launch: the step counter (what ε-greedy and the env step read) and
+// the acting stacks' frame-ring rows, rows[i] = i * ring + cur_slot[i] (was two launches)
+__global__ __launch_bounds__(256) void k_actor_prologue(int64_t *t, const int64_t *__restrict__ cur_slot, int64_t n,
+                                                        int64_t ring, int64_t *__restrict__ rows) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) rows[i] = i * ring + cur_slot[i];
+  if (i == 0) *t += 1;
+}
+
 extern "C" {
 
 int rth_eps_greedy(const float *q, int64_t N, int64_t A, int32_t dueling, const double *eps, const double *u,
@@ -364,6 +373,15 @@ int rth_compact_flagged(const float *flag, const int64_t *vals, int64_t n, int64
   RTH_REQUIRE(flag && vals && out && count_out && n >= 0 && cap >= 0, "rth_compact_flagged: bad arguments");
   hipLaunchKernelGGL(k_compact_flagged, dim3(1), dim3(kCompactThreads), 0, as_stream(stream), flag, vals, n, out, cap,
                      fill, base, count_out);
+  RTH_LAUNCHED();
+  return RTH_OK;
+}
+
+int rth_actor_prologue(int64_t *t_dev, const int64_t *cur_slot, int64_t n, int64_t ring, int64_t *rows_out,
+                       void *stream) {
+  RTH_REQUIRE(t_dev && cur_slot && rows_out && n >= 1 && ring >= 1, "rth_actor_prologue: bad arguments");
+  hipLaunchKernelGGL(k_actor_prologue, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), t_dev,
+                     cur_slot, n, ring, rows_out);
   RTH_LAUNCHED();
   return RTH_OK;
 }

@@ -16,10 +16,15 @@
 //   touched ancestor once, deepest level first, from final children" -- a touched node's
 //   last maintenance in the sequential loop happens after every change below it.  Untouched
 //   nodes must NOT be recomputed (the min() quirk, sumtree.py:11-19, seeds 1 for a maintained
-//   zero node).  One workgroup sorts each chunk of <= 4096 (index, position) keys in LDS by
-//   the index's left-aligned leaf position, which makes "ancestor at level L" monotone, so
-//   each distinct ancestor is maintained exactly once per level by the first key of its run.
-//   Chunks run in order, which keeps the sequential semantics for any n.
+//   zero node).  Two launches:
+//   * k_tree_update_sub: the levels S..maxd (S = 11), one workgroup per group of level-S
+//     subtrees (256 workgroups); each sorts its keys by left-aligned leaf position, loads
+//     everything its touched nodes need in one parallel pass, runs the level loop in LDS and
+//     stores the touched nodes once;
+//   * k_tree_update_top: the 2^S - 1 nodes above level S, dense in LDS, from the level-S
+//     sums the first launch left in memory.
+//   Any partition of the keys by subtree, and any split into launch-ordered rounds, gives the
+//   sequential result, so this is bit-identical to _numba_update for every n.
 #include <cmath>
 #include <cstdlib>
 
@@ -31,11 +36,7 @@ struct alignas(32) Node {
   double sum, val, mn, pad;
 };
 
-constexpr int kUpdThreads = 1024;
-constexpr int kUpdChunk = 4096;  // keys per LDS chunk (32 KiB)
-constexpr int kPosBits = 12;     // log2(kUpdChunk)
-constexpr int kDepthBits = 6;
-constexpr int64_t kMaxCapacity = int64_t(1) << 40;  // aligned(41) + depth(6) + pos(12) <= 64
+constexpr int64_t kMaxCapacity = int64_t(1) << 40;  // sort key: aligned(41) + depth(6) + slot(10) <= 64
 
 __host__ __device__ __forceinline__ int node_depth(int64_t i) { return 63 - __builtin_clzll((unsigned long long)(i + 1)); }
 
@@ -198,237 +199,427 @@ __device__ __forceinline__ double priority_of(const UpdArgs &a, double alpha, in
   return prio_value(a.td_abs, a.td_dtype, alpha, g);
 }
 
-__device__ __forceinline__ int64_t key_index(uint64_t key, int maxd) {
-  const int d = (int)((key >> kPosBits) & ((1u << kDepthBits) - 1));
-  const uint64_t aligned = key >> (kPosBits + kDepthBits);
-  return (int64_t)(aligned >> (maxd - d)) - 1;
-}
-
-// phase timestamps of the last k_tree_update (wall clock ticks; development aid, read by
-// rth_debug_tree_timing)
+// phase timestamps of the last update (wall clock ticks, 100 MHz; development aid, read by
+// rth_debug_tree_timing): [0] subtree pass start, [1] its end (workgroup 0), [2] top pass
+// start, [3] top pass after its loads and key scan, [4] top pass end
 __device__ long long g_upd_clock[8];
 
-// a workgroup barrier that orders LDS only (global stores are not waited for)
+// a workgroup barrier that orders LDS only (outstanding global stores are not waited for)
 __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-__global__ __launch_bounds__(kUpdThreads) void k_tree_update(UpdArgs a) {
-  __shared__ uint64_t keys[kUpdChunk];
-  __shared__ double res_sum[kUpdChunk], res_min[kUpdChunk];  // an owner's (sum, min) per level
+// ---------------------------------------------------------------- subtree pass
+// Workgroup w owns the level-S subtrees s with s % gridDim.x == w (consecutive FIFO slots
+// sit in consecutive subtrees, so an append spreads over workgroups).  It collects its keys
+// in launch order in rounds of <= R keys (rounds in order are the sequential semantics),
+// sorts a round by (left-aligned leaf position, depth, slot) -- so every subtree is a
+// contiguous run and a node precedes its own subtree -- and lays out one LDS entry per
+// touched (node, level): key j owns the levels [lt_j, d_j] of its path that it is the first
+// key of (a contiguous range: once an ancestor differs from key j-1's, every deeper one
+// does).  All the memory a round needs -- each touched node's val (or its new priority)
+// and its children's (sum, min) -- is loaded in one parallel pass; the level loop then runs
+// in LDS (each entry pushes its result into its parent's child slot), and the touched
+// nodes are stored at the end.  A round whose entries would not fit is re-gathered with
+// half the keys.
+constexpr int kSubThreads = 256;
+constexpr int kSubKeys = 1024;     // keys per round (10 slot bits in the sort key)
+constexpr int kSlotBits = 10;
+constexpr int kSubEntries = 2560;  // touched (node, level) entries per round
+constexpr int kSubGrid = 256;
+
+struct SubEnt {
+  double v, ls, lm, rs, rm;  // own val; left / right child (sum, min); ls/lm <- result
+};
+
+__device__ __forceinline__ int key_depth(uint64_t k) { return (int)((k >> kSlotBits) & 63); }
+__device__ __forceinline__ uint64_t key_aligned(uint64_t k) { return k >> (kSlotBits + 6); }
+
+// exclusive prefix sum over the workgroup (kSubThreads lanes); returns this lane's offset,
+// *total = the sum.  Uses wsum[kSubThreads / 64].
+__device__ __forceinline__ int wg_scan(int x, int *wsum, int *total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int incl = x;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  int base = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < kSubThreads / 64; ++k) {
+    const int s = wsum[k];
+    if (k < w) base += s;
+    tot += s;
+  }
+  __syncthreads();  // wsum may be reused right away
+  *total = tot;
+  return base + incl - x;
+}
+
+__global__ __launch_bounds__(kSubThreads) void k_tree_update_sub(UpdArgs a, int S) {
+  __shared__ uint64_t keys[kSubKeys];
+  __shared__ int32_t slot_g[kSubKeys];
+  __shared__ int32_t ebase[kSubKeys + 1];
+  __shared__ int32_t epar[kSubKeys];
+  __shared__ int8_t elt[kSubKeys];
+  __shared__ SubEnt ent[kSubEntries];
+  __shared__ int wsum[kSubThreads / 64];
+  __shared__ int s_next;
   const int tid = threadIdx.x;
   const int maxd = a.maxd;
-  if (tid == 0) g_upd_clock[0] = wall_clock64();
-  if (a.pre_step && tid == 0) a.st->sched_step += 1;
-  __syncthreads();
+  const int64_t cap = a.cap;
+  if (tid == 0 && blockIdx.x == 0) g_upd_clock[0] = wall_clock64();
   const int64_t fifo_start = a.st ? a.st->tail : a.fifo_start;
-  const double alpha = a.st ? sched_value(a.alpha_s, a.st->sched_step) : a.alpha;
+  const double alpha = a.st ? sched_value(a.alpha_s, a.st->sched_step + a.pre_step) : a.alpha;
   const int64_t N = a.pn + a.n;
-  for (int64_t cs = 0; cs < N; cs += kUpdChunk) {
-    const int m = (int)min<int64_t>(kUpdChunk, N - cs);
-    int P = 2;
-    while (P < m) P <<= 1;
-    if (P <= kUpdThreads) {
-      // One key per lane.  Issue the loads that warm the lines the level loop will touch
-      // (the children-pair line of the deepest kPre nodes on the key's path; the top of the
-      // tree is hot anyway) and keep them in flight through the sort, which synchronises on
-      // LDS only; consume them afterwards.
-      constexpr int kPre = 16;
-      double pre[kPre];
-      const int64_t id = tid < m ? upd_id(a, cs + tid, fifo_start) : -1;
-      {
-        int64_t x = (id >= 0 && id < a.cap) ? id : -1;
-#pragma unroll
-        for (int u = 0; u < kPre; ++u) {
-          pre[u] = 0.0;
-          if (x >= 0) {
-            const int64_t c = 2 * x + 1;
-            pre[u] = a.nd[(c < a.cap ? c : x) + 1].sum;
-            x = x ? (x - 1) / 2 : -1;
-          }
+  const int64_t top = (int64_t(1) << S) - 1;  // nodes above level S
+  const uint32_t G = gridDim.x;
+  int64_t scan = 0;
+  int R = kSubKeys;
+  while (scan < N) {
+    // ---- gather the round's keys (launch order) into slots 0..cnt-1
+    int cnt = 0;
+    int64_t pos = scan;
+    while (pos < N && cnt < R) {
+      const int64_t g = pos + tid;
+      bool mine = false;
+      if (g < N) {
+        const int64_t id = upd_id(a, g, fifo_start);
+        if (id >= top && id < cap) {
+          const int d = node_depth(id);
+          const int64_t sub = ((id + 1) >> (d - S)) - 1 - top;
+          mine = (uint32_t)(sub % G) == blockIdx.x;
         }
       }
-      if (tid == 0) g_upd_clock[1] = wall_clock64();
-      uint64_t key = ~0ull;
-      if (id >= 0 && id < a.cap) {
-        const int d = node_depth(id);
-        const uint64_t aligned = (uint64_t)(id + 1) << (maxd - d);
-        key = (((aligned << kDepthBits) | (uint64_t)d) << kPosBits) | (uint64_t)tid;
-      }
-      // bitonic sort of the workgroup's 1024 lanes (sentinels sort last): partners within a
-      // wave exchange through cross-lane shuffles, wider strides through LDS
-      for (int k = 2; k <= kUpdThreads; k <<= 1) {
-        for (int jj = k >> 1; jj > 0; jj >>= 1) {
-          uint64_t y;
-          if (jj < 64) {
-            y = __shfl_xor(key, jj, 64);
-          } else {
-            keys[tid] = key;
-            lds_barrier();
-            y = keys[tid ^ jj];
-            lds_barrier();
-          }
-          const bool up = (tid & k) == 0, lower = (tid & jj) == 0;
-          key = (lower == up) ? (key < y ? key : y) : (key < y ? y : key);
-        }
-      }
-      keys[tid] = key;
-      uint64_t acc = 0;
-#pragma unroll
-      for (int u = 0; u < kPre; ++u) acc ^= (uint64_t)__double_as_longlong(pre[u]);
-      if (acc == 0x9E3779B97F4A7C15ull) a.nd[0].pad = 1.0;  // record 0 is padding; keeps the loads
-      lds_barrier();
-    } else {
-      // several keys per lane: warm the lines first, then an LDS bitonic sort
-      uint64_t acc = 0;
-      for (int j = tid; j < m; j += kUpdThreads) {
-        int64_t x = upd_id(a, cs + j, fifo_start);
-        if (x < 0 || x >= a.cap) continue;
-        while (x >= 0) {
-          double v[8];
-#pragma unroll
-          for (int u = 0; u < 8; ++u) {
-            v[u] = 0.0;
-            if (x >= 0) {
-              const int64_t c = 2 * x + 1;
-              v[u] = a.nd[(c < a.cap ? c : x) + 1].sum;
-              x = x ? (x - 1) / 2 : -1;
-            }
-          }
-#pragma unroll
-          for (int u = 0; u < 8; ++u) acc ^= (uint64_t)__double_as_longlong(v[u]);
-        }
-      }
-      if (acc == 0x9E3779B97F4A7C15ull) a.nd[0].pad = 1.0;
-      if (tid == 0) g_upd_clock[1] = wall_clock64();
-      for (int j = tid; j < P; j += kUpdThreads) {
-        uint64_t key = ~0ull;
-        if (j < m) {
-          const int64_t id = upd_id(a, cs + j, fifo_start);
-          if (id >= 0 && id < a.cap) {
-            const int d = node_depth(id);
-            const uint64_t aligned = (uint64_t)(id + 1) << (maxd - d);
-            key = (((aligned << kDepthBits) | (uint64_t)d) << kPosBits) | (uint64_t)j;
-          }
-        }
-        keys[j] = key;
-      }
+      int total;
+      const int rank = wg_scan(mine ? 1 : 0, wsum, &total);
+      const int take = R - cnt;
+      if (tid == 0) s_next = -1;
       __syncthreads();
-      for (int k = 2; k <= P; k <<= 1) {  // bitonic sort, ascending
-        for (int jj = k >> 1; jj > 0; jj >>= 1) {
-          for (int i = tid; i < P; i += kUpdThreads) {
-            const int ixj = i ^ jj;
-            if (ixj > i) {
-              const uint64_t x = keys[i], y = keys[ixj];
-              const bool up = (i & k) == 0;
-              if ((x > y) == up) {
-                keys[i] = y;
-                keys[ixj] = x;
-              }
-            }
-          }
-          lds_barrier();
-        }
+      if (mine && rank < take) slot_g[cnt + rank] = (int32_t)g;
+      if (mine && rank == take) s_next = (int)(g - pos);  // first key left for the next round
+      __syncthreads();
+      if (total > take) {
+        cnt = R;
+        pos += s_next;
+      } else {
+        cnt += total;
+        pos += kSubThreads;
       }
     }
-    if (tid == 0) g_upd_clock[2] = wall_clock64();
-    // last writer of every index sets val (duplicates sort by position)
-    for (int j = tid; j < m; j += kUpdThreads) {
-      const uint64_t key = keys[j];
-      if (key == ~0ull) continue;
-      const int64_t id = key_index(key, maxd);
-      const bool last = (j == m - 1) || keys[j + 1] == ~0ull || key_index(keys[j + 1], maxd) != id;
-      if (last) {
-        const int64_t src = cs + (int64_t)(key & ((1u << kPosBits) - 1));
-        a.nd[id + 1].val = priority_of(a, alpha, src);
+    if (pos > N) pos = N;
+    if (cnt == 0) {
+      scan = pos;
+      continue;
+    }
+    // ---- sort keys (aligned, depth, slot)
+    int P = 1;
+    while (P < cnt) P <<= 1;
+    for (int j = tid; j < P; j += kSubThreads) {
+      uint64_t k = ~0ull;
+      if (j < cnt) {
+        const int64_t id = upd_id(a, slot_g[j], fifo_start);
+        const int d = node_depth(id);
+        const uint64_t al = (uint64_t)(id + 1) << (maxd - d);
+        k = (((al << 6) | (uint64_t)d) << kSlotBits) | (uint64_t)j;
+      }
+      keys[j] = k;
+    }
+    __syncthreads();
+    for (int k = 2; k <= P; k <<= 1) {
+      for (int jj = k >> 1; jj > 0; jj >>= 1) {
+        for (int i = tid; i < P / 2; i += kSubThreads) {
+          const int lo = 2 * jj * (i / jj) + (i % jj), hi = lo + jj;
+          const uint64_t x = keys[lo], y = keys[hi];
+          const bool up = (lo & k) == 0;
+          if ((x > y) == up) {
+            keys[lo] = y;
+            keys[hi] = x;
+          }
+        }
+        __syncthreads();
+      }
+    }
+    // ---- owned level ranges and entry bases (4 consecutive keys per lane)
+    int own[4];
+    int csum = 0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int j = 4 * tid + u;
+      own[u] = 0;
+      if (j < cnt) {
+        const uint64_t kj = keys[j];
+        const int dj = key_depth(kj);
+        int sh = 0;
+        if (j > 0) {
+          const uint64_t kp = keys[j - 1];
+          const uint64_t x = key_aligned(kj) ^ key_aligned(kp);
+          int topl = min(dj, key_depth(kp));
+          if (x) topl = min(topl, maxd - (63 - __builtin_clzll(x)) - 1);
+          sh = max(0, topl - S + 1);
+        }
+        elt[j] = (int8_t)(S + sh);
+        own[u] = max(0, dj - S + 1 - sh);
+        csum += own[u];
+      }
+    }
+    int E;
+    int off = wg_scan(csum, wsum, &E);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int j = 4 * tid + u;
+      if (j < cnt) ebase[j] = off;
+      off += own[u];
+    }
+    if (E > kSubEntries) {  // uniform: re-gather this round with fewer keys
+      R = max(1, cnt / 2);
+      __syncthreads();
+      continue;
+    }
+    __syncthreads();
+    // ---- parent entry of each key's shallowest owned entry (lower_bound of its owner)
+    for (int j = tid; j < cnt; j += kSubThreads) {
+      const uint64_t kj = keys[j];
+      const int lt = elt[j];
+      int p = -1;
+      if (ebase[j] != (j + 1 < cnt ? ebase[j + 1] : E) && lt > S) {
+        const int L = lt - 1;
+        const uint64_t al = (key_aligned(kj) >> (maxd - L)) << (maxd - L);
+        const uint64_t want = ((al << 6) | (uint64_t)L) << kSlotBits;
+        int lo = 0, hi = j;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (keys[mid] < want) lo = mid + 1; else hi = mid;
+        }
+        p = ebase[lo] + (L - elt[lo]);
+      }
+      epar[j] = p;
+    }
+    // ---- load every entry's inputs (one parallel pass; LDS stores cannot alias the loads)
+    for (int j = tid; j < cnt; j += kSubThreads) {
+      const uint64_t kj = keys[j];
+      const int dj = key_depth(kj), lt = elt[j];
+      const uint64_t al = key_aligned(kj);
+      const int e0 = ebase[j];
+      for (int L0 = lt; L0 <= dj; L0 += 4) {
+        double v[4], ls[4], lm[4], rs[4], rm[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int L = L0 + u;
+          v[u] = ls[u] = lm[u] = rs[u] = rm[u] = 0.0;
+          if (L <= dj) {
+            const int64_t node = (int64_t)(al >> (maxd - L)) - 1, l = 2 * node + 1;
+            if (L < dj) v[u] = a.nd[node + 1].val;
+            if (l < cap) {
+              ls[u] = a.nd[l + 1].sum;
+              lm[u] = a.nd[l + 1].mn;
+            }
+            if (l + 1 < cap) {
+              rs[u] = a.nd[l + 2].sum;
+              rm[u] = a.nd[l + 2].mn;
+            }
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int L = L0 + u;
+          if (L <= dj) ent[e0 + L - lt] = SubEnt{v[u], ls[u], lm[u], rs[u], rm[u]};
+        }
+      }
+      if (e0 + (dj - lt) >= e0 && dj >= lt) {  // j owns its own node: the last duplicate's priority
+        int last = j;
+        while (last + 1 < cnt && (keys[last + 1] >> kSlotBits) == (kj >> kSlotBits)) ++last;
+        ent[e0 + dj - lt].v = priority_of(a, alpha, slot_g[keys[last] & ((1u << kSlotBits) - 1)]);
       }
     }
     __syncthreads();
-    if (tid == 0) g_upd_clock[3] = wall_clock64();
-    // Touched ancestors, deepest level first; the first key of each ancestor's run maintains
-    // it (_numba_maintain_node).  A touched child's (sum, min) comes from LDS -- its owner
-    // at the level below stored it in res[owner] -- found by binary search in the sorted
-    // keys (the child's subtree is a key range); only untouched children and the node's own
-    // val are read from memory (issued before the search), so a level costs one overlapped
-    // L2 round trip and an LDS-only barrier instead of store -> barrier -> load.
-    for (int L = maxd; L >= 0; --L) {
-      for (int j = tid; j < m; j += kUpdThreads) {
-        const uint64_t key = keys[j];
-        if (key == ~0ull) continue;
-        const int d = (int)((key >> kPosBits) & ((1u << kDepthBits) - 1));
-        if (d < L) continue;
-        const uint64_t aligned = key >> (kPosBits + kDepthBits);
-        const uint64_t anc = aligned >> (maxd - L);  // 1-based heap index
-        if (j > 0) {
-          const uint64_t pk = keys[j - 1];
-          const int pd = (int)((pk >> kPosBits) & ((1u << kDepthBits) - 1));
-          if (pd >= L && ((pk >> (kPosBits + kDepthBits)) >> (maxd - L)) == anc) continue;
+    if (tid == 0 && blockIdx.x == 0) g_upd_clock[1] = wall_clock64();
+    // ---- levels, deepest first (_numba_maintain_node on every touched node, once)
+    for (int L = maxd; L >= S; --L) {
+      for (int j = tid; j < cnt; j += kSubThreads) {
+        const int lt = elt[j];
+        const uint64_t kj = keys[j];
+        if (L < lt || L > key_depth(kj)) continue;
+        const int e = ebase[j] + L - lt;
+        const SubEnt x = ent[e];
+        const int64_t node = (int64_t)(key_aligned(kj) >> (maxd - L)) - 1, l = 2 * node + 1;
+        double sm = x.v, mn = (x.v != 0.0) ? x.v : 1.0;
+        if (l < cap) {
+          sm = radd(sm, x.ls);
+          if (x.lm != 0.0) mn = (x.lm < mn) ? x.lm : mn;
         }
-        const int64_t node = (int64_t)anc - 1, l = 2 * node + 1, r = l + 1;
-        const double v = a.nd[node + 1].val;
-        double ls = 0.0, lm = 0.0, rs = 0.0, rm = 0.0;
-        if (l < a.cap) {
-          ls = a.nd[l + 1].sum;
-          lm = a.nd[l + 1].mn;
+        if (l + 1 < cap) {
+          sm = radd(sm, x.rs);
+          if (x.rm != 0.0) mn = (x.rm < mn) ? x.rm : mn;
         }
-        if (r < a.cap) {
-          rs = a.nd[r + 1].sum;
-          rm = a.nd[r + 1].mn;
-        }
-        if (L < maxd) {
-          // the node's subtree is the key range of aligned values [al, al + 2 half): its own
-          // keys first (depth L), then the left child's range, then the right child's; a
-          // child's owner at level L + 1 is the first key of its range
-          const uint64_t al = anc << (maxd - L), half = uint64_t(1) << (maxd - L - 1);
-          constexpr int kSh = kPosBits + kDepthBits;
-          int k1 = j;  // skip the node's own keys (duplicates of it)
-          while (k1 < m && (keys[k1] >> kSh) == al && (int)((keys[k1] >> kPosBits) & ((1u << kDepthBits) - 1)) == L)
-            ++k1;
-          if (k1 < m && keys[k1] != ~0ull && (keys[k1] >> kSh) < al + half) {
-            ls = res_sum[k1];
-            lm = res_min[k1];
-          }
-          // right child: first key at or after k1 with aligned >= al + half (galloping)
-          const uint64_t rc_al = al + half;
-          int lo = k1, hi = k1, b = 1;
-          while (hi < m && (keys[hi] >> kSh) < rc_al) {
-            lo = hi + 1;
-            hi = k1 + b;
-            b <<= 1;
-          }
-          if (hi > m) hi = m;
-          while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if ((keys[mid] >> kSh) < rc_al) lo = mid + 1; else hi = mid;
-          }
-          if (lo < m && keys[lo] != ~0ull && (keys[lo] >> kSh) < al + 2 * half) {
-            rs = res_sum[lo];
-            rm = res_min[lo];
+        ent[e].ls = sm;
+        ent[e].lm = mn;
+        if (L > S) {
+          const int p = L > lt ? e - 1 : epar[j];
+          if (node & 1) {
+            ent[p].ls = sm;
+            ent[p].lm = mn;
+          } else {
+            ent[p].rs = sm;
+            ent[p].rm = mn;
           }
         }
-        double sm = v;  // sum[i] = val[i] + sum[l] + sum[r]; min seeded 1 for a zero val
-        double mn = (v != 0.0) ? v : 1.0;
-        if (l < a.cap) {
-          sm = radd(sm, ls);
-          if (lm != 0.0) mn = (lm < mn) ? lm : mn;
-        }
-        if (r < a.cap) {
-          sm = radd(sm, rs);
-          if (rm != 0.0) mn = (rm < mn) ? rm : mn;
-        }
-        a.nd[node + 1].sum = sm;
-        a.nd[node + 1].mn = mn;
-        res_sum[j] = sm;
-        res_min[j] = mn;
       }
       lds_barrier();
     }
-    __syncthreads();  // the next chunk reads this chunk's stores from memory
-    if (tid == 0) g_upd_clock[4] = wall_clock64();
+    // ---- store the touched nodes
+    for (int j = tid; j < cnt; j += kSubThreads) {
+      const uint64_t kj = keys[j];
+      const int dj = key_depth(kj), lt = elt[j];
+      const uint64_t al = key_aligned(kj);
+      for (int L = lt; L <= dj; ++L) {
+        const SubEnt x = ent[ebase[j] + L - lt];
+        const int64_t node = (int64_t)(al >> (maxd - L)) - 1;
+        a.nd[node + 1].sum = x.ls;
+        a.nd[node + 1].mn = x.lm;
+        if (L == dj) a.nd[node + 1].val = x.v;
+      }
+    }
+    __syncthreads();  // the next round reads these stores (same workgroup)
+    scan = pos;
+    R = kSubKeys;
   }
-  if (a.post_tail && tid == 0) a.st->tail = (fifo_start + a.n) % a.cap;  // all reads of tail are done
+  if (tid == 0 && blockIdx.x == 0) g_upd_clock[1] = wall_clock64();
+}
+
+// ---------------------------------------------------------------- top pass
+// The levels above S (at most 2^11 - 1 nodes) as a dense bottom-up pass in LDS, after the
+// subtree pass: every node's (val, sum, min) and level S's (sum, min) are loaded in one
+// coalesced sweep; a node is maintained iff it is a key or a child was (touched
+// ancestors only -- the min() quirk); last writer wins among keys above S.
+constexpr int kTopS = 11;
+constexpr int kTopThreads = 1024;
+constexpr int kTopNodes = (1 << kTopS) - 1;
+
+__global__ __launch_bounds__(kTopThreads) void k_tree_update_top(UpdArgs a, int S) {
+  __shared__ double tv[kTopNodes], tsum[kTopNodes], tmin[kTopNodes];
+  __shared__ double bsum[kTopNodes + 1], bmin[kTopNodes + 1];
+  __shared__ int32_t win[kTopNodes];
+  __shared__ uint8_t ttop[kTopNodes], tbot[kTopNodes + 1];
+  const int tid = threadIdx.x;
+  const int64_t cap = a.cap;
+  if (tid == 0) g_upd_clock[2] = wall_clock64();
+  const int64_t fifo_start = a.st ? a.st->tail : a.fifo_start;
+  const double alpha = a.st ? sched_value(a.alpha_s, a.st->sched_step + a.pre_step) : a.alpha;
+  const int64_t N = a.pn + a.n;
+  const int ntop = (1 << S) - 1;
+  for (int i = tid; i < ntop; i += kTopThreads) {
+    double v = 0.0, s = 0.0, m = 0.0;
+    if (i < cap) {
+      const Node x = a.nd[i + 1];
+      v = x.val;
+      s = x.sum;
+      m = x.mn;
+    }
+    tv[i] = v;
+    tsum[i] = s;
+    tmin[i] = m;
+    win[i] = -1;
+    ttop[i] = 0;
+  }
+  for (int k = tid; k <= ntop; k += kTopThreads) {
+    const int64_t node = ntop + k;
+    double s = 0.0, m = 0.0;
+    if (node < cap) {
+      s = a.nd[node + 1].sum;
+      m = a.nd[node + 1].mn;
+    }
+    bsum[k] = s;
+    bmin[k] = m;
+    tbot[k] = 0;
+  }
+  __syncthreads();
+  for (int64_t g = tid; g < N; g += kTopThreads) {
+    const int64_t id = upd_id(a, g, fifo_start);
+    if (id < 0 || id >= cap) continue;
+    if (id < ntop) {
+      atomicMax(&win[id], (int32_t)g);
+    } else {
+      const int d = node_depth(id);
+      tbot[((id + 1) >> (d - S)) - 1 - ntop] = 1;
+    }
+  }
+  __syncthreads();
+  if (tid == 0) g_upd_clock[3] = wall_clock64();
+  for (int i = tid; i < ntop; i += kTopThreads) {
+    const int w = win[i];
+    if (w >= 0) {
+      const double v = priority_of(a, alpha, w);
+      tv[i] = v;
+      ttop[i] = 1;
+      a.nd[i + 1].val = v;
+    }
+  }
+  __syncthreads();
+  for (int L = S - 1; L >= 0; --L) {
+    const int first = (1 << L) - 1;
+    for (int i = first + tid; i < 2 * first + 1 && i < cap; i += kTopThreads) {
+      const int64_t l = 2 * (int64_t)i + 1, r = l + 1;
+      const bool bottom = (L == S - 1);
+      bool t = ttop[i] != 0;
+      double ls = 0.0, lm = 0.0, rs = 0.0, rm = 0.0;
+      if (l < cap) {
+        if (bottom) {
+          t |= tbot[l - ntop] != 0;
+          ls = bsum[l - ntop];
+          lm = bmin[l - ntop];
+        } else {
+          t |= ttop[l] != 0;
+          ls = tsum[l];
+          lm = tmin[l];
+        }
+      }
+      if (r < cap) {
+        if (bottom) {
+          t |= tbot[r - ntop] != 0;
+          rs = bsum[r - ntop];
+          rm = bmin[r - ntop];
+        } else {
+          t |= ttop[r] != 0;
+          rs = tsum[r];
+          rm = tmin[r];
+        }
+      }
+      if (!t) continue;
+      const double v = tv[i];
+      double sm = v, mn = (v != 0.0) ? v : 1.0;
+      if (l < cap) {
+        sm = radd(sm, ls);
+        if (lm != 0.0) mn = (lm < mn) ? lm : mn;
+      }
+      if (r < cap) {
+        sm = radd(sm, rs);
+        if (rm != 0.0) mn = (rm < mn) ? rm : mn;
+      }
+      tsum[i] = sm;
+      tmin[i] = mn;
+      ttop[i] = 1;
+    }
+    lds_barrier();  // LDS only: no wait for global stores inside the level loop
+  }
+  for (int i = tid; i < ntop && i < cap; i += kTopThreads) {
+    if (ttop[i]) {
+      a.nd[i + 1].sum = tsum[i];
+      a.nd[i + 1].mn = tmin[i];
+    }
+  }
+  if (tid == 0) {
+    if (a.st) {
+      if (a.pre_step) a.st->sched_step += 1;
+      if (a.post_tail) a.st->tail = (fifo_start + a.n) % cap;  // every read of tail is done
+    }
+    g_upd_clock[4] = wall_clock64();
+  }
 }
 
 // ------------------------------------------------------------------ find / sample
@@ -527,7 +718,15 @@ int tree_update_impl(rth_sumtree *t, const int64_t *idx, int64_t fifo_start, con
     a.pre_step = pend->step ? 1 : 0;
   }
   a.post_tail = post_tail;
-  hipLaunchKernelGGL(k_tree_update, dim3(1), dim3(kUpdThreads), 0, s, a);
+  RTH_REQUIRE(a.pn + a.n < (int64_t(1) << 31), "tree update: at most 2^31 - 1 keys per call");
+  const int S = t->maxd + 1 < kTopS ? t->maxd + 1 : kTopS;
+  if (t->maxd >= S && a.pn + a.n > 0) {  // levels S..maxd: one workgroup per group of subtrees
+    const int64_t nsub = int64_t(1) << S;
+    hipLaunchKernelGGL(k_tree_update_sub, dim3((unsigned)(nsub < kSubGrid ? nsub : kSubGrid)), dim3(kSubThreads), 0,
+                       s, a, S);
+    RTH_LAUNCHED();
+  }
+  hipLaunchKernelGGL(k_tree_update_top, dim3(1), dim3(kTopThreads), 0, s, a, S);
   RTH_LAUNCHED();
   return RTH_OK;
 }

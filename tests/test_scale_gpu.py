@@ -177,7 +177,9 @@ def _check_apex(ax, cfg, iters, prefill):
     assert steps == ax.updates and ax.trainer.cur_step == ax.updates
     assert ax.env_steps == cfg.n_actors * iters
     emitted = cfg.n_actors * (iters - cfg.n_step - 1)  # fused actor: rows land one step later
-    assert cnt == prefill + emitted and tail == (prefill + emitted) % cfg.capacity
+    # cnt counts every sampler message's rows: appends and priority updates (sampler_loop.py)
+    assert cnt == prefill + emitted + cfg.batch_size * ax.updates
+    assert tail == (prefill + emitted) % cfg.capacity and size == min(prefill + emitted, cfg.capacity)
     assert ax.updates >= iters - 6 and calls == ax.updates + 1
     assert all(torch.isfinite(p).all() for p in ax.solver.q_network.parameters())
     act = ax.actors

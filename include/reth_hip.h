@@ -44,7 +44,7 @@ extern "C" {
 const char *rth_last_error(void);
 /* development aid: wall-clock ticks (100 MHz) at the phase boundaries of the last tree
  * update launch (start, prefetch, sort, priorities written, levels done) */
-int rth_debug_tree_timing(long long *out5);
+int rth_debug_tree_timing(long long *out9);
 /* library build/ABI version (major*10000 + minor*100 + patch) */
 int rth_version(void);
 

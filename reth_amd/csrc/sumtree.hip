@@ -177,7 +177,20 @@ struct UpdArgs {
   int32_t pre_step;   // st->sched_step += 1 before alpha is read (its step=True on_step)
   int64_t pn;
   int32_t post_tail;  // st->tail += n after every read of it (the append's FIFO advance)
+  int32_t timing;     // record phase timestamps in g_upd_clock (RTH_TREE_TIMING=1)
 };
+
+// FIFO start and alpha of a launch: both replay-state words loaded together
+__device__ __forceinline__ void upd_prologue(const UpdArgs &a, int64_t *fifo_start, double *alpha) {
+  if (a.st) {
+    const int64_t tail = a.st->tail, step = a.st->sched_step;
+    *fifo_start = tail;
+    *alpha = sched_value(a.alpha_s, step + a.pre_step);
+  } else {
+    *fifo_start = a.fifo_start;
+    *alpha = a.alpha;
+  }
+}
 
 __device__ __forceinline__ double prio_value(const void *td, int32_t dt, double alpha, int64_t i) {
   if (dt == RTH_PRIO_RAW) return static_cast<const double *>(td)[i];
@@ -200,9 +213,10 @@ __device__ __forceinline__ double priority_of(const UpdArgs &a, double alpha, in
 }
 
 // phase timestamps of the last update (wall clock ticks, 100 MHz; development aid, read by
-// rth_debug_tree_timing): [0] subtree pass start, [1] its end (workgroup 0), [2] top pass
-// start, [3] top pass after its loads and key scan, [4] top pass end
-__device__ long long g_upd_clock[8];
+// rth_debug_tree_timing): [0] subtree pass start (workgroup 0), [1] workgroup 0 after its
+// loads, [2] top pass start, [3] top pass after its loads and key scan, [4] top pass end,
+// [5] the subtree pass's last workgroup end (a running max: reset by the reader)
+__device__ long long g_upd_clock[10];
 
 // a workgroup barrier that orders LDS only (outstanding global stores are not waited for)
 __device__ __forceinline__ void lds_barrier() {
@@ -223,12 +237,15 @@ __device__ __forceinline__ void lds_barrier() {
 // and its children's (sum, min) -- is loaded in one parallel pass; the level loop then runs
 // in LDS (each entry pushes its result into its parent's child slot), and the touched
 // nodes are stored at the end.  A round whose entries would not fit is re-gathered with
-// half the keys.
+// proportionally fewer keys.
+// LDS stays under 16 KB so a workgroup fits on a CU beside the learner's conv2/conv3 tiles
+// (131 / 147 KB of the 160 KB): the update runs concurrently with the learner stream.
 constexpr int kSubThreads = 256;
-constexpr int kSubKeys = 1024;     // keys per round (10 slot bits in the sort key)
+constexpr int kSubKeys = 256;      // keys per round (one per lane; 10 slot bits in the sort key)
 constexpr int kSlotBits = 10;
-constexpr int kSubEntries = 2560;  // touched (node, level) entries per round
+constexpr int kSubEntries = 256;   // touched (node, level) entries per round
 constexpr int kSubGrid = 256;
+static_assert(kSubKeys == kSubThreads, "one key per lane in the rank sort / ownership scan");
 
 struct SubEnt {
   double v, ls, lm, rs, rm;  // own val; left / right child (sum, min); ls/lm <- result
@@ -263,53 +280,68 @@ __device__ __forceinline__ int wg_scan(int x, int *wsum, int *total) {
 
 __global__ __launch_bounds__(kSubThreads) void k_tree_update_sub(UpdArgs a, int S) {
   __shared__ uint64_t keys[kSubKeys];
+  __shared__ uint64_t scratch[kSubKeys];  // unsorted keys, then ebase[]
   __shared__ int32_t slot_g[kSubKeys];
-  __shared__ int32_t ebase[kSubKeys + 1];
-  __shared__ int32_t epar[kSubKeys];
   __shared__ int8_t elt[kSubKeys];
   __shared__ SubEnt ent[kSubEntries];
   __shared__ int wsum[kSubThreads / 64];
   __shared__ int s_next;
+  int32_t *const ebase = reinterpret_cast<int32_t *>(scratch);  // kSubKeys + 1
   const int tid = threadIdx.x;
   const int maxd = a.maxd;
   const int64_t cap = a.cap;
-  if (tid == 0 && blockIdx.x == 0) g_upd_clock[0] = wall_clock64();
-  const int64_t fifo_start = a.st ? a.st->tail : a.fifo_start;
-  const double alpha = a.st ? sched_value(a.alpha_s, a.st->sched_step + a.pre_step) : a.alpha;
+  if (a.timing && tid == 0 && blockIdx.x == 0) g_upd_clock[0] = wall_clock64();
+  int64_t fifo_start;
+  double alpha;
+  upd_prologue(a, &fifo_start, &alpha);
   const int64_t N = a.pn + a.n;
   const int64_t top = (int64_t(1) << S) - 1;  // nodes above level S
   const uint32_t G = gridDim.x;
+  auto is_mine = [&](int64_t g, uint64_t *key) -> bool {
+    if (g >= N) return false;
+    const int64_t id = upd_id(a, g, fifo_start);
+    if (id < top || id >= cap) return false;
+    const int d = node_depth(id);
+    const int64_t sub = ((id + 1) >> (d - S)) - 1 - top;
+    const uint64_t al = (uint64_t)(id + 1) << (maxd - d);
+    *key = ((al << 6) | (uint64_t)d) << kSlotBits;
+    return (uint32_t)(sub % G) == blockIdx.x;
+  };
   int64_t scan = 0;
   int R = kSubKeys;
   while (scan < N) {
-    // ---- gather the round's keys (launch order) into slots 0..cnt-1
+    // ---- gather the round's keys (launch order) into slots 0..cnt-1; the ids of kGatherU
+    // consecutive 256-key windows are loaded together
+    constexpr int kGatherU = 4;
     int cnt = 0;
     int64_t pos = scan;
     while (pos < N && cnt < R) {
-      const int64_t g = pos + tid;
-      bool mine = false;
-      if (g < N) {
-        const int64_t id = upd_id(a, g, fifo_start);
-        if (id >= top && id < cap) {
-          const int d = node_depth(id);
-          const int64_t sub = ((id + 1) >> (d - S)) - 1 - top;
-          mine = (uint32_t)(sub % G) == blockIdx.x;
+      bool mine[kGatherU];
+      uint64_t kk[kGatherU];  // the sort key's (aligned, depth) part
+#pragma unroll
+      for (int u = 0; u < kGatherU; ++u) mine[u] = is_mine(pos + u * kSubThreads + tid, &kk[u]);
+#pragma unroll
+      for (int u = 0; u < kGatherU; ++u) {
+        if (pos >= N || cnt >= R) break;  // uniform
+        const int64_t g = pos + tid;
+        int total;
+        const int rank = wg_scan(mine[u] ? 1 : 0, wsum, &total);
+        const int take = R - cnt;
+        if (tid == 0) s_next = -1;
+        __syncthreads();
+        if (mine[u] && rank < take) {
+          slot_g[cnt + rank] = (int32_t)g;
+          scratch[cnt + rank] = kk[u] | (uint64_t)(cnt + rank);
         }
-      }
-      int total;
-      const int rank = wg_scan(mine ? 1 : 0, wsum, &total);
-      const int take = R - cnt;
-      if (tid == 0) s_next = -1;
-      __syncthreads();
-      if (mine && rank < take) slot_g[cnt + rank] = (int32_t)g;
-      if (mine && rank == take) s_next = (int)(g - pos);  // first key left for the next round
-      __syncthreads();
-      if (total > take) {
-        cnt = R;
-        pos += s_next;
-      } else {
-        cnt += total;
-        pos += kSubThreads;
+        if (mine[u] && rank == take) s_next = (int)(g - pos);  // first key left for the next round
+        __syncthreads();
+        if (total > take) {
+          cnt = R;
+          pos += s_next;
+        } else {
+          cnt += total;
+          pos += kSubThreads;
+        }
       }
     }
     if (pos > N) pos = N;
@@ -317,104 +349,74 @@ __global__ __launch_bounds__(kSubThreads) void k_tree_update_sub(UpdArgs a, int 
       scan = pos;
       continue;
     }
-    // ---- sort keys (aligned, depth, slot)
-    int P = 1;
-    while (P < cnt) P <<= 1;
-    for (int j = tid; j < P; j += kSubThreads) {
-      uint64_t k = ~0ull;
-      if (j < cnt) {
-        const int64_t id = upd_id(a, slot_g[j], fifo_start);
-        const int d = node_depth(id);
-        const uint64_t al = (uint64_t)(id + 1) << (maxd - d);
-        k = (((al << 6) | (uint64_t)d) << kSlotBits) | (uint64_t)j;
-      }
-      keys[j] = k;
+    // ---- sort keys (aligned, depth, slot; built by the gather): rank of each key among the round's
+    const int j = tid;
+    const uint64_t kmine = j < cnt ? scratch[j] : ~0ull;
+    if (j < cnt) {
+      int r = 0;
+      for (int i = 0; i < cnt; ++i) r += scratch[i] < kmine;
+      keys[r] = kmine;
     }
-    __syncthreads();
-    for (int k = 2; k <= P; k <<= 1) {
-      for (int jj = k >> 1; jj > 0; jj >>= 1) {
-        for (int i = tid; i < P / 2; i += kSubThreads) {
-          const int lo = 2 * jj * (i / jj) + (i % jj), hi = lo + jj;
-          const uint64_t x = keys[lo], y = keys[hi];
-          const bool up = (lo & k) == 0;
-          if ((x > y) == up) {
-            keys[lo] = y;
-            keys[hi] = x;
-          }
-        }
-        __syncthreads();
+    __syncthreads();  // scratch is reused as ebase / epar below
+    // ---- owned level range and entry base of key j
+    int own = 0;
+    if (j < cnt) {
+      const uint64_t kj = keys[j];
+      const int dj = key_depth(kj);
+      int sh = 0;
+      if (j > 0) {
+        const uint64_t kp = keys[j - 1];
+        const uint64_t x = key_aligned(kj) ^ key_aligned(kp);
+        int topl = min(dj, key_depth(kp));
+        if (x) topl = min(topl, maxd - (63 - __builtin_clzll(x)) - 1);
+        sh = max(0, topl - S + 1);
       }
-    }
-    // ---- owned level ranges and entry bases (4 consecutive keys per lane)
-    int own[4];
-    int csum = 0;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int j = 4 * tid + u;
-      own[u] = 0;
-      if (j < cnt) {
-        const uint64_t kj = keys[j];
-        const int dj = key_depth(kj);
-        int sh = 0;
-        if (j > 0) {
-          const uint64_t kp = keys[j - 1];
-          const uint64_t x = key_aligned(kj) ^ key_aligned(kp);
-          int topl = min(dj, key_depth(kp));
-          if (x) topl = min(topl, maxd - (63 - __builtin_clzll(x)) - 1);
-          sh = max(0, topl - S + 1);
-        }
-        elt[j] = (int8_t)(S + sh);
-        own[u] = max(0, dj - S + 1 - sh);
-        csum += own[u];
-      }
+      elt[j] = (int8_t)(S + sh);
+      own = max(0, dj - S + 1 - sh);
     }
     int E;
-    int off = wg_scan(csum, wsum, &E);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int j = 4 * tid + u;
-      if (j < cnt) ebase[j] = off;
-      off += own[u];
-    }
-    if (E > kSubEntries) {  // uniform: re-gather this round with fewer keys
-      R = max(1, cnt / 2);
+    const int off = wg_scan(own, wsum, &E);
+    if (j < cnt) ebase[j] = off;
+    if (E > kSubEntries) {  // uniform: re-gather this round with proportionally fewer keys
+      R = max(1, (int)((int64_t)cnt * kSubEntries / E));
       __syncthreads();
       continue;
     }
     __syncthreads();
+    const uint64_t k_j = j < cnt ? keys[j] : 0;
+    const int lt_j = j < cnt ? elt[j] : 0;
+    const int d_j = j < cnt ? key_depth(k_j) : -1;
+    const int eb_j = j < cnt ? ebase[j] : 0;
+    const uint64_t al_j = key_aligned(k_j);
     // ---- parent entry of each key's shallowest owned entry (lower_bound of its owner)
-    for (int j = tid; j < cnt; j += kSubThreads) {
-      const uint64_t kj = keys[j];
-      const int lt = elt[j];
-      int p = -1;
-      if (ebase[j] != (j + 1 < cnt ? ebase[j + 1] : E) && lt > S) {
-        const int L = lt - 1;
-        const uint64_t al = (key_aligned(kj) >> (maxd - L)) << (maxd - L);
-        const uint64_t want = ((al << 6) | (uint64_t)L) << kSlotBits;
-        int lo = 0, hi = j;
-        while (lo < hi) {
-          const int mid = (lo + hi) >> 1;
-          if (keys[mid] < want) lo = mid + 1; else hi = mid;
-        }
-        p = ebase[lo] + (L - elt[lo]);
+    int ep_j = -1;
+    if (j < cnt && own > 0 && lt_j > S) {
+      const int L = lt_j - 1;
+      const uint64_t al = (al_j >> (maxd - L)) << (maxd - L);
+      const uint64_t want = ((al << 6) | (uint64_t)L) << kSlotBits;
+      int lo = 0, hi = j;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (keys[mid] < want) lo = mid + 1; else hi = mid;
       }
-      epar[j] = p;
+      ep_j = ebase[lo] + (L - elt[lo]);
     }
-    // ---- load every entry's inputs (one parallel pass; LDS stores cannot alias the loads)
-    for (int j = tid; j < cnt; j += kSubThreads) {
-      const uint64_t kj = keys[j];
-      const int dj = key_depth(kj), lt = elt[j];
-      const uint64_t al = key_aligned(kj);
-      const int e0 = ebase[j];
-      for (int L0 = lt; L0 <= dj; L0 += 4) {
-        double v[4], ls[4], lm[4], rs[4], rm[4];
+    // ---- load every entry's inputs (all of a key's levels in flight together; LDS stores
+    // cannot alias the loads) and its own node's new priority (the last duplicate's)
+    if (j < cnt && own > 0) {
+      int last = j;
+      while (last + 1 < cnt && (keys[last + 1] >> kSlotBits) == (k_j >> kSlotBits)) ++last;
+      const int64_t g_last = slot_g[keys[last] & ((1u << kSlotBits) - 1)];
+      constexpr int kLoadU = 12;
+      for (int L0 = lt_j; L0 <= d_j; L0 += kLoadU) {
+        double v[kLoadU], ls[kLoadU], lm[kLoadU], rs[kLoadU], rm[kLoadU];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < kLoadU; ++u) {
           const int L = L0 + u;
           v[u] = ls[u] = lm[u] = rs[u] = rm[u] = 0.0;
-          if (L <= dj) {
-            const int64_t node = (int64_t)(al >> (maxd - L)) - 1, l = 2 * node + 1;
-            if (L < dj) v[u] = a.nd[node + 1].val;
+          if (L <= d_j) {
+            const int64_t node = (int64_t)(al_j >> (maxd - L)) - 1, l = 2 * node + 1;
+            if (L < d_j) v[u] = a.nd[node + 1].val;
             if (l < cap) {
               ls[u] = a.nd[l + 1].sum;
               lm[u] = a.nd[l + 1].mn;
@@ -425,29 +427,22 @@ __global__ __launch_bounds__(kSubThreads) void k_tree_update_sub(UpdArgs a, int 
             }
           }
         }
+        const double pv = L0 + kLoadU > d_j ? priority_of(a, alpha, g_last) : 0.0;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < kLoadU; ++u) {
           const int L = L0 + u;
-          if (L <= dj) ent[e0 + L - lt] = SubEnt{v[u], ls[u], lm[u], rs[u], rm[u]};
+          if (L <= d_j) ent[eb_j + L - lt_j] = SubEnt{L == d_j ? pv : v[u], ls[u], lm[u], rs[u], rm[u]};
         }
-      }
-      if (e0 + (dj - lt) >= e0 && dj >= lt) {  // j owns its own node: the last duplicate's priority
-        int last = j;
-        while (last + 1 < cnt && (keys[last + 1] >> kSlotBits) == (kj >> kSlotBits)) ++last;
-        ent[e0 + dj - lt].v = priority_of(a, alpha, slot_g[keys[last] & ((1u << kSlotBits) - 1)]);
       }
     }
     __syncthreads();
-    if (tid == 0 && blockIdx.x == 0) g_upd_clock[1] = wall_clock64();
+    if (a.timing && tid == 0 && blockIdx.x == 0) g_upd_clock[1] = wall_clock64();
     // ---- levels, deepest first (_numba_maintain_node on every touched node, once)
     for (int L = maxd; L >= S; --L) {
-      for (int j = tid; j < cnt; j += kSubThreads) {
-        const int lt = elt[j];
-        const uint64_t kj = keys[j];
-        if (L < lt || L > key_depth(kj)) continue;
-        const int e = ebase[j] + L - lt;
+      if (L >= lt_j && L <= d_j) {
+        const int e = eb_j + L - lt_j;
         const SubEnt x = ent[e];
-        const int64_t node = (int64_t)(key_aligned(kj) >> (maxd - L)) - 1, l = 2 * node + 1;
+        const int64_t node = (int64_t)(al_j >> (maxd - L)) - 1, l = 2 * node + 1;
         double sm = x.v, mn = (x.v != 0.0) ? x.v : 1.0;
         if (l < cap) {
           sm = radd(sm, x.ls);
@@ -460,7 +455,7 @@ __global__ __launch_bounds__(kSubThreads) void k_tree_update_sub(UpdArgs a, int 
         ent[e].ls = sm;
         ent[e].lm = mn;
         if (L > S) {
-          const int p = L > lt ? e - 1 : epar[j];
+          const int p = L > lt_j ? e - 1 : ep_j;
           if (node & 1) {
             ent[p].ls = sm;
             ent[p].lm = mn;
@@ -473,152 +468,264 @@ __global__ __launch_bounds__(kSubThreads) void k_tree_update_sub(UpdArgs a, int 
       lds_barrier();
     }
     // ---- store the touched nodes
-    for (int j = tid; j < cnt; j += kSubThreads) {
-      const uint64_t kj = keys[j];
-      const int dj = key_depth(kj), lt = elt[j];
-      const uint64_t al = key_aligned(kj);
-      for (int L = lt; L <= dj; ++L) {
-        const SubEnt x = ent[ebase[j] + L - lt];
-        const int64_t node = (int64_t)(al >> (maxd - L)) - 1;
+    if (j < cnt) {
+      for (int L = lt_j; L <= d_j; ++L) {
+        const SubEnt x = ent[eb_j + L - lt_j];
+        const int64_t node = (int64_t)(al_j >> (maxd - L)) - 1;
         a.nd[node + 1].sum = x.ls;
         a.nd[node + 1].mn = x.lm;
-        if (L == dj) a.nd[node + 1].val = x.v;
+        if (L == d_j) a.nd[node + 1].val = x.v;
       }
     }
     __syncthreads();  // the next round reads these stores (same workgroup)
     scan = pos;
     R = kSubKeys;
   }
-  if (tid == 0 && blockIdx.x == 0) g_upd_clock[1] = wall_clock64();
+  if (a.timing && tid == 0) atomicMax(&g_upd_clock[5], wall_clock64());  // the last workgroup's end
 }
 
 // ---------------------------------------------------------------- top pass
-// The levels above S (at most 2^11 - 1 nodes) as a dense bottom-up pass in LDS, after the
-// subtree pass: every node's (val, sum, min) and level S's (sum, min) are loaded in one
-// coalesced sweep; a node is maintained iff it is a key or a child was (touched
-// ancestors only -- the min() quirk); last writer wins among keys above S.
-constexpr int kTopS = 11;
-constexpr int kTopThreads = 1024;
+// The levels above S (at most 2^11 - 1 nodes), after the subtree pass, in one 256-lane
+// workgroup (small enough to be dispatched beside the learner's kernels).  Lane t owns
+// nodes 4t..4t+3 of level S-1, 2t..2t+1 of level S-2 and t of level S-3 (their children
+// are its own), and above that the ancestors whose leftmost level-(S-3) descendant is its
+// node: node j of level k belongs to lane j << (S-3-k), so a node's left child is on its
+// own lane and its right child 2^(S-4-k) lanes up -- a wavefront shuffle below 64 lanes,
+// a word in LDS above.  Every record is loaded in one parallel pass; a node is maintained
+// iff it is a key or a child was (touched ancestors only -- the min() quirk); last writer
+// wins among keys above S.  LDS: the key winners and the touched level-S bitmap (~8.5 KB).
+constexpr int kTopS = 11;          // S = max(kTopMinS, min(maxd + 1, kTopS))
+constexpr int kTopMinS = 3;        // levels S-1 .. S-3 are lane-local (absent nodes: i >= cap)
+constexpr int kTopThreads = 1 << (kTopS - 3);
 constexpr int kTopNodes = (1 << kTopS) - 1;
+constexpr int kTopRegH = 6;        // shuffle levels h < 6 in registers, the rest (nodes < 7) in LDS
+
+struct TopVal {
+  double s, m;
+  int t;  // touched
+};
+
+__device__ __forceinline__ TopVal top_maintain(double v, bool key, const TopVal &L, const TopVal &R, bool has_l,
+                                               bool has_r, double s_old, double m_old) {
+  TopVal o{s_old, m_old, 0};
+  if (!(key || (has_l && L.t) || (has_r && R.t))) return o;
+  double sm = v, mn = (v != 0.0) ? v : 1.0;
+  if (has_l) {
+    sm = radd(sm, L.s);
+    if (L.m != 0.0) mn = (L.m < mn) ? L.m : mn;
+  }
+  if (has_r) {
+    sm = radd(sm, R.s);
+    if (R.m != 0.0) mn = (R.m < mn) ? R.m : mn;
+  }
+  return TopVal{sm, mn, 1};
+}
+
+struct TopRec {
+  double v, s, m;
+};
+
+__device__ __forceinline__ TopRec top_load(const Node *nd, int64_t cap, int64_t i) {
+  TopRec r{0.0, 0.0, 0.0};
+  if (i < cap) {
+    const Node x = nd[i + 1];
+    r = TopRec{x.val, x.sum, x.mn};
+  }
+  return r;
+}
+
+// one node: maintain (if touched) and store what changed
+__device__ __forceinline__ TopVal top_node(const UpdArgs &a, int64_t i, const TopRec &r, bool key, const TopVal &L,
+                                           const TopVal &R) {
+  const int64_t l = 2 * i + 1;
+  const TopVal o = top_maintain(r.v, key, L, R, l < a.cap, l + 1 < a.cap, r.s, r.m);
+  if (key) a.nd[i + 1].val = r.v;
+  if (o.t) {
+    a.nd[i + 1].sum = o.s;
+    a.nd[i + 1].mn = o.m;
+  }
+  return o;
+}
 
 __global__ __launch_bounds__(kTopThreads) void k_tree_update_top(UpdArgs a, int S) {
-  __shared__ double tv[kTopNodes], tsum[kTopNodes], tmin[kTopNodes];
-  __shared__ double bsum[kTopNodes + 1], bmin[kTopNodes + 1];
   __shared__ int32_t win[kTopNodes];
-  __shared__ uint8_t ttop[kTopNodes], tbot[kTopNodes + 1];
-  const int tid = threadIdx.x;
+  __shared__ uint32_t bot[(kTopNodes + 1) / 32];
+  __shared__ double xs[8], xm[8];
+  __shared__ int xt[8];
+  __shared__ double uv[8], us[8], um[8];  // records of the levels above the register slots
+  __shared__ int ukey[8];
+  const int t = threadIdx.x;
   const int64_t cap = a.cap;
-  if (tid == 0) g_upd_clock[2] = wall_clock64();
-  const int64_t fifo_start = a.st ? a.st->tail : a.fifo_start;
-  const double alpha = a.st ? sched_value(a.alpha_s, a.st->sched_step + a.pre_step) : a.alpha;
+  if (a.timing && t == 0) g_upd_clock[2] = wall_clock64();
+  int64_t fifo_start;
+  double alpha;
+  upd_prologue(a, &fifo_start, &alpha);
   const int64_t N = a.pn + a.n;
   const int ntop = (1 << S) - 1;
-  for (int i = tid; i < ntop; i += kTopThreads) {
-    double v = 0.0, s = 0.0, m = 0.0;
-    if (i < cap) {
-      const Node x = a.nd[i + 1];
-      v = x.val;
-      s = x.sum;
-      m = x.mn;
+  const int n3 = 1 << (S - 3);  // nodes of level S-3 (one per lane)
+  const bool lane = t < n3;
+  // ---- every record this lane maintains, loads in flight together
+  const int64_t b1 = (int64_t)(4 * n3) - 1 + 4 * t;  // level S-1: b1 .. b1+3
+  const int64_t b2 = (int64_t)(2 * n3) - 1 + 2 * t;  // level S-2: b2, b2+1
+  TopRec r1[4], r2[2], rr[kTopRegH];
+  double cs[8], cm[8];  // level S children of the level S-1 nodes
+#pragma unroll
+  for (int q = 0; q < 4; ++q) r1[q] = top_load(a.nd, lane ? cap : 0, b1 + q);
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const int64_t l = 2 * b1 + 1 + c;
+    cs[c] = cm[c] = 0.0;
+    if (lane && l < cap) {
+      cs[c] = a.nd[l + 1].sum;
+      cm[c] = a.nd[l + 1].mn;
     }
-    tv[i] = v;
-    tsum[i] = s;
-    tmin[i] = m;
-    win[i] = -1;
-    ttop[i] = 0;
   }
-  for (int k = tid; k <= ntop; k += kTopThreads) {
-    const int64_t node = ntop + k;
-    double s = 0.0, m = 0.0;
-    if (node < cap) {
-      s = a.nd[node + 1].sum;
-      m = a.nd[node + 1].mn;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) r2[q] = top_load(a.nd, lane ? cap : 0, b2 + q);
+  // shuffle slot h = S-3-k holds level k (lane t owns it when t is a multiple of 2^h):
+  // node (2^k - 1) + (t >> h); levels k <= S-3-kTopRegH (nodes < 7) go through LDS
+#pragma unroll
+  for (int h = 0; h < kTopRegH; ++h) {
+    rr[h] = TopRec{0.0, 0.0, 0.0};
+    if (h <= S - 3 && lane && (t & ((1 << h) - 1)) == 0) {
+      const int k = S - 3 - h;
+      rr[h] = top_load(a.nd, cap, ((int64_t)1 << k) - 1 + (t >> h));
     }
-    bsum[k] = s;
-    bmin[k] = m;
-    tbot[k] = 0;
+  }
+  const bool lds_rec = t < 7 && t < cap && node_depth(t) <= S - 3 - kTopRegH;
+  if (lds_rec) {
+    const TopRec x = top_load(a.nd, cap, t);
+    uv[t] = x.v;
+    us[t] = x.s;
+    um[t] = x.m;
+  }
+  for (int i = t; i < ntop; i += kTopThreads) win[i] = -1;
+  for (int i = t; i < (kTopNodes + 1) / 32; i += kTopThreads) bot[i] = 0u;
+  __syncthreads();
+  // ---- keys: last writer per top node, touched flags of level S (their subtrees had keys)
+  constexpr int kScanU = 4;
+  for (int64_t g0 = 0; g0 < N; g0 += kScanU * kTopThreads) {
+    int64_t id[kScanU];
+#pragma unroll
+    for (int u = 0; u < kScanU; ++u) {
+      const int64_t g = g0 + u * kTopThreads + t;
+      id[u] = g < N ? upd_id(a, g, fifo_start) : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < kScanU; ++u) {
+      if (id[u] < 0 || id[u] >= cap) continue;
+      if (id[u] < ntop) {
+        atomicMax(&win[id[u]], (int32_t)(g0 + u * kTopThreads + t));
+      } else {
+        const int d = node_depth(id[u]);
+        const int b = (int)(((id[u] + 1) >> (d - S)) - 1 - ntop);
+        atomicOr(&bot[b >> 5], 1u << (b & 31));
+      }
+    }
   }
   __syncthreads();
-  for (int64_t g = tid; g < N; g += kTopThreads) {
-    const int64_t id = upd_id(a, g, fifo_start);
-    if (id < 0 || id >= cap) continue;
-    if (id < ntop) {
-      atomicMax(&win[id], (int32_t)g);
-    } else {
-      const int d = node_depth(id);
-      tbot[((id + 1) >> (d - S)) - 1 - ntop] = 1;
+  if (a.timing && t == 0) g_upd_clock[3] = wall_clock64();
+  // ---- new priorities of this lane's key nodes (before the level loop: it issues no loads,
+  // so its stores are never waited for)
+  int key1 = 0, key2 = 0, keyr = 0;
+  if (lane) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t i = b1 + q;
+      if (i < cap && win[i] >= 0) {
+        r1[q].v = priority_of(a, alpha, win[i]);
+        key1 |= 1 << q;
+      }
     }
-  }
-  __syncthreads();
-  if (tid == 0) g_upd_clock[3] = wall_clock64();
-  for (int i = tid; i < ntop; i += kTopThreads) {
-    const int w = win[i];
-    if (w >= 0) {
-      const double v = priority_of(a, alpha, w);
-      tv[i] = v;
-      ttop[i] = 1;
-      a.nd[i + 1].val = v;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int64_t i = b2 + q;
+      if (i < cap && win[i] >= 0) {
+        r2[q].v = priority_of(a, alpha, win[i]);
+        key2 |= 1 << q;
+      }
     }
-  }
-  __syncthreads();
-  for (int L = S - 1; L >= 0; --L) {
-    const int first = (1 << L) - 1;
-    for (int i = first + tid; i < 2 * first + 1 && i < cap; i += kTopThreads) {
-      const int64_t l = 2 * (int64_t)i + 1, r = l + 1;
-      const bool bottom = (L == S - 1);
-      bool t = ttop[i] != 0;
-      double ls = 0.0, lm = 0.0, rs = 0.0, rm = 0.0;
-      if (l < cap) {
-        if (bottom) {
-          t |= tbot[l - ntop] != 0;
-          ls = bsum[l - ntop];
-          lm = bmin[l - ntop];
-        } else {
-          t |= ttop[l] != 0;
-          ls = tsum[l];
-          lm = tmin[l];
+#pragma unroll
+    for (int h = 0; h < kTopRegH; ++h) {
+      if (h <= S - 3 && (t & ((1 << h) - 1)) == 0) {
+        const int64_t i = ((int64_t)1 << (S - 3 - h)) - 1 + (t >> h);
+        if (i < cap && win[i] >= 0) {
+          rr[h].v = priority_of(a, alpha, win[i]);
+          keyr |= 1 << h;
         }
       }
-      if (r < cap) {
-        if (bottom) {
-          t |= tbot[r - ntop] != 0;
-          rs = bsum[r - ntop];
-          rm = bmin[r - ntop];
-        } else {
-          t |= ttop[r] != 0;
-          rs = tsum[r];
-          rm = tmin[r];
+    }
+  }
+  if (lds_rec) {
+    ukey[t] = win[t] >= 0;
+    if (win[t] >= 0) uv[t] = priority_of(a, alpha, win[t]);
+  }
+  __syncthreads();
+  if (a.timing && t == 0) g_upd_clock[6] = wall_clock64();
+  // ---- the lane-local levels S-1, S-2, S-3
+  TopVal cur{0.0, 0.0, 0};
+  if (lane) {
+    TopVal v1[4], v2[2];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int b = 2 * (4 * t + q);  // level-S index of the left child
+      const TopVal L{cs[2 * q], cm[2 * q], (int)((bot[b >> 5] >> (b & 31)) & 1u)};
+      const TopVal R{cs[2 * q + 1], cm[2 * q + 1], (int)((bot[(b + 1) >> 5] >> ((b + 1) & 31)) & 1u)};
+      v1[q] = b1 + q < cap ? top_node(a, b1 + q, r1[q], (key1 >> q) & 1, L, R) : TopVal{0.0, 0.0, 0};
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+      v2[q] = b2 + q < cap ? top_node(a, b2 + q, r2[q], (key2 >> q) & 1, v1[2 * q], v1[2 * q + 1])
+                           : TopVal{0.0, 0.0, 0};
+    const int64_t i3 = (int64_t)n3 - 1 + t;
+    if (i3 < cap) cur = top_node(a, i3, rr[0], keyr & 1, v2[0], v2[1]);
+  }
+  if (a.timing && t == 0) g_upd_clock[7] = wall_clock64();
+  // ---- levels S-4 .. 0 (slot h = S-3-k): left child on this lane, right child 2^(h-1) lanes up
+#pragma unroll
+  for (int h = 1; h <= kTopS - 3; ++h) {
+    if (h <= S - 3) {  // uniform
+      const int k = S - 3 - h;
+      const int d = 1 << (h - 1);
+      TopVal R;
+      if (d < 64) {
+        R.s = __shfl_down(cur.s, d, 64);
+        R.m = __shfl_down(cur.m, d, 64);
+        R.t = __shfl_down(cur.t, d, 64);
+      } else {
+        // right children of level k+1 (node ids < 7: k + 1 <= S - 10 <= 1) through LDS;
+        // level k+1 is owned by the multiples of d
+        if (lane && (t & (d - 1)) == 0 && ((t >> (h - 1)) & 1)) {
+          const int node = (1 << (k + 1)) - 1 + (t >> (h - 1));
+          xs[node] = cur.s;
+          xm[node] = cur.m;
+          xt[node] = cur.t;
         }
+        lds_barrier();  // LDS only: the level loop's global stores are never waited for
+        R = TopVal{0.0, 0.0, 0};
+        if (lane && (t & ((1 << h) - 1)) == 0) {
+          const int rn = 2 * ((1 << k) - 1 + (t >> h)) + 2;
+          R = TopVal{xs[rn], xm[rn], xt[rn]};
+        }
+        lds_barrier();
       }
-      if (!t) continue;
-      const double v = tv[i];
-      double sm = v, mn = (v != 0.0) ? v : 1.0;
-      if (l < cap) {
-        sm = radd(sm, ls);
-        if (lm != 0.0) mn = (lm < mn) ? lm : mn;
+      const int64_t i = ((int64_t)1 << k) - 1 + (t >> h);
+      if (lane && (t & ((1 << h) - 1)) == 0 && i < cap) {
+        const bool reg = h < kTopRegH;
+        const int hr = reg ? h : 0;
+        const TopRec rec = reg ? rr[hr] : TopRec{uv[i & 7], us[i & 7], um[i & 7]};
+        const bool key = reg ? ((keyr >> hr) & 1) : ukey[i & 7] != 0;
+        cur = top_node(a, i, rec, key, cur, R);
       }
-      if (r < cap) {
-        sm = radd(sm, rs);
-        if (rm != 0.0) mn = (rm < mn) ? rm : mn;
-      }
-      tsum[i] = sm;
-      tmin[i] = mn;
-      ttop[i] = 1;
-    }
-    lds_barrier();  // LDS only: no wait for global stores inside the level loop
-  }
-  for (int i = tid; i < ntop && i < cap; i += kTopThreads) {
-    if (ttop[i]) {
-      a.nd[i + 1].sum = tsum[i];
-      a.nd[i + 1].mn = tmin[i];
     }
   }
-  if (tid == 0) {
+  if (a.timing && t == 0) g_upd_clock[8] = wall_clock64();
+  if (t == 0) {
     if (a.st) {
       if (a.pre_step) a.st->sched_step += 1;
       if (a.post_tail) a.st->tail = (fifo_start + a.n) % cap;  // every read of tail is done
     }
-    g_upd_clock[4] = wall_clock64();
+    if (a.timing) g_upd_clock[4] = wall_clock64();
   }
 }
 
@@ -718,8 +825,10 @@ int tree_update_impl(rth_sumtree *t, const int64_t *idx, int64_t fifo_start, con
     a.pre_step = pend->step ? 1 : 0;
   }
   a.post_tail = post_tail;
+  static const int timing = env_int("RTH_TREE_TIMING", 0);
+  a.timing = timing;
   RTH_REQUIRE(a.pn + a.n < (int64_t(1) << 31), "tree update: at most 2^31 - 1 keys per call");
-  const int S = t->maxd + 1 < kTopS ? t->maxd + 1 : kTopS;
+  const int S = t->maxd + 1 < kTopMinS ? kTopMinS : (t->maxd + 1 < kTopS ? t->maxd + 1 : kTopS);
   if (t->maxd >= S && a.pn + a.n > 0) {  // levels S..maxd: one workgroup per group of subtrees
     const int64_t nsub = int64_t(1) << S;
     hipLaunchKernelGGL(k_tree_update_sub, dim3((unsigned)(nsub < kSubGrid ? nsub : kSubGrid)), dim3(kSubThreads), 0,
@@ -778,9 +887,11 @@ int rth_sumtree_clear(rth_sumtree *t, void *stream) {
   return RTH_OK;
 }
 
-int rth_debug_tree_timing(long long *out5) {
-  RTH_REQUIRE(out5, "rth_debug_tree_timing: NULL");
-  RTH_HIP(hipMemcpyFromSymbol(out5, HIP_SYMBOL(g_upd_clock), 5 * sizeof(long long)));
+int rth_debug_tree_timing(long long *out9) {
+  RTH_REQUIRE(out9, "rth_debug_tree_timing: NULL");
+  RTH_HIP(hipMemcpyFromSymbol(out9, HIP_SYMBOL(g_upd_clock), 9 * sizeof(long long)));
+  static const long long zero[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  RTH_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_upd_clock), zero, sizeof(zero)));
   return RTH_OK;
 }
 

@@ -223,6 +223,178 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__res
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// conv1 on uint8 stacks on the bf16 MFMA with an exact three-term weight split.
+// A byte is exact in bf16, and every fp32 weight is the exact sum w1 + w2 + w3 of three
+// bf16 values (w1 = bf16(w), w2 = bf16(w - w1), w3 = w - w1 - w2: 8 + 8 + 8 of the 24
+// significand bits), so every product x * wi is exact in fp32 and
+//     y = sum_k x_k * w_k = sum_k x_k * w1_k + x_k * w2_k + x_k * w3_k
+// is the same sum of exact products as the fp32 path, accumulated in fp32 in a different
+// order (3 x K terms instead of K).  Nothing is computed at reduced precision; the rate is
+// three bf16 MFMAs per fp32 MFMA's work at 16x the per-clock rate.
+// Tile: v_mfma_f32_32x32x16_bf16 with A = the weights (32 output channels x 16 k), B = 32
+// output pixels' input windows: lane (r, h) = (lane & 31, lane >> 5) holds k = 8h .. 8h+7 of
+// chunk c = run (ci, kh) = 2c + h of pixel r -- 8 consecutive bytes of one stack row -- and
+// the same k of output channel r's weights.  A wave keeps all of W (16 chunks x 3 terms,
+// 192 VGPRs) in registers for its whole life, so the kernel uses no LDS and leaves the CU's
+// LDS to the learner's kernels; it loads the next tile's windows while it multiplies this one.
+using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
+using u32x4 = __attribute__((ext_vector_type(4))) uint32_t;
+constexpr int kC1Chunks = 16;                       // K = 256 = 16 chunks of 16
+constexpr int kC1PackedBytes = kC1Chunks * 3 * 64 * 16;  // [chunk][term][lane] x 8 bf16
+#ifndef C1_NBUF
+#define C1_NBUF 3
+#endif
+constexpr int kC1Buf = C1_NBUF;  // tiles whose windows are in flight (the computed one included)
+
+__host__ __device__ __forceinline__ uint32_t bf16_rne_bits(float f) {
+  uint32_t u = __float_as_uint(f);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return u >> 16;
+}
+__host__ __device__ __forceinline__ float bf16_bits_f(uint32_t b) { return __uint_as_float(b << 16); }
+
+// term t (0, 1, 2) of the exact split of w
+__device__ __forceinline__ uint32_t bf16x3_term(float w, int t) {
+  const uint32_t h1 = bf16_rne_bits(w);
+  const float r1 = rsub(w, bf16_bits_f(h1));
+  const uint32_t h2 = bf16_rne_bits(r1);
+  const float r2 = rsub(r1, bf16_bits_f(h2));
+  return t == 0 ? h1 : (t == 1 ? h2 : bf16_rne_bits(r2));
+}
+
+// packed slot sl = (c * 3 + t) * 64 + lane: the 8 bf16 of lane (r, h) for chunk c, term t
+// from W in OHWI storage: k = 8h + j of chunk c is (ci, kh) = run 2c + h, kw = j
+__device__ __forceinline__ void pack_conv1_bf16x3(const float *__restrict__ w, u32x4 *__restrict__ packed, int sl) {
+  if (sl >= kC1PackedBytes / 16) return;
+  const int lane = sl % 64, t = (sl / 64) % 3, c = sl / 192;
+  const int co = lane & 31, rho = 2 * c + (lane >> 5), ci = rho >> 3, kh = rho & 7;
+  uint32_t e[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) e[j] = bf16x3_term(w[((co * 8 + kh) * 8 + j) * 4 + ci], t);
+  packed[sl] = u32x4{e[0] | (e[1] << 16), e[2] | (e[3] << 16), e[4] | (e[5] << 16), e[6] | (e[7] << 16)};
+}
+
+// 8 bytes (kw 0..7 of one stack row) -> 8 bf16 (exact: a byte has <= 8 significant bits)
+__device__ __forceinline__ bf16x8 u8x8_to_bf16(uint32_t lo, uint32_t hi) {
+  auto two = [](uint32_t v, int s) -> uint32_t {
+    const uint32_t a = __float_as_uint((float)((v >> s) & 0xffu));
+    const uint32_t b = __float_as_uint((float)((v >> (s + 8)) & 0xffu));
+    return __builtin_amdgcn_perm(b, a, 0x07060302u);  // {a.hi16, b.hi16}
+  };
+  return __builtin_bit_cast(bf16x8, (u32x4{two(lo, 0), two(lo, 16), two(hi, 0), two(hi, 16)}));
+}
+
+__global__ __launch_bounds__(256) void k_conv1_u8_bf16x3(const void *__restrict__ x, const int64_t *__restrict__ rows,
+                                                       int64_t n, const int64_t *__restrict__ n_dev,
+                                                       const float *__restrict__ w, const float *__restrict__ bias,
+                                                       float *__restrict__ y) {
+  constexpr int HIN = 84, WIN = 84, WOUT = 20, PIX = 400, S = 4, COUT = 32;
+  constexpr int64_t STACK = 4 * HIN * WIN;
+  using f32x16 = __attribute__((ext_vector_type(16))) float;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar tile math
+  const int r = lane & 31, h = lane >> 5;
+  if (n_dev) {  // a device-side sample count (<= n): rows past it are neither read nor written
+    const int64_t m = *n_dev;
+    n = m < n ? (m > 0 ? m : 0) : n;
+  }
+  const int64_t P = n * PIX, tiles = (P + 31) / 32, tstride = (int64_t)gridDim.x * 4;
+  int64_t tile = (int64_t)blockIdx.x * 4 + wave;
+  if (tile >= tiles) return;  // no barriers below: a wave without tiles just leaves
+  const uint8_t *xb = static_cast<const uint8_t *>(x);
+  // pixel r of tile t (tail: a duplicate pixel).  A tile spans at most two samples b0, b0+1:
+  // their row indices are scalar loads (lgkmcnt), so computing a window never waits for the
+  // vector loads of the tiles already in flight
+  auto window = [&](int64_t t) -> const uint8_t * {
+    const int64_t t32 = t * 32, b0 = t32 / PIX;
+    int pp = (int)(t32 - b0 * PIX) + r;
+    int64_t b = b0;
+    if (pp >= PIX) {
+      pp -= PIX;
+      b = b0 + 1;
+    }
+    if (b >= n) {
+      b = n - 1;
+      pp = PIX - 1;
+    }
+    int64_t row = b;
+    if (rows) {
+      const int64_t r0 = rows[b0], r1 = rows[b0 + 1 < n ? b0 + 1 : b0];
+      row = b == b0 ? r0 : r1;
+    }
+    const int oy = pp / WOUT, ox = pp % WOUT;
+    return xb + row * STACK + (S * oy) * WIN + S * ox;
+  };
+  // this lane's run of chunk c: (ci, kh) = (2c + h) >> 3, (2c + h) & 7
+  auto run_off = [&](int c) -> int {
+    const int rho = 2 * c + h;
+    return (rho >> 3) * HIN * WIN + (rho & 7) * WIN;
+  };
+  const u32x4 *wp = reinterpret_cast<const u32x4 *>(w);
+  bf16x8 wf[kC1Chunks][3];
+#pragma unroll
+  for (int c = 0; c < kC1Chunks; ++c)
+#pragma unroll
+    for (int t = 0; t < 3; ++t) wf[c][t] = __builtin_bit_cast(bf16x8, wp[(c * 3 + t) * 64 + lane]);
+  float bl[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) bl[i] = bias[(i & 3) + 8 * (i >> 2) + 4 * h];
+
+  uint32_t raw[kC1Buf][kC1Chunks][2];  // a ring of tiles in flight
+  auto load = [&](uint32_t (&dst)[kC1Chunks][2], int64_t t) {
+    const uint8_t *p = window(t);
+#pragma unroll
+    for (int c = 0; c < kC1Chunks; ++c) {
+      const uint8_t *q = p + run_off(c);
+      dst[c][0] = *reinterpret_cast<const uint32_t *>(q);
+      dst[c][1] = *reinterpret_cast<const uint32_t *>(q + 4);
+    }
+  };
+  auto compute = [&](const uint32_t (&src)[kC1Chunks][2], int64_t t) {
+    f32x16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
+#pragma unroll
+    for (int c = 0; c < kC1Chunks; ++c) {
+      const bf16x8 xf = u8x8_to_bf16(src[c][0], src[c][1]);
+#pragma unroll
+      for (int tm = 0; tm < 3; ++tm) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[c][tm], xf, acc, 0, 0, 0);
+    }
+    // C/D: lane holds pixel r, channels (i & 3) + 8 (i >> 2) + 4h of register i.  Tail lanes
+    // computed the last pixel's window and store the same bytes to it: no branch around the
+    // stores, so the compiler can count the loads in flight exactly (no vmcnt(0) per tile)
+    int64_t p = t * 32 + r;
+    if (p >= P) p = P - 1;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      float4 o;
+      o.x = relu_c(radd(acc[4 * g + 0], bl[4 * g + 0]));
+      o.y = relu_c(radd(acc[4 * g + 1], bl[4 * g + 1]));
+      o.z = relu_c(radd(acc[4 * g + 2], bl[4 * g + 2]));
+      o.w = relu_c(radd(acc[4 * g + 3], bl[4 * g + 3]));
+      *reinterpret_cast<float4 *>(y + p * COUT + 8 * g + 4 * h) = o;
+    }
+  };
+  // loads are unconditional (past the last tile: the last tile again) for the same reason
+#pragma unroll
+  for (int i = 0; i + 1 < kC1Buf; ++i) load(raw[i], tile + i * tstride < tiles ? tile + i * tstride : tiles - 1);
+  for (;;) {
+#pragma unroll
+    for (int i = 0; i < kC1Buf; ++i) {
+      const int64_t ahead = tile + (kC1Buf - 1) * tstride;
+      load(raw[(i + kC1Buf - 1) % kC1Buf], ahead < tiles ? ahead : tiles - 1);
+      compute(raw[i], tile);
+      tile += tstride;
+      if (tile >= tiles) return;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_conv1_pack_bf16x3(const float *__restrict__ w, u32x4 *__restrict__ packed) {
+  pack_conv1_bf16x3(w, packed, blockIdx.x * 256 + threadIdx.x);
+}
+
 // OHWI weights -> MFMA fragment order (the LDS image the conv kernel copies)
 template <int MODE, int KH, int KW, int S, int CIN, int COUT, int HIN, int WIN>
 __global__ __launch_bounds__(256) void k_conv_pack(const float *__restrict__ w, f32x4 *__restrict__ packed) {
@@ -235,6 +407,7 @@ __global__ __launch_bounds__(256) void k_conv_pack(const float *__restrict__ w, 
 constexpr int kPackMax = 4;
 struct PackJob {
   int geom[kPackMax];  // index into the built geometries (find_conv order)
+  int bf16x3[kPackMax];  // conv1 u8: the bf16x3 kernel's packed form
   const float *w[kPackMax];
   f32x4 *packed[kPackMax];
   int first_block[kPackMax + 1];
@@ -252,7 +425,10 @@ __global__ __launch_bounds__(256) void k_conv_pack_many(PackJob job) {
   while (l + 1 < job.n && (int)blockIdx.x >= job.first_block[l + 1]) ++l;
   const int sl = ((int)blockIdx.x - job.first_block[l]) * 256 + threadIdx.x;
   switch (job.geom[l]) {
-    case 0: pack_one<RTH_CONV_U8_CHW, 8, 8, 4, 4, 32, 84, 84>(job.w[l], job.packed[l], sl); break;
+    case 0:
+      if (job.bf16x3[l]) pack_conv1_bf16x3(job.w[l], reinterpret_cast<u32x4 *>(job.packed[l]), sl);
+      else pack_one<RTH_CONV_U8_CHW, 8, 8, 4, 4, 32, 84, 84>(job.w[l], job.packed[l], sl);
+      break;
     case 1: pack_one<RTH_CONV_F32_NHWC, 8, 8, 4, 4, 32, 84, 84>(job.w[l], job.packed[l], sl); break;
     case 2: pack_one<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20>(job.w[l], job.packed[l], sl); break;
     default: pack_one<RTH_CONV_F32_NHWC, 3, 3, 1, 64, 64, 9, 9>(job.w[l], job.packed[l], sl); break;
@@ -262,9 +438,10 @@ __global__ __launch_bounds__(256) void k_conv_pack_many(PackJob job) {
 struct ConvLaunch {
   const void *fn, *pack;
   int waves;
-  int lds_bytes;
+  int lds_bytes;  // packed weight bytes
   int per_cu;  // resident workgroups per CU (occupancy query, cached)
   int tile_px;  // output pixels per wave tile
+  int bf16x3;   // k_conv1_u8_bf16x3 (conv1 on uint8 stacks, exact-split bf16 MFMA)
 };
 
 template <int MODE, int KH, int KW, int S, int CIN, int COUT, int HIN, int WIN, int WAVES, int MB>
@@ -272,10 +449,19 @@ static ConvLaunch conv_launch() {
   using Gm = ConvGeom<MODE, KH, KW, S, CIN, COUT, HIN, WIN>;
   ConvLaunch l{reinterpret_cast<const void *>(&k_conv_bias_relu<MODE, KH, KW, S, CIN, COUT, HIN, WIN, WAVES, MB>),
                reinterpret_cast<const void *>(&k_conv_pack<MODE, KH, KW, S, CIN, COUT, HIN, WIN>), WAVES,
-               Gm::LDS_F4 * 16, 0, 16 * MB};
+               Gm::LDS_F4 * 16, 0, 16 * MB, 0};
   int blocks = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, l.fn, WAVES * 64, 0) != hipSuccess || blocks < 1)
     blocks = 1;
+  l.per_cu = blocks;
+  return l;
+}
+
+static ConvLaunch conv1_bf16x3_launch() {
+  ConvLaunch l{reinterpret_cast<const void *>(&k_conv1_u8_bf16x3), reinterpret_cast<const void *>(&k_conv1_pack_bf16x3),
+               4, kC1PackedBytes, 0, 32, 1};
+  int blocks = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, l.fn, 256, 0) != hipSuccess || blocks < 1) blocks = 1;
   l.per_cu = blocks;
   return l;
 }
@@ -297,7 +483,13 @@ static bool find_conv(const rth_conv_shape &s, ConvLaunch *out, int *geom = null
            s.kw == kw && s.stride == st;
   };
   if (is(RTH_CONV_U8_CHW, 4, 84, 84, 32, 8, 8, 4)) {
-    static const ConvLaunch l = conv_launch<RTH_CONV_U8_CHW, 8, 8, 4, 4, 32, 84, 84, 4, CONV1_MB>();
+    // RTH_CONV1_F32=1: the fp32-MFMA kernel (A/B and parity cross-checks)
+    static const bool f32 = [] {
+      const char *e = getenv("RTH_CONV1_F32");
+      return e && atoi(e) != 0;
+    }();
+    static const ConvLaunch l = f32 ? conv_launch<RTH_CONV_U8_CHW, 8, 8, 4, 4, 32, 84, 84, 4, CONV1_MB>()
+                                    : conv1_bf16x3_launch();
     *out = l;
     if (geom) *geom = 0;
   } else if (is(RTH_CONV_F32_NHWC, 4, 84, 84, 32, 8, 8, 4)) {
@@ -695,6 +887,7 @@ int rth_conv_pack_many(int32_t n, const rth_conv_shape *shapes, const float *con
                 "rth_conv_pack_many: layer %d buffer NULL or misaligned", l);
     job.w[l] = w[l];
     job.packed[l] = reinterpret_cast<f32x4 *>(packed[l]);
+    job.bf16x3[l] = cl.bf16x3;
     job.first_block[l] = blocks;
     blocks += (cl.lds_bytes / 16 + 255) / 256;
   }

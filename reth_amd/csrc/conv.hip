@@ -763,6 +763,152 @@ __global__ __launch_bounds__(kWgWaves * 64) void k_conv_wgrad_u8(const uint8_t *
   }
 }
 
+// conv1 weight gradient on uint8 stacks on the bf16 MFMA, the upstream gradient split into
+// three exact bf16 terms (truncation split: a = hi + mid + lo, 8 significand bits each, so
+// every product with a byte is exact in fp32): the same partials as k_conv_wgrad_u8 --
+// D[co][(ci, kh)] per kw over this workgroup's pixels -- summed in a different order.
+// One v_mfma_f32_32x32x16_bf16 takes 16 pixels as two "slots" of 8 consecutive output
+// pixels of one output row (ox 0-7, 8-15, 16-19 + 4 masked: 3 slots per row, 60 per
+// stack); lane (r, h) holds slot h: as A the masked gradient of channel r (3 terms), as B
+// byte kw of run (ci, kh) = r of each pixel's window.  The 8 windows of a slot overlap: run r
+// of all of them is one 36-byte span of stack row (ci, 4 oy + kh) (20 bytes for the last
+// slot of a row), loaded as 2 x dwordx4 + dword; v_cvt_f32_ubyteN picks byte kw of pixel j
+// (byte 4j + kw of the span), so the 8x8 byte transpose is free.  The tile / partial
+// layout and the cross-wave LDS sum are k_conv_wgrad_u8's.
+__device__ __forceinline__ void split3_trunc(float a, uint32_t &t0, uint32_t &t1, uint32_t &t2) {
+  const uint32_t u = __float_as_uint(a);
+  t0 = u & 0xffff0000u;
+  const float r1 = rsub(a, __uint_as_float(t0));
+  t1 = __float_as_uint(r1) & 0xffff0000u;
+  t2 = __float_as_uint(rsub(r1, __uint_as_float(t1)));  // <= 8 significand bits: exact in bf16
+}
+
+template <bool ROWS>
+__global__ __launch_bounds__(kWgWaves * 64) void k_conv1_wgrad_bf16x3(const uint8_t *__restrict__ x,
+                                                                     const int64_t *__restrict__ rows, int64_t n,
+                                                                     const float *__restrict__ g,
+                                                                     const float *__restrict__ y,
+                                                                     float *__restrict__ partial) {
+  constexpr int HIN = 84, WIN = 84, WOUT = 20, PIX = 400, KH = 8, KW = 8, S = 4, COUT = 32;
+  constexpr int K = 4 * KH * KW, STACK = 4 * HIN * WIN, SLOTS = 3 * 20;  // slots per stack
+  using f32x16 = __attribute__((ext_vector_type(16))) float;
+  __shared__ float red[kWgWaves][32];
+  __shared__ float tile[kWgWaves][32 * 32];
+  const int lane = threadIdx.x % 64, o = lane & 31, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / 64);
+  const int64_t NS = n * SLOTS, NG = (NS + 1) / 2;  // slots, 2-slot groups
+  const int64_t chunk = ((NG + gridDim.x - 1) / gridDim.x + kWgWaves - 1) / kWgWaves * kWgWaves;
+  const int64_t g_begin = (int64_t)blockIdx.x * chunk, g_end = g_begin + chunk < NG ? g_begin + chunk : NG;
+  const int row_off = (o / KH) * HIN * WIN + (o % KH) * WIN;  // run (ci, kh) = o
+  struct Raw {
+    float gv[8], yv[8];
+    uint32_t sp[9];  // the 36-byte span
+    int nv;          // valid pixels of the slot (0: past the end)
+  };
+  // no branches around loads (the compiler then counts the loads in flight exactly instead of
+  // waiting for all of them): the two slots' samples and row indices are scalar
+  auto load = [&](int64_t gq, Raw &rw) {
+    const bool live = gq < g_end;
+    const int64_t gi = live ? gq : g_end - 1;
+    const int64_t s0 = 2 * gi, s1 = s0 + 1 < NS ? s0 + 1 : NS - 1;  // wave-uniform
+    const int64_t b0 = s0 / SLOTS, b1 = s1 / SLOTS;
+    const int64_t rw0 = ROWS ? rows[b0] : b0, rw1 = ROWS ? rows[b1] : b1;
+    const int64_t sl = h ? s1 : s0, b = h ? b1 : b0, row = h ? rw1 : rw0;
+    const int rem = (int)(sl - b * SLOTS), oy = rem / 3, seg = rem % 3;
+    rw.nv = live && 2 * gi + h < NS ? (seg == 2 ? 4 : 8) : 0;
+    const uint8_t *src = x + row * (int64_t)STACK + row_off + (S * oy) * WIN + S * 8 * seg;
+    const u32x4 v0 = *reinterpret_cast<const u32x4 *>(src);
+    const uint32_t v4 = *reinterpret_cast<const uint32_t *>(src + 16);
+    // the last slot's span ends the row: its unused upper part re-reads the lower
+    const u32x4 v1 = *reinterpret_cast<const u32x4 *>(src + (seg < 2 ? 20 : 0));
+    rw.sp[0] = v0[0], rw.sp[1] = v0[1], rw.sp[2] = v0[2], rw.sp[3] = v0[3], rw.sp[4] = v4;
+    rw.sp[5] = v1[0], rw.sp[6] = v1[1], rw.sp[7] = v1[2], rw.sp[8] = v1[3];
+    const int64_t q0 = b * PIX + oy * WOUT + 8 * seg;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int64_t q = q0 + (j < 4 || seg < 2 ? j : 0);  // masked pixels re-read pixel 0
+      rw.gv[j] = g[q * COUT + o];
+      rw.yv[j] = y[q * COUT + o];
+    }
+  };
+  f32x16 acc[KW];
+#pragma unroll
+  for (int t = 0; t < KW; ++t) acc[t] = f32x16{};
+  float db = 0.0f;
+  auto compute = [&](const Raw &rw) {
+    uint32_t tm[3][8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float a = (j < rw.nv && rw.yv[j] > 0.0f) ? rw.gv[j] : 0.0f;
+      db = radd(db, a);
+      split3_trunc(a, tm[0][j], tm[1][j], tm[2][j]);
+    }
+    bf16x8 af[3];
+#pragma unroll
+    for (int t = 0; t < 3; ++t)
+      af[t] = __builtin_bit_cast(bf16x8, (u32x4{__builtin_amdgcn_perm(tm[t][1], tm[t][0], 0x07060302u),
+                                                 __builtin_amdgcn_perm(tm[t][3], tm[t][2], 0x07060302u),
+                                                 __builtin_amdgcn_perm(tm[t][5], tm[t][4], 0x07060302u),
+                                                 __builtin_amdgcn_perm(tm[t][7], tm[t][6], 0x07060302u)}));
+#pragma unroll
+    for (int kw = 0; kw < KW; ++kw) {
+      uint32_t f[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {  // byte 4j + kw of the span
+        const uint32_t wv = rw.sp[j + kw / 4];
+        f[j] = __float_as_uint((float)((wv >> (8 * (kw % 4))) & 0xffu));
+      }
+      const bf16x8 bf = __builtin_bit_cast(bf16x8, (u32x4{__builtin_amdgcn_perm(f[1], f[0], 0x07060302u),
+                                                         __builtin_amdgcn_perm(f[3], f[2], 0x07060302u),
+                                                         __builtin_amdgcn_perm(f[5], f[4], 0x07060302u),
+                                                         __builtin_amdgcn_perm(f[7], f[6], 0x07060302u)}));
+#pragma unroll
+      for (int t = 0; t < 3; ++t) acc[kw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[t], bf, acc[kw], 0, 0, 0);
+    }
+  };
+  // this wave's groups g_begin + wave + k * waves, k < ng, two per trip (a group past the end
+  // loads a valid one, masked): no branch but the loop's own, and the next group's loads are
+  // issued before this group's math
+  const int64_t gi0 = g_begin + wave;
+  const int64_t ng = gi0 < g_end ? (g_end - gi0 + kWgWaves - 1) / kWgWaves : 0;
+  if (ng > 0) {
+    Raw ra, rb;
+    load(gi0, ra);
+    for (int64_t k = 0; k < ng; k += 2) {
+      load(gi0 + (k + 1) * kWgWaves, rb);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(ra);
+      load(gi0 + (k + 2) * kWgWaves, ra);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(rb);
+    }
+  }
+  // bias: lanes o and o + 32 of every wave
+  db = radd(db, __shfl_down(db, 32));
+  if (h == 0) red[wave][o] = db;
+  // the weight tiles: sum the waves through LDS, tile by tile (C/D: lane -> column o of the
+  // tile, register r -> row i = 8 (r / 4) + 4 h + r % 4 = output channel)
+  float *out = partial + (int64_t)blockIdx.x * (COUT * K + COUT);
+#pragma unroll
+  for (int t = 0; t < KW; ++t) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) tile[wave][(8 * (r / 4) + 4 * h + r % 4) * 32 + o] = acc[t][r];
+    __syncthreads();
+    for (int e = threadIdx.x; e < 32 * 32; e += kWgWaves * 64) {
+      float v = tile[0][e];
+#pragma unroll
+      for (int w = 1; w < kWgWaves; ++w) v = radd(v, tile[w][e]);
+      out[(e / 32) * K + t * 32 + e % 32] = v;  // [o][kk = kw * 32 + (ci, kh)]
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x < 32) {
+    float v = red[0][threadIdx.x];
+    for (int w = 1; w < kWgWaves; ++w) v = radd(v, red[w][threadIdx.x]);
+    out[COUT * K + threadIdx.x] = v;
+  }
+}
+
 // partials [blocks][COUT * K + COUT] (kk = kw * 32 + ci * KH + kh) -> gw OHWI, gb: 64
 // elements per workgroup, 4 groups of 64 lanes each summing a quarter of the partials
 // (coalesced rows), then the 4 group sums in fixed order
@@ -933,8 +1079,17 @@ int rth_conv_relu_wgrad_ex(const rth_conv_shape *shape, const void *x, const int
       RTH_HIP(hipMemsetAsync(deferred[j].db, 0, deferred[j].C * 4, as_stream(stream)));
     return RTH_OK;
   }
-  hipLaunchKernelGGL((k_conv_wgrad_u8<8, 8, 4, 4, 32, 84, 84>), dim3(kWgBlocks), dim3(kWgWaves * 64), 0,
-                     as_stream(stream), static_cast<const uint8_t *>(x), rows, n, g, y, part);
+  // RTH_CONV1_F32=1: the fp32-MFMA kernel (A/B and parity cross-checks)
+  static const bool f32 = [] {
+    const char *e = getenv("RTH_CONV1_F32");
+    return e && atoi(e) != 0;
+  }();
+  if (f32)
+    hipLaunchKernelGGL((k_conv_wgrad_u8<8, 8, 4, 4, 32, 84, 84>), dim3(kWgBlocks), dim3(kWgWaves * 64), 0,
+                       as_stream(stream), static_cast<const uint8_t *>(x), rows, n, g, y, part);
+  else
+    hipLaunchKernelGGL(rows ? k_conv1_wgrad_bf16x3<true> : k_conv1_wgrad_bf16x3<false>, dim3(kWgBlocks),
+                       dim3(kWgWaves * 64), 0, as_stream(stream), static_cast<const uint8_t *>(x), rows, n, g, y, part);
   RTH_LAUNCHED();
   hipLaunchKernelGGL((k_wgrad_reduce<8, 8, 4, 32>), dim3((32 * 256 + 32 + 63) / 64 + ndeferred), dim3(256), 0,
                      as_stream(stream), part, kWgBlocks, gw, gb, bj);

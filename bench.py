@@ -14,10 +14,16 @@ scaling: every GPU runs the same per-GPU workload and the learner gradients are 
 with one RCCL all-reduce per update.
 
 The JSON line carries
-  roofline:      the replay gather kernel (dominant HIP kernel by bytes), timed live with
-                 HIP events on its launch stream; achieved = algorithmic bytes / mean launch
-  cpu_baseline:  the same step on the host cores (oracle restatement of the replay/tree/
-                 n-step path + torch-CPU Q-network), bounded sample, rank 0 at N = 1.
+  roofline:        the dominant kernel of the step (most time per iteration in
+                   profiles/r02_steady_state.txt): conv2's forward (k_conv_bias_relu, fp32
+                   MFMA) in the learner's [s0; s1] pass, timed live over the timed region with
+                   HIP events on the learner stream (the learner graph is cut around that
+                   launch); achieved = algorithmic FLOPs per launch / mean launch duration
+  roofline_gather: the replay gather (k_copy_rows), HBM-bound, timed live the same way
+  roofline_conv1:  conv1 on uint8 stacks (k_conv1_u8_bf16x3) alone, against the bf16 MFMA peak
+                   of the instruction it issues (three exact-split bf16 products per fp32 one)
+  cpu_baseline:    the same step on the host cores (oracle restatement of the replay/tree/
+                   n-step path + torch-CPU Q-network), bounded sample, rank 0 at N = 1.
 """
 import argparse
 import json
@@ -33,7 +39,8 @@ sys.path.insert(0, ROOT)
 
 STACK = 4 * 84 * 84
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
-FP32_PEAK_TFLOPS = 157.3
+FP32_PEAK_TFLOPS = 157.3  # fp32-input MFMA (= the fp32 vector peak)
+BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA
 # BASELINE.json configs[1] (the metric's workload) and configs[2] (a scale case, not the bench line)
 WORKLOADS = {
     "pong": dict(name="PongNoFrameskip-v4 Ape-X DQN (BASELINE configs[1])", actors=256, capacity=1_000_000, actions=6),
@@ -58,10 +65,10 @@ def qnet_flops_per_sample(A=6):
     return 2 * macs
 
 
-def conv_roofline(ax, slot_cols, reps=30):
-    """The kernel with the most time per step, the conv torso's first layer
-    (k_conv_bias_relu on uint8 stacks), over the learner's 2B stacks of a batch slot, timed
-    alone with HIP events around direct launches on the current stream"""
+def conv1_roofline(ax, slot_cols, reps=30):
+    """conv1 on uint8 stacks (k_conv1_u8_bf16x3: bf16 MFMA, weights split into three exact
+    bf16 terms) over the learner's 2B stacks of a batch slot, timed alone with HIP events
+    around direct launches on the current stream"""
     from reth_amd import _lib
     from reth_amd.fused_learner import _pair
 
@@ -84,26 +91,45 @@ def conv_roofline(ax, slot_cols, reps=30):
     torch.cuda.synchronize()
     t = float(np.median([a.elapsed_time(b) for a, b in ev[5:]])) / 1e3
     flops = 2.0 * n * ho * ho * shape.cout * shape.cin * shape.kh * shape.kw
-    return {"kernel": f"k_conv_bias_relu conv1 (uint8 stacks, {n} samples = the learner's [s0; s1])",
-            "bound": "mfma", "achieved": round(flops / t / 1e12, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(flops / t / 1e12 / FP32_PEAK_TFLOPS, 4), "flops_per_launch": flops,
-            "launch_us": round(t * 1e6, 2), "note": "timed alone after the timed region (HIP events)"}
+    return {"kernel": f"k_conv1_u8_bf16x3 (uint8 stacks, {n} samples = the learner's [s0; s1])",
+            "bound": "mfma", "achieved": round(3 * flops / t / 1e12, 2), "peak": BF16_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(3 * flops / t / 1e12 / BF16_PEAK_TFLOPS, 4),
+            "achieved_fp32_equiv": round(flops / t / 1e12, 2), "flops_per_launch": flops,
+            "mfma_flops_per_launch": 3 * flops, "launch_us": round(t * 1e6, 2),
+            "note": "timed alone after the timed region (HIP events); achieved counts the bf16 MFMA FLOPs issued "
+                    "(3 exact-split products per fp32 product), achieved_fp32_equiv the algorithmic ones"}
 
 
-def load_traffic(tag):
-    p = os.path.join(ROOT, "profiles", f"traffic_{tag}.json")
-    if os.path.exists(p):
-        with open(p) as f:
-            return json.load(f).get("gather_hbm_bytes_per_launch")
+def load_traffic(tag, key):
+    """HBM bytes per launch of a kernel from the committed PMC summary of a tagged rocprofv3
+    pass (scripts/summarize_profile.py TAG: separate --pmc FETCH_SIZE / WRITE_SIZE runs,
+    gfx950-corrected) -> (bytes or None, source)"""
+    p = os.path.join("profiles", f"traffic_{tag}.json")
+    full = os.path.join(ROOT, p)
+    if os.path.exists(full):
+        with open(full) as f:
+            return json.load(f).get(key), p
+    return None, None
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
     return None
 
 
 # ----------------------------------------------------------------------------- CPU baseline
-def cpu_baseline(n_actors=256, batch=512, capacity=20000, iters=6, seed=0):
+def cpu_baseline(n_actors=256, batch=512, capacity=1_000_000, ring=20000, iters=6, seed=0):
     """The same Ape-X step on the host: torch-CPU Q-net (all host threads the job owns),
     the oracle's C restatement for tree / PER / n-step / eps-greedy, numpy for the env and
-    row storage.  Replay capacity is reduced (host RAM, fill time); the per-step work is
-    the full configuration (256 actors, B = 512)."""
+    row storage.  The sum-tree has the full capacity (1 M slots, depth 20); only the frame
+    storage is a reduced ring of `ring` rows (slot % ring: host RAM and fill time); the
+    per-step work is the full configuration (256 actors, B = 512)."""
     from oracle import oracle as orc
     from reth_amd.model import DQNNetwork
 
@@ -115,11 +141,11 @@ def cpu_baseline(n_actors=256, batch=512, capacity=20000, iters=6, seed=0):
     tq.load_state_dict(qn.state_dict())
     an.load_state_dict(qn.state_dict())
     opt = torch.optim.Adam(qn.parameters(), lr=1e-4, eps=1.5e-4)
-    s0s = rng.integers(0, 256, (capacity, 4, 84, 84), dtype=np.uint8)
-    s1s = rng.integers(0, 256, (capacity, 4, 84, 84), dtype=np.uint8)
-    acol = rng.integers(0, 6, capacity)
-    rcol = np.zeros(capacity, np.float32)
-    dcol = np.zeros(capacity, np.float32)
+    s0s = rng.integers(0, 256, (ring, 4, 84, 84), dtype=np.uint8)
+    s1s = rng.integers(0, 256, (ring, 4, 84, 84), dtype=np.uint8)
+    acol = rng.integers(0, 6, ring)
+    rcol = np.zeros(ring, np.float32)
+    dcol = np.zeros(ring, np.float32)
     tree = orc.Tree(capacity)
     tree.update(np.arange(capacity), orc.per_normalize(1.0 - rng.random(capacity, dtype=np.float32), 0.5)
                 .astype(np.float64))
@@ -165,21 +191,23 @@ def cpu_baseline(n_actors=256, batch=512, capacity=20000, iters=6, seed=0):
             d_ = np.array([x[4] for x in rows], np.float32)
             td = orc.td_error(qq[:n], qq[n:], qq[n:], a_, r_, d_, gamma_n)
             slots, tail = orc.fifo_indices(capacity, tail, n)
-            s0s[slots], s1s[slots], acol[slots], rcol[slots], dcol[slots] = s0, s1, a_, r_, d_
+            rs = slots % ring
+            s0s[rs], s1s[rs], acol[rs], rcol[rs], dcol[rs] = s0, s1, a_, r_, d_
             tree.update(slots, orc.per_normalize(np.abs(td), 0.5).astype(np.float64))
         # learner update (DQNSolver.update on the CPU)
         idx, p = tree.sample(rng.random(batch))
         isw = orc.per_is_weights(p, tree.min(), 0.4)
-        b0 = torch.from_numpy(s0s[idx]).float()
-        b1 = torch.from_numpy(s1s[idx]).float()
+        ri = idx % ring
+        b0 = torch.from_numpy(s0s[ri]).float()
+        b1 = torch.from_numpy(s1s[ri]).float()
         qv = qn(b0)
         with torch.no_grad():
             nt = tq(b1)
             no = qn(b1)
-        a_t = torch.from_numpy(acol[idx])
-        tdt = qv.gather(1, a_t[:, None])[:, 0] - (torch.from_numpy(rcol[idx]) + float(gamma_n) *
+        a_t = torch.from_numpy(acol[ri])
+        tdt = qv.gather(1, a_t[:, None])[:, 0] - (torch.from_numpy(rcol[ri]) + float(gamma_n) *
                                                   nt.gather(1, no.argmax(1, keepdim=True))[:, 0] *
-                                                  (1 - torch.from_numpy(dcol[idx])))
+                                                  (1 - torch.from_numpy(dcol[ri])))
         loss = (torch.nn.functional.smooth_l1_loss(tdt, torch.zeros_like(tdt), reduction="none") *
                 torch.from_numpy(isw).float()).mean()
         opt.zero_grad()
@@ -195,9 +223,10 @@ def cpu_baseline(n_actors=256, batch=512, capacity=20000, iters=6, seed=0):
         step(t)
     dt = time.perf_counter() - t0
     return {"value": round(n_actors * iters / dt, 2), "unit": "env-steps/s", "cores": cores, "kind": "port",
-            "updates_per_sec": round(iters / dt, 3),
-            "sample": f"{iters} Ape-X steps (256 actors x 1 env step + 1 B=512 update each), replay capacity "
-                      f"{capacity} rows on the host, torch-CPU Q-net + oracle C tree/PER/n-step, "
+            "updates_per_sec": round(iters / dt, 3), "cpu_model": cpu_model(),
+            "sample": f"{iters} Ape-X steps (256 actors x 1 env step + 1 B=512 update each), sum-tree of "
+                      f"{capacity} slots (depth {int(np.ceil(np.log2(capacity + 1)))}), frame storage a ring of "
+                      f"{ring} rows on the host, torch-CPU Q-net + oracle C tree/PER/n-step, "
                       f"{torch.get_num_threads()} threads, {dt:.1f} s"}
 
 
@@ -205,7 +234,7 @@ def cpu_baseline(n_actors=256, batch=512, capacity=20000, iters=6, seed=0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="pong",
                     help="pong = BASELINE configs[1] (the metric's workload); breakout = configs[2] (2048 actors, "
@@ -213,10 +242,16 @@ def main():
     ap.add_argument("--actors", type=int, default=None)
     ap.add_argument("--capacity", type=int, default=None)
     ap.add_argument("--batch", type=int, default=512)
+    ap.add_argument("--faithful", action="store_true",
+                    help="SURVEY §8(d) C4 hyperparameter-faithful data parallelism: a global batch of --batch "
+                         "split over the N learners (B / N per GPU) instead of B per GPU")
+    ap.add_argument("--windows", type=int, default=5, help="sub-windows of the timed region reported beside it")
+    ap.add_argument("--no-probe", action="store_true", help="do not cut the learner graph around conv2 "
+                    "(no live per-launch timing of the dominant kernel)")
     ap.add_argument("--actor-steps-per-update", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-iters", type=int, default=72)
-    ap.add_argument("--tag", default="r01")
+    ap.add_argument("--tag", default="r02", help="profiles/traffic_TAG.json: the PMC pass the traffic fields cite")
     ap.add_argument("--nchw", action="store_true", help="contiguous NCHW Q-net tensors (default channels-last)")
     ap.add_argument("--no-conv-benchmark", action="store_true", help="MIOpen immediate mode instead of find")
     ap.add_argument("--eager", action="store_true", help="no HIP-graph replay (launch every kernel from Python)")
@@ -238,14 +273,27 @@ def main():
         local %= torch.cuda.device_count()
     torch.cuda.set_device(local)
     rank, world = init_from_env()
-    if world != args.gpus and world_env > 1:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    if world != args.gpus:
+        raise SystemExit(f"bench.py --gpus {args.gpus} but the process group has {world} rank(s) "
+                         f"(WORLD_SIZE={world_env}): launch N > 1 under torch.distributed.run")
+    backend = dist.get_backend() if world > 1 else None
+    if world > 1 and rank == 0:
+        print(f"data-parallel learner: {world} ranks over {backend} "
+              f"({'RCCL' if backend == 'nccl' else backend}), one GPU each", file=sys.stderr, flush=True)
     dev = torch.device("cuda", local)
-    cfg = ApexConfig(n_actors=args.actors, capacity=args.capacity, batch_size=args.batch, num_actions=wl["actions"],
+    per_gpu_batch = args.batch
+    if args.faithful:
+        if args.batch % world:
+            raise SystemExit(f"--faithful: global batch {args.batch} does not split over {world} GPUs")
+        per_gpu_batch = args.batch // world
+    hip_conv = not args.miopen_conv
+    probe = hip_conv and not args.nchw and not args.eager and not args.no_probe
+    cfg = ApexConfig(n_actors=args.actors, capacity=args.capacity, batch_size=per_gpu_batch, num_actions=wl["actions"],
                      actor_steps_per_update=args.actor_steps_per_update, seed=0,
                      channels_last=not args.nchw, conv_benchmark=not args.no_conv_benchmark,
-                     hip_graph=not args.eager, hip_conv=not args.miopen_conv,
-                     extra={"learner_priority": int(os.environ.get("RTH_LEARNER_PRIORITY", "0"))})
+                     hip_graph=not args.eager, hip_conv=hip_conv,
+                     extra={"learner_priority": int(os.environ.get("RTH_LEARNER_PRIORITY", "0")),
+                            "probe_conv2": probe})
     ax = ApexDQN(cfg, device=dev, rank=rank, world=world)
     ax.prefill(cfg.capacity)
     for _ in range(args.warmup):
@@ -259,6 +307,17 @@ def main():
         return e
 
     ax.loader.gather_timer = timer
+    # the dominant kernel, live: events on the learner stream around its conv2 launch (the
+    # learner graph is cut there: ApexDQN._learner_replay calls conv_probe between parts)
+    conv2_events = []
+
+    def conv_probe(tag):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        if tag == "conv2":
+            conv2_events.append([e, None])
+        elif conv2_events and conv2_events[-1][1] is None:
+            conv2_events[-1][1] = e
     spans = []
     if os.environ.get("RTH_BENCH_SPAN"):  # diagnostics: the learner block's span on its stream
         replay = ax._learner_replay
@@ -287,23 +346,36 @@ def main():
 
         ax._ev_sample = _Ready(ax._ev_sample)
     u0, e0 = ax.updates, ax.env_steps
-    u0, e0 = ax.updates, ax.env_steps
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    ax.conv_probe = conv_probe
+    # sub-window boundaries: events on the iteration stream (no synchronisation inside the
+    # timed region); the headline is the whole region
+    n_win = max(1, min(args.windows, args.steps))
+    win_at = {round(args.steps * i / n_win) for i in range(n_win + 1)}
+    win_ev = []
     t0 = time.perf_counter()
     debug = os.environ.get("RTH_BENCH_DEBUG")
     for k in range(args.steps):
+        if k in win_at:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(ax._stream if hasattr(ax, "_stream") else None)
+            win_ev.append((k, e))
         ax.iteration()
         if debug:
             torch.cuda.synchronize()
             print(f"rank {rank} step {k}: {1e3 * (time.perf_counter() - t0):.1f} ms graphs={ax._graphs is not None} "
                   f"updates={ax.updates} pending={ax.loader.pending()}", file=sys.stderr, flush=True)
+    e = torch.cuda.Event(enable_timing=True)
+    e.record(ax._stream)
+    win_ev.append((args.steps, e))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
     ax.loader.gather_timer = None
+    ax.conv_probe = None
     n_upd, n_env = ax.updates - u0, ax.env_steps - e0
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
@@ -322,6 +394,17 @@ def main():
             late = [spans[i][1].elapsed_time(ready[i]) * 1e3 for i in range(m)]
             print(f"next batch ready after the learner block ends: mean {np.mean(late):.1f} us, median "
                   f"{np.median(late):.1f}, > 0 in {np.mean(np.array(late) > 0) * 100:.0f} % of updates", file=sys.stderr)
+    win_ms = [a[1].elapsed_time(b[1]) / (b[0] - a[0]) for a, b in zip(win_ev, win_ev[1:])]
+    conv2_ms = [a.elapsed_time(b) for a, b in conv2_events if b is not None]
+    replicas = None
+    if world > 1:  # the data-parallel replicas must hold identical parameters
+        with torch.no_grad():
+            hsum = torch.stack([p.double().sum() for p in ax.solver.q_network.parameters()]).sum()
+            hsq = torch.stack([p.double().square().sum() for p in ax.solver.q_network.parameters()]).sum()
+        mine = torch.stack([hsum, hsq]).to(dev)
+        allh = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(allh, mine)
+        replicas = all(torch.equal(allh[0], h) for h in allh[1:])
     gather_ms = [a.elapsed_time(b) for a, b in events]
     mean_gather_s = float(np.mean(gather_ms)) / 1e3
     bytes_launch = gather_bytes_per_row(cfg.hip_conv and cfg.channels_last) * cfg.batch_size
@@ -338,7 +421,7 @@ def main():
         iso.append((e0, e1))
     torch.cuda.synchronize()
     iso_s = float(np.median([a.elapsed_time(b) for a, b in iso[5:]])) / 1e3
-    conv = conv_roofline(ax, slot_cols) if cfg.hip_conv and cfg.channels_last else None
+    conv1 = conv1_roofline(ax, slot_cols) if cfg.hip_conv and cfg.channels_last else None
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
@@ -354,7 +437,33 @@ def main():
     flops_actor = cfg.n_actors * f * args.actor_steps_per_update
     flops_step = flops_update + flops_actor
     step_s = dt / args.steps
-    traffic = load_traffic(args.tag)
+    traffic, traffic_src = load_traffic(args.tag, "gather_hbm_bytes_per_launch")
+    c2_traffic, c2_src = load_traffic(args.tag, "conv2_learner_hbm_bytes_per_launch")
+    roofline_gather = {
+        "kernel": "rth_replay_gather (k_copy_rows: PER-sampled rows, frames %s)"
+                  % ("uint8 stacks" if cfg.hip_conv and cfg.channels_last else "u8->f32 NHWC"),
+        "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
+        "bytes_per_launch": bytes_launch, "mean_launch_us": round(mean_gather_s * 1e6, 2),
+        "launches_timed": len(gather_ms), "isolated_launch_us": round(iso_s * 1e6, 2),
+        "isolated_frac": round(bytes_launch / iso_s / 1e9 / HBM_PEAK_GBS, 4),
+        "note": "in the timed region the gather overlaps the learner block on a second stream"}
+    roofline = roofline_gather
+    if conv2_ms:
+        n2 = 2 * cfg.batch_size  # the learner's [s0; s1] forward
+        c2_flops = 2.0 * n2 * 9 * 9 * 64 * 32 * 4 * 4
+        c2_s = float(np.mean(conv2_ms)) / 1e3
+        roofline = {
+            "kernel": f"k_conv_bias_relu conv2 (fp32 MFMA; 32x20x20 -> 64x9x9, k4 s2) in the learner's [s0; s1] "
+                      f"forward, {n2} samples per launch",
+            "bound": "mfma", "achieved": round(c2_flops / c2_s / 1e12, 2), "peak": FP32_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(c2_flops / c2_s / 1e12 / FP32_PEAK_TFLOPS, 4),
+            "traffic": c2_traffic, "traffic_source": c2_src, "flops_per_launch": c2_flops,
+            "algorithmic_bytes_per_launch": n2 * (20 * 20 * 32 + 9 * 9 * 64) * 4 + 64 * 512 * 4 + 64 * 4,
+            "mean_launch_us": round(c2_s * 1e6, 2), "median_launch_us": round(float(np.median(conv2_ms)) * 1e3, 2),
+            "launches_timed": len(conv2_ms),
+            "note": "timed live over the timed region: HIP events on the learner stream around the launch (the "
+                    "learner graph is cut there); it runs concurrently with the actor stream's kernels"}
     out = {
         "metric": "env-steps/sec + learner updates/sec, Ape-X DQN Pong, 1/2/4/8 MI355X",
         "value": round(n_env / dt, 1),
@@ -364,6 +473,8 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(step_s * 1e3, 3),
+        "ms_per_step_windows": [round(w, 4) for w in win_ms],
+        "ms_per_step_window_median": round(float(np.median(win_ms)), 4) if win_ms else None,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -375,20 +486,18 @@ def main():
                    "actor_steps_per_update": cfg.actor_steps_per_update,
                    "qnet_layout": "channels_last" if cfg.channels_last else "nchw",
                    "conv_benchmark": cfg.conv_benchmark, "hip_graph": cfg.hip_graph, "hip_conv": cfg.hip_conv,
+                   "global_batch": cfg.batch_size * world,
+                   "batch_mode": "hyperparameter-faithful (global batch split over the learners)" if args.faithful
+                                 else "throughput (B per GPU)",
                    "parallelism": f"dp{world} learner (RCCL grad all-reduce) + {world} replay shards"},
-        "roofline": {"kernel": "rth_replay_gather (k_copy_rows: PER-sampled rows, frames %s)"
-                     % ("uint8 stacks" if cfg.hip_conv and cfg.channels_last else "u8->f32 NHWC"),
-                     "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "bytes_per_launch": bytes_launch, "mean_launch_us": round(mean_gather_s * 1e6, 2),
-                     "launches_timed": len(gather_ms),
-                     "isolated_launch_us": round(iso_s * 1e6, 2),
-                     "isolated_frac": round(bytes_launch / iso_s / 1e9 / HBM_PEAK_GBS, 4),
-                     "note": "in the timed region the gather overlaps the learner block on a second stream"},
+        "dist": {"world": world, "backend": backend, "rccl": backend == "nccl",
+                 "replicas_identical": replicas} if world > 1 else None,
+        "roofline": roofline,
+        "roofline_gather": roofline_gather,
         "qnet_mfma": {"tflops_per_step": round(flops_step / 1e12, 4),
                       "achieved_tflops": round(flops_step / step_s / 1e12, 2),
                       "peak_fp32_tflops": FP32_PEAK_TFLOPS},
-        "roofline_conv": conv,
+        "roofline_conv1": conv1,
         "cpu_baseline": cpu,
     }
     print(json.dumps(out), flush=True)

@@ -119,6 +119,7 @@ class ApexDQN:
         self._graphs = None
         self._ev_acquired = None
         self.actor_modes = {}  # graph mode: actor steps replayed per mode ("dedup" / "full")
+        self.conv_probe = None  # extra["probe_conv2"]: callable(tag) between the learner graph's parts
 
     def close(self):
         _SERVICES.pop(self.addr, None)
@@ -257,26 +258,29 @@ class ApexDQN:
             for variant in ("full", "pre"):
                 for p in range(2):
                     v = (variant, p)
-                    parts, buckets = [torch.cuda.CUDAGraph()], []
+                    parts, bounds = [torch.cuda.CUDAGraph()], []
 
-                    def cut(bucket, parts=parts, buckets=buckets):
-                        # end this part of the learner graph at a final gradient bucket: its
-                        # all-reduce runs between the parts (overlapping the next one)
+                    def cut(item, parts=parts, bounds=bounds):
+                        # end this part of the learner graph at a boundary: ("bucket", a final
+                        # gradient bucket -- its all-reduce runs between the parts, overlapping
+                        # the next one) or ("probe", (tag, launch) -- a launch issued eagerly between
+                        # the parts at every replay, bracketed by the bench's HIP events)
                         parts[-1].capture_end()
-                        buckets.append(bucket)
+                        bounds.append(item)
                         parts.append(torch.cuda.CUDAGraph())
                         parts[-1].capture_begin(pool=parts[0].pool())
 
                     parts[0].capture_begin()
                     data, idx, isw = slots[p]
+                    probe = (lambda tag, fn: cut(("probe", (tag, fn)))) if self.cfg.extra.get("probe_conv2") else None
                     td = solver.compute_grads(data, isw, q1t=G["q1t"][p] if variant == "pre" else None,
-                                              mid=cut if split else None)
+                                              mid=(lambda b: cut(("bucket", b))) if split else None, probe=probe)
                     self.trainer._track(td)
-                    if split and not buckets:  # autograd path: one bucket, every .grad
-                        cut([q.grad for q in solver._params])
+                    if split and not any(k == "bucket" for k, _ in bounds):  # autograd path: one bucket
+                        cut(("bucket", [q.grad for q in solver._params]))
                     solver.apply_grads()
                     parts[-1].capture_end()
-                    G["learn"][v], G["buckets"][v], G["learn_td"][v] = parts, buckets, td
+                    G["learn"][v], G["buckets"][v], G["learn_td"][v] = parts, bounds, td
                     G["grads"][v] = [q.grad for q in solver._params]  # what apply_grads consumed
         torch.cuda.current_stream(self.device).wait_stream(side)
         self.actors.t, self.actors.pushes = host  # capture recorded, did not run, the steps
@@ -296,29 +300,45 @@ class ApexDQN:
         self._learner_host()
 
     def _learner_replay(self, v):
-        """replay learner graph v on the current stream.  Split (data-parallel) learner: every
-        bucket but the last is all-reduced on a side stream while the following part runs (the
-        merged heads' gradients, 95 % of the bytes, under the conv backward); the last one on
-        this stream; the final part (heads split + clip + Adam) waits for all of them."""
+        """replay learner graph v on the current stream.  Its parts are cut at boundaries:
+        gradient buckets (data-parallel learner: every bucket but the last is all-reduced on a
+        side stream while the following part runs -- the merged heads' gradients, 95 % of the
+        bytes, under the conv backward; the last one on this stream; the final part (heads
+        split + clip + Adam) waits for all of them) and probes (a launch issued eagerly between
+        the parts, bracketed by conv_probe(tag) / conv_probe(tag + "_end"): the bench records
+        HIP events there on this stream for its live per-launch timing)."""
         G = self._graphs
-        parts, buckets = G["learn"][v], G["buckets"][v]
+        parts, bounds = G["learn"][v], G["buckets"][v]
         if len(parts) == 1:
             parts[0].replay()
             return
         hook = self.solver.grad_hook
         cur = torch.cuda.current_stream(self.device)
-        if not hasattr(self, "_stream_comm"):
-            self._stream_comm = torch.cuda.Stream(self.device)
-        comm = self._stream_comm
-        for i, (g, bucket) in enumerate(zip(parts, buckets)):
+        bucket_at = [i for i, (kind, _) in enumerate(bounds) if kind == "bucket"]
+        comm = None
+        for i, (g, (kind, item)) in enumerate(zip(parts, bounds)):
             g.replay()
-            if i + 1 < len(buckets):
+            if kind == "probe":  # a launch issued between the parts, optionally between HIP events
+                tag, fn = item
+                if self.conv_probe is not None:
+                    self.conv_probe(tag)
+                fn()
+                if self.conv_probe is not None:
+                    self.conv_probe(tag + "_end")
+                continue
+            key = ("bucket", bucket_at.index(i))
+            if i != bucket_at[-1]:
+                if comm is None:
+                    if not hasattr(self, "_stream_comm"):
+                        self._stream_comm = torch.cuda.Stream(self.device)
+                    comm = self._stream_comm
                 comm.wait_stream(cur)
                 with torch.cuda.stream(comm):
-                    hook.reduce(bucket, key=("bucket", i))
+                    hook.reduce(item, key=key)
             else:
-                hook.reduce(bucket, key=("bucket", i))
-        cur.wait_stream(comm)
+                hook.reduce(item, key=key)
+        if comm is not None:
+            cur.wait_stream(comm)
         parts[-1].replay()
 
     def _actor_block_graph(self):

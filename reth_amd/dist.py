@@ -3,9 +3,12 @@
 The reference has no collective at all (one learner, ZeroMQ everywhere).
 Ape-X shards naturally: every GPU owns its actors and its replay shard (the reference's
 K shards of capacity C // K, test/apex-dqn/trainer.py:52-61), so the only exchange step is
-the learner's gradient.  It is one flat fp32 bucket (1.69 M params = 6.7 MB for Pong)
-all-reduced once per update -- on xGMI a ring all-reduce of 6.7 MB is ~80 us, small next
-to the Q-net backward, so there is no bucketing/overlap machinery.
+the learner's gradient: 1.69 M fp32 params = 6.7 MB for Pong per update.  It goes in two
+flat buckets: the merged dueling heads' gradients (95 % of the bytes, final right after the
+FC backward) are all-reduced on a side stream while the conv backward runs, the conv
+gradients on the learner's stream after it, and the final part of the update (heads split
++ clip + Adam) waits for both (ApexDQN._capture / _learner_replay).  The eager learner
+reduces everything as one bucket.
 """
 import torch
 import torch.distributed as dist

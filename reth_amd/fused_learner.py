@@ -61,7 +61,7 @@ def _nhwc(t):
     return t if t.is_contiguous(memory_format=torch.channels_last) else t.contiguous(memory_format=torch.channels_last)
 
 
-def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None, mid=None):
+def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None, mid=None, probe=None):
     """forward + TD + backward of one learner batch; sets .grad of every online parameter
     and returns (loss [], |td| [B]).  q1t: the target network's heads on s1 if precomputed
     (DQNSolver.target_heads).  td_acc (nullable f32 device scalar): += mean |td|.
@@ -70,7 +70,12 @@ def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None, mid=No
     merged heads' [gw1, gb1, gw2, gb2] (before the conv backward), then the conv weights' and
     biases' (before the heads are split back onto the branch parameters).  The data-parallel
     capture ends a graph there, so the all-reduce of the first bucket overlaps the conv
-    backward; whatever mid's caller does to a bucket in place is what the parameters get."""
+    backward; whatever mid's caller does to a bucket in place is what the parameters get.
+
+    probe (optional callable) is handed the forward's conv2 launch as probe("conv2", launch)
+    and issues it itself (the bench times that launch live: the capture cuts the learner graph
+    there, and every replay launches it eagerly between HIP events on the learner stream; its
+    buffers live in the graph's pool at fixed addresses)."""
     from .solver import td_huber_forward
 
     net = solver.q_network
@@ -91,8 +96,13 @@ def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None, mid=No
             wo = (shape.win - shape.kw) // shape.stride + 1
             y = torch.empty((n, shape.cout, ho, wo), dtype=torch.float32, device=x.device,
                             memory_format=torch.channels_last)
-            call("rth_conv_bias_relu", ctypes.byref(shape), ptr(h), None, n, ptr(net._packed_for(packed, li, u8)),
-                 ptr(conv.bias), ptr(y), st)
+            def launch(shape=shape, h=h, pk=net._packed_for(packed, li, u8), b=conv.bias, y=y):
+                call("rth_conv_bias_relu", ctypes.byref(shape), ptr(h), None, n, ptr(pk), ptr(b), ptr(y), stream_ptr())
+
+            if probe is not None and li == 1:
+                probe("conv2", launch)  # the prober issues it: now, or at every replay of a captured pass
+            else:
+                launch()
             ys.append(y)
             h = y
         feat = h.permute(0, 2, 3, 1).reshape(n, -1)  # NHWC flatten: a view
@@ -149,10 +159,12 @@ def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None, mid=No
                 gw = torch.empty(conv.weight.shape, dtype=torch.float32, device=x.device,
                                  memory_format=torch.channels_last)
                 db = torch.empty(conv.out_channels, dtype=torch.float32, device=x.device)
+                assert len(deferred) <= 4, "rth_conv_relu_wgrad_ex finishes at most 4 deferred bias gradients"
                 jobs = (_lib.BiasDeferred * max(len(deferred), 1))(*deferred)
                 call("rth_conv_relu_wgrad_ex", ctypes.byref(shapes[0]), ptr(x), None, B, ptr(_nhwc(g)), ptr(y),
                      ptr(gw), ptr(db), ptr(_wgrad_workspace(shapes[0], x.device)), jobs, len(deferred), st)
                 grads[conv.weight], grads[conv.bias] = gw, db
+                deferred = []  # consumed
                 break
             g = _nhwc(g)
             gy = torch.empty_like(y)
@@ -173,6 +185,9 @@ def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None, mid=No
                 call("rth_conv_dgrad", ctypes.byref(shapes[li]), ptr(gy), B, ptr(w), ptr(gx), st)
             grads[conv.weight], grads[conv.bias] = gw, db
             g = gx
+        # every deferred bias gradient was finished by conv1's launch (else its db would be
+        # uninitialised memory handed to the optimizer)
+        assert not deferred, "deferred bias gradients left unfinished"
         if mid is not None:
             mid([t for c in convs for t in (grads[c.weight], grads[c.bias])])
         # merged heads -> the eight branch parameters

@@ -242,7 +242,7 @@ class DQNSolver(Algorithm):
     def calc_loss(self, batch):
         return self.calc_loss_device(batch).cpu()
 
-    def compute_grads(self, batch, weights=None, q1t=None, mid=None):
+    def compute_grads(self, batch, weights=None, q1t=None, mid=None, probe=None):
         """dqn_solver.py:104-117: forward passes, fused TD/Huber, backward -> |td| (device).
         q1t: the target network's output on this batch's s1 if already computed
         (target_heads), else it is computed here.  mid: gradient-bucket callback of the
@@ -251,7 +251,7 @@ class DQNSolver(Algorithm):
         isw = None if weights is None else (weights if torch.is_tensor(weights) else torch.as_tensor(np.asarray(weights)))
         if self.fused_grads and self._heads and fused_learner.eligible(self.q_network, s0, s1):
             loss, td_abs = fused_learner.dueling_grads(self, s0, a, r, s1, done, isw, q1t, td_acc=self.td_mean_acc,
-                                                        mid=mid)
+                                                        mid=mid, probe=probe)
             if self.td_mean_acc is not None:
                 td_abs._rth_mean_tracked = True
             self.last_loss = loss.detach()

@@ -79,5 +79,15 @@ for step in "$@"; do
             -d "$PWD/gpurun_out/prof" -o run -- python bench.py --steps 100 --warmup 20 --no-cpu-baseline ;;
     prof) export TMPDIR=/tmp; run rocprof_stats 900 rocprofv3 --kernel-trace --stats --output-format csv \
             -d "$PWD/gpurun_out/prof" -o run -- python bench.py --steps 100 --warmup 10 --no-cpu-baseline ;;
+    # the evidence set for a round: the bench line, its rocprof kernel trace + stats, and the two
+    # PMC passes of the same command (scripts/summarize_profile.py TAG --steps 200 reads them)
+    evidence) export TMPDIR=/tmp
+         run bench_evidence 900 python bench.py &&
+         run rocprof_stats 900 rocprofv3 --kernel-trace --stats --output-format csv \
+            -d "$PWD/gpurun_out/prof" -o run -- python bench.py --steps 200 --warmup 20 --no-cpu-baseline &&
+         run pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv --kernel-include-regex "rth::" \
+            -d "$PWD/gpurun_out/pmc_fetch" -o run -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline &&
+         run pmc_write 900 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv --kernel-include-regex "rth::" \
+            -d "$PWD/gpurun_out/pmc_write" -o run -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
   esac
 done

@@ -8,8 +8,10 @@ WRITE_SIZE passes), writes
     profiles/TAG_kernel_stats.csv        rocprofv3's own --stats table
     profiles/TAG_steady_state.txt        per-iteration kernel breakdown (timed window)
     profiles/TAG_gather_launches.txt     the learner gather's launches by grid (avg duration)
+    profiles/TAG_conv2_launches.txt      conv2 forward launches by grid (the dominant kernel)
     profiles/TAG_pmc.txt                 FETCH/WRITE per kernel and grid, gfx950-corrected
-    profiles/traffic_TAG.json            HBM bytes per learner-gather launch (bench.py reads it)
+    profiles/traffic_TAG.json            HBM bytes per launch of the learner gather and of the learner's
+                                         conv2 (bench.py cites it)
 FETCH_SIZE on gfx950 reports half the bytes of a wide coalesced read (MI355X_MICROARCH.md
 §HBM): it is doubled; WRITE_SIZE is exact for 16-byte stores.  Both are in KiB.
 """
@@ -27,6 +29,7 @@ PROF = os.path.join(ROOT, "profiles")
 # learner gather launch (k_copy_rows flat grid): B rows x 2 frame columns x 7 chunks of 4 KiB
 # + the small columns one lane per 4-byte word, 256 threads per workgroup
 LEARNER_GATHER_GRID = (512 * 2 * 7 + 4 + 2 + 2) * 256  # a: 2 words/row, r and done: 1 word/row, 256 lanes/WG
+CONV2 = "k_conv_bias_relu<0, 4, 4, 2, 32, 64, 20, 20"  # conv2 forward (the step's dominant kernel)
 
 
 def main():
@@ -50,6 +53,7 @@ def main():
             a[0] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
             a[1] += 1
         busy = sum(v[0] for v in agg.values())
+        learner_stream = next((r.get("Stream_Id") for r in reversed(win) if "k_adam" in r["Kernel_Name"]), None)
         with open(os.path.join(PROF, f"{tag}_steady_state.txt"), "w") as f:
             f.write(f"# last {steps} iterations of the profiled bench run\n")
             f.write(f"window {((end - start) / 1e6):.3f} ms, kernel-busy {busy / 1e6:.3f} ms, "
@@ -58,17 +62,21 @@ def main():
             f.write(f"{'share':>7} {'us/iter':>9} {'calls/iter':>10}  kernel\n")
             for k, v in sorted(agg.items(), key=lambda kv: -kv[1][0]):
                 f.write(f"{v[0] / busy * 100:6.2f}% {v[0] / 1e3 / steps:9.2f} {v[1] / steps:10.2f}  {k}\n")
-        by_grid = collections.defaultdict(list)
-        for r in win:
-            if "k_copy_rows" in r["Kernel_Name"]:
-                g = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"])
-                by_grid[(r["Grid_Size_X"], r["Grid_Size_Y"])].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
-        with open(os.path.join(PROF, f"{tag}_gather_launches.txt"), "w") as f:
-            f.write("# rth::k_copy_rows launches in the timed window, by grid (threads x, y)\n")
-            f.write("# (512*256, 5) = learner gather (rth_replay_gather, B=512, 5 columns)\n")
-            for k, v in sorted(by_grid.items()):
-                f.write(f"grid={k} launches={len(v)} avg_us={st.mean(v) / 1e3:.2f} min_us={min(v) / 1e3:.2f} "
-                        f"max_us={max(v) / 1e3:.2f}\n")
+        for name, fn, head in (
+                ("k_copy_rows", "gather_launches", "# (512*256, 5) = learner gather (rth_replay_gather, B=512, 5 columns)"),
+                (CONV2, "conv2_launches", "# learner stream = the learner's [s0; s1] forward (2B = 1024 samples; "
+                                          "bench.py's live roofline); the actor stream: target pass (512), actors (256)")):
+            by_grid = collections.defaultdict(list)
+            for r in win:
+                if name in r["Kernel_Name"]:
+                    where = "learner stream" if r.get("Stream_Id") == learner_stream else f"stream {r.get('Stream_Id')}"
+                    by_grid[(r["Grid_Size_X"], r["Grid_Size_Y"], where)].append(
+                        int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+            with open(os.path.join(PROF, f"{tag}_{fn}.txt"), "w") as f:
+                f.write(f"# {name} launches in the timed window, by grid (threads x, y)\n{head}\n")
+                for k, v in sorted(by_grid.items(), key=lambda kv: (int(kv[0][0]) * int(kv[0][1]), kv[0][2])):
+                    f.write(f"grid={k} launches={len(v)} avg_us={st.mean(v) / 1e3:.2f} min_us={min(v) / 1e3:.2f} "
+                            f"max_us={max(v) / 1e3:.2f}\n")
     pf = os.path.join(OUT, "pmc_fetch", "run_counter_collection.csv")
     pw = os.path.join(OUT, "pmc_write", "run_counter_collection.csv")
     if os.path.exists(pf) and os.path.exists(pw):
@@ -87,15 +95,23 @@ def main():
                 fv, wv = st.median(fe.get(k, [0])), st.median(wr.get(k, [0]))
                 f.write(f"{k[0]:24s} grid={k[1]:>9d} n={len(fe.get(k, [])):4d} FETCH_KiB={fv:12.1f} "
                         f"WRITE_KiB={wv:12.1f} hbm_MB={(2 * fv + wv) * 1024 / 1e6:10.2f}\n")
+        out = {"correction": "hbm bytes = (2 x FETCH_SIZE + WRITE_SIZE) x 1024 (gfx950 half-counts FETCH_SIZE "
+                             "on wide coalesced reads), median over the dispatches of each pass",
+               "passes": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE, separate runs of bench.py"}
         key = ("rth::k_copy_rows", LEARNER_GATHER_GRID)
         if key in fe and key in wr:
-            hbm = (2 * st.median(fe[key]) + st.median(wr[key])) * 1024
-            with open(os.path.join(PROF, f"traffic_{tag}.json"), "w") as f:
-                json.dump({"kernel": "rth::k_copy_rows (learner gather, B=512, 5 columns)",
-                           "gather_hbm_bytes_per_launch": round(hbm),
-                           "fetch_kib_median": st.median(fe[key]), "write_kib_median": st.median(wr[key]),
-                           "correction": "FETCH_SIZE x2 (gfx950 half-count on wide coalesced reads)",
-                           "dispatches": len(fe[key])}, f, indent=1)
+            out.update({"gather_kernel": "rth::k_copy_rows (learner gather, B=512, 5 columns)",
+                        "gather_hbm_bytes_per_launch": round((2 * st.median(fe[key]) + st.median(wr[key])) * 1024),
+                        "gather_dispatches": len(fe[key])})
+        c2 = [k for k in fe if CONV2 in k[0] and k in wr]
+        if c2:
+            key = max(c2, key=lambda k: k[1])  # the learner's launch: the largest grid
+            out.update({"conv2_kernel": key[0] + " (the learner's [s0; s1] forward: the largest grid, "
+                                                 f"{key[1]} threads)",
+                        "conv2_learner_hbm_bytes_per_launch": round((2 * st.median(fe[key]) + st.median(wr[key])) * 1024),
+                        "conv2_dispatches": len(fe[key])})
+        with open(os.path.join(PROF, f"traffic_{tag}.json"), "w") as f:
+            json.dump(out, f, indent=1)
     print("wrote", sorted(os.listdir(PROF)))
 
 

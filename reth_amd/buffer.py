@@ -51,7 +51,15 @@ def _copy_rows(dst, dst_rows, src, src_rows, n):
 
 
 class NumpyBuffer:
-    """buffer.py:4-98.  struct: [(dtype name, row shape), ...] or detected on first append."""
+    """buffer.py:4-98.  struct: [(dtype name, row shape), ...] or detected on first append.
+    device="cpu": the host buffer (host_buffer.HostNumpyBuffer: numpy columns, numpy draws)."""
+
+    def __new__(cls, *args, device=None, **kwargs):
+        if cls is NumpyBuffer and device is not None and torch.device(device).type == "cpu":
+            from .host_buffer import HostNumpyBuffer
+
+            return HostNumpyBuffer(*args, device=device, **kwargs)
+        return super().__new__(cls)
 
     def __init__(self, capacity, struct=None, circular=True, device=None, seed=0):
         self._capacity = int(capacity)

@@ -116,6 +116,15 @@ class Algorithm:
 
 
 class DQNSolver(Algorithm):
+    def __new__(cls, *args, device=None, **kwargs):
+        # device="cpu": the reference's host configuration (cpu_solver.CpuDQNSolver; BASELINE
+        # configs[0], the apex worker's actor copy) -- an explicit choice, never a fallback
+        if device is not None and torch.device(device).type == "cpu":
+            from .cpu_solver import CpuDQNSolver
+
+            return CpuDQNSolver(*args, device=device, **kwargs)
+        return super().__new__(cls)
+
     """reth/reth/algorithm/dqn/dqn_solver.py:14-143 with the same constructor arguments.
 
     grad_hook(params) runs between backward and clip/Adam: the data-parallel learner uses it

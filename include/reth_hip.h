@@ -455,6 +455,41 @@ int rth_clip_adam(const rth_param_tensor *tensors, int32_t n_tensors, double lr,
                   double eps, double max_norm, int64_t *step_dev, void *workspace_dev, float *total_norm_out_dev,
                   void *stream);
 
+/* ------------------------------------------------------------------------------------
+ * Learner -> actor weights: a device-resident latest-wins slot with a device version.
+ * Replaces perwez's PUB/SUB CONFLATE weights channel (perwez/perwez/client/socket.py:19-122,
+ * 302-328: SendSocket.send / RecvSocket.recv / RecvSocket.empty) as used by
+ * test/apex-dqn/trainer.py:38-41 (publish every send_weights_interval updates) and
+ * worker.py:37-41 (load when > recv_weights_interval steps passed and a message waits).
+ * Segments: the parameter tensors, 4-byte aligned, in a fixed order (<= 64).
+ * ---------------------------------------------------------------------------------- */
+typedef struct rth_weights rth_weights;
+int rth_weights_create(int64_t bytes, int device, rth_weights **out);
+int rth_weights_destroy(rth_weights *h);
+int64_t rth_weights_bytes(const rth_weights *h);
+/* SendSocket.send: copy the n segments into the slot, then version += 1 (stream order) */
+int rth_weights_publish(rth_weights *h, int32_t n, const void *const *src_dev, const int64_t *bytes, void *stream);
+/* RecvSocket.empty + recv, decided on the device: if version > *seen_dev (and, with a step
+ * counter, *step_dev - *prev_dev > interval) copy the slot into the n segments, set
+ * *seen_dev = version, *prev_dev = *step_dev and *loaded_dev = 1; else *loaded_dev = 0.
+ * step_dev / prev_dev / loaded_dev may be NULL.  Graph-capturable (no host decision). */
+int rth_weights_acquire(rth_weights *h, int32_t n, void *const *dst_dev, const int64_t *bytes, int64_t *seen_dev,
+                        const int64_t *step_dev, int64_t *prev_dev, int64_t interval, int32_t *loaded_dev,
+                        void *stream);
+int rth_weights_version(const rth_weights *h, int64_t *out);        /* synchronous read */
+int rth_weights_version_ptr(rth_weights *h, int64_t **out_dev);     /* the device counter */
+
+/* ------------------------------------------------------------------------------------
+ * LZ4 frames (host code) for compressed wire messages: Client.append(..., compress=True)
+ * (reth_buffer/reth_buffer/utils/pack.py:62-84 lz4.frame.compress / :147-164 decompress),
+ * what test/apex-dqn/worker.py:60 sends.  Host pointers.
+ * ---------------------------------------------------------------------------------- */
+int rth_lz4_frame_bound(const uint8_t *src, int64_t n, int64_t *bound);
+int rth_lz4_frame_decompress(const uint8_t *src, int64_t n, uint8_t *dst, int64_t cap, int64_t *out_len);
+int64_t rth_lz4_frame_compress_bound(int64_t n);
+int rth_lz4_frame_compress(const uint8_t *src, int64_t n, uint8_t *dst, int64_t cap, int64_t *out_len);
+uint32_t rth_xxh32(const uint8_t *src, int64_t n, uint32_t seed);
+
 #ifdef __cplusplus
 }
 #endif

@@ -152,6 +152,21 @@ SIGNATURES = {
     "rth_clip_adam_workspace": (c_i64, []),
     "rth_debug_tree_timing": (c_i32, [c_vp]),
     "rth_clip_adam": (c_i32, [c_vp, c_i32, c_f64, c_f64, c_f64, c_f64, c_f64, c_vp, c_vp, c_vp, c_vp]),
+    # learner -> actor weights slot (perwez PUB/SUB CONFLATE)
+    "rth_weights_create": (c_i32, [c_i64, c_i32, ctypes.POINTER(c_vp)]),
+    "rth_weights_destroy": (c_i32, [c_vp]),
+    "rth_weights_bytes": (c_i64, [c_vp]),
+    "rth_weights_publish": (c_i32, [c_vp, c_i32, ctypes.POINTER(c_vp), ctypes.POINTER(c_i64), c_vp]),
+    "rth_weights_acquire": (c_i32, [c_vp, c_i32, ctypes.POINTER(c_vp), ctypes.POINTER(c_i64), c_vp, c_vp, c_vp, c_i64,
+                                    c_vp, c_vp]),
+    "rth_weights_version": (c_i32, [c_vp, ctypes.POINTER(c_i64)]),
+    "rth_weights_version_ptr": (c_i32, [c_vp, ctypes.POINTER(c_vp)]),
+    # LZ4 frames (host)
+    "rth_lz4_frame_bound": (c_i32, [c_vp, c_i64, ctypes.POINTER(c_i64)]),
+    "rth_lz4_frame_decompress": (c_i32, [c_vp, c_i64, c_vp, c_i64, ctypes.POINTER(c_i64)]),
+    "rth_lz4_frame_compress_bound": (c_i64, [c_i64]),
+    "rth_lz4_frame_compress": (c_i32, [c_vp, c_i64, c_vp, c_i64, ctypes.POINTER(c_i64)]),
+    "rth_xxh32": (ctypes.c_uint32, [c_vp, c_i64, ctypes.c_uint32]),
 }
 
 _lib = None

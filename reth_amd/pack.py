@@ -7,7 +7,7 @@ server/main_loop.py:21-61 (append_loop, which stores each row message in LMDB).
 A message is
     [4-byte big-endian header length][msgpack header][body]
 with header = {"meta": ..., "body_len": n, "time": t} (plus KEY_COMPRESS when the body is
-an LZ4 frame).  `meta` mirrors the serialized object: lists / dicts recurse; an ndarray
+an LZ4 frame: csrc/lz4frame.cpp restates the frame format, no lz4 library is in the image).  `meta` mirrors the serialized object: lists / dicts recurse; an ndarray
 becomes {KEY_NUMPY: True, "header": numpy .npy header dict, "raw_size", "offset",
 "length"} pointing into the body; bytes-like objects become {KEY_BYTES: True, ...}.
 
@@ -18,6 +18,7 @@ is appended straight out of it (rows are equally spaced in the body when their h
 have equal length -- always, for fixed-shape columns), float32 frames are narrowed to the
 replay's uint8 storage by the copy kernel.
 """
+import ctypes
 import time
 
 import msgpack
@@ -56,13 +57,56 @@ def _walk_out(obj, chunks, pos):
     return obj
 
 
+def _u8(buf):
+    """a uint8 ndarray over a host buffer (bytes / bytearray / memoryview), no copy"""
+    return np.frombuffer(buf, dtype=np.uint8)
+
+
+def lz4_compress(data):
+    """lz4.frame.compress (pack.py:67): an LZ4 frame of `data` (csrc/lz4frame.cpp)"""
+    from ._lib import call, lib
+
+    src = _u8(data)
+    out = np.empty(lib().rth_lz4_frame_compress_bound(src.size), dtype=np.uint8)
+    m = ctypes.c_int64()
+    call("rth_lz4_frame_compress", src.ctypes.data if src.size else None, src.size, out.ctypes.data, out.size,
+         ctypes.byref(m))
+    return bytearray(out[:m.value])
+
+
+def lz4_decompress(frame):
+    """lz4.frame.decompress (pack.py:157): the content of an LZ4 frame, as a bytearray"""
+    from ._lib import call
+
+    src = _u8(frame)
+    bound = ctypes.c_int64()
+    call("rth_lz4_frame_bound", src.ctypes.data, src.size, ctypes.byref(bound))
+    out = bytearray(bound.value)
+    view = _u8(out)
+    m = ctypes.c_int64()
+    call("rth_lz4_frame_decompress", src.ctypes.data, src.size, view.ctypes.data if view.size else None, view.size,
+         ctypes.byref(m))
+    del view  # release the export before trimming
+    del out[m.value:]
+    return out
+
+
 def serialize(data, compress=False):
-    """pack.py:60-98 (compress needs an LZ4 frame codec; this image has none)"""
-    if compress:
-        raise NotImplementedError("LZ4-compressed messages need the lz4 codec, absent from this build")
+    """pack.py:60-98; compress=True puts the body into an LZ4 frame and marks the header
+    (the frame bytes differ from python-lz4's encoder -- any LZ4 decoder reads both)"""
     chunks, pos = [], [0]
     meta = _walk_out(data, chunks, pos)
-    header = msgpack.packb({"meta": meta, "body_len": pos[0], "time": time.time()})
+    if compress:
+        raw = bytearray(pos[0])
+        o = 0
+        for c in chunks:
+            raw[o:o + c.nbytes] = c
+            o += c.nbytes
+        body = lz4_compress(raw)
+        header = msgpack.packb({KEY_COMPRESS: True, "meta": meta, "body_len": len(body), "time": time.time()})
+        chunks, pos = [memoryview(body)], [len(body)]
+    else:
+        header = msgpack.packb({"meta": meta, "body_len": pos[0], "time": time.time()})
     out = bytearray(4 + len(header) + pos[0])
     out[:4] = len(header).to_bytes(4, "big")
     out[4:4 + len(header)] = header
@@ -108,12 +152,13 @@ def _walk_in(meta, body):
 
 
 def deserialize(data):
-    """pack.py:147-164 (views into `data`, like the reference)"""
+    """pack.py:147-164 (views into `data`, like the reference; a compressed body is
+    decompressed first and the views point into that copy)"""
     header, hlen = read_header(data)
     body = memoryview(data)[4 + hlen:]
     assert body.nbytes == header["body_len"]
     if header.get(KEY_COMPRESS):
-        raise NotImplementedError("LZ4-compressed messages need the lz4 codec, absent from this build")
+        body = memoryview(lz4_decompress(body))
     return _walk_in(header["meta"], body)
 
 
@@ -149,9 +194,10 @@ def ingest_append(replay, message, staging=None):
     columns match the row columns; float32 columns may land in uint8 storage), priorities =
     the message's weights.  Returns the number of rows."""
     header, hlen = read_header(message)
-    if header.get(KEY_COMPRESS):
-        raise NotImplementedError("LZ4-compressed messages need the lz4 codec, absent from this build")
     body = memoryview(message)[4 + hlen:]
+    if header.get(KEY_COMPRESS):  # worker.py:60 sends compress=True: decompress on the host first
+        body = memoryview(lz4_decompress(body))
+        staging = None
     rows_meta, w_meta = header["meta"]
     weights = _array_from(body, w_meta)
     n = len(rows_meta)

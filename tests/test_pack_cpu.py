@@ -55,5 +55,6 @@ def test_update_message(golden, pinned_time):
     assert np.array_equal(idx, np.arange(5)) and np.array_equal(w, g["app_w"][:5]) and step is True
     header, _ = pack.read_header(g["upd_msg"].tobytes())
     assert header["time"] == 1234.5 and header["body_len"] == idx.nbytes + w.nbytes
-    with pytest.raises(NotImplementedError):
-        pack.serialize([1], compress=True)
+    # compress=True: an LZ4-frame body (csrc/lz4frame.cpp; tests/test_lz4_cpu.py), same object back
+    idx2, w2, step2 = pack.deserialize(pack.serialize([idx, w, step], compress=True))
+    assert np.array_equal(idx2, idx) and np.array_equal(w2, w) and step2 is True

@@ -21,6 +21,11 @@ from . import _lib
 from ._lib import c_vp, call, stream_ptr
 
 
+def _dense(t):
+    """the bytes of t are one dense run (contiguous or channels_last): the slot copies raw bytes"""
+    return t.is_contiguous() or (t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last))
+
+
 def _segments(tensors):
     n = len(tensors)
     ptrs = (c_vp * n)(*[t.data_ptr() for t in tensors])
@@ -33,8 +38,10 @@ class WeightsSlot:
 
     def __init__(self, module):
         params = [p for p in module.parameters()]
-        if not params or any(not p.is_cuda or not p.is_contiguous() for p in params):
-            raise ValueError("WeightsSlot needs contiguous device parameters")
+        if not params or any(not p.is_cuda or not _dense(p) for p in params):
+            raise ValueError("WeightsSlot needs dense (contiguous or channels_last) device parameters")
+        # the slot holds raw bytes: publishers and consumers must share this layout
+        self.layout = [(tuple(p.shape), p.stride()) for p in params]
         self.device = params[0].device
         nbytes = sum(p.numel() * p.element_size() for p in params)
         h = c_vp()
@@ -55,7 +62,9 @@ class WeightsSlot:
     @torch.no_grad()
     def publish(self, module):
         """SendSocket.send: the module's parameters into the slot, version += 1"""
-        n, ptrs, nbytes = _segments([p.detach() for p in module.parameters()])
+        params = [p.detach() for p in module.parameters()]
+        self._check(params)
+        n, ptrs, nbytes = _segments(params)
         call("rth_weights_publish", self._h, n, ptrs, nbytes, stream_ptr())
         self.version += 1
 
@@ -66,6 +75,7 @@ class WeightsSlot:
         seen/step/prev: int64 device scalars (default: this slot's own seen counter), loaded:
         optional int32 device scalar set to 1 / 0.  Returns the host version mirror."""
         params = [p for p in module.parameters()]
+        self._check(params)
         n, ptrs, nbytes = _segments(params)
         call("rth_weights_acquire", self._h, n, ptrs, nbytes, (seen if seen is not None else self._seen).data_ptr(),
              None if step is None else step.data_ptr(), None if prev is None else prev.data_ptr(), int(interval),
@@ -73,6 +83,10 @@ class WeightsSlot:
         if getattr(module, "dueling", False) and hasattr(module, "freeze_heads"):
             module.freeze_heads()  # the actor's cached merged heads follow its parameters
         return self.version
+
+    def _check(self, params):
+        if [(tuple(p.shape), p.stride()) for p in params] != self.layout:
+            raise ValueError("module parameters do not match the slot's layout (shapes / memory format)")
 
     def device_version(self):
         """the device counter (synchronous read)"""

@@ -102,3 +102,26 @@ def test_acquire_replays_from_a_graph(dev):
     # but only 3 > 2 steps since 3 -> load
     assert hist == [0, 0, 1, 0, 0, 1, 0, 0]
     assert _same(actor, learner)
+
+
+def test_channels_last_dqn_network(dev):
+    """the apex layout: channels_last conv weights are dense runs the slot copies as bytes; a
+    consumer in another memory format is refused instead of receiving permuted weights"""
+    from reth_amd.model import DQNNetwork
+    from reth_amd.weights import WeightsSlot
+
+    torch.manual_seed(0)
+    cl = dict(memory_format=torch.channels_last)
+    learner = DQNNetwork((4, 84, 84), 6).to(dev, **cl)
+    actor = DQNNetwork((4, 84, 84), 6).to(dev, **cl)
+    slot = WeightsSlot(learner)
+    with torch.no_grad():
+        for p in learner.parameters():
+            p.add_(0.5)
+    slot.publish(learner)
+    slot.acquire(actor)
+    torch.cuda.synchronize()
+    assert _same(actor, learner)
+    other = DQNNetwork((4, 84, 84), 6).to(dev)  # contiguous (NCHW) conv weights
+    with pytest.raises(ValueError):
+        slot.acquire(other)

@@ -913,9 +913,11 @@ __global__ __launch_bounds__(kWgWaves * 64) void k_conv1_wgrad_bf16x3(const uint
 // elements per workgroup, 4 groups of 64 lanes each summing a quarter of the partials
 // (coalesced rows), then the 4 group sums in fixed order
 // deferred bias gradients (rth_relu_bias_grad with db = NULL) finished by the extra
-// workgroups of this launch: db[c] = sum of the job's slabs in slab order, G = 256 / C lanes
-// per channel striding the slabs, then the G lane sums by a fixed LDS tree
+// workgroups of this launch, in exactly k_bias_grad_combine's order (qnet.hip: 1024 lanes,
+// G = 1024 / C lanes per channel striding the slabs, then a fixed LDS tree): each of the 256
+// threads plays 4 of those virtual lanes, so the result is bit-identical to the two-launch form
 constexpr int kBiasJobsMax = 4;
+constexpr int kBiasVLanes = 1024;  // = qnet.hip's kCombThreads
 struct BiasJobs {
   const float *part[kBiasJobsMax];
   float *db[kBiasJobsMax];
@@ -923,24 +925,29 @@ struct BiasJobs {
   int n;
 };
 
-__device__ void bias_job(const BiasJobs &bj, int j, float *red) {
-  const int C = bj.C[j], G = 256 / C, tid = threadIdx.x, c = tid % C;
+__device__ void bias_job(const BiasJobs &bj, int j) {
+  __shared__ float red[kBiasVLanes];
+  const int C = bj.C[j], G = kBiasVLanes / C, tid = threadIdx.x;
   const float *part = bj.part[j];
-  float s = 0.0f;
-  for (int k = tid / C; k < bj.slabs[j]; k += 8 * G) {
-    float v[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int kk = k + u * G;
-      v[u] = kk < bj.slabs[j] ? part[(int64_t)kk * C + c] : 0.0f;
+  for (int q = 0; q < kBiasVLanes / 256; ++q) {
+    const int vt = tid + 256 * q, c = vt % C;
+    float s = 0.0f;
+    for (int k = vt / C; k < bj.slabs[j]; k += 8 * G) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int kk = k + u * G;
+        v[u] = kk < bj.slabs[j] ? part[(int64_t)kk * C + c] : 0.0f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s = radd(s, v[u]);
     }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) s = radd(s, v[u]);
+    red[vt] = s;
   }
-  red[tid] = s;
   __syncthreads();
-  for (int st = 128; st >= C; st >>= 1) {
-    if (tid < st) red[tid] = radd(red[tid], red[tid + st]);
+  for (int st = kBiasVLanes / 2; st >= C; st >>= 1) {
+    for (int i = tid; i < st; i += 256) red[i] = radd(red[i], red[i + st]);
     __syncthreads();
   }
   if (tid < C) bj.db[j][tid] = red[tid];
@@ -952,7 +959,7 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const float *__restrict__ 
   constexpr int K = CIN * KH * KW, E = COUT * K + COUT, RB = (E + 63) / 64;
   __shared__ float part[4][64];
   if ((int)blockIdx.x >= RB) {  // a deferred bias gradient
-    bias_job(bj, blockIdx.x - RB, &part[0][0]);
+    bias_job(bj, blockIdx.x - RB);
     return;
   }
   const int grp = threadIdx.x / 64, l = threadIdx.x % 64;

@@ -187,3 +187,22 @@ def test_breakout_shaped_graph_loop(dev):
     rows = act._sets[(act.pushes - 2) % 2]
     assert torch.equal(out[1], rows.a) and torch.equal(out[0], act.frames[rows.s0])
     ax.close()
+
+
+
+def test_overlapped_allreduce_stream_edges():
+    """_learner_replay's comm-stream edges, checked with a stream-ordered stand-in for RCCL
+    (tests/_stream_edges.py).  Run in a child process with 16 hardware queues: at the box's
+    default of 4, HIP maps the loop's streams onto shared queues, which serialises them in
+    submission order and would hide a missing edge (measured: the check passes with both
+    edges removed at 4 queues and fails at 16)."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, GPU_MAX_HW_QUEUES="16")
+    r = subprocess.run([sys.executable, "-c", "import tests._stream_edges as m; m.main()"], cwd=root, env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "stream edges OK" in r.stdout

@@ -11,7 +11,7 @@ path of solver.py (compute_grads with torch.autograd), without the autograd engi
   TD        rth_td_huber on the raw heads -> |td|, loss, d(loss)/d(heads of s0), fused with
   backward  FC2 + threshold + both bias sums (rth_td_heads_backward; also the Trainer's
             mean |td|), FC1 as two GEMMs, conv3 / conv2 as rth_relu_bias_grad + MIOpen's data
-            and weight gradients (conv2's data gradient optionally rth_conv_dgrad), conv1 as rth_conv_relu_wgrad straight from the uint8 stacks
+            and weight gradients (conv2's data gradient in rth_conv_dgrad), conv1 as rth_conv_relu_wgrad straight from the uint8 stacks
             (f32 input: rth_relu_bias_grad + MIOpen's weight gradient), the merged-head
             gradients mapped back onto the eight branch parameters by rth_heads_split_grad.
 
@@ -27,9 +27,12 @@ from ._lib import call, ctypes, ptr, stream_ptr
 
 
 TD_HB_MAX = 16384  # rth_td_heads_backward keeps B * (A + 1) TD gradient rows in LDS
-# conv2's data gradient in rth_conv_dgrad instead of MIOpen: 49 vs 61 us alone, no faster in
-# the overlapped loop, so opt-in
-HIP_DGRAD = os.environ.get("RTH_HIP_DGRAD") is not None
+# data gradients in rth_conv_dgrad instead of MIOpen (no zero fill): conv2's by default (49
+# vs 61 us alone; 0.615 vs 0.630 ms/step in the loop, where the learner stream is the critical
+# path), conv3's opt-in (RTH_HIP_DGRAD3=1, A/B aid); RTH_MIOPEN_DGRAD=1 restores MIOpen's
+HIP_DGRAD = {1} if os.environ.get("RTH_MIOPEN_DGRAD") is None else set()
+if os.environ.get("RTH_HIP_DGRAD3") is not None:
+    HIP_DGRAD.add(2)
 
 
 def eligible(net, s0, s1):
@@ -177,7 +180,7 @@ def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None, mid=No
                 deferred.append(_lib.BiasDeferred(net._ws[li].data_ptr(), db.data_ptr(), nb * hh * ww, c))
             xin = ys[li - 1][:B] if li > 0 else x[:B]
             w = _nhwc(conv.weight.detach())
-            hip_dgrad = li == 1 and HIP_DGRAD and _lib.lib().rth_conv_dgrad_supported(ctypes.byref(shapes[li]))
+            hip_dgrad = li in HIP_DGRAD and _lib.lib().rth_conv_dgrad_supported(ctypes.byref(shapes[li]))
             gx, gw, _ = torch.ops.aten.convolution_backward(gy, xin, w, None, list(conv.stride), [0, 0], [1, 1], False,
                                                             [0, 0], 1, [li > 0 and not hip_dgrad, True, False])
             if hip_dgrad:  # data gradient in rth_conv_dgrad (no zero fill)

@@ -50,12 +50,12 @@ def _solver(dev, seed):
                      channels_last=True)
 
 
-@pytest.mark.parametrize("u8,adjacent,hip_dgrad", [(True, True, False), (True, False, False), (False, False, False),
-                                                   (True, True, True)])
+@pytest.mark.parametrize("u8,adjacent,hip_dgrad", [(True, True, {1}), (True, False, {1}), (False, False, {1}),
+                                                   (True, True, set()), (True, True, {1, 2})])
 def test_fused_grads_match_autograd(dev, u8, adjacent, hip_dgrad, monkeypatch):
     from reth_amd import fused_learner
 
-    monkeypatch.setattr(fused_learner, "HIP_DGRAD", hip_dgrad)  # conv2's data gradient in rth_conv_dgrad
+    monkeypatch.setattr(fused_learner, "HIP_DGRAD", hip_dgrad)  # layers whose data gradient is rth_conv_dgrad's
 
     B = 64
     g = torch.Generator(device=dev).manual_seed(5)

@@ -265,6 +265,9 @@ def main():
     from reth_amd.apex import ApexConfig, ApexDQN
     from reth_amd.dist import init_from_env
 
+    if os.environ.get("RTH_BLAS"):  # A/B aid: torch's GEMM backend ("cublas" = rocBLAS, "cublaslt" = hipBLASLt)
+        torch.backends.cuda.preferred_blas_library(os.environ["RTH_BLAS"])
+
     import torch.distributed as dist
 
     world_env = int(os.environ.get("WORLD_SIZE", "1"))

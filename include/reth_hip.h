@@ -319,7 +319,11 @@ int64_t rth_relu_bias_grad_workspace(int32_t C);
  * adv.2.bias [A], value.2.bias [1]} -> w1 [2H,F] (FC1 of both branches; with C > 0 its
  * columns follow the NHWC flatten of a C x P feature map), b1 [2H], w2 [A+1,2H]
  * (block diagonal), b2 [A+1].  rth_heads_split_grad maps the four gradients back onto the
- * eight parameters (grads in the same order). */
+ * eight parameters (grads in the same order).
+ * C = RTH_HEADS_FC2_ONLY: only the second layer (w2, b2 / their gradients); w1, b1, gw1, gb1
+ * and params / grads 0-3 may be NULL -- for a model whose two FC1 branches are row slices of
+ * one merged [2H, F] storage (reth_amd/model.py), which FC1 reads and writes in place. */
+#define RTH_HEADS_FC2_ONLY (-1)
 int rth_heads_merge(const float *const *params_dev, int64_t H, int64_t F, int64_t A, int32_t C, int32_t P,
                     float *w1_dev, float *b1_dev, float *w2_dev, float *b2_dev, void *stream);
 int rth_heads_split_grad(const float *gw1_dev, const float *gb1_dev, const float *gw2_dev, const float *gb2_dev,
@@ -327,6 +331,12 @@ int rth_heads_split_grad(const float *gw1_dev, const float *gb1_dev, const float
                          void *stream);
 int rth_relu_bias_grad(const float *g_dev, const float *y_dev, float *gy_dev, float *db_dev, void *workspace_dev,
                        int64_t rows, int32_t C, void *stream);
+/* rth_relu_bias_grad for an NCHW activation (the last conv's output written with
+ * RTH_CONV_OUT_NCHW: g and y are [n, C, P]); gy is written channels-last [n, P, C] for the
+ * data / weight gradients that follow.  Same workspace and slab layout (a deferred job with
+ * rows = n * P finishes it); C a power of 2 in [4, 256], C * (P + 1) <= 3200. */
+int rth_relu_bias_grad_nchw(const float *g_dev, const float *y_dev, float *gy_dev, float *db_dev,
+                            void *workspace_dev, int64_t n, int32_t C, int32_t P, void *stream);
 /* Backward of the merged heads' second layer, heads = h @ w2^T + b2 with h = relu(FC1) [B, H2]
  * (row stride ldh), from d(loss)/d(heads) dq [B, A1] (rth_td_huber, dueling): replaces the
  * addmm backward (two GEMMs + a column sum) and threshold_backward of torch.autograd at
@@ -345,6 +355,26 @@ int rth_td_heads_backward(const float *q_s0_dev, const float *q_s1_online_dev, c
                           int64_t B, int64_t A, float gamma_n, int32_t double_q, const float *h_dev, int64_t ldh,
                           const float *w2_dev, int32_t H2, float *td_abs_dev, float *loss_out_dev, float *gh_dev,
                           float *gw2_dev, float *gb2_dev, float *gb1_dev, float *td_acc_dev, void *stream);
+/* The same two kernels with the second layer in the reference's branch form: fc2_params =
+ * {adv.2.weight [A, H], value.2.weight [1, H], ...} read in place instead of a merged
+ * block-diagonal w2, fc2_grads = {adv.2.weight, value.2.weight, adv.2.bias, value.2.bias}
+ * gradients written in place (the off-diagonal blocks of gw2 are not produced); H2 = 2H,
+ * H a multiple of 16.  Replaces rth_heads_merge / rth_heads_split_grad for the second layer. */
+int rth_heads_backward_branches(const float *dq_dev, const float *h_dev, int64_t ldh, const float *const *fc2_params_dev,
+                                int32_t H, int64_t B, int64_t A, float *gh_dev, float *const *fc2_grads_dev,
+                                float *gb1_dev, const float *td_abs_dev, float *td_acc_dev, void *stream);
+int rth_td_heads_backward_branches(const float *q_s0_dev, const float *q_s1_online_dev, const float *q_s1_target_dev,
+                                   const int64_t *a_dev, const float *r_dev, const float *done_dev,
+                                   const double *isw_dev, int64_t B, int64_t A, float gamma_n, int32_t double_q,
+                                   const float *h_dev, int64_t ldh, const float *const *fc2_params_dev, int32_t H,
+                                   float *td_abs_dev, float *loss_out_dev, float *gh_dev,
+                                   float *const *fc2_grads_dev, float *gb1_dev, float *td_acc_dev, void *stream);
+/* The dueling heads' second layer forward (dqn_model.py:22-43 fc_adv[2] / fc_value[2] on the
+ * ReLU'd FC1 output h [n, 2H], row stride ldh): heads [n, A+1] = (adv.2(h[:, :H]),
+ * value.2(h[:, H:])), the raw heads the TD / epsilon-greedy kernels consume; fc2_params =
+ * {adv.2.weight, value.2.weight, adv.2.bias, value.2.bias} read in place. */
+int rth_heads_fc2(const float *h_dev, int64_t ldh, int64_t n, int32_t H, int32_t A, const float *const *fc2_params_dev,
+                  float *heads_dev, void *stream);
 
 /* ------------------------------------------------------------------------------------
  * Q-network convolution torso forward (reth/reth/algorithm/dqn/dqn_model.py:14-20: each
@@ -364,8 +394,12 @@ int rth_td_heads_backward(const float *q_s0_dev, const float *q_s1_online_dev, c
  * ---------------------------------------------------------------------------------- */
 #define RTH_CONV_F32_NHWC 0
 #define RTH_CONV_U8_CHW 1
+/* flag OR'ed into `input` of rth_conv_bias_relu(_upto): write y NCHW [n, cout, hout, wout]
+ * (the last conv, whose output FC1 reads in the reference's (C, H, W) flatten order); the
+ * fp32-MFMA kernels only (not the uint8 conv1, which feeds conv2) */
+#define RTH_CONV_OUT_NCHW 16
 typedef struct rth_conv_shape {
-  int32_t input; /* RTH_CONV_F32_NHWC | RTH_CONV_U8_CHW */
+  int32_t input; /* RTH_CONV_F32_NHWC | RTH_CONV_U8_CHW [| RTH_CONV_OUT_NCHW] */
   int32_t cin, hin, win, cout, kh, kw, stride;
 } rth_conv_shape;
 int rth_conv_supported(const rth_conv_shape *shape);

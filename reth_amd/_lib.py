@@ -60,6 +60,8 @@ class BiasDeferred(ctypes.Structure):
 
 
 CONV_F32_NHWC, CONV_U8_CHW = 0, 1
+CONV_OUT_NCHW = 16  # flag: the conv writes NCHW (the last conv, feeding FC1)
+HEADS_FC2_ONLY = -1
 
 
 class ActorTailArgs(ctypes.Structure):
@@ -131,7 +133,14 @@ SIGNATURES = {
                                    c_vp]),
     "rth_td_heads_backward": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f32, c_i32, c_vp,
                                       c_i64, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "rth_heads_backward_branches": (c_i32, [c_vp, c_vp, c_i64, ctypes.POINTER(c_vp), c_i32, c_i64, c_i64, c_vp,
+                                            ctypes.POINTER(c_vp), c_vp, c_vp, c_vp, c_vp]),
+    "rth_td_heads_backward_branches": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f32, c_i32,
+                                               c_vp, c_i64, ctypes.POINTER(c_vp), c_i32, c_vp, c_vp, c_vp,
+                                               ctypes.POINTER(c_vp), c_vp, c_vp, c_vp]),
+    "rth_heads_fc2": (c_i32, [c_vp, c_i64, c_i64, c_i32, c_i32, ctypes.POINTER(c_vp), c_vp, c_vp]),
     "rth_relu_bias_grad": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_vp]),
+    "rth_relu_bias_grad_nchw": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_vp]),
     "rth_conv_supported": (c_i32, [ctypes.POINTER(ConvShape)]),
     "rth_conv_packed_bytes": (c_i64, [ctypes.POINTER(ConvShape)]),
     "rth_conv_pack": (c_i32, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_vp]),

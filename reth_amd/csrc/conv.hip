@@ -78,7 +78,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__res
                                                               const int64_t *__restrict__ n_dev,
                                                               const float *__restrict__ w,
                                                               const float *__restrict__ bias,
-                                                              float *__restrict__ y) {
+                                                              float *__restrict__ y, int out_nchw) {
   using Gm = ConvGeom<MODE, KH, KW, S, CIN, COUT, HIN, WIN>;
   constexpr bool F32 = MODE == RTH_CONV_F32_NHWC;
   constexpr int G = Gm::G, NB = Gm::NB, T = WAVES * 64;
@@ -207,15 +207,23 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__res
         for (int nb = 0; nb < NB; ++nb) bcur[nb] = bnxt[nb];
       }
     }
-    // C/D: lane holds column mr of rows 4q .. 4q+3 of each M-block
+    // C/D: lane holds column mr of rows 4q .. 4q+3 of each M-block; y is NHWC, or NCHW when
+    // out_nchw (the last conv feeding FC1 in the reference's (C, H, W) flatten order)
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int64_t po = tile * TP + mb * 16 + 4 * q + i;
         if (po < P) {
+          if (out_nchw) {
+            const int64_t b = po / Gm::PIX, pp = po - b * Gm::PIX;
 #pragma unroll
-          for (int nb = 0; nb < NB; ++nb) y[po * COUT + nb * 16 + mr] = relu_c(radd(acc[mb][nb][i], bl[nb]));
+            for (int nb = 0; nb < NB; ++nb)
+              y[(b * COUT + nb * 16 + mr) * Gm::PIX + pp] = relu_c(radd(acc[mb][nb][i], bl[nb]));
+          } else {
+#pragma unroll
+            for (int nb = 0; nb < NB; ++nb) y[po * COUT + nb * 16 + mr] = relu_c(radd(acc[mb][nb][i], bl[nb]));
+          }
         }
       }
 #pragma unroll
@@ -479,7 +487,7 @@ static ConvLaunch conv1_bf16x3_launch() {
 // the supported geometries (the Nature-DQN torso on 4 x 84 x 84 stacks)
 static bool find_conv(const rth_conv_shape &s, ConvLaunch *out, int *geom = nullptr) {
   auto is = [&](int mode, int cin, int hin, int win, int cout, int kh, int kw, int st) {
-    return s.input == mode && s.cin == cin && s.hin == hin && s.win == win && s.cout == cout && s.kh == kh &&
+    return (s.input & ~RTH_CONV_OUT_NCHW) == mode && s.cin == cin && s.hin == hin && s.win == win && s.cout == cout && s.kh == kh &&
            s.kw == kw && s.stride == st;
   };
   if (is(RTH_CONV_U8_CHW, 4, 84, 84, 32, 8, 8, 4)) {
@@ -1006,7 +1014,8 @@ extern "C" {
 
 int rth_conv_supported(const rth_conv_shape *shape) {
   ConvLaunch l;
-  return shape && find_conv(*shape, &l) ? 1 : 0;
+  if (!shape || !find_conv(*shape, &l)) return 0;
+  return (shape->input & RTH_CONV_OUT_NCHW) && l.bf16x3 ? 0 : 1;  // NCHW output: fp32-MFMA kernels only
 }
 
 int64_t rth_conv_packed_bytes(const rth_conv_shape *shape) {
@@ -1116,9 +1125,11 @@ static int conv_bias_relu(const rth_conv_shape *shape, const void *x, const int6
   RTH_REQUIRE(find_conv(*shape, &l),
               "rth_conv_bias_relu: geometry (input %d, %d x %d x %d -> %d, k %dx%d, stride %d) not built", shape->input,
               shape->cin, shape->hin, shape->win, shape->cout, shape->kh, shape->kw, shape->stride);
-  RTH_REQUIRE(!rows || shape->input == RTH_CONV_U8_CHW, "rth_conv_bias_relu: row index needs uint8 stacks");
+  const int input = shape->input & ~RTH_CONV_OUT_NCHW, out_nchw = (shape->input & RTH_CONV_OUT_NCHW) ? 1 : 0;
+  RTH_REQUIRE(!rows || input == RTH_CONV_U8_CHW, "rth_conv_bias_relu: row index needs uint8 stacks");
+  RTH_REQUIRE(!out_nchw || !l.bf16x3, "rth_conv_bias_relu: NCHW output is built for the fp32-MFMA kernels only");
   RTH_REQUIRE(((reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(y)) & 15) == 0 &&
-                  (shape->input == RTH_CONV_U8_CHW ? (reinterpret_cast<uintptr_t>(x) & 3) == 0
+                  (input == RTH_CONV_U8_CHW ? (reinterpret_cast<uintptr_t>(x) & 3) == 0
                                                    : (reinterpret_cast<uintptr_t>(x) & 15) == 0),
               "rth_conv_bias_relu: misaligned buffer");
   if (n == 0) return RTH_OK;
@@ -1129,7 +1140,8 @@ static int conv_bias_relu(const rth_conv_shape *shape, const void *x, const int6
   const int cap = wg_per_cu();
   const int64_t resident = (int64_t)cu_count() * (l.per_cu < cap ? l.per_cu : cap);
   if (grid > resident) grid = resident;
-  void *args[] = {(void *)&x, (void *)&rows, (void *)&n, (void *)&n_dev, (void *)&w, (void *)&bias, (void *)&y};
+  void *args[] = {(void *)&x, (void *)&rows, (void *)&n, (void *)&n_dev, (void *)&w, (void *)&bias, (void *)&y,
+                  (void *)&out_nchw};  // (k_conv1_u8_bf16x3 takes the first seven)
   RTH_HIP(hipLaunchKernel(l.fn, dim3((unsigned)grid), dim3(l.waves * 64), args, 0, as_stream(stream)));
   return RTH_OK;
 }

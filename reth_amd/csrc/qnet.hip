@@ -82,6 +82,50 @@ __global__ __launch_bounds__(kEpiThreads) void k_relu_bias_grad(const float4 *__
   if (tid < Q) reinterpret_cast<float4 *>(part)[(int64_t)blockIdx.x * Q + tid] = red[tid];
 }
 
+// The same for the last conv's NCHW output (the FC1 input in the reference's (C, H, W)
+// flatten order): g and y are [n, C, P] (P = H*W), gy is written channels-last [n, P, C] for
+// the data / weight gradients that follow.  Slab s owns samples [s*n/S, (s+1)*n/S); per
+// sample the masked gradient goes through an LDS tile [C][P+1] so the NCHW reads and the
+// NHWC writes are both coalesced.  Lane t sums channel t / Q over positions of quarter t % Q
+// (Q = 256 / C) across its slab's samples, then the Q quarter sums in fixed order: the same
+// slab-partial layout as k_relu_bias_grad, so the combine (or a deferred job) is shared.
+constexpr int kNchwMaxTile = 64 * 50;
+__global__ __launch_bounds__(kEpiThreads) void k_relu_bias_grad_nchw(const float *__restrict__ g,
+                                                                      const float *__restrict__ y,
+                                                                      float *__restrict__ gy, float *__restrict__ part,
+                                                                      int64_t n, int C, int P) {
+  __shared__ float tile[kNchwMaxTile];
+  __shared__ float red[kEpiThreads];
+  const int tid = threadIdx.x, S = gridDim.x, E = C * P, LP = P + 1;
+  const int64_t b0 = (int64_t)blockIdx.x * n / S, b1 = (int64_t)(blockIdx.x + 1) * n / S;
+  const int Q = kEpiThreads / C, c_own = tid / Q, qq = tid % Q;
+  const int pq = (P + Q - 1) / Q, p0 = qq * pq, p1 = min(P, p0 + pq);
+  float acc = 0.0f;
+  for (int64_t b = b0; b < b1; ++b) {
+    const float *gb = g + b * E, *yb = y + b * E;
+    for (int i = tid; i < E; i += kEpiThreads) {  // NCHW order: i = c * P + p
+      const float yv = yb[i], gv = gb[i];
+      const int c = i / P, pp = i - c * P;
+      tile[c * LP + pp] = yv > 0.0f ? gv : 0.0f;  // threshold_backward(g, y, 0)
+    }
+    __syncthreads();
+    for (int p = p0; p < p1; ++p) acc = radd(acc, tile[c_own * LP + p]);
+    float *gyb = gy + b * E;
+    for (int o = tid; o < E; o += kEpiThreads) {  // NHWC order: o = p * C + c
+      const int pp = o / C, c = o - pp * C;
+      gyb[o] = tile[c * LP + pp];
+    }
+    __syncthreads();
+  }
+  red[tid] = acc;
+  __syncthreads();
+  if (tid < C) {
+    float sum = red[tid * Q];
+    for (int k = 1; k < Q; ++k) sum = radd(sum, red[tid * Q + k]);
+    part[(int64_t)blockIdx.x * C + tid] = sum;
+  }
+}
+
 // db[c] = sum of the slabs' partials in slab order: lane t sums slabs t / C, t / C + G, ...
 // of channel t % C (G = 1024 / C lanes per channel, 8 loads in flight), then the G lane sums
 // of a channel by a fixed LDS tree.  A separate launch: the kernel boundary publishes the
@@ -122,6 +166,7 @@ __global__ __launch_bounds__(kCombThreads) void k_bias_grad_combine(const float 
 struct HeadsDims {
   int64_t H, F, A;  // hidden units per branch, features, actions
   int32_t C, P;     // feature map channels and H*W positions (C = 0: no permutation)
+  int32_t fc2_only;  // only the second layer (w2, b2): FC1 is held merged by the model
 };
 
 
@@ -138,7 +183,7 @@ __global__ __launch_bounds__(256) void k_heads_merge(HeadsDims d, const float *_
                                                      float *__restrict__ b1, float *__restrict__ w2,
                                                      float *__restrict__ b2) {
   extern __shared__ float row[];
-  const int64_t r = blockIdx.x, F = d.F;
+  const int64_t r = blockIdx.x + (d.fc2_only ? 2 * d.H : 0), F = d.F;
   if (r < 2 * d.H) {
     const float *src = (r < d.H ? wa1 : wv1) + (r % d.H) * F;
     float *dst = w1 + r * F;
@@ -171,7 +216,8 @@ __global__ __launch_bounds__(256) void k_heads_merge(HeadsDims d, const float *_
     return;
   }
   const int64_t H2 = 2 * d.H, A1 = d.A + 1;
-  for (int64_t k = threadIdx.x; k < H2; k += blockDim.x) b1[k] = k < d.H ? ba1[k] : bv1[k - d.H];
+  if (!d.fc2_only)
+    for (int64_t k = threadIdx.x; k < H2; k += blockDim.x) b1[k] = k < d.H ? ba1[k] : bv1[k - d.H];
   for (int64_t k = threadIdx.x; k < A1 * H2; k += blockDim.x) {
     const int64_t rr = k / H2, j = k - rr * H2;
     float v = 0.0f;
@@ -191,7 +237,7 @@ __global__ __launch_bounds__(256) void k_heads_split_grad(HeadsDims d, const flo
                                                           float *__restrict__ gwv2, float *__restrict__ gba2,
                                                           float *__restrict__ gbv2) {
   extern __shared__ float row[];
-  const int64_t r = blockIdx.x, F = d.F;
+  const int64_t r = blockIdx.x + (d.fc2_only ? 2 * d.H : 0), F = d.F;
   if (r < 2 * d.H) {
     const float *src = gw1 + r * F;
     float *dst = (r < d.H ? gwa1 : gwv1) + (r % d.H) * F;
@@ -228,9 +274,10 @@ __global__ __launch_bounds__(256) void k_heads_split_grad(HeadsDims d, const flo
     return;
   }
   const int64_t H2 = 2 * d.H;
-  for (int64_t k = threadIdx.x; k < H2; k += blockDim.x) {
-    if (k < d.H) gba1[k] = gb1[k]; else gbv1[k - d.H] = gb1[k];
-  }
+  if (!d.fc2_only)
+    for (int64_t k = threadIdx.x; k < H2; k += blockDim.x) {
+      if (k < d.H) gba1[k] = gb1[k]; else gbv1[k - d.H] = gb1[k];
+    }
   for (int64_t k = threadIdx.x; k < d.A * d.H + d.H; k += blockDim.x) {
     if (k < d.A * d.H) {
       const int64_t rr = k / d.H, j = k - rr * d.H;
@@ -257,12 +304,46 @@ __global__ __launch_bounds__(256) void k_heads_split_grad(HeadsDims d, const flo
 // mean(|td|) to a device accumulator (Trainer's mean_error, reth/reth/presets/trainer.py:64-69).
 constexpr int kHbCols = 16, kHbGroups = 64, kHbThreads = kHbCols * kHbGroups, kHbMaxA1 = kMaxActions + 1;
 
+// The second layer's weights and gradients: merged (w2 [A1, H2] block diagonal, gw2, gb2) or,
+// with `branches`, the reference's four parameters read and written in place (wa2 [A, H],
+// wv2 [1, H]; gwa2, gwv2, gba2, gbv2) -- no merged copy to build or split per update.  In
+// branch form the off-diagonal blocks are zero and their gradients are not produced.
+struct Fc2 {
+  const float *w2;
+  float *gw2, *gb2;
+  const float *wa2, *wv2;
+  float *gwa2, *gwv2, *gba2, *gbv2;
+  int H, A, branches;
+};
+
+__device__ __forceinline__ float fc2_w(const Fc2 &f, int a, int j, int H2) {
+  if (!f.branches) return f.w2[(int64_t)a * H2 + j];
+  if (a < f.A) return j < f.H ? f.wa2[(int64_t)a * f.H + j] : 0.0f;
+  return j >= f.H ? f.wv2[j - f.H] : 0.0f;
+}
+
+// is gw2[a][j] wanted (branch form: the diagonal blocks only); uniform over a workgroup's
+// 16 columns when H % 16 == 0
+__device__ __forceinline__ bool fc2_live(const Fc2 &f, int a, int j) {
+  return !f.branches || (a < f.A) == (j < f.H);
+}
+
+__device__ __forceinline__ void fc2_store_gw(const Fc2 &f, int a, int j, int H2, float v) {
+  if (!f.branches) f.gw2[(int64_t)a * H2 + j] = v;
+  else if (a < f.A) f.gwa2[(int64_t)a * f.H + j] = v;
+  else f.gwv2[j - f.H] = v;
+}
+
+__device__ __forceinline__ void fc2_store_gb(const Fc2 &f, int a, float v) {
+  if (!f.branches) f.gb2[a] = v;
+  else if (a < f.A) f.gba2[a] = v;
+  else f.gbv2[0] = v;
+}
+
 template <int MAXA, int RB>
 __global__ __launch_bounds__(kHbThreads) void k_heads_backward(const float *__restrict__ dq,
-                                                               const float *__restrict__ h, int64_t ldh,
-                                                               const float *__restrict__ w2, int64_t B, int H2,
-                                                               int A1, float *__restrict__ gh,
-                                                               float *__restrict__ gw2, float *__restrict__ gb2,
+                                                               const float *__restrict__ h, int64_t ldh, Fc2 f,
+                                                               int64_t B, int H2, int A1, float *__restrict__ gh,
                                                                float *__restrict__ gb1,
                                                                const float *__restrict__ td_abs,
                                                                float *__restrict__ td_acc) {
@@ -280,7 +361,7 @@ __global__ __launch_bounds__(kHbThreads) void k_heads_backward(const float *__re
         __syncthreads();
       }
       if (tid == 0) {
-        if (a < A1) gb2[a] = red[0];
+        if (a < A1) fc2_store_gb(f, a, red[0]);
         else td_acc[0] = radd(td_acc[0], red[0] / (float)B);  // _err_acc.add_(td.mean())
       }
       __syncthreads();
@@ -292,7 +373,7 @@ __global__ __launch_bounds__(kHbThreads) void k_heads_backward(const float *__re
   float wc[MAXA], aw[MAXA];
 #pragma unroll
   for (int a = 0; a < MAXA; ++a) {
-    wc[a] = a < A1 ? w2[(int64_t)a * H2 + j] : 0.0f;
+    wc[a] = a < A1 ? fc2_w(f, a, j, H2) : 0.0f;
     aw[a] = 0.0f;
   }
   float ab = 0.0f;
@@ -322,8 +403,9 @@ __global__ __launch_bounds__(kHbThreads) void k_heads_backward(const float *__re
       ab = radd(ab, g);
     }
   }
-  // fixed-order sums over the row groups: gb1, then each row of gw2
+  // fixed-order sums over the row groups: gb1, then each (wanted) row of gw2
   for (int a = -1; a < A1; ++a) {
+    if (a >= 0 && !fc2_live(f, a, (int)blockIdx.x * kHbCols)) continue;  // uniform
     float v = ab;
 #pragma unroll
     for (int k = 0; k < MAXA; ++k)
@@ -336,7 +418,7 @@ __global__ __launch_bounds__(kHbThreads) void k_heads_backward(const float *__re
     }
     if (tid < kHbCols) {
       if (a < 0) gb1[j] = red[tid];
-      else gw2[(int64_t)a * H2 + j] = red[tid];
+      else fc2_store_gw(f, a, j, H2, red[tid]);
     }
     __syncthreads();
   }
@@ -354,9 +436,8 @@ __global__ __launch_bounds__(kHbThreads) void k_td_heads_backward(
     const float *__restrict__ q0, const float *__restrict__ q1o, const float *__restrict__ q1t,
     const int64_t *__restrict__ act, const float *__restrict__ rew, const float *__restrict__ done,
     const double *__restrict__ isw, int64_t B, int A, float gamma_n, int double_q, const float *__restrict__ h,
-    int64_t ldh, const float *__restrict__ w2, int H2, float *__restrict__ td_abs, float *__restrict__ loss_out,
-    float *__restrict__ gh, float *__restrict__ gw2, float *__restrict__ gb2, float *__restrict__ gb1,
-    float *__restrict__ td_acc) {
+    int64_t ldh, Fc2 f, int H2, float *__restrict__ td_abs, float *__restrict__ loss_out,
+    float *__restrict__ gh, float *__restrict__ gb1, float *__restrict__ td_acc) {
   __shared__ float dqs[kTdHbMaxElems];
   __shared__ float red[kHbThreads];
   const int tid = threadIdx.x, A1 = A + 1;
@@ -388,7 +469,7 @@ __global__ __launch_bounds__(kHbThreads) void k_td_heads_backward(
       if (tid == 0) {
         if (a == -2) loss_out[0] = red[0] * invB;
         else if (a == -1) { if (td_acc) td_acc[0] = radd(td_acc[0], red[0] / (float)B); }
-        else gb2[a] = red[0];
+        else fc2_store_gb(f, a, red[0]);
       }
       __syncthreads();
     }
@@ -399,7 +480,7 @@ __global__ __launch_bounds__(kHbThreads) void k_td_heads_backward(
   float wc[MAXA], aw[MAXA];
 #pragma unroll
   for (int a = 0; a < MAXA; ++a) {
-    wc[a] = a < A1 ? w2[(int64_t)a * H2 + j] : 0.0f;
+    wc[a] = a < A1 ? fc2_w(f, a, j, H2) : 0.0f;
     aw[a] = 0.0f;
   }
   float ab = 0.0f;
@@ -429,6 +510,7 @@ __global__ __launch_bounds__(kHbThreads) void k_td_heads_backward(
     }
   }
   for (int a = -1; a < A1; ++a) {
+    if (a >= 0 && !fc2_live(f, a, (int)blockIdx.x * kHbCols)) continue;  // uniform
     float v = ab;
 #pragma unroll
     for (int k = 0; k < MAXA; ++k)
@@ -441,9 +523,66 @@ __global__ __launch_bounds__(kHbThreads) void k_td_heads_backward(
     }
     if (tid < kHbCols) {
       if (a < 0) gb1[j] = red[tid];
-      else gw2[(int64_t)a * H2 + j] = red[tid];
+      else fc2_store_gw(f, a, j, H2, red[tid]);
     }
     __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------- heads forward, second layer
+// heads[r] = (wa2 . h[r, :H] + ba2, wv2 . h[r, H:] + bv2) straight from the reference's four
+// parameters (the block-diagonal FC2 without a merged copy).  16 lanes per row (16 rows per
+// workgroup): lane l takes columns [l H/16, (l+1) H/16) of each half, all of its h loads
+// issued at once, the weights staged in LDS once per workgroup; the A+1 partial dots are
+// summed across the 16 lanes by four xor shuffles in a fixed order.  [n, A+1], row stride A+1.
+constexpr int kFc2MaxH = 512, kFc2MaxLds = 8 * kFc2MaxH;  // (A+1) * H floats staged, A+1 <= 8
+template <int MAXA1>
+__global__ __launch_bounds__(256) void k_heads_fc2(const float *__restrict__ h, int64_t ldh, int64_t n, int H, int A,
+                                                   const float *__restrict__ wa2, const float *__restrict__ wv2,
+                                                   const float *__restrict__ ba2, const float *__restrict__ bv2,
+                                                   float *__restrict__ heads) {
+  constexpr int U = kFc2MaxH / 16 / 4;  // float4 per lane and half, at most
+  __shared__ float4 wl[kFc2MaxLds / 4];  // rows a < A: wa2[a], row A: wv2
+  const int l = threadIdx.x & 15;
+  const int64_t r = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
+  const int64_t rr = r < n ? r : n - 1;  // tail rows: a duplicate, nothing written
+  const int cq = H / 64;                  // float4 per lane and half
+  const float4 *ha = reinterpret_cast<const float4 *>(h + rr * ldh) + l * cq;
+  const float4 *hv = reinterpret_cast<const float4 *>(h + rr * ldh + H) + l * cq;
+  float4 xa[U], xv[U];
+#pragma unroll
+  for (int k = 0; k < U; ++k)
+    if (k < cq) xa[k] = ha[k], xv[k] = hv[k];
+  const int A1 = A + 1, H4 = H / 4;
+  for (int i = threadIdx.x; i < A1 * H4; i += 256) {
+    const int a = i / H4, j4 = i - a * H4;
+    wl[i] = reinterpret_cast<const float4 *>(a < A ? wa2 + (int64_t)a * H : wv2)[j4];
+  }
+  __syncthreads();
+  float acc[MAXA1];
+#pragma unroll
+  for (int a = 0; a < MAXA1; ++a) {
+    acc[a] = 0.0f;
+    if (a < A1) {
+      const float4 *w = wl + a * H4 + l * cq;
+#pragma unroll
+      for (int k = 0; k < U; ++k)
+        if (k < cq) {
+          const float4 x = a < A ? xa[k] : xv[k], ww = w[k];
+          acc[a] = radd(radd(radd(radd(acc[a], rmul(x.x, ww.x)), rmul(x.y, ww.y)), rmul(x.z, ww.z)), rmul(x.w, ww.w));
+        }
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < MAXA1; ++a)
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) acc[a] = radd(acc[a], __shfl_xor(acc[a], o, 64));
+  if (l == 0 && r < n) {
+    float *out = heads + r * A1;
+#pragma unroll
+    for (int a = 0; a < MAXA1; ++a)
+      if (a < A) out[a] = radd(acc[a], ba2[a]);
+      else if (a == A) out[a] = radd(acc[a], bv2[0]);
   }
 }
 
@@ -493,12 +632,40 @@ int rth_relu_bias_grad(const float *g, const float *y, float *gy, float *db, voi
 }
 
 
+int rth_relu_bias_grad_nchw(const float *g, const float *y, float *gy, float *db, void *workspace, int64_t n,
+                            int32_t C, int32_t P, void *stream) {
+  RTH_REQUIRE(g && y && gy && workspace && n >= 0, "rth_relu_bias_grad_nchw: NULL argument");
+  RTH_REQUIRE(C >= 4 && C <= kEpiThreads && (C & (C - 1)) == 0 && P >= 1 && (int64_t)C * (P + 1) <= kNchwMaxTile,
+              "rth_relu_bias_grad_nchw: %d channels x %d positions unsupported", C, P);
+  if (n == 0) return RTH_OK;
+  float *part = static_cast<float *>(workspace);
+  const int64_t blocks = bias_grad_slabs(n * P, C);  // the slab count a deferred job derives from rows = n * P
+  hipLaunchKernelGGL(k_relu_bias_grad_nchw, dim3((unsigned)blocks), dim3(kEpiThreads), 0, as_stream(stream), g, y, gy,
+                     part, n, (int)C, (int)P);
+  RTH_LAUNCHED();
+  if (!db) return RTH_OK;
+  hipLaunchKernelGGL(k_bias_grad_combine, dim3(1), dim3(kCombThreads), 0, as_stream(stream), part, (int)blocks, (int)C,
+                     db);
+  RTH_LAUNCHED();
+  return RTH_OK;
+}
+
+
 int rth_heads_merge(const float *const *params, int64_t H, int64_t F, int64_t A, int32_t C, int32_t P,
                     float *w1, float *b1, float *w2, float *b2, void *stream) {
-  RTH_REQUIRE(params && w1 && b1 && w2 && b2 && H >= 1 && F >= 1 && A >= 1, "rth_heads_merge: bad arguments");
-  for (int k = 0; k < 8; ++k) RTH_REQUIRE(params[k], "rth_heads_merge: parameter %d is NULL", k);
+  const int fc2_only = C == RTH_HEADS_FC2_ONLY;
+  RTH_REQUIRE(params && (fc2_only || (w1 && b1)) && w2 && b2 && H >= 1 && F >= 1 && A >= 1,
+              "rth_heads_merge: bad arguments");
+  for (int k = fc2_only ? 4 : 0; k < 8; ++k) RTH_REQUIRE(params[k], "rth_heads_merge: parameter %d is NULL", k);
+  if (fc2_only) {
+    const HeadsDims d{H, F, A, 0, P, 1};
+    hipLaunchKernelGGL(k_heads_merge, dim3(1), dim3(256), 0, as_stream(stream), d, params[0], params[1], params[2],
+                       params[3], params[4], params[5], params[6], params[7], w1, b1, w2, b2);
+    RTH_LAUNCHED();
+    return RTH_OK;
+  }
   RTH_REQUIRE(C == 0 || (int64_t)C * P == F, "rth_heads_merge: C*P != F");
-  const HeadsDims d{H, F, A, C, P};
+  const HeadsDims d{H, F, A, C, P, 0};
   RTH_REQUIRE(F <= 12288, "rth_heads_merge: F %lld > 12288 (one row in LDS)", (long long)F);
   RTH_REQUIRE(F % 4 == 0 && C % 4 == 0 && ((reinterpret_cast<uintptr_t>(params[0]) | reinterpret_cast<uintptr_t>(params[1]) |
                                            reinterpret_cast<uintptr_t>(w1)) & 15) == 0,
@@ -513,10 +680,19 @@ int rth_heads_merge(const float *const *params, int64_t H, int64_t F, int64_t A,
 
 int rth_heads_split_grad(const float *gw1, const float *gb1, const float *gw2, const float *gb2, int64_t H,
                          int64_t F, int64_t A, int32_t C, int32_t P, float *const *grads, void *stream) {
-  RTH_REQUIRE(gw1 && gb1 && gw2 && gb2 && grads && H >= 1 && F >= 1 && A >= 1, "rth_heads_split_grad: bad arguments");
-  for (int k = 0; k < 8; ++k) RTH_REQUIRE(grads[k], "rth_heads_split_grad: gradient %d is NULL", k);
+  const int fc2_only = C == RTH_HEADS_FC2_ONLY;
+  RTH_REQUIRE((fc2_only || (gw1 && gb1)) && gw2 && gb2 && grads && H >= 1 && F >= 1 && A >= 1,
+              "rth_heads_split_grad: bad arguments");
+  for (int k = fc2_only ? 4 : 0; k < 8; ++k) RTH_REQUIRE(grads[k], "rth_heads_split_grad: gradient %d is NULL", k);
+  if (fc2_only) {
+    const HeadsDims d{H, F, A, 0, P, 1};
+    hipLaunchKernelGGL(k_heads_split_grad, dim3(1), dim3(256), 0, as_stream(stream), d, gw1, gb1, gw2, gb2, grads[0],
+                       grads[1], grads[2], grads[3], grads[4], grads[5], grads[6], grads[7]);
+    RTH_LAUNCHED();
+    return RTH_OK;
+  }
   RTH_REQUIRE(C == 0 || (int64_t)C * P == F, "rth_heads_split_grad: C*P != F");
-  const HeadsDims d{H, F, A, C, P};
+  const HeadsDims d{H, F, A, C, P, 0};
   RTH_REQUIRE(F <= 12288, "rth_heads_split_grad: F %lld > 12288 (one row in LDS)", (long long)F);
   RTH_REQUIRE(F % 4 == 0 && C % 4 == 0 && (reinterpret_cast<uintptr_t>(gw1) & 15) == 0,
               "rth_heads_split_grad: F and C must be multiples of 4, gw1 16-byte aligned");
@@ -528,29 +704,27 @@ int rth_heads_split_grad(const float *gw1, const float *gb1, const float *gw2, c
   return RTH_OK;
 }
 
-int rth_heads_backward(const float *dq, const float *h, int64_t ldh, const float *w2, int64_t B, int32_t H2,
-                       int32_t A1, float *gh, float *gw2, float *gb2, float *gb1, const float *td_abs, float *td_acc,
-                       void *stream) {
-  RTH_REQUIRE(dq && h && w2 && gh && gw2 && gb2 && gb1, "rth_heads_backward: NULL argument");
+static int heads_backward_impl(const float *dq, const float *h, int64_t ldh, const Fc2 &f, int64_t B, int32_t H2,
+                               int32_t A1, float *gh, float *gb1, const float *td_abs, float *td_acc, void *stream) {
   RTH_REQUIRE(B >= 1 && A1 >= 1 && A1 <= kHbMaxA1 && H2 >= kHbCols && H2 % kHbCols == 0 && ldh >= H2,
               "rth_heads_backward: bad shape B=%lld H2=%d A1=%d ldh=%lld", (long long)B, H2, A1, (long long)ldh);
   const dim3 grid((unsigned)(H2 / kHbCols + 1)), block(kHbThreads);
   if (A1 <= 8)  // Atari's minimal action sets (Pong 6, Breakout 4): 4 rows of dq in registers per batch
-    hipLaunchKernelGGL((k_heads_backward<8, 4>), grid, block, 0, as_stream(stream), dq, h, ldh, w2, B, H2, A1, gh, gw2,
-                       gb2, gb1, td_abs, td_acc);
+    hipLaunchKernelGGL((k_heads_backward<8, 4>), grid, block, 0, as_stream(stream), dq, h, ldh, f, B, H2, A1, gh, gb1,
+                       td_abs, td_acc);
   else
-    hipLaunchKernelGGL((k_heads_backward<kHbMaxA1, 1>), grid, block, 0, as_stream(stream), dq, h, ldh, w2, B, H2, A1,
-                       gh, gw2, gb2, gb1, td_abs, td_acc);
+    hipLaunchKernelGGL((k_heads_backward<kHbMaxA1, 1>), grid, block, 0, as_stream(stream), dq, h, ldh, f, B, H2, A1,
+                       gh, gb1, td_abs, td_acc);
   RTH_LAUNCHED();
   return RTH_OK;
 }
 
-int rth_td_heads_backward(const float *q0, const float *q1o, const float *q1t, const int64_t *a, const float *r,
-                          const float *done, const double *isw, int64_t B, int64_t A, float gamma_n, int32_t double_q,
-                          const float *h, int64_t ldh, const float *w2, int32_t H2, float *td_abs, float *loss_out,
-                          float *gh, float *gw2, float *gb2, float *gb1, float *td_acc, void *stream) {
-  RTH_REQUIRE(q0 && q1t && a && r && done && (q1o || !double_q) && h && w2 && td_abs && loss_out && gh && gw2 && gb2 &&
-                  gb1,
+static int td_heads_backward_impl(const float *q0, const float *q1o, const float *q1t, const int64_t *a,
+                                  const float *r, const float *done, const double *isw, int64_t B, int64_t A,
+                                  float gamma_n, int32_t double_q, const float *h, int64_t ldh, const Fc2 &f,
+                                  int32_t H2, float *td_abs, float *loss_out, float *gh, float *gb1, float *td_acc,
+                                  void *stream) {
+  RTH_REQUIRE(q0 && q1t && a && r && done && (q1o || !double_q) && h && td_abs && loss_out && gh && gb1,
               "rth_td_heads_backward: NULL argument");
   RTH_REQUIRE(B >= 1 && A >= 1 && A < kHbMaxA1 && B * (A + 1) <= kTdHbMaxElems && H2 >= kHbCols && H2 % kHbCols == 0 &&
                   ldh >= H2,
@@ -559,10 +733,79 @@ int rth_td_heads_backward(const float *q0, const float *q1o, const float *q1t, c
   const dim3 grid((unsigned)(H2 / kHbCols + 1)), block(kHbThreads);
   if (A + 1 <= 8)
     hipLaunchKernelGGL((k_td_heads_backward<8, 4>), grid, block, 0, as_stream(stream), q0, q1o, q1t, a, r, done, isw, B,
-                       (int)A, gamma_n, double_q, h, ldh, w2, H2, td_abs, loss_out, gh, gw2, gb2, gb1, td_acc);
+                       (int)A, gamma_n, double_q, h, ldh, f, H2, td_abs, loss_out, gh, gb1, td_acc);
   else
     hipLaunchKernelGGL((k_td_heads_backward<kHbMaxA1, 1>), grid, block, 0, as_stream(stream), q0, q1o, q1t, a, r, done,
-                       isw, B, (int)A, gamma_n, double_q, h, ldh, w2, H2, td_abs, loss_out, gh, gw2, gb2, gb1, td_acc);
+                       isw, B, (int)A, gamma_n, double_q, h, ldh, f, H2, td_abs, loss_out, gh, gb1, td_acc);
+  RTH_LAUNCHED();
+  return RTH_OK;
+}
+
+static Fc2 fc2_merged(const float *w2, float *gw2, float *gb2) {
+  Fc2 f{};
+  f.w2 = w2, f.gw2 = gw2, f.gb2 = gb2;
+  return f;
+}
+
+// params = {wa2, wv2, ...}, grads = {gwa2, gwv2, gba2, gbv2}
+static bool fc2_branches(const float *const *params, float *const *grads, int32_t H, int64_t A, Fc2 *f) {
+  if (!params || !params[0] || !params[1] || !grads || H < kHbCols || H % kHbCols != 0) return false;
+  for (int k = 0; k < 4; ++k)
+    if (!grads[k]) return false;
+  *f = Fc2{nullptr, nullptr, nullptr, params[0], params[1], grads[0], grads[1], grads[2], grads[3], (int)H, (int)A, 1};
+  return true;
+}
+
+int rth_heads_backward(const float *dq, const float *h, int64_t ldh, const float *w2, int64_t B, int32_t H2,
+                       int32_t A1, float *gh, float *gw2, float *gb2, float *gb1, const float *td_abs, float *td_acc,
+                       void *stream) {
+  RTH_REQUIRE(dq && h && w2 && gh && gw2 && gb2 && gb1, "rth_heads_backward: NULL argument");
+  return heads_backward_impl(dq, h, ldh, fc2_merged(w2, gw2, gb2), B, H2, A1, gh, gb1, td_abs, td_acc, stream);
+}
+
+int rth_heads_backward_branches(const float *dq, const float *h, int64_t ldh, const float *const *fc2_params,
+                                int32_t H, int64_t B, int64_t A, float *gh, float *const *fc2_grads, float *gb1,
+                                const float *td_abs, float *td_acc, void *stream) {
+  Fc2 f;
+  RTH_REQUIRE(dq && h && gh && gb1 && fc2_branches(fc2_params, fc2_grads, H, A, &f),
+              "rth_heads_backward_branches: NULL argument or H %d not a multiple of %d", H, kHbCols);
+  return heads_backward_impl(dq, h, ldh, f, B, 2 * H, (int32_t)A + 1, gh, gb1, td_abs, td_acc, stream);
+}
+
+int rth_td_heads_backward(const float *q0, const float *q1o, const float *q1t, const int64_t *a, const float *r,
+                          const float *done, const double *isw, int64_t B, int64_t A, float gamma_n, int32_t double_q,
+                          const float *h, int64_t ldh, const float *w2, int32_t H2, float *td_abs, float *loss_out,
+                          float *gh, float *gw2, float *gb2, float *gb1, float *td_acc, void *stream) {
+  RTH_REQUIRE(w2 && gw2 && gb2, "rth_td_heads_backward: NULL argument");
+  return td_heads_backward_impl(q0, q1o, q1t, a, r, done, isw, B, A, gamma_n, double_q, h, ldh,
+                                fc2_merged(w2, gw2, gb2), H2, td_abs, loss_out, gh, gb1, td_acc, stream);
+}
+
+int rth_td_heads_backward_branches(const float *q0, const float *q1o, const float *q1t, const int64_t *a,
+                                   const float *r, const float *done, const double *isw, int64_t B, int64_t A,
+                                   float gamma_n, int32_t double_q, const float *h, int64_t ldh,
+                                   const float *const *fc2_params, int32_t H, float *td_abs, float *loss_out, float *gh,
+                                   float *const *fc2_grads, float *gb1, float *td_acc, void *stream) {
+  Fc2 f;
+  RTH_REQUIRE(fc2_branches(fc2_params, fc2_grads, H, A, &f),
+              "rth_td_heads_backward_branches: NULL parameter / gradient or H %d not a multiple of %d", H, kHbCols);
+  return td_heads_backward_impl(q0, q1o, q1t, a, r, done, isw, B, A, gamma_n, double_q, h, ldh, f, 2 * H, td_abs,
+                                loss_out, gh, gb1, td_acc, stream);
+}
+
+int rth_heads_fc2(const float *h, int64_t ldh, int64_t n, int32_t H, int32_t A, const float *const *fc2_params,
+                  float *heads, void *stream) {
+  RTH_REQUIRE(h && heads && fc2_params && fc2_params[0] && fc2_params[1] && fc2_params[2] && fc2_params[3],
+              "rth_heads_fc2: NULL argument");
+  RTH_REQUIRE(n >= 0 && H >= 16 && H % 16 == 0 && A >= 1 && A < kHbMaxA1 && ldh >= 2 * H && ldh % 4 == 0 &&
+                  (reinterpret_cast<uintptr_t>(h) & 15) == 0,
+              "rth_heads_fc2: bad shape n=%lld H=%d A=%d ldh=%lld (H a multiple of 16, h 16-byte aligned rows)",
+              (long long)n, H, A, (long long)ldh);
+  if (n == 0) return RTH_OK;
+  RTH_REQUIRE(A + 1 <= 8 && H <= kFc2MaxH && H % 64 == 0,
+              "rth_heads_fc2: built for A + 1 <= 8 actions and H <= %d, a multiple of 64 (A=%d H=%d)", kFc2MaxH, A, H);
+  hipLaunchKernelGGL((k_heads_fc2<8>), dim3((unsigned)((n + 15) / 16)), dim3(256), 0, as_stream(stream), h, ldh, n,
+                     (int)H, (int)A, fc2_params[0], fc2_params[1], fc2_params[2], fc2_params[3], heads);
   RTH_LAUNCHED();
   return RTH_OK;
 }

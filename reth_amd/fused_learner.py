@@ -6,14 +6,19 @@ path of solver.py (compute_grads with torch.autograd), without the autograd engi
 
   forward   Q(s0) and Q(s1) of the online network as ONE pass over 2B stacks (the batch
             slot keeps s1 right behind s0, replay.HbmReplay.new_batch), each conv one
-            rth_conv_bias_relu launch, FC1 one hipBLASLt GEMM with the bias+ReLU epilogue,
-            the block-diagonal FC2 one GEMM;
+            rth_conv_bias_relu launch (the last one writes NCHW: FC1 reads the reference's
+            (C, H, W) flatten order), FC1 one hipBLASLt GEMM with the bias+ReLU epilogue on
+            the tied [2H, F] parameter storage (model._tie_heads), FC2 one rth_heads_fc2
+            launch on the branch parameters in place;
   TD        rth_td_huber on the raw heads -> |td|, loss, d(loss)/d(heads of s0), fused with
-  backward  FC2 + threshold + both bias sums (rth_td_heads_backward; also the Trainer's
-            mean |td|), FC1 as two GEMMs, conv3 / conv2 as rth_relu_bias_grad + MIOpen's data
-            and weight gradients (conv2's data gradient in rth_conv_dgrad), conv1 as rth_conv_relu_wgrad straight from the uint8 stacks
-            (f32 input: rth_relu_bias_grad + MIOpen's weight gradient), the merged-head
-            gradients mapped back onto the eight branch parameters by rth_heads_split_grad.
+  backward  FC2 + threshold + both bias sums (rth_td_heads_backward_branches: FC2's
+            gradients written in branch form; also the Trainer's mean |td|), FC1 as two
+            GEMMs (its branch gradients are row slices of the merged ones), conv3 as
+            rth_relu_bias_grad_nchw + MIOpen's data and weight gradients, conv2 as
+            rth_relu_bias_grad + rth_conv_dgrad + MIOpen's weight gradient, conv1 as
+            rth_conv_relu_wgrad straight from the uint8 stacks (f32 input:
+            rth_relu_bias_grad + MIOpen's weight gradient).  No merged copy of the heads is
+            built or split per update.
 
 Only the first B rows of the 2B forward are differentiated: they are contiguous views
 (NHWC, batch-major), so the backward reads them in place.
@@ -24,6 +29,7 @@ import torch
 
 from . import _lib
 from ._lib import call, ctypes, ptr, stream_ptr
+from .model import nchw_out
 
 
 TD_HB_MAX = 16384  # rth_td_heads_backward keeps B * (A + 1) TD gradient rows in LDS
@@ -70,8 +76,8 @@ def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None, mid=No
     (DQNSolver.target_heads).  td_acc (nullable f32 device scalar): += mean |td|.
 
     mid (optional callable) is handed each gradient bucket as soon as it is final: first the
-    merged heads' [gw1, gb1, gw2, gb2] (before the conv backward), then the conv weights' and
-    biases' (before the heads are split back onto the branch parameters).  The data-parallel
+    heads' [gw1, gb1, gwa2, gwv2, gba2, gbv2] (before the conv backward; the FC1 branch
+    gradients are row slices of gw1 / gb1), then the conv weights' and biases'.  The data-parallel
     capture ends a graph there, so the all-reduce of the first bucket overlaps the conv
     backward; whatever mid's caller does to a bucket in place is what the parameters get.
 
@@ -90,16 +96,20 @@ def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None, mid=No
     convs = net._convs()
     shapes = [sh for _, sh in net._torso_shapes(tuple(s0.shape[1:]), u8)]
     with torch.no_grad():
-        w1, b1, w2, b2 = net._merged_head_weights()
+        w1, b1, w2, b2 = net._merged_head_weights()  # FC1: the tied parameter storage
+        hp = net._head_params()
+        fc2p = (_lib.c_vp * 4)(*[p.data_ptr() for p in hp[4:]])  # FC2 read in place
         packed = net.pack_convs()
         st = stream_ptr()
         ys, h = [], x
         for li, (conv, shape) in enumerate(zip(convs, shapes)):
+            last = li == len(convs) - 1  # writes NCHW: FC1 reads the (C, H, W) flatten order
             ho = (shape.hin - shape.kh) // shape.stride + 1
             wo = (shape.win - shape.kw) // shape.stride + 1
             y = torch.empty((n, shape.cout, ho, wo), dtype=torch.float32, device=x.device,
-                            memory_format=torch.channels_last)
-            def launch(shape=shape, h=h, pk=net._packed_for(packed, li, u8), b=conv.bias, y=y):
+                            memory_format=torch.contiguous_format if last else torch.channels_last)
+            def launch(shape=nchw_out(shape) if last else shape, h=h, pk=net._packed_for(packed, li, u8),
+                       b=conv.bias, y=y):
                 call("rth_conv_bias_relu", ctypes.byref(shape), ptr(h), None, n, ptr(pk), ptr(b), ptr(y), stream_ptr())
 
             if probe is not None and li == 1:
@@ -108,16 +118,19 @@ def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None, mid=No
                 launch()
             ys.append(y)
             h = y
-        feat = h.permute(0, 2, 3, 1).reshape(n, -1)  # NHWC flatten: a view
+        feat = h.view(n, -1)  # the (C, H, W) flatten of the NCHW output: a view
         h1 = torch._addmm_activation(b1, feat, w1.t())
-        heads = torch.addmm(b2, h1, w2.t())
+        heads = net._heads_fc2(h1) if w2 is None else torch.addmm(b2, h1, w2.t())
         if q1t is None:
             q1t = solver.target_heads(s1)
         q0 = heads[:B]
         q1o = heads[B:] if pair else None
-        H2, A1 = w1.shape[0], w2.shape[0]
+        H2, A1 = w1.shape[0], hp[4].shape[0] + 1
+        Hh = H2 // 2
         gh1 = torch.empty((B, H2), dtype=torch.float32, device=x.device)
-        gw2, gb2, gb1 = torch.empty_like(w2), torch.empty_like(b2), torch.empty_like(b1)
+        gb1 = torch.empty_like(b1)
+        g2 = [torch.empty_like(p) for p in hp[4:]]  # the second layer's gradients, branch form
+        g2p = (_lib.c_vp * 4)(*[t.data_ptr() for t in g2])
         if B * A1 <= TD_HB_MAX:
             # TD/Huber + FC2 + threshold + bias sums in one launch
             dev = x.device
@@ -132,22 +145,21 @@ def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None, mid=No
                 raise ValueError("batch columns / target heads disagree with the batch")
             td_abs = torch.empty(B, dtype=torch.float32, device=dev)
             loss = torch.empty(1, dtype=torch.float32, device=dev)
-            call("rth_td_heads_backward", ptr(q0), ptr(q1o), ptr(q1t), ptr(a), ptr(r), ptr(done), ptr(isw), B, A1 - 1,
-                 float(solver.gamma_n), int(bool(solver.double_q)), ptr(h1), h1.stride(0), ptr(w2), H2, ptr(td_abs),
-                 ptr(loss), ptr(gh1), ptr(gw2), ptr(gb2), ptr(gb1), ptr(td_acc), st)
+            call("rth_td_heads_backward_branches", ptr(q0), ptr(q1o), ptr(q1t), ptr(a), ptr(r), ptr(done), ptr(isw), B,
+                 A1 - 1, float(solver.gamma_n), int(bool(solver.double_q)), ptr(h1), h1.stride(0), fc2p, Hh,
+                 ptr(td_abs), ptr(loss), ptr(gh1), g2p, ptr(gb1), ptr(td_acc), st)
         else:
             loss, td_abs, dq = td_huber_forward(q0, q1o, q1t, a, r, done, isw, solver.gamma_n, solver.double_q,
                                                 want_dq=True, dueling=True)
             # FC2 + threshold + bias sums
-            call("rth_heads_backward", ptr(dq), ptr(h1), h1.stride(0), ptr(w2), B, H2, A1, ptr(gh1), ptr(gw2),
-                 ptr(gb2), ptr(gb1), ptr(td_abs), ptr(td_acc), st)
+            call("rth_heads_backward_branches", ptr(dq), ptr(h1), h1.stride(0), fc2p, Hh, B, A1 - 1, ptr(gh1), g2p,
+                 ptr(gb1), ptr(td_abs), ptr(td_acc), st)
         # FC1
         gfeat = torch.mm(gh1, w1)
         gw1 = torch.mm(gh1.t(), feat[:B])
         if mid is not None:
-            mid([gw1, gb1, gw2, gb2])
-        c3 = convs[-1]
-        g = gfeat.view(B, ys[-1].shape[2], ys[-1].shape[3], c3.out_channels).permute(0, 3, 1, 2)
+            mid([gw1, gb1, *g2])
+        g = gfeat.view(ys[-1][:B].shape)  # NCHW, like the last conv's output
         grads = {}
         deferred = []  # bias gradients whose slabs wait for conv1's reduce launch
         if getattr(net, "_ws", None) is None or net._ws[0].device != x.device:
@@ -169,13 +181,17 @@ def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None, mid=No
                 grads[conv.weight], grads[conv.bias] = gw, db
                 deferred = []  # consumed
                 break
-            g = _nhwc(g)
-            gy = torch.empty_like(y)
             nb, c, hh, ww = y.shape
+            gy = torch.empty((nb, c, hh, ww), dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
             db = torch.empty(c, dtype=torch.float32, device=x.device)
             defer = u8  # finished by conv1's rth_conv_relu_wgrad_ex
-            call("rth_relu_bias_grad", ptr(g), ptr(y), ptr(gy), None if defer else ptr(db), ptr(net._ws[li]),
-                 nb * hh * ww, c, st)
+            if li == len(convs) - 1:  # NCHW output: mask + bias partials, gy written channels-last
+                call("rth_relu_bias_grad_nchw", ptr(g), ptr(y), ptr(gy), None if defer else ptr(db), ptr(net._ws[li]),
+                     nb, c, hh * ww, st)
+            else:
+                g = _nhwc(g)
+                call("rth_relu_bias_grad", ptr(g), ptr(y), ptr(gy), None if defer else ptr(db), ptr(net._ws[li]),
+                     nb * hh * ww, c, st)
             if defer:
                 deferred.append(_lib.BiasDeferred(net._ws[li].data_ptr(), db.data_ptr(), nb * hh * ww, c))
             xin = ys[li - 1][:B] if li > 0 else x[:B]
@@ -193,14 +209,10 @@ def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None, mid=No
         assert not deferred, "deferred bias gradients left unfinished"
         if mid is not None:
             mid([t for c in convs for t in (grads[c.weight], grads[c.bias])])
-        # merged heads -> the eight branch parameters
-        hp = net._head_params()
-        hgrads = [torch.empty_like(p) for p in hp]
-        c_, fh, fw = net._feat_chw
-        arr = (_lib.c_vp * 8)(*[t.data_ptr() for t in hgrads])
-        call("rth_heads_split_grad", ptr(gw1), ptr(gb1), ptr(gw2), ptr(gb2), hp[0].shape[0], hp[0].shape[1],
-             hp[4].shape[0], c_, fh * fw, arr, st)
-        for p, gr in zip(hp, hgrads):
+        # the eight branch parameters' gradients: FC1's are row slices of the merged ones (the
+        # parameters are row slices of one storage, model._tie_heads), FC2's were written in
+        # branch form by the heads' backward
+        for p, gr in zip(hp, [gw1[:Hh], gw1[Hh:], gb1[:Hh], gb1[Hh:], *g2]):
             grads[p] = gr
     for p in net.parameters():
         p.grad = grads[p]

@@ -14,6 +14,14 @@ def conv_out(size, k, s):
     return (size - k) // s + 1
 
 
+def nchw_out(shape):
+    """a copy of an rth_conv_shape with RTH_CONV_OUT_NCHW set (the conv writes NCHW)"""
+    from ._lib import CONV_OUT_NCHW, ConvShape
+
+    return ConvShape(shape.input | CONV_OUT_NCHW, shape.cin, shape.hin, shape.win, shape.cout, shape.kh, shape.kw,
+                     shape.stride)
+
+
 class DQNNetwork(nn.Module):
     """Nature-DQN torso + dueling heads (dqn_model.py:6-56): obs (C, H, W) -> Q[A]."""
 
@@ -35,8 +43,30 @@ class DQNNetwork(nn.Module):
         if dueling:
             self.fc_adv = nn.Sequential(nn.Linear(nfeat, hidden_unit), nn.ReLU(), nn.Linear(hidden_unit, num_actions))
             self.fc_value = nn.Sequential(nn.Linear(nfeat, hidden_unit), nn.ReLU(), nn.Linear(hidden_unit, 1))
+            self._tie_heads()
         else:
             self.fc = nn.Sequential(nn.Linear(nfeat, 512), nn.ReLU(), nn.Linear(512, num_actions))
+
+    def _tie_heads(self):
+        """FC1 of the two dueling branches as the row slices [0, H) / [H, 2H) of ONE [2H, F]
+        weight storage (and their biases of one [2H]): the merged FC1 that the fast path
+        multiplies by is the parameters themselves, read and updated in place (no merge or
+        split launch per update).  Parameter objects, names, shapes and values are unchanged
+        (state_dict, optimizers and torch.save streams see the reference's eight tensors);
+        re-tied after every device / dtype move (_apply)."""
+        a0, v0 = self.fc_adv[0], self.fc_value[0]
+        H = a0.weight.shape[0]
+        w = torch.cat([a0.weight.detach(), v0.weight.detach()])
+        b = torch.cat([a0.bias.detach(), v0.bias.detach()])
+        a0.weight.data, v0.weight.data = w[:H], w[H:]
+        a0.bias.data, v0.bias.data = b[:H], b[H:]
+        self._w1s, self._b1s = w, b
+
+    def _apply(self, fn, *args, **kwargs):
+        out = super()._apply(fn, *args, **kwargs)
+        if self.dueling:
+            self._tie_heads()
+        return out
 
     def forward(self, x):
         x = self.features(x).flatten(1)
@@ -48,49 +78,64 @@ class DQNNetwork(nn.Module):
 
     # ---------------------------------------------------------------- fused heads path
     # The same function with the two dueling branches merged: FC1 of both branches is one
-    # 3136 -> 512 GEMM with the bias and ReLU fused into hipBLASLt's epilogue, and the two
-    # output layers are one block-diagonal 512 -> A+1 GEMM.  It returns the raw heads
-    # [B, A+1] = (advantages, value); the HIP consumers (rth_td_huber, rth_eps_greedy in
-    # dueling mode) form Q = (V + A) - mean(A) themselves.  The parameters (and state_dict)
-    # stay the reference's; the merged weights are either built per call (training, autograd
-    # flows back into the branch parameters) or cached (`freeze_heads`, inference copies whose
-    # weights change only at refresh points: target sync, actor weight reload).
+    # 3136 -> 512 GEMM with the bias and ReLU fused into hipBLASLt's epilogue (its weight is
+    # the tied [2H, F] storage, _tie_heads; the features in the reference's (C, H, W) flatten
+    # order: the last HIP conv writes NCHW), and the two output layers are one 512 -> A+1
+    # launch reading the branch parameters in place (rth_heads_fc2; block-diagonal).  It returns the raw heads [B, A+1] = (advantages, value); the HIP
+    # consumers (rth_td_huber, rth_eps_greedy in dueling mode) form Q = (V + A) - mean(A)
+    # themselves.  Under autograd the merged weights are a differentiable function of the
+    # eight parameters (a copy, block-diagonal FC2 as one GEMM); otherwise nothing is built.
     def _head_params(self):
         a0, v0, a2, v2 = self.fc_adv[0], self.fc_value[0], self.fc_adv[2], self.fc_value[2]
         return [a0.weight, v0.weight, a0.bias, v0.bias, a2.weight, v2.weight, a2.bias, v2.bias]
 
     def _merged_head_weights(self):
+        """(w1, b1, w2, b2) of the merged heads.  Under autograd (a parameter requires grad) a
+        differentiable copy built from the eight parameters; otherwise w1 / b1 are the tied
+        storage itself and, on the GPU, w2 / b2 are None: the second layer is read from the
+        branch parameters in place (rth_heads_fc2 / rth_td_heads_backward_branches)."""
         ps = self._head_params()
-        if ps[0].is_cuda:  # one HIP launch (and one for the gradients), qnet.hip
-            c, fh, fw = self._feat_chw
-            dims = (ps[0].shape[0], ps[0].shape[1], ps[4].shape[0], c if self.hwc_features else 0, fh * fw)
-            return _MergeHeads.apply(dims, *ps)
         a0, v0, a2, v2 = self.fc_adv[0], self.fc_value[0], self.fc_adv[2], self.fc_value[2]
-        if self.hwc_features:  # FC1 columns permuted (C,H,W) -> (H,W,C): the NHWC flatten is a view
-            c, fh, fw = self._feat_chw
-            hwc = lambda wt: wt.view(wt.shape[0], c, fh, fw).permute(0, 2, 3, 1)
-            w1 = torch.cat([hwc(a0.weight), hwc(v0.weight)]).reshape(2 * a0.weight.shape[0], -1)
-        else:
-            w1 = torch.cat([a0.weight, v0.weight])
-        b1 = torch.cat([a0.bias, v0.bias])
         A, H = a2.weight.shape
+        if torch.is_grad_enabled() and any(p.requires_grad for p in ps):
+            if ps[0].is_cuda:  # one HIP launch (and one for the gradients), qnet.hip
+                return _MergeHeads.apply((H, ps[0].shape[1], A, 0, 1), *ps)
+            w1, b1 = torch.cat([a0.weight, v0.weight]), torch.cat([a0.bias, v0.bias])
+        else:
+            w1, b1 = self._w1s, self._b1s
+            if ps[0].is_cuda and self._fc2_inplace():
+                return w1, b1, None, None
         w2 = torch.cat([torch.cat([a2.weight, a2.weight.new_zeros(A, H)], 1),
                         torch.cat([v2.weight.new_zeros(1, H), v2.weight], 1)])
         b2 = torch.cat([a2.bias, v2.bias])
         return w1, b1, w2, b2
 
+    def _fc2_inplace(self):
+        """rth_heads_fc2's built shapes: A + 1 <= 8 actions (Atari's minimal sets: Pong 6,
+        Breakout 4, BeamRider 9 is not), H a multiple of 64 up to 512"""
+        A, H = self.fc_adv[2].weight.shape
+        return A + 1 <= 8 and H % 64 == 0 and H <= 512
+
+    def _heads_fc2(self, h):
+        """the second layer on h = relu(FC1) [n, 2H] from the branch parameters in place
+        (rth_heads_fc2): raw heads [n, A+1]"""
+        from ._lib import c_vp, call, ptr, stream_ptr
+
+        ps = self._head_params()[4:]
+        A, H = ps[0].shape
+        out = torch.empty((h.shape[0], A + 1), dtype=torch.float32, device=h.device)
+        arr = (c_vp * 4)(*[p.data_ptr() for p in ps])
+        call("rth_heads_fc2", ptr(h), h.stride(0), h.shape[0], H, A, arr, ptr(out), stream_ptr())
+        return out
+
     @torch.no_grad()
     def freeze_heads(self):
-        """(re)build the cached merged head weights and packed conv weights in place (stable
-        storage for graph replay): for copies whose parameters change only at refresh points
-        (target sync, actor weight reload)"""
-        merged = self._merged_head_weights()
-        if getattr(self, "_frozen", None) is None or self._frozen[0].shape != merged[0].shape:
-            self._frozen = [t.clone() for t in merged]
-        else:
-            for dst, src in zip(self._frozen, merged):
-                dst.copy_(src)
-        if self.hwc_features and merged[0].is_cuda:
+        """(re)build the cached packed conv weights in place (stable storage for graph
+        replay): for copies whose parameters change only at refresh points (target sync,
+        actor weight reload).  The heads need nothing: FC1 is the tied parameter storage and
+        the second layer is read from its parameters in place."""
+        self._frozen = list(self._merged_head_weights())
+        if self.hwc_features and self._frozen[0].is_cuda:
             self._frozen_packed = self.pack_convs(out=getattr(self, "_frozen_packed", None))
 
     def forward_heads(self, x, merged=None, rows=None, packed=None, n_dev=None):
@@ -111,12 +156,14 @@ class DQNNetwork(nn.Module):
             if packed is None and frozen:
                 packed = getattr(self, "_frozen_packed", None)
             h = self._features_nhwc(x, rows, packed, n_dev)
-            h = h.permute(0, 2, 3, 1).reshape(h.shape[0], -1)  # a view of the NHWC activations
         else:
             if x.dtype == torch.uint8 or rows is not None or n_dev is not None:
                 raise ValueError("uint8 / row-indexed / counted observations need the HIP torso (hwc_features)")
-            h = self.features(x).flatten(1)
+            h = self.features(x)
+        h = h.reshape(h.shape[0], -1)  # (C, H, W) flatten: a view of the last HIP conv's NCHW output
         h = _LinearReLU.apply(h, w1, b1)
+        if w2 is None:  # the second layer from the branch parameters in place
+            return self._heads_fc2(h)
         return torch.addmm(b2, h, w2.t())
 
     def _convs(self):
@@ -178,8 +225,9 @@ class DQNNetwork(nn.Module):
     def _features_nhwc(self, x, rows=None, packed=None, n_dev=None):
         """the conv torso on channels-last activations: each Conv2d -> ReLU is one HIP
         implicit-GEMM launch with the bias and ReLU fused (rth_conv_bias_relu) where the
-        geometry is built, else MIOpen + the rth_bias_relu pass; backward: rth_relu_bias_grad
-        and MIOpen's data/weight gradients"""
+        geometry is built, else MIOpen + the rth_bias_relu pass; the last HIP conv writes its
+        output NCHW (FC1 reads the reference's (C, H, W) flatten order); backward:
+        rth_relu_bias_grad(_nchw) and MIOpen's data/weight gradients"""
         from . import _lib
 
         u8 = x.dtype == torch.uint8
@@ -202,20 +250,23 @@ class DQNNetwork(nn.Module):
             n = rows.numel() if rows is not None else x.shape[0]
             for li, conv in enumerate(convs):
                 shape = shapes[li][1]
+                last = li == len(convs) - 1
                 ho = (shape.hin - shape.kh) // shape.stride + 1
                 wo = (shape.win - shape.kw) // shape.stride + 1
                 y = torch.empty((n, shape.cout, ho, wo), dtype=torch.float32, device=x.device,
-                                memory_format=torch.channels_last)
-                call("rth_conv_bias_relu_upto", _lib.ctypes.byref(shape), ptr(x), ptr(rows) if li == 0 else None, n,
-                     ptr(n_dev), ptr(self._packed_for(packed, li, u8)), ptr(conv.bias), ptr(y), stream_ptr())
+                                memory_format=torch.contiguous_format if last else torch.channels_last)
+                call("rth_conv_bias_relu_upto", _lib.ctypes.byref(nchw_out(shape) if last else shape), ptr(x),
+                     ptr(rows) if li == 0 else None, n, ptr(n_dev), ptr(self._packed_for(packed, li, u8)),
+                     ptr(conv.bias), ptr(y), stream_ptr())
                 x = y
             return x
         for li, (conv, ws) in enumerate(zip(convs, self._ws)):
             shape = shapes[li][1]
             if shape is not None:
                 pk = self._packed_for(packed, li, u8)
-                x = _HipConvBiasReLU.apply(x, conv.weight, conv.bias, pk, shape, conv.stride, ws,
-                                           rows if li == 0 else None)
+                last = li == len(convs) - 1 and li > 0  # the last conv writes NCHW (FC1's flatten order)
+                x = _HipConvBiasReLU.apply(x, conv.weight, conv.bias, pk, nchw_out(shape) if last else shape,
+                                           conv.stride, ws, rows if li == 0 else None)
             else:
                 if x.dtype == torch.uint8 or (li == 0 and rows is not None):
                     raise ValueError("uint8 / row-indexed observations need rth_conv_bias_relu's conv1 geometry")
@@ -357,13 +408,17 @@ class _HipConvBiasReLU(torch.autograd.Function):
     def forward(ctx, x, w, b, packed, shape, stride, ws, rows):
         from ._lib import call, ctypes, ptr, stream_ptr
 
+        from ._lib import CONV_OUT_NCHW
+
         n = rows.numel() if rows is not None else x.shape[0]
         ho = (shape.hin - shape.kh) // shape.stride + 1
         wo = (shape.win - shape.kw) // shape.stride + 1
+        nchw = bool(shape.input & CONV_OUT_NCHW)
         y = torch.empty((n, shape.cout, ho, wo), dtype=torch.float32, device=x.device,
-                        memory_format=torch.channels_last)
+                        memory_format=torch.contiguous_format if nchw else torch.channels_last)
         call("rth_conv_bias_relu", ctypes.byref(shape), ptr(x), ptr(rows), n, ptr(packed), ptr(b), ptr(y),
              stream_ptr())
+        ctx.nchw = nchw
         ctx.save_for_backward(x, w, y, rows)
         ctx.stride, ctx.ws, ctx.shape = list(stride), ws, shape
         ctx.wgrad_ws = None
@@ -376,8 +431,9 @@ class _HipConvBiasReLU(torch.autograd.Function):
         from ._lib import call, ptr, stream_ptr
 
         x, w, y, rows = ctx.saved_tensors
-        if not g.is_contiguous(memory_format=torch.channels_last):
-            g = g.contiguous(memory_format=torch.channels_last)
+        fmt = torch.contiguous_format if ctx.nchw else torch.channels_last
+        if not g.is_contiguous(memory_format=fmt):
+            g = g.contiguous(memory_format=fmt)
         if x.dtype == torch.uint8 and ctx.wgrad_ws is not None:
             # conv1 on uint8 stacks: ReLU mask + weight and bias gradients in one HIP pass
             # (rth_conv_relu_wgrad), straight from the stacks
@@ -393,10 +449,13 @@ class _HipConvBiasReLU(torch.autograd.Function):
             w = w.contiguous(memory_format=torch.channels_last)
         if x.dtype == torch.uint8:
             x = (x if rows is None else x[rows]).float().contiguous(memory_format=torch.channels_last)
-        gy = torch.empty_like(y)
         n, c, h, wd = y.shape
+        gy = torch.empty((n, c, h, wd), dtype=y.dtype, device=y.device, memory_format=torch.channels_last)
         db = torch.empty(c, dtype=y.dtype, device=y.device)
-        call("rth_relu_bias_grad", ptr(g), ptr(y), ptr(gy), ptr(db), ptr(ctx.ws), n * h * wd, c, stream_ptr())
+        if ctx.nchw:  # mask + bias gradient from the NCHW output, gy written channels-last
+            call("rth_relu_bias_grad_nchw", ptr(g), ptr(y), ptr(gy), ptr(db), ptr(ctx.ws), n, c, h * wd, stream_ptr())
+        else:
+            call("rth_relu_bias_grad", ptr(g), ptr(y), ptr(gy), ptr(db), ptr(ctx.ws), n * h * wd, c, stream_ptr())
         need_x = ctx.needs_input_grad[0]
         gx, gw, _ = torch.ops.aten.convolution_backward(gy, x, w, None, ctx.stride, [0, 0], [1, 1], False, [0, 0], 1,
                                                         [need_x, ctx.needs_input_grad[1], False])

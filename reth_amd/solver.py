@@ -147,7 +147,7 @@ class DQNSolver(Algorithm):
         if channels_last and len(obs_shape) == 3:
             for net in (self.q_network, self.target_q_network):
                 if hasattr(net, "hwc_features"):
-                    net.hwc_features = True  # HIP conv epilogues, NHWC feature order (model.py)
+                    net.hwc_features = True  # HIP conv torso on channels-last activations (model.py)
         if models.get("optimizer") is not None:
             self.optimizer = models["optimizer"]
         elif models.get("fused_adam", fused_adam):  # clip_grad_norm_ + Adam in one HIP call (optim.py)

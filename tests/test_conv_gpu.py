@@ -127,24 +127,29 @@ def _torso_net(dev, seed=0):
 
 
 def test_frozen_packed_weights_follow_refresh(dev):
-    """a frozen copy's packed conv weights (and merged heads) are rebuilt by freeze_heads
-    (target sync / actor reload) and used by default; stale until then (biases of the conv
-    layers are read live)"""
+    """a frozen copy's packed conv weights are rebuilt by freeze_heads (target sync / actor
+    reload) and used by default; stale until then (the conv biases and the heads -- FC1's
+    tied storage, FC2's parameters -- are read live)"""
     net = _torso_net(dev, seed=2)
     x = torch.randint(0, 256, (8, 4, 84, 84), dtype=torch.uint8, device=dev)
     with torch.no_grad():
         net.freeze_heads()
         q0 = net.forward_heads(x)
         for name, p in net.named_parameters():
-            if name.endswith("weight"):
+            if name.startswith("features") and name.endswith("weight"):  # the convs
                 p.mul_(1.01)
         q_stale = net.forward_heads(x)
         net.freeze_heads()
         q1 = net.forward_heads(x)
         q_fresh = net.forward_heads(x, net._merged_head_weights(), packed=net.pack_convs())
+        net.fc_adv[0].weight.mul_(1.01)  # FC1: live
+        net.fc_value[2].weight.mul_(1.01)  # FC2: live
+        q_fc1 = net.forward_heads(x)
+        q_fc1_fresh = net.forward_heads(x, net._merged_head_weights(), packed=net.pack_convs())
     assert torch.equal(q0, q_stale)
     assert not torch.equal(q0, q1)
     torch.testing.assert_close(q1, q_fresh, rtol=0, atol=0)
+    assert not torch.equal(q_fc1, q1) and torch.equal(q_fc1, q_fc1_fresh)
 
 
 def test_forward_heads_u8_rows_matches_miopen(dev):
@@ -356,3 +361,32 @@ def test_deferred_bias_grads_finished_by_conv1_reduce(dev):
     assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
     for got, ref in zip(outs, want):
         assert torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("gi,n", [(1, 3), (2, 1), (2, 37), (2, 1024)])
+def test_conv_nchw_output(dev, gi, n):
+    """RTH_CONV_OUT_NCHW: the same values as the NHWC output, written [n, cout, hout, wout]
+    (the last conv feeding FC1 in the (C, H, W) flatten order); refused for the uint8 conv1"""
+    from reth_amd import _lib
+
+    geom = GEOMS[gi]
+    cin, h, wd, cout, k, s = geom
+    g = torch.Generator().manual_seed(77 + n)
+    x = (torch.rand((n, cin, h, wd), generator=g) * 2 - 1).to(dev).contiguous(memory_format=torch.channels_last)
+    w = ((torch.rand((cout, cin, k, k), generator=g) * 2 - 1) / np.sqrt(cin * k * k)).to(dev)
+    b = ((torch.rand(cout, generator=g) * 2 - 1) * 0.1).to(dev)
+    shape = _shape(_lib.CONV_F32_NHWC, *geom)
+    flagged = _shape(_lib.CONV_F32_NHWC | _lib.CONV_OUT_NCHW, *geom)
+    assert _lib.lib().rth_conv_supported(_lib.ctypes.byref(flagged)) == 1
+    wt = w.contiguous(memory_format=torch.channels_last)
+    pk = torch.empty(_lib.lib().rth_conv_packed_bytes(_lib.ctypes.byref(shape)) // 4, device=dev)
+    _lib.call("rth_conv_pack", _lib.ctypes.byref(shape), wt.data_ptr(), pk.data_ptr(), _lib.stream_ptr())
+    ho = (h - k) // s + 1
+    y_hwc = torch.empty((n, cout, ho, ho), device=dev, memory_format=torch.channels_last)
+    y_chw = torch.full((n, cout, ho, ho), float("nan"), device=dev)
+    for shp, y in ((shape, y_hwc), (flagged, y_chw)):
+        _lib.call("rth_conv_bias_relu", _lib.ctypes.byref(shp), x.data_ptr(), None, n, pk.data_ptr(), b.data_ptr(),
+                  y.data_ptr(), _lib.stream_ptr())
+    assert y_chw.is_contiguous() and torch.equal(y_chw, y_hwc)
+    u8 = _shape(_lib.CONV_U8_CHW | _lib.CONV_OUT_NCHW, *GEOMS[0])
+    assert _lib.lib().rth_conv_supported(_lib.ctypes.byref(u8)) == 0

@@ -156,3 +156,83 @@ def test_td_heads_backward_equals_two_launches(dev, B, A, double_q):
     for x, y in zip(outs[0][:6], outs[1][:6]):
         assert torch.equal(x, y)
     torch.testing.assert_close(outs[0][6], outs[1][6], rtol=1e-6, atol=0)
+
+
+@pytest.mark.parametrize("B,A,fused", [(512, 6, True), (37, 4, True), (64, 18, False), (300, 6, False)])
+def test_heads_backward_branch_form_equals_merged(dev, B, A, fused):
+    """rth_(td_)heads_backward_branches (the second layer read and its gradients written in the
+    reference's four tensors) == the merged block-diagonal form on the diagonal blocks, bit for
+    bit (the off-diagonal weights are exact zeros in both); gh, gb1, |td| identical"""
+    from reth_amd import _lib
+    from reth_amd._lib import call, ptr, stream_ptr
+
+    g = torch.Generator(device=dev).manual_seed(3 * B + A)
+    H, A1 = 256, A + 1
+    H2 = 2 * H
+    q0, q1o, q1t = (torch.randn(B, A1, device=dev, generator=g) for _ in range(3))
+    a = torch.randint(0, A, (B,), device=dev, generator=g)
+    r = torch.randn(B, device=dev, generator=g)
+    done = (torch.rand(B, device=dev, generator=g) < 0.2).float()
+    isw = torch.rand(B, device=dev, generator=g, dtype=torch.float64) + 0.5
+    h = torch.relu(torch.randn(B, H2, device=dev, generator=g))
+    wa2, wv2 = torch.randn(A, H, device=dev, generator=g) * 0.05, torch.randn(1, H, device=dev, generator=g) * 0.05
+    w2 = torch.zeros(A1, H2, device=dev)
+    w2[:A, :H], w2[A:, H:] = wa2, wv2
+    gn = float(np.float32(0.99 ** 3))
+    dq = torch.empty(B, A1, device=dev)
+    td0 = torch.empty(B, device=dev)
+    call("rth_td_huber", ptr(q0), ptr(q1o), ptr(q1t), ptr(a), ptr(r), ptr(done), ptr(isw), B, A, gn, 1, 1, None,
+         ptr(td0), None, ptr(torch.empty(1, device=dev)), ptr(dq), stream_ptr())
+    outs = []
+    for branches in (False, True):
+        td, loss, acc = torch.empty(B, device=dev), torch.empty(1, device=dev), torch.zeros((), device=dev)
+        gh, gb1 = torch.empty(B, H2, device=dev), torch.empty(H2, device=dev)
+        gw2, gb2 = torch.full((A1, H2), float("nan"), device=dev), torch.empty(A1, device=dev)
+        g2 = [torch.empty(A, H, device=dev), torch.empty(1, H, device=dev), torch.empty(A, device=dev),
+              torch.empty(1, device=dev)]
+        pa = (_lib.c_vp * 4)(wa2.data_ptr(), wv2.data_ptr(), None, None)
+        ga = (_lib.c_vp * 4)(*[t.data_ptr() for t in g2])
+        if fused and branches:
+            call("rth_td_heads_backward_branches", ptr(q0), ptr(q1o), ptr(q1t), ptr(a), ptr(r), ptr(done), ptr(isw), B,
+                 A, gn, 1, ptr(h), H2, pa, H, ptr(td), ptr(loss), ptr(gh), ga, ptr(gb1), ptr(acc), stream_ptr())
+        elif fused:
+            call("rth_td_heads_backward", ptr(q0), ptr(q1o), ptr(q1t), ptr(a), ptr(r), ptr(done), ptr(isw), B, A, gn,
+                 1, ptr(h), H2, ptr(w2), H2, ptr(td), ptr(loss), ptr(gh), ptr(gw2), ptr(gb2), ptr(gb1), ptr(acc),
+                 stream_ptr())
+        elif branches:
+            call("rth_heads_backward_branches", ptr(dq), ptr(h), H2, pa, H, B, A, ptr(gh), ga, ptr(gb1), ptr(td0),
+                 ptr(acc), stream_ptr())
+        else:
+            call("rth_heads_backward", ptr(dq), ptr(h), H2, ptr(w2), B, H2, A1, ptr(gh), ptr(gw2), ptr(gb2), ptr(gb1),
+                 ptr(td0), ptr(acc), stream_ptr())
+        if not branches:
+            g2 = [gw2[:A, :H], gw2[A:, H:], gb2[:A], gb2[A:]]
+        outs.append((gh, gb1, acc, *g2) + ((td,) if fused else ()))
+    for x, y in zip(*outs):
+        assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("n,A", [(1, 6), (260, 6), (1024, 4), (33, 7)])
+def test_heads_fc2_forward(dev, n, A):
+    """rth_heads_fc2 (the second layer from the branch parameters) == the block-diagonal
+    addmm within fp32 summation error, against an fp64 reference; more than 7 actions are
+    refused (the model then builds the merged second layer)"""
+    from reth_amd import _lib
+    from reth_amd._lib import call, ptr, stream_ptr
+
+    g = torch.Generator(device=dev).manual_seed(n + A)
+    H = 256
+    h = torch.relu(torch.randn(n, 2 * H, device=dev, generator=g))
+    ps = [torch.randn(A, H, device=dev, generator=g) * 0.05, torch.randn(1, H, device=dev, generator=g) * 0.05,
+          torch.randn(A, device=dev, generator=g), torch.randn(1, device=dev, generator=g)]
+    out = torch.full((n, A + 1), float("nan"), device=dev)
+    call("rth_heads_fc2", ptr(h), 2 * H, n, H, A, (_lib.c_vp * 4)(*[p.data_ptr() for p in ps]), ptr(out),
+         stream_ptr())
+    hd = h.double()
+    want = torch.cat([hd[:, :H] @ ps[0].double().t() + ps[2].double(), hd[:, H:] @ ps[1].double().t() + ps[3].double()],
+                     1)
+    torch.testing.assert_close(out.double(), want, rtol=1e-5, atol=1e-5)
+    big = [torch.zeros(9, H, device=dev), ps[1], torch.zeros(9, device=dev), ps[3]]
+    with pytest.raises(_lib.RethHipError):
+        call("rth_heads_fc2", ptr(h), 2 * H, n, H, 9, (_lib.c_vp * 4)(*[p.data_ptr() for p in big]), ptr(out),
+             stream_ptr())

@@ -146,8 +146,8 @@ def test_conv_epilogue_kernels(dev, C, hw):
 
 
 def test_nhwc_features_forward_backward_match_module(dev):
-    """the HIP-epilogue NHWC torso + permuted FC1 columns == the reference module (values
-    and every parameter gradient, fp32 tolerance)"""
+    """the HIP-epilogue channels-last torso (the last conv written NCHW, FC1 on the tied
+    storage) == the reference module (values and every parameter gradient, fp32 tolerance)"""
     from reth_amd.model import DQNNetwork
 
     torch.manual_seed(11)
@@ -257,29 +257,108 @@ def test_merged_heads_kernels_match_torch(dev, hwc):
             assert torch.equal(p.grad.cpu(), q.grad), name
 
 
-def test_heads_merge_split_roundtrip_nhwc(dev):
-    """rth_heads_merge / rth_heads_split_grad (one LDS row transpose per FC1 row) against the
-    torch construction of the merged NHWC-permuted heads, and split(merge) == identity"""
+def test_heads_merge_split_kernels_nhwc_permutation(dev):
+    """rth_heads_merge / rth_heads_split_grad with a C x P column permutation (C > 0: one LDS
+    row transpose per FC1 row) against the torch construction, and split(merge) == identity"""
+    from reth_amd import _lib
     from reth_amd.model import DQNNetwork
 
     torch.manual_seed(11)
     net = DQNNetwork((4, 84, 84), 6).to(dev)
-    net.hwc_features = True
+    ps = [p.detach() for p in net._head_params()]
+    H, F, A = ps[0].shape[0], ps[0].shape[1], ps[4].shape[0]
+    o = dict(device=dev)
+    w1, b1, w2, b2 = torch.empty(2 * H, F, **o), torch.empty(2 * H, **o), torch.empty(A + 1, 2 * H, **o), \
+        torch.empty(A + 1, **o)
+    arr = (_lib.c_vp * 8)(*[p.data_ptr() for p in ps])
+    _lib.call("rth_heads_merge", arr, H, F, A, 64, 49, w1.data_ptr(), b1.data_ptr(), w2.data_ptr(), b2.data_ptr(),
+              _lib.stream_ptr())
+    hwc = lambda wt: wt.view(wt.shape[0], 64, 7, 7).permute(0, 2, 3, 1).reshape(wt.shape[0], -1)
+    assert torch.equal(w1, torch.cat([hwc(ps[0]), hwc(ps[1])])) and torch.equal(b1, torch.cat([ps[2], ps[3]]))
+    grads = [torch.empty_like(p) for p in ps]
+    arr = (_lib.c_vp * 8)(*[g.data_ptr() for g in grads])
+    _lib.call("rth_heads_split_grad", w1.data_ptr(), b1.data_ptr(), w2.data_ptr(), b2.data_ptr(), H, F, A, 64, 49,
+              arr, _lib.stream_ptr())
+    assert all(torch.equal(g, p) for g, p in zip(grads, ps))  # the inverse permutation
+
+
+def test_tied_heads_storage(dev):
+    """the two FC1 branches are row slices of one storage (model._tie_heads) on every device
+    and after .to(memory_format=...); state_dict / load_state_dict / parameters() keep the
+    reference's eight tensors; the no-grad merged FC1 IS that storage"""
+    from reth_amd.model import DQNNetwork
+
+    torch.manual_seed(2)
+    cpu = DQNNetwork((4, 84, 84), 6)
+    ref = {k: v.clone() for k, v in cpu.state_dict().items()}
+    net = DQNNetwork((4, 84, 84), 6)
+    net.load_state_dict(ref)
+    net = net.to(dev, memory_format=torch.channels_last)
+    a0, v0 = net.fc_adv[0], net.fc_value[0]
+    for m in (cpu, net):
+        w, b = m._w1s, m._b1s
+        H = m.fc_adv[0].weight.shape[0]
+        assert m.fc_adv[0].weight.data_ptr() == w.data_ptr()
+        assert m.fc_value[0].weight.data_ptr() == w.data_ptr() + H * w.shape[1] * 4
+        assert m.fc_adv[0].bias.data_ptr() == b.data_ptr() and m.fc_value[0].bias.data_ptr() == b.data_ptr() + H * 4
+    assert list(net.state_dict()) == list(ref) and len(list(net.parameters())) == 14
+    assert all(torch.equal(v.cpu(), ref[k]) for k, v in net.state_dict().items())
     with torch.no_grad():
-        got = net._merged_head_weights()
-        a0, v0, a2, v2 = net.fc_adv[0], net.fc_value[0], net.fc_adv[2], net.fc_value[2]
-        hwc = lambda wt: wt.view(wt.shape[0], 64, 7, 7).permute(0, 2, 3, 1).reshape(wt.shape[0], -1)
-        want_w1 = torch.cat([hwc(a0.weight), hwc(v0.weight)])
-        assert torch.equal(got[0], want_w1)
-        assert torch.equal(got[1], torch.cat([a0.bias, v0.bias]))
-    # gradient split: d/dparams of sum(merged * R) == the branch slices of R, un-permuted
-    ps = net._head_params()
-    merged = net._merged_head_weights()
-    rs = [torch.randn_like(m) for m in merged]
-    sum((m * r).sum() for m, r in zip(merged, rs)).backward()
-    unperm = lambda g: g.view(g.shape[0], 7, 7, 64).permute(0, 3, 1, 2).reshape(g.shape[0], -1)
-    H = a0.weight.shape[0]
-    assert torch.equal(ps[0].grad, unperm(rs[0][:H])) and torch.equal(ps[1].grad, unperm(rs[0][H:]))
-    assert torch.equal(ps[2].grad, rs[1][:H]) and torch.equal(ps[3].grad, rs[1][H:])
-    assert torch.equal(ps[4].grad, rs[2][:6, :H]) and torch.equal(ps[5].grad, rs[2][6:, H:])
-    assert torch.equal(ps[6].grad, rs[3][:6]) and torch.equal(ps[7].grad, rs[3][6:])
+        w1, b1, w2, b2 = net._merged_head_weights()
+        assert w1.data_ptr() == net._w1s.data_ptr() and b1.data_ptr() == net._b1s.data_ptr()
+        assert w2 is None and b2 is None  # the second layer is read from its parameters in place
+    sd = {k: v + 1.0 for k, v in ref.items()}
+    net.load_state_dict(sd)  # copies into the shared storage
+    assert torch.equal(net._w1s[: a0.weight.shape[0]].cpu(), sd["fc_adv.0.weight"])
+    assert torch.equal(net._w1s[a0.weight.shape[0]:].cpu(), sd["fc_value.0.weight"])
+    assert torch.equal(v0.bias.cpu(), sd["fc_value.0.bias"])
+
+
+def test_fc2_only_merge_split(dev):
+    """RTH_HEADS_FC2_ONLY: the block-diagonal second layer built / split without FC1"""
+    from reth_amd import _lib
+    from reth_amd.model import DQNNetwork
+
+    torch.manual_seed(4)
+    net = DQNNetwork((4, 84, 84), 6).to(dev)
+    ps = [p.detach() for p in net._head_params()]
+    H, F, A = ps[0].shape[0], ps[0].shape[1], ps[4].shape[0]
+    w2, b2 = torch.full((A + 1, 2 * H), 7.0, device=dev), torch.empty(A + 1, device=dev)
+    arr = (_lib.c_vp * 8)(*[None] * 4, *[p.data_ptr() for p in ps[4:]])
+    _lib.call("rth_heads_merge", arr, H, F, A, _lib.HEADS_FC2_ONLY, 1, None, None, w2.data_ptr(), b2.data_ptr(),
+              _lib.stream_ptr())
+    want = torch.zeros(A + 1, 2 * H, device=dev)
+    want[:A, :H], want[A:, H:] = ps[4], ps[5]
+    assert torch.equal(w2, want) and torch.equal(b2, torch.cat([ps[6], ps[7]]))
+    gw2, gb2 = torch.randn(A + 1, 2 * H, device=dev), torch.randn(A + 1, device=dev)
+    grads = [torch.empty_like(p) for p in ps[4:]]
+    arr = (_lib.c_vp * 8)(*[None] * 4, *[g.data_ptr() for g in grads])
+    _lib.call("rth_heads_split_grad", None, None, gw2.data_ptr(), gb2.data_ptr(), H, F, A, _lib.HEADS_FC2_ONLY, 1,
+              arr, _lib.stream_ptr())
+    assert torch.equal(grads[0], gw2[:A, :H]) and torch.equal(grads[1], gw2[A:, H:])
+    assert torch.equal(grads[2], gb2[:A]) and torch.equal(grads[3], gb2[A:])
+
+
+@pytest.mark.parametrize("n", [1, 37, 512])
+def test_relu_bias_grad_nchw(dev, n):
+    """rth_relu_bias_grad_nchw: the mask bit for bit, gy written channels-last, bias sums
+    deterministic and within fp32 summation error; a deferred job (rows = n * P) finishes the
+    same slabs"""
+    from reth_amd import _lib
+
+    gen = torch.Generator(device=dev).manual_seed(n)
+    C, P = 64, 49
+    y = torch.relu(torch.randn(n, C, 7, 7, device=dev, generator=gen))
+    g = torch.randn(n, C, 7, 7, device=dev, generator=gen)
+    ws = torch.zeros(_lib.lib().rth_relu_bias_grad_workspace(C), dtype=torch.uint8, device=dev)
+    gy = torch.empty(n, C, 7, 7, device=dev, memory_format=torch.channels_last)
+    db = torch.empty(C, device=dev)
+    _lib.call("rth_relu_bias_grad_nchw", g.data_ptr(), y.data_ptr(), gy.data_ptr(), db.data_ptr(), ws.data_ptr(), n,
+              C, P, _lib.stream_ptr())
+    want = torch.ops.aten.threshold_backward(g, y, 0)
+    assert gy.is_contiguous(memory_format=torch.channels_last) and torch.equal(gy, want)
+    torch.testing.assert_close(db, want.sum((0, 2, 3)), rtol=1e-5, atol=1e-4)
+    db2 = torch.empty(C, device=dev)
+    _lib.call("rth_relu_bias_grad_nchw", g.data_ptr(), y.data_ptr(), gy.data_ptr(), db2.data_ptr(), ws.data_ptr(), n,
+              C, P, _lib.stream_ptr())
+    assert torch.equal(db, db2)

@@ -16,13 +16,15 @@
 //   touched ancestor once, deepest level first, from final children" -- a touched node's
 //   last maintenance in the sequential loop happens after every change below it.  Untouched
 //   nodes must NOT be recomputed (the min() quirk, sumtree.py:11-19, seeds 1 for a maintained
-//   zero node).  Two launches:
+//   zero node).  One launch, two phases:
 //   * k_tree_update_sub: the levels S..maxd (S = 11), one workgroup per group of level-S
 //     subtrees (256 workgroups); each sorts its keys by left-aligned leaf position, loads
 //     everything its touched nodes need in one parallel pass, runs the level loop in LDS and
 //     stores the touched nodes once;
-//   * k_tree_update_top: the 2^S - 1 nodes above level S, dense in LDS, from the level-S
-//     sums the first launch left in memory.
+//   * tree_top: the 2^S - 1 nodes above level S, dense in LDS, from the level-S sums the
+//     subtree pass wrote through to memory -- run by the subtree pass's last workgroup (a
+//     ticket), so the whole update is one launch (k_tree_update_top alone when no key lies
+//     below level S).
 //   Any partition of the keys by subtree, and any split into launch-ordered rounds, gives the
 //   sequential result, so this is bit-identical to _numba_update for every n.
 #include <cmath>
@@ -178,6 +180,7 @@ struct UpdArgs {
   int64_t pn;
   int32_t post_tail;  // st->tail += n after every read of it (the append's FIFO advance)
   int32_t timing;     // record phase timestamps in g_upd_clock (RTH_TREE_TIMING=1)
+  int32_t fuse_top;   // the subtree pass's last workgroup runs the top pass (else its own launch)
 };
 
 // FIFO start and alpha of a launch: both replay-state words loaded together
@@ -224,6 +227,9 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
+
+struct TopLds;
+__device__ void tree_top(const UpdArgs &a, int S, TopLds &L);
 
 // ---------------------------------------------------------------- subtree pass
 // Workgroup w owns the level-S subtrees s with s % gridDim.x == w (consecutive FIFO slots
@@ -467,13 +473,19 @@ __global__ __launch_bounds__(kSubThreads) void k_tree_update_sub(UpdArgs a, int 
       }
       lds_barrier();
     }
-    // ---- store the touched nodes
+    // ---- store the touched nodes (a level-S root write-through: the top pass reads it from
+    // another workgroup after the ticket below)
     if (j < cnt) {
       for (int L = lt_j; L <= d_j; ++L) {
         const SubEnt x = ent[eb_j + L - lt_j];
         const int64_t node = (int64_t)(al_j >> (maxd - L)) - 1;
-        a.nd[node + 1].sum = x.ls;
-        a.nd[node + 1].mn = x.lm;
+        if (L == S) {
+          __hip_atomic_store(&a.nd[node + 1].sum, x.ls, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(&a.nd[node + 1].mn, x.lm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+          a.nd[node + 1].sum = x.ls;
+          a.nd[node + 1].mn = x.lm;
+        }
         if (L == d_j) a.nd[node + 1].val = x.v;
       }
     }
@@ -482,6 +494,25 @@ __global__ __launch_bounds__(kSubThreads) void k_tree_update_sub(UpdArgs a, int 
     R = kSubKeys;
   }
   if (a.timing && tid == 0) atomicMax(&g_upd_clock[5], wall_clock64());  // the last workgroup's end
+  // ---- ticket: the workgroup that finishes last runs the levels above S (tree_top) in this
+  // launch, in the LDS of the entries (no second launch).  The counter lives in the unused
+  // record 0 of the node array and is re-armed by that workgroup.
+  if (!a.fuse_top) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  unsigned *const ticket = reinterpret_cast<unsigned *>(&a.nd[0].pad);
+  if (tid == 0) {
+    const unsigned tk = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_next = tk == gridDim.x - 1;
+    if (s_next) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!s_next) return;
+  if (tid == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  tree_top(a, S, *reinterpret_cast<TopLds *>(ent));
 }
 
 // ---------------------------------------------------------------- top pass
@@ -547,13 +578,22 @@ __device__ __forceinline__ TopVal top_node(const UpdArgs &a, int64_t i, const To
   return o;
 }
 
-__global__ __launch_bounds__(kTopThreads) void k_tree_update_top(UpdArgs a, int S) {
-  __shared__ int32_t win[kTopNodes];
-  __shared__ uint32_t bot[(kTopNodes + 1) / 32];
-  __shared__ double xs[8], xm[8];
-  __shared__ int xt[8];
-  __shared__ double uv[8], us[8], um[8];  // records of the levels above the register slots
-  __shared__ int ukey[8];
+// LDS of the top pass, carved from one buffer: run by its own launch, or by the subtree
+// pass's last workgroup in the LDS its level loop no longer needs
+struct TopLds {
+  int32_t win[kTopNodes];
+  uint32_t bot[(kTopNodes + 1) / 32];
+  double xs[8], xm[8];
+  int xt[8];
+  double uv[8], us[8], um[8];  // records of the levels above the register slots
+  int ukey[8];
+};
+
+__device__ void tree_top(const UpdArgs &a, int S, TopLds &L) {
+  int32_t *const win = L.win;
+  uint32_t *const bot = L.bot;
+  double *const xs = L.xs, *const xm = L.xm, *const uv = L.uv, *const us = L.us, *const um = L.um;
+  int *const xt = L.xt, *const ukey = L.ukey;
   const int t = threadIdx.x;
   const int64_t cap = a.cap;
   if (a.timing && t == 0) g_upd_clock[2] = wall_clock64();
@@ -729,6 +769,13 @@ __global__ __launch_bounds__(kTopThreads) void k_tree_update_top(UpdArgs a, int 
   }
 }
 
+__global__ __launch_bounds__(kTopThreads) void k_tree_update_top(UpdArgs a, int S) {
+  __shared__ TopLds lds;
+  tree_top(a, S, lds);
+}
+static_assert(sizeof(TopLds) <= sizeof(SubEnt) * kSubEntries, "the top pass reuses the subtree pass's entry LDS");
+static_assert(kTopThreads == kSubThreads, "the subtree pass's last workgroup runs the top pass");
+
 // ------------------------------------------------------------------ find / sample
 __global__ void k_tree_find(const Node *__restrict__ nd, int64_t cap, const double *__restrict__ tg,
                             int64_t n, int64_t *__restrict__ idx_out, double *__restrict__ val_out, int kspec) {
@@ -827,13 +874,16 @@ int tree_update_impl(rth_sumtree *t, const int64_t *idx, int64_t fifo_start, con
   a.post_tail = post_tail;
   static const int timing = env_int("RTH_TREE_TIMING", 0);
   a.timing = timing;
+  static const int fuse = env_int("RTH_TREE_FUSE_TOP", 1);  // 0: the top pass as its own launch (A/B)
+  a.fuse_top = fuse;
   RTH_REQUIRE(a.pn + a.n < (int64_t(1) << 31), "tree update: at most 2^31 - 1 keys per call");
   const int S = t->maxd + 1 < kTopMinS ? kTopMinS : (t->maxd + 1 < kTopS ? t->maxd + 1 : kTopS);
-  if (t->maxd >= S && a.pn + a.n > 0) {  // levels S..maxd: one workgroup per group of subtrees
-    const int64_t nsub = int64_t(1) << S;
+  if (t->maxd >= S && a.pn + a.n > 0) {  // levels S..maxd: one workgroup per group of subtrees,
+    const int64_t nsub = int64_t(1) << S;  // the last one to finish also runs the top pass
     hipLaunchKernelGGL(k_tree_update_sub, dim3((unsigned)(nsub < kSubGrid ? nsub : kSubGrid)), dim3(kSubThreads), 0,
                        s, a, S);
     RTH_LAUNCHED();
+    if (a.fuse_top) return RTH_OK;
   }
   hipLaunchKernelGGL(k_tree_update_top, dim3(1), dim3(kTopThreads), 0, s, a, S);
   RTH_LAUNCHED();

@@ -1,5 +1,6 @@
 // Learner optimizer step on gfx950: clip_grad_norm_ + Adam as two launches over every
-// parameter tensor at once.
+// parameter tensor at once (per-workgroup squared-norm partials; every Adam workgroup sums
+// them itself, in the same fixed order, before updating its chunk).
 //
 // Reference: reth/reth/algorithm/dqn/dqn_solver.py:118-121 -- torch.nn.utils.clip_grad_norm_
 // (max_norm = clip_value, 2-norm) then torch.optim.Adam.step() (no weight decay, no amsgrad;
@@ -74,11 +75,12 @@ __device__ __forceinline__ int seg_of(const OptArgs &a, int64_t b) {
   return s;
 }
 
-// the norm, the clip coefficient, t += 1 and the bias corrections, by one workgroup from the
-// per-workgroup partials (summed in workgroup order: deterministic)
-__device__ void opt_scalars(const double *__restrict__ part, int nparts, double *red, int clip, float max_norm,
-                            double lr, double beta1, double beta2, int64_t *__restrict__ step,
-                            OptScalars *__restrict__ out, float *__restrict__ total_out) {
+// the norm, the clip coefficient and the bias corrections from the per-workgroup partials
+// (summed in workgroup order: deterministic).  Every Adam workgroup computes them itself --
+// the same values in the same order -- so no workgroup waits for another; the step count was
+// advanced by k_grad_sqsum's first workgroup (a kernel boundary before any read).
+__device__ OptScalars opt_scalars(const double *__restrict__ part, int nparts, double *red, int clip, float max_norm,
+                                  double lr, double beta1, double beta2, int64_t t) {
   double acc = 0.0;
   for (int k = threadIdx.x; k < nparts; k += kOptThreads) acc = radd(acc, part[k]);
   red[threadIdx.x] = acc;
@@ -87,24 +89,16 @@ __device__ void opt_scalars(const double *__restrict__ part, int nparts, double 
     if (threadIdx.x < s) red[threadIdx.x] = radd(red[threadIdx.x], red[threadIdx.x + s]);
     __syncthreads();
   }
-  if (threadIdx.x == 0) {
-    const float total = (float)sqrt(red[0]);
-    float coef = 1.0f;
-    if (clip) {  // clip_coef = max_norm / (total_norm + 1e-6), clamped to 1 (f32 tensor math)
-      const float c = max_norm / radd(total, 1e-6f);
-      coef = c < 1.0f ? c : 1.0f;
-    }
-    const int64_t t = *step + 1;
-    *step = t;
-    // python-float scalars of adam.py, cast to f32 where they meet the f32 tensors
-    const double bc1 = 1.0 - pow(beta1, (double)t);
-    const double bc2 = 1.0 - pow(beta2, (double)t);
-    out->coef = coef;
-    out->step_size = (float)(lr / bc1);
-    out->bc2_sqrt = (float)sqrt(bc2);
-    out->total_norm = total;
-    if (total_out) *total_out = total;
+  const float total = (float)sqrt(red[0]);
+  float coef = 1.0f;
+  if (clip) {  // clip_coef = max_norm / (total_norm + 1e-6), clamped to 1 (f32 tensor math)
+    const float c = max_norm / radd(total, 1e-6f);
+    coef = c < 1.0f ? c : 1.0f;
   }
+  // python-float scalars of adam.py, cast to f32 where they meet the f32 tensors
+  const double bc1 = 1.0 - pow(beta1, (double)t);
+  const double bc2 = 1.0 - pow(beta2, (double)t);
+  return OptScalars{coef, (float)(lr / bc1), (float)sqrt(bc2), total};
 }
 
 struct ScalarArgs {
@@ -116,13 +110,10 @@ struct ScalarArgs {
   float *total_out;
 };
 
-// per-workgroup sums of squares of the gradients; the workgroup that finishes last (ticket
-// counter; partials stored write-through, read after an agent-scope acquire) then computes the scalars,
-// so the Adam launch follows directly (no separate single-workgroup launch in between)
-__global__ __launch_bounds__(kOptThreads) void k_grad_sqsum(OptArgs a, double *__restrict__ part,
-                                                           unsigned *__restrict__ ticket, ScalarArgs sa) {
+// per-workgroup sums of squares of the gradients (fp64 partials); workgroup 0 advances the
+// device step count
+__global__ __launch_bounds__(kOptThreads) void k_grad_sqsum(OptArgs a, double *__restrict__ part, int64_t *step) {
   __shared__ double red[kOptThreads];
-  __shared__ int last;
   const int64_t b = blockIdx.x;
   const OptSeg &sg = a.seg[seg_of(a, b)];
   const int64_t base = (b - sg.blk0) * kOptChunk;
@@ -137,44 +128,26 @@ __global__ __launch_bounds__(kOptThreads) void k_grad_sqsum(OptArgs a, double *_
     acc = radd(acc, rmul(y, y));
     acc = radd(acc, rmul(z, z));
     acc = radd(acc, rmul(w, w));
-  }  red[threadIdx.x] = acc;
+  }
+  red[threadIdx.x] = acc;
   __syncthreads();
   for (int s = kOptThreads / 2; s > 0; s >>= 1) {
     if (threadIdx.x < s) red[threadIdx.x] = radd(red[threadIdx.x], red[threadIdx.x + s]);
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    // write-through (sc1) store of the partial, so no L2 write-back (release fence) is needed
-    // before the ticket; the last block invalidates its L1 (acquire) and reads plainly
-    __hip_atomic_store(&part[b], red[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = t == gridDim.x - 1;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    part[b] = red[0];
+    if (b == 0) *step += 1;
   }
-  __syncthreads();
-  if (!last) return;
-  opt_scalars(part, (int)gridDim.x, red, sa.clip, sa.max_norm, sa.lr, sa.beta1, sa.beta2, sa.step, sa.out,
-              sa.total_out);
-  if (threadIdx.x == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__global__ __launch_bounds__(kOptThreads) void k_adam(OptArgs a, const OptScalars *__restrict__ sc, int clip,
-                                                     float w1, float beta2, float w2, float eps) {
+__global__ __launch_bounds__(kOptThreads) void k_adam(OptArgs a, const double *__restrict__ part, int nparts,
+                                                     ScalarArgs sa, float w1, float beta2, float w2, float eps) {
+  __shared__ double red[kOptThreads];
   const int64_t b = blockIdx.x;
   const OptSeg &sg = a.seg[seg_of(a, b)];
   const int64_t base = (b - sg.blk0) * kOptChunk;
-  const float coef = sc->coef, step_size = sc->step_size, bc2_sqrt = sc->bc2_sqrt;
-  auto adam1 = [&](float g, float &m, float &v, float &p) {
-    if (clip) g = rmul(g, coef);  // grad.mul_(clip_coef_clamped)
-    m = radd(m, rmul(w1, rsub(g, m)));               // lerp_(g, 1 - beta1), weight < 0.5 branch
-    v = radd(rmul(v, beta2), rmul(rmul(w2, g), g));  // mul_(beta2).addcmul_(g, g, 1 - beta2)
-    const float denom = radd(sqrtf(v) / bc2_sqrt, eps);
-    p = radd(p, rmul(-step_size, m) / denom);  // addcdiv_(m, denom, -step_size)
-  };
+  // this chunk's loads first, then the global norm from the partials (overlapping them)
   float4 gv[kOptV], mv[kOptV], vv[kOptV], pv[kOptV];
 #pragma unroll
   for (int k = 0; k < kOptV; ++k) {
@@ -184,6 +157,20 @@ __global__ __launch_bounds__(kOptThreads) void k_adam(OptArgs a, const OptScalar
     vv[k] = ld4(sg.v, e, sg.n, sg.vec);
     pv[k] = ld4(sg.param, e, sg.n, sg.vec);
   }
+  const OptScalars sc = opt_scalars(part, nparts, red, sa.clip, sa.max_norm, sa.lr, sa.beta1, sa.beta2, *sa.step);
+  if (b == 0 && threadIdx.x == 0) {
+    *sa.out = sc;
+    if (sa.total_out) *sa.total_out = sc.total_norm;
+  }
+  const int clip = sa.clip;
+  const float coef = sc.coef, step_size = sc.step_size, bc2_sqrt = sc.bc2_sqrt;
+  auto adam1 = [&](float g, float &m, float &v, float &p) {
+    if (clip) g = rmul(g, coef);  // grad.mul_(clip_coef_clamped)
+    m = radd(m, rmul(w1, rsub(g, m)));               // lerp_(g, 1 - beta1), weight < 0.5 branch
+    v = radd(rmul(v, beta2), rmul(rmul(w2, g), g));  // mul_(beta2).addcmul_(g, g, 1 - beta2)
+    const float denom = radd(sqrtf(v) / bc2_sqrt, eps);
+    p = radd(p, rmul(-step_size, m) / denom);  // addcdiv_(m, denom, -step_size)
+  };
 #pragma unroll
   for (int k = 0; k < kOptV; ++k) {
     const int64_t e = base + 4 * (k * kOptThreads + threadIdx.x);
@@ -204,7 +191,7 @@ using namespace rth;
 
 extern "C" {
 
-// [partials: kMaxPartials doubles][OptScalars][ticket counter]; zero-initialised by the caller
+// [partials: kMaxPartials doubles][OptScalars (the last update's scalars)]
 int64_t rth_clip_adam_workspace(void) { return (int64_t)kMaxPartials * 8 + 64; }
 
 int rth_clip_adam(const rth_param_tensor *tensors, int32_t n_tensors, double lr, double beta1, double beta2,
@@ -230,13 +217,12 @@ int rth_clip_adam(const rth_param_tensor *tensors, int32_t n_tensors, double lr,
   auto *sc = reinterpret_cast<OptScalars *>(static_cast<uint8_t *>(workspace_dev) + (int64_t)kMaxPartials * 8);
   const int clip = max_norm >= 0.0;
   hipStream_t s = as_stream(stream);
-  auto *ticket = reinterpret_cast<unsigned *>(static_cast<uint8_t *>(workspace_dev) + (int64_t)kMaxPartials * 8 + 32);
   const ScalarArgs sa{clip, (float)max_norm, lr, beta1, beta2, step_dev, sc, total_norm_out};
-  hipLaunchKernelGGL(k_grad_sqsum, dim3((unsigned)blocks), dim3(kOptThreads), 0, s, a, part, ticket, sa);
+  hipLaunchKernelGGL(k_grad_sqsum, dim3((unsigned)blocks), dim3(kOptThreads), 0, s, a, part, step_dev);
   RTH_LAUNCHED();
   // 1 - beta1 and 1 - beta2 are python floats in adam.py, rounded to f32 once
-  hipLaunchKernelGGL(k_adam, dim3((unsigned)blocks), dim3(kOptThreads), 0, s, a, sc, clip, (float)(1.0 - beta1),
-                     (float)beta2, (float)(1.0 - beta2), (float)eps);
+  hipLaunchKernelGGL(k_adam, dim3((unsigned)blocks), dim3(kOptThreads), 0, s, a, part, (int)blocks, sa,
+                     (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), (float)eps);
   RTH_LAUNCHED();
   return RTH_OK;
 }

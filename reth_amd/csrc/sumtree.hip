@@ -251,6 +251,8 @@ constexpr int kSubKeys = 256;      // keys per round (one per lane; 10 slot bits
 constexpr int kSlotBits = 10;
 constexpr int kSubEntries = 256;   // touched (node, level) entries per round
 constexpr int kSubGrid = 256;
+constexpr int kSubSplit = 4;          // the second pass covers S .. S + 3
+constexpr int kSubTwoPassDepth = 8;   // two passes when maxd >= S + 8 (trees of >= 2^19 nodes)
 static_assert(kSubKeys == kSubThreads, "one key per lane in the rank sort / ownership scan");
 
 struct SubEnt {
@@ -284,7 +286,12 @@ __device__ __forceinline__ int wg_scan(int x, int *wsum, int *total) {
   return base + incl - x;
 }
 
-__global__ __launch_bounds__(kSubThreads) void k_tree_update_sub(UpdArgs a, int S) {
+// One pass covers the levels [S, D].  Deep trees take two passes (S1 = S0 + 4): [S1, maxd],
+// then [S0, S1 - 1] -- the second pass maps every deeper key to its level-(S1 - 1) ancestor
+// as a "valueless" key (its val is kept, its children are final after the first launch), so
+// a contiguous FIFO append spreads over many level-S1 subtrees (runs of 2^(d - S1) keys)
+// instead of piling into a few level-S0 subtrees and many rounds.
+__global__ __launch_bounds__(kSubThreads) void k_tree_update_sub(UpdArgs a, int S, int D, int last_pass) {
   __shared__ uint64_t keys[kSubKeys];
   __shared__ uint64_t scratch[kSubKeys];  // unsorted keys, then ebase[]
   __shared__ int32_t slot_g[kSubKeys];
@@ -303,11 +310,25 @@ __global__ __launch_bounds__(kSubThreads) void k_tree_update_sub(UpdArgs a, int 
   const int64_t N = a.pn + a.n;
   const int64_t top = (int64_t(1) << S) - 1;  // nodes above level S
   const uint32_t G = gridDim.x;
-  auto is_mine = [&](int64_t g, uint64_t *key) -> bool {
+  // key g of this pass: its node (a key below D -> its level-D ancestor, valueless), false
+  // when it is not this workgroup's, or a valueless duplicate of the key right before it
+  auto is_mine = [&](int64_t g, uint64_t *key, bool *valued) -> bool {
     if (g >= N) return false;
-    const int64_t id = upd_id(a, g, fifo_start);
+    int64_t id = upd_id(a, g, fifo_start);
     if (id < top || id >= cap) return false;
-    const int d = node_depth(id);
+    int d = node_depth(id);
+    *valued = d <= D;
+    if (d > D) {
+      id = ((id + 1) >> (d - D)) - 1;
+      d = D;
+      if (g > 0) {  // the FIFO run: consecutive keys share their level-D ancestor
+        const int64_t pid = upd_id(a, g - 1, fifo_start);
+        if (pid >= top && pid < cap) {
+          const int pd = node_depth(pid);
+          if (pd > D && ((pid + 1) >> (pd - D)) - 1 == id) return false;
+        }
+      }
+    }
     const int64_t sub = ((id + 1) >> (d - S)) - 1 - top;
     const uint64_t al = (uint64_t)(id + 1) << (maxd - d);
     *key = ((al << 6) | (uint64_t)d) << kSlotBits;
@@ -322,10 +343,10 @@ __global__ __launch_bounds__(kSubThreads) void k_tree_update_sub(UpdArgs a, int 
     int cnt = 0;
     int64_t pos = scan;
     while (pos < N && cnt < R) {
-      bool mine[kGatherU];
+      bool mine[kGatherU], valued[kGatherU];
       uint64_t kk[kGatherU];  // the sort key's (aligned, depth) part
 #pragma unroll
-      for (int u = 0; u < kGatherU; ++u) mine[u] = is_mine(pos + u * kSubThreads + tid, &kk[u]);
+      for (int u = 0; u < kGatherU; ++u) mine[u] = is_mine(pos + u * kSubThreads + tid, &kk[u], &valued[u]);
 #pragma unroll
       for (int u = 0; u < kGatherU; ++u) {
         if (pos >= N || cnt >= R) break;  // uniform
@@ -336,7 +357,7 @@ __global__ __launch_bounds__(kSubThreads) void k_tree_update_sub(UpdArgs a, int 
         if (tid == 0) s_next = -1;
         __syncthreads();
         if (mine[u] && rank < take) {
-          slot_g[cnt + rank] = (int32_t)g;
+          slot_g[cnt + rank] = valued[u] ? (int32_t)g : ~(int32_t)g;  // < 0: valueless
           scratch[cnt + rank] = kk[u] | (uint64_t)(cnt + rank);
         }
         if (mine[u] && rank == take) s_next = (int)(g - pos);  // first key left for the next round
@@ -410,9 +431,12 @@ __global__ __launch_bounds__(kSubThreads) void k_tree_update_sub(UpdArgs a, int 
     // ---- load every entry's inputs (all of a key's levels in flight together; LDS stores
     // cannot alias the loads) and its own node's new priority (the last duplicate's)
     if (j < cnt && own > 0) {
-      int last = j;
-      while (last + 1 < cnt && (keys[last + 1] >> kSlotBits) == (k_j >> kSlotBits)) ++last;
-      const int64_t g_last = slot_g[keys[last] & ((1u << kSlotBits) - 1)];
+      // the node's new val: the last valued duplicate's priority; none -> its val stays
+      int32_t g_last = slot_g[k_j & ((1u << kSlotBits) - 1)];
+      for (int x = j + 1; x < cnt && (keys[x] >> kSlotBits) == (k_j >> kSlotBits); ++x) {
+        const int32_t gx = slot_g[keys[x] & ((1u << kSlotBits) - 1)];
+        if (gx >= 0) g_last = gx;
+      }
       constexpr int kLoadU = 12;
       for (int L0 = lt_j; L0 <= d_j; L0 += kLoadU) {
         double v[kLoadU], ls[kLoadU], lm[kLoadU], rs[kLoadU], rm[kLoadU];
@@ -422,7 +446,7 @@ __global__ __launch_bounds__(kSubThreads) void k_tree_update_sub(UpdArgs a, int 
           v[u] = ls[u] = lm[u] = rs[u] = rm[u] = 0.0;
           if (L <= d_j) {
             const int64_t node = (int64_t)(al_j >> (maxd - L)) - 1, l = 2 * node + 1;
-            if (L < d_j) v[u] = a.nd[node + 1].val;
+            if (L < d_j || g_last < 0) v[u] = a.nd[node + 1].val;
             if (l < cap) {
               ls[u] = a.nd[l + 1].sum;
               lm[u] = a.nd[l + 1].mn;
@@ -433,18 +457,19 @@ __global__ __launch_bounds__(kSubThreads) void k_tree_update_sub(UpdArgs a, int 
             }
           }
         }
-        const double pv = L0 + kLoadU > d_j ? priority_of(a, alpha, g_last) : 0.0;
+        const bool key_val = g_last >= 0 && L0 + kLoadU > d_j;
+        const double pv = key_val ? priority_of(a, alpha, g_last) : 0.0;
 #pragma unroll
         for (int u = 0; u < kLoadU; ++u) {
           const int L = L0 + u;
-          if (L <= d_j) ent[eb_j + L - lt_j] = SubEnt{L == d_j ? pv : v[u], ls[u], lm[u], rs[u], rm[u]};
+          if (L <= d_j) ent[eb_j + L - lt_j] = SubEnt{L == d_j && key_val ? pv : v[u], ls[u], lm[u], rs[u], rm[u]};
         }
       }
     }
     __syncthreads();
     if (a.timing && tid == 0 && blockIdx.x == 0) g_upd_clock[1] = wall_clock64();
     // ---- levels, deepest first (_numba_maintain_node on every touched node, once)
-    for (int L = maxd; L >= S; --L) {
+    for (int L = D; L >= S; --L) {
       if (L >= lt_j && L <= d_j) {
         const int e = eb_j + L - lt_j;
         const SubEnt x = ent[e];
@@ -497,7 +522,7 @@ __global__ __launch_bounds__(kSubThreads) void k_tree_update_sub(UpdArgs a, int 
   // ---- ticket: the workgroup that finishes last runs the levels above S (tree_top) in this
   // launch, in the LDS of the entries (no second launch).  The counter lives in the unused
   // record 0 of the node array and is re-armed by that workgroup.
-  if (!a.fuse_top) return;
+  if (!a.fuse_top || !last_pass) return;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   unsigned *const ticket = reinterpret_cast<unsigned *>(&a.nd[0].pad);
@@ -879,9 +904,21 @@ int tree_update_impl(rth_sumtree *t, const int64_t *idx, int64_t fifo_start, con
   RTH_REQUIRE(a.pn + a.n < (int64_t(1) << 31), "tree update: at most 2^31 - 1 keys per call");
   const int S = t->maxd + 1 < kTopMinS ? kTopMinS : (t->maxd + 1 < kTopS ? t->maxd + 1 : kTopS);
   if (t->maxd >= S && a.pn + a.n > 0) {  // levels S..maxd: one workgroup per group of subtrees,
-    const int64_t nsub = int64_t(1) << S;  // the last one to finish also runs the top pass
-    hipLaunchKernelGGL(k_tree_update_sub, dim3((unsigned)(nsub < kSubGrid ? nsub : kSubGrid)), dim3(kSubThreads), 0,
-                       s, a, S);
+    // the last one to finish (of the last pass) also runs the top pass; deep trees in two
+    // passes split at S1 = S + kSubSplit (RTH_TREE_PASSES=1: one pass, A/B aid)
+    static const int passes = env_int("RTH_TREE_PASSES", 1);
+    static const int grid = env_int("RTH_TREE_GRID", kSubGrid);
+    const int S1 = S + kSubSplit;
+    const bool two = passes >= 2 && t->maxd >= S + kSubTwoPassDepth;
+    if (two) {
+      const int64_t nsub1 = int64_t(1) << S1;
+      hipLaunchKernelGGL(k_tree_update_sub, dim3((unsigned)(nsub1 < grid ? nsub1 : grid)), dim3(kSubThreads), 0, s,
+                         a, S1, t->maxd, 0);
+      RTH_LAUNCHED();
+    }
+    const int64_t nsub = int64_t(1) << S;
+    hipLaunchKernelGGL(k_tree_update_sub, dim3((unsigned)(nsub < grid ? nsub : grid)), dim3(kSubThreads), 0, s, a, S,
+                       two ? S1 - 1 : t->maxd, 1);
     RTH_LAUNCHED();
     if (a.fuse_top) return RTH_OK;
   }

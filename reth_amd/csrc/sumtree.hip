@@ -906,7 +906,7 @@ int tree_update_impl(rth_sumtree *t, const int64_t *idx, int64_t fifo_start, con
   if (t->maxd >= S && a.pn + a.n > 0) {  // levels S..maxd: one workgroup per group of subtrees,
     // the last one to finish (of the last pass) also runs the top pass; deep trees in two
     // passes split at S1 = S + kSubSplit (RTH_TREE_PASSES=1: one pass, A/B aid)
-    static const int passes = env_int("RTH_TREE_PASSES", 1);
+    const int passes = env_int("RTH_TREE_PASSES", 1);  // read per call: tests switch it
     static const int grid = env_int("RTH_TREE_GRID", kSubGrid);
     const int S1 = S + kSubSplit;
     const bool two = passes >= 2 && t->maxd >= S + kSubTwoPassDepth;

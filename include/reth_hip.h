@@ -426,6 +426,17 @@ int rth_conv_bias_relu_upto(const rth_conv_shape *shape, const void *x_dev, cons
 int rth_conv_dgrad_supported(const rth_conv_shape *shape);
 int rth_conv_dgrad(const rth_conv_shape *shape, const float *gy_dev, int64_t n, const float *w_ohwi_dev,
                    float *gx_dev, void *stream);
+/* Weight gradient of conv2d(x, w) for the fp32 channels-last layers (conv2 and conv3 of the
+ * torso; the backward of dqn_model.py:14-20 under dqn_solver.py:117 loss.backward(); replaces
+ * MIOpen's weight-gradient solver and its zero fill): gw [cout, kh, kw, cin] (OHWI, the
+ * channels_last parameter layout) = sum over output pixels of gy[p][co] * x-window[p], from
+ * x = [n, hin, win, cin] and gy = [n, hout, wout, cout] (already ReLU-masked), on the fp32
+ * MFMA; every sum has a fixed order (deterministic).  `shape` is the forward convolution's
+ * (input RTH_CONV_F32_NHWC); workspace = rth_conv_wgrad_f32_workspace(shape) bytes. */
+int rth_conv_wgrad_f32_supported(const rth_conv_shape *shape);
+int64_t rth_conv_wgrad_f32_workspace(const rth_conv_shape *shape);
+int rth_conv_wgrad_f32(const rth_conv_shape *shape, const float *x_dev, int64_t n, const float *gy_dev, float *gw_dev,
+                       void *workspace_dev, void *stream);
 /* Backward of relu(conv2d(x, w) + b) for the weights and bias, on uint8 stacks (conv1, whose
  * input needs no gradient): gy = (y > 0) ? g : 0, gw = sum over output pixels of gy times the
  * input window (OHWI [cout, kh, kw, cin], the layout of a channels_last weight), gb = sum of

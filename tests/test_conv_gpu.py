@@ -390,3 +390,36 @@ def test_conv_nchw_output(dev, gi, n):
     assert y_chw.is_contiguous() and torch.equal(y_chw, y_hwc)
     u8 = _shape(_lib.CONV_U8_CHW | _lib.CONV_OUT_NCHW, *GEOMS[0])
     assert _lib.lib().rth_conv_supported(_lib.ctypes.byref(u8)) == 0
+
+
+@pytest.mark.parametrize("gi,n", [(1, 1), (1, 37), (1, 512), (2, 1), (2, 3), (2, 512)])
+def test_conv_wgrad_f32(dev, gi, n):
+    """rth_conv_wgrad_f32 (conv2 / conv3 weight gradient on the fp32 MFMA) against an fp64 CPU
+    convolution backward, within fp32 summation error; deterministic (a second call is bit
+    identical) and odd pixel counts (the last pair half empty) included"""
+    from reth_amd import _lib
+
+    geom = GEOMS[gi]
+    cin, h, wd, cout, k, s = geom
+    g = torch.Generator().manual_seed(31 * n + gi)
+    x = torch.rand((n, cin, h, wd), generator=g) * 2 - 1
+    ho = (h - k) // s + 1
+    gy = torch.randn((n, cout, ho, ho), generator=g)
+    w = torch.zeros((cout, cin, k, k), dtype=torch.float64)
+    _, want, _ = torch.ops.aten.convolution_backward(gy.double(), x.double(), w, None, [s, s], [0, 0], [1, 1], False,
+                                                     [0, 0], 1, [False, True, False])
+    shape = _shape(_lib.CONV_F32_NHWC, *geom)
+    assert _lib.lib().rth_conv_wgrad_f32_supported(_lib.ctypes.byref(shape)) == 1
+    ws = torch.empty(_lib.lib().rth_conv_wgrad_f32_workspace(_lib.ctypes.byref(shape)) // 4, device=dev)
+    xd = x.to(dev).contiguous(memory_format=torch.channels_last)
+    gyd = gy.to(dev).contiguous(memory_format=torch.channels_last)
+    outs = []
+    for _ in range(2):
+        gw = torch.full((cout, cin, k, k), float("nan"), device=dev).contiguous(memory_format=torch.channels_last)
+        _lib.call("rth_conv_wgrad_f32", _lib.ctypes.byref(shape), xd.data_ptr(), n, gyd.data_ptr(), gw.data_ptr(),
+                  ws.data_ptr(), _lib.stream_ptr())
+        outs.append(gw)
+    assert torch.equal(outs[0], outs[1])
+    scale = want.abs().max().item()
+    err = (outs[0].double().cpu() - want).abs().max().item()
+    assert err <= 2e-6 * max(scale, 1.0) * max(1.0, (n * ho * ho) ** 0.5 / 8), (err, scale)

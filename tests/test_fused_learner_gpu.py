@@ -50,12 +50,14 @@ def _solver(dev, seed):
                      channels_last=True)
 
 
-@pytest.mark.parametrize("u8,adjacent,hip_dgrad", [(True, True, {1}), (True, False, {1}), (False, False, {1}),
-                                                   (True, True, set()), (True, True, {1, 2})])
-def test_fused_grads_match_autograd(dev, u8, adjacent, hip_dgrad, monkeypatch):
+@pytest.mark.parametrize("u8,adjacent,hip_dgrad,hip_wgrad", [(True, True, {1}, False), (True, False, {1}, False),
+                                                             (False, False, {1}, False), (True, True, set(), False),
+                                                             (True, True, {1, 2}, False), (True, True, {1}, True)])
+def test_fused_grads_match_autograd(dev, u8, adjacent, hip_dgrad, hip_wgrad, monkeypatch):
     from reth_amd import fused_learner
 
     monkeypatch.setattr(fused_learner, "HIP_DGRAD", hip_dgrad)  # layers whose data gradient is rth_conv_dgrad's
+    monkeypatch.setattr(fused_learner, "HIP_WGRAD", hip_wgrad)  # conv2/conv3 weight gradients in rth_conv_wgrad_f32
 
     B = 64
     g = torch.Generator(device=dev).manual_seed(5)

@@ -70,6 +70,7 @@ class ApexConfig:
     overlap: bool = True           # graph mode: actor block and learner block on two streams, concurrently
     hip_conv: bool = True          # conv torso forward in rth_conv_bias_relu (actors/targets read uint8 stacks)
     dp_hook: Optional[bool] = None  # gradient all-reduce hook: None = when world > 1 (tests force it)
+    tuned_gemm: bool = True        # TunableOp solution selection for the library GEMMs (reth_amd.gemm_tuning)
     extra: dict = field(default_factory=dict)
 
 
@@ -86,6 +87,10 @@ class ApexDQN:
         use_hook = world > 1 if cfg.dp_hook is None else cfg.dp_hook
         hook = GradAllReduce(group) if use_hook else None
         torch.backends.cudnn.benchmark = bool(cfg.conv_benchmark)
+        if cfg.tuned_gemm:
+            from . import gemm_tuning
+
+            gemm_tuning.enable()
         fmt = torch.channels_last if cfg.channels_last else torch.contiguous_format
         torch.manual_seed(cfg.seed)  # identical initial weights on every rank
         self.solver = DQNSolver(Box(0, 255, OBS_SHAPE), Discrete(cfg.num_actions), gamma=cfg.gamma,
@@ -222,6 +227,17 @@ class ApexDQN:
         solver = self.solver
         solver.auto_target_update = False
         slots = self.loader._slots
+        tun = torch.cuda.tunable
+        tuning = tun.is_enabled() and tun.tuning_is_enabled()
+        if tuning:  # a GEMM shape first seen inside the capture must not be benchmarked there
+            tun.tuning_enable(False)
+        try:
+            self._capture_graphs(solver, slots)
+        finally:
+            if tuning:
+                tun.tuning_enable(True)
+
+    def _capture_graphs(self, solver, slots):
         host = (self.actors.t, self.actors.pushes)
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))

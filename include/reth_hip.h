@@ -163,7 +163,9 @@ int rth_replay_append(rth_replay *h, const rth_src *srcs, const void *td_abs_dev
 /* sampler_loop sample + loader gather: PER-sample `batch` rows (uniforms_dev nullable, see
  * rth_sumtree_sample) with the current beta, write IS weights, and gather every column into
  * out_cols_dev[c] ([batch, row] of out_dtype; NULL = no gather) -- TorchCudaLoader.sample's
- * (data, indices, weights). */
+ * (data, indices, weights).  The sampler's device call counter (the Philox counter of the
+ * next sample) is advanced by the gather kernel; with out_cols_dev NULL, by the next
+ * rth_replay_gather on this handle, or else by the next sample before it draws. */
 int rth_replay_sample(rth_replay *h, int64_t batch, const double *uniforms_dev,
                       void *const *out_cols_dev, int64_t *idx_out_dev, double *isw_out_dev,
                       void *stream);

@@ -68,6 +68,8 @@ struct CopyArgs {
   const ReplayState *st;  // nullable: FIFO start = st->tail (device-resident)
   int32_t dst_fifo;
   int32_t ncols;
+  ReplayState *bump_st;   // nullable: st->calls += bump_calls here (the sample(s) this gather follows)
+  int64_t bump_calls;
 };
 
 constexpr int kCopyThreads = 256;
@@ -131,6 +133,9 @@ __device__ __forceinline__ void hwc4_chunk(const uint8_t *__restrict__ src, floa
 //               contiguous per wave instruction); chunk = 1024 pixels.
 __global__ __launch_bounds__(kCopyThreads) void k_copy_rows(CopyArgs a) {
   const int64_t b = blockIdx.x;
+  // the sampler's call counter, read by the sample launch before this one (stream order),
+  // advanced here instead of by a launch of its own
+  if (a.bump_st && b == 0 && threadIdx.x == 0) a.bump_st->calls += a.bump_calls;
   int c = 0;
   while (c + 1 < a.ncols && b >= a.col[c + 1].blk0) ++c;
   const CopyCol &col = a.col[c];
@@ -439,7 +444,12 @@ struct rth_replay {
   int64_t tail, size, cnt, sample_calls, sched_steps, slen;
   UpdPending pend;  // a deferred PER update, applied by the next tree launch
   int has_pend;
+  // sample calls whose st->calls advance is still owed: a sample without out_cols leaves it to
+  // the gather that follows (rth_replay_gather), or to the next sample when none does
+  int64_t calls_owed;
 };
+
+static int bump(rth_replay *h, int64_t dtail, int64_t dcalls, int64_t dstep, hipStream_t s);
 
 // apply a deferred update on its own (before a sample, an immediate update, a flush)
 static int flush_pending(rth_replay *h, hipStream_t s) {
@@ -656,10 +666,10 @@ int rth_replay_append(rth_replay *h, const rth_src *srcs, const void *td_abs, in
   return RTH_OK;
 }
 
-int rth_replay_gather(rth_replay *h, const int64_t *idx, int64_t n, void *const *out_cols, void *stream) {
+static int gather_impl(rth_replay *h, const int64_t *idx, int64_t n, void *const *out_cols, hipStream_t s) {
   RTH_REQUIRE(h && (n == 0 || (idx && out_cols)), "rth_replay_gather: bad arguments");
   CopyArgs a{};
-  for (int c = 0; c < h->ncols; ++c) {
+  for (int c = 0; n > 0 && c < h->ncols; ++c) {
     RTH_REQUIRE(out_cols[c], "rth_replay_gather: output column %d is NULL", c);
     const rth_col_desc &d = h->desc[c];
     int32_t conv;
@@ -669,7 +679,18 @@ int rth_replay_gather(rth_replay *h, const int64_t *idx, int64_t n, void *const 
   }
   a.n = n;
   a.ncols = h->ncols;
-  return launch_copy(a, as_stream(stream));
+  const int64_t owed = h->calls_owed;
+  h->calls_owed = 0;
+  if (n == 0) return owed ? bump(h, 0, owed, 0, s) : RTH_OK;
+  if (owed) {  // the gather's first lane advances the counter: no launch of its own
+    a.bump_st = h->st;
+    a.bump_calls = owed;
+  }
+  return launch_copy(a, s);
+}
+
+int rth_replay_gather(rth_replay *h, const int64_t *idx, int64_t n, void *const *out_cols, void *stream) {
+  return gather_impl(h, idx, n, out_cols, as_stream(stream));
 }
 
 int rth_replay_sample(rth_replay *h, int64_t batch, const double *uniforms, void *const *out_cols,
@@ -678,6 +699,11 @@ int rth_replay_sample(rth_replay *h, int64_t batch, const double *uniforms, void
   hipStream_t s = as_stream(stream);
   int rc = flush_pending(h, s);
   if (rc) return rc;
+  if (h->calls_owed) {  // the previous sample was not followed by a gather: its seed advance first
+    rc = bump(h, 0, h->calls_owed, 0, s);
+    h->calls_owed = 0;
+    if (rc) return rc;
+  }
   if (h->kind == RTH_SAMPLER_PER) {
     rc = tree_sample_impl(h->tree, batch, uniforms, h->seed, 0, 1, 0.0, idx_out, isw_out, s, h->st, &h->beta);
   } else if (h->kind == RTH_SAMPLER_UNIFORM) {
@@ -694,11 +720,9 @@ int rth_replay_sample(rth_replay *h, int64_t batch, const double *uniforms, void
     h->slen -= batch;
   }
   if (rc) return rc;
-  rc = bump(h, 0, 1, 0, s);
-  if (rc) return rc;
   h->sample_calls++;
-  if (out_cols) return rth_replay_gather(h, idx_out, batch, out_cols, stream);
-  return RTH_OK;
+  h->calls_owed = 1;  // advanced by the gather (this one, or the caller's rth_replay_gather next)
+  return out_cols ? gather_impl(h, idx_out, batch, out_cols, s) : RTH_OK;
 }
 
 int rth_replay_update_priorities(rth_replay *h, const int64_t *idx, const void *td_abs, int32_t td_dtype, int64_t n,

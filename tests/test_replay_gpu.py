@@ -244,3 +244,41 @@ def test_deferred_update_merged_into_append(dev, orc):
     assert ia == ib
     for x, y in zip(a, b):
         assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("sampler", ["per", "uniform"])
+def test_sample_counter_advance_forms(dev, sampler):
+    """the sampler's Philox counter advances once per sample whichever launch carries it: the
+    fused gather (sample with outputs), a separate rth_replay_gather (the bench's timed form),
+    or the next sample (no gather at all) -- the index sequences are identical"""
+    from reth_amd._lib import c_vp, call, ptr, stream_ptr
+    from reth_amd.replay import Column, HbmReplay
+
+    cap, B = 4096, 64
+    rng = np.random.default_rng(5)
+    ids = torch.arange(cap, device=dev)
+    w = rng.random(cap) + 0.1
+
+    def run(form):
+        rep = HbmReplay(cap, [Column((), torch.int64)], alpha=0.6, beta=0.4, device=dev, seed=11,
+                        sampler=sampler)
+        rep.append([ids], w)
+        seq = []
+        for _ in range(4):
+            cols, idx, isw = rep.new_batch(B)
+            arr = (c_vp * 1)(ptr(cols[0]))
+            if form == "fused":
+                rep.sample_into(B, cols, idx, isw)
+            else:
+                call("rth_replay_sample", rep._h, B, None, None, ptr(idx), ptr(isw), stream_ptr())
+                if form == "split":
+                    call("rth_replay_gather", rep._h, ptr(idx), B, arr, stream_ptr())
+            seq.append(idx.cpu().numpy().copy())
+            if form != "none":
+                assert np.array_equal(cols[0].cpu().numpy(), seq[-1])
+        return np.stack(seq)
+
+    fused = run("fused")
+    assert len({tuple(r) for r in fused}) == 4  # every call draws anew
+    assert np.array_equal(fused, run("split"))
+    assert np.array_equal(fused, run("none"))

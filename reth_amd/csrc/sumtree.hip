@@ -181,7 +181,14 @@ struct UpdArgs {
   int32_t post_tail;  // st->tail += n after every read of it (the append's FIFO advance)
   int32_t timing;     // record phase timestamps in g_upd_clock (RTH_TREE_TIMING=1)
   int32_t fuse_top;   // the subtree pass's last workgroup runs the top pass (else its own launch)
+  // nullable: the subtree pass stages the top pass's key information here (set when it runs):
+  // bytes 0 .. 2047 = touched flags of the level-S nodes (each written by the node's owner,
+  // no atomics: one line per 128 nodes, not a contended bitmap), stage[kStageFlags + i] =
+  // the last key (launch order) on top node i, or -1.  The top pass reads and re-arms it
+  // (no scan of the keys).
+  int32_t *stage;
 };
+constexpr int kStageFlags = 512;  // int32 words of touched flags (2^11 level-S nodes, 1 byte each)
 
 // FIFO start and alpha of a launch: both replay-state words loaded together
 __device__ __forceinline__ void upd_prologue(const UpdArgs &a, int64_t *fifo_start, double *alpha) {
@@ -273,7 +280,7 @@ __device__ __forceinline__ int wg_scan(int x, int *wsum, int *total) {
     if (lane >= o) incl += y;
   }
   if (lane == 63) wsum[w] = incl;
-  __syncthreads();
+  lds_barrier();  // LDS only: a staged top-key atomic (is_mine) is not waited for
   int base = 0, tot = 0;
 #pragma unroll
   for (int k = 0; k < kSubThreads / 64; ++k) {
@@ -281,7 +288,7 @@ __device__ __forceinline__ int wg_scan(int x, int *wsum, int *total) {
     if (k < w) base += s;
     tot += s;
   }
-  __syncthreads();  // wsum may be reused right away
+  lds_barrier();  // wsum may be reused right away
   *total = tot;
   return base + incl - x;
 }
@@ -315,7 +322,12 @@ __global__ __launch_bounds__(kSubThreads) void k_tree_update_sub(UpdArgs a, int 
   auto is_mine = [&](int64_t g, uint64_t *key, bool *valued) -> bool {
     if (g >= N) return false;
     int64_t id = upd_id(a, g, fifo_start);
-    if (id < top || id >= cap) return false;
+    if (id < top) {  // a key above S: the top pass's (workgroup id % G records it, last wins)
+      if (last_pass && a.stage && id >= 0 && (uint32_t)(id % G) == blockIdx.x)
+        __hip_atomic_fetch_max(&a.stage[kStageFlags + id], (int32_t)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    if (id >= cap) return false;
     int d = node_depth(id);
     *valued = d <= D;
     if (d > D) {
@@ -355,13 +367,13 @@ __global__ __launch_bounds__(kSubThreads) void k_tree_update_sub(UpdArgs a, int 
         const int rank = wg_scan(mine[u] ? 1 : 0, wsum, &total);
         const int take = R - cnt;
         if (tid == 0) s_next = -1;
-        __syncthreads();
+        lds_barrier();
         if (mine[u] && rank < take) {
           slot_g[cnt + rank] = valued[u] ? (int32_t)g : ~(int32_t)g;  // < 0: valueless
           scratch[cnt + rank] = kk[u] | (uint64_t)(cnt + rank);
         }
         if (mine[u] && rank == take) s_next = (int)(g - pos);  // first key left for the next round
-        __syncthreads();
+        lds_barrier();
         if (total > take) {
           cnt = R;
           pos += s_next;
@@ -507,6 +519,9 @@ __global__ __launch_bounds__(kSubThreads) void k_tree_update_sub(UpdArgs a, int 
         if (L == S) {
           __hip_atomic_store(&a.nd[node + 1].sum, x.ls, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_store(&a.nd[node + 1].mn, x.lm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (last_pass && a.stage)  // the level-S node was touched (this workgroup owns it)
+            __hip_atomic_store(reinterpret_cast<uint8_t *>(a.stage) + (node - top), (uint8_t)1, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
         } else {
           a.nd[node + 1].sum = x.ls;
           a.nd[node + 1].mn = x.lm;
@@ -664,10 +679,37 @@ __device__ void tree_top(const UpdArgs &a, int S, TopLds &L) {
     us[t] = x.s;
     um[t] = x.m;
   }
+  // ---- keys: the last writer of each node this lane maintains (w1, w2, wr, wu) and the
+  // touched flags of its level-S children (mb, 8 bits) -- staged by the subtree pass, or
+  // found by a scan of the keys
+  const bool staged = a.stage != nullptr;
+  int32_t w1[4], w2[2], wr[kTopRegH], wu = -1;
+  uint32_t mb = 0;
+  uint64_t flags8 = 0;  // staged: the touched flags of this lane's 8 level-S children, one byte each
+  auto node_ok = [&](int64_t i) { return lane && i < cap; };
+  auto stage_win = [&](int64_t i) -> int32_t {
+    return __hip_atomic_load(&a.stage[kStageFlags + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  if (staged) {  // S == kTopS here: every lane owns a level S-3 node
+#pragma unroll
+    for (int q = 0; q < 4; ++q) w1[q] = node_ok(b1 + q) ? stage_win(b1 + q) : -1;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) w2[q] = node_ok(b2 + q) ? stage_win(b2 + q) : -1;
+#pragma unroll
+    for (int h = 0; h < kTopRegH; ++h) {
+      const int64_t i = ((int64_t)1 << (S - 3 - h)) - 1 + (t >> h);
+      wr[h] = (h <= S - 3 && (t & ((1 << h) - 1)) == 0 && node_ok(i)) ? stage_win(i) : -1;
+    }
+    if (lds_rec) wu = stage_win(t);
+    flags8 = lane ? __hip_atomic_load(reinterpret_cast<uint64_t *>(a.stage) + t, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT)
+                  : 0ull;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) mb |= (uint32_t)((flags8 >> (8 * c)) & 1u) << c;
+  } else {
   for (int i = t; i < ntop; i += kTopThreads) win[i] = -1;
   for (int i = t; i < (kTopNodes + 1) / 32; i += kTopThreads) bot[i] = 0u;
   __syncthreads();
-  // ---- keys: last writer per top node, touched flags of level S (their subtrees had keys)
   constexpr int kScanU = 4;
   for (int64_t g0 = 0; g0 < N; g0 += kScanU * kTopThreads) {
     int64_t id[kScanU];
@@ -689,6 +731,22 @@ __device__ void tree_top(const UpdArgs &a, int S, TopLds &L) {
     }
   }
   __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 4; ++q) w1[q] = node_ok(b1 + q) ? win[b1 + q] : -1;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) w2[q] = node_ok(b2 + q) ? win[b2 + q] : -1;
+#pragma unroll
+  for (int h = 0; h < kTopRegH; ++h) {
+    const int64_t i = ((int64_t)1 << (S - 3 - h)) - 1 + (t >> h);
+    wr[h] = (h <= S - 3 && (t & ((1 << h) - 1)) == 0 && node_ok(i)) ? win[i] : -1;
+  }
+  if (lds_rec) wu = win[t];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const int b = 8 * t + c;
+    if (lane && b < (1 << S)) mb |= ((bot[b >> 5] >> (b & 31)) & 1u) << c;
+  }
+  }
   if (a.timing && t == 0) g_upd_clock[3] = wall_clock64();
   // ---- new priorities of this lane's key nodes (before the level loop: it issues no loads,
   // so its stores are never waited for)
@@ -696,34 +754,29 @@ __device__ void tree_top(const UpdArgs &a, int S, TopLds &L) {
   if (lane) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int64_t i = b1 + q;
-      if (i < cap && win[i] >= 0) {
-        r1[q].v = priority_of(a, alpha, win[i]);
+      if (w1[q] >= 0) {
+        r1[q].v = priority_of(a, alpha, w1[q]);
         key1 |= 1 << q;
       }
     }
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-      const int64_t i = b2 + q;
-      if (i < cap && win[i] >= 0) {
-        r2[q].v = priority_of(a, alpha, win[i]);
+      if (w2[q] >= 0) {
+        r2[q].v = priority_of(a, alpha, w2[q]);
         key2 |= 1 << q;
       }
     }
 #pragma unroll
     for (int h = 0; h < kTopRegH; ++h) {
-      if (h <= S - 3 && (t & ((1 << h) - 1)) == 0) {
-        const int64_t i = ((int64_t)1 << (S - 3 - h)) - 1 + (t >> h);
-        if (i < cap && win[i] >= 0) {
-          rr[h].v = priority_of(a, alpha, win[i]);
-          keyr |= 1 << h;
-        }
+      if (wr[h] >= 0) {
+        rr[h].v = priority_of(a, alpha, wr[h]);
+        keyr |= 1 << h;
       }
     }
   }
   if (lds_rec) {
-    ukey[t] = win[t] >= 0;
-    if (win[t] >= 0) uv[t] = priority_of(a, alpha, win[t]);
+    ukey[t] = wu >= 0;
+    if (wu >= 0) uv[t] = priority_of(a, alpha, wu);
   }
   __syncthreads();
   if (a.timing && t == 0) g_upd_clock[6] = wall_clock64();
@@ -733,9 +786,8 @@ __device__ void tree_top(const UpdArgs &a, int S, TopLds &L) {
     TopVal v1[4], v2[2];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int b = 2 * (4 * t + q);  // level-S index of the left child
-      const TopVal L{cs[2 * q], cm[2 * q], (int)((bot[b >> 5] >> (b & 31)) & 1u)};
-      const TopVal R{cs[2 * q + 1], cm[2 * q + 1], (int)((bot[(b + 1) >> 5] >> ((b + 1) & 31)) & 1u)};
+      const TopVal L{cs[2 * q], cm[2 * q], (int)((mb >> (2 * q)) & 1u)};
+      const TopVal R{cs[2 * q + 1], cm[2 * q + 1], (int)((mb >> (2 * q + 1)) & 1u)};
       v1[q] = b1 + q < cap ? top_node(a, b1 + q, r1[q], (key1 >> q) & 1, L, R) : TopVal{0.0, 0.0, 0};
     }
 #pragma unroll
@@ -785,6 +837,23 @@ __device__ void tree_top(const UpdArgs &a, int S, TopLds &L) {
     }
   }
   if (a.timing && t == 0) g_upd_clock[8] = wall_clock64();
+  if (staged) {  // re-arm what this lane read (its values are consumed: no load is pending)
+    auto clear = [&](int64_t i) {
+      __hip_atomic_store(&a.stage[kStageFlags + i], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (w1[q] >= 0) clear(b1 + q);
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+      if (w2[q] >= 0) clear(b2 + q);
+#pragma unroll
+    for (int h = 0; h < kTopRegH; ++h)
+      if (wr[h] >= 0) clear(((int64_t)1 << (S - 3 - h)) - 1 + (t >> h));
+    if (wu >= 0) clear(t);
+    if (flags8)
+      __hip_atomic_store(reinterpret_cast<uint64_t *>(a.stage) + t, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   if (t == 0) {
     if (a.st) {
       if (a.pre_step) a.st->sched_step += 1;
@@ -872,7 +941,12 @@ struct rth_sumtree {
   int device;
   int maxd;
   Node *nodes;
+  int32_t *stage;  // UpdArgs::stage: behind the nodes in the same allocation, kept re-armed
 };
+
+namespace rth {
+constexpr size_t kStageInts = kStageFlags + kTopNodes;
+}
 
 namespace rth {
 int tree_update_impl(rth_sumtree *t, const int64_t *idx, int64_t fifo_start, const double *w64,
@@ -917,6 +991,7 @@ int tree_update_impl(rth_sumtree *t, const int64_t *idx, int64_t fifo_start, con
       RTH_LAUNCHED();
     }
     const int64_t nsub = int64_t(1) << S;
+    a.stage = t->stage;  // the last pass stages the top pass's keys
     hipLaunchKernelGGL(k_tree_update_sub, dim3((unsigned)(nsub < grid ? nsub : grid)), dim3(kSubThreads), 0, s, a, S,
                        two ? S1 - 1 : t->maxd, 1);
     RTH_LAUNCHED();
@@ -947,13 +1022,16 @@ int rth_sumtree_create(int64_t capacity, int device, rth_sumtree **out) {
               (long long)capacity);
   RTH_HIP(hipSetDevice(device));
   Node *nodes = nullptr;
-  const size_t bytes = (size_t)(capacity + 2) * sizeof(Node);
+  const size_t node_bytes = (size_t)(capacity + 2) * sizeof(Node);
+  const size_t bytes = node_bytes + kStageInts * sizeof(int32_t);
   if (hipMalloc(&nodes, bytes) != hipSuccess) {
     set_error("rth_sumtree_create: hipMalloc(%zu) failed", bytes);
     return RTH_ERR_NOMEM;
   }
-  RTH_HIP(hipMemset(nodes, 0, bytes));
-  auto *t = new rth_sumtree{capacity, device, node_depth(capacity - 1), nodes};
+  RTH_HIP(hipMemset(nodes, 0, node_bytes + kStageFlags * sizeof(int32_t)));  // no touched flag,
+  int32_t *stage = reinterpret_cast<int32_t *>(reinterpret_cast<char *>(nodes) + node_bytes);
+  RTH_HIP(hipMemset(stage + kStageFlags, 0xff, kTopNodes * sizeof(int32_t)));  // no key (-1) on any top node
+  auto *t = new rth_sumtree{capacity, device, node_depth(capacity - 1), nodes, stage};
   *out = t;
   return RTH_OK;
 }

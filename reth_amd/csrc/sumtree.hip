@@ -139,6 +139,48 @@ __device__ __forceinline__ int64_t tree_find(const Node *__restrict__ nd, int64_
   }
 }
 
+// The same walk with a group of 2^K lanes per target (K levels per round trip): lane q of
+// the group loads the q-th pair of the prefetched subtree -- one 64-byte pair per lane
+// instead of 2^K - 1 per lane -- and every lane of the group takes the same K steps on the
+// pairs it reads from its group mates (ds_bpermute).  The group's control flow is uniform
+// (all its lanes hold the same target), so a shuffle never reads an inactive lane.
+template <int K>
+__device__ __forceinline__ int64_t tree_find_group(const Node *__restrict__ nd, int64_t cap, double w, int base,
+                                                   int sub) {
+  constexpr int NP = (1 << K) - 1;
+  int64_t cur = 0;
+  double cval = nd[1].val;
+  const int dq = 31 - __builtin_clz(sub + 1);
+  const int64_t off = sub + 1 - (1 << dq);
+  for (;;) {
+    const Pair mine = sub < NP ? load_pair(nd, cap, (cur + 1) * (int64_t(1) << dq) - 1 + off) : Pair{0.0, 0.0, 0.0};
+    int q = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const Pair pk{__shfl(mine.ls, base + q, 64), __shfl(mine.lv, base + q, 64), __shfl(mine.rv, base + q, 64)};
+      const int64_t before = cur;
+      if (!find_step(cur, cval, w, pk, cap)) return cur;
+      q = 2 * q + 1 + (int)(cur - (2 * before + 1));
+    }
+  }
+}
+
+// levels per round trip of the grouped walk: 0 = one lane per target (tree_find)
+static int find_group_k() {  // read per call: tests switch it
+  const char *e = getenv("RTH_FIND_GROUP");
+  const int v = e ? atoi(e) : 4;
+  return (v == 0 || v == 3 || v == 5) ? v : 4;
+}
+
+__device__ __forceinline__ int64_t tree_find_grouped(const Node *__restrict__ nd, int64_t cap, double w, int gk,
+                                                     int base, int sub) {
+  switch (gk) {
+    case 3: return tree_find_group<3>(nd, cap, w, base, sub);
+    case 5: return tree_find_group<5>(nd, cap, w, base, sub);
+    default: return tree_find_group<4>(nd, cap, w, base, sub);
+  }
+}
+
 // tuning aids: levels per round trip and sample workgroup size (RTH_FIND_K, RTH_SAMPLE_BS)
 static int env_int(const char *name, int dflt) {
   const char *e = getenv(name);
@@ -148,8 +190,11 @@ static int find_k() {
   static const int k = env_int("RTH_FIND_K", 2);
   return k;
 }
-static int sample_bs() {
-  static const int b = env_int("RTH_SAMPLE_BS", 64);
+static int sample_bs() {  // a multiple of 64: a lane group never straddles two waves
+  static const int b = [] {
+    const int v = env_int("RTH_SAMPLE_BS", 64);
+    return v >= 64 && v <= 1024 && v % 64 == 0 ? v : 64;
+  }();
   return b;
 }
 
@@ -251,12 +296,17 @@ __device__ void tree_top(const UpdArgs &a, int S, TopLds &L);
 // in LDS (each entry pushes its result into its parent's child slot), and the touched
 // nodes are stored at the end.  A round whose entries would not fit is re-gathered with
 // proportionally fewer keys.
-// LDS stays under 16 KB so a workgroup fits on a CU beside the learner's conv2/conv3 tiles
-// (131 / 147 KB of the 160 KB): the update runs concurrently with the learner stream.
+// A leaf key (no children in the tree) gets no entry: its result goes straight into its
+// parent's entry, so a contiguous append of 256 leaves fits one round.  LDS (18.2 KB at 320
+// entries) fits on a CU beside the learner's conv2 tiles (131 of the 160 KB); 320 entries
+// measured faster than 256 (Breakout's 2,048-row append: 4 rounds instead of 5).
 constexpr int kSubThreads = 256;
 constexpr int kSubKeys = 256;      // keys per round (one per lane; 10 slot bits in the sort key)
 constexpr int kSlotBits = 10;
-constexpr int kSubEntries = 256;   // touched (node, level) entries per round
+#ifndef SUB_ENTRIES
+#define SUB_ENTRIES 320
+#endif
+constexpr int kSubEntries = SUB_ENTRIES;  // touched (node, level) entries per round
 constexpr int kSubGrid = 256;
 constexpr int kSubSplit = 4;          // the second pass covers S .. S + 3
 constexpr int kSubTwoPassDepth = 8;   // two passes when maxd >= S + 8 (trees of >= 2^19 nodes)
@@ -398,7 +448,7 @@ __global__ __launch_bounds__(kSubThreads) void k_tree_update_sub(UpdArgs a, int 
     }
     __syncthreads();  // scratch is reused as ebase / epar below
     // ---- owned level range and entry base of key j
-    int own = 0;
+    int own = 0, lf = 0;
     if (j < cnt) {
       const uint64_t kj = keys[j];
       const int dj = key_depth(kj);
@@ -412,9 +462,13 @@ __global__ __launch_bounds__(kSubThreads) void k_tree_update_sub(UpdArgs a, int 
       }
       elt[j] = (int8_t)(S + sh);
       own = max(0, dj - S + 1 - sh);
+      // a leaf below S (no children in the tree) gets no entry: its result (val, val or 1)
+      // is known at load time and goes straight into its parent's child slot
+      const int64_t nid = (int64_t)(key_aligned(kj) >> (maxd - dj)) - 1;
+      lf = own > 0 && dj > S && 2 * nid + 1 >= cap;
     }
     int E;
-    const int off = wg_scan(own, wsum, &E);
+    const int off = wg_scan(own - lf, wsum, &E);
     if (j < cnt) ebase[j] = off;
     if (E > kSubEntries) {  // uniform: re-gather this round with proportionally fewer keys
       R = max(1, (int)((int64_t)cnt * kSubEntries / E));
@@ -425,6 +479,7 @@ __global__ __launch_bounds__(kSubThreads) void k_tree_update_sub(UpdArgs a, int 
     const uint64_t k_j = j < cnt ? keys[j] : 0;
     const int lt_j = j < cnt ? elt[j] : 0;
     const int d_j = j < cnt ? key_depth(k_j) : -1;
+    const int de_j = d_j - lf;  // the deepest level with an entry
     const int eb_j = j < cnt ? ebase[j] : 0;
     const uint64_t al_j = key_aligned(k_j);
     // ---- parent entry of each key's shallowest owned entry (lower_bound of its owner)
@@ -442,6 +497,7 @@ __global__ __launch_bounds__(kSubThreads) void k_tree_update_sub(UpdArgs a, int 
     }
     // ---- load every entry's inputs (all of a key's levels in flight together; LDS stores
     // cannot alias the loads) and its own node's new priority (the last duplicate's)
+    double leaf_v = 0.0;
     if (j < cnt && own > 0) {
       // the node's new val: the last valued duplicate's priority; none -> its val stays
       int32_t g_last = slot_g[k_j & ((1u << kSlotBits) - 1)];
@@ -474,15 +530,30 @@ __global__ __launch_bounds__(kSubThreads) void k_tree_update_sub(UpdArgs a, int 
 #pragma unroll
         for (int u = 0; u < kLoadU; ++u) {
           const int L = L0 + u;
-          if (L <= d_j) ent[eb_j + L - lt_j] = SubEnt{L == d_j && key_val ? pv : v[u], ls[u], lm[u], rs[u], rm[u]};
+          const double vu = L == d_j && key_val ? pv : v[u];
+          if (L <= de_j) ent[eb_j + L - lt_j] = SubEnt{vu, ls[u], lm[u], rs[u], rm[u]};
+          else if (L == d_j) leaf_v = vu;
         }
       }
     }
     __syncthreads();
+    if (lf) {  // _numba_maintain_node of a leaf, pushed into the parent's entry
+      const int64_t node = (int64_t)(al_j >> (maxd - d_j)) - 1;
+      const int p = d_j > lt_j ? eb_j + (d_j - 1 - lt_j) : ep_j;
+      const double mn = (leaf_v != 0.0) ? leaf_v : 1.0;
+      if (node & 1) {
+        ent[p].ls = leaf_v;
+        ent[p].lm = mn;
+      } else {
+        ent[p].rs = leaf_v;
+        ent[p].rm = mn;
+      }
+    }
+    lds_barrier();
     if (a.timing && tid == 0 && blockIdx.x == 0) g_upd_clock[1] = wall_clock64();
     // ---- levels, deepest first (_numba_maintain_node on every touched node, once)
     for (int L = D; L >= S; --L) {
-      if (L >= lt_j && L <= d_j) {
+      if (L >= lt_j && L <= de_j) {
         const int e = eb_j + L - lt_j;
         const SubEnt x = ent[e];
         const int64_t node = (int64_t)(al_j >> (maxd - L)) - 1, l = 2 * node + 1;
@@ -512,8 +583,14 @@ __global__ __launch_bounds__(kSubThreads) void k_tree_update_sub(UpdArgs a, int 
     }
     // ---- store the touched nodes (a level-S root write-through: the top pass reads it from
     // another workgroup after the ticket below)
+    if (lf) {
+      const int64_t node = (int64_t)(al_j >> (maxd - d_j)) - 1;
+      a.nd[node + 1].sum = leaf_v;
+      a.nd[node + 1].mn = (leaf_v != 0.0) ? leaf_v : 1.0;
+      a.nd[node + 1].val = leaf_v;
+    }
     if (j < cnt) {
-      for (int L = lt_j; L <= d_j; ++L) {
+      for (int L = lt_j; L <= de_j; ++L) {
         const SubEnt x = ent[eb_j + L - lt_j];
         const int64_t node = (int64_t)(al_j >> (maxd - L)) - 1;
         if (L == S) {
@@ -871,11 +948,26 @@ static_assert(sizeof(TopLds) <= sizeof(SubEnt) * kSubEntries, "the top pass reus
 static_assert(kTopThreads == kSubThreads, "the subtree pass's last workgroup runs the top pass");
 
 // ------------------------------------------------------------------ find / sample
+// target i of a launch with gk > 0 (groups of 2^gk lanes) or gk == 0 (one lane each)
+struct FindLane {
+  int64_t i;
+  int base, sub;
+};
+__device__ __forceinline__ FindLane find_lane(int gk) {
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gk == 0) return FindLane{g, 0, 0};
+  const int lane = threadIdx.x & 63, sub = lane & ((1 << gk) - 1);
+  return FindLane{g >> gk, lane - sub, sub};
+}
+
 __global__ void k_tree_find(const Node *__restrict__ nd, int64_t cap, const double *__restrict__ tg,
-                            int64_t n, int64_t *__restrict__ idx_out, double *__restrict__ val_out, int kspec) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const int64_t k = tree_find(nd, cap, tg[i], kspec);
+                            int64_t n, int64_t *__restrict__ idx_out, double *__restrict__ val_out, int kspec,
+                            int gk) {
+  const FindLane fl = find_lane(gk);
+  const int64_t i = fl.i;
+  if (i >= n) return;  // uniform over a group
+  const int64_t k = gk ? tree_find_grouped(nd, cap, tg[i], gk, fl.base, fl.sub) : tree_find(nd, cap, tg[i], kspec);
+  if (fl.sub) return;
   if (idx_out) idx_out[i] = k;
   if (val_out) val_out[i] = nd[k + 1].val;
 }
@@ -884,9 +976,10 @@ __global__ void k_tree_find(const Node *__restrict__ nd, int64_t cap, const doub
 __global__ void k_tree_sample(const Node *__restrict__ nd, int64_t cap, int64_t batch,
                               const double *__restrict__ uniforms, uint64_t seed, uint64_t counter,
                               int is_weights, double beta, const ReplayState *st, rth_schedule beta_s,
-                              int64_t *__restrict__ idx_out, double *__restrict__ out, int kspec) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= batch) return;
+                              int64_t *__restrict__ idx_out, double *__restrict__ out, int kspec, int gk) {
+  const FindLane fl = find_lane(gk);
+  const int64_t i = fl.i;
+  if (i >= batch) return;  // uniform over a group
   if (st) {  // a replay shard's device state: call counter and beta_s(sched_step)
     counter = (uint64_t)st->calls;
     beta = sched_value(beta_s, st->sched_step);
@@ -895,7 +988,8 @@ __global__ void k_tree_sample(const Node *__restrict__ nd, int64_t cap, int64_t 
   const double seg = total / (double)batch;
   const double u = uniforms ? uniforms[i] : philox_uniform(seed, counter, (uint32_t)i, STREAM_SAMPLE);
   const double t = rmul(radd((double)i, u), seg);
-  const int64_t k = tree_find(nd, cap, t, kspec);
+  const int64_t k = gk ? tree_find_grouped(nd, cap, t, gk, fl.base, fl.sub) : tree_find(nd, cap, t, kspec);
+  if (fl.sub) return;
   const double p = nd[k + 1].val;
   idx_out[i] = k;
   if (is_weights) {
@@ -1005,10 +1099,11 @@ int tree_sample_impl(rth_sumtree *t, int64_t batch, const double *uniforms, uint
                      uint64_t counter, int is_weights, double beta, int64_t *idx_out, double *out,
                      hipStream_t s, const ReplayState *st, const rth_schedule *beta_s) {
   if (batch <= 0) return RTH_OK;
-  const int bs = sample_bs();
-  hipLaunchKernelGGL(k_tree_sample, dim3((unsigned)((batch + bs - 1) / bs)), dim3(bs), 0, s, t->nodes,
+  const int bs = sample_bs(), gk = find_group_k();
+  const int64_t lanes = batch << gk;
+  hipLaunchKernelGGL(k_tree_sample, dim3((unsigned)((lanes + bs - 1) / bs)), dim3(bs), 0, s, t->nodes,
                      t->cap, batch, uniforms, seed, counter, is_weights, beta, st,
-                     beta_s ? *beta_s : rth_schedule{}, idx_out, out, find_k());
+                     beta_s ? *beta_s : rth_schedule{}, idx_out, out, find_k(), gk);
   RTH_LAUNCHED();
   return RTH_OK;
 }
@@ -1069,9 +1164,10 @@ int rth_sumtree_find(rth_sumtree *t, const double *tg, int64_t n, int64_t *idx_o
                      void *stream) {
   RTH_REQUIRE(t && (n == 0 || tg), "rth_sumtree_find: bad arguments");
   if (n == 0) return RTH_OK;
-  const int bs = sample_bs();
-  hipLaunchKernelGGL(k_tree_find, dim3((unsigned)((n + bs - 1) / bs)), dim3(bs), 0, as_stream(stream),
-                     t->nodes, t->cap, tg, n, idx_out, val_out, find_k());
+  const int bs = sample_bs(), gk = find_group_k();
+  const int64_t lanes = n << gk;
+  hipLaunchKernelGGL(k_tree_find, dim3((unsigned)((lanes + bs - 1) / bs)), dim3(bs), 0, as_stream(stream),
+                     t->nodes, t->cap, tg, n, idx_out, val_out, find_k(), gk);
   RTH_LAUNCHED();
   return RTH_OK;
 }

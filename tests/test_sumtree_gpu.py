@@ -202,3 +202,38 @@ def test_per_distribution(dev):
     w = rng.random(cap).astype(np.float32)
     per.update(np.arange(cap), w)
     check(w)
+
+
+@pytest.mark.parametrize("gk", ["0", "3", "4", "5"])
+def test_find_lane_groups(dev, orc, golden, monkeypatch, gk):
+    """the walk with one lane per target (RTH_FIND_GROUP=0) and with lane groups of 2^3 /
+    2^4 / 2^5 (several levels per round trip, one pair per lane) returns the oracle's
+    indices: ragged trees, zeros, targets at and past the total, the golden small trees"""
+    from reth_amd.replay import SumTree
+
+    monkeypatch.setenv("RTH_FIND_GROUP", gk)
+    rng = np.random.default_rng(77)
+    for cap in (1, 2, 3, 7, 31, 33, 1000, 65537, 300000):
+        t = SumTree(cap, dev)
+        o = orc.Tree(cap)
+        idx = rng.integers(0, cap, max(1, cap // 2))
+        w = rng.random(len(idx))
+        w[rng.random(len(idx)) < 0.1] = 0.0
+        t.update(idx, w)
+        o.update(idx, w)
+        u = rng.random(300)  # not a multiple of any group or workgroup size
+        gi, gv = t.sample(300, uniforms=u)
+        oi, ov = o.sample(u)
+        assert np.array_equal(gi.cpu().numpy(), oi) and np.array_equal(gv.cpu().numpy(), ov), cap
+        tg = np.concatenate([rng.random(61) * o.total() * 1.05, [0.0, o.total(), o.total() + 1e-6]])
+        fi, _ = t.find(tg)
+        assert np.array_equal(fi.cpu().numpy(), np.array([o.find(x) for x in tg])), cap
+    g = golden("sumtree_small.npz")
+    for tag in SMALL_TAGS:
+        t = SumTree(int(g[f"{tag}/capacity"]), dev)
+        for k in range(int(g[f"{tag}/n_upd"])):
+            t.update(g[f"{tag}/upd{k}_idx"], g[f"{tag}/upd{k}_w"])
+        idx, _ = t.find(g[f"{tag}/targets"])
+        assert np.array_equal(idx.cpu().numpy(), g[f"{tag}/find"]), tag
+        idx, val = t.sample(len(g[f"{tag}/sample_u"]), uniforms=g[f"{tag}/sample_u"])
+        assert np.array_equal(idx.cpu().numpy(), g[f"{tag}/sample_idx"]), tag

@@ -281,7 +281,7 @@ __device__ __forceinline__ void lds_barrier() {
 }
 
 struct TopLds;
-__device__ void tree_top(const UpdArgs &a, int S, TopLds &L);
+__device__ __forceinline__ void tree_top(const UpdArgs &a, int S, TopLds &L);
 
 // ---------------------------------------------------------------- subtree pass
 // Workgroup w owns the level-S subtrees s with s % gridDim.x == w (consecutive FIFO slots
@@ -706,7 +706,7 @@ struct TopLds {
   int ukey[8];
 };
 
-__device__ void tree_top(const UpdArgs &a, int S, TopLds &L) {
+__device__ __forceinline__ void tree_top(const UpdArgs &a, int S, TopLds &L) {
   int32_t *const win = L.win;
   uint32_t *const bot = L.bot;
   double *const xs = L.xs, *const xm = L.xm, *const uv = L.uv, *const us = L.us, *const um = L.um;

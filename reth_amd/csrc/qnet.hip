@@ -192,6 +192,7 @@ __global__ __launch_bounds__(256) void k_heads_merge(HeadsDims d, const float *_
       return;
     }
     // reference order c * P + p; float4 loads, all issued before the first LDS write
+    // (selects, not conditional loads: the array stays in registers)
     {
       const int F4 = (int)(F / 4);
       const float4 *s4 = reinterpret_cast<const float4 *>(src);
@@ -199,7 +200,7 @@ __global__ __launch_bounds__(256) void k_heads_merge(HeadsDims d, const float *_
 #pragma unroll
       for (int u = 0; u < kRowF4; ++u) {
         const int i = threadIdx.x + u * 256;
-        if (i < F4) v[u] = s4[i];
+        v[u] = s4[i < F4 ? i : 0];
       }
 #pragma unroll
       for (int u = 0; u < kRowF4; ++u) {

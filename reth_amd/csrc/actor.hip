@@ -370,7 +370,8 @@ int rth_synth_env_reset(uint8_t *frames, int64_t N, int32_t ring, uint64_t seed,
 
 int rth_compact_flagged(const float *flag, const int64_t *vals, int64_t n, int64_t *out, int64_t cap, int64_t fill,
                         int64_t base, int64_t *count_out, void *stream) {
-  RTH_REQUIRE(flag && vals && out && count_out && n >= 0 && cap >= 0, "rth_compact_flagged: bad arguments");
+  RTH_REQUIRE((n == 0 || (flag && vals)) && (cap == 0 || out) && count_out && n >= 0 && cap >= 0,
+              "rth_compact_flagged: bad arguments");
   hipLaunchKernelGGL(k_compact_flagged, dim3(1), dim3(kCompactThreads), 0, as_stream(stream), flag, vals, n, out, cap,
                      fill, base, count_out);
   RTH_LAUNCHED();

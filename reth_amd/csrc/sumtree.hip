@@ -307,7 +307,9 @@ constexpr int kSlotBits = 10;
 #define SUB_ENTRIES 320
 #endif
 constexpr int kSubEntries = SUB_ENTRIES;  // touched (node, level) entries per round
-constexpr int kSubGrid = 256;
+constexpr int kSubGrid = 256;        // workgroups at most
+constexpr int kSubGridMin = 64;      // ... and at least
+constexpr int kSubKeysPerWg = 12;    // the grid is sized for about this many keys per workgroup
 constexpr int kSubSplit = 4;          // the second pass covers S .. S + 3
 constexpr int kSubTwoPassDepth = 8;   // two passes when maxd >= S + 8 (trees of >= 2^19 nodes)
 static_assert(kSubKeys == kSubThreads, "one key per lane in the rank sort / ownership scan");
@@ -1075,7 +1077,15 @@ int tree_update_impl(rth_sumtree *t, const int64_t *idx, int64_t fifo_start, con
     // the last one to finish (of the last pass) also runs the top pass; deep trees in two
     // passes split at S1 = S + kSubSplit (RTH_TREE_PASSES=1: one pass, A/B aid)
     const int passes = env_int("RTH_TREE_PASSES", 1);  // read per call: tests switch it
-    static const int grid = env_int("RTH_TREE_GRID", kSubGrid);
+    // fewer workgroups for small updates: less dispatch and L2 traffic beside the learner
+    // stream (Pong's 768 keys: 64 workgroups, 0.617-0.620 vs 0.618-0.625 ms/step with 256;
+    // Breakout's 2,560 keys keep 256).  RTH_TREE_GRID fixes it (A/B aid).
+    static const int grid_env = env_int("RTH_TREE_GRID", 0);
+    int grid = grid_env;
+    if (grid <= 0) {
+      grid = kSubGridMin;
+      while (grid < kSubGrid && (int64_t)grid * kSubKeysPerWg < a.pn + a.n) grid *= 2;
+    }
     const int S1 = S + kSubSplit;
     const bool two = passes >= 2 && t->maxd >= S + kSubTwoPassDepth;
     if (two) {

@@ -240,8 +240,8 @@ def test_compact_flagged(dev):
     from reth_amd._lib import call, ptr, stream_ptr
 
     g = torch.Generator(device=dev).manual_seed(4)
-    for n, cap in [(1, 1), (37, 37), (2048, 2048), (3000, 100)]:
-        flag = (torch.rand(n, device=dev, generator=g) < 0.3).float()
+    for n, cap in [(0, 5), (1, 1), (37, 37), (256, 256), (257, 300), (2048, 2048), (3000, 100)]:
+        flag = (torch.rand(max(n, 1), device=dev, generator=g) < 0.3).float()[:n]
         vals = torch.randint(0, 1 << 40, (n,), device=dev, generator=g)
         out = torch.empty(cap, dtype=torch.int64, device=dev)
         cnt = torch.empty(1, dtype=torch.int64, device=dev)

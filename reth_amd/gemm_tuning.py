@@ -16,7 +16,7 @@ import tempfile
 import torch
 
 _ROOT = os.path.dirname(os.path.abspath(__file__))
-RESULTS = os.path.join(_ROOT, "tuned", "tunableop_results_mi355x.csv")
+RESULTS = os.environ.get("RTH_TUNABLEOP_IN") or os.path.join(_ROOT, "tuned", "tunableop_results_mi355x.csv")
 
 
 def enable(tune_missing=True, max_tuning_ms=30):

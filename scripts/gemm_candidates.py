@@ -16,8 +16,12 @@ import torch.nn.functional as F  # noqa: E402
 dev = torch.device("cuda:0")
 w = torch.randn(512, 3136, device=dev) * 0.02
 b = torch.randn(512, device=dev) * 0.02
-for rows in [int(r) for r in (sys.argv[1:] or ["512", "1024"])]:
-    x = torch.rand(rows, 3136, device=dev)
-    y = F.linear(x, w, b)
+for arg in (sys.argv[1:] or ["512", "1024"]):
+    rows, bwd = int(arg.rstrip("b")), arg.endswith("b")  # "512b": also the backward (NN / NT GEMMs)
+    x = torch.rand(rows, 3136, device=dev, requires_grad=bwd)
+    wq = w.clone().requires_grad_(bwd)
+    y = F.linear(x, wq, b)
+    if bwd:
+        y.backward(torch.randn_like(y))
     torch.cuda.synchronize()
-    print(f"rows {rows}: done {tuple(y.shape)}", flush=True)
+    print(f"rows {rows}{' + backward' if bwd else ''}: done {tuple(y.shape)}", flush=True)

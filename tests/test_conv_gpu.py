@@ -163,9 +163,14 @@ def test_forward_heads_u8_rows_matches_miopen(dev):
         net.hip_conv = False
         want = net.forward_heads(frames[rows].float().contiguous(memory_format=torch.channels_last))
         net.hip_conv = True
+        q_gathered = net.forward_heads(frames[rows].contiguous())
         q_all = net.forward_heads(frames)
     torch.testing.assert_close(q, want, rtol=1e-5, atol=1e-4)
-    torch.testing.assert_close(q_all[rows], q, rtol=0, atol=0)  # same kernel, same data
+    # the row index only changes where the torso reads: same kernels, same shapes, same bits
+    torch.testing.assert_close(q_gathered, q, rtol=0, atol=0)
+    # the 40-row batch runs FC1 at another M, where the library GEMM may pick another
+    # solution (another summation order), so only close
+    torch.testing.assert_close(q_all[rows], q, rtol=1e-5, atol=1e-5)
 
 
 def test_hip_torso_gradients_match_miopen(dev):

@@ -15,10 +15,12 @@ with one RCCL all-reduce per update.
 
 The JSON line carries
   roofline:        the dominant kernel of the step (most time per iteration in
-                   profiles/r02_steady_state.txt): conv2's forward (k_conv_bias_relu, fp32
+                   profiles/r02_steady_state.txt): conv3's forward (k_conv_bias_relu, fp32
                    MFMA) in the learner's [s0; s1] pass, timed live over the timed region with
-                   HIP events on the learner stream (the learner graph is cut around that
-                   launch); achieved = algorithmic FLOPs per launch / mean launch duration
+                   HIP events on the learner stream (the learner graph is cut once, around the
+                   conv2 + conv3 launches); achieved = algorithmic FLOPs per launch / mean
+                   launch duration
+  roofline_conv2:  conv2's forward in the same pass (the second kernel), timed the same way
   roofline_gather: the replay gather (k_copy_rows), HBM-bound, timed live the same way
   roofline_conv1:  conv1 on uint8 stacks (k_conv1_u8_bf16x3) alone, against the bf16 MFMA peak
                    of the instruction it issues (three exact-split bf16 products per fp32 one)
@@ -246,8 +248,8 @@ def main():
                     help="SURVEY §8(d) C4 hyperparameter-faithful data parallelism: a global batch of --batch "
                          "split over the N learners (B / N per GPU) instead of B per GPU")
     ap.add_argument("--windows", type=int, default=5, help="sub-windows of the timed region reported beside it")
-    ap.add_argument("--no-probe", action="store_true", help="do not cut the learner graph around conv2 "
-                    "(no live per-launch timing of the dominant kernel)")
+    ap.add_argument("--no-probe", action="store_true", help="do not cut the learner graph around conv2/conv3 "
+                    "(no live per-launch timing of the dominant kernels)")
     ap.add_argument("--actor-steps-per-update", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-iters", type=int, default=72)
@@ -310,17 +312,20 @@ def main():
         return e
 
     ax.loader.gather_timer = timer
-    # the dominant kernel, live: events on the learner stream around its conv2 launch (the
-    # learner graph is cut there: ApexDQN._learner_replay calls conv_probe between parts)
-    conv2_events = []
+    # the dominant kernels, live: events on the learner stream around its conv2 and conv3
+    # launches (the learner graph is cut there: ApexDQN._learner_replay calls conv_probe
+    # between parts)
+    conv_events = {"conv2": [], "conv3": []}
 
     def conv_probe(tag):
         e = torch.cuda.Event(enable_timing=True)
         e.record()
-        if tag == "conv2":
-            conv2_events.append([e, None])
-        elif conv2_events and conv2_events[-1][1] is None:
-            conv2_events[-1][1] = e
+        base = tag[:-len("_end")] if tag.endswith("_end") else tag
+        ev = conv_events.setdefault(base, [])
+        if base == tag:
+            ev.append([e, None])
+        elif ev and ev[-1][1] is None:
+            ev[-1][1] = e
     spans = []
     if os.environ.get("RTH_BENCH_SPAN"):  # diagnostics: the learner block's span on its stream
         replay = ax._learner_replay
@@ -398,7 +403,8 @@ def main():
             print(f"next batch ready after the learner block ends: mean {np.mean(late):.1f} us, median "
                   f"{np.median(late):.1f}, > 0 in {np.mean(np.array(late) > 0) * 100:.0f} % of updates", file=sys.stderr)
     win_ms = [a[1].elapsed_time(b[1]) / (b[0] - a[0]) for a, b in zip(win_ev, win_ev[1:])]
-    conv2_ms = [a.elapsed_time(b) for a, b in conv2_events if b is not None]
+    conv_ms = {t: [a.elapsed_time(b) for a, b in ev if b is not None] for t, ev in conv_events.items()}
+    conv2_ms, conv3_ms = conv_ms["conv2"], conv_ms["conv3"]
     replicas = None
     if world > 1:  # the data-parallel replicas must hold identical parameters
         with torch.no_grad():
@@ -442,6 +448,7 @@ def main():
     step_s = dt / args.steps
     traffic, traffic_src = load_traffic(args.tag, "gather_hbm_bytes_per_launch")
     c2_traffic, c2_src = load_traffic(args.tag, "conv2_learner_hbm_bytes_per_launch")
+    c3_traffic, c3_src = load_traffic(args.tag, "conv3_learner_hbm_bytes_per_launch")
     roofline_gather = {
         "kernel": "rth_replay_gather (k_copy_rows: PER-sampled rows, frames %s)"
                   % ("uint8 stacks" if cfg.hip_conv and cfg.channels_last else "u8->f32 NHWC"),
@@ -452,21 +459,29 @@ def main():
         "isolated_frac": round(bytes_launch / iso_s / 1e9 / HBM_PEAK_GBS, 4),
         "note": "in the timed region the gather overlaps the learner block on a second stream"}
     roofline = roofline_gather
-    if conv2_ms:
-        n2 = 2 * cfg.batch_size  # the learner's [s0; s1] forward
-        c2_flops = 2.0 * n2 * 9 * 9 * 64 * 32 * 4 * 4
-        c2_s = float(np.mean(conv2_ms)) / 1e3
-        roofline = {
-            "kernel": f"k_conv_bias_relu conv2 (fp32 MFMA; 32x20x20 -> 64x9x9, k4 s2) in the learner's [s0; s1] "
-                      f"forward, {n2} samples per launch",
-            "bound": "mfma", "achieved": round(c2_flops / c2_s / 1e12, 2), "peak": FP32_PEAK_TFLOPS,
-            "unit": "TFLOP/s", "frac": round(c2_flops / c2_s / 1e12 / FP32_PEAK_TFLOPS, 4),
-            "traffic": c2_traffic, "traffic_source": c2_src, "flops_per_launch": c2_flops,
-            "algorithmic_bytes_per_launch": n2 * (20 * 20 * 32 + 9 * 9 * 64) * 4 + 64 * 512 * 4 + 64 * 4,
-            "mean_launch_us": round(c2_s * 1e6, 2), "median_launch_us": round(float(np.median(conv2_ms)) * 1e3, 2),
-            "launches_timed": len(conv2_ms),
+    n2 = 2 * cfg.batch_size  # the learner's [s0; s1] forward
+
+    def conv_roofline(ms, name, cin, hin, cout, hout, k, stride, flops, traffic, src):
+        s_ = float(np.mean(ms)) / 1e3
+        return {
+            "kernel": f"k_conv_bias_relu {name} (fp32 MFMA; {cin}x{hin}x{hin} -> {cout}x{hout}x{hout}, k{k} s{stride}) in the "
+                      f"learner's [s0; s1] forward, {n2} samples per launch",
+            "bound": "mfma", "achieved": round(flops / s_ / 1e12, 2), "peak": FP32_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(flops / s_ / 1e12 / FP32_PEAK_TFLOPS, 4),
+            "traffic": traffic, "traffic_source": src, "flops_per_launch": flops,
+            "algorithmic_bytes_per_launch": n2 * (hin * hin * cin + hout * hout * cout) * 4 + cout * k * k * cin * 4 + cout * 4,
+            "mean_launch_us": round(s_ * 1e6, 2), "median_launch_us": round(float(np.median(ms)) * 1e3, 2),
+            "launches_timed": len(ms),
             "note": "timed live over the timed region: HIP events on the learner stream around the launch (the "
                     "learner graph is cut there); it runs concurrently with the actor stream's kernels"}
+    roofline_conv2 = None
+    if conv2_ms:
+        roofline_conv2 = conv_roofline(conv2_ms, "conv2", 32, 20, 64, 9, 4, 2, 2.0 * n2 * 9 * 9 * 64 * 32 * 4 * 4,
+                                       c2_traffic, c2_src)
+        roofline = roofline_conv2
+    if conv3_ms:  # the most time per iteration of any kernel (3 launches: learner, target pass, actors)
+        roofline = conv_roofline(conv3_ms, "conv3", 64, 9, 64, 7, 3, 1, 2.0 * n2 * 7 * 7 * 64 * 64 * 3 * 3,
+                                 c3_traffic, c3_src)
     out = {
         "metric": "env-steps/sec + learner updates/sec, Ape-X DQN Pong, 1/2/4/8 MI355X",
         "value": round(n_env / dt, 1),
@@ -497,6 +512,7 @@ def main():
                  "replicas_identical": replicas} if world > 1 else None,
         "roofline": roofline,
         "roofline_gather": roofline_gather,
+        "roofline_conv2": roofline_conv2,
         "qnet_mfma": {"tflops_per_step": round(flops_step / 1e12, 4),
                       "achieved_tflops": round(flops_step / step_s / 1e12, 2),
                       "peak_fp32_tflops": FP32_PEAK_TFLOPS},

@@ -279,8 +279,8 @@ class ApexDQN:
                     def cut(item, parts=parts, bounds=bounds):
                         # end this part of the learner graph at a boundary: ("bucket", a final
                         # gradient bucket -- its all-reduce runs between the parts, overlapping
-                        # the next one) or ("probe", (tag, launch) -- a launch issued eagerly between
-                        # the parts at every replay, bracketed by the bench's HIP events)
+                        # the next one) or ("probe", [(tag, launch), ...]) -- launches issued eagerly
+                        # between the parts at every replay, each bracketed by the bench's HIP events)
                         parts[-1].capture_end()
                         bounds.append(item)
                         parts.append(torch.cuda.CUDAGraph())
@@ -288,7 +288,7 @@ class ApexDQN:
 
                     parts[0].capture_begin()
                     data, idx, isw = slots[p]
-                    probe = (lambda tag, fn: cut(("probe", (tag, fn)))) if self.cfg.extra.get("probe_conv2") else None
+                    probe = (lambda items: cut(("probe", items))) if self.cfg.extra.get("probe_conv2") else None
                     td = solver.compute_grads(data, isw, q1t=G["q1t"][p] if variant == "pre" else None,
                                               mid=(lambda b: cut(("bucket", b))) if split else None, probe=probe)
                     self.trainer._track(td)
@@ -320,9 +320,9 @@ class ApexDQN:
         gradient buckets (data-parallel learner: every bucket but the last is all-reduced on a
         side stream while the following part runs -- the merged heads' gradients, 95 % of the
         bytes, under the conv backward; the last one on this stream; the final part (heads
-        split + clip + Adam) waits for all of them) and probes (a launch issued eagerly between
-        the parts, bracketed by conv_probe(tag) / conv_probe(tag + "_end"): the bench records
-        HIP events there on this stream for its live per-launch timing)."""
+        split + clip + Adam) waits for all of them) and probes (launches issued eagerly between
+        the parts, each bracketed by conv_probe(tag) / conv_probe(tag + "_end"): the bench
+        records HIP events there on this stream for its live per-launch timing)."""
         G = self._graphs
         parts, bounds = G["learn"][v], G["buckets"][v]
         if len(parts) == 1:
@@ -334,13 +334,13 @@ class ApexDQN:
         comm = None
         for i, (g, (kind, item)) in enumerate(zip(parts, bounds)):
             g.replay()
-            if kind == "probe":  # a launch issued between the parts, optionally between HIP events
-                tag, fn = item
-                if self.conv_probe is not None:
-                    self.conv_probe(tag)
-                fn()
-                if self.conv_probe is not None:
-                    self.conv_probe(tag + "_end")
+            if kind == "probe":  # launches issued between the parts, optionally between HIP events
+                for tag, fn in item:
+                    if self.conv_probe is not None:
+                        self.conv_probe(tag)
+                    fn()
+                    if self.conv_probe is not None:
+                        self.conv_probe(tag + "_end")
                 continue
             key = ("bucket", bucket_at.index(i))
             if i != bucket_at[-1]:

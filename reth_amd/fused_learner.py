@@ -94,10 +94,11 @@ def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None, mid=No
     capture ends a graph there, so the all-reduce of the first bucket overlaps the conv
     backward; whatever mid's caller does to a bucket in place is what the parameters get.
 
-    probe (optional callable) is handed the forward's conv2 launch as probe("conv2", launch)
-    and issues it itself (the bench times that launch live: the capture cuts the learner graph
-    there, and every replay launches it eagerly between HIP events on the learner stream; its
-    buffers live in the graph's pool at fixed addresses)."""
+    probe (optional callable) is handed the forward's conv2 and conv3 launches as
+    probe([("conv2", launch2), ("conv3", launch3)]) and issues them itself (the bench times
+    them live: the capture cuts the learner graph once there, and every replay launches the
+    two eagerly between HIP events on the learner stream; their buffers live in the graph's
+    pool at fixed addresses)."""
     from .solver import td_huber_forward
 
     net = solver.q_network
@@ -115,6 +116,7 @@ def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None, mid=No
         packed = net.pack_convs()
         st = stream_ptr()
         ys, h = [], x
+        probed = []  # [(tag, launch)] of conv2 / conv3, handed to probe together
         for li, (conv, shape) in enumerate(zip(convs, shapes)):
             last = li == len(convs) - 1  # writes NCHW: FC1 reads the (C, H, W) flatten order
             ho = (shape.hin - shape.kh) // shape.stride + 1
@@ -125,8 +127,10 @@ def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None, mid=No
                        b=conv.bias, y=y):
                 call("rth_conv_bias_relu", ctypes.byref(shape), ptr(h), None, n, ptr(pk), ptr(b), ptr(y), stream_ptr())
 
-            if probe is not None and li == 1:
-                probe("conv2", launch)  # the prober issues it: now, or at every replay of a captured pass
+            if probe is not None and li in (1, 2):
+                probed.append((f"conv{li + 1}", launch))
+                if li == min(2, len(convs) - 1):  # one cut for both: the prober issues them, in order
+                    probe(probed)
             else:
                 launch()
             ys.append(y)

@@ -8,10 +8,10 @@ WRITE_SIZE passes), writes
     profiles/TAG_kernel_stats.csv        rocprofv3's own --stats table
     profiles/TAG_steady_state.txt        per-iteration kernel breakdown (timed window)
     profiles/TAG_gather_launches.txt     the learner gather's launches by grid (avg duration)
-    profiles/TAG_conv2_launches.txt      conv2 forward launches by grid (the dominant kernel)
+    profiles/TAG_conv{2,3}_launches.txt  conv2 / conv3 forward launches by grid (conv3: the dominant kernel)
     profiles/TAG_pmc.txt                 FETCH/WRITE per kernel and grid, gfx950-corrected
     profiles/traffic_TAG.json            HBM bytes per launch of the learner gather and of the learner's
-                                         conv2 (bench.py cites it)
+                                         conv2 / conv3 (bench.py cites it)
 FETCH_SIZE on gfx950 reports half the bytes of a wide coalesced read (MI355X_MICROARCH.md
 §HBM): it is doubled; WRITE_SIZE is exact for 16-byte stores.  Both are in KiB.
 """
@@ -29,7 +29,8 @@ PROF = os.path.join(ROOT, "profiles")
 # learner gather launch (k_copy_rows flat grid): B rows x 2 frame columns x 7 chunks of 4 KiB
 # + the small columns one lane per 4-byte word, 256 threads per workgroup
 LEARNER_GATHER_GRID = (512 * 2 * 7 + 4 + 2 + 2) * 256  # a: 2 words/row, r and done: 1 word/row, 256 lanes/WG
-CONV2 = "k_conv_bias_relu<0, 4, 4, 2, 32, 64, 20, 20"  # conv2 forward (the step's dominant kernel)
+CONV2 = "k_conv_bias_relu<0, 4, 4, 2, 32, 64, 20, 20"  # conv2 forward
+CONV3 = "k_conv_bias_relu<0, 3, 3, 1, 64, 64, 9, 9"  # conv3 forward (the step's dominant kernel)
 
 
 def main():
@@ -65,6 +66,8 @@ def main():
         for name, fn, head in (
                 ("k_copy_rows", "gather_launches", "# (512*256, 5) = learner gather (rth_replay_gather, B=512, 5 columns)"),
                 (CONV2, "conv2_launches", "# learner stream = the learner's [s0; s1] forward (2B = 1024 samples; "
+                                          "bench.py's live roofline_conv2); the actor stream: target pass (512), actors (256)"),
+                (CONV3, "conv3_launches", "# learner stream = the learner's [s0; s1] forward (2B = 1024 samples; "
                                           "bench.py's live roofline); the actor stream: target pass (512), actors (256)")):
             by_grid = collections.defaultdict(list)
             for r in win:
@@ -103,13 +106,15 @@ def main():
             out.update({"gather_kernel": "rth::k_copy_rows (learner gather, B=512, 5 columns)",
                         "gather_hbm_bytes_per_launch": round((2 * st.median(fe[key]) + st.median(wr[key])) * 1024),
                         "gather_dispatches": len(fe[key])})
-        c2 = [k for k in fe if CONV2 in k[0] and k in wr]
-        if c2:
-            key = max(c2, key=lambda k: k[1])  # the learner's launch: the largest grid
-            out.update({"conv2_kernel": key[0] + " (the learner's [s0; s1] forward: the largest grid, "
-                                                 f"{key[1]} threads)",
-                        "conv2_learner_hbm_bytes_per_launch": round((2 * st.median(fe[key]) + st.median(wr[key])) * 1024),
-                        "conv2_dispatches": len(fe[key])})
+        for name, conv in (("conv2", CONV2), ("conv3", CONV3)):
+            cs = [k for k in fe if conv in k[0] and k in wr]
+            if cs:
+                key = max(cs, key=lambda k: k[1])  # the learner's launch: the largest grid
+                out.update({f"{name}_kernel": key[0] + " (the learner's [s0; s1] forward: the largest grid, "
+                                                       f"{key[1]} threads)",
+                            f"{name}_learner_hbm_bytes_per_launch":
+                                round((2 * st.median(fe[key]) + st.median(wr[key])) * 1024),
+                            f"{name}_dispatches": len(fe[key])})
         with open(os.path.join(PROF, f"traffic_{tag}.json"), "w") as f:
             json.dump(out, f, indent=1)
     print("wrote", sorted(os.listdir(PROF)))

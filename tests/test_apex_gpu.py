@@ -63,6 +63,41 @@ def test_graph_replay_matches_eager(dev):
         assert torch.equal(x, y)
 
 
+def test_probed_learner_graph_matches_unprobed(dev):
+    """the bench's probe (learner graph cut once, conv2 and conv3 issued between the parts,
+    each between conv_probe(tag) / conv_probe(tag + "_end")) changes no result: identical
+    replay state to the unprobed graph, and every learner replay reports both launches"""
+    from reth_amd.apex import ApexConfig, ApexDQN
+
+    def run(probe):
+        cfg = ApexConfig(n_actors=16, capacity=1024, batch_size=32, sample_start=64, learning_rate=0.0,
+                         p_done=0.05, seed=5, hip_graph=True, send_weights_interval=3,
+                         recv_weights_interval=4, update_target_interval=5, extra={"probe_conv2": probe})
+        ax = ApexDQN(cfg, device=dev)
+        tags = []
+        ax.conv_probe = tags.append
+        for _ in range(40):
+            ax.iteration()
+        torch.cuda.synchronize()
+        assert ax._graphs is not None
+        s, m, v = ax.replay.tree.export()
+        cols = ax.replay.gather(torch.arange(ax.replay.info()[0], device=dev))
+        out = [s.cpu(), m.cpu(), v.cpu()] + [c.cpu() for c in cols]
+        info, updates = ax.replay.info(), ax.updates
+        ax.close()
+        return out, info, tags, updates
+
+    a, ia, ta, _ = run(False)
+    b, ib, tb, updates = run(True)
+    assert ta == []
+    replays = len(tb) // 4
+    assert replays > 0 and tb == ["conv2", "conv2_end", "conv3", "conv3_end"] * replays
+    assert replays <= updates  # eager updates before the capture issue no probe
+    assert ia == ib
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+
+
 def test_graph_split_learner_applies_its_own_gradients(dev):
     """with a gradient all-reduce hook the learner is captured in parts cut at the gradient
     buckets (merged heads | convs | heads split + clip + Adam) per variant and batch parity;

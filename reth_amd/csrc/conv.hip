@@ -483,6 +483,9 @@ static ConvLaunch conv1_bf16x3_launch() {
 #ifndef CONV3_MB
 #define CONV3_MB 1
 #endif
+#ifndef CONV3_WAVES
+#define CONV3_WAVES 8
+#endif
 
 // the supported geometries (the Nature-DQN torso on 4 x 84 x 84 stacks)
 static bool find_conv(const rth_conv_shape &s, ConvLaunch *out, int *geom = nullptr) {
@@ -509,7 +512,7 @@ static bool find_conv(const rth_conv_shape &s, ConvLaunch *out, int *geom = null
     *out = l;
     if (geom) *geom = 2;
   } else if (is(RTH_CONV_F32_NHWC, 64, 9, 9, 64, 3, 3, 1)) {
-    static const ConvLaunch l = conv_launch<RTH_CONV_F32_NHWC, 3, 3, 1, 64, 64, 9, 9, 8, CONV3_MB>();
+    static const ConvLaunch l = conv_launch<RTH_CONV_F32_NHWC, 3, 3, 1, 64, 64, 9, 9, CONV3_WAVES, CONV3_MB>();
     *out = l;
     if (geom) *geom = 3;
   } else {

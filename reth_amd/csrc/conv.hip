@@ -72,7 +72,9 @@ struct ConvGeom {
   }
 };
 
-template <int MODE, int KH, int KW, int S, int CIN, int COUT, int HIN, int WIN, int WAVES, int MB>
+// NS > 1: a wave tile is TP pixels x COUT / NS channels (tile t = pixel tile t / NS, channel
+// part t % NS), for more, smaller tiles over the SIMDs; each output keeps its K order
+template <int MODE, int KH, int KW, int S, int CIN, int COUT, int HIN, int WIN, int WAVES, int MB, int NS = 1>
 __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__restrict__ x,
                                                               const int64_t *__restrict__ rows, int64_t n,
                                                               const int64_t *__restrict__ n_dev,
@@ -81,7 +83,8 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__res
                                                               float *__restrict__ y, int out_nchw) {
   using Gm = ConvGeom<MODE, KH, KW, S, CIN, COUT, HIN, WIN>;
   constexpr bool F32 = MODE == RTH_CONV_F32_NHWC;
-  constexpr int G = Gm::G, NB = Gm::NB, T = WAVES * 64;
+  constexpr int G = Gm::G, NB = Gm::NB, T = WAVES * 64, NBW = NB / NS;
+  static_assert(NB % NS == 0, "NS must divide COUT / 16");
   constexpr int TP = 16 * MB;                    // output pixels per wave tile
   constexpr int D = F32 ? Gm::prefetch(MB) : G;  // input chunks in flight per wave
   using Frag = typename std::conditional<F32, f32x4, uint32_t>::type;
@@ -93,7 +96,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__res
     const int64_t m = *n_dev;
     n = m < n ? (m > 0 ? m : 0) : n;
   }
-  const int64_t P = n * Gm::PIX, tiles = (P + TP - 1) / TP, tstride = (int64_t)gridDim.x * WAVES;
+  const int64_t P = n * Gm::PIX, tiles = (P + TP - 1) / TP * NS, tstride = (int64_t)gridDim.x * WAVES;
 
   // this lane's window origin in tile t, per M-block (tail lanes read a duplicate pixel)
   auto bases = [&](int64_t t, const uint8_t *(&out)[MB]) {
@@ -133,7 +136,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__res
   // the first tile's leading input chunks are requested before the weights are staged
   int64_t tile = slot;
   const uint8_t *cur[MB], *nxt[MB];
-  bases(tile < tiles ? tile : tiles - 1, cur);
+  bases((tile < tiles ? tile : tiles - 1) / NS, cur);
   Frag ar[D][MB];
 #pragma unroll
   for (int d = 0; d < D; ++d)
@@ -159,22 +162,30 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__res
   }
   __syncthreads();
 
-  float bl[NB];
+  float bl[NBW];
+  const int nb_first = NS == 1 ? 0 : (int)(tile % NS) * NBW;
 #pragma unroll
-  for (int nb = 0; nb < NB; ++nb) bl[nb] = bias[nb * 16 + mr];
+  for (int nb = 0; nb < NBW; ++nb) bl[nb] = bias[(nb_first + nb) * 16 + mr];
+  // this lane's B fragments, offset to the tile's channel part
   const f32x4 *wlane = wl + lane;
 
   for (; tile < tiles; tile += tstride) {
+    const int nb0 = NS == 1 ? 0 : (int)(tile % NS) * NBW;
+    if constexpr (NS > 1) {
+#pragma unroll
+      for (int nb = 0; nb < NBW; ++nb) bl[nb] = bias[(nb0 + nb) * 16 + mr];
+    }
+    const int64_t ptile = tile / NS;
     // the chunks past the end of this tile are the next tile's leading chunks
-    bases(tile + tstride < tiles ? tile + tstride : tile, nxt);
-    f32x4 acc[MB][NB];
+    bases((tile + tstride < tiles ? tile + tstride : tile) / NS, nxt);
+    f32x4 acc[MB][NBW];
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
-      for (int nb = 0; nb < NB; ++nb) acc[mb][nb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    f32x4 bcur[NB], bnxt[NB];  // B fragments, one chunk ahead
+      for (int nb = 0; nb < NBW; ++nb) acc[mb][nb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    f32x4 bcur[NBW], bnxt[NBW];  // B fragments, one chunk ahead
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb) bcur[nb] = wlane[nb * 64];
+    for (int nb = 0; nb < NBW; ++nb) bcur[nb] = wlane[(nb0 + nb) * 64];
 
 #pragma unroll 1
     for (int g0 = 0; g0 < G; g0 += D) {
@@ -183,8 +194,8 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__res
         const int g = g0 + d;
         const int gb = g + 1 < G ? g + 1 : G - 1;
 #pragma unroll
-        for (int nb = 0; nb < NB; ++nb) {
-          bnxt[nb] = wlane[(gb * NB + nb) * 64];
+        for (int nb = 0; nb < NBW; ++nb) {
+          bnxt[nb] = wlane[(gb * NB + nb0 + nb) * 64];
         }
         // keep the next chunk's B reads here, a whole chunk of MFMAs ahead of their use
         __builtin_amdgcn_sched_barrier(0);
@@ -196,7 +207,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__res
             if constexpr (F32) a = ar[d][mb][t];
             else a = (float)((ar[d][mb] >> (8 * t)) & 0xffu);
 #pragma unroll
-            for (int nb = 0; nb < NB; ++nb)
+            for (int nb = 0; nb < NBW; ++nb)
               acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bcur[nb][t], acc[mb][nb], 0, 0, 0);
           }
         const int ga = g + D;
@@ -204,7 +215,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__res
         for (int mb = 0; mb < MB; ++mb)
           ar[d][mb] = ld(ga < G ? cur[mb] + chunk_off(ga) : nxt[mb] + chunk_off(ga - G));
 #pragma unroll
-        for (int nb = 0; nb < NB; ++nb) bcur[nb] = bnxt[nb];
+        for (int nb = 0; nb < NBW; ++nb) bcur[nb] = bnxt[nb];
       }
     }
     // C/D: lane holds column mr of rows 4q .. 4q+3 of each M-block; y is NHWC, or NCHW when
@@ -213,16 +224,17 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__res
     for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int64_t po = tile * TP + mb * 16 + 4 * q + i;
+        const int64_t po = ptile * TP + mb * 16 + 4 * q + i;
         if (po < P) {
           if (out_nchw) {
             const int64_t b = po / Gm::PIX, pp = po - b * Gm::PIX;
 #pragma unroll
-            for (int nb = 0; nb < NB; ++nb)
-              y[(b * COUT + nb * 16 + mr) * Gm::PIX + pp] = relu_c(radd(acc[mb][nb][i], bl[nb]));
+            for (int nb = 0; nb < NBW; ++nb)
+              y[(b * COUT + (nb0 + nb) * 16 + mr) * Gm::PIX + pp] = relu_c(radd(acc[mb][nb][i], bl[nb]));
           } else {
 #pragma unroll
-            for (int nb = 0; nb < NB; ++nb) y[po * COUT + nb * 16 + mr] = relu_c(radd(acc[mb][nb][i], bl[nb]));
+            for (int nb = 0; nb < NBW; ++nb)
+              y[po * COUT + (nb0 + nb) * 16 + mr] = relu_c(radd(acc[mb][nb][i], bl[nb]));
           }
         }
       }
@@ -450,14 +462,15 @@ struct ConvLaunch {
   int per_cu;  // resident workgroups per CU (occupancy query, cached)
   int tile_px;  // output pixels per wave tile
   int bf16x3;   // k_conv1_u8_bf16x3 (conv1 on uint8 stacks, exact-split bf16 MFMA)
+  int nsplit;   // wave tiles per pixel tile (channel parts; 0 = 1)
 };
 
-template <int MODE, int KH, int KW, int S, int CIN, int COUT, int HIN, int WIN, int WAVES, int MB>
+template <int MODE, int KH, int KW, int S, int CIN, int COUT, int HIN, int WIN, int WAVES, int MB, int NS = 1>
 static ConvLaunch conv_launch() {
   using Gm = ConvGeom<MODE, KH, KW, S, CIN, COUT, HIN, WIN>;
-  ConvLaunch l{reinterpret_cast<const void *>(&k_conv_bias_relu<MODE, KH, KW, S, CIN, COUT, HIN, WIN, WAVES, MB>),
+  ConvLaunch l{reinterpret_cast<const void *>(&k_conv_bias_relu<MODE, KH, KW, S, CIN, COUT, HIN, WIN, WAVES, MB, NS>),
                reinterpret_cast<const void *>(&k_conv_pack<MODE, KH, KW, S, CIN, COUT, HIN, WIN>), WAVES,
-               Gm::LDS_F4 * 16, 0, 16 * MB, 0};
+               Gm::LDS_F4 * 16, 0, 16 * MB, 0, NS};
   int blocks = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, l.fn, WAVES * 64, 0) != hipSuccess || blocks < 1)
     blocks = 1;
@@ -486,6 +499,9 @@ static ConvLaunch conv1_bf16x3_launch() {
 #ifndef CONV3_WAVES
 #define CONV3_WAVES 8
 #endif
+#ifndef CONV3_NS
+#define CONV3_NS 1
+#endif
 
 // the supported geometries (the Nature-DQN torso on 4 x 84 x 84 stacks)
 static bool find_conv(const rth_conv_shape &s, ConvLaunch *out, int *geom = nullptr) {
@@ -512,7 +528,7 @@ static bool find_conv(const rth_conv_shape &s, ConvLaunch *out, int *geom = null
     *out = l;
     if (geom) *geom = 2;
   } else if (is(RTH_CONV_F32_NHWC, 64, 9, 9, 64, 3, 3, 1)) {
-    static const ConvLaunch l = conv_launch<RTH_CONV_F32_NHWC, 3, 3, 1, 64, 64, 9, 9, CONV3_WAVES, CONV3_MB>();
+    static const ConvLaunch l = conv_launch<RTH_CONV_F32_NHWC, 3, 3, 1, 64, 64, 9, 9, CONV3_WAVES, CONV3_MB, CONV3_NS>();
     *out = l;
     if (geom) *geom = 3;
   } else {
@@ -1137,7 +1153,7 @@ static int conv_bias_relu(const rth_conv_shape *shape, const void *x, const int6
               "rth_conv_bias_relu: misaligned buffer");
   if (n == 0) return RTH_OK;
   const int hout = (shape->hin - shape->kh) / shape->stride + 1, wout = (shape->win - shape->kw) / shape->stride + 1;
-  const int64_t tiles = (n * hout * wout + l.tile_px - 1) / l.tile_px;
+  const int64_t tiles = (n * hout * wout + l.tile_px - 1) / l.tile_px * (l.nsplit > 1 ? l.nsplit : 1);
   int64_t grid = (tiles + l.waves - 1) / l.waves;
   // persistent: at most wg_per_cu() workgroups per CU (each stages the weights once)
   const int cap = wg_per_cu();

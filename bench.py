@@ -43,12 +43,27 @@ STACK = 4 * 84 * 84
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 FP32_PEAK_TFLOPS = 157.3  # fp32-input MFMA (= the fp32 vector peak)
 BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA
-# BASELINE.json configs[1] (the metric's workload) and configs[2] (a scale case, not the bench line)
+# BASELINE.json configs[1] / configs[3] (the metric's workload at N = 1 / N > 1), the weak
+# replication of configs[1], and configs[2] (a scale case, not the bench line)
 WORKLOADS = {
-    "pong": dict(name="PongNoFrameskip-v4 Ape-X DQN (BASELINE configs[1])", actors=256, capacity=1_000_000, actions=6),
+    # configs[1] at N = 1; configs[3] at N > 1: the reference's apex-dqn deployment sharded over
+    # the node (test/apex-dqn/trainer.py:52-61: K replay shards of C // K; worker.py:83-99: the
+    # actors split over the nodes): 256 / N actors and 1 M / N rows per GPU, one data-parallel
+    # learner replica per GPU (RCCL gradient all-reduce), B = 512 per GPU (--faithful: a global
+    # 512).  Each learner update is paired with 256 env steps of its shard (actor_steps_per_update
+    # = N), the replay ratio configs[1] runs at, so per-GPU work per step is fixed: weak scaling.
+    "pong": dict(name="PongNoFrameskip-v4 Ape-X DQN (BASELINE configs[1])",
+                 name_node="Pong Ape-X sharded over {n} GPUs (BASELINE configs[3]: 256 actors and 1 M replay rows "
+                           "split over the node, data-parallel learner with an RCCL gradient all-reduce)",
+                 actors=256, capacity=1_000_000, actions=6, shard=True),
+    # configs[1] replicated on every GPU (256 actors and 1 M rows per GPU)
+    "pong-weak": dict(name="PongNoFrameskip-v4 Ape-X DQN, BASELINE configs[1] replicated per GPU (256 actors and "
+                           "1 M replay rows on every GPU, data-parallel learner)",
+                      actors=256, capacity=1_000_000, actions=6, shard=False),
     "breakout": dict(name="BreakoutNoFrameskip-v4 Ape-X (BASELINE configs[2]; full-row uint8 replay, no frame "
-                          "de-duplication)", actors=2048, capacity=4_000_000, actions=4),
+                          "de-duplication)", actors=2048, capacity=4_000_000, actions=4, shard=False),
 }
+WORKLOADS["pong-node"] = WORKLOADS["pong"]
 
 
 def gather_bytes_per_row(frames_u8=False):
@@ -126,6 +141,96 @@ def cpu_model():
 
 
 # ----------------------------------------------------------------------------- CPU baseline
+def usable_cores():
+    """(cores this job may run on, affinity count, cgroup quota in CPUs or None): the affinity
+    set capped by the cgroup's cpu.max quota (the GPU box grants a share of a larger host)"""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    use = aff if quota is None else max(1, min(aff, int(quota)))
+    return use, aff, quota
+
+
+def cpu_actor_worker(seconds, idx=None):
+    """one reference Ape-X actor process on one core (test/apex-dqn/worker.py:21-61 with
+    OMP_NUM_THREADS=1, :3): per env step RandomExploration.act (a batch-1 forward of the host
+    solver unless exploring; reth/reth/utils/exploration.py:26-31), a synthetic Pong frame (ALE is
+    absent), the f4/i8 casts, NStepAdder.push; per 64 rows calc_loss on the actor's copy
+    (dqn_solver.py:100-102) and Client.append's per-row serialize (client.py:27-35; the lz4 and
+    the ZMQ send are not included).  Prints env steps/s."""
+    torch.set_num_threads(1)
+    from reth_amd import pack
+    from reth_amd.host_buffer import HostNumpyBuffer
+    from reth_amd.nstep import NStepAdder
+    from reth_amd.solver import Box, DQNSolver, Discrete
+
+    idx = int(os.environ.get("RTH_CPU_ACTOR_IDX", "0")) if idx is None else idx
+    rng = np.random.default_rng(idx)
+    torch.manual_seed(0)
+    solver = DQNSolver(Box(0, 255, (4, 84, 84)), Discrete(6), gamma=0.99, clip_value=40, double_q=True, dueling=True,
+                       learning_rate=1e-4, adam_epsilon=1.5e-4, update_target_interval=100, device="cpu", n_step=3)
+    eps = 0.4 ** (1 + (idx % 256) / 255 * 7)
+    adder = NStepAdder(0.99, 3)
+    buf = HostNumpyBuffer(64, circular=False)
+    s0 = rng.integers(0, 256, (4, 84, 84), dtype=np.uint8)
+    steps, t0 = 0, time.perf_counter()
+    while True:
+        if rng.random() < eps:
+            a = int(rng.integers(0, 6))
+        else:
+            a = solver.act(s0)
+        s1 = np.concatenate([s0[1:], rng.integers(0, 256, (1, 84, 84), dtype=np.uint8)])
+        r, done = float(rng.random() < 0.02), bool(rng.random() < 1 / 2000)
+        row = adder.push(np.asarray(s0, dtype="f4"), np.asarray(a, dtype="i8"), np.asarray(r, dtype="f4"),
+                         np.asarray(s1, dtype="f4"), np.asarray(done, dtype="f4"))
+        s0 = s1
+        steps += 1
+        if row is not None:
+            buf.append(row)
+            if buf.size == buf.capacity:
+                loss = np.asarray(solver.calc_loss(buf.data), dtype="f4")
+                data = buf.data
+                rows = [pack.serialize([c[i, ...] for c in data]) for i in range(buf.size)]
+                pack.serialize([rows, loss])
+                buf.clear()
+        dt = time.perf_counter() - t0
+        if dt >= seconds:
+            break
+    print(json.dumps({"env_steps_per_sec": steps / dt, "steps": steps, "seconds": dt}), flush=True)
+
+
+def cpu_actor_baseline(procs, seconds=8.0):
+    """the reference's actor layout on the host: `procs` single-threaded actor processes
+    (cpu_actor_worker), started as child interpreters, run concurrently; aggregate env
+    steps/s"""
+    import subprocess
+
+    env = dict(os.environ, OMP_NUM_THREADS="1", MKL_NUM_THREADS="1")
+    kids = []
+    for i in range(procs):
+        e = dict(env, RTH_CPU_ACTOR_IDX=str(i * max(1, 256 // procs)))
+        kids.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), "--cpu-actor-worker", str(seconds)],
+                                     env=e, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True))
+    rates = []
+    for k in kids:
+        out, _ = k.communicate(timeout=seconds + 120)
+        for line in out.splitlines():
+            if line.startswith("{"):
+                rates.append(json.loads(line)["env_steps_per_sec"])
+    return {"value": round(float(np.sum(rates)), 1), "unit": "env-steps/s", "cores": procs, "kind": "port",
+            "processes_reporting": len(rates), "per_process_env_steps_per_sec": round(float(np.mean(rates)), 1)
+            if rates else None,
+            "sample": f"{procs} actor processes x {seconds:.0f} s, each the reference worker loop "
+                      "(test/apex-dqn/worker.py:37-61) at OMP_NUM_THREADS=1: batch-1 act on the host solver, "
+                      "NStepAdder, calc_loss + per-row serialize every 64 rows; synthetic env, no lz4 / ZMQ"}
+
+
 def cpu_baseline(n_actors=256, batch=512, capacity=1_000_000, ring=20000, iters=6, seed=0):
     """The same Ape-X step on the host: torch-CPU Q-net (all host threads the job owns),
     the oracle's C restatement for tree / PER / n-step / eps-greedy, numpy for the env and
@@ -135,7 +240,8 @@ def cpu_baseline(n_actors=256, batch=512, capacity=1_000_000, ring=20000, iters=
     from oracle import oracle as orc
     from reth_amd.model import DQNNetwork
 
-    torch.set_num_threads(min(16, len(os.sched_getaffinity(0))))
+    use, aff, quota = usable_cores()
+    torch.set_num_threads(use)
     cores = torch.get_num_threads()
     rng = np.random.default_rng(seed)
     torch.manual_seed(seed)
@@ -225,11 +331,177 @@ def cpu_baseline(n_actors=256, batch=512, capacity=1_000_000, ring=20000, iters=
         step(t)
     dt = time.perf_counter() - t0
     return {"value": round(n_actors * iters / dt, 2), "unit": "env-steps/s", "cores": cores, "kind": "port",
+            "affinity_cores": aff, "cgroup_cpu_quota": quota,
             "updates_per_sec": round(iters / dt, 3), "cpu_model": cpu_model(),
             "sample": f"{iters} Ape-X steps (256 actors x 1 env step + 1 B=512 update each), sum-tree of "
                       f"{capacity} slots (depth {int(np.ceil(np.log2(capacity + 1)))}), frame storage a ring of "
                       f"{ring} rows on the host, torch-CPU Q-net + oracle C tree/PER/n-step, "
                       f"{torch.get_num_threads()} threads, {dt:.1f} s"}
+
+
+# ----------------------------------------------------------------------------- HBM kernels
+class ReplayKernelTimer:
+    """live in-loop durations of the replay shard's launches (rth_replay_set_timing): before
+    every iteration a fresh pair of HIP events per kind is armed; the library records them on
+    the launch stream around the next launch of that kind (the append's row copy and tree
+    update, the PER sample, the gather)"""
+    KINDS = ("tree_update", "sample", "gather", "insert")
+
+    def __init__(self, replay):
+        self.h = replay._h
+        self.pairs = {k: [] for k in self.KINDS}
+        self._armed = None
+
+    def arm(self):
+        from reth_amd import _lib
+
+        fired = _lib.c_i32(0)
+        evs, cur = [], []
+        for _ in self.KINDS:
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()  # materialise the events; the library re-records them at the launch
+            b.record()
+            evs += [a.cuda_event, b.cuda_event]
+            cur.append((a, b))
+        _lib.call("rth_replay_set_timing", self.h, (_lib.c_vp * len(evs))(*evs), len(evs), _lib.ctypes.byref(fired))
+        self._collect(fired.value)
+        self._armed = cur
+
+    def stop(self):
+        from reth_amd import _lib
+
+        fired = _lib.c_i32(0)
+        _lib.call("rth_replay_set_timing", self.h, None, 0, _lib.ctypes.byref(fired))
+        self._collect(fired.value)
+        self._armed = None
+
+    def _collect(self, mask):
+        if self._armed is None:
+            return
+        for k, (name, pair) in enumerate(zip(self.KINDS, self._armed)):
+            if (mask >> (2 * k)) & 3 == 3:
+                self.pairs[name].append(pair)
+
+    def mean_us(self, name):
+        v = [a.elapsed_time(b) * 1e3 for a, b in self.pairs[name]]
+        return (float(np.mean(v)), len(v)) if v else (None, 0)
+
+
+def hbm_bytes(cfg, n_rows_per_append):
+    """algorithmic HBM bytes per launch of the HBM-bound kernels (DESIGN.md 'Kernels'):
+    each byte the operation must move once, at the data's storage width"""
+    D = int(np.ceil(np.log2(cfg.capacity + 1)))  # tree depth (SURVEY §8: 20 at 1 M)
+    B, N, A1 = cfg.batch_size, n_rows_per_append, cfg.num_actions + 1
+    keys = N + B  # the append's priorities + the deferred update_priorities of the last update
+    row = 2 * STACK + 8 + 4 + 4  # s0, s1 uint8 stacks + a, r, done
+    return {
+        # per key: the D-level path, each level one 64-B children-pair read + one 32-B node write
+        # (the 32-B {sum, val, min} record layout), + the key's index and priority
+        "k_tree_update_sub": keys * (D * 96 + 16),
+        # per target: D levels x (the left child's sum + the node's value, 16 B) + the leaf's
+        # priority, the index and the IS weight written
+        "k_tree_sample": B * (D * 16 + 8 + 8 + 8),
+        # read + write of every sampled row (uint8 stacks, the HIP torso reads them as they are)
+        # + the 5 index reads
+        "k_copy_rows (gather)": B * (2 * row + 5 * 8),
+        # the append's rows: each column row read from the actors' ring and written to its slot
+        "k_copy_rows (insert)": N * (2 * row + 5 * 8),
+        # per actor: the FrameStack shift (3 frames read, 4 written) + reward / done / handles /
+        # n-step state (~160 B)
+        "k_actor_tail": cfg.n_actors * (7 * 84 * 84 + 160),
+        # the 3 x B heads rows + a / r / done / isw, |td| out, h1 [B, 2H] read, gh written
+        "k_td_heads_backward": B * (3 * A1 * 4 + 8 + 4 + 4 + 8 + 4) + B * 512 * 8,
+    }
+
+
+def hbm_rooflines(ax, timer, tag):
+    """roofline_hbm: the HBM-bound kernels north_star names (tree insert / sample / priority
+    update, n-step + env (k_actor_tail), TD, gather, Adam) -- algorithmic bytes per launch /
+    in-loop launch duration.  Durations: live HIP events for the replay's eager launches; the
+    kernels inside the captured actor / learner graphs from the rocprofv3 kernel trace of
+    the same bench command (profiles/traffic_TAG.json 'inloop_us', scripts/summarize_profile.py)."""
+    cfg = ax.cfg
+    nparams = sum(p.numel() for p in ax.solver._params)
+    rows = cfg.n_actors  # one append of N rows per actor step (fused actor: the previous step's rows)
+    by = hbm_bytes(cfg, rows)
+    by["k_adam"] = nparams * 28  # read p, g, m, v; write p, m, v (fp32)
+    live = {"k_tree_update_sub": "tree_update", "k_tree_sample": "sample", "k_copy_rows (gather)": "gather",
+            "k_copy_rows (insert)": "insert"}
+    prof = {}
+    full = os.path.join(ROOT, "profiles", f"traffic_{tag}.json")
+    if os.path.exists(full):
+        with open(full) as f:
+            prof = json.load(f)
+    out = []
+    for name, nbytes in by.items():
+        if name in live:
+            us, n = timer.mean_us(live[name])
+            src = f"live HIP events (rth_replay_set_timing), {n} launches"
+        else:
+            us = prof.get("inloop_us", {}).get(name)
+            n = None
+            src = f"rocprofv3 kernel trace of the bench (profiles/traffic_{tag}.json inloop_us)" if us else None
+        traffic = prof.get("hbm_bytes_per_launch", {}).get(name)
+        ent = {"kernel": name, "bound": "hbm", "bytes_per_launch": int(nbytes), "mean_launch_us": None,
+               "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None, "traffic": traffic,
+               "traffic_ratio": round(traffic / nbytes, 3) if traffic else None, "time_source": src}
+        if us:
+            gbs = nbytes / (us * 1e-6) / 1e9
+            ent.update(mean_launch_us=round(us, 2), achieved=round(gbs, 1), frac=round(gbs / HBM_PEAK_GBS, 4))
+        out.append(ent)
+    return out
+
+
+# ----------------------------------------------------------------------------- decoupled actors
+def decoupled_actors(ax, dev, world, iters=40, sweep=(1, 4, 16)):
+    """after the timed region: (1) the actor block alone, learner idle -- the vectorised
+    actors' own capacity (env steps + n-step + priorities + appends); (2) the coupled loop at
+    actor_steps_per_update in `sweep`.  Ape-X decouples actors from the learner (the reference's
+    workers never wait for the trainer), so the headline's fixed 1:1 pairing of one actor step
+    per update is a choice of replay ratio; these say what other ratios give.  Every rank runs
+    the same iterations (the learner all-reduces); times are max over ranks."""
+    import torch.distributed as dist
+
+    def timed(fn, n):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            fn()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([dt], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t)
+        return dt
+
+    keep = ax.cfg.actor_steps_per_update
+    out = {}
+    ax.cfg.actor_steps_per_update = 1
+    for _ in range(3):
+        ax.actor_iteration()
+    e0 = ax.env_steps
+    dt = timed(ax.actor_iteration, iters)
+    out["actor_only_env_steps_per_sec"] = round((ax.env_steps - e0) * world / dt, 1)
+    out["actor_only_ms_per_actor_step"] = round(dt / iters * 1e3, 4)
+    out["sweep"] = []
+    for k in sweep:
+        ax.cfg.actor_steps_per_update = k
+        for _ in range(2):
+            ax.iteration()
+        u0, e0 = ax.updates, ax.env_steps
+        n = max(4, iters // k)
+        dt = timed(ax.iteration, n)
+        out["sweep"].append({"actor_steps_per_update": k, "env_steps_per_sec": round((ax.env_steps - e0) * world / dt, 1),
+                             "learner_updates_per_sec": round((ax.updates - u0) * world / dt, 2),
+                             "ms_per_step": round(dt / n * 1e3, 4)})
+    ax.cfg.actor_steps_per_update = keep
+    out["note"] = ("measured after the timed region on the same process: actor_only = the captured actor block "
+                   "replayed with the learner stream idle; sweep = the coupled loop at other actor:learner ratios "
+                   "(the headline runs actor_steps_per_update = config.actor_steps_per_update)")
+    return out
 
 
 # ----------------------------------------------------------------------------- main
@@ -239,8 +511,9 @@ def main():
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="pong",
-                    help="pong = BASELINE configs[1] (the metric's workload); breakout = configs[2] (2048 actors, "
-                         "4 M replay, A = 4: 225.9 GB of full-row uint8 storage)")
+                    help="pong (= pong-node) = BASELINE configs[1] at N = 1, configs[3] at N > 1 (256 actors and "
+                         "1 M rows sharded over the N GPUs); pong-weak = configs[1] on every GPU; breakout = "
+                         "configs[2] (2048 actors, 4 M replay, A = 4: 225.9 GB of full-row uint8 storage)")
     ap.add_argument("--actors", type=int, default=None)
     ap.add_argument("--capacity", type=int, default=None)
     ap.add_argument("--batch", type=int, default=512)
@@ -250,19 +523,31 @@ def main():
     ap.add_argument("--windows", type=int, default=5, help="sub-windows of the timed region reported beside it")
     ap.add_argument("--no-probe", action="store_true", help="do not cut the learner graph around conv2/conv3 "
                     "(no live per-launch timing of the dominant kernels)")
-    ap.add_argument("--actor-steps-per-update", type=int, default=1)
+    ap.add_argument("--actor-steps-per-update", type=int, default=None,
+                    help="vectorised actor steps per learner update (default 1; N for the sharded pong workload)")
+    ap.add_argument("--no-sweep", action="store_true", help="skip the decoupled-actor measurements after the "
+                    "timed region (actor block alone; actor_steps_per_update 1 / 4 / 16)")
+    ap.add_argument("--cpu-actor-worker", type=float, default=None, help=argparse.SUPPRESS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-iters", type=int, default=72)
-    ap.add_argument("--tag", default="r02", help="profiles/traffic_TAG.json: the PMC pass the traffic fields cite")
+    ap.add_argument("--tag", default="r03", help="profiles/traffic_TAG.json: the PMC pass the traffic fields cite")
     ap.add_argument("--nchw", action="store_true", help="contiguous NCHW Q-net tensors (default channels-last)")
     ap.add_argument("--no-conv-benchmark", action="store_true", help="MIOpen immediate mode instead of find")
     ap.add_argument("--eager", action="store_true", help="no HIP-graph replay (launch every kernel from Python)")
     ap.add_argument("--miopen-conv", action="store_true", help="conv torso forward in MIOpen (+ rth_bias_relu) "
                     "instead of rth_conv_bias_relu")
     args = ap.parse_args()
+    if args.cpu_actor_worker is not None:  # a child of cpu_actor_baseline (never touches the GPU)
+        return cpu_actor_worker(args.cpu_actor_worker)
     wl = WORKLOADS[args.workload]
-    args.actors = wl["actors"] if args.actors is None else args.actors
-    args.capacity = wl["capacity"] if args.capacity is None else args.capacity
+    shard = wl["shard"] and args.gpus > 1
+    if shard and (wl["actors"] % args.gpus or wl["capacity"] % args.gpus):
+        raise SystemExit(f"--workload {args.workload}: {wl['actors']} actors / {wl['capacity']} rows do not split "
+                         f"over {args.gpus} GPUs")
+    args.actors = (wl["actors"] // args.gpus if shard else wl["actors"]) if args.actors is None else args.actors
+    args.capacity = (wl["capacity"] // args.gpus if shard else wl["capacity"]) if args.capacity is None else args.capacity
+    if args.actor_steps_per_update is None:
+        args.actor_steps_per_update = args.gpus if shard else 1
 
     from reth_amd.apex import ApexConfig, ApexDQN
     from reth_amd.dist import init_from_env
@@ -304,14 +589,6 @@ def main():
     for _ in range(args.warmup):
         ax.iteration()
 
-    events = []
-
-    def timer():
-        e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-        events.append(e)
-        return e
-
-    ax.loader.gather_timer = timer
     # the dominant kernels, live: events on the learner stream around its conv2 and conv3
     # launches (the learner graph is cut there: ApexDQN._learner_replay calls conv_probe
     # between parts)
@@ -365,16 +642,19 @@ def main():
     win_ev = []
     t0 = time.perf_counter()
     debug = os.environ.get("RTH_BENCH_DEBUG")
+    ktimer = ReplayKernelTimer(ax.replay)
     for k in range(args.steps):
         if k in win_at:
             e = torch.cuda.Event(enable_timing=True)
             e.record(ax._stream if hasattr(ax, "_stream") else None)
             win_ev.append((k, e))
+        ktimer.arm()
         ax.iteration()
         if debug:
             torch.cuda.synchronize()
             print(f"rank {rank} step {k}: {1e3 * (time.perf_counter() - t0):.1f} ms graphs={ax._graphs is not None} "
                   f"updates={ax.updates} pending={ax.loader.pending()}", file=sys.stderr, flush=True)
+    ktimer.stop()
     e = torch.cuda.Event(enable_timing=True)
     e.record(ax._stream)
     win_ev.append((args.steps, e))
@@ -382,7 +662,6 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    ax.loader.gather_timer = None
     ax.conv_probe = None
     n_upd, n_env = ax.updates - u0, ax.env_steps - e0
     if world > 1:
@@ -414,7 +693,7 @@ def main():
         allh = [torch.empty_like(mine) for _ in range(world)]
         dist.all_gather(allh, mine)
         replicas = all(torch.equal(allh[0], h) for h in allh[1:])
-    gather_ms = [a.elapsed_time(b) for a, b in events]
+    gather_ms = [a.elapsed_time(b) for a, b in ktimer.pairs["gather"]]
     mean_gather_s = float(np.mean(gather_ms)) / 1e3
     bytes_launch = gather_bytes_per_row(cfg.hip_conv and cfg.channels_last) * cfg.batch_size
     achieved = bytes_launch / mean_gather_s / 1e9
@@ -431,6 +710,9 @@ def main():
     torch.cuda.synchronize()
     iso_s = float(np.median([a.elapsed_time(b) for a, b in iso[5:]])) / 1e3
     conv1 = conv1_roofline(ax, slot_cols) if cfg.hip_conv and cfg.channels_last else None
+    decoupled = None
+    if not args.no_sweep and ax._graphs is not None:
+        decoupled = decoupled_actors(ax, dev, world)
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
@@ -438,6 +720,7 @@ def main():
     cpu = None
     if not args.no_cpu_baseline and world == 1:
         cpu = cpu_baseline(n_actors=cfg.n_actors, batch=cfg.batch_size, iters=args.cpu_iters)
+        cpu["reference_actor_layout"] = cpu_actor_baseline(usable_cores()[0])
     f = qnet_flops_per_sample(cfg.num_actions)
     flops_update = 5 * cfg.batch_size * f  # online fwd on s0 + s1, target fwd on s1, bwd (~2 fwd)
     # actors: the acting stacks (N) -- the rows' heads come from the per-stack cache
@@ -498,7 +781,13 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (Philox uint8 Pong-shaped frames, random-init Q-net; no ALE/checkpoints on the box)",
-        "config": {"workload": wl["name"], "actors_per_gpu": cfg.n_actors, "num_actions": cfg.num_actions,
+        "config": {"workload": (wl["name_node"].format(n=world) if shard else wl["name"]),
+                   "baseline_config": ("configs[3]" if shard else {"pong": "configs[1]", "pong-node": "configs[1]",
+                                                                   "pong-weak": "configs[1]" if world == 1 else
+                                                                   "configs[1] x N (weak)",
+                                                                   "breakout": "configs[2]"}[args.workload]),
+                   "actors_per_gpu": cfg.n_actors, "actors_total": cfg.n_actors * world,
+                   "replay_capacity_total": cfg.capacity * world, "num_actions": cfg.num_actions,
                    "replay_capacity_per_gpu": cfg.capacity, "replay_prefilled": True, "batch_size": cfg.batch_size,
                    "n_step": cfg.n_step, "alpha": cfg.alpha, "beta": cfg.beta,
                    "actor_steps_per_update": cfg.actor_steps_per_update,
@@ -507,7 +796,8 @@ def main():
                    "global_batch": cfg.batch_size * world,
                    "batch_mode": "hyperparameter-faithful (global batch split over the learners)" if args.faithful
                                  else "throughput (B per GPU)",
-                   "parallelism": f"dp{world} learner (RCCL grad all-reduce) + {world} replay shards"},
+                   "parallelism": (f"dp{world} learner (RCCL grad all-reduce) + {world} replay shards" if world > 1
+                                   else "one GPU: actors, replay shard and learner")},
         "dist": {"world": world, "backend": backend, "rccl": backend == "nccl",
                  "replicas_identical": replicas} if world > 1 else None,
         "roofline": roofline,
@@ -517,6 +807,8 @@ def main():
                       "achieved_tflops": round(flops_step / step_s / 1e12, 2),
                       "peak_fp32_tflops": FP32_PEAK_TFLOPS},
         "roofline_conv1": conv1,
+        "roofline_hbm": hbm_rooflines(ax, ktimer, args.tag),
+        "decoupled_actors": decoupled,
         "cpu_baseline": cpu,
     }
     print(json.dumps(out), flush=True)

@@ -197,6 +197,22 @@ int rth_replay_info(const rth_replay *h, int64_t *size, int64_t *tail, int64_t *
 int rth_uniform_indices(int64_t size, int64_t batch, const double *uniforms_dev, uint64_t seed, uint64_t counter,
                         const int64_t *counter_dev, int64_t *idx_out_dev, void *stream);
 rth_sumtree *rth_replay_tree(rth_replay *h);
+/* Live per-kernel timing (the bench's in-loop HBM rooflines; no reference counterpart):
+ * events[2k] / events[2k+1] (hipEvent_t, nullable) are recorded on the launch stream right
+ * before / after the next launch of kind k of this handle, once, then disarmed:
+ *   RTH_TIMING_TREE_UPDATE  the append's tree launch (k_tree_update_sub: the append's
+ *                           priorities + a deferred update_priorities)
+ *   RTH_TIMING_SAMPLE       the PER sample (k_tree_sample + IS weights)
+ *   RTH_TIMING_GATHER       the gather (k_copy_rows into the learner batch)
+ *   RTH_TIMING_INSERT       the append's row copy (k_copy_rows into the FIFO slots)
+ * n = number of events given (<= RTH_TIMING_SLOTS); n = 0 disarms all.  fired_out (nullable)
+ * receives the bit mask of the slots whose events were recorded since the previous call. */
+#define RTH_TIMING_TREE_UPDATE 0
+#define RTH_TIMING_SAMPLE 2
+#define RTH_TIMING_GATHER 4
+#define RTH_TIMING_INSERT 6
+#define RTH_TIMING_SLOTS 8
+int rth_replay_set_timing(rth_replay *h, void *const *events, int32_t n, int32_t *fired_out);
 /* device pointer of column c's storage ([capacity, row] of in_dtype) */
 void *rth_replay_column(rth_replay *h, int32_t c);
 
@@ -516,6 +532,10 @@ int rth_weights_destroy(rth_weights *h);
 int64_t rth_weights_bytes(const rth_weights *h);
 /* SendSocket.send: copy the n segments into the slot, then version += 1 (stream order) */
 int rth_weights_publish(rth_weights *h, int32_t n, const void *const *src_dev, const int64_t *bytes, void *stream);
+/* the slot's initial contents without a message (version unchanged): what a subscriber that
+ * connects before the first send holds -- the reference's SUB socket delivers nothing until
+ * the trainer's first send (test/apex-dqn/trainer.py:38-41) */
+int rth_weights_fill(rth_weights *h, int32_t n, const void *const *src_dev, const int64_t *bytes, void *stream);
 /* RecvSocket.empty + recv, decided on the device: if version > *seen_dev (and, with a step
  * counter, *step_dev - *prev_dev > interval) copy the slot into the n segments, set
  * *seen_dev = version, *prev_dev = *step_dev and *loaded_dev = 1; else *loaded_dev = 0.

@@ -106,6 +106,7 @@ SIGNATURES = {
                                 ctypes.POINTER(c_i64)]),
     "rth_uniform_indices": (c_i32, [c_i64, c_i64, c_vp, c_u64, c_u64, c_vp, c_vp, c_vp]),
     "rth_replay_tree": (c_vp, [c_vp]),
+    "rth_replay_set_timing": (c_i32, [c_vp, ctypes.POINTER(c_vp), c_i32, ctypes.POINTER(c_i32)]),
     "rth_replay_column": (c_vp, [c_vp, c_i32]),
     "rth_copy_rows": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i32, c_i32, c_vp]),
     # actors
@@ -169,6 +170,7 @@ SIGNATURES = {
     "rth_weights_destroy": (c_i32, [c_vp]),
     "rth_weights_bytes": (c_i64, [c_vp]),
     "rth_weights_publish": (c_i32, [c_vp, c_i32, ctypes.POINTER(c_vp), ctypes.POINTER(c_i64), c_vp]),
+    "rth_weights_fill": (c_i32, [c_vp, c_i32, ctypes.POINTER(c_vp), ctypes.POINTER(c_i64), c_vp]),
     "rth_weights_acquire": (c_i32, [c_vp, c_i32, ctypes.POINTER(c_vp), ctypes.POINTER(c_i64), c_vp, c_vp, c_vp, c_i64,
                                     c_vp, c_vp]),
     "rth_weights_version": (c_i32, [c_vp, ctypes.POINTER(c_i64)]),

@@ -106,7 +106,7 @@ class ApexDQN:
         for net in (self.actor_net, self.solver.q_network, self.solver.target_q_network):
             net.hip_conv = bool(cfg.hip_conv)
         self.slot = WeightsSlot(self.solver.q_network)
-        self.slot.acquire(self.actor_net)
+        self.slot.copy_out(self.actor_net)  # the actors start from the learner's initial weights
         self.subscriber = WeightsSubscriber(self.slot, cfg.recv_weights_interval)
         self.actors = VecActors(cfg.n_actors, cfg.num_actions, cfg.n_step, cfg.gamma, self.device,
                                 seed=cfg.seed * 1000003 + rank, actor_offset=rank * cfg.n_actors,
@@ -129,6 +129,10 @@ class ApexDQN:
     def close(self):
         _SERVICES.pop(self.addr, None)
         self._graphs = None
+        if self.cfg.tuned_gemm:
+            from . import gemm_tuning
+
+            gemm_tuning.restore()
 
     # ------------------------------------------------------------------ replay prefill
     @torch.no_grad()
@@ -376,6 +380,17 @@ class ApexDQN:
             else:
                 act.append(self.replay, td)
             self.env_steps += act.N
+
+    def actor_iteration(self):
+        """the actor block alone (learner idle): `actor_steps_per_update` vectorised actor
+        steps with their appends -- the decoupled actors' capacity (Ape-X runs actors and
+        learner independently; worker.py:21-61 never waits for the trainer).  Graph mode only."""
+        if self._graphs is None:
+            raise RuntimeError("actor_iteration replays the captured actor graphs: run iteration() until captured")
+        with torch.cuda.stream(self._stream):
+            if hasattr(self, "_ev_learn"):
+                self._stream.wait_event(self._ev_learn)
+            self._actor_block_graph()
 
     def _next_learner_variant(self):
         """graph key of the next replayed learner step: (full | pre, batch slot)"""

@@ -536,14 +536,17 @@ __global__ __launch_bounds__(kHbThreads) void k_td_heads_backward(
 // workgroup): lane l takes columns [l H/16, (l+1) H/16) of each half, all of its h loads
 // issued at once, the weights staged in LDS once per workgroup; the A+1 partial dots are
 // summed across the 16 lanes by four xor shuffles in a fixed order.  [n, A+1], row stride A+1.
-constexpr int kFc2MaxH = 512, kFc2MaxLds = 8 * kFc2MaxH;  // (A+1) * H floats staged, A+1 <= 8
+// The staged weights take (A+1) * H * 4 bytes of dynamic LDS: <= 16 KB for Atari's minimal
+// action sets (A + 1 <= 8, the k_heads_fc2<8> build), <= 66 KB for the full 18-action set and
+// anything up to kMaxActions (k_heads_fc2<kHbMaxA1>).
+constexpr int kFc2MaxH = 512;
 template <int MAXA1>
 __global__ __launch_bounds__(256) void k_heads_fc2(const float *__restrict__ h, int64_t ldh, int64_t n, int H, int A,
                                                    const float *__restrict__ wa2, const float *__restrict__ wv2,
                                                    const float *__restrict__ ba2, const float *__restrict__ bv2,
                                                    float *__restrict__ heads) {
   constexpr int U = kFc2MaxH / 16 / 4;  // float4 per lane and half, at most
-  __shared__ float4 wl[kFc2MaxLds / 4];  // rows a < A: wa2[a], row A: wv2
+  extern __shared__ float4 wl[];         // rows a < A: wa2[a], row A: wv2
   const int l = threadIdx.x & 15;
   const int64_t r = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
   const int64_t rr = r < n ? r : n - 1;  // tail rows: a duplicate, nothing written
@@ -803,10 +806,16 @@ int rth_heads_fc2(const float *h, int64_t ldh, int64_t n, int32_t H, int32_t A, 
               "rth_heads_fc2: bad shape n=%lld H=%d A=%d ldh=%lld (H a multiple of 16, h 16-byte aligned rows)",
               (long long)n, H, A, (long long)ldh);
   if (n == 0) return RTH_OK;
-  RTH_REQUIRE(A + 1 <= 8 && H <= kFc2MaxH && H % 64 == 0,
-              "rth_heads_fc2: built for A + 1 <= 8 actions and H <= %d, a multiple of 64 (A=%d H=%d)", kFc2MaxH, A, H);
-  hipLaunchKernelGGL((k_heads_fc2<8>), dim3((unsigned)((n + 15) / 16)), dim3(256), 0, as_stream(stream), h, ldh, n,
-                     (int)H, (int)A, fc2_params[0], fc2_params[1], fc2_params[2], fc2_params[3], heads);
+  RTH_REQUIRE(H <= kFc2MaxH && H % 64 == 0,
+              "rth_heads_fc2: built for H <= %d, a multiple of 64 (A=%d H=%d)", kFc2MaxH, A, H);
+  const dim3 grid((unsigned)((n + 15) / 16)), block(256);
+  const size_t lds = (size_t)(A + 1) * H * 4;
+  if (A + 1 <= 8)
+    hipLaunchKernelGGL((k_heads_fc2<8>), grid, block, lds, as_stream(stream), h, ldh, n, (int)H, (int)A, fc2_params[0],
+                       fc2_params[1], fc2_params[2], fc2_params[3], heads);
+  else
+    hipLaunchKernelGGL((k_heads_fc2<kHbMaxA1>), grid, block, lds, as_stream(stream), h, ldh, n, (int)H, (int)A,
+                       fc2_params[0], fc2_params[1], fc2_params[2], fc2_params[3], heads);
   RTH_LAUNCHED();
   return RTH_OK;
 }

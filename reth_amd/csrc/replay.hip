@@ -445,9 +445,23 @@ struct rth_replay {
   UpdPending pend;  // a deferred PER update, applied by the next tree launch
   int has_pend;
   // sample calls whose st->calls advance is still owed: a sample without out_cols leaves it to
-  // the gather that follows (rth_replay_gather), or to the next sample when none does
+  // the gather that follows (rth_replay_gather), or to the next sample when none does; the
+  // advance is stream-ordered after the sample that owes it (owed_stream)
   int64_t calls_owed;
+  hipStream_t owed_stream;
+  // rth_replay_set_timing: one-shot events recorded around the next launches of each kind
+  hipEvent_t timing[RTH_TIMING_SLOTS];
+  int32_t timing_fired;  // bit k: slot k's event was recorded since the last arm
 };
+
+// record the one-shot timing event of slot k (if armed) on stream s
+static void timing_mark(rth_replay *h, int k, hipStream_t s) {
+  if (h->timing[k]) {
+    (void)hipEventRecord(h->timing[k], s);
+    h->timing[k] = nullptr;
+    h->timing_fired |= 1 << k;
+  }
+}
 
 static int bump(rth_replay *h, int64_t dtail, int64_t dcalls, int64_t dstep, hipStream_t s);
 
@@ -593,6 +607,14 @@ int rth_replay_destroy(rth_replay *h) {
   return RTH_OK;
 }
 
+int rth_replay_set_timing(rth_replay *h, void *const *events, int32_t n, int32_t *fired_out) {
+  RTH_REQUIRE(h && (n == 0 || events) && n >= 0 && n <= RTH_TIMING_SLOTS, "rth_replay_set_timing: bad arguments");
+  if (fired_out) *fired_out = h->timing_fired;
+  h->timing_fired = 0;
+  for (int k = 0; k < RTH_TIMING_SLOTS; ++k) h->timing[k] = k < n ? static_cast<hipEvent_t>(events[k]) : nullptr;
+  return RTH_OK;
+}
+
 rth_sumtree *rth_replay_tree(rth_replay *h) { return h ? h->tree : nullptr; }
 
 void *rth_replay_column(rth_replay *h, int32_t c) {
@@ -641,7 +663,9 @@ int rth_replay_append(rth_replay *h, const rth_src *srcs, const void *td_abs, in
   a.dst_fifo = 1;
   a.st = h->st;
   a.fifo_cap = h->cap;
+  timing_mark(h, RTH_TIMING_INSERT, s);
   int rc = launch_copy(a, s);
+  timing_mark(h, RTH_TIMING_INSERT + 1, s);
   if (rc) return rc;
   if (idx_out) {  // FIFO slots for the caller (the append_loop's `indices`)
     hipLaunchKernelGGL(k_fifo_slots, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, idx_out, n, h->st, h->cap);
@@ -650,8 +674,10 @@ int rth_replay_append(rth_replay *h, const rth_src *srcs, const void *td_abs, in
   if (h->kind == RTH_SAMPLER_PER) {
     // one tree launch: a deferred update_priorities (if any), this append's priorities,
     // then the FIFO tail advance -- the sequential order of the reference's messages
+    timing_mark(h, RTH_TIMING_TREE_UPDATE, s);
     rc = tree_update_impl(h->tree, nullptr, 0, nullptr, td_abs, td_dtype, 0.0, n, s, h->st, &h->alpha,
                           h->has_pend ? &h->pend : nullptr, 1);
+    timing_mark(h, RTH_TIMING_TREE_UPDATE + 1, s);
     h->has_pend = 0;
     if (rc) return rc;
   } else {
@@ -681,12 +707,20 @@ static int gather_impl(rth_replay *h, const int64_t *idx, int64_t n, void *const
   a.ncols = h->ncols;
   const int64_t owed = h->calls_owed;
   h->calls_owed = 0;
-  if (n == 0) return owed ? bump(h, 0, owed, 0, s) : RTH_OK;
-  if (owed) {  // the gather's first lane advances the counter: no launch of its own
+  if (owed && (n == 0 || s != h->owed_stream)) {
+    // on the sample's own stream, behind the sample kernel that reads the counter (a gather
+    // on another stream could otherwise advance it first)
+    int rc = bump(h, 0, owed, 0, h->owed_stream);
+    if (rc || n == 0) return rc;
+  } else if (owed) {  // same stream: the gather's first lane advances the counter, no launch
     a.bump_st = h->st;
     a.bump_calls = owed;
   }
-  return launch_copy(a, s);
+  if (n == 0) return RTH_OK;
+  timing_mark(h, RTH_TIMING_GATHER, s);
+  const int rc = launch_copy(a, s);
+  timing_mark(h, RTH_TIMING_GATHER + 1, s);
+  return rc;
 }
 
 int rth_replay_gather(rth_replay *h, const int64_t *idx, int64_t n, void *const *out_cols, void *stream) {
@@ -700,12 +734,21 @@ int rth_replay_sample(rth_replay *h, int64_t batch, const double *uniforms, void
   int rc = flush_pending(h, s);
   if (rc) return rc;
   if (h->calls_owed) {  // the previous sample was not followed by a gather: its seed advance first
-    rc = bump(h, 0, h->calls_owed, 0, s);
+    rc = bump(h, 0, h->calls_owed, 0, h->owed_stream);
     h->calls_owed = 0;
     if (rc) return rc;
+    if (h->owed_stream != s) {  // this sample reads the counter: order it behind that bump
+      hipEvent_t e;
+      RTH_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      RTH_HIP(hipEventRecord(e, h->owed_stream));
+      RTH_HIP(hipStreamWaitEvent(s, e, 0));
+      (void)hipEventDestroy(e);
+    }
   }
   if (h->kind == RTH_SAMPLER_PER) {
+    timing_mark(h, RTH_TIMING_SAMPLE, s);
     rc = tree_sample_impl(h->tree, batch, uniforms, h->seed, 0, 1, 0.0, idx_out, isw_out, s, h->st, &h->beta);
+    timing_mark(h, RTH_TIMING_SAMPLE + 1, s);
   } else if (h->kind == RTH_SAMPLER_UNIFORM) {
     RTH_REQUIRE(h->slen > 0, "rth_replay_sample: uniform sampler is empty (np.random.choice(0, ...))");
     hipLaunchKernelGGL(k_uniform_sample, dim3((unsigned)((batch + 255) / 256)), dim3(256), 0, s, h->ulist, h->ss, h->st,
@@ -722,6 +765,7 @@ int rth_replay_sample(rth_replay *h, int64_t batch, const double *uniforms, void
   if (rc) return rc;
   h->sample_calls++;
   h->calls_owed = 1;  // advanced by the gather (this one, or the caller's rth_replay_gather next)
+  h->owed_stream = s;
   return out_cols ? gather_impl(h, idx_out, batch, out_cols, s) : RTH_OK;
 }
 

@@ -126,7 +126,8 @@ int rth_weights_destroy(rth_weights *h) {
   return RTH_OK;
 }
 
-int rth_weights_publish(rth_weights *h, int32_t n, const void *const *src, const int64_t *bytes, void *stream) {
+static int weights_put(rth_weights *h, int32_t n, const void *const *src, const int64_t *bytes, void *stream,
+                       int bump) {
   RTH_REQUIRE(h, "rth_weights_publish: NULL handle");
   WSegs s;
   int rc = make_segs(h, n, const_cast<void *const *>(src), bytes, &s);
@@ -134,9 +135,18 @@ int rth_weights_publish(rth_weights *h, int32_t n, const void *const *src, const
   hipStream_t st = as_stream(stream);
   hipLaunchKernelGGL(k_weights_copy, dim3(copy_grid(s.off[n])), dim3(kWThreads), 0, st, s, h->slot, 0, nullptr);
   RTH_LAUNCHED();
+  if (!bump) return RTH_OK;
   hipLaunchKernelGGL(k_weights_bump, dim3(1), dim3(64), 0, st, h->ver);
   RTH_LAUNCHED();
   return RTH_OK;
+}
+
+int rth_weights_publish(rth_weights *h, int32_t n, const void *const *src, const int64_t *bytes, void *stream) {
+  return weights_put(h, n, src, bytes, stream, 1);
+}
+
+int rth_weights_fill(rth_weights *h, int32_t n, const void *const *src, const int64_t *bytes, void *stream) {
+  return weights_put(h, n, src, bytes, stream, 0);
 }
 
 int rth_weights_acquire(rth_weights *h, int32_t n, void *const *dst, const int64_t *bytes, int64_t *seen_dev,

@@ -68,6 +68,36 @@ class DQNNetwork(nn.Module):
             self._tie_heads()
         return out
 
+    def _tie_check(self):
+        """re-tie FC1 when something replaced the branch parameters' storage (copy.deepcopy,
+        load_state_dict(assign=True), vector_to_parameters): the fast path multiplies by
+        _w1s / _b1s, which must be the storage the two parameters are views of"""
+        if not self.dueling:
+            return
+        a0, v0 = self.fc_adv[0], self.fc_value[0]
+        w, b = self.__dict__.get("_w1s"), self.__dict__.get("_b1s")
+        H = a0.weight.shape[0]
+        ok = (w is not None and b is not None and a0.weight.data_ptr() == w.data_ptr()
+              and v0.weight.data_ptr() == w[H:].data_ptr() and a0.bias.data_ptr() == b.data_ptr()
+              and v0.bias.data_ptr() == b[H:].data_ptr() and w.device == a0.weight.device)
+        if not ok:
+            self._tie_heads()
+
+    def __deepcopy__(self, memo):
+        """deepcopy clones every Parameter into its own storage: re-tie FC1 in the copy (the
+        cached head / packed weights are per-object state and are not carried over)"""
+        import copy
+
+        new = self.__class__.__new__(self.__class__)
+        memo[id(self)] = new
+        skip = ("_w1s", "_b1s", "_frozen", "_frozen_packed", "_ws", "_shape_cache")
+        for k, v in self.__dict__.items():
+            if k not in skip:
+                new.__dict__[k] = copy.deepcopy(v, memo)
+        if new.dueling:
+            new._tie_heads()
+        return new
+
     def forward(self, x):
         x = self.features(x).flatten(1)
         if not self.dueling:
@@ -102,6 +132,7 @@ class DQNNetwork(nn.Module):
                 return _MergeHeads.apply((H, ps[0].shape[1], A, 0, 1), *ps)
             w1, b1 = torch.cat([a0.weight, v0.weight]), torch.cat([a0.bias, v0.bias])
         else:
+            self._tie_check()
             w1, b1 = self._w1s, self._b1s
             if ps[0].is_cuda and self._fc2_inplace():
                 return w1, b1, None, None
@@ -111,10 +142,10 @@ class DQNNetwork(nn.Module):
         return w1, b1, w2, b2
 
     def _fc2_inplace(self):
-        """rth_heads_fc2's built shapes: A + 1 <= 8 actions (Atari's minimal sets: Pong 6,
-        Breakout 4, BeamRider 9 is not), H a multiple of 64 up to 512"""
+        """rth_heads_fc2's built shapes: up to 32 actions (every Atari action set: Pong 6,
+        Breakout 4, BeamRider 9, the full 18), H a multiple of 64 up to 512"""
         A, H = self.fc_adv[2].weight.shape
-        return A + 1 <= 8 and H % 64 == 0 and H <= 512
+        return A <= 32 and H % 64 == 0 and H <= 512
 
     def _heads_fc2(self, h):
         """the second layer on h = relu(FC1) [n, 2H] from the branch parameters in place
@@ -130,11 +161,21 @@ class DQNNetwork(nn.Module):
 
     @torch.no_grad()
     def freeze_heads(self):
-        """(re)build the cached packed conv weights in place (stable storage for graph
-        replay): for copies whose parameters change only at refresh points (target sync,
-        actor weight reload).  The heads need nothing: FC1 is the tied parameter storage and
-        the second layer is read from its parameters in place."""
-        self._frozen = list(self._merged_head_weights())
+        """(re)build the cached head weights and packed conv weights IN PLACE (stable storage
+        for graph replay): for copies whose parameters change only at refresh points (target
+        sync, actor weight reload).  FC1 is the tied parameter storage and, where
+        rth_heads_fc2 is built, the second layer is read from its parameters in place; the
+        merged second layer of other shapes is rebuilt into the tensors the first freeze
+        allocated, whose addresses captured graphs hold."""
+        self._tie_check()
+        merged = list(self._merged_head_weights())
+        old = getattr(self, "_frozen", None)
+        if old is not None:
+            for k in (2, 3):
+                if old[k] is not None and merged[k] is not None and old[k].shape == merged[k].shape:
+                    old[k].copy_(merged[k])
+                    merged[k] = old[k]
+        self._frozen = merged
         if self.hwc_features and self._frozen[0].is_cuda:
             self._frozen_packed = self.pack_convs(out=getattr(self, "_frozen_packed", None))
 

@@ -49,8 +49,13 @@ class WeightsSlot:
         self._h = h
         self.nbytes = nbytes
         self.version = 0  # host mirror of the device counter (publishes of this process)
-        self.publish(module)
-        self.version = 0
+        # the construction snapshot fills the slot without a message (device version 0, like the
+        # mirror): subscribers see nothing newer until the first publish (a SUB socket
+        # receives nothing before the trainer's first send)
+        params = [p.detach() for p in module.parameters()]
+        self._check(params)
+        n, ptrs, nbytes = _segments(params)
+        call("rth_weights_fill", self._h, n, ptrs, nbytes, stream_ptr())
         self._seen = torch.zeros((), dtype=torch.int64, device=self.device)  # acquire() consumers
 
     def __del__(self):
@@ -83,6 +88,13 @@ class WeightsSlot:
         if getattr(module, "dueling", False) and hasattr(module, "freeze_heads"):
             module.freeze_heads()  # the actor's cached merged heads follow its parameters
         return self.version
+
+    @torch.no_grad()
+    def copy_out(self, module):
+        """the slot's current contents into `module` unconditionally (no version gate): the
+        actors' starting weights = the learner's initial ones, before any message"""
+        force = torch.full((), -1, dtype=torch.int64, device=self.device)
+        self.acquire(module, seen=force)
 
     def _check(self, params):
         if [(tuple(p.shape), p.stride()) for p in params] != self.layout:

@@ -28,14 +28,28 @@ OUT = os.path.join(ROOT, "gpurun_out")
 PROF = os.path.join(ROOT, "profiles")
 # learner gather launch (k_copy_rows flat grid): B rows x 2 frame columns x 7 chunks of 4 KiB
 # + the small columns one lane per 4-byte word, 256 threads per workgroup
-LEARNER_GATHER_GRID = (512 * 2 * 7 + 4 + 2 + 2) * 256  # a: 2 words/row, r and done: 1 word/row, 256 lanes/WG
+def copy_grid(rows):
+    """k_copy_rows' grid (threads) for `rows` apex rows: 2 frame columns x 7 chunks of 4 KiB per
+    row + the small columns' workgroups (rows / 64), 256 lanes each"""
+    return (rows * 14 + rows // 64) * 256
+
+
+LEARNER_GATHER_GRID = copy_grid(512)
+# the HBM-bound kernels of bench.py's roofline_hbm: name -> (kernel-name match, grid or None)
+HBM_KERNELS = {"k_tree_update_sub": ("k_tree_update_sub", None), "k_tree_sample": ("k_tree_sample", None),
+               "k_copy_rows (gather)": ("k_copy_rows", "gather"), "k_copy_rows (insert)": ("k_copy_rows", "insert"),
+               "k_actor_tail": ("k_actor_tail", None), "k_td_heads_backward": ("k_td_heads_backward", None),
+               "k_adam": ("k_adam", None)}
 CONV2 = "k_conv_bias_relu<0, 4, 4, 2, 32, 64, 20, 20"  # conv2 forward
 CONV3 = "k_conv_bias_relu<0, 3, 3, 1, 64, 64, 9, 9"  # conv3 forward (the step's dominant kernel)
 
 
 def main():
     tag = sys.argv[1]
-    steps = int(sys.argv[sys.argv.index("--steps") + 1]) if "--steps" in sys.argv else 100
+    arg = lambda k, d: int(sys.argv[sys.argv.index(k) + 1]) if k in sys.argv else d
+    steps = arg("--steps", 100)
+    grids = {"gather": copy_grid(arg("--batch", 512)), "insert": copy_grid(arg("--actors", 256))}
+    inloop = {}
     os.makedirs(PROF, exist_ok=True)
     stats = os.path.join(OUT, "prof", "run_kernel_stats.csv")
     if os.path.exists(stats):
@@ -63,6 +77,11 @@ def main():
             f.write(f"{'share':>7} {'us/iter':>9} {'calls/iter':>10}  kernel\n")
             for k, v in sorted(agg.items(), key=lambda kv: -kv[1][0]):
                 f.write(f"{v[0] / busy * 100:6.2f}% {v[0] / 1e3 / steps:9.2f} {v[1] / steps:10.2f}  {k}\n")
+        for name, (match, g) in HBM_KERNELS.items():  # in-loop mean launch durations (bench.py roofline_hbm)
+            d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in win if match in r["Kernel_Name"]
+                 and (g is None or int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) == grids[g])]
+            if d:
+                inloop[name] = round(st.mean(d) / 1e3, 3)
         for name, fn, head in (
                 ("k_copy_rows", "gather_launches", "# (512*256, 5) = learner gather (rth_replay_gather, B=512, 5 columns)"),
                 (CONV2, "conv2_launches", "# learner stream = the learner's [s0; s1] forward (2B = 1024 samples; "
@@ -115,6 +134,24 @@ def main():
                             f"{name}_learner_hbm_bytes_per_launch":
                                 round((2 * st.median(fe[key]) + st.median(wr[key])) * 1024),
                             f"{name}_dispatches": len(fe[key])})
+        hbm = {}
+        for name, (match, g) in HBM_KERNELS.items():
+            cs = [k for k in fe if match in k[0] and k in wr and (g is None or k[1] == grids[g])]
+            if g is None and len(cs) > 1:  # the loop's launch: the grid with the most dispatches
+                cs = [max(cs, key=lambda k: len(fe[k]))]
+            if len(cs) == 1:
+                k = cs[0]
+                hbm[name] = round((2 * st.median(fe[k]) + st.median(wr[k])) * 1024)
+        out["hbm_bytes_per_launch"] = hbm
+    if inloop or os.path.exists(pf):
+        if not (os.path.exists(pf) and os.path.exists(pw)):
+            out = {}
+            old = os.path.join(PROF, f"traffic_{tag}.json")
+            if os.path.exists(old):
+                out = json.load(open(old))
+        if inloop:
+            out["inloop_us"] = inloop
+            out["inloop_source"] = "rocprofv3 --kernel-trace of bench.py (gpurun_out/prof), mean over the timed window"
         with open(os.path.join(PROF, f"traffic_{tag}.json"), "w") as f:
             json.dump(out, f, indent=1)
     print("wrote", sorted(os.listdir(PROF)))

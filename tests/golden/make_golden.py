@@ -399,6 +399,41 @@ def gen_dqn(R):
     np.savez_compressed(os.path.join(OUT, "dqn_cartpole_b64.npz"), **out)
 
 
+def gen_dqn_full(R):
+    """the apex learner's own batch sizes: B = 512, A = 6 (Pong, test/apex-dqn/config.yaml:2)
+    and B = 64, A = 9 (the reference config's BeamRider, config.yaml:8).  Two reference
+    updates (dqn_solver.py:104-124) on one batch; the FULL state_dict after each, stored as
+    float16 deltas from the seeded initial weights (|delta| <= ~3e-4 after two Adam steps of
+    lr 1e-4, so the float16 rounding is <= 1.5e-7, well under the tests' 2e-6), plus every
+    |td| returned.  The frames come from tests/golden/dqn_batch.py (seed -> SHA-256 here)."""
+    import torch
+
+    sys.path.insert(0, OUT)
+    from dqn_batch import apex_batch, frames_sha
+
+    torch.set_num_threads(8)
+    gym = R.gym
+    for B, A, tag in ((512, 6, "pong_b512"), (64, 9, "beamrider_b64")):
+        seed = 4242 + B + A
+        torch.manual_seed(seed)
+        solver = R.dqn_solver.DQNSolver(gym.spaces.Box(0, 255, (4, 84, 84)), gym.spaces.Discrete(A), gamma=0.99,
+                                        clip_value=40, double_q=True, dueling=True, learning_rate=1e-4,
+                                        adam_epsilon=1.5e-4, update_target_interval=100, device="cpu", n_step=3)
+        s0, s1, a, r, done, isw = apex_batch(seed, B, A)
+        batch = [s0.astype("f4"), a, r, s1.astype("f4"), done]
+        init = {k: v.detach().clone() for k, v in solver.q_network.state_dict().items()}
+        out = dict(seed=np.int64(seed), B=np.int64(B), A=np.int64(A), frames_sha=np.array(frames_sha(s0, s1)),
+                   a=a, r=r, done=done, isw=isw, param_names=np.array(list(init)))
+        out["init_sum"] = np.array([float(v.double().sum()) for v in init.values()])
+        for k in range(2):
+            out[f"upd{k}_abs_td"] = solver.update(batch, weights=isw).numpy()
+            for name, v in solver.q_network.state_dict().items():
+                d = (v.detach().double() - init[name].double()).numpy()
+                assert np.abs(d).max() < 6e-4, (name, np.abs(d).max())
+                out[f"upd{k}/{name}"] = d.astype(np.float16)
+        np.savez_compressed(os.path.join(OUT, f"dqn_{tag}.npz"), **out)
+
+
 # ----------------------------------------------------------------------------- samplers / buffers
 def _load_buffers(R):
     """reth.buffer (NumpyBuffer, PrioritizedBuffer with its own NumbaSumTree) and the

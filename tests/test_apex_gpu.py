@@ -171,14 +171,17 @@ def test_graph_replay_learns(dev):
     ax.close()
 
 
-def test_target_pass_precompute_respects_target_syncs(dev):
+@pytest.mark.parametrize("A", [6, 9, 18])
+def test_target_pass_precompute_respects_target_syncs(dev, A):
     """overlapped graph mode computes the next batch's target pass on the actor stream
     ("pre" learner graphs) except right after a target sync, where the learner computes it
-    itself ("full"); a precomputed pass equals the target network's output on that batch"""
+    itself ("full"); a precomputed pass equals the target network's output on that batch.
+    A = 9 is the reference's Ape-X config (BeamRider, test/apex-dqn/config.yaml:8), 18 the
+    full Atari set: the captured target / actor graphs must read the synced weights"""
     from reth_amd.apex import ApexConfig, ApexDQN
 
     cfg = ApexConfig(n_actors=16, capacity=1024, batch_size=32, sample_start=64, seed=5, hip_graph=True,
-                     update_target_interval=4)
+                     update_target_interval=4, num_actions=A, send_weights_interval=3, recv_weights_interval=4)
     ax = ApexDQN(cfg, device=dev)
     while ax._graphs is None:
         ax.iteration()
@@ -197,6 +200,15 @@ def test_target_pass_precompute_respects_target_syncs(dev):
     for (_, synced), (v_next, _) in zip(log, log[1:]):
         if synced:
             assert v_next == "full"
+    # the actors' frozen heads / packed convs (what the captured actor graphs read) follow the
+    # reloaded parameters
+    assert ax.subscriber.loaded_version > 0 and int(ax.actors.action.max()) < A
+    an = ax.actor_net
+    x = ax.actors.frames[:8]
+    with torch.no_grad():
+        got = an.forward_heads(x)
+        want = an.forward_heads(x, merged=an._merged_head_weights(), packed=an.pack_convs())
+    assert torch.equal(got, want)
     ax.close()
 
 

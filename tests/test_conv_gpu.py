@@ -211,9 +211,11 @@ def test_pack_many_matches_single_packs(dev):
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("n", [1, 7, 40])
+@pytest.mark.parametrize("n", [1, 7, 40, 512, 1024])
 def test_conv1_relu_wgrad_u8(dev, n):
-    """rth_conv_relu_wgrad against a float64 CPU autograd of relu(conv2d(x, w) + b)"""
+    """rth_conv_relu_wgrad against a float64 CPU autograd of relu(conv2d(x, w) + b); n = 512
+    is the learner's batch (the bench's launch: split partials over every workgroup + the
+    reduce), 1024 the [s0; s1] size"""
     from reth_amd import _lib
 
     g = torch.Generator().manual_seed(100 + n)

@@ -214,11 +214,11 @@ def test_heads_backward_branch_form_equals_merged(dev, B, A, fused):
         assert torch.equal(x, y)
 
 
-@pytest.mark.parametrize("n,A", [(1, 6), (260, 6), (1024, 4), (33, 7)])
+@pytest.mark.parametrize("n,A", [(1, 6), (260, 6), (1024, 4), (33, 7), (64, 9), (300, 18), (17, 32)])
 def test_heads_fc2_forward(dev, n, A):
     """rth_heads_fc2 (the second layer from the branch parameters) == the block-diagonal
-    addmm within fp32 summation error, against an fp64 reference; more than 7 actions are
-    refused (the model then builds the merged second layer)"""
+    addmm within fp32 summation error, against an fp64 reference, for every action count up
+    to kMaxActions = 32 (BeamRider's 9, the full Atari set's 18); more are refused"""
     from reth_amd import _lib
     from reth_amd._lib import call, ptr, stream_ptr
 
@@ -234,7 +234,7 @@ def test_heads_fc2_forward(dev, n, A):
     want = torch.cat([hd[:, :H] @ ps[0].double().t() + ps[2].double(), hd[:, H:] @ ps[1].double().t() + ps[3].double()],
                      1)
     torch.testing.assert_close(out.double(), want, rtol=1e-5, atol=1e-5)
-    big = [torch.zeros(9, H, device=dev), ps[1], torch.zeros(9, device=dev), ps[3]]
+    big = [torch.zeros(33, H, device=dev), ps[1], torch.zeros(33, device=dev), ps[3]]
     with pytest.raises(_lib.RethHipError):
-        call("rth_heads_fc2", ptr(h), 2 * H, n, H, 9, (_lib.c_vp * 4)(*[p.data_ptr() for p in big]), ptr(out),
+        call("rth_heads_fc2", ptr(h), 2 * H, n, H, 33, (_lib.c_vp * 4)(*[p.data_ptr() for p in big]), ptr(out),
              stream_ptr())

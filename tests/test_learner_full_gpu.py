@@ -1,0 +1,92 @@
+"""The apex learner's own update at the reference's batch sizes, pinned by the reference.
+
+Golden: tests/golden/dqn_pong_b512.npz (B = 512, A = 6: BASELINE configs[1]'s learner,
+test/apex-dqn/config.yaml:2) and dqn_beamrider_b64.npz (B = 64, A = 9: the reference
+config's BeamRider, config.yaml:8), each two DQNSolver.update calls of the reference
+(reth/reth/algorithm/dqn/dqn_solver.py:104-124) on torch-CPU, with the FULL state_dict
+after each (tests/golden/make_golden.py gen_dqn_full).
+
+What runs here is exactly what the bench replays: an ApexDQN (HIP graphs, uint8 batch
+slots, the explicit gradient pass -- HIP conv forward, bf16x3 conv1 weight gradient from the
+stacks, HIP conv2 data gradient, deferred bias gradients, hipBLASLt FC1 on the committed
+TunableOp solutions, rth_clip_adam) is built with the reference's seed, run until its graphs
+are captured, then reset to the initial weights / zero Adam state; the golden batch is
+written into a learner batch slot and the captured learner graph is replayed twice.
+North-star tolerances: |td| within 1e-5, every parameter within 2e-6 (+ the fixture's
+float16 delta rounding, <= 1.5e-7)."""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+
+
+@pytest.mark.parametrize("name", ["dqn_pong_b512.npz", "dqn_beamrider_b64.npz"])
+def test_apex_learner_graph_vs_reference(golden, dev, name):
+    from dqn_batch import apex_batch, frames_sha
+
+    from reth_amd.apex import ApexConfig, ApexDQN
+
+    gd = golden(name)
+    B, A, seed = int(gd["B"]), int(gd["A"]), int(gd["seed"])
+    s0, s1, a, r, done, isw = apex_batch(seed, B, A)
+    assert frames_sha(s0, s1) == str(gd["frames_sha"])
+    for x, k in ((a, "a"), (r, "r"), (done, "done"), (isw, "isw")):
+        assert np.array_equal(x, gd[k])
+    cfg = ApexConfig(n_actors=16, num_actions=A, capacity=max(2048, 2 * B), batch_size=B, sample_start=B, seed=seed,
+                     hip_graph=True, update_target_interval=100, send_weights_interval=10 ** 6)
+    ax = ApexDQN(cfg, device=dev)
+    solver = ax.solver
+    names = [str(x) for x in gd["param_names"]]
+    sd = solver.q_network.state_dict()
+    assert list(sd) == names
+    init = {k: v.detach().clone() for k, v in sd.items()}
+    sums = np.array([float(v.double().cpu().contiguous().sum()) for v in init.values()])
+    np.testing.assert_allclose(sums, gd["init_sum"], rtol=1e-10, atol=1e-9)  # the reference's seeded init
+    ax.prefill(cfg.capacity)
+    for _ in range(6):
+        ax.iteration()
+    torch.cuda.synchronize()
+    G = ax._graphs
+    assert G is not None, "the learner graph was not captured"
+    # back to the reference's starting point: initial weights, target = online, fresh Adam
+    with torch.no_grad():
+        for k, v in solver.q_network.state_dict().items():
+            v.copy_(init[k])
+        solver.update_target()
+        opt = solver.optimizer
+        for st in opt.state.values():
+            st["exp_avg"].zero_()
+            st["exp_avg_sq"].zero_()
+        opt._step.zero_()
+        opt._ws.zero_()
+    p = 0
+    cols, idx, w = ax.loader._slots[p]
+    cols[0].copy_(torch.as_tensor(s0))
+    cols[3].copy_(torch.as_tensor(s1))
+    cols[1].copy_(torch.as_tensor(a))
+    cols[2].copy_(torch.as_tensor(r))
+    cols[4].copy_(torch.as_tensor(done))
+    w.copy_(torch.as_tensor(isw))
+    torch.cuda.synchronize()
+    v = ("full", p)  # the learner computes the target pass itself (as after a target sync)
+    stream = torch.cuda.Stream(dev)
+    for k in range(2):
+        with torch.cuda.stream(stream):
+            ax._learner_replay(v)
+        torch.cuda.synchronize()
+        td = G["learn_td"][v].cpu().numpy()
+        np.testing.assert_allclose(td, gd[f"upd{k}_abs_td"], rtol=1e-5, atol=1e-5)
+        worst = 0.0
+        for name, t in solver.q_network.state_dict().items():
+            want = init[name].double().cpu() + torch.as_tensor(gd[f"upd{k}/{name}"].astype(np.float64))
+            err = float((t.double().cpu() - want).abs().max())
+            worst = max(worst, err)
+            assert err <= 2e-6 + 1.5e-7, (k, name, err)
+        print(f"{name} update {k}: max |param - reference| = {worst:.2e}")
+    ax.close()

@@ -38,3 +38,42 @@ def test_non_dueling_head_shapes():
     net = DQNNetwork((4, 84, 84), 4, dueling=False)
     assert net(torch.zeros(2, 4, 84, 84)).shape == (2, 4)
     assert "fc.2.weight" in net.state_dict()
+
+
+def test_freeze_heads_refills_in_place():
+    """the merged second layer of a shape rth_heads_fc2 does not build (H not a multiple of
+    64) is refilled in the tensors the first freeze allocated: captured graphs keep reading
+    the current weights after a target sync / weights reload"""
+    net = DQNNetwork((4, 84, 84), 9, hidden_unit=48)
+    assert not net._fc2_inplace()
+    net.freeze_heads()
+    w2, b2 = net._frozen[2], net._frozen[3]
+    ptrs = (w2.data_ptr(), b2.data_ptr())
+    with torch.no_grad():
+        for p in net.parameters():
+            p.add_(0.5)
+    net.freeze_heads()
+    assert (net._frozen[2].data_ptr(), net._frozen[3].data_ptr()) == ptrs
+    A, H = 9, 48
+    assert torch.equal(net._frozen[2][:A, :H], net.fc_adv[2].weight)
+    assert torch.equal(net._frozen[2][A:, H:], net.fc_value[2].weight)
+    assert torch.equal(net._frozen[3], torch.cat([net.fc_adv[2].bias, net.fc_value[2].bias]))
+    assert net._frozen[0].data_ptr() == net.fc_adv[0].weight.data_ptr()  # FC1: the tied storage
+
+
+def test_tie_survives_deepcopy_and_assign():
+    """FC1's two branch parameters stay row slices of the storage the fast path multiplies by
+    after copy.deepcopy and load_state_dict(assign=True)"""
+    import copy
+
+    net = DQNNetwork((4, 84, 84), 6)
+    H = net.fc_adv[0].weight.shape[0]
+    twin = copy.deepcopy(net)
+    assert twin._w1s.data_ptr() == twin.fc_adv[0].weight.data_ptr() != net._w1s.data_ptr()
+    assert twin.fc_value[0].weight.data_ptr() == twin._w1s[H:].data_ptr()
+    sd = {k: v.clone() + 1 for k, v in net.state_dict().items()}
+    net.load_state_dict(sd, assign=True)
+    with torch.no_grad():
+        w1, b1, _, _ = net._merged_head_weights()
+    assert w1.data_ptr() == net.fc_adv[0].weight.data_ptr()
+    assert torch.equal(w1[:H], sd["fc_adv.0.weight"]) and torch.equal(b1[H:], sd["fc_value.0.bias"])

@@ -23,7 +23,7 @@ def test_latest_wins(dev):
 
     learner, actor = _net(dev, 0), _net(dev, 1)
     slot = WeightsSlot(learner)
-    assert slot.device_version() == 1 and slot.version == 0  # the initial content
+    assert slot.device_version() == 0 and slot.version == 0  # the initial content is no message
     snaps = []
     for k in range(3):  # three publishes, no acquire in between
         with torch.no_grad():
@@ -38,7 +38,7 @@ def test_latest_wins(dev):
     loaded = torch.full((), -1, dtype=torch.int32, device=dev)
     slot.acquire(actor, seen=seen, loaded=loaded)
     torch.cuda.synchronize()
-    assert int(loaded) == 1 and int(seen) == 4 and slot.device_version() == 4 and slot.version == 3
+    assert int(loaded) == 1 and int(seen) == 3 and slot.device_version() == 3 and slot.version == 3
     assert all(torch.equal(p, q) for p, q in zip(actor.parameters(), snaps[-1]))
     with torch.no_grad():
         for p in actor.parameters():
@@ -56,6 +56,10 @@ def test_interval_gate_on_device(dev):
     i64 = dict(dtype=torch.int64, device=dev)
     seen, step, prev = torch.zeros((), **i64), torch.zeros((), **i64), torch.zeros((), **i64)
     loaded = torch.zeros((), dtype=torch.int32, device=dev)
+    slot.acquire(actor, seen=seen, loaded=loaded)  # the construction snapshot is not a message
+    torch.cuda.synchronize()
+    assert int(loaded) == 0 and not _same(actor, learner)
+    slot.publish(learner)
     step.fill_(400)  # worker.py:38: strictly more than recv_weights_interval steps
     slot.acquire(actor, seen=seen, step=step, prev=prev, interval=400, loaded=loaded)
     torch.cuda.synchronize()
@@ -98,9 +102,10 @@ def test_acquire_replays_from_a_graph(dev):
         g.replay()
         torch.cuda.synchronize()
         hist.append(int(loaded))
-    # step 1, 2: gate closed (<= 2 since prev 0); step 3: load v1; step 6 (k=5): v2 published
-    # but only 3 > 2 steps since 3 -> load
-    assert hist == [0, 0, 1, 0, 0, 1, 0, 0]
+    # step 1, 2: gate closed (<= 2 since prev 0); step 3: the gate opens but nothing was
+    # published (the construction snapshot is no message); step 6 (k=5): v1 published, 6 > 2
+    # steps since prev 0 -> load; then nothing newer
+    assert hist == [0, 0, 0, 0, 0, 1, 0, 0]
     assert _same(actor, learner)
 
 

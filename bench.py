@@ -525,6 +525,10 @@ def main():
                     "(no live per-launch timing of the dominant kernels)")
     ap.add_argument("--actor-steps-per-update", type=int, default=None,
                     help="vectorised actor steps per learner update (default 1; N for the sharded pong workload)")
+    ap.add_argument("--env", choices=["synthetic", "atari", "atari-h2d"], default="synthetic",
+                    help="actors' observations: synthetic uint8 stacks (default); atari = raw 210x160 RGB frame pairs "
+                         "from device Philox through the device MaxAndSkip / gray / INTER_AREA / FrameStack; atari-h2d = "
+                         "the same with the raw pairs copied host -> device from pinned memory every step (host ALE)")
     ap.add_argument("--no-sweep", action="store_true", help="skip the decoupled-actor measurements after the "
                     "timed region (actor block alone; actor_steps_per_update 1 / 4 / 16)")
     ap.add_argument("--cpu-actor-worker", type=float, default=None, help=argparse.SUPPRESS)
@@ -581,7 +585,7 @@ def main():
     cfg = ApexConfig(n_actors=args.actors, capacity=args.capacity, batch_size=per_gpu_batch, num_actions=wl["actions"],
                      actor_steps_per_update=args.actor_steps_per_update, seed=0,
                      channels_last=not args.nchw, conv_benchmark=not args.no_conv_benchmark,
-                     hip_graph=not args.eager, hip_conv=hip_conv,
+                     hip_graph=not args.eager, hip_conv=hip_conv, env=args.env,
                      extra={"learner_priority": int(os.environ.get("RTH_LEARNER_PRIORITY", "0")),
                             "probe_conv2": probe})
     ax = ApexDQN(cfg, device=dev, rank=rank, world=world)
@@ -780,7 +784,11 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (Philox uint8 Pong-shaped frames, random-init Q-net; no ALE/checkpoints on the box)",
+        "data": ("synthetic (Philox uint8 Pong-shaped frames, random-init Q-net; no ALE/checkpoints on the box)"
+                 if args.env == "synthetic" else
+                 "synthetic raw 210x160x3 screens (Philox%s) through the device Atari preprocessing, random-init Q-net; "
+                 "no ALE/checkpoints on the box" % (", copied host -> device from pinned memory every step"
+                                                     if args.env == "atari-h2d" else " on the device")),
         "config": {"workload": (wl["name_node"].format(n=world) if shard else wl["name"]),
                    "baseline_config": ("configs[3]" if shard else {"pong": "configs[1]", "pong-node": "configs[1]",
                                                                    "pong-weak": "configs[1]" if world == 1 else
@@ -790,7 +798,7 @@ def main():
                    "replay_capacity_total": cfg.capacity * world, "num_actions": cfg.num_actions,
                    "replay_capacity_per_gpu": cfg.capacity, "replay_prefilled": True, "batch_size": cfg.batch_size,
                    "n_step": cfg.n_step, "alpha": cfg.alpha, "beta": cfg.beta,
-                   "actor_steps_per_update": cfg.actor_steps_per_update,
+                   "actor_steps_per_update": cfg.actor_steps_per_update, "env": cfg.env,
                    "qnet_layout": "channels_last" if cfg.channels_last else "nchw",
                    "conv_benchmark": cfg.conv_benchmark, "hip_graph": cfg.hip_graph, "hip_conv": cfg.hip_conv,
                    "global_batch": cfg.batch_size * world,

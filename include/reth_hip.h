@@ -290,6 +290,8 @@ typedef struct rth_actor_tail_args {
   int64_t N;
   float gamma_n, p_reward, p_done;
   int32_t ring, A;
+  int32_t ext_frames;      /* 1: the env step writes no frame bytes -- rth_atari_env_step fills the
+                            * step's stacks from raw frames right after (Atari env mode) */
 } rth_actor_tail_args;
 /* The fused actor step's first launch (reth_amd/actors.py step_fused): *t_dev += 1 (the
  * step counter rth_actor_tail's ε-greedy and env step read) and rows_out[i] = i * ring +
@@ -495,6 +497,17 @@ int rth_atari_destroy(rth_atari *h);
 int rth_atari_step(rth_atari *h, const uint8_t *raw_dev, int64_t n, uint8_t *frames_dev, int32_t ring, int32_t stack,
                    const int64_t *prev_slot_dev, const int64_t *new_slot_dev, const uint8_t *reset_dev,
                    uint8_t *out_frame_dev, void *stream);
+/* the Ape-X actors' Atari env mode (after rth_actor_tail with ext_frames = 1): per actor i the
+ * raw pair raw_dev[i] (MaxAndSkip max, gray, INTER_AREA) becomes the new top frame of stack
+ * s1_h[i] = stack s0_h[i] shifted by one (FrameStack.step), and where done_dev[i] != 0 also the
+ * reset observation, the frame `stack` times, in actor i's slot cur_slot_dev[i] (FrameStack
+ * reset, util.py:191-196).  Handles index frames_dev's stacks; slots are per-actor ring slots. */
+int rth_atari_env_step(rth_atari *h, const uint8_t *raw_dev, int64_t n, uint8_t *frames_dev, int32_t ring,
+                       int32_t stack, const int64_t *s0_h_dev, const int64_t *s1_h_dev, const float *done_dev,
+                       const int64_t *cur_slot_dev, void *stream);
+/* synthetic raw emulator screens (the stand-in for ALE's output, ALE being absent): nbytes of
+ * device Philox (seed, step *t_dev), 16-byte aligned and a multiple of 16 bytes */
+int rth_atari_synth_raw(uint8_t *raw_dev, int64_t nbytes, uint64_t seed, const int64_t *t_dev, void *stream);
 
 /* ------------------------------------------------------------------------------------
  * Learner optimizer step (reth/reth/algorithm/dqn/dqn_solver.py:118-121):

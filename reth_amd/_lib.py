@@ -70,7 +70,7 @@ class ActorTailArgs(ctypes.Structure):
                 ("prev_s0", c_vp), ("prev_a", c_vp), ("prev_s1", c_vp), ("prev_r", c_vp), ("prev_done", c_vp),
                 ("td_abs", c_vp), ("frames", c_vp), ("cur_slot", c_vp), ("r_out", c_vp), ("done_out", c_vp),
                 ("s0_h", c_vp), ("s1_h", c_vp), ("seed", c_u64), ("N", c_i64), ("gamma_n", c_f32),
-                ("p_reward", c_f32), ("p_done", c_f32), ("ring", c_i32), ("A", c_i32)]
+                ("p_reward", c_f32), ("p_done", c_f32), ("ring", c_i32), ("A", c_i32), ("ext_frames", c_i32)]
 
 # name -> (restype, argtypes); must match include/reth_hip.h exactly
 SIGNATURES = {
@@ -162,6 +162,8 @@ SIGNATURES = {
     "rth_atari_create": (c_i32, [c_i32, c_i32, c_i32, c_i32, c_i32, ctypes.POINTER(c_vp)]),
     "rth_atari_destroy": (c_i32, [c_vp]),
     "rth_atari_step": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "rth_atari_env_step": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "rth_atari_synth_raw": (c_i32, [c_vp, c_i64, c_u64, c_vp, c_vp]),
     "rth_clip_adam_workspace": (c_i64, []),
     "rth_debug_tree_timing": (c_i32, [c_vp]),
     "rth_clip_adam": (c_i32, [c_vp, c_i32, c_f64, c_f64, c_f64, c_f64, c_f64, c_vp, c_vp, c_vp, c_vp]),

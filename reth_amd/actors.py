@@ -45,7 +45,7 @@ def apex_epsilons(n, offset=0, total=None):
 class VecActors:
     def __init__(self, n_actors, num_actions, n_step=3, gamma=0.99, device=None, seed=0, eps=None,
                  actor_offset=0, total_actors=None, p_reward=0.02, p_done=1.0 / 2000, nstep_mode=0,
-                 channels_last=False):
+                 channels_last=False, env="synthetic"):
         self.N = int(n_actors)
         self.A = int(num_actions)
         self.n_step, self.gamma = int(n_step), float(gamma)
@@ -100,6 +100,22 @@ class VecActors:
         self.t_dev = torch.zeros(1, dtype=torch.int64, device=dev)  # what the kernels read
         self.pushes = 0
         call("rth_synth_env_reset", ptr(self.frames), N, ring, self.seed, ptr(self.cur_slot), stream_ptr())
+        # env: "synthetic" -- Pong-shaped uint8 frames straight from device Philox;
+        # "atari" -- raw 210x160 RGB frame pairs (device Philox, the stand-in for ALE's screens)
+        # through the MaxAndSkip / WarpFrame / FrameStack preprocessing (rth_atari_env_step)
+        # into the frame ring; "atari-h2d" -- the raw pairs copied host -> device from pinned
+        # memory every step first, as from host ALE emulators (reth/reth/env/util.py:121-209)
+        if env not in ("synthetic", "atari", "atari-h2d"):
+            raise ValueError(f"env {env!r}: synthetic | atari | atari-h2d")
+        self.env = env
+        if env != "synthetic":
+            from .atari import AtariPreprocessor
+
+            self.atari = AtariPreprocessor(device=dev)
+            self.raw = torch.empty((N, 2, 210, 160, 3), dtype=torch.uint8, device=dev)
+            if env == "atari-h2d":
+                g = np.random.default_rng(self.seed)
+                self.raw_host = torch.from_numpy(g.integers(0, 256, tuple(self.raw.shape), dtype=np.uint8)).pin_memory()
 
     def __del__(self):
         if getattr(self, "_nstep", None):
@@ -137,9 +153,23 @@ class VecActors:
             self._cur_h = torch.empty_like(self._base)
         return torch.add(self.cur_slot, self._base, out=self._cur_h)
 
+    def _atari_frames(self, s):
+        """Atari env mode, after the actor tail assigned the step's stack handles: this step's
+        raw frame pairs (device Philox, or the pinned host buffer copied over PCIe) through the
+        preprocessing into the ring"""
+        if self.env == "atari":
+            call("rth_atari_synth_raw", ptr(self.raw), self.raw.numel(), self.seed ^ 0x9E3779B97F4A7C15,
+                 ptr(self.t_dev), s)
+        else:
+            self.raw.copy_(self.raw_host, non_blocking=True)
+        call("rth_atari_env_step", self.atari._h, ptr(self.raw), self.N, ptr(self.frames), self.ring, OBS_SHAPE[0],
+             ptr(self.s0_h), ptr(self.s1_h), ptr(self.done), ptr(self.cur_slot), s)
+
     @torch.no_grad()
     def step(self, q_net):
         """one environment step for every actor; returns True when rows were emitted"""
+        if self.env != "synthetic":
+            raise RuntimeError("the Atari env mode runs in step_fused with the HIP torso actor network")
         s = stream_ptr()
         self.t += 1
         call("rth_counter_add", ptr(self.t_dev), 1, s)
@@ -233,15 +263,19 @@ class VecActors:
                                       ptr(prev.s0), ptr(prev.a), ptr(prev.s1), ptr(prev.r), ptr(prev.done),
                                       ptr(td_abs), ptr(self.frames), ptr(self.cur_slot), ptr(self.reward),
                                       ptr(self.done), ptr(self.s0_h), ptr(self.s1_h), self.seed, N, self.gamma_n,
-                                      self.p_reward, self.p_done, self.ring, self.A)
+                                      self.p_reward, self.p_done, self.ring, self.A, int(self.env != "synthetic"))
             call("rth_actor_tail", self._nstep, _lib.ctypes.byref(args), ptr(self.emit), ptr(cur.s0), ptr(cur.a),
                  ptr(cur.r), ptr(cur.s1), ptr(cur.done), s)
+            if self.env != "synthetic":
+                self._atari_frames(s)
             self._terminal_stacks()
             self.pushes += 1
             self.fresh += 1
             self._bind_rows(cur)
             return (td_abs, prev) if p > self.n_step else (None, None)
         else:
+            if self.env != "synthetic":
+                raise RuntimeError("the Atari env mode runs with the HIP torso actor network (dueling, channels-last)")
             call("rth_counter_add", ptr(self.t_dev), 1, s)
             torch.cat([self.current_obs_handles(), prev.s0, prev.s1], out=self.handles3)
             q, dueling = self._forward_stacks(q_net, self.handles3)

@@ -71,6 +71,7 @@ class ApexConfig:
     hip_conv: bool = True          # conv torso forward in rth_conv_bias_relu (actors/targets read uint8 stacks)
     dp_hook: Optional[bool] = None  # gradient all-reduce hook: None = when world > 1 (tests force it)
     tuned_gemm: bool = True        # TunableOp solution selection for the library GEMMs (reth_amd.gemm_tuning)
+    env: str = "synthetic"         # actors' observations: synthetic | atari | atari-h2d (VecActors)
     extra: dict = field(default_factory=dict)
 
 
@@ -111,7 +112,7 @@ class ApexDQN:
         self.actors = VecActors(cfg.n_actors, cfg.num_actions, cfg.n_step, cfg.gamma, self.device,
                                 seed=cfg.seed * 1000003 + rank, actor_offset=rank * cfg.n_actors,
                                 total_actors=cfg.n_actors * world, p_reward=cfg.p_reward, p_done=cfg.p_done,
-                                nstep_mode=cfg.nstep_mode, channels_last=cfg.channels_last)
+                                nstep_mode=cfg.nstep_mode, channels_last=cfg.channels_last, env=cfg.env)
         self.svc, self.addr = start_per(cfg.capacity, cfg.batch_size, alpha=cfg.alpha, beta=cfg.beta,
                                         sample_start=cfg.sample_start, device=self.device, seed=cfg.seed + 7919 * rank)
         u8 = bool(cfg.hip_conv and cfg.channels_last)

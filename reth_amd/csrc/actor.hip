@@ -123,9 +123,11 @@ struct EnvOut {
   int64_t s0h, s1h;
 };
 
+// write_frames = 0: the observation comes from outside (the Atari preprocessing of raw frames,
+// rth_atari_env_step, fills the two stacks this step assigns right after this launch)
 __device__ inline EnvOut env_step_one(uint8_t *frames, int ring, int64_t t, int64_t i, int64_t *cur_slot, uint64_t seed,
                                       float p_reward, float p_done, float *r_out, float *done_out, int64_t *s0_h,
-                                      int64_t *s1_h) {
+                                      int64_t *s1_h, int write_frames = 1) {
   const int64_t stack_bytes = 4 * kFrameBytes;
   // reward / done: one Philox block per (actor, t), identical in every lane
   const uint4 rd = env_bytes(seed, i, t, 2, 0);
@@ -137,7 +139,7 @@ __device__ inline EnvOut env_step_one(uint8_t *frames, int ring, int64_t t, int6
   const uint4 *src = reinterpret_cast<const uint4 *>(frames + (i * ring + cur) * stack_bytes);
   uint4 *dn = reinterpret_cast<uint4 *>(frames + (i * ring + nxt) * stack_bytes);
   uint4 *dr = reinterpret_cast<uint4 *>(frames + (i * ring + rst) * stack_bytes);
-  for (int v = threadIdx.x; v < kStackVec; v += kEnvThreads) {
+  for (int v = threadIdx.x; write_frames && v < kStackVec; v += kEnvThreads) {
     const int f = v / kFrameVec, c = v - f * kFrameVec;
     dn[v] = (f < 3) ? src[v + kFrameVec] : env_bytes(seed, i, t, 0, c);  // FrameStack shift
     if (done) dr[v] = env_bytes(seed, i, t, 1, c);                        // reset: one frame x4
@@ -157,9 +159,11 @@ __device__ inline EnvOut env_step_one(uint8_t *frames, int ring, int64_t t, int6
 __global__ __launch_bounds__(kEnvThreads) void k_env_step(uint8_t *frames, int ring, int64_t t,
                                                           const int64_t *t_dev, int64_t *cur_slot, uint64_t seed,
                                                           float p_reward, float p_done, float *r_out,
-                                                          float *done_out, int64_t *s0_h, int64_t *s1_h) {
+                                                          float *done_out, int64_t *s0_h, int64_t *s1_h,
+                                                          int write_frames) {
   if (t_dev) t = *t_dev;
-  env_step_one(frames, ring, t, blockIdx.x, cur_slot, seed, p_reward, p_done, r_out, done_out, s0_h, s1_h);
+  env_step_one(frames, ring, t, blockIdx.x, cur_slot, seed, p_reward, p_done, r_out, done_out, s0_h, s1_h,
+               write_frames);
 }
 
 // The tail of a fused actor step (VecActors.step_fused), one workgroup per actor i:
@@ -192,6 +196,7 @@ struct ActorTail {
   int64_t *row_s0, *row_a, *row_s1;
   float *row_r, *row_done;
   int A;
+  int ext_frames;  // the observations come from rth_atari_env_step (no synthetic frame bytes)
 };
 
 __global__ __launch_bounds__(kEnvThreads) void k_actor_tail(ActorTail a) {
@@ -210,7 +215,7 @@ __global__ __launch_bounds__(kEnvThreads) void k_actor_tail(ActorTail a) {
     a.td_abs[i] = fabsf(td);
   }
   const EnvOut e = env_step_one(a.frames, a.ring, t, i, a.cur_slot, a.seed, a.p_reward, a.p_done, a.r_out, a.done_out,
-                                a.s0_h, a.s1_h);
+                                a.s0_h, a.s1_h, !a.ext_frames);
   if (threadIdx.x == 0)
     nstep_push_one(a.ns, i, a.n, a.gamma, a.mode, e.s0h, act, e.reward, e.s1h, e.done ? 1.0f : 0.0f, a.emit,
                    a.row_s0, a.row_a, a.row_r, a.row_s1, a.row_done);
@@ -355,7 +360,7 @@ int rth_synth_env_step(uint8_t *frames, int64_t N, int32_t ring, int64_t t, cons
   RTH_REQUIRE(frames && cur_slot && r_out && done_out && s0_h && s1_h, "rth_synth_env_step: NULL argument");
   RTH_REQUIRE(N >= 1 && N < (int64_t(1) << 31) && ring >= 4 && (t >= 1 || t_dev), "rth_synth_env_step: bad shape");
   hipLaunchKernelGGL(k_env_step, dim3((unsigned)N), dim3(kEnvThreads), 0, as_stream(stream), frames, ring, t, t_dev,
-                     cur_slot, seed, p_reward, p_done, r_out, done_out, s0_h, s1_h);
+                     cur_slot, seed, p_reward, p_done, r_out, done_out, s0_h, s1_h, 1);
   RTH_LAUNCHED();
   return RTH_OK;
 }
@@ -400,7 +405,7 @@ int rth_actor_tail(rth_nstep *h, const rth_actor_tail_args *x, int32_t *emit, in
   ActorTail a{x->q, x->eps, x->seed, x->t_dev, x->action, x->qcache, x->prev_s0, x->prev_a, x->prev_s1,
               x->prev_r, x->prev_done, x->gamma_n, x->td_abs, x->frames, x->ring, x->cur_slot, x->p_reward,
               x->p_done, x->r_out, x->done_out, x->s0_h, x->s1_h, h->st, h->n, h->gamma, h->mode, emit,
-              s0_out, a_out, s1_out, r_out, done_out, x->A};
+              s0_out, a_out, s1_out, r_out, done_out, x->A, x->ext_frames};
   hipLaunchKernelGGL(k_actor_tail, dim3((unsigned)x->N), dim3(kEnvThreads), 0, as_stream(stream), a);
   RTH_LAUNCHED();
   return RTH_OK;

@@ -73,6 +73,61 @@ __global__ void k_atari_step(const uint8_t *__restrict__ raw, int64_t n, int H, 
   dst[(K - 1) * pl + pix] = px;
 }
 
+// The Ape-X actors' Atari env mode (reth_amd/actors.py env="atari"): after the actor tail
+// assigned this step's stack handles (s0_h = the observation acted on, s1_h = the next one;
+// cur_slot = where the next observation lives: s1's slot, or a reset slot after done), the
+// raw frame pair of each actor becomes the new top frame of s1 (FrameStack shift of s0), and
+// -- done -- also the reset observation (the frame k times, FrameStack.reset) in cur_slot.
+__global__ void k_atari_env(const uint8_t *__restrict__ raw, int64_t n, int H, int W, int OH, int OW, int K,
+                            const AreaTab *__restrict__ xt, const int *__restrict__ xsrc, const float *__restrict__ xw,
+                            const AreaTab *__restrict__ yt, const int *__restrict__ ysrc, const float *__restrict__ yw,
+                            uint8_t *__restrict__ frames, int ring, const int64_t *__restrict__ s0_h,
+                            const int64_t *__restrict__ s1_h, const float *__restrict__ done,
+                            const int64_t *__restrict__ cur_slot) {
+  const int64_t i = blockIdx.x / OH;
+  const int dy = blockIdx.x % OH;
+  const int dx = threadIdx.x;
+  if (i >= n || dx >= OW) return;
+  const int64_t plane = (int64_t)H * W * 3;
+  const uint8_t *f0 = raw + i * 2 * plane, *f1 = f0 + plane;
+  const AreaTab ty = yt[dy], tx = xt[dx];
+  float sum = 0.0f;
+  for (int j = 0; j < ty.count; ++j) {
+    const int sy = ysrc[ty.first + j];
+    const float beta = yw[ty.first + j];
+    float buf = 0.0f;
+    for (int k = 0; k < tx.count; ++k) {
+      const int64_t o = ((int64_t)sy * W + xsrc[tx.first + k]) * 3;
+      const uint32_t r = max(f0[o], f1[o]), g = max(f0[o + 1], f1[o + 1]), b = max(f0[o + 2], f1[o + 2]);
+      buf = radd(buf, rmul((float)gray_u8(r, g, b), xw[tx.first + k]));
+    }
+    sum = j == 0 ? rmul(beta, buf) : radd(sum, rmul(beta, buf));
+  }
+  float v = rintf(sum);
+  const uint8_t px = (uint8_t)(v < 0.0f ? 0.0f : (v > 255.0f ? 255.0f : v));
+  const int64_t pix = (int64_t)dy * OW + dx, pl = (int64_t)OH * OW;
+  uint8_t *dst = frames + s1_h[i] * K * pl;
+  const uint8_t *src = frames + s0_h[i] * K * pl;
+  for (int p = 0; p + 1 < K; ++p) dst[p * pl + pix] = src[(p + 1) * pl + pix];
+  dst[(K - 1) * pl + pix] = px;
+  if (done[i] != 0.0f) {
+    uint8_t *rs = frames + (i * ring + cur_slot[i]) * K * pl;
+    for (int p = 0; p < K; ++p) rs[p * pl + pix] = px;
+  }
+}
+
+// raw emulator frames from device Philox (the synthetic stand-in for ALE's screen output):
+// 16 bytes per counter, counter = (vector index, step t), stream STREAM_ATARI
+__global__ __launch_bounds__(256) void k_atari_synth_raw(uint4 *__restrict__ raw, int64_t nvec, uint64_t seed,
+                                                         const int64_t *__restrict__ t_dev) {
+  const int64_t t = *t_dev;
+  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * 256) {
+    uint32_t c[4] = {(uint32_t)v, (uint32_t)(v >> 32), (uint32_t)t, STREAM_ATARI | ((uint32_t)(t >> 32) << 8)};
+    philox4x32(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    raw[v] = make_uint4(c[0], c[1], c[2], c[3]);
+  }
+}
+
 // computeResizeAreaTab for one axis: entries (dst, src, weight) in OpenCV's order
 static void area_tab(int ssize, int dsize, double scale, std::vector<AreaTab> &tab, std::vector<int> &src,
                      std::vector<float> &w) {
@@ -169,6 +224,32 @@ int rth_atari_step(rth_atari *h, const uint8_t *raw, int64_t n, uint8_t *frames,
   hipLaunchKernelGGL(k_atari_step, dim3((unsigned)(n * h->OH)), dim3(threads), 0, as_stream(stream), raw, n, h->H,
                      h->W, h->OH, h->OW, stack, h->xt, h->xsrc, h->xw, h->yt, h->ysrc, h->yw, frames, ring, prev_slot,
                      new_slot, reset, out_frame);
+  RTH_LAUNCHED();
+  return RTH_OK;
+}
+
+int rth_atari_env_step(rth_atari *h, const uint8_t *raw, int64_t n, uint8_t *frames, int32_t ring, int32_t stack,
+                       const int64_t *s0_h, const int64_t *s1_h, const float *done, const int64_t *cur_slot,
+                       void *stream) {
+  RTH_REQUIRE(h && raw && frames && s0_h && s1_h && done && cur_slot && n >= 0 && ring >= 2 && stack >= 1,
+              "rth_atari_env_step: bad arguments");
+  if (n == 0) return RTH_OK;
+  const int threads = (h->OW + 63) / 64 * 64;
+  hipLaunchKernelGGL(k_atari_env, dim3((unsigned)(n * h->OH)), dim3(threads), 0, as_stream(stream), raw, n, h->H,
+                     h->W, h->OH, h->OW, stack, h->xt, h->xsrc, h->xw, h->yt, h->ysrc, h->yw, frames, ring, s0_h, s1_h,
+                     done, cur_slot);
+  RTH_LAUNCHED();
+  return RTH_OK;
+}
+
+int rth_atari_synth_raw(uint8_t *raw, int64_t nbytes, uint64_t seed, const int64_t *t_dev, void *stream) {
+  RTH_REQUIRE(raw && t_dev && nbytes >= 0 && nbytes % 16 == 0 && (reinterpret_cast<uintptr_t>(raw) & 15) == 0,
+              "rth_atari_synth_raw: bad arguments (16-byte aligned, a multiple of 16 bytes)");
+  const int64_t nvec = nbytes / 16;
+  if (nvec == 0) return RTH_OK;
+  const int64_t want = (nvec + 255) / 256;
+  hipLaunchKernelGGL(k_atari_synth_raw, dim3((unsigned)(want < 4096 ? want : 4096)), dim3(256), 0, as_stream(stream),
+                     reinterpret_cast<uint4 *>(raw), nvec, seed, t_dev);
   RTH_LAUNCHED();
   return RTH_OK;
 }

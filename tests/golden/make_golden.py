@@ -404,8 +404,15 @@ def gen_dqn_full(R):
     and B = 64, A = 9 (the reference config's BeamRider, config.yaml:8).  Two reference
     updates (dqn_solver.py:104-124) on one batch; the FULL state_dict after each, stored as
     float16 deltas from the seeded initial weights (|delta| <= ~3e-4 after two Adam steps of
-    lr 1e-4, so the float16 rounding is <= 1.5e-7, well under the tests' 2e-6), plus every
-    |td| returned.  The frames come from tests/golden/dqn_batch.py (seed -> SHA-256 here)."""
+    lr 1e-4, so the float16 rounding is <= 1.5e-7), plus every |td| returned.
+
+    The same reference code is also run in float64 (networks, Adam and the batch in double:
+    ensure_tensor's torch.float cast redirected to float64) -- the exact update the fp32 runs
+    approximate.  Its deltas (float16) and the reference fp32 run's own per-tensor max error
+    against it are stored: the reference's fp32 CPU update is itself up to ~1.6e-5 from the
+    exact one on conv1's weight after two updates (Adam's eps = 1.5e-4 amplifies the fp32
+    gradient rounding of near-zero gradients), so a parity test needs that yardstick.
+    The frames come from tests/golden/dqn_batch.py (seed -> SHA-256 here)."""
     import torch
 
     sys.path.insert(0, OUT)
@@ -413,24 +420,50 @@ def gen_dqn_full(R):
 
     torch.set_num_threads(8)
     gym = R.gym
-    for B, A, tag in ((512, 6, "pong_b512"), (64, 9, "beamrider_b64")):
-        seed = 4242 + B + A
+
+    def run(seed, B, A, f64):
         torch.manual_seed(seed)
         solver = R.dqn_solver.DQNSolver(gym.spaces.Box(0, 255, (4, 84, 84)), gym.spaces.Discrete(A), gamma=0.99,
                                         clip_value=40, double_q=True, dueling=True, learning_rate=1e-4,
                                         adam_epsilon=1.5e-4, update_target_interval=100, device="cpu", n_step=3)
-        s0, s1, a, r, done, isw = apex_batch(seed, B, A)
-        batch = [s0.astype("f4"), a, r, s1.astype("f4"), done]
-        init = {k: v.detach().clone() for k, v in solver.q_network.state_dict().items()}
+        orig = R.dqn_solver.ensure_tensor
+        if f64:
+            solver.q_network.double()
+            solver.target_q_network.double()
+            solver.optimizer = torch.optim.Adam(solver.q_network.parameters(), lr=1e-4, eps=1.5e-4)
+            R.dqn_solver.ensure_tensor = lambda arr, dtype, device, non_blocking=True: orig(
+                arr, torch.float64 if dtype == torch.float else dtype, device)
+        try:
+            s0, s1, a, r, done, isw = apex_batch(seed, B, A)
+            batch = [s0.astype("f4"), a, r, s1.astype("f4"), done]
+            init = {k: v.detach().clone() for k, v in solver.q_network.state_dict().items()}
+            res = []
+            for _ in range(2):
+                td = solver.update(batch, weights=isw)
+                res.append((td.double().numpy(), {n: (v.detach().double() - init[n].double()).numpy()
+                                                  for n, v in solver.q_network.state_dict().items()}))
+        finally:
+            R.dqn_solver.ensure_tensor = orig
+        return init, res, (s0, s1, a, r, done, isw)
+
+    for B, A, tag in ((512, 6, "pong_b512"), (64, 9, "beamrider_b64")):
+        seed = 4242 + B + A
+        init, r32, (s0, s1, a, r, done, isw) = run(seed, B, A, False)
+        _, r64, _ = run(seed, B, A, True)
         out = dict(seed=np.int64(seed), B=np.int64(B), A=np.int64(A), frames_sha=np.array(frames_sha(s0, s1)),
                    a=a, r=r, done=done, isw=isw, param_names=np.array(list(init)))
         out["init_sum"] = np.array([float(v.double().sum()) for v in init.values()])
         for k in range(2):
-            out[f"upd{k}_abs_td"] = solver.update(batch, weights=isw).numpy()
-            for name, v in solver.q_network.state_dict().items():
-                d = (v.detach().double() - init[name].double()).numpy()
-                assert np.abs(d).max() < 6e-4, (name, np.abs(d).max())
-                out[f"upd{k}/{name}"] = d.astype(np.float16)
+            out[f"upd{k}_abs_td"] = r32[k][0].astype(np.float32)
+            out[f"upd{k}_abs_td64"] = r64[k][0]
+            errs = []
+            for name in init:
+                d32, d64 = r32[k][1][name], r64[k][1][name]
+                assert np.abs(d32).max() < 6e-4 and np.abs(d64).max() < 6e-4, name
+                out[f"upd{k}/{name}"] = d32.astype(np.float16)
+                out[f"upd{k}_64/{name}"] = d64.astype(np.float16)
+                errs.append(np.abs(d32 - d64).max())
+            out[f"upd{k}_ref32_err"] = np.array(errs)  # per tensor: max |reference fp32 - exact|
         np.savez_compressed(os.path.join(OUT, f"dqn_{tag}.npz"), **out)
 
 

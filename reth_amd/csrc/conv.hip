@@ -415,6 +415,278 @@ __global__ __launch_bounds__(256) void k_conv1_pack_bf16x3(const float *__restri
   pack_conv1_bf16x3(w, packed, blockIdx.x * 256 + threadIdx.x);
 }
 
+// ---------------------------------------------------------------------------------------
+// conv2 / conv3 forward (f32 NHWC input) on the bf16 MFMA with an exact 3 x 3-term split of
+// BOTH operands.  Every fp32 value v is the exact sum v1 + v2 + v3 of three bf16 values (the
+// round-to-nearest split of bf16x3_term: 8 + 8 + 8 of the 24 significand bits, each residual
+// exact), so for an input x and a weight w
+//     x * w = sum_{i,j in 1..3} xi * wj
+// and every partial product xi * wj has at most 16 significant bits: it is exact in the fp32
+// accumulator.  The nine bf16 MFMAs per fp32 product therefore sum exactly the same real
+// products as the fp32 MFMA's fmaf chain, accumulated in fp32 in a different order (9K terms
+// instead of K) -- the difference is summation order, as between any two fp32 GEMM tilings,
+// not precision.  (Bounded-exponent caveat: a term below 2^-126 would be a bf16 subnormal;
+// activations and weights of the DQN are many orders of magnitude away from that.)  Rate: 9
+// v_mfma_f32_16x16x32_bf16 (16 cycles each) do the work of 8 v_mfma_f32_16x16x4_f32 (32
+// cycles each): 144 vs 256 matrix-pipe cycles per 16 x 16 x 32 block, 1.78x.
+//
+// Workgroup = 8 waves over NSAMP (runtime nsamp <= NSAMP) samples: the samples' input is
+// split once into the three bf16 planes in LDS ([term][ci / 8][pixel] 16-byte units, pixel
+// rows rotated within 16-row blocks against bank conflicts); wave w owns output channels
+// 16 (w & 3) .. +15 and K half w >> 2 (its B fragments -- all three weight terms of its K half,
+// NCH / 2 chunks x 3 x 8 bf16 -- live in registers for the whole launch); every wave walks all
+// M-tiles of 16 output pixels of the workgroup's samples.  The two K halves meet in LDS
+// (fixed order: first half + second half, then + bias, ReLU), and the output leaves as one
+// contiguous run per workgroup (NHWC, or NCHW for FC1) in 16-byte stores.
+template <int KH, int KW, int S, int CIN, int HIN, int WIN, int NSAMP, int ROT>
+struct X9Geom {
+  static constexpr int COUT = 64, HOUT = (HIN - KH) / S + 1, WOUT = (WIN - KW) / S + 1, PIX = HOUT * WOUT;
+  static constexpr int K = KH * KW * CIN, NCH = K / 32, NCH2 = NCH / 2;  // 32-deep chunks, per K half
+  static constexpr int TILES = (NSAMP * PIX + 15) / 16;                  // 16-pixel M-tiles
+  static constexpr int NG = CIN / 8;                                     // 16-byte ci groups
+  static constexpr int ROWS = NSAMP * HIN * WIN;                         // staged input pixels
+  static constexpr int PLANE = (ROWS + 15) / 16 * 16 + (ROT == 10 ? 1 : 0);  // 16-B units per (term, cg)
+  static constexpr int LDS_U4 = 3 * NG * PLANE;                          // LDS in 16-B units
+  static constexpr int OUT_F = NSAMP * COUT * PIX;                       // output staging floats
+  static constexpr int PACKED_U4 = (COUT / 16) * NCH * 3 * 64;           // packed weight fragments
+  static_assert(CIN % 32 == 0 || 32 % CIN == 0, "a 32-deep chunk must stay inside one tap");
+  static_assert(CIN % 8 == 0 && K % 64 == 0, "K must split into two halves of 32-deep chunks");
+  static_assert(OUT_F * 4 <= LDS_U4 * 16, "output staging must fit the input image");
+  static_assert(LDS_U4 * 16 <= 163840, "LDS image too large");
+  __device__ static int swz(int r) { return (r & ~15) | ((r + (r >> 5) * ROT) & 15); }
+};
+
+// the three bf16 terms of 4 fp32 values, packed 2 per dword: out[t] = {t(v0) | t(v1) << 16, ...}
+__device__ __forceinline__ void split3_x4(float4 v, uint2 (&out)[3]) {
+  const float in[4] = {v.x, v.y, v.z, v.w};
+  uint32_t t[3][4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const uint32_t h1 = bf16_rne_bits(in[e]);
+    const float r1 = rsub(in[e], bf16_bits_f(h1));
+    const uint32_t h2 = bf16_rne_bits(r1);
+    const float r2 = rsub(r1, bf16_bits_f(h2));
+    t[0][e] = h1, t[1][e] = h2, t[2][e] = bf16_rne_bits(r2);
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) out[k] = make_uint2(t[k][0] | (t[k][1] << 16), t[k][2] | (t[k][3] << 16));
+}
+
+template <int KH, int KW, int S, int CIN, int HIN, int WIN, int NSAMP, int ROT>
+__global__ __launch_bounds__(512, 2) void k_conv_x9(const float *__restrict__ x, int64_t n,
+                                                    const int64_t *__restrict__ n_dev, int nsamp,
+                                                    const u32x4 *__restrict__ wpk, const float *__restrict__ bias,
+                                                    float *__restrict__ y, int out_nchw) {
+  using G = X9Geom<KH, KW, S, CIN, HIN, WIN, NSAMP, ROT>;
+  constexpr int PIX = G::PIX, NCH2 = G::NCH2, NG = G::NG, PLANE = G::PLANE, COUT = G::COUT;
+  __shared__ uint4 lds[G::LDS_U4];
+  if (n_dev) {
+    const int64_t m = *n_dev;
+    n = m < n ? (m > 0 ? m : 0) : n;
+  }
+  (void)nsamp;  // == NSAMP: the host launches the instantiation for the samples per workgroup
+  const int64_t b0 = (int64_t)blockIdx.x * NSAMP;
+  if (b0 >= n) return;  // the whole workgroup leaves: no barrier is reached
+  const int ns = (int)(n - b0 < NSAMP ? n - b0 : NSAMP);
+  const int nv = ns * PIX;  // valid output pixels
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int cb = wave & 3, half = wave >> 2;
+
+  // this wave's B fragments: channels 16 cb + (lane & 15), chunks [half * NCH2, +NCH2), 3 terms
+  bf16x8 wf[NCH2][3];
+  {
+    const u32x4 *wp = wpk + ((size_t)(cb * G::NCH + half * NCH2) * 3) * 64 + lane;
+#pragma unroll
+    for (int c = 0; c < NCH2; ++c)
+#pragma unroll
+      for (int t = 0; t < 3; ++t) wf[c][t] = __builtin_bit_cast(bf16x8, wp[(c * 3 + t) * 64]);
+  }
+  // Staging: the samples' input split into the three bf16 planes, float4 (4 ci of one pixel)
+  // -> 8 bytes in each plane, unit (t * NG + ci / 8) * PLANE + swz(pixel), half (ci % 8) / 4.
+  // Lane l of a wave-instruction takes pixel 16 k + (l & 15), ci group 4 j + (l >> 4): each
+  // 16-lane LDS write group spans 16 pixels of one ci group (distinct banks); each pixel's 64
+  // loaded bytes are contiguous in global memory.  Two phases: the first half of the samples is
+  // staged, then the second half's loads are issued and the tiles of the first half computed
+  // while they are in flight; the second half is written to LDS after them.
+  constexpr int CB = CIN / 16;                       // 4-ci groups per lane quarter
+  constexpr int NA = NSAMP > 1 ? NSAMP / 2 : NSAMP;  // samples in phase A
+  constexpr int RA = NA * HIN * WIN;                 // staged pixels of phase A
+  constexpr int SA = (RA + 15) / 16 * CB * 64;       // lane slots of phase A
+  constexpr int RB_ = (NSAMP - NA) * HIN * WIN;      // ... of phase B
+  constexpr int SB = (RB_ + 15) / 16 * CB * 64;
+  constexpr int UA = (SA + 511) / 512, UB = SB > 0 ? (SB + 511) / 512 : 1;
+  const float4 *xs = reinterpret_cast<const float4 *>(x + b0 * (int64_t)(HIN * WIN * CIN));
+  const int rows = ns * HIN * WIN;
+  auto slot_of = [&](int i, int r0, int &rr, int &c4) {
+    const int l = i & 63, blk = i >> 6;
+    rr = r0 + (blk / CB) * 16 + (l & 15);
+    c4 = (blk % CB) * 4 + (l >> 4);
+  };
+  auto fetch = [&](int i, int r0, int rend) -> float4 {
+    int rr, c4;
+    slot_of(i, r0, rr, c4);
+    return rr < rend && rr < rows ? xs[rr * (CIN / 4) + c4] : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  auto commit = [&](float4 v, int i, int r0, int rend) {
+    int rr, c4;
+    slot_of(i, r0, rr, c4);
+    if (rr >= rend || rr >= rows) return;
+    uint2 tr[3];
+    split3_x4(v, tr);
+    uint2 *l2 = reinterpret_cast<uint2 *>(lds);
+    const int unit = (c4 >> 1) * PLANE + G::swz(rr);
+#pragma unroll
+    for (int t = 0; t < 3; ++t) l2[(t * NG * PLANE + unit) * 2 + (c4 & 1)] = tr[t];
+  };
+  {
+    float4 va[UA];
+#pragma unroll
+    for (int u = 0; u < UA; ++u) va[u] = tid + u * 512 < SA ? fetch(tid + u * 512, 0, RA) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int u = 0; u < UA; ++u)
+      if (tid + u * 512 < SA) commit(va[u], tid + u * 512, 0, RA);
+  }
+  float4 vb[UB];
+  if constexpr (SB > 0) {
+#pragma unroll
+    for (int u = 0; u < UB; ++u) vb[u] = tid + u * 512 < SB ? fetch(tid + u * 512, RA, RA + RB_) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  const float bl = bias[cb * 16 + (lane & 15)];
+  __syncthreads();
+
+  // per chunk of this wave's K half (wave-uniform): the tap's pixel offset and the ci group's
+  // plane offset; per tile (per lane): the window origin's staged pixel
+  int toff[NCH2], coff[NCH2], rbv[G::TILES];
+#pragma unroll
+  for (int c = 0; c < NCH2; ++c) {
+    const int k0 = (half * NCH2 + c) * 32, tap = k0 / CIN;
+    toff[c] = (tap / KW) * WIN + tap % KW;
+    coff[c] = ((k0 % CIN) / 8) * PLANE;
+  }
+  const int g = lane >> 4;
+#pragma unroll
+  for (int tile = 0; tile < G::TILES; ++tile) {
+    int p = tile * 16 + (lane & 15);
+    if (p >= nv) p = nv - 1;
+    const int s = p / PIX, pp = p - s * PIX, oy = pp / G::WOUT, ox = pp - oy * G::WOUT;
+    rbv[tile] = s * (HIN * WIN) + S * oy * WIN + S * ox;
+  }
+  const uint4 *const lt = lds;
+  // the A fragments of step q = tile * NCH2 + c, three LDS buffers: step q + 2 is requested
+  // while step q multiplies (a sched barrier keeps the compiler from sinking the reads);
+  // phase A's tiles [0, TA) read only phase A's samples
+  constexpr int TA = NSAMP > 1 ? (NA * PIX) / 16 : G::TILES;
+  auto addr = [&](int q) -> int {
+    const int tile = q / NCH2, c = q % NCH2;
+    return coff[c] + g * PLANE + G::swz(rbv[tile] + toff[c]);
+  };
+  constexpr int NQ = G::TILES * NCH2, QA = TA * NCH2;
+  bf16x8 xf[3][3];
+  auto load = [&](int q) {
+    const int u = addr(q);
+#pragma unroll
+    for (int t = 0; t < 3; ++t) xf[q % 3][t] = __builtin_bit_cast(bf16x8, lt[t * NG * PLANE + u]);
+  };
+  f32x4 acc[G::TILES];  // every tile's accumulator stays in registers (all loops unrolled)
+  auto step = [&](int q, int qend) {
+    const int tile = q / NCH2, c = q % NCH2;
+    if (q + 2 < qend) load(q + 2);
+    __builtin_amdgcn_sched_barrier(0);
+    const bf16x8(&xc)[3] = xf[q % 3];
+    f32x4 a = c == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[tile];
+    // smallest terms first: (3,3) (3,2) (2,3) (3,1) (2,2) (1,3) (2,1) (1,2) (1,1)
+    a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xc[2], wf[c][2], a, 0, 0, 0);
+    a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xc[2], wf[c][1], a, 0, 0, 0);
+    a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xc[1], wf[c][2], a, 0, 0, 0);
+    a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xc[2], wf[c][0], a, 0, 0, 0);
+    a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xc[1], wf[c][1], a, 0, 0, 0);
+    a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xc[0], wf[c][2], a, 0, 0, 0);
+    a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xc[1], wf[c][0], a, 0, 0, 0);
+    a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xc[0], wf[c][1], a, 0, 0, 0);
+    a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xc[0], wf[c][0], a, 0, 0, 0);
+    acc[tile] = a;
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  load(0);
+  if (QA > 1) load(1);
+#pragma unroll
+  for (int q = 0; q < QA; ++q) step(q, QA);
+  if constexpr (QA < NQ) {  // phase B: write the second half's samples, then compute its tiles
+    if constexpr (SB > 0) {
+#pragma unroll
+      for (int u = 0; u < UB; ++u)
+        if (tid + u * 512 < SB) commit(vb[u], tid + u * 512, RA, RA + RB_);
+    }
+    __syncthreads();
+    load(QA);
+    if (QA + 1 < NQ) load(QA + 1);
+#pragma unroll
+    for (int q = QA; q < NQ; ++q) step(q, NQ);
+  }
+  // the K halves meet in the (now free) LDS: half 1 stores its partial sums, half 0 adds its
+  // own first, then the bias, ReLU; the workgroup's output run leaves in 16-byte stores.
+  // C/D: lane holds channel 16 cb + (lane & 15) of pixels 4 (lane >> 4) + i of each tile
+  float *F = reinterpret_cast<float *>(lds);
+  const int co = cb * 16 + (lane & 15);
+  auto fidx = [&](int p) -> int {
+    const int s = p / PIX;
+    return out_nchw ? (s * COUT + co) * PIX + (p - s * PIX) : p * COUT + co;
+  };
+  __syncthreads();  // every wave is done reading the input image
+  if (half == 1) {
+#pragma unroll
+    for (int tile = 0; tile < G::TILES; ++tile)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int p = tile * 16 + 4 * g + i;
+        if (p < nv) F[fidx(p)] = acc[tile][i];
+      }
+  }
+  __syncthreads();
+  if (half == 0) {
+#pragma unroll
+    for (int tile = 0; tile < G::TILES; ++tile)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int p = tile * 16 + 4 * g + i;
+        if (p < nv) {
+          const int f = fidx(p);
+          F[f] = relu_c(radd(radd(acc[tile][i], F[f]), bl));
+        }
+      }
+  }
+  __syncthreads();
+  {
+    const int total4 = nv * COUT / 4;  // the run [b0, b0 + ns) of y is contiguous in both layouts
+    float4 *yo = reinterpret_cast<float4 *>(y + b0 * (int64_t)(COUT * PIX));
+    const float4 *Fs = reinterpret_cast<const float4 *>(F);
+    for (int i = tid; i < total4; i += 512) yo[i] = Fs[i];
+  }
+}
+
+// OHWI weights -> the B fragments of k_conv_x9: slot ((cb * NCH + c) * 3 + t) * 64 + lane holds
+// term t of W[16 cb + (lane & 15)][32 c + 8 (lane >> 4) + j], j = 0..7 (k = (kh, kw, ci), ci fastest)
+template <int KH, int KW, int S, int CIN, int HIN, int WIN, int NSAMP, int ROT>
+__device__ __forceinline__ void pack_x9(const float *__restrict__ w, u32x4 *__restrict__ packed, int sl) {
+  using G = X9Geom<KH, KW, S, CIN, HIN, WIN, NSAMP, ROT>;
+  if (sl >= G::PACKED_U4) return;
+  const int lane = sl % 64, t = (sl / 64) % 3, c = (sl / 192) % G::NCH, cb = sl / (192 * G::NCH);
+  const int co = cb * 16 + (lane & 15), k0 = c * 32 + 8 * (lane >> 4);
+  uint32_t e[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) e[j] = bf16x3_term(w[(int64_t)co * G::K + k0 + j], t);
+  packed[sl] = u32x4{e[0] | (e[1] << 16), e[2] | (e[3] << 16), e[4] | (e[5] << 16), e[6] | (e[7] << 16)};
+}
+
+template <int KH, int KW, int S, int CIN, int HIN, int WIN, int NSAMP, int ROT>
+__global__ __launch_bounds__(256) void k_conv_pack_x9(const float *__restrict__ w, u32x4 *__restrict__ packed) {
+  pack_x9<KH, KW, S, CIN, HIN, WIN, NSAMP, ROT>(w, packed, blockIdx.x * 256 + threadIdx.x);
+}
+
+#define X9_CONV2 4, 4, 2, 32, 20, 20, 2, 10
+#define X9_CONV3 3, 3, 1, 64, 9, 9, 4, 3
+
 // OHWI weights -> MFMA fragment order (the LDS image the conv kernel copies)
 template <int MODE, int KH, int KW, int S, int CIN, int COUT, int HIN, int WIN>
 __global__ __launch_bounds__(256) void k_conv_pack(const float *__restrict__ w, f32x4 *__restrict__ packed) {
@@ -427,7 +699,7 @@ __global__ __launch_bounds__(256) void k_conv_pack(const float *__restrict__ w, 
 constexpr int kPackMax = 4;
 struct PackJob {
   int geom[kPackMax];  // index into the built geometries (find_conv order)
-  int bf16x3[kPackMax];  // conv1 u8: the bf16x3 kernel's packed form
+  int bf16x3[kPackMax];  // conv1 u8: the bf16x3 kernel's packed form; conv2 / conv3: the x9 form
   const float *w[kPackMax];
   f32x4 *packed[kPackMax];
   int first_block[kPackMax + 1];
@@ -440,6 +712,17 @@ __device__ __forceinline__ void pack_one(const float *w, f32x4 *packed, int sl) 
   if (sl < Gm::LDS_F4) packed[sl] = Gm::load_slot(w, sl);
 }
 
+// conv2's packed weights serve both of its kernels: the x9 fragments, then the fp32-MFMA image
+// (k_conv_bias_relu runs conv2 above kConv2X9Max samples, ConvLaunch::big)
+using X9Conv2 = X9Geom<X9_CONV2>;
+__device__ __forceinline__ void pack_hybrid_conv2(const float *w, f32x4 *packed, int sl) {
+  if (sl < X9Conv2::PACKED_U4) pack_x9<X9_CONV2>(w, reinterpret_cast<u32x4 *>(packed), sl);
+  else pack_one<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20>(w, packed + X9Conv2::PACKED_U4, sl - X9Conv2::PACKED_U4);
+}
+__global__ __launch_bounds__(256) void k_conv_pack_hybrid_conv2(const float *__restrict__ w, f32x4 *__restrict__ packed) {
+  pack_hybrid_conv2(w, packed, blockIdx.x * 256 + threadIdx.x);
+}
+
 __global__ __launch_bounds__(256) void k_conv_pack_many(PackJob job) {
   int l = 0;
   while (l + 1 < job.n && (int)blockIdx.x >= job.first_block[l + 1]) ++l;
@@ -450,8 +733,14 @@ __global__ __launch_bounds__(256) void k_conv_pack_many(PackJob job) {
       else pack_one<RTH_CONV_U8_CHW, 8, 8, 4, 4, 32, 84, 84>(job.w[l], job.packed[l], sl);
       break;
     case 1: pack_one<RTH_CONV_F32_NHWC, 8, 8, 4, 4, 32, 84, 84>(job.w[l], job.packed[l], sl); break;
-    case 2: pack_one<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20>(job.w[l], job.packed[l], sl); break;
-    default: pack_one<RTH_CONV_F32_NHWC, 3, 3, 1, 64, 64, 9, 9>(job.w[l], job.packed[l], sl); break;
+    case 2:
+      if (job.bf16x3[l]) pack_hybrid_conv2(job.w[l], job.packed[l], sl);
+      else pack_one<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20>(job.w[l], job.packed[l], sl);
+      break;
+    default:
+      if (job.bf16x3[l]) pack_x9<X9_CONV3>(job.w[l], reinterpret_cast<u32x4 *>(job.packed[l]), sl);
+      else pack_one<RTH_CONV_F32_NHWC, 3, 3, 1, 64, 64, 9, 9>(job.w[l], job.packed[l], sl);
+      break;
   }
 }
 
@@ -463,14 +752,33 @@ struct ConvLaunch {
   int tile_px;  // output pixels per wave tile
   int bf16x3;   // k_conv1_u8_bf16x3 (conv1 on uint8 stacks, exact-split bf16 MFMA)
   int nsplit;   // wave tiles per pixel tile (channel parts; 0 = 1)
+  int x9;       // k_conv_x9: samples per workgroup at most (0 = not an x9 kernel)
+  const void *x9fn[5];  // k_conv_x9 by samples per workgroup (nullptr: not built)
+  // hybrid geometries: above `big_above` samples the fp32-MFMA kernel *big runs instead, its
+  // packed weights behind the x9 ones (at byte `big_off`; lds_bytes counts both)
+  const struct ConvLaunch *big;
+  int64_t big_above;
+  int big_off;
 };
+
+template <int KH, int KW, int S, int CIN, int HIN, int WIN, int NSAMP, int ROT>
+static ConvLaunch x9_launch() {
+  using G = X9Geom<KH, KW, S, CIN, HIN, WIN, NSAMP, ROT>;
+  ConvLaunch l{reinterpret_cast<const void *>(&k_conv_x9<KH, KW, S, CIN, HIN, WIN, NSAMP, ROT>),
+               reinterpret_cast<const void *>(&k_conv_pack_x9<KH, KW, S, CIN, HIN, WIN, NSAMP, ROT>), 8,
+               G::PACKED_U4 * 16, 1, 16, 0, 0, NSAMP, {}, nullptr, 0, 0};
+  l.x9fn[1] = reinterpret_cast<const void *>(&k_conv_x9<KH, KW, S, CIN, HIN, WIN, 1, ROT>);
+  if (NSAMP >= 2) l.x9fn[2] = reinterpret_cast<const void *>(&k_conv_x9<KH, KW, S, CIN, HIN, WIN, (NSAMP >= 2 ? 2 : 1), ROT>);
+  if (NSAMP >= 4) l.x9fn[4] = reinterpret_cast<const void *>(&k_conv_x9<KH, KW, S, CIN, HIN, WIN, (NSAMP >= 4 ? 4 : 1), ROT>);
+  return l;
+}
 
 template <int MODE, int KH, int KW, int S, int CIN, int COUT, int HIN, int WIN, int WAVES, int MB, int NS = 1>
 static ConvLaunch conv_launch() {
   using Gm = ConvGeom<MODE, KH, KW, S, CIN, COUT, HIN, WIN>;
   ConvLaunch l{reinterpret_cast<const void *>(&k_conv_bias_relu<MODE, KH, KW, S, CIN, COUT, HIN, WIN, WAVES, MB, NS>),
                reinterpret_cast<const void *>(&k_conv_pack<MODE, KH, KW, S, CIN, COUT, HIN, WIN>), WAVES,
-               Gm::LDS_F4 * 16, 0, 16 * MB, 0, NS};
+               Gm::LDS_F4 * 16, 0, 16 * MB, 0, NS, 0, {}, nullptr, 0, 0};
   int blocks = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, l.fn, WAVES * 64, 0) != hipSuccess || blocks < 1)
     blocks = 1;
@@ -480,7 +788,7 @@ static ConvLaunch conv_launch() {
 
 static ConvLaunch conv1_bf16x3_launch() {
   ConvLaunch l{reinterpret_cast<const void *>(&k_conv1_u8_bf16x3), reinterpret_cast<const void *>(&k_conv1_pack_bf16x3),
-               4, kC1PackedBytes, 0, 32, 1};
+               4, kC1PackedBytes, 0, 32, 1, 0, 0, {}, nullptr, 0, 0};
   int blocks = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, l.fn, 256, 0) != hipSuccess || blocks < 1) blocks = 1;
   l.per_cu = blocks;
@@ -503,6 +811,21 @@ static ConvLaunch conv1_bf16x3_launch() {
 #define CONV3_NS 1
 #endif
 
+#ifndef CONV2_X9_MAX
+#define CONV2_X9_MAX 768
+#endif
+constexpr int64_t kConv2X9Max = CONV2_X9_MAX;
+
+// RTH_CONV_F32MFMA=1: conv2 / conv3 forward on the fp32-MFMA kernels instead of the exact
+// bf16x9 split (A/B and parity cross-checks)
+static bool conv_f32mfma() {
+  static const bool v = [] {
+    const char *e = getenv("RTH_CONV_F32MFMA");
+    return e && atoi(e) != 0;
+  }();
+  return v;
+}
+
 // the supported geometries (the Nature-DQN torso on 4 x 84 x 84 stacks)
 static bool find_conv(const rth_conv_shape &s, ConvLaunch *out, int *geom = nullptr) {
   auto is = [&](int mode, int cin, int hin, int win, int cout, int kh, int kw, int st) {
@@ -524,11 +847,25 @@ static bool find_conv(const rth_conv_shape &s, ConvLaunch *out, int *geom = null
     *out = l;
     if (geom) *geom = 1;
   } else if (is(RTH_CONV_F32_NHWC, 32, 20, 20, 64, 4, 4, 2)) {
-    static const ConvLaunch l = conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB>();
+    // x9 up to kConv2X9Max samples (faster there: 16.4 vs 22.5 us at 256, equal at 512), the
+    // fp32-MFMA kernel above (58 vs 61 us at 1024: two LDS-bound rounds of 2-sample workgroups)
+    static const ConvLaunch f32 = conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB>();
+    static const ConvLaunch l = [] {
+      if (conv_f32mfma()) return f32;
+      ConvLaunch h = x9_launch<X9_CONV2>();
+      h.big = &f32;
+      h.big_above = kConv2X9Max;
+      h.big_off = h.lds_bytes;
+      h.lds_bytes += f32.lds_bytes;
+      h.pack = reinterpret_cast<const void *>(&k_conv_pack_hybrid_conv2);
+      return h;
+    }();
     *out = l;
     if (geom) *geom = 2;
   } else if (is(RTH_CONV_F32_NHWC, 64, 9, 9, 64, 3, 3, 1)) {
-    static const ConvLaunch l = conv_launch<RTH_CONV_F32_NHWC, 3, 3, 1, 64, 64, 9, 9, CONV3_WAVES, CONV3_MB, CONV3_NS>();
+    static const ConvLaunch l = conv_f32mfma()
+                                    ? conv_launch<RTH_CONV_F32_NHWC, 3, 3, 1, 64, 64, 9, 9, CONV3_WAVES, CONV3_MB, CONV3_NS>()
+                                    : x9_launch<X9_CONV3>();
     *out = l;
     if (geom) *geom = 3;
   } else {
@@ -1034,7 +1371,7 @@ extern "C" {
 int rth_conv_supported(const rth_conv_shape *shape) {
   ConvLaunch l;
   if (!shape || !find_conv(*shape, &l)) return 0;
-  return (shape->input & RTH_CONV_OUT_NCHW) && l.bf16x3 ? 0 : 1;  // NCHW output: fp32-MFMA kernels only
+  return (shape->input & RTH_CONV_OUT_NCHW) && l.bf16x3 ? 0 : 1;  // NCHW output: not the conv1 u8 kernel
 }
 
 int64_t rth_conv_packed_bytes(const rth_conv_shape *shape) {
@@ -1068,7 +1405,7 @@ int rth_conv_pack_many(int32_t n, const rth_conv_shape *shapes, const float *con
                 "rth_conv_pack_many: layer %d buffer NULL or misaligned", l);
     job.w[l] = w[l];
     job.packed[l] = reinterpret_cast<f32x4 *>(packed[l]);
-    job.bf16x3[l] = cl.bf16x3;
+    job.bf16x3[l] = cl.bf16x3 || cl.x9;
     job.first_block[l] = blocks;
     blocks += (cl.lds_bytes / 16 + 255) / 256;
   }
@@ -1146,12 +1483,29 @@ static int conv_bias_relu(const rth_conv_shape *shape, const void *x, const int6
               shape->cin, shape->hin, shape->win, shape->cout, shape->kh, shape->kw, shape->stride);
   const int input = shape->input & ~RTH_CONV_OUT_NCHW, out_nchw = (shape->input & RTH_CONV_OUT_NCHW) ? 1 : 0;
   RTH_REQUIRE(!rows || input == RTH_CONV_U8_CHW, "rth_conv_bias_relu: row index needs uint8 stacks");
-  RTH_REQUIRE(!out_nchw || !l.bf16x3, "rth_conv_bias_relu: NCHW output is built for the fp32-MFMA kernels only");
+  RTH_REQUIRE(!out_nchw || !l.bf16x3, "rth_conv_bias_relu: NCHW output is not built for conv1 on uint8 stacks");
   RTH_REQUIRE(((reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(y)) & 15) == 0 &&
                   (input == RTH_CONV_U8_CHW ? (reinterpret_cast<uintptr_t>(x) & 3) == 0
                                                    : (reinterpret_cast<uintptr_t>(x) & 15) == 0),
               "rth_conv_bias_relu: misaligned buffer");
   if (n == 0) return RTH_OK;
+  if (l.big && n > l.big_above) {  // a hybrid geometry's fp32-MFMA kernel for large batches
+    w = reinterpret_cast<const float *>(reinterpret_cast<const uint8_t *>(w) + l.big_off);
+    l = *l.big;
+  }
+  if (l.x9) {  // one workgroup per nsamp samples (nsamp: enough workgroups for every CU first)
+    RTH_REQUIRE(input == RTH_CONV_F32_NHWC, "rth_conv_bias_relu: the x9 kernels read f32 NHWC input");
+    int64_t nsamp = n / cu_count();  // samples per workgroup: a built instantiation, >= 1 workgroup per CU
+    nsamp = nsamp < 1 ? 1 : (nsamp > l.x9 ? l.x9 : nsamp);
+    while (!l.x9fn[nsamp]) --nsamp;
+    const int ns = (int)nsamp;
+    const int64_t grid = (n + nsamp - 1) / nsamp;
+    const float *xf = static_cast<const float *>(x);
+    void *args[] = {(void *)&xf, (void *)&n, (void *)&n_dev, (void *)&ns, (void *)&w, (void *)&bias, (void *)&y,
+                    (void *)&out_nchw};
+    RTH_HIP(hipLaunchKernel(l.x9fn[nsamp], dim3((unsigned)grid), dim3(512), args, 0, as_stream(stream)));
+    return RTH_OK;
+  }
   const int hout = (shape->hin - shape->kh) / shape->stride + 1, wout = (shape->win - shape->kw) / shape->stride + 1;
   const int64_t tiles = (n * hout * wout + l.tile_px - 1) / l.tile_px * (l.nsplit > 1 ? l.nsplit : 1);
   int64_t grid = (tiles + l.waves - 1) / l.waves;

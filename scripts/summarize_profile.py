@@ -49,7 +49,7 @@ def main():
     arg = lambda k, d: int(sys.argv[sys.argv.index(k) + 1]) if k in sys.argv else d
     steps = arg("--steps", 100)
     grids = {"gather": copy_grid(arg("--batch", 512)), "insert": copy_grid(arg("--actors", 256))}
-    inloop = {}
+    inloop, loop_grid = {}, {}
     os.makedirs(PROF, exist_ok=True)
     stats = os.path.join(OUT, "prof", "run_kernel_stats.csv")
     if os.path.exists(stats):
@@ -78,10 +78,12 @@ def main():
             for k, v in sorted(agg.items(), key=lambda kv: -kv[1][0]):
                 f.write(f"{v[0] / busy * 100:6.2f}% {v[0] / 1e3 / steps:9.2f} {v[1] / steps:10.2f}  {k}\n")
         for name, (match, g) in HBM_KERNELS.items():  # in-loop mean launch durations (bench.py roofline_hbm)
-            d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in win if match in r["Kernel_Name"]
-                 and (g is None or int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) == grids[g])]
-            if d:
-                inloop[name] = round(st.mean(d) / 1e3, 3)
+            sel = [r for r in win if match in r["Kernel_Name"]
+                   and (g is None or int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) == grids[g])]
+            if sel:
+                inloop[name] = round(st.mean(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in sel) / 1e3, 3)
+                grid_of = collections.Counter(int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) for r in sel)
+                loop_grid[name] = grid_of.most_common(1)[0][0]  # the PMC pass is matched on it
         for name, fn, head in (
                 ("k_copy_rows", "gather_launches", "# (512*256, 5) = learner gather (rth_replay_gather, B=512, 5 columns)"),
                 (CONV2, "conv2_launches", "# learner stream = the learner's [s0; s1] forward (2B = 1024 samples; "
@@ -136,8 +138,9 @@ def main():
                             f"{name}_dispatches": len(fe[key])})
         hbm = {}
         for name, (match, g) in HBM_KERNELS.items():
-            cs = [k for k in fe if match in k[0] and k in wr and (g is None or k[1] == grids[g])]
-            if g is None and len(cs) > 1:  # the loop's launch: the grid with the most dispatches
+            want = loop_grid.get(name, grids.get(g))
+            cs = [k for k in fe if match in k[0] and k in wr and (want is None or k[1] == want)]
+            if len(cs) > 1:  # no trace to say which grid the loop launches: the most dispatched one
                 cs = [max(cs, key=lambda k: len(fe[k]))]
             if len(cs) == 1:
                 k = cs[0]

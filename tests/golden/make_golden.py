@@ -439,23 +439,71 @@ def gen_dqn_full(R):
             init = {k: v.detach().clone() for k, v in solver.q_network.state_dict().items()}
             res = []
             for _ in range(2):
+                tgt = None
+                if f64:  # the TD target r + gamma^n Q_target(s1, argmax_a Q(s1, a)) (1 - done) of this
+                    # update (dqn_solver.py:84-96), in float64: the scale the north-star 1e-5 applies to
+                    with torch.no_grad():
+                        x1 = torch.as_tensor(s1).double()
+                        best = solver.q_network(x1).argmax(1, keepdim=True)
+                        nxt = solver.target_q_network(x1).gather(1, best).view(-1)
+                        tgt = (torch.as_tensor(r).double() + 0.99 ** 3 * nxt *
+                               (1 - torch.as_tensor(done).double())).numpy()
                 td = solver.update(batch, weights=isw)
                 res.append((td.double().numpy(), {n: (v.detach().double() - init[n].double()).numpy()
-                                                  for n, v in solver.q_network.state_dict().items()}))
+                                                  for n, v in solver.q_network.state_dict().items()}, tgt))
         finally:
             R.dqn_solver.ensure_tensor = orig
         return init, res, (s0, s1, a, r, done, isw)
 
+    def margins(seed, B, A):
+        """float64 decision margins of the first update's forward, relative to sum |x| |w|: the
+        FC1 ReLUs of the s0 rows (a flipped unit there moves a whole row of FC1's gradient:
+        one flip at a relative margin of 1.3e-8 -- below fp32 rounding -- put 2e-3 into
+        fc_adv.0.weight's gradient on seed 4760) and the double-Q argmax of the online heads
+        on s1 (top-2 gap relative to the heads' magnitude)"""
+        torch.manual_seed(seed)
+        solver = R.dqn_solver.DQNSolver(gym.spaces.Box(0, 255, (4, 84, 84)), gym.spaces.Discrete(A), gamma=0.99,
+                                        clip_value=40, double_q=True, dueling=True, learning_rate=1e-4,
+                                        adam_epsilon=1.5e-4, update_target_interval=100, device="cpu", n_step=3)
+        net = solver.q_network.double()
+        s0, s1, *_ = apex_batch(seed, B, A)
+        with torch.no_grad():
+            f = net.features(torch.as_tensor(np.concatenate([s0, s1])).double()).reshape(2 * B, -1)
+            relu = np.inf
+            for fc in (net.fc_adv[0], net.fc_value[0]):
+                pre = f[:B] @ fc.weight.t() + fc.bias
+                scale = f[:B].abs() @ fc.weight.abs().t() + fc.bias.abs()
+                relu = min(relu, float((pre.abs() / scale).min()))
+            q1 = net(torch.as_tensor(s1).double())
+            top = torch.topk(q1, 2, dim=1).values
+            gap = float(((top[:, 0] - top[:, 1]) / q1.abs().max(1).values.clamp_min(1e-30)).min())
+        return relu, gap
+
     for B, A, tag in ((512, 6, "pong_b512"), (64, 9, "beamrider_b64")):
-        seed = 4242 + B + A
+        # the batch + seeded init is screened: of 40 candidate seeds the one whose closest FC1
+        # ReLU / double-Q argmax decision of the exact update lies farthest from its threshold
+        # (~1e-6 relative at B = 512, where a 512 x 1024 FC1 has a few pre-activations per 1e-6
+        # of relative margin): decisions closer than fp32 rounding are coin flips that any two
+        # fp32 summation orders -- the reference's own CPU run included -- may take differently
+        cands = []
+        for k in range(40):
+            sd = 4242 + B + A + 1000 * k
+            cands.append((min(margins(sd, B, A)), sd))
+            print(f"  dqn_{tag}: seed {sd} min margin {cands[-1][0]:.2e}", flush=True)
+        seed = max(cands)[1]
+        relu_m, gap_m = margins(seed, B, A)
         init, r32, (s0, s1, a, r, done, isw) = run(seed, B, A, False)
         _, r64, _ = run(seed, B, A, True)
         out = dict(seed=np.int64(seed), B=np.int64(B), A=np.int64(A), frames_sha=np.array(frames_sha(s0, s1)),
                    a=a, r=r, done=done, isw=isw, param_names=np.array(list(init)))
         out["init_sum"] = np.array([float(v.double().sum()) for v in init.values()])
+        out["margin_fc1_relu"], out["margin_argmax"] = np.float64(relu_m), np.float64(gap_m)
         for k in range(2):
             out[f"upd{k}_abs_td"] = r32[k][0].astype(np.float32)
             out[f"upd{k}_abs_td64"] = r64[k][0]
+            out[f"upd{k}_target64"] = r64[k][2]
+            rel = np.abs(r32[k][0] - r64[k][0]) / np.maximum(1.0, np.abs(r64[k][2]))
+            print(f"  dqn_{tag} update {k}: reference fp32 |td| error / max(1, |target|) <= {rel.max():.2e}")
             errs = []
             for name in init:
                 d32, d64 = r32[k][1][name], r64[k][1][name]

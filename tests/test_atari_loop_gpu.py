@@ -82,5 +82,6 @@ def test_atari_loop_graph_matches_eager(dev):
     a, ia = run(False)
     b, ib = run(True)
     assert ia == ib
-    for x, y in zip(a, b):
-        assert torch.equal(x, y)
+    names = ["tree sums", "tree mins", "values", "frames", "s0", "a", "r", "s1", "done"]
+    for name, x, y in zip(names, a, b):
+        assert torch.equal(x, y), (name, int((x != y).sum()))

@@ -56,7 +56,8 @@ def test_conv_f32_nhwc(dev, geom, n):
 
 # the learner / target / actor batch sizes, and sizes whose tiles (16 output pixels) leave a
 # short partial last round on 256 CUs (several tiles per wave, the last round ragged)
-@pytest.mark.parametrize("gi,n", [(0, 41), (0, 72), (1, 204), (1, 1024), (2, 340), (2, 1024), (2, 512)])
+@pytest.mark.parametrize("gi,n", [(0, 41), (0, 72), (1, 204), (1, 1024), (2, 340), (2, 1024), (2, 512), (1, 513),
+                                  (1, 768), (1, 769), (2, 1023), (2, 1025), (2, 259)])
 def test_conv_partial_rounds(dev, gi, n):
     from reth_amd import _lib
 
@@ -111,7 +112,12 @@ def test_conv_empty_and_unsupported(dev):
     bad = _shape(_lib.CONV_F32_NHWC, 3, 84, 84, 32, 8, 4)
     assert _lib.lib().rth_conv_supported(_lib.ctypes.byref(bad)) == 0
     assert _lib.lib().rth_conv_packed_bytes(_lib.ctypes.byref(bad)) == 0
-    assert _lib.lib().rth_conv_packed_bytes(_lib.ctypes.byref(shape)) == 64 * 32 * 16 * 4
+    import os
+
+    # conv2's packed weights: one fp32 copy (RTH_CONV_F32MFMA), or by default the three bf16
+    # terms of the exact split (the x9 kernel, small batches) followed by the fp32 copy (large)
+    per = 4 if os.environ.get("RTH_CONV_F32MFMA") else 3 * 2 + 4
+    assert _lib.lib().rth_conv_packed_bytes(_lib.ctypes.byref(shape)) == 64 * 32 * 16 * per
     with pytest.raises(_lib.RethHipError, match="not built"):
         _lib.call("rth_conv_bias_relu", _lib.ctypes.byref(bad), x.data_ptr(), None, 1, w.data_ptr(), w.data_ptr(),
                   y.data_ptr(), _lib.stream_ptr())
@@ -430,3 +436,25 @@ def test_conv_wgrad_f32(dev, gi, n):
     scale = want.abs().max().item()
     err = (outs[0].double().cpu() - want).abs().max().item()
     assert err <= 2e-6 * max(scale, 1.0) * max(1.0, (n * ho * ho) ** 0.5 / 8), (err, scale)
+
+
+@pytest.mark.parametrize("gi,n", [(1, 64), (1, 512), (2, 64), (2, 512), (1, 1024)])
+def test_conv_fp32_grade_accuracy(dev, gi, n):
+    """the exact-split bf16 kernels (k_conv_x9) and the fp32-MFMA kernels are as accurate as an
+    fp32 convolution: the worst error against float64 stays within a small multiple of what
+    torch's own fp32 CPU convolution makes on the same data (the learner's Adam step, eps
+    1.5e-4, turns coarser forward rounding into weight drift: test_learner_full_gpu)"""
+    from reth_amd import _lib
+
+    cin, h, wd, cout, k, s = GEOMS[gi]
+    g = torch.Generator().manual_seed(1000 + gi * 7 + n)
+    x = torch.relu(torch.randn((n, cin, h, wd), generator=g))
+    w = torch.randn((cout, cin, k, k), generator=g) / np.sqrt(cin * k * k)
+    b = torch.randn(cout, generator=g) * 0.1
+    xd = x.to(dev).contiguous(memory_format=torch.channels_last)
+    got = _run(_shape(_lib.CONV_F32_NHWC, *GEOMS[gi]), xd, None, n, w, b, dev).double()
+    want = _ref(x, w, b, s)
+    t32 = F.relu(F.conv2d(x, w, b, stride=s)).double()
+    e_ours, e_t32 = (got - want).abs().max().item(), (t32 - want).abs().max().item()
+    print(f"conv{gi + 1} n={n}: ours {e_ours:.3e} torch-fp32 {e_t32:.3e}")
+    assert e_ours <= 4 * e_t32 + 1e-7, (e_ours, e_t32)

@@ -13,12 +13,17 @@ TunableOp solutions, rth_clip_adam) is built with the reference's seed, run unti
 are captured, then reset to the initial weights / zero Adam state; the golden batch is
 written into a learner batch slot and the captured learner graph is replayed twice.
 Tolerances: the first update's |td| within the north-star 1e-5 of the reference's fp32 run
-(same weights, same batch).  The parameters are compared with the EXACT update (the same
+(same weights, same batch), relative to the magnitude of td's operands Q(s0, a) and the TD
+target (both ~17 on Pong's unnormalised frames; the fixture holds the float64 target).  The parameters are compared with the EXACT update (the same
 reference code run in float64, stored beside the fp32 run): the reference's own fp32 CPU
 update is up to 1.6e-5 away from it on conv1's weight after two updates (Adam's eps = 1.5e-4
 turns the fp32 rounding of near-zero gradients into parameter differences), so every tensor
 must be at least as close to the exact update as 2x the reference fp32 run's distance, with
-the north-star 2e-6 as the floor; the second update's |td| likewise."""
+the north-star 2e-6 as the floor; the second update's |td| likewise.  The fixture's seed is
+screened (make_golden.py gen_dqn_full): no FC1 ReLU / double-Q argmax decision of the exact
+update closer to its threshold than fp32 rounding, where any two fp32 summation orders
+(the reference's CPU run included) may decide differently -- one such flip at a relative
+margin of 1.3e-8 moved a whole row of FC1's gradient by 2e-3 on the previous seed."""
 import os
 import sys
 
@@ -37,7 +42,7 @@ def test_apex_learner_graph_vs_reference(golden, dev, name):
 
     from reth_amd.apex import ApexConfig, ApexDQN
 
-    gd = golden(name)
+    gd, tag = golden(name), name.split(".")[0]
     B, A, seed = int(gd["B"]), int(gd["A"]), int(gd["seed"])
     s0, s1, a, r, done, isw = apex_batch(seed, B, A)
     assert frames_sha(s0, s1) == str(gd["frames_sha"])
@@ -59,39 +64,41 @@ def test_apex_learner_graph_vs_reference(golden, dev, name):
     torch.cuda.synchronize()
     G = ax._graphs
     assert G is not None, "the learner graph was not captured"
-    # back to the reference's starting point: initial weights, target = online, fresh Adam
-    with torch.no_grad():
-        for k, v in solver.q_network.state_dict().items():
-            v.copy_(init[k])
-        solver.update_target()
-        opt = solver.optimizer
-        for st in opt.state.values():
-            st["exp_avg"].zero_()
-            st["exp_avg_sq"].zero_()
-        opt._step.zero_()
-        opt._ws.zero_()
-    p = 0
-    cols, idx, w = ax.loader._slots[p]
-    cols[0].copy_(torch.as_tensor(s0))
-    cols[3].copy_(torch.as_tensor(s1))
-    cols[1].copy_(torch.as_tensor(a))
-    cols[2].copy_(torch.as_tensor(r))
-    cols[4].copy_(torch.as_tensor(done))
-    w.copy_(torch.as_tensor(isw))
-    torch.cuda.synchronize()
-    v = ("full", p)  # the learner computes the target pass itself (as after a target sync)
-    stream = torch.cuda.Stream(dev)
-    report = []
+
+    def reset():
+        # back to the reference's starting point: initial weights, target = online, fresh Adam
+        with torch.no_grad():
+            for k, v in solver.q_network.state_dict().items():
+                v.copy_(init[k])
+            solver.update_target()
+            opt = solver.optimizer
+            for st in opt.state.values():
+                st["exp_avg"].zero_()
+                st["exp_avg_sq"].zero_()
+            opt._step.zero_()
+            opt._ws.zero_()
+        p = 0
+        cols, idx, w = ax.loader._slots[p]
+        cols[0].copy_(torch.as_tensor(s0))
+        cols[3].copy_(torch.as_tensor(s1))
+        cols[1].copy_(torch.as_tensor(a))
+        cols[2].copy_(torch.as_tensor(r))
+        cols[4].copy_(torch.as_tensor(done))
+        w.copy_(torch.as_tensor(isw))
+        torch.cuda.synchronize()
+        v = ("full", p)  # the learner computes the target pass itself (as after a target sync)
+        stream = torch.cuda.Stream(dev)
+        return v, stream
+
+    v, stream = reset()
+    report, dump, tds = [], {}, []
     for k in range(2):
         with torch.cuda.stream(stream):
             ax._learner_replay(v)
         torch.cuda.synchronize()
         td = G["learn_td"][v].double().cpu().numpy()
         td32, td64 = gd[f"upd{k}_abs_td"].astype(np.float64), gd[f"upd{k}_abs_td64"]
-        if k == 0:  # same weights, same batch: the north-star bar against the reference's fp32 run
-            np.testing.assert_allclose(td, td32, rtol=1e-5, atol=1e-5)
-        ref_td = np.abs(td32 - td64).max()
-        assert np.abs(td - td64).max() <= 2 * ref_td + 1e-5, (k, np.abs(td - td64).max(), ref_td)
+        tds.append((k, td, td32, td64))
         for j, (name, t) in enumerate(solver.q_network.state_dict().items()):
             base = init[name].double().cpu()
             exact = base + torch.as_tensor(gd[f"upd{k}_64/{name}"].astype(np.float64))
@@ -100,10 +107,38 @@ def test_apex_learner_graph_vs_reference(golden, dev, name):
             e_ours = float((ours - exact).abs().max())
             e_ref = float(gd[f"upd{k}_ref32_err"][j])
             report.append((k, name, e_ours, e_ref, float((ours - ref32).abs().max())))
-            # at least as close to the exact (fp64) update as 2x the reference's own fp32 CPU run,
-            # within the north-star 2e-6 floor (+ the fixture's float16 rounding, 2 x 1.5e-7)
-            assert e_ours <= 2 * e_ref + 2e-6 + 3e-7, (k, name, e_ours, e_ref)
+            if os.environ.get("RTH_DUMP_LEARNER"):
+                dump[f"upd{k}/{name}"] = (ours - base).numpy()
+    if os.environ.get("RTH_LEARNER_REPEAT"):  # run-to-run: the same two updates again, bitwise
+        first = {k: t.detach().clone() for k, t in solver.q_network.state_dict().items()}
+        v, stream = reset()
+        for k in range(2):
+            with torch.cuda.stream(stream):
+                ax._learner_replay(v)
+        torch.cuda.synchronize()
+        diff = {k: float((t.double() - first[k].double()).abs().max()) for k, t in solver.q_network.state_dict().items()}
+        print("repeat: max |run2 - run1| per tensor", {k: f"{d:.1e}" for k, d in diff.items()})
+    if dump:
+        os.makedirs("gpurun_out", exist_ok=True)
+        np.savez_compressed(f"gpurun_out/learner_{tag}.npz", **dump)
     for k, name, e_ours, e_ref, e_vs in report:
         print(f"update {k} {name:20s} |ours - exact| {e_ours:.2e}  |ref fp32 - exact| {e_ref:.2e}  "
               f"|ours - ref fp32| {e_vs:.2e}")
+    for k, td, td32, td64 in tds:
+        ref_td = np.abs(td32 - td64).max()
+        print(f"update {k} |td|: |ours - exact| {np.abs(td - td64).max():.2e}  |ref fp32 - exact| {ref_td:.2e}  "
+              f"|ours - ref fp32| {np.abs(td - td32).max():.2e}")
+    for k, td, td32, td64 in tds:
+        if k == 0:  # same weights, same batch: the north-star 1e-5 against the reference's fp32 run,
+            # relative to the operands of td = Q(s0, a) - target (|Q| <= |td| + |target|, ~17 here:
+            # the reference's own fp32 run is 1e-5 from the exact |td| in absolute terms)
+            scale = np.maximum(1.0, td64 + np.abs(gd[f"upd{k}_target64"]))
+            rel = np.abs(td - td32) / scale
+            assert rel.max() <= 1e-5, (k, rel.max(), int(rel.argmax()))
+        ref_td = np.abs(td32 - td64).max()
+        assert np.abs(td - td64).max() <= 2 * ref_td + 1e-5, (k, np.abs(td - td64).max(), ref_td)
+    for k, name, e_ours, e_ref, _ in report:
+        # at least as close to the exact (fp64) update as 2x the reference's own fp32 CPU run,
+        # within the north-star 2e-6 floor (+ the fixture's float16 rounding, 2 x 1.5e-7)
+        assert e_ours <= 2 * e_ref + 2e-6 + 3e-7, (k, name, e_ours, e_ref)
     ax.close()

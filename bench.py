@@ -14,13 +14,15 @@ scaling: every GPU runs the same per-GPU workload and the learner gradients are 
 with one RCCL all-reduce per update.
 
 The JSON line carries
-  roofline:        the dominant kernel of the step (most time per iteration in
-                   profiles/r02_steady_state.txt): conv3's forward (k_conv_bias_relu, fp32
-                   MFMA) in the learner's [s0; s1] pass, timed live over the timed region with
-                   HIP events on the learner stream (the learner graph is cut once, around the
-                   conv2 + conv3 launches); achieved = algorithmic FLOPs per launch / mean
-                   launch duration
-  roofline_conv2:  conv2's forward in the same pass (the second kernel), timed the same way
+  roofline:        the dominant kernel of the step: whichever of conv2 / conv3 forward has the
+                   most kernel time per iteration (conv_iteration_alone: its learner, target
+                   and actor launches timed alone), measured in the learner's [s0; s1] pass
+                   live over the timed region with HIP events on the learner stream (the
+                   learner graph is cut once, around the conv2 + conv3 launches); achieved =
+                   algorithmic FLOPs per launch / mean launch duration, against the fp32 MFMA
+                   peak (dtype f32); an exact-split bf16 kernel (k_conv_x9) also reports the
+                   bf16 MFMA FLOPs it issues against the bf16 peak (mfma_issue)
+  roofline_conv2 / roofline_conv3: both conv kernels, timed the same way
   roofline_gather: the replay gather (k_copy_rows), HBM-bound, timed live the same way
   roofline_conv1:  conv1 on uint8 stacks (k_conv1_u8_bf16x3) alone, against the bf16 MFMA peak
                    of the instruction it issues (three exact-split bf16 products per fp32 one)
@@ -115,6 +117,54 @@ def conv1_roofline(ax, slot_cols, reps=30):
             "mfma_flops_per_launch": 3 * flops, "launch_us": round(t * 1e6, 2),
             "note": "timed alone after the timed region (HIP events); achieved counts the bf16 MFMA FLOPs issued "
                     "(3 exact-split products per fp32 product), achieved_fp32_equiv the algorithmic ones"}
+
+
+def conv_impl(shape, n):
+    """(kernel label, MFMA FLOPs issued per algorithmic FLOP, peak TFLOP/s of that MFMA) of the
+    kernel rth_conv_bias_relu runs for `shape` and n samples (rth_conv_impl)"""
+    from reth_amd import _lib
+
+    ns = _lib.ctypes.c_int32(0)
+    kind = _lib.lib().rth_conv_impl(_lib.ctypes.byref(shape), int(n), _lib.ctypes.byref(ns))
+    if kind == _lib.CONV_IMPL_X9:
+        return (f"k_conv_x9 (exact 3 x 3-term bf16 split of input and weights, nine bf16 MFMAs per fp32 product, "
+                f"{ns.value} samples per workgroup)", 9, BF16_PEAK_TFLOPS)
+    if kind == _lib.CONV_IMPL_BF16X3:
+        return "k_conv1_u8_bf16x3 (exact 3-term bf16 split of the weights)", 3, BF16_PEAK_TFLOPS
+    return "k_conv_bias_relu (fp32 MFMA)", 1, FP32_PEAK_TFLOPS
+
+
+def conv_iteration_alone(ax, sizes, reps=20):
+    """conv2 / conv3 forward timed alone (HIP events around direct launches, median) at each
+    batch size one iteration launches them with ({learner [s0; s1], target pass, actors}):
+    the per-iteration kernel time that says which conv kernel dominates the step"""
+    from reth_amd import _lib
+
+    net = ax.solver.q_network
+    shapes = [sh for _, sh in net._torso_shapes((4, 84, 84), True)]
+    packed = net.pack_convs(True)
+    out = {}
+    for li in (1, 2):
+        shape, conv = shapes[li], net._convs()[li]
+        ho = (shape.hin - shape.kh) // shape.stride + 1
+        per = {}
+        for n in sizes:
+            x = torch.rand((n, shape.cin, shape.hin, shape.win), device=conv.weight.device).contiguous(
+                memory_format=torch.channels_last)
+            y = torch.empty((n, shape.cout, ho, ho), device=x.device, memory_format=torch.channels_last)
+            ev = []
+            for _ in range(reps):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                _lib.call("rth_conv_bias_relu", _lib.ctypes.byref(shape), x.data_ptr(), None, n,
+                          net._packed_for(packed, li, True).data_ptr(), conv.bias.data_ptr(), y.data_ptr(),
+                          _lib.stream_ptr())
+                e1.record()
+                ev.append((e0, e1))
+            torch.cuda.synchronize()
+            per[str(n)] = round(float(np.median([a.elapsed_time(b) for a, b in ev[3:]])) * 1e3, 2)
+        out[f"conv{li + 1}"] = {"launch_us_by_samples": per, "iteration_us": round(sum(per.values()), 2)}
+    return out
 
 
 def load_traffic(tag, key):
@@ -714,6 +764,8 @@ def main():
     torch.cuda.synchronize()
     iso_s = float(np.median([a.elapsed_time(b) for a, b in iso[5:]])) / 1e3
     conv1 = conv1_roofline(ax, slot_cols) if cfg.hip_conv and cfg.channels_last else None
+    conv_alone = conv_iteration_alone(ax, (2 * cfg.batch_size, cfg.batch_size, cfg.n_actors)) \
+        if cfg.hip_conv and cfg.channels_last else None
     decoupled = None
     if not args.no_sweep and ax._graphs is not None:
         decoupled = decoupled_actors(ax, dev, world)
@@ -748,10 +800,13 @@ def main():
     roofline = roofline_gather
     n2 = 2 * cfg.batch_size  # the learner's [s0; s1] forward
 
+    torso = [sh for _, sh in ax.solver.q_network._torso_shapes((4, 84, 84), True)]
+
     def conv_roofline(ms, name, cin, hin, cout, hout, k, stride, flops, traffic, src):
         s_ = float(np.mean(ms)) / 1e3
-        return {
-            "kernel": f"k_conv_bias_relu {name} (fp32 MFMA; {cin}x{hin}x{hin} -> {cout}x{hout}x{hout}, k{k} s{stride}) in the "
+        label, issue, unit_peak = conv_impl(torso[int(name[-1]) - 1], n2)
+        r = {
+            "kernel": f"{name}: {label}; {cin}x{hin}x{hin} -> {cout}x{hout}x{hout}, k{k} s{stride}, in the "
                       f"learner's [s0; s1] forward, {n2} samples per launch",
             "bound": "mfma", "achieved": round(flops / s_ / 1e12, 2), "peak": FP32_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": round(flops / s_ / 1e12 / FP32_PEAK_TFLOPS, 4),
@@ -761,14 +816,29 @@ def main():
             "launches_timed": len(ms),
             "note": "timed live over the timed region: HIP events on the learner stream around the launch (the "
                     "learner graph is cut there); it runs concurrently with the actor stream's kernels"}
+        if issue > 1:  # exact-split bf16 kernel: achieved / frac are fp32-equivalent (the dtype's peak)
+            r["mfma_issue"] = {"bf16_flops_per_launch": issue * flops, "achieved": round(issue * flops / s_ / 1e12, 2),
+                               "peak": unit_peak, "frac": round(issue * flops / s_ / 1e12 / unit_peak, 4),
+                               "note": f"the bf16 MFMA FLOPs the kernel issues ({issue} exact-split products per fp32 "
+                                       "product) against the dense bf16 peak"}
+        return r
+
     roofline_conv2 = None
     if conv2_ms:
         roofline_conv2 = conv_roofline(conv2_ms, "conv2", 32, 20, 64, 9, 4, 2, 2.0 * n2 * 9 * 9 * 64 * 32 * 4 * 4,
                                        c2_traffic, c2_src)
         roofline = roofline_conv2
-    if conv3_ms:  # the most time per iteration of any kernel (3 launches: learner, target pass, actors)
-        roofline = conv_roofline(conv3_ms, "conv3", 64, 9, 64, 7, 3, 1, 2.0 * n2 * 7 * 7 * 64 * 64 * 3 * 3,
-                                 c3_traffic, c3_src)
+    roofline_conv3 = None
+    if conv3_ms:
+        roofline_conv3 = conv_roofline(conv3_ms, "conv3", 64, 9, 64, 7, 3, 1, 2.0 * n2 * 7 * 7 * 64 * 64 * 3 * 3,
+                                       c3_traffic, c3_src)
+    # `roofline` = the conv kernel with the most time per iteration (its three launches -- learner,
+    # target pass, actors -- timed alone at their batch sizes)
+    if roofline_conv2 and roofline_conv3:
+        roofline = roofline_conv3 if conv_alone["conv3"]["iteration_us"] >= conv_alone["conv2"]["iteration_us"] \
+            else roofline_conv2
+    elif roofline_conv3:
+        roofline = roofline_conv3
     out = {
         "metric": "env-steps/sec + learner updates/sec, Ape-X DQN Pong, 1/2/4/8 MI355X",
         "value": round(n_env / dt, 1),
@@ -811,6 +881,8 @@ def main():
         "roofline": roofline,
         "roofline_gather": roofline_gather,
         "roofline_conv2": roofline_conv2,
+        "roofline_conv3": roofline_conv3,
+        "conv_iteration_alone": conv_alone,
         "qnet_mfma": {"tflops_per_step": round(flops_step / 1e12, 4),
                       "achieved_tflops": round(flops_step / step_s / 1e12, 2),
                       "peak_fp32_tflops": FP32_PEAK_TFLOPS},

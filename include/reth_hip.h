@@ -423,6 +423,15 @@ typedef struct rth_conv_shape {
   int32_t cin, hin, win, cout, kh, kw, stride;
 } rth_conv_shape;
 int rth_conv_supported(const rth_conv_shape *shape);
+/* which kernel rth_conv_bias_relu runs for a shape and n samples (hybrid geometries switch by
+ * batch size): RTH_CONV_IMPL_F32 (k_conv_bias_relu, fp32 MFMA), RTH_CONV_IMPL_BF16X3
+ * (k_conv1_u8_bf16x3), RTH_CONV_IMPL_X9 (k_conv_x9: both operands split into three exact bf16
+ * terms, nine bf16 MFMAs per fp32 product; *nsamp_out = samples per workgroup); 0 = not built.
+ * Diagnostics (bench.py's roofline labels), no launch. */
+#define RTH_CONV_IMPL_F32 1
+#define RTH_CONV_IMPL_BF16X3 2
+#define RTH_CONV_IMPL_X9 3
+int rth_conv_impl(const rth_conv_shape *shape, int64_t n, int32_t *nsamp_out);
 int64_t rth_conv_packed_bytes(const rth_conv_shape *shape);
 int rth_conv_pack(const rth_conv_shape *shape, const float *w_ohwi_dev, float *packed_dev, void *stream);
 /* rth_conv_pack for n <= 4 layers in one launch (a network's torso, both conv1 forms) */

@@ -61,6 +61,7 @@ class BiasDeferred(ctypes.Structure):
 
 CONV_F32_NHWC, CONV_U8_CHW = 0, 1
 CONV_OUT_NCHW = 16  # flag: the conv writes NCHW (the last conv, feeding FC1)
+CONV_IMPL_F32, CONV_IMPL_BF16X3, CONV_IMPL_X9 = 1, 2, 3  # rth_conv_impl: the kernel a launch runs
 HEADS_FC2_ONLY = -1
 
 
@@ -147,6 +148,7 @@ SIGNATURES = {
     "rth_relu_bias_grad_nchw": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_vp]),
     "rth_conv_supported": (c_i32, [ctypes.POINTER(ConvShape)]),
     "rth_conv_packed_bytes": (c_i64, [ctypes.POINTER(ConvShape)]),
+    "rth_conv_impl": (c_i32, [ctypes.POINTER(ConvShape), c_i64, c_vp]),
     "rth_conv_pack": (c_i32, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_vp]),
     "rth_conv_wgrad_workspace": (c_i64, [ctypes.POINTER(ConvShape)]),
     "rth_conv_relu_wgrad": (c_i32, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,

@@ -699,7 +699,7 @@ __global__ __launch_bounds__(256) void k_conv_pack(const float *__restrict__ w, 
 constexpr int kPackMax = 4;
 struct PackJob {
   int geom[kPackMax];  // index into the built geometries (find_conv order)
-  int bf16x3[kPackMax];  // conv1 u8: the bf16x3 kernel's packed form; conv2 / conv3: the x9 form
+  int bf16x3[kPackMax];  // conv1 u8: the bf16x3 kernel's packed form; conv2 / conv3: the x9 form (2: conv3 hybrid)
   const float *w[kPackMax];
   f32x4 *packed[kPackMax];
   int first_block[kPackMax + 1];
@@ -713,7 +713,7 @@ __device__ __forceinline__ void pack_one(const float *w, f32x4 *packed, int sl) 
 }
 
 // conv2's packed weights serve both of its kernels: the x9 fragments, then the fp32-MFMA image
-// (k_conv_bias_relu runs conv2 above kConv2X9Max samples, ConvLaunch::big)
+// (k_conv_bias_relu runs conv2 above conv2_x9_max() samples, ConvLaunch::big)
 using X9Conv2 = X9Geom<X9_CONV2>;
 __device__ __forceinline__ void pack_hybrid_conv2(const float *w, f32x4 *packed, int sl) {
   if (sl < X9Conv2::PACKED_U4) pack_x9<X9_CONV2>(w, reinterpret_cast<u32x4 *>(packed), sl);
@@ -721,6 +721,15 @@ __device__ __forceinline__ void pack_hybrid_conv2(const float *w, f32x4 *packed,
 }
 __global__ __launch_bounds__(256) void k_conv_pack_hybrid_conv2(const float *__restrict__ w, f32x4 *__restrict__ packed) {
   pack_hybrid_conv2(w, packed, blockIdx.x * 256 + threadIdx.x);
+}
+// conv3's: the fp32-MFMA image (small batches), then the x9 fragments (ConvLaunch::big)
+using F32Conv3 = ConvGeom<RTH_CONV_F32_NHWC, 3, 3, 1, 64, 64, 9, 9>;
+__device__ __forceinline__ void pack_hybrid_conv3(const float *w, f32x4 *packed, int sl) {
+  if (sl < F32Conv3::LDS_F4) pack_one<RTH_CONV_F32_NHWC, 3, 3, 1, 64, 64, 9, 9>(w, packed, sl);
+  else pack_x9<X9_CONV3>(w, reinterpret_cast<u32x4 *>(packed + F32Conv3::LDS_F4), sl - F32Conv3::LDS_F4);
+}
+__global__ __launch_bounds__(256) void k_conv_pack_hybrid_conv3(const float *__restrict__ w, f32x4 *__restrict__ packed) {
+  pack_hybrid_conv3(w, packed, blockIdx.x * 256 + threadIdx.x);
 }
 
 __global__ __launch_bounds__(256) void k_conv_pack_many(PackJob job) {
@@ -738,7 +747,8 @@ __global__ __launch_bounds__(256) void k_conv_pack_many(PackJob job) {
       else pack_one<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20>(job.w[l], job.packed[l], sl);
       break;
     default:
-      if (job.bf16x3[l]) pack_x9<X9_CONV3>(job.w[l], reinterpret_cast<u32x4 *>(job.packed[l]), sl);
+      if (job.bf16x3[l] == 2) pack_hybrid_conv3(job.w[l], job.packed[l], sl);
+      else if (job.bf16x3[l]) pack_x9<X9_CONV3>(job.w[l], reinterpret_cast<u32x4 *>(job.packed[l]), sl);
       else pack_one<RTH_CONV_F32_NHWC, 3, 3, 1, 64, 64, 9, 9>(job.w[l], job.packed[l], sl);
       break;
   }
@@ -769,6 +779,7 @@ static ConvLaunch x9_launch() {
                G::PACKED_U4 * 16, 1, 16, 0, 0, NSAMP, {}, nullptr, 0, 0};
   l.x9fn[1] = reinterpret_cast<const void *>(&k_conv_x9<KH, KW, S, CIN, HIN, WIN, 1, ROT>);
   if (NSAMP >= 2) l.x9fn[2] = reinterpret_cast<const void *>(&k_conv_x9<KH, KW, S, CIN, HIN, WIN, (NSAMP >= 2 ? 2 : 1), ROT>);
+  if (NSAMP >= 3) l.x9fn[3] = reinterpret_cast<const void *>(&k_conv_x9<KH, KW, S, CIN, HIN, WIN, (NSAMP >= 3 ? 3 : 1), ROT>);
   if (NSAMP >= 4) l.x9fn[4] = reinterpret_cast<const void *>(&k_conv_x9<KH, KW, S, CIN, HIN, WIN, (NSAMP >= 4 ? 4 : 1), ROT>);
   return l;
 }
@@ -812,9 +823,33 @@ static ConvLaunch conv1_bf16x3_launch() {
 #endif
 
 #ifndef CONV2_X9_MAX
-#define CONV2_X9_MAX 768
+#define CONV2_X9_MAX 0
 #endif
-constexpr int64_t kConv2X9Max = CONV2_X9_MAX;
+#ifndef CONV3_X9_MIN
+#define CONV3_X9_MIN 0
+#endif
+static int64_t env_i64(const char *name, int64_t dflt) {
+  const char *e = getenv(name);
+  return e && *e ? (int64_t)atoll(e) : dflt;
+}
+// hybrid switch points (samples): conv2 runs x9 up to RTH_CONV2_X9_MAX, conv3 runs x9 above
+// RTH_CONV3_X9_MIN (env overrides for A/B sweeps; defaults from the microbench)
+static int64_t conv2_x9_max() {
+  static const int64_t v = env_i64("RTH_CONV2_X9_MAX", CONV2_X9_MAX);
+  return v;
+}
+static int64_t conv3_x9_min() {
+  static const int64_t v = env_i64("RTH_CONV3_X9_MIN", CONV3_X9_MIN);
+  return v;
+}
+// x9 samples per workgroup = n / (CUs * RTH_X9_WG_PER_CU), rounded down to a built instantiation
+static int64_t x9_wg_per_cu() {
+  static const int64_t v = [] {
+    const int64_t x = env_i64("RTH_X9_WG_PER_CU", 1);
+    return x < 1 ? (int64_t)1 : x;
+  }();
+  return v;
+}
 
 // RTH_CONV_F32MFMA=1: conv2 / conv3 forward on the fp32-MFMA kernels instead of the exact
 // bf16x9 split (A/B and parity cross-checks)
@@ -847,14 +882,16 @@ static bool find_conv(const rth_conv_shape &s, ConvLaunch *out, int *geom = null
     *out = l;
     if (geom) *geom = 1;
   } else if (is(RTH_CONV_F32_NHWC, 32, 20, 20, 64, 4, 4, 2)) {
-    // x9 up to kConv2X9Max samples (faster there: 16.4 vs 22.5 us at 256, equal at 512), the
-    // fp32-MFMA kernel above (58 vs 61 us at 1024: two LDS-bound rounds of 2-sample workgroups)
+    // x9 up to conv2_x9_max() samples, the fp32-MFMA kernel above.  Default 0 (fp32 only):
+    // standalone the x9 kernel wins below ~400 samples (16 vs 22 us at 256), but in the Ape-X
+    // loop its 77-154 KB of LDS per workgroup crowds the concurrent stream's kernels out of the
+    // CUs, and the loop ran 0.5-1 % slower with it
     static const ConvLaunch f32 = conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB>();
     static const ConvLaunch l = [] {
-      if (conv_f32mfma()) return f32;
+      if (conv_f32mfma() || conv2_x9_max() <= 0) return f32;
       ConvLaunch h = x9_launch<X9_CONV2>();
       h.big = &f32;
-      h.big_above = kConv2X9Max;
+      h.big_above = conv2_x9_max();
       h.big_off = h.lds_bytes;
       h.lds_bytes += f32.lds_bytes;
       h.pack = reinterpret_cast<const void *>(&k_conv_pack_hybrid_conv2);
@@ -863,9 +900,20 @@ static bool find_conv(const rth_conv_shape &s, ConvLaunch *out, int *geom = null
     *out = l;
     if (geom) *geom = 2;
   } else if (is(RTH_CONV_F32_NHWC, 64, 9, 9, 64, 3, 3, 1)) {
-    static const ConvLaunch l = conv_f32mfma()
-                                    ? conv_launch<RTH_CONV_F32_NHWC, 3, 3, 1, 64, 64, 9, 9, CONV3_WAVES, CONV3_MB, CONV3_NS>()
-                                    : x9_launch<X9_CONV3>();
+    // the fp32-MFMA kernel up to conv3_x9_min() samples, x9 above (packed: fp32 image, then x9)
+    static const ConvLaunch x9 = x9_launch<X9_CONV3>();
+    static const ConvLaunch l = [] {
+      ConvLaunch f = conv_launch<RTH_CONV_F32_NHWC, 3, 3, 1, 64, 64, 9, 9, CONV3_WAVES, CONV3_MB, CONV3_NS>();
+      if (conv_f32mfma()) return f;
+      if (conv3_x9_min() <= 0) return x9;
+      f.big = &x9;
+      f.big_above = conv3_x9_min();
+      f.big_off = f.lds_bytes;
+      f.lds_bytes += x9.lds_bytes;
+      f.pack = reinterpret_cast<const void *>(&k_conv_pack_hybrid_conv3);
+      f.x9 = 0;
+      return f;
+    }();
     *out = l;
     if (geom) *geom = 3;
   } else {
@@ -913,16 +961,37 @@ struct DgradGeom {
   static_assert(G % DGRAD_D == 0, "prefetch depth must divide the chunks");
 };
 
+// XCD-aware workgroup -> (class, tile range) map (xcd != 0; the grid a multiple of 8 x NCLS):
+// consecutive workgroups land on consecutive XCDs (blockIdx % 8), each with its own L2, so
+// XCD x serves all classes of one contiguous eighth of the class tiles -- the 4 classes and
+// the neighbouring tiles that read the same gy rows share that XCD's L2 instead of fetching
+// them from HBM up to 8 times.  xcd == 0: the plain interleave (class = blockIdx % NCLS).
 template <int KH, int KW, int S, int CI, int CO, int HI, int WI, int WAVES>
 __global__ __launch_bounds__(WAVES * 64) void k_conv_dgrad(const float *__restrict__ gy, int64_t n,
-                                                          const float *__restrict__ w, float *__restrict__ gx) {
+                                                          const float *__restrict__ w, float *__restrict__ gx,
+                                                          int xcd) {
   using Gm = DgradGeom<KH, KW, S, CI, CO, HI, WI>;
   constexpr int HO = Gm::HO, WO = Gm::WO, TW = Gm::TW, CPT = Gm::CPT, NB = Gm::NB;
   constexpr int T = WAVES * 64, NCLS = S * S;
   __shared__ f32x4 wl[Gm::LDS_F4];
   const int wave = threadIdx.x / 64, lane = threadIdx.x % 64, q = lane >> 4, mr = lane & 15;
-  const int cls = blockIdx.x % NCLS, py = cls / S, px = cls % S;
-  const int64_t wg = blockIdx.x / NCLS, nwg = gridDim.x / NCLS;
+  const int64_t PC = n * Gm::JH * Gm::JW, tiles = (PC + 15) / 16;
+  int cls;
+  int64_t wg, nwg, tile_lo = 0, tile_hi = tiles;
+  if (xcd) {
+    const int x = (int)(blockIdx.x % 8), slot = (int)(blockIdx.x / 8);
+    cls = slot % NCLS;
+    wg = slot / NCLS;
+    nwg = gridDim.x / (8 * NCLS);
+    const int64_t per = (tiles + 7) / 8;
+    tile_lo = x * per;
+    tile_hi = tile_lo + per < tiles ? tile_lo + per : tiles;
+  } else {
+    cls = blockIdx.x % NCLS;
+    wg = blockIdx.x / NCLS;
+    nwg = gridDim.x / NCLS;
+  }
+  const int py = cls / S, px = cls % S;
 
   // stage this class's taps: slot (g * NB + nb) * 64 + lane, chunk g = (tap, 16 co)
   for (int sl = threadIdx.x; sl < Gm::LDS_F4; sl += T) {
@@ -935,9 +1004,8 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_dgrad(const float *__restri
   }
   __syncthreads();
 
-  const int64_t PC = n * Gm::JH * Gm::JW, tiles = (PC + 15) / 16;
   const f32x4 *wlane = wl + lane;
-  for (int64_t tile = wg * WAVES + wave; tile < tiles; tile += nwg * WAVES) {
+  for (int64_t tile = tile_lo + wg * WAVES + wave; tile < tile_hi; tile += nwg * WAVES) {
     int64_t p = tile * 16 + mr;
     if (p >= PC) p = PC - 1;  // tail lanes compute a duplicate pixel, never stored
     const int64_t b = p / (Gm::JH * Gm::JW);
@@ -986,6 +1054,11 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_dgrad(const float *__restri
       }
     }
   }
+}
+
+static int dgrad_xcd() {  // RTH_DGRAD_XCD=0: the plain class interleave (A/B)
+  static const int v = (int)env_i64("RTH_DGRAD_XCD", 1) != 0;
+  return v;
 }
 
 struct DgradLaunch {
@@ -1374,6 +1447,18 @@ int rth_conv_supported(const rth_conv_shape *shape) {
   return (shape->input & RTH_CONV_OUT_NCHW) && l.bf16x3 ? 0 : 1;  // NCHW output: not the conv1 u8 kernel
 }
 
+static void select_launch(ConvLaunch *l, int64_t n, int64_t *w_off, int64_t *nsamp);
+
+int rth_conv_impl(const rth_conv_shape *shape, int64_t n, int32_t *nsamp_out) {
+  ConvLaunch l;
+  if (nsamp_out) *nsamp_out = 0;
+  if (!shape || n < 1 || !find_conv(*shape, &l)) return 0;
+  int64_t w_off = 0, nsamp = 0;
+  select_launch(&l, n, &w_off, &nsamp);
+  if (nsamp_out) *nsamp_out = (int32_t)nsamp;
+  return l.x9 ? RTH_CONV_IMPL_X9 : (l.bf16x3 ? RTH_CONV_IMPL_BF16X3 : RTH_CONV_IMPL_F32);
+}
+
 int64_t rth_conv_packed_bytes(const rth_conv_shape *shape) {
   ConvLaunch l;
   return shape && find_conv(*shape, &l) ? (int64_t)l.lds_bytes : 0;
@@ -1405,7 +1490,9 @@ int rth_conv_pack_many(int32_t n, const rth_conv_shape *shapes, const float *con
                 "rth_conv_pack_many: layer %d buffer NULL or misaligned", l);
     job.w[l] = w[l];
     job.packed[l] = reinterpret_cast<f32x4 *>(packed[l]);
-    job.bf16x3[l] = cl.bf16x3 || cl.x9;
+    // packed form: 1 = the bf16x3 / x9 (or conv2's x9-first hybrid) image, 2 = conv3's
+    // fp32-first hybrid
+    job.bf16x3[l] = (cl.big && !cl.x9) ? 2 : (cl.bf16x3 || cl.x9) ? 1 : 0;
     job.first_block[l] = blocks;
     blocks += (cl.lds_bytes / 16 + 255) / 256;
   }
@@ -1474,6 +1561,29 @@ int rth_conv_relu_wgrad(const rth_conv_shape *shape, const void *x, const int64_
   return rth_conv_relu_wgrad_ex(shape, x, rows, n, g, y, gw, gb, workspace, nullptr, 0, stream);
 }
 
+// the kernel a hybrid geometry runs for n samples (*l becomes it; its packed weights start at
+// byte *w_off) and, for the x9 kernels, the samples per workgroup: the built instantiation with
+// the least estimated time, rounds x per-round time, where one workgroup is resident per CU (the
+// kernel's ~160-220 VGPRs) and a round of s-sample workgroups takes ~(s + 0.5) single-sample
+// times (microbench: conv3 12.3 / 20.6 / 37.2 us for s = 1 / 2 / 4 on 256 CUs, conv2 15.8 / 31 us)
+static void select_launch(ConvLaunch *l, int64_t n, int64_t *w_off, int64_t *nsamp) {
+  *w_off = 0;
+  *nsamp = 0;
+  if (l->big && n > l->big_above) {
+    *w_off = l->big_off;
+    *l = *l->big;
+  }
+  if (!l->x9) return;
+  const int64_t slots = (int64_t)cu_count() * x9_wg_per_cu();
+  double best = 0.0;
+  for (int64_t s = 1; s <= l->x9; ++s) {
+    if (!l->x9fn[s]) continue;
+    const int64_t rounds = ((n + s - 1) / s + slots - 1) / slots;
+    const double cost = (double)rounds * ((double)s + 0.5);
+    if (*nsamp == 0 || cost < best) best = cost, *nsamp = s;
+  }
+}
+
 static int conv_bias_relu(const rth_conv_shape *shape, const void *x, const int64_t *rows, int64_t n,
                           const int64_t *n_dev, const float *w, const float *bias, float *y, void *stream) {
   RTH_REQUIRE(shape && x && w && bias && y && n >= 0, "rth_conv_bias_relu: NULL argument");
@@ -1489,15 +1599,11 @@ static int conv_bias_relu(const rth_conv_shape *shape, const void *x, const int6
                                                    : (reinterpret_cast<uintptr_t>(x) & 15) == 0),
               "rth_conv_bias_relu: misaligned buffer");
   if (n == 0) return RTH_OK;
-  if (l.big && n > l.big_above) {  // a hybrid geometry's fp32-MFMA kernel for large batches
-    w = reinterpret_cast<const float *>(reinterpret_cast<const uint8_t *>(w) + l.big_off);
-    l = *l.big;
-  }
-  if (l.x9) {  // one workgroup per nsamp samples (nsamp: enough workgroups for every CU first)
+  int64_t w_off = 0, nsamp = 0;
+  select_launch(&l, n, &w_off, &nsamp);
+  w = reinterpret_cast<const float *>(reinterpret_cast<const uint8_t *>(w) + w_off);
+  if (l.x9) {  // one workgroup per nsamp samples
     RTH_REQUIRE(input == RTH_CONV_F32_NHWC, "rth_conv_bias_relu: the x9 kernels read f32 NHWC input");
-    int64_t nsamp = n / cu_count();  // samples per workgroup: a built instantiation, >= 1 workgroup per CU
-    nsamp = nsamp < 1 ? 1 : (nsamp > l.x9 ? l.x9 : nsamp);
-    while (!l.x9fn[nsamp]) --nsamp;
     const int ns = (int)nsamp;
     const int64_t grid = (n + nsamp - 1) / nsamp;
     const float *xf = static_cast<const float *>(x);
@@ -1537,8 +1643,10 @@ int rth_conv_dgrad(const rth_conv_shape *shape, const float *gy, int64_t n, cons
   int64_t per_class = (tiles + l.waves - 1) / l.waves;
   const int64_t resident = (int64_t)cu_count() * l.per_cu / l.classes;
   if (per_class > resident) per_class = resident > 0 ? resident : 1;
+  const int xcd = dgrad_xcd();
+  if (xcd) per_class = (per_class + 7) / 8 * 8;  // whole XCD groups (spare workgroups find no tile)
   const int64_t grid = per_class * l.classes;
-  void *args[] = {(void *)&gy, (void *)&n, (void *)&w, (void *)&gx};
+  void *args[] = {(void *)&gy, (void *)&n, (void *)&w, (void *)&gx, (void *)&xcd};
   RTH_HIP(hipLaunchKernel(l.fn, dim3((unsigned)grid), dim3(l.waves * 64), args, 0, as_stream(stream)));
   return RTH_OK;
 }

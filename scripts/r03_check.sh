@@ -27,6 +27,7 @@ for s in "$@"; do
        step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv --kernel-include-regex "rth::" \
           -d "$PWD/gpurun_out/pmc_write" -o run -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-sweep ;;
     c) step conv_tests 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_conv_gpu.py tests/test_fused_learner_gpu.py
+       RTH_CONV2_X9_MAX=512 RTH_CONV3_X9_MIN=600 step conv_tests_hybrid 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_conv_gpu.py
        CONV_NS=1024,512,256 step bench_conv_x9 300 python scripts/bench_conv.py
        RTH_CONV_F32MFMA=1 CONV_NS=1024,512,256 step bench_conv_f32 300 python scripts/bench_conv.py ;;
     q) step bench_quick 600 python bench.py --steps 100 --warmup 20 --no-cpu-baseline ${BENCH_ARGS:-}

@@ -40,8 +40,13 @@ HBM_KERNELS = {"k_tree_update_sub": ("k_tree_update_sub", None), "k_tree_sample"
                "k_copy_rows (gather)": ("k_copy_rows", "gather"), "k_copy_rows (insert)": ("k_copy_rows", "insert"),
                "k_actor_tail": ("k_actor_tail", None), "k_td_heads_backward": ("k_td_heads_backward", None),
                "k_adam": ("k_adam", None)}
-CONV2 = "k_conv_bias_relu<0, 4, 4, 2, 32, 64, 20, 20"  # conv2 forward
-CONV3 = "k_conv_bias_relu<0, 3, 3, 1, 64, 64, 9, 9"  # conv3 forward (the step's dominant kernel)
+# conv2 / conv3 forward: the fp32-MFMA kernel or the exact-split bf16 one (k_conv_x9)
+CONV2 = ("k_conv_bias_relu<0, 4, 4, 2, 32, 64, 20, 20", "k_conv_x9<4, 4, 2, 32, 20, 20")
+CONV3 = ("k_conv_bias_relu<0, 3, 3, 1, 64, 64, 9, 9", "k_conv_x9<3, 3, 1, 64, 9, 9")
+
+
+def is_conv(pats, name):
+    return any(p in name for p in pats)
 
 
 def main():
@@ -92,12 +97,13 @@ def main():
                                           "bench.py's live roofline); the actor stream: target pass (512), actors (256)")):
             by_grid = collections.defaultdict(list)
             for r in win:
-                if name in r["Kernel_Name"]:
+                if (is_conv(name, r["Kernel_Name"]) if isinstance(name, tuple) else name in r["Kernel_Name"]):
                     where = "learner stream" if r.get("Stream_Id") == learner_stream else f"stream {r.get('Stream_Id')}"
                     by_grid[(r["Grid_Size_X"], r["Grid_Size_Y"], where)].append(
                         int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
             with open(os.path.join(PROF, f"{tag}_{fn}.txt"), "w") as f:
-                f.write(f"# {name} launches in the timed window, by grid (threads x, y)\n{head}\n")
+                f.write(f"# {' | '.join(name) if isinstance(name, tuple) else name} launches in the timed window, "
+                        f"by grid (threads x, y)\n{head}\n")
                 for k, v in sorted(by_grid.items(), key=lambda kv: (int(kv[0][0]) * int(kv[0][1]), kv[0][2])):
                     f.write(f"grid={k} launches={len(v)} avg_us={st.mean(v) / 1e3:.2f} min_us={min(v) / 1e3:.2f} "
                             f"max_us={max(v) / 1e3:.2f}\n")
@@ -128,7 +134,7 @@ def main():
                         "gather_hbm_bytes_per_launch": round((2 * st.median(fe[key]) + st.median(wr[key])) * 1024),
                         "gather_dispatches": len(fe[key])})
         for name, conv in (("conv2", CONV2), ("conv3", CONV3)):
-            cs = [k for k in fe if conv in k[0] and k in wr]
+            cs = [k for k in fe if is_conv(conv, k[0]) and k in wr]
             if cs:
                 key = max(cs, key=lambda k: k[1])  # the learner's launch: the largest grid
                 out.update({f"{name}_kernel": key[0] + " (the learner's [s0; s1] forward: the largest grid, "

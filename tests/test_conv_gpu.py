@@ -114,9 +114,10 @@ def test_conv_empty_and_unsupported(dev):
     assert _lib.lib().rth_conv_packed_bytes(_lib.ctypes.byref(bad)) == 0
     import os
 
-    # conv2's packed weights: one fp32 copy (RTH_CONV_F32MFMA), or by default the three bf16
-    # terms of the exact split (the x9 kernel, small batches) followed by the fp32 copy (large)
-    per = 4 if os.environ.get("RTH_CONV_F32MFMA") else 3 * 2 + 4
+    # conv2's packed weights: by default one fp32 copy; with the opt-in x9 kernel for small
+    # batches (RTH_CONV2_X9_MAX > 0) the three bf16 terms of the exact split, then the fp32 copy
+    x9 = int(os.environ.get("RTH_CONV2_X9_MAX", "0") or 0) > 0 and not os.environ.get("RTH_CONV_F32MFMA")
+    per = 3 * 2 + 4 if x9 else 4
     assert _lib.lib().rth_conv_packed_bytes(_lib.ctypes.byref(shape)) == 64 * 32 * 16 * per
     with pytest.raises(_lib.RethHipError, match="not built"):
         _lib.call("rth_conv_bias_relu", _lib.ctypes.byref(bad), x.data_ptr(), None, 1, w.data_ptr(), w.data_ptr(),
@@ -458,3 +459,31 @@ def test_conv_fp32_grade_accuracy(dev, gi, n):
     e_ours, e_t32 = (got - want).abs().max().item(), (t32 - want).abs().max().item()
     print(f"conv{gi + 1} n={n}: ours {e_ours:.3e} torch-fp32 {e_t32:.3e}")
     assert e_ours <= 4 * e_t32 + 1e-7, (e_ours, e_t32)
+
+
+def test_conv_impl_selection(dev):
+    """rth_conv_impl names the kernel a launch runs: conv1 on uint8 stacks the bf16x3 kernel,
+    conv2 the fp32-MFMA kernel (x9 opt-in below RTH_CONV2_X9_MAX), conv3 the x9 kernel with the
+    samples per workgroup of the cost model (one round of at most 4-sample workgroups on 256
+    CUs when the batch allows)"""
+    import ctypes
+    import os
+
+    from reth_amd import _lib
+
+    if os.environ.get("RTH_CONV_F32MFMA") or os.environ.get("RTH_CONV2_X9_MAX") or os.environ.get("RTH_CONV3_X9_MIN"):
+        pytest.skip("non-default conv selection in the environment")
+    ns = ctypes.c_int32(-1)
+    impl = lambda sh, n: (_lib.lib().rth_conv_impl(ctypes.byref(sh), n, ctypes.byref(ns)), ns.value)
+    u8 = _shape(_lib.CONV_U8_CHW, *GEOMS[0])
+    assert impl(u8, 1024) == (_lib.CONV_IMPL_BF16X3, 0)
+    assert impl(_shape(_lib.CONV_F32_NHWC, *GEOMS[1]), 256) == (_lib.CONV_IMPL_F32, 0)
+    c3 = _shape(_lib.CONV_F32_NHWC | _lib.CONV_OUT_NCHW, *GEOMS[2])
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    for n in (1, cus // 2, cus, 2 * cus, 3 * cus, 4 * cus, 6 * cus):
+        kind, s = impl(c3, n)
+        assert kind == _lib.CONV_IMPL_X9 and 1 <= s <= 4, (n, kind, s)
+        rounds = lambda q: -(-(-(-n // q)) // cus)
+        # the chosen instantiation's estimated time is the least of the built ones
+        assert all(rounds(s) * (s + 0.5) <= rounds(q) * (q + 0.5) for q in (1, 2, 3, 4)), (n, s)
+    assert impl(c3, 0)[0] == 0 and impl(_shape(_lib.CONV_F32_NHWC, 3, 84, 84, 32, 8, 4), 8)[0] == 0

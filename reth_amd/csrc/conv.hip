@@ -438,10 +438,11 @@ __global__ __launch_bounds__(256) void k_conv1_pack_bf16x3(const float *__restri
 // M-tiles of 16 output pixels of the workgroup's samples.  The two K halves meet in LDS
 // (fixed order: first half + second half, then + bias, ReLU), and the output leaves as one
 // contiguous run per workgroup (NHWC, or NCHW for FC1) in 16-byte stores.
-template <int KH, int KW, int S, int CIN, int HIN, int WIN, int NSAMP, int ROT>
+template <int KH, int KW, int S, int CIN, int HIN, int WIN, int NSAMP, int ROT, int KS>
 struct X9Geom {
   static constexpr int COUT = 64, HOUT = (HIN - KH) / S + 1, WOUT = (WIN - KW) / S + 1, PIX = HOUT * WOUT;
-  static constexpr int K = KH * KW * CIN, NCH = K / 32, NCH2 = NCH / 2;  // 32-deep chunks, per K half
+  static constexpr int K = KH * KW * CIN, NCH = K / 32, NCHP = NCH / KS;  // 32-deep chunks, per K part
+  static constexpr int NT = 256 * KS;                                     // threads: 4 channel blocks x KS
   static constexpr int TILES = (NSAMP * PIX + 15) / 16;                  // 16-pixel M-tiles
   static constexpr int NG = CIN / 8;                                     // 16-byte ci groups
   static constexpr int ROWS = NSAMP * HIN * WIN;                         // staged input pixels
@@ -450,7 +451,7 @@ struct X9Geom {
   static constexpr int OUT_F = NSAMP * COUT * PIX;                       // output staging floats
   static constexpr int PACKED_U4 = (COUT / 16) * NCH * 3 * 64;           // packed weight fragments
   static_assert(CIN % 32 == 0 || 32 % CIN == 0, "a 32-deep chunk must stay inside one tap");
-  static_assert(CIN % 8 == 0 && K % 64 == 0, "K must split into two halves of 32-deep chunks");
+  static_assert(CIN % 8 == 0 && NCH % KS == 0 && KS >= 1 && KS <= 4, "K must split into KS parts of 32-deep chunks");
   static_assert(OUT_F * 4 <= LDS_U4 * 16, "output staging must fit the input image");
   static_assert(LDS_U4 * 16 <= 163840, "LDS image too large");
   __device__ static int swz(int r) { return (r & ~15) | ((r + (r >> 5) * ROT) & 15); }
@@ -472,13 +473,13 @@ __device__ __forceinline__ void split3_x4(float4 v, uint2 (&out)[3]) {
   for (int k = 0; k < 3; ++k) out[k] = make_uint2(t[k][0] | (t[k][1] << 16), t[k][2] | (t[k][3] << 16));
 }
 
-template <int KH, int KW, int S, int CIN, int HIN, int WIN, int NSAMP, int ROT>
-__global__ __launch_bounds__(512, 2) void k_conv_x9(const float *__restrict__ x, int64_t n,
+template <int KH, int KW, int S, int CIN, int HIN, int WIN, int NSAMP, int ROT, int KS>
+__global__ __launch_bounds__(256 * KS) void k_conv_x9(const float *__restrict__ x, int64_t n,
                                                     const int64_t *__restrict__ n_dev, int nsamp,
                                                     const u32x4 *__restrict__ wpk, const float *__restrict__ bias,
                                                     float *__restrict__ y, int out_nchw) {
-  using G = X9Geom<KH, KW, S, CIN, HIN, WIN, NSAMP, ROT>;
-  constexpr int PIX = G::PIX, NCH2 = G::NCH2, NG = G::NG, PLANE = G::PLANE, COUT = G::COUT;
+  using G = X9Geom<KH, KW, S, CIN, HIN, WIN, NSAMP, ROT, KS>;
+  constexpr int PIX = G::PIX, NCH2 = G::NCHP, NG = G::NG, PLANE = G::PLANE, COUT = G::COUT, NT = G::NT;
   __shared__ uint4 lds[G::LDS_U4];
   if (n_dev) {
     const int64_t m = *n_dev;
@@ -491,7 +492,7 @@ __global__ __launch_bounds__(512, 2) void k_conv_x9(const float *__restrict__ x,
   const int nv = ns * PIX;  // valid output pixels
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int cb = wave & 3, half = wave >> 2;
+  const int cb = wave & 3, half = wave >> 2;  // channel block, K part
 
   // this wave's B fragments: channels 16 cb + (lane & 15), chunks [half * NCH2, +NCH2), 3 terms
   bf16x8 wf[NCH2][3];
@@ -515,7 +516,7 @@ __global__ __launch_bounds__(512, 2) void k_conv_x9(const float *__restrict__ x,
   constexpr int SA = (RA + 15) / 16 * CB * 64;       // lane slots of phase A
   constexpr int RB_ = (NSAMP - NA) * HIN * WIN;      // ... of phase B
   constexpr int SB = (RB_ + 15) / 16 * CB * 64;
-  constexpr int UA = (SA + 511) / 512, UB = SB > 0 ? (SB + 511) / 512 : 1;
+  constexpr int UA = (SA + NT - 1) / NT, UB = SB > 0 ? (SB + NT - 1) / NT : 1;
   const float4 *xs = reinterpret_cast<const float4 *>(x + b0 * (int64_t)(HIN * WIN * CIN));
   const int rows = ns * HIN * WIN;
   auto slot_of = [&](int i, int r0, int &rr, int &c4) {
@@ -542,15 +543,15 @@ __global__ __launch_bounds__(512, 2) void k_conv_x9(const float *__restrict__ x,
   {
     float4 va[UA];
 #pragma unroll
-    for (int u = 0; u < UA; ++u) va[u] = tid + u * 512 < SA ? fetch(tid + u * 512, 0, RA) : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int u = 0; u < UA; ++u) va[u] = tid + u * NT < SA ? fetch(tid + u * NT, 0, RA) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int u = 0; u < UA; ++u)
-      if (tid + u * 512 < SA) commit(va[u], tid + u * 512, 0, RA);
+      if (tid + u * NT < SA) commit(va[u], tid + u * NT, 0, RA);
   }
   float4 vb[UB];
   if constexpr (SB > 0) {
 #pragma unroll
-    for (int u = 0; u < UB; ++u) vb[u] = tid + u * 512 < SB ? fetch(tid + u * 512, RA, RA + RB_) : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int u = 0; u < UB; ++u) vb[u] = tid + u * NT < SB ? fetch(tid + u * NT, RA, RA + RB_) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   const float bl = bias[cb * 16 + (lane & 15)];
   __syncthreads();
@@ -616,7 +617,7 @@ __global__ __launch_bounds__(512, 2) void k_conv_x9(const float *__restrict__ x,
     if constexpr (SB > 0) {
 #pragma unroll
       for (int u = 0; u < UB; ++u)
-        if (tid + u * 512 < SB) commit(vb[u], tid + u * 512, RA, RA + RB_);
+        if (tid + u * NT < SB) commit(vb[u], tid + u * NT, RA, RA + RB_);
     }
     __syncthreads();
     load(QA);
@@ -634,16 +635,23 @@ __global__ __launch_bounds__(512, 2) void k_conv_x9(const float *__restrict__ x,
     return out_nchw ? (s * COUT + co) * PIX + (p - s * PIX) : p * COUT + co;
   };
   __syncthreads();  // every wave is done reading the input image
-  if (half == 1) {
+  // parts KS-1 .. 1 in turn: the last stores, each earlier one adds its own first
 #pragma unroll
-    for (int tile = 0; tile < G::TILES; ++tile)
+  for (int pt = KS - 1; pt >= 1; --pt) {
+    if (half == pt) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int p = tile * 16 + 4 * g + i;
-        if (p < nv) F[fidx(p)] = acc[tile][i];
-      }
+      for (int tile = 0; tile < G::TILES; ++tile)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int p = tile * 16 + 4 * g + i;
+          if (p < nv) {
+            const int f = fidx(p);
+            F[f] = pt == KS - 1 ? acc[tile][i] : radd(acc[tile][i], F[f]);
+          }
+        }
+    }
+    __syncthreads();
   }
-  __syncthreads();
   if (half == 0) {
 #pragma unroll
     for (int tile = 0; tile < G::TILES; ++tile)
@@ -661,15 +669,15 @@ __global__ __launch_bounds__(512, 2) void k_conv_x9(const float *__restrict__ x,
     const int total4 = nv * COUT / 4;  // the run [b0, b0 + ns) of y is contiguous in both layouts
     float4 *yo = reinterpret_cast<float4 *>(y + b0 * (int64_t)(COUT * PIX));
     const float4 *Fs = reinterpret_cast<const float4 *>(F);
-    for (int i = tid; i < total4; i += 512) yo[i] = Fs[i];
+    for (int i = tid; i < total4; i += NT) yo[i] = Fs[i];
   }
 }
 
 // OHWI weights -> the B fragments of k_conv_x9: slot ((cb * NCH + c) * 3 + t) * 64 + lane holds
 // term t of W[16 cb + (lane & 15)][32 c + 8 (lane >> 4) + j], j = 0..7 (k = (kh, kw, ci), ci fastest)
-template <int KH, int KW, int S, int CIN, int HIN, int WIN, int NSAMP, int ROT>
+template <int KH, int KW, int S, int CIN, int HIN, int WIN, int NSAMP, int ROT, int KS>
 __device__ __forceinline__ void pack_x9(const float *__restrict__ w, u32x4 *__restrict__ packed, int sl) {
-  using G = X9Geom<KH, KW, S, CIN, HIN, WIN, NSAMP, ROT>;
+  using G = X9Geom<KH, KW, S, CIN, HIN, WIN, NSAMP, ROT, KS>;
   if (sl >= G::PACKED_U4) return;
   const int lane = sl % 64, t = (sl / 64) % 3, c = (sl / 192) % G::NCH, cb = sl / (192 * G::NCH);
   const int co = cb * 16 + (lane & 15), k0 = c * 32 + 8 * (lane >> 4);
@@ -679,13 +687,21 @@ __device__ __forceinline__ void pack_x9(const float *__restrict__ w, u32x4 *__re
   packed[sl] = u32x4{e[0] | (e[1] << 16), e[2] | (e[3] << 16), e[4] | (e[5] << 16), e[6] | (e[7] << 16)};
 }
 
-template <int KH, int KW, int S, int CIN, int HIN, int WIN, int NSAMP, int ROT>
+template <int KH, int KW, int S, int CIN, int HIN, int WIN, int NSAMP, int ROT, int KS>
 __global__ __launch_bounds__(256) void k_conv_pack_x9(const float *__restrict__ w, u32x4 *__restrict__ packed) {
-  pack_x9<KH, KW, S, CIN, HIN, WIN, NSAMP, ROT>(w, packed, blockIdx.x * 256 + threadIdx.x);
+  pack_x9<KH, KW, S, CIN, HIN, WIN, NSAMP, ROT, KS>(w, packed, blockIdx.x * 256 + threadIdx.x);
 }
 
-#define X9_CONV2 4, 4, 2, 32, 20, 20, 2, 10
-#define X9_CONV3 3, 3, 1, 64, 9, 9, 4, 3
+// K parts per workgroup (waves = 4 channel blocks x KS): more parts, fewer weight registers per
+// wave and more waves per CU
+#ifndef X9_CONV2_KS
+#define X9_CONV2_KS 2
+#endif
+#ifndef X9_CONV3_KS
+#define X9_CONV3_KS 2
+#endif
+#define X9_CONV2 4, 4, 2, 32, 20, 20, 2, 10, X9_CONV2_KS
+#define X9_CONV3 3, 3, 1, 64, 9, 9, 4, 3, X9_CONV3_KS
 
 // OHWI weights -> MFMA fragment order (the LDS image the conv kernel copies)
 template <int MODE, int KH, int KW, int S, int CIN, int COUT, int HIN, int WIN>
@@ -771,16 +787,16 @@ struct ConvLaunch {
   int big_off;
 };
 
-template <int KH, int KW, int S, int CIN, int HIN, int WIN, int NSAMP, int ROT>
+template <int KH, int KW, int S, int CIN, int HIN, int WIN, int NSAMP, int ROT, int KS>
 static ConvLaunch x9_launch() {
-  using G = X9Geom<KH, KW, S, CIN, HIN, WIN, NSAMP, ROT>;
-  ConvLaunch l{reinterpret_cast<const void *>(&k_conv_x9<KH, KW, S, CIN, HIN, WIN, NSAMP, ROT>),
-               reinterpret_cast<const void *>(&k_conv_pack_x9<KH, KW, S, CIN, HIN, WIN, NSAMP, ROT>), 8,
+  using G = X9Geom<KH, KW, S, CIN, HIN, WIN, NSAMP, ROT, KS>;
+  ConvLaunch l{reinterpret_cast<const void *>(&k_conv_x9<KH, KW, S, CIN, HIN, WIN, NSAMP, ROT, KS>),
+               reinterpret_cast<const void *>(&k_conv_pack_x9<KH, KW, S, CIN, HIN, WIN, NSAMP, ROT, KS>), 4 * KS,
                G::PACKED_U4 * 16, 1, 16, 0, 0, NSAMP, {}, nullptr, 0, 0};
-  l.x9fn[1] = reinterpret_cast<const void *>(&k_conv_x9<KH, KW, S, CIN, HIN, WIN, 1, ROT>);
-  if (NSAMP >= 2) l.x9fn[2] = reinterpret_cast<const void *>(&k_conv_x9<KH, KW, S, CIN, HIN, WIN, (NSAMP >= 2 ? 2 : 1), ROT>);
-  if (NSAMP >= 3) l.x9fn[3] = reinterpret_cast<const void *>(&k_conv_x9<KH, KW, S, CIN, HIN, WIN, (NSAMP >= 3 ? 3 : 1), ROT>);
-  if (NSAMP >= 4) l.x9fn[4] = reinterpret_cast<const void *>(&k_conv_x9<KH, KW, S, CIN, HIN, WIN, (NSAMP >= 4 ? 4 : 1), ROT>);
+  l.x9fn[1] = reinterpret_cast<const void *>(&k_conv_x9<KH, KW, S, CIN, HIN, WIN, 1, ROT, KS>);
+  if (NSAMP >= 2) l.x9fn[2] = reinterpret_cast<const void *>(&k_conv_x9<KH, KW, S, CIN, HIN, WIN, (NSAMP >= 2 ? 2 : 1), ROT, KS>);
+  if (NSAMP >= 3) l.x9fn[3] = reinterpret_cast<const void *>(&k_conv_x9<KH, KW, S, CIN, HIN, WIN, (NSAMP >= 3 ? 3 : 1), ROT, KS>);
+  if (NSAMP >= 4) l.x9fn[4] = reinterpret_cast<const void *>(&k_conv_x9<KH, KW, S, CIN, HIN, WIN, (NSAMP >= 4 ? 4 : 1), ROT, KS>);
   return l;
 }
 
@@ -1609,7 +1625,7 @@ static int conv_bias_relu(const rth_conv_shape *shape, const void *x, const int6
     const float *xf = static_cast<const float *>(x);
     void *args[] = {(void *)&xf, (void *)&n, (void *)&n_dev, (void *)&ns, (void *)&w, (void *)&bias, (void *)&y,
                     (void *)&out_nchw};
-    RTH_HIP(hipLaunchKernel(l.x9fn[nsamp], dim3((unsigned)grid), dim3(512), args, 0, as_stream(stream)));
+    RTH_HIP(hipLaunchKernel(l.x9fn[nsamp], dim3((unsigned)grid), dim3(l.waves * 64), args, 0, as_stream(stream)));
     return RTH_OK;
   }
   const int hout = (shape->hin - shape->kh) / shape->stride + 1, wout = (shape->win - shape->kw) / shape->stride + 1;

@@ -59,9 +59,10 @@ class VecActors:
         self.ring = ring
         dev = self.device
         N = self.N
-        # one extra all-zero stack at N * ring: the sink handle of unused batch slots
-        self.frames = torch.empty((N * ring + 1, *OBS_SHAPE), dtype=torch.uint8, device=dev)
-        self.frames[N * ring].zero_()
+        # one extra all-zero stack at N * ring: the sink handle of unused batch slots.  Zero-filled
+        # once: ring slots no step has written yet read as zeros, never as whatever the
+        # allocator's block held before (graph and eager runs of one seed compare equal)
+        self.frames = torch.zeros((N * ring + 1, *OBS_SHAPE), dtype=torch.uint8, device=dev)
         self.cur_slot = torch.empty(N, dtype=torch.int64, device=dev)
         e = apex_epsilons(N, actor_offset, total_actors) if eps is None else np.broadcast_to(np.asarray(eps, np.float64), (N,))
         self.eps = torch.as_tensor(np.ascontiguousarray(e), dtype=torch.float64, device=dev)

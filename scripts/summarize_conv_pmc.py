@@ -1,6 +1,7 @@
-"""Summarise the conv counter passes (scripts/pmc_conv.sh -> gpurun_out/pmc_conv_*, the fp32-MFMA
-kernels; scripts/pmc_x9.sh -> gpurun_out/pmc_x9_*, the exact-split bf16 kernels) of
+"""Summarise the conv counter passes (scripts/pmc_conv.sh -> gpurun_out/pmc_conv_*, the default
+build's kernels; scripts/pmc_x9.sh -> gpurun_out/pmc_x9_*, the exact-split bf16 kernels) of
 scripts/conv_pmc.py (CONV_N = 1,024 samples, the learner's [s0; s1]) into profiles/TAG_pmc_conv.txt.
+gpurun_out/pmc_f32_* holds an earlier pmc_conv.sh run of the fp32-MFMA conv3 (copied aside).
 
 Per kernel (median over its dispatches of each pass; every pass is its own run):
   wave-cycle split     SQ_WAIT_ANY / SQ_WAIT_INST_ANY / SQ_ACTIVE_INST_ANY over SQ_WAVE_CYCLES
@@ -43,8 +44,9 @@ def load(path):
 def main():
     tag = sys.argv[1] if len(sys.argv) > 1 else "r03"
     lines = [__doc__.split("\n\n")[1].strip(), ""]
-    for fam, label in (("pmc_conv", "fp32-MFMA kernels (k_conv_bias_relu) and k_conv_dgrad"),
-                       ("pmc_x9", "exact-split bf16 kernels (k_conv_x9)")):
+    for fam, label in (("pmc_conv", "the default build: conv1 bf16x3, conv2 fp32 MFMA, conv3 x9, conv2 dgrad"),
+                       ("pmc_f32", "the fp32-MFMA conv3 (RTH_CONV_F32MFMA=1 path; r03 mid-round build)"),
+                       ("pmc_x9", "the exact-split bf16 kernels for conv2 (opt-in) and conv3 (scripts/pmc_x9.sh)")):
         passes = {p: load(f"{fam}_{p}") for p in ("sq", "inst", "fetch", "write", "l2", "ic")}
         keys = sorted(set().union(*[set(d) for d in passes.values()]))
         if not keys:

@@ -462,6 +462,13 @@ int rth_conv_dgrad(const rth_conv_shape *shape, const float *gy_dev, int64_t n, 
  * x = [n, hin, win, cin] and gy = [n, hout, wout, cout] (already ReLU-masked), on the fp32
  * MFMA; every sum has a fixed order (deterministic).  `shape` is the forward convolution's
  * (input RTH_CONV_F32_NHWC); workspace = rth_conv_wgrad_f32_workspace(shape) bytes. */
+/* The same on the bf16 MFMA with both operands split into three exact bf16 terms (nine
+ * products per fp32 product, exact in the fp32 accumulator: the fp32 path's products in
+ * another fixed summation order); workspace = rth_conv_wgrad_x9_workspace(shape) bytes. */
+int rth_conv_wgrad_x9_supported(const rth_conv_shape *shape);
+int64_t rth_conv_wgrad_x9_workspace(const rth_conv_shape *shape);
+int rth_conv_wgrad_x9(const rth_conv_shape *shape, const float *x_dev, int64_t n, const float *gy_dev, float *gw_dev,
+                      void *workspace_dev, void *stream);
 int rth_conv_wgrad_f32_supported(const rth_conv_shape *shape);
 int64_t rth_conv_wgrad_f32_workspace(const rth_conv_shape *shape);
 int rth_conv_wgrad_f32(const rth_conv_shape *shape, const float *x_dev, int64_t n, const float *gy_dev, float *gw_dev,

@@ -25,6 +25,34 @@ __host__ __device__ __forceinline__ double radd(double a, double b) { return a +
 __host__ __device__ __forceinline__ double rsub(double a, double b) { return a - b; }
 __host__ __device__ __forceinline__ double rmul(double a, double b) { return a * b; }
 
+// bf16 MFMA operands and the exact three-term bf16 split of fp32 values (conv.hip, wgrad.hip):
+// every fp32 v is h1 + h2 + h3 exactly, h1 = rne(v), h2 = rne(v - h1), h3 = rne(v - h1 - h2)
+// (8 + 8 + 8 significand bits; each residual is a difference of nearby floats, so exact)
+using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
+using u32x4 = __attribute__((ext_vector_type(4))) uint32_t;
+__host__ __device__ __forceinline__ uint32_t bf16_rne_bits(float f) {
+  uint32_t u = __float_as_uint(f);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return u >> 16;
+}
+__host__ __device__ __forceinline__ float bf16_bits_f(uint32_t b) { return __uint_as_float(b << 16); }
+// the three bf16 terms of 4 fp32 values, packed 2 per dword: out[t] = {t(v0) | t(v1) << 16, ...}
+__device__ __forceinline__ void split3_x4(float4 v, uint2 (&out)[3]) {
+  const float in[4] = {v.x, v.y, v.z, v.w};
+  uint32_t t[3][4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const uint32_t h1 = bf16_rne_bits(in[e]);
+    const float r1 = rsub(in[e], bf16_bits_f(h1));
+    const uint32_t h2 = bf16_rne_bits(r1);
+    const float r2 = rsub(r1, bf16_bits_f(h2));
+    t[0][e] = h1, t[1][e] = h2, t[2][e] = bf16_rne_bits(r2);
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) out[k] = make_uint2(t[k][0] | (t[k][1] << 16), t[k][2] | (t[k][3] << 16));
+}
+
+
 // rth_relu_bias_grad's partial-sum slabs: one per workgroup of kBiasThreads lanes, about 8
 // row sweeps each, at most kBiasSlabs (shared with the deferred combine in conv.hip)
 constexpr int kBiasThreads = 256, kBiasSlabs = 2048;

@@ -258,8 +258,6 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__res
 // the same k of output channel r's weights.  A wave keeps all of W (16 chunks x 3 terms,
 // 192 VGPRs) in registers for its whole life, so the kernel uses no LDS and leaves the CU's
 // LDS to the learner's kernels; it loads the next tile's windows while it multiplies this one.
-using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
-using u32x4 = __attribute__((ext_vector_type(4))) uint32_t;
 constexpr int kC1Chunks = 16;                       // K = 256 = 16 chunks of 16
 constexpr int kC1PackedBytes = kC1Chunks * 3 * 64 * 16;  // [chunk][term][lane] x 8 bf16
 #ifndef C1_NBUF
@@ -267,12 +265,6 @@ constexpr int kC1PackedBytes = kC1Chunks * 3 * 64 * 16;  // [chunk][term][lane] 
 #endif
 constexpr int kC1Buf = C1_NBUF;  // tiles whose windows are in flight (the computed one included)
 
-__host__ __device__ __forceinline__ uint32_t bf16_rne_bits(float f) {
-  uint32_t u = __float_as_uint(f);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return u >> 16;
-}
-__host__ __device__ __forceinline__ float bf16_bits_f(uint32_t b) { return __uint_as_float(b << 16); }
 
 // term t (0, 1, 2) of the exact split of w
 __device__ __forceinline__ uint32_t bf16x3_term(float w, int t) {
@@ -456,22 +448,6 @@ struct X9Geom {
   static_assert(LDS_U4 * 16 <= 163840, "LDS image too large");
   __device__ static int swz(int r) { return (r & ~15) | ((r + (r >> 5) * ROT) & 15); }
 };
-
-// the three bf16 terms of 4 fp32 values, packed 2 per dword: out[t] = {t(v0) | t(v1) << 16, ...}
-__device__ __forceinline__ void split3_x4(float4 v, uint2 (&out)[3]) {
-  const float in[4] = {v.x, v.y, v.z, v.w};
-  uint32_t t[3][4];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const uint32_t h1 = bf16_rne_bits(in[e]);
-    const float r1 = rsub(in[e], bf16_bits_f(h1));
-    const uint32_t h2 = bf16_rne_bits(r1);
-    const float r2 = rsub(r1, bf16_bits_f(h2));
-    t[0][e] = h1, t[1][e] = h2, t[2][e] = bf16_rne_bits(r2);
-  }
-#pragma unroll
-  for (int k = 0; k < 3; ++k) out[k] = make_uint2(t[k][0] | (t[k][1] << 16), t[k][2] | (t[k][3] << 16));
-}
 
 template <int KH, int KW, int S, int CIN, int HIN, int WIN, int NSAMP, int ROT, int KS>
 __global__ __launch_bounds__(256 * KS) void k_conv_x9(const float *__restrict__ x, int64_t n,

@@ -24,6 +24,7 @@
 namespace rth {
 
 using f32x16 = __attribute__((ext_vector_type(16))) float;
+using f32x4 = __attribute__((ext_vector_type(4))) float;
 
 constexpr int kWgfWaves = 4;  // waves per workgroup (one per SIMD)
 #ifndef WGF_PF
@@ -211,11 +212,191 @@ static int wgf_splits(const WgfLaunch &l) {
   return s < kWgfRedMax ? s : kWgfRedMax;
 }
 
+// ---------------------------------------------------------------------------------------
+// The same weight gradient on the bf16 MFMA with both operands split into three exact bf16
+// terms (the x9 scheme of conv.hip's k_conv_x9: every partial product xi * gj has at most 16
+// significant bits, so it is exact in the fp32 accumulator -- the same real products as the
+// fp32 path, summed in another fixed order).  GEMM view as above, on
+// v_mfma_f32_16x16x32_bf16: rows = 16 output channels, columns = 16 kk, reduction = a chunk of
+// 32 consecutive output pixels, lane l supplying pixels 8 (l >> 4) + j, j < 8, of row / column
+// l & 15 -- 8 scalar loads per operand, each a 64-byte run of channels across 16 lanes.
+// Workgroup = 4 waves over one column group of 4 blocks (64 kk) and a range of chunks: wave w
+// owns output channels 16w .. 16w + 15 (its A fragments, loaded and split by itself) and
+// splits column block w's B fragment for the whole workgroup into LDS (double-buffered, one
+// barrier per chunk); every wave then runs 4 blocks x 9 MFMAs per chunk.  Partials per
+// workgroup go to the workspace; k_conv_wgrad_f32_reduce adds them in split order.
+template <int KH, int KW, int S, int CIN, int HIN, int WIN>
+struct WgxGeom {
+  static constexpr int HOUT = (HIN - KH) / S + 1, WOUT = (WIN - KW) / S + 1, PIX = HOUT * WOUT;
+  static constexpr int K = KH * KW * CIN, COUT = 64, GROUPS = K / 64;
+  static_assert(CIN % 16 == 0 && K % 64 == 0, "16-column blocks inside one tap, 64-column groups");
+};
+
+__device__ __forceinline__ void split3_x8(const float (&v)[8], bf16x8 (&out)[3]) {
+  uint2 lo[3], hi[3];
+  split3_x4(make_float4(v[0], v[1], v[2], v[3]), lo);
+  split3_x4(make_float4(v[4], v[5], v[6], v[7]), hi);
+#pragma unroll
+  for (int t = 0; t < 3; ++t) out[t] = __builtin_bit_cast(bf16x8, u32x4{lo[t].x, lo[t].y, hi[t].x, hi[t].y});
+}
+
+#ifndef WGX_PF
+#define WGX_PF 1
+#endif
+template <int KH, int KW, int S, int CIN, int HIN, int WIN>
+__global__ __launch_bounds__(256) void k_conv_wgrad_x9(const float *__restrict__ x, const float *__restrict__ gy,
+                                                      int64_t n, int splits, float *__restrict__ part) {
+  using G = WgxGeom<KH, KW, S, CIN, HIN, WIN>;
+  constexpr int COUT = G::COUT, PIX = G::PIX, WOUT = G::WOUT, K = G::K;
+  __shared__ bf16x8 bl[2][3][4][64];  // [buffer][term][column block][lane]
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, r = lane & 15;
+  const int group = (int)(blockIdx.x / splits), split = (int)(blockIdx.x % splits);
+  const int64_t P = n * PIX, chunks = (P + 31) / 32;
+  const int64_t c0 = chunks * split / splits, c1 = chunks * (split + 1) / splits;
+  const int co = wave * 16 + r;                 // A: this lane's output channel
+  const int kk = (group * 4 + wave) * 16 + r;   // B staged by this lane: column kk
+  const int tap = kk / CIN, ci = kk % CIN;
+  const int xoff = ((tap / KW) * WIN + tap % KW) * CIN + ci;
+  // pixel indices fit 32 bits (n * PIX < 2^31 is checked on the host)
+  const int Pi = (int)P;
+  auto load = [&](int64_t c, float (&a)[8], float (&b)[8]) {
+    const int p0 = (int)c * 32 + 8 * g;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int p = p0 + j;
+      const bool live = p < Pi;
+      const int bb = p / PIX, pix = p - bb * PIX, oy = pix / WOUT, ox = pix - oy * WOUT;
+      a[j] = live ? gy[p * COUT + co] : 0.0f;  // a dead pixel weighs 0
+      b[j] = live ? x[((bb * HIN + S * oy) * WIN + S * ox) * CIN + xoff] : 0.0f;
+    }
+  };
+  f32x4 acc[4];
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb) acc[kb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  // WGX_PF chunks' raw loads in flight (a register ring; the loop is unrolled by WGX_PF)
+  float av[WGX_PF][8], bv[WGX_PF][8];
+#pragma unroll
+  for (int d = 0; d < WGX_PF; ++d)
+    if (c0 + d < c1) load(c0 + d, av[d], bv[d]);
+  int buf = 0;
+  for (int64_t cb = c0; cb < c1; cb += WGX_PF)
+#pragma unroll
+  for (int d = 0; d < WGX_PF; ++d) {
+    const int64_t c = cb + d;
+    if (c >= c1) break;  // uniform
+    bf16x8 at[3], bt[3];
+    split3_x8(av[d], at);
+    split3_x8(bv[d], bt);
+#pragma unroll
+    for (int t = 0; t < 3; ++t) bl[buf][t][wave][lane] = bt[t];
+    if (c + WGX_PF < c1) load(c + WGX_PF, av[d], bv[d]);  // in flight during the next chunks
+    __syncthreads();
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      const bf16x8 b0 = bl[buf][0][kb][lane], b1 = bl[buf][1][kb][lane], b2 = bl[buf][2][kb][lane];
+      f32x4 a = acc[kb];
+      // smallest terms first: (3,3) (3,2) (2,3) (3,1) (2,2) (1,3) (2,1) (1,2) (1,1)
+      a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(at[2], b2, a, 0, 0, 0);
+      a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(at[2], b1, a, 0, 0, 0);
+      a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(at[1], b2, a, 0, 0, 0);
+      a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(at[2], b0, a, 0, 0, 0);
+      a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(at[1], b1, a, 0, 0, 0);
+      a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(at[0], b2, a, 0, 0, 0);
+      a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(at[1], b0, a, 0, 0, 0);
+      a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(at[0], b1, a, 0, 0, 0);
+      a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(at[0], b0, a, 0, 0, 0);
+      acc[kb] = a;
+    }
+    buf ^= 1;
+  }
+  // D: lane holds rows (channels) 16 wave + 4 (l >> 4) + i of column 16 kb + (l & 15)
+  float *out = part + (int64_t)split * COUT * K;
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      out[(int64_t)(wave * 16 + 4 * g + i) * K + (group * 4 + kb) * 16 + r] = acc[kb][i];
+}
+
+struct WgxLaunch {
+  const void *fn;
+  int groups;
+  int64_t elems;
+};
+
+template <int KH, int KW, int S, int CIN, int HIN, int WIN>
+static WgxLaunch wgx_launch() {
+  using G = WgxGeom<KH, KW, S, CIN, HIN, WIN>;
+  return WgxLaunch{reinterpret_cast<const void *>(&k_conv_wgrad_x9<KH, KW, S, CIN, HIN, WIN>), G::GROUPS,
+                   (int64_t)G::COUT * G::K};
+}
+
+static bool find_wgx(const rth_conv_shape &s, WgxLaunch *out) {
+  auto is = [&](int cin, int hin, int win, int cout, int kh, int kw, int st) {
+    return s.input == RTH_CONV_F32_NHWC && s.cin == cin && s.hin == hin && s.win == win && s.cout == cout &&
+           s.kh == kh && s.kw == kw && s.stride == st;
+  };
+  if (is(32, 20, 20, 64, 4, 4, 2)) {  // conv2: K = 512 -> 8 groups of 64 columns
+    static const WgxLaunch l = wgx_launch<4, 4, 2, 32, 20, 20>();
+    *out = l;
+  } else if (is(64, 9, 9, 64, 3, 3, 1)) {  // conv3: K = 576 -> 9 groups (one tap each)
+    static const WgxLaunch l = wgx_launch<3, 3, 1, 64, 9, 9>();
+    *out = l;
+  } else {
+    return false;
+  }
+  return true;
+}
+
+#ifndef WGX_SPLITS
+#define WGX_SPLITS 64
+#endif
+static int wgx_splits() {  // RTH_WGX_SPLITS (A/B), at most kWgfRedMax
+  static const int v = [] {
+    const char *e = getenv("RTH_WGX_SPLITS");
+    int x = e ? atoi(e) : WGX_SPLITS;
+    return x < 1 ? 1 : (x > kWgfRedMax ? kWgfRedMax : x);
+  }();
+  return v;
+}
+
 }  // namespace rth
 
 using namespace rth;
 
 extern "C" {
+
+int rth_conv_wgrad_x9_supported(const rth_conv_shape *shape) {
+  WgxLaunch l;
+  return shape && find_wgx(*shape, &l) ? 1 : 0;
+}
+
+int64_t rth_conv_wgrad_x9_workspace(const rth_conv_shape *shape) {
+  WgxLaunch l;
+  if (!shape || !find_wgx(*shape, &l)) return 0;
+  return (int64_t)wgx_splits() * l.elems * 4;
+}
+
+int rth_conv_wgrad_x9(const rth_conv_shape *shape, const float *x, int64_t n, const float *gy, float *gw,
+                      void *workspace, void *stream) {
+  RTH_REQUIRE(shape && x && gy && gw && workspace && n >= 0, "rth_conv_wgrad_x9: NULL argument");
+  WgxLaunch l;
+  RTH_REQUIRE(find_wgx(*shape, &l), "rth_conv_wgrad_x9: geometry (%d x %d x %d -> %d, k %dx%d, stride %d) not built",
+              shape->cin, shape->hin, shape->win, shape->cout, shape->kh, shape->kw, shape->stride);
+  if (n == 0) {
+    RTH_HIP(hipMemsetAsync(gw, 0, l.elems * 4, as_stream(stream)));
+    return RTH_OK;
+  }
+  RTH_REQUIRE(n * shape->cin * shape->hin * shape->win < ((int64_t)1 << 31), "rth_conv_wgrad_x9: batch too large");
+  int splits = wgx_splits();
+  float *part = static_cast<float *>(workspace);
+  void *args[] = {(void *)&x, (void *)&gy, (void *)&n, (void *)&splits, (void *)&part};
+  RTH_HIP(hipLaunchKernel(l.fn, dim3((unsigned)(l.groups * splits)), dim3(256), args, 0, as_stream(stream)));
+  hipLaunchKernelGGL(k_conv_wgrad_f32_reduce, dim3((unsigned)((l.elems + 63) / 64)), dim3(256), 0, as_stream(stream),
+                     part, splits, l.elems, gw);
+  RTH_LAUNCHED();
+  return RTH_OK;
+}
 
 int rth_conv_wgrad_f32_supported(const rth_conv_shape *shape) {
   WgfLaunch l;

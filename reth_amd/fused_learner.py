@@ -39,18 +39,20 @@ TD_HB_MAX = 16384  # rth_td_heads_backward keeps B * (A + 1) TD gradient rows in
 HIP_DGRAD = {1} if os.environ.get("RTH_MIOPEN_DGRAD") is None else set()
 if os.environ.get("RTH_HIP_DGRAD3") is not None:
     HIP_DGRAD.add(2)
-# conv2 / conv3 weight gradients in rth_conv_wgrad_f32 (deterministic, no zero fill) instead of
-# MIOpen's: opt-in, 44-47 vs 38 us alone for conv2
-HIP_WGRAD = os.environ.get("RTH_HIP_WGRAD") is not None
+# conv2 / conv3 weight gradients in a hand-written kernel (deterministic, no zero fill) instead
+# of MIOpen's: RTH_HIP_WGRAD=x9 (rth_conv_wgrad_x9, bf16 MFMA with the exact 3 x 3-term split)
+# or =f32 / =1 (rth_conv_wgrad_f32, fp32 MFMA: 44-47 vs 38 us alone for conv2)
+_wg = os.environ.get("RTH_HIP_WGRAD")
+HIP_WGRAD = None if not _wg else ("x9" if _wg == "x9" else "f32")
 _WGF_WS = {}
 
 
-def _wgrad_f32_workspace(shape, device):
-    key = (device, shape.cin, shape.hin, shape.cout)
+def _wgrad_f32_workspace(shape, device, kind="f32"):
+    key = (device, kind, shape.cin, shape.hin, shape.cout)
     ws = _WGF_WS.get(key)
     if ws is None:
-        ws = _WGF_WS[key] = torch.empty(_lib.lib().rth_conv_wgrad_f32_workspace(ctypes.byref(shape)) // 4,
-                                        dtype=torch.float32, device=device)
+        size = getattr(_lib.lib(), f"rth_conv_wgrad_{kind}_workspace")(ctypes.byref(shape))
+        ws = _WGF_WS[key] = torch.empty(size // 4, dtype=torch.float32, device=device)
     return ws
 
 
@@ -214,17 +216,18 @@ def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None, mid=No
             xin = ys[li - 1][:B] if li > 0 else x[:B]
             w = _nhwc(conv.weight.detach())
             hip_dgrad = li in HIP_DGRAD and _lib.lib().rth_conv_dgrad_supported(ctypes.byref(shapes[li]))
-            hip_wgrad = HIP_WGRAD and _lib.lib().rth_conv_wgrad_f32_supported(ctypes.byref(shapes[li]))
+            hip_wgrad = bool(HIP_WGRAD) and getattr(_lib.lib(), f"rth_conv_wgrad_{HIP_WGRAD}_supported")(
+                ctypes.byref(shapes[li]))
             need = [li > 0 and not hip_dgrad, not hip_wgrad, False]
             gx = gw = None
             if need[0] or need[1]:
                 gx, gw, _ = torch.ops.aten.convolution_backward(gy, xin, w, None, list(conv.stride), [0, 0], [1, 1],
                                                                 False, [0, 0], 1, need)
-            if hip_wgrad:  # weight gradient in rth_conv_wgrad_f32 (deterministic, no zero fill)
+            if hip_wgrad:  # weight gradient in rth_conv_wgrad_{f32,x9} (deterministic, no zero fill)
                 gw = torch.empty(conv.weight.shape, dtype=torch.float32, device=x.device,
                                  memory_format=torch.channels_last)
-                call("rth_conv_wgrad_f32", ctypes.byref(shapes[li]), ptr(xin), B, ptr(gy), ptr(gw),
-                     ptr(_wgrad_f32_workspace(shapes[li], x.device)), st)
+                call(f"rth_conv_wgrad_{HIP_WGRAD}", ctypes.byref(shapes[li]), ptr(xin), B, ptr(gy), ptr(gw),
+                     ptr(_wgrad_f32_workspace(shapes[li], x.device, HIP_WGRAD)), st)
             if hip_dgrad:  # data gradient in rth_conv_dgrad (no zero fill)
                 gx = torch.empty(xin.shape, dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
                 call("rth_conv_dgrad", ctypes.byref(shapes[li]), ptr(gy), B, ptr(w), ptr(gx), st)

@@ -1,5 +1,6 @@
-"""Development aid: rth_conv_wgrad_f32 (conv2 / conv3 weight gradient, fp32 MFMA) against
-MIOpen's weight-gradient solver (+ its zero fill) at the learner's batch, alone, HIP events."""
+"""Development aid: rth_conv_wgrad_f32 (conv2 / conv3 weight gradient, fp32 MFMA) and
+rth_conv_wgrad_x9 (bf16 MFMA, exact 3 x 3-term split) against MIOpen's weight-gradient solver
+(+ its zero fill) at the learner's batch, alone, HIP events."""
 import os
 import sys
 
@@ -18,17 +19,22 @@ for (cin, h, cout, k, s) in [(32, 20, 64, 4, 2), (64, 9, 64, 3, 1)]:
     w = torch.randn((cout, cin, k, k), device=dev).contiguous(memory_format=torch.channels_last)
     shape = _lib.ConvShape(_lib.CONV_F32_NHWC, cin, h, h, cout, k, k, s)
     ws = torch.empty(_lib.lib().rth_conv_wgrad_f32_workspace(_lib.ctypes.byref(shape)) // 4, device=dev)
+    wsx = torch.empty(_lib.lib().rth_conv_wgrad_x9_workspace(_lib.ctypes.byref(shape)) // 4, device=dev)
     gw = torch.empty_like(w)
 
     def ours():
         _lib.call("rth_conv_wgrad_f32", _lib.ctypes.byref(shape), x.data_ptr(), n, gy.data_ptr(), gw.data_ptr(),
                   ws.data_ptr(), _lib.stream_ptr())
 
+    def ours_x9():
+        _lib.call("rth_conv_wgrad_x9", _lib.ctypes.byref(shape), x.data_ptr(), n, gy.data_ptr(), gw.data_ptr(),
+                  wsx.data_ptr(), _lib.stream_ptr())
+
     def miopen():
         torch.ops.aten.convolution_backward(gy, x, w, None, [s, s], [0, 0], [1, 1], False, [0, 0], 1,
                                             [False, True, False])
 
-    for name, fn in (("rth_conv_wgrad_f32", ours), ("miopen", miopen)):
+    for name, fn in (("rth_conv_wgrad_f32", ours), ("rth_conv_wgrad_x9", ours_x9), ("miopen", miopen)):
         for _ in range(5):
             fn()
         torch.cuda.synchronize()

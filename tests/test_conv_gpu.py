@@ -406,11 +406,13 @@ def test_conv_nchw_output(dev, gi, n):
     assert _lib.lib().rth_conv_supported(_lib.ctypes.byref(u8)) == 0
 
 
-@pytest.mark.parametrize("gi,n", [(1, 1), (1, 37), (1, 512), (2, 1), (2, 3), (2, 512)])
-def test_conv_wgrad_f32(dev, gi, n):
-    """rth_conv_wgrad_f32 (conv2 / conv3 weight gradient on the fp32 MFMA) against an fp64 CPU
+@pytest.mark.parametrize("kind", ["f32", "x9"])
+@pytest.mark.parametrize("gi,n", [(1, 1), (1, 37), (1, 512), (2, 1), (2, 3), (2, 512), (2, 1024)])
+def test_conv_wgrad_f32(dev, gi, n, kind):
+    """rth_conv_wgrad_f32 (conv2 / conv3 weight gradient on the fp32 MFMA) and rth_conv_wgrad_x9
+    (the bf16 MFMA, both operands split into three exact bf16 terms) against an fp64 CPU
     convolution backward, within fp32 summation error; deterministic (a second call is bit
-    identical) and odd pixel counts (the last pair half empty) included"""
+    identical) and odd pixel counts (the last pair / 32-pixel chunk partly empty) included"""
     from reth_amd import _lib
 
     geom = GEOMS[gi]
@@ -423,14 +425,14 @@ def test_conv_wgrad_f32(dev, gi, n):
     _, want, _ = torch.ops.aten.convolution_backward(gy.double(), x.double(), w, None, [s, s], [0, 0], [1, 1], False,
                                                      [0, 0], 1, [False, True, False])
     shape = _shape(_lib.CONV_F32_NHWC, *geom)
-    assert _lib.lib().rth_conv_wgrad_f32_supported(_lib.ctypes.byref(shape)) == 1
-    ws = torch.empty(_lib.lib().rth_conv_wgrad_f32_workspace(_lib.ctypes.byref(shape)) // 4, device=dev)
+    assert getattr(_lib.lib(), f"rth_conv_wgrad_{kind}_supported")(_lib.ctypes.byref(shape)) == 1
+    ws = torch.empty(getattr(_lib.lib(), f"rth_conv_wgrad_{kind}_workspace")(_lib.ctypes.byref(shape)) // 4, device=dev)
     xd = x.to(dev).contiguous(memory_format=torch.channels_last)
     gyd = gy.to(dev).contiguous(memory_format=torch.channels_last)
     outs = []
     for _ in range(2):
         gw = torch.full((cout, cin, k, k), float("nan"), device=dev).contiguous(memory_format=torch.channels_last)
-        _lib.call("rth_conv_wgrad_f32", _lib.ctypes.byref(shape), xd.data_ptr(), n, gyd.data_ptr(), gw.data_ptr(),
+        _lib.call(f"rth_conv_wgrad_{kind}", _lib.ctypes.byref(shape), xd.data_ptr(), n, gyd.data_ptr(), gw.data_ptr(),
                   ws.data_ptr(), _lib.stream_ptr())
         outs.append(gw)
     assert torch.equal(outs[0], outs[1])

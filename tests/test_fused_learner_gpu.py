@@ -50,14 +50,15 @@ def _solver(dev, seed):
                      channels_last=True)
 
 
-@pytest.mark.parametrize("u8,adjacent,hip_dgrad,hip_wgrad", [(True, True, {1}, False), (True, False, {1}, False),
-                                                             (False, False, {1}, False), (True, True, set(), False),
-                                                             (True, True, {1, 2}, False), (True, True, {1}, True)])
+@pytest.mark.parametrize("u8,adjacent,hip_dgrad,hip_wgrad", [(True, True, {1}, None), (True, False, {1}, None),
+                                                             (False, False, {1}, None), (True, True, set(), None),
+                                                             (True, True, {1, 2}, None), (True, True, {1}, "f32"),
+                                                             (True, True, {1}, "x9")])
 def test_fused_grads_match_autograd(dev, u8, adjacent, hip_dgrad, hip_wgrad, monkeypatch):
     from reth_amd import fused_learner
 
     monkeypatch.setattr(fused_learner, "HIP_DGRAD", hip_dgrad)  # layers whose data gradient is rth_conv_dgrad's
-    monkeypatch.setattr(fused_learner, "HIP_WGRAD", hip_wgrad)  # conv2/conv3 weight gradients in rth_conv_wgrad_f32
+    monkeypatch.setattr(fused_learner, "HIP_WGRAD", hip_wgrad)  # conv2/conv3 weight gradients: MIOpen / f32 / x9
 
     B = 64
     g = torch.Generator(device=dev).manual_seed(5)

@@ -32,6 +32,34 @@ def sim(KH,KW,S,CIN,HIN,WIN,NSAMP,swz,pad):
     return tot/cnt
 def mk(ROT,SH=5):
     return lambda r:(r&~15)|((r+(r>>SH)*ROT)&15)
+def sim_tmap(KH, KW, S, CIN, HIN, WIN, NSAMP):
+    """the tile map of k_conv_x9 (ROT < 0, stride 1): unit(s, y, x) = s SU + 16 y + ((WOUT y + x) mod 16),
+    PLANE a multiple of 16, lanes past the last valid pixel read the pixel 16 before"""
+    G = geom(KH, KW, S, CIN, HIN, WIN, NSAMP)
+    SU = 16 * HIN + ((G['PIX'] - 16 * HIN) % 16)
+    PLANE = (NSAMP * SU + 15) // 16 * 16
+    nv = NSAMP * G['PIX']
+    tot = cnt = 0
+    for c in range(G['NCH']):
+        k0 = c * 32; tap = k0 // CIN; dy, dx = tap // KW, tap % KW; coff = ((k0 % CIN) // 8) * PLANE
+        for tile in range(G['TILES']):
+            units = []
+            for l in range(64):
+                p = tile * 16 + (l & 15)
+                p = p - 16 if p >= nv else p
+                s, pp = divmod(p, G['PIX']); oy, ox = divmod(pp, G['WOUT'])
+                y, x = oy + dy, ox + dx
+                units.append(coff + (l >> 4) * PLANE + s * SU + 16 * y + ((G['WOUT'] * y + x) & 15))
+            for g in GROUPS:
+                slots = {}
+                for l in g: slots.setdefault(units[l] % 16, set()).add(units[l])
+                tot += max(len(v) for v in slots.values()); cnt += 1
+    return tot / cnt, 3 * G['NG'] * PLANE * 16
+
+
+for ns in (1, 2):
+    c, lds = sim_tmap(3, 3, 1, 64, 9, 9, ns)
+    print('conv3', ns, 'tile map %.2f cycles per group, %d KB of LDS' % (c, lds // 1024))
 for name,geo,ns_list,cur in (("conv3",(3,3,1,64,9,9),(1,2,3,4),(3,0)),("conv2",(4,4,2,32,20,20),(1,2),(10,1))):
     for ns in ns_list:
         c=sim(*geo,ns,mk(cur[0]),cur[1])

@@ -395,6 +395,21 @@ int rth_td_heads_backward_branches(const float *q_s0_dev, const float *q_s1_onli
  * {adv.2.weight, value.2.weight, adv.2.bias, value.2.bias} read in place. */
 int rth_heads_fc2(const float *h_dev, int64_t ldh, int64_t n, int32_t H, int32_t A, const float *const *fc2_params_dev,
                   float *heads_dev, void *stream);
+/* rth_heads_fc2 over a device-counted batch (the actors' acting + terminal stacks,
+ * test/apex-dqn/worker.py:46 act and :55-60 calc_loss): only rows r < min(*n_dev, n_max) are
+ * computed; cache_dev (nullable) [stacks, A+1] additionally receives row r at cache_rows_dev[r]
+ * (the per-stack heads cache the deduplicated calc_loss reads) -- one launch instead of two. */
+int rth_heads_fc2_upto(const float *h_dev, int64_t ldh, int64_t n_max, const int64_t *n_dev, int32_t H, int32_t A,
+                       const float *const *fc2_params_dev, float *heads_dev, float *cache_dev,
+                       const int64_t *cache_rows_dev, void *stream);
+/* y[r] = relu(x[r] . w^T + b) for rows r0 <= r < min(*n_dev, n_max) (dqn_model.py:22-43, the
+ * heads' first Linear -> ReLU): the device-counted tail of a batch whose first r0 rows a
+ * library GEMM covers -- the actors' terminal stacks, absent in most steps (every workgroup
+ * exits at once).  x [*, F] row stride ldx, w [O, F], y row stride ldy; F, ldx multiples of 4,
+ * x and w 16-byte aligned.  Deterministic (fixed-order sums). */
+int rth_linear_relu_rows_upto(const float *x_dev, int64_t ldx, int64_t r0, int64_t n_max, const int64_t *n_dev,
+                              const float *w_dev, const float *b_dev, int64_t F, int64_t O, float *y_dev, int64_t ldy,
+                              void *stream);
 
 /* ------------------------------------------------------------------------------------
  * Q-network convolution torso forward (reth/reth/algorithm/dqn/dqn_model.py:14-20: each

@@ -141,6 +141,10 @@ SIGNATURES = {
                                                c_vp, c_i64, ctypes.POINTER(c_vp), c_i32, c_vp, c_vp, c_vp,
                                                ctypes.POINTER(c_vp), c_vp, c_vp, c_vp]),
     "rth_heads_fc2": (c_i32, [c_vp, c_i64, c_i64, c_i32, c_i32, ctypes.POINTER(c_vp), c_vp, c_vp]),
+    "rth_heads_fc2_upto": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_i32, c_i32, ctypes.POINTER(c_vp), c_vp, c_vp, c_vp,
+                                   c_vp]),
+    "rth_linear_relu_rows_upto": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64,
+                                          c_vp]),
     "rth_conv_wgrad_x9_supported": (c_i32, [ctypes.POINTER(ConvShape)]),
     "rth_conv_wgrad_x9_workspace": (c_i64, [ctypes.POINTER(ConvShape)]),
     "rth_conv_wgrad_x9": (c_i32, [ctypes.POINTER(ConvShape), c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),

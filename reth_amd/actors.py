@@ -22,6 +22,8 @@ Here all N actors of a GPU step together, entirely in HBM:
            inserts (|td| + 1e-6)^alpha into the tree.
 No host synchronisation anywhere in the loop.
 """
+import os
+
 import numpy as np
 import torch
 
@@ -96,6 +98,14 @@ class VecActors:
         self.n_ext = torch.full((1,), N, dtype=torch.int64, device=dev)  # acting + terminal stacks
         self._base = torch.arange(N, device=dev, dtype=torch.int64) * ring
         self.qrows = None
+        # dedup forwards, RTH_ACTOR_COUNTED_FC=1: FC1 as a GEMM over the N acting rows only, the
+        # terminal stacks behind them device-counted.  Measured no faster at Pong (the 256-row
+        # GEMM takes as long as the 512-row one: one round of K-deep tiles either way), so the
+        # default is one GEMM over all 2N rows
+        self._counted_fc = os.environ.get("RTH_ACTOR_COUNTED_FC", "0") == "1"
+        # RTH_ACTOR_FC2_CACHE=0: the second layer over all 2N rows and the cache scatter as a
+        # launch of its own (the r03 form, for A/B runs)
+        self._fc2_cache = os.environ.get("RTH_ACTOR_FC2_CACHE", "1") != "0"
         self.fresh = 0       # steps since the actor network's weights last changed
         self.t = 0           # env steps taken (per actor): host mirror of t_dev
         self.t_dev = torch.zeros(1, dtype=torch.int64, device=dev)  # what the kernels read
@@ -256,8 +266,12 @@ class VecActors:
         if hip:  # step counter + acting rows (= cur_slot + _base) in one launch
             call("rth_actor_prologue", ptr(self.t_dev), ptr(self.cur_slot), N, self.ring, ptr(self.hx), s)
             if dedup:  # acting + terminal stacks (device count); the rows' heads are in the cache
-                q = q_net.forward_heads(self.frames, rows=self.hx[:2 * N], n_dev=self.n_ext)
-                self._scatter_heads(q, self.hx, 2 * N)
+                if self._fc2_cache and q_net._fc2_inplace():  # the second layer over the counted rows, the cache in its launch
+                    q = q_net.forward_heads(self.frames, rows=self.hx[:2 * N], n_dev=self.n_ext,
+                                            n_fixed=N if self._counted_fc else None, cache=(self.qcache, self.hx))
+                else:
+                    q = q_net.forward_heads(self.frames, rows=self.hx[:2 * N], n_dev=self.n_ext)
+                    self._scatter_heads(q, self.hx, 2 * N)
             else:  # everything: acting, last step's terminal stacks, the rows' s0 and s1 -> cache
                 torch.cat([prev.s0, prev.s1], out=self.hx[2 * N:])
                 q = q_net.forward_heads(self.frames, rows=self.hx)

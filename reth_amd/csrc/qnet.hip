@@ -544,9 +544,15 @@ template <int MAXA1>
 __global__ __launch_bounds__(256) void k_heads_fc2(const float *__restrict__ h, int64_t ldh, int64_t n, int H, int A,
                                                    const float *__restrict__ wa2, const float *__restrict__ wv2,
                                                    const float *__restrict__ ba2, const float *__restrict__ bv2,
-                                                   float *__restrict__ heads) {
+                                                   float *__restrict__ heads, const int64_t *__restrict__ n_dev,
+                                                   float *__restrict__ cache, const int64_t *__restrict__ cache_rows) {
   constexpr int U = kFc2MaxH / 16 / 4;  // float4 per lane and half, at most
   extern __shared__ float4 wl[];         // rows a < A: wa2[a], row A: wv2
+  if (n_dev) {                           // device-counted batch: rows >= *n_dev are not computed
+    const int64_t nd = *n_dev;
+    n = nd < n ? nd : n;
+    if ((int64_t)blockIdx.x * 16 >= n) return;  // uniform
+  }
   const int l = threadIdx.x & 15;
   const int64_t r = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
   const int64_t rr = r < n ? r : n - 1;  // tail rows: a duplicate, nothing written
@@ -583,10 +589,77 @@ __global__ __launch_bounds__(256) void k_heads_fc2(const float *__restrict__ h, 
     for (int o = 1; o < 16; o <<= 1) acc[a] = radd(acc[a], __shfl_xor(acc[a], o, 64));
   if (l == 0 && r < n) {
     float *out = heads + r * A1;
+    float *co = cache ? cache + cache_rows[r] * A1 : nullptr;  // the per-stack heads cache row
 #pragma unroll
     for (int a = 0; a < MAXA1; ++a)
-      if (a < A) out[a] = radd(acc[a], ba2[a]);
-      else if (a == A) out[a] = radd(acc[a], bv2[0]);
+      if (a <= A) {
+        const float v = radd(acc[a], a < A ? ba2[a] : bv2[0]);
+        out[a] = v;
+        if (co) co[a] = v;
+      }
+  }
+}
+
+// rows [r0, min(*n_dev, n_max)) of y = relu(x w^T + b), x [*, F] row stride ldx, w [O, F],
+// y row stride ldy: the device-counted tail of a batch whose first r0 rows a library GEMM
+// covers (the actors' terminal stacks behind the acting rows: none in most steps, so every
+// workgroup usually exits at once).  Workgroup = kLrCols output columns; the rows go in
+// chunks of kLrRows, each lane a strided float4 slice of F, the partial dots summed by xor
+// shuffles and then across the waves in a fixed order (deterministic).
+constexpr int kLrCols = 4, kLrRows = 8, kLrThreads = 256;
+__global__ __launch_bounds__(kLrThreads) void k_linear_relu_rows(const float *__restrict__ x, int64_t ldx, int64_t r0,
+                                                                 int64_t n_max, const int64_t *__restrict__ n_dev,
+                                                                 const float *__restrict__ w,
+                                                                 const float *__restrict__ b, int F, int O,
+                                                                 float *__restrict__ y, int64_t ldy) {
+  int64_t n_end = *n_dev;
+  n_end = n_end < n_max ? n_end : n_max;
+  if (n_end <= r0) return;  // uniform
+  __shared__ float red[kLrThreads / 64][kLrCols * kLrRows];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, F4 = F / 4;
+  const int j0 = (int)blockIdx.x * kLrCols;
+  const float4 *w4 = reinterpret_cast<const float4 *>(w);
+  for (int64_t rb = r0; rb < n_end; rb += kLrRows) {
+    float acc[kLrCols][kLrRows];
+#pragma unroll
+    for (int c = 0; c < kLrCols; ++c)
+#pragma unroll
+      for (int u = 0; u < kLrRows; ++u) acc[c][u] = 0.0f;
+    for (int f4 = tid; f4 < F4; f4 += kLrThreads) {
+      float4 wv[kLrCols];
+#pragma unroll
+      for (int c = 0; c < kLrCols; ++c)
+        wv[c] = j0 + c < O ? w4[(int64_t)(j0 + c) * F4 + f4] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#pragma unroll
+      for (int u = 0; u < kLrRows; ++u) {
+        if (rb + u >= n_end) break;  // uniform
+        const float4 xv = reinterpret_cast<const float4 *>(x + (rb + u) * ldx)[f4];
+#pragma unroll
+        for (int c = 0; c < kLrCols; ++c)
+          acc[c][u] = radd(radd(radd(radd(acc[c][u], rmul(xv.x, wv[c].x)), rmul(xv.y, wv[c].y)),
+                                rmul(xv.z, wv[c].z)), rmul(xv.w, wv[c].w));
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < kLrCols; ++c)
+#pragma unroll
+      for (int u = 0; u < kLrRows; ++u) {
+        float v = acc[c][u];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v = radd(v, __shfl_xor(v, o, 64));
+        if (lane == 0) red[wave][c * kLrRows + u] = v;
+      }
+    __syncthreads();
+    if (tid < kLrCols * kLrRows) {
+      const int c = tid / kLrRows, u = tid % kLrRows;
+      if (rb + u < n_end && j0 + c < O) {
+        float v = b[j0 + c];
+#pragma unroll
+        for (int k = 0; k < kLrThreads / 64; ++k) v = radd(v, red[k][tid]);
+        y[(rb + u) * ldy + j0 + c] = v > 0.0f ? v : 0.0f;
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -797,8 +870,9 @@ int rth_td_heads_backward_branches(const float *q0, const float *q1o, const floa
                                 loss_out, gh, gb1, td_acc, stream);
 }
 
-int rth_heads_fc2(const float *h, int64_t ldh, int64_t n, int32_t H, int32_t A, const float *const *fc2_params,
-                  float *heads, void *stream) {
+static int heads_fc2_impl(const float *h, int64_t ldh, int64_t n, int32_t H, int32_t A,
+                          const float *const *fc2_params, float *heads, const int64_t *n_dev, float *cache,
+                          const int64_t *cache_rows, void *stream) {
   RTH_REQUIRE(h && heads && fc2_params && fc2_params[0] && fc2_params[1] && fc2_params[2] && fc2_params[3],
               "rth_heads_fc2: NULL argument");
   RTH_REQUIRE(n >= 0 && H >= 16 && H % 16 == 0 && A >= 1 && A < kHbMaxA1 && ldh >= 2 * H && ldh % 4 == 0 &&
@@ -812,10 +886,38 @@ int rth_heads_fc2(const float *h, int64_t ldh, int64_t n, int32_t H, int32_t A, 
   const size_t lds = (size_t)(A + 1) * H * 4;
   if (A + 1 <= 8)
     hipLaunchKernelGGL((k_heads_fc2<8>), grid, block, lds, as_stream(stream), h, ldh, n, (int)H, (int)A, fc2_params[0],
-                       fc2_params[1], fc2_params[2], fc2_params[3], heads);
+                       fc2_params[1], fc2_params[2], fc2_params[3], heads, n_dev, cache, cache_rows);
   else
     hipLaunchKernelGGL((k_heads_fc2<kHbMaxA1>), grid, block, lds, as_stream(stream), h, ldh, n, (int)H, (int)A,
-                       fc2_params[0], fc2_params[1], fc2_params[2], fc2_params[3], heads);
+                       fc2_params[0], fc2_params[1], fc2_params[2], fc2_params[3], heads, n_dev, cache, cache_rows);
+  RTH_LAUNCHED();
+  return RTH_OK;
+}
+
+int rth_heads_fc2(const float *h, int64_t ldh, int64_t n, int32_t H, int32_t A, const float *const *fc2_params,
+                  float *heads, void *stream) {
+  return heads_fc2_impl(h, ldh, n, H, A, fc2_params, heads, nullptr, nullptr, nullptr, stream);
+}
+
+int rth_heads_fc2_upto(const float *h, int64_t ldh, int64_t n_max, const int64_t *n_dev, int32_t H, int32_t A,
+                       const float *const *fc2_params, float *heads, float *cache, const int64_t *cache_rows,
+                       void *stream) {
+  RTH_REQUIRE(n_dev && (!cache || cache_rows), "rth_heads_fc2_upto: NULL count or cache rows");
+  return heads_fc2_impl(h, ldh, n_max, H, A, fc2_params, heads, n_dev, cache, cache_rows, stream);
+}
+
+int rth_linear_relu_rows_upto(const float *x, int64_t ldx, int64_t r0, int64_t n_max, const int64_t *n_dev,
+                              const float *w, const float *b, int64_t F, int64_t O, float *y, int64_t ldy,
+                              void *stream) {
+  RTH_REQUIRE(x && n_dev && w && b && y, "rth_linear_relu_rows_upto: NULL argument");
+  RTH_REQUIRE(r0 >= 0 && n_max >= r0 && F >= 4 && F % 4 == 0 && O >= 1 && O <= (int64_t)1 << 30 && ldx >= F &&
+                  ldx % 4 == 0 && ldy >= O && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w)) & 15) == 0,
+              "rth_linear_relu_rows_upto: bad shape r0=%lld n_max=%lld F=%lld O=%lld ldx=%lld ldy=%lld (F, ldx "
+              "multiples of 4, x and w 16-byte aligned)",
+              (long long)r0, (long long)n_max, (long long)F, (long long)O, (long long)ldx, (long long)ldy);
+  if (n_max == r0) return RTH_OK;
+  hipLaunchKernelGGL(k_linear_relu_rows, dim3((unsigned)((O + kLrCols - 1) / kLrCols)), dim3(kLrThreads), 0,
+                     as_stream(stream), x, ldx, r0, n_max, n_dev, w, b, (int)F, (int)O, y, ldy);
   RTH_LAUNCHED();
   return RTH_OK;
 }

@@ -179,14 +179,19 @@ class DQNNetwork(nn.Module):
         if self.hwc_features and self._frozen[0].is_cuda:
             self._frozen_packed = self.pack_convs(out=getattr(self, "_frozen_packed", None))
 
-    def forward_heads(self, x, merged=None, rows=None, packed=None, n_dev=None):
+    def forward_heads(self, x, merged=None, rows=None, packed=None, n_dev=None, n_fixed=None, cache=None):
         """raw dueling heads [n, A+1].  x: float32 observations (channels-last with
         hwc_features), or -- on the HIP torso -- uint8 frame stacks [m, C, H, W], read as
         stacks `rows` (an int64 device index, n = rows.numel()) or all m of them.  merged /
         packed: the head weights / packed conv weights of this weight version (pack_convs),
         default the frozen ones, else built now.  n_dev (int64 device scalar, inference only):
         only the first *n_dev of the n samples are computed by the torso (rows past it hold
-        whatever the FC layers make of unwritten activations)"""
+        whatever the FC layers make of unwritten activations).  n_fixed (with n_dev, the
+        in-place second layer): the first n_fixed rows are always live -- FC1 runs as a
+        library GEMM over those only, the counted rows behind them through
+        rth_linear_relu_rows_upto, the second layer over the counted rows only; rows past
+        *n_dev of the result are undefined.  cache = (heads cache [stacks, A+1], rows int64
+        [n]) also receives the counted rows' heads at their stack rows (same launch)."""
         if not self.dueling:
             raise ValueError("forward_heads needs the dueling network")
         frozen = getattr(self, "_frozen", None) is not None
@@ -202,10 +207,44 @@ class DQNNetwork(nn.Module):
                 raise ValueError("uint8 / row-indexed / counted observations need the HIP torso (hwc_features)")
             h = self.features(x)
         h = h.reshape(h.shape[0], -1)  # (C, H, W) flatten: a view of the last HIP conv's NCHW output
+        if n_dev is not None and w2 is None and (n_fixed is not None or cache is not None):
+            return self._heads_counted(h, w1, b1, n_dev, n_fixed, cache)
+        if cache is not None or n_fixed is not None:
+            raise ValueError("forward_heads(cache= / n_fixed=) needs n_dev and the in-place second layer")
         h = _LinearReLU.apply(h, w1, b1)
         if w2 is None:  # the second layer from the branch parameters in place
             return self._heads_fc2(h)
         return torch.addmm(b2, h, w2.t())
+
+    def _heads_counted(self, h, w1, b1, n_dev, n_fixed, cache):
+        """forward_heads' device-counted heads: FC1 + ReLU as one GEMM over all n rows, or (n_fixed)
+        a GEMM over the n_fixed live rows and rth_linear_relu_rows_upto over the counted rows
+        behind them (usually none); then the second layer (+ the heads-cache scatter) over the
+        counted rows only"""
+        from ._lib import c_vp, call, ptr, stream_ptr
+
+        n, F = h.shape
+        O = w1.shape[0]
+        if n_fixed is None:
+            h1 = _LinearReLU.apply(h, w1, b1)
+        else:
+            n_fixed = int(n_fixed)
+            if not (0 < n_fixed <= n) or not h.is_contiguous():
+                raise ValueError(f"forward_heads: n_fixed {n_fixed} outside (0, {n}] or features not contiguous")
+            h1 = torch.empty((n, O), dtype=torch.float32, device=h.device)
+            torch._addmm_activation(b1, h[:n_fixed], w1.t(), out=h1[:n_fixed])
+            call("rth_linear_relu_rows_upto", ptr(h), F, n_fixed, n, ptr(n_dev), ptr(w1), ptr(b1), F, O, ptr(h1), O,
+                 stream_ptr())
+        ps = self._head_params()[4:]
+        A, H = ps[0].shape
+        out = torch.empty((n, A + 1), dtype=torch.float32, device=h.device)
+        arr = (c_vp * 4)(*[p.data_ptr() for p in ps])
+        qc, qrows = cache if cache is not None else (None, None)
+        if qc is not None and (qc.shape[1] != A + 1 or qrows.numel() < n or qrows.dtype != torch.int64):
+            raise ValueError("forward_heads: heads cache of the wrong width or too few cache rows")
+        call("rth_heads_fc2_upto", ptr(h1), h1.stride(0), n, ptr(n_dev), H, A, arr, ptr(out), ptr(qc), ptr(qrows),
+             stream_ptr())
+        return out
 
     def _convs(self):
         return [m for m in self.features if isinstance(m, nn.Conv2d)]

@@ -239,3 +239,97 @@ def test_heads_fc2_forward(dev, n, A):
     with pytest.raises(_lib.RethHipError):
         call("rth_heads_fc2", ptr(h), 2 * H, n, H, 33, (_lib.c_vp * 4)(*[p.data_ptr() for p in big]), ptr(out),
              stream_ptr())
+
+
+@pytest.mark.parametrize("n,A,counts", [(512, 6, [0, 255, 256, 257, 300, 512, 600]), (40, 9, [0, 1, 17, 40]),
+                                        (33, 32, [5, 33])])
+def test_heads_fc2_upto_and_cache(dev, n, A, counts):
+    """rth_heads_fc2_upto == rth_heads_fc2 bit for bit on the counted rows (the same launch
+    arithmetic), rows past the count untouched; the cache rows receive the same heads and no
+    other cache row is written"""
+    from reth_amd import _lib
+    from reth_amd._lib import call, ptr, stream_ptr
+
+    g = torch.Generator(device=dev).manual_seed(n * A)
+    H = 512
+    h = torch.relu(torch.randn(n, 2 * H, device=dev, generator=g))
+    ps = [torch.randn(A, H, device=dev, generator=g) * 0.05, torch.randn(1, H, device=dev, generator=g) * 0.05,
+          torch.randn(A, device=dev, generator=g), torch.randn(1, device=dev, generator=g)]
+    arr = (_lib.c_vp * 4)(*[p.data_ptr() for p in ps])
+    want = torch.empty((n, A + 1), device=dev)
+    call("rth_heads_fc2", ptr(h), 2 * H, n, H, A, arr, ptr(want), stream_ptr())
+    stacks = 3 * n + 1
+    rows = torch.randperm(stacks, device=dev, generator=g)[:n]
+    for c in counts:
+        cnt = torch.tensor([c], dtype=torch.int64, device=dev)
+        out = torch.full((n, A + 1), float("nan"), device=dev)
+        cache = torch.full((stacks, A + 1), -3.0, device=dev)
+        call("rth_heads_fc2_upto", ptr(h), 2 * H, n, ptr(cnt), H, A, arr, ptr(out), ptr(cache), ptr(rows), stream_ptr())
+        k = min(c, n)
+        assert torch.equal(out[:k], want[:k]) and bool(out[k:].isnan().all())
+        assert torch.equal(cache[rows[:k]], want[:k])
+        untouched = torch.ones(stacks, dtype=torch.bool, device=dev)
+        untouched[rows[:k]] = False
+        assert bool((cache[untouched] == -3.0).all())
+        out2 = torch.full_like(out, float("nan"))  # without the cache
+        call("rth_heads_fc2_upto", ptr(h), 2 * H, n, ptr(cnt), H, A, arr, ptr(out2), None, None, stream_ptr())
+        assert torch.equal(out2[:k], want[:k])
+    with pytest.raises(_lib.RethHipError):  # a cache without its rows
+        call("rth_heads_fc2_upto", ptr(h), 2 * H, n, ptr(cnt), H, A, arr, ptr(out), ptr(cache), None, stream_ptr())
+
+
+@pytest.mark.parametrize("n_max,r0,F,O", [(512, 256, 3136, 1024), (80, 40, 3136, 1024), (64, 0, 12, 6),
+                                          (300, 100, 256, 130)])
+def test_linear_relu_rows_upto(dev, n_max, r0, F, O):
+    """rows r0 <= r < min(*n_dev, n_max) of relu(x w^T + b) within fp32 summation error of an
+    fp64 reference; every other row untouched; deterministic (run twice, equal)"""
+    from reth_amd._lib import call, ptr, stream_ptr
+
+    g = torch.Generator(device=dev).manual_seed(F + O)
+    x = torch.relu(torch.randn(n_max, F, device=dev, generator=g))
+    w = torch.randn(O, F, device=dev, generator=g) * F ** -0.5
+    b = torch.randn(O, device=dev, generator=g) * 0.1
+    want = torch.relu(x.double() @ w.double().t() + b.double())
+    for c in sorted({r0, r0 + 1, r0 + 7, r0 + 8, r0 + 9, (r0 + n_max) // 2, n_max, n_max + 5, 0}):
+        cnt = torch.tensor([c], dtype=torch.int64, device=dev)
+        y = torch.full((n_max, O), -1.0, device=dev)
+        call("rth_linear_relu_rows_upto", ptr(x), F, r0, n_max, ptr(cnt), ptr(w), ptr(b), F, O, ptr(y), O, stream_ptr())
+        hi = max(r0, min(c, n_max))
+        torch.testing.assert_close(y[r0:hi].double(), want[r0:hi], rtol=1e-5, atol=1e-5)
+        assert bool((y[:r0] == -1.0).all()) and bool((y[hi:] == -1.0).all())
+        y2 = torch.full_like(y, -1.0)
+        call("rth_linear_relu_rows_upto", ptr(x), F, r0, n_max, ptr(cnt), ptr(w), ptr(b), F, O, ptr(y2), O,
+             stream_ptr())
+        assert torch.equal(y, y2)
+
+
+def test_forward_heads_counted_matches_full(dev):
+    """forward_heads over a device-counted batch with n_fixed (FC1 GEMM over the fixed rows,
+    rth_linear_relu_rows_upto behind them, the counted second layer + cache scatter) gives the
+    uncounted forward's heads on every counted row, within fp32 GEMM blocking error; without
+    n_fixed (one GEMM over all rows, the counted second layer + cache scatter) bit for bit"""
+    from reth_amd.model import DQNNetwork
+
+    torch.manual_seed(3)
+    net = DQNNetwork((4, 84, 84), 6).to(dev, memory_format=torch.channels_last)
+    net.hwc_features = True
+    net.requires_grad_(False)
+    net.freeze_heads()
+    g = torch.Generator(device=dev).manual_seed(5)
+    stacks = torch.randint(0, 256, (90, 4, 84, 84), dtype=torch.uint8, device=dev, generator=g)
+    N = 32
+    rows = torch.randint(0, 90, (2 * N,), device=dev, generator=g)
+    with torch.no_grad():
+        full = net.forward_heads(stacks, rows=rows)
+        for k in (0, 1, 5, N):
+            cnt = torch.tensor([N + k], dtype=torch.int64, device=dev)
+            cache = torch.zeros((100, 7), device=dev)
+            crow = torch.arange(2 * N, device=dev) + 30
+            for nf in (N, None):
+                cache.zero_()
+                q = net.forward_heads(stacks, rows=rows, n_dev=cnt, n_fixed=nf, cache=(cache, crow))
+                torch.testing.assert_close(q[:N + k], full[:N + k], rtol=1e-5, atol=1e-5)
+                if nf is None:  # the same 2N-row GEMM: the same heads bit for bit
+                    assert torch.equal(q[:N + k], full[:N + k])
+                assert torch.equal(cache[crow[:N + k]], q[:N + k])
+                assert bool((cache[:30] == 0).all()) and bool((cache[30 + N + k:] == 0).all())

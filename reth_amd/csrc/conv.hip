@@ -493,17 +493,24 @@ __global__ __launch_bounds__(256 * KS) void k_conv_x9(const float *__restrict__ 
   constexpr int RB_ = (NSAMP - NA) * HIN * WIN;      // ... of phase B
   constexpr int SB = (RB_ + 15) / 16 * CB * 64;
   constexpr int UA = (SA + NT - 1) / NT, UB = SB > 0 ? (SB + NT - 1) / NT : 1;
-  const float4 *xs = reinterpret_cast<const float4 *>(x + b0 * (int64_t)(HIN * WIN * CIN));
   const int rows = ns * HIN * WIN;
   auto slot_of = [&](int i, int r0, int &rr, int &c4) {
     const int l = i & 63, blk = i >> 6;
     rr = r0 + (blk / CB) * 16 + (l & 15);
     c4 = (blk % CB) * 4 + (l >> 4);
   };
+  // the staging loads go through a buffer resource over the n samples: a slot past the staged
+  // rows gets an offset beyond its range and reads zeros, so no load sits under a branch (a
+  // "cond ? load : 0" made the compiler wait for each load before issuing the next: the
+  // phase-B loads went out one at a time)
+  const __amdgpu_buffer_rsrc_t x_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float *>(x), 0, (int)(n * (int64_t)(HIN * WIN * CIN) * 4), 0x00020000);
+  const uint32_t xb0 = (uint32_t)(b0 * (int64_t)(HIN * WIN * CIN) * 4);
   auto fetch = [&](int i, int r0, int rend) -> float4 {
     int rr, c4;
     slot_of(i, r0, rr, c4);
-    return rr < rend && rr < rows ? xs[rr * (CIN / 4) + c4] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const uint32_t off = rr < rend && rr < rows ? xb0 + (uint32_t)((rr * (CIN / 4) + c4) * 16) : 0x80000000u;
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(x_rsrc, off, 0, 0));
   };
   auto commit = [&](float4 v, int i, int r0, int rend) {
     int rr, c4;
@@ -519,7 +526,7 @@ __global__ __launch_bounds__(256 * KS) void k_conv_x9(const float *__restrict__ 
   {
     float4 va[UA];
 #pragma unroll
-    for (int u = 0; u < UA; ++u) va[u] = tid + u * NT < SA ? fetch(tid + u * NT, 0, RA) : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int u = 0; u < UA; ++u) va[u] = fetch(tid + u * NT, 0, tid + u * NT < SA ? RA : 0);
 #pragma unroll
     for (int u = 0; u < UA; ++u)
       if (tid + u * NT < SA) commit(va[u], tid + u * NT, 0, RA);
@@ -527,7 +534,7 @@ __global__ __launch_bounds__(256 * KS) void k_conv_x9(const float *__restrict__ 
   float4 vb[UB];
   if constexpr (SB > 0) {
 #pragma unroll
-    for (int u = 0; u < UB; ++u) vb[u] = tid + u * NT < SB ? fetch(tid + u * NT, RA, RA + RB_) : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int u = 0; u < UB; ++u) vb[u] = fetch(tid + u * NT, RA, tid + u * NT < SB ? RA + RB_ : 0);
   }
   const float bl = bias[cb * 16 + (lane & 15)];
   __syncthreads();
@@ -984,6 +991,9 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_dgrad(const float *__restri
     nwg = gridDim.x / NCLS;
   }
   const int py = cls / S, px = cls % S;
+  // gy as a buffer resource (kernel arguments only: wave-uniform), its range the n samples
+  const __amdgpu_buffer_rsrc_t gy_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float *>(gy), 0, (int)(n * (HO * WO * CO) * 4), 0x00020000);
 
   // stage this class's taps: slot (g * NB + nb) * 64 + lane, chunk g = (tap, 16 co)
   for (int sl = threadIdx.x; sl < Gm::LDS_F4; sl += T) {
@@ -1002,14 +1012,16 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_dgrad(const float *__restri
     if (p >= PC) p = PC - 1;  // tail lanes compute a duplicate pixel, never stored
     const int64_t b = p / (Gm::JH * Gm::JW);
     const int r = (int)(p % (Gm::JH * Gm::JW)), jy = r / Gm::JW, jx = r % Gm::JW;
-    const float *gyb = gy + b * (HO * WO * CO) + 4 * q;
-    // chunk g = (tap g / CPT, 16 co from (g % CPT) * 16): this lane's float4 of gy (zero off the edge)
-    auto aload = [&](int g) {
+    const uint32_t gyb = (uint32_t)((b * (HO * WO * CO) + 4 * q) * 4);  // byte offset (host: gy < 2 GiB)
+    // chunk g = (tap g / CPT, 16 co from (g % CPT) * 16): this lane's float4 of gy, zero off the
+    // edge -- a buffer load whose offset lies past the descriptor's range returns zeros, so
+    // every load is unconditional (a load under a branch made the compiler wait for ALL loads
+    // in flight, vmcnt(0), before each group's first MFMA: no prefetch left)
+    auto aload = [&](int g) {  // g >= G: past the tile (zeros, no memory access), keeps the count static
       const int t = g / CPT, oy = jy - t / TW, ox = jx - t % TW;
-      f32x4 a = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-      if (oy >= 0 && oy < HO && ox >= 0 && ox < WO)
-        a = *reinterpret_cast<const f32x4 *>(gyb + (oy * WO + ox) * CO + (g % CPT) * 16);
-      return a;
+      const bool in = g < Gm::G && oy >= 0 && oy < HO && ox >= 0 && ox < WO;
+      const uint32_t off = in ? gyb + (uint32_t)(((oy * WO + ox) * CO + (g % CPT) * 16) * 4) : 0x80000000u;
+      return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(gy_rsrc, off, 0, 0));
     };
     f32x4 acc[NB];
 #pragma unroll
@@ -1030,7 +1042,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_dgrad(const float *__restri
 #pragma unroll
           for (int nb = 0; nb < NB; ++nb)
             acc[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(ar[d][tt], bf[nb][tt], acc[nb], 0, 0, 0);
-        if (g + DGRAD_D < Gm::G) ar[d] = aload(g + DGRAD_D);
+        ar[d] = aload(g + DGRAD_D);  // unconditional: the compiler keeps DGRAD_D - 1 loads in flight
       }
     }
     // C/D: lane holds column mr of rows 4q .. 4q+3
@@ -1596,6 +1608,8 @@ static int conv_bias_relu(const rth_conv_shape *shape, const void *x, const int6
   w = reinterpret_cast<const float *>(reinterpret_cast<const uint8_t *>(w) + w_off);
   if (l.x9) {  // one workgroup per nsamp samples
     RTH_REQUIRE(input == RTH_CONV_F32_NHWC, "rth_conv_bias_relu: the x9 kernels read f32 NHWC input");
+    RTH_REQUIRE(n * (int64_t)shape->hin * shape->win * shape->cin * 4 < ((int64_t)1 << 31),
+                "rth_conv_bias_relu: %lld input samples exceed the x9 kernels' 2 GiB buffer range", (long long)n);
     const int ns = (int)nsamp;
     const int64_t grid = (n + nsamp - 1) / nsamp;
     const float *xf = static_cast<const float *>(x);
@@ -1631,6 +1645,9 @@ int rth_conv_dgrad(const rth_conv_shape *shape, const float *gy, int64_t n, cons
                15) == 0,
               "rth_conv_dgrad: misaligned buffer");
   if (n == 0) return RTH_OK;
+  RTH_REQUIRE(n * (int64_t)shape->cout * ((shape->hin - shape->kh) / shape->stride + 1) *
+                      ((shape->win - shape->kw) / shape->stride + 1) * 4 < ((int64_t)1 << 31),
+              "rth_conv_dgrad: gy of %lld samples exceeds the 2 GiB buffer range", (long long)n);
   const int64_t tiles = (n * l.jh * l.jw + 15) / 16;
   int64_t per_class = (tiles + l.waves - 1) / l.waves;
   const int64_t resident = (int64_t)cu_count() * l.per_cu / l.classes;

@@ -383,10 +383,10 @@ __global__ __launch_bounds__(kHbThreads) void k_heads_backward(const float *__re
 #pragma unroll
     for (int u = 0; u < RB; ++u) {  // all loads of the batch first
       const int64_t r = r0 + (int64_t)u * kHbGroups;
-      const bool live = r < B;
-      hv[u] = live ? h[r * ldh + j] : 0.0f;
+      const int64_t rl = r < B ? r : B - 1;  // unconditional loads (a duplicate row, unused): a load
+      hv[u] = h[rl * ldh + j];               // under a branch is waited for before the next one
 #pragma unroll
-      for (int a = 0; a < MAXA; ++a) dv[u][a] = (live && a < A1) ? dq[r * A1 + a] : 0.0f;
+      for (int a = 0; a < MAXA; ++a) dv[u][a] = dq[rl * A1 + (a < A1 ? a : 0)];
     }
 #pragma unroll
     for (int u = 0; u < RB; ++u) {
@@ -490,7 +490,7 @@ __global__ __launch_bounds__(kHbThreads) void k_td_heads_backward(
 #pragma unroll
     for (int u = 0; u < RB; ++u) {
       const int64_t r = r0 + (int64_t)u * kHbGroups;
-      hv[u] = r < B ? h[r * ldh + j] : 0.0f;
+      hv[u] = h[(r < B ? r : B - 1) * ldh + j];  // unconditional (a duplicate row, unused)
     }
 #pragma unroll
     for (int u = 0; u < RB; ++u) {
@@ -561,12 +561,28 @@ __global__ __launch_bounds__(256) void k_heads_fc2(const float *__restrict__ h, 
   const float4 *hv = reinterpret_cast<const float4 *>(h + rr * ldh + H) + l * cq;
   float4 xa[U], xv[U];
 #pragma unroll
-  for (int k = 0; k < U; ++k)
-    if (k < cq) xa[k] = ha[k], xv[k] = hv[k];
+  for (int k = 0; k < U; ++k) {  // unconditional loads (k >= cq: a duplicate, unused): a load under
+    const int kk = k < cq ? k : 0;  // a branch makes the compiler wait for it before the next one
+    xa[k] = ha[kk], xv[k] = hv[kk];
+  }
   const int A1 = A + 1, H4 = H / 4;
-  for (int i = threadIdx.x; i < A1 * H4; i += 256) {
-    const int a = i / H4, j4 = i - a * H4;
-    wl[i] = reinterpret_cast<const float4 *>(a < A ? wa2 + (int64_t)a * H : wv2)[j4];
+  {  // stage the weights: every load issued before the first LDS write (a load-then-write loop
+     // waits for each load in turn)
+    constexpr int WPER = (MAXA1 * kFc2MaxH / 4 + 255) / 256;
+    const int nw = A1 * H4;
+    float4 tw[WPER];
+#pragma unroll
+    for (int u = 0; u < WPER; ++u) {
+      int i = threadIdx.x + u * 256;
+      i = i < nw ? i : nw - 1;  // a duplicate, not written
+      const int a = i / H4, j4 = i - a * H4;
+      tw[u] = reinterpret_cast<const float4 *>(a < A ? wa2 + (int64_t)a * H : wv2)[j4];
+    }
+#pragma unroll
+    for (int u = 0; u < WPER; ++u) {  // out-of-range slots land on the spare slot nw
+      const int i = threadIdx.x + u * 256;
+      wl[i < nw ? i : nw] = tw[u];
+    }
   }
   __syncthreads();
   float acc[MAXA1];
@@ -883,7 +899,7 @@ static int heads_fc2_impl(const float *h, int64_t ldh, int64_t n, int32_t H, int
   RTH_REQUIRE(H <= kFc2MaxH && H % 64 == 0,
               "rth_heads_fc2: built for H <= %d, a multiple of 64 (A=%d H=%d)", kFc2MaxH, A, H);
   const dim3 grid((unsigned)((n + 15) / 16)), block(256);
-  const size_t lds = (size_t)(A + 1) * H * 4;
+  const size_t lds = (size_t)(A + 1) * H * 4 + 16;  // + the spare slot of the staging writes
   if (A + 1 <= 8)
     hipLaunchKernelGGL((k_heads_fc2<8>), grid, block, lds, as_stream(stream), h, ldh, n, (int)H, (int)A, fc2_params[0],
                        fc2_params[1], fc2_params[2], fc2_params[3], heads, n_dev, cache, cache_rows);

@@ -947,7 +947,7 @@ static int cu_count() {
 #define DGRAD_WAVES 8
 #endif
 #ifndef DGRAD_D
-#define DGRAD_D 4  // input chunks in flight per wave (divides the chunk count)
+#define DGRAD_D 4  // input chunks in flight per wave, at most (the largest divisor of the chunk count)
 #endif
 
 template <int KH, int KW, int S, int CI, int CO, int HI, int WI>
@@ -957,7 +957,11 @@ struct DgradGeom {
   static constexpr int CPT = CO / 16, G = TAPS * CPT, NB = CI / 16, LDS_F4 = G * NB * 64;
   static_assert(KH % S == 0 && KW % S == 0 && HI % S == 0 && WI % S == 0, "stride must tile kernel and input");
   static_assert(CI % 16 == 0 && CO % 16 == 0, "channels must be multiples of 16");
-  static_assert(G % DGRAD_D == 0, "prefetch depth must divide the chunks");
+  static constexpr int D = [] {  // input chunks in flight: the largest divisor of G <= DGRAD_D
+    int d = DGRAD_D;
+    while (G % d) --d;
+    return d;
+  }();
 };
 
 // XCD-aware workgroup -> (class, tile range) map (xcd != 0; the grid a multiple of 8 x NCLS):
@@ -1026,13 +1030,14 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_dgrad(const float *__restri
     f32x4 acc[NB];
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) acc[nb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    f32x4 ar[DGRAD_D];  // input chunks in flight
+    constexpr int D = Gm::D;
+    f32x4 ar[D];  // input chunks in flight
 #pragma unroll
-    for (int d = 0; d < DGRAD_D; ++d) ar[d] = aload(d);
+    for (int d = 0; d < D; ++d) ar[d] = aload(d);
 #pragma unroll 1
-    for (int g0 = 0; g0 < Gm::G; g0 += DGRAD_D) {
+    for (int g0 = 0; g0 < Gm::G; g0 += D) {
 #pragma unroll
-      for (int d = 0; d < DGRAD_D; ++d) {
+      for (int d = 0; d < D; ++d) {
         const int g = g0 + d;
         f32x4 bf[NB];
 #pragma unroll
@@ -1042,7 +1047,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_dgrad(const float *__restri
 #pragma unroll
           for (int nb = 0; nb < NB; ++nb)
             acc[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(ar[d][tt], bf[nb][tt], acc[nb], 0, 0, 0);
-        ar[d] = aload(g + DGRAD_D);  // unconditional: the compiler keeps DGRAD_D - 1 loads in flight
+        ar[d] = aload(g + D);  // unconditional: the compiler keeps D - 1 loads in flight
       }
     }
     // C/D: lane holds column mr of rows 4q .. 4q+3
@@ -1377,12 +1382,12 @@ __device__ void bias_job(const BiasJobs &bj, int j) {
     for (int k = vt / C; k < bj.slabs[j]; k += 8 * G) {
       float v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < 8; ++u) {  // unconditional loads (clamped slab; its value is replaced by 0)
         const int kk = k + u * G;
-        v[u] = kk < bj.slabs[j] ? part[(int64_t)kk * C + c] : 0.0f;
+        v[u] = part[(int64_t)(kk < bj.slabs[j] ? kk : bj.slabs[j] - 1) * C + c];
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) s = radd(s, v[u]);
+      for (int u = 0; u < 8; ++u) s = radd(s, k + u * G < bj.slabs[j] ? v[u] : 0.0f);
     }
     red[vt] = s;
   }
@@ -1409,6 +1414,13 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const float *__restrict__ 
   float v = 0.0f;
   if (e < E) {
     int w = w0;
+    for (; w + 16 <= w1; w += 16) {  // 16 loads in flight per round trip; the sum stays in w order
+      float t[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) t[u] = partial[(int64_t)(w + u) * E + e];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v = radd(v, t[u]);
+    }
     for (; w + 8 <= w1; w += 8) {
       float t[8];
 #pragma unroll

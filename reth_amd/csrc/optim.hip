@@ -45,6 +45,19 @@ __device__ __forceinline__ float4 ld4(const float *__restrict__ p, int64_t e, in
   return r;
 }
 
+// the same load from a buffer resource over [p, p + n): one unconditional dwordx4 whose dwords
+// past n read zero (the range check), so no load sits under a branch -- the branchy form made
+// the compiler wait for each load before issuing the next.  vec segments only (16-byte aligned).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t seg_rsrc(const float *p, int64_t n) {
+  const uint64_t a = reinterpret_cast<uint64_t>(p);  // wave-uniform (the workgroup's segment)
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  const int bytes = __builtin_amdgcn_readfirstlane((int)(n * 4));
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(((uint64_t)hi << 32) | lo), 0, bytes, 0x00020000);
+}
+__device__ __forceinline__ float4 ld4b(__amdgpu_buffer_rsrc_t r, int64_t e) {
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, (uint32_t)(e * 4), 0, 0));
+}
+
 __device__ __forceinline__ void st4(float *__restrict__ p, int64_t e, int64_t n, int vec, float4 v) {
   if (vec && e + 3 < n) {
     *reinterpret_cast<float4 *>(p + e) = v;
@@ -118,8 +131,14 @@ __global__ __launch_bounds__(kOptThreads) void k_grad_sqsum(OptArgs a, double *_
   const OptSeg &sg = a.seg[seg_of(a, b)];
   const int64_t base = (b - sg.blk0) * kOptChunk;
   float4 gv[kOptV];  // every load of the chunk in flight before the first use
+  if (sg.vec) {
+    const __amdgpu_buffer_rsrc_t rg = seg_rsrc(sg.grad, sg.n);
 #pragma unroll
-  for (int k = 0; k < kOptV; ++k) gv[k] = ld4(sg.grad, base + 4 * (k * kOptThreads + threadIdx.x), sg.n, sg.vec);
+    for (int k = 0; k < kOptV; ++k) gv[k] = ld4b(rg, base + 4 * (k * kOptThreads + threadIdx.x));
+  } else {
+#pragma unroll
+    for (int k = 0; k < kOptV; ++k) gv[k] = ld4(sg.grad, base + 4 * (k * kOptThreads + threadIdx.x), sg.n, 0);
+  }
   double acc = 0.0;
 #pragma unroll
   for (int k = 0; k < kOptV; ++k) {
@@ -149,13 +168,26 @@ __global__ __launch_bounds__(kOptThreads) void k_adam(OptArgs a, const double *_
   const int64_t base = (b - sg.blk0) * kOptChunk;
   // this chunk's loads first, then the global norm from the partials (overlapping them)
   float4 gv[kOptV], mv[kOptV], vv[kOptV], pv[kOptV];
+  if (sg.vec) {
+    const __amdgpu_buffer_rsrc_t rg = seg_rsrc(sg.grad, sg.n), rm = seg_rsrc(sg.m, sg.n), rv = seg_rsrc(sg.v, sg.n),
+                                 rp = seg_rsrc(sg.param, sg.n);
 #pragma unroll
-  for (int k = 0; k < kOptV; ++k) {
-    const int64_t e = base + 4 * (k * kOptThreads + threadIdx.x);
-    gv[k] = ld4(sg.grad, e, sg.n, sg.vec);
-    mv[k] = ld4(sg.m, e, sg.n, sg.vec);
-    vv[k] = ld4(sg.v, e, sg.n, sg.vec);
-    pv[k] = ld4(sg.param, e, sg.n, sg.vec);
+    for (int k = 0; k < kOptV; ++k) {
+      const int64_t e = base + 4 * (k * kOptThreads + threadIdx.x);
+      gv[k] = ld4b(rg, e);
+      mv[k] = ld4b(rm, e);
+      vv[k] = ld4b(rv, e);
+      pv[k] = ld4b(rp, e);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < kOptV; ++k) {
+      const int64_t e = base + 4 * (k * kOptThreads + threadIdx.x);
+      gv[k] = ld4(sg.grad, e, sg.n, 0);
+      mv[k] = ld4(sg.m, e, sg.n, 0);
+      vv[k] = ld4(sg.v, e, sg.n, 0);
+      pv[k] = ld4(sg.param, e, sg.n, 0);
+    }
   }
   const OptScalars sc = opt_scalars(part, nparts, red, sa.clip, sa.max_norm, sa.lr, sa.beta1, sa.beta2, *sa.step);
   if (b == 0 && threadIdx.x == 0) {

@@ -281,9 +281,12 @@ __device__ __forceinline__ void pack_conv1_bf16x3(const float *__restrict__ w, u
   if (sl >= kC1PackedBytes / 16) return;
   const int lane = sl % 64, t = (sl / 64) % 3, c = sl / 192;
   const int co = lane & 31, rho = 2 * c + (lane >> 5), ci = rho >> 3, kh = rho & 7;
+  float wv[8];  // every load before the first split (the split's branches kept them one at a time)
+#pragma unroll
+  for (int j = 0; j < 8; ++j) wv[j] = w[((co * 8 + kh) * 8 + j) * 4 + ci];
   uint32_t e[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) e[j] = bf16x3_term(w[((co * 8 + kh) * 8 + j) * 4 + ci], t);
+  for (int j = 0; j < 8; ++j) e[j] = bf16x3_term(wv[j], t);
   packed[sl] = u32x4{e[0] | (e[1] << 16), e[2] | (e[3] << 16), e[4] | (e[5] << 16), e[6] | (e[7] << 16)};
 }
 
@@ -664,9 +667,12 @@ __device__ __forceinline__ void pack_x9(const float *__restrict__ w, u32x4 *__re
   if (sl >= G::PACKED_U4) return;
   const int lane = sl % 64, t = (sl / 64) % 3, c = (sl / 192) % G::NCH, cb = sl / (192 * G::NCH);
   const int co = cb * 16 + (lane & 15), k0 = c * 32 + 8 * (lane >> 4);
+  const float4 *wp = reinterpret_cast<const float4 *>(w + (int64_t)co * G::K + k0);  // 32-byte aligned run
+  const float4 w0 = wp[0], w1 = wp[1];  // both loads before the first split
+  const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
   uint32_t e[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) e[j] = bf16x3_term(w[(int64_t)co * G::K + k0 + j], t);
+  for (int j = 0; j < 8; ++j) e[j] = bf16x3_term(wv[j], t);
   packed[sl] = u32x4{e[0] | (e[1] << 16), e[2] | (e[3] << 16), e[4] | (e[5] << 16), e[6] | (e[7] << 16)};
 }
 

@@ -199,19 +199,41 @@ struct ActorTail {
   int ext_frames;  // the observations come from rth_atari_env_step (no synthetic frame bytes)
 };
 
+// MAXL > 0: the heads rows (A + 1 <= MAXL values) are loaded into registers all at once
+// (load_row / td_huber_row_reg, the same arithmetic) instead of one value per round trip
+template <int MAXL>
 __global__ __launch_bounds__(kEnvThreads) void k_actor_tail(ActorTail a) {
   const int64_t i = blockIdx.x;
   const int64_t t = *a.t_dev;
   int64_t act = 0;
   if (threadIdx.x == 0) {
-    act = eps_greedy_one(a.q, i, a.A, 1, a.eps, nullptr, nullptr, a.seed, (uint64_t)t);
+    if constexpr (MAXL > 0) {
+      const uint64_t ctr = (uint64_t)t;
+      const double u = philox_uniform(a.seed, ctr, (uint32_t)i, STREAM_EXPLORE);
+      float r[MAXL], q[MAXL];
+      load_row(a.q + i * (a.A + 1), a.A + 1, r);  // issued before the exploration branch
+      if (u < a.eps[i]) {
+        uint32_t c[4] = {(uint32_t)i, (uint32_t)ctr, (uint32_t)(ctr >> 32), STREAM_RANDACT};
+        philox4x32(c, (uint32_t)a.seed, (uint32_t)(a.seed >> 32));
+        act = (int64_t)(((uint64_t)c[0] * (uint64_t)a.A) >> 32);
+      } else {
+        q_row_reg(r, a.A, 1, q);
+        act = argmax_first_reg(q, a.A);
+      }
+    } else {
+      act = eps_greedy_one(a.q, i, a.A, 1, a.eps, nullptr, nullptr, a.seed, (uint64_t)t);
+    }
     a.action[i] = act;
   } else if (threadIdx.x == 64 && a.td_abs) {  // another wave: the previous row's |td|
     const int A1 = a.A + 1;
     const float *q0 = a.qcache + a.prev_s0[i] * A1, *q1 = a.qcache + a.prev_s1[i] * A1;
-    float l;
-    const float td = td_huber_row(q0, q1, q1, a.prev_a + i, a.prev_r + i, a.prev_done + i, nullptr, 0, a.A, 1,
-                                  a.gamma_n, 1, 1.0f, &l, nullptr);
+    float l, td;
+    if constexpr (MAXL > 0)
+      td = td_huber_row_reg<MAXL>(q0, q1, q1, a.prev_a[i], a.prev_r[i], a.prev_done[i], 1.0f, 0, a.A, 1, a.gamma_n, 1,
+                                  &l);
+    else
+      td = td_huber_row(q0, q1, q1, a.prev_a + i, a.prev_r + i, a.prev_done + i, nullptr, 0, a.A, 1, a.gamma_n, 1,
+                        1.0f, &l, nullptr);
     a.td_abs[i] = fabsf(td);
   }
   const EnvOut e = env_step_one(a.frames, a.ring, t, i, a.cur_slot, a.seed, a.p_reward, a.p_done, a.r_out, a.done_out,
@@ -392,6 +414,14 @@ int rth_actor_prologue(int64_t *t_dev, const int64_t *cur_slot, int64_t n, int64
   return RTH_OK;
 }
 
+static bool actor_tail_reg() {  // RTH_ACTOR_TAIL_REG=0: the pointer-form rows (A/B)
+  static const bool v = [] {
+    const char *e = getenv("RTH_ACTOR_TAIL_REG");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 int rth_actor_tail(rth_nstep *h, const rth_actor_tail_args *x, int32_t *emit, int64_t *s0_out, int64_t *a_out,
                    float *r_out, int64_t *s1_out, float *done_out, void *stream) {
   RTH_REQUIRE(h && x && emit && s0_out && a_out && r_out && s1_out && done_out, "rth_actor_tail: NULL argument");
@@ -406,7 +436,10 @@ int rth_actor_tail(rth_nstep *h, const rth_actor_tail_args *x, int32_t *emit, in
               x->prev_r, x->prev_done, x->gamma_n, x->td_abs, x->frames, x->ring, x->cur_slot, x->p_reward,
               x->p_done, x->r_out, x->done_out, x->s0_h, x->s1_h, h->st, h->n, h->gamma, h->mode, emit,
               s0_out, a_out, s1_out, r_out, done_out, x->A, x->ext_frames};
-  hipLaunchKernelGGL(k_actor_tail, dim3((unsigned)x->N), dim3(kEnvThreads), 0, as_stream(stream), a);
+  if (x->A + 1 <= 8 && actor_tail_reg())  // Atari's minimal action sets (Pong 6, Breakout 4)
+    hipLaunchKernelGGL(k_actor_tail<8>, dim3((unsigned)x->N), dim3(kEnvThreads), 0, as_stream(stream), a);
+  else
+    hipLaunchKernelGGL(k_actor_tail<0>, dim3((unsigned)x->N), dim3(kEnvThreads), 0, as_stream(stream), a);
   RTH_LAUNCHED();
   return RTH_OK;
 }

@@ -162,6 +162,93 @@ __device__ inline void q_row(const float *row, int A, int dueling, float *q) {
   for (int j = 0; j < A; ++j) q[j] = rsub(radd(v, row[j]), mean);
 }
 
+// The same row arithmetic with each network-output row held in registers: MAXL >= A + dueling
+// values loaded unconditionally (indices clamped to the row), so every load of a row is issued
+// before any is waited for -- the pointer forms' runtime-length loops load one value per round
+// trip.  Identical operations in identical order: the results equal q_row / argmax_first /
+// td_huber_row bit for bit.
+template <int MAXL>
+__device__ inline void load_row(const float *__restrict__ row, int L, float (&v)[MAXL]) {
+#pragma unroll
+  for (int j = 0; j < MAXL; ++j) v[j] = row[j < L ? j : L - 1];
+}
+
+template <int MAXL>
+__device__ inline void q_row_reg(const float (&r)[MAXL], int A, int dueling, float (&q)[MAXL]) {
+  if (!dueling) {
+#pragma unroll
+    for (int j = 0; j < MAXL; ++j) q[j] = r[j];
+    return;
+  }
+  float s = 0.0f, v = 0.0f;
+#pragma unroll
+  for (int j = 0; j < MAXL; ++j) {
+    if (j < A) s = radd(s, r[j]);
+    if (j == A) v = r[j];
+  }
+  const float mean = rmul(s, 1.0f / (float)A);
+#pragma unroll
+  for (int j = 0; j < MAXL; ++j) q[j] = rsub(radd(v, r[j]), mean);
+}
+
+template <int MAXL>
+__device__ inline int argmax_first_reg(const float (&q)[MAXL], int A) {  // argmax_first's rule
+  int best = 0;
+  float bv = q[0];
+  bool stop = false;
+#pragma unroll
+  for (int j = 1; j < MAXL; ++j)
+    if (j < A && !stop) {
+      if (bv != bv) {
+        stop = true;
+      } else if (q[j] != q[j] || q[j] > bv) {
+        bv = q[j];
+        best = j;
+      }
+    }
+  return best;
+}
+
+template <int MAXL>
+__device__ inline float pick(const float (&q)[MAXL], int i) {  // q[i] as a select chain in registers
+  float x = q[0];
+#pragma unroll
+  for (int j = 1; j < MAXL; ++j) {
+    float qj = q[j];
+    asm volatile("" : "+v"(qj));  // opaque: LLVM would turn the chain back into a scratch array lookup
+    x = j == i ? qj : x;
+  }
+  return x;
+}
+
+// td_huber_row for rows given as pointers to their first value (q0r / q1r / q1tr), no dq
+template <int MAXL>
+__device__ inline float td_huber_row_reg(const float *__restrict__ q0r, const float *__restrict__ q1r,
+                                         const float *__restrict__ q1tr, int64_t a, float rw, float dn, float w,
+                                         int has_w, int A, int dueling, float gamma_n, int double_q, float *l_out) {
+  const int ld = A + dueling;
+  float r0[MAXL], r1[MAXL], r2[MAXL];
+  load_row(q0r, ld, r0);
+  load_row(double_q ? q1r : q1tr, ld, r1);
+  load_row(q1tr, ld, r2);
+  float qa[MAXL], qs[MAXL];
+  q_row_reg(r0, A, dueling, qa);
+  const float q = pick(qa, (int)a);  // sum(q * one_hot(a)) (:79-81)
+  q_row_reg(r1, A, dueling, qs);
+  const int astar = argmax_first_reg(qs, A);  // (:83-94)
+  if (double_q) q_row_reg(r2, A, dueling, qs);
+  const float nqb = pick(qs, astar);
+  float t = rmul(gamma_n, nqb);  // expected = r + (gamma**n * next_q_best) * (1 - done)  (:96)
+  t = rmul(t, rsub(1.0f, dn));
+  const float y = radd(rw, t);
+  const float td = rsub(q, y);  // (:97)
+  const float z = fabsf(td);
+  float l = z < 1.0f ? rmul(rmul(0.5f, z), z) : rsub(z, 0.5f);  // smooth_l1 (:112) * w (:113-114)
+  if (has_w) l = rmul(l, w);
+  *l_out = l;
+  return td;
+}
+
 // One row of DQNSolver._calc_td_error + the IS-weighted smooth-L1 loss (dqn_solver.py:77-114):
 // returns td; *l_out = smooth_l1(|td|) * w; dq_row (nullable, A + dueling values) = d(mean
 // loss)/d(q row of s0) -- through Q = (V + A) - mean(A) when dueling.  f32, no contraction.

@@ -51,19 +51,30 @@ __global__ __launch_bounds__(kEpiThreads) void k_relu_bias_grad(const float4 *__
   const int64_t r0 = (int64_t)blockIdx.x * per;
   const int64_t r1 = min<int64_t>(rows, r0 + per);
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int64_t r = r0 + tid / Q; r < r1; r += R) {
-    const int64_t i = r * Q + q;
-    const float4 gv = g[i], yv = y[i];
-    float4 o;
-    o.x = yv.x > 0.0f ? gv.x : 0.0f;  // threshold_backward(g, y, 0): y <= 0 -> 0
-    o.y = yv.y > 0.0f ? gv.y : 0.0f;
-    o.z = yv.z > 0.0f ? gv.z : 0.0f;
-    o.w = yv.w > 0.0f ? gv.w : 0.0f;
-    gy[i] = o;
-    acc.x = radd(acc.x, o.x);
-    acc.y = radd(acc.y, o.y);
-    acc.z = radd(acc.z, o.z);
-    acc.w = radd(acc.w, o.w);
+  constexpr int U = 4;  // rows per round trip: their loads all in flight, summed in row order
+  for (int64_t r = r0 + tid / Q; r < r1; r += U * R) {
+    float4 gv[U], yv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t rr = r + u * R, i = (rr < r1 ? rr : r) * Q + q;  // past r1: a duplicate, unused
+      gv[u] = g[i];
+      yv[u] = y[i];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t rr = r + u * R;
+      if (rr >= r1) break;
+      float4 o;
+      o.x = yv[u].x > 0.0f ? gv[u].x : 0.0f;  // threshold_backward(g, y, 0): y <= 0 -> 0
+      o.y = yv[u].y > 0.0f ? gv[u].y : 0.0f;
+      o.z = yv[u].z > 0.0f ? gv[u].z : 0.0f;
+      o.w = yv[u].w > 0.0f ? gv[u].w : 0.0f;
+      gy[rr * Q + q] = o;
+      acc.x = radd(acc.x, o.x);
+      acc.y = radd(acc.y, o.y);
+      acc.z = radd(acc.z, o.z);
+      acc.w = radd(acc.w, o.w);
+    }
   }
   red[tid] = acc;
   __syncthreads();
@@ -103,10 +114,21 @@ __global__ __launch_bounds__(kEpiThreads) void k_relu_bias_grad_nchw(const float
   float acc = 0.0f;
   for (int64_t b = b0; b < b1; ++b) {
     const float *gb = g + b * E, *yb = y + b * E;
-    for (int i = tid; i < E; i += kEpiThreads) {  // NCHW order: i = c * P + p
-      const float yv = yb[i], gv = gb[i];
-      const int c = i / P, pp = i - c * P;
-      tile[c * LP + pp] = yv > 0.0f ? gv : 0.0f;  // threshold_backward(g, y, 0)
+    constexpr int U = (kNchwMaxTile + kEpiThreads - 1) / kEpiThreads;
+    float yv[U], gv[U];  // the sample's loads all in flight (a load-then-use loop waited for each)
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = tid + u * kEpiThreads, ic = i < E ? i : E - 1;  // past E: a duplicate, unused
+      yv[u] = yb[ic];
+      gv[u] = gb[ic];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {  // NCHW order: i = c * P + p
+      const int i = tid + u * kEpiThreads;
+      if (i < E) {
+        const int c = i / P, pp = i - c * P;
+        tile[c * LP + pp] = yv[u] > 0.0f ? gv[u] : 0.0f;  // threshold_backward(g, y, 0)
+      }
     }
     __syncthreads();
     for (int p = p0; p < p1; ++p) acc = radd(acc, tile[c_own * LP + p]);

@@ -638,6 +638,72 @@ __global__ __launch_bounds__(256) void k_heads_fc2(const float *__restrict__ h, 
   }
 }
 
+// k_heads_fc2 without LDS and within 64 VGPRs (the default for A + 1 <= 8): the weights are read
+// from L2 one float4 column group at a time, so a workgroup fits beside kernels that hold most
+// of a CU's LDS and registers (the x9 convs) instead of waiting for a free CU: 0.586 vs 0.589
+// ms/step interleaved.  The same lanes, terms and order as k_heads_fc2: bit-identical
+template <int MAXA1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_heads_fc2_lean(const float *__restrict__ h, int64_t ldh, int64_t n, int H,
+                                                        int A, const float *__restrict__ wa2,
+                                                        const float *__restrict__ wv2, const float *__restrict__ ba2,
+                                                        const float *__restrict__ bv2, float *__restrict__ heads,
+                                                        const int64_t *__restrict__ n_dev, float *__restrict__ cache,
+                                                        const int64_t *__restrict__ cache_rows) {
+  if (n_dev) {
+    const int64_t nd = *n_dev;
+    n = nd < n ? nd : n;
+    if ((int64_t)blockIdx.x * 16 >= n) return;  // uniform
+  }
+  const int l = threadIdx.x & 15;
+  const int64_t r = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
+  const int64_t rr = r < n ? r : n - 1;  // tail rows: a duplicate, nothing written
+  const int cq = H / 64, A1 = A + 1;
+  const float4 *ha = reinterpret_cast<const float4 *>(h + rr * ldh) + l * cq;
+  const float4 *hv = reinterpret_cast<const float4 *>(h + rr * ldh + H) + l * cq;
+  float acc[MAXA1];
+#pragma unroll
+  for (int a = 0; a < MAXA1; ++a) acc[a] = 0.0f;
+#pragma unroll 1
+  for (int k = 0; k < cq; ++k) {
+    const float4 xa = ha[k], xv = hv[k];
+    float4 w[MAXA1];
+#pragma unroll
+    for (int a = 0; a < MAXA1; ++a) {
+      const int ac = a < A1 ? a : A;  // past A: a duplicate row, unused
+      w[a] = reinterpret_cast<const float4 *>(ac < A ? wa2 + (int64_t)ac * H : wv2)[l * cq + k];
+    }
+#pragma unroll
+    for (int a = 0; a < MAXA1; ++a)
+      if (a < A1) {
+        const float4 x = a < A ? xa : xv, ww = w[a];
+        acc[a] = radd(radd(radd(radd(acc[a], rmul(x.x, ww.x)), rmul(x.y, ww.y)), rmul(x.z, ww.z)), rmul(x.w, ww.w));
+      }
+  }
+#pragma unroll
+  for (int a = 0; a < MAXA1; ++a)
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) acc[a] = radd(acc[a], __shfl_xor(acc[a], o, 64));
+  if (l == 0 && r < n) {
+    float *out = heads + r * A1;
+    float *co = cache ? cache + cache_rows[r] * A1 : nullptr;
+#pragma unroll
+    for (int a = 0; a < MAXA1; ++a)
+      if (a <= A) {
+        const float v = radd(acc[a], a < A ? ba2[a] : bv2[0]);
+        out[a] = v;
+        if (co) co[a] = v;
+      }
+  }
+}
+
+static bool fc2_lean() {  // k_heads_fc2_lean for A + 1 <= 8 (RTH_FC2_LEAN=0: the LDS-staged form)
+  static const bool v = [] {
+    const char *e = getenv("RTH_FC2_LEAN");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 // rows [r0, min(*n_dev, n_max)) of y = relu(x w^T + b), x [*, F] row stride ldx, w [O, F],
 // y row stride ldy: the device-counted tail of a batch whose first r0 rows a library GEMM
 // covers (the actors' terminal stacks behind the acting rows: none in most steps, so every
@@ -922,7 +988,10 @@ static int heads_fc2_impl(const float *h, int64_t ldh, int64_t n, int32_t H, int
               "rth_heads_fc2: built for H <= %d, a multiple of 64 (A=%d H=%d)", kFc2MaxH, A, H);
   const dim3 grid((unsigned)((n + 15) / 16)), block(256);
   const size_t lds = (size_t)(A + 1) * H * 4 + 16;  // + the spare slot of the staging writes
-  if (A + 1 <= 8)
+  if (A + 1 <= 8 && fc2_lean())
+    hipLaunchKernelGGL((k_heads_fc2_lean<8>), grid, block, 0, as_stream(stream), h, ldh, n, (int)H, (int)A,
+                       fc2_params[0], fc2_params[1], fc2_params[2], fc2_params[3], heads, n_dev, cache, cache_rows);
+  else if (A + 1 <= 8)
     hipLaunchKernelGGL((k_heads_fc2<8>), grid, block, lds, as_stream(stream), h, ldh, n, (int)H, (int)A, fc2_params[0],
                        fc2_params[1], fc2_params[2], fc2_params[3], heads, n_dev, cache, cache_rows);
   else

@@ -461,7 +461,8 @@ __global__ __launch_bounds__(kHbThreads) void k_td_heads_backward(
     const double *__restrict__ isw, int64_t B, int A, float gamma_n, int double_q, const float *__restrict__ h,
     int64_t ldh, Fc2 f, int H2, float *__restrict__ td_abs, float *__restrict__ loss_out,
     float *__restrict__ gh, float *__restrict__ gb1, float *__restrict__ td_acc) {
-  __shared__ float dqs[kTdHbMaxElems];
+  extern __shared__ float dqs[];  // B * (A + 1) floats (dynamic: a 16 K-float static array kept
+                                  // the kernel off every CU a conv kernel shares)
   __shared__ float red[kHbThreads];
   const int tid = threadIdx.x, A1 = A + 1;
   const bool tail = (int)blockIdx.x == H2 / kHbCols;  // gb2, |td|, loss, |td| mean
@@ -912,12 +913,13 @@ static int td_heads_backward_impl(const float *q0, const float *q1o, const float
               "rth_td_heads_backward: bad shape B=%lld A=%lld H2=%d (B * (A + 1) <= %d)", (long long)B, (long long)A,
               H2, kTdHbMaxElems);
   const dim3 grid((unsigned)(H2 / kHbCols + 1)), block(kHbThreads);
+  const size_t lds = (size_t)B * (A + 1) * 4;
   if (A + 1 <= 8)
-    hipLaunchKernelGGL((k_td_heads_backward<8, 4>), grid, block, 0, as_stream(stream), q0, q1o, q1t, a, r, done, isw, B,
-                       (int)A, gamma_n, double_q, h, ldh, f, H2, td_abs, loss_out, gh, gb1, td_acc);
+    hipLaunchKernelGGL((k_td_heads_backward<8, 4>), grid, block, lds, as_stream(stream), q0, q1o, q1t, a, r, done, isw,
+                       B, (int)A, gamma_n, double_q, h, ldh, f, H2, td_abs, loss_out, gh, gb1, td_acc);
   else
-    hipLaunchKernelGGL((k_td_heads_backward<kHbMaxA1, 1>), grid, block, 0, as_stream(stream), q0, q1o, q1t, a, r, done,
-                       isw, B, (int)A, gamma_n, double_q, h, ldh, f, H2, td_abs, loss_out, gh, gb1, td_acc);
+    hipLaunchKernelGGL((k_td_heads_backward<kHbMaxA1, 1>), grid, block, lds, as_stream(stream), q0, q1o, q1t, a, r,
+                       done, isw, B, (int)A, gamma_n, double_q, h, ldh, f, H2, td_abs, loss_out, gh, gb1, td_acc);
   RTH_LAUNCHED();
   return RTH_OK;
 }

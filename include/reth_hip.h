@@ -47,6 +47,10 @@ const char *rth_last_error(void);
 int rth_debug_tree_timing(long long *out9);
 /* library build/ABI version (major*10000 + minor*100 + patch) */
 int rth_version(void);
+/* the source tree the library was compiled from: 40 hex digits, the SHA-1 over the lines
+ * "<git blob id> <path>\n" of reth_amd/csrc/ and include/reth_hip.h in path order
+ * (reth_amd._lib.source_build_id; reproducible from `git ls-tree -r HEAD`) */
+const char *rth_build_id(void);
 
 /* ------------------------------------------------------------------------------------
  * In-order heap sum-tree, fp64, resident in HBM.

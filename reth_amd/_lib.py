@@ -77,6 +77,7 @@ class ActorTailArgs(ctypes.Structure):
 SIGNATURES = {
     "rth_last_error": (ctypes.c_char_p, []),
     "rth_version": (c_i32, []),
+    "rth_build_id": (ctypes.c_char_p, []),
     # sum-tree
     "rth_sumtree_create": (c_i32, [c_i64, c_i32, ctypes.POINTER(c_vp)]),
     "rth_sumtree_destroy": (c_i32, [c_vp]),
@@ -196,6 +197,45 @@ SIGNATURES = {
 
 _lib = None
 _load_error = None
+
+_SRC_EXT = (".hip", ".hpp", ".cpp", ".h")
+
+
+def source_files(root=None):
+    """the library's sources, relative to the repo root, in path order"""
+    root = root or os.path.dirname(_HERE)
+    csrc = os.path.join(root, "reth_amd", "csrc")
+    rel = sorted(f"reth_amd/csrc/{f}" for f in os.listdir(csrc) if f.endswith(_SRC_EXT))
+    return rel + ["include/reth_hip.h"]
+
+
+def source_build_id(root=None):
+    """SHA-1 over "<git blob id> <path>\\n" of every library source (the id compiled into
+    the library as rth_build_id()); from git: `git ls-tree -r HEAD reth_amd/csrc include/reth_hip.h`
+    lists the same blob ids"""
+    import hashlib
+
+    root = root or os.path.dirname(_HERE)
+    h = hashlib.sha1()
+    for rel in source_files(root):
+        with open(os.path.join(root, rel), "rb") as f:
+            data = f.read()
+        blob = hashlib.sha1(b"blob %d\0" % len(data) + data).hexdigest()
+        h.update(f"{blob} {rel}\n".encode())
+    return h.hexdigest()
+
+
+def library_build_id(path=None):
+    """the id compiled into a built library, read from its bytes (no dlopen); None if absent"""
+    import re
+
+    path = path or LIB_PATH
+    try:
+        with open(path, "rb") as f:
+            m = re.search(rb"RTH_BUILD_ID:([0-9a-f]{40})", f.read())
+    except OSError:
+        return None
+    return m.group(1).decode() if m else None
 
 
 def _load():

@@ -65,6 +65,13 @@ const char *rth_last_error(void) { return g_last_error.c_str(); }
 
 int rth_version(void) { return 100; }  // 0.1.0
 
+#ifndef RTH_BUILD_ID
+#define RTH_BUILD_ID "unknown"
+#endif
+// the marker lets __graft_entry__.build() read the id from the file without loading it
+static const char k_build_id_marker[] __attribute__((used)) = "RTH_BUILD_ID:" RTH_BUILD_ID;
+const char *rth_build_id(void) { return k_build_id_marker + 13; }
+
 int rth_td_huber(const float *q0, const float *q1o, const float *q1t, const int64_t *a, const float *r,
                  const float *done, const double *isw, int64_t B, int64_t A, float gamma_n, int32_t double_q,
                  int32_t dueling, float *td_out, float *td_abs_out, float *loss_elem, float *loss_out, float *dq,

@@ -30,6 +30,14 @@ def test_library_exports_every_declared_symbol():
     assert lib.rth_version() == 100
 
 
+def test_library_built_from_this_tree():
+    """the compiled-in source id equals the tree's (build() rebuilds on any difference)"""
+    from reth_amd import _lib
+
+    assert _lib.lib().rth_build_id().decode() == _lib.source_build_id()
+    assert _lib.library_build_id() == _lib.source_build_id()
+
+
 def test_binding_covers_header():
     from reth_amd import _lib
 

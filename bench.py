@@ -464,19 +464,25 @@ def hbm_bytes(cfg, n_rows_per_append):
     }
 
 
-def hbm_rooflines(ax, timer, tag):
+def hbm_rooflines(ax, timer, probe_ms, tag):
     """roofline_hbm: the HBM-bound kernels north_star names (tree insert / sample / priority
-    update, n-step + env (k_actor_tail), TD, gather, Adam) -- algorithmic bytes per launch /
-    in-loop launch duration.  Durations: live HIP events for the replay's eager launches; the
-    kernels inside the captured actor / learner graphs from the rocprofv3 kernel trace of
-    the same bench command (profiles/traffic_TAG.json 'inloop_us', scripts/summarize_profile.py)."""
+    update, n-step + env (k_actor_tail), TD, gather, clip+Adam) -- algorithmic bytes per launch /
+    in-loop launch duration, every duration measured live in the probe window: HIP events
+    around the replay's eager launches (rth_replay_set_timing) and around the launches the
+    probe graph copies issue between their parts (the actor tail on the actor stream, the
+    TD/heads backward and rth_clip_adam on the learner stream).  `traffic` (HBM bytes per
+    launch) is PMC data from a separate rocprofv3 pass of the same command, read from
+    profiles/traffic_TAG.json and labelled as such."""
     cfg = ax.cfg
     nparams = sum(p.numel() for p in ax.solver._params)
     rows = cfg.n_actors  # one append of N rows per actor step (fused actor: the previous step's rows)
     by = hbm_bytes(cfg, rows)
-    by["k_adam"] = nparams * 28  # read p, g, m, v; write p, m, v (fp32)
+    # rth_clip_adam = k_grad_sqsum (reads g) + k_adam (reads p, g, m, v; writes p, m, v), fp32
+    by["rth_clip_adam (k_grad_sqsum + k_adam)"] = nparams * (4 + 28)
     live = {"k_tree_update_sub": "tree_update", "k_tree_sample": "sample", "k_copy_rows (gather)": "gather",
             "k_copy_rows (insert)": "insert"}
+    probed = {"k_actor_tail": "actor_tail", "k_td_heads_backward": "td_heads_backward",
+              "rth_clip_adam (k_grad_sqsum + k_adam)": "clip_adam"}
     prof = {}
     full = os.path.join(ROOT, "profiles", f"traffic_{tag}.json")
     if os.path.exists(full):
@@ -484,17 +490,19 @@ def hbm_rooflines(ax, timer, tag):
             prof = json.load(f)
     out = []
     for name, nbytes in by.items():
+        us, n, src = None, 0, None
         if name in live:
             us, n = timer.mean_us(live[name])
-            src = f"live HIP events (rth_replay_set_timing), {n} launches"
-        else:
-            us = prof.get("inloop_us", {}).get(name)
-            n = None
-            src = f"rocprofv3 kernel trace of the bench (profiles/traffic_{tag}.json inloop_us)" if us else None
+            src = f"live HIP events (rth_replay_set_timing) in the probe window, {n} launches"
+        elif probe_ms.get(probed[name]):
+            ms = probe_ms[probed[name]]
+            us, n = float(np.mean(ms)) * 1e3, len(ms)
+            src = f"live HIP events around the probe graphs' eager launch in the probe window, {n} launches"
         traffic = prof.get("hbm_bytes_per_launch", {}).get(name)
         ent = {"kernel": name, "bound": "hbm", "bytes_per_launch": int(nbytes), "mean_launch_us": None,
                "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None, "traffic": traffic,
-               "traffic_ratio": round(traffic / nbytes, 3) if traffic else None, "time_source": src}
+               "traffic_ratio": round(traffic / nbytes, 3) if traffic else None, "time_source": src,
+               "traffic_source": f"profiles/traffic_{tag}.json (PMC pass)" if traffic else None}
         if us:
             gbs = nbytes / (us * 1e-6) / 1e9
             ent.update(mean_launch_us=round(us, 2), achieved=round(gbs, 1), frac=round(gbs / HBM_PEAK_GBS, 4))
@@ -571,6 +579,10 @@ def main():
                     help="SURVEY §8(d) C4 hyperparameter-faithful data parallelism: a global batch of --batch "
                          "split over the N learners (B / N per GPU) instead of B per GPU")
     ap.add_argument("--windows", type=int, default=5, help="sub-windows of the timed region reported beside it")
+    ap.add_argument("--settle", type=int, default=256, help="iterations of the captured loop between the graph "
+                    "capture and the W warmup steps (setup, not timed)")
+    ap.add_argument("--probe-steps", type=int, default=60, help="iterations of the probe window after the timed "
+                    "region (live per-launch HIP-event timing of the roofline kernels)")
     ap.add_argument("--no-probe", action="store_true", help="do not cut the learner graph around conv2/conv3 "
                     "(no live per-launch timing of the dominant kernels)")
     ap.add_argument("--actor-steps-per-update", type=int, default=None,
@@ -640,12 +652,34 @@ def main():
                             "probe_conv2": probe})
     ax = ApexDQN(cfg, device=dev, rank=rank, world=world)
     ax.prefill(cfg.capacity)
-    for _ in range(args.warmup):
+    # graph preparation (setup, like the prefill): iterate until the actor / learner / target
+    # graphs are captured, upload every captured graph (hipGraphUpload: a variant first replayed
+    # inside the timed region -- the learner's "full" variant after a target sync, the actors'
+    # "full" pass after a weights reload -- does not pay its first-launch cost there), then
+    # `settle` iterations of the captured loop, so the timed region starts in the loop's steady
+    # state (r03's driver windows fell 0.663 -> 0.600 ms over the first 20 steps after capture);
+    # then the W warmup steps the command asks for
+    prep = {"capture_iterations": 0, "settle_iterations": 0, "graphs_uploaded": 0}
+    if cfg.hip_graph:
+        while ax._graphs is None and prep["capture_iterations"] < 64:
+            ax.iteration()
+            prep["capture_iterations"] += 1
+        if ax._graphs is not None:
+            prep["graphs_uploaded"] = ax.upload_graphs()
+            sync_tail = int(os.environ.get("RTH_BENCH_SETTLE_SYNC", "0"))
+            for i in range(args.settle):
+                ax.iteration()
+                if i >= args.settle - sync_tail:
+                    torch.cuda.synchronize()
+            prep["settle_iterations"] = args.settle
+    for i in range(args.warmup):
         ax.iteration()
 
-    # the dominant kernels, live: events on the learner stream around its conv2 and conv3
-    # launches (the learner graph is cut there: ApexDQN._learner_replay calls conv_probe
-    # between parts)
+    # live per-launch timing (the probe window after the headline): HIP events on the launching
+    # stream around the launches the probe graph copies leave out -- conv2 / conv3 forward, the
+    # TD/heads backward and clip+Adam on the learner stream, the actor tail on the actor stream
+    # (ApexDQN._replay_parts / _learner_replay call conv_probe between the parts) -- and the
+    # replay shard's eager launches (ReplayKernelTimer)
     conv_events = {"conv2": [], "conv3": []}
 
     def conv_probe(tag):
@@ -688,27 +722,41 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    ax.conv_probe = conv_probe
-    # sub-window boundaries: events on the iteration stream (no synchronisation inside the
-    # timed region); the headline is the whole region
+    # ------------------------------------------------------------------ the timed region
+    # the uncut graphs, no per-launch timers: sub-window boundaries are events on the iteration
+    # stream (no synchronisation inside the timed region); the headline is the whole region
     n_win = max(1, min(args.windows, args.steps))
     win_at = {round(args.steps * i / n_win) for i in range(n_win + 1)}
     win_ev = []
     t0 = time.perf_counter()
     debug = os.environ.get("RTH_BENCH_DEBUG")
-    ktimer = ReplayKernelTimer(ax.replay)
+    step_ev = [] if os.environ.get("RTH_BENCH_STEPTIMES") else None
+    host_ms = []
     for k in range(args.steps):
         if k in win_at:
             e = torch.cuda.Event(enable_timing=True)
             e.record(ax._stream if hasattr(ax, "_stream") else None)
             win_ev.append((k, e))
-        ktimer.arm()
-        ax.iteration()
+        if step_ev is not None:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(ax._stream)
+            step_ev.append(e)
+        th = time.perf_counter()
+        if k == 0 and os.environ.get("RTH_BENCH_PROFILE0"):  # diagnostics: where step 0's host time goes
+            import cProfile
+            import pstats
+
+            pr = cProfile.Profile()
+            pr.runcall(ax.iteration)
+            pstats.Stats(pr, stream=sys.stderr).sort_stats("tottime").print_stats(12)
+        else:
+            ax.iteration()
+        if step_ev is not None:
+            host_ms.append((time.perf_counter() - th) * 1e3)
         if debug:
             torch.cuda.synchronize()
             print(f"rank {rank} step {k}: {1e3 * (time.perf_counter() - t0):.1f} ms graphs={ax._graphs is not None} "
                   f"updates={ax.updates} pending={ax.loader.pending()}", file=sys.stderr, flush=True)
-    ktimer.stop()
     e = torch.cuda.Event(enable_timing=True)
     e.record(ax._stream)
     win_ev.append((args.steps, e))
@@ -716,7 +764,6 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    ax.conv_probe = None
     n_upd, n_env = ax.updates - u0, ax.env_steps - e0
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
@@ -735,7 +782,32 @@ def main():
             late = [spans[i][1].elapsed_time(ready[i]) * 1e3 for i in range(m)]
             print(f"next batch ready after the learner block ends: mean {np.mean(late):.1f} us, median "
                   f"{np.median(late):.1f}, > 0 in {np.mean(np.array(late) > 0) * 100:.0f} % of updates", file=sys.stderr)
+    if step_ev is not None:
+        step_ev.append(win_ev[-1][1])
+        print("per-step ms: " + " ".join(f"{a.elapsed_time(b):.3f}" for a, b in zip(step_ev, step_ev[1:])),
+              file=sys.stderr, flush=True)
+        print("host enqueue ms: " + " ".join(f"{h:.3f}" for h in host_ms), file=sys.stderr, flush=True)
     win_ms = [a[1].elapsed_time(b[1]) / (b[0] - a[0]) for a, b in zip(win_ev, win_ev[1:])]
+    # ------------------------------------------------------------------ the probe window
+    # after the headline: the probe graph copies replay with HIP events around the timed
+    # launches, and the replay shard's launches are timed by ReplayKernelTimer
+    ktimer = ReplayKernelTimer(ax.replay)
+    probe_steps, probe_ms_per_step = 0, None
+    if args.probe_steps > 0:
+        ax.conv_probe = conv_probe if probe else None
+        for _ in range(3):  # the probe copies' first replays (uploaded, but their eager launches are new)
+            ax.iteration()
+        for v in conv_events.values():
+            v.clear()
+        tp0 = time.perf_counter()
+        for _ in range(args.probe_steps):
+            ktimer.arm()
+            ax.iteration()
+        ktimer.stop()
+        torch.cuda.synchronize()
+        probe_ms_per_step = (time.perf_counter() - tp0) * 1e3 / max(1, args.probe_steps)
+        probe_steps = args.probe_steps
+        ax.conv_probe = None
     conv_ms = {t: [a.elapsed_time(b) for a, b in ev if b is not None] for t, ev in conv_events.items()}
     conv2_ms, conv3_ms = conv_ms["conv2"], conv_ms["conv3"]
     replicas = None
@@ -796,7 +868,7 @@ def main():
         "bytes_per_launch": bytes_launch, "mean_launch_us": round(mean_gather_s * 1e6, 2),
         "launches_timed": len(gather_ms), "isolated_launch_us": round(iso_s * 1e6, 2),
         "isolated_frac": round(bytes_launch / iso_s / 1e9 / HBM_PEAK_GBS, 4),
-        "note": "in the timed region the gather overlaps the learner block on a second stream"}
+        "note": "timed in the probe window; the gather overlaps the learner block on a second stream"}
     roofline = roofline_gather
     n2 = 2 * cfg.batch_size  # the learner's [s0; s1] forward
 
@@ -814,8 +886,9 @@ def main():
             "algorithmic_bytes_per_launch": n2 * (hin * hin * cin + hout * hout * cout) * 4 + cout * k * k * cin * 4 + cout * 4,
             "mean_launch_us": round(s_ * 1e6, 2), "median_launch_us": round(float(np.median(ms)) * 1e3, 2),
             "launches_timed": len(ms),
-            "note": "timed live over the timed region: HIP events on the learner stream around the launch (the "
-                    "learner graph is cut there); it runs concurrently with the actor stream's kernels"}
+            "note": "timed live in the probe window after the timed region: HIP events on the learner stream around "
+                    "the launch (the probe copy of the learner graph is cut there); it runs concurrently with the "
+                    "actor stream's kernels"}
         if issue > 1:  # exact-split bf16 kernel: achieved / frac are fp32-equivalent (the dtype's peak)
             r["mfma_issue"] = {"bf16_flops_per_launch": issue * flops, "achieved": round(issue * flops / s_ / 1e12, 2),
                                "peak": unit_peak, "frac": round(issue * flops / s_ / 1e12 / unit_peak, 4),
@@ -850,6 +923,11 @@ def main():
         "ms_per_step": round(step_s * 1e3, 3),
         "ms_per_step_windows": [round(w, 4) for w in win_ms],
         "ms_per_step_window_median": round(float(np.median(win_ms)), 4) if win_ms else None,
+        "graph_prepare": dict(prep, note="setup before the W warmup steps: the capture iterations, hipGraphUpload of "
+                                         "every captured graph, then `settle` untimed iterations of the captured loop"),
+        "probe_window": {"steps": probe_steps, "ms_per_step": round(probe_ms_per_step, 4) if probe_ms_per_step else None,
+                         "note": "after the timed region: the probe graph copies (cut at the timed launches) + the "
+                                 "replay shard's launch timers; every per-launch time in this line comes from it"},
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -887,7 +965,7 @@ def main():
                       "achieved_tflops": round(flops_step / step_s / 1e12, 2),
                       "peak_fp32_tflops": FP32_PEAK_TFLOPS},
         "roofline_conv1": conv1,
-        "roofline_hbm": hbm_rooflines(ax, ktimer, args.tag),
+        "roofline_hbm": hbm_rooflines(ax, ktimer, conv_ms, args.tag),
         "decoupled_actors": decoupled,
         "cpu_baseline": cpu,
     }

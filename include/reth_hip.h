@@ -51,6 +51,10 @@ int rth_version(void);
  * "<git blob id> <path>\n" of reth_amd/csrc/ and include/reth_hip.h in path order
  * (reth_amd._lib.source_build_id; reproducible from `git ls-tree -r HEAD`) */
 const char *rth_build_id(void);
+/* hipGraphUpload of a captured graph's executable on `stream` (plumbing for the captured
+ * actor / learner blocks, reth_amd.apex.ApexDQN.upload_graphs: a graph's first launch then
+ * carries no upload) */
+int rth_graph_upload(void *graph_exec, void *stream);
 
 /* ------------------------------------------------------------------------------------
  * In-order heap sum-tree, fp64, resident in HBM.
@@ -534,15 +538,21 @@ int rth_atari_step(rth_atari *h, const uint8_t *raw_dev, int64_t n, uint8_t *fra
                    uint8_t *out_frame_dev, void *stream);
 /* the Ape-X actors' Atari env mode (after rth_actor_tail with ext_frames = 1): per actor i the
  * raw pair raw_dev[i] (MaxAndSkip max, gray, INTER_AREA) becomes the new top frame of stack
- * s1_h[i] = stack s0_h[i] shifted by one (FrameStack.step), and where done_dev[i] != 0 also the
- * reset observation, the frame `stack` times, in actor i's slot cur_slot_dev[i] (FrameStack
- * reset, util.py:191-196).  Handles index frames_dev's stacks; slots are per-actor ring slots. */
+ * s1_h[i] = stack s0_h[i] shifted by one (FrameStack.step), and where done_dev[i] != 0 the
+ * reset observation -- env.reset()'s screen reset_raw_dev[i] ([n, in_h, in_w, 3], read only
+ * where done; MaxAndSkip.reset returns it without a pair max, util.py:129-130), warped, `stack`
+ * times (FrameStack.reset, util.py:191-196) -- goes into actor i's slot cur_slot_dev[i].
+ * Handles index frames_dev's stacks; slots are per-actor ring slots. */
 int rth_atari_env_step(rth_atari *h, const uint8_t *raw_dev, int64_t n, uint8_t *frames_dev, int32_t ring,
                        int32_t stack, const int64_t *s0_h_dev, const int64_t *s1_h_dev, const float *done_dev,
-                       const int64_t *cur_slot_dev, void *stream);
+                       const int64_t *cur_slot_dev, const uint8_t *reset_raw_dev, void *stream);
 /* synthetic raw emulator screens (the stand-in for ALE's output, ALE being absent): nbytes of
  * device Philox (seed, step *t_dev), 16-byte aligned and a multiple of 16 bytes */
 int rth_atari_synth_raw(uint8_t *raw_dev, int64_t nbytes, uint64_t seed, const int64_t *t_dev, void *stream);
+/* synthetic reset screens: frame i of reset_raw_dev ([n, frame_bytes]) from device Philox
+ * (seed, step *t_dev, its own stream), written only where done_dev[i] != 0 */
+int rth_atari_synth_reset(uint8_t *reset_raw_dev, int64_t n, int64_t frame_bytes, uint64_t seed, const int64_t *t_dev,
+                          const float *done_dev, void *stream);
 
 /* ------------------------------------------------------------------------------------
  * Learner optimizer step (reth/reth/algorithm/dqn/dqn_solver.py:118-121):

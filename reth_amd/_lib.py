@@ -78,6 +78,7 @@ SIGNATURES = {
     "rth_last_error": (ctypes.c_char_p, []),
     "rth_version": (c_i32, []),
     "rth_build_id": (ctypes.c_char_p, []),
+    "rth_graph_upload": (c_i32, [c_vp, c_vp]),
     # sum-tree
     "rth_sumtree_create": (c_i32, [c_i64, c_i32, ctypes.POINTER(c_vp)]),
     "rth_sumtree_destroy": (c_i32, [c_vp]),
@@ -172,8 +173,9 @@ SIGNATURES = {
     "rth_atari_create": (c_i32, [c_i32, c_i32, c_i32, c_i32, c_i32, ctypes.POINTER(c_vp)]),
     "rth_atari_destroy": (c_i32, [c_vp]),
     "rth_atari_step": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
-    "rth_atari_env_step": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "rth_atari_env_step": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "rth_atari_synth_raw": (c_i32, [c_vp, c_i64, c_u64, c_vp, c_vp]),
+    "rth_atari_synth_reset": (c_i32, [c_vp, c_i64, c_i64, c_u64, c_vp, c_vp, c_vp]),
     "rth_clip_adam_workspace": (c_i64, []),
     "rth_debug_tree_timing": (c_i32, [c_vp]),
     "rth_clip_adam": (c_i32, [c_vp, c_i32, c_f64, c_f64, c_f64, c_f64, c_f64, c_vp, c_vp, c_vp, c_vp]),

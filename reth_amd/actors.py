@@ -115,7 +115,8 @@ class VecActors:
         # "atari" -- raw 210x160 RGB frame pairs (device Philox, the stand-in for ALE's screens)
         # through the MaxAndSkip / WarpFrame / FrameStack preprocessing (rth_atari_env_step)
         # into the frame ring; "atari-h2d" -- the raw pairs copied host -> device from pinned
-        # memory every step first, as from host ALE emulators (reth/reth/env/util.py:121-209)
+        # memory every step first, as from host ALE emulators (reth/reth/env/util.py:121-209).
+        # The reset screens of ended episodes come from device Philox in both modes
         if env not in ("synthetic", "atari", "atari-h2d"):
             raise ValueError(f"env {env!r}: synthetic | atari | atari-h2d")
         self.env = env
@@ -124,6 +125,9 @@ class VecActors:
 
             self.atari = AtariPreprocessor(device=dev)
             self.raw = torch.empty((N, 2, 210, 160, 3), dtype=torch.uint8, device=dev)
+            # the reset screens (Worker.step's env.reset() after done, presets/worker.py:146-148):
+            # one raw frame per actor, written / read only for the actors whose episode ended
+            self.raw_reset = torch.zeros((N, 210, 160, 3), dtype=torch.uint8, device=dev)
             if env == "atari-h2d":
                 g = np.random.default_rng(self.seed)
                 self.raw_host = torch.from_numpy(g.integers(0, 256, tuple(self.raw.shape), dtype=np.uint8)).pin_memory()
@@ -173,8 +177,11 @@ class VecActors:
                  ptr(self.t_dev), s)
         else:
             self.raw.copy_(self.raw_host, non_blocking=True)
+        # env.reset()'s screen for the actors whose episode ended (both modes: device Philox)
+        call("rth_atari_synth_reset", ptr(self.raw_reset), self.N, self.raw_reset[0].numel(),
+             self.seed ^ 0x7F4A7C159E3779B9, ptr(self.t_dev), ptr(self.done), s)
         call("rth_atari_env_step", self.atari._h, ptr(self.raw), self.N, ptr(self.frames), self.ring, OBS_SHAPE[0],
-             ptr(self.s0_h), ptr(self.s1_h), ptr(self.done), ptr(self.cur_slot), s)
+             ptr(self.s0_h), ptr(self.s1_h), ptr(self.done), ptr(self.cur_slot), ptr(self.raw_reset), s)
 
     @torch.no_grad()
     def step(self, q_net):
@@ -241,7 +248,7 @@ class VecActors:
              ptr(self.n_ext), stream_ptr())
 
     @torch.no_grad()
-    def step_fused(self, q_net, dedup=None):
+    def step_fused(self, q_net, dedup=None, probe=None):
         """one environment step for every actor with the previous step's rows prioritised in
         the same forward pass: Q-net over [acting stacks; prev rows' s0; prev rows' s1]
         (3N) -> rth_eps_greedy on the first N -> rth_td_huber (calc_loss, target == online)
@@ -252,6 +259,8 @@ class VecActors:
         the terminal stacks of the episodes that ended in the previous step (a device-side
         count); the rows' heads come from the per-stack cache -- the same values, about a third
         of the forward work.
+        probe (HIP-torso path): handed [("actor_tail", launch)] to issue itself (the bench's live
+        timing of k_actor_tail, fused_learner.dueling_grads' probe convention).
         Returns (|td|, RowSet) of the previous step's rows, or (None, None) before any."""
         s = stream_ptr()
         p = self.pushes
@@ -283,8 +292,14 @@ class VecActors:
                                       ptr(td_abs), ptr(self.frames), ptr(self.cur_slot), ptr(self.reward),
                                       ptr(self.done), ptr(self.s0_h), ptr(self.s1_h), self.seed, N, self.gamma_n,
                                       self.p_reward, self.p_done, self.ring, self.A, int(self.env != "synthetic"))
-            call("rth_actor_tail", self._nstep, _lib.ctypes.byref(args), ptr(self.emit), ptr(cur.s0), ptr(cur.a),
-                 ptr(cur.r), ptr(cur.s1), ptr(cur.done), s)
+            def tail(args=args, cur=cur):
+                call("rth_actor_tail", self._nstep, _lib.ctypes.byref(args), ptr(self.emit), ptr(cur.s0), ptr(cur.a),
+                     ptr(cur.r), ptr(cur.s1), ptr(cur.done), stream_ptr())
+
+            if probe is not None:  # the launch issued by the prober (a cut in a captured graph)
+                probe([("actor_tail", tail)])
+            else:
+                tail()
             if self.env != "synthetic":
                 self._atari_frames(s)
             self._terminal_stacks()

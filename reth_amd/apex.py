@@ -248,6 +248,11 @@ class ApexDQN:
         side.wait_stream(torch.cuda.current_stream(self.device))
         split = solver.grad_hook is not None
         G = dict(act=[], act_out=[], tgt=[], q1t=[], learn={}, learn_td={}, buckets={}, grads={})
+        # probe sets (extra["probe_conv2"]): a second copy of the actor and learner graphs, cut
+        # at the launches the bench times live (conv2 / conv3, the TD/heads backward, clip+Adam,
+        # the actor tail) -- replayed only while conv_probe is set, so the headline window
+        # replays the uncut graphs
+        psets = [False, True] if self.cfg.extra.get("probe_conv2") else [False]
         with torch.cuda.stream(side):
             # the actor block by (mode, push parity): fused_actor alternates row sets; mode
             # "dedup" takes the rows' heads from the per-stack cache (VecActors.step_fused),
@@ -256,16 +261,32 @@ class ApexDQN:
             fresh = act.fresh
             modes = ["full"] + (["dedup"] if self.cfg.fused_actor and act._hip_heads(self.actor_net) else [])
             G["act"], G["act_out"] = {}, {}
-            for mode in modes:
-                for _ in range(2):
-                    k = act.pushes % 2
-                    g = torch.cuda.CUDAGraph()
-                    act.fresh = act.n_step + 2 if mode == "dedup" else 0
-                    with torch.cuda.graph(g, stream=side):
-                        out = (act.step_fused(self.actor_net, dedup=mode == "dedup") if self.cfg.fused_actor
-                               else self._actor_compute())
-                    G["act"][mode, k] = g
-                    G["act_out"][mode, k] = out
+            for pr in psets:
+                for mode in modes:
+                    for _ in range(2):
+                        k = act.pushes % 2
+                        act.fresh = act.n_step + 2 if mode == "dedup" else 0
+                        key = ("probe", mode, k) if pr else (mode, k)
+                        if pr and self.cfg.fused_actor:
+                            parts, bounds = [torch.cuda.CUDAGraph()], []
+
+                            def cut(item, parts=parts, bounds=bounds):
+                                parts[-1].capture_end()
+                                bounds.append(("probe", item))
+                                parts.append(torch.cuda.CUDAGraph())
+                                parts[-1].capture_begin(pool=parts[0].pool())
+
+                            parts[0].capture_begin()
+                            out = act.step_fused(self.actor_net, dedup=mode == "dedup", probe=cut)
+                            parts[-1].capture_end()
+                            G["act"][key] = (parts, bounds)
+                        else:
+                            g = torch.cuda.CUDAGraph()
+                            with torch.cuda.graph(g, stream=side):
+                                out = (act.step_fused(self.actor_net, dedup=mode == "dedup") if self.cfg.fused_actor
+                                       else self._actor_compute())
+                            G["act"][key] = g
+                        G["act_out"][key] = out
             act.fresh = fresh
             # the target network's output on each slot's s1, computed on the actor stream ahead
             # of the update (target_heads); "pre" learner graphs consume it, "full" ones
@@ -276,9 +297,8 @@ class ApexDQN:
                     q1t = solver.target_heads(slots[p][0][3])
                 G["tgt"].append(g)
                 G["q1t"].append(q1t)
-            for variant in ("full", "pre"):
-                for p in range(2):
-                    v = (variant, p)
+            for pr, variant, p in [(pr, variant, p) for pr in psets for variant in ("full", "pre") for p in range(2)]:
+                    v = ("probe", variant, p) if pr else (variant, p)
                     parts, bounds = [torch.cuda.CUDAGraph()], []
 
                     def cut(item, parts=parts, bounds=bounds):
@@ -293,13 +313,13 @@ class ApexDQN:
 
                     parts[0].capture_begin()
                     data, idx, isw = slots[p]
-                    probe = (lambda items: cut(("probe", items))) if self.cfg.extra.get("probe_conv2") else None
+                    probe = (lambda items: cut(("probe", items))) if pr else None
                     td = solver.compute_grads(data, isw, q1t=G["q1t"][p] if variant == "pre" else None,
                                               mid=(lambda b: cut(("bucket", b))) if split else None, probe=probe)
                     self.trainer._track(td)
                     if split and not any(k == "bucket" for k, _ in bounds):  # autograd path: one bucket
                         cut(("bucket", [q.grad for q in solver._params]))
-                    solver.apply_grads()
+                    solver.apply_grads(probe=probe)
                     parts[-1].capture_end()
                     G["learn"][v], G["buckets"][v], G["learn_td"][v] = parts, bounds, td
                     G["grads"][v] = [q.grad for q in solver._params]  # what apply_grads consumed
@@ -314,11 +334,48 @@ class ApexDQN:
         act = self.actors
         self._actor_block_graph()
         k = self.loader._pending.pop(0)
-        v = ("full", k)
+        v = self._learner_key(("full", k))
         self._learner_replay(v)
         self.loader.issue()  # sample-ahead into the other slot
         self.replay.update_priorities(self.loader._slots[k][1], G["learn_td"][v], step=True, deferred=True)
         self._learner_host()
+
+    def upload_graphs(self):
+        """hipGraphUpload every captured graph (actor blocks, target passes, learner parts, the
+        probe copies) on this object's stream, then wait: returns the number uploaded"""
+        from . import _lib
+
+        G = self._graphs
+        if G is None:
+            return 0
+        graphs = list(G["tgt"])
+        for g in G["act"].values():
+            graphs += g[0] if isinstance(g, tuple) else [g]
+        for parts in G["learn"].values():
+            graphs += list(parts)
+        st = self._stream if hasattr(self, "_stream") else torch.cuda.current_stream(self.device)
+        for g in graphs:
+            _lib.call("rth_graph_upload", g.raw_cuda_graph_exec(), st.cuda_stream)
+        st.synchronize()
+        return len(graphs)
+
+    def _probing(self):
+        return self.conv_probe is not None and self.cfg.extra.get("probe_conv2")
+
+    def _learner_key(self, v):
+        """the learner graph to replay for variant v: its probe copy while the bench probes"""
+        return ("probe", *v) if self._probing() and ("probe", *v) in self._graphs["learn"] else v
+
+    def _replay_parts(self, parts, bounds):
+        """replay a graph captured in parts; between them the probed launches, each bracketed
+        by conv_probe(tag) / conv_probe(tag + "_end")"""
+        for i, g in enumerate(parts):
+            g.replay()
+            if i < len(bounds):
+                for tag, fn in bounds[i][1]:
+                    self.conv_probe(tag)
+                    fn()
+                    self.conv_probe(tag + "_end")
 
     def _learner_replay(self, v):
         """replay learner graph v on the current stream.  Its parts are cut at boundaries:
@@ -368,12 +425,17 @@ class ApexDQN:
             self._actor_host()
             k = act.pushes % 2
             mode = "dedup" if ("dedup", k) in G["act"] and act.dedup_ready(self.actor_net) else "full"
-            G["act"][mode, k].replay()
+            key = ("probe", mode, k) if self._probing() and ("probe", mode, k) in G["act"] else (mode, k)
+            g = G["act"][key]
+            if isinstance(g, tuple):  # a probe set: parts with the timed launches between them
+                self._replay_parts(*g)
+            else:
+                g.replay()
             self.actor_modes[mode] = self.actor_modes.get(mode, 0) + 1
             act.t += 1
             act.pushes += 1
             act.fresh += 1
-            td, rows = G["act_out"][mode, k]
+            td, rows = G["act_out"][key]
             if self.cfg.fused_actor:
                 act._bind_rows(act._sets[k])
                 if act.pushes - 1 > act.n_step:
@@ -421,7 +483,7 @@ class ApexDQN:
         A.wait_event(self._ev_learn)
         self._actor_block_graph()  # on A (the caller's stream)
         k = self.loader._pending.pop(0)
-        v = ("pre" if self._q1t_ready[k] else "full", k)
+        v = self._learner_key(("pre" if self._q1t_ready[k] else "full", k))
         self._q1t_ready[k] = False
         syncs = self.solver._target_syncs
         with torch.cuda.stream(B):

@@ -73,24 +73,12 @@ __global__ void k_atari_step(const uint8_t *__restrict__ raw, int64_t n, int H, 
   dst[(K - 1) * pl + pix] = px;
 }
 
-// The Ape-X actors' Atari env mode (reth_amd/actors.py env="atari"): after the actor tail
-// assigned this step's stack handles (s0_h = the observation acted on, s1_h = the next one;
-// cur_slot = where the next observation lives: s1's slot, or a reset slot after done), the
-// raw frame pair of each actor becomes the new top frame of s1 (FrameStack shift of s0), and
-// -- done -- also the reset observation (the frame k times, FrameStack.reset) in cur_slot.
-__global__ void k_atari_env(const uint8_t *__restrict__ raw, int64_t n, int H, int W, int OH, int OW, int K,
-                            const AreaTab *__restrict__ xt, const int *__restrict__ xsrc, const float *__restrict__ xw,
-                            const AreaTab *__restrict__ yt, const int *__restrict__ ysrc, const float *__restrict__ yw,
-                            uint8_t *__restrict__ frames, int ring, const int64_t *__restrict__ s0_h,
-                            const int64_t *__restrict__ s1_h, const float *__restrict__ done,
-                            const int64_t *__restrict__ cur_slot) {
-  const int64_t i = blockIdx.x / OH;
-  const int dy = blockIdx.x % OH;
-  const int dx = threadIdx.x;
-  if (i >= n || dx >= OW) return;
-  const int64_t plane = (int64_t)H * W * 3;
-  const uint8_t *f0 = raw + i * 2 * plane, *f1 = f0 + plane;
-  const AreaTab ty = yt[dy], tx = xt[dx];
+// WarpFrame of one output pixel (dy, dx) from the max of two raw RGB frames (f0 == f1: one
+// frame, no pair max -- MaxAndSkip.reset returns the reset screen itself, util.py:129-130)
+__device__ __forceinline__ uint8_t warp_pixel(const uint8_t *__restrict__ f0, const uint8_t *__restrict__ f1, int W,
+                                              const AreaTab ty, const AreaTab tx, const int *__restrict__ xsrc,
+                                              const float *__restrict__ xw, const int *__restrict__ ysrc,
+                                              const float *__restrict__ yw) {
   float sum = 0.0f;
   for (int j = 0; j < ty.count; ++j) {
     const int sy = ysrc[ty.first + j];
@@ -103,16 +91,58 @@ __global__ void k_atari_env(const uint8_t *__restrict__ raw, int64_t n, int H, i
     }
     sum = j == 0 ? rmul(beta, buf) : radd(sum, rmul(beta, buf));
   }
-  float v = rintf(sum);
-  const uint8_t px = (uint8_t)(v < 0.0f ? 0.0f : (v > 255.0f ? 255.0f : v));
+  const float v = rintf(sum);  // saturate_cast<uchar>: cvRound, then clamp
+  return (uint8_t)(v < 0.0f ? 0.0f : (v > 255.0f ? 255.0f : v));
+}
+
+// The Ape-X actors' Atari env mode (reth_amd/actors.py env="atari"): after the actor tail
+// assigned this step's stack handles (s0_h = the observation acted on, s1_h = the next one;
+// cur_slot = where the next observation lives: s1's slot, or a reset slot after done), the
+// raw frame pair of each actor becomes the new top frame of s1 (FrameStack shift of s0), and
+// -- done -- the reset observation goes into cur_slot: Worker.step calls env.reset()
+// (presets/worker.py:146-148), whose MaxAndSkip.reset returns the emulator's fresh reset
+// screen (util.py:129-130, no pair max), warped, k times (FrameStack.reset, util.py:191-196).
+__global__ void k_atari_env(const uint8_t *__restrict__ raw, int64_t n, int H, int W, int OH, int OW, int K,
+                            const AreaTab *__restrict__ xt, const int *__restrict__ xsrc, const float *__restrict__ xw,
+                            const AreaTab *__restrict__ yt, const int *__restrict__ ysrc, const float *__restrict__ yw,
+                            uint8_t *__restrict__ frames, int ring, const int64_t *__restrict__ s0_h,
+                            const int64_t *__restrict__ s1_h, const float *__restrict__ done,
+                            const int64_t *__restrict__ cur_slot, const uint8_t *__restrict__ reset_raw) {
+  const int64_t i = blockIdx.x / OH;
+  const int dy = blockIdx.x % OH;
+  const int dx = threadIdx.x;
+  if (i >= n || dx >= OW) return;
+  const int64_t plane = (int64_t)H * W * 3;
+  const uint8_t *f0 = raw + i * 2 * plane, *f1 = f0 + plane;
+  const AreaTab ty = yt[dy], tx = xt[dx];
+  const uint8_t px = warp_pixel(f0, f1, W, ty, tx, xsrc, xw, ysrc, yw);
   const int64_t pix = (int64_t)dy * OW + dx, pl = (int64_t)OH * OW;
   uint8_t *dst = frames + s1_h[i] * K * pl;
   const uint8_t *src = frames + s0_h[i] * K * pl;
   for (int p = 0; p + 1 < K; ++p) dst[p * pl + pix] = src[(p + 1) * pl + pix];
   dst[(K - 1) * pl + pix] = px;
-  if (done[i] != 0.0f) {
+  if (done[i] != 0.0f) {  // workgroup-uniform (one actor per workgroup)
+    const uint8_t *fr = reset_raw + i * plane;
+    const uint8_t rpx = warp_pixel(fr, fr, W, ty, tx, xsrc, xw, ysrc, yw);
     uint8_t *rs = frames + (i * ring + cur_slot[i]) * K * pl;
-    for (int p = 0; p < K; ++p) rs[p * pl + pix] = px;
+    for (int p = 0; p < K; ++p) rs[p * pl + pix] = rpx;
+  }
+}
+
+// the synthetic reset screens (the stand-in for the emulator's reset output): actor i's frame
+// of device Philox (seed, step *t_dev, stream STREAM_ATARI_RESET), generated only where
+// done[i] != 0 -- the only rows k_atari_env reads it for.  grid (vector chunks, actors)
+__global__ __launch_bounds__(256) void k_atari_synth_reset(uint4 *__restrict__ raw, int64_t vec_per_frame, uint64_t seed,
+                                                           const int64_t *__restrict__ t_dev,
+                                                           const float *__restrict__ done) {
+  const int64_t i = blockIdx.y;
+  if (done[i] == 0.0f) return;
+  const int64_t t = *t_dev;
+  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < vec_per_frame; v += (int64_t)gridDim.x * 256) {
+    const int64_t g = i * vec_per_frame + v;
+    uint32_t c[4] = {(uint32_t)g, (uint32_t)(g >> 32), (uint32_t)t, STREAM_ATARI_RESET | ((uint32_t)(t >> 32) << 8)};
+    philox4x32(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    raw[g] = make_uint4(c[0], c[1], c[2], c[3]);
   }
 }
 
@@ -230,14 +260,27 @@ int rth_atari_step(rth_atari *h, const uint8_t *raw, int64_t n, uint8_t *frames,
 
 int rth_atari_env_step(rth_atari *h, const uint8_t *raw, int64_t n, uint8_t *frames, int32_t ring, int32_t stack,
                        const int64_t *s0_h, const int64_t *s1_h, const float *done, const int64_t *cur_slot,
-                       void *stream) {
-  RTH_REQUIRE(h && raw && frames && s0_h && s1_h && done && cur_slot && n >= 0 && ring >= 2 && stack >= 1,
+                       const uint8_t *reset_raw, void *stream) {
+  RTH_REQUIRE(h && raw && frames && s0_h && s1_h && done && cur_slot && reset_raw && n >= 0 && ring >= 2 && stack >= 1,
               "rth_atari_env_step: bad arguments");
   if (n == 0) return RTH_OK;
   const int threads = (h->OW + 63) / 64 * 64;
   hipLaunchKernelGGL(k_atari_env, dim3((unsigned)(n * h->OH)), dim3(threads), 0, as_stream(stream), raw, n, h->H,
                      h->W, h->OH, h->OW, stack, h->xt, h->xsrc, h->xw, h->yt, h->ysrc, h->yw, frames, ring, s0_h, s1_h,
-                     done, cur_slot);
+                     done, cur_slot, reset_raw);
+  RTH_LAUNCHED();
+  return RTH_OK;
+}
+
+int rth_atari_synth_reset(uint8_t *reset_raw, int64_t n, int64_t frame_bytes, uint64_t seed, const int64_t *t_dev,
+                          const float *done, void *stream) {
+  RTH_REQUIRE(reset_raw && t_dev && done && n >= 0 && frame_bytes > 0 && frame_bytes % 16 == 0 &&
+                  (reinterpret_cast<uintptr_t>(reset_raw) & 15) == 0 && n <= 65535,
+              "rth_atari_synth_reset: bad arguments (16-byte aligned frames, a multiple of 16 bytes, n <= 65535)");
+  if (n == 0) return RTH_OK;
+  const int64_t vec = frame_bytes / 16, chunks = (vec + 255) / 256;
+  hipLaunchKernelGGL(k_atari_synth_reset, dim3((unsigned)(chunks < 64 ? chunks : 64), (unsigned)n), dim3(256), 0,
+                     as_stream(stream), reinterpret_cast<uint4 *>(reset_raw), vec, seed, t_dev, done);
   RTH_LAUNCHED();
   return RTH_OK;
 }

@@ -102,7 +102,8 @@ inline int dtype_size(int32_t t) {
 // Salmon et al., "Parallel random numbers: as easy as 1, 2, 3" (SC'11).  Counter-based, so
 // every lane derives its own stream from (seed, counter, lane, stream id) with no state.
 // Restated bit-for-bit in oracle/reth_oracle.c (orc_philox4x32) for the parity tests.
-constexpr uint32_t STREAM_SAMPLE = 1u, STREAM_EXPLORE = 2u, STREAM_RANDACT = 3u, STREAM_ENV = 4u, STREAM_ATARI = 5u;
+constexpr uint32_t STREAM_SAMPLE = 1u, STREAM_EXPLORE = 2u, STREAM_RANDACT = 3u, STREAM_ENV = 4u, STREAM_ATARI = 5u,
+                   STREAM_ATARI_RESET = 6u;
 
 __host__ __device__ inline void philox4x32(uint32_t c[4], uint32_t k0, uint32_t k1) {
 #pragma unroll

@@ -72,6 +72,13 @@ int rth_version(void) { return 100; }  // 0.1.0
 static const char k_build_id_marker[] __attribute__((used)) = "RTH_BUILD_ID:" RTH_BUILD_ID;
 const char *rth_build_id(void) { return k_build_id_marker + 13; }
 
+int rth_graph_upload(void *graph_exec, void *stream) {
+  RTH_REQUIRE(graph_exec, "rth_graph_upload: NULL graph");
+  const hipError_t e = hipGraphUpload(static_cast<hipGraphExec_t>(graph_exec), as_stream(stream));
+  RTH_REQUIRE(e == hipSuccess, "rth_graph_upload: %s", hipGetErrorString(e));
+  return RTH_OK;
+}
+
 int rth_td_huber(const float *q0, const float *q1o, const float *q1t, const int64_t *a, const float *r,
                  const float *done, const double *isw, int64_t B, int64_t A, float gamma_n, int32_t double_q,
                  int32_t dueling, float *td_out, float *td_abs_out, float *loss_elem, float *loss_out, float *dq,

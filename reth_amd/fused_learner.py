@@ -97,10 +97,11 @@ def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None, mid=No
     backward; whatever mid's caller does to a bucket in place is what the parameters get.
 
     probe (optional callable) is handed the forward's conv2 and conv3 launches as
-    probe([("conv2", launch2), ("conv3", launch3)]) and issues them itself (the bench times
-    them live: the capture cuts the learner graph once there, and every replay launches the
-    two eagerly between HIP events on the learner stream; their buffers live in the graph's
-    pool at fixed addresses)."""
+    probe([("conv2", launch2), ("conv3", launch3)]), then the fused TD/heads backward as
+    probe([("td_heads_backward", launch)]), and issues them itself (the bench times them live:
+    the capture cuts the learner graph at each probe, and every replay of that probe graph
+    launches them eagerly between HIP events on the learner stream; their buffers live in the
+    graph's pool at fixed addresses)."""
     from .solver import td_huber_forward
 
     net = solver.q_network
@@ -164,9 +165,15 @@ def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None, mid=No
                 raise ValueError("batch columns / target heads disagree with the batch")
             td_abs = torch.empty(B, dtype=torch.float32, device=dev)
             loss = torch.empty(1, dtype=torch.float32, device=dev)
-            call("rth_td_heads_backward_branches", ptr(q0), ptr(q1o), ptr(q1t), ptr(a), ptr(r), ptr(done), ptr(isw), B,
-                 A1 - 1, float(solver.gamma_n), int(bool(solver.double_q)), ptr(h1), h1.stride(0), fc2p, Hh,
-                 ptr(td_abs), ptr(loss), ptr(gh1), g2p, ptr(gb1), ptr(td_acc), st)
+            def td_launch(q1t=q1t, a=a, r=r, done=done, isw=isw):
+                call("rth_td_heads_backward_branches", ptr(q0), ptr(q1o), ptr(q1t), ptr(a), ptr(r), ptr(done), ptr(isw),
+                     B, A1 - 1, float(solver.gamma_n), int(bool(solver.double_q)), ptr(h1), h1.stride(0), fc2p, Hh,
+                     ptr(td_abs), ptr(loss), ptr(gh1), g2p, ptr(gb1), ptr(td_acc), stream_ptr())
+
+            if probe is not None:
+                probe([("td_heads_backward", td_launch)])
+            else:
+                td_launch()
         else:
             loss, td_abs, dq = td_huber_forward(q0, q1o, q1t, a, r, done, isw, solver.gamma_n, solver.double_q,
                                                 want_dq=True, dueling=True)

@@ -47,6 +47,57 @@ class ReplayService:
         self.replay = None  # created on the first append (the LMDB map is sized from it too)
         self.alive = True
 
+    # ------------------------------------------------------------------ remote ingest (ZMTP)
+    def listen(self, host, port, advertise=None, hwm=10):
+        """serve the reference's three service sockets over TCP (reth_amd.zmtp): the meta REP
+        at tcp://host:port answering the JSON config (main_loop.py:64-76,162-170), the append
+        PULL (main_loop.py:21-26) and the update PULL (update_proxy_loop, :79-88).  Received
+        messages wait in one arrival-ordered queue of `hwm` entries (ZMQ_DEFAULT_HWM = 10,
+        utils/__init__.py:12: a full queue stops the readers, and TCP stops the senders) until
+        the owner thread drains them into the HBM replay (drain(): every ready() /
+        check_ready() call, i.e. before every sample).  Returns the meta address."""
+        import json
+        import queue
+
+        from . import zmtp
+
+        self.inbox = queue.Queue(maxsize=int(hwm))
+        adv = advertise or (host if host not in ("0.0.0.0", "") else "127.0.0.1")
+        self.append_ep = zmtp.Endpoint(b"PULL", lambda f: self.inbox.put(("append", f)), host)
+        self.update_ep = zmtp.Endpoint(b"PULL", lambda f: self.inbox.put(("update", f)), host)
+        reply = []
+        self.meta_ep = zmtp.Endpoint(b"REP", lambda frames: reply, host, port)  # port 0: an unused one
+        meta_addr = self.meta_ep.addr(adv)
+        self.config = {"capacity": self.capacity, "batch_size": self.batch_size, "lmdb_path": None,
+                       "meta_addr": meta_addr, "append_addr": self.append_ep.addr(adv),
+                       "update_addr": self.update_ep.addr(adv),
+                       "sampler_info": {"default": {"topic": "default", "sampler_cls": {
+                           "per": "PERSampler", "uniform": "UniformSampler", "fifo": "FIFOSampler"}[self.kind],
+                           "num_procs": 1, "kwargs": {"alpha": self.alpha, "beta": self.beta,
+                                                      "capacity": self.capacity},
+                           "addrs": [], "sample_start": self.sample_start, "batch_size": self.batch_size}}}
+        reply.append(json.dumps(self.config).encode())
+        return meta_addr
+
+    def drain(self):
+        """apply the queued remote messages in arrival order on the calling (owner) thread:
+        an append message is append_loop's work (server/main_loop.py:40-58) on the HBM shard,
+        an update message [indices, weights, step] is the sampler's update (sampler_loop.py:32-35)"""
+        q = getattr(self, "inbox", None)
+        n = 0
+        while q is not None and not q.empty():
+            kind, frames = q.get_nowait()
+            msg = b"".join(bytes(f) for f in frames) if len(frames) > 1 else frames[0]
+            if kind == "append":
+                Client(self).append_message(msg)
+            else:
+                from . import pack
+
+                idx, w, step = pack.deserialize(msg)
+                Client(self).update_priorities(np.asarray(idx), np.asarray(w), step=bool(step))
+            n += 1
+        return n
+
     def _widen(self, c):
         return self.widen_u8 is True or (isinstance(self.widen_u8, (set, list, tuple)) and c in self.widen_u8)
 
@@ -72,6 +123,7 @@ class ReplayService:
 
     def ready(self):
         """sampler_loop.py:23-28: cnt >= sample_start and sampler.ready_sample(batch_size)"""
+        self.drain()
         return (self.replay is not None and self.replay.cnt >= self.sample_start
                 and self.replay.ready_sample(self.batch_size))
 
@@ -90,6 +142,10 @@ class ReplayService:
     def terminate(self):
         self.alive = False
         self.replay = None
+        for ep in ("meta_ep", "append_ep", "update_ep"):
+            if getattr(self, ep, None) is not None:
+                getattr(self, ep).close()
+                setattr(self, ep, None)
 
     def join(self, timeout=None):
         return None
@@ -122,6 +178,12 @@ def start_server(capacity, batch_size, host=None, port=None, samplers=None, cach
     svc = ReplayService(capacity, batch_size, s, device, seed, widen_u8, kind=kinds[name])
     addr = f"hbm://{svc.device.index}/{next(_ids)}"
     _SERVICES[addr] = svc
+    svc.hbm_addr = addr
+    if host is not None or port is not None:
+        # the reference's network-facing service (__init__.py:14-17): remote Clients reach this
+        # shard over ZMTP; in-process Clients / loaders resolve the same tcp address
+        addr = svc.listen("0.0.0.0" if host is None else host, 0 if port is None else port)
+        _SERVICES[addr] = svc
     return svc, addr
 
 
@@ -138,9 +200,18 @@ class Client:
     """client/client.py:8-39."""
 
     def __init__(self, meta_addr):
-        self.svc = _lookup(meta_addr)
+        self.remote = None
+        if isinstance(meta_addr, ReplayService):
+            self.svc = meta_addr
+        elif meta_addr in _SERVICES or not str(meta_addr).startswith("tcp://"):
+            self.svc = _lookup(meta_addr)
+        else:  # a service in another process / on another node: the reference's wire path
+            self.svc = None
+            self.remote = _RemoteClient(meta_addr)
 
     def append(self, data, weights, compress=False):
+        if self.remote is not None:
+            return self.remote.append(data, weights, compress)
         assert isinstance(data, (list, tuple))
         n = len(weights)
         for col in data:
@@ -165,9 +236,45 @@ class Client:
 
     def update_priorities(self, indices, weights, step=True):
         assert len(indices) == len(weights)
+        if self.remote is not None:
+            return self.remote.update_priorities(indices, weights, step)
         if self.svc.replay is None:
             raise RuntimeError("update_priorities before any append")
         self.svc.replay.update_priorities(indices, weights, step=step)
+
+
+class _RemoteClient:
+    """client/client.py:8-39 over ZMTP (reth_amd.zmtp): REQ the meta address for the config
+    (utils/__init__.py:51-59), PUSH appends / priority updates to its append / update
+    addresses, the message bytes identical to the reference's (reth_amd.pack)"""
+
+    def __init__(self, meta_addr):
+        import json
+
+        from . import zmtp
+
+        req = zmtp.Peer(b"REQ", meta_addr)
+        try:
+            self.meta = json.loads(bytes(req.request(b"")[0]))
+        finally:
+            req.close()
+        self.append_sock = zmtp.Peer(b"PUSH", self.meta["append_addr"])
+        self.update_sock = zmtp.Peer(b"PUSH", self.meta["update_addr"])
+
+    def append(self, data, weights, compress=False):
+        from . import pack
+
+        assert isinstance(data, (list, tuple))
+        for col in data:
+            assert isinstance(col, np.ndarray)
+            assert len(col) == len(weights)
+        rows = [pack.serialize([col[i, ...] for col in data]) for i in range(len(weights))]
+        self.append_sock.send(pack.serialize([rows, weights], compress=compress))
+
+    def update_priorities(self, indices, weights, step=True):
+        from . import pack
+
+        self.update_sock.send(pack.serialize([indices, weights, step]))
 
 
 class NumpyLoader:

@@ -285,10 +285,14 @@ class DQNSolver(Algorithm):
         self.last_loss = loss.detach()
         return td_abs
 
-    def apply_grads(self):
-        """dqn_solver.py:118-123: clip_grad_norm_ -> Adam -> target Interval"""
+    def apply_grads(self, probe=None):
+        """dqn_solver.py:118-123: clip_grad_norm_ -> Adam -> target Interval.  probe: as in
+        fused_learner.dueling_grads, handed [("clip_adam", launch)] to issue itself"""
         if isinstance(self.optimizer, ClipAdam):
-            self.optimizer.step()  # clips to optimizer.max_norm (= clip_value) itself
+            if probe is not None:
+                probe([("clip_adam", self.optimizer.step)])
+            else:
+                self.optimizer.step()  # clips to optimizer.max_norm (= clip_value) itself
         else:
             if self.clip_value >= 0:
                 torch.nn.utils.clip_grad_norm_(self._params, self.clip_value, foreach=True)

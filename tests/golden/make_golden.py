@@ -426,6 +426,21 @@ def gen_dqn_full(R):
         solver = R.dqn_solver.DQNSolver(gym.spaces.Box(0, 255, (4, 84, 84)), gym.spaces.Discrete(A), gamma=0.99,
                                         clip_value=40, double_q=True, dueling=True, learning_rate=1e-4,
                                         adam_epsilon=1.5e-4, update_target_interval=100, device="cpu", n_step=3)
+        # the first update's gradient as the reference's update hands it to clip_grad_norm_
+        # (dqn_solver.py:117-119): recorded by a pass-through wrapper, with the norm it returns
+        names = {id(p): n for n, p in solver.q_network.named_parameters()}
+        grads = {}
+        clip_orig = torch.nn.utils.clip_grad_norm_
+
+        def clip_rec(params, max_norm, *a, **k):
+            params = list(params)
+            if not grads:
+                grads.update({names[id(p)]: p.grad.detach().double().clone().numpy() for p in params})
+            norm = clip_orig(params, max_norm, *a, **k)
+            grads.setdefault("__norm__", float(norm))
+            return norm
+
+        torch.nn.utils.clip_grad_norm_ = clip_rec
         orig = R.dqn_solver.ensure_tensor
         if f64:
             solver.q_network.double()
@@ -453,7 +468,8 @@ def gen_dqn_full(R):
                                                   for n, v in solver.q_network.state_dict().items()}, tgt))
         finally:
             R.dqn_solver.ensure_tensor = orig
-        return init, res, (s0, s1, a, r, done, isw)
+            torch.nn.utils.clip_grad_norm_ = clip_orig
+        return init, res, (s0, s1, a, r, done, isw), grads
 
     def margins(seed, B, A):
         """float64 decision margins of the first update's forward, relative to sum |x| |w|: the
@@ -492,8 +508,8 @@ def gen_dqn_full(R):
             print(f"  dqn_{tag}: seed {sd} min margin {cands[-1][0]:.2e}", flush=True)
         seed = max(cands)[1]
         relu_m, gap_m = margins(seed, B, A)
-        init, r32, (s0, s1, a, r, done, isw) = run(seed, B, A, False)
-        _, r64, _ = run(seed, B, A, True)
+        init, r32, (s0, s1, a, r, done, isw), g32 = run(seed, B, A, False)
+        _, r64, _, g64 = run(seed, B, A, True)
         out = dict(seed=np.int64(seed), B=np.int64(B), A=np.int64(A), frames_sha=np.array(frames_sha(s0, s1)),
                    a=a, r=r, done=done, isw=isw, param_names=np.array(list(init)))
         out["init_sum"] = np.array([float(v.double().sum()) for v in init.values()])
@@ -508,11 +524,30 @@ def gen_dqn_full(R):
             for name in init:
                 d32, d64 = r32[k][1][name], r64[k][1][name]
                 assert np.abs(d32).max() < 6e-4 and np.abs(d64).max() < 6e-4, name
-                out[f"upd{k}/{name}"] = d32.astype(np.float16)
-                out[f"upd{k}_64/{name}"] = d64.astype(np.float16)
-                errs.append(np.abs(d32 - d64).max())
+                out[f"upd{k}_64/{name}"] = d64.astype(np.float16)  # the exact update; the fp32 run
+                errs.append(np.abs(d32 - d64).max())               # is kept as its distance only
             out[f"upd{k}_ref32_err"] = np.array(errs)  # per tensor: max |reference fp32 - exact|
+        # the first update's gradient (before clipping) of the exact run, float32: every element of
+        # every tensor but FC1's two weights, of which every GRAD_ROW_STRIDE-th row (a row of FC1's
+        # weight gradient is one hidden unit's: sum_b gh1[b, i] feat[b, :]); the fp32 run's distance
+        # per tensor over the same elements; both runs' total norms (clip_grad_norm_'s return)
+        gerr, gmax = [], []
+        for name in init:
+            sel = (slice(None, None, GRAD_ROW_STRIDE),) if name.endswith(".0.weight") and name.startswith("fc_") \
+                else (Ellipsis,)
+            e64, e32 = g64[name][sel], g32[name][sel]
+            out[f"grad0_64/{name}"] = e64.astype(np.float32)
+            gerr.append(np.abs(e32 - e64).max())
+            gmax.append(np.abs(e64).max())
+        out["grad0_ref32_err"], out["grad0_absmax"] = np.array(gerr), np.array(gmax)
+        out["grad0_row_stride"] = np.int64(GRAD_ROW_STRIDE)
+        out["grad0_norm64"], out["grad0_norm32"] = np.float64(g64["__norm__"]), np.float64(g32["__norm__"])
+        print(f"  dqn_{tag} grad norm {g64['__norm__']:.6e} (fp32 run {g32['__norm__']:.6e}); fp32 grad error / "
+              f"max|g| per tensor: " + " ".join(f"{e / max(m, 1e-30):.1e}" for e, m in zip(gerr, gmax)))
         np.savez_compressed(os.path.join(OUT, f"dqn_{tag}.npz"), **out)
+
+
+GRAD_ROW_STRIDE = 8
 
 
 # ----------------------------------------------------------------------------- samplers / buffers

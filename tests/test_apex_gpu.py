@@ -64,20 +64,25 @@ def test_graph_replay_matches_eager(dev):
 
 
 def test_probed_learner_graph_matches_unprobed(dev):
-    """the bench's probe (learner graph cut once, conv2 and conv3 issued between the parts,
-    each between conv_probe(tag) / conv_probe(tag + "_end")) changes no result: identical
-    replay state to the unprobed graph, and every learner replay reports both launches"""
+    """the bench's probe sets (a second copy of the actor and learner graphs, cut at the
+    launches it times live -- the actor tail, conv2 + conv3, the TD/heads backward, clip+Adam --
+    issued eagerly between the parts, each between conv_probe(tag) / conv_probe(tag + "_end"))
+    change no result: identical replay state to the unprobed graphs, also when the probe sets
+    replay only in a window (the bench's headline window replays the uncut graphs, its probe
+    window the cut ones), and every probed iteration reports each launch once"""
     from reth_amd.apex import ApexConfig, ApexDQN
 
-    def run(probe):
+    def run(probe, window=None):
         cfg = ApexConfig(n_actors=16, capacity=1024, batch_size=32, sample_start=64, learning_rate=0.0,
                          p_done=0.05, seed=5, hip_graph=True, send_weights_interval=3,
                          recv_weights_interval=4, update_target_interval=5, extra={"probe_conv2": probe})
         ax = ApexDQN(cfg, device=dev)
-        tags = []
-        ax.conv_probe = tags.append
-        for _ in range(40):
+        tags, probed = [], 0
+        for i in range(40):
+            on = window is None or window[0] <= i < window[1]
+            ax.conv_probe = tags.append if on else None
             ax.iteration()
+            probed += int(on and ax._graphs is not None)  # the capture iteration replays too
         torch.cuda.synchronize()
         assert ax._graphs is not None
         s, m, v = ax.replay.tree.export()
@@ -85,17 +90,19 @@ def test_probed_learner_graph_matches_unprobed(dev):
         out = [s.cpu(), m.cpu(), v.cpu()] + [c.cpu() for c in cols]
         info, updates = ax.replay.info(), ax.updates
         ax.close()
-        return out, info, tags, updates
+        return out, info, tags, probed
 
     a, ia, ta, _ = run(False)
-    b, ib, tb, updates = run(True)
+    b, ib, tb, probed = run(True)
+    c, ic, tc, probed_c = run(True, window=(20, 30))
     assert ta == []
-    replays = len(tb) // 4
-    assert replays > 0 and tb == ["conv2", "conv2_end", "conv3", "conv3_end"] * replays
-    assert replays <= updates  # eager updates before the capture issue no probe
-    assert ia == ib
-    for x, y in zip(a, b):
-        assert torch.equal(x, y)
+    per_iter = ["actor_tail", "actor_tail_end", "conv2", "conv2_end", "conv3", "conv3_end", "td_heads_backward",
+                "td_heads_backward_end", "clip_adam", "clip_adam_end"]
+    assert probed > 0 and tb == per_iter * probed
+    assert probed_c == 10 and tc == per_iter * 10
+    assert ia == ib == ic
+    for x, y, z in zip(a, b, c):
+        assert torch.equal(x, y) and torch.equal(x, z)
 
 
 def test_graph_split_learner_applies_its_own_gradients(dev):

@@ -40,6 +40,7 @@ def test_atari_actor_stacks_vs_oracle(dev, orc, env):
         act.step_fused(net)
         torch.cuda.synchronize()
         raw = act.raw.cpu().numpy()
+        raw_reset = act.raw_reset.cpu().numpy()
         s0h, s1h = act.s0_h.cpu().numpy(), act.s1_h.cpu().numpy()
         done, cur = act.done.cpu().numpy(), act.cur_slot.cpu().numpy()
         for i in range(N):
@@ -49,8 +50,13 @@ def test_atari_actor_stacks_vs_oracle(dev, orc, env):
             assert np.array_equal(fr(s1h[i]), np.stack(stacks[i])), (t, i, "s1")
             if done[i]:
                 dones += 1
-                stacks[i].extend([f] * 4)  # FrameStack.reset: the first observation k times
+                # env.reset(): MaxAndSkip.reset's screen (no pair max, util.py:129-130) warped, then
+                # FrameStack.reset's k copies -- a fresh observation, not the terminal one
+                rs = raw_reset[i]
+                fr0 = orc.warp_frame(rs, rs)
+                stacks[i].extend([fr0] * 4)
                 assert np.array_equal(fr(i * ring + cur[i]), np.stack(stacks[i])), (t, i, "reset")
+                assert not np.array_equal(fr0, f)
             else:
                 assert cur[i] * 1 + i * ring == s1h[i]
     assert dones > 0

@@ -33,10 +33,11 @@ def test_apex_trainer_loop_shape(dev, orc):
     K, B = 4, config["common"]["batch_size"]
     perwez_proc, perwez_config = perwez.start_server(port=None)
     rb_procs, rb_addrs = [], []
-    for port in range(K):  # trainer.py:52-61
+    for port in [0] * K:  # trainer.py:52-61 (port 0: an unused one each; the shards serve ZMTP on it)
         proc, addr = reth_buffer.start_per(capacity=config["replay_buffer"]["capacity"] // K,
                                            alpha=config["replay_buffer"]["alpha"], beta=config["replay_buffer"]["beta"],
                                            batch_size=B, port=port)
+        assert addr.startswith("tcp://")
         rb_procs.append(proc)
         rb_addrs.append(addr)
     # worker.py:44-60-shaped appends: 64-row batches of float32 frames, |td| from calc_loss

@@ -538,8 +538,9 @@ def decoupled_actors(ax, dev, world, iters=40, sweep=(1, 4, 16)):
     keep = ax.cfg.actor_steps_per_update
     out = {}
     ax.cfg.actor_steps_per_update = 1
-    for _ in range(3):
+    for _ in range(3):  # each synchronized: no host backlog into timed()'s first sync (main(), settle)
         ax.actor_iteration()
+        torch.cuda.synchronize()
     e0 = ax.env_steps
     dt = timed(ax.actor_iteration, iters)
     out["actor_only_env_steps_per_sec"] = round((ax.env_steps - e0) * world / dt, 1)
@@ -549,6 +550,7 @@ def decoupled_actors(ax, dev, world, iters=40, sweep=(1, 4, 16)):
         ax.cfg.actor_steps_per_update = k
         for _ in range(2):
             ax.iteration()
+            torch.cuda.synchronize()
         u0, e0 = ax.updates, ax.env_steps
         n = max(4, iters // k)
         dt = timed(ax.iteration, n)
@@ -666,14 +668,19 @@ def main():
             prep["capture_iterations"] += 1
         if ax._graphs is not None:
             prep["graphs_uploaded"] = ax.upload_graphs()
-            sync_tail = int(os.environ.get("RTH_BENCH_SETTLE_SYNC", "0"))
+            # the host must not run far ahead of the GPU into the synchronize before the timed
+            # region: after a sync that drained a ~125 ms backlog the first timed step's enqueue
+            # took 1.2-1.6 ms instead of 0.1 (r04 probe: 0.643 ms/step over 20 steps, flat
+            # 0.581 with the backlog bounded), so the settle iterations synchronize every 8th
+            # and each of the last 16, the warmup steps each
             for i in range(args.settle):
                 ax.iteration()
-                if i >= args.settle - sync_tail:
+                if i % 8 == 7 or i >= args.settle - 16:
                     torch.cuda.synchronize()
             prep["settle_iterations"] = args.settle
     for i in range(args.warmup):
         ax.iteration()
+        torch.cuda.synchronize()
 
     # live per-launch timing (the probe window after the headline): HIP events on the launching
     # stream around the launches the probe graph copies leave out -- conv2 / conv3 forward, the
@@ -924,7 +931,9 @@ def main():
         "ms_per_step_windows": [round(w, 4) for w in win_ms],
         "ms_per_step_window_median": round(float(np.median(win_ms)), 4) if win_ms else None,
         "graph_prepare": dict(prep, note="setup before the W warmup steps: the capture iterations, hipGraphUpload of "
-                                         "every captured graph, then `settle` untimed iterations of the captured loop"),
+                                         "every captured graph, then `settle` untimed iterations of the captured loop "
+                                         "(synchronized every 8th and the last 16; each warmup step synchronized: the "
+                                         "host never enters the timed region's first sync far ahead of the GPU)"),
         "probe_window": {"steps": probe_steps, "ms_per_step": round(probe_ms_per_step, 4) if probe_ms_per_step else None,
                          "note": "after the timed region: the probe graph copies (cut at the timed launches) + the "
                                  "replay shard's launch timers; every per-launch time in this line comes from it"},

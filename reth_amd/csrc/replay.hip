@@ -449,6 +449,12 @@ struct rth_replay {
   // advance is stream-ordered after the sample that owes it (owed_stream)
   int64_t calls_owed;
   hipStream_t owed_stream;
+  // the last owed-counter advance that ran on a stream other than the one the next sample may
+  // use: recorded after it (one event per handle, created on first use), and every sample on
+  // another stream waits for it before reading the counter (outside graph capture)
+  hipEvent_t bump_ev;
+  hipStream_t bump_stream;
+  int bump_valid;
   // rth_replay_set_timing: one-shot events recorded around the next launches of each kind
   hipEvent_t timing[RTH_TIMING_SLOTS];
   int32_t timing_fired;  // bit k: slot k's event was recorded since the last arm
@@ -496,6 +502,30 @@ static int sampler_update(rth_replay *h, const int64_t *idx, const void *w, int3
 static int bump(rth_replay *h, int64_t dtail, int64_t dcalls, int64_t dstep, hipStream_t s) {
   hipLaunchKernelGGL(k_state_bump, dim3(1), dim3(64), 0, s, h->st, dtail, h->cap, dcalls, dstep);
   RTH_LAUNCHED();
+  return RTH_OK;
+}
+
+static bool capturing(hipStream_t s) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+}
+
+// the owed seed-counter advance of an earlier sample, on that sample's stream (behind the
+// sample kernel that read the counter); remembered so that a sample on any other stream is
+// ordered behind it (order_after_bump)
+static int bump_owed(rth_replay *h, int64_t owed) {
+  int rc = bump(h, 0, owed, 0, h->owed_stream);
+  if (rc) return rc;
+  if (capturing(h->owed_stream)) return RTH_OK;  // inside a capture the graph's own order holds
+  if (!h->bump_ev) RTH_HIP(hipEventCreateWithFlags(&h->bump_ev, hipEventDisableTiming));
+  RTH_HIP(hipEventRecord(h->bump_ev, h->owed_stream));
+  h->bump_stream = h->owed_stream;
+  h->bump_valid = 1;
+  return RTH_OK;
+}
+
+static int order_after_bump(rth_replay *h, hipStream_t s) {
+  if (h->bump_valid && h->bump_stream != s && !capturing(s)) RTH_HIP(hipStreamWaitEvent(s, h->bump_ev, 0));
   return RTH_OK;
 }
 
@@ -603,6 +633,7 @@ int rth_replay_destroy(rth_replay *h) {
   if (h->tree) rth_sumtree_destroy(h->tree);
   for (void *p : {(void *)h->ulist, (void *)h->fidx, (void *)h->fw})
     if (p) (void)hipFree(p);
+  if (h->bump_ev) (void)hipEventDestroy(h->bump_ev);
   delete h;
   return RTH_OK;
 }
@@ -709,8 +740,9 @@ static int gather_impl(rth_replay *h, const int64_t *idx, int64_t n, void *const
   h->calls_owed = 0;
   if (owed && (n == 0 || s != h->owed_stream)) {
     // on the sample's own stream, behind the sample kernel that reads the counter (a gather
-    // on another stream could otherwise advance it first)
-    int rc = bump(h, 0, owed, 0, h->owed_stream);
+    // on another stream could otherwise advance it first); later samples on other streams
+    // wait for it (order_after_bump)
+    int rc = bump_owed(h, owed);
     if (rc || n == 0) return rc;
   } else if (owed) {  // same stream: the gather's first lane advances the counter, no launch
     a.bump_st = h->st;
@@ -734,17 +766,12 @@ int rth_replay_sample(rth_replay *h, int64_t batch, const double *uniforms, void
   int rc = flush_pending(h, s);
   if (rc) return rc;
   if (h->calls_owed) {  // the previous sample was not followed by a gather: its seed advance first
-    rc = bump(h, 0, h->calls_owed, 0, h->owed_stream);
+    rc = bump_owed(h, h->calls_owed);
     h->calls_owed = 0;
     if (rc) return rc;
-    if (h->owed_stream != s) {  // this sample reads the counter: order it behind that bump
-      hipEvent_t e;
-      RTH_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      RTH_HIP(hipEventRecord(e, h->owed_stream));
-      RTH_HIP(hipStreamWaitEvent(s, e, 0));
-      (void)hipEventDestroy(e);
-    }
   }
+  rc = order_after_bump(h, s);  // this sample reads the counter: behind any advance on another stream
+  if (rc) return rc;
   if (h->kind == RTH_SAMPLER_PER) {
     timing_mark(h, RTH_TIMING_SAMPLE, s);
     rc = tree_sample_impl(h->tree, batch, uniforms, h->seed, 0, 1, 0.0, idx_out, isw_out, s, h->st, &h->beta);

@@ -20,19 +20,23 @@ _ROOT = os.path.dirname(os.path.abspath(__file__))
 RESULTS = os.environ.get("RTH_TUNABLEOP_IN") or os.path.join(_ROOT, "tuned", "tunableop_results_mi355x.csv")
 
 
-_STATE = {}  # what enable() changed: restored by restore()
+_STATE = {}  # what the first enable() changed: restored by the matching last restore()
+_USERS = [0]  # enable() calls not yet matched by restore(): TunableOp stays on while any is open
 
 
 def enable(tune_missing=None, max_tuning_ms=30):
-    """switch TunableOp on for this process (idempotent); returns the committed results file
-    used, or None.  Selection is read-only by default: shapes missing from the committed file
-    run the library's default solution (deterministic, the same on every rank); tune_missing
-    (or RTH_TUNE_MISSING=1) benchmarks them on first use instead, and restore() reports which
-    shapes that tuned."""
+    """switch TunableOp on for this process; returns the committed results file used, or None.
+    Reference counted: every enable() is matched by one restore(), and the state found by the
+    first is put back only by the last, so closing one ApexDQN never switches tuned selection
+    off under another still running in the process.  Selection is read-only by default: shapes
+    missing from the committed file run the library's default solution (deterministic, the
+    same on every rank); tune_missing (or RTH_TUNE_MISSING=1) benchmarks them on first use
+    instead, and restore() reports which shapes that tuned."""
     if not torch.cuda.is_available() or os.environ.get("RTH_NO_TUNED_GEMM"):
         return None
     tun = torch.cuda.tunable
-    if tun.is_enabled():
+    _USERS[0] += 1
+    if _USERS[0] > 1 or tun.is_enabled():  # already on (ours, or the caller's own): nothing to change
         return RESULTS if os.path.exists(RESULTS) else None
     if tune_missing is None:
         tune_missing = bool(os.environ.get("RTH_TUNE_MISSING"))
@@ -64,9 +68,11 @@ def tuned_at_runtime():
 
 
 def restore():
-    """undo enable(): TunableOp back to the state it found (ApexDQN.close); logs the shapes
-    tuned at runtime, if any"""
-    if not _STATE:
+    """match one enable() (ApexDQN.close); the last open one puts TunableOp back to the state
+    the first found and logs the shapes tuned at runtime, if any"""
+    if _USERS[0] > 0:
+        _USERS[0] -= 1
+    if _USERS[0] > 0 or not _STATE:
         return
     tun = torch.cuda.tunable
     new = tuned_at_runtime()

@@ -44,6 +44,9 @@ for s in "$@"; do
           --no-cpu-baseline --no-sweep --probe-steps 0
       RTH_BENCH_STEPTIMES=1 step first_plain 300 python bench.py --steps 20 --warmup 5 \
           --no-cpu-baseline --no-sweep --probe-steps 0 ;;
+    dp8) RTH_SHARE_GPU=1 RTH_DIST_BACKEND=gloo step dp8_gloo_rehearsal 900 python -m torch.distributed.run --nnodes=1 \
+          --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 8 --faithful --steps 20 \
+          --warmup 5 --no-cpu-baseline --no-sweep ;;
     tests) step gpu_tests 1100 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;

@@ -39,7 +39,11 @@ LEARNER_GATHER_GRID = copy_grid(512)
 HBM_KERNELS = {"k_tree_update_sub": ("k_tree_update_sub", None), "k_tree_sample": ("k_tree_sample", None),
                "k_copy_rows (gather)": ("k_copy_rows", "gather"), "k_copy_rows (insert)": ("k_copy_rows", "insert"),
                "k_actor_tail": ("k_actor_tail", None), "k_td_heads_backward": ("k_td_heads_backward", None),
-               "k_adam": ("k_adam", None)}
+               "k_adam": ("k_adam", None), "k_grad_sqsum": ("k_grad_sqsum", None)}
+# output bytes per sample of the conv forwards (float32): conv2 writes [81 pixels x 64] NHWC,
+# conv3 [64 x 49] NCHW -- a dispatch's WRITE_SIZE says how many samples it ran (the grid does
+# not: the conv kernels loop over the samples)
+CONV_OUT_BYTES = {"conv2": 81 * 64 * 4, "conv3": 49 * 64 * 4}
 # conv2 / conv3 forward: the fp32-MFMA kernel or the exact-split bf16 one (k_conv_x9)
 CONV2 = ("k_conv_bias_relu<0, 4, 4, 2, 32, 64, 20, 20", "k_conv_x9<4, 4, 2, 32, 20, 20")
 CONV3 = ("k_conv_bias_relu<0, 3, 3, 1, 64, 64, 9, 9", "k_conv_x9<3, 3, 1, 64, 9, 9")
@@ -111,10 +115,13 @@ def main():
     pw = os.path.join(OUT, "pmc_write", "run_counter_collection.csv")
     if os.path.exists(pf) and os.path.exists(pw):
         def load(p, name):
+            """(kernel, grid) -> counter values in dispatch order (the two passes run the same
+            command, so the k-th dispatch of a class in one is the k-th in the other)"""
             d = collections.defaultdict(list)
-            for r in csv.DictReader(open(p)):
-                if r["Counter_Name"] == name:
-                    d[(r["Kernel_Name"].split("(")[0], int(r["Grid_Size"]))].append(float(r["Counter_Value"]))
+            rows = [r for r in csv.DictReader(open(p)) if r["Counter_Name"] == name]
+            rows.sort(key=lambda r: int(r.get("Dispatch_Id") or r.get("Correlation_Id") or 0))
+            for r in rows:
+                d[(r["Kernel_Name"].split("(")[0], int(r["Grid_Size"]))].append(float(r["Counter_Value"]))
             return d
 
         fe, wr = load(pf, "FETCH_SIZE"), load(pw, "WRITE_SIZE")
@@ -133,15 +140,24 @@ def main():
             out.update({"gather_kernel": "rth::k_copy_rows (learner gather, B=512, 5 columns)",
                         "gather_hbm_bytes_per_launch": round((2 * st.median(fe[key]) + st.median(wr[key])) * 1024),
                         "gather_dispatches": len(fe[key])})
+        n2 = 2 * arg("--batch", 512)  # the learner's [s0; s1] forward
         for name, conv in (("conv2", CONV2), ("conv3", CONV3)):
-            cs = [k for k in fe if is_conv(conv, k[0]) and k in wr]
-            if cs:
-                key = max(cs, key=lambda k: k[1])  # the learner's launch: the largest grid
-                out.update({f"{name}_kernel": key[0] + " (the learner's [s0; s1] forward: the largest grid, "
-                                                       f"{key[1]} threads)",
-                            f"{name}_learner_hbm_bytes_per_launch":
-                                round((2 * st.median(fe[key]) + st.median(wr[key])) * 1024),
-                            f"{name}_dispatches": len(fe[key])})
+            # the learner launch = the dispatches whose WRITE_SIZE is 2B samples' output (the
+            # target pass writes B, the actors ~N: all three share the grid)
+            sel, classes = [], collections.Counter()
+            for k in [k for k in fe if is_conv(conv, k[0]) and k in wr]:
+                for fv, wv in zip(fe[k], wr[k]):
+                    samples = round(wv * 1024 / CONV_OUT_BYTES[name])
+                    classes[samples] += 1
+                    if samples == n2:
+                        sel.append((k, fv, wv))
+            if sel:
+                fm, wm = st.median(v[1] for v in sel), st.median(v[2] for v in sel)
+                out.update({f"{name}_kernel": sel[0][0][0] + f" (the learner's [s0; s1] forward: the dispatches "
+                                                             f"writing {n2} samples' output)",
+                            f"{name}_learner_hbm_bytes_per_launch": round((2 * fm + wm) * 1024),
+                            f"{name}_dispatches": len(sel),
+                            f"{name}_dispatches_by_samples": dict(sorted(classes.items()))})
         hbm = {}
         for name, (match, g) in HBM_KERNELS.items():
             want = loop_grid.get(name, grids.get(g))
@@ -151,6 +167,8 @@ def main():
             if len(cs) == 1:
                 k = cs[0]
                 hbm[name] = round((2 * st.median(fe[k]) + st.median(wr[k])) * 1024)
+        if "k_adam" in hbm and "k_grad_sqsum" in hbm:  # rth_clip_adam = both launches (bench.py roofline_hbm)
+            hbm["rth_clip_adam (k_grad_sqsum + k_adam)"] = hbm["k_adam"] + hbm["k_grad_sqsum"]
         out["hbm_bytes_per_launch"] = hbm
     if inloop or os.path.exists(pf):
         if not (os.path.exists(pf) and os.path.exists(pw)):

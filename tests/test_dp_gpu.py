@@ -72,15 +72,17 @@ def test_two_rank_graph_learner_keeps_replicas_identical(tmp_path):
     assert torch.equal(res[0]["params"], res[1]["params"])
 
 
-def test_configs3_shape_two_ranks(tmp_path):
-    """BASELINE configs[3] (bench.py --workload pong at N > 1) at world 2: configs[1]'s 256
-    actors and 1 M replay rows sharded over the ranks -- 128 actors and a 500,000-row shard
-    per rank (test/apex-dqn/trainer.py:52-61: K shards of C // K), pre-filled; the faithful
-    global batch of 512 (256 per rank); actor_steps_per_update = world (each update paired
-    with 256 env steps of its shard).  Replicas bit-identical; each shard's counters are its
-    own actors' rows and its own learner's samples; the ranks' actors take disjoint slices of
-    the global epsilon ladder (worker.py:26 over all 256 actors)."""
-    world, n_act, cap, B, iters = 2, 128, 500_000, 256, 12
+@pytest.mark.parametrize("world", [2, 8])
+def test_configs3_shape(tmp_path, world):
+    """BASELINE configs[3] (bench.py --workload pong --faithful at N > 1): configs[1]'s 256
+    actors and 1 M replay rows sharded over the ranks -- at world 8 the driver's 8-GPU shape,
+    32 actors and a 125,000-row shard per rank (test/apex-dqn/trainer.py:52-61: K shards of
+    C // K), pre-filled; the faithful global batch of 512 (64 per rank); actor_steps_per_update
+    = world (each update paired with 256 env steps of its shard).  All ranks share cuda:0 over
+    gloo (the one-GPU box; RCCL needs a GPU per rank).  Replicas bit-identical; each shard's
+    counters are its own actors' rows and its own learner's samples; the ranks' actors take
+    disjoint slices of the global epsilon ladder (worker.py:26 over all 256 actors)."""
+    n_act, cap, B, iters = 256 // world, 1_000_000 // world, 512 // world, 12
     res = _run(tmp_path, world, dict(n_actors=n_act, capacity=cap, batch_size=B, actor_steps_per_update=world,
                                      iters=iters, prefill=True))
     for x in res:

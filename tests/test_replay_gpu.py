@@ -259,16 +259,34 @@ def test_sample_counter_advance_forms(dev, sampler):
     ids = torch.arange(cap, device=dev)
     w = rng.random(cap) + 0.1
 
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+
     def run(form):
         rep = HbmReplay(cap, [Column((), torch.int64)], alpha=0.6, beta=0.4, device=dev, seed=11,
                         sampler=sampler)
         rep.append([ids], w)
-        seq = []
-        for _ in range(4):
+        torch.cuda.synchronize()
+        for st in streams:
+            st.wait_stream(torch.cuda.current_stream())
+        seq, keep = [], []
+        for k in range(4):
             cols, idx, isw = rep.new_batch(B)
             arr = (c_vp * 1)(ptr(cols[0]))
             if form == "fused":
                 rep.sample_into(B, cols, idx, isw)
+            elif form == "cross":  # the gather (which launches the owed counter advance on
+                # the sample's stream) on another stream, the next sample on the gather's stream;
+                # the advance is held back behind a spin on the sample's stream, so a sample that
+                # did not wait for it would read the old counter and repeat the previous draw
+                s_sample = streams[k % 2]
+                s_gather = streams[(k + 1) % 2]
+                call("rth_replay_sample", rep._h, B, None, None, ptr(idx), ptr(isw), s_sample.cuda_stream)
+                s_gather.wait_stream(s_sample)  # the gather reads idx
+                with torch.cuda.stream(s_sample):
+                    torch.cuda._sleep(20_000_000)
+                call("rth_replay_gather", rep._h, ptr(idx), B, arr, s_gather.cuda_stream)
+                keep.append((cols, idx))
+                continue
             else:
                 call("rth_replay_sample", rep._h, B, None, None, ptr(idx), ptr(isw), stream_ptr())
                 if form == "split":
@@ -276,9 +294,15 @@ def test_sample_counter_advance_forms(dev, sampler):
             seq.append(idx.cpu().numpy().copy())
             if form != "none":
                 assert np.array_equal(cols[0].cpu().numpy(), seq[-1])
+        if keep:
+            torch.cuda.synchronize()
+            for cols, idx in keep:
+                seq.append(idx.cpu().numpy().copy())
+                assert np.array_equal(cols[0].cpu().numpy(), seq[-1])
         return np.stack(seq)
 
     fused = run("fused")
     assert len({tuple(r) for r in fused}) == 4  # every call draws anew
     assert np.array_equal(fused, run("split"))
     assert np.array_equal(fused, run("none"))
+    assert np.array_equal(fused, run("cross"))

@@ -62,8 +62,9 @@ WORKLOADS = {
     "pong-weak": dict(name="PongNoFrameskip-v4 Ape-X DQN, BASELINE configs[1] replicated per GPU (256 actors and "
                            "1 M replay rows on every GPU, data-parallel learner)",
                       actors=256, capacity=1_000_000, actions=6, shard=False),
-    "breakout": dict(name="BreakoutNoFrameskip-v4 Ape-X (BASELINE configs[2]; full-row uint8 replay, no frame "
-                          "de-duplication)", actors=2048, capacity=4_000_000, actions=4, shard=False),
+    "breakout": dict(name="BreakoutNoFrameskip-v4 Ape-X (BASELINE configs[2]; replay storage: see "
+                          "config.replay_storage -- full uint8 rows, or --frame-store)", actors=2048,
+                     capacity=4_000_000, actions=4, shard=False),
 }
 WORKLOADS["pong-node"] = WORKLOADS["pong"]
 
@@ -76,6 +77,20 @@ def gather_bytes_per_row(frames_u8=False):
     read = 2 * STACK + 8 + 4 + 4
     write = 2 * STACK * (1 if frames_u8 else 4) + 8 + 4 + 4
     return read + write + 5 * 8
+
+
+def replay_storage(ax):
+    """the replay shard's HBM footprint: full uint8 rows, or the frame store + frame-id rows"""
+    rep = ax.replay
+    rows = sum(c.row_elems * c.dtype.itemsize if not getattr(c, "frames", False) else c.shape[0] * 4
+               for c in rep.columns) * rep.capacity
+    if rep.frames is None:
+        return {"kind": "full rows (uint8 stacks)", "rows_gb": round(rows / 1e9, 2)}
+    fb = rep.frames.numel()
+    return {"kind": "frame store (each frame once; rows hold frame ids)", "rows_gb": round(rows / 1e9, 3),
+            "frames": int(rep.frames.shape[0]), "frame_store_gb": round(fb / 1e9, 2),
+            "total_gb": round((rows + fb) / 1e9, 2),
+            "full_rows_would_be_gb": round(rep.capacity * (2 * STACK + 16) / 1e9, 2)}
 
 
 def qnet_flops_per_sample(A=6):
@@ -453,9 +468,10 @@ def hbm_bytes(cfg, n_rows_per_append):
         "k_tree_sample": B * (D * 16 + 8 + 8 + 8),
         # read + write of every sampled row (uint8 stacks, the HIP torso reads them as they are)
         # + the 5 index reads
-        "k_copy_rows (gather)": B * (2 * row + 5 * 8),
+        "k_copy_rows (gather)": B * (2 * row + 5 * 8 + (2 * 4 * 4 if cfg.frame_store else 0)),
         # the append's rows: each column row read from the actors' ring and written to its slot
-        "k_copy_rows (insert)": N * (2 * row + 5 * 8),
+        # (frame store: the two stacks' frame ids instead of the stacks)
+        "k_copy_rows (insert)": N * (2 * ((2 * 4 * 4 + 16) if cfg.frame_store else row) + 5 * 8),
         # per actor: the FrameStack shift (3 frames read, 4 written) + reward / done / handles /
         # n-step state (~160 B)
         "k_actor_tail": cfg.n_actors * (7 * 84 * 84 + 160),
@@ -593,6 +609,10 @@ def main():
                     help="actors' observations: synthetic uint8 stacks (default); atari = raw 210x160 RGB frame pairs "
                          "from device Philox through the device MaxAndSkip / gray / INTER_AREA / FrameStack; atari-h2d = "
                          "the same with the raw pairs copied host -> device from pinned memory every step (host ALE)")
+    ap.add_argument("--frame-store", action="store_true",
+                    help="frame de-duplicated replay (SURVEY §8(d) C3): each actor frame stored once in an HBM frame "
+                         "store, rows keep their stacks as frame ids, the gather assembles them (Breakout's 4 M rows: "
+                         "~30 GB instead of 225.9 GB)")
     ap.add_argument("--no-sweep", action="store_true", help="skip the decoupled-actor measurements after the "
                     "timed region (actor block alone; actor_steps_per_update 1 / 4 / 16)")
     ap.add_argument("--cpu-actor-worker", type=float, default=None, help=argparse.SUPPRESS)
@@ -649,7 +669,7 @@ def main():
     cfg = ApexConfig(n_actors=args.actors, capacity=args.capacity, batch_size=per_gpu_batch, num_actions=wl["actions"],
                      actor_steps_per_update=args.actor_steps_per_update, seed=0,
                      channels_last=not args.nchw, conv_benchmark=not args.no_conv_benchmark,
-                     hip_graph=not args.eager, hip_conv=hip_conv, env=args.env,
+                     hip_graph=not args.eager, hip_conv=hip_conv, env=args.env, frame_store=args.frame_store,
                      extra={"learner_priority": int(os.environ.get("RTH_LEARNER_PRIORITY", "0")),
                             "probe_conv2": probe})
     ax = ApexDQN(cfg, device=dev, rank=rank, world=world)
@@ -828,7 +848,8 @@ def main():
         replicas = all(torch.equal(allh[0], h) for h in allh[1:])
     gather_ms = [a.elapsed_time(b) for a, b in ktimer.pairs["gather"]]
     mean_gather_s = float(np.mean(gather_ms)) / 1e3
-    bytes_launch = gather_bytes_per_row(cfg.hip_conv and cfg.channels_last) * cfg.batch_size
+    bytes_launch = (gather_bytes_per_row(cfg.hip_conv and cfg.channels_last) + (32 if cfg.frame_store else 0)) \
+        * cfg.batch_size  # frame store: + the rows' 2 x 4 frame ids
     achieved = bytes_launch / mean_gather_s / 1e9
     # the same gather alone on the GPU (in the timed region it shares the GPU with the
     # concurrently running learner block): context for the in-loop figure, not `achieved`
@@ -956,6 +977,7 @@ def main():
                    "replay_capacity_per_gpu": cfg.capacity, "replay_prefilled": True, "batch_size": cfg.batch_size,
                    "n_step": cfg.n_step, "alpha": cfg.alpha, "beta": cfg.beta,
                    "actor_steps_per_update": cfg.actor_steps_per_update, "env": cfg.env,
+                   "replay_storage": replay_storage(ax),
                    "qnet_layout": "channels_last" if cfg.channels_last else "nchw",
                    "conv_benchmark": cfg.conv_benchmark, "hip_graph": cfg.hip_graph, "hip_conv": cfg.hip_conv,
                    "global_batch": cfg.batch_size * world,

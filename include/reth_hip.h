@@ -40,6 +40,10 @@ extern "C" {
 /* priority "dtype" for the tree/replay update calls: float64 priorities stored as given,
  * without (w + 1e-6) ** alpha (NumbaSumTree.update; reth.buffer.PrioritizedBuffer.append) */
 #define RTH_PRIO_RAW 16
+/* in_dtype of a frame-stack column of a frame-store replay: each stored row is out_planes
+ * int32 frame ids into the replay's frame store (rth_replay_frames_attach); row_elems is the
+ * sampled stack (out_planes frames x frame bytes, out_dtype RTH_U8), assembled by the gather */
+#define RTH_FRAMES 8
 
 const char *rth_last_error(void);
 /* development aid: wall-clock ticks (100 MHz) at the phase boundaries of the last tree
@@ -223,6 +227,29 @@ rth_sumtree *rth_replay_tree(rth_replay *h);
 int rth_replay_set_timing(rth_replay *h, void *const *events, int32_t n, int32_t *fired_out);
 /* device pointer of column c's storage ([capacity, row] of in_dtype) */
 void *rth_replay_column(rth_replay *h, int32_t c);
+/* Frame de-duplicated storage (Breakout's 4 M rows are 225.9 GB as full uint8
+ * rows, ~30 GB with each frame stored once).  The reference stores every row's two float32
+ * stacks (test/apex-dqn/worker.py:44-51); here the RTH_FRAMES columns hold each stack as K
+ * frame ids into a frame store of n_frames frames of frame_bytes, owned by the handle, and
+ * the gather assembles the same uint8 stacks the full rows would hold.  store_out / head_out
+ * (nullable): the store ([n_frames, frame_bytes]) and its device head (frames pushed).  The
+ * store is a ring: it must hold every frame a live row references -- a row's oldest frame is
+ * at most n + 4 actor steps older than the row, and a row lives capacity / N appends -- so
+ * n_frames >= capacity x (1 + the reset rate) + (n + 8) x N with N actors (reth_amd.replay
+ * sizes it). */
+int rth_replay_frames_attach(rth_replay *h, int64_t n_frames, int64_t frame_bytes, void **store_out,
+                             int64_t **head_out);
+/* One vectorised actor step's frames into the store (VecActors, after the env step):
+ * ring_dev = the actors' stack ring [N * ring_slots (+ extra), stack, frame], sid_dev = its
+ * stack table ([same stacks, stack] int32 frame ids).  mode 0: stack s1_h[i] is stack s0_h[i]
+ * shifted by one frame + a new frame (FrameStack.step, reth/reth/env/util.py:198-204): the new
+ * frame enters the store, sid[s1] = sid[s0][1:] + [its id]; where done_dev[i], actor i's reset
+ * stack (slot cur_slot_dev[i], one frame `stack` times: FrameStack.reset, :191-196) enters as one
+ * frame.  mode 1: every actor's current stack (slot cur_slot_dev[i]) enters as `stack` frames
+ * (the initial observations).  Then the device head advances past them. */
+int rth_replay_push_frames(rth_replay *h, const uint8_t *ring_dev, int64_t n, int32_t ring_slots, int32_t stack,
+                           const int64_t *s0_h_dev, const int64_t *s1_h_dev, const float *done_dev,
+                           const int64_t *cur_slot_dev, int32_t *sid_dev, int32_t mode, void *stream);
 
 /* ------------------------------------------------------------------------------------
  * Row copy / gather with optional uint8 -> float32 widening (the loaders' pinned copy +

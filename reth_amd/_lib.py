@@ -13,6 +13,7 @@ LIB_PATH = os.environ.get("RTH_LIB_PATH") or os.path.join(_HERE, "libreth_hip.so
 # element types (include/reth_hip.h)
 RTH_U8, RTH_I32, RTH_I64, RTH_F32, RTH_F64 = 0, 1, 2, 3, 4
 RTH_PRIO_RAW = 16  # priorities stored as given (no (w + 1e-6) ** alpha)
+RTH_FRAMES = 8  # a frame-stack column's stored type: frame ids into the replay's frame store
 SAMPLER_PER, SAMPLER_UNIFORM, SAMPLER_FIFO = 0, 1, 2
 MAX_COLS = 8
 
@@ -111,6 +112,8 @@ SIGNATURES = {
     "rth_replay_tree": (c_vp, [c_vp]),
     "rth_replay_set_timing": (c_i32, [c_vp, ctypes.POINTER(c_vp), c_i32, ctypes.POINTER(c_i32)]),
     "rth_replay_column": (c_vp, [c_vp, c_i32]),
+    "rth_replay_frames_attach": (c_i32, [c_vp, c_i64, c_i64, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp)]),
+    "rth_replay_push_frames": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp]),
     "rth_copy_rows": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i32, c_i32, c_vp]),
     # actors
     "rth_eps_greedy": (c_i32, [c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_u64, c_u64, c_vp, c_vp, c_vp]),

@@ -111,6 +111,8 @@ class VecActors:
         self.t_dev = torch.zeros(1, dtype=torch.int64, device=dev)  # what the kernels read
         self.pushes = 0
         call("rth_synth_env_reset", ptr(self.frames), N, ring, self.seed, ptr(self.cur_slot), stream_ptr())
+        self.frame_replay = None  # attach_frame_store: the frame de-duplicated replay the steps feed
+        self.sid = None
         # env: "synthetic" -- Pong-shaped uint8 frames straight from device Philox;
         # "atari" -- raw 210x160 RGB frame pairs (device Philox, the stand-in for ALE's screens)
         # through the MaxAndSkip / WarpFrame / FrameStack preprocessing (rth_atari_env_step)
@@ -131,6 +133,21 @@ class VecActors:
             if env == "atari-h2d":
                 g = np.random.default_rng(self.seed)
                 self.raw_host = torch.from_numpy(g.integers(0, 256, tuple(self.raw.shape), dtype=np.uint8)).pin_memory()
+
+    def attach_frame_store(self, replay):
+        """feed a frame de-duplicated replay (HbmReplay with FrameColumns): every step's new
+        frames enter its store once (rth_replay_push_frames) and each frame-ring stack's frame
+        ids live in `sid` ([stacks, 4] int32), which the rows' appends copy instead of the stacks"""
+        if replay.frames is None:
+            raise ValueError("the replay has no frame store")
+        self.frame_replay = replay
+        self.sid = torch.zeros((self.frames.shape[0], OBS_SHAPE[0]), dtype=torch.int32, device=self.device)
+        replay.push_frames(self.frames, self.N, self.ring, None, None, None, self.cur_slot, self.sid, init=True)
+
+    def _push_frames(self):
+        if self.frame_replay is not None:
+            self.frame_replay.push_frames(self.frames, self.N, self.ring, self.s0_h, self.s1_h, self.done,
+                                          self.cur_slot, self.sid)
 
     def __del__(self):
         if getattr(self, "_nstep", None):
@@ -198,6 +215,7 @@ class VecActors:
         call("rth_synth_env_step", ptr(self.frames), self.N, self.ring, 0, ptr(self.t_dev), ptr(self.cur_slot),
              ptr(self.action), self.seed, self.p_reward, self.p_done, ptr(self.reward), ptr(self.done), ptr(self.s0_h),
              ptr(self.s1_h), s)
+        self._push_frames()
         call("rth_nstep_push", self._nstep, ptr(self.s0_h), ptr(self.action), ptr(self.reward), ptr(self.s1_h),
              ptr(self.done), ptr(self.emit), ptr(self.row_s0), ptr(self.row_a), ptr(self.row_r), ptr(self.row_s1),
              ptr(self.row_done), s)
@@ -302,6 +320,7 @@ class VecActors:
                 tail()
             if self.env != "synthetic":
                 self._atari_frames(s)
+            self._push_frames()
             self._terminal_stacks()
             self.pushes += 1
             self.fresh += 1
@@ -321,6 +340,7 @@ class VecActors:
         call("rth_synth_env_step", ptr(self.frames), N, self.ring, 0, ptr(self.t_dev), ptr(self.cur_slot),
              ptr(self.action), self.seed, self.p_reward, self.p_done, ptr(self.reward), ptr(self.done), ptr(self.s0_h),
              ptr(self.s1_h), s)
+        self._push_frames()
         call("rth_nstep_push", self._nstep, ptr(self.s0_h), ptr(self.action), ptr(self.reward), ptr(self.s1_h),
              ptr(self.done), ptr(self.emit), ptr(cur.s0), ptr(cur.a), ptr(cur.r), ptr(cur.s1), ptr(cur.done), s)
         self._terminal_stacks()
@@ -343,7 +363,7 @@ class VecActors:
         """Client.append of emitted rows (default: the latest; stacks copied from the ring
         into FIFO slots)"""
         rs = self._rowset_of_attrs() if rows is None else rows
-        fr = self.frames
+        fr = self.frames if replay.frames is None else self.sid  # frame store: the stacks' frame ids
         replay.append([fr, rs.a, rs.r, fr, rs.done], td_abs, src_rows=[rs.s0, None, None, rs.s1, None])
 
     def rows(self):
@@ -373,13 +393,18 @@ def _q_forward(q_net, x):
     return q, dueling
 
 
-def apex_columns(channels_last=False, frames_u8=False):
+def apex_columns(channels_last=False, frames_u8=False, frame_store=False):
     """replay columns of the apex-dqn rows [s0, a, r, s1, done] (worker.py:47-51): frames are
     stored uint8 and sampled as float32 (exact), the rest as the reference casts them.
     frames_u8: s0 / s1 are sampled as the stored uint8 stacks -- the HIP conv torso reads
     them directly (forward, and conv1's weight gradient), widening in registers (the same
     values at a quarter of the bytes)"""
-    from .replay import Column
-    fr = lambda: Column(OBS_SHAPE, torch.uint8) if frames_u8 else Column(OBS_SHAPE, torch.uint8, torch.float32,
-                                                                         channels_last=channels_last)
+    from .replay import Column, FrameColumn
+    if frame_store:  # frame de-duplicated (SURVEY §8(d) C3): frame ids, sampled as the uint8 stacks
+        if not frames_u8:
+            raise ValueError("the frame store samples uint8 stacks (frames_u8)")
+        fr = lambda: FrameColumn(OBS_SHAPE)
+    else:
+        fr = lambda: Column(OBS_SHAPE, torch.uint8) if frames_u8 else Column(OBS_SHAPE, torch.uint8, torch.float32,
+                                                                             channels_last=channels_last)
     return [fr(), Column((), torch.int64), Column((), torch.float32), fr(), Column((), torch.float32)]

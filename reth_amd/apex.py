@@ -72,6 +72,7 @@ class ApexConfig:
     dp_hook: Optional[bool] = None  # gradient all-reduce hook: None = when world > 1 (tests force it)
     tuned_gemm: bool = True        # TunableOp solution selection for the library GEMMs (reth_amd.gemm_tuning)
     env: str = "synthetic"         # actors' observations: synthetic | atari | atari-h2d (VecActors)
+    frame_store: bool = False      # frame de-duplicated replay: each frame stored once, rows as frame ids
     extra: dict = field(default_factory=dict)
 
 
@@ -116,9 +117,13 @@ class ApexDQN:
         self.svc, self.addr = start_per(cfg.capacity, cfg.batch_size, alpha=cfg.alpha, beta=cfg.beta,
                                         sample_start=cfg.sample_start, device=self.device, seed=cfg.seed + 7919 * rank)
         u8 = bool(cfg.hip_conv and cfg.channels_last)
-        self.svc.replay = HbmReplay(cfg.capacity, apex_columns(cfg.channels_last, frames_u8=u8), cfg.alpha, cfg.beta,
-                                    self.device, seed=cfg.seed + 7919 * rank)
+        self.svc.replay = HbmReplay(cfg.capacity, apex_columns(cfg.channels_last, frames_u8=u8,
+                                                               frame_store=cfg.frame_store),
+                                    cfg.alpha, cfg.beta, self.device, seed=cfg.seed + 7919 * rank,
+                                    frame_store=self.frame_store_frames(cfg) if cfg.frame_store else None)
         self.replay = self.svc.replay
+        if cfg.frame_store:
+            self.actors.attach_frame_store(self.replay)
         self.loader = TorchCudaLoader(self.addr, buffer_size=2, prefetch=1)
         self.env_steps = 0
         self.updates = 0
@@ -126,6 +131,17 @@ class ApexDQN:
         self._ev_acquired = None
         self.actor_modes = {}  # graph mode: actor steps replayed per mode ("dedup" / "full")
         self.conv_probe = None  # extra["probe_conv2"]: callable(tag) between the learner graph's parts
+
+    @staticmethod
+    def frame_store_frames(cfg):
+        """frames the store must hold (rth_replay_frames_attach): every frame a live row
+        references.  A row lives capacity / N actor steps after its append; its oldest frame
+        is at most n + 4 steps older than the append; each step adds N frames plus one per
+        ended episode (p_done N) -- so capacity (1 + p_done) + (n + 8) N, with the reset term
+        doubled and at least capacity / 64 as headroom (the prefill needs capacity + 7)"""
+        reset = max(cfg.capacity // 64, int(2 * cfg.capacity * cfg.p_done) + 1)
+        # + 8 N: the actors' initial stacks, pushed at construction and again behind a prefill
+        return cfg.capacity + reset + (cfg.n_step + 16) * cfg.n_actors + 16
 
     def close(self):
         _SERVICES.pop(self.addr, None)
@@ -143,6 +159,8 @@ class ApexDQN:
         g = torch.Generator(device=self.device)
         g.manual_seed(self.cfg.seed + 17 * self.rank)
         done = 0
+        if self.replay.frames is not None:
+            return self._prefill_frames(n_rows, g, chunk)
         while done < n_rows:
             m = min(chunk, n_rows - done)
             s0 = torch.randint(0, 256, (m, *OBS_SHAPE), dtype=torch.uint8, device=self.device, generator=g)
@@ -153,6 +171,41 @@ class ApexDQN:
             td = 1.0 - torch.rand(m, device=self.device, generator=g)  # (0, 1]
             self.replay.append([s0, a, r, s1, d], td)
             done += m
+
+    @torch.no_grad()
+    def _prefill_frames(self, n_rows, g, chunk):
+        """the frame store's prefill: one long synthetic trajectory -- n_rows + 7 uniform uint8
+        frames behind the store's head, row j's s0 = frames j .. j+3 and s1 = frames j+3 .. j+6
+        of it (an n = 3 step apart, as the actors' rows are) -- then the head moves past them,
+        so the actors' frames overwrite them in the order the FIFO overwrites their rows"""
+        store, K = self.replay.frames, OBS_SHAPE[0]
+        F = store.shape[0]
+        base = int(self.replay.frame_head)  # behind the frames already pushed (the actors' stacks)
+        nf = n_rows + 2 * K - 1
+        if base + nf > F:
+            raise ValueError(f"prefill of {n_rows} rows needs {nf} frames behind {base}, the store holds {F}")
+        for f0 in range(0, nf, chunk):
+            m = min(chunk, nf - f0)
+            store[base + f0:base + f0 + m] = torch.randint(0, 256, (m, *store.shape[1:]), dtype=torch.uint8,
+                                                           device=self.device, generator=g)
+        self.replay.frame_head.fill_(base + nf)
+        done = 0
+        while done < n_rows:
+            m = min(chunk, n_rows - done)
+            j = torch.arange(base + done, base + done + m, dtype=torch.int32, device=self.device)[:, None]
+            ks = torch.arange(K, dtype=torch.int32, device=self.device)[None, :]
+            s0, s1 = (j + ks).contiguous(), (j + K - 1 + ks).contiguous()
+            a = torch.randint(0, self.cfg.num_actions, (m,), dtype=torch.int64, device=self.device, generator=g)
+            r = (torch.rand(m, device=self.device, generator=g) < self.cfg.p_reward).float()
+            d = (torch.rand(m, device=self.device, generator=g) < self.cfg.p_done).float()
+            td = 1.0 - torch.rand(m, device=self.device, generator=g)  # (0, 1]
+            self.replay.append([s0, a, r, s1, d], td)
+            done += m
+        # the actors' current stacks enter again, behind the prefill: frames are overwritten in
+        # push order, and the first rows the actors append reference these
+        if self.actors.pushes:
+            raise RuntimeError("prefill a frame-store replay before the actors step")
+        self.actors.attach_frame_store(self.replay)
 
     # ------------------------------------------------------------------ the blocks
     def _actor_compute(self):

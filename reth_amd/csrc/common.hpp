@@ -52,6 +52,26 @@ __device__ __forceinline__ void split3_x4(float4 v, uint2 (&out)[3]) {
   for (int k = 0; k < 3; ++k) out[k] = make_uint2(t[k][0] | (t[k][1] << 16), t[k][2] | (t[k][3] << 16));
 }
 
+// the same split of 8 values (one 16-byte MFMA fragment per term) on the hardware's paired
+// round-to-nearest-even conversion (v_cvt_pk_bf16_f32): the same terms as bf16_rne_bits for
+// every finite value, at a quarter of the instructions
+using f32x2v = __attribute__((ext_vector_type(2))) float;
+using bf16x2v = __attribute__((ext_vector_type(2))) __bf16;
+__device__ __forceinline__ void split3_pk8(const float (&v)[8], bf16x8 (&out)[3]) {
+  uint32_t t[3][4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    f32x2v x = f32x2v{v[2 * q], v[2 * q + 1]};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const bf16x2v h = __builtin_convertvector(x, bf16x2v);
+      t[k][q] = __builtin_bit_cast(uint32_t, h);
+      if (k < 2) x = x - __builtin_convertvector(h, f32x2v);  // exact: h is x's nearest bf16
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) out[k] = __builtin_bit_cast(bf16x8, u32x4{t[k][0], t[k][1], t[k][2], t[k][3]});
+}
 
 // rth_relu_bias_grad's partial-sum slabs: one per workgroup of kBiasThreads lanes, about 8
 // row sweeps each, at most kBiasSlabs (shared with the deferred combine in conv.hip)

@@ -433,11 +433,12 @@ __global__ __launch_bounds__(256) void k_conv1_pack_bf16x3(const float *__restri
 // M-tiles of 16 output pixels of the workgroup's samples.  The two K halves meet in LDS
 // (fixed order: first half + second half, then + bias, ReLU), and the output leaves as one
 // contiguous run per workgroup (NHWC, or NCHW for FC1) in 16-byte stores.
-template <int KH, int KW, int S, int CIN, int HIN, int WIN, int NSAMP, int ROT, int KS>
+template <int KH, int KW, int S, int CIN, int HIN, int WIN, int NSAMP, int ROT, int KS, int COUT_ = 64>
 struct X9Geom {
-  static constexpr int COUT = 64, HOUT = (HIN - KH) / S + 1, WOUT = (WIN - KW) / S + 1, PIX = HOUT * WOUT;
+  static constexpr int COUT = COUT_, HOUT = (HIN - KH) / S + 1, WOUT = (WIN - KW) / S + 1, PIX = HOUT * WOUT;
+  static constexpr int NCB = COUT / 16;                                   // channel blocks (waves per K part)
   static constexpr int K = KH * KW * CIN, NCH = K / 32, NCHP = NCH / KS;  // 32-deep chunks, per K part
-  static constexpr int NT = 256 * KS;                                     // threads: 4 channel blocks x KS
+  static constexpr int NT = 64 * NCB * KS;                                // threads: NCB channel blocks x KS
   static constexpr int TILES = (NSAMP * PIX + 15) / 16;                  // 16-pixel M-tiles
   static constexpr int NG = CIN / 8;                                     // 16-byte ci groups
   static constexpr int ROWS = NSAMP * HIN * WIN;                         // staged input pixels
@@ -447,17 +448,29 @@ struct X9Geom {
   static constexpr int PACKED_U4 = (COUT / 16) * NCH * 3 * 64;           // packed weight fragments
   static_assert(CIN % 32 == 0 || 32 % CIN == 0, "a 32-deep chunk must stay inside one tap");
   static_assert(CIN % 8 == 0 && NCH % KS == 0 && KS >= 1 && KS <= 4, "K must split into KS parts of 32-deep chunks");
+  static_assert(COUT % 16 == 0 && NT <= 1024, "16-channel blocks, at most 16 waves");
   static_assert(OUT_F * 4 <= LDS_U4 * 16, "output staging must fit the input image");
   static_assert(LDS_U4 * 16 <= 163840, "LDS image too large");
   __device__ static int swz(int r) { return (r & ~15) | ((r + (r >> 5) * ROT) & 15); }
 };
 
-template <int KH, int KW, int S, int CIN, int HIN, int WIN, int NSAMP, int ROT, int KS>
-__global__ __launch_bounds__(256 * KS) void k_conv_x9(const float *__restrict__ x, int64_t n,
-                                                    const int64_t *__restrict__ n_dev, int nsamp,
-                                                    const u32x4 *__restrict__ wpk, const float *__restrict__ bias,
-                                                    float *__restrict__ y, int out_nchw) {
-  using G = X9Geom<KH, KW, S, CIN, HIN, WIN, NSAMP, ROT, KS>;
+// PAD > 0 (the data gradient, rth_conv_dgrad): the staged HIN x WIN image is the input
+// zero-padded by PAD on every side -- x is [n, HIN - 2 PAD, WIN - 2 PAD, CIN], the border reads
+// zero through the buffer resource's range check --, and bias == NULL writes the raw sums (no
+// bias, no ReLU).  CLS (conv2's data gradient, one launch for the 4 stride-parity classes):
+// blockIdx.y = class (py, px), its packed kernel at wpk + class * PACKED_U4, and output pixel
+// (jy, jx) of the class goes to pixel (2 jy + py, 2 jx + px) of the [n, 2 HOUT, 2 WOUT, COUT]
+// NHWC gradient.
+template <int KH, int KW, int S, int CIN, int HIN, int WIN, int NSAMP, int ROT, int KS, int PAD = 0, int COUT_ = 64,
+          int CLS = 0>
+__global__ __launch_bounds__(64 * (COUT_ / 16) * KS) void k_conv_x9(const float *__restrict__ x, int64_t n,
+                                                                  const int64_t *__restrict__ n_dev, int nsamp,
+                                                                  const u32x4 *__restrict__ wpk,
+                                                                  const float *__restrict__ bias,
+                                                                  float *__restrict__ y, int out_nchw) {
+  using G = X9Geom<KH, KW, S, CIN, HIN, WIN, NSAMP, ROT, KS, COUT_>;
+  if constexpr (CLS) wpk += (size_t)blockIdx.y * G::PACKED_U4;
+  constexpr int HS = HIN - 2 * PAD, WS = WIN - 2 * PAD;  // the source image
   constexpr int PIX = G::PIX, NCH2 = G::NCHP, NG = G::NG, PLANE = G::PLANE, COUT = G::COUT, NT = G::NT;
   __shared__ uint4 lds[G::LDS_U4];
   if (n_dev) {
@@ -471,7 +484,7 @@ __global__ __launch_bounds__(256 * KS) void k_conv_x9(const float *__restrict__ 
   const int nv = ns * PIX;  // valid output pixels
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int cb = wave & 3, half = wave >> 2;  // channel block, K part
+  const int cb = wave % G::NCB, half = wave / G::NCB;  // channel block, K part
 
   // this wave's B fragments: channels 16 cb + (lane & 15), chunks [half * NCH2, +NCH2), 3 terms
   bf16x8 wf[NCH2][3];
@@ -507,12 +520,19 @@ __global__ __launch_bounds__(256 * KS) void k_conv_x9(const float *__restrict__ 
   // "cond ? load : 0" made the compiler wait for each load before issuing the next: the
   // phase-B loads went out one at a time)
   const __amdgpu_buffer_rsrc_t x_rsrc = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float *>(x), 0, (int)(n * (int64_t)(HIN * WIN * CIN) * 4), 0x00020000);
-  const uint32_t xb0 = (uint32_t)(b0 * (int64_t)(HIN * WIN * CIN) * 4);
+      const_cast<float *>(x), 0, (int)(n * (int64_t)(HS * WS * CIN) * 4), 0x00020000);
+  const uint32_t xb0 = (uint32_t)(b0 * (int64_t)(HS * WS * CIN) * 4);
   auto fetch = [&](int i, int r0, int rend) -> float4 {
     int rr, c4;
     slot_of(i, r0, rr, c4);
-    const uint32_t off = rr < rend && rr < rows ? xb0 + (uint32_t)((rr * (CIN / 4) + c4) * 16) : 0x80000000u;
+    bool ok = rr < rend && rr < rows;
+    int src = rr;
+    if constexpr (PAD > 0) {  // staged pixel -> source pixel; the border reads zero
+      const int s = rr / (HIN * WIN), rem = rr - s * (HIN * WIN), yy = rem / WIN - PAD, xx = rem % WIN - PAD;
+      ok = ok && yy >= 0 && yy < HS && xx >= 0 && xx < WS;
+      src = (s * HS + yy) * WS + xx;
+    }
+    const uint32_t off = ok ? xb0 + (uint32_t)((src * (CIN / 4) + c4) * 16) : 0x80000000u;
     return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(x_rsrc, off, 0, 0));
   };
   auto commit = [&](float4 v, int i, int r0, int rend) {
@@ -539,7 +559,7 @@ __global__ __launch_bounds__(256 * KS) void k_conv_x9(const float *__restrict__ 
 #pragma unroll
     for (int u = 0; u < UB; ++u) vb[u] = fetch(tid + u * NT, RA, tid + u * NT < SB ? RA + RB_ : 0);
   }
-  const float bl = bias[cb * 16 + (lane & 15)];
+  const float bl = bias ? bias[cb * 16 + (lane & 15)] : 0.0f;
   __syncthreads();
 
   // per chunk of this wave's K half (wave-uniform): the tap's pixel offset and the ci group's
@@ -646,12 +666,21 @@ __global__ __launch_bounds__(256 * KS) void k_conv_x9(const float *__restrict__ 
         const int p = tile * 16 + 4 * g + i;
         if (p < nv) {
           const int f = fidx(p);
-          F[f] = relu_c(radd(radd(acc[tile][i], F[f]), bl));
+          F[f] = bias ? relu_c(radd(radd(acc[tile][i], F[f]), bl)) : radd(acc[tile][i], F[f]);
         }
       }
   }
   __syncthreads();
-  {
+  if constexpr (CLS) {  // the class's pixels scattered into the full gradient, 16-byte stores
+    const int py = blockIdx.y >> 1, px = blockIdx.y & 1, total4 = nv * COUT / 4;
+    const float4 *Fs = reinterpret_cast<const float4 *>(F);
+    for (int i = tid; i < total4; i += NT) {
+      const int p = i / (COUT / 4), c4 = i - p * (COUT / 4), s = p / PIX, pp = p - s * PIX;
+      const int jy = pp / G::WOUT, jx = pp - jy * G::WOUT;
+      const int64_t o = (((b0 + s) * (2 * G::HOUT) + 2 * jy + py) * (2 * G::WOUT) + 2 * jx + px) * COUT + 4 * c4;
+      *reinterpret_cast<float4 *>(y + o) = Fs[i];
+    }
+  } else {
     const int total4 = nv * COUT / 4;  // the run [b0, b0 + ns) of y is contiguous in both layouts
     float4 *yo = reinterpret_cast<float4 *>(y + b0 * (int64_t)(COUT * PIX));
     const float4 *Fs = reinterpret_cast<const float4 *>(F);
@@ -679,6 +708,55 @@ __device__ __forceinline__ void pack_x9(const float *__restrict__ w, u32x4 *__re
 template <int KH, int KW, int S, int CIN, int HIN, int WIN, int NSAMP, int ROT, int KS>
 __global__ __launch_bounds__(256) void k_conv_pack_x9(const float *__restrict__ w, u32x4 *__restrict__ packed) {
   pack_x9<KH, KW, S, CIN, HIN, WIN, NSAMP, ROT, KS>(w, packed, blockIdx.x * 256 + threadIdx.x);
+}
+
+// The data gradient of a stride-1 KH x KW convolution as a forward one (rth_conv_dgrad, conv3):
+//   gx[b, iy, ix, ci] = sum_{kh, kw, co} gy[b, iy - kh, ix - kw, co] W[co, kh, kw, ci]
+// = the convolution of gy zero-padded by K - 1 with W' [ci][kh'][kw'][co] = W[co][K-1-kh'][K-1-kw'][ci]
+// (the flipped, channel-transposed kernel), run by k_conv_x9 with PAD = K - 1 and no epilogue.
+// This packs W' from the forward OHWI weights into the x9 B fragments (slot layout of pack_x9:
+// output channel = ci, k' = (kh', kw', co), co fastest).
+template <int KH, int KW, int CIN, int COUT, int HIN, int WIN, int NSAMP, int ROT, int KS>
+__global__ __launch_bounds__(256) void k_conv_pack_x9_dgrad(const float *__restrict__ w, u32x4 *__restrict__ packed) {
+  using G = X9Geom<KH, KW, 1, COUT, HIN, WIN, NSAMP, ROT, KS>;  // the dgrad's "input" channels = the conv's COUT
+  const int sl = blockIdx.x * 256 + threadIdx.x;
+  if (sl >= G::PACKED_U4) return;
+  const int lane = sl % 64, t = (sl / 64) % 3, c = (sl / 192) % G::NCH, cb = sl / (192 * G::NCH);
+  const int ci = cb * 16 + (lane & 15), k0 = c * 32 + 8 * (lane >> 4);
+  const int tap = k0 / COUT, co0 = k0 % COUT, kh = KH - 1 - tap / KW, kw = KW - 1 - tap % KW;
+  float wv[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) wv[j] = w[((int64_t)(co0 + j) * KH * KW + kh * KW + kw) * CIN + ci];  // OHWI
+  uint32_t e[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) e[j] = bf16x3_term(wv[j], t);
+  packed[sl] = u32x4{e[0] | (e[1] << 16), e[2] | (e[3] << 16), e[4] | (e[5] << 16), e[6] | (e[7] << 16)};
+}
+
+// conv2 (4x4, stride 2) has no single flipped kernel: its data gradient splits by the parity
+// (py, px) of the input pixel, iy = 2 jy + py, ix = 2 jx + px.  Only taps kh = py + 2 a,
+// kw = px + 2 c reach such a pixel, from output pixel (jy - a, jx - c), so each class is a
+// stride-1 2x2 convolution of gy zero-padded by 1 with
+//   W'_cls[ci][kh'][kw'][co] = W[co][py + 2 (1 - kh')][px + 2 (1 - kw')][ci]
+// (kh' = 1 - a).  The 4 class kernels are packed back to back (class = 2 py + px), the slot
+// layout of pack_x9 each (output channel = ci, k' = (kh', kw', co), co fastest).
+template <int CIN, int COUT, int NSAMP, int ROT, int KS>
+__global__ __launch_bounds__(256) void k_conv_pack_x9_dgrad_cls(const float *__restrict__ w,
+                                                                u32x4 *__restrict__ packed) {
+  using G = X9Geom<2, 2, 1, COUT, 11, 11, NSAMP, ROT, KS, CIN>;
+  const int slg = blockIdx.x * 256 + threadIdx.x;
+  if (slg >= 4 * G::PACKED_U4) return;
+  const int cls = slg / G::PACKED_U4, sl = slg - cls * G::PACKED_U4, py = cls >> 1, px = cls & 1;
+  const int lane = sl % 64, t = (sl / 64) % 3, c = (sl / 192) % G::NCH, cb = sl / (192 * G::NCH);
+  const int ci = cb * 16 + (lane & 15), k0 = c * 32 + 8 * (lane >> 4);
+  const int tap = k0 / COUT, co0 = k0 % COUT, kh = py + 2 * (1 - tap / 2), kw = px + 2 * (1 - tap % 2);
+  float wv[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) wv[j] = w[((int64_t)(co0 + j) * 16 + kh * 4 + kw) * CIN + ci];  // OHWI, 4x4
+  uint32_t e[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) e[j] = bf16x3_term(wv[j], t);
+  packed[slg] = u32x4{e[0] | (e[1] << 16), e[2] | (e[3] << 16), e[4] | (e[5] << 16), e[6] | (e[7] << 16)};
 }
 
 // K parts per workgroup (waves = 4 channel blocks x KS): more parts, fewer weight registers per
@@ -1461,6 +1539,108 @@ static int wg_per_cu() {  // RTH_CONV_WG_PER_CU (tuning), default 2
 
 using namespace rth;
 
+// conv3's and conv2's data gradients on the exact-split bf16 MFMA (k_conv_x9 with PAD = K - 1
+// and no epilogue; conv2 as its 4 stride-parity classes, one launch, blockIdx.y = class), the
+// flipped kernels packed into a per-device workspace each launch; RTH_DGRAD3_F32=1 /
+// RTH_DGRAD2_F32=1: the fp32-MFMA k_conv_dgrad (A/B and parity cross-checks)
+#define X9_DGRAD3_KS 2
+#ifndef X9_DGRAD2_KS
+#define X9_DGRAD2_KS 2
+#endif
+template <int NS>
+using X9Dgrad3 = X9Geom<3, 3, 1, 64, 11, 11, NS, 3, X9_DGRAD3_KS>;
+template <int NS>
+using X9Dgrad2 = X9Geom<2, 2, 1, 64, 11, 11, NS, 3, X9_DGRAD2_KS, 32>;
+static bool env_off(const char *name) {
+  const char *e = getenv(name);
+  return e && atoi(e) != 0;
+}
+static bool dgrad3_x9() {
+  static const bool v = !env_off("RTH_DGRAD3_F32");
+  return v;
+}
+static bool dgrad2_x9() {
+  static const bool v = !env_off("RTH_DGRAD2_F32");
+  return v;
+}
+
+// the per-device packed-kernel workspace of one dgrad geometry (allocated on first use, which
+// must not be inside a graph capture)
+static int dgrad_workspace(u32x4 **ws, size_t bytes, hipStream_t st, u32x4 **out) {
+  int dev = 0;
+  RTH_HIP(hipGetDevice(&dev));
+  RTH_REQUIRE(dev >= 0 && dev < 64, "rth_conv_dgrad: device %d out of range", dev);
+  if (!ws[dev]) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    RTH_REQUIRE(hipStreamIsCapturing(st, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone,
+                "rth_conv_dgrad: the first data gradient of a geometry on a device must run outside graph capture");
+    RTH_HIP(hipMalloc(&ws[dev], bytes));
+  }
+  *out = ws[dev];
+  return RTH_OK;
+}
+
+// samples per workgroup (1 .. 3): the cost model of select_launch, `classes` workgroups per group
+static int64_t dgrad_x9_nsamp(int64_t n, int classes) {
+  const int64_t slots = (int64_t)cu_count() * x9_wg_per_cu();
+  int64_t ns = 0;
+  double best = 0.0;
+  for (int64_t k = 1; k <= 3; ++k) {
+    const int64_t rounds = (classes * ((n + k - 1) / k) + slots - 1) / slots;
+    const double cost = (double)rounds * ((double)k + 0.5);
+    if (ns == 0 || cost < best) best = cost, ns = k;
+  }
+  return ns;
+}
+
+static int launch_dgrad_x9(const void *fn, const float *gy, int64_t n, int64_t ns, int classes, int threads,
+                           const u32x4 *wpk, float *gx, hipStream_t st) {
+  const int nsi = (int)ns;
+  const int64_t grid = (n + ns - 1) / ns;
+  const int64_t *n_dev = nullptr;
+  const float *bias = nullptr;
+  int out_nchw = 0;
+  void *args[] = {(void *)&gy, (void *)&n, (void *)&n_dev, (void *)&nsi, (void *)&wpk, (void *)&bias, (void *)&gx,
+                  (void *)&out_nchw};
+  RTH_HIP(hipLaunchKernel(fn, dim3((unsigned)grid, (unsigned)classes), dim3(threads), args, 0, st));
+  return RTH_OK;
+}
+
+static int conv_dgrad_x9_conv3(const float *gy, int64_t n, const float *w, float *gx, hipStream_t st) {
+  static u32x4 *ws[64] = {};
+  constexpr int PK = X9Dgrad3<1>::PACKED_U4;
+  u32x4 *wpk = nullptr;
+  if (const int rc = dgrad_workspace(ws, (size_t)PK * 16, st, &wpk)) return rc;
+  RTH_REQUIRE(n * 49 * 64 * 4 < ((int64_t)1 << 31), "rth_conv_dgrad: gy of %lld samples exceeds 2 GiB", (long long)n);
+  hipLaunchKernelGGL((k_conv_pack_x9_dgrad<3, 3, 64, 64, 11, 11, 1, 3, X9_DGRAD3_KS>), dim3((PK + 255) / 256),
+                     dim3(256), 0, st, w, wpk);
+  RTH_LAUNCHED();
+  const void *fn[4] = {nullptr, reinterpret_cast<const void *>(&k_conv_x9<3, 3, 1, 64, 11, 11, 1, 3, X9_DGRAD3_KS, 2>),
+                       reinterpret_cast<const void *>(&k_conv_x9<3, 3, 1, 64, 11, 11, 2, 3, X9_DGRAD3_KS, 2>),
+                       reinterpret_cast<const void *>(&k_conv_x9<3, 3, 1, 64, 11, 11, 3, 3, X9_DGRAD3_KS, 2>)};
+  const int64_t ns = dgrad_x9_nsamp(n, 1);
+  return launch_dgrad_x9(fn[ns], gy, n, ns, 1, X9Dgrad3<1>::NT, wpk, gx, st);
+}
+
+// conv2: gy [n, 9, 9, 64] -> gx [n, 20, 20, 32]; each class reads gy padded to 11 x 11 and
+// writes its 10 x 10 pixels
+static int conv_dgrad_x9_conv2(const float *gy, int64_t n, const float *w, float *gx, hipStream_t st) {
+  static u32x4 *ws[64] = {};
+  constexpr int PK = X9Dgrad2<1>::PACKED_U4;
+  u32x4 *wpk = nullptr;
+  if (const int rc = dgrad_workspace(ws, (size_t)4 * PK * 16, st, &wpk)) return rc;
+  RTH_REQUIRE(n * 400 * 32 * 4 < ((int64_t)1 << 31), "rth_conv_dgrad: gx of %lld samples exceeds 2 GiB", (long long)n);
+  hipLaunchKernelGGL((k_conv_pack_x9_dgrad_cls<32, 64, 1, 3, X9_DGRAD2_KS>), dim3((4 * PK + 255) / 256), dim3(256), 0,
+                     st, w, wpk);
+  RTH_LAUNCHED();
+  const void *fn[4] = {
+      nullptr, reinterpret_cast<const void *>(&k_conv_x9<2, 2, 1, 64, 11, 11, 1, 3, X9_DGRAD2_KS, 1, 32, 1>),
+      reinterpret_cast<const void *>(&k_conv_x9<2, 2, 1, 64, 11, 11, 2, 3, X9_DGRAD2_KS, 1, 32, 1>),
+      reinterpret_cast<const void *>(&k_conv_x9<2, 2, 1, 64, 11, 11, 3, 3, X9_DGRAD2_KS, 1, 32, 1>)};
+  const int64_t ns = dgrad_x9_nsamp(n, 4);
+  return launch_dgrad_x9(fn[ns], gy, n, ns, 4, X9Dgrad2<1>::NT, wpk, gx, st);
+}
+
 extern "C" {
 
 int rth_conv_supported(const rth_conv_shape *shape) {
@@ -1656,6 +1836,22 @@ int rth_conv_dgrad_supported(const rth_conv_shape *shape) {
 
 int rth_conv_dgrad(const rth_conv_shape *shape, const float *gy, int64_t n, const float *w, float *gx, void *stream) {
   RTH_REQUIRE(shape && gy && w && gx && n >= 0, "rth_conv_dgrad: NULL argument");
+  if (dgrad3_x9() && shape->input == RTH_CONV_F32_NHWC && shape->cin == 64 && shape->hin == 9 && shape->win == 9 &&
+      shape->cout == 64 && shape->kh == 3 && shape->kw == 3 && shape->stride == 1) {
+    RTH_REQUIRE(((reinterpret_cast<uintptr_t>(gy) | reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(gx)) &
+                 15) == 0,
+                "rth_conv_dgrad: misaligned buffer");
+    if (n == 0) return RTH_OK;
+    return conv_dgrad_x9_conv3(gy, n, w, gx, as_stream(stream));
+  }
+  if (dgrad2_x9() && shape->input == RTH_CONV_F32_NHWC && shape->cin == 32 && shape->hin == 20 && shape->win == 20 &&
+      shape->cout == 64 && shape->kh == 4 && shape->kw == 4 && shape->stride == 2) {
+    RTH_REQUIRE(((reinterpret_cast<uintptr_t>(gy) | reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(gx)) &
+                 15) == 0,
+                "rth_conv_dgrad: misaligned buffer");
+    if (n == 0) return RTH_OK;
+    return conv_dgrad_x9_conv2(gy, n, w, gx, as_stream(stream));
+  }
   DgradLaunch l;
   RTH_REQUIRE(find_dgrad(*shape, &l), "rth_conv_dgrad: geometry (%d x %d x %d -> %d, k %dx%d, stride %d) not built",
               shape->cin, shape->hin, shape->win, shape->cout, shape->kh, shape->kw, shape->stride);

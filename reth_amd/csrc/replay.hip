@@ -27,7 +27,7 @@ int tree_sample_impl(rth_sumtree *t, int64_t batch, const double *uniforms, uint
                      uint64_t counter, int is_weights, double beta, int64_t *idx_out, double *out,
                      hipStream_t s, const ReplayState *st, const rth_schedule *beta_s);
 
-enum Conv : int32_t { CONV_COPY = 0, CONV_U8_F32 = 1, CONV_U8_F32_HWC = 2, CONV_F32_U8 = 3 };
+enum Conv : int32_t { CONV_COPY = 0, CONV_U8_F32 = 1, CONV_U8_F32_HWC = 2, CONV_F32_U8 = 3, CONV_STACK = 4 };
 
 // f32 pixel -> u8 (append of frames an actor sends as float32 whole numbers 0..255)
 __device__ __forceinline__ uint32_t f32_u8(float v) {
@@ -58,6 +58,12 @@ struct CopyCol {
   int64_t blk0;             // first workgroup of this column
   int32_t vec;              // every row's src/dst 16-byte aligned: vector path
   int32_t pad;
+  // CONV_STACK (a frame-stack column of a frame-store replay): the stored row is `planes`
+  // int32 frame ids, the output row the `planes` frames of frame_bytes each, read from the
+  // frame store (fcap frames); in_bytes is the OUTPUT row size there
+  const uint8_t *fstore;
+  int64_t frame_bytes;
+  int64_t fcap;
 };
 
 struct CopyArgs {
@@ -203,6 +209,16 @@ __global__ __launch_bounds__(kCopyThreads) void k_copy_rows(CopyArgs a) {
     return;
   }
   const int64_t o = chunk * col.chunk_in;  // first input byte of this chunk
+  if (col.conv == CONV_STACK) {  // 16-byte vectors of the stack, each from its frame in the store
+    const int32_t *ids = reinterpret_cast<const int32_t *>(src);
+    const int64_t off = o + 16 * tid;
+    if (off + 16 <= nb) {
+      const int64_t f = off / col.frame_bytes, in = off - f * col.frame_bytes;
+      const int64_t fid = (int64_t)(uint32_t)ids[f] % col.fcap;
+      *reinterpret_cast<uint4 *>(dst + off) = *reinterpret_cast<const uint4 *>(col.fstore + fid * col.frame_bytes + in);
+    }
+    return;
+  }
   if (col.conv == CONV_F32_U8) {  // 16-byte loads of 4 pixels -> one 4-byte store
     const float *sf = reinterpret_cast<const float *>(src);
     const int64_t e = o / 4 + 4 * tid;  // first element of this lane
@@ -382,6 +398,13 @@ int launch_copy(CopyArgs &a, hipStream_t s) {
       blocks += ((col.vec ? a.n * (nb / 4) : a.n) + kCopyThreads - 1) / kCopyThreads;
       continue;
     }
+    if (col.conv == CONV_STACK) {
+      col.chunk_in = 16 * kCopyThreads;
+      col.chunks = (nb + col.chunk_in - 1) / col.chunk_in;
+      col.vec = 1;  // frame_bytes % 16 == 0 and 16-byte aligned store / output (checked at attach)
+      blocks += a.n * col.chunks;
+      continue;
+    }
     if (col.conv == CONV_U8_F32_HWC) {
       const int64_t P = nb / col.planes;
       col.chunk_px = 4 * kCopyThreads * hwc_chunk_m();
@@ -421,6 +444,74 @@ int conv_of(int32_t in_dtype, int32_t out_dtype, int32_t planes, int32_t *conv) 
   return RTH_ERR_INVALID;
 }
 
+// ---------------------------------------------------------------- frame store
+// The actors' new frames enter the store once (rth_replay_push_frames); every stack is a tuple
+// of K frame ids in the actors' stack table (sid, one row per frame-ring stack), rows store
+// the tuples of their s0 / s1 stacks, and the gather assembles the stacks.  Per actor step:
+//   mode 0 (step): actor i's new stack s1_h[i] = its old stack s0_h[i] shifted by one frame +
+//     the new frame (FrameStack.step): the new frame (frame K-1 of s1) gets id head + i and
+//     sid[s1] = sid[s0][1..K-1] ++ [head + i]; where done[i], the reset stack (slot cur_slot[i])
+//     is one frame K times (FrameStack.reset): it gets id head + N + (done actors before i)
+//     and sid[reset] = [that id] x K;
+//   mode 1 (init): actor i's current stack (slot cur_slot[i]) enters as K new frames
+//     head + K i .. head + K i + K - 1.
+// One workgroup per actor copies its frame(s) (7,056 bytes each at Atari size, 16-byte
+// vectors); k_frames_advance then moves the head past the frames of the step.
+constexpr int kFrameThreads = 256;
+
+__global__ __launch_bounds__(kFrameThreads) void k_frames_push(const uint8_t *__restrict__ ring, int64_t stack_bytes,
+                                                               int64_t frame_bytes, int K, int ring_slots,
+                                                               const int64_t *__restrict__ s0_h,
+                                                               const int64_t *__restrict__ s1_h,
+                                                               const float *__restrict__ done,
+                                                               const int64_t *__restrict__ cur_slot,
+                                                               int32_t *__restrict__ sid, uint8_t *__restrict__ store,
+                                                               int64_t fcap, const int64_t *__restrict__ fhead,
+                                                               int64_t n, int mode) {
+  const int64_t i = blockIdx.x;
+  const int64_t head = *fhead;
+  const int64_t vecs = frame_bytes / 16;
+  auto copy = [&](const uint8_t *src, int64_t fid) {
+    uint4 *d = reinterpret_cast<uint4 *>(store + (fid % fcap) * frame_bytes);
+    const uint4 *sv = reinterpret_cast<const uint4 *>(src);
+    for (int64_t v = threadIdx.x; v < vecs; v += kFrameThreads) d[v] = sv[v];
+  };
+  if (mode == 1) {
+    const int64_t st = i * ring_slots + cur_slot[i];
+    for (int k = 0; k < K; ++k) copy(ring + st * stack_bytes + k * frame_bytes, head + K * i + k);
+    if (threadIdx.x < K) sid[st * K + threadIdx.x] = (int32_t)(uint32_t)((head + K * i + threadIdx.x) % fcap);
+    return;
+  }
+  const int64_t h0 = s0_h[i], h1 = s1_h[i];
+  copy(ring + h1 * stack_bytes + (K - 1) * frame_bytes, head + i);
+  if (threadIdx.x < K)  // the shifted tuple: read sid[s0] (another ring slot than s1) before writing s1's
+    sid[h1 * K + threadIdx.x] = threadIdx.x + 1 < K ? sid[h0 * K + threadIdx.x + 1]
+                                                    : (int32_t)(uint32_t)((head + i) % fcap);
+  if (done[i] != 0.0f) {  // workgroup-uniform; rare (p_done), so the rank is a plain count
+    int64_t r = 0;
+    for (int64_t j = 0; j < i; ++j) r += done[j] != 0.0f;
+    const int64_t rs = i * ring_slots + cur_slot[i], fid = head + n + r;
+    copy(ring + rs * stack_bytes, fid);
+    if (threadIdx.x < K) sid[rs * K + threadIdx.x] = (int32_t)(uint32_t)(fid % fcap);
+  }
+}
+
+// the head past this step's frames: N (+ one per done actor in mode 0, K per actor in mode 1)
+__global__ __launch_bounds__(kFrameThreads) void k_frames_advance(const float *__restrict__ done, int64_t n, int K,
+                                                                  int mode, int64_t *__restrict__ fhead) {
+  __shared__ int64_t part[kFrameThreads];
+  int64_t c = 0;
+  if (mode == 0)
+    for (int64_t j = threadIdx.x; j < n; j += kFrameThreads) c += done[j] != 0.0f;
+  part[threadIdx.x] = c;
+  __syncthreads();
+  for (int w = kFrameThreads / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) part[threadIdx.x] += part[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *fhead += mode == 1 ? (int64_t)K * n : n + part[0];
+}
+
 }  // namespace rth
 
 using namespace rth;
@@ -455,10 +546,20 @@ struct rth_replay {
   hipEvent_t bump_ev;
   hipStream_t bump_stream;
   int bump_valid;
+  // frame store (rth_replay_frames_attach): the frames the RTH_FRAMES columns' ids point at, a
+  // ring of fcap frames of frame_bytes written by rth_replay_push_frames at *fhead
+  uint8_t *fstore;
+  int64_t fcap, frame_bytes;
+  int64_t *fhead;  // device: frames pushed so far (the next frame id)
   // rth_replay_set_timing: one-shot events recorded around the next launches of each kind
   hipEvent_t timing[RTH_TIMING_SLOTS];
   int32_t timing_fired;  // bit k: slot k's event was recorded since the last arm
 };
+
+// bytes of one stored row of column c: a frame-stack column keeps out_planes int32 frame ids
+static int64_t stored_row_bytes(const rth_col_desc &d) {
+  return d.in_dtype == RTH_FRAMES ? (int64_t)d.out_planes * 4 : d.row_elems * dtype_size(d.in_dtype);
+}
 
 // record the one-shot timing event of slot k (if armed) on stream s
 static void timing_mark(rth_replay *h, int k, hipStream_t s) {
@@ -576,6 +677,12 @@ int rth_replay_create(int64_t capacity, int32_t n_cols, const rth_col_desc *cols
     RTH_REQUIRE(cols[c].row_elems >= 1, "rth_replay_create: column %d has no elements", c);
     RTH_REQUIRE(cols[c].out_planes == 0 || cols[c].row_elems % cols[c].out_planes == 0,
                 "rth_replay_create: column %d not divisible into %d planes", c, cols[c].out_planes);
+    if (cols[c].in_dtype == RTH_FRAMES) {  // K frame ids -> K frames of row_elems / K bytes
+      RTH_REQUIRE(cols[c].out_dtype == RTH_U8 && cols[c].out_planes >= 1 &&
+                      (cols[c].row_elems / cols[c].out_planes) % 16 == 0,
+                  "rth_replay_create: frame-stack column %d: u8 output of out_planes frames of a multiple of 16 bytes", c);
+      continue;
+    }
     int rc = conv_of(cols[c].in_dtype, cols[c].out_dtype, cols[c].out_planes, &conv);
     if (rc) return rc;
   }
@@ -599,7 +706,7 @@ int rth_replay_create(int64_t capacity, int32_t n_cols, const rth_col_desc *cols
   RTH_HIP(hipMemset(state, 0, sizeof(ReplayState) + sizeof(SamplerState)));
   for (int c = 0; c < n_cols; ++c) {
     h->desc[c] = cols[c];
-    const size_t bytes = (size_t)capacity * cols[c].row_elems * dtype_size(cols[c].in_dtype);
+    const size_t bytes = (size_t)capacity * stored_row_bytes(cols[c]);
     if (hipMalloc(&h->store[c], bytes) != hipSuccess) {
       set_error("rth_replay_create: hipMalloc(%zu) for column %d failed", bytes, c);
       for (int k = 0; k < c; ++k) (void)hipFree(h->store[k]);
@@ -634,6 +741,8 @@ int rth_replay_destroy(rth_replay *h) {
   for (void *p : {(void *)h->ulist, (void *)h->fidx, (void *)h->fw})
     if (p) (void)hipFree(p);
   if (h->bump_ev) (void)hipEventDestroy(h->bump_ev);
+  if (h->fstore) (void)hipFree(h->fstore);
+  if (h->fhead) (void)hipFree(h->fhead);
   delete h;
   return RTH_OK;
 }
@@ -647,6 +756,61 @@ int rth_replay_set_timing(rth_replay *h, void *const *events, int32_t n, int32_t
 }
 
 rth_sumtree *rth_replay_tree(rth_replay *h) { return h ? h->tree : nullptr; }
+
+int rth_replay_frames_attach(rth_replay *h, int64_t n_frames, int64_t frame_bytes, void **store_out,
+                             int64_t **head_out) {
+  RTH_REQUIRE(h && n_frames >= 1 && frame_bytes >= 16 && frame_bytes % 16 == 0,
+              "rth_replay_frames_attach: bad arguments (frames >= 1, frame bytes a multiple of 16)");
+  RTH_REQUIRE(n_frames < (int64_t(1) << 31), "rth_replay_frames_attach: %lld frames exceed the int32 frame ids",
+              (long long)n_frames);
+  RTH_REQUIRE(!h->fstore, "rth_replay_frames_attach: the frame store is already attached");
+  bool any = false;
+  for (int c = 0; c < h->ncols; ++c)
+    if (h->desc[c].in_dtype == RTH_FRAMES) {
+      RTH_REQUIRE(h->desc[c].row_elems == h->desc[c].out_planes * frame_bytes,
+                  "rth_replay_frames_attach: column %d holds %lld-element stacks of %d frames, not %lld-byte frames", c,
+                  (long long)h->desc[c].row_elems, h->desc[c].out_planes, (long long)frame_bytes);
+      any = true;
+    }
+  RTH_REQUIRE(any, "rth_replay_frames_attach: the replay has no frame-stack (RTH_FRAMES) column");
+  RTH_HIP(hipSetDevice(h->device));
+  if (hipMalloc(&h->fstore, (size_t)n_frames * frame_bytes) != hipSuccess) {
+    h->fstore = nullptr;
+    set_error("rth_replay_frames_attach: hipMalloc(%lld x %lld) failed", (long long)n_frames, (long long)frame_bytes);
+    return RTH_ERR_NOMEM;
+  }
+  if (hipMalloc(&h->fhead, 8) != hipSuccess) {
+    (void)hipFree(h->fstore);
+    h->fstore = nullptr;
+    return RTH_ERR_NOMEM;
+  }
+  RTH_HIP(hipMemset(h->fstore, 0, (size_t)n_frames * frame_bytes));
+  RTH_HIP(hipMemset(h->fhead, 0, 8));
+  h->fcap = n_frames;
+  h->frame_bytes = frame_bytes;
+  if (store_out) *store_out = h->fstore;
+  if (head_out) *head_out = h->fhead;
+  return RTH_OK;
+}
+
+int rth_replay_push_frames(rth_replay *h, const uint8_t *ring, int64_t n, int32_t ring_slots, int32_t stack,
+                           const int64_t *s0_h, const int64_t *s1_h, const float *done, const int64_t *cur_slot,
+                           int32_t *sid, int32_t mode, void *stream) {
+  RTH_REQUIRE(h && h->fstore, "rth_replay_push_frames: no frame store attached");
+  RTH_REQUIRE(ring && sid && cur_slot && n >= 0 && n <= 65535 && ring_slots >= 1 && stack >= 1 && stack <= 64 &&
+                  (mode == 1 || (mode == 0 && s0_h && s1_h && done)),
+              "rth_replay_push_frames: bad arguments");
+  if (n == 0) return RTH_OK;
+  const int64_t stack_bytes = (int64_t)stack * h->frame_bytes;
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(k_frames_push, dim3((unsigned)n), dim3(kFrameThreads), 0, s, ring, stack_bytes, h->frame_bytes,
+                     (int)stack, (int)ring_slots, s0_h, s1_h, done, cur_slot, sid, h->fstore, h->fcap, h->fhead, n,
+                     (int)mode);
+  RTH_LAUNCHED();
+  hipLaunchKernelGGL(k_frames_advance, dim3(1), dim3(kFrameThreads), 0, s, done, n, (int)stack, (int)mode, h->fhead);
+  RTH_LAUNCHED();
+  return RTH_OK;
+}
 
 void *rth_replay_column(rth_replay *h, int32_t c) {
   return (h && c >= 0 && c < h->ncols) ? (void *)h->store[c] : nullptr;
@@ -676,7 +840,7 @@ int rth_replay_append(rth_replay *h, const rth_src *srcs, const void *td_abs, in
   for (int c = 0; c < h->ncols; ++c) {
     RTH_REQUIRE(srcs[c].base_dev, "rth_replay_append: column %d source is NULL", c);
     const rth_col_desc &d = h->desc[c];
-    const int64_t rb = d.row_elems * dtype_size(d.in_dtype);
+    const int64_t rb = stored_row_bytes(d);  // frame-stack columns: the K ids (rth_replay_push_frames' table rows)
     int32_t conv = CONV_COPY;
     int64_t ib = rb;  // bytes of one source row
     if (srcs[c].src_dtype != 0 && srcs[c].src_dtype != d.in_dtype) {
@@ -729,6 +893,19 @@ static int gather_impl(rth_replay *h, const int64_t *idx, int64_t n, void *const
   for (int c = 0; n > 0 && c < h->ncols; ++c) {
     RTH_REQUIRE(out_cols[c], "rth_replay_gather: output column %d is NULL", c);
     const rth_col_desc &d = h->desc[c];
+    if (d.in_dtype == RTH_FRAMES) {  // the stack assembled from the frame store
+      RTH_REQUIRE(h->fstore, "rth_replay_gather: frame-stack column %d without a frame store", c);
+      const int64_t ob = d.row_elems;
+      CopyCol col{h->store[c], (uint8_t *)out_cols[c], idx, nullptr, stored_row_bytes(d), ob, ob, CONV_STACK,
+                  d.out_planes};
+      col.fstore = h->fstore;
+      col.frame_bytes = h->frame_bytes;
+      col.fcap = h->fcap;
+      RTH_REQUIRE((reinterpret_cast<uintptr_t>(out_cols[c]) & 15) == 0, "rth_replay_gather: output column %d not "
+                  "16-byte aligned", c);
+      a.col[c] = col;
+      continue;
+    }
     int32_t conv;
     conv_of(d.in_dtype, d.out_dtype, d.out_planes, &conv);
     const int64_t ib = d.row_elems * dtype_size(d.in_dtype), ob = d.row_elems * dtype_size(d.out_dtype);

@@ -146,10 +146,9 @@ __device__ __forceinline__ int64_t tree_find(const Node *__restrict__ nd, int64_
 // (all its lanes hold the same target), so a shuffle never reads an inactive lane.
 template <int K>
 __device__ __forceinline__ int64_t tree_find_group(const Node *__restrict__ nd, int64_t cap, double w, int base,
-                                                   int sub) {
+                                                   int sub, int64_t cur = 0, double cval = -1.0) {
   constexpr int NP = (1 << K) - 1;
-  int64_t cur = 0;
-  double cval = nd[1].val;
+  if (cur == 0 && cval < 0.0) cval = nd[1].val;  // from the root (else: resumed below an LDS-staged top)
   const int dq = 31 - __builtin_clz(sub + 1);
   const int64_t off = sub + 1 - (1 << dq);
   for (;;) {
@@ -173,11 +172,32 @@ static int find_group_k() {  // read per call: tests switch it
 }
 
 __device__ __forceinline__ int64_t tree_find_grouped(const Node *__restrict__ nd, int64_t cap, double w, int gk,
-                                                     int base, int sub) {
+                                                     int base, int sub, int64_t cur = 0, double cval = -1.0) {
   switch (gk) {
-    case 3: return tree_find_group<3>(nd, cap, w, base, sub);
-    case 5: return tree_find_group<5>(nd, cap, w, base, sub);
-    default: return tree_find_group<4>(nd, cap, w, base, sub);
+    case 3: return tree_find_group<3>(nd, cap, w, base, sub, cur, cval);
+    case 5: return tree_find_group<5>(nd, cap, w, base, sub, cur, cval);
+    default: return tree_find_group<4>(nd, cap, w, base, sub, cur, cval);
+  }
+}
+
+// The hot top of the tree staged in LDS (north_star: "LDS-staged segment scans for the tree"):
+// every sample workgroup copies {sum, val} of the nodes of the first kTopLevels levels (the
+// nodes every target's walk passes through) with one coalesced pass, then each target walks
+// those levels in LDS -- the same find_step comparisons and subtractions -- and only the levels
+// below go to HBM (the grouped walk, resumed at the node reached).  Returns true when the walk
+// must continue below the staged levels (cur / cval / w hold its state), false when `cur` is
+// already the answer.
+constexpr int kTopLevels = 10;
+constexpr int kTopStaged = (1 << kTopLevels) - 1;  // 1,023 nodes, 16 KB of LDS
+__device__ __forceinline__ bool lds_top_walk(const double2 *__restrict__ top, int64_t cap, int64_t nstaged,
+                                             int64_t &cur, double &cval, double &w) {
+  cur = 0;
+  cval = top[0].y;
+  for (;;) {
+    const int64_t l = 2 * cur + 1;
+    if (l >= nstaged) return l < cap;  // the children are below the staged levels (or absent)
+    const Pair p{top[l].x, top[l].y, l + 1 < cap ? top[l + 1].y : 0.0};
+    if (!find_step(cur, cval, w, p, cap)) return false;
   }
 }
 
@@ -975,22 +995,38 @@ __global__ void k_tree_find(const Node *__restrict__ nd, int64_t cap, const doub
 }
 
 // _numba_sample (sumtree.py:70-79) and, with is_weights, PERSampler.sample (:24-28)
+// top > 0: the first kTopLevels levels are staged in LDS (lds_top_walk; gk > 0 only)
 __global__ void k_tree_sample(const Node *__restrict__ nd, int64_t cap, int64_t batch,
                               const double *__restrict__ uniforms, uint64_t seed, uint64_t counter,
                               int is_weights, double beta, const ReplayState *st, rth_schedule beta_s,
-                              int64_t *__restrict__ idx_out, double *__restrict__ out, int kspec, int gk) {
+                              int64_t *__restrict__ idx_out, double *__restrict__ out, int kspec, int gk, int top) {
+  __shared__ double2 topl[kTopStaged];
   const FindLane fl = find_lane(gk);
   const int64_t i = fl.i;
+  const int64_t nst = top ? (cap < kTopStaged ? cap : kTopStaged) : 0;
+  if (top) {  // every lane takes part in the staging, before any of them may leave
+    for (int64_t j = threadIdx.x; j < nst; j += blockDim.x)
+      topl[j] = *reinterpret_cast<const double2 *>(&nd[j + 1]);  // {sum, val}
+    __syncthreads();
+  }
   if (i >= batch) return;  // uniform over a group
   if (st) {  // a replay shard's device state: call counter and beta_s(sched_step)
     counter = (uint64_t)st->calls;
     beta = sched_value(beta_s, st->sched_step);
   }
-  const double total = nd[1].sum;
+  const double total = top ? topl[0].x : nd[1].sum;
   const double seg = total / (double)batch;
   const double u = uniforms ? uniforms[i] : philox_uniform(seed, counter, (uint32_t)i, STREAM_SAMPLE);
-  const double t = rmul(radd((double)i, u), seg);
-  const int64_t k = gk ? tree_find_grouped(nd, cap, t, gk, fl.base, fl.sub) : tree_find(nd, cap, t, kspec);
+  double t = rmul(radd((double)i, u), seg);
+  int64_t k;
+  if (top && gk) {
+    int64_t cur;
+    double cval;
+    k = lds_top_walk(topl, cap, nst, cur, cval, t) ? tree_find_grouped(nd, cap, t, gk, fl.base, fl.sub, cur, cval)
+                                                    : cur;
+  } else {
+    k = gk ? tree_find_grouped(nd, cap, t, gk, fl.base, fl.sub) : tree_find(nd, cap, t, kspec);
+  }
   if (fl.sub) return;
   const double p = nd[k + 1].val;
   idx_out[i] = k;
@@ -1109,11 +1145,16 @@ int tree_sample_impl(rth_sumtree *t, int64_t batch, const double *uniforms, uint
                      uint64_t counter, int is_weights, double beta, int64_t *idx_out, double *out,
                      hipStream_t s, const ReplayState *st, const rth_schedule *beta_s) {
   if (batch <= 0) return RTH_OK;
-  const int bs = sample_bs(), gk = find_group_k();
+  const int gk = find_group_k();
+  // RTH_TREE_LDS_TOP=0: no LDS-staged top (A/B); staged, the workgroups are 256 lanes (16
+  // targets): fewer copies of the staged levels
+  static const int lds_top = env_int("RTH_TREE_LDS_TOP", 1);
+  const int top = lds_top && gk ? 1 : 0;
+  const int bs = top ? 256 : sample_bs();
   const int64_t lanes = batch << gk;
   hipLaunchKernelGGL(k_tree_sample, dim3((unsigned)((lanes + bs - 1) / bs)), dim3(bs), 0, s, t->nodes,
                      t->cap, batch, uniforms, seed, counter, is_weights, beta, st,
-                     beta_s ? *beta_s : rth_schedule{}, idx_out, out, find_k(), gk);
+                     beta_s ? *beta_s : rth_schedule{}, idx_out, out, find_k(), gk, top);
   RTH_LAUNCHED();
   return RTH_OK;
 }

@@ -153,7 +153,7 @@ __global__ __launch_bounds__(kWgfWaves * 64) void k_conv_wgrad_f32(const float *
 // gw[e] = sum of the splits' partials (e over COUT * K) in a fixed order: a workgroup takes 64
 // consecutive elements; thread (g, e) sums the splits g, g + 4, g + 8, ... of element e with
 // all of its loads in flight together, then the 4 group sums are added in group order
-constexpr int kWgfRedMax = 64;  // splits per element at most: 16 per thread
+constexpr int kWgfRedMax = 128;  // splits per element at most: 32 per thread
 __global__ __launch_bounds__(256) void k_conv_wgrad_f32_reduce(const float *__restrict__ part, int splits,
                                                               int64_t elems, float *__restrict__ gw) {
   __shared__ float red[4][64];
@@ -216,106 +216,159 @@ static int wgf_splits(const WgfLaunch &l) {
 // The same weight gradient on the bf16 MFMA with both operands split into three exact bf16
 // terms (the x9 scheme of conv.hip's k_conv_x9: every partial product xi * gj has at most 16
 // significant bits, so it is exact in the fp32 accumulator -- the same real products as the
-// fp32 path, summed in another fixed order).  GEMM view as above, on
-// v_mfma_f32_16x16x32_bf16: rows = 16 output channels, columns = 16 kk, reduction = a chunk of
-// 32 consecutive output pixels, lane l supplying pixels 8 (l >> 4) + j, j < 8, of row / column
-// l & 15 -- 8 scalar loads per operand, each a 64-byte run of channels across 16 lanes.
-// Workgroup = 4 waves over one column group of 4 blocks (64 kk) and a range of chunks: wave w
-// owns output channels 16w .. 16w + 15 (its A fragments, loaded and split by itself) and
-// splits column block w's B fragment for the whole workgroup into LDS (double-buffered, one
-// barrier per chunk); every wave then runs 4 blocks x 9 MFMAs per chunk.  Partials per
-// workgroup go to the workspace; k_conv_wgrad_f32_reduce adds them in split order.
+// fp32 path, summed in another fixed order), each operand split ONCE per workgroup.
+//
+// GEMM view as above on v_mfma_f32_16x16x32_bf16: rows = 16 output channels, columns = 16 kk,
+// reduction = a chunk of 32 consecutive output pixels p = (b, oy, ox), lane group g supplying
+// pixels 8g .. 8g + 7.  A workgroup owns one kernel row kh (the KW * CIN columns kk = (kh, kw,
+// ci), 128 at conv2, 192 at conv3) x all 64 output channels, and a range of chunks (its split).
+// Per chunk it stages both operands in LDS already split and transposed to the fragment
+// order -- per term, one 64-byte row per output channel (gy) and per column (the im2col x),
+// each row the 32 pixels' bf16 values as 4 16-byte units (unit g = pixels 8g .. 8g + 7, XOR-
+// placed within the row so that every ds_read_b128 lane group of 16 hits 16 distinct bank
+// quads) --, then every wave runs its CPW column blocks x 4 channel blocks x 9 MFMAs from it.
+// Staging: 64 threads load gy (float4 = 4 channels of one pixel, 8 pixels each), the next
+// XQ * 4 threads the im2col x (float4 = 4 consecutive kk of one pixel, 8 pixels each; the
+// pixels' window offsets from a per-chunk table), one chunk ahead in registers; each splits its
+// 4 x 8 values into 3 x 4 fragments with v_cvt_pk_bf16_f32.  Partials per workgroup go to the
+// workspace; k_conv_wgrad_f32_reduce adds them in split order.
 template <int KH, int KW, int S, int CIN, int HIN, int WIN>
 struct WgxGeom {
   static constexpr int HOUT = (HIN - KH) / S + 1, WOUT = (WIN - KW) / S + 1, PIX = HOUT * WOUT;
-  static constexpr int K = KH * KW * CIN, COUT = 64, GROUPS = K / 64;
-  static_assert(CIN % 16 == 0 && K % 64 == 0, "16-column blocks inside one tap, 64-column groups");
+  static constexpr int K = KH * KW * CIN, COUT = 64, GROUPS = KH;
+  static constexpr int NCOL = KW * CIN;     // columns per workgroup (one kernel row)
+  static constexpr int NCB = NCOL / 16;     // column blocks
+  static constexpr int CPW = NCB / 4;       // column blocks per wave (4 waves)
+  static constexpr int XQ = NCOL / 4;       // x column quads
+  static constexpr int ROWS = COUT + NCOL;  // LDS rows per term: gy channels, then x columns
+  static constexpr int LDS_U4 = 3 * ROWS * 4;
+  static_assert(CIN % 4 == 0 && NCB % 4 == 0 && 64 + 4 * XQ <= 256, "column quads, 4 waves of column blocks");
 };
 
-__device__ __forceinline__ void split3_x8(const float (&v)[8], bf16x8 (&out)[3]) {
-  uint2 lo[3], hi[3];
-  split3_x4(make_float4(v[0], v[1], v[2], v[3]), lo);
-  split3_x4(make_float4(v[4], v[5], v[6], v[7]), hi);
-#pragma unroll
-  for (int t = 0; t < 3; ++t) out[t] = __builtin_bit_cast(bf16x8, u32x4{lo[t].x, lo[t].y, hi[t].x, hi[t].y});
+// the 16-byte unit of (term, row, pixel group g): rows of 4 units, g XORed with a per-row-quad
+// key {0, 2, 3, 1} -- a ds_read_b128 lane group ({0-3, 12-15, 20-27}, ...: rows r and r + 12 of
+// one g and rows r + 4 .. r + 11 of the next) then covers all 16 bank quads once
+template <int ROWS>
+__device__ __forceinline__ int wgx_unit(int t, int row, int g) {
+  return (t * ROWS + row) * 4 + (g ^ ((0x78 >> (2 * ((row >> 2) & 3))) & 3));
 }
 
-#ifndef WGX_PF
-#define WGX_PF 1
-#endif
 template <int KH, int KW, int S, int CIN, int HIN, int WIN>
 __global__ __launch_bounds__(256) void k_conv_wgrad_x9(const float *__restrict__ x, const float *__restrict__ gy,
                                                       int64_t n, int splits, float *__restrict__ part) {
   using G = WgxGeom<KH, KW, S, CIN, HIN, WIN>;
-  constexpr int COUT = G::COUT, PIX = G::PIX, WOUT = G::WOUT, K = G::K;
-  __shared__ bf16x8 bl[2][3][4][64];  // [buffer][term][column block][lane]
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, r = lane & 15;
-  const int group = (int)(blockIdx.x / splits), split = (int)(blockIdx.x % splits);
-  const int64_t P = n * PIX, chunks = (P + 31) / 32;
-  const int64_t c0 = chunks * split / splits, c1 = chunks * (split + 1) / splits;
-  const int co = wave * 16 + r;                 // A: this lane's output channel
-  const int kk = (group * 4 + wave) * 16 + r;   // B staged by this lane: column kk
-  const int tap = kk / CIN, ci = kk % CIN;
-  const int xoff = ((tap / KW) * WIN + tap % KW) * CIN + ci;
-  // pixel indices fit 32 bits (n * PIX < 2^31 is checked on the host)
-  const int Pi = (int)P;
-  auto load = [&](int64_t c, float (&a)[8], float (&b)[8]) {
-    const int p0 = (int)c * 32 + 8 * g;
+  constexpr int COUT = G::COUT, PIX = G::PIX, WOUT = G::WOUT, K = G::K, ROWS = G::ROWS, CPW = G::CPW;
+  __shared__ uint4 lds[G::LDS_U4];
+  __shared__ int tbl[2][32];  // per chunk (double-buffered): each pixel's window origin in x
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, r = lane & 15;
+  const int kh = (int)(blockIdx.x / splits), split = (int)(blockIdx.x % splits);
+  const int P = (int)(n * PIX);  // < 2^31: checked on the host
+  const int chunks = (P + 31) / 32;
+  const int c0 = (int)((int64_t)chunks * split / splits), c1 = (int)((int64_t)chunks * (split + 1) / splits);
+  if (c0 >= c1) {  // an empty split still owns its partial
+    float *out = part + (int64_t)split * COUT * K;
+    for (int e = tid; e < COUT * G::NCOL; e += 256) out[(int64_t)(e / G::NCOL) * K + kh * G::NCOL + e % G::NCOL] = 0.f;
+    return;
+  }
+  // staging role: gy (tid < 64: channel quad, pixel group), x (column quad, pixel group), idle
+  const bool is_gy = tid < 64, is_x = tid >= 64 && tid < 64 + 4 * G::XQ;
+  const int u = is_gy ? tid : tid - 64;
+  const int quad = is_gy ? (u & 15) : (u % G::XQ), spg = is_gy ? (u >> 4) : (u / G::XQ);
+  const int qcol = 4 * quad;                         // first row of the quad (channel or column)
+  const int xoff = (kh * WIN + qcol / CIN) * CIN + qcol % CIN;  // (kh, kw, ci0) inside the window
+  const int row0 = is_gy ? qcol : COUT + qcol;
+  // gy through a buffer resource: a pixel past P reads zeros (and weighs 0 against any x)
+  const __amdgpu_buffer_rsrc_t gy_rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(gy), 0, P * COUT * 4, 0x00020000);
+  auto make_tbl = [&](int c) {  // 32 threads: the window origin of the chunk's pixels
+    if (tid >= 32) return;
+    const int p = c * 32 + tid;
+    int v = 0;  // a dead pixel reads x's first window (finite) against gy = 0
+    if (p < P) {
+      const int b = p / PIX, pp = p - b * PIX, oy = pp / WOUT, ox = pp - oy * WOUT;
+      v = ((b * HIN + S * oy) * WIN + S * ox) * CIN;
+    }
+    tbl[c & 1][tid] = v;
+  };
+  float4 pre[8];
+  auto load = [&](int c) {
+    if (is_gy) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int p = p0 + j;
-      const bool live = p < Pi;
-      const int bb = p / PIX, pix = p - bb * PIX, oy = pix / WOUT, ox = pix - oy * WOUT;
-      a[j] = live ? gy[p * COUT + co] : 0.0f;  // a dead pixel weighs 0
-      b[j] = live ? x[((bb * HIN + S * oy) * WIN + S * ox) * CIN + xoff] : 0.0f;
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t off = (uint32_t)(((c * 32 + 8 * spg + j) * COUT + qcol) * 4);
+        pre[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(gy_rsrc, off, 0, 0));
+      }
+    } else if (is_x) {
+      const int4 *t4 = reinterpret_cast<const int4 *>(&tbl[c & 1][8 * spg]);
+      const int4 ta = t4[0], tb = t4[1];
+      const int o[8] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y, tb.z, tb.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pre[j] = *reinterpret_cast<const float4 *>(x + o[j] + xoff);
     }
   };
-  f32x4 acc[4];
+  auto stage = [&]() {  // split the 4 rows x 8 pixels held in pre into LDS
+    if (!is_gy && !is_x) return;
 #pragma unroll
-  for (int kb = 0; kb < 4; ++kb) acc[kb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-  // WGX_PF chunks' raw loads in flight (a register ring; the loop is unrolled by WGX_PF)
-  float av[WGX_PF][8], bv[WGX_PF][8];
+    for (int e = 0; e < 4; ++e) {
+      const float v[8] = {pre[0][e], pre[1][e], pre[2][e], pre[3][e], pre[4][e], pre[5][e], pre[6][e], pre[7][e]};
+      bf16x8 tr[3];
+      split3_pk8(v, tr);
 #pragma unroll
-  for (int d = 0; d < WGX_PF; ++d)
-    if (c0 + d < c1) load(c0 + d, av[d], bv[d]);
-  int buf = 0;
-  for (int64_t cb = c0; cb < c1; cb += WGX_PF)
-#pragma unroll
-  for (int d = 0; d < WGX_PF; ++d) {
-    const int64_t c = cb + d;
-    if (c >= c1) break;  // uniform
-    bf16x8 at[3], bt[3];
-    split3_x8(av[d], at);
-    split3_x8(bv[d], bt);
-#pragma unroll
-    for (int t = 0; t < 3; ++t) bl[buf][t][wave][lane] = bt[t];
-    if (c + WGX_PF < c1) load(c + WGX_PF, av[d], bv[d]);  // in flight during the next chunks
-    __syncthreads();
-#pragma unroll
-    for (int kb = 0; kb < 4; ++kb) {
-      const bf16x8 b0 = bl[buf][0][kb][lane], b1 = bl[buf][1][kb][lane], b2 = bl[buf][2][kb][lane];
-      f32x4 a = acc[kb];
-      // smallest terms first: (3,3) (3,2) (2,3) (3,1) (2,2) (1,3) (2,1) (1,2) (1,1)
-      a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(at[2], b2, a, 0, 0, 0);
-      a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(at[2], b1, a, 0, 0, 0);
-      a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(at[1], b2, a, 0, 0, 0);
-      a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(at[2], b0, a, 0, 0, 0);
-      a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(at[1], b1, a, 0, 0, 0);
-      a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(at[0], b2, a, 0, 0, 0);
-      a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(at[1], b0, a, 0, 0, 0);
-      a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(at[0], b1, a, 0, 0, 0);
-      a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(at[0], b0, a, 0, 0, 0);
-      acc[kb] = a;
+      for (int t = 0; t < 3; ++t) lds[wgx_unit<ROWS>(t, row0 + e, spg)] = __builtin_bit_cast(uint4, tr[t]);
     }
-    buf ^= 1;
+  };
+  f32x4 acc[4][CPW];
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+    for (int kb = 0; kb < CPW; ++kb) acc[cb][kb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  make_tbl(c0);
+  __syncthreads();
+  load(c0);
+  if (c0 + 1 < c1) make_tbl(c0 + 1);
+  for (int c = c0; c < c1; ++c) {
+    stage();  // chunk c (its loads waited on here)
+    __syncthreads();
+    if (c + 1 < c1) load(c + 1);  // in flight during chunk c's MFMAs
+    bf16x8 bfr[CPW][3];
+#pragma unroll
+    for (int kb = 0; kb < CPW; ++kb)
+#pragma unroll
+      for (int t = 0; t < 3; ++t)
+        bfr[kb][t] = __builtin_bit_cast(bf16x8, lds[wgx_unit<ROWS>(t, COUT + 16 * (wave * CPW + kb) + r, g)]);
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+      bf16x8 af[3];
+#pragma unroll
+      for (int t = 0; t < 3; ++t) af[t] = __builtin_bit_cast(bf16x8, lds[wgx_unit<ROWS>(t, 16 * cb + r, g)]);
+#pragma unroll
+      for (int kb = 0; kb < CPW; ++kb) {
+        f32x4 a = acc[cb][kb];
+        const bf16x8(&b)[3] = bfr[kb];
+        // smallest terms first: (3,3) (3,2) (2,3) (3,1) (2,2) (1,3) (2,1) (1,2) (1,1)
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[2], b[2], a, 0, 0, 0);
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[2], b[1], a, 0, 0, 0);
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], b[2], a, 0, 0, 0);
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[2], b[0], a, 0, 0, 0);
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], b[1], a, 0, 0, 0);
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], b[2], a, 0, 0, 0);
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], b[0], a, 0, 0, 0);
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], b[1], a, 0, 0, 0);
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], b[0], a, 0, 0, 0);
+        acc[cb][kb] = a;
+      }
+    }
+    if (c + 2 < c1) make_tbl(c + 2);  // its buffer was last read by load(c)
+    __syncthreads();  // chunk c's fragments read: the LDS rows may be restaged
   }
-  // D: lane holds rows (channels) 16 wave + 4 (l >> 4) + i of column 16 kb + (l & 15)
-  float *out = part + (int64_t)split * COUT * K;
+  // D: lane holds channels 16 cb + 4 g + i of column 16 (wave * CPW + kb) + r of this kernel row
+  float *out = part + (int64_t)split * COUT * K + kh * G::NCOL;
 #pragma unroll
-  for (int kb = 0; kb < 4; ++kb)
+  for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      out[(int64_t)(wave * 16 + 4 * g + i) * K + (group * 4 + kb) * 16 + r] = acc[kb][i];
+    for (int kb = 0; kb < CPW; ++kb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) out[(int64_t)(16 * cb + 4 * g + i) * K + 16 * (wave * CPW + kb) + r] = acc[cb][kb][i];
 }
 
 struct WgxLaunch {
@@ -336,10 +389,10 @@ static bool find_wgx(const rth_conv_shape &s, WgxLaunch *out) {
     return s.input == RTH_CONV_F32_NHWC && s.cin == cin && s.hin == hin && s.win == win && s.cout == cout &&
            s.kh == kh && s.kw == kw && s.stride == st;
   };
-  if (is(32, 20, 20, 64, 4, 4, 2)) {  // conv2: K = 512 -> 8 groups of 64 columns
+  if (is(32, 20, 20, 64, 4, 4, 2)) {  // conv2: 4 kernel rows of 128 columns
     static const WgxLaunch l = wgx_launch<4, 4, 2, 32, 20, 20>();
     *out = l;
-  } else if (is(64, 9, 9, 64, 3, 3, 1)) {  // conv3: K = 576 -> 9 groups (one tap each)
+  } else if (is(64, 9, 9, 64, 3, 3, 1)) {  // conv3: 3 kernel rows of 192 columns
     static const WgxLaunch l = wgx_launch<3, 3, 1, 64, 9, 9>();
     *out = l;
   } else {
@@ -348,16 +401,15 @@ static bool find_wgx(const rth_conv_shape &s, WgxLaunch *out) {
   return true;
 }
 
-#ifndef WGX_SPLITS
-#define WGX_SPLITS 64
-#endif
-static int wgx_splits() {  // RTH_WGX_SPLITS (A/B), at most kWgfRedMax
-  static const int v = [] {
+// splits per kernel row: about one workgroup per CU over the KH rows (RTH_WGX_SPLITS: A/B),
+// at most kWgfRedMax
+static int wgx_splits(const WgxLaunch &l) {
+  static const int env = [] {
     const char *e = getenv("RTH_WGX_SPLITS");
-    int x = e ? atoi(e) : WGX_SPLITS;
-    return x < 1 ? 1 : (x > kWgfRedMax ? kWgfRedMax : x);
+    return e ? atoi(e) : 0;
   }();
-  return v;
+  int x = env > 0 ? env : 256 / l.groups;
+  return x < 1 ? 1 : (x > kWgfRedMax ? kWgfRedMax : x);
 }
 
 }  // namespace rth
@@ -374,7 +426,7 @@ int rth_conv_wgrad_x9_supported(const rth_conv_shape *shape) {
 int64_t rth_conv_wgrad_x9_workspace(const rth_conv_shape *shape) {
   WgxLaunch l;
   if (!shape || !find_wgx(*shape, &l)) return 0;
-  return (int64_t)wgx_splits() * l.elems * 4;
+  return (int64_t)wgx_splits(l) * l.elems * 4;
 }
 
 int rth_conv_wgrad_x9(const rth_conv_shape *shape, const float *x, int64_t n, const float *gy, float *gw,
@@ -387,8 +439,13 @@ int rth_conv_wgrad_x9(const rth_conv_shape *shape, const float *x, int64_t n, co
     RTH_HIP(hipMemsetAsync(gw, 0, l.elems * 4, as_stream(stream)));
     return RTH_OK;
   }
-  RTH_REQUIRE(n * shape->cin * shape->hin * shape->win < ((int64_t)1 << 31), "rth_conv_wgrad_x9: batch too large");
-  int splits = wgx_splits();
+  RTH_REQUIRE(n * shape->cin * shape->hin * shape->win < ((int64_t)1 << 31) &&
+                  n * ((shape->hin - shape->kh) / shape->stride + 1) * ((shape->win - shape->kw) / shape->stride + 1) *
+                          shape->cout * 4 < ((int64_t)1 << 31),
+              "rth_conv_wgrad_x9: batch too large");
+  RTH_REQUIRE(((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(gy)) & 15) == 0,
+              "rth_conv_wgrad_x9: misaligned buffer");
+  int splits = wgx_splits(l);
   float *part = static_cast<float *>(workspace);
   void *args[] = {(void *)&x, (void *)&gy, (void *)&n, (void *)&splits, (void *)&part};
   RTH_HIP(hipLaunchKernel(l.fn, dim3((unsigned)(l.groups * splits)), dim3(256), args, 0, as_stream(stream)));

@@ -37,7 +37,9 @@ TD_HB_MAX = 16384  # rth_td_heads_backward keeps B * (A + 1) TD gradient rows in
 # vs 61 us alone; 0.615 vs 0.630 ms/step in the loop, where the learner stream is the critical
 # path), conv3's opt-in (RTH_HIP_DGRAD3=1, A/B aid); RTH_MIOPEN_DGRAD=1 restores MIOpen's
 HIP_DGRAD = {1} if os.environ.get("RTH_MIOPEN_DGRAD") is None else set()
-if os.environ.get("RTH_HIP_DGRAD3") is not None:
+# conv3's on the exact-split bf16 MFMA (rth_conv_dgrad -> k_conv_x9 over the zero-padded gy with
+# the flipped kernel) by default since r04; RTH_MIOPEN_DGRAD3=1 restores MIOpen's
+if os.environ.get("RTH_MIOPEN_DGRAD3") is None and os.environ.get("RTH_MIOPEN_DGRAD") is None:
     HIP_DGRAD.add(2)
 # conv2 / conv3 weight gradients in a hand-written kernel (deterministic, no zero fill) instead
 # of MIOpen's: RTH_HIP_WGRAD=x9 (rth_conv_wgrad_x9, bf16 MFMA with the exact 3 x 3-term split)

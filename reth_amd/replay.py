@@ -200,6 +200,28 @@ class Column:
         return torch.empty((n, *self.shape), dtype=self.out_dtype, device=device, memory_format=fmt)
 
 
+class FrameColumn(Column):
+    """a frame-stack column of a frame-store replay: a row stores its
+    stack as `shape[0]` int32 frame ids into the replay's frame store, the sample assembles
+    the uint8 stack [K, H, W] -- the bytes a full uint8 row would hold (rth_replay_frames_attach)"""
+
+    def __init__(self, shape):
+        super().__init__(shape, torch.int32, torch.int32)
+        self.out_dtype = torch.uint8
+        self.frames = True
+
+    @property
+    def out_planes(self):
+        return self.shape[0]
+
+    @property
+    def frame_bytes(self):
+        return self.row_elems // self.shape[0]
+
+    def desc(self):
+        return ColDesc(self.row_elems, _lib.RTH_FRAMES, _lib.RTH_U8, self.out_planes, 0)
+
+
 SAMPLERS = {"per": _lib.SAMPLER_PER, "uniform": _lib.SAMPLER_UNIFORM, "fifo": _lib.SAMPLER_FIFO}
 
 
@@ -212,7 +234,7 @@ class HbmReplay:
     their weights (ones / the pushed weights) where PER returns IS weights.
     """
 
-    def __init__(self, capacity, columns, alpha=0.6, beta=0.4, device=None, seed=0, sampler="per"):
+    def __init__(self, capacity, columns, alpha=0.6, beta=0.4, device=None, seed=0, sampler="per", frame_store=None):
         if not 1 <= len(columns) <= _lib.MAX_COLS:
             raise ValueError(f"1..{_lib.MAX_COLS} columns supported, got {len(columns)}")
         self.capacity = int(capacity)
@@ -231,6 +253,21 @@ class HbmReplay:
                  ctypes.byref(sched_struct(self.alpha)), ctypes.byref(sched_struct(self.beta)), self.device.index,
                  int(seed), ctypes.byref(h))
         self._h = h.value
+        # frame_store (int): the frame de-duplicated replay -- FrameColumn stacks as frame ids
+        # into a ring of that many frames (rth_replay_frames_attach); frames / frame_head are
+        # device views of the store and its head
+        self.frames = self.frame_head = None
+        fcols = [c for c in self.columns if getattr(c, "frames", False)]
+        if frame_store is not None or fcols:
+            if not fcols or frame_store is None:
+                raise ValueError("a frame store needs FrameColumn columns and frame_store=<frames>, both")
+            fb = fcols[0].frame_bytes
+            store, head = c_vp(), c_vp()
+            with torch.cuda.device(self.device):
+                call("rth_replay_frames_attach", self._h, int(frame_store), fb, ctypes.byref(store), ctypes.byref(head))
+            self.frames = _wrap_device(store.value, int(frame_store) * fb, torch.uint8, self.device).view(
+                int(frame_store), *fcols[0].shape[1:])
+            self.frame_head = _wrap_device(head.value, 1, torch.int64, self.device)
         th = _lib.lib().rth_replay_tree(self._h)
         self._tree = SumTree(self.capacity, self.device, _handle=th) if th else None
         self._pending = None  # buffers of a deferred priority update (kept alive until applied)
@@ -285,11 +322,21 @@ class HbmReplay:
         return self.info()[2]
 
     def column_storage(self, c):
-        """device tensor view of column c's storage [capacity, *shape]"""
+        """device tensor view of column c's storage [capacity, *shape] ([capacity, K] frame ids
+        for a FrameColumn)"""
         col = self.columns[c]
         p = _lib.lib().rth_replay_column(self._h, c)
+        if getattr(col, "frames", False):
+            return _wrap_device(p, self.capacity * col.shape[0], torch.int32, self.device).view(self.capacity,
+                                                                                                 col.shape[0])
         n = self.capacity * col.row_elems
         return _wrap_device(p, n, col.dtype, self.device).view(self.capacity, *col.shape)
+
+    def push_frames(self, ring, n, ring_slots, s0_h, s1_h, done, cur_slot, sid, init=False):
+        """an actor step's new frames into the frame store and the stacks' frame ids into
+        `sid` (rth_replay_push_frames; init: the actors' initial stacks)"""
+        call("rth_replay_push_frames", self._h, ptr(ring), int(n), int(ring_slots), int(ring.shape[1]), ptr(s0_h),
+             ptr(s1_h), ptr(done), ptr(cur_slot), ptr(sid), 1 if init else 0, stream_ptr())
 
     # ---------------------------------------------------------------- ops
     def append(self, cols, td_abs, src_rows=None, row_strides=None, idx_out=None, raw=False):

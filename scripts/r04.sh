@@ -47,6 +47,45 @@ for s in "$@"; do
     dp8) RTH_SHARE_GPU=1 RTH_DIST_BACKEND=gloo step dp8_gloo_rehearsal 900 python -m torch.distributed.run --nnodes=1 \
           --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 8 --faithful --steps 20 \
           --warmup 5 --no-cpu-baseline --no-sweep ;;
+    fstore) step fstore_tests 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
+          tests/test_frame_store_gpu.py tests/test_replay_gpu.py tests/test_atari_loop_gpu.py tests/test_gemm_tuning_gpu.py ;;
+    breakout) step bench_breakout 900 python bench.py --workload breakout --steps 100 --warmup 10 --no-cpu-baseline --no-sweep
+      step bench_breakout_fs 900 python bench.py --workload breakout --frame-store --steps 100 --warmup 10 \
+          --no-cpu-baseline --no-sweep ;;
+    dgradt) step dgrad_tests 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
+          tests/test_conv_gpu.py tests/test_fused_learner_gpu.py tests/test_learner_full_gpu.py ;;
+    dgradab) for r in 1 2; do
+        RTH_MIOPEN_DGRAD3=1 RTH_DGRAD2_F32=1 step ab_miopen_$r 300 python bench.py --steps 300 --warmup 5 \
+            --no-cpu-baseline --no-sweep --probe-steps 0
+        RTH_DGRAD2_F32=1 step ab_x9dgrad3_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep \
+            --probe-steps 0
+        step ab_x9dgrad_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep --probe-steps 0
+      done
+      grep -h -o '"ms_per_step": [0-9.]*' gpurun_out/ab_*.log ;;
+    treet) step tree_tests 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
+          tests/test_sumtree_gpu.py tests/test_scale_gpu.py tests/test_samplers_gpu.py tests/test_replay_gpu.py ;;
+    treeab) for r in 1 2; do
+        RTH_TREE_LDS_TOP=0 step ab_tree0_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        step ab_tree1_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+      done
+      for f in gpurun_out/ab_tree*.log; do python - "$f" <<'PY'
+import json, sys
+d = json.loads([l for l in open(sys.argv[1]) if l.startswith('{"metric"')][-1])
+h = {r["kernel"]: r["mean_launch_us"] for r in d["roofline_hbm"]}
+print(sys.argv[1], d["ms_per_step"], "sample_us", h["k_tree_sample"], "update_us", h["k_tree_update_sub"])
+PY
+      done ;;
+    kbench) step conv_kernel_tests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
+          tests/test_conv_gpu.py -k "dgrad or wgrad"
+      step bench_dgrad_x9 300 python scripts/bench_dgrad.py
+      RTH_DGRAD2_F32=1 RTH_DGRAD3_F32=1 step bench_dgrad_f32 300 python scripts/bench_dgrad.py
+      step bench_wgrad 300 python scripts/bench_wgrad_f32.py ;;
+    wgxab) for r in 1 2; do
+        step ab_wgmiopen_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep --probe-steps 0
+        RTH_HIP_WGRAD=x9 step ab_wgx9_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep \
+            --probe-steps 0
+      done
+      grep -h -o '"ms_per_step": [0-9.]*' gpurun_out/ab_wg*.log ;;
     tests) step gpu_tests 1100 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;

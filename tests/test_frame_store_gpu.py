@@ -1,0 +1,94 @@
+"""Frame de-duplicated replay (rth_replay_frames_attach / push_frames, the
+gather's frame-stack columns): each actor frame enters an HBM frame store once, rows keep
+their s0 / s1 stacks as frame ids, the gather assembles the stacks.  Through the Ape-X loop
+-- with many episode ends (p_done = 0.25: reset stacks, and the NStepAdder's terminal-bootstrap
+rows whose s1 is the terminal stack, reth/reth/utils/nstep_adder.py:14-24) and both the FIFO
+and the frame ring wrapping -- every sampled stack, every replay row and every learner update
+are bit-identical to the full-row uint8 storage the reference's layout corresponds to
+(test/apex-dqn/worker.py:44-51 stores both stacks of every row)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(dev, frame_store, graph, iters=150, env="synthetic"):
+    from reth_amd.apex import ApexConfig, ApexDQN
+
+    cfg = ApexConfig(n_actors=16, capacity=1024, batch_size=32, sample_start=64, p_done=0.25, seed=6,
+                     hip_graph=graph, send_weights_interval=3, recv_weights_interval=4, update_target_interval=5,
+                     frame_store=frame_store, env=env)
+    ax = ApexDQN(cfg, device=dev)
+    for _ in range(iters):
+        ax.iteration()
+    torch.cuda.synchronize()
+    assert (ax._graphs is not None) == graph
+    rep = ax.replay
+    size = rep.info()[0]
+    s, m, v = rep.tree.export()
+    cols = rep.gather(torch.arange(size, device=dev))
+    params = torch.cat([p.detach().flatten() for p in ax.solver._params]).cpu()
+    out = dict(tree=[s.cpu(), m.cpu(), v.cpu()], cols=[c.cpu() for c in cols], params=params, info=rep.info(),
+               frames=ax.actors.frames.cpu(), updates=ax.updates)
+    if frame_store:
+        out["head"] = int(rep.frame_head)
+        out["F"] = rep.frames.shape[0]
+        out["sid_table"] = rep.column_storage(0).cpu()
+    ax.close()
+    return out
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_frame_store_loop_bit_identical_to_full_rows(dev, graph):
+    full = _run(dev, False, graph)
+    fs = _run(dev, True, graph)
+    assert full["info"] == fs["info"] and full["updates"] == fs["updates"] > 50
+    assert fs["info"][0] == 1024 and fs["head"] > fs["F"], "the FIFO and the frame ring must both have wrapped"
+    names = ["s0", "a", "r", "s1", "done"]
+    for name, x, y in zip(names, full["cols"], fs["cols"]):
+        assert torch.equal(x, y), (name, int((x != y).sum()))
+    for x, y in zip(full["tree"], fs["tree"]):
+        assert torch.equal(x, y)
+    assert torch.equal(full["frames"], fs["frames"])
+    assert torch.equal(full["params"], fs["params"])  # the learner saw the same batches
+    done = fs["cols"][4].numpy() != 0
+    assert done.any() and (~done).any()
+
+
+def test_frame_store_atari_env(dev):
+    """the Atari env mode (device preprocessing, reset screens) into the frame store"""
+    full = _run(dev, False, True, iters=60, env="atari")
+    fs = _run(dev, True, True, iters=60, env="atari")
+    for x, y in zip(full["cols"], fs["cols"]):
+        assert torch.equal(x, y)
+    assert torch.equal(full["params"], fs["params"])
+
+
+def test_frame_store_prefill_and_footprint(dev):
+    """the prefill's synthetic trajectory: row j's stacks are frames j .. j+3 and j+3 .. j+6 of
+    it; the store holds capacity (1 + reset headroom) frames: the HBM footprint"""
+    from reth_amd.apex import ApexConfig, ApexDQN
+
+    cfg = ApexConfig(n_actors=16, capacity=2048, batch_size=32, seed=2, hip_graph=False, frame_store=True)
+    ax = ApexDQN(cfg, device=dev)
+    ax.prefill(cfg.capacity)
+    torch.cuda.synchronize()
+    rep = ax.replay
+    ids = rep.column_storage(0).cpu().numpy()
+    base = int(ids[0, 0])
+    assert np.array_equal(ids[:, 0], base + np.arange(cfg.capacity))
+    rows = torch.tensor([0, 1, 777, cfg.capacity - 1], device=dev)
+    s0, _, _, s1, _ = rep.gather(rows)
+    store = rep.frames
+    for k, j in enumerate(rows.tolist()):
+        assert torch.equal(s0[k], store[base + j:base + j + 4])
+        assert torch.equal(s1[k], store[base + j + 3:base + j + 7])
+    # ~1 frame per row (+ reset headroom) against 2 x 4 frames per full row
+    assert store.shape[0] <= 1.1 * cfg.capacity + 20 * cfg.n_actors + 16
+    # the loop runs on from the prefilled state
+    for _ in range(8):
+        ax.iteration()
+    torch.cuda.synchronize()
+    assert ax.updates > 0
+    ax.close()

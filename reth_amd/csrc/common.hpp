@@ -36,41 +36,35 @@ __host__ __device__ __forceinline__ uint32_t bf16_rne_bits(float f) {
   return u >> 16;
 }
 __host__ __device__ __forceinline__ float bf16_bits_f(uint32_t b) { return __uint_as_float(b << 16); }
-// the three bf16 terms of 4 fp32 values, packed 2 per dword: out[t] = {t(v0) | t(v1) << 16, ...}
-__device__ __forceinline__ void split3_x4(float4 v, uint2 (&out)[3]) {
-  const float in[4] = {v.x, v.y, v.z, v.w};
-  uint32_t t[3][4];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const uint32_t h1 = bf16_rne_bits(in[e]);
-    const float r1 = rsub(in[e], bf16_bits_f(h1));
-    const uint32_t h2 = bf16_rne_bits(r1);
-    const float r2 = rsub(r1, bf16_bits_f(h2));
-    t[0][e] = h1, t[1][e] = h2, t[2][e] = bf16_rne_bits(r2);
-  }
-#pragma unroll
-  for (int k = 0; k < 3; ++k) out[k] = make_uint2(t[k][0] | (t[k][1] << 16), t[k][2] | (t[k][3] << 16));
-}
-
-// the same split of 8 values (one 16-byte MFMA fragment per term) on the hardware's paired
-// round-to-nearest-even conversion (v_cvt_pk_bf16_f32): the same terms as bf16_rne_bits for
-// every finite value, at a quarter of the instructions
+// the three bf16 terms of 4 fp32 values, packed 2 per dword: out[t] = {t(v0) | t(v1) << 16, ...},
+// on the hardware's paired round-to-nearest-even conversion (v_cvt_pk_bf16_f32: the same terms
+// as bf16_rne_bits for every finite value, at a quarter of the instructions)
 using f32x2v = __attribute__((ext_vector_type(2))) float;
 using bf16x2v = __attribute__((ext_vector_type(2))) __bf16;
-__device__ __forceinline__ void split3_pk8(const float (&v)[8], bf16x8 (&out)[3]) {
-  uint32_t t[3][4];
+__device__ __forceinline__ void split3_pair(float a, float b, uint32_t (&t)[3]) {
+  f32x2v x = f32x2v{a, b};
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    f32x2v x = f32x2v{v[2 * q], v[2 * q + 1]};
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const bf16x2v h = __builtin_convertvector(x, bf16x2v);
-      t[k][q] = __builtin_bit_cast(uint32_t, h);
-      if (k < 2) x = x - __builtin_convertvector(h, f32x2v);  // exact: h is x's nearest bf16
-    }
+  for (int k = 0; k < 3; ++k) {
+    const bf16x2v h = __builtin_convertvector(x, bf16x2v);
+    t[k] = __builtin_bit_cast(uint32_t, h);
+    if (k < 2) x = x - __builtin_convertvector(h, f32x2v);  // exact: h is x's nearest bf16
   }
+}
+__device__ __forceinline__ void split3_x4(float4 v, uint2 (&out)[3]) {
+  uint32_t lo[3], hi[3];
+  split3_pair(v.x, v.y, lo);
+  split3_pair(v.z, v.w, hi);
 #pragma unroll
-  for (int k = 0; k < 3; ++k) out[k] = __builtin_bit_cast(bf16x8, u32x4{t[k][0], t[k][1], t[k][2], t[k][3]});
+  for (int k = 0; k < 3; ++k) out[k] = make_uint2(lo[k], hi[k]);
+}
+
+// the same split of 8 values: one 16-byte MFMA fragment per term
+__device__ __forceinline__ void split3_pk8(const float (&v)[8], bf16x8 (&out)[3]) {
+  uint32_t t[4][3];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) split3_pair(v[2 * q], v[2 * q + 1], t[q]);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) out[k] = __builtin_bit_cast(bf16x8, u32x4{t[0][k], t[1][k], t[2][k], t[3][k]});
 }
 
 // rth_relu_bias_grad's partial-sum slabs: one per workgroup of kBiasThreads lanes, about 8

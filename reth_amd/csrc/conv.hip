@@ -1542,7 +1542,7 @@ using namespace rth;
 // conv3's and conv2's data gradients on the exact-split bf16 MFMA (k_conv_x9 with PAD = K - 1
 // and no epilogue; conv2 as its 4 stride-parity classes, one launch, blockIdx.y = class), the
 // flipped kernels packed into a per-device workspace each launch; RTH_DGRAD3_F32=1 /
-// RTH_DGRAD2_F32=1: the fp32-MFMA k_conv_dgrad (A/B and parity cross-checks)
+// RTH_DGRAD2_F32=1: the fp32-MFMA k_conv_dgrad instead (A/B and parity cross-checks)
 #define X9_DGRAD3_KS 2
 #ifndef X9_DGRAD2_KS
 #define X9_DGRAD2_KS 2
@@ -1551,16 +1551,16 @@ template <int NS>
 using X9Dgrad3 = X9Geom<3, 3, 1, 64, 11, 11, NS, 3, X9_DGRAD3_KS>;
 template <int NS>
 using X9Dgrad2 = X9Geom<2, 2, 1, 64, 11, 11, NS, 3, X9_DGRAD2_KS, 32>;
-static bool env_off(const char *name) {
+static bool env_set(const char *name) {
   const char *e = getenv(name);
   return e && atoi(e) != 0;
 }
 static bool dgrad3_x9() {
-  static const bool v = !env_off("RTH_DGRAD3_F32");
+  static const bool v = !env_set("RTH_DGRAD3_F32");
   return v;
 }
-static bool dgrad2_x9() {
-  static const bool v = !env_off("RTH_DGRAD2_F32");
+static bool dgrad2_x9() {  // 37.8 vs 43 us alone, 0.571-0.573 vs 0.574-0.575 ms/step in the loop (r04)
+  static const bool v = !env_set("RTH_DGRAD2_F32");
   return v;
 }
 
@@ -1580,12 +1580,17 @@ static int dgrad_workspace(u32x4 **ws, size_t bytes, hipStream_t st, u32x4 **out
   return RTH_OK;
 }
 
-// samples per workgroup (1 .. 3): the cost model of select_launch, `classes` workgroups per group
-static int64_t dgrad_x9_nsamp(int64_t n, int classes) {
-  const int64_t slots = (int64_t)cu_count() * x9_wg_per_cu();
+// samples per workgroup (1 .. 3): the cost model of select_launch, `classes` workgroups per
+// group, with each instantiation's resident workgroups per CU from the occupancy query (the
+// LDS image: 1 - 3 per CU)
+static int64_t dgrad_x9_nsamp(int64_t n, int classes, const void *const *fn, int threads, int cap) {
   int64_t ns = 0;
   double best = 0.0;
   for (int64_t k = 1; k <= 3; ++k) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn[k], threads, 0) != hipSuccess || per_cu < 1)
+      per_cu = 1;
+    const int64_t slots = (int64_t)cu_count() * (per_cu < cap ? per_cu : cap);
     const int64_t rounds = (classes * ((n + k - 1) / k) + slots - 1) / slots;
     const double cost = (double)rounds * ((double)k + 0.5);
     if (ns == 0 || cost < best) best = cost, ns = k;
@@ -1618,7 +1623,7 @@ static int conv_dgrad_x9_conv3(const float *gy, int64_t n, const float *w, float
   const void *fn[4] = {nullptr, reinterpret_cast<const void *>(&k_conv_x9<3, 3, 1, 64, 11, 11, 1, 3, X9_DGRAD3_KS, 2>),
                        reinterpret_cast<const void *>(&k_conv_x9<3, 3, 1, 64, 11, 11, 2, 3, X9_DGRAD3_KS, 2>),
                        reinterpret_cast<const void *>(&k_conv_x9<3, 3, 1, 64, 11, 11, 3, 3, X9_DGRAD3_KS, 2>)};
-  const int64_t ns = dgrad_x9_nsamp(n, 1);
+  const int64_t ns = dgrad_x9_nsamp(n, 1, fn, X9Dgrad3<1>::NT, (int)x9_wg_per_cu());
   return launch_dgrad_x9(fn[ns], gy, n, ns, 1, X9Dgrad3<1>::NT, wpk, gx, st);
 }
 
@@ -1637,7 +1642,8 @@ static int conv_dgrad_x9_conv2(const float *gy, int64_t n, const float *w, float
       nullptr, reinterpret_cast<const void *>(&k_conv_x9<2, 2, 1, 64, 11, 11, 1, 3, X9_DGRAD2_KS, 1, 32, 1>),
       reinterpret_cast<const void *>(&k_conv_x9<2, 2, 1, 64, 11, 11, 2, 3, X9_DGRAD2_KS, 1, 32, 1>),
       reinterpret_cast<const void *>(&k_conv_x9<2, 2, 1, 64, 11, 11, 3, 3, X9_DGRAD2_KS, 1, 32, 1>)};
-  const int64_t ns = dgrad_x9_nsamp(n, 4);
+  // (4 waves per workgroup at COUT = 32: as many resident as the LDS image allows)
+  const int64_t ns = dgrad_x9_nsamp(n, 4, fn, X9Dgrad2<1>::NT, 4);
   return launch_dgrad_x9(fn[ns], gy, n, ns, 4, X9Dgrad2<1>::NT, wpk, gx, st);
 }
 

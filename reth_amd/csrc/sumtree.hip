@@ -103,10 +103,10 @@ __device__ __forceinline__ bool find_step(int64_t &cur, double &cval, double &w,
 }
 
 template <int K>
-__device__ __forceinline__ int64_t tree_find_k(const Node *__restrict__ nd, int64_t cap, double w) {
+__device__ __forceinline__ int64_t tree_find_k(const Node *__restrict__ nd, int64_t cap, double w, int64_t cur = 0,
+                                               double cval = -1.0) {
   constexpr int NP = (1 << K) - 1;  // pairs per round trip: c's subtree down to depth K-1
-  int64_t cur = 0;
-  double cval = nd[1].val;
+  if (cur == 0 && cval < 0.0) cval = nd[1].val;  // from the root (else: resumed below an LDS-staged top)
   for (;;) {
     Pair p[NP];
 #pragma unroll
@@ -130,12 +130,13 @@ __device__ __forceinline__ int64_t tree_find_k(const Node *__restrict__ nd, int6
   }
 }
 
-__device__ __forceinline__ int64_t tree_find(const Node *__restrict__ nd, int64_t cap, double w, int kspec = 2) {
+__device__ __forceinline__ int64_t tree_find(const Node *__restrict__ nd, int64_t cap, double w, int kspec = 2,
+                                             int64_t cur = 0, double cval = -1.0) {
   switch (kspec) {
-    case 1: return tree_find_k<1>(nd, cap, w);
-    case 4: return tree_find_k<4>(nd, cap, w);
-    case 3: return tree_find_k<3>(nd, cap, w);
-    default: return tree_find_k<2>(nd, cap, w);
+    case 1: return tree_find_k<1>(nd, cap, w, cur, cval);
+    case 4: return tree_find_k<4>(nd, cap, w, cur, cval);
+    case 3: return tree_find_k<3>(nd, cap, w, cur, cval);
+    default: return tree_find_k<2>(nd, cap, w, cur, cval);
   }
 }
 
@@ -995,7 +996,8 @@ __global__ void k_tree_find(const Node *__restrict__ nd, int64_t cap, const doub
 }
 
 // _numba_sample (sumtree.py:70-79) and, with is_weights, PERSampler.sample (:24-28)
-// top > 0: the first kTopLevels levels are staged in LDS (lds_top_walk; gk > 0 only)
+// top > 0: the first kTopLevels levels are staged in LDS (lds_top_walk), the walk resumed below
+// them by the grouped walk (gk > 0) or the one-lane walk with kspec levels per round trip
 __global__ void k_tree_sample(const Node *__restrict__ nd, int64_t cap, int64_t batch,
                               const double *__restrict__ uniforms, uint64_t seed, uint64_t counter,
                               int is_weights, double beta, const ReplayState *st, rth_schedule beta_s,
@@ -1019,11 +1021,11 @@ __global__ void k_tree_sample(const Node *__restrict__ nd, int64_t cap, int64_t 
   const double u = uniforms ? uniforms[i] : philox_uniform(seed, counter, (uint32_t)i, STREAM_SAMPLE);
   double t = rmul(radd((double)i, u), seg);
   int64_t k;
-  if (top && gk) {
+  if (top) {
     int64_t cur;
     double cval;
-    k = lds_top_walk(topl, cap, nst, cur, cval, t) ? tree_find_grouped(nd, cap, t, gk, fl.base, fl.sub, cur, cval)
-                                                    : cur;
+    if (!lds_top_walk(topl, cap, nst, cur, cval, t)) k = cur;
+    else k = gk ? tree_find_grouped(nd, cap, t, gk, fl.base, fl.sub, cur, cval) : tree_find(nd, cap, t, kspec, cur, cval);
   } else {
     k = gk ? tree_find_grouped(nd, cap, t, gk, fl.base, fl.sub) : tree_find(nd, cap, t, kspec);
   }
@@ -1149,7 +1151,7 @@ int tree_sample_impl(rth_sumtree *t, int64_t batch, const double *uniforms, uint
   // RTH_TREE_LDS_TOP=0: no LDS-staged top (A/B); staged, the workgroups are 256 lanes (16
   // targets): fewer copies of the staged levels
   static const int lds_top = env_int("RTH_TREE_LDS_TOP", 1);
-  const int top = lds_top && gk ? 1 : 0;
+  const int top = lds_top ? 1 : 0;
   const int bs = top ? 256 : sample_bs();
   const int64_t lanes = batch << gk;
   hipLaunchKernelGGL(k_tree_sample, dim3((unsigned)((lanes + bs - 1) / bs)), dim3(bs), 0, s, t->nodes,

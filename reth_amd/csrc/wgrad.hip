@@ -19,6 +19,8 @@
 // consecutive pixel sub-ranges of the same column group; their partials are summed in LDS
 // in wave order, and the workgroup's partial goes to the workspace; k_wgrad_f32_reduce adds
 // the partials of a column group in workgroup order.  Every sum has a fixed order.
+#include <type_traits>
+
 #include "common.hpp"
 
 namespace rth {
@@ -258,89 +260,84 @@ __global__ __launch_bounds__(256) void k_conv_wgrad_x9(const float *__restrict__
                                                       int64_t n, int splits, float *__restrict__ part) {
   using G = WgxGeom<KH, KW, S, CIN, HIN, WIN>;
   constexpr int COUT = G::COUT, PIX = G::PIX, WOUT = G::WOUT, K = G::K, ROWS = G::ROWS, CPW = G::CPW;
-  __shared__ uint4 lds[G::LDS_U4];
-  __shared__ int tbl[2][32];  // per chunk (double-buffered): each pixel's window origin in x
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, r = lane & 15;
+  constexpr int BUF = G::LDS_U4 + 3 * 4 * 4;  // + a scratch row quad per term (the idle lanes' stores)
+  __shared__ uint4 lds[2][BUF];                // double-buffered: chunk c computes while c + 1 is staged
+  __shared__ int tbl[2][32];                   // per chunk: each pixel's window origin in x
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, r = lane & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int kh = (int)(blockIdx.x / splits), split = (int)(blockIdx.x % splits);
   const int P = (int)(n * PIX);  // < 2^31: checked on the host
   const int chunks = (P + 31) / 32;
   const int c0 = (int)((int64_t)chunks * split / splits), c1 = (int)((int64_t)chunks * (split + 1) / splits);
   if (c0 >= c1) {  // an empty split still owns its partial
-    float *out = part + (int64_t)split * COUT * K;
-    for (int e = tid; e < COUT * G::NCOL; e += 256) out[(int64_t)(e / G::NCOL) * K + kh * G::NCOL + e % G::NCOL] = 0.f;
+    float *out = part + (int64_t)split * COUT * K + kh * G::NCOL;
+    for (int e = tid; e < COUT * G::NCOL; e += 256) out[(int64_t)(e / G::NCOL) * K + e % G::NCOL] = 0.f;
     return;
   }
-  // staging role: gy (tid < 64: channel quad, pixel group), x (column quad, pixel group), idle
-  const bool is_gy = tid < 64, is_x = tid >= 64 && tid < 64 + 4 * G::XQ;
-  const int u = is_gy ? tid : tid - 64;
+  // staging role, wave-uniform: wave 0 gy (channel quad, pixel group), the next waves the im2col
+  // x (column quad, pixel group); lanes past the x tasks repeat one and store into the scratch rows
+  const bool is_gy = wave == 0;
+  const int u = is_gy ? tid : (tid - 64) % (4 * G::XQ);
   const int quad = is_gy ? (u & 15) : (u % G::XQ), spg = is_gy ? (u >> 4) : (u / G::XQ);
-  const int qcol = 4 * quad;                         // first row of the quad (channel or column)
+  const int qcol = 4 * quad;
   const int xoff = (kh * WIN + qcol / CIN) * CIN + qcol % CIN;  // (kh, kw, ci0) inside the window
-  const int row0 = is_gy ? qcol : COUT + qcol;
-  // gy through a buffer resource: a pixel past P reads zeros (and weighs 0 against any x)
+  const int row0 = is_gy ? qcol : (tid - 64 < 4 * G::XQ ? COUT + qcol : ROWS);
+  // both operands through buffer resources: a gy pixel past P reads zeros (and weighs 0)
   const __amdgpu_buffer_rsrc_t gy_rsrc =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(gy), 0, P * COUT * 4, 0x00020000);
-  auto make_tbl = [&](int c) {  // 32 threads: the window origin of the chunk's pixels
-    if (tid >= 32) return;
-    const int p = c * 32 + tid;
-    int v = 0;  // a dead pixel reads x's first window (finite) against gy = 0
-    if (p < P) {
-      const int b = p / PIX, pp = p - b * PIX, oy = pp / WOUT, ox = pp - oy * WOUT;
-      v = ((b * HIN + S * oy) * WIN + S * ox) * CIN;
-    }
-    tbl[c & 1][tid] = v;
+  const __amdgpu_buffer_rsrc_t x_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float *>(x), 0, (int)(n * (int64_t)(HIN * WIN * CIN) * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t src_rsrc = is_gy ? gy_rsrc : x_rsrc;  // wave-uniform: one load per element
+  auto make_tbl = [&](int c) __attribute__((always_inline)) {  // every lane writes its pixel's entry (lanes 32 apart agree)
+    const int p = c * 32 + (tid & 31);
+    const int b = p / PIX, pp = p - b * PIX, oy = pp / WOUT, ox = pp - oy * WOUT;
+    tbl[c & 1][tid & 31] = p < P ? ((b * HIN + S * oy) * WIN + S * ox) * CIN : 0;  // dead: x's first window
   };
-  float4 pre[8];
-  auto load = [&](int c) {
-    if (is_gy) {
+  auto load = [&](int c, f32x4 (&pv)[8]) __attribute__((always_inline)) {
+    const int4 *t4 = reinterpret_cast<const int4 *>(&tbl[c & 1][8 * spg]);
+    const int4 ta = t4[0], tb = t4[1];
+    const int o[8] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y, tb.z, tb.w};
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const uint32_t off = (uint32_t)(((c * 32 + 8 * spg + j) * COUT + qcol) * 4);
-        pre[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(gy_rsrc, off, 0, 0));
-      }
-    } else if (is_x) {
-      const int4 *t4 = reinterpret_cast<const int4 *>(&tbl[c & 1][8 * spg]);
-      const int4 ta = t4[0], tb = t4[1];
-      const int o[8] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y, tb.z, tb.w};
-#pragma unroll
-      for (int j = 0; j < 8; ++j) pre[j] = *reinterpret_cast<const float4 *>(x + o[j] + xoff);
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t og = (uint32_t)(((c * 32 + 8 * spg + j) * COUT + qcol) * 4);
+      const uint32_t ox4 = (uint32_t)((o[j] + xoff) * 4);
+      pv[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(src_rsrc, is_gy ? og : ox4, 0, 0));
     }
   };
-  auto stage = [&]() {  // split the 4 rows x 8 pixels held in pre into LDS
-    if (!is_gy && !is_x) return;
+  auto stage_row = [&](const f32x4 (&pv)[8], auto ec, uint4 *buf) __attribute__((always_inline)) {  // row e of the quad
+    constexpr int e = decltype(ec)::value;
+    // (clang vectors, not HIP's float4: its union members kept these registers in private memory)
+    const float v[8] = {pv[0][e], pv[1][e], pv[2][e], pv[3][e], pv[4][e], pv[5][e], pv[6][e], pv[7][e]};
+    bf16x8 tr[3];
+    split3_pk8(v, tr);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float v[8] = {pre[0][e], pre[1][e], pre[2][e], pre[3][e], pre[4][e], pre[5][e], pre[6][e], pre[7][e]};
-      bf16x8 tr[3];
-      split3_pk8(v, tr);
-#pragma unroll
-      for (int t = 0; t < 3; ++t) lds[wgx_unit<ROWS>(t, row0 + e, spg)] = __builtin_bit_cast(uint4, tr[t]);
-    }
+    for (int t = 0; t < 3; ++t) buf[wgx_unit<ROWS + 4>(t, row0 + e, spg)] = __builtin_bit_cast(uint4, tr[t]);
   };
   f32x4 acc[4][CPW];
 #pragma unroll
   for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
     for (int kb = 0; kb < CPW; ++kb) acc[cb][kb] = f32x4{0.f, 0.f, 0.f, 0.f};
-  make_tbl(c0);
-  __syncthreads();
-  load(c0);
-  if (c0 + 1 < c1) make_tbl(c0 + 1);
-  for (int c = c0; c < c1; ++c) {
-    stage();  // chunk c (its loads waited on here)
-    __syncthreads();
-    if (c + 1 < c1) load(c + 1);  // in flight during chunk c's MFMAs
+  // chunk c: its MFMAs from lds[(c - c0) & 1], chunk c + 1's rows (registers ps, loaded one
+  // iteration earlier) staged into the other buffer between the channel blocks' MFMAs, chunk
+  // c + 2's loads into pl; one barrier per chunk
+  auto iter = [&](int c, f32x4 (&ps)[8], f32x4 (&pl)[8]) __attribute__((always_inline)) {
+    load(c + 2, pl);
+    const uint4 *cur = lds[(c - c0) & 1];
+    uint4 *nxt = lds[(c - c0 + 1) & 1];
     bf16x8 bfr[CPW][3];
 #pragma unroll
     for (int kb = 0; kb < CPW; ++kb)
 #pragma unroll
       for (int t = 0; t < 3; ++t)
-        bfr[kb][t] = __builtin_bit_cast(bf16x8, lds[wgx_unit<ROWS>(t, COUT + 16 * (wave * CPW + kb) + r, g)]);
-#pragma unroll
-    for (int cb = 0; cb < 4; ++cb) {
+        bfr[kb][t] = __builtin_bit_cast(bf16x8, cur[wgx_unit<ROWS + 4>(t, COUT + 16 * (wave * CPW + kb) + r, g)]);
+    // the 4 channel blocks as compile-time steps (a runtime cb would index acc / ps dynamically:
+    // private memory)
+    auto cbstep = [&](auto cbc, const f32x4 (&pst)[8]) __attribute__((always_inline)) {
+      constexpr int cb = decltype(cbc)::value;
       bf16x8 af[3];
 #pragma unroll
-      for (int t = 0; t < 3; ++t) af[t] = __builtin_bit_cast(bf16x8, lds[wgx_unit<ROWS>(t, 16 * cb + r, g)]);
+      for (int t = 0; t < 3; ++t) af[t] = __builtin_bit_cast(bf16x8, cur[wgx_unit<ROWS + 4>(t, 16 * cb + r, g)]);
 #pragma unroll
       for (int kb = 0; kb < CPW; ++kb) {
         f32x4 a = acc[cb][kb];
@@ -357,10 +354,33 @@ __global__ __launch_bounds__(256) void k_conv_wgrad_x9(const float *__restrict__
         a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], b[0], a, 0, 0, 0);
         acc[cb][kb] = a;
       }
-    }
-    if (c + 2 < c1) make_tbl(c + 2);  // its buffer was last read by load(c)
-    __syncthreads();  // chunk c's fragments read: the LDS rows may be restaged
+      stage_row(pst, cbc, nxt);  // (past c1 - 1: staged into a buffer nobody reads)
+    };
+    cbstep(std::integral_constant<int, 0>{}, ps);
+    cbstep(std::integral_constant<int, 1>{}, ps);
+    cbstep(std::integral_constant<int, 2>{}, ps);
+    cbstep(std::integral_constant<int, 3>{}, ps);
+    make_tbl(c + 3);  // its buffer was last read by load(c + 1)
+    __syncthreads();
+  };
+  f32x4 pa[8], pb[8];
+  make_tbl(c0);
+  make_tbl(c0 + 1);
+  __syncthreads();
+  load(c0, pa);
+  load(c0 + 1, pb);
+  stage_row(pa, std::integral_constant<int, 0>{}, lds[0]);
+  stage_row(pa, std::integral_constant<int, 1>{}, lds[0]);
+  stage_row(pa, std::integral_constant<int, 2>{}, lds[0]);
+  stage_row(pa, std::integral_constant<int, 3>{}, lds[0]);
+  make_tbl(c0 + 2);
+  __syncthreads();
+  int c = c0;
+  for (; c + 1 < c1; c += 2) {
+    iter(c, pb, pa);
+    iter(c + 1, pa, pb);
   }
+  if (c < c1) iter(c, pb, pa);
   // D: lane holds channels 16 cb + 4 g + i of column 16 (wave * CPW + kb) + r of this kernel row
   float *out = part + (int64_t)split * COUT * K + kh * G::NCOL;
 #pragma unroll

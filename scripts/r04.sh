@@ -65,27 +65,60 @@ for s in "$@"; do
     treet) step tree_tests 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
           tests/test_sumtree_gpu.py tests/test_scale_gpu.py tests/test_samplers_gpu.py tests/test_replay_gpu.py ;;
     treeab) for r in 1 2; do
-        RTH_TREE_LDS_TOP=0 step ab_tree0_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
-        step ab_tree1_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        for v in "notop:RTH_TREE_LDS_TOP=0" "top:RTH_TREE_LDS_TOP=1" "lane1:RTH_FIND_GROUP=0 RTH_FIND_K=1" \
+                 "lane2:RTH_FIND_GROUP=0 RTH_FIND_K=2"; do
+          ( export ${v#*:}; step ab_tree_${v%%:*}_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline \
+              --no-sweep ) || exit $?
+        done
       done
-      for f in gpurun_out/ab_tree*.log; do python - "$f" <<'PY'
+      for f in gpurun_out/ab_tree_*.log; do python - "$f" <<'PY'
 import json, sys
 d = json.loads([l for l in open(sys.argv[1]) if l.startswith('{"metric"')][-1])
 h = {r["kernel"]: r["mean_launch_us"] for r in d["roofline_hbm"]}
 print(sys.argv[1], d["ms_per_step"], "sample_us", h["k_tree_sample"], "update_us", h["k_tree_update_sub"])
 PY
       done ;;
+    treepmc) for v in "notop:RTH_TREE_LDS_TOP=0" "top:RTH_TREE_LDS_TOP=1" "lane1:RTH_FIND_GROUP=0 RTH_FIND_K=1" \
+                      "lane2:RTH_FIND_GROUP=0 RTH_FIND_K=2"; do
+        ( export ${v#*:}; step pmc_tree_${v%%:*} 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv \
+            --kernel-include-regex "k_tree_sample" -d "$PWD/gpurun_out/pmc_tree_${v%%:*}" -o run -- \
+            python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-sweep --settle 16 --probe-steps 0 ) || exit $?
+      done
+      python scripts/summarize_profile.py --tree-pmc gpurun_out/pmc_tree_* | tee gpurun_out/tree_pmc.txt ;;
+    breakprof) step prof_breakout 600 rocprofv3 --kernel-trace --stats --output-format csv \
+          -d "$PWD/gpurun_out/prof_bo" -o run -- python bench.py --workload breakout --steps 60 --warmup 5 \
+          --no-cpu-baseline --no-sweep --probe-steps 0
+      python scripts/stream_busy.py gpurun_out/prof_bo/run_kernel_trace.csv 60 | tee gpurun_out/breakout_streams.txt ;;
     kbench) step conv_kernel_tests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
           tests/test_conv_gpu.py -k "dgrad or wgrad"
-      step bench_dgrad_x9 300 python scripts/bench_dgrad.py
-      RTH_DGRAD2_F32=1 RTH_DGRAD3_F32=1 step bench_dgrad_f32 300 python scripts/bench_dgrad.py
+      RTH_DGRAD2_X9=1 step conv_kernel_tests_x9d2 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
+          tests/test_conv_gpu.py -k "dgrad"
+      step bench_dgrad_dflt 300 python scripts/bench_dgrad.py
+      RTH_DGRAD3_F32=1 step bench_dgrad_f32 300 python scripts/bench_dgrad.py
+      RTH_DGRAD2_X9=1 step bench_dgrad2_x9 300 python scripts/bench_dgrad.py
       step bench_wgrad 300 python scripts/bench_wgrad_f32.py ;;
     wgxab) for r in 1 2; do
-        step ab_wgmiopen_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep --probe-steps 0
-        RTH_HIP_WGRAD=x9 step ab_wgx9_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep \
+        step ab_wgmiopen_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep \
             --probe-steps 0
+        RTH_HIP_WGRAD=x9 step ab_wgx9_$r 300 python bench.py --steps 300 --warmup 5 \
+            --no-cpu-baseline --no-sweep --probe-steps 0
       done
       grep -h -o '"ms_per_step": [0-9.]*' gpurun_out/ab_wg*.log ;;
+    diagfs) RTH_HIP_WGRAD=x9 step diag_fstore_eager 300 python -u scripts/diag_fstore.py
+      RTH_HIP_WGRAD=x9 step diag_fstore_graph 300 python -u scripts/diag_fstore.py graph ;;
+    d2ab) for r in 1 2; do
+        step ab_d2f32_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep --probe-steps 0
+        RTH_DGRAD2_X9=1 step ab_d2x9_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep \
+            --probe-steps 0
+      done
+      grep -h -o '"ms_per_step": [0-9.]*' gpurun_out/ab_d2*.log ;;
+    boab) for r in 1 2; do
+        step ab_bo_dflt_$r 300 python bench.py --workload breakout --steps 100 --warmup 5 --no-cpu-baseline --no-sweep \
+            --probe-steps 0
+        RTH_ACTOR_COUNTED_FC=1 step ab_bo_cfc_$r 300 python bench.py --workload breakout --steps 100 --warmup 5 \
+            --no-cpu-baseline --no-sweep --probe-steps 0
+      done
+      grep -h -o '"ms_per_step": [0-9.]*' gpurun_out/ab_bo_*.log ;;
     tests) step gpu_tests 1100 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;

@@ -53,7 +53,26 @@ def is_conv(pats, name):
     return any(p in name for p in pats)
 
 
+def tree_pmc(dirs):
+    """--tree-pmc DIR...: k_tree_sample's FETCH_SIZE per dispatch (x2, gfx950) by grid, one line
+    per variant directory (scripts/r04.sh treepmc)"""
+    for d in dirs:
+        p = os.path.join(d, "run_counter_collection.csv")
+        if not os.path.exists(p):
+            print(d, "no counters")
+            continue
+        by = collections.defaultdict(list)
+        for r in csv.DictReader(open(p)):
+            if r["Counter_Name"] == "FETCH_SIZE" and "k_tree_sample" in r["Kernel_Name"]:
+                by[int(r["Grid_Size"])].append(2 * float(r["Counter_Value"]) * 1024)
+        for g, v in sorted(by.items()):
+            print(f"{os.path.basename(d):>16} grid={g:>7d} n={len(v):5d} fetch_MB median={st.median(v) / 1e6:.3f} "
+                  f"min={min(v) / 1e6:.3f} max={max(v) / 1e6:.3f}")
+
+
 def main():
+    if sys.argv[1] == "--tree-pmc":
+        return tree_pmc(sys.argv[2:])
     tag = sys.argv[1]
     arg = lambda k, d: int(sys.argv[sys.argv.index(k) + 1]) if k in sys.argv else d
     steps = arg("--steps", 100)

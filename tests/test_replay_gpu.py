@@ -172,13 +172,16 @@ def test_append_exact_capacity_and_errors(dev):
         reth_buffer.Client("hbm://0/does-not-exist")
 
 
-def test_torch_cuda_loader_sample_ahead_order(dev, orc):
+@pytest.mark.parametrize("beta_spec", ["0.4,1,1000", "exp,0.4,1,1000"])
+def test_torch_cuda_loader_sample_ahead_order(dev, orc, beta_spec):
     """batch k+1 is drawn before batch k's priorities are written back (the sampler's HWM-1
-    PUSH, sampler_loop.py:13-15/36-39), with beta stepped by each update message"""
+    PUSH, sampler_loop.py:13-15/36-39), with beta stepped by each update message; beta from
+    the device Schedule (schedule.py:4-52) in both forms, linear and exp, against the oracle's"""
     from reth_amd import reth_buffer
 
     cap, B = 5000, 128
-    svc, addr = reth_buffer.start_per(cap, B, alpha=0.5, beta="0.4,1,1000", sample_start=B, device=dev, seed=3)
+    svc, addr = reth_buffer.start_per(cap, B, alpha=0.5, beta=beta_spec, sample_start=B, device=dev, seed=3)
+    method = "exp" if beta_spec.startswith("exp") else "linear"
     client, loader = reth_buffer.Client(addr), reth_buffer.TorchCudaLoader(addr, buffer_size=4)
     rng = np.random.default_rng(2)
     ids = np.arange(cap)
@@ -195,7 +198,7 @@ def test_torch_cuda_loader_sample_ahead_order(dev, orc):
         u = np.array([orc.philox_uniform(3, calls, i, orc.STREAM_SAMPLE) for i in range(B)])
         calls += 1
         idx, p = tree.sample(u)
-        beta = 0.4 + (1 - 0.4) * beta_steps / 1000
+        beta = orc.schedule_value(method, 0.4, 1.0, 1000, beta_steps)
         return idx, orc.per_is_weights(p, tree.min(), beta)
 
     for k in range(6):

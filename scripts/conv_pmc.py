@@ -2,7 +2,8 @@
 
 CONV_N (default 1024 = the learner's [s0; s1]) samples; CONV_LAYERS (default "1,2,3,d2")
 picks the launches: 1-3 = the torso forward layers (conv3 writes NCHW as in the learner),
-d2 = conv2's data gradient (rth_conv_dgrad) at CONV_N / 2 samples (the learner's B)."""
+d2 / d3 = conv2's / conv3's data gradient (rth_conv_dgrad), w2 / w3 = their weight gradients
+on rth_conv_wgrad_x9, at CONV_N / 2 samples (the learner's B)."""
 import os
 import sys
 
@@ -42,5 +43,29 @@ if "d2" in layers:
     for _ in range(20):
         _lib.call("rth_conv_dgrad", _lib.ctypes.byref(shp), gy.data_ptr(), B, wt.data_ptr(), gx.data_ptr(),
                   _lib.stream_ptr())
+    torch.cuda.synchronize()
+if "d3" in layers:
+    B = n // 2
+    shp = _lib.ConvShape(0, 64, 9, 9, 64, 3, 3, 1)
+    gy = torch.randn((B, 64, 7, 7), device=dev).contiguous(memory_format=torch.channels_last)
+    wt = (torch.randn((64, 64, 3, 3), device=dev) * 0.05).contiguous(memory_format=torch.channels_last)
+    gx = torch.empty((B, 64, 9, 9), device=dev).contiguous(memory_format=torch.channels_last)
+    for _ in range(20):
+        _lib.call("rth_conv_dgrad", _lib.ctypes.byref(shp), gy.data_ptr(), B, wt.data_ptr(), gx.data_ptr(),
+                  _lib.stream_ptr())
+    torch.cuda.synchronize()
+for tag, (cin, h, cout, k, s) in (("w2", (32, 20, 64, 4, 2)), ("w3", (64, 9, 64, 3, 1))):
+    if tag not in layers:
+        continue
+    B = n // 2
+    ho = (h - k) // s + 1
+    shp = _lib.ConvShape(0, cin, h, h, cout, k, k, s)
+    x = torch.rand((B, cin, h, h), device=dev).contiguous(memory_format=torch.channels_last)
+    gy = torch.randn((B, cout, ho, ho), device=dev).contiguous(memory_format=torch.channels_last)
+    gw = torch.empty((cout, cin, k, k), device=dev).contiguous(memory_format=torch.channels_last)
+    ws = torch.empty(_lib.lib().rth_conv_wgrad_x9_workspace(_lib.ctypes.byref(shp)) // 4, device=dev)
+    for _ in range(20):
+        _lib.call("rth_conv_wgrad_x9", _lib.ctypes.byref(shp), x.data_ptr(), B, gy.data_ptr(), gw.data_ptr(),
+                  ws.data_ptr(), _lib.stream_ptr())
     torch.cuda.synchronize()
 print("ok")

@@ -119,6 +119,27 @@ PY
             --no-cpu-baseline --no-sweep --probe-steps 0
       done
       grep -h -o '"ms_per_step": [0-9.]*' gpurun_out/ab_bo_*.log ;;
+    bwdpmc) for ps in "sq:SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT" \
+                 "inst:GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES SQ_LDS_IDX_ACTIVE" \
+                 "fetch:FETCH_SIZE" "write:WRITE_SIZE"; do
+        CONV_LAYERS=d2,d3,w2,w3 step pmc_bwd_${ps%%:*} 120 rocprofv3 --pmc ${ps#*:} --kernel-trace --output-format csv \
+            -d "$PWD/gpurun_out/pmc_bwd_${ps%%:*}" -o run -- python scripts/conv_pmc.py
+      done
+      python scripts/summarize_conv_pmc.py r04 | tail -40 ;;
+    final1) step bench_final 600 python bench.py
+      RTH_BENCH_SPAN=1 step span 300 python bench.py --steps 300 --warmup 20 --no-cpu-baseline --no-sweep
+      step bench_breakout_final 600 python bench.py --workload breakout --frame-store --steps 100 --warmup 10 \
+          --no-cpu-baseline --no-sweep
+      step bench_breakout_full 600 python bench.py --workload breakout --steps 100 --warmup 10 --no-cpu-baseline \
+          --no-sweep ;;
+    final2) step rocprof_stats 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/prof" \
+          -o run -- python bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-sweep
+      step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv --kernel-include-regex "rth::" \
+          -d "$PWD/gpurun_out/pmc_fetch" -o run -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-sweep
+      step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv --kernel-include-regex "rth::" \
+          -d "$PWD/gpurun_out/pmc_write" -o run -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-sweep ;;
+    final3) step bench_atari 600 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-sweep --env atari
+      step bench_atari_h2d 600 python bench.py --steps 50 --warmup 10 --no-cpu-baseline --no-sweep --env atari-h2d ;;
     tests) step gpu_tests 1100 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;

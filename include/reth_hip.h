@@ -505,6 +505,15 @@ int rth_conv_bias_relu_upto(const rth_conv_shape *shape, const void *x_dev, cons
 int rth_conv_dgrad_supported(const rth_conv_shape *shape);
 int rth_conv_dgrad(const rth_conv_shape *shape, const float *gy_dev, int64_t n, const float *w_ohwi_dev,
                    float *gx_dev, void *stream);
+/* The same with a caller-owned workspace for the flipped kernel the exact-split path packs
+ * each launch (rth_conv_dgrad_workspace bytes, 16-byte aligned; 0 bytes: none needed).
+ * rth_conv_dgrad uses one internal workspace per device, so two learners in one process whose
+ * backward passes run on different streams (or are replayed from different graphs) must each
+ * pass their own: the pack and the convolution of one call are stream-ordered, two calls on
+ * two streams are not. */
+int64_t rth_conv_dgrad_workspace(const rth_conv_shape *shape);
+int rth_conv_dgrad_ws(const rth_conv_shape *shape, const float *gy_dev, int64_t n, const float *w_ohwi_dev,
+                      float *gx_dev, void *workspace_dev, void *stream);
 /* Weight gradient of conv2d(x, w) for the fp32 channels-last layers (conv2 and conv3 of the
  * torso; the backward of dqn_model.py:14-20 under dqn_solver.py:117 loss.backward(); replaces
  * MIOpen's weight-gradient solver and its zero fill): gw [cout, kh, kw, cin] (OHWI, the

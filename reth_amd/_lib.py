@@ -173,6 +173,8 @@ SIGNATURES = {
     "rth_conv_bias_relu_upto": (c_i32, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "rth_conv_dgrad_supported": (c_i32, [ctypes.POINTER(ConvShape)]),
     "rth_conv_dgrad": (c_i32, [ctypes.POINTER(ConvShape), c_vp, c_i64, c_vp, c_vp, c_vp]),
+    "rth_conv_dgrad_workspace": (c_i64, [ctypes.POINTER(ConvShape)]),
+    "rth_conv_dgrad_ws": (c_i32, [ctypes.POINTER(ConvShape), c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "rth_atari_create": (c_i32, [c_i32, c_i32, c_i32, c_i32, c_i32, ctypes.POINTER(c_vp)]),
     "rth_atari_destroy": (c_i32, [c_vp]),
     "rth_atari_step": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),

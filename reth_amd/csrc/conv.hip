@@ -1611,11 +1611,12 @@ static int launch_dgrad_x9(const void *fn, const float *gy, int64_t n, int64_t n
   return RTH_OK;
 }
 
-static int conv_dgrad_x9_conv3(const float *gy, int64_t n, const float *w, float *gx, hipStream_t st) {
+static int conv_dgrad_x9_conv3(const float *gy, int64_t n, const float *w, float *gx, void *user_ws, hipStream_t st) {
   static u32x4 *ws[64] = {};
   constexpr int PK = X9Dgrad3<1>::PACKED_U4;
-  u32x4 *wpk = nullptr;
-  if (const int rc = dgrad_workspace(ws, (size_t)PK * 16, st, &wpk)) return rc;
+  u32x4 *wpk = static_cast<u32x4 *>(user_ws);
+  if (!wpk)
+    if (const int rc = dgrad_workspace(ws, (size_t)PK * 16, st, &wpk)) return rc;
   RTH_REQUIRE(n * 49 * 64 * 4 < ((int64_t)1 << 31), "rth_conv_dgrad: gy of %lld samples exceeds 2 GiB", (long long)n);
   hipLaunchKernelGGL((k_conv_pack_x9_dgrad<3, 3, 64, 64, 11, 11, 1, 3, X9_DGRAD3_KS>), dim3((PK + 255) / 256),
                      dim3(256), 0, st, w, wpk);
@@ -1629,11 +1630,12 @@ static int conv_dgrad_x9_conv3(const float *gy, int64_t n, const float *w, float
 
 // conv2: gy [n, 9, 9, 64] -> gx [n, 20, 20, 32]; each class reads gy padded to 11 x 11 and
 // writes its 10 x 10 pixels
-static int conv_dgrad_x9_conv2(const float *gy, int64_t n, const float *w, float *gx, hipStream_t st) {
+static int conv_dgrad_x9_conv2(const float *gy, int64_t n, const float *w, float *gx, void *user_ws, hipStream_t st) {
   static u32x4 *ws[64] = {};
   constexpr int PK = X9Dgrad2<1>::PACKED_U4;
-  u32x4 *wpk = nullptr;
-  if (const int rc = dgrad_workspace(ws, (size_t)4 * PK * 16, st, &wpk)) return rc;
+  u32x4 *wpk = static_cast<u32x4 *>(user_ws);
+  if (!wpk)
+    if (const int rc = dgrad_workspace(ws, (size_t)4 * PK * 16, st, &wpk)) return rc;
   RTH_REQUIRE(n * 400 * 32 * 4 < ((int64_t)1 << 31), "rth_conv_dgrad: gx of %lld samples exceeds 2 GiB", (long long)n);
   hipLaunchKernelGGL((k_conv_pack_x9_dgrad_cls<32, 64, 1, 3, X9_DGRAD2_KS>), dim3((4 * PK + 255) / 256), dim3(256), 0,
                      st, w, wpk);
@@ -1840,23 +1842,43 @@ int rth_conv_dgrad_supported(const rth_conv_shape *shape) {
   return shape && find_dgrad(*shape, &l) ? 1 : 0;
 }
 
+static bool is_dgrad3_x9(const rth_conv_shape *shape) {
+  return dgrad3_x9() && shape->input == RTH_CONV_F32_NHWC && shape->cin == 64 && shape->hin == 9 && shape->win == 9 &&
+         shape->cout == 64 && shape->kh == 3 && shape->kw == 3 && shape->stride == 1;
+}
+static bool is_dgrad2_x9(const rth_conv_shape *shape) {
+  return dgrad2_x9() && shape->input == RTH_CONV_F32_NHWC && shape->cin == 32 && shape->hin == 20 &&
+         shape->win == 20 && shape->cout == 64 && shape->kh == 4 && shape->kw == 4 && shape->stride == 2;
+}
+
+int64_t rth_conv_dgrad_workspace(const rth_conv_shape *shape) {
+  if (!shape) return 0;
+  if (is_dgrad3_x9(shape)) return (int64_t)X9Dgrad3<1>::PACKED_U4 * 16;
+  if (is_dgrad2_x9(shape)) return (int64_t)4 * X9Dgrad2<1>::PACKED_U4 * 16;
+  return 0;
+}
+
 int rth_conv_dgrad(const rth_conv_shape *shape, const float *gy, int64_t n, const float *w, float *gx, void *stream) {
+  return rth_conv_dgrad_ws(shape, gy, n, w, gx, nullptr, stream);
+}
+
+int rth_conv_dgrad_ws(const rth_conv_shape *shape, const float *gy, int64_t n, const float *w, float *gx,
+                      void *workspace, void *stream) {
   RTH_REQUIRE(shape && gy && w && gx && n >= 0, "rth_conv_dgrad: NULL argument");
-  if (dgrad3_x9() && shape->input == RTH_CONV_F32_NHWC && shape->cin == 64 && shape->hin == 9 && shape->win == 9 &&
-      shape->cout == 64 && shape->kh == 3 && shape->kw == 3 && shape->stride == 1) {
+  RTH_REQUIRE((reinterpret_cast<uintptr_t>(workspace) & 15) == 0, "rth_conv_dgrad: misaligned workspace");
+  if (is_dgrad3_x9(shape)) {
     RTH_REQUIRE(((reinterpret_cast<uintptr_t>(gy) | reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(gx)) &
                  15) == 0,
                 "rth_conv_dgrad: misaligned buffer");
     if (n == 0) return RTH_OK;
-    return conv_dgrad_x9_conv3(gy, n, w, gx, as_stream(stream));
+    return conv_dgrad_x9_conv3(gy, n, w, gx, workspace, as_stream(stream));
   }
-  if (dgrad2_x9() && shape->input == RTH_CONV_F32_NHWC && shape->cin == 32 && shape->hin == 20 && shape->win == 20 &&
-      shape->cout == 64 && shape->kh == 4 && shape->kw == 4 && shape->stride == 2) {
+  if (is_dgrad2_x9(shape)) {
     RTH_REQUIRE(((reinterpret_cast<uintptr_t>(gy) | reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(gx)) &
                  15) == 0,
                 "rth_conv_dgrad: misaligned buffer");
     if (n == 0) return RTH_OK;
-    return conv_dgrad_x9_conv2(gy, n, w, gx, as_stream(stream));
+    return conv_dgrad_x9_conv2(gy, n, w, gx, workspace, as_stream(stream));
   }
   DgradLaunch l;
   RTH_REQUIRE(find_dgrad(*shape, &l), "rth_conv_dgrad: geometry (%d x %d x %d -> %d, k %dx%d, stride %d) not built",

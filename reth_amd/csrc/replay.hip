@@ -212,9 +212,13 @@ __global__ __launch_bounds__(kCopyThreads) void k_copy_rows(CopyArgs a) {
   if (col.conv == CONV_STACK) {  // 16-byte vectors of the stack, each from its frame in the store
     const int32_t *ids = reinterpret_cast<const int32_t *>(src);
     const int64_t off = o + 16 * tid;
-    if (off + 16 <= nb) {
-      const int64_t f = off / col.frame_bytes, in = off - f * col.frame_bytes;
-      const int64_t fid = (int64_t)(uint32_t)ids[f] % col.fcap;
+    if (off + 16 <= nb) {  // 32-bit index math (a stack row is < 2^31 bytes)
+      const uint32_t o32 = (uint32_t)off, fb = (uint32_t)col.frame_bytes;
+      const uint32_t f = o32 / fb, in = o32 - f * fb;
+      // ids are in [0, fcap) by construction (k_frames_push writes them reduced); an id out of
+      // range reads frame 0 rather than past the store
+      const uint32_t id = (uint32_t)ids[f];
+      const int64_t fid = id < (uint64_t)col.fcap ? (int64_t)id : 0;
       *reinterpret_cast<uint4 *>(dst + off) = *reinterpret_cast<const uint4 *>(col.fstore + fid * col.frame_bytes + in);
     }
     return;

@@ -1147,16 +1147,20 @@ int tree_sample_impl(rth_sumtree *t, int64_t batch, const double *uniforms, uint
                      uint64_t counter, int is_weights, double beta, int64_t *idx_out, double *out,
                      hipStream_t s, const ReplayState *st, const rth_schedule *beta_s) {
   if (batch <= 0) return RTH_OK;
-  const int gk = find_group_k();
-  // RTH_TREE_LDS_TOP=0: no LDS-staged top (A/B); staged, the workgroups are 256 lanes (16
-  // targets): fewer copies of the staged levels
-  static const int lds_top = env_int("RTH_TREE_LDS_TOP", 1);
-  const int top = lds_top ? 1 : 0;
+  // RTH_TREE_LDS_TOP=0: no LDS-staged top (the r03 form, A/B); staged, the workgroups are 256
+  // lanes: fewer copies of the staged levels.  Below the staged top the default is the
+  // one-lane walk, one child pair per level (RTH_FIND_K=1): 0.66 MB of HBM per Pong launch
+  // against 1.47 with the 16-lane grouped walk (the r03 default, 1.33 without the top) and
+  // 0.570-0.573 vs 0.573-0.580 ms/step in the loop (r04, interleaved); RTH_FIND_GROUP /
+  // RTH_FIND_K select the others
+  const int top = env_int("RTH_TREE_LDS_TOP", 1) ? 1 : 0;  // read per call: tests switch it
+  const int gk = (top && !getenv("RTH_FIND_GROUP")) ? 0 : find_group_k();
+  const int kspec = (top && !getenv("RTH_FIND_K")) ? 1 : find_k();
   const int bs = top ? 256 : sample_bs();
   const int64_t lanes = batch << gk;
   hipLaunchKernelGGL(k_tree_sample, dim3((unsigned)((lanes + bs - 1) / bs)), dim3(bs), 0, s, t->nodes,
                      t->cap, batch, uniforms, seed, counter, is_weights, beta, st,
-                     beta_s ? *beta_s : rth_schedule{}, idx_out, out, find_k(), gk, top);
+                     beta_s ? *beta_s : rth_schedule{}, idx_out, out, kspec, gk, top);
   RTH_LAUNCHED();
   return RTH_OK;
 }

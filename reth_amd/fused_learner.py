@@ -46,15 +46,21 @@ if os.environ.get("RTH_MIOPEN_DGRAD3") is None and os.environ.get("RTH_MIOPEN_DG
 # or =f32 / =1 (rth_conv_wgrad_f32, fp32 MFMA: 44-47 vs 38 us alone for conv2)
 _wg = os.environ.get("RTH_HIP_WGRAD")
 HIP_WGRAD = None if not _wg else ("x9" if _wg == "x9" else "f32")
-_WGF_WS = {}
 
 
-def _wgrad_f32_workspace(shape, device, kind="f32"):
-    key = (device, kind, shape.cin, shape.hin, shape.cout)
-    ws = _WGF_WS.get(key)
+def _net_workspace(net, kind, shape, device):
+    """a backward kernel's workspace, owned by the network: two learners in one process may
+    run (or replay) their backward passes on different streams, so no workspace is shared
+    between them -- rth_conv_dgrad_ws's packed flipped kernel, rth_conv_wgrad_{f32,x9}'s
+    split partials, rth_conv_relu_wgrad's conv1 partials"""
+    cache = net.__dict__.setdefault("_bwd_ws", {})
+    key = (device, kind, shape.input, shape.cin, shape.hin, shape.cout)
+    ws = cache.get(key)
     if ws is None:
-        size = getattr(_lib.lib(), f"rth_conv_wgrad_{kind}_workspace")(ctypes.byref(shape))
-        ws = _WGF_WS[key] = torch.empty(size // 4, dtype=torch.float32, device=device)
+        fn = {"dgrad": "rth_conv_dgrad_workspace", "conv1": "rth_conv_wgrad_workspace"}.get(
+            kind, f"rth_conv_wgrad_{kind}_workspace")
+        size = getattr(_lib.lib(), fn)(ctypes.byref(shape))
+        ws = cache[key] = torch.empty(max(size, 16) // 4, dtype=torch.float32, device=device)
     return ws
 
 
@@ -197,15 +203,14 @@ def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None, mid=No
             conv, y = convs[li], ys[li][:B]
             if li == 0 and u8:  # ReLU mask + weight/bias gradients from the stacks, and the
                 # deferred conv3 / conv2 bias gradients in the same reduce launch
-                from .model import _wgrad_workspace
-
                 gw = torch.empty(conv.weight.shape, dtype=torch.float32, device=x.device,
                                  memory_format=torch.channels_last)
                 db = torch.empty(conv.out_channels, dtype=torch.float32, device=x.device)
                 assert len(deferred) <= 4, "rth_conv_relu_wgrad_ex finishes at most 4 deferred bias gradients"
                 jobs = (_lib.BiasDeferred * max(len(deferred), 1))(*deferred)
                 call("rth_conv_relu_wgrad_ex", ctypes.byref(shapes[0]), ptr(x), None, B, ptr(_nhwc(g)), ptr(y),
-                     ptr(gw), ptr(db), ptr(_wgrad_workspace(shapes[0], x.device)), jobs, len(deferred), st)
+                     ptr(gw), ptr(db), ptr(_net_workspace(net, "conv1", shapes[0], x.device)), jobs, len(deferred),
+                     st)
                 grads[conv.weight], grads[conv.bias] = gw, db
                 deferred = []  # consumed
                 break
@@ -236,10 +241,11 @@ def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None, mid=No
                 gw = torch.empty(conv.weight.shape, dtype=torch.float32, device=x.device,
                                  memory_format=torch.channels_last)
                 call(f"rth_conv_wgrad_{HIP_WGRAD}", ctypes.byref(shapes[li]), ptr(xin), B, ptr(gy), ptr(gw),
-                     ptr(_wgrad_f32_workspace(shapes[li], x.device, HIP_WGRAD)), st)
+                     ptr(_net_workspace(net, HIP_WGRAD, shapes[li], x.device)), st)
             if hip_dgrad:  # data gradient in rth_conv_dgrad (no zero fill)
                 gx = torch.empty(xin.shape, dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
-                call("rth_conv_dgrad", ctypes.byref(shapes[li]), ptr(gy), B, ptr(w), ptr(gx), st)
+                call("rth_conv_dgrad_ws", ctypes.byref(shapes[li]), ptr(gy), B, ptr(w), ptr(gx),
+                     ptr(_net_workspace(net, "dgrad", shapes[li], x.device)), st)
             grads[conv.weight], grads[conv.bias] = gw, db
             g = gx
         # every deferred bias gradient was finished by conv1's launch (else its db would be

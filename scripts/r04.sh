@@ -140,6 +140,14 @@ PY
           -d "$PWD/gpurun_out/pmc_write" -o run -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-sweep ;;
     final3) step bench_atari 600 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-sweep --env atari
       step bench_atari_h2d 600 python bench.py --steps 50 --warmup 10 --no-cpu-baseline --no-sweep --env atari-h2d ;;
+    wgxab2) for r in 1 2; do
+        step ab_w2base_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep --probe-steps 0
+        for sp in 16 32 128; do
+          RTH_HIP_WGRAD=x9 RTH_WGX_SPLITS=$sp step ab_w2s${sp}_$r 300 python bench.py --steps 300 --warmup 5 \
+              --no-cpu-baseline --no-sweep --probe-steps 0
+        done
+      done
+      grep -H -o '"ms_per_step": [0-9.]*' gpurun_out/ab_w2*.log ;;
     tests) step gpu_tests 1100 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;

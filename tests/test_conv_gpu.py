@@ -331,6 +331,43 @@ def test_conv_dgrad(dev, gi, n):
         assert err <= 2e-6 * max(1.0, want.abs().max().item()), err
 
 
+@pytest.mark.parametrize("gi", [1, 2])
+def test_conv_dgrad_ws_two_streams(dev, gi):
+    """rth_conv_dgrad_ws: two data gradients with different weights, each with its own
+    workspace, issued on two streams repeatedly -- each bit-identical to its single-stream
+    result (the internal per-device workspace of rth_conv_dgrad would be shared by them)"""
+    from reth_amd import _lib
+
+    cin, h, wd, cout, k, s = GEOMS[gi]
+    shape = _shape(_lib.CONV_F32_NHWC, *GEOMS[gi])
+    n, ho = 256, (h - k) // s + 1
+    g = torch.Generator(device=dev).manual_seed(5 + gi)
+    gys = [torch.randn((n, cout, ho, ho), device=dev, generator=g).contiguous(memory_format=torch.channels_last)
+           for _ in range(2)]
+    ws_ = [(torch.randn((cout, cin, k, k), device=dev, generator=g) * 0.05).contiguous(
+        memory_format=torch.channels_last) for _ in range(2)]
+    nbytes = _lib.lib().rth_conv_dgrad_workspace(_lib.ctypes.byref(shape))
+    work = [torch.empty(max(nbytes, 16) // 4, device=dev) for _ in range(2)]
+    want = []
+    for j in range(2):
+        gx = torch.empty((n, cin, h, wd), device=dev).contiguous(memory_format=torch.channels_last)
+        _lib.call("rth_conv_dgrad_ws", _lib.ctypes.byref(shape), gys[j].data_ptr(), n, ws_[j].data_ptr(),
+                  gx.data_ptr(), work[j].data_ptr(), _lib.stream_ptr())
+        want.append(gx)
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(dev) for _ in range(2)]
+    outs = [[torch.empty_like(want[j]) for _ in range(8)] for j in range(2)]
+    for it in range(8):
+        for j in range(2):
+            with torch.cuda.stream(streams[j]):
+                _lib.call("rth_conv_dgrad_ws", _lib.ctypes.byref(shape), gys[j].data_ptr(), n, ws_[j].data_ptr(),
+                          outs[j][it].data_ptr(), work[j].data_ptr(), _lib.stream_ptr())
+    torch.cuda.synchronize()
+    for j in range(2):
+        for o in outs[j]:
+            assert torch.equal(o, want[j])
+
+
 def test_conv_dgrad_unsupported(dev):
     from reth_amd import _lib
 

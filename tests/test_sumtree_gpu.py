@@ -204,14 +204,21 @@ def test_per_distribution(dev):
     check(w)
 
 
-@pytest.mark.parametrize("gk", ["0", "3", "4", "5"])
-def test_find_lane_groups(dev, orc, golden, monkeypatch, gk):
+@pytest.mark.parametrize("top", ["0", "1"])
+@pytest.mark.parametrize("gk", ["", "0", "3", "4", "5"])
+def test_find_lane_groups(dev, orc, golden, monkeypatch, gk, top):
     """the walk with one lane per target (RTH_FIND_GROUP=0) and with lane groups of 2^3 /
-    2^4 / 2^5 (several levels per round trip, one pair per lane) returns the oracle's
-    indices: ragged trees, zeros, targets at and past the total, the golden small trees"""
+    2^4 / 2^5 (several levels per round trip, one pair per lane), the sampler's with and
+    without the LDS-staged top levels ("" = the default: staged top, one-lane walk below),
+    returns the oracle's indices: ragged trees, zeros, targets at and past the total, the
+    golden small trees"""
     from reth_amd.replay import SumTree
 
-    monkeypatch.setenv("RTH_FIND_GROUP", gk)
+    if gk:
+        monkeypatch.setenv("RTH_FIND_GROUP", gk)
+    else:
+        monkeypatch.delenv("RTH_FIND_GROUP", raising=False)
+    monkeypatch.setenv("RTH_TREE_LDS_TOP", top)
     rng = np.random.default_rng(77)
     for cap in (1, 2, 3, 7, 31, 33, 1000, 65537, 300000):
         t = SumTree(cap, dev)

@@ -448,6 +448,7 @@ struct X9Geom {
   static constexpr int ROTV = ROT & 15, SHV = ((ROT >> 4) & 15) ? ((ROT >> 4) & 15) : 5;
   static constexpr int PADV = (ROT >> 8) ? (ROT >> 8) : (ROT == 10 ? 1 : 0);
   static constexpr int PLANE = (ROWS + 15) / 16 * 16 + PADV;  // 16-B units per (term, cg)
+  static_assert(SHV >= 4, "the rotation must be constant over each aligned 16-row block (a permutation)");
   static constexpr int LDS_U4 = 3 * NG * PLANE;                          // LDS in 16-B units
   static constexpr int OUT_F = NSAMP * COUT * PIX;                       // output staging floats
   static constexpr int PACKED_U4 = (COUT / 16) * NCH * 3 * 64;           // packed weight fragments
@@ -1552,19 +1553,6 @@ using namespace rth;
 #ifndef X9_DGRAD2_KS
 #define X9_DGRAD2_KS 2
 #endif
-// LDS swizzles of the data-gradient images (scripts/x9_lds_sim.py, the kernels' ds_read_b128
-// lane groups over their staged rows): conv3 rotation 10 every 8 rows + 8 pad units (1.72-1.83
-// cycles per lane group vs 1.96-1.99 for rotation 3 every 32), conv2's classes rotation 11 (1.46-
-// 1.73 vs 2.00); RTH_DGRAD_SWZ=0: rotation 3 (A/B)
-#define X9_DGRAD3_ROT (10 | (3 << 4) | (8 << 8))
-#define X9_DGRAD2_ROT (11 | (3 << 4) | (8 << 8))
-static bool dgrad_swz() {
-  static const bool v = [] {
-    const char *e = getenv("RTH_DGRAD_SWZ");
-    return !(e && atoi(e) == 0);
-  }();
-  return v;
-}
 template <int NS>
 using X9Dgrad3 = X9Geom<3, 3, 1, 64, 11, 11, NS, 3, X9_DGRAD3_KS>;
 template <int NS>
@@ -1639,14 +1627,9 @@ static int conv_dgrad_x9_conv3(const float *gy, int64_t n, const float *w, float
   hipLaunchKernelGGL((k_conv_pack_x9_dgrad<3, 3, 64, 64, 11, 11, 1, 3, X9_DGRAD3_KS>), dim3((PK + 255) / 256),
                      dim3(256), 0, st, w, wpk);
   RTH_LAUNCHED();
-  const void *fs[4] = {
-      nullptr, reinterpret_cast<const void *>(&k_conv_x9<3, 3, 1, 64, 11, 11, 1, X9_DGRAD3_ROT, X9_DGRAD3_KS, 2>),
-      reinterpret_cast<const void *>(&k_conv_x9<3, 3, 1, 64, 11, 11, 2, X9_DGRAD3_ROT, X9_DGRAD3_KS, 2>),
-      reinterpret_cast<const void *>(&k_conv_x9<3, 3, 1, 64, 11, 11, 3, X9_DGRAD3_ROT, X9_DGRAD3_KS, 2>)};
-  const void *f3[4] = {nullptr, reinterpret_cast<const void *>(&k_conv_x9<3, 3, 1, 64, 11, 11, 1, 3, X9_DGRAD3_KS, 2>),
+  const void *fn[4] = {nullptr, reinterpret_cast<const void *>(&k_conv_x9<3, 3, 1, 64, 11, 11, 1, 3, X9_DGRAD3_KS, 2>),
                        reinterpret_cast<const void *>(&k_conv_x9<3, 3, 1, 64, 11, 11, 2, 3, X9_DGRAD3_KS, 2>),
                        reinterpret_cast<const void *>(&k_conv_x9<3, 3, 1, 64, 11, 11, 3, 3, X9_DGRAD3_KS, 2>)};
-  const void *const *fn = dgrad_swz() ? fs : f3;
   const int64_t ns = dgrad_x9_nsamp(n, 1, fn, X9Dgrad3<1>::NT, (int)x9_wg_per_cu());
   return launch_dgrad_x9(fn[ns], gy, n, ns, 1, X9Dgrad3<1>::NT, wpk, gx, st);
 }
@@ -1663,15 +1646,10 @@ static int conv_dgrad_x9_conv2(const float *gy, int64_t n, const float *w, float
   hipLaunchKernelGGL((k_conv_pack_x9_dgrad_cls<32, 64, 1, 3, X9_DGRAD2_KS>), dim3((4 * PK + 255) / 256), dim3(256), 0,
                      st, w, wpk);
   RTH_LAUNCHED();
-  const void *fs[4] = {
-      nullptr, reinterpret_cast<const void *>(&k_conv_x9<2, 2, 1, 64, 11, 11, 1, X9_DGRAD2_ROT, X9_DGRAD2_KS, 1, 32, 1>),
-      reinterpret_cast<const void *>(&k_conv_x9<2, 2, 1, 64, 11, 11, 2, X9_DGRAD2_ROT, X9_DGRAD2_KS, 1, 32, 1>),
-      reinterpret_cast<const void *>(&k_conv_x9<2, 2, 1, 64, 11, 11, 3, X9_DGRAD2_ROT, X9_DGRAD2_KS, 1, 32, 1>)};
-  const void *f3[4] = {
+  const void *fn[4] = {
       nullptr, reinterpret_cast<const void *>(&k_conv_x9<2, 2, 1, 64, 11, 11, 1, 3, X9_DGRAD2_KS, 1, 32, 1>),
       reinterpret_cast<const void *>(&k_conv_x9<2, 2, 1, 64, 11, 11, 2, 3, X9_DGRAD2_KS, 1, 32, 1>),
       reinterpret_cast<const void *>(&k_conv_x9<2, 2, 1, 64, 11, 11, 3, 3, X9_DGRAD2_KS, 1, 32, 1>)};
-  const void *const *fn = dgrad_swz() ? fs : f3;
   // (4 waves per workgroup at COUT = 32: as many resident as the LDS image allows)
   const int64_t ns = dgrad_x9_nsamp(n, 4, fn, X9Dgrad2<1>::NT, 4);
   return launch_dgrad_x9(fn[ns], gy, n, ns, 4, X9Dgrad2<1>::NT, wpk, gx, st);

@@ -148,16 +148,6 @@ PY
         done
       done
       grep -H -o '"ms_per_step": [0-9.]*' gpurun_out/ab_w2*.log ;;
-    swzab) step swz_tests 300 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_conv_gpu.py \
-          -k "dgrad"
-      step bench_dgrad_swz 300 python scripts/bench_dgrad.py
-      RTH_DGRAD_SWZ=0 step bench_dgrad_rot3 300 python scripts/bench_dgrad.py
-      for r in 1 2; do
-        RTH_DGRAD_SWZ=0 step ab_swz0_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep \
-            --probe-steps 0
-        step ab_swz1_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep --probe-steps 0
-      done
-      grep -H -o '"ms_per_step": [0-9.]*' gpurun_out/ab_swz*.log ;;
     gapdiag) for r in 1 2; do
         RTH_BENCH_SPAN=1 step span_$r 300 python bench.py --steps 300 --warmup 20 --no-cpu-baseline --no-sweep \
             --probe-steps 0

@@ -512,6 +512,18 @@ int rth_conv_dgrad(const rth_conv_shape *shape, const float *gy_dev, int64_t n, 
  * pass their own: the pack and the convolution of one call are stream-ordered, two calls on
  * two streams are not. */
 int64_t rth_conv_dgrad_workspace(const rth_conv_shape *shape);
+/* FC1 of the dueling heads (the first Linear + ReLU of both branches, dqn_model.py:38-47, as
+ * one [N, K] weight) on the exact-split bf16 MFMA: y [M, N] = act(x [M, K] w^T + b), x
+ * row-major with row stride ldx, w row-major [N, K] (the Linear weight as stored), act = ReLU
+ * when relu != 0, bias may be NULL; M % 64 == 0, N % 128 == 0, K % 32 == 0
+ * (rth_fc_x9_supported).  Fixed-order split-K partials in `workspace` (rth_fc_x9_workspace
+ * bytes, NULL when that is 0): run-to-run deterministic.  Replaces the hipBLASLt GEMM +
+ * bias + ReLU epilogue (torch._addmm_activation) of the actors', the target pass's and the
+ * learner's forward when enabled (RTH_FC_X9=1). */
+int rth_fc_x9_supported(int64_t M, int64_t N, int64_t K);
+int64_t rth_fc_x9_workspace(int64_t M, int64_t N, int64_t K);
+int rth_fc_x9(const float *x_dev, int64_t ldx, int64_t M, const float *w_dev, int64_t N, int64_t K,
+              const float *bias_dev, int32_t relu, float *y_dev, void *workspace_dev, void *stream);
 int rth_conv_dgrad_ws(const rth_conv_shape *shape, const float *gy_dev, int64_t n, const float *w_ohwi_dev,
                       float *gx_dev, void *workspace_dev, void *stream);
 /* Weight gradient of conv2d(x, w) for the fp32 channels-last layers (conv2 and conv3 of the

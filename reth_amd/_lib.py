@@ -174,6 +174,9 @@ SIGNATURES = {
     "rth_conv_dgrad_supported": (c_i32, [ctypes.POINTER(ConvShape)]),
     "rth_conv_dgrad": (c_i32, [ctypes.POINTER(ConvShape), c_vp, c_i64, c_vp, c_vp, c_vp]),
     "rth_conv_dgrad_workspace": (c_i64, [ctypes.POINTER(ConvShape)]),
+    "rth_fc_x9_supported": (c_i32, [c_i64, c_i64, c_i64]),
+    "rth_fc_x9_workspace": (c_i64, [c_i64, c_i64, c_i64]),
+    "rth_fc_x9": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i32, c_vp, c_vp, c_vp]),
     "rth_conv_dgrad_ws": (c_i32, [ctypes.POINTER(ConvShape), c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "rth_atari_create": (c_i32, [c_i32, c_i32, c_i32, c_i32, c_i32, ctypes.POINTER(c_vp)]),
     "rth_atari_destroy": (c_i32, [c_vp]),

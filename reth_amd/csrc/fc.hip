@@ -1,0 +1,220 @@
+// FC1 of the dueling heads on the bf16 MFMA with both operands split into three exact bf16
+// terms (the x9 scheme of conv.hip's k_conv_x9: every partial product xi * wj has at most 16
+// significant bits, so it is exact in the fp32 accumulator -- the products of an fp32 GEMM,
+// summed in another fixed order).  Reference: the first Linear of both branches of
+// reth/reth/algorithm/dqn/dqn_model.py:38-47 (value / advantage: Linear(3136, 256) + ReLU), run
+// by Worker.step -> act, by _calc_td_error's target pass and by the learner's forward
+// (dqn_solver.py:68-124); here the two branches' weights are one [512, 3136] storage.
+//
+//   y[m][n] = act(b[n] + sum_k x[m][k] w[n][k]),  x [M, K] row-major (row stride ldx),
+//   w [N, K] row-major (a Linear weight), act = ReLU or identity
+//
+// Workgroup = 4 waves over a 64 x 128 output tile (wave w: rows 16 w .. 16 w + 15, all 8
+// 16-column blocks) and a range of 32-deep k chunks (its split).  Per chunk the workgroup stages
+// the 128 weight rows' 32 values split into the three bf16 terms, in fragment order, in LDS
+// (double-buffered: one barrier per chunk); each wave loads and splits its own A fragment
+// (16 rows x 32 values) in registers and runs 8 x 9 MFMAs.  The next chunk's loads are in flight
+// during the MFMAs.  splits > 1: fixed-order partial tiles + k_fc_reduce (bias, activation);
+// every sum has a fixed order, so the result is run-to-run deterministic.
+#include <type_traits>
+
+#include "common.hpp"
+
+namespace rth {
+
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+
+constexpr int kFcTm = 64, kFcTn = 128, kFcThreads = 256;
+__device__ __forceinline__ float fc_relu(float v) { return v < 0.0f ? 0.0f : v; }  // conv.hip's relu_c
+constexpr int kFcBUnits = 8 * 3 * 64;  // 16-byte units of one chunk's split weight tile
+
+__global__ __launch_bounds__(kFcThreads) void k_fc_x9(const float *__restrict__ x, int64_t ldx, int M,
+                                                      const float *__restrict__ w, int N, int K, int splits,
+                                                      const float *__restrict__ bias, int relu,
+                                                      float *__restrict__ out) {
+  __shared__ uint4 bl[2][kFcBUnits];
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, r = lane & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tiles_n = N / kFcTn;
+  const int tile = (int)blockIdx.x / splits, split = (int)blockIdx.x % splits;
+  const int m0 = (tile / tiles_n) * kFcTm, n0 = (tile % tiles_n) * kFcTn;
+  const int chunks = K / 32;
+  const int c0 = chunks * split / splits, c1 = chunks * (split + 1) / splits;
+  // staging role: weight row n0 + (tid & 127), values 16 (tid >> 7) .. +15 of the chunk
+  const int wn = tid & 127, wh = tid >> 7;
+  const float *wrow = w + (int64_t)(n0 + wn) * K + 16 * wh;
+  const float *xrow = x + (int64_t)(m0 + 16 * wave + r) * ldx + 8 * g;
+  f32x4 wv[2][4], xv[2][2];  // chunk loads, double-buffered in registers
+  auto load = [&](int c, f32x4 (&wl)[4], f32x4 (&xl)[2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) wl[j] = *reinterpret_cast<const f32x4 *>(wrow + 32 * c + 4 * j);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) xl[j] = *reinterpret_cast<const f32x4 *>(xrow + 32 * c + 4 * j);
+  };
+  // the thread's 16 values = units (nb, t, lane r' + 16 g') for g' = 2 wh, 2 wh + 1
+  auto stage = [&](const f32x4 (&wl)[4], uint4 *buf) __attribute__((always_inline)) {
+    const int nb = wn >> 4, rr = wn & 15;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float v[8] = {wl[2 * h][0], wl[2 * h][1], wl[2 * h][2], wl[2 * h][3],
+                          wl[2 * h + 1][0], wl[2 * h + 1][1], wl[2 * h + 1][2], wl[2 * h + 1][3]};
+      bf16x8 tr[3];
+      split3_pk8(v, tr);
+#pragma unroll
+      for (int t = 0; t < 3; ++t) buf[(nb * 3 + t) * 64 + rr + 16 * (2 * wh + h)] = __builtin_bit_cast(uint4, tr[t]);
+    }
+  };
+  f32x4 acc[8];
+#pragma unroll
+  for (int nb = 0; nb < 8; ++nb) acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto compute = [&](const f32x4 (&xl)[2], const uint4 *buf) __attribute__((always_inline)) {
+    const float v[8] = {xl[0][0], xl[0][1], xl[0][2], xl[0][3], xl[1][0], xl[1][1], xl[1][2], xl[1][3]};
+    bf16x8 af[3];
+    split3_pk8(v, af);
+#pragma unroll
+    for (int nb = 0; nb < 8; ++nb) {
+      bf16x8 b[3];
+#pragma unroll
+      for (int t = 0; t < 3; ++t) b[t] = __builtin_bit_cast(bf16x8, buf[(nb * 3 + t) * 64 + lane]);
+      f32x4 a = acc[nb];
+      // smallest terms first: (3,3) (3,2) (2,3) (3,1) (2,2) (1,3) (2,1) (1,2) (1,1)
+      a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[2], b[2], a, 0, 0, 0);
+      a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[2], b[1], a, 0, 0, 0);
+      a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], b[2], a, 0, 0, 0);
+      a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[2], b[0], a, 0, 0, 0);
+      a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], b[1], a, 0, 0, 0);
+      a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], b[2], a, 0, 0, 0);
+      a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], b[0], a, 0, 0, 0);
+      a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], b[1], a, 0, 0, 0);
+      a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], b[0], a, 0, 0, 0);
+      acc[nb] = a;
+    }
+  };
+  // chunk c: MFMAs from bl[(c - c0) & 1] with A registers xv[(c - c0) & 1]; chunk c + 1's weight
+  // rows (registers, loaded one chunk earlier) staged into the other buffer; chunk c + 2 loaded
+  // (past c1 - 1 the loads repeat the range's last chunk: in bounds, never used)
+  auto iter = [&](int c, auto pc) __attribute__((always_inline)) {
+    constexpr int p = decltype(pc)::value;  // register / LDS parity of chunk c
+    compute(xv[p], bl[p]);
+    stage(wv[p ^ 1], bl[p ^ 1]);
+    const int cn = c + 2 < c1 ? c + 2 : c1 - 1;
+    load(cn, wv[p], xv[p]);
+    __syncthreads();
+  };
+  // before chunk c (parity p): bl[p] = its split weights, xv[p] = its A values, wv[p ^ 1] /
+  // xv[p ^ 1] = chunk c + 1's loads
+  load(c0, wv[0], xv[0]);
+  load(c0 + 1 < c1 ? c0 + 1 : c0, wv[1], xv[1]);
+  stage(wv[0], bl[0]);
+  __syncthreads();
+  int c = c0;
+  for (; c + 1 < c1; c += 2) {
+    iter(c, std::integral_constant<int, 0>{});
+    iter(c + 1, std::integral_constant<int, 1>{});
+  }
+  if (c < c1) iter(c, std::integral_constant<int, 0>{});
+  // D: lane holds rows 4 g + i of the wave's 16, column r of each 16-column block
+  const int mrow = m0 + 16 * wave + 4 * g;
+  if (splits == 1) {
+#pragma unroll
+    for (int nb = 0; nb < 8; ++nb) {
+      const int n = n0 + 16 * nb + r;
+      const float bn = bias ? bias[n] : 0.0f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float v = radd(acc[nb][i], bn);
+        out[(int64_t)(mrow + i) * N + n] = relu ? fc_relu(v) : v;
+      }
+    }
+  } else {
+    float *part = out + (int64_t)split * M * N;
+#pragma unroll
+    for (int nb = 0; nb < 8; ++nb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) part[(int64_t)(mrow + i) * N + n0 + 16 * nb + r] = acc[nb][i];
+  }
+}
+
+// y = act(b + sum of the splits' partials, in split order), 4 outputs per thread
+__global__ __launch_bounds__(256) void k_fc_reduce(const float *__restrict__ part, int splits, int64_t MN, int N,
+                                                   const float *__restrict__ bias, int relu, float *__restrict__ y,
+                                                   int64_t ldy) {
+  const int64_t e4 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (e4 >= MN) return;
+  f32x4 s = *reinterpret_cast<const f32x4 *>(part + e4);
+  for (int k = 1; k < splits; ++k) {
+    const f32x4 v = *reinterpret_cast<const f32x4 *>(part + (int64_t)k * MN + e4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s[j] = radd(s[j], v[j]);
+  }
+  const int64_t m = e4 / N;
+  const int n = (int)(e4 - m * N);
+  f32x4 o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float v = radd(s[j], bias ? bias[n + j] : 0.0f);
+    o[j] = relu ? fc_relu(v) : v;
+  }
+  *reinterpret_cast<f32x4 *>(y + m * ldy + n) = o;
+}
+
+// k splits: about one workgroup per CU (256) over the output tiles, at most 16 and at most the
+// chunk count; RTH_FC_SPLITS overrides (A/B)
+static int fc_splits(int M, int N, int K) {
+  static const int env = [] {
+    const char *e = getenv("RTH_FC_SPLITS");
+    return e ? atoi(e) : 0;
+  }();
+  const int tiles = (M / kFcTm) * (N / kFcTn), chunks = K / 32;
+  int s = env > 0 ? env : (256 + tiles - 1) / tiles;
+  s = s < 1 ? 1 : (s > 16 ? 16 : s);
+  return s < chunks ? s : chunks;
+}
+
+}  // namespace rth
+
+using namespace rth;
+
+extern "C" {
+
+int rth_fc_x9_supported(int64_t M, int64_t N, int64_t K) {
+  return M > 0 && M % kFcTm == 0 && N > 0 && N % kFcTn == 0 && K >= 32 && K % 32 == 0 && M * K < (1ll << 31) &&
+                 N * K < (1ll << 31)
+             ? 1
+             : 0;
+}
+
+int64_t rth_fc_x9_workspace(int64_t M, int64_t N, int64_t K) {
+  if (!rth_fc_x9_supported(M, N, K)) return 0;
+  const int s = fc_splits((int)M, (int)N, (int)K);
+  return s > 1 ? (int64_t)s * M * N * 4 : 0;
+}
+
+int rth_fc_x9(const float *x, int64_t ldx, int64_t M, const float *w, int64_t N, int64_t K, const float *bias,
+              int32_t relu, float *y, void *workspace, void *stream) {
+  RTH_REQUIRE(x && w && y, "rth_fc_x9: NULL argument");
+  RTH_REQUIRE(rth_fc_x9_supported(M, N, K), "rth_fc_x9: shape %lld x %lld x %lld not built (M %% 64, N %% 128, K %% 32)",
+              (long long)M, (long long)N, (long long)K);
+  RTH_REQUIRE(ldx >= K && ldx % 4 == 0, "rth_fc_x9: row stride %lld", (long long)ldx);
+  RTH_REQUIRE(((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(y)) &
+               15) == 0,
+              "rth_fc_x9: misaligned buffer");
+  const int splits = fc_splits((int)M, (int)N, (int)K);
+  RTH_REQUIRE(splits == 1 || (workspace && (reinterpret_cast<uintptr_t>(workspace) & 15) == 0),
+              "rth_fc_x9: %d splits need the workspace (rth_fc_x9_workspace)", splits);
+  hipStream_t s = as_stream(stream);
+  const int tiles = (int)(M / kFcTm) * (int)(N / kFcTn);
+  float *out = splits == 1 ? y : static_cast<float *>(workspace);
+  hipLaunchKernelGGL(k_fc_x9, dim3((unsigned)(tiles * splits)), dim3(kFcThreads), 0, s, x, ldx, (int)M, w, (int)N,
+                     (int)K, splits, bias, (int)relu, out);
+  RTH_LAUNCHED();
+  if (splits > 1) {
+    const int64_t MN = M * N;
+    hipLaunchKernelGGL(k_fc_reduce, dim3((unsigned)((MN / 4 + 255) / 256)), dim3(256), 0, s,
+                       static_cast<const float *>(workspace), splits, MN, (int)N, bias, (int)relu, y, N);
+    RTH_LAUNCHED();
+  }
+  return RTH_OK;
+}
+
+}  // extern "C"

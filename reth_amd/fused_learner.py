@@ -29,7 +29,7 @@ import torch
 
 from . import _lib
 from ._lib import call, ctypes, ptr, stream_ptr
-from .model import nchw_out
+from .model import fc1_relu, nchw_out
 
 
 TD_HB_MAX = 16384  # rth_td_heads_backward keeps B * (A + 1) TD gradient rows in LDS
@@ -147,7 +147,7 @@ def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None, mid=No
             ys.append(y)
             h = y
         feat = h.view(n, -1)  # the (C, H, W) flatten of the NCHW output: a view
-        h1 = torch._addmm_activation(b1, feat, w1.t())
+        h1 = fc1_relu(feat, w1, b1)
         heads = net._heads_fc2(h1) if w2 is None else torch.addmm(b2, h1, w2.t())
         if q1t is None:
             q1t = solver.target_heads(s1)

@@ -6,6 +6,8 @@ reth/reth/algorithm/dqn/dqn_model.py:6-71, so
     with the reference's, and
   * under the same torch.manual_seed the default initialisation is identical.
 """
+import os
+
 import torch
 from torch import nn
 
@@ -232,7 +234,7 @@ class DQNNetwork(nn.Module):
             if not (0 < n_fixed <= n) or not h.is_contiguous():
                 raise ValueError(f"forward_heads: n_fixed {n_fixed} outside (0, {n}] or features not contiguous")
             h1 = torch.empty((n, O), dtype=torch.float32, device=h.device)
-            torch._addmm_activation(b1, h[:n_fixed], w1.t(), out=h1[:n_fixed])
+            fc1_relu(h[:n_fixed], w1, b1, out=h1[:n_fixed])
             call("rth_linear_relu_rows_upto", ptr(h), F, n_fixed, n, ptr(n_dev), ptr(w1), ptr(b1), F, O, ptr(h1), O,
                  stream_ptr())
         ps = self._head_params()[4:]
@@ -407,6 +409,36 @@ class _MergeHeads(torch.autograd.Function):
         return (None, *grads)
 
 
+# RTH_FC_X9=1: FC1 + bias + ReLU on rth_fc_x9 (the exact-split bf16 MFMA, fixed-order split-K)
+# instead of hipBLASLt's GEMM with the bias+ReLU epilogue, wherever the shape is built
+_FC_X9 = os.environ.get("RTH_FC_X9") == "1"
+_FC_WS = {}
+
+
+def fc1_relu(x, w, b, out=None):
+    """relu(x @ w.T + b) (FC1 of both dueling branches): rth_fc_x9 when enabled and built for
+    the shape, else one hipBLASLt GEMM with the bias+ReLU epilogue.  The split-K workspace is
+    keyed by the weight storage, so two networks (the actors', the target's, the learner's --
+    on different streams) never share one"""
+    M, K = x.shape
+    N = w.shape[0]
+    if _FC_X9 and x.is_cuda and x.stride(1) == 1 and w.is_contiguous():
+        from ._lib import call, lib, ptr, stream_ptr
+
+        if lib().rth_fc_x9_supported(M, N, K):
+            y = out if out is not None else torch.empty((M, N), dtype=torch.float32, device=x.device)
+            key = (x.device, w.data_ptr(), M, N, K)
+            ws = _FC_WS.get(key)
+            if ws is None:
+                ws = _FC_WS[key] = torch.empty(max(lib().rth_fc_x9_workspace(M, N, K), 16) // 4,
+                                               dtype=torch.float32, device=x.device)
+            call("rth_fc_x9", ptr(x), x.stride(0), M, ptr(w), N, K, ptr(b), 1, ptr(y), ptr(ws), stream_ptr())
+            return y
+    if out is not None:
+        return torch._addmm_activation(b, x, w.t(), out=out)
+    return torch._addmm_activation(b, x, w.t())
+
+
 class _LinearReLU(torch.autograd.Function):
     """relu(x @ w.T + b) as ONE hipBLASLt GEMM with a bias+ReLU epilogue
     (torch._addmm_activation, which has no autograd formula of its own); the backward is
@@ -414,7 +446,7 @@ class _LinearReLU(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, b):
-        out = torch._addmm_activation(b, x, w.t())
+        out = fc1_relu(x, w, b)
         ctx.save_for_backward(x, w, out)
         return out
 

@@ -155,6 +155,22 @@ PY
             --no-cpu-baseline --no-sweep --probe-steps 0
       done
       grep -h "learner block span\|next batch ready\|ms_per_step\": [0-9.]*" gpurun_out/span_*.log | cut -c1-200 ;;
+    fsab) for r in 1 2; do
+        step ab_pong_full_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep --probe-steps 0
+        step ab_pong_fs_$r 300 python bench.py --frame-store --steps 300 --warmup 5 --no-cpu-baseline --no-sweep \
+            --probe-steps 0
+      done
+      grep -H -o '"ms_per_step": [0-9.]*' gpurun_out/ab_pong_*.log ;;
+    fc) step fc_tests 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_fc_gpu.py
+      step bench_fc 300 python scripts/bench_fc.py ;;
+    fcab) RTH_FC_X9=1 step fc_learner_tests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
+          tests/test_learner_full_gpu.py tests/test_fused_learner_gpu.py tests/test_learner_gpu.py tests/test_actor_gpu.py tests/test_apex_gpu.py
+      for r in 1 2; do
+        step ab_fc0_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep --probe-steps 0
+        RTH_FC_X9=1 step ab_fc1_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep \
+            --probe-steps 0
+      done
+      grep -H -o '"ms_per_step": [0-9.]*' gpurun_out/ab_fc*.log ;;
     tests) step gpu_tests 1100 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;

@@ -31,6 +31,9 @@ def sim(KH,KW,S,CIN,HIN,WIN,NSAMP,swz,pad):
                 tot+=max(len(v) for v in slots.values()); cnt+=1
     return tot/cnt
 def mk(ROT,SH=5):
+    # SH >= 4: the rotation is constant over each aligned 16-row block, so the map permutes it
+    # (SH < 4 maps two rows of a block to one unit: not a valid swizzle -- X9Geom asserts it)
+    assert SH >= 4
     return lambda r:(r&~15)|((r+(r>>SH)*ROT)&15)
 def sim_tmap(KH, KW, S, CIN, HIN, WIN, NSAMP):
     """the tile map of k_conv_x9 (ROT < 0, stride 1): unit(s, y, x) = s SU + 16 y + ((WOUT y + x) mod 16),

@@ -609,10 +609,14 @@ def main():
                     help="actors' observations: synthetic uint8 stacks (default); atari = raw 210x160 RGB frame pairs "
                          "from device Philox through the device MaxAndSkip / gray / INTER_AREA / FrameStack; atari-h2d = "
                          "the same with the raw pairs copied host -> device from pinned memory every step (host ALE)")
-    ap.add_argument("--frame-store", action="store_true",
-                    help="frame de-duplicated replay (SURVEY §8(d) C3): each actor frame stored once in an HBM frame "
-                         "store, rows keep their stacks as frame ids, the gather assembles them (Breakout's 4 M rows: "
-                         "~30 GB instead of 225.9 GB)")
+    ap.add_argument("--frame-store", action="store_true", default=True,
+                    help="frame de-duplicated replay (SURVEY §8(d) C3; the default since r04): each actor frame "
+                         "stored once in an HBM frame store, rows keep their stacks as frame ids, the gather "
+                         "assembles them -- bit-identical rows and updates (tests/test_frame_store_gpu.py), Pong's 1 M "
+                         "rows in 7.3 GB instead of 56.5, Breakout's 4 M in 29.1 instead of 225.9, and no 56 KB stack "
+                         "copies per inserted row (Pong 0.563-0.564 vs 0.571-0.574 ms/step interleaved)")
+    ap.add_argument("--full-rows", dest="frame_store", action="store_false",
+                    help="store both uint8 stacks of every row, as the reference's worker does (worker.py:44-51)")
     ap.add_argument("--no-sweep", action="store_true", help="skip the decoupled-actor measurements after the "
                     "timed region (actor block alone; actor_steps_per_update 1 / 4 / 16)")
     ap.add_argument("--cpu-actor-worker", type=float, default=None, help=argparse.SUPPRESS)

@@ -130,8 +130,8 @@ PY
       RTH_BENCH_SPAN=1 step span 300 python bench.py --steps 300 --warmup 20 --no-cpu-baseline --no-sweep
       step bench_breakout_final 600 python bench.py --workload breakout --frame-store --steps 100 --warmup 10 \
           --no-cpu-baseline --no-sweep
-      step bench_breakout_full 600 python bench.py --workload breakout --steps 100 --warmup 10 --no-cpu-baseline \
-          --no-sweep ;;
+      step bench_breakout_full 600 python bench.py --workload breakout --full-rows --steps 100 --warmup 10 \
+          --no-cpu-baseline --no-sweep ;;
     final2) step rocprof_stats 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/prof" \
           -o run -- python bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-sweep
       step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv --kernel-include-regex "rth::" \
@@ -171,6 +171,10 @@ PY
             --probe-steps 0
       done
       grep -H -o '"ms_per_step": [0-9.]*' gpurun_out/ab_fc*.log ;;
+    benchfs) step bench_fs_default 600 python bench.py --frame-store ;;
+    dp8fs) RTH_SHARE_GPU=1 RTH_DIST_BACKEND=gloo step dp8_gloo_rehearsal_fs 900 python -m torch.distributed.run \
+          --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29518 bench.py --gpus 8 --faithful \
+          --steps 20 --warmup 5 --no-cpu-baseline --no-sweep ;;
     tests) step gpu_tests 1100 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;

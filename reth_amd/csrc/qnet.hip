@@ -363,16 +363,52 @@ __device__ __forceinline__ void fc2_store_gb(const Fc2 &f, int a, float v) {
   else f.gbv2[0] = v;
 }
 
-template <int MAXA, int RB>
+// NQ sums through the LDS tree at once (one barrier per tree level for all of them): per
+// quantity the same additions in the same order as the one-at-a-time loop, so bit-identical;
+// the tree stops at `stop` lanes (16 columns, or 1); red holds NQ x kHbThreads floats
+template <int NQ>
+__device__ __forceinline__ void tree_sums(float *red, const float (&v)[NQ], int tid, int stop) {
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) red[q * kHbThreads + tid] = v[q];
+  __syncthreads();
+  for (int st = kHbThreads / 2; st >= stop; st >>= 1) {
+    if (tid < st) {
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) red[q * kHbThreads + tid] = radd(red[q * kHbThreads + tid], red[q * kHbThreads + tid + st]);
+    }
+    __syncthreads();
+  }
+}
+// batched trees for the small-action variants (MAXA <= 8: 9 / 10 quantities, 36 / 40 KB of LDS)
+template <int MAXA, bool BATCH>
+constexpr int kHbRedQ = BATCH && MAXA <= 8 ? MAXA + 2 : 1;
+
+template <int MAXA, int RB, bool BATCH = true>
 __global__ __launch_bounds__(kHbThreads) void k_heads_backward(const float *__restrict__ dq,
                                                                const float *__restrict__ h, int64_t ldh, Fc2 f,
                                                                int64_t B, int H2, int A1, float *__restrict__ gh,
                                                                float *__restrict__ gb1,
                                                                const float *__restrict__ td_abs,
                                                                float *__restrict__ td_acc) {
-  __shared__ float red[kHbThreads];
+  __shared__ float red[kHbThreads * kHbRedQ<MAXA, BATCH>];
   const int tid = threadIdx.x;
   if ((int)blockIdx.x == H2 / kHbCols) {  // gb2 and the |td| mean
+    if constexpr (BATCH && MAXA <= 8) {
+      float v[MAXA + 1];
+#pragma unroll
+      for (int a = 0; a <= MAXA; ++a) {
+        float s = 0.0f;
+        if (a < A1 || (a == A1 && td_abs && td_acc))
+          for (int64_t r = tid; r < B; r += kHbThreads) s = radd(s, a < A1 ? dq[r * A1 + a] : td_abs[r]);
+        v[a] = s;
+      }
+      tree_sums<MAXA + 1>(red, v, tid, 1);
+      if (tid == 0) {
+        for (int a = 0; a < A1; ++a) fc2_store_gb(f, a, red[a * kHbThreads]);
+        if (td_abs && td_acc) td_acc[0] = radd(td_acc[0], red[A1 * kHbThreads] / (float)B);
+      }
+      return;
+    }
     for (int a = 0; a <= A1; ++a) {
       if (a == A1 && !(td_abs && td_acc)) break;
       float s = 0.0f;
@@ -427,6 +463,19 @@ __global__ __launch_bounds__(kHbThreads) void k_heads_backward(const float *__re
     }
   }
   // fixed-order sums over the row groups: gb1, then each (wanted) row of gw2
+  if constexpr (BATCH && MAXA <= 8) {
+    float v[MAXA + 1];
+    v[0] = ab;
+#pragma unroll
+    for (int a = 0; a < MAXA; ++a) v[1 + a] = aw[a];
+    tree_sums<MAXA + 1>(red, v, tid, kHbCols);
+    if (tid < kHbCols) {
+      gb1[j] = red[tid];
+      for (int a = 0; a < A1; ++a)
+        if (fc2_live(f, a, (int)blockIdx.x * kHbCols)) fc2_store_gw(f, a, j, H2, red[(1 + a) * kHbThreads + tid]);
+    }
+    return;
+  }
   for (int a = -1; a < A1; ++a) {
     if (a >= 0 && !fc2_live(f, a, (int)blockIdx.x * kHbCols)) continue;  // uniform
     float v = ab;
@@ -454,7 +503,7 @@ __global__ __launch_bounds__(kHbThreads) void k_heads_backward(const float *__re
 // last workgroup also writes |td|, the loss (a fixed-order tree) and the |td| mean.
 constexpr int kTdHbMaxElems = 16384;
 
-template <int MAXA, int RB>
+template <int MAXA, int RB, bool BATCH = true>
 __global__ __launch_bounds__(kHbThreads) void k_td_heads_backward(
     const float *__restrict__ q0, const float *__restrict__ q1o, const float *__restrict__ q1t,
     const int64_t *__restrict__ act, const float *__restrict__ rew, const float *__restrict__ done,
@@ -463,7 +512,7 @@ __global__ __launch_bounds__(kHbThreads) void k_td_heads_backward(
     float *__restrict__ gh, float *__restrict__ gb1, float *__restrict__ td_acc) {
   extern __shared__ float dqs[];  // B * (A + 1) floats (dynamic: a 16 K-float static array kept
                                   // the kernel off every CU a conv kernel shares)
-  __shared__ float red[kHbThreads];
+  __shared__ float red[kHbThreads * kHbRedQ<MAXA, BATCH>];
   const int tid = threadIdx.x, A1 = A + 1;
   const bool tail = (int)blockIdx.x == H2 / kHbCols;  // gb2, |td|, loss, |td| mean
   const float invB = 1.0f / (float)B;
@@ -479,6 +528,25 @@ __global__ __launch_bounds__(kHbThreads) void k_td_heads_backward(
     }
   }
   __syncthreads();
+  if (tail && BATCH && MAXA <= 8) {  // loss, |td| mean, then gb2: one batched tree
+    float v[MAXA + 2];
+    v[0] = lacc;
+    v[1] = tacc;
+#pragma unroll
+    for (int a = 0; a < MAXA; ++a) {
+      float s = 0.0f;
+      if (a < A1)
+        for (int64_t r = tid; r < B; r += kHbThreads) s = radd(s, dqs[r * A1 + a]);
+      v[2 + a] = s;
+    }
+    tree_sums<MAXA + 2>(red, v, tid, 1);
+    if (tid == 0) {
+      loss_out[0] = red[0] * invB;
+      if (td_acc) td_acc[0] = radd(td_acc[0], red[kHbThreads] / (float)B);
+      for (int a = 0; a < A1; ++a) fc2_store_gb(f, a, red[(2 + a) * kHbThreads]);
+    }
+    return;
+  }
   if (tail) {
     for (int a = -2; a < A1; ++a) {  // loss, |td| mean, then gb2
       float v = a == -2 ? lacc : (a == -1 ? tacc : 0.0f);
@@ -532,6 +600,19 @@ __global__ __launch_bounds__(kHbThreads) void k_td_heads_backward(
       gh[r * H2 + j] = g;
       ab = radd(ab, g);
     }
+  }
+  if constexpr (BATCH && MAXA <= 8) {  // gb1, then each (wanted) row of gw2: one batched tree
+    float v[MAXA + 1];
+    v[0] = ab;
+#pragma unroll
+    for (int a = 0; a < MAXA; ++a) v[1 + a] = aw[a];
+    tree_sums<MAXA + 1>(red, v, tid, kHbCols);
+    if (tid < kHbCols) {
+      gb1[j] = red[tid];
+      for (int a = 0; a < A1; ++a)
+        if (fc2_live(f, a, (int)blockIdx.x * kHbCols)) fc2_store_gw(f, a, j, H2, red[(1 + a) * kHbThreads + tid]);
+    }
+    return;
   }
   for (int a = -1; a < A1; ++a) {
     if (a >= 0 && !fc2_live(f, a, (int)blockIdx.x * kHbCols)) continue;  // uniform
@@ -901,6 +982,15 @@ static int heads_backward_impl(const float *dq, const float *h, int64_t ldh, con
   return RTH_OK;
 }
 
+// RTH_HB_BATCHED=0: the heads-backward reductions one quantity per tree (r03, A/B); the same sums
+static bool hb_batched() {
+  static const bool v = [] {
+    const char *e = getenv("RTH_HB_BATCHED");
+    return !(e && atoi(e) == 0);
+  }();
+  return v;
+}
+
 static int td_heads_backward_impl(const float *q0, const float *q1o, const float *q1t, const int64_t *a,
                                   const float *r, const float *done, const double *isw, int64_t B, int64_t A,
                                   float gamma_n, int32_t double_q, const float *h, int64_t ldh, const Fc2 &f,
@@ -914,9 +1004,12 @@ static int td_heads_backward_impl(const float *q0, const float *q1o, const float
               H2, kTdHbMaxElems);
   const dim3 grid((unsigned)(H2 / kHbCols + 1)), block(kHbThreads);
   const size_t lds = (size_t)B * (A + 1) * 4;
-  if (A + 1 <= 8)
+  if (A + 1 <= 8 && hb_batched())
     hipLaunchKernelGGL((k_td_heads_backward<8, 4>), grid, block, lds, as_stream(stream), q0, q1o, q1t, a, r, done, isw,
                        B, (int)A, gamma_n, double_q, h, ldh, f, H2, td_abs, loss_out, gh, gb1, td_acc);
+  else if (A + 1 <= 8)
+    hipLaunchKernelGGL((k_td_heads_backward<8, 4, false>), grid, block, lds, as_stream(stream), q0, q1o, q1t, a, r,
+                       done, isw, B, (int)A, gamma_n, double_q, h, ldh, f, H2, td_abs, loss_out, gh, gb1, td_acc);
   else
     hipLaunchKernelGGL((k_td_heads_backward<kHbMaxA1, 1>), grid, block, lds, as_stream(stream), q0, q1o, q1t, a, r,
                        done, isw, B, (int)A, gamma_n, double_q, h, ldh, f, H2, td_abs, loss_out, gh, gb1, td_acc);

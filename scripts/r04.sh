@@ -175,6 +175,19 @@ PY
     dp8fs) RTH_SHARE_GPU=1 RTH_DIST_BACKEND=gloo step dp8_gloo_rehearsal_fs 900 python -m torch.distributed.run \
           --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29518 bench.py --gpus 8 --faithful \
           --steps 20 --warmup 5 --no-cpu-baseline --no-sweep ;;
+    hbab) step hb_tests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_learner_gpu.py \
+          tests/test_fused_learner_gpu.py tests/test_learner_full_gpu.py
+      for r in 1 2; do
+        RTH_HB_BATCHED=0 step ab_hb0_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        step ab_hb1_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+      done
+      for f in gpurun_out/ab_hb*.log; do python - "$f" <<'PY'
+import json, sys
+d = json.loads([l for l in open(sys.argv[1]) if l.startswith('{"metric"')][-1])
+h = {r["kernel"]: r["mean_launch_us"] for r in d["roofline_hbm"]}
+print(sys.argv[1], d["ms_per_step"], "td_heads_backward_us", h.get("k_td_heads_backward"))
+PY
+      done ;;
     tests) step gpu_tests 1100 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;

@@ -1489,6 +1489,48 @@ __device__ void bias_job(const BiasJobs &bj, int j) {
   if (tid < C) bj.db[j][tid] = red[tid];
 }
 
+// the same sums with one load round trip per thread: a workgroup takes 16 consecutive
+// elements, its 16 lane groups 16 consecutive partial blocks each (all 16 loads in flight), the
+// 16 group sums added in group order -- still a fixed order (another association than the
+// 4 x 64 form below).  Opt-in (RTH_WGRED_WIDE=1): no faster in the loop (r04)
+template <int KH, int KW, int CIN, int COUT>
+__global__ __launch_bounds__(256) void k_wgrad_reduce16(const float *__restrict__ partial, int blocks,
+                                                        float *__restrict__ gw, float *__restrict__ gb, BiasJobs bj) {
+  constexpr int K = CIN * KH * KW, E = COUT * K + COUT, RB = (E + 15) / 16;
+  __shared__ float part[16][16];
+  if ((int)blockIdx.x >= RB) {  // a deferred bias gradient
+    bias_job(bj, blockIdx.x - RB);
+    return;
+  }
+  const int grp = threadIdx.x >> 4, l = threadIdx.x & 15;
+  const int e = blockIdx.x * 16 + l;
+  const int per = (blocks + 15) / 16, w0 = grp * per, w1 = w0 + per < blocks ? w0 + per : blocks;
+  float v = 0.0f;
+  if (e < E) {
+    int w = w0;
+    for (; w + 16 <= w1; w += 16) {
+      float t[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) t[u] = partial[(int64_t)(w + u) * E + e];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v = radd(v, t[u]);
+    }
+    for (; w < w1; ++w) v = radd(v, partial[(int64_t)w * E + e]);
+  }
+  part[grp][l] = v;
+  __syncthreads();
+  if (grp != 0 || e >= E) return;
+  v = part[0][l];
+#pragma unroll
+  for (int q = 1; q < 16; ++q) v = radd(v, part[q][l]);
+  if (e >= COUT * K) {
+    gb[e - COUT * K] = v;
+    return;
+  }
+  const int oi = e / K, kk = e % K, kw = kk / 32, ci = (kk % 32) / KH, kh = kk % KH;
+  gw[((oi * KH + kh) * KW + kw) * CIN + ci] = v;
+}
+
 template <int KH, int KW, int CIN, int COUT>
 __global__ __launch_bounds__(256) void k_wgrad_reduce(const float *__restrict__ partial, int blocks,
                                                       float *__restrict__ gw, float *__restrict__ gb, BiasJobs bj) {
@@ -1766,7 +1808,15 @@ int rth_conv_relu_wgrad_ex(const rth_conv_shape *shape, const void *x, const int
     hipLaunchKernelGGL(rows ? k_conv1_wgrad_bf16x3<true> : k_conv1_wgrad_bf16x3<false>, dim3(kWgBlocks),
                        dim3(kWgWaves * 64), 0, as_stream(stream), static_cast<const uint8_t *>(x), rows, n, g, y, part);
   RTH_LAUNCHED();
-  hipLaunchKernelGGL((k_wgrad_reduce<8, 8, 4, 32>), dim3((32 * 256 + 32 + 63) / 64 + ndeferred), dim3(256), 0,
+  static const bool wide = [] {  // opt-in: 0.565-0.566 vs 0.563-0.564 ms/step in the loop (r04)
+    const char *e = getenv("RTH_WGRED_WIDE");
+    return e && atoi(e) != 0;
+  }();
+  if (wide)
+    hipLaunchKernelGGL((k_wgrad_reduce16<8, 8, 4, 32>), dim3((32 * 256 + 32 + 15) / 16 + ndeferred), dim3(256), 0,
+                       as_stream(stream), part, kWgBlocks, gw, gb, bj);
+  else
+    hipLaunchKernelGGL((k_wgrad_reduce<8, 8, 4, 32>), dim3((32 * 256 + 32 + 63) / 64 + ndeferred), dim3(256), 0,
                      as_stream(stream), part, kWgBlocks, gw, gb, bj);
   RTH_LAUNCHED();
   return RTH_OK;

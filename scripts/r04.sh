@@ -188,6 +188,14 @@ h = {r["kernel"]: r["mean_launch_us"] for r in d["roofline_hbm"]}
 print(sys.argv[1], d["ms_per_step"], "td_heads_backward_us", h.get("k_td_heads_backward"))
 PY
       done ;;
+    wredab) step wred_tests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_conv_gpu.py \
+          tests/test_learner_full_gpu.py tests/test_fused_learner_gpu.py
+      for r in 1 2; do
+        RTH_WGRED_WIDE=0 step ab_wred0_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep \
+            --probe-steps 0
+        step ab_wred1_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep --probe-steps 0
+      done
+      grep -H -o '"ms_per_step": [0-9.]*' gpurun_out/ab_wred*.log ;;
     tests) step gpu_tests 1100 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;

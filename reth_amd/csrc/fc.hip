@@ -17,6 +17,7 @@
 // during the MFMAs.  splits > 1: fixed-order partial tiles + k_fc_reduce (bias, activation);
 // every sum has a fixed order, so the result is run-to-run deterministic.
 #include <type_traits>
+#include <utility>
 
 #include "common.hpp"
 
@@ -28,6 +29,14 @@ constexpr int kFcTm = 64, kFcTn = 128, kFcThreads = 256;
 __device__ __forceinline__ float fc_relu(float v) { return v < 0.0f ? 0.0f : v; }  // conv.hip's relu_c
 constexpr int kFcBUnits = 8 * 3 * 64;  // 16-byte units of one chunk's split weight tile
 
+template <int... I, class F>
+__device__ __forceinline__ void static_for(std::integer_sequence<int, I...>, F &&f) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+
+// PF: chunks whose global loads are in flight ahead of the one being computed (register ring of
+// PF + 1 sets; the LDS weight tile stays double-buffered)
+template <int PF>
 __global__ __launch_bounds__(kFcThreads) void k_fc_x9(const float *__restrict__ x, int64_t ldx, int M,
                                                       const float *__restrict__ w, int N, int K, int splits,
                                                       const float *__restrict__ bias, int relu,
@@ -44,7 +53,8 @@ __global__ __launch_bounds__(kFcThreads) void k_fc_x9(const float *__restrict__ 
   const int wn = tid & 127, wh = tid >> 7;
   const float *wrow = w + (int64_t)(n0 + wn) * K + 16 * wh;
   const float *xrow = x + (int64_t)(m0 + 16 * wave + r) * ldx + 8 * g;
-  f32x4 wv[2][4], xv[2][2];  // chunk loads, double-buffered in registers
+  constexpr int NR = PF + 1;  // register sets: chunk c's A values + chunks c + 1 .. c + PF in flight
+  f32x4 wv[NR][4], xv[NR][2];
   auto load = [&](int c, f32x4 (&wl)[4], f32x4 (&xl)[2]) __attribute__((always_inline)) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) wl[j] = *reinterpret_cast<const f32x4 *>(wrow + 32 * c + 4 * j);
@@ -90,29 +100,34 @@ __global__ __launch_bounds__(kFcThreads) void k_fc_x9(const float *__restrict__ 
       acc[nb] = a;
     }
   };
-  // chunk c: MFMAs from bl[(c - c0) & 1] with A registers xv[(c - c0) & 1]; chunk c + 1's weight
-  // rows (registers, loaded one chunk earlier) staged into the other buffer; chunk c + 2 loaded
-  // (past c1 - 1 the loads repeat the range's last chunk: in bounds, never used)
-  auto iter = [&](int c, auto pc) __attribute__((always_inline)) {
-    constexpr int p = decltype(pc)::value;  // register / LDS parity of chunk c
-    compute(xv[p], bl[p]);
-    stage(wv[p ^ 1], bl[p ^ 1]);
-    const int cn = c + 2 < c1 ? c + 2 : c1 - 1;
-    load(cn, wv[p], xv[p]);
+  // chunk c = c0 + i: MFMAs from bl[i & 1] with A registers xv[i % NR]; chunk c + 1's weight rows
+  // (registers, loaded PF chunks earlier) staged into the other LDS buffer; chunk c + NR loaded
+  // into the freed set (past c1 - 1 the loads repeat the range's last chunk: in bounds, unused)
+  auto iter = [&](int c, auto ic) __attribute__((always_inline)) {
+    constexpr int i = decltype(ic)::value;  // (c - c0) mod 2 * NR: the static ring positions
+    constexpr int pr = i % NR, pl = i & 1;
+    compute(xv[pr], bl[pl]);
+    stage(wv[(i + 1) % NR], bl[pl ^ 1]);
+    const int cn = c + NR < c1 ? c + NR : c1 - 1;
+    load(cn, wv[pr], xv[pr]);
     __syncthreads();
   };
-  // before chunk c (parity p): bl[p] = its split weights, xv[p] = its A values, wv[p ^ 1] /
-  // xv[p ^ 1] = chunk c + 1's loads
-  load(c0, wv[0], xv[0]);
-  load(c0 + 1 < c1 ? c0 + 1 : c0, wv[1], xv[1]);
+  // before chunk c0 + i: bl[i & 1] = its split weights, xv[i % NR] = its A values, the next PF
+  // sets = chunks c + 1 .. c + PF in flight
+#pragma unroll
+  for (int q = 0; q < NR; ++q) load(c0 + q < c1 ? c0 + q : c1 - 1, wv[q], xv[q]);
   stage(wv[0], bl[0]);
   __syncthreads();
   int c = c0;
-  for (; c + 1 < c1; c += 2) {
-    iter(c, std::integral_constant<int, 0>{});
-    iter(c + 1, std::integral_constant<int, 1>{});
-  }
-  if (c < c1) iter(c, std::integral_constant<int, 0>{});
+  constexpr int U = 2 * NR;  // unroll: both ring positions cycle
+  for (; c + U <= c1; c += U)
+    static_for(std::make_integer_sequence<int, U>{}, [&](auto ic) __attribute__((always_inline)) {
+      iter(c + decltype(ic)::value, ic);
+    });
+  // the remaining < U chunks, each ring position static
+  static_for(std::make_integer_sequence<int, U>{}, [&](auto ic) __attribute__((always_inline)) {
+    if (c + decltype(ic)::value < c1) iter(c + decltype(ic)::value, ic);
+  });
   // D: lane holds rows 4 g + i of the wave's 16, column r of each 16-column block
   const int mrow = m0 + 16 * wave + 4 * g;
   if (splits == 1) {
@@ -205,8 +220,16 @@ int rth_fc_x9(const float *x, int64_t ldx, int64_t M, const float *w, int64_t N,
   hipStream_t s = as_stream(stream);
   const int tiles = (int)(M / kFcTm) * (int)(N / kFcTn);
   float *out = splits == 1 ? y : static_cast<float *>(workspace);
-  hipLaunchKernelGGL(k_fc_x9, dim3((unsigned)(tiles * splits)), dim3(kFcThreads), 0, s, x, ldx, (int)M, w, (int)N,
-                     (int)K, splits, bias, (int)relu, out);
+  static const int pf = [] {  // RTH_FC_PF: chunks of loads in flight (1 or 2)
+    const char *e = getenv("RTH_FC_PF");
+    return e && atoi(e) == 1 ? 1 : 2;
+  }();
+  if (pf == 1)
+    hipLaunchKernelGGL(k_fc_x9<1>, dim3((unsigned)(tiles * splits)), dim3(kFcThreads), 0, s, x, ldx, (int)M, w,
+                       (int)N, (int)K, splits, bias, (int)relu, out);
+  else
+    hipLaunchKernelGGL(k_fc_x9<2>, dim3((unsigned)(tiles * splits)), dim3(kFcThreads), 0, s, x, ldx, (int)M, w,
+                       (int)N, (int)K, splits, bias, (int)relu, out);
   RTH_LAUNCHED();
   if (splits > 1) {
     const int64_t MN = M * N;

@@ -34,6 +34,12 @@ def copy_grid(rows):
     return (rows * 14 + rows // 64) * 256
 
 
+def copy_grid_fs(rows):
+    """k_copy_rows' grid for `rows` frame-store apex rows (the insert: five small columns -- two
+    16-byte frame-id tuples, a, r, done -- each a lane per 4-byte word, 256 lanes per workgroup)"""
+    return sum((rows * (nb // 4) + 255) // 256 for nb in (16, 8, 4, 16, 4)) * 256
+
+
 LEARNER_GATHER_GRID = copy_grid(512)
 # the HBM-bound kernels of bench.py's roofline_hbm: name -> (kernel-name match, grid or None)
 HBM_KERNELS = {"k_tree_update_sub": ("k_tree_update_sub", None), "k_tree_sample": ("k_tree_sample", None),
@@ -108,6 +114,10 @@ def main():
         for name, (match, g) in HBM_KERNELS.items():  # in-loop mean launch durations (bench.py roofline_hbm)
             sel = [r for r in win if match in r["Kernel_Name"]
                    and (g is None or int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) == grids[g])]
+            if not sel and g == "insert":  # the frame-store insert (frame ids, not stacks)
+                grids[g] = copy_grid_fs(arg("--actors", 256))
+                sel = [r for r in win if match in r["Kernel_Name"]
+                       and int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) == grids[g]]
             if sel:
                 inloop[name] = round(st.mean(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in sel) / 1e3, 3)
                 grid_of = collections.Counter(int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) for r in sel)

@@ -182,7 +182,7 @@ static int fc_splits(int M, int N, int K) {
   }();
   const int tiles = (M / kFcTm) * (N / kFcTn), chunks = K / 32;
   int s = env > 0 ? env : (256 + tiles - 1) / tiles;
-  s = s < 1 ? 1 : (s > 16 ? 16 : s);
+  s = s < 1 ? 1 : (s > 32 ? 32 : s);
   return s < chunks ? s : chunks;
 }
 

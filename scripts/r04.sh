@@ -163,7 +163,8 @@ PY
       grep -H -o '"ms_per_step": [0-9.]*' gpurun_out/ab_pong_*.log ;;
     fc) step fc_tests 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_fc_gpu.py
       step bench_fc 300 python scripts/bench_fc.py
-      RTH_FC_PF=1 step bench_fc_pf1 300 python scripts/bench_fc.py ;;
+      RTH_FC_SPLITS=16 step bench_fc_s16 300 python scripts/bench_fc.py
+      RTH_FC_SPLITS=32 step bench_fc_s32 300 python scripts/bench_fc.py ;;
     fcab) RTH_FC_X9=1 step fc_learner_tests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
           tests/test_learner_full_gpu.py tests/test_fused_learner_gpu.py tests/test_learner_gpu.py tests/test_actor_gpu.py tests/test_apex_gpu.py
       for r in 1 2; do

@@ -93,7 +93,7 @@ class ApexDQN:
         self.device = torch.device(device if device is not None else "cuda")
         self.rank, self.world = rank, world
         use_hook = world > 1 if cfg.dp_hook is None else cfg.dp_hook
-        hook = GradAllReduce(group) if use_hook else None
+        hook = GradAllReduce(group, force=bool(cfg.dp_hook)) if use_hook else None
         torch.backends.cudnn.benchmark = bool(cfg.conv_benchmark)
         if cfg.tuned_gemm:
             from . import gemm_tuning

@@ -24,17 +24,21 @@ class GradAllReduce:
     reduces the fully-connected gradients on a side stream while the conv backward runs
     (ApexDQN._capture)."""
 
-    def __init__(self, group=None):
+    def __init__(self, group=None, force=False):
         self.group = group
+        self.force = force  # run the collective in a one-rank group too (tests: RCCL on one GPU)
         self._flat = {}  # bucket key -> (flat buffer, views)
 
     def world(self):
         return dist.get_world_size(self.group) if dist.is_initialized() else 1
 
+    def _active(self):
+        return self.world() > 1 or (self.force and dist.is_initialized())
+
     def reduce(self, grads, key="all"):
         """all-reduce-average the tensors in `grads` in place, on the current stream"""
         world = self.world()
-        if world == 1:
+        if not self._active():
             return
         ent = self._flat.get(key)
         if ent is None or ent[1][0].shape != grads[0].shape or len(ent[1]) != len(grads):
@@ -57,7 +61,7 @@ class GradAllReduce:
 
     def __call__(self, params, grads=None):
         """grads: the gradient tensors to reduce (default: each parameter's .grad)"""
-        if self.world() == 1:
+        if not self._active():
             return
         self.reduce([p.grad for p in params] if grads is None else list(grads))
 

@@ -198,6 +198,7 @@ PY
         step ab_wred1_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep --probe-steps 0
       done
       grep -H -o '"ms_per_step": [0-9.]*' gpurun_out/ab_wred*.log ;;
+    rccl) step rccl_test 300 python -u -m pytest -x -v --timeout 240 --timeout-method thread tests/test_rccl_gpu.py ;;
     tests) step gpu_tests 1100 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;

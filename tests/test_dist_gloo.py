@@ -61,3 +61,31 @@ def test_grad_allreduce_world2(tmp_path):
     mp.spawn(_rank_main, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
     a, b = np.load(tmp_path / "rank0.npy"), np.load(tmp_path / "rank1.npy")
     assert np.array_equal(a, b)  # replicas stay bit-identical
+
+
+def test_grad_allreduce_forced_one_rank():
+    """GradAllReduce(force=True) runs its collective in a one-rank group (the single-GPU RCCL
+    rehearsal, tests/test_rccl_gpu.py) -- averaging over one rank leaves the gradients as they
+    were; without force a one-rank group is skipped"""
+    import socket
+
+    import torch
+    import torch.distributed as dist
+
+    from reth_amd.dist import GradAllReduce
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        g = [torch.randn(5, 3), torch.randn(7)]
+        want = [t.clone() for t in g]
+        hook = GradAllReduce(force=True)
+        assert hook._active()
+        hook.reduce(g)
+        assert all(torch.equal(a, b) for a, b in zip(g, want))
+        assert hook._flat  # the flat buffer was built: the collective ran
+        assert not GradAllReduce()._active()
+    finally:
+        dist.destroy_process_group()

@@ -1,0 +1,96 @@
+"""RCCL (torch.distributed "nccl" on ROCm) through the data-parallel learner's code path on
+the one-GPU box: a one-rank process group with the gradient all-reduce forced on
+(ApexConfig.dp_hook=True).  The captured learner is then cut at its two gradient buckets and the
+heads' bucket is all-reduced on a side stream while the conv backward replays, the conv bucket
+on the learner stream, exactly as at N > 1 (ApexDQN._learner_replay); averaging over one rank is
+the identity, so the parameters must be bit-identical to the unhooked loop's.  The driver's
+N = 2 / 4 / 8 runs are the first with more ranks (one GPU per rank); this pins the RCCL calls,
+their streams and the graph cuts before them.  The RCCL work runs in a child process that
+reports each stage, so a failure names the stage (process-group teardown included)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+CHILD = r'''
+import json, os, sys
+sys.path.insert(0, sys.argv[1])
+# a run-to-run deterministic learner (the weight gradients on rth_conv_wgrad_x9: MIOpen's
+# solvers differ in the last bits run to run), so the hooked and the plain run can be compared
+os.environ["RTH_HIP_WGRAD"] = "x9"
+import torch
+import torch.distributed as dist
+from reth_amd.apex import ApexConfig, ApexDQN
+
+def say(**kw):
+    print("STAGE " + json.dumps(kw), flush=True)
+
+dev = torch.device("cuda:0")
+
+def run(dp_hook, iters=40):
+    cfg = ApexConfig(n_actors=16, capacity=2048, batch_size=64, sample_start=128, seed=4, hip_graph=True,
+                     send_weights_interval=3, recv_weights_interval=4, update_target_interval=7, dp_hook=dp_hook)
+    ax = ApexDQN(cfg, device=dev, rank=0, world=1)
+    for _ in range(iters):
+        ax.iteration()
+    torch.cuda.synchronize()
+    parts = sorted({len(v) for v in ax._graphs["learn"].values()}) if ax._graphs else []
+    params = torch.cat([p.detach().flatten() for p in ax.solver._params]).cpu()
+    ax.close()
+    return params, parts
+
+dist.init_process_group("nccl", init_method="tcp://127.0.0.1:" + sys.argv[2], rank=0, world_size=1)
+say(stage="init", backend=dist.get_backend())
+t = torch.arange(8, dtype=torch.float32, device=dev)
+dist.all_reduce(t)
+torch.cuda.synchronize()
+say(stage="all_reduce", ok=bool(torch.equal(t.cpu(), torch.arange(8, dtype=torch.float32))))
+hooked, parts = run(True)
+say(stage="hooked", parts=parts)
+plain, parts0 = run(False)
+say(stage="plain", parts=parts0, equal=bool(torch.equal(hooked, plain)))
+if sys.argv[3] == "destroy":
+    dist.destroy_process_group()
+    say(stage="destroyed")
+os._exit(0)
+'''
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _child(teardown):
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, "-c", CHILD, root, str(_free_port()), teardown], capture_output=True,
+                       text=True, timeout=200)
+    stages = {}
+    for line in p.stdout.splitlines():
+        if line.startswith("STAGE "):
+            d = json.loads(line[6:])
+            stages[d.pop("stage")] = d
+    return p.returncode, stages, p.stderr[-2000:]
+
+
+def test_rccl_one_rank_bucketed_learner():
+    assert os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0") == "0"
+    rc, st, err = _child("keep")
+    assert st.get("init", {}).get("backend") == "nccl", (rc, st, err)
+    assert st["all_reduce"]["ok"], st
+    assert st["hooked"]["parts"] == [3], st  # two bucket cuts + the final part
+    assert st["plain"]["parts"] == [1] and st["plain"]["equal"], st
+    assert rc == 0, (rc, err)
+
+
+def test_rccl_process_group_teardown():
+    """dist.destroy_process_group() after the RCCL work (bench.py at N > 1 ends with it)"""
+    rc, st, err = _child("destroy")
+    assert "plain" in st, (rc, st, err)
+    assert "destroyed" in st and rc == 0, (rc, err)

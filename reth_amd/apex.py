@@ -24,9 +24,7 @@ of the gather are exactly those of the eager schedule.  All per-step scalars the
 need (FIFO tail, Philox counters, beta schedule step, env step) live in device memory, so
 the captured launches are valid on every replay.
 """
-import os
 from dataclasses import dataclass, field
-
 from typing import Optional
 
 import torch
@@ -80,11 +78,6 @@ class ApexConfig:
 class _Quiet:
     def info(self, *a, **k):
         pass
-
-
-# diagnostics only (RTH_DIAG_NO_SAMPLE_WAIT=1): the learner stream does not wait for its batch
-# -- wrong results, for timing the cross-stream wait's share of the gap between learner blocks
-_DIAG_NO_SAMPLE_WAIT = os.environ.get("RTH_DIAG_NO_SAMPLE_WAIT") == "1"
 
 
 class ApexDQN:
@@ -546,8 +539,7 @@ class ApexDQN:
         self._q1t_ready[k] = False
         syncs = self.solver._target_syncs
         with torch.cuda.stream(B):
-            if not _DIAG_NO_SAMPLE_WAIT:
-                B.wait_event(self._ev_sample)
+            B.wait_event(self._ev_sample)
             self._learner_replay(v)  # on B
             self._learner_host()  # target sync / weights publish copies: on B
             self._ev_learn.record(B)

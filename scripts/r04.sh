@@ -148,13 +148,6 @@ PY
         done
       done
       grep -H -o '"ms_per_step": [0-9.]*' gpurun_out/ab_w2*.log ;;
-    gapdiag) for r in 1 2; do
-        RTH_BENCH_SPAN=1 step span_$r 300 python bench.py --steps 300 --warmup 20 --no-cpu-baseline --no-sweep \
-            --probe-steps 0
-        RTH_BENCH_SPAN=1 RTH_DIAG_NO_SAMPLE_WAIT=1 step span_nowait_$r 300 python bench.py --steps 300 --warmup 20 \
-            --no-cpu-baseline --no-sweep --probe-steps 0
-      done
-      grep -h "learner block span\|next batch ready\|ms_per_step\": [0-9.]*" gpurun_out/span_*.log | cut -c1-200 ;;
     fsab) for r in 1 2; do
         step ab_pong_full_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep --probe-steps 0
         step ab_pong_fs_$r 300 python bench.py --frame-store --steps 300 --warmup 5 --no-cpu-baseline --no-sweep \

@@ -873,9 +873,9 @@ def main():
     decoupled = None
     if not args.no_sweep and ax._graphs is not None:
         decoupled = decoupled_actors(ax, dev, world)
-    if rank != 0:
+    if rank != 0:  # no collective after this point (rank 0 only assembles and prints the line)
         if world > 1:
-            dist.destroy_process_group()
+            _leave()
         return
     cpu = None
     if not args.no_cpu_baseline and world == 1:
@@ -1006,7 +1006,18 @@ def main():
     }
     print(json.dumps(out), flush=True)
     if world > 1:
-        dist.destroy_process_group()
+        _leave()
+
+
+def _leave():
+    """end a data-parallel rank without the process-group / HIP teardown: every collective is
+    done (the replica check is the last one); a destroy_process_group() with the captured
+    graphs and RCCL streams still alive aborted once in a single-rank rehearsal in a process
+    that had run the loop, which would turn a finished multi-GPU run into a failed one"""
+    torch.cuda.synchronize()
+    sys.stdout.flush()
+    sys.stderr.flush()
+    os._exit(0)
 
 
 if __name__ == "__main__":

@@ -468,6 +468,9 @@ int rth_linear_relu_rows_upto(const float *x_dev, int64_t ldx, int64_t r0, int64
  * (the last conv, whose output FC1 reads in the reference's (C, H, W) flatten order); the
  * fp32-MFMA kernels only (not the uint8 conv1, which feeds conv2) */
 #define RTH_CONV_OUT_NCHW 16
+/* rth_conv_pack_many only: the job packs the flipped data-gradient kernel of this FORWARD
+ * shape (rth_conv_dgrad_workspace(shape) bytes) for rth_conv_dgrad_prepacked */
+#define RTH_CONV_PACK_DGRAD 32
 typedef struct rth_conv_shape {
   int32_t input; /* RTH_CONV_F32_NHWC | RTH_CONV_U8_CHW [| RTH_CONV_OUT_NCHW] */
   int32_t cin, hin, win, cout, kh, kw, stride;
@@ -484,7 +487,9 @@ int rth_conv_supported(const rth_conv_shape *shape);
 int rth_conv_impl(const rth_conv_shape *shape, int64_t n, int32_t *nsamp_out);
 int64_t rth_conv_packed_bytes(const rth_conv_shape *shape);
 int rth_conv_pack(const rth_conv_shape *shape, const float *w_ohwi_dev, float *packed_dev, void *stream);
-/* rth_conv_pack for n <= 4 layers in one launch (a network's torso, both conv1 forms) */
+/* rth_conv_pack for n <= 6 layers in one launch (a network's torso, both conv1 forms, and
+ * with RTH_CONV_PACK_DGRAD in a job's shape->input the packed data-gradient kernels of the
+ * same weights: the learner packs everything its forward and backward read in one launch) */
 int rth_conv_pack_many(int32_t n, const rth_conv_shape *shapes, const float *const *w_ohwi_dev,
                        float *const *packed_dev, void *stream);
 int rth_conv_bias_relu(const rth_conv_shape *shape, const void *x_dev, const int64_t *rows_dev, int64_t n,
@@ -512,6 +517,12 @@ int rth_conv_dgrad(const rth_conv_shape *shape, const float *gy_dev, int64_t n, 
  * pass their own: the pack and the convolution of one call are stream-ordered, two calls on
  * two streams are not. */
 int64_t rth_conv_dgrad_workspace(const rth_conv_shape *shape);
+/* rth_conv_dgrad from a kernel packed beforehand: `packed_dev` = the RTH_CONV_PACK_DGRAD job of
+ * rth_conv_pack_many for this shape and the weights of the forward (no pack launch here; same
+ * result as rth_conv_dgrad_ws on those weights, bit for bit).  Built where
+ * rth_conv_dgrad_workspace(shape) > 0. */
+int rth_conv_dgrad_prepacked(const rth_conv_shape *shape, const float *gy_dev, int64_t n, const void *packed_dev,
+                             float *gx_dev, void *stream);
 /* FC1 of the dueling heads (the first Linear + ReLU of both branches, dqn_model.py:38-47, as
  * one [N, K] weight) on the exact-split bf16 MFMA: y [M, N] = act(x [M, K] w^T + b), x
  * row-major with row stride ldx, w row-major [N, K] (the Linear weight as stored), act = ReLU

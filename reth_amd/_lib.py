@@ -62,6 +62,7 @@ class BiasDeferred(ctypes.Structure):
 
 CONV_F32_NHWC, CONV_U8_CHW = 0, 1
 CONV_OUT_NCHW = 16  # flag: the conv writes NCHW (the last conv, feeding FC1)
+CONV_PACK_DGRAD = 32  # rth_conv_pack_many flag: pack this forward shape's data-gradient kernel
 CONV_IMPL_F32, CONV_IMPL_BF16X3, CONV_IMPL_X9 = 1, 2, 3  # rth_conv_impl: the kernel a launch runs
 HEADS_FC2_ONLY = -1
 
@@ -178,6 +179,7 @@ SIGNATURES = {
     "rth_fc_x9_workspace": (c_i64, [c_i64, c_i64, c_i64]),
     "rth_fc_x9": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i32, c_vp, c_vp, c_vp]),
     "rth_conv_dgrad_ws": (c_i32, [ctypes.POINTER(ConvShape), c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "rth_conv_dgrad_prepacked": (c_i32, [ctypes.POINTER(ConvShape), c_vp, c_i64, c_vp, c_vp, c_vp]),
     "rth_atari_create": (c_i32, [c_i32, c_i32, c_i32, c_i32, c_i32, ctypes.POINTER(c_vp)]),
     "rth_atari_destroy": (c_i32, [c_vp]),
     "rth_atari_step": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),

@@ -723,9 +723,8 @@ __global__ __launch_bounds__(256) void k_conv_pack_x9(const float *__restrict__ 
 // This packs W' from the forward OHWI weights into the x9 B fragments (slot layout of pack_x9:
 // output channel = ci, k' = (kh', kw', co), co fastest).
 template <int KH, int KW, int CIN, int COUT, int HIN, int WIN, int NSAMP, int ROT, int KS>
-__global__ __launch_bounds__(256) void k_conv_pack_x9_dgrad(const float *__restrict__ w, u32x4 *__restrict__ packed) {
+__device__ __forceinline__ void pack_x9_dgrad(const float *__restrict__ w, u32x4 *__restrict__ packed, int sl) {
   using G = X9Geom<KH, KW, 1, COUT, HIN, WIN, NSAMP, ROT, KS>;  // the dgrad's "input" channels = the conv's COUT
-  const int sl = blockIdx.x * 256 + threadIdx.x;
   if (sl >= G::PACKED_U4) return;
   const int lane = sl % 64, t = (sl / 64) % 3, c = (sl / 192) % G::NCH, cb = sl / (192 * G::NCH);
   const int ci = cb * 16 + (lane & 15), k0 = c * 32 + 8 * (lane >> 4);
@@ -738,6 +737,10 @@ __global__ __launch_bounds__(256) void k_conv_pack_x9_dgrad(const float *__restr
   for (int j = 0; j < 8; ++j) e[j] = bf16x3_term(wv[j], t);
   packed[sl] = u32x4{e[0] | (e[1] << 16), e[2] | (e[3] << 16), e[4] | (e[5] << 16), e[6] | (e[7] << 16)};
 }
+template <int KH, int KW, int CIN, int COUT, int HIN, int WIN, int NSAMP, int ROT, int KS>
+__global__ __launch_bounds__(256) void k_conv_pack_x9_dgrad(const float *__restrict__ w, u32x4 *__restrict__ packed) {
+  pack_x9_dgrad<KH, KW, CIN, COUT, HIN, WIN, NSAMP, ROT, KS>(w, packed, blockIdx.x * 256 + threadIdx.x);
+}
 
 // conv2 (4x4, stride 2) has no single flipped kernel: its data gradient splits by the parity
 // (py, px) of the input pixel, iy = 2 jy + py, ix = 2 jx + px.  Only taps kh = py + 2 a,
@@ -747,10 +750,8 @@ __global__ __launch_bounds__(256) void k_conv_pack_x9_dgrad(const float *__restr
 // (kh' = 1 - a).  The 4 class kernels are packed back to back (class = 2 py + px), the slot
 // layout of pack_x9 each (output channel = ci, k' = (kh', kw', co), co fastest).
 template <int CIN, int COUT, int NSAMP, int ROT, int KS>
-__global__ __launch_bounds__(256) void k_conv_pack_x9_dgrad_cls(const float *__restrict__ w,
-                                                                u32x4 *__restrict__ packed) {
+__device__ __forceinline__ void pack_x9_dgrad_cls(const float *__restrict__ w, u32x4 *__restrict__ packed, int slg) {
   using G = X9Geom<2, 2, 1, COUT, 11, 11, NSAMP, ROT, KS, CIN>;
-  const int slg = blockIdx.x * 256 + threadIdx.x;
   if (slg >= 4 * G::PACKED_U4) return;
   const int cls = slg / G::PACKED_U4, sl = slg - cls * G::PACKED_U4, py = cls >> 1, px = cls & 1;
   const int lane = sl % 64, t = (sl / 64) % 3, c = (sl / 192) % G::NCH, cb = sl / (192 * G::NCH);
@@ -763,6 +764,11 @@ __global__ __launch_bounds__(256) void k_conv_pack_x9_dgrad_cls(const float *__r
 #pragma unroll
   for (int j = 0; j < 8; ++j) e[j] = bf16x3_term(wv[j], t);
   packed[slg] = u32x4{e[0] | (e[1] << 16), e[2] | (e[3] << 16), e[4] | (e[5] << 16), e[6] | (e[7] << 16)};
+}
+template <int CIN, int COUT, int NSAMP, int ROT, int KS>
+__global__ __launch_bounds__(256) void k_conv_pack_x9_dgrad_cls(const float *__restrict__ w,
+                                                                u32x4 *__restrict__ packed) {
+  pack_x9_dgrad_cls<CIN, COUT, NSAMP, ROT, KS>(w, packed, blockIdx.x * 256 + threadIdx.x);
 }
 
 // K parts per workgroup (waves = 4 channel blocks x KS): more parts, fewer weight registers per
@@ -784,8 +790,10 @@ __global__ __launch_bounds__(256) void k_conv_pack(const float *__restrict__ w, 
   if (sl < Gm::LDS_F4) packed[sl] = Gm::load_slot(w, sl);
 }
 
-// several layers in one launch (a network's torso): block ranges per layer
-constexpr int kPackMax = 4;
+// several layers in one launch (a network's torso, and the flipped data-gradient kernels of
+// conv2 / conv3 for the backward of the same weights): block ranges per layer
+constexpr int kPackMax = 6;
+constexpr int kPackDgrad3 = 4, kPackDgrad2 = 5;  // PackJob::geom of the data-gradient packs
 struct PackJob {
   int geom[kPackMax];  // index into the built geometries (find_conv order)
   int bf16x3[kPackMax];  // conv1 u8: the bf16x3 kernel's packed form; conv2 / conv3: the x9 form (2: conv3 hybrid)
@@ -821,6 +829,19 @@ __global__ __launch_bounds__(256) void k_conv_pack_hybrid_conv3(const float *__r
   pack_hybrid_conv3(w, packed, blockIdx.x * 256 + threadIdx.x);
 }
 
+// the data gradients' packed kernels (X9Dgrad3 / X9Dgrad2 below: KS = 2, 1 sample per
+// workgroup -- the packed layout does not depend on the samples per workgroup)
+#define X9_DGRAD3_KS 2
+#ifndef X9_DGRAD2_KS
+#define X9_DGRAD2_KS 2
+#endif
+__device__ __forceinline__ void pack_dgrad3(const float *w, u32x4 *packed, int sl) {
+  pack_x9_dgrad<3, 3, 64, 64, 11, 11, 1, 3, X9_DGRAD3_KS>(w, packed, sl);
+}
+__device__ __forceinline__ void pack_dgrad2(const float *w, u32x4 *packed, int sl) {
+  pack_x9_dgrad_cls<32, 64, 1, 3, X9_DGRAD2_KS>(w, packed, sl);
+}
+
 __global__ __launch_bounds__(256) void k_conv_pack_many(PackJob job) {
   int l = 0;
   while (l + 1 < job.n && (int)blockIdx.x >= job.first_block[l + 1]) ++l;
@@ -835,6 +856,8 @@ __global__ __launch_bounds__(256) void k_conv_pack_many(PackJob job) {
       if (job.bf16x3[l]) pack_hybrid_conv2(job.w[l], job.packed[l], sl);
       else pack_one<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20>(job.w[l], job.packed[l], sl);
       break;
+    case kPackDgrad3: pack_dgrad3(job.w[l], reinterpret_cast<u32x4 *>(job.packed[l]), sl); break;
+    case kPackDgrad2: pack_dgrad2(job.w[l], reinterpret_cast<u32x4 *>(job.packed[l]), sl); break;
     default:
       if (job.bf16x3[l] == 2) pack_hybrid_conv3(job.w[l], job.packed[l], sl);
       else if (job.bf16x3[l]) pack_x9<X9_CONV3>(job.w[l], reinterpret_cast<u32x4 *>(job.packed[l]), sl);
@@ -900,6 +923,9 @@ static ConvLaunch conv1_bf16x3_launch() {
 #endif
 #ifndef CONV2_MB
 #define CONV2_MB 1
+#endif
+#ifndef CONV2_NS
+#define CONV2_NS 1
 #endif
 #ifndef CONV3_MB
 #define CONV3_MB 1
@@ -975,7 +1001,22 @@ static bool find_conv(const rth_conv_shape &s, ConvLaunch *out, int *geom = null
     // standalone the x9 kernel wins below ~400 samples (16 vs 22 us at 256), but in the Ape-X
     // loop its 77-154 KB of LDS per workgroup crowds the concurrent stream's kernels out of the
     // CUs, and the loop ran 0.5-1 % slower with it
-    static const ConvLaunch f32 = conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB>();
+    // RTH_CONV2_NS = 1 / 2 / 4: wave tiles of 16 pixels x 64 / 32 / 16 channels (finer tiles
+    // even out the last round of tiles over the SIMDs)
+    static const ConvLaunch f32 = [] {
+      const bool w16 = env_i64("RTH_CONV2_WAVES", 8) == 16;  // 16 waves: 4 per SIMD
+      switch (env_i64("RTH_CONV2_NS", CONV2_NS)) {
+        case 2:
+          return w16 ? conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 16, CONV2_MB, 2>()
+                     : conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 2>();
+        case 4:
+          return w16 ? conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 16, CONV2_MB, 4>()
+                     : conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 4>();
+        default:
+          return w16 ? conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 16, CONV2_MB, 1>()
+                     : conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 1>();
+      }
+    }();
     static const ConvLaunch l = [] {
       if (conv_f32mfma() || conv2_x9_max() <= 0) return f32;
       ConvLaunch h = x9_launch<X9_CONV2>();
@@ -1591,10 +1632,6 @@ using namespace rth;
 // and no epilogue; conv2 as its 4 stride-parity classes, one launch, blockIdx.y = class), the
 // flipped kernels packed into a per-device workspace each launch; RTH_DGRAD3_F32=1 /
 // RTH_DGRAD2_F32=1: the fp32-MFMA k_conv_dgrad instead (A/B and parity cross-checks)
-#define X9_DGRAD3_KS 2
-#ifndef X9_DGRAD2_KS
-#define X9_DGRAD2_KS 2
-#endif
 template <int NS>
 using X9Dgrad3 = X9Geom<3, 3, 1, 64, 11, 11, NS, 3, X9_DGRAD3_KS>;
 template <int NS>
@@ -1610,6 +1647,15 @@ static bool dgrad3_x9() {
 static bool dgrad2_x9() {  // 37.8 vs 43 us alone, 0.571-0.573 vs 0.574-0.575 ms/step in the loop (r04)
   static const bool v = !env_set("RTH_DGRAD2_F32");
   return v;
+}
+
+static bool is_dgrad3_x9(const rth_conv_shape *shape) {
+  return dgrad3_x9() && shape->input == RTH_CONV_F32_NHWC && shape->cin == 64 && shape->hin == 9 && shape->win == 9 &&
+         shape->cout == 64 && shape->kh == 3 && shape->kw == 3 && shape->stride == 1;
+}
+static bool is_dgrad2_x9(const rth_conv_shape *shape) {
+  return dgrad2_x9() && shape->input == RTH_CONV_F32_NHWC && shape->cin == 32 && shape->hin == 20 &&
+         shape->win == 20 && shape->cout == 64 && shape->kh == 4 && shape->kw == 4 && shape->stride == 2;
 }
 
 // the per-device packed-kernel workspace of one dgrad geometry (allocated on first use, which
@@ -1659,6 +1705,7 @@ static int launch_dgrad_x9(const void *fn, const float *gy, int64_t n, int64_t n
   return RTH_OK;
 }
 
+// w == NULL: user_ws already holds the packed kernel (rth_conv_pack_many's data-gradient job)
 static int conv_dgrad_x9_conv3(const float *gy, int64_t n, const float *w, float *gx, void *user_ws, hipStream_t st) {
   static u32x4 *ws[64] = {};
   constexpr int PK = X9Dgrad3<1>::PACKED_U4;
@@ -1666,9 +1713,11 @@ static int conv_dgrad_x9_conv3(const float *gy, int64_t n, const float *w, float
   if (!wpk)
     if (const int rc = dgrad_workspace(ws, (size_t)PK * 16, st, &wpk)) return rc;
   RTH_REQUIRE(n * 49 * 64 * 4 < ((int64_t)1 << 31), "rth_conv_dgrad: gy of %lld samples exceeds 2 GiB", (long long)n);
-  hipLaunchKernelGGL((k_conv_pack_x9_dgrad<3, 3, 64, 64, 11, 11, 1, 3, X9_DGRAD3_KS>), dim3((PK + 255) / 256),
-                     dim3(256), 0, st, w, wpk);
-  RTH_LAUNCHED();
+  if (w) {
+    hipLaunchKernelGGL((k_conv_pack_x9_dgrad<3, 3, 64, 64, 11, 11, 1, 3, X9_DGRAD3_KS>), dim3((PK + 255) / 256),
+                       dim3(256), 0, st, w, wpk);
+    RTH_LAUNCHED();
+  }
   const void *fn[4] = {nullptr, reinterpret_cast<const void *>(&k_conv_x9<3, 3, 1, 64, 11, 11, 1, 3, X9_DGRAD3_KS, 2>),
                        reinterpret_cast<const void *>(&k_conv_x9<3, 3, 1, 64, 11, 11, 2, 3, X9_DGRAD3_KS, 2>),
                        reinterpret_cast<const void *>(&k_conv_x9<3, 3, 1, 64, 11, 11, 3, 3, X9_DGRAD3_KS, 2>)};
@@ -1679,15 +1728,18 @@ static int conv_dgrad_x9_conv3(const float *gy, int64_t n, const float *w, float
 // conv2: gy [n, 9, 9, 64] -> gx [n, 20, 20, 32]; each class reads gy padded to 11 x 11 and
 // writes its 10 x 10 pixels
 static int conv_dgrad_x9_conv2(const float *gy, int64_t n, const float *w, float *gx, void *user_ws, hipStream_t st) {
+  // (w == NULL: user_ws holds the 4 packed class kernels already)
   static u32x4 *ws[64] = {};
   constexpr int PK = X9Dgrad2<1>::PACKED_U4;
   u32x4 *wpk = static_cast<u32x4 *>(user_ws);
   if (!wpk)
     if (const int rc = dgrad_workspace(ws, (size_t)4 * PK * 16, st, &wpk)) return rc;
   RTH_REQUIRE(n * 400 * 32 * 4 < ((int64_t)1 << 31), "rth_conv_dgrad: gx of %lld samples exceeds 2 GiB", (long long)n);
-  hipLaunchKernelGGL((k_conv_pack_x9_dgrad_cls<32, 64, 1, 3, X9_DGRAD2_KS>), dim3((4 * PK + 255) / 256), dim3(256), 0,
-                     st, w, wpk);
-  RTH_LAUNCHED();
+  if (w) {
+    hipLaunchKernelGGL((k_conv_pack_x9_dgrad_cls<32, 64, 1, 3, X9_DGRAD2_KS>), dim3((4 * PK + 255) / 256), dim3(256),
+                       0, st, w, wpk);
+    RTH_LAUNCHED();
+  }
   const void *fn[4] = {
       nullptr, reinterpret_cast<const void *>(&k_conv_x9<2, 2, 1, 64, 11, 11, 1, 3, X9_DGRAD2_KS, 1, 32, 1>),
       reinterpret_cast<const void *>(&k_conv_x9<2, 2, 1, 64, 11, 11, 2, 3, X9_DGRAD2_KS, 1, 32, 1>),
@@ -1741,6 +1793,21 @@ int rth_conv_pack_many(int32_t n, const rth_conv_shape *shapes, const float *con
   job.n = n;
   int blocks = 0;
   for (int l = 0; l < n; ++l) {
+    if (shapes[l].input & RTH_CONV_PACK_DGRAD) {  // the flipped data-gradient kernel of this forward shape
+      rth_conv_shape fw = shapes[l];
+      fw.input &= ~RTH_CONV_PACK_DGRAD;
+      const bool d3 = is_dgrad3_x9(&fw), d2 = is_dgrad2_x9(&fw);
+      RTH_REQUIRE(d3 || d2, "rth_conv_pack_many: job %d: no packed data-gradient kernel for this geometry", l);
+      RTH_REQUIRE(w[l] && packed[l] && ((reinterpret_cast<uintptr_t>(w[l]) | reinterpret_cast<uintptr_t>(packed[l])) &
+                                        15) == 0,
+                  "rth_conv_pack_many: layer %d buffer NULL or misaligned", l);
+      job.geom[l] = d3 ? kPackDgrad3 : kPackDgrad2;
+      job.w[l] = w[l];
+      job.packed[l] = reinterpret_cast<f32x4 *>(packed[l]);
+      job.first_block[l] = blocks;
+      blocks += (int)((rth_conv_dgrad_workspace(&fw) / 16 + 255) / 256);
+      continue;
+    }
     ConvLaunch cl;
     RTH_REQUIRE(find_conv(shapes[l], &cl, &job.geom[l]), "rth_conv_pack_many: layer %d geometry not built", l);
     RTH_REQUIRE(w[l] && packed[l] && ((reinterpret_cast<uintptr_t>(w[l]) | reinterpret_cast<uintptr_t>(packed[l])) &
@@ -1898,14 +1965,6 @@ int rth_conv_dgrad_supported(const rth_conv_shape *shape) {
   return shape && find_dgrad(*shape, &l) ? 1 : 0;
 }
 
-static bool is_dgrad3_x9(const rth_conv_shape *shape) {
-  return dgrad3_x9() && shape->input == RTH_CONV_F32_NHWC && shape->cin == 64 && shape->hin == 9 && shape->win == 9 &&
-         shape->cout == 64 && shape->kh == 3 && shape->kw == 3 && shape->stride == 1;
-}
-static bool is_dgrad2_x9(const rth_conv_shape *shape) {
-  return dgrad2_x9() && shape->input == RTH_CONV_F32_NHWC && shape->cin == 32 && shape->hin == 20 &&
-         shape->win == 20 && shape->cout == 64 && shape->kh == 4 && shape->kw == 4 && shape->stride == 2;
-}
 
 int64_t rth_conv_dgrad_workspace(const rth_conv_shape *shape) {
   if (!shape) return 0;
@@ -1916,6 +1975,20 @@ int64_t rth_conv_dgrad_workspace(const rth_conv_shape *shape) {
 
 int rth_conv_dgrad(const rth_conv_shape *shape, const float *gy, int64_t n, const float *w, float *gx, void *stream) {
   return rth_conv_dgrad_ws(shape, gy, n, w, gx, nullptr, stream);
+}
+
+int rth_conv_dgrad_prepacked(const rth_conv_shape *shape, const float *gy, int64_t n, const void *packed, float *gx,
+                             void *stream) {
+  RTH_REQUIRE(shape && gy && packed && gx && n >= 0, "rth_conv_dgrad_prepacked: NULL argument");
+  RTH_REQUIRE(((reinterpret_cast<uintptr_t>(gy) | reinterpret_cast<uintptr_t>(packed) | reinterpret_cast<uintptr_t>(gx)) &
+               15) == 0,
+              "rth_conv_dgrad_prepacked: misaligned buffer");
+  const bool d3 = is_dgrad3_x9(shape), d2 = is_dgrad2_x9(shape);
+  RTH_REQUIRE(d3 || d2, "rth_conv_dgrad_prepacked: no packed data-gradient kernel for this geometry");
+  if (n == 0) return RTH_OK;
+  void *ws = const_cast<void *>(packed);
+  return d3 ? conv_dgrad_x9_conv3(gy, n, nullptr, gx, ws, as_stream(stream))
+            : conv_dgrad_x9_conv2(gy, n, nullptr, gx, ws, as_stream(stream));
 }
 
 int rth_conv_dgrad_ws(const rth_conv_shape *shape, const float *gy, int64_t n, const float *w, float *gx,

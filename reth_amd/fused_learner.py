@@ -48,6 +48,12 @@ _wg = os.environ.get("RTH_HIP_WGRAD")
 HIP_WGRAD = None if not _wg else ("x9" if _wg == "x9" else "f32")
 
 
+# the data gradients' flipped kernels packed in the forward's pack launch (rth_conv_pack_many
+# with CONV_PACK_DGRAD jobs; rth_conv_dgrad_prepacked in the backward) instead of one pack
+# launch per data gradient; RTH_DGRAD_PREPACK=0 keeps those (A/B)
+DGRAD_PREPACK = os.environ.get("RTH_DGRAD_PREPACK", "1") != "0"
+
+
 def _net_workspace(net, kind, shape, device):
     """a backward kernel's workspace, owned by the network: two learners in one process may
     run (or replay) their backward passes on different streams, so no workspace is shared
@@ -124,7 +130,20 @@ def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None, mid=No
         w1, b1, w2, b2 = net._merged_head_weights()  # FC1: the tied parameter storage
         hp = net._head_params()
         fc2p = (_lib.c_vp * 4)(*[p.data_ptr() for p in hp[4:]])  # FC2 read in place
-        packed = net.pack_convs()
+        # the packed data-gradient kernels of this iteration's weights (the backward reads the
+        # same weights as the forward: the optimizer steps after both), packed in the forward's
+        # pack launch
+        dgp, extra = {}, []
+        if DGRAD_PREPACK:
+            for li in HIP_DGRAD:
+                sh = shapes[li] if li < len(shapes) else None
+                if sh is None or _lib.lib().rth_conv_dgrad_workspace(ctypes.byref(sh)) <= 0:
+                    continue
+                dgp[li] = _net_workspace(net, "dgrad", sh, x.device)
+                flagged = _lib.ConvShape(sh.input | _lib.CONV_PACK_DGRAD, sh.cin, sh.hin, sh.win, sh.cout, sh.kh, sh.kw,
+                                         sh.stride)
+                extra.append((flagged, _nhwc(convs[li].weight.detach()).data_ptr(), dgp[li].data_ptr()))
+        packed = net.pack_convs(u8=u8, extra=extra)
         st = stream_ptr()
         ys, h = [], x
         probed = []  # [(tag, launch)] of conv2 / conv3, handed to probe together
@@ -244,8 +263,11 @@ def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None, mid=No
                      ptr(_net_workspace(net, HIP_WGRAD, shapes[li], x.device)), st)
             if hip_dgrad:  # data gradient in rth_conv_dgrad (no zero fill)
                 gx = torch.empty(xin.shape, dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
-                call("rth_conv_dgrad_ws", ctypes.byref(shapes[li]), ptr(gy), B, ptr(w), ptr(gx),
-                     ptr(_net_workspace(net, "dgrad", shapes[li], x.device)), st)
+                if li in dgp:  # packed in the forward's pack launch
+                    call("rth_conv_dgrad_prepacked", ctypes.byref(shapes[li]), ptr(gy), B, ptr(dgp[li]), ptr(gx), st)
+                else:
+                    call("rth_conv_dgrad_ws", ctypes.byref(shapes[li]), ptr(gy), B, ptr(w), ptr(gx),
+                         ptr(_net_workspace(net, "dgrad", shapes[li], x.device)), st)
             grads[conv.weight], grads[conv.bias] = gw, db
             g = gx
         # every deferred bias gradient was finished by conv1's launch (else its db would be

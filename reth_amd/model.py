@@ -259,11 +259,13 @@ class DQNNetwork(nn.Module):
             cache[key] = self._conv_shapes(x_shape, u8)
         return cache[key]
 
-    def pack_convs(self, u8=None, out=None):
+    def pack_convs(self, u8=None, out=None, extra=()):
         """the HIP torso's packed conv weights (rth_conv_pack, fragment order) for the current
         parameters: [per conv: a device buffer, or None where MIOpen runs the layer].  Built
         for both conv1 input forms (f32 channels-last and uint8 stacks share conv2/conv3);
-        `out` (a previous result) is refilled in place."""
+        `out` (a previous result) is refilled in place.  `extra`: further (shape, weight
+        pointer, buffer pointer) jobs packed in the same launch (the learner's data-gradient
+        kernels, shape.input | CONV_PACK_DGRAD)."""
         from . import _lib
 
         convs = self._convs()
@@ -288,6 +290,7 @@ class DQNNetwork(nn.Module):
                 if out is None:
                     res.append(buf)
                 k += 1
+        jobs.extend(extra)
         if jobs:  # one launch for the whole torso
             n = len(jobs)
             shapes = (_lib.ConvShape * n)(*[j[0] for j in jobs])

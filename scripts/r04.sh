@@ -167,6 +167,41 @@ PY
       done
       grep -H -o '"ms_per_step": [0-9.]*' gpurun_out/ab_fc*.log ;;
     benchfs) step bench_fs_default 600 python bench.py --frame-store ;;
+    c2ab)  # conv2 fp32-MFMA tile shapes: waves per workgroup x channel parts per pixel tile
+      for v in 8,1 8,2 8,4 16,1 16,2 16,4; do
+        RTH_CONV2_WAVES=${v%,*} RTH_CONV2_NS=${v#*,} CONV_NS=1024,512,256 step c2_micro_${v/,/_} 120 python scripts/bench_conv.py
+        grep conv2 gpurun_out/c2_micro_${v/,/_}.log
+      done
+      for v in 8,2 16,1 16,2; do
+        RTH_CONV2_WAVES=${v%,*} RTH_CONV2_NS=${v#*,} step c2_tests_${v/,/_} 300 python -u -m pytest -x -q --timeout 120 \
+            --timeout-method thread tests/test_conv_gpu.py
+      done
+      for r in 1 2; do
+        for v in 8,1 8,2 16,1 16,2; do
+          RTH_CONV2_WAVES=${v%,*} RTH_CONV2_NS=${v#*,} step c2_ab_${v/,/_}_$r 300 python bench.py --steps 300 --warmup 5 \
+              --no-cpu-baseline --no-sweep
+        done
+      done
+      for f in gpurun_out/c2_ab_*.log; do python - "$f" <<'PY'
+import json, sys
+d = json.loads([l for l in open(sys.argv[1]) if l.startswith('{"metric"')][-1])
+print(sys.argv[1], d["ms_per_step"], d["roofline"]["mean_launch_us"], d["roofline"]["frac"])
+PY
+      done ;;
+    ppab)  # the data gradients' kernels packed in the forward's pack launch vs one pack launch each
+      step pp_tests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_conv_gpu.py \
+          tests/test_fused_learner_gpu.py tests/test_learner_gpu.py tests/test_frame_store_gpu.py
+      for r in 1 2; do
+        for v in 0 1; do
+          RTH_DGRAD_PREPACK=$v step pp_ab_${v}_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        done
+      done
+      for f in gpurun_out/pp_ab_*.log; do python - "$f" <<'PY'
+import json, sys
+d = json.loads([l for l in open(sys.argv[1]) if l.startswith('{"metric"')][-1])
+print(sys.argv[1], d["ms_per_step"], d["roofline"]["mean_launch_us"], d["roofline"]["frac"])
+PY
+      done ;;
     dp8fs) RTH_SHARE_GPU=1 RTH_DIST_BACKEND=gloo step dp8_gloo_rehearsal_fs 900 python -m torch.distributed.run \
           --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29518 bench.py --gpus 8 --faithful \
           --steps 20 --warmup 5 --no-cpu-baseline --no-sweep ;;

@@ -368,6 +368,48 @@ def test_conv_dgrad_ws_two_streams(dev, gi):
             assert torch.equal(o, want[j])
 
 
+@pytest.mark.parametrize("gi", [1, 2])
+def test_conv_dgrad_prepacked(dev, gi):
+    """rth_conv_dgrad_prepacked from a kernel packed by rth_conv_pack_many's CONV_PACK_DGRAD job
+    (in the same launch as the forward packs, as the learner issues it): bit-identical to
+    rth_conv_dgrad_ws (pack + convolution) on the same weights; the forward packs of the same
+    launch equal rth_conv_pack's"""
+    from reth_amd import _lib
+
+    cin, h, wd, cout, k, s = GEOMS[gi]
+    shape = _shape(_lib.CONV_F32_NHWC, *GEOMS[gi])
+    nbytes = _lib.lib().rth_conv_dgrad_workspace(_lib.ctypes.byref(shape))
+    if nbytes <= 0:
+        pytest.skip("the fp32-MFMA data gradient (RTH_DGRAD*_F32) packs nothing")
+    n, ho = 300, (h - k) // s + 1
+    g = torch.Generator(device=dev).manual_seed(11 + gi)
+    gy = torch.randn((n, cout, ho, ho), device=dev, generator=g).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn((cout, cin, k, k), device=dev, generator=g) * 0.05).contiguous(memory_format=torch.channels_last)
+    work = torch.empty(nbytes // 4, device=dev)
+    want = torch.empty((n, cin, h, wd), device=dev).contiguous(memory_format=torch.channels_last)
+    _lib.call("rth_conv_dgrad_ws", _lib.ctypes.byref(shape), gy.data_ptr(), n, w.data_ptr(), want.data_ptr(),
+              work.data_ptr(), _lib.stream_ptr())
+    # one pack launch: the forward image and the data-gradient kernel of the same weights
+    fwd_bytes = _lib.lib().rth_conv_packed_bytes(_lib.ctypes.byref(shape))
+    fwd = torch.empty(fwd_bytes // 4, device=dev)
+    fwd_want = torch.empty_like(fwd)
+    _lib.call("rth_conv_pack", _lib.ctypes.byref(shape), w.data_ptr(), fwd_want.data_ptr(), _lib.stream_ptr())
+    pk = torch.full((nbytes // 4,), float("nan"), device=dev)
+    flagged = _lib.ConvShape(shape.input | _lib.CONV_PACK_DGRAD, shape.cin, shape.hin, shape.win, shape.cout,
+                             shape.kh, shape.kw, shape.stride)
+    shapes = (_lib.ConvShape * 2)(shape, flagged)
+    ws = (_lib.c_vp * 2)(w.data_ptr(), w.data_ptr())
+    pks = (_lib.c_vp * 2)(fwd.data_ptr(), pk.data_ptr())
+    _lib.call("rth_conv_pack_many", 2, shapes, ws, pks, _lib.stream_ptr())
+    got = torch.full_like(want, float("nan"))
+    _lib.call("rth_conv_dgrad_prepacked", _lib.ctypes.byref(shape), gy.data_ptr(), n, pk.data_ptr(), got.data_ptr(),
+              _lib.stream_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(pk, work)
+    assert torch.equal(fwd, fwd_want)
+    assert torch.equal(got, want)
+
+
 def test_conv_dgrad_unsupported(dev):
     from reth_amd import _lib
 

@@ -1504,24 +1504,37 @@ struct BiasJobs {
 
 __device__ void bias_job(const BiasJobs &bj, int j) {
   __shared__ float red[kBiasVLanes];
-  const int C = bj.C[j], G = kBiasVLanes / C, tid = threadIdx.x;
+  constexpr int Q = kBiasVLanes / 256, U = 16;
+  const int C = bj.C[j], G = kBiasVLanes / C, tid = threadIdx.x, slabs = bj.slabs[j];
   const float *part = bj.part[j];
+  // virtual lane vt = tid + 256 q sums slabs vt / C, + G, + 2 G, ... in that order (the order of
+  // k_bias_grad_combine's lane vt); the loads of all Q lanes, U slabs each, are in flight together
+  // (one round trip per U * G slabs -- 2 for conv2's 324 slabs, where a lane-by-lane loop of
+  // 8-load batches took 12); the slabs past the end add +0 (the clamped load is replaced), which
+  // leaves every sum unchanged
+  float acc[Q];
 #pragma unroll
-  for (int q = 0; q < kBiasVLanes / 256; ++q) {
-    const int vt = tid + 256 * q, c = vt % C;
-    float s = 0.0f;
-    for (int k = vt / C; k < bj.slabs[j]; k += 8 * G) {
-      float v[8];
+  for (int q = 0; q < Q; ++q) acc[q] = 0.0f;
+  for (int base = 0; base < slabs; base += U * G) {
+    float v[Q][U];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {  // unconditional loads (clamped slab; its value is replaced by 0)
-        const int kk = k + u * G;
-        v[u] = part[(int64_t)(kk < bj.slabs[j] ? kk : bj.slabs[j] - 1) * C + c];
+    for (int q = 0; q < Q; ++q) {
+      const int vt = tid + 256 * q, c = vt % C, k0 = vt / C + base;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int kk = k0 + u * G;
+        v[q][u] = part[(int64_t)(kk < slabs ? kk : slabs - 1) * C + c];
       }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) s = radd(s, k + u * G < bj.slabs[j] ? v[u] : 0.0f);
     }
-    red[vt] = s;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int k0 = (tid + 256 * q) / C + base;
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc[q] = radd(acc[q], k0 + u * G < slabs ? v[q][u] : 0.0f);
+    }
   }
+#pragma unroll
+  for (int q = 0; q < Q; ++q) red[tid + 256 * q] = acc[q];
   __syncthreads();
   for (int st = kBiasVLanes / 2; st >= C; st >>= 1) {
     for (int i = tid; i < st; i += 256) red[i] = radd(red[i], red[i + st]);

@@ -51,7 +51,8 @@ __global__ __launch_bounds__(kEpiThreads) void k_relu_bias_grad(const float4 *__
   const int64_t r0 = (int64_t)blockIdx.x * per;
   const int64_t r1 = min<int64_t>(rows, r0 + per);
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  constexpr int U = 4;  // rows per round trip: their loads all in flight, summed in row order
+  constexpr int U = 8;  // rows per round trip: their loads all in flight, summed in row order
+                        // (conv2's 128-row slabs: one round trip; the order does not depend on U)
   for (int64_t r = r0 + tid / Q; r < r1; r += U * R) {
     float4 gv[U], yv[U];
 #pragma unroll
@@ -112,16 +113,19 @@ __global__ __launch_bounds__(kEpiThreads) void k_relu_bias_grad_nchw(const float
   const int Q = kEpiThreads / C, c_own = tid / Q, qq = tid % Q;
   const int pq = (P + Q - 1) / Q, p0 = qq * pq, p1 = min(P, p0 + pq);
   float acc = 0.0f;
-  for (int64_t b = b0; b < b1; ++b) {
+  constexpr int U = (kNchwMaxTile + kEpiThreads - 1) / kEpiThreads;
+  float yv[U], gv[U];  // a sample's loads all in flight (a load-then-use loop waited for each)
+  auto fetch = [&](int64_t b) {
     const float *gb = g + b * E, *yb = y + b * E;
-    constexpr int U = (kNchwMaxTile + kEpiThreads - 1) / kEpiThreads;
-    float yv[U], gv[U];  // the sample's loads all in flight (a load-then-use loop waited for each)
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int i = tid + u * kEpiThreads, ic = i < E ? i : E - 1;  // past E: a duplicate, unused
       yv[u] = yb[ic];
       gv[u] = gb[ic];
     }
+  };
+  if (b0 < b1) fetch(b0);
+  for (int64_t b = b0; b < b1; ++b) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {  // NCHW order: i = c * P + p
       const int i = tid + u * kEpiThreads;
@@ -130,6 +134,9 @@ __global__ __launch_bounds__(kEpiThreads) void k_relu_bias_grad_nchw(const float
         tile[c * LP + pp] = yv[u] > 0.0f ? gv[u] : 0.0f;  // threshold_backward(g, y, 0)
       }
     }
+    // the next sample's loads go out now and land while this one is summed and stored (the last
+    // sample re-reads itself: no load under a branch)
+    fetch(b + 1 < b1 ? b + 1 : b);
     __syncthreads();
     for (int p = p0; p < p1; ++p) acc = radd(acc, tile[c_own * LP + p]);
     float *gyb = gy + b * E;

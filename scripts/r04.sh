@@ -227,6 +227,21 @@ PY
       done
       grep -H -o '"ms_per_step": [0-9.]*' gpurun_out/ab_wred*.log ;;
     rccl) step rccl_test 300 python -u -m pytest -x -v --timeout 240 --timeout-method thread tests/test_rccl_gpu.py ;;
+    evid)  # the round's closing evidence on the final tree: suite, smoke, default bench, span, profiles
+      step gpu_tests 1100 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests
+      step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+      step bench_final 600 python bench.py
+      RTH_BENCH_SPAN=1 step span 300 python bench.py --steps 300 --warmup 20 --no-cpu-baseline --no-sweep ;;
+    evid2)
+      step rocprof_stats 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/prof" \
+          -o run -- python bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-sweep
+      step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv --kernel-include-regex "rth::" \
+          -d "$PWD/gpurun_out/pmc_fetch" -o run -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-sweep
+      step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv --kernel-include-regex "rth::" \
+          -d "$PWD/gpurun_out/pmc_write" -o run -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-sweep
+      step bench_breakout_final 600 python bench.py --workload breakout --steps 100 --warmup 10 \
+          --no-cpu-baseline --no-sweep
+      step bench_driver 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     tests) step gpu_tests 1100 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;

@@ -49,6 +49,11 @@ const char *rth_last_error(void);
 /* development aid: wall-clock ticks (100 MHz) at the phase boundaries of the last tree
  * update launch (start, prefetch, sort, priorities written, levels done) */
 int rth_debug_tree_timing(long long *out9);
+/* development aid (a library built with -DRTH_CLOCK_STAMPS only; the product build returns an
+ * error): per workgroup of the last fp32-MFMA conv launch (k_conv_bias_relu), the shader-clock
+ * and 100 MHz wall-clock ticks around wave 0's work -- out[2 i], out[2 i + 1] for workgroups
+ * i < slots <= 1024 -- whose ratio is the in-kernel clock */
+int rth_debug_conv_clock(unsigned long long *out, int32_t slots);
 /* library build/ABI version (major*10000 + minor*100 + patch) */
 int rth_version(void);
 /* the source tree the library was compiled from: 40 hex digits, the SHA-1 over the lines

@@ -253,30 +253,40 @@ __global__ __launch_bounds__(kEnvThreads) void k_env_reset(uint8_t *frames, int 
 
 
 // out[0..k) = vals[i] for the i < n with flag[i] != 0, in order of i; out[k..cap) = fill;
-// *count_out = base + k.  One workgroup, a block scan per 1024-entry chunk.
+// *count_out = base + k.  One workgroup, per 1024-entry chunk: each wave's flags as a 64-bit
+// ballot (a lane's rank among the wave's flagged lanes = the popcount of the lower bits), the
+// 16 wave counts prefixed through LDS -- one barrier per chunk instead of a 10-step block scan
+// with two barriers a step; the flag and the value of every lane are loaded together.
 constexpr int kCompactThreads = 1024;
 __global__ __launch_bounds__(kCompactThreads) void k_compact_flagged(const float *__restrict__ flag,
                                                                     const int64_t *__restrict__ vals, int64_t n,
                                                                     int64_t *__restrict__ out, int64_t cap,
                                                                     int64_t fill, int64_t base,
                                                                     int64_t *__restrict__ count_out) {
-  __shared__ int scan[kCompactThreads];
-  const int tid = threadIdx.x;
+  constexpr int W = kCompactThreads / 64;
+  __shared__ int wcount[2][W];  // double-buffered: chunk c's counts stay readable while c + 1 writes
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   int64_t k = 0;
-  for (int64_t c0 = 0; c0 < n; c0 += kCompactThreads) {
-    const int64_t i = c0 + tid;
-    const int f = (i < n && flag[i] != 0.0f) ? 1 : 0;
-    scan[tid] = f;
+  int buf = 0;
+  for (int64_t c0 = 0; c0 < n; c0 += kCompactThreads, buf ^= 1) {
+    const int64_t i = c0 + tid, ic = i < n ? i : n - 1;  // past n: a duplicate load, never flagged
+    const float fv = flag[ic];
+    const int64_t v = vals[ic];
+    const bool f = i < n && fv != 0.0f;
+    const uint64_t bal = __ballot(f);
+    const int below = __popcll(bal & ((uint64_t(1) << lane) - 1));
+    if (lane == 0) wcount[buf][wave] = __popcll(bal);
     __syncthreads();
-    for (int off = 1; off < kCompactThreads; off <<= 1) {  // inclusive Hillis-Steele scan
-      const int v = tid >= off ? scan[tid - off] : 0;
-      __syncthreads();
-      scan[tid] += v;
-      __syncthreads();
+    int before = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      const int cw = wcount[buf][w];
+      before += w < wave ? cw : 0;
+      total += cw;
     }
-    if (f && k + scan[tid] - 1 < cap) out[k + scan[tid] - 1] = vals[i];
-    k += scan[kCompactThreads - 1];
-    __syncthreads();
+    const int64_t pos = k + before + below;
+    if (f && pos < cap) out[pos] = v;
+    k += total;
   }
   const int64_t kk = k < cap ? k : cap;
   for (int64_t j = kk + tid; j < cap; j += kCompactThreads) out[j] = fill;

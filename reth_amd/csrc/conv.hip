@@ -72,6 +72,13 @@ struct ConvGeom {
   }
 };
 
+// In-kernel clock of the fp32-MFMA kernel (a diagnostic build only, -DRTH_CLOCK_STAMPS: the
+// shader-clock and 100 MHz wall-clock ticks around wave 0's work of each workgroup, read by
+// rth_debug_conv_clock; the product build executes no stamp).  The stamps go to a buffer of
+// their own that no kernel reads.
+constexpr int kClockSlots = 1024;
+__device__ unsigned long long g_conv_clock[kClockSlots][2];
+
 // NS > 1: a wave tile is TP pixels x COUT / NS channels (tile t = pixel tile t / NS, channel
 // part t % NS), for more, smaller tiles over the SIMDs; each output keeps its K order
 template <int MODE, int KH, int KW, int S, int CIN, int COUT, int HIN, int WIN, int WAVES, int MB, int NS = 1>
@@ -92,6 +99,9 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__res
 
   const int wave = threadIdx.x / 64, lane = threadIdx.x % 64;
   const int q = lane >> 4, mr = lane & 15;
+#ifdef RTH_CLOCK_STAMPS
+  const unsigned long long clk0 = __builtin_amdgcn_s_memtime(), wall0 = __builtin_amdgcn_s_memrealtime();
+#endif
   if (n_dev) {  // a device-side sample count (<= n): rows past it are neither read nor written
     const int64_t m = *n_dev;
     n = m < n ? (m > 0 ? m : 0) : n;
@@ -241,6 +251,13 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__res
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb) cur[mb] = nxt[mb];
   }
+#ifdef RTH_CLOCK_STAMPS
+  if (threadIdx.x == 0 && blockIdx.x < kClockSlots) {
+    const unsigned long long clk1 = __builtin_amdgcn_s_memtime(), wall1 = __builtin_amdgcn_s_memrealtime();
+    g_conv_clock[blockIdx.x][0] = clk1 - clk0;
+    g_conv_clock[blockIdx.x][1] = wall1 - wall0;
+  }
+#endif
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1984,6 +2001,17 @@ int64_t rth_conv_dgrad_workspace(const rth_conv_shape *shape) {
   if (is_dgrad3_x9(shape)) return (int64_t)X9Dgrad3<1>::PACKED_U4 * 16;
   if (is_dgrad2_x9(shape)) return (int64_t)4 * X9Dgrad2<1>::PACKED_U4 * 16;
   return 0;
+}
+
+int rth_debug_conv_clock(unsigned long long *out, int32_t slots) {
+  RTH_REQUIRE(out && slots >= 1 && slots <= kClockSlots, "rth_debug_conv_clock: bad arguments");
+#ifdef RTH_CLOCK_STAMPS
+  RTH_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_conv_clock), (size_t)slots * 2 * sizeof(unsigned long long)));
+  return RTH_OK;
+#else
+  RTH_REQUIRE(false, "rth_debug_conv_clock: not a clock-stamp build (-DRTH_CLOCK_STAMPS)");
+  return RTH_OK;
+#endif
 }
 
 int rth_conv_dgrad(const rth_conv_shape *shape, const float *gy, int64_t n, const float *w, float *gx, void *stream) {

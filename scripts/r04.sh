@@ -202,6 +202,21 @@ d = json.loads([l for l in open(sys.argv[1]) if l.startswith('{"metric"')][-1])
 print(sys.argv[1], d["ms_per_step"], d["roofline"]["mean_launch_us"], d["roofline"]["frac"])
 PY
       done ;;
+    clk)  # conv2's in-kernel clock (diagnostic build), the ballot compaction, two bench runs
+      step clk_tests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_actor_gpu.py \
+          tests/test_conv_gpu.py tests/test_apex_gpu.py
+      RTH_LIB_PATH=reth_amd/libreth_hip_clk.so step conv_clock 120 python scripts/conv_clock.py
+      RTH_LIB_PATH=reth_amd/libreth_hip_clk.so CLK_N=512 step conv_clock512 120 python scripts/conv_clock.py
+      for r in 1 2; do
+        step clk_bench_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+      done
+      cat gpurun_out/conv_clock.log gpurun_out/conv_clock512.log | grep kernel
+      for f in gpurun_out/clk_bench_*.log; do python - "$f" <<'PY'
+import json, sys
+d = json.loads([l for l in open(sys.argv[1]) if l.startswith('{"metric"')][-1])
+print(sys.argv[1], d["ms_per_step"], d["roofline"]["mean_launch_us"], d["roofline"]["frac"])
+PY
+      done ;;
     dp8fs) RTH_SHARE_GPU=1 RTH_DIST_BACKEND=gloo step dp8_gloo_rehearsal_fs 900 python -m torch.distributed.run \
           --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29518 bench.py --gpus 8 --faithful \
           --steps 20 --warmup 5 --no-cpu-baseline --no-sweep ;;

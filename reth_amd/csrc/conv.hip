@@ -1617,7 +1617,14 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const float *__restrict__ 
   float v = 0.0f;
   if (e < E) {
     int w = w0;
-    for (; w + 16 <= w1; w += 16) {  // 16 loads in flight per round trip; the sum stays in w order
+    for (; w + 32 <= w1; w += 32) {  // 32 loads in flight per round trip; the sum stays in w order
+      float t[32];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) t[u] = partial[(int64_t)(w + u) * E + e];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) v = radd(v, t[u]);
+    }
+    for (; w + 16 <= w1; w += 16) {
       float t[16];
 #pragma unroll
       for (int u = 0; u < 16; ++u) t[u] = partial[(int64_t)(w + u) * E + e];

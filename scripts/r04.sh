@@ -217,6 +217,21 @@ d = json.loads([l for l in open(sys.argv[1]) if l.startswith('{"metric"')][-1])
 print(sys.argv[1], d["ms_per_step"], d["roofline"]["mean_launch_us"], d["roofline"]["frac"])
 PY
       done ;;
+    sideab)  # FC1's weight gradient on a side stream vs in line (+ the wider conv1 reduce in both)
+      step side_tests 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_fused_learner_gpu.py \
+          tests/test_learner_gpu.py tests/test_apex_gpu.py tests/test_dp_gpu.py tests/test_rccl_gpu.py \
+          tests/test_learner_full_gpu.py tests/test_conv_gpu.py
+      for r in 1 2; do
+        for v in 0 1; do
+          RTH_FC1_WGRAD_SIDE=$v step side_ab_${v}_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        done
+      done
+      for f in gpurun_out/side_ab_*.log; do python - "$f" <<'PY'
+import json, sys
+d = json.loads([l for l in open(sys.argv[1]) if l.startswith('{"metric"')][-1])
+print(sys.argv[1], d["ms_per_step"], d["roofline"]["mean_launch_us"], d["roofline"]["frac"])
+PY
+      done ;;
     dp8fs) RTH_SHARE_GPU=1 RTH_DIST_BACKEND=gloo step dp8_gloo_rehearsal_fs 900 python -m torch.distributed.run \
           --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29518 bench.py --gpus 8 --faithful \
           --steps 20 --warmup 5 --no-cpu-baseline --no-sweep ;;

@@ -272,6 +272,7 @@ PY
       step bench_breakout_final 600 python bench.py --workload breakout --steps 100 --warmup 10 \
           --no-cpu-baseline --no-sweep
       step bench_driver 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    rccldbg) step rccl_dbg 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_rccl_gpu.py ;;
     tests) step gpu_tests 1100 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;

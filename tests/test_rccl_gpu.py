@@ -83,14 +83,15 @@ def test_rccl_one_rank_bucketed_learner():
     assert os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0") == "0"
     rc, st, err = _child("keep")
     assert st.get("init", {}).get("backend") == "nccl", (rc, st, err)
-    assert st["all_reduce"]["ok"], st
-    assert st["hooked"]["parts"] == [3], st  # two bucket cuts + the final part
-    assert st["plain"]["parts"] == [1] and st["plain"]["equal"], st
+    assert st["all_reduce"]["ok"], (rc, st, err)
+    assert "hooked" in st and st["hooked"]["parts"] == [3], (rc, st, err)  # two bucket cuts + the final part
+    assert "plain" in st and st["plain"]["parts"] == [1] and st["plain"]["equal"], (rc, st, err)
     assert rc == 0, (rc, err)
 
 
 def test_rccl_process_group_teardown():
-    """dist.destroy_process_group() after the RCCL work (bench.py at N > 1 ends with it)"""
+    """dist.destroy_process_group() after the RCCL work (bench.py at N > 1 leaves without it,
+    after its last collective: DESIGN.md (e))"""
     rc, st, err = _child("destroy")
     assert "plain" in st, (rc, st, err)
     assert "destroyed" in st and rc == 0, (rc, err)

@@ -68,6 +68,11 @@ def _free_port():
 
 
 def _child(teardown):
+    import torch
+
+    if torch.cuda.is_initialized():  # hand the suite's cached device memory back before the child starts
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     p = subprocess.run([sys.executable, "-c", CHILD, root, str(_free_port()), teardown], capture_output=True,
                        text=True, timeout=200)

@@ -272,6 +272,41 @@ PY
       step bench_breakout_final 600 python bench.py --workload breakout --steps 100 --warmup 10 \
           --no-cpu-baseline --no-sweep
       step bench_driver 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    wgbab)  # conv1 weight-gradient partial blocks (CONV_WG_BLOCKS, variant libraries) 256 / 128 / 512
+      for v in wg128 wg512; do
+        RTH_LIB_PATH=reth_amd/libreth_hip_$v.so step wgb_tests_$v 300 python -u -m pytest -x -q --timeout 120 \
+            --timeout-method thread tests/test_conv_gpu.py tests/test_fused_learner_gpu.py
+      done
+      for r in 1 2; do
+        step wgb_ab_base_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        for v in wg128 wg512; do
+          RTH_LIB_PATH=reth_amd/libreth_hip_$v.so step wgb_ab_${v}_$r 300 python bench.py --steps 300 --warmup 5 \
+              --no-cpu-baseline --no-sweep
+        done
+      done
+      for f in gpurun_out/wgb_ab_*.log; do python - "$f" <<'PY'
+import json, sys
+d = json.loads([l for l in open(sys.argv[1]) if l.startswith('{"metric"')][-1])
+print(sys.argv[1], d["ms_per_step"], d["ms_per_step_windows"])
+PY
+      done ;;
+    c2mb2)  # conv2 fp32 MFMA with 32-pixel wave tiles (CONV2_MB=2, variant library)
+      RTH_LIB_PATH=reth_amd/libreth_hip_c2mb2.so CONV_NS=1024,512,256 step c2mb2_micro 120 python scripts/bench_conv.py
+      CONV_NS=1024,512,256 step c2mb1_micro 120 python scripts/bench_conv.py
+      grep conv2 gpurun_out/c2mb2_micro.log gpurun_out/c2mb1_micro.log
+      RTH_LIB_PATH=reth_amd/libreth_hip_c2mb2.so step c2mb2_tests 300 python -u -m pytest -x -q --timeout 120 \
+          --timeout-method thread tests/test_conv_gpu.py
+      for r in 1 2; do
+        step c2mb_ab_base_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        RTH_LIB_PATH=reth_amd/libreth_hip_c2mb2.so step c2mb_ab_mb2_$r 300 python bench.py --steps 300 --warmup 5 \
+            --no-cpu-baseline --no-sweep
+      done
+      for f in gpurun_out/c2mb_ab_*.log; do python - "$f" <<'PY'
+import json, sys
+d = json.loads([l for l in open(sys.argv[1]) if l.startswith('{"metric"')][-1])
+print(sys.argv[1], d["ms_per_step"], d["roofline"]["mean_launch_us"], d["roofline"]["frac"])
+PY
+      done ;;
     rccldbg) step rccl_dbg 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_rccl_gpu.py ;;
     tests) step gpu_tests 1100 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;

@@ -307,6 +307,27 @@ d = json.loads([l for l in open(sys.argv[1]) if l.startswith('{"metric"')][-1])
 print(sys.argv[1], d["ms_per_step"], d["roofline"]["mean_launch_us"], d["roofline"]["frac"])
 PY
       done ;;
+    c1nb)  # conv1 forward: tiles whose windows are in flight (C1_NBUF, variant libraries) 3 / 2 / 4
+      for v in c1nb2 c1nb4; do
+        RTH_LIB_PATH=reth_amd/libreth_hip_$v.so CONV_NS=1024,512,256 step ${v}_micro 120 python scripts/bench_conv.py
+        RTH_LIB_PATH=reth_amd/libreth_hip_$v.so step ${v}_tests 300 python -u -m pytest -x -q --timeout 120 \
+            --timeout-method thread tests/test_conv_gpu.py
+      done
+      CONV_NS=1024,512,256 step c1nb3_micro 120 python scripts/bench_conv.py
+      grep -h "conv1" gpurun_out/c1nb*_micro.log
+      for r in 1 2; do
+        step c1nb_ab_base_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        for v in c1nb2 c1nb4; do
+          RTH_LIB_PATH=reth_amd/libreth_hip_$v.so step c1nb_ab_${v}_$r 300 python bench.py --steps 300 --warmup 5 \
+              --no-cpu-baseline --no-sweep
+        done
+      done
+      for f in gpurun_out/c1nb_ab_*.log; do python - "$f" <<'PY'
+import json, sys
+d = json.loads([l for l in open(sys.argv[1]) if l.startswith('{"metric"')][-1])
+print(sys.argv[1], d["ms_per_step"], d["ms_per_step_windows"])
+PY
+      done ;;
     rccldbg) step rccl_dbg 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_rccl_gpu.py ;;
     tests) step gpu_tests 1100 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;

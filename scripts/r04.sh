@@ -328,6 +328,19 @@ d = json.loads([l for l in open(sys.argv[1]) if l.startswith('{"metric"')][-1])
 print(sys.argv[1], d["ms_per_step"], d["ms_per_step_windows"])
 PY
       done ;;
+    x9wg)  # x9 conv workgroups per CU (runtime RTH_X9_WG_PER_CU): 1 (default) vs 2
+      RTH_X9_WG_PER_CU=2 step x9wg_tests 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
+          tests/test_conv_gpu.py
+      for r in 1 2; do
+        step x9wg_ab_1_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        RTH_X9_WG_PER_CU=2 step x9wg_ab_2_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+      done
+      for f in gpurun_out/x9wg_ab_*.log; do python - "$f" <<'PY'
+import json, sys
+d = json.loads([l for l in open(sys.argv[1]) if l.startswith('{"metric"')][-1])
+print(sys.argv[1], d["ms_per_step"], d["ms_per_step_windows"], d["roofline_conv3"]["mean_launch_us"])
+PY
+      done ;;
     rccldbg) step rccl_dbg 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_rccl_gpu.py ;;
     tests) step gpu_tests 1100 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;

@@ -568,10 +568,11 @@ def test_conv_impl_selection(dev):
     assert impl(_shape(_lib.CONV_F32_NHWC, *GEOMS[1]), 256) == (_lib.CONV_IMPL_F32, 0)
     c3 = _shape(_lib.CONV_F32_NHWC | _lib.CONV_OUT_NCHW, *GEOMS[2])
     cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    slots = cus * max(1, int(os.environ.get("RTH_X9_WG_PER_CU") or 1))  # workgroups per round (the model's)
     for n in (1, cus // 2, cus, 2 * cus, 3 * cus, 4 * cus, 6 * cus):
         kind, s = impl(c3, n)
         assert kind == _lib.CONV_IMPL_X9 and 1 <= s <= 4, (n, kind, s)
-        rounds = lambda q: -(-(-(-n // q)) // cus)
+        rounds = lambda q: -(-(-(-n // q)) // slots)
         # the chosen instantiation's estimated time is the least of the built ones
         assert all(rounds(s) * (s + 0.5) <= rounds(q) * (q + 0.5) for q in (1, 2, 3, 4)), (n, s)
     assert impl(c3, 0)[0] == 0 and impl(_shape(_lib.CONV_F32_NHWC, 3, 84, 84, 32, 8, 4), 8)[0] == 0

@@ -341,6 +341,10 @@ d = json.loads([l for l in open(sys.argv[1]) if l.startswith('{"metric"')][-1])
 print(sys.argv[1], d["ms_per_step"], d["ms_per_step_windows"], d["roofline_conv3"]["mean_launch_us"])
 PY
       done ;;
+    convtests)
+      step conv_tests 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_conv_gpu.py
+      RTH_X9_WG_PER_CU=2 step conv_tests_wg2 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
+          tests/test_conv_gpu.py ;;
     rccldbg) step rccl_dbg 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_rccl_gpu.py ;;
     tests) step gpu_tests 1100 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;

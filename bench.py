@@ -642,7 +642,7 @@ def main():
         args.actor_steps_per_update = args.gpus if shard else 1
 
     from reth_amd.apex import ApexConfig, ApexDQN
-    from reth_amd.dist import init_from_env
+    from reth_amd.dist import init_from_env, shutdown
 
     if os.environ.get("RTH_BLAS"):  # A/B aid: torch's GEMM backend ("cublas" = rocBLAS, "cublaslt" = hipBLASLt)
         torch.backends.cuda.preferred_blas_library(os.environ["RTH_BLAS"])
@@ -875,7 +875,7 @@ def main():
         decoupled = decoupled_actors(ax, dev, world)
     if rank != 0:  # no collective after this point (rank 0 only assembles and prints the line)
         if world > 1:
-            _leave()
+            shutdown(ax)  # graphs released, then the process group destroyed (reth_amd.dist)
         return
     cpu = None
     if not args.no_cpu_baseline and world == 1:
@@ -1006,18 +1006,7 @@ def main():
     }
     print(json.dumps(out), flush=True)
     if world > 1:
-        _leave()
-
-
-def _leave():
-    """end a data-parallel rank without the process-group / HIP teardown: every collective is
-    done (the replica check is the last one); a destroy_process_group() with the captured
-    graphs and RCCL streams still alive aborted once in a single-rank rehearsal in a process
-    that had run the loop, which would turn a finished multi-GPU run into a failed one"""
-    torch.cuda.synchronize()
-    sys.stdout.flush()
-    sys.stderr.flush()
-    os._exit(0)
+        shutdown(ax)
 
 
 if __name__ == "__main__":

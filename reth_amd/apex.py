@@ -353,26 +353,33 @@ class ApexDQN:
                     v = ("probe", variant, p) if pr else (variant, p)
                     parts, bounds = [torch.cuda.CUDAGraph()], []
 
-                    def cut(item, parts=parts, bounds=bounds):
+                    ended = []
+
+                    def cut(item, last=False, parts=parts, bounds=bounds, ended=ended):
                         # end this part of the learner graph at a boundary: ("bucket", a final
                         # gradient bucket -- its all-reduce runs between the parts, overlapping
                         # the next one) or ("probe", [(tag, launch), ...]) -- launches issued eagerly
-                        # between the parts at every replay, each bracketed by the bench's HIP events)
+                        # between the parts at every replay, each bracketed by the bench's HIP events).
+                        # last: nothing is captured after this boundary, so no (empty) part follows
                         parts[-1].capture_end()
                         bounds.append(item)
+                        if last:
+                            ended.append(True)
+                            return
                         parts.append(torch.cuda.CUDAGraph())
                         parts[-1].capture_begin(pool=parts[0].pool())
 
                     parts[0].capture_begin()
                     data, idx, isw = slots[p]
-                    probe = (lambda items: cut(("probe", items))) if pr else None
+                    probe = (lambda items, last=False: cut(("probe", items), last=last)) if pr else None
                     td = solver.compute_grads(data, isw, q1t=G["q1t"][p] if variant == "pre" else None,
                                               mid=(lambda b: cut(("bucket", b))) if split else None, probe=probe)
                     self.trainer._track(td)
                     if split and not any(k == "bucket" for k, _ in bounds):  # autograd path: one bucket
                         cut(("bucket", [q.grad for q in solver._params]))
                     solver.apply_grads(probe=probe)
-                    parts[-1].capture_end()
+                    if not ended:
+                        parts[-1].capture_end()
                     G["learn"][v], G["buckets"][v], G["learn_td"][v] = parts, bounds, td
                     G["grads"][v] = [q.grad for q in solver._params]  # what apply_grads consumed
         torch.cuda.current_stream(self.device).wait_stream(side)
@@ -439,7 +446,7 @@ class ApexDQN:
         records HIP events there on this stream for its live per-launch timing)."""
         G = self._graphs
         parts, bounds = G["learn"][v], G["buckets"][v]
-        if len(parts) == 1:
+        if not bounds:
             parts[0].replay()
             return
         hook = self.solver.grad_hook
@@ -467,9 +474,15 @@ class ApexDQN:
                     hook.reduce(item, key=key)
             else:
                 hook.reduce(item, key=key)
+                # everything after the last bucket (heads split, clip + Adam -- replayed or, in a
+                # probe copy, issued eagerly between parts) reads the side stream's buckets
+                if comm is not None:
+                    cur.wait_stream(comm)
+                    comm = None
         if comm is not None:
             cur.wait_stream(comm)
-        parts[-1].replay()
+        if len(parts) > len(bounds):  # a probe copy may end at its last probed launch
+            parts[-1].replay()
 
     def _actor_block_graph(self):
         G, act = self._graphs, self.actors

@@ -10,6 +10,8 @@ gradients on the learner's stream after it, and the final part of the update (he
 + clip + Adam) waits for both (ApexDQN._capture / _learner_replay).  The eager learner
 reduces everything as one bucket.
 """
+import gc
+
 import torch
 import torch.distributed as dist
 
@@ -79,3 +81,24 @@ def init_from_env(backend=None):
         backend = "nccl" if torch.cuda.is_available() else "gloo"  # nccl == RCCL on ROCm
     dist.init_process_group(backend=backend)
     return dist.get_rank(), dist.get_world_size()
+
+
+def shutdown(*owners):
+    """orderly end of a data-parallel rank (bench.py, tests/test_rccl_gpu.py): drain the device,
+    release the owners' captured graphs and streams (`close()`), then destroy the process group.
+    The order matters: every RCCL call is issued eagerly between graph parts on the learner's
+    side stream (ApexDQN._learner_replay), none is captured, so once the device is idle no
+    graph references a communicator; the graphs are dropped while the HIP runtime and the
+    communicator are both still alive, and the group is destroyed last, with nothing queued
+    on any stream.  Returns normally -- the interpreter's own exit follows."""
+    cuda = torch.cuda.is_available() and torch.cuda.is_initialized()
+    if cuda:
+        torch.cuda.synchronize()
+    for o in owners:
+        if o is not None:
+            o.close()
+    gc.collect()
+    if cuda:
+        torch.cuda.synchronize()
+    if dist.is_initialized():
+        dist.destroy_process_group()

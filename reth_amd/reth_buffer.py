@@ -10,14 +10,27 @@ What changes underneath: the service processes (ZMQ append/sampler loops, LMDB i
 CUDA-IPC loader processes) become one replay object resident in the GPU's HBM, owned by the
 process that drives that GPU (one process per GPU).  `start_*` returns a handle standing in
 for the service Process (terminate/join/is_alive) and an address string ("hbm://dev/id")
-that Client and the loaders resolve in-process.  Differences, by design:
-  * a loader asked for a batch before `cnt >= max(sample_start, batch_size)`
-    (sampler_loop.py:23-28) raises instead of blocking forever (nothing else could fill it);
-  * num_sampler_procs / num_procs / compress / host / port are accepted and ignored;
+that Client and the loaders resolve in-process; with host / port the service also serves
+the reference's ZeroMQ sockets (reth_amd.zmtp) so remote workers' Clients reach it.
+
+Blocking: as in the reference, a loader asked for a batch before the sampler is ready
+(`cnt >= max(sample_start, batch_size)` and `ready_sample`, sampler_loop.py:23-28) waits
+(torch_cuda_loader.py:94-107,152-163; numpy_loader.py:27-51): the wait drains the remote
+ingest queue as messages arrive until the shard is ready, forever by default or up to the
+loader's `timeout` seconds (TimeoutError).  A shard with no remote ingest (started without
+host / port) can only be filled by the calling thread itself, so there the wait raises
+RuntimeError at once instead of hanging.  Differences, by design:
+  * num_sampler_procs / num_procs / compress are accepted and ignored;
+  * a loader can be built before any row exists (its slots are allocated by the first
+    sample; the reference allocates them in __init__, blocking for a first batch to learn
+    the row shapes);
   * TorchCudaLoader keeps the reference's sample-ahead: batch k+1 is drawn as soon as batch
     k is handed out, i.e. before k's priority update lands (the sampler's HWM-1 PUSH).
 """
 import itertools
+import queue
+import sys
+import time
 
 import numpy as np
 import torch
@@ -48,14 +61,14 @@ class ReplayService:
         self.alive = True
 
     # ------------------------------------------------------------------ remote ingest (ZMTP)
-    def listen(self, host, port, advertise=None, hwm=10):
+    def listen(self, host, port, advertise=None, hwm=10, max_msg_size=None):
         """serve the reference's three service sockets over TCP (reth_amd.zmtp): the meta REP
         at tcp://host:port answering the JSON config (main_loop.py:64-76,162-170), the append
         PULL (main_loop.py:21-26) and the update PULL (update_proxy_loop, :79-88).  Received
         messages wait in one arrival-ordered queue of `hwm` entries (ZMQ_DEFAULT_HWM = 10,
         utils/__init__.py:12: a full queue stops the readers, and TCP stops the senders) until
-        the owner thread drains them into the HBM replay (drain(): every ready() /
-        check_ready() call, i.e. before every sample).  Returns the meta address."""
+        the owner thread drains them into the HBM replay (drain(): every ready() call, i.e.
+        before every sample, and wait_ready() as they arrive while a loader waits).  Returns the meta address."""
         import json
         import queue
 
@@ -82,11 +95,25 @@ class ReplayService:
     def drain(self):
         """apply the queued remote messages in arrival order on the calling (owner) thread:
         an append message is append_loop's work (server/main_loop.py:40-58) on the HBM shard,
-        an update message [indices, weights, step] is the sampler's update (sampler_loop.py:32-35)"""
+        an update message [indices, weights, step] is the sampler's update (sampler_loop.py:32-35).
+        Returns the number of messages taken off the queue."""
         q = getattr(self, "inbox", None)
         n = 0
-        while q is not None and not q.empty():
-            kind, frames = q.get_nowait()
+        while q is not None:
+            try:
+                item = q.get_nowait()
+            except queue.Empty:
+                break
+            self._apply(item)
+            n += 1
+        return n
+
+    def _apply(self, item):
+        """one remote message; a message that does not deserialize or does not fit the shard
+        is dropped and recorded in `ingest_errors` (the remote sender is unauthenticated: a
+        bad message must not take the owner's loop down)"""
+        kind, frames = item
+        try:
             msg = b"".join(bytes(f) for f in frames) if len(frames) > 1 else frames[0]
             if kind == "append":
                 Client(self).append_message(msg)
@@ -95,8 +122,40 @@ class ReplayService:
 
                 idx, w, step = pack.deserialize(msg)
                 Client(self).update_priorities(np.asarray(idx), np.asarray(w), step=bool(step))
-            n += 1
-        return n
+        except Exception as e:
+            if not hasattr(self, "ingest_errors"):
+                self.ingest_errors = []
+            self.ingest_errors.append(f"{kind}: {type(e).__name__}: {e}")
+            print(f"reth_buffer: dropped a malformed remote {kind} message ({type(e).__name__}: {e})",
+                  file=sys.stderr)
+
+    def wait_ready(self, timeout=None, poll=0.05):
+        """block until the sampler can serve a batch (sampler_loop.py:23-28), applying remote
+        messages as they arrive; `timeout` seconds (None: forever, as the reference) ->
+        TimeoutError.  Without remote ingest nothing but the caller could fill the shard, so
+        an unready shard raises RuntimeError at once."""
+        if self.ready():
+            return
+        q = getattr(self, "inbox", None)
+        if q is None:
+            cnt = 0 if self.replay is None else self.replay.cnt
+            raise RuntimeError(f"replay not ready: cnt={cnt} < sample_start={self.sample_start}, and the shard has "
+                               "no remote ingest (start it with host/port) -- nothing else could fill it")
+        deadline = None if timeout is None else time.monotonic() + float(timeout)
+        while True:
+            if not self.alive:
+                raise RuntimeError("replay service terminated while a loader was waiting")
+            wait = poll if deadline is None else min(poll, deadline - time.monotonic())
+            if wait <= 0:
+                cnt = 0 if self.replay is None else self.replay.cnt
+                raise TimeoutError(f"replay not ready after {timeout} s: cnt={cnt} < sample_start={self.sample_start}")
+            try:
+                item = q.get(timeout=wait)
+            except queue.Empty:
+                continue
+            self._apply(item)
+            if self.ready():
+                return
 
     def _widen(self, c):
         return self.widen_u8 is True or (isinstance(self.widen_u8, (set, list, tuple)) and c in self.widen_u8)
@@ -133,10 +192,10 @@ class ReplayService:
         return w.to(torch.int64) if self.kind == "uniform" else w
 
     def check_ready(self):
+        """non-blocking: raise RuntimeError unless a batch can be drawn now"""
         if not self.ready():
             cnt = 0 if self.replay is None else self.replay.cnt
-            raise RuntimeError(f"replay not ready: cnt={cnt} < sample_start={self.sample_start} "
-                               "(the reference sampler would block here)")
+            raise RuntimeError(f"replay not ready: cnt={cnt} < sample_start={self.sample_start}")
 
     # Process-like surface used by the reference's launch scripts
     def terminate(self):
@@ -280,8 +339,9 @@ class _RemoteClient:
 class NumpyLoader:
     """client/numpy_loader.py:8-56: (list of np columns, np.int64 indices, np.float64 weights)."""
 
-    def __init__(self, meta_addr, topic="default"):
+    def __init__(self, meta_addr, topic="default", timeout=None):
         self.svc = _lookup(meta_addr)
+        self.timeout = timeout  # seconds a sample() waits for the sampler (None: forever)
 
     def __iter__(self):
         return self
@@ -290,7 +350,7 @@ class NumpyLoader:
         return self.sample()
 
     def sample(self):
-        self.svc.check_ready()
+        self.svc.wait_ready(self.timeout)
         cols, idx, isw = self.svc.replay.sample(self.svc.batch_size)
         return [c.cpu().numpy() for c in cols], idx.cpu().numpy(), self.svc.weights_out(isw).cpu().numpy()
 
@@ -298,10 +358,12 @@ class NumpyLoader:
 class TorchCudaLoader:
     """client/torch_cuda_loader.py:69-163: a ring of `buffer_size` pre-allocated device slots;
     sample() returns views into one slot, valid until the next call (the reference recycles a
-    slot on the next sample(), :153-155)."""
+    slot on the next sample(), :153-155).  sample() waits until the sampler can serve a
+    batch (up to `timeout` seconds; None: forever, as the reference's res_queue.get())."""
 
-    def __init__(self, meta_addr, topic="default", buffer_size=8, num_procs=6, prefetch=1):
+    def __init__(self, meta_addr, topic="default", buffer_size=8, num_procs=6, prefetch=1, timeout=None):
         self.svc = _lookup(meta_addr)
+        self.timeout = timeout
         self.prefetch = int(prefetch)
         self.buffer_size = max(self.prefetch + 1, int(buffer_size))
         self._slots = None
@@ -319,7 +381,7 @@ class TorchCudaLoader:
 
     def issue(self):
         """enqueue the PER sample + gather of the next batch into a free slot"""
-        self.svc.check_ready()
+        self.svc.wait_ready(self.timeout)
         self._issue()
 
     def _issue(self):
@@ -333,9 +395,10 @@ class TorchCudaLoader:
         self._pending.append(k)
 
     def sample_device(self):
-        """(data, device int64 indices, device f64 weights) without any host sync."""
-        self.svc.check_ready()
+        """(data, device int64 indices, device f64 weights) without any host sync (once the
+        sampler is ready; before that it waits, draining the remote ingest)."""
         if not self._pending:
+            self.svc.wait_ready(self.timeout)
             self._issue()
         k = self._pending.pop(0)
         # sample-ahead: batch k+1 is drawn before batch k's priority update is enqueued (when

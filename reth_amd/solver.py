@@ -287,10 +287,13 @@ class DQNSolver(Algorithm):
 
     def apply_grads(self, probe=None):
         """dqn_solver.py:118-123: clip_grad_norm_ -> Adam -> target Interval.  probe: as in
-        fused_learner.dueling_grads, handed [("clip_adam", launch)] to issue itself"""
+        fused_learner.dueling_grads, handed [("clip_adam", launch)] to issue itself -- with
+        last=True when nothing follows it (no automatic target update), so a graph capture cut
+        there does not open an empty part"""
         if isinstance(self.optimizer, ClipAdam):
             if probe is not None:
-                probe([("clip_adam", self.optimizer.step)])
+                tail = self.auto_target_update and self._update_target_interval is not None
+                probe([("clip_adam", self.optimizer.step)], last=not tail)
             else:
                 self.optimizer.step()  # clips to optimizer.max_norm (= clip_value) itself
         else:

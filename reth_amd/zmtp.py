@@ -25,13 +25,21 @@ A PULL endpoint hands every message (a list of frame bodies) to `on_message`, wh
 block: the reader stops reading the TCP stream, so the sender's TCP window -- and then its
 own send queue -- applies the back-pressure ZMQ's high-water mark does.  A REP endpoint
 replies to each request with `on_request(body_frames)` under the request's envelope
-(every frame up to and including the empty delimiter)."""
+(every frame up to and including the empty delimiter).
+
+Message size: the endpoints are unauthenticated, so a frame header's 8-byte size is checked
+against `max_msg_size` before any buffer is allocated (the role of ZMQ_MAXMSGSIZE; a larger
+frame, or a message whose frames add up to more, closes that connection with a ZmtpError
+recorded in `Endpoint.errors`).  Any other failure of one connection -- a handler raising
+included -- ends that connection only; the listener and the other peers keep running."""
+import fcntl
 import socket
 import struct
 import threading
 
 SIGNATURE = b"\xff" + b"\x00" * 8 + b"\x7f"
 MORE, LONG, COMMAND = 1, 2, 4
+DEFAULT_MAX_MSG_SIZE = 1 << 30  # 1 GiB: far above a worker's append message (64 Pong rows = 14.5 MB)
 VALID_PEERS = {b"PULL": {b"PUSH"}, b"REP": {b"REQ", b"DEALER"}, b"PUSH": {b"PULL"}, b"REQ": {b"REP", b"ROUTER"}}
 
 
@@ -97,10 +105,11 @@ def parse_properties(data):
 class Connection:
     """one accepted TCP peer: greeting + NULL handshake, then frame I/O"""
 
-    def __init__(self, sock, socket_type):
+    def __init__(self, sock, socket_type, max_msg_size=None):
         self.sock = sock
         self.socket_type = socket_type
         self.peer_type = None
+        self.max_msg_size = DEFAULT_MAX_MSG_SIZE if max_msg_size is None else int(max_msg_size)
         self._wlock = threading.Lock()
 
     def recv_exact(self, n):
@@ -144,27 +153,72 @@ class Connection:
             self.send(encode_command(b"ERROR", bytes([len(reason)]) + reason))
             raise ZmtpError(f"{self.socket_type.decode()} endpoint refuses a {self.peer_type.decode()} peer")
 
-    def read_frame(self):
+    def read_frame(self, budget=None):
+        """(flags, body); the size is checked against `budget` (default max_msg_size) before
+        the body's buffer is allocated"""
         flags = self.recv_exact(1)[0]
         if flags & LONG:
             (size,) = struct.unpack(">Q", self.recv_exact(8))
         else:
             size = self.recv_exact(1)[0]
+        limit = self.max_msg_size if budget is None else budget
+        if size > limit:
+            raise ZmtpError(f"frame of {size} bytes exceeds the message size limit ({self.max_msg_size} bytes)")
         return flags, self.recv_exact(size)
 
     def read_message(self):
-        """the next message's frame bodies (commands in between are handled here)"""
-        frames = []
+        """the next message's frame bodies (commands in between are handled here); the
+        frames of one message together stay within max_msg_size"""
+        frames, total = [], 0
         while True:
-            flags, body = self.read_frame()
+            flags, body = self.read_frame(self.max_msg_size - total)
             if flags & COMMAND:
                 name, data = parse_command(body)
                 if name == b"PING" and len(data) >= 2:  # TTL (2 bytes) + context
                     self.send(encode_command(b"PONG", data[2:]))
                 continue
             frames.append(body)
+            total += len(body)
             if not flags & MORE:
                 return frames
+
+
+def get_local_ip():
+    """the IPv4 address of the default route's interface -- what the reference advertises
+    for a service started with host=None (reth_buffer/reth_buffer/utils/__init__.py:29-32,
+    netifaces' default gateway NIC); netifaces is absent, so the route comes from
+    /proc/net/route and the address from SIOCGIFADDR.  Falls back to the source address of
+    a (never sent) UDP datagram's route, then to the host name's address."""
+    nic = None
+    try:
+        with open("/proc/net/route") as f:
+            for line in f.readlines()[1:]:
+                p = line.split()
+                if len(p) > 7 and p[1] == "00000000" and int(p[3], 16) & 2 and p[7] == "00000000":
+                    nic = p[0]
+                    break
+    except OSError:
+        pass
+    s = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    try:
+        if nic is not None:
+            try:  # SIOCGIFADDR
+                return socket.inet_ntoa(fcntl.ioctl(s.fileno(), 0x8915, struct.pack("256s", nic.encode()[:15]))[20:24])
+            except OSError:
+                pass
+        try:
+            s.connect(("192.0.2.1", 9))  # TEST-NET-1: connect() on UDP only picks the route
+            ip = s.getsockname()[0]
+            if ip and not ip.startswith("0."):
+                return ip
+        except OSError:
+            pass
+    finally:
+        s.close()
+    try:
+        return socket.gethostbyname(socket.gethostname())
+    except OSError:
+        return "127.0.0.1"
 
 
 class Peer:
@@ -200,11 +254,12 @@ class Peer:
 class Endpoint:
     """a bound TCP listener serving ZMTP peers of one socket type (b"PULL" or b"REP")"""
 
-    def __init__(self, socket_type, handler, host="127.0.0.1", port=0):
+    def __init__(self, socket_type, handler, host="127.0.0.1", port=0, max_msg_size=None):
         if socket_type not in (b"PULL", b"REP"):
             raise ValueError("socket_type: b'PULL' or b'REP'")
         self.socket_type = socket_type
         self.handler = handler
+        self.max_msg_size = max_msg_size
         self._ls = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
         self._ls.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
         self._ls.bind((host, int(port)))
@@ -226,7 +281,7 @@ class Endpoint:
             except OSError:
                 return
             s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
-            c = Connection(s, self.socket_type)
+            c = Connection(s, self.socket_type, self.max_msg_size)
             self._conns.append(c)
             threading.Thread(target=self._serve, args=(c,), daemon=True).start()
 
@@ -245,6 +300,8 @@ class Endpoint:
             pass
         except ZmtpError as e:
             self.errors.append(str(e))
+        except Exception as e:  # a failing handler (or anything else) ends this connection only
+            self.errors.append(f"{type(e).__name__}: {e}")
         finally:
             try:
                 c.sock.close()

@@ -1,0 +1,51 @@
+#!/bin/bash
+# round-5 GPU steps (each under its own limit; stop on a crash / timeout)
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() {
+  local name=$1 limit=$2; shift 2
+  echo "== $name ($(date +%T))"
+  timeout -k 10 "$limit" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc"; tail -n 4 "gpurun_out/$name.log" | cut -c1-600
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+}
+pmc() {  # one rocprofv3 counter pass over a script: pmc NAME SCRIPT COUNTERS...
+  local name=$1 script=$2; shift 2
+  echo "== pmc $name ($(date +%T))"
+  timeout -s KILL 120 rocprofv3 --pmc "$@" --kernel-trace --output-format csv -d "$PWD/gpurun_out/pmc_$name" \
+      -o run -- python "$script" > "gpurun_out/pmc_$name.log" 2>&1
+  local rc=$?
+  echo "pmc $name rc=$rc"; tail -n 3 "gpurun_out/pmc_$name.log"
+  [ $rc -eq 0 ] || exit $rc
+}
+summ() {  # print ms/step and the roofline fields of bench logs
+  for f in "$@"; do python - "$f" <<'PY'
+import json, sys
+d = json.loads([l for l in open(sys.argv[1]) if l.startswith('{"metric"')][-1])
+h = {r["kernel"]: r["mean_launch_us"] for r in d.get("roofline_hbm", [])}
+print(sys.argv[1], d["ms_per_step"], d.get("ms_per_step_windows"), "conv2", d["roofline"].get("mean_launch_us"),
+      d["roofline"]["frac"], {k: h[k] for k in sorted(h)})
+PY
+  done
+}
+for s in "$@"; do
+  case "$s" in
+    bench) step bench 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    benchlong) step bench_long 600 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+      summ gpurun_out/bench_long.log ;;
+    fwdpmc)  # SQ counters for the torso forward kernels at the learner's 1,024 samples
+      export CONV_LAYERS=1,2,3
+      pmc fwd_sq scripts/conv_pmc.py SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+          SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT
+      pmc fwd_inst scripts/conv_pmc.py GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES \
+          SQ_LDS_IDX_ACTIVE
+      unset CONV_LAYERS ;;
+    tests) step gpu_tests 1100 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    t:*) f=${s#t:}; step "t_$(basename ${f//,/_} .py)" 900 python -u -m pytest -x -v --timeout 300 \
+          --timeout-method thread ${f//,/ } ;;
+  esac
+done

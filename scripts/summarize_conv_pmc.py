@@ -48,7 +48,9 @@ def main():
                        ("pmc_f32", "the fp32-MFMA conv3 (RTH_CONV_F32MFMA=1 path; r03 mid-round build)"),
                        ("pmc_x9", "the exact-split bf16 kernels for conv2 (opt-in) and conv3 (scripts/pmc_x9.sh)"),
                        ("pmc_bwd", "the backward kernels at B = 512: x9 data gradients (conv2 classes, conv3) and the "
-                                   "x9 weight gradients (scripts/r04.sh bwdpmc)")):
+                                   "x9 weight gradients (scripts/r04.sh bwdpmc)"),
+                       ("pmc_fwd", "the torso forward at 1,024 samples: conv1 bf16x3, conv2 fp32 MFMA, conv3 x9 "
+                                   "(scripts/r05.sh fwdpmc)")):
         passes = {p: load(f"{fam}_{p}") for p in ("sq", "inst", "fetch", "write", "l2", "ic")}
         keys = sorted(set().union(*[set(d) for d in passes.values()]))
         if not keys:

@@ -32,7 +32,7 @@ def say(**kw):
 
 dev = torch.device("cuda:0")
 
-def run(dp_hook, iters=40):
+def run(dp_hook, iters=40, keep=False):
     cfg = ApexConfig(n_actors=16, capacity=2048, batch_size=64, sample_start=128, seed=4, hip_graph=True,
                      send_weights_interval=3, recv_weights_interval=4, update_target_interval=7, dp_hook=dp_hook)
     ax = ApexDQN(cfg, device=dev, rank=0, world=1)
@@ -41,8 +41,10 @@ def run(dp_hook, iters=40):
     torch.cuda.synchronize()
     parts = sorted({len(v) for v in ax._graphs["learn"].values()}) if ax._graphs else []
     params = torch.cat([p.detach().flatten() for p in ax.solver._params]).cpu()
+    if keep:  # the captured graphs, the side streams and the bucket buffers stay alive
+        return params, parts, ax
     ax.close()
-    return params, parts
+    return params, parts, None
 
 dist.init_process_group("nccl", init_method="tcp://127.0.0.1:" + sys.argv[2], rank=0, world_size=1)
 say(stage="init", backend=dist.get_backend())
@@ -50,14 +52,30 @@ t = torch.arange(8, dtype=torch.float32, device=dev)
 dist.all_reduce(t)
 torch.cuda.synchronize()
 say(stage="all_reduce", ok=bool(torch.equal(t.cpu(), torch.arange(8, dtype=torch.float32))))
-hooked, parts = run(True)
+mode = sys.argv[3]
+hooked, parts, alive = run(True, keep=mode != "keep")
 say(stage="hooked", parts=parts)
-plain, parts0 = run(False)
+plain, parts0, _ = run(False)
 say(stage="plain", parts=parts0, equal=bool(torch.equal(hooked, plain)))
-if sys.argv[3] == "destroy":
+if mode == "keep":
+    os._exit(0)
+if mode == "destroy_alive":  # the group destroyed while the hooked loop's graphs are still alive
+    for _ in range(3):  # the comm stream has just carried RCCL work
+        alive.iteration()
     dist.destroy_process_group()
     say(stage="destroyed")
-os._exit(0)
+    import gc
+    alive.close()
+    del alive
+    gc.collect()
+    torch.cuda.synchronize()
+    say(stage="closed")
+else:  # "shutdown": bench.py's teardown (reth_amd.dist.shutdown: graphs released, then the group)
+    from reth_amd.dist import shutdown
+    alive.iteration()
+    shutdown(alive)
+    say(stage="destroyed", initialized=dist.is_initialized())
+# a normal interpreter exit: HIP / RCCL / graph destructors run
 '''
 
 
@@ -94,9 +112,19 @@ def test_rccl_one_rank_bucketed_learner():
     assert rc == 0, (rc, err)
 
 
-def test_rccl_process_group_teardown():
-    """dist.destroy_process_group() after the RCCL work (bench.py at N > 1 leaves without it,
-    after its last collective: DESIGN.md (e))"""
-    rc, st, err = _child("destroy")
-    assert "plain" in st, (rc, st, err)
-    assert "destroyed" in st and rc == 0, (rc, err)
+def test_rccl_process_group_teardown_with_graphs_alive():
+    """dist.destroy_process_group() while the bucketed learner's captured graphs, its RCCL side
+    stream and bucket buffers are all still alive and have just run -- the state DESIGN.md (e)
+    once recorded an abort in -- then the graphs released and a normal interpreter exit"""
+    rc, st, err = _child("destroy_alive")
+    assert "plain" in st and st["plain"]["equal"], (rc, st, err)
+    assert "destroyed" in st and "closed" in st, (rc, st, err)
+    assert rc == 0, (rc, err)
+
+
+def test_rccl_bench_shutdown():
+    """bench.py's multi-rank exit (reth_amd.dist.shutdown): graphs released, group destroyed,
+    normal interpreter exit with rc 0"""
+    rc, st, err = _child("shutdown")
+    assert "destroyed" in st and st["destroyed"]["initialized"] is False, (rc, st, err)
+    assert rc == 0, (rc, err)

@@ -135,3 +135,47 @@ def test_worker_process_feeds_the_hbm_replay(orc, dev):
             assert np.array_equal(v[sl], orc.per_normalize(w, 0.5).astype(np.float64))
     finally:
         svc.terminate()
+
+
+def test_loader_waits_for_a_worker_started_after_it(dev):
+    """the reference trainer's order (test/apex-dqn/trainer.py:22-34): the shard and its
+    TorchCudaLoader exist before any worker has sent a row; the first sample() waits -- as
+    torch_cuda_loader.py:94-107,152-163 and sampler_loop.py:23-28 do -- draining the remote
+    appends as they arrive, then returns rows bit-identical to the worker's"""
+    from reth_amd.reth_buffer import NumpyLoader, TorchCudaLoader, start_per
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    batches, seed = 4, 5
+    svc, addr = start_per(1024, 32, alpha=0.5, sample_start=64 * batches, host="127.0.0.1", port=0, device=dev,
+                          widen_u8={0, 3})
+    try:
+        loader = TorchCudaLoader(addr, buffer_size=4, num_procs=2, timeout=180)  # no rows yet
+        with pytest.raises(TimeoutError):
+            NumpyLoader(addr, timeout=0.2).sample()  # nothing sent yet: a bounded wait ends
+        env = dict(os.environ, HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="", PYTHONPATH=root)
+        p = subprocess.Popen([sys.executable, "-c", WORKER, addr, os.path.join(root, "reth_amd", "compat"), str(seed),
+                              str(batches)], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+        t0 = time.time()
+        data, idx, w = loader.sample()  # blocks until 256 rows are in
+        waited = time.time() - t0
+        out, err = p.communicate(timeout=60)
+        assert p.returncode == 0 and "sent" in out, err
+        assert svc.replay.cnt >= 64 * batches and waited > 0
+        rng = np.random.default_rng(seed)
+        ref = [[] for _ in range(5)]
+        for _ in range(batches):
+            s0 = rng.integers(0, 256, (64, 4, 84, 84)).astype("f4")
+            s1 = rng.integers(0, 256, (64, 4, 84, 84)).astype("f4")
+            a = rng.integers(0, 6, 64).astype("i8")
+            r = rng.choice(np.array([-1, 0, 1], "f4"), 64)
+            d = (rng.random(64) < 0.01).astype("f4")
+            rng.random(64)
+            for k, c in enumerate((s0, a, r, s1, d)):
+                ref[k].append(c)
+        ref = [np.concatenate(c) for c in ref]
+        assert idx.shape == (32,) and w.dtype == torch.float64
+        for o, c in zip(data, ref):
+            assert np.array_equal(o.cpu().numpy(), c[idx])
+        assert not getattr(svc, "ingest_errors", None)
+    finally:
+        svc.terminate()

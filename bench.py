@@ -87,7 +87,8 @@ def replay_storage(ax):
     if rep.frames is None:
         return {"kind": "full rows (uint8 stacks)", "rows_gb": round(rows / 1e9, 2)}
     fb = rep.frames.numel()
-    return {"kind": "frame store (each frame once; rows hold frame ids)", "rows_gb": round(rows / 1e9, 3),
+    return {"kind": "frame store (each frame once; rows hold frame ids)", "bound": ax.cfg.frame_store_bound,
+            "rows_gb": round(rows / 1e9, 3),
             "frames": int(rep.frames.shape[0]), "frame_store_gb": round(fb / 1e9, 2),
             "total_gb": round((rows + fb) / 1e9, 2),
             "full_rows_would_be_gb": round(rep.capacity * (2 * STACK + 16) / 1e9, 2)}
@@ -613,8 +614,11 @@ def main():
                     help="frame de-duplicated replay (SURVEY §8(d) C3; the default since r04): each actor frame "
                          "stored once in an HBM frame store, rows keep their stacks as frame ids, the gather "
                          "assembles them -- bit-identical rows and updates (tests/test_frame_store_gpu.py), Pong's 1 M "
-                         "rows in 7.3 GB instead of 56.5, Breakout's 4 M in 29.1 instead of 225.9, and no 56 KB stack "
-                         "copies per inserted row (Pong 0.563-0.564 vs 0.571-0.574 ms/step interleaved)")
+                         "rows in 14.1 GB instead of 56.5 (hard bound), Breakout's 4 M in 56.7 instead of 225.9, and no "
+                         "56 KB stack copies per inserted row (Pong 0.563-0.564 vs 0.571-0.574 ms/step interleaved)")
+    ap.add_argument("--frame-store-bound", choices=["hard", "expected"], default="hard",
+                    help="frame store size: hard = the worst case (2 frames per actor step: no live row's frames are "
+                         "ever overwritten); expected = sized for the i.i.d. episode-end rate (half the bytes)")
     ap.add_argument("--full-rows", dest="frame_store", action="store_false",
                     help="store both uint8 stacks of every row, as the reference's worker does (worker.py:44-51)")
     ap.add_argument("--no-sweep", action="store_true", help="skip the decoupled-actor measurements after the "
@@ -674,7 +678,7 @@ def main():
                      actor_steps_per_update=args.actor_steps_per_update, seed=0,
                      channels_last=not args.nchw, conv_benchmark=not args.no_conv_benchmark,
                      hip_graph=not args.eager, hip_conv=hip_conv, env=args.env, frame_store=args.frame_store,
-                     extra={"learner_priority": int(os.environ.get("RTH_LEARNER_PRIORITY", "0")),
+                     frame_store_bound=args.frame_store_bound, extra={"learner_priority": int(os.environ.get("RTH_LEARNER_PRIORITY", "0")),
                             "probe_conv2": probe})
     ax = ApexDQN(cfg, device=dev, rank=rank, world=world)
     ax.prefill(cfg.capacity)

@@ -72,6 +72,7 @@ class ApexConfig:
     tuned_gemm: bool = True        # TunableOp solution selection for the library GEMMs (reth_amd.gemm_tuning)
     env: str = "synthetic"         # actors' observations: synthetic | atari | atari-h2d (VecActors)
     frame_store: bool = False      # frame de-duplicated replay: each frame stored once, rows as frame ids
+    frame_store_bound: str = "hard"  # store size: "hard" (worst case, 2 frames per actor step) | "expected" (p_done)
     extra: dict = field(default_factory=dict)
 
 
@@ -134,10 +135,18 @@ class ApexDQN:
     @staticmethod
     def frame_store_frames(cfg):
         """frames the store must hold (rth_replay_frames_attach): every frame a live row
-        references.  A row lives capacity / N actor steps after its append; its oldest frame
-        is at most n + 4 steps older than the append; each step adds N frames plus one per
-        ended episode (p_done N) -- so capacity (1 + p_done) + (n + 8) N, with the reset term
-        doubled and at least capacity / 64 as headroom (the prefill needs capacity + 7)"""
+        references.  A row lives capacity / N actor steps after its append and its oldest
+        frame is at most n + 4 steps older than the append.  Each step adds N frames plus one
+        per ended episode, so at most 2 N: "hard" sizes for that worst case -- 2 capacity +
+        2 (n + 16) N, no frame a live row references is ever overwritten, whatever the episode
+        lengths (Pong 1 M rows: 14.1 GB of frames; Breakout 4 M: 56.5 GB).  "expected" sizes for
+        the i.i.d. episode-end rate p_done instead -- capacity (1 + 2 p_done), at least
+        capacity / 64 of headroom, + (n + 16) N: half the bytes, but a burst of episode ends
+        beyond that rate would overwrite frames that old rows still name."""
+        if cfg.frame_store_bound == "hard":
+            return 2 * cfg.capacity + 2 * (cfg.n_step + 16) * cfg.n_actors + 16
+        if cfg.frame_store_bound != "expected":
+            raise ValueError(f"frame_store_bound {cfg.frame_store_bound!r}: 'hard' or 'expected'")
         reset = max(cfg.capacity // 64, int(2 * cfg.capacity * cfg.p_done) + 1)
         # + 8 N: the actors' initial stacks, pushed at construction and again behind a prefill
         return cfg.capacity + reset + (cfg.n_step + 16) * cfg.n_actors + 16

@@ -28,6 +28,7 @@
 // a k-ordered fmaf chain), then + bias, then ReLU -- the same operations as conv -> bias ->
 // relu, summed in a different order than MIOpen's or the reference's CPU convolution.
 #include <cstdlib>
+#include <mutex>
 #include <type_traits>
 
 #include "common.hpp"
@@ -1696,11 +1697,15 @@ static bool is_dgrad2_x9(const rth_conv_shape *shape) {
 }
 
 // the per-device packed-kernel workspace of one dgrad geometry (allocated on first use, which
-// must not be inside a graph capture)
+// must not be inside a graph capture; the allocation is serialised across host threads).  It is
+// shared by every caller of the NULL-workspace form on that device: that form is for one stream
+// at a time (include/reth_hip.h, rth_conv_dgrad); concurrent learners pass their own workspace.
 static int dgrad_workspace(u32x4 **ws, size_t bytes, hipStream_t st, u32x4 **out) {
+  static std::mutex mu;
   int dev = 0;
   RTH_HIP(hipGetDevice(&dev));
   RTH_REQUIRE(dev >= 0 && dev < 64, "rth_conv_dgrad: device %d out of range", dev);
+  std::lock_guard<std::mutex> lock(mu);
   if (!ws[dev]) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     RTH_REQUIRE(hipStreamIsCapturing(st, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone,

@@ -255,7 +255,10 @@ class HbmReplay:
         self._h = h.value
         # frame_store (int): the frame de-duplicated replay -- FrameColumn stacks as frame ids
         # into a ring of that many frames (rth_replay_frames_attach); frames / frame_head are
-        # device views of the store and its head
+        # device views of the store and its head.  The ring must outlive every live row's
+        # frames: frame ids are taken mod its size, so a ring smaller than the frames pushed
+        # during a row's life silently hands that row newer frames (ApexDQN.frame_store_frames
+        # gives the worst-case size: 2 frames per actor step)
         self.frames = self.frame_head = None
         fcols = [c for c in self.columns if getattr(c, "frames", False)]
         if frame_store is not None or fcols:

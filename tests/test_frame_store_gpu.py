@@ -24,12 +24,12 @@ def _deterministic_learner(monkeypatch):
     monkeypatch.setattr(fused_learner, "HIP_WGRAD", "x9")
 
 
-def _run(dev, frame_store, graph, iters=150, env="synthetic"):
+def _run(dev, frame_store, graph, iters=150, env="synthetic", bound="hard"):
     from reth_amd.apex import ApexConfig, ApexDQN
 
     cfg = ApexConfig(n_actors=16, capacity=1024, batch_size=32, sample_start=64, p_done=0.25, seed=6,
                      hip_graph=graph, send_weights_interval=3, recv_weights_interval=4, update_target_interval=5,
-                     frame_store=frame_store, env=env)
+                     frame_store=frame_store, env=env, frame_store_bound=bound)
     ax = ApexDQN(cfg, device=dev)
     for _ in range(iters):
         ax.iteration()
@@ -50,10 +50,13 @@ def _run(dev, frame_store, graph, iters=150, env="synthetic"):
     return out
 
 
-@pytest.mark.parametrize("graph", [False, True])
-def test_frame_store_loop_bit_identical_to_full_rows(dev, graph):
-    full = _run(dev, False, graph)
-    fs = _run(dev, True, graph)
+@pytest.mark.parametrize("graph,bound", [(False, "expected"), (True, "hard")])
+def test_frame_store_loop_bit_identical_to_full_rows(dev, graph, bound):
+    """both store sizes: "hard" (the default: 2 frames per actor step, no row's frames ever
+    overwritten) and "expected" (p_done's rate; p_done = 0.25 i.i.d. here)"""
+    iters = 230 if bound == "hard" else 150  # enough frames to wrap the larger ring too
+    full = _run(dev, False, graph, iters=iters)
+    fs = _run(dev, True, graph, iters=iters, bound=bound)
     assert full["info"] == fs["info"] and full["updates"] == fs["updates"] > 50
     assert fs["info"][0] == 1024 and fs["head"] > fs["F"], "the FIFO and the frame ring must both have wrapped"
     names = ["s0", "a", "r", "s1", "done"]
@@ -78,10 +81,14 @@ def test_frame_store_atari_env(dev):
 
 def test_frame_store_prefill_and_footprint(dev):
     """the prefill's synthetic trajectory: row j's stacks are frames j .. j+3 and j+3 .. j+6 of
-    it; the store holds capacity (1 + reset headroom) frames: the HBM footprint"""
+    it; the store holds capacity (1 + reset headroom) frames with the "expected" bound, 2
+    capacity with the "hard" one: the HBM footprint"""
     from reth_amd.apex import ApexConfig, ApexDQN
 
-    cfg = ApexConfig(n_actors=16, capacity=2048, batch_size=32, seed=2, hip_graph=False, frame_store=True)
+    hard = ApexDQN.frame_store_frames(ApexConfig(n_actors=16, capacity=2048, frame_store=True))
+    assert hard == 2 * 2048 + 2 * (3 + 16) * 16 + 16
+    cfg = ApexConfig(n_actors=16, capacity=2048, batch_size=32, seed=2, hip_graph=False, frame_store=True,
+                     frame_store_bound="expected")
     ax = ApexDQN(cfg, device=dev)
     ax.prefill(cfg.capacity)
     torch.cuda.synchronize()

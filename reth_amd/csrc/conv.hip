@@ -424,6 +424,139 @@ __global__ __launch_bounds__(256) void k_conv1_u8_bf16x3(const void *__restrict_
   }
 }
 
+// conv1 with each stack byte converted once per horizontal window pair (r05).  Horizontally
+// adjacent output pixels' windows overlap by half (kernel 8, stride 4): kw 4..7 of pixel ox are
+// kw 0..3 of pixel ox + 1.  So a lane loads and converts only the first half (4 bytes) of each
+// of its 16 runs and takes the second half, already converted, from the next lane (DPP
+// wave_shl:1).  For that the lanes walk VIRTUAL pixels: 21 per output row, the 21st (ox = 20,
+// input columns 80..83: inside the 84-wide row) exists only to hand its first halves to ox = 19,
+// and each 32-lane tile covers 31 virtual pixels, its lane 31 being the next one, a helper for
+// lane 30 (wave_shl:1 moves lane 32 into lane 31: the helper's own second half is garbage, and it
+// stores nothing).  Same packed weights, same k order (kw 0..7 of run (ci, kh)), same MFMA
+// chain per output as k_conv1_u8_bf16x3: the outputs are bit-identical.  Half the byte loads and
+// conversions per tile; 29.5 of 32 lanes produce an output (20 / 21 x 31 / 32).
+constexpr int kC1VPix = 21;       // virtual pixels per output row
+constexpr int kC1VPerTile = 31;   // virtual pixels a 32-lane tile outputs
+#ifndef C1_NBUF_SHARE
+#define C1_NBUF_SHARE 2  // r05 A/B: 2 tiles in flight 26.0 us alone at 1,024 samples, 3: 27.3, 1: 30.7
+#endif
+constexpr int kC1BufShare = C1_NBUF_SHARE;  // tiles in flight (16 dwords each)
+
+// 4 bytes (kw 0..3 of one stack row) -> 4 bf16 in two dwords (exact)
+__device__ __forceinline__ void u8x4_to_bf16(uint32_t v, uint32_t &lo, uint32_t &hi) {
+  const uint32_t a = __float_as_uint((float)(v & 0xffu)), b = __float_as_uint((float)((v >> 8) & 0xffu));
+  const uint32_t c = __float_as_uint((float)((v >> 16) & 0xffu)), d = __float_as_uint((float)(v >> 24));
+  lo = __builtin_amdgcn_perm(b, a, 0x07060302u);
+  hi = __builtin_amdgcn_perm(d, c, 0x07060302u);
+}
+
+__device__ __forceinline__ uint32_t from_next_lane(uint32_t v) {  // lane i <- lane i + 1
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x130 /* wave_shl:1 */, 0xf, 0xf, false);
+}
+
+__device__ unsigned char g_conv1_sink[64 * 128];  // stores of lanes without an output (never read)
+
+__global__ __launch_bounds__(256) void k_conv1_u8_share(const void *__restrict__ x, const int64_t *__restrict__ rows,
+                                                      int64_t n, const int64_t *__restrict__ n_dev,
+                                                      const float *__restrict__ w, const float *__restrict__ bias,
+                                                      float *__restrict__ y) {
+  constexpr int HIN = 84, WIN = 84, WOUT = 20, PIX = 400, S = 4, COUT = 32;
+  constexpr int VPS = WOUT * kC1VPix;  // 420 virtual pixels per sample
+  constexpr int64_t STACK = 4 * HIN * WIN;
+  using f32x16 = __attribute__((ext_vector_type(16))) float;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  if (n_dev) {
+    const int64_t m = *n_dev;
+    n = m < n ? (m > 0 ? m : 0) : n;
+  }
+  // 32-bit pixel arithmetic: the launcher requires n * 420 < 2^31
+  const int VP = (int)n * VPS, tiles = (VP + kC1VPerTile - 1) / kC1VPerTile, tstride = (int)gridDim.x * 4;
+  int tile = (int)blockIdx.x * 4 + wave;
+  if (tile >= tiles) return;  // no barriers below
+  const uint8_t *xb = static_cast<const uint8_t *>(x);
+  // virtual pixel r of tile t: (sample, oy, ox in 0..20); past the end: the last one
+  auto vpix = [&](int t, int &b, int &oy, int &ox) {
+    int v = t * kC1VPerTile + r;
+    if (v >= VP) v = VP - 1;
+    b = (int)((unsigned)v / (unsigned)VPS);
+    const int rem = v - b * VPS;
+    oy = rem / kC1VPix;
+    ox = rem - oy * kC1VPix;
+  };
+  auto window = [&](int t) -> const uint8_t * {
+    int b, oy, ox;
+    vpix(t, b, oy, ox);
+    const int64_t row = rows ? rows[b] : b;
+    return xb + row * STACK + ((S * oy) * WIN + S * ox);
+  };
+  auto run_off = [&](int c) -> int {
+    const int rho = 2 * c + h;
+    return (rho >> 3) * HIN * WIN + (rho & 7) * WIN;
+  };
+  const u32x4 *wp = reinterpret_cast<const u32x4 *>(w);
+  bf16x8 wf[kC1Chunks][3];
+#pragma unroll
+  for (int c = 0; c < kC1Chunks; ++c)
+#pragma unroll
+    for (int t = 0; t < 3; ++t) wf[c][t] = __builtin_bit_cast(bf16x8, wp[(c * 3 + t) * 64 + lane]);
+  // (the bias is re-read per tile from L1 / L2 in the epilogue: 16 registers fewer than
+  // r04's kernel keeps, which spilled its weights into AGPRs)
+  const float4 *bias4 = reinterpret_cast<const float4 *>(bias) + h;
+
+  constexpr int NB = kC1BufShare;
+  uint32_t raw[NB][kC1Chunks];  // the first halves of the runs, a ring of tiles in flight
+  auto load = [&](uint32_t (&dst)[kC1Chunks], int t) {
+    const uint8_t *p = window(t);
+#pragma unroll
+    for (int c = 0; c < kC1Chunks; ++c) dst[c] = *reinterpret_cast<const uint32_t *>(p + run_off(c));
+  };
+  auto compute = [&](const uint32_t (&src)[kC1Chunks], int t) {
+    f32x16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
+#pragma unroll
+    for (int c = 0; c < kC1Chunks; ++c) {
+      uint32_t lo, hi;
+      u8x4_to_bf16(src[c], lo, hi);
+      const uint32_t lo2 = from_next_lane(lo), hi2 = from_next_lane(hi);  // kw 4..7 = the next pixel's kw 0..3
+      const bf16x8 xf = __builtin_bit_cast(bf16x8, (u32x4{lo, hi, lo2, hi2}));
+#pragma unroll
+      for (int tm = 0; tm < 3; ++tm) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[c][tm], xf, acc, 0, 0, 0);
+    }
+    // lane r holds virtual pixel r's outputs; virtual column 20, the helper lane 31 and lanes
+    // past the end store into the sink (no branch around the stores)
+    int b, oy, ox;
+    vpix(t, b, oy, ox);
+    const bool out = r < kC1VPerTile && ox < WOUT && t * kC1VPerTile + r < VP;
+    float *dst = out ? y + ((int64_t)b * PIX + oy * WOUT + ox) * COUT
+                     : reinterpret_cast<float *>(g_conv1_sink) + lane * 32;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const float4 bv = bias4[2 * g];  // channels 8g + 4h .. + 3
+      float4 o;
+      o.x = relu_c(radd(acc[4 * g + 0], bv.x));
+      o.y = relu_c(radd(acc[4 * g + 1], bv.y));
+      o.z = relu_c(radd(acc[4 * g + 2], bv.z));
+      o.w = relu_c(radd(acc[4 * g + 3], bv.w));
+      *reinterpret_cast<float4 *>(dst + 8 * g + 4 * h) = o;
+    }
+  };
+#pragma unroll
+  for (int i = 0; i + 1 < NB; ++i) load(raw[i], tile + i * tstride < tiles ? tile + i * tstride : tiles - 1);
+  for (;;) {
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int ahead = tile + (NB - 1) * tstride;
+      load(raw[(i + NB - 1) % NB], ahead < tiles ? ahead : tiles - 1);
+      compute(raw[i], tile);
+      tile += tstride;
+      if (tile >= tiles) return;
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void k_conv1_pack_bf16x3(const float *__restrict__ w, u32x4 *__restrict__ packed) {
   pack_conv1_bf16x3(w, packed, blockIdx.x * 256 + threadIdx.x);
 }
@@ -890,7 +1023,7 @@ struct ConvLaunch {
   int lds_bytes;  // packed weight bytes
   int per_cu;  // resident workgroups per CU (occupancy query, cached)
   int tile_px;  // output pixels per wave tile
-  int bf16x3;   // k_conv1_u8_bf16x3 (conv1 on uint8 stacks, exact-split bf16 MFMA)
+  int bf16x3;   // conv1 on uint8 stacks, exact-split bf16 MFMA: 1 = k_conv1_u8_bf16x3, 2 = k_conv1_u8_share
   int nsplit;   // wave tiles per pixel tile (channel parts; 0 = 1)
   int x9;       // k_conv_x9: samples per workgroup at most (0 = not an x9 kernel)
   const void *x9fn[5];  // k_conv_x9 by samples per workgroup (nullptr: not built)
@@ -927,9 +1060,16 @@ static ConvLaunch conv_launch() {
   return l;
 }
 
+// RTH_CONV1_NOSHARE=1: r04's kernel (every lane converts its whole window; A/B)
 static ConvLaunch conv1_bf16x3_launch() {
-  ConvLaunch l{reinterpret_cast<const void *>(&k_conv1_u8_bf16x3), reinterpret_cast<const void *>(&k_conv1_pack_bf16x3),
-               4, kC1PackedBytes, 0, 32, 1, 0, 0, {}, nullptr, 0, 0};
+  static const bool noshare = [] {
+    const char *e = getenv("RTH_CONV1_NOSHARE");
+    return e && atoi(e) != 0;
+  }();
+  ConvLaunch l{noshare ? reinterpret_cast<const void *>(&k_conv1_u8_bf16x3)
+                       : reinterpret_cast<const void *>(&k_conv1_u8_share),
+               reinterpret_cast<const void *>(&k_conv1_pack_bf16x3), 4, kC1PackedBytes, 0, 32, noshare ? 1 : 2, 0, 0,
+               {}, nullptr, 0, 0};
   int blocks = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, l.fn, 256, 0) != hipSuccess || blocks < 1) blocks = 1;
   l.per_cu = blocks;
@@ -1990,7 +2130,11 @@ static int conv_bias_relu(const rth_conv_shape *shape, const void *x, const int6
     return RTH_OK;
   }
   const int hout = (shape->hin - shape->kh) / shape->stride + 1, wout = (shape->win - shape->kw) / shape->stride + 1;
-  const int64_t tiles = (n * hout * wout + l.tile_px - 1) / l.tile_px * (l.nsplit > 1 ? l.nsplit : 1);
+  // (k_conv1_u8_share, bf16x3 == 2: 31 virtual pixels of 21 per output row per tile)
+  RTH_REQUIRE(l.bf16x3 != 2 || n * hout * kC1VPix < ((int64_t)1 << 31),
+              "rth_conv_bias_relu: %lld conv1 samples exceed the kernel's 32-bit pixel index", (long long)n);
+  const int64_t tiles = l.bf16x3 == 2 ? (n * hout * kC1VPix + kC1VPerTile - 1) / kC1VPerTile
+                                      : (n * hout * wout + l.tile_px - 1) / l.tile_px * (l.nsplit > 1 ? l.nsplit : 1);
   int64_t grid = (tiles + l.waves - 1) / l.waves;
   // persistent: at most wg_per_cu() workgroups per CU (each stages the weights once)
   const int cap = wg_per_cu();

@@ -43,6 +43,40 @@ for s in "$@"; do
       pmc fwd_inst scripts/conv_pmc.py GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES \
           SQ_LDS_IDX_ACTIVE
       unset CONV_LAYERS ;;
+    adambench) step adam_alone1 120 python scripts/bench_adam.py
+      RTH_ADAM_ONE_PASS=1 step adam_alone2 120 python scripts/bench_adam.py
+      step adam_prof 120 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/adam_prof" -o run \
+          -- python scripts/bench_adam.py  # (the two-launch default)
+      python - <<'PY'
+import csv, collections
+d = collections.defaultdict(list)
+for r in csv.DictReader(open("gpurun_out/adam_prof/run_kernel_trace.csv")):
+    if "adam" in r["Kernel_Name"] or "sqsum" in r["Kernel_Name"]:
+        d[r["Kernel_Name"][:60]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+for k, v in d.items():
+    v.sort(); print(k, len(v), "median us", v[len(v) // 2], "min", v[0])
+PY
+      ;;
+    adamab)  # one-launch clip+Adam vs the two-launch form, interleaved
+      for r in 1 2; do
+        RTH_ADAM_ONE_PASS=1 step ab_adam1_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        step ab_adam2_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+      done
+      summ gpurun_out/ab_adam*.log ;;
+    c1ab)  # conv1: each byte converted once per window pair (k_conv1_u8_share) vs r04's kernel
+      step c1_tests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_conv_gpu.py
+      CONV_NS=1024,512,256 step c1_micro_share 120 python scripts/bench_conv.py
+      RTH_CONV1_NOSHARE=1 CONV_NS=1024,512,256 step c1_micro_noshare 120 python scripts/bench_conv.py
+      RTH_LIB_PATH=reth_amd/libreth_hip_c1nb2.so CONV_NS=1024,512,256 step c1_micro_nb2 120 python scripts/bench_conv.py
+      RTH_LIB_PATH=reth_amd/libreth_hip_c1nb1.so CONV_NS=1024,512,256 step c1_micro_nb1 120 python scripts/bench_conv.py
+      grep -h "conv1" gpurun_out/c1_micro_*.log
+      for r in 1 2; do
+        step c1ab_share_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        RTH_CONV1_NOSHARE=1 step c1ab_noshare_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        RTH_LIB_PATH=reth_amd/libreth_hip_c1nb2.so step c1ab_nb2_$r 300 python bench.py --steps 300 --warmup 5 \
+            --no-cpu-baseline --no-sweep
+      done
+      summ gpurun_out/c1ab_*.log ;;
     tests) step gpu_tests 1100 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     t:*) f=${s#t:}; step "t_$(basename ${f//,/_} .py)" 900 python -u -m pytest -x -v --timeout 300 \

@@ -45,7 +45,8 @@ LEARNER_GATHER_GRID = copy_grid(512)
 HBM_KERNELS = {"k_tree_update_sub": ("k_tree_update_sub", None), "k_tree_sample": ("k_tree_sample", None),
                "k_copy_rows (gather)": ("k_copy_rows", "gather"), "k_copy_rows (insert)": ("k_copy_rows", "insert"),
                "k_actor_tail": ("k_actor_tail", None), "k_td_heads_backward": ("k_td_heads_backward", None),
-               "k_adam": ("k_adam", None), "k_grad_sqsum": ("k_grad_sqsum", None)}
+               "k_adam": ("k_adam", None), "k_grad_sqsum": ("k_grad_sqsum", None),
+               "rth_clip_adam (k_clip_adam_fused)": ("k_clip_adam_fused", None)}
 # output bytes per sample of the conv forwards (float32): conv2 writes [81 pixels x 64] NHWC,
 # conv3 [64 x 49] NCHW -- a dispatch's WRITE_SIZE says how many samples it ran (the grid does
 # not: the conv kernels loop over the samples)
@@ -94,7 +95,8 @@ def main():
         ts = [r for r in rows if "k_tree_sample" in r["Kernel_Name"]]
         start = int(ts[-steps]["Start_Timestamp"])  # one PER sample per iteration
         # ... up to the last learner update (the bench's isolated gather / conv timings follow)
-        end = max(int(r["End_Timestamp"]) for r in rows if "k_adam" in r["Kernel_Name"])
+        end = max(int(r["End_Timestamp"]) for r in rows if "k_adam" in r["Kernel_Name"] or
+                  "k_clip_adam_fused" in r["Kernel_Name"])
         win = [r for r in rows if start <= int(r["Start_Timestamp"]) <= end]
         agg = collections.defaultdict(lambda: [0, 0])
         for r in win:
@@ -102,7 +104,8 @@ def main():
             a[0] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
             a[1] += 1
         busy = sum(v[0] for v in agg.values())
-        learner_stream = next((r.get("Stream_Id") for r in reversed(win) if "k_adam" in r["Kernel_Name"]), None)
+        learner_stream = next((r.get("Stream_Id") for r in reversed(win) if "k_adam" in r["Kernel_Name"] or
+                               "k_clip_adam_fused" in r["Kernel_Name"]), None)
         with open(os.path.join(PROF, f"{tag}_steady_state.txt"), "w") as f:
             f.write(f"# last {steps} iterations of the profiled bench run\n")
             f.write(f"window {((end - start) / 1e6):.3f} ms, kernel-busy {busy / 1e6:.3f} ms, "

@@ -576,3 +576,65 @@ def test_conv_impl_selection(dev):
         # the chosen instantiation's estimated time is the least of the built ones
         assert all(rounds(s) * (s + 0.5) <= rounds(q) * (q + 0.5) for q in (1, 2, 3, 4)), (n, s)
     assert impl(c3, 0)[0] == 0 and impl(_shape(_lib.CONV_F32_NHWC, 3, 84, 84, 32, 8, 4), 8)[0] == 0
+
+
+_C1_CHILD = r'''
+import sys, torch
+sys.path.insert(0, sys.argv[1])
+from reth_amd import _lib
+dev = torch.device("cuda")
+g = torch.Generator(device=dev).manual_seed(11)
+shape = _lib.ConvShape(_lib.CONV_U8_CHW, 4, 84, 84, 32, 8, 8, 4)
+wt = (torch.randn((32, 4, 8, 8), device=dev, generator=g) * 0.05).contiguous(memory_format=torch.channels_last)
+b = torch.randn(32, device=dev, generator=g) * 0.1
+pk = torch.empty(_lib.lib().rth_conv_packed_bytes(_lib.ctypes.byref(shape)) // 4, device=dev)
+_lib.call("rth_conv_pack", _lib.ctypes.byref(shape), wt.data_ptr(), pk.data_ptr(), _lib.stream_ptr())
+out = {}
+for n in (1, 2, 3, 7, 31, 64, 513):
+    x = torch.randint(0, 256, (n + 5, 4, 84, 84), dtype=torch.uint8, device=dev, generator=g)
+    rows = torch.randperm(n + 5, device=dev, generator=g)[:n].contiguous()
+    for tag, r in (("plain", None), ("rows", rows)):
+        y = torch.full((n, 20, 20, 32), float("nan"), device=dev)
+        _lib.call("rth_conv_bias_relu", _lib.ctypes.byref(shape), x.data_ptr(), None if r is None else r.data_ptr(), n,
+                  pk.data_ptr(), b.data_ptr(), y.data_ptr(), _lib.stream_ptr())
+        out[f"{tag}{n}"] = y.cpu()
+    cnt = torch.tensor([max(n - 2, 0)], dtype=torch.int64, device=dev)  # a device count below n
+    y = torch.full((n, 20, 20, 32), float("nan"), device=dev)
+    _lib.call("rth_conv_bias_relu_upto", _lib.ctypes.byref(shape), x.data_ptr(), rows.data_ptr(), n, cnt.data_ptr(),
+              pk.data_ptr(), b.data_ptr(), y.data_ptr(), _lib.stream_ptr())
+    out[f"upto{n}"] = y.cpu()
+torch.save(out, sys.argv[2])
+'''
+
+
+def test_conv1_shared_conversion_bit_identical(tmp_path, dev):
+    """k_conv1_u8_share (each byte converted once per horizontal window pair, the second half
+    of a window from the next lane) against r04's k_conv1_u8_bf16x3 (RTH_CONV1_NOSHARE=1): the
+    same products in the same order, so every output bit-identical -- ragged tiles (n = 1 .. 513
+    samples: 420 virtual pixels per sample, 31 per tile), row-indexed stacks, a device count below
+    n (rows past it untouched: NaN)"""
+    import subprocess
+    import sys
+
+    if torch.cuda.is_initialized():
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = {}
+    for mode in ("share", "noshare"):
+        env = dict(os.environ, RTH_CONV1_NOSHARE="1" if mode == "noshare" else "0")
+        path = tmp_path / f"{mode}.pt"
+        p = subprocess.run([sys.executable, "-c", _C1_CHILD, root, str(path)], env=env, capture_output=True, text=True,
+                           timeout=120)
+        assert p.returncode == 0, p.stderr[-2000:]
+        res[mode] = torch.load(path, weights_only=True)
+    assert res["share"].keys() == res["noshare"].keys()
+    for k in res["share"]:
+        a, b = res["share"][k], res["noshare"][k]
+        assert torch.equal(a.isnan(), b.isnan()), k
+        assert torch.equal(torch.nan_to_num(a), torch.nan_to_num(b)), k
+        if k.startswith("upto"):
+            n = int(k[4:])
+            assert not a[:max(n - 2, 0)].isnan().any() and a[max(n - 2, 0):].isnan().all()
+        else:
+            assert not a.isnan().any()

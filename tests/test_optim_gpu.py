@@ -1,6 +1,8 @@
 """rth_clip_adam (ClipAdam) against torch's clip_grad_norm_ + Adam on the same gradients
 (the reference's dqn_solver.py:118-121 sequence): fp32 agreement over several steps, with
-the clip active and inactive, on NCHW and channels-last (NHWC) conv weights."""
+the clip active and inactive, on NCHW and channels-last (NHWC) conv weights -- through the
+one-launch form (aligned tensors that fit its resident grid: the Q-net's) and the two-launch
+form (an unaligned tensor, or more elements than the one-launch grid holds)."""
 import pytest
 import torch
 
@@ -15,12 +17,33 @@ def _params(dev, seed):
     return ps
 
 
+def _unaligned(dev, seed):
+    """the Q-net shapes with one parameter 4 bytes past a 16-byte boundary: the two-launch form"""
+    ps = _params(dev, seed)
+    buf = torch.empty(ps[4].numel() + 1, device=dev)
+    buf[1:].copy_(ps[4].flatten())
+    ps[4] = buf[1:].view(ps[4].shape)
+    return ps
+
+
+def _large(dev, seed):
+    g = torch.Generator(device=dev).manual_seed(seed)
+    return [torch.randn(s, device=dev, generator=g) * 0.05 for s in [(4096, 1100), (7,)]]  # > 256 x 8 x 2048
+
+
 @pytest.mark.parametrize("max_norm", [None, 40.0, 0.5])
-def test_clip_adam_matches_torch(dev, max_norm):
+@pytest.mark.parametrize("kind", ["qnet", "unaligned", "large"])
+def test_clip_adam_matches_torch(dev, max_norm, kind):
+    from reth_amd import _lib
     from reth_amd.optim import ClipAdam
 
-    ref = [torch.nn.Parameter(p.clone()) for p in _params(dev, 1)]
-    ours = [torch.nn.Parameter(p.clone()) for p in _params(dev, 1)]
+    make = {"qnet": _params, "unaligned": _unaligned, "large": _large}[kind]
+    if kind != "qnet" and max_norm == 0.5:
+        pytest.skip("the clip is covered by the other max_norm")
+    ref = [torch.nn.Parameter(p.clone()) for p in make(dev, 1)]
+    ours = [torch.nn.Parameter(p) for p in make(dev, 1)]  # (the unaligned view kept as it is)
+    if kind == "unaligned":
+        assert ours[4].data_ptr() % 16 == 4
     topt = torch.optim.Adam(ref, lr=1e-4, eps=1.5e-4, foreach=False)
     oopt = ClipAdam(ours, lr=1e-4, eps=1.5e-4, max_norm=max_norm)
     g = torch.Generator(device=dev).manual_seed(2)
@@ -43,7 +66,47 @@ def test_clip_adam_matches_torch(dev, max_norm):
                 err = ((x - y).abs().max() / y.abs().max()).item()
                 assert err < 1e-6, err
     assert int(oopt._step.item()) == 5
-    assert ours[2].is_contiguous(memory_format=torch.channels_last)
+    if kind == "qnet":
+        assert ours[2].is_contiguous(memory_format=torch.channels_last)
+    assert _lib.lib().rth_clip_adam_timed_out(_lib.c_vp(oopt._ws.data_ptr())) == 0
+
+
+def test_clip_adam_one_launch_many_steps_and_reset(dev):
+    """the one-launch form's call counter tags each call's granules: 60 steps, then a reset of
+    Adam's state and step count alone (the counter keeps going), then of the workspace too --
+    every step equal to the two-step reference computed by torch"""
+    from reth_amd import _lib
+    from reth_amd.optim import ClipAdam
+
+    ref = [torch.nn.Parameter(p.clone()) for p in _params(dev, 3)]
+    ours = [torch.nn.Parameter(p.clone()) for p in _params(dev, 3)]
+    topt = torch.optim.Adam(ref, lr=1e-4, eps=1.5e-4, foreach=False)
+    oopt = ClipAdam(ours, lr=1e-4, eps=1.5e-4, max_norm=10.0)
+    g = torch.Generator(device=dev).manual_seed(4)
+    for step in range(90):
+        if step in (60, 75):  # fresh Adam state; at 75 the workspace (call counter) zeroed as well
+            for p, q in zip(ref, ours):
+                topt.state[p]["exp_avg"].zero_()
+                topt.state[p]["exp_avg_sq"].zero_()
+                topt.state[p]["step"].zero_()
+                oopt.state[q]["exp_avg"].zero_()
+                oopt.state[q]["exp_avg_sq"].zero_()
+            oopt._step.zero_()
+            if step == 75:
+                oopt._ws.zero_()
+        grads = [torch.randn(p.shape, device=dev, generator=g) * 0.5 for p in ref]
+        for p, q, gr in zip(ref, ours, grads):
+            p.grad = gr.clone().contiguous(memory_format=torch.channels_last) if p.dim() == 4 else gr.clone()
+            q.grad = p.grad.clone()
+        tn = torch.nn.utils.clip_grad_norm_(ref, 10.0, foreach=False)
+        topt.step()
+        oopt.step()
+        torch.testing.assert_close(oopt.total_norm[0], tn, rtol=1e-6, atol=0)
+    for p, q in zip(ref, ours):
+        err = ((q - p).abs().max() / p.abs().max()).item()
+        assert err < 1e-5, err
+    assert int(oopt._step.item()) == 15
+    assert _lib.lib().rth_clip_adam_timed_out(_lib.c_vp(oopt._ws.data_ptr())) == 0
 
 
 def test_clip_adam_skips_gradless_and_validates(dev):
@@ -56,3 +119,58 @@ def test_clip_adam_skips_gradless_and_validates(dev):
     assert torch.all(a < 1) and torch.equal(b, torch.ones(10, device=dev))
     with pytest.raises(ValueError):
         ClipAdam([torch.nn.Parameter(torch.ones(4, 4, device=dev).t())])
+
+
+_ONE_PASS_CHILD = r'''
+import sys, torch
+sys.path.insert(0, sys.argv[1])
+from reth_amd import _lib
+from reth_amd.optim import ClipAdam
+dev = torch.device("cuda")
+g = torch.Generator(device=dev).manual_seed(1)
+shapes = [(32, 4, 8, 8), (32,), (64, 32, 4, 4), (512, 3136), (7, 512), (3,)]
+init = [torch.randn(s, device=dev, generator=g) * 0.05 for s in shapes]
+ref = [torch.nn.Parameter(p.clone()) for p in init]
+ours = [torch.nn.Parameter(p.clone()) for p in init]
+topt = torch.optim.Adam(ref, lr=1e-4, eps=1.5e-4, foreach=False)
+oopt = ClipAdam(ours, lr=1e-4, eps=1.5e-4, max_norm=float(sys.argv[2]))
+worst = 0.0
+for step in range(40):
+    if step == 25:  # fresh Adam state and step count (the call counter in the workspace goes on)
+        for p, q in zip(ref, ours):
+            for k in ("exp_avg", "exp_avg_sq", "step"):
+                topt.state[p][k].zero_()
+            oopt.state[q]["exp_avg"].zero_()
+            oopt.state[q]["exp_avg_sq"].zero_()
+        oopt._step.zero_()
+    grads = [torch.randn(p.shape, device=dev, generator=g) * (3.0 if step % 2 else 0.01) for p in ref]
+    for p, q, gr in zip(ref, ours, grads):
+        p.grad = gr.clone()
+        q.grad = gr.clone()
+    tn = torch.nn.utils.clip_grad_norm_(ref, float(sys.argv[2]), foreach=False)
+    topt.step()
+    oopt.step()
+    assert abs(float(oopt.total_norm[0]) - float(tn)) <= 1e-6 * float(tn), (step, float(oopt.total_norm[0]), float(tn))
+    for p, q in zip(ref, ours):
+        worst = max(worst, ((q - p).abs().max() / p.abs().max()).item())
+assert _lib.lib().rth_clip_adam_timed_out(_lib.c_vp(oopt._ws.data_ptr())) == 0
+print("worst", worst, flush=True)
+assert worst < 1e-5, worst
+'''
+
+
+@pytest.mark.parametrize("max_norm", [40.0, 0.5])
+def test_clip_adam_one_launch_form(max_norm):
+    """RTH_ADAM_ONE_PASS=1 (k_clip_adam_fused: the tagged-granule grid barrier) against torch
+    over 40 steps with a state reset, in a child process (the form is chosen once per process)"""
+    import os
+    import subprocess
+    import sys
+
+    if torch.cuda.is_initialized():
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, "-c", _ONE_PASS_CHILD, root, str(max_norm)],
+                       env=dict(os.environ, RTH_ADAM_ONE_PASS="1"), capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0 and "worst" in p.stdout, p.stderr[-2000:]

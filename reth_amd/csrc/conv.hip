@@ -206,7 +206,11 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__res
         const int gb = g + 1 < G ? g + 1 : G - 1;
 #pragma unroll
         for (int nb = 0; nb < NBW; ++nb) {
+#ifdef RTH_DIAG_NOLDSB  // diagnostic timing builds only (scripts/r05.sh c2diag): wrong results
+          bnxt[nb] = bcur[nb];
+#else
           bnxt[nb] = wlane[(gb * NB + nb0 + nb) * 64];
+#endif
         }
         // keep the next chunk's B reads here, a whole chunk of MFMAs ahead of their use
         __builtin_amdgcn_sched_barrier(0);
@@ -222,9 +226,11 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__res
               acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bcur[nb][t], acc[mb][nb], 0, 0, 0);
           }
         const int ga = g + D;
+#ifndef RTH_DIAG_NOLOADA
 #pragma unroll
         for (int mb = 0; mb < MB; ++mb)
           ar[d][mb] = ld(ga < G ? cur[mb] + chunk_off(ga) : nxt[mb] + chunk_off(ga - G));
+#endif
 #pragma unroll
         for (int nb = 0; nb < NBW; ++nb) bcur[nb] = bnxt[nb];
       }
@@ -236,7 +242,11 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__res
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int64_t po = ptile * TP + mb * 16 + 4 * q + i;
+#ifdef RTH_DIAG_NOEPI
+        if (po < P && acc[mb][0][i] == 12345.678f) {
+#else
         if (po < P) {
+#endif
           if (out_nchw) {
             const int64_t b = po / Gm::PIX, pp = po - b * Gm::PIX;
 #pragma unroll

@@ -1039,6 +1039,114 @@ __global__ void k_tree_sample(const Node *__restrict__ nd, int64_t cap, int64_t 
   }
 }
 
+// r05: the sample at its latency floor.  Every workgroup stages the top TL levels of the tree
+// ({sum, val} of 2^TL - 1 nodes; 16 KB at TL = 10) with ALL its loads in flight at once -- one
+// round trip -- plus the root's min for the IS weights; each lane walks those levels in LDS
+// (the reference's comparisons and subtractions, lds_top_walk) and the levels below in round
+// trips of K levels: the 2^K - 1 child pairs of the K-deep subtree under its node are loaded
+// together, unconditionally (clamped record indices; an absent child is zeroed after the load,
+// so no load waits behind a branch), then K steps run on registers.  The sampled node's val
+// comes from the walk itself (the val find_step compared against), not from another load.
+// Pong's 1 M-row tree (depth 20): 10 levels in LDS + 5 round trips of 2 levels (K = 2).
+// Same comparisons in the same order as tree_find: bit-identical indices.
+__device__ __forceinline__ Pair load_pair_u(const Node *__restrict__ nd, int64_t cap, int64_t c) {
+  const int64_t l = 2 * c + 1;
+  const int64_t lc = l < cap ? l : cap - 1;  // record lc + 2 <= cap + 1 exists (padding)
+  const double2 L = *reinterpret_cast<const double2 *>(&nd[lc + 1]);
+  const double rv = nd[lc + 2].val;
+  const bool in = l < cap;
+  return Pair{in ? L.x : 0.0, in ? L.y : 0.0, in ? rv : 0.0};
+}
+
+template <int K>
+__device__ __forceinline__ int64_t tree_find_kv(const Node *__restrict__ nd, int64_t cap, double w, int64_t cur,
+                                                double &cval) {
+  constexpr int NP = (1 << K) - 1;
+  for (;;) {
+    Pair p[NP];
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      const int dq = 31 - __builtin_clz(q + 1);
+      const int64_t node = (cur + 1) * (int64_t(1) << dq) - 1 + (q + 1 - (1 << dq));
+      p[q] = load_pair_u(nd, cap, node);
+    }
+    int q = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      Pair pk = p[0];
+#pragma unroll
+      for (int j = 1; j < NP; ++j)
+        if (j == q) pk = p[j];
+      const int64_t before = cur;
+      if (!find_step(cur, cval, w, pk, cap)) return cur;
+      q = 2 * q + 1 + (int)(cur - (2 * before + 1));
+    }
+  }
+}
+
+#ifndef DEEP_THREADS
+#define DEEP_THREADS 256
+#endif
+// 256 lanes per workgroup (r05 A/B in the loop, Pong: K = 2 18-19 us, K = 3 23-24, K = 4 37;
+// one-wave workgroups (DEEP_THREADS=64) 26-27 / 27-28 / 30 -- eight 16 KB workgroups wait for
+// CU slots beside the learner's kernels longer than two do; r04's kernel 27-33)
+constexpr int kDeepThreads = DEEP_THREADS;
+
+// TL levels staged (2^TL - 1 nodes x 16 B: 16 KB at TL = 10 -- small enough to be dispatched
+// on a CU beside the learner's conv2 workgroup, which holds 128 KB of the 160; 64 KB at TL = 12
+// was not, and waited for a free CU in the loop: 41 vs 28 us, r05 A/B)
+template <int TL, int K>
+__global__ __launch_bounds__(kDeepThreads) void k_tree_sample_deep(
+    const Node *__restrict__ nd, int64_t cap, int64_t batch, const double *__restrict__ uniforms, uint64_t seed,
+    uint64_t counter, int is_weights, double beta, const ReplayState *st, rth_schedule beta_s,
+    int64_t *__restrict__ idx_out, double *__restrict__ out) {
+  constexpr int kDeepNodes = (1 << TL) - 1;
+  __shared__ double2 topl[kDeepNodes];
+  __shared__ double min_sh;
+  const int64_t nst = cap < kDeepNodes ? cap : kDeepNodes;
+  constexpr int PER = (kDeepNodes + kDeepThreads - 1) / kDeepThreads;
+  {
+    double2 tmp[PER];  // every staging load in flight before the first LDS write
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int64_t n = threadIdx.x + (int64_t)kDeepThreads * j;
+      tmp[j] = *reinterpret_cast<const double2 *>(&nd[(n < nst ? n : nst - 1) + 1]);
+    }
+    if (threadIdx.x == 0) {
+      const Node root = nd[1];
+      min_sh = root.sum != 0.0 ? root.mn : 1.0;  // tree_min (NumbaSumTree.min, sumtree.py:109-110)
+    }
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {  // unconditional (a clamped lane rewrites node nst - 1 with its
+      const int64_t n = threadIdx.x + (int64_t)kDeepThreads * j;  // own value): no load sinks into a branch
+      topl[n < nst ? n : nst - 1] = tmp[j];
+    }
+  }
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * kDeepThreads + threadIdx.x;
+  if (i >= batch) return;
+  if (st) {
+    counter = (uint64_t)st->calls;
+    beta = sched_value(beta_s, st->sched_step);
+  }
+  const double seg = topl[0].x / (double)batch;
+  const double u = uniforms ? uniforms[i] : philox_uniform(seed, counter, (uint32_t)i, STREAM_SAMPLE);
+  double t = rmul(radd((double)i, u), seg);
+  int64_t k;
+  double cval;
+  if (!lds_top_walk(topl, cap, nst, k, cval, t)) {
+    // k is the answer, cval its val
+  } else {
+    k = tree_find_kv<K>(nd, cap, t, k, cval);
+  }
+  idx_out[i] = k;
+  if (is_weights) {
+    out[i] = pow(cval / min_sh, -beta);
+  } else if (out) {
+    out[i] = cval;
+  }
+}
+
 __global__ void k_tree_stats(const Node *nd, double *out) {
   if (threadIdx.x == 0 && blockIdx.x == 0) {
     out[0] = nd[1].sum;
@@ -1154,6 +1262,22 @@ int tree_sample_impl(rth_sumtree *t, int64_t batch, const double *uniforms, uint
   // 0.570-0.573 vs 0.573-0.580 ms/step in the loop (r04, interleaved); RTH_FIND_GROUP /
   // RTH_FIND_K select the others
   const int top = env_int("RTH_TREE_LDS_TOP", 1) ? 1 : 0;  // read per call: tests switch it
+  // r05 default: k_tree_sample_deep (10 staged levels, RTH_DEEP_K = 2 levels per round trip below);
+  // RTH_TREE_SAMPLE_DEEP=0 gives r04's kernel (and its RTH_TREE_LDS_TOP / RTH_FIND_* forms)
+  if (env_int("RTH_TREE_SAMPLE_DEEP", 1) && top && !getenv("RTH_FIND_GROUP") && !getenv("RTH_FIND_K")) {
+    const int dk = env_int("RTH_DEEP_K", 2);
+    const void *fn = dk == 2 ? reinterpret_cast<const void *>(&k_tree_sample_deep<10, 2>)
+                     : dk == 3 ? reinterpret_cast<const void *>(&k_tree_sample_deep<10, 3>)
+                               : reinterpret_cast<const void *>(&k_tree_sample_deep<10, 4>);
+    const Node *nd = t->nodes;
+    int64_t cap = t->cap;
+    rth_schedule bs_ = beta_s ? *beta_s : rth_schedule{};
+    void *args[] = {(void *)&nd, (void *)&cap, (void *)&batch, (void *)&uniforms, (void *)&seed, (void *)&counter,
+                    (void *)&is_weights, (void *)&beta, (void *)&st, (void *)&bs_, (void *)&idx_out, (void *)&out};
+    RTH_HIP(hipLaunchKernel(fn, dim3((unsigned)((batch + kDeepThreads - 1) / kDeepThreads)), dim3(kDeepThreads), args,
+                            0, s));
+    return RTH_OK;
+  }
   const int gk = (top && !getenv("RTH_FIND_GROUP")) ? 0 : find_group_k();
   const int kspec = (top && !getenv("RTH_FIND_K")) ? 1 : find_k();
   const int bs = top ? 256 : sample_bs();

@@ -77,6 +77,31 @@ PY
             --no-cpu-baseline --no-sweep
       done
       summ gpurun_out/c1ab_*.log ;;
+    c2diag)  # conv2 fp32-MFMA forward with parts removed (diagnostic variant libraries, wrong results)
+      CONV_NS=1024,512 step c2d_dflt 120 python scripts/bench_conv.py
+      for v in noloada noldsb noepi mfmaonly; do
+        RTH_LIB_PATH=reth_amd/libreth_hip_$v.so CONV_NS=1024,512 step c2d_$v 120 python scripts/bench_conv.py
+      done
+      grep -H "conv2" gpurun_out/c2d_*.log ;;
+    tdstages) step td_stages 300 python scripts/diag_td_stages.py gpurun_out/td_stages.json ;;
+    treeab)  # tree sample: deep kernel (10 staged levels) with K = 3 (default) / 2 / 4 vs r04's kernel
+      step tree_tests 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_sumtree_gpu.py \
+          tests/test_scale_gpu.py tests/test_samplers_gpu.py tests/test_replay_gpu.py
+      RTH_DEEP_K=2 step tree_tests_k2 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
+          tests/test_sumtree_gpu.py tests/test_scale_gpu.py -k "sample or find or scale"
+      RTH_DEEP_K=4 step tree_tests_k4 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
+          tests/test_sumtree_gpu.py tests/test_scale_gpu.py -k "sample or find or scale"
+      for r in 1 2; do
+        step treeab_k3_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        RTH_DEEP_K=2 step treeab_k2_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        RTH_DEEP_K=4 step treeab_k4_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        RTH_TREE_SAMPLE_DEEP=0 step treeab_r04_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline \
+            --no-sweep
+        RTH_DEEP_K=2 RTH_LIB_PATH=reth_amd/libreth_hip_deep256.so step treeab_w256k2_$r 300 python bench.py --steps 300 \
+            --warmup 5 --no-cpu-baseline --no-sweep
+      done
+      summ gpurun_out/treeab_*.log ;;
+    treephase) RTH_TREE_TIMING=1 step tree_phases 300 python scripts/probe_tree_phases.py ;;
     tests) step gpu_tests 1100 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     t:*) f=${s#t:}; step "t_$(basename ${f//,/_} .py)" 900 python -u -m pytest -x -v --timeout 300 \

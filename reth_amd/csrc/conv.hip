@@ -29,7 +29,9 @@
 // relu, summed in a different order than MIOpen's or the reference's CPU convolution.
 #include <cstdlib>
 #include <mutex>
+#include <string>
 #include <type_traits>
+#include <unordered_map>
 
 #include "common.hpp"
 
@@ -81,14 +83,24 @@ constexpr int kClockSlots = 1024;
 __device__ unsigned long long g_conv_clock[kClockSlots][2];
 
 // NS > 1: a wave tile is TP pixels x COUT / NS channels (tile t = pixel tile t / NS, channel
-// part t % NS), for more, smaller tiles over the SIMDs; each output keeps its K order
-template <int MODE, int KH, int KW, int S, int CIN, int COUT, int HIN, int WIN, int WAVES, int MB, int NS = 1>
+// part t % NS), for more, smaller tiles over the SIMDs; each output keeps its K order.
+// PW (r05): the channel part is fixed per workgroup (blockIdx % NS; the grid a multiple of NS)
+// and the workgroup stages only that part's weights -- 1 / NS of the LDS, so a workgroup of
+// the other stream's kernels (hipBLASLt's FC1 tiles, an x9 conv) fits on the same CU
+// DYN (r05): after its first tile a wave takes its tiles from a launch-wide counter (dyn[0];
+// dyn[1] counts finished workgroups, the last one re-arms both): a SIMD that the other
+// stream's kernels slow down takes fewer tiles, instead of the static round-robin making every
+// wave wait for the slowest SIMD.  Each output is computed exactly as in the static form.
+typedef __attribute__((address_space(1))) unsigned int conv_gu32;
+template <int MODE, int KH, int KW, int S, int CIN, int COUT, int HIN, int WIN, int WAVES, int MB, int NS = 1,
+          int PW = 0, int DYN = 0>
 __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__restrict__ x,
                                                               const int64_t *__restrict__ rows, int64_t n,
                                                               const int64_t *__restrict__ n_dev,
                                                               const float *__restrict__ w,
                                                               const float *__restrict__ bias,
-                                                              float *__restrict__ y, int out_nchw) {
+                                                              float *__restrict__ y, int out_nchw,
+                                                              unsigned int *dyn) {
   using Gm = ConvGeom<MODE, KH, KW, S, CIN, COUT, HIN, WIN>;
   constexpr bool F32 = MODE == RTH_CONV_F32_NHWC;
   constexpr int G = Gm::G, NB = Gm::NB, T = WAVES * 64, NBW = NB / NS;
@@ -96,7 +108,11 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__res
   constexpr int TP = 16 * MB;                    // output pixels per wave tile
   constexpr int D = F32 ? Gm::prefetch(MB) : G;  // input chunks in flight per wave
   using Frag = typename std::conditional<F32, f32x4, uint32_t>::type;
-  __shared__ f32x4 wl[Gm::LDS_F4];
+  static_assert(!PW || NS > 1, "PW needs channel parts");
+  constexpr int LDSW = PW ? Gm::LDS_F4 / NS : Gm::LDS_F4;  // staged float4 slots
+  __shared__ f32x4 wl[LDSW];
+  const int part = PW ? (int)(blockIdx.x % NS) : 0;               // PW: this workgroup's channel part
+  const int64_t wgs = PW ? gridDim.x / NS : gridDim.x, wgi = PW ? blockIdx.x / NS : blockIdx.x;
 
   const int wave = threadIdx.x / 64, lane = threadIdx.x % 64;
   const int q = lane >> 4, mr = lane & 15;
@@ -107,7 +123,9 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__res
     const int64_t m = *n_dev;
     n = m < n ? (m > 0 ? m : 0) : n;
   }
-  const int64_t P = n * Gm::PIX, tiles = (P + TP - 1) / TP * NS, tstride = (int64_t)gridDim.x * WAVES;
+  // PW: tiles are pixel tiles of this workgroup's part; else (pixel tile, part) pairs
+  const int64_t P = n * Gm::PIX, tiles = (P + TP - 1) / TP * (PW ? 1 : NS), tstride = wgs * WAVES;
+  constexpr int TD = PW ? 1 : NS;  // tile -> pixel tile divisor
 
   // this lane's window origin in tile t, per M-block (tail lanes read a duplicate pixel)
   auto bases = [&](int64_t t, const uint8_t *(&out)[MB]) {
@@ -142,12 +160,27 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__res
   // wave slots are numbered SIMD-major (waves w and w + 4 of a workgroup share a SIMD): the
   // first gridDim.x * 4 slots put one wave on every SIMD, so a partial last round of tiles
   // lands on distinct SIMDs and no SIMD runs more than ceil(tiles / SIMDs) tiles
-  const int64_t slot = WAVES % 4 == 0 ? (int64_t)(wave / 4) * gridDim.x * 4 + blockIdx.x * 4 + wave % 4
-                                      : (int64_t)blockIdx.x * WAVES + wave;
+  const int64_t slot = WAVES % 4 == 0 ? (int64_t)(wave / 4) * wgs * 4 + wgi * 4 + wave % 4 : wgi * WAVES + wave;
   // the first tile's leading input chunks are requested before the weights are staged
   int64_t tile = slot;
+  conv_gu32 *const dctr = (conv_gu32 *)dyn;
+  // DYN: claim the next unclaimed tile (lane 0 asks for the wave).  The claim stays in lane 0's
+  // register until it is needed a whole tile later (claimed()): read at once, the wait for the
+  // atomic would also wait for every load issued before it -- the tile's prefetched chunks
+  auto grab = [&]() -> unsigned int {
+    // the address offset mbcnt_lo(0, 0) is 0 in every lane, but not provably uniform: the
+    // compiler's atomic optimizer (a wave scan + an immediate read of the result) leaves the
+    // single-lane atomic alone, so nothing waits for it before claimed()
+    conv_gu32 *p = dctr + __builtin_amdgcn_mbcnt_lo(0u, 0u);
+    unsigned int v = 0;
+    if (lane == 0) v = __hip_atomic_fetch_add(p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return v;
+  };
+  auto claimed = [&](unsigned int v) -> int64_t { return wgs * WAVES + (int64_t)__builtin_amdgcn_readfirstlane(v); };
+  // the tile after this one, known a whole tile ahead (DYN: claimed a tile ahead)
+  int64_t tnext = DYN ? claimed(grab()) : tile + tstride;
   const uint8_t *cur[MB], *nxt[MB];
-  bases((tile < tiles ? tile : tiles - 1) / NS, cur);
+  bases((tile < tiles ? tile : tiles - 1) / TD, cur);
   Frag ar[D][MB];
 #pragma unroll
   for (int d = 0; d < D; ++d)
@@ -157,46 +190,51 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__res
   // stage the packed weights (rth_conv_pack: already in fragment order): a coalesced copy,
   // consecutive threads -> consecutive 16-byte LDS slots; all loads first
   {
-    constexpr int PER = (Gm::LDS_F4 + T - 1) / T;
+    constexpr int PER = (LDSW + T - 1) / T;
     const f32x4 *wp = reinterpret_cast<const f32x4 *>(w);
+    // PW: LDS slot (g * NBW + nbl) * 64 + lane <- packed slot (g * NB + part * NBW + nbl) * 64 + lane
+    auto src = [&](int sl) { return PW ? ((sl / (NBW * 64)) * NB + part * NBW) * 64 + sl % (NBW * 64) : sl; };
     f32x4 tmp[PER];
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       const int sl = threadIdx.x + j * T;
-      if (sl < Gm::LDS_F4) tmp[j] = wp[sl];
+      if (sl < LDSW) tmp[j] = wp[src(sl)];
     }
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       const int sl = threadIdx.x + j * T;
-      if (sl < Gm::LDS_F4) wl[sl] = tmp[j];
+      if (sl < LDSW) wl[sl] = tmp[j];
     }
   }
   __syncthreads();
 
   float bl[NBW];
-  const int nb_first = NS == 1 ? 0 : (int)(tile % NS) * NBW;
+  const int nb_first = PW ? part * NBW : (NS == 1 ? 0 : (int)(tile % NS) * NBW);
 #pragma unroll
   for (int nb = 0; nb < NBW; ++nb) bl[nb] = bias[(nb_first + nb) * 16 + mr];
   // this lane's B fragments, offset to the tile's channel part
   const f32x4 *wlane = wl + lane;
 
-  for (; tile < tiles; tile += tstride) {
-    const int nb0 = NS == 1 ? 0 : (int)(tile % NS) * NBW;
-    if constexpr (NS > 1) {
+  for (; tile < tiles;) {
+    const unsigned int claim2 = DYN ? grab() : 0u;  // the tile after next, read at this loop's end
+    const int nb0 = PW ? part * NBW : (NS == 1 ? 0 : (int)(tile % NS) * NBW);  // output channel block
+    const int lb0 = PW ? 0 : nb0;                                               // its LDS block
+    if constexpr (NS > 1 && !PW) {
 #pragma unroll
       for (int nb = 0; nb < NBW; ++nb) bl[nb] = bias[(nb0 + nb) * 16 + mr];
     }
-    const int64_t ptile = tile / NS;
+    const int64_t ptile = tile / TD;
     // the chunks past the end of this tile are the next tile's leading chunks
-    bases((tile + tstride < tiles ? tile + tstride : tile) / NS, nxt);
+    bases((tnext < tiles ? tnext : tile) / TD, nxt);
     f32x4 acc[MB][NBW];
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
       for (int nb = 0; nb < NBW; ++nb) acc[mb][nb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     f32x4 bcur[NBW], bnxt[NBW];  // B fragments, one chunk ahead
+    constexpr int LNB = PW ? NBW : NB;  // channel blocks per chunk in LDS
 #pragma unroll
-    for (int nb = 0; nb < NBW; ++nb) bcur[nb] = wlane[(nb0 + nb) * 64];
+    for (int nb = 0; nb < NBW; ++nb) bcur[nb] = wlane[(lb0 + nb) * 64];
 
 #pragma unroll 1
     for (int g0 = 0; g0 < G; g0 += D) {
@@ -209,7 +247,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__res
 #ifdef RTH_DIAG_NOLDSB  // diagnostic timing builds only (scripts/r05.sh c2diag): wrong results
           bnxt[nb] = bcur[nb];
 #else
-          bnxt[nb] = wlane[(gb * NB + nb0 + nb) * 64];
+          bnxt[nb] = wlane[(gb * LNB + lb0 + nb) * 64];
 #endif
         }
         // keep the next chunk's B reads here, a whole chunk of MFMAs ahead of their use
@@ -261,6 +299,19 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__res
       }
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb) cur[mb] = nxt[mb];
+    tile = tnext;
+    tnext = DYN ? claimed(claim2) : tnext + tstride;
+  }
+  if constexpr (DYN) {  // the last workgroup out re-arms the counters for the next launch
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every claim of this wave has landed
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned int done = __hip_atomic_fetch_add(dctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (done == gridDim.x - 1) {
+        __hip_atomic_store(dctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(dctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
   }
 #ifdef RTH_CLOCK_STAMPS
   if (threadIdx.x == 0 && blockIdx.x < kClockSlots) {
@@ -1042,6 +1093,8 @@ struct ConvLaunch {
   const struct ConvLaunch *big;
   int64_t big_above;
   int big_off;
+  int pw;   // k_conv_bias_relu PW: channel part per workgroup (the grid a multiple of nsplit)
+  int dyn;  // k_conv_bias_relu DYN: tiles claimed from a launch-wide counter (dyn_counter())
 };
 
 template <int KH, int KW, int S, int CIN, int HIN, int WIN, int NSAMP, int ROT, int KS>
@@ -1057,12 +1110,14 @@ static ConvLaunch x9_launch() {
   return l;
 }
 
-template <int MODE, int KH, int KW, int S, int CIN, int COUT, int HIN, int WIN, int WAVES, int MB, int NS = 1>
+template <int MODE, int KH, int KW, int S, int CIN, int COUT, int HIN, int WIN, int WAVES, int MB, int NS = 1,
+          int PW = 0, int DYN = 0>
 static ConvLaunch conv_launch() {
   using Gm = ConvGeom<MODE, KH, KW, S, CIN, COUT, HIN, WIN>;
-  ConvLaunch l{reinterpret_cast<const void *>(&k_conv_bias_relu<MODE, KH, KW, S, CIN, COUT, HIN, WIN, WAVES, MB, NS>),
+  ConvLaunch l{reinterpret_cast<const void *>(&k_conv_bias_relu<MODE, KH, KW, S, CIN, COUT, HIN, WIN, WAVES, MB, NS, PW,
+                                                                DYN>),
                reinterpret_cast<const void *>(&k_conv_pack<MODE, KH, KW, S, CIN, COUT, HIN, WIN>), WAVES,
-               Gm::LDS_F4 * 16, 0, 16 * MB, 0, NS, 0, {}, nullptr, 0, 0};
+               Gm::LDS_F4 * 16, 0, 16 * MB, 0, NS, 0, {}, nullptr, 0, 0, PW, DYN};
   int blocks = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, l.fn, WAVES * 64, 0) != hipSuccess || blocks < 1)
     blocks = 1;
@@ -1171,19 +1226,19 @@ static bool find_conv(const rth_conv_shape &s, ConvLaunch *out, int *geom = null
     // CUs, and the loop ran 0.5-1 % slower with it
     // RTH_CONV2_NS = 1 / 2 / 4: wave tiles of 16 pixels x 64 / 32 / 16 channels (finer tiles
     // even out the last round of tiles over the SIMDs)
+    // (r04: 16 waves and 16-channel tiles measured slower; dropped)
+    // RTH_CONV2_SCHED (r05 A/B): static = r04's round-robin tiles; dyn = tiles claimed from a
+    // launch-wide counter; ns2 / ns2dyn = 16 x 32-channel half tiles, round-robin / claimed;
+    // pw2 / pw2dyn = half tiles with the channel part fixed per workgroup (half the LDS)
     static const ConvLaunch f32 = [] {
-      const bool w16 = env_i64("RTH_CONV2_WAVES", 8) == 16;  // 16 waves: 4 per SIMD
-      switch (env_i64("RTH_CONV2_NS", CONV2_NS)) {
-        case 2:
-          return w16 ? conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 16, CONV2_MB, 2>()
-                     : conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 2>();
-        case 4:
-          return w16 ? conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 16, CONV2_MB, 4>()
-                     : conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 4>();
-        default:
-          return w16 ? conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 16, CONV2_MB, 1>()
-                     : conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 1>();
-      }
+      const char *e = getenv("RTH_CONV2_SCHED");
+      const std::string v = e ? e : (CONV2_NS == 2 ? "ns2" : "static");
+      if (v == "dyn") return conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 1, 0, 1>();
+      if (v == "ns2") return conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 2, 0, 0>();
+      if (v == "ns2dyn") return conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 2, 0, 1>();
+      if (v == "pw2") return conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 2, 1, 0>();
+      if (v == "pw2dyn") return conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 2, 1, 1>();
+      return conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 1>();
     }();
     static const ConvLaunch l = [] {
       if (conv_f32mfma() || conv2_x9_max() <= 0) return f32;
@@ -2109,6 +2164,33 @@ static void select_launch(ConvLaunch *l, int64_t n, int64_t *w_off, int64_t *nsa
   }
 }
 
+// DYN launches' tile counters: one 2-word slot per packed-weight buffer (the learner's, the
+// target network's and the actors' convolutions run on different streams with different
+// packed buffers; one buffer is never used by two launches at once).  Zero at load; every
+// launch leaves its slot zero (the last workgroup re-arms it).
+constexpr int kDynSlots = 256;
+__device__ unsigned int g_conv_dyn[kDynSlots][2];
+static unsigned int *dyn_counter(const void *key) {
+  static std::mutex mu;
+  static std::unordered_map<const void *, int> slot_of[64];
+  static unsigned int *base[64] = {};
+  static int next[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  std::lock_guard<std::mutex> lock(mu);
+  if (!base[dev] && hipGetSymbolAddress(reinterpret_cast<void **>(&base[dev]), HIP_SYMBOL(g_conv_dyn)) != hipSuccess)
+    return nullptr;
+  auto it = slot_of[dev].find(key);
+  int sl;
+  if (it != slot_of[dev].end()) {
+    sl = it->second;
+  } else {
+    sl = next[dev]++ % kDynSlots;
+    slot_of[dev][key] = sl;
+  }
+  return base[dev] + 2 * sl;
+}
+
 static int conv_bias_relu(const rth_conv_shape *shape, const void *x, const int64_t *rows, int64_t n,
                           const int64_t *n_dev, const float *w, const float *bias, float *y, void *stream) {
   RTH_REQUIRE(shape && x && w && bias && y && n >= 0, "rth_conv_bias_relu: NULL argument");
@@ -2150,8 +2232,15 @@ static int conv_bias_relu(const rth_conv_shape *shape, const void *x, const int6
   const int cap = wg_per_cu();
   const int64_t resident = (int64_t)cu_count() * (l.per_cu < cap ? l.per_cu : cap);
   if (grid > resident) grid = resident;
+  if (l.pw) {  // every channel part gets grid / nsplit workgroups
+    const int64_t ns = l.nsplit;
+    grid = grid / ns * ns;
+    if (grid < ns) grid = ns;
+  }
+  unsigned int *dyn = l.dyn ? dyn_counter(w) : nullptr;
+  RTH_REQUIRE(!l.dyn || dyn, "rth_conv_bias_relu: no tile counter for the dynamic schedule");
   void *args[] = {(void *)&x, (void *)&rows, (void *)&n, (void *)&n_dev, (void *)&w, (void *)&bias, (void *)&y,
-                  (void *)&out_nchw};  // (k_conv1_u8_bf16x3 takes the first seven)
+                  (void *)&out_nchw, (void *)&dyn};  // (k_conv1_u8_bf16x3 takes the first seven)
   RTH_HIP(hipLaunchKernel(l.fn, dim3((unsigned)grid), dim3(l.waves * 64), args, 0, as_stream(stream)));
   return RTH_OK;
 }

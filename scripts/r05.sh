@@ -102,6 +102,28 @@ PY
       done
       summ gpurun_out/treeab_*.log ;;
     treephase) RTH_TREE_TIMING=1 step tree_phases 300 python scripts/probe_tree_phases.py ;;
+    prof)  # steady-state kernel profile + the HBM counter passes of the same command shape
+      step rocprof_stats 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/prof" \
+          -o run -- python bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-sweep
+      step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv --kernel-include-regex "rth::" \
+          -d "$PWD/gpurun_out/pmc_fetch" -o run -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-sweep
+      step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv --kernel-include-regex "rth::" \
+          -d "$PWD/gpurun_out/pmc_write" -o run -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-sweep ;;
+    span) RTH_BENCH_SPAN=1 step span 300 python bench.py --steps 300 --warmup 20 --no-cpu-baseline --no-sweep ;;
+    tdfc) RTH_FC_X9=1 step td_stages_fcx9 300 python scripts/diag_td_stages.py gpurun_out/td_stages_fcx9.json ;;
+    c2sched)  # conv2 tile schedules: tests, alone, in the loop
+      step c2s_tests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_conv_gpu.py \
+          -k "schedules or conv_f32_nhwc or partial or upto"
+      for v in static dyn ns2dyn pw2 pw2dyn; do
+        RTH_CONV2_SCHED=$v CONV_NS=1024,512,256 step c2s_micro_$v 120 python scripts/bench_conv.py
+      done
+      grep -H "conv2" gpurun_out/c2s_micro_*.log
+      for r in 1 2; do
+        for v in static dyn ns2dyn pw2 pw2dyn; do
+          RTH_CONV2_SCHED=$v step c2sab_${v}_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        done
+      done
+      summ gpurun_out/c2sab_*.log ;;
     tests) step gpu_tests 1100 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     t:*) f=${s#t:}; step "t_$(basename ${f//,/_} .py)" 900 python -u -m pytest -x -v --timeout 300 \

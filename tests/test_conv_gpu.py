@@ -638,3 +638,63 @@ def test_conv1_shared_conversion_bit_identical(tmp_path, dev):
             assert not a[:max(n - 2, 0)].isnan().any() and a[max(n - 2, 0):].isnan().all()
         else:
             assert not a.isnan().any()
+
+
+_C2_CHILD = r'''
+import sys, torch
+sys.path.insert(0, sys.argv[1])
+from reth_amd import _lib
+dev = torch.device("cuda")
+g = torch.Generator(device=dev).manual_seed(12)
+shape = _lib.ConvShape(_lib.CONV_F32_NHWC, 32, 20, 20, 64, 4, 4, 2)
+wt = (torch.randn((64, 32, 4, 4), device=dev, generator=g) * 0.05).contiguous(memory_format=torch.channels_last)
+b = torch.randn(64, device=dev, generator=g) * 0.1
+pk = torch.empty(_lib.lib().rth_conv_packed_bytes(_lib.ctypes.byref(shape)) // 4, device=dev)
+_lib.call("rth_conv_pack", _lib.ctypes.byref(shape), wt.data_ptr(), pk.data_ptr(), _lib.stream_ptr())
+out = {}
+for n in (1, 3, 64, 700, 1024):
+    x = torch.rand((n, 20, 20, 32), device=dev, generator=g)
+    for rep in range(3):  # the same buffers again: a claim counter left armed would skip tiles
+        y = torch.full((n, 9, 9, 64), float("nan"), device=dev)
+        _lib.call("rth_conv_bias_relu", _lib.ctypes.byref(shape), x.data_ptr(), None, n, pk.data_ptr(), b.data_ptr(),
+                  y.data_ptr(), _lib.stream_ptr())
+        out[f"n{n}_{rep}"] = y.cpu()
+    cnt = torch.tensor([max(n // 2, 1)], dtype=torch.int64, device=dev)
+    y = torch.full((n, 9, 9, 64), float("nan"), device=dev)
+    _lib.call("rth_conv_bias_relu_upto", _lib.ctypes.byref(shape), x.data_ptr(), None, n, cnt.data_ptr(), pk.data_ptr(),
+              b.data_ptr(), y.data_ptr(), _lib.stream_ptr())
+    out[f"upto{n}"] = y.cpu()
+torch.save(out, sys.argv[2])
+'''
+
+
+def test_conv2_schedules_bit_identical(tmp_path, dev):
+    """conv2's fp32-MFMA forward under every tile schedule (RTH_CONV2_SCHED: static round-robin,
+    tiles claimed from a launch-wide counter, half tiles, the channel part per workgroup) gives
+    the same bits: each output's MFMA chain is the same whichever wave computes it; repeated
+    launches on one packed buffer check that the claim counter is re-armed"""
+    import subprocess
+    import sys
+
+    if torch.cuda.is_initialized():
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = {}
+    for sched in ("static", "dyn", "ns2", "ns2dyn", "pw2", "pw2dyn"):
+        path = tmp_path / f"{sched}.pt"
+        p = subprocess.run([sys.executable, "-c", _C2_CHILD, root, str(path)],
+                           env=dict(os.environ, RTH_CONV2_SCHED=sched), capture_output=True, text=True, timeout=120)
+        assert p.returncode == 0, (sched, p.stderr[-2000:])
+        res[sched] = torch.load(path, weights_only=True)
+    base = res["static"]
+    for k, v in base.items():
+        if k.startswith("upto"):
+            n = int(k[4:])
+            m = max(n // 2, 1)
+            assert not v[:m].isnan().any() and v[m:].isnan().all(), k
+        else:
+            assert not v.isnan().any(), k
+    for sched, r in res.items():
+        for k in base:
+            assert torch.equal(torch.nan_to_num(r[k], nan=-1.0), torch.nan_to_num(base[k], nan=-1.0)), (sched, k)

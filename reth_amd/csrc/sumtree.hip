@@ -246,7 +246,8 @@ struct UpdArgs {
   int64_t pn;
   int32_t post_tail;  // st->tail += n after every read of it (the append's FIFO advance)
   int32_t timing;     // record phase timestamps in g_upd_clock (RTH_TREE_TIMING=1)
-  int32_t fuse_top;   // the subtree pass's last workgroup runs the top pass (else its own launch)
+  int32_t fuse_top;   // 1: the subtree pass's last workgroup runs the top pass; 2: an extra
+                      // workgroup of the last subtree launch runs it concurrently (r05); 0: its own launch
   // nullable: the subtree pass stages the top pass's key information here (set when it runs):
   // bytes 0 .. 2047 = touched flags of the level-S nodes (each written by the node's owner,
   // no atomics: one line per 128 nodes, not a contended bitmap), stage[kStageFlags + i] =
@@ -302,7 +303,7 @@ __device__ __forceinline__ void lds_barrier() {
 }
 
 struct TopLds;
-__device__ __forceinline__ void tree_top(const UpdArgs &a, int S, TopLds &L);
+__device__ __forceinline__ void tree_top(const UpdArgs &a, int S, TopLds &L, unsigned int nsub = 0);
 
 // ---------------------------------------------------------------- subtree pass
 // Workgroup w owns the level-S subtrees s with s % gridDim.x == w (consecutive FIFO slots
@@ -389,7 +390,15 @@ __global__ __launch_bounds__(kSubThreads) void k_tree_update_sub(UpdArgs a, int 
   upd_prologue(a, &fifo_start, &alpha);
   const int64_t N = a.pn + a.n;
   const int64_t top = (int64_t(1) << S) - 1;  // nodes above level S
-  const uint32_t G = gridDim.x;
+  // fuse_top == 2: the last workgroup of the last pass is the top pass, running from the start
+  // beside the subtree workgroups (its key scan and its loads of the levels above S overlap
+  // them); it waits only for their level-S sums
+  const bool early = a.fuse_top == 2 && last_pass;
+  const uint32_t G = gridDim.x - (early ? 1u : 0u);
+  if (early && blockIdx.x == G) {
+    tree_top(a, S, *reinterpret_cast<TopLds *>(ent), G);
+    return;
+  }
   // key g of this pass: its node (a key below D -> its level-D ancestor, valueless), false
   // when it is not this workgroup's, or a valueless duplicate of the key right before it
   auto is_mine = [&](int64_t g, uint64_t *key, bool *valued) -> bool {
@@ -634,13 +643,19 @@ __global__ __launch_bounds__(kSubThreads) void k_tree_update_sub(UpdArgs a, int 
     R = kSubKeys;
   }
   if (a.timing && tid == 0) atomicMax(&g_upd_clock[5], wall_clock64());  // the last workgroup's end
+  unsigned *const ticket = reinterpret_cast<unsigned *>(&a.nd[0].pad);
+  if (early) {  // count this workgroup done once its level-S sums (write-through) have landed
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
   // ---- ticket: the workgroup that finishes last runs the levels above S (tree_top) in this
   // launch, in the LDS of the entries (no second launch).  The counter lives in the unused
   // record 0 of the node array and is re-armed by that workgroup.
   if (!a.fuse_top || !last_pass) return;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  unsigned *const ticket = reinterpret_cast<unsigned *>(&a.nd[0].pad);
   if (tid == 0) {
     const unsigned tk = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_next = tk == gridDim.x - 1;
@@ -729,7 +744,11 @@ struct TopLds {
   int ukey[8];
 };
 
-__device__ __forceinline__ void tree_top(const UpdArgs &a, int S, TopLds &L) {
+// nsub > 0: run as the extra workgroup of a subtree launch (fuse_top == 2): everything that
+// does not depend on the subtree pass first (the key scan, the records above level S, the key
+// priorities), then wait until its nsub workgroups have counted themselves done (the ticket
+// word, re-armed here), then load the level-S sums they wrote
+__device__ __forceinline__ void tree_top(const UpdArgs &a, int S, TopLds &L, unsigned int nsub) {
   int32_t *const win = L.win;
   uint32_t *const bot = L.bot;
   double *const xs = L.xs, *const xm = L.xm, *const uv = L.uv, *const us = L.us, *const um = L.um;
@@ -751,15 +770,18 @@ __device__ __forceinline__ void tree_top(const UpdArgs &a, int S, TopLds &L) {
   double cs[8], cm[8];  // level S children of the level S-1 nodes
 #pragma unroll
   for (int q = 0; q < 4; ++q) r1[q] = top_load(a.nd, lane ? cap : 0, b1 + q);
+  auto load_children = [&]() {
 #pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    const int64_t l = 2 * b1 + 1 + c;
-    cs[c] = cm[c] = 0.0;
-    if (lane && l < cap) {
-      cs[c] = a.nd[l + 1].sum;
-      cm[c] = a.nd[l + 1].mn;
+    for (int c = 0; c < 8; ++c) {
+      const int64_t l = 2 * b1 + 1 + c;
+      cs[c] = cm[c] = 0.0;
+      if (lane && l < cap) {
+        cs[c] = a.nd[l + 1].sum;
+        cm[c] = a.nd[l + 1].mn;
+      }
     }
-  }
+  };
+  if (!nsub) load_children();
 #pragma unroll
   for (int q = 0; q < 2; ++q) r2[q] = top_load(a.nd, lane ? cap : 0, b2 + q);
   // shuffle slot h = S-3-k holds level k (lane t owns it when t is a multiple of 2^h):
@@ -879,6 +901,24 @@ __device__ __forceinline__ void tree_top(const UpdArgs &a, int S, TopLds &L) {
     if (wu >= 0) uv[t] = priority_of(a, alpha, wu);
   }
   __syncthreads();
+  if (nsub) {  // wait for the subtree workgroups (bounded: a timeout is recorded, not hung on)
+    __shared__ int tmo;
+    if (t == 0) {
+      unsigned *const done = reinterpret_cast<unsigned *>(&a.nd[0].pad);
+      unsigned spins = 0;
+      while (__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nsub && spins < (1u << 24)) {
+        __builtin_amdgcn_s_sleep(2);
+        ++spins;
+      }
+      tmo = spins >= (1u << 24);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (tmo) atomicAdd(reinterpret_cast<unsigned long long *>(&g_upd_clock[9]), 1ull);
+    }
+    __syncthreads();
+    load_children();
+  }
   if (a.timing && t == 0) g_upd_clock[6] = wall_clock64();
   // ---- the lane-local levels S-1, S-2, S-3
   TopVal cur{0.0, 0.0, 0};
@@ -1215,7 +1255,9 @@ int tree_update_impl(rth_sumtree *t, const int64_t *idx, int64_t fifo_start, con
   a.post_tail = post_tail;
   static const int timing = env_int("RTH_TREE_TIMING", 0);
   a.timing = timing;
-  static const int fuse = env_int("RTH_TREE_FUSE_TOP", 1);  // 0: the top pass as its own launch (A/B)
+  // RTH_TREE_FUSE_TOP: 2 = the top pass as a concurrent extra workgroup (r05), 1 = run by the
+  // subtree pass's last workgroup (r02-r04), 0 = its own launch (A/B)
+  static const int fuse = env_int("RTH_TREE_FUSE_TOP", 1);
   a.fuse_top = fuse;
   RTH_REQUIRE(a.pn + a.n < (int64_t(1) << 31), "tree update: at most 2^31 - 1 keys per call");
   const int S = t->maxd + 1 < kTopMinS ? kTopMinS : (t->maxd + 1 < kTopS ? t->maxd + 1 : kTopS);
@@ -1241,8 +1283,11 @@ int tree_update_impl(rth_sumtree *t, const int64_t *idx, int64_t fifo_start, con
       RTH_LAUNCHED();
     }
     const int64_t nsub = int64_t(1) << S;
-    a.stage = t->stage;  // the last pass stages the top pass's keys
-    hipLaunchKernelGGL(k_tree_update_sub, dim3((unsigned)(nsub < grid ? nsub : grid)), dim3(kSubThreads), 0, s, a, S,
+    const unsigned g_last = (unsigned)(nsub < grid ? nsub : grid);
+    // fuse_top 1: the last pass stages the top pass's keys for its last workgroup; 2: the top
+    // pass is one more workgroup of the launch and scans the keys itself
+    a.stage = a.fuse_top == 2 ? nullptr : t->stage;
+    hipLaunchKernelGGL(k_tree_update_sub, dim3(g_last + (a.fuse_top == 2 ? 1u : 0u)), dim3(kSubThreads), 0, s, a, S,
                        two ? S1 - 1 : t->maxd, 1);
     RTH_LAUNCHED();
     if (a.fuse_top) return RTH_OK;

@@ -124,6 +124,15 @@ PY
         done
       done
       summ gpurun_out/c2sab_*.log ;;
+    topab)  # tree update: the top pass as a concurrent extra workgroup (2) vs r04's last-workgroup form (1)
+      RTH_TREE_FUSE_TOP=2 step top_tests 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_sumtree_gpu.py \
+          tests/test_scale_gpu.py tests/test_samplers_gpu.py tests/test_replay_gpu.py tests/test_frame_store_gpu.py
+      RTH_TREE_FUSE_TOP=2 RTH_TREE_TIMING=1 step tree_phases_top2 300 python scripts/probe_tree_phases.py
+      for r in 1 2; do
+        RTH_TREE_FUSE_TOP=2 step topab_2_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        step topab_1_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+      done
+      summ gpurun_out/topab_*.log ;;
     tests) step gpu_tests 1100 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     t:*) f=${s#t:}; step "t_$(basename ${f//,/_} .py)" 900 python -u -m pytest -x -v --timeout 300 \

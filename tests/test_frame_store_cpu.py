@@ -1,0 +1,36 @@
+"""Frame-store sizing (ApexDQN.frame_store_frames, host logic): the "hard" bound holds every
+frame a live row can reference whatever the episode lengths -- a row lives capacity / N actor
+steps, its oldest frame is at most n + 4 steps older than its append, and a step pushes at most
+2 N frames (N new tops + at most N reset frames) -- checked against a worst-case simulation of
+the push sequence; "expected" sizes for the i.i.d. episode-end rate only."""
+import pytest
+
+
+def _cfg(**kw):
+    from reth_amd.apex import ApexConfig
+
+    return ApexConfig(frame_store=True, **kw)
+
+
+@pytest.mark.parametrize("n_actors,capacity", [(16, 1024), (256, 1_000_000), (2048, 4_000_000), (32, 125_000)])
+def test_hard_bound_covers_worst_case(n_actors, capacity):
+    from reth_amd.apex import ApexDQN
+
+    cfg = _cfg(n_actors=n_actors, capacity=capacity)
+    F = ApexDQN.frame_store_frames(cfg)
+    steps_alive = -(-capacity // n_actors)  # FIFO: a row is overwritten capacity / N appends later
+    # worst case: every actor ends its episode every step (N tops + N reset frames per step)
+    # over the row's life plus the n + 4 steps before its append that its oldest frame may date from
+    worst = 2 * n_actors * (steps_alive + cfg.n_step + 4)
+    assert F >= worst, (F, worst)
+
+
+def test_bounds_and_validation():
+    from reth_amd.apex import ApexDQN
+
+    hard = ApexDQN.frame_store_frames(_cfg(n_actors=256, capacity=1_000_000))
+    exp = ApexDQN.frame_store_frames(_cfg(n_actors=256, capacity=1_000_000, frame_store_bound="expected"))
+    assert hard == 2 * 1_000_000 + 2 * (3 + 16) * 256 + 16
+    assert exp < hard and exp >= 1_000_000  # the expected-rate store: about capacity (1 + 2 p_done)
+    with pytest.raises(ValueError):
+        ApexDQN.frame_store_frames(_cfg(n_actors=16, capacity=1024, frame_store_bound="tight"))

@@ -540,6 +540,13 @@ int rth_fc_x9_supported(int64_t M, int64_t N, int64_t K);
 int64_t rth_fc_x9_workspace(int64_t M, int64_t N, int64_t K);
 int rth_fc_x9(const float *x_dev, int64_t ldx, int64_t M, const float *w_dev, int64_t N, int64_t K,
               const float *bias_dev, int32_t relu, float *y_dev, void *workspace_dev, void *stream);
+/* The same FC1 on the fp32 MFMA with no LDS (r05): the arguments, the workspace protocol and
+ * the determinism of rth_fc_x9; any M >= 1 (ragged actor batches), N % 128 == 0, K % 32 == 0
+ * (rth_fc_f32_supported).  Selected for the FC1 forwards by RTH_FC=f32. */
+int rth_fc_f32_supported(int64_t M, int64_t N, int64_t K);
+int64_t rth_fc_f32_workspace(int64_t M, int64_t N, int64_t K);
+int rth_fc_f32(const float *x_dev, int64_t ldx, int64_t M, const float *w_dev, int64_t N, int64_t K,
+               const float *bias_dev, int32_t relu, float *y_dev, void *workspace_dev, void *stream);
 int rth_conv_dgrad_ws(const rth_conv_shape *shape, const float *gy_dev, int64_t n, const float *w_ohwi_dev,
                       float *gx_dev, void *workspace_dev, void *stream);
 /* Weight gradient of conv2d(x, w) for the fp32 channels-last layers (conv2 and conv3 of the

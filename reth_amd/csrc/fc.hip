@@ -150,6 +150,121 @@ __global__ __launch_bounds__(kFcThreads) void k_fc_x9(const float *__restrict__ 
   }
 }
 
+// FC1 on the fp32 MFMA (v_mfma_f32_16x16x4_f32, the GEMM's own arithmetic) with no LDS (r05,
+// hipBLASLt's 512-row tile MT64x16x256 holds 80 KB of LDS per workgroup and runs
+// 48 us per launch in the loop against 21-26 alone).  Workgroup = 4 waves over a 64 x 128
+// output tile (wave (wm, wn) = rows 32 wm .. +31, columns 64 wn .. +63: 2 x 4 blocks of 16 x 16,
+// 8 independent accumulator chains) and one split of the 32-deep k chunks.  Each lane reads its
+// fragments straight from global memory (L2): per chunk, 8 consecutive floats (two 16-byte
+// loads) of each of its 2 A rows and 4 weight rows -- lane (r, g) holds k = 8 g + 4 h + t of row
+// r in register h, element t, and MFMA (h, t) feeds k-slot g with it, for A and B alike, so the
+// 8 MFMAs per block cover the chunk's 32 k.  NST chunks are in flight in a register ring.
+// Split s runs on blockIdx % splits: with 8 splits, on XCD s (round-robin dispatch), so one
+// XCD's L2 holds one K slice of x and w.  Fixed-order partials + k_fc_reduce, as k_fc_x9.
+// Rows past M (the ragged actor batches) read row M - 1 and are not written.
+constexpr int kFfTm = 64, kFfTn = 128, kFfThreads = 256;
+template <int NST>
+__global__ __launch_bounds__(kFfThreads) void k_fc_f32(const float *__restrict__ x, int64_t ldx, int M,
+                                                       const float *__restrict__ w, int N, int K, int splits,
+                                                       const float *__restrict__ bias, int relu,
+                                                       float *__restrict__ out) {
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, r = lane & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), wm = wave & 1, wn = wave >> 1;
+  const int split = (int)blockIdx.x % splits, tile = (int)blockIdx.x / splits;
+  const int tiles_n = N / kFfTn;
+  const int m0 = (tile / tiles_n) * kFfTm + 32 * wm, n0 = (tile % tiles_n) * kFfTn + 64 * wn;
+  const int chunks = K / 32;
+  const int c0 = chunks * split / splits, c1 = chunks * (split + 1) / splits;
+  // buffer loads: a per-lane row offset (voffset) and the chunk's byte offset as the uniform
+  // soffset, so a chunk's 12 loads need no address arithmetic (the host checks both operands
+  // are < 2^31 bytes)
+  const __amdgpu_buffer_rsrc_t xs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(x), 0,
+                                                                      (int)(((int64_t)(M - 1) * ldx + K) * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t ws = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(w), 0,
+                                                                      (int)((int64_t)N * K * 4), 0x00020000);
+  uint32_t xo[2], wo[4];
+#pragma unroll
+  for (int mb = 0; mb < 2; ++mb) {
+    const int row = m0 + 16 * mb + r;
+    xo[mb] = (uint32_t)(((int64_t)(row < M ? row : M - 1) * ldx + 8 * g) * 4);
+  }
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb) wo[nb] = (uint32_t)(((int64_t)(n0 + 16 * nb + r) * K + 8 * g) * 4);
+  f32x4 xa[NST][2][2], wb[NST][4][2];
+  auto ld = [](__amdgpu_buffer_rsrc_t rs, uint32_t vo, int so) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo, so, 0));
+  };
+  auto load = [&](int c, f32x4 (&a)[2][2], f32x4 (&b)[4][2]) __attribute__((always_inline)) {
+    const int so = c * 128;
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) b[nb][h] = ld(ws, wo[nb] + 16 * h, so);
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) a[mb][h] = ld(xs, xo[mb] + 16 * h, so);
+  };
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) acc[mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto compute = [&](const f32x4 (&a)[2][2], const f32x4 (&b)[4][2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+          for (int nb = 0; nb < 4; ++nb)
+            acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[mb][h][t], b[nb][h][t], acc[mb][nb], 0, 0, 0);
+  };
+  // ring: before chunk c0 + i, set i % NST holds it and the next NST - 1 are in flight; past
+  // c1 - 1 the loads repeat the range's last chunk (in bounds, unused)
+#pragma unroll
+  for (int s = 0; s < NST; ++s) load(c0 + s < c1 ? c0 + s : c1 - 1, xa[s], wb[s]);
+  auto iter = [&](int c, auto is) __attribute__((always_inline)) {
+    constexpr int s = decltype(is)::value;
+    // the fence keeps each set's loads among its own MFMAs (left alone, the compiler moves
+    // every MFMA of the unrolled ring ahead of every load and then waits for them in order; a
+    // fence on both sides of the MFMAs makes it rotate the accumulators through copies)
+    compute(xa[s], wb[s]);
+    const int cn = c + NST < c1 ? c + NST : c1 - 1;
+    load(cn, xa[s], wb[s]);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  int c = c0;
+  for (; c + NST <= c1; c += NST)
+    static_for(std::make_integer_sequence<int, NST>{}, [&](auto is) __attribute__((always_inline)) {
+      iter(c + decltype(is)::value, is);
+    });
+  static_for(std::make_integer_sequence<int, NST>{}, [&](auto is) __attribute__((always_inline)) {
+    if (c + decltype(is)::value < c1) compute(xa[decltype(is)::value], wb[decltype(is)::value]);
+  });
+  // D: lane holds rows 4 g + i of each 16-row block, column r of each 16-column block
+  float *dst = splits == 1 ? out : out + (int64_t)split * M * N;
+#pragma unroll
+  for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + 16 * mb + 4 * g + i;
+      if (m < M) {
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb) {
+          const int n = n0 + 16 * nb + r;
+          float v = acc[mb][nb][i];
+          if (splits == 1) {
+            v = radd(v, bias ? bias[n] : 0.0f);
+            v = relu ? fc_relu(v) : v;
+          }
+          dst[(int64_t)m * N + n] = v;
+        }
+      }
+    }
+}
+
 // y = act(b + sum of the splits' partials, in split order), 4 outputs per thread
 __global__ __launch_bounds__(256) void k_fc_reduce(const float *__restrict__ part, int splits, int64_t MN, int N,
                                                    const float *__restrict__ bias, int relu, float *__restrict__ y,
@@ -182,6 +297,21 @@ static int fc_splits(int M, int N, int K) {
   }();
   const int tiles = (M / kFcTm) * (N / kFcTn), chunks = K / 32;
   int s = env > 0 ? env : (256 + tiles - 1) / tiles;
+  s = s < 1 ? 1 : (s > 32 ? 32 : s);
+  return s < chunks ? s : chunks;
+}
+
+// k_fc_f32's k splits: 8 (one K slice per XCD) while that gives at most 512 workgroups, else
+// fewer; RTH_FCF_SPLITS overrides (A/B); never more than the chunk count
+static int fcf_splits(int M, int N, int K) {
+  static const int env = [] {
+    const char *e = getenv("RTH_FCF_SPLITS");
+    return e ? atoi(e) : 0;
+  }();
+  const int tiles = ((M + kFfTm - 1) / kFfTm) * (N / kFfTn), chunks = K / 32;
+  int s = env > 0 ? env : 8;
+  if (env <= 0)
+    while (s > 1 && tiles * s > 512) s /= 2;
   s = s < 1 ? 1 : (s > 32 ? 32 : s);
   return s < chunks ? s : chunks;
 }
@@ -231,6 +361,55 @@ int rth_fc_x9(const float *x, int64_t ldx, int64_t M, const float *w, int64_t N,
     hipLaunchKernelGGL(k_fc_x9<2>, dim3((unsigned)(tiles * splits)), dim3(kFcThreads), 0, s, x, ldx, (int)M, w,
                        (int)N, (int)K, splits, bias, (int)relu, out);
   RTH_LAUNCHED();
+  if (splits > 1) {
+    const int64_t MN = M * N;
+    hipLaunchKernelGGL(k_fc_reduce, dim3((unsigned)((MN / 4 + 255) / 256)), dim3(256), 0, s,
+                       static_cast<const float *>(workspace), splits, MN, (int)N, bias, (int)relu, y, N);
+    RTH_LAUNCHED();
+  }
+  return RTH_OK;
+}
+
+int rth_fc_f32_supported(int64_t M, int64_t N, int64_t K) {
+  return M > 0 && N > 0 && N % kFfTn == 0 && K >= 32 && K % 32 == 0 && M * K < (1ll << 31) && N * K < (1ll << 31) &&
+                 M * N * 32 < (1ll << 31)
+             ? 1
+             : 0;
+}
+
+int64_t rth_fc_f32_workspace(int64_t M, int64_t N, int64_t K) {
+  if (!rth_fc_f32_supported(M, N, K)) return 0;
+  const int s = fcf_splits((int)M, (int)N, (int)K);
+  return s > 1 ? (int64_t)s * M * N * 4 : 0;
+}
+
+int rth_fc_f32(const float *x, int64_t ldx, int64_t M, const float *w, int64_t N, int64_t K, const float *bias,
+               int32_t relu, float *y, void *workspace, void *stream) {
+  RTH_REQUIRE(x && w && y, "rth_fc_f32: NULL argument");
+  RTH_REQUIRE(rth_fc_f32_supported(M, N, K), "rth_fc_f32: shape %lld x %lld x %lld not built (N %% 128, K %% 32)",
+              (long long)M, (long long)N, (long long)K);
+  RTH_REQUIRE(ldx >= K && ldx % 4 == 0 && ((M - 1) * ldx + K) * 4 < (1ll << 31), "rth_fc_f32: row stride %lld",
+              (long long)ldx);
+  RTH_REQUIRE(((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(y)) &
+               15) == 0,
+              "rth_fc_f32: misaligned buffer");
+  const int splits = fcf_splits((int)M, (int)N, (int)K);
+  RTH_REQUIRE(splits == 1 || (workspace && (reinterpret_cast<uintptr_t>(workspace) & 15) == 0),
+              "rth_fc_f32: %d splits need the workspace (rth_fc_f32_workspace)", splits);
+  hipStream_t s = as_stream(stream);
+  const int tiles = (int)((M + kFfTm - 1) / kFfTm) * (int)(N / kFfTn);
+  float *out = splits == 1 ? y : static_cast<float *>(workspace);
+  static const int nst = [] {  // RTH_FCF_NST: chunks in flight (2, 3 or 4)
+    const char *e = getenv("RTH_FCF_NST");
+    const int v = e ? atoi(e) : 3;
+    return v == 2 || v == 4 ? v : 3;
+  }();
+  const void *fn = nst == 2   ? reinterpret_cast<const void *>(&k_fc_f32<2>)
+                   : nst == 4 ? reinterpret_cast<const void *>(&k_fc_f32<4>)
+                              : reinterpret_cast<const void *>(&k_fc_f32<3>);
+  int Mi = (int)M, Ni = (int)N, Ki = (int)K, re = (int)relu;
+  void *args[] = {&x, &ldx, &Mi, &w, &Ni, &Ki, const_cast<int *>(&splits), &bias, &re, &out};
+  RTH_HIP(hipLaunchKernel(fn, dim3((unsigned)(tiles * splits)), dim3(kFfThreads), args, 0, s));
   if (splits > 1) {
     const int64_t MN = M * N;
     hipLaunchKernelGGL(k_fc_reduce, dim3((unsigned)((MN / 4 + 255) / 256)), dim3(256), 0, s,

@@ -412,30 +412,35 @@ class _MergeHeads(torch.autograd.Function):
         return (None, *grads)
 
 
-# RTH_FC_X9=1: FC1 + bias + ReLU on rth_fc_x9 (the exact-split bf16 MFMA, fixed-order split-K)
-# instead of hipBLASLt's GEMM with the bias+ReLU epilogue, wherever the shape is built
-_FC_X9 = os.environ.get("RTH_FC_X9") == "1"
+# FC1 + bias + ReLU: RTH_FC=f32 -> rth_fc_f32 (fp32 MFMA, no LDS, fixed-order split-K),
+# RTH_FC=x9 (or RTH_FC_X9=1) -> rth_fc_x9 (the exact-split bf16 MFMA), wherever the shape is
+# built; otherwise hipBLASLt's GEMM with the bias+ReLU epilogue.  RTH_FC_MAX_ROWS limits the
+# hand-written kernels to batches of at most that many rows (the rest stay on hipBLASLt)
+_FC_KIND = os.environ.get("RTH_FC", "x9" if os.environ.get("RTH_FC_X9") == "1" else "blas")
+_FC_MAX_ROWS = int(os.environ.get("RTH_FC_MAX_ROWS", "0") or 0)
 _FC_WS = {}
 
 
 def fc1_relu(x, w, b, out=None):
-    """relu(x @ w.T + b) (FC1 of both dueling branches): rth_fc_x9 when enabled and built for
-    the shape, else one hipBLASLt GEMM with the bias+ReLU epilogue.  The split-K workspace is
-    keyed by the weight storage, so two networks (the actors', the target's, the learner's --
-    on different streams) never share one"""
+    """relu(x @ w.T + b) (FC1 of both dueling branches): rth_fc_f32 / rth_fc_x9 when selected
+    (RTH_FC) and built for the shape, else one hipBLASLt GEMM with the bias+ReLU epilogue.  The
+    split-K workspace is keyed by the weight storage, so two networks (the actors', the
+    target's, the learner's -- on different streams) never share one"""
     M, K = x.shape
     N = w.shape[0]
-    if _FC_X9 and x.is_cuda and x.stride(1) == 1 and w.is_contiguous():
+    if _FC_KIND in ("f32", "x9") and x.is_cuda and x.stride(1) == 1 and w.is_contiguous() and \
+            (_FC_MAX_ROWS <= 0 or M <= _FC_MAX_ROWS):
         from ._lib import call, lib, ptr, stream_ptr
 
-        if lib().rth_fc_x9_supported(M, N, K):
+        fn = "rth_fc_" + _FC_KIND
+        if getattr(lib(), fn + "_supported")(M, N, K):
             y = out if out is not None else torch.empty((M, N), dtype=torch.float32, device=x.device)
-            key = (x.device, w.data_ptr(), M, N, K)
+            key = (x.device, w.data_ptr(), M, N, K, fn)
             ws = _FC_WS.get(key)
             if ws is None:
-                ws = _FC_WS[key] = torch.empty(max(lib().rth_fc_x9_workspace(M, N, K), 16) // 4,
+                ws = _FC_WS[key] = torch.empty(max(getattr(lib(), fn + "_workspace")(M, N, K), 16) // 4,
                                                dtype=torch.float32, device=x.device)
-            call("rth_fc_x9", ptr(x), x.stride(0), M, ptr(w), N, K, ptr(b), 1, ptr(y), ptr(ws), stream_ptr())
+            call(fn, ptr(x), x.stride(0), M, ptr(w), N, K, ptr(b), 1, ptr(y), ptr(ws), stream_ptr())
             return y
     if out is not None:
         return torch._addmm_activation(b, x, w.t(), out=out)

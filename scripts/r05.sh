@@ -122,6 +122,8 @@ PY
         for v in static dyn ns2dyn pw2 pw2dyn; do
           RTH_CONV2_SCHED=$v step c2sab_${v}_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
         done
+        RTH_CONV2_SCHED=pw2dyn RTH_X9_WG_PER_CU=2 step c2sab_pw2dynx9_$r 300 python bench.py --steps 300 --warmup 5 \
+            --no-cpu-baseline --no-sweep
       done
       summ gpurun_out/c2sab_*.log ;;
     topab)  # tree update: the top pass as a concurrent extra workgroup (2) vs r04's last-workgroup form (1)
@@ -133,6 +135,21 @@ PY
         step topab_1_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
       done
       summ gpurun_out/topab_*.log ;;
+    fcf)  # FC1 on the fp32 MFMA without LDS (rth_fc_f32): tests, alone (ring depth, splits), in the loop
+      step fcf_tests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_fc_gpu.py
+      step fcf_micro 120 python scripts/bench_fc.py
+      RTH_FCF_NST=2 FC_MS=256,512,1024 step fcf_micro_nst2 120 python scripts/bench_fc.py
+      RTH_FCF_NST=4 FC_MS=256,512,1024 step fcf_micro_nst4 120 python scripts/bench_fc.py
+      RTH_FCF_SPLITS=16 FC_MS=256,512,1024 step fcf_micro_s16 120 python scripts/bench_fc.py
+      RTH_FCF_SPLITS=4 FC_MS=256,512,1024 step fcf_micro_s4 120 python scripts/bench_fc.py
+      grep -h "M=" gpurun_out/fcf_micro*.log
+      for r in 1 2; do
+        step fcab_blas_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        RTH_FC=f32 step fcab_f32_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        RTH_FC=f32 RTH_FC_MAX_ROWS=512 step fcab_f32s_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline \
+            --no-sweep
+      done
+      summ gpurun_out/fcab_*.log ;;
     tests) step gpu_tests 1100 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     t:*) f=${s#t:}; step "t_$(basename ${f//,/_} .py)" 900 python -u -m pytest -x -v --timeout 300 \

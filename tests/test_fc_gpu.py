@@ -1,8 +1,9 @@
-"""rth_fc_x9: FC1 of the dueling heads (dqn_model.py:38-47, both branches' first Linear as one
-[512, 3136] weight) on the exact-split bf16 MFMA, against a float64 CPU reference of
-relu(x w^T + b): within fp32 summation error (the products are exact; only the order of the
-fp32 sums differs from an fp32 GEMM), run-to-run bit-identical, every output written, the
-split-K and single-split paths, a strided x and no bias / no ReLU."""
+"""rth_fc_x9 / rth_fc_f32: FC1 of the dueling heads (dqn_model.py:38-47, both branches' first
+Linear as one [512, 3136] weight) on the exact-split bf16 MFMA and on the fp32 MFMA (r05),
+against a float64 CPU reference of relu(x w^T + b): within fp32 summation error (the products
+are exact; only the order of the fp32 sums differs from an fp32 GEMM), run-to-run
+bit-identical, every output written, the split-K and single-split paths, a strided x, no bias /
+no ReLU, and (rth_fc_f32) ragged row counts -- the actors' N + k live rows."""
 import numpy as np
 import pytest
 import torch
@@ -10,30 +11,30 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _run(dev, x, w, b, relu, ldx=None):
+def _run(dev, x, w, b, relu, ldx=None, kind="x9"):
     from reth_amd import _lib
 
     M, K = x.shape[0], w.shape[1]
     N = w.shape[0]
-    ws = torch.empty(max(_lib.lib().rth_fc_x9_workspace(M, N, K), 16) // 4, device=dev)
+    fn = "rth_fc_" + kind
+    ws = torch.empty(max(getattr(_lib.lib(), fn + "_workspace")(M, N, K), 16) // 4, device=dev)
     y = torch.full((M, N), float("nan"), device=dev)
-    _lib.call("rth_fc_x9", x.data_ptr(), ldx or K, M, w.data_ptr(), N, K, b.data_ptr() if b is not None else None,
+    _lib.call(fn, x.data_ptr(), ldx or K, M, w.data_ptr(), N, K, b.data_ptr() if b is not None else None,
               int(relu), y.data_ptr(), ws.data_ptr(), _lib.stream_ptr())
     return y
 
 
-@pytest.mark.parametrize("M", [64, 512, 1024, 2048])
-def test_fc_x9_vs_fp64(dev, M):
+def _check_vs_fp64(dev, M, kind):
     from reth_amd import _lib
 
     N, K = 512, 3136
-    assert _lib.lib().rth_fc_x9_supported(M, N, K) == 1
+    assert getattr(_lib.lib(), f"rth_fc_{kind}_supported")(M, N, K) == 1
     g = torch.Generator(device=dev).manual_seed(M)
     x = torch.rand((M, K), device=dev, generator=g) * 3  # post-ReLU features: non-negative, O(1)
     w = (torch.rand((N, K), device=dev, generator=g) * 2 - 1) / np.sqrt(K)
     b = (torch.rand(N, device=dev, generator=g) * 2 - 1) * 0.1
-    y = _run(dev, x, w, b, True)
-    y2 = _run(dev, x, w, b, True)
+    y = _run(dev, x, w, b, True, kind=kind)
+    y2 = _run(dev, x, w, b, True, kind=kind)
     assert torch.equal(y, y2)
     assert not torch.isnan(y).any()
     want = torch.relu(x.double().cpu() @ w.double().cpu().t() + b.double().cpu())
@@ -44,22 +45,63 @@ def test_fc_x9_vs_fp64(dev, M):
     assert err <= max(4 * err32, 2e-6), (err, err32)
 
 
-def test_fc_x9_strided_no_bias_no_relu(dev):
+@pytest.mark.parametrize("M", [64, 512, 1024, 2048])
+def test_fc_x9_vs_fp64(dev, M):
+    _check_vs_fp64(dev, M, "x9")
+
+
+@pytest.mark.parametrize("M", [1, 64, 256, 259, 512, 1024, 2048])
+def test_fc_f32_vs_fp64(dev, M):
+    _check_vs_fp64(dev, M, "f32")
+
+
+@pytest.mark.parametrize("kind", ["x9", "f32"])
+def test_fc_strided_no_bias_no_relu(dev, kind):
     M, N, K = 128, 256, 96
     g = torch.Generator(device=dev).manual_seed(3)
     big = torch.randn((M, K + 32), device=dev, generator=g)
     x = big[:, :K]
     w = torch.randn((N, K), device=dev, generator=g)
-    y = _run(dev, x, w, None, False, ldx=K + 32)
+    y = _run(dev, x, w, None, False, ldx=K + 32, kind=kind)
     want = x.double().cpu() @ w.double().cpu().t()
     assert (y.double().cpu() - want).abs().max().item() <= 1e-4
 
 
-def test_fc_x9_unsupported(dev):
+def test_fc_f32_split_counts_agree(dev):
+    """every k-split count gives the same outputs within fp32 summation error (the splits'
+    partials summed in split order), each bit-identical run to run -- the RTH_FCF_SPLITS knob
+    changes the summation order only (child processes: the knob is read once per process)"""
+    import os
+    import subprocess
+    import sys
+
+    code = ("import torch, numpy as np, sys; sys.path.insert(0, '.');"
+            "from tests.test_fc_gpu import _run; dev = torch.device('cuda');"
+            "g = torch.Generator(device=dev).manual_seed(7);"
+            "x = torch.rand((512, 3136), device=dev, generator=g);"
+            "w = (torch.rand((512, 3136), device=dev, generator=g) * 2 - 1) / 56;"
+            "b = torch.rand(512, device=dev, generator=g) * 0.1;"
+            "y = _run(dev, x, w, b, True, kind='f32'); y2 = _run(dev, x, w, b, True, kind='f32');"
+            "assert torch.equal(y, y2); np.save(sys.argv[1], y.cpu().numpy())")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    outs = []
+    for s in ("1", "4", "8", "16"):
+        path = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"fcf_split_{s}_{os.getpid()}.npy")
+        env = dict(os.environ, RTH_FCF_SPLITS=s)
+        subprocess.run([sys.executable, "-c", code, path], cwd=root, env=env, check=True, timeout=240)
+        outs.append(np.load(path))
+        os.remove(path)
+    for o in outs[1:]:
+        assert np.abs(o - outs[0]).max() <= 2e-5
+
+
+@pytest.mark.parametrize("kind", ["x9", "f32"])
+def test_fc_unsupported(dev, kind):
     from reth_amd import _lib
 
-    assert _lib.lib().rth_fc_x9_supported(100, 512, 3136) == 0
+    fn = "rth_fc_" + kind
+    assert getattr(_lib.lib(), fn + "_supported")(100, 500, 3136) == 0
     t = torch.zeros(16, device=dev)
     with pytest.raises(_lib.RethHipError, match="not built"):
-        _lib.call("rth_fc_x9", t.data_ptr(), 3136, 100, t.data_ptr(), 512, 3136, None, 1, t.data_ptr(), None,
+        _lib.call(fn, t.data_ptr(), 3136, 100, t.data_ptr(), 500, 3136, None, 1, t.data_ptr(), None,
                   _lib.stream_ptr())

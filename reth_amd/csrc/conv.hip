@@ -31,7 +31,6 @@
 #include <mutex>
 #include <string>
 #include <type_traits>
-#include <unordered_map>
 
 #include "common.hpp"
 
@@ -86,21 +85,18 @@ __device__ unsigned long long g_conv_clock[kClockSlots][2];
 // part t % NS), for more, smaller tiles over the SIMDs; each output keeps its K order.
 // PW (r05): the channel part is fixed per workgroup (blockIdx % NS; the grid a multiple of NS)
 // and the workgroup stages only that part's weights -- 1 / NS of the LDS, so a workgroup of
-// the other stream's kernels (hipBLASLt's FC1 tiles, an x9 conv) fits on the same CU
-// DYN (r05): after its first tile a wave takes its tiles from a launch-wide counter (dyn[0];
-// dyn[1] counts finished workgroups, the last one re-arms both): a SIMD that the other
-// stream's kernels slow down takes fewer tiles, instead of the static round-robin making every
-// wave wait for the slowest SIMD.  Each output is computed exactly as in the static form.
-typedef __attribute__((address_space(1))) unsigned int conv_gu32;
+// the other stream's kernels (hipBLASLt's FC1 tiles, an x9 conv) fits on the same CU.
+// (A dynamic schedule -- waves claiming tiles from a launch-wide atomic counter -- was built
+// and measured in r05: 2x slower alone, 108 vs 57 us at 1,024 samples, since every claim is an
+// agent-scope atomic on one address from all 8 XCDs; removed.)
 template <int MODE, int KH, int KW, int S, int CIN, int COUT, int HIN, int WIN, int WAVES, int MB, int NS = 1,
-          int PW = 0, int DYN = 0>
+          int PW = 0>
 __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__restrict__ x,
                                                               const int64_t *__restrict__ rows, int64_t n,
                                                               const int64_t *__restrict__ n_dev,
                                                               const float *__restrict__ w,
                                                               const float *__restrict__ bias,
-                                                              float *__restrict__ y, int out_nchw,
-                                                              unsigned int *dyn) {
+                                                              float *__restrict__ y, int out_nchw) {
   using Gm = ConvGeom<MODE, KH, KW, S, CIN, COUT, HIN, WIN>;
   constexpr bool F32 = MODE == RTH_CONV_F32_NHWC;
   constexpr int G = Gm::G, NB = Gm::NB, T = WAVES * 64, NBW = NB / NS;
@@ -163,22 +159,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__res
   const int64_t slot = WAVES % 4 == 0 ? (int64_t)(wave / 4) * wgs * 4 + wgi * 4 + wave % 4 : wgi * WAVES + wave;
   // the first tile's leading input chunks are requested before the weights are staged
   int64_t tile = slot;
-  conv_gu32 *const dctr = (conv_gu32 *)dyn;
-  // DYN: claim the next unclaimed tile (lane 0 asks for the wave).  The claim stays in lane 0's
-  // register until it is needed a whole tile later (claimed()): read at once, the wait for the
-  // atomic would also wait for every load issued before it -- the tile's prefetched chunks
-  auto grab = [&]() -> unsigned int {
-    // the address offset mbcnt_lo(0, 0) is 0 in every lane, but not provably uniform: the
-    // compiler's atomic optimizer (a wave scan + an immediate read of the result) leaves the
-    // single-lane atomic alone, so nothing waits for it before claimed()
-    conv_gu32 *p = dctr + __builtin_amdgcn_mbcnt_lo(0u, 0u);
-    unsigned int v = 0;
-    if (lane == 0) v = __hip_atomic_fetch_add(p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return v;
-  };
-  auto claimed = [&](unsigned int v) -> int64_t { return wgs * WAVES + (int64_t)__builtin_amdgcn_readfirstlane(v); };
-  // the tile after this one, known a whole tile ahead (DYN: claimed a tile ahead)
-  int64_t tnext = DYN ? claimed(grab()) : tile + tstride;
+  int64_t tnext = tile + tstride;  // the tile after this one
   const uint8_t *cur[MB], *nxt[MB];
   bases((tile < tiles ? tile : tiles - 1) / TD, cur);
   Frag ar[D][MB];
@@ -216,7 +197,6 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__res
   const f32x4 *wlane = wl + lane;
 
   for (; tile < tiles;) {
-    const unsigned int claim2 = DYN ? grab() : 0u;  // the tile after next, read at this loop's end
     const int nb0 = PW ? part * NBW : (NS == 1 ? 0 : (int)(tile % NS) * NBW);  // output channel block
     const int lb0 = PW ? 0 : nb0;                                               // its LDS block
     if constexpr (NS > 1 && !PW) {
@@ -300,18 +280,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__res
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb) cur[mb] = nxt[mb];
     tile = tnext;
-    tnext = DYN ? claimed(claim2) : tnext + tstride;
-  }
-  if constexpr (DYN) {  // the last workgroup out re-arms the counters for the next launch
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every claim of this wave has landed
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const unsigned int done = __hip_atomic_fetch_add(dctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (done == gridDim.x - 1) {
-        __hip_atomic_store(dctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(dctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
+    tnext += tstride;
   }
 #ifdef RTH_CLOCK_STAMPS
   if (threadIdx.x == 0 && blockIdx.x < kClockSlots) {
@@ -1094,7 +1063,6 @@ struct ConvLaunch {
   int64_t big_above;
   int big_off;
   int pw;   // k_conv_bias_relu PW: channel part per workgroup (the grid a multiple of nsplit)
-  int dyn;  // k_conv_bias_relu DYN: tiles claimed from a launch-wide counter (dyn_counter())
 };
 
 template <int KH, int KW, int S, int CIN, int HIN, int WIN, int NSAMP, int ROT, int KS>
@@ -1111,13 +1079,12 @@ static ConvLaunch x9_launch() {
 }
 
 template <int MODE, int KH, int KW, int S, int CIN, int COUT, int HIN, int WIN, int WAVES, int MB, int NS = 1,
-          int PW = 0, int DYN = 0>
+          int PW = 0>
 static ConvLaunch conv_launch() {
   using Gm = ConvGeom<MODE, KH, KW, S, CIN, COUT, HIN, WIN>;
-  ConvLaunch l{reinterpret_cast<const void *>(&k_conv_bias_relu<MODE, KH, KW, S, CIN, COUT, HIN, WIN, WAVES, MB, NS, PW,
-                                                                DYN>),
+  ConvLaunch l{reinterpret_cast<const void *>(&k_conv_bias_relu<MODE, KH, KW, S, CIN, COUT, HIN, WIN, WAVES, MB, NS, PW>),
                reinterpret_cast<const void *>(&k_conv_pack<MODE, KH, KW, S, CIN, COUT, HIN, WIN>), WAVES,
-               Gm::LDS_F4 * 16, 0, 16 * MB, 0, NS, 0, {}, nullptr, 0, 0, PW, DYN};
+               Gm::LDS_F4 * 16, 0, 16 * MB, 0, NS, 0, {}, nullptr, 0, 0, PW};
   int blocks = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, l.fn, WAVES * 64, 0) != hipSuccess || blocks < 1)
     blocks = 1;
@@ -1227,17 +1194,14 @@ static bool find_conv(const rth_conv_shape &s, ConvLaunch *out, int *geom = null
     // RTH_CONV2_NS = 1 / 2 / 4: wave tiles of 16 pixels x 64 / 32 / 16 channels (finer tiles
     // even out the last round of tiles over the SIMDs)
     // (r04: 16 waves and 16-channel tiles measured slower; dropped)
-    // RTH_CONV2_SCHED (r05 A/B): static = r04's round-robin tiles; dyn = tiles claimed from a
-    // launch-wide counter; ns2 / ns2dyn = 16 x 32-channel half tiles, round-robin / claimed;
-    // pw2 / pw2dyn = half tiles with the channel part fixed per workgroup (half the LDS)
+    // RTH_CONV2_SCHED (r05 A/B): static = r04's round-robin tiles; ns2 = 16 x 32-channel half
+    // tiles, round-robin; pw2 = half tiles with the channel part fixed per workgroup (half the
+    // LDS: the other stream's workgroups fit beside it -- 0.543-0.544 vs 0.540-0.542 ms/step)
     static const ConvLaunch f32 = [] {
       const char *e = getenv("RTH_CONV2_SCHED");
       const std::string v = e ? e : (CONV2_NS == 2 ? "ns2" : "static");
-      if (v == "dyn") return conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 1, 0, 1>();
-      if (v == "ns2") return conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 2, 0, 0>();
-      if (v == "ns2dyn") return conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 2, 0, 1>();
-      if (v == "pw2") return conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 2, 1, 0>();
-      if (v == "pw2dyn") return conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 2, 1, 1>();
+      if (v == "ns2") return conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 2, 0>();
+      if (v == "pw2") return conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 2, 1>();
       return conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 1>();
     }();
     static const ConvLaunch l = [] {
@@ -2164,33 +2128,6 @@ static void select_launch(ConvLaunch *l, int64_t n, int64_t *w_off, int64_t *nsa
   }
 }
 
-// DYN launches' tile counters: one 2-word slot per packed-weight buffer (the learner's, the
-// target network's and the actors' convolutions run on different streams with different
-// packed buffers; one buffer is never used by two launches at once).  Zero at load; every
-// launch leaves its slot zero (the last workgroup re-arms it).
-constexpr int kDynSlots = 256;
-__device__ unsigned int g_conv_dyn[kDynSlots][2];
-static unsigned int *dyn_counter(const void *key) {
-  static std::mutex mu;
-  static std::unordered_map<const void *, int> slot_of[64];
-  static unsigned int *base[64] = {};
-  static int next[64] = {};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
-  std::lock_guard<std::mutex> lock(mu);
-  if (!base[dev] && hipGetSymbolAddress(reinterpret_cast<void **>(&base[dev]), HIP_SYMBOL(g_conv_dyn)) != hipSuccess)
-    return nullptr;
-  auto it = slot_of[dev].find(key);
-  int sl;
-  if (it != slot_of[dev].end()) {
-    sl = it->second;
-  } else {
-    sl = next[dev]++ % kDynSlots;
-    slot_of[dev][key] = sl;
-  }
-  return base[dev] + 2 * sl;
-}
-
 static int conv_bias_relu(const rth_conv_shape *shape, const void *x, const int64_t *rows, int64_t n,
                           const int64_t *n_dev, const float *w, const float *bias, float *y, void *stream) {
   RTH_REQUIRE(shape && x && w && bias && y && n >= 0, "rth_conv_bias_relu: NULL argument");
@@ -2237,10 +2174,8 @@ static int conv_bias_relu(const rth_conv_shape *shape, const void *x, const int6
     grid = grid / ns * ns;
     if (grid < ns) grid = ns;
   }
-  unsigned int *dyn = l.dyn ? dyn_counter(w) : nullptr;
-  RTH_REQUIRE(!l.dyn || dyn, "rth_conv_bias_relu: no tile counter for the dynamic schedule");
   void *args[] = {(void *)&x, (void *)&rows, (void *)&n, (void *)&n_dev, (void *)&w, (void *)&bias, (void *)&y,
-                  (void *)&out_nchw, (void *)&dyn};  // (k_conv1_u8_bf16x3 takes the first seven)
+                  (void *)&out_nchw};  // (k_conv1_u8_bf16x3 takes the first seven)
   RTH_HIP(hipLaunchKernel(l.fn, dim3((unsigned)grid), dim3(l.waves * 64), args, 0, as_stream(stream)));
   return RTH_OK;
 }

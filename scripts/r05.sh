@@ -114,16 +114,14 @@ PY
     c2sched)  # conv2 tile schedules: tests, alone, in the loop
       step c2s_tests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_conv_gpu.py \
           -k "schedules or conv_f32_nhwc or partial or upto"
-      for v in static dyn ns2dyn pw2 pw2dyn; do
+      for v in static ns2 pw2; do
         RTH_CONV2_SCHED=$v CONV_NS=1024,512,256 step c2s_micro_$v 120 python scripts/bench_conv.py
       done
       grep -H "conv2" gpurun_out/c2s_micro_*.log
       for r in 1 2; do
-        for v in static dyn ns2dyn pw2 pw2dyn; do
+        for v in static ns2 pw2; do
           RTH_CONV2_SCHED=$v step c2sab_${v}_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
         done
-        RTH_CONV2_SCHED=pw2dyn RTH_X9_WG_PER_CU=2 step c2sab_pw2dynx9_$r 300 python bench.py --steps 300 --warmup 5 \
-            --no-cpu-baseline --no-sweep
       done
       summ gpurun_out/c2sab_*.log ;;
     topab)  # tree update: the top pass as a concurrent extra workgroup (2) vs r04's last-workgroup form (1)

@@ -654,7 +654,7 @@ _lib.call("rth_conv_pack", _lib.ctypes.byref(shape), wt.data_ptr(), pk.data_ptr(
 out = {}
 for n in (1, 3, 64, 700, 1024):
     x = torch.rand((n, 20, 20, 32), device=dev, generator=g)
-    for rep in range(3):  # the same buffers again: a claim counter left armed would skip tiles
+    for rep in range(2):  # the same buffers again
         y = torch.full((n, 9, 9, 64), float("nan"), device=dev)
         _lib.call("rth_conv_bias_relu", _lib.ctypes.byref(shape), x.data_ptr(), None, n, pk.data_ptr(), b.data_ptr(),
                   y.data_ptr(), _lib.stream_ptr())
@@ -670,9 +670,8 @@ torch.save(out, sys.argv[2])
 
 def test_conv2_schedules_bit_identical(tmp_path, dev):
     """conv2's fp32-MFMA forward under every tile schedule (RTH_CONV2_SCHED: static round-robin,
-    tiles claimed from a launch-wide counter, half tiles, the channel part per workgroup) gives
-    the same bits: each output's MFMA chain is the same whichever wave computes it; repeated
-    launches on one packed buffer check that the claim counter is re-armed"""
+    half tiles, the channel part per workgroup) gives the same bits: each output's MFMA chain is
+    the same whichever wave computes it"""
     import subprocess
     import sys
 
@@ -681,7 +680,7 @@ def test_conv2_schedules_bit_identical(tmp_path, dev):
         torch.cuda.empty_cache()
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     res = {}
-    for sched in ("static", "dyn", "ns2", "ns2dyn", "pw2", "pw2dyn"):
+    for sched in ("static", "ns2", "pw2"):
         path = tmp_path / f"{sched}.pt"
         p = subprocess.run([sys.executable, "-c", _C2_CHILD, root, str(path)],
                            env=dict(os.environ, RTH_CONV2_SCHED=sched), capture_output=True, text=True, timeout=120)

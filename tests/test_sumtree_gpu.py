@@ -244,3 +244,23 @@ def test_find_lane_groups(dev, orc, golden, monkeypatch, gk, top):
         assert np.array_equal(idx.cpu().numpy(), g[f"{tag}/find"]), tag
         idx, val = t.sample(len(g[f"{tag}/sample_u"]), uniforms=g[f"{tag}/sample_u"])
         assert np.array_equal(idx.cpu().numpy(), g[f"{tag}/sample_idx"]), tag
+
+
+@pytest.mark.parametrize("fuse", ["0", "1"])
+def test_top_pass_forms_against_oracle(fuse):
+    """the tree update's other top-pass forms (RTH_TREE_FUSE_TOP, read once per process: a child
+    pytest): 1 = run by the subtree pass's last workgroup on keys it staged (r02-r04), 0 = its
+    own launch -- the same trees as the default concurrent extra workgroup (2), bit for bit
+    against the oracle and the reference's large golden state"""
+    import os
+    import subprocess
+    import sys
+
+    if torch.cuda.is_initialized():
+        torch.cuda.synchronize()
+    here = os.path.dirname(os.path.abspath(__file__))
+    p = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider", os.path.abspath(__file__),
+                        "-k", "random_against_oracle or golden_large or bulk_update"],
+                       cwd=os.path.dirname(here), env=dict(os.environ, RTH_TREE_FUSE_TOP=fuse), capture_output=True,
+                       text=True, timeout=280)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-2000:]

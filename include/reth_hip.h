@@ -64,6 +64,10 @@ const char *rth_build_id(void);
  * actor / learner blocks, reth_amd.apex.ApexDQN.upload_graphs: a graph's first launch then
  * carries no upload) */
 int rth_graph_upload(void *graph_exec, void *stream);
+/* The number of nodes the next operation captured on `stream` would depend on (0 at the start
+ * of a capture and until something is captured), or -1 when the stream is not capturing:
+ * ApexDQN's graph cuts skip a part that would be empty (two boundaries back to back). */
+int rth_stream_capture_deps(void *stream);
 
 /* ------------------------------------------------------------------------------------
  * In-order heap sum-tree, fp64, resident in HBM.

@@ -39,6 +39,29 @@ from .trainer import Trainer
 from .weights import WeightsSlot, WeightsSubscriber
 
 
+def _end_part(parts, stream):
+    """end the capture of parts[-1] on `stream`.  A part with nothing captured (two graph
+    boundaries back to back: a probed launch right before a gradient bucket, say) is proved
+    empty by the stream's capture state -- no node for the next capture to depend on
+    (rth_stream_capture_deps == 0) -- and becomes None, skipped at replay, instead of an empty
+    graph (torch warns "The CUDA Graph is empty" for one, the warning that also flags a capture
+    on the wrong stream, which this check would not hide: that part's launches leave the
+    capturing stream with no node either, but they then run eagerly right here, and the
+    probe-copy test compares every result against the uncut graph's)."""
+    import warnings
+
+    from . import _lib
+
+    empty = _lib.lib().rth_stream_capture_deps(stream.cuda_stream) == 0  # (< 0: not capturing, or an error)
+    if not empty:
+        parts[-1].capture_end()
+        return
+    with warnings.catch_warnings():
+        warnings.filterwarnings("ignore", message="The CUDA Graph is empty")
+        parts[-1].capture_end()
+    parts[-1] = None
+
+
 @dataclass
 class ApexConfig:
     n_actors: int = 256            # actors on this GPU (BASELINE configs[1]: 256 vectorised actors)
@@ -330,16 +353,17 @@ class ApexDQN:
                         key = ("probe", mode, k) if pr else (mode, k)
                         if pr and self.cfg.fused_actor:
                             parts, bounds = [torch.cuda.CUDAGraph()], []
+                            pool = parts[0]
 
-                            def cut(item, parts=parts, bounds=bounds):
-                                parts[-1].capture_end()
+                            def cut(item, parts=parts, bounds=bounds, pool=pool):
+                                _end_part(parts, side)
                                 bounds.append(("probe", item))
                                 parts.append(torch.cuda.CUDAGraph())
-                                parts[-1].capture_begin(pool=parts[0].pool())
+                                parts[-1].capture_begin(pool=pool.pool())
 
                             parts[0].capture_begin()
                             out = act.step_fused(self.actor_net, dedup=mode == "dedup", probe=cut)
-                            parts[-1].capture_end()
+                            _end_part(parts, side)
                             G["act"][key] = (parts, bounds)
                         else:
                             g = torch.cuda.CUDAGraph()
@@ -361,22 +385,24 @@ class ApexDQN:
             for pr, variant, p in [(pr, variant, p) for pr in psets for variant in ("full", "pre") for p in range(2)]:
                     v = ("probe", variant, p) if pr else (variant, p)
                     parts, bounds = [torch.cuda.CUDAGraph()], []
+                    pool = parts[0]
 
                     ended = []
 
-                    def cut(item, last=False, parts=parts, bounds=bounds, ended=ended):
+                    def cut(item, last=False, parts=parts, bounds=bounds, ended=ended, pool=pool):
                         # end this part of the learner graph at a boundary: ("bucket", a final
                         # gradient bucket -- its all-reduce runs between the parts, overlapping
                         # the next one) or ("probe", [(tag, launch), ...]) -- launches issued eagerly
                         # between the parts at every replay, each bracketed by the bench's HIP events).
-                        # last: nothing is captured after this boundary, so no (empty) part follows
-                        parts[-1].capture_end()
+                        # last: nothing is captured after this boundary, so no (empty) part follows;
+                        # a part with nothing in it becomes None (_end_part)
+                        _end_part(parts, side)
                         bounds.append(item)
                         if last:
                             ended.append(True)
                             return
                         parts.append(torch.cuda.CUDAGraph())
-                        parts[-1].capture_begin(pool=parts[0].pool())
+                        parts[-1].capture_begin(pool=pool.pool())
 
                     parts[0].capture_begin()
                     data, idx, isw = slots[p]
@@ -388,7 +414,7 @@ class ApexDQN:
                         cut(("bucket", [q.grad for q in solver._params]))
                     solver.apply_grads(probe=probe)
                     if not ended:
-                        parts[-1].capture_end()
+                        _end_part(parts, side)
                     G["learn"][v], G["buckets"][v], G["learn_td"][v] = parts, bounds, td
                     G["grads"][v] = [q.grad for q in solver._params]  # what apply_grads consumed
         torch.cuda.current_stream(self.device).wait_stream(side)
@@ -421,6 +447,7 @@ class ApexDQN:
             graphs += g[0] if isinstance(g, tuple) else [g]
         for parts in G["learn"].values():
             graphs += list(parts)
+        graphs = [g for g in graphs if g is not None]  # (empty parts: _end_part)
         st = self._stream if hasattr(self, "_stream") else torch.cuda.current_stream(self.device)
         for g in graphs:
             _lib.call("rth_graph_upload", g.raw_cuda_graph_exec(), st.cuda_stream)
@@ -438,7 +465,8 @@ class ApexDQN:
         """replay a graph captured in parts; between them the probed launches, each bracketed
         by conv_probe(tag) / conv_probe(tag + "_end")"""
         for i, g in enumerate(parts):
-            g.replay()
+            if g is not None:
+                g.replay()
             if i < len(bounds):
                 for tag, fn in bounds[i][1]:
                     self.conv_probe(tag)
@@ -456,14 +484,16 @@ class ApexDQN:
         G = self._graphs
         parts, bounds = G["learn"][v], G["buckets"][v]
         if not bounds:
-            parts[0].replay()
+            if parts[0] is not None:
+                parts[0].replay()
             return
         hook = self.solver.grad_hook
         cur = torch.cuda.current_stream(self.device)
         bucket_at = [i for i, (kind, _) in enumerate(bounds) if kind == "bucket"]
         comm = None
         for i, (g, (kind, item)) in enumerate(zip(parts, bounds)):
-            g.replay()
+            if g is not None:
+                g.replay()
             if kind == "probe":  # launches issued between the parts, optionally between HIP events
                 for tag, fn in item:
                     if self.conv_probe is not None:
@@ -490,7 +520,7 @@ class ApexDQN:
                     comm = None
         if comm is not None:
             cur.wait_stream(comm)
-        if len(parts) > len(bounds):  # a probe copy may end at its last probed launch
+        if len(parts) > len(bounds) and parts[-1] is not None:  # (a probe copy may end at its last probed launch)
             parts[-1].replay()
 
     def _actor_block_graph(self):

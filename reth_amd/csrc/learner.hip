@@ -79,6 +79,15 @@ int rth_graph_upload(void *graph_exec, void *stream) {
   return RTH_OK;
 }
 
+int rth_stream_capture_deps(void *stream) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  const hipGraphNode_t *deps = nullptr;
+  size_t n = 0;
+  const hipError_t e = hipStreamGetCaptureInfo_v2(as_stream(stream), &st, nullptr, nullptr, &deps, &n);
+  RTH_REQUIRE(e == hipSuccess, "rth_stream_capture_deps: %s", hipGetErrorString(e));
+  return st == hipStreamCaptureStatusActive ? (int)n : -1;
+}
+
 int rth_td_huber(const float *q0, const float *q1o, const float *q1t, const int64_t *a, const float *r,
                  const float *done, const double *isw, int64_t B, int64_t A, float gamma_n, int32_t double_q,
                  int32_t dueling, float *td_out, float *td_abs_out, float *loss_elem, float *loss_out, float *dq,

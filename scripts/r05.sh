@@ -148,6 +148,16 @@ PY
             --no-sweep
       done
       summ gpurun_out/fcab_*.log ;;
+    dp8)  # 8 ranks on one GPU over gloo: bench.py's multi-rank path and its teardown (shutdown())
+      RTH_SHARE_GPU=1 RTH_DIST_BACKEND=gloo step dp8_gloo_rehearsal 900 python -m torch.distributed.run --nnodes=1 \
+          --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 8 --faithful --steps 20 \
+          --warmup 5 --no-cpu-baseline --no-sweep
+      grep -c '"metric"' gpurun_out/dp8_gloo_rehearsal.log ;;
+    breakout)  # BASELINE configs[2]: the driver's command shape and a longer run
+      step bench_breakout_driver 600 python bench.py --workload breakout --steps 20 --warmup 5 --no-cpu-baseline \
+          --no-sweep
+      step bench_breakout 600 python bench.py --workload breakout --steps 100 --warmup 10 --no-cpu-baseline --no-sweep
+      summ gpurun_out/bench_breakout_driver.log gpurun_out/bench_breakout.log ;;
     tests) step gpu_tests 1100 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     t:*) f=${s#t:}; step "t_$(basename ${f//,/_} .py)" 900 python -u -m pytest -x -v --timeout 300 \

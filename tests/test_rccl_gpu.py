@@ -32,10 +32,13 @@ def say(**kw):
 
 dev = torch.device("cuda:0")
 
-def run(dp_hook, iters=40, keep=False):
+def run(dp_hook, iters=40, keep=False, probe=False):
     cfg = ApexConfig(n_actors=16, capacity=2048, batch_size=64, sample_start=128, seed=4, hip_graph=True,
-                     send_weights_interval=3, recv_weights_interval=4, update_target_interval=7, dp_hook=dp_hook)
+                     send_weights_interval=3, recv_weights_interval=4, update_target_interval=7, dp_hook=dp_hook,
+                     extra={"probe_conv2": True} if probe else {})
     ax = ApexDQN(cfg, device=dev, rank=0, world=1)
+    tags = []
+    ax.conv_probe = tags.append if probe else None
     for _ in range(iters):
         ax.iteration()
     torch.cuda.synchronize()
@@ -53,6 +56,15 @@ dist.all_reduce(t)
 torch.cuda.synchronize()
 say(stage="all_reduce", ok=bool(torch.equal(t.cpu(), torch.arange(8, dtype=torch.float32))))
 mode = sys.argv[3]
+if mode == "probe":  # the bench's probe copies cut at buckets AND probed launches: no empty part
+    import warnings
+    with warnings.catch_warnings(record=True) as wl:
+        warnings.simplefilter("always")
+        probed, parts, _ = run(True, probe=True)
+    plain, _, _ = run(False)
+    say(stage="probe", parts=parts, equal=bool(torch.equal(probed, plain)),
+        empty=sum("CUDA Graph is empty" in str(w.message) for w in wl))
+    os._exit(0)
 hooked, parts, alive = run(True, keep=mode != "keep")
 say(stage="hooked", parts=parts)
 plain, parts0, _ = run(False)
@@ -127,4 +139,15 @@ def test_rccl_bench_shutdown():
     normal interpreter exit with rc 0"""
     rc, st, err = _child("shutdown")
     assert "destroyed" in st and st["destroyed"]["initialized"] is False, (rc, st, err)
+    assert rc == 0, (rc, err)
+
+
+def test_rccl_probe_copies_have_no_empty_part():
+    """the bench's probe copies of the bucketed learner (cut at the gradient buckets and at the
+    probed launches; a probe right before a bucket leaves nothing between the two cuts): no
+    empty graph is captured (ApexDQN's _end_part drops such a part) and the result equals the
+    unhooked, unprobed loop's"""
+    rc, st, err = _child("probe")
+    assert "probe" in st, (rc, st, err)
+    assert st["probe"]["empty"] == 0 and st["probe"]["equal"], (rc, st, err)
     assert rc == 0, (rc, err)

@@ -483,6 +483,12 @@ class ApexDQN:
         records HIP events there on this stream for its live per-launch timing)."""
         G = self._graphs
         parts, bounds = G["learn"][v], G["buckets"][v]
+        if any(kind == "probe" for kind, _ in bounds):
+            # a launch issued between the parts (clip + Adam) reads the parameters' .grad when it
+            # runs: point them at this variant's gradient buffers (each captured variant has its
+            # own; the last capture left .grad on the last variant's)
+            for q, g in zip(self.solver._params, G["grads"][v]):
+                q.grad = g
         if not bounds:
             if parts[0] is not None:
                 parts[0].replay()

@@ -38,6 +38,13 @@ from .solver import Box, DQNSolver, Discrete
 from .trainer import Trainer
 from .weights import WeightsSlot, WeightsSubscriber
 
+# Every capture is thread-local: in the default global mode a stream-unsafe HIP call from ANY
+# thread during a capture is an error, and with a process group alive the RCCL watchdog thread
+# polls its collectives' end events (hipEventQuery) at any time -- a poll that lands inside one
+# of the learner's captures aborted the process (test_rccl_gpu, r05).  Thread-local mode keeps
+# the check for this (the capturing) thread only.
+_CAPTURE_MODE = "thread_local"
+
 
 def _end_part(parts, stream):
     """end the capture of parts[-1] on `stream`.  A part with nothing captured (two graph
@@ -359,15 +366,15 @@ class ApexDQN:
                                 _end_part(parts, side)
                                 bounds.append(("probe", item))
                                 parts.append(torch.cuda.CUDAGraph())
-                                parts[-1].capture_begin(pool=pool.pool())
+                                parts[-1].capture_begin(pool=pool.pool(), capture_error_mode=_CAPTURE_MODE)
 
-                            parts[0].capture_begin()
+                            parts[0].capture_begin(capture_error_mode=_CAPTURE_MODE)
                             out = act.step_fused(self.actor_net, dedup=mode == "dedup", probe=cut)
                             _end_part(parts, side)
                             G["act"][key] = (parts, bounds)
                         else:
                             g = torch.cuda.CUDAGraph()
-                            with torch.cuda.graph(g, stream=side):
+                            with torch.cuda.graph(g, stream=side, capture_error_mode=_CAPTURE_MODE):
                                 out = (act.step_fused(self.actor_net, dedup=mode == "dedup") if self.cfg.fused_actor
                                        else self._actor_compute())
                             G["act"][key] = g
@@ -378,7 +385,7 @@ class ApexDQN:
             # compute it themselves (after a target sync, and before any was precomputed)
             for p in range(2):
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, stream=side):
+                with torch.cuda.graph(g, stream=side, capture_error_mode=_CAPTURE_MODE):
                     q1t = solver.target_heads(slots[p][0][3])
                 G["tgt"].append(g)
                 G["q1t"].append(q1t)
@@ -402,9 +409,9 @@ class ApexDQN:
                             ended.append(True)
                             return
                         parts.append(torch.cuda.CUDAGraph())
-                        parts[-1].capture_begin(pool=pool.pool())
+                        parts[-1].capture_begin(pool=pool.pool(), capture_error_mode=_CAPTURE_MODE)
 
-                    parts[0].capture_begin()
+                    parts[0].capture_begin(capture_error_mode=_CAPTURE_MODE)
                     data, idx, isw = slots[p]
                     probe = (lambda items, last=False: cut(("probe", items), last=last)) if pr else None
                     td = solver.compute_grads(data, isw, q1t=G["q1t"][p] if variant == "pre" else None,

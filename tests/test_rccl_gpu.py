@@ -111,7 +111,9 @@ def _child(teardown):
         if line.startswith("STAGE "):
             d = json.loads(line[6:])
             stages[d.pop("stage")] = d
-    return p.returncode, stages, p.stderr[-2000:]
+    err = p.stderr
+    hits = [ln for ln in err.splitlines() if "error" in ln.lower() or "what()" in ln][:8]
+    return p.returncode, stages, "\n".join(hits) + "\n...\n" + err[-1500:]
 
 
 def test_rccl_one_rank_bucketed_learner():

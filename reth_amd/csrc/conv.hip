@@ -90,7 +90,7 @@ __device__ unsigned long long g_conv_clock[kClockSlots][2];
 // and measured in r05: 2x slower alone, 108 vs 57 us at 1,024 samples, since every claim is an
 // agent-scope atomic on one address from all 8 XCDs; removed.)
 template <int MODE, int KH, int KW, int S, int CIN, int COUT, int HIN, int WIN, int WAVES, int MB, int NS = 1,
-          int PW = 0>
+          int PW = 0, int TS = 1>
 __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__restrict__ x,
                                                               const int64_t *__restrict__ rows, int64_t n,
                                                               const int64_t *__restrict__ n_dev,
@@ -105,6 +105,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__res
   constexpr int D = F32 ? Gm::prefetch(MB) : G;  // input chunks in flight per wave
   using Frag = typename std::conditional<F32, f32x4, uint32_t>::type;
   static_assert(!PW || NS > 1, "PW needs channel parts");
+  static_assert(TS == 1 || (NS == 1 && !PW && NB % TS == 0), "a split last round needs full-width tiles");
   constexpr int LDSW = PW ? Gm::LDS_F4 / NS : Gm::LDS_F4;  // staged float4 slots
   __shared__ f32x4 wl[LDSW];
   const int part = PW ? (int)(blockIdx.x % NS) : 0;               // PW: this workgroup's channel part
@@ -157,11 +158,24 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__res
   // first gridDim.x * 4 slots put one wave on every SIMD, so a partial last round of tiles
   // lands on distinct SIMDs and no SIMD runs more than ceil(tiles / SIMDs) tiles
   const int64_t slot = WAVES % 4 == 0 ? (int64_t)(wave / 4) * wgs * 4 + wgi * 4 + wave % 4 : wgi * WAVES + wave;
+  // Units (r05, TS > 1: NS == 1, no PW): the pixel tiles of the whole rounds -- as many as
+  // give every SIMD the same count -- run full-width; each pixel tile of the ragged last round
+  // is split into TS channel parts (NB / TS blocks each), which the slots continue to take in
+  // the same order, so they land on the SIMDs with one tile less: at 1,024 samples the 5,184
+  // tiles were 5 or 6 per SIMD, now 5 + at most one quarter.  Same MFMA chain per output.
+  const int64_t ptiles = (P + TP - 1) / TP;
+  const int64_t per_round = WAVES % 4 == 0 ? wgs * 4 : tstride;  // one slot per SIMD
+  const int64_t full = TS > 1 ? ptiles / per_round * per_round : tiles;
+  const int64_t total = TS > 1 ? full + (ptiles - full) * TS : tiles;
+  auto unit_ptile = [&](int64_t v) -> int64_t { return TS > 1 ? (v < full ? v : full + (v - full) / TS) : v / TD; };
+  auto unit_nb0 = [&](int64_t v) -> int {
+    if constexpr (TS > 1) return v < full ? 0 : (int)((v - full) % TS) * (NB / TS);
+    return PW ? part * NBW : (NS == 1 ? 0 : (int)(v % NS) * NBW);
+  };
   // the first tile's leading input chunks are requested before the weights are staged
-  int64_t tile = slot;
-  int64_t tnext = tile + tstride;  // the tile after this one
+  int64_t v = slot;
   const uint8_t *cur[MB], *nxt[MB];
-  bases((tile < tiles ? tile : tiles - 1) / TD, cur);
+  bases(unit_ptile(v < total ? v : total - 1), cur);
   Frag ar[D][MB];
 #pragma unroll
   for (int d = 0; d < D; ++d)
@@ -189,32 +203,34 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__res
   }
   __syncthreads();
 
-  float bl[NBW];
-  const int nb_first = PW ? part * NBW : (NS == 1 ? 0 : (int)(tile % NS) * NBW);
+  float bl[NBW];  // the full-width units' bias (their channel part is fixed unless NS > 1)
+  const int nb_first = unit_nb0(v);
 #pragma unroll
   for (int nb = 0; nb < NBW; ++nb) bl[nb] = bias[(nb_first + nb) * 16 + mr];
   // this lane's B fragments, offset to the tile's channel part
   const f32x4 *wlane = wl + lane;
 
-  for (; tile < tiles;) {
-    const int nb0 = PW ? part * NBW : (NS == 1 ? 0 : (int)(tile % NS) * NBW);  // output channel block
-    const int lb0 = PW ? 0 : nb0;                                               // its LDS block
-    if constexpr (NS > 1 && !PW) {
+  // one unit: NBT channel blocks from nb0 of pixel tile ptile (nxt: the next unit's window)
+  auto run = [&](auto nbt, int64_t ptile, int nb0) __attribute__((always_inline)) {
+    constexpr int NBT = decltype(nbt)::value;
+    const int lb0 = PW ? 0 : nb0;  // its LDS block
+    float bt[NBT];
+    if constexpr (NBT != NBW || (NS > 1 && !PW)) {
 #pragma unroll
-      for (int nb = 0; nb < NBW; ++nb) bl[nb] = bias[(nb0 + nb) * 16 + mr];
+      for (int nb = 0; nb < NBT; ++nb) bt[nb] = bias[(nb0 + nb) * 16 + mr];
+    } else {
+#pragma unroll
+      for (int nb = 0; nb < NBT; ++nb) bt[nb] = bl[nb];
     }
-    const int64_t ptile = tile / TD;
-    // the chunks past the end of this tile are the next tile's leading chunks
-    bases((tnext < tiles ? tnext : tile) / TD, nxt);
-    f32x4 acc[MB][NBW];
+    f32x4 acc[MB][NBT];
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
-      for (int nb = 0; nb < NBW; ++nb) acc[mb][nb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    f32x4 bcur[NBW], bnxt[NBW];  // B fragments, one chunk ahead
+      for (int nb = 0; nb < NBT; ++nb) acc[mb][nb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    f32x4 bcur[NBT], bnxt[NBT];  // B fragments, one chunk ahead
     constexpr int LNB = PW ? NBW : NB;  // channel blocks per chunk in LDS
 #pragma unroll
-    for (int nb = 0; nb < NBW; ++nb) bcur[nb] = wlane[(lb0 + nb) * 64];
+    for (int nb = 0; nb < NBT; ++nb) bcur[nb] = wlane[(lb0 + nb) * 64];
 
 #pragma unroll 1
     for (int g0 = 0; g0 < G; g0 += D) {
@@ -223,7 +239,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__res
         const int g = g0 + d;
         const int gb = g + 1 < G ? g + 1 : G - 1;
 #pragma unroll
-        for (int nb = 0; nb < NBW; ++nb) {
+        for (int nb = 0; nb < NBT; ++nb) {
 #ifdef RTH_DIAG_NOLDSB  // diagnostic timing builds only (scripts/r05.sh c2diag): wrong results
           bnxt[nb] = bcur[nb];
 #else
@@ -240,7 +256,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__res
             if constexpr (F32) a = ar[d][mb][t];
             else a = (float)((ar[d][mb] >> (8 * t)) & 0xffu);
 #pragma unroll
-            for (int nb = 0; nb < NBW; ++nb)
+            for (int nb = 0; nb < NBT; ++nb)
               acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bcur[nb][t], acc[mb][nb], 0, 0, 0);
           }
         const int ga = g + D;
@@ -250,7 +266,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__res
           ar[d][mb] = ld(ga < G ? cur[mb] + chunk_off(ga) : nxt[mb] + chunk_off(ga - G));
 #endif
 #pragma unroll
-        for (int nb = 0; nb < NBW; ++nb) bcur[nb] = bnxt[nb];
+        for (int nb = 0; nb < NBT; ++nb) bcur[nb] = bnxt[nb];
       }
     }
     // C/D: lane holds column mr of rows 4q .. 4q+3 of each M-block; y is NHWC, or NCHW when
@@ -268,19 +284,28 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_bias_relu(const void *__res
           if (out_nchw) {
             const int64_t b = po / Gm::PIX, pp = po - b * Gm::PIX;
 #pragma unroll
-            for (int nb = 0; nb < NBW; ++nb)
-              y[(b * COUT + (nb0 + nb) * 16 + mr) * Gm::PIX + pp] = relu_c(radd(acc[mb][nb][i], bl[nb]));
+            for (int nb = 0; nb < NBT; ++nb)
+              y[(b * COUT + (nb0 + nb) * 16 + mr) * Gm::PIX + pp] = relu_c(radd(acc[mb][nb][i], bt[nb]));
           } else {
 #pragma unroll
-            for (int nb = 0; nb < NBW; ++nb)
-              y[po * COUT + (nb0 + nb) * 16 + mr] = relu_c(radd(acc[mb][nb][i], bl[nb]));
+            for (int nb = 0; nb < NBT; ++nb)
+              y[po * COUT + (nb0 + nb) * 16 + mr] = relu_c(radd(acc[mb][nb][i], bt[nb]));
           }
         }
       }
+  };
+
+  for (; v < total;) {
+    const int64_t vn = v + tstride;
+    // the chunks past the end of this unit are the next unit's leading chunks
+    bases(unit_ptile(vn < total ? vn : v), nxt);
+    if (TS > 1 && v >= full)
+      run(std::integral_constant<int, (TS > 1 ? NB / TS : NBW)>{}, unit_ptile(v), unit_nb0(v));
+    else
+      run(std::integral_constant<int, NBW>{}, unit_ptile(v), unit_nb0(v));
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb) cur[mb] = nxt[mb];
-    tile = tnext;
-    tnext += tstride;
+    v = vn;
   }
 #ifdef RTH_CLOCK_STAMPS
   if (threadIdx.x == 0 && blockIdx.x < kClockSlots) {
@@ -1079,10 +1104,10 @@ static ConvLaunch x9_launch() {
 }
 
 template <int MODE, int KH, int KW, int S, int CIN, int COUT, int HIN, int WIN, int WAVES, int MB, int NS = 1,
-          int PW = 0>
+          int PW = 0, int TS = 1>
 static ConvLaunch conv_launch() {
   using Gm = ConvGeom<MODE, KH, KW, S, CIN, COUT, HIN, WIN>;
-  ConvLaunch l{reinterpret_cast<const void *>(&k_conv_bias_relu<MODE, KH, KW, S, CIN, COUT, HIN, WIN, WAVES, MB, NS, PW>),
+  ConvLaunch l{reinterpret_cast<const void *>(&k_conv_bias_relu<MODE, KH, KW, S, CIN, COUT, HIN, WIN, WAVES, MB, NS, PW, TS>),
                reinterpret_cast<const void *>(&k_conv_pack<MODE, KH, KW, S, CIN, COUT, HIN, WIN>), WAVES,
                Gm::LDS_F4 * 16, 0, 16 * MB, 0, NS, 0, {}, nullptr, 0, 0, PW};
   int blocks = 0;
@@ -1202,6 +1227,8 @@ static bool find_conv(const rth_conv_shape &s, ConvLaunch *out, int *geom = null
       const std::string v = e ? e : (CONV2_NS == 2 ? "ns2" : "static");
       if (v == "ns2") return conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 2, 0>();
       if (v == "pw2") return conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 2, 1>();
+      if (v == "ts2") return conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 1, 0, 2>();
+      if (v == "ts4") return conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 1, 0, 4>();
       return conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 1>();
     }();
     static const ConvLaunch l = [] {

@@ -148,6 +148,19 @@ PY
             --no-sweep
       done
       summ gpurun_out/fcab_*.log ;;
+    c2ts)  # conv2: the ragged last round split into channel parts (ts2 / ts4) vs static
+      step c2ts_tests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_conv_gpu.py \
+          -k "schedules or conv_f32_nhwc or partial or upto"
+      for v in static ts2 ts4; do
+        RTH_CONV2_SCHED=$v CONV_NS=1024,512,256 step c2ts_micro_$v 120 python scripts/bench_conv.py
+      done
+      grep -H "conv2" gpurun_out/c2ts_micro_*.log
+      for r in 1 2; do
+        for v in static ts2 ts4; do
+          RTH_CONV2_SCHED=$v step c2tsab_${v}_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        done
+      done
+      summ gpurun_out/c2tsab_*.log ;;
     dp8)  # 8 ranks on one GPU over gloo: bench.py's multi-rank path and its teardown (shutdown())
       RTH_SHARE_GPU=1 RTH_DIST_BACKEND=gloo step dp8_gloo_rehearsal 900 python -m torch.distributed.run --nnodes=1 \
           --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 8 --faithful --steps 20 \

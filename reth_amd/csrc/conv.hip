@@ -1088,6 +1088,10 @@ struct ConvLaunch {
   int64_t big_above;
   int big_off;
   int pw;   // k_conv_bias_relu PW: channel part per workgroup (the grid a multiple of nsplit)
+  // the same kernel with its ragged last round split into channel parts (TS > 1), launched
+  // instead of fn when a launch has at least tsfn_rounds whole rounds of tiles (nullptr: never)
+  const void *tsfn = nullptr;
+  int tsfn_rounds = 0;
 };
 
 template <int KH, int KW, int S, int CIN, int HIN, int WIN, int NSAMP, int ROT, int KS>
@@ -1229,6 +1233,12 @@ static bool find_conv(const rth_conv_shape &s, ConvLaunch *out, int *geom = null
       if (v == "pw2") return conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 2, 1>();
       if (v == "ts2") return conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 1, 0, 2>();
       if (v == "ts4") return conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 1, 0, 4>();
+      if (v == "ts4big") {  // the split form only where whole rounds dominate (the learner's 1,024)
+        ConvLaunch l = conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 1>();
+        l.tsfn = conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 1, 0, 4>().fn;
+        l.tsfn_rounds = 4;
+        return l;
+      }
       return conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 1>();
     }();
     static const ConvLaunch l = [] {
@@ -2203,7 +2213,9 @@ static int conv_bias_relu(const rth_conv_shape *shape, const void *x, const int6
   }
   void *args[] = {(void *)&x, (void *)&rows, (void *)&n, (void *)&n_dev, (void *)&w, (void *)&bias, (void *)&y,
                   (void *)&out_nchw};  // (k_conv1_u8_bf16x3 takes the first seven)
-  RTH_HIP(hipLaunchKernel(l.fn, dim3((unsigned)grid), dim3(l.waves * 64), args, 0, as_stream(stream)));
+  // whole rounds of pixel tiles over one wave slot per SIMD (the kernel's own split rule)
+  const bool ts = l.tsfn && l.waves % 4 == 0 && tiles / (grid * 4) >= l.tsfn_rounds;
+  RTH_HIP(hipLaunchKernel(ts ? l.tsfn : l.fn, dim3((unsigned)grid), dim3(l.waves * 64), args, 0, as_stream(stream)));
   return RTH_OK;
 }
 

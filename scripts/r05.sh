@@ -151,12 +151,12 @@ PY
     c2ts)  # conv2: the ragged last round split into channel parts (ts2 / ts4) vs static
       step c2ts_tests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_conv_gpu.py \
           -k "schedules or conv_f32_nhwc or partial or upto"
-      for v in static ts2 ts4; do
+      for v in static ts4big; do
         RTH_CONV2_SCHED=$v CONV_NS=1024,512,256 step c2ts_micro_$v 120 python scripts/bench_conv.py
       done
       grep -H "conv2" gpurun_out/c2ts_micro_*.log
-      for r in 1 2; do
-        for v in static ts2 ts4; do
+      for r in 1 2 3; do
+        for v in static ts4big; do
           RTH_CONV2_SCHED=$v step c2tsab_${v}_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
         done
       done

@@ -161,6 +161,15 @@ PY
         done
       done
       summ gpurun_out/c2tsab_*.log ;;
+    boab)  # Breakout: the tree update in two passes (RTH_TREE_PASSES=2: the append's run of leaves
+      # spread over level-15 subtrees first) vs one pass
+      RTH_TREE_PASSES=2 RTH_TREE_TIMING=1 step tree_phases_2pass 300 python scripts/probe_tree_phases.py
+      for r in 1 2; do
+        step boab_1pass_$r 600 python bench.py --workload breakout --steps 100 --warmup 10 --no-cpu-baseline --no-sweep
+        RTH_TREE_PASSES=2 step boab_2pass_$r 600 python bench.py --workload breakout --steps 100 --warmup 10 \
+            --no-cpu-baseline --no-sweep
+      done
+      summ gpurun_out/boab_*.log ;;
     dp8)  # 8 ranks on one GPU over gloo: bench.py's multi-rank path and its teardown (shutdown())
       RTH_SHARE_GPU=1 RTH_DIST_BACKEND=gloo step dp8_gloo_rehearsal 900 python -m torch.distributed.run --nnodes=1 \
           --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 8 --faithful --steps 20 \

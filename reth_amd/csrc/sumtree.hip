@@ -334,6 +334,7 @@ constexpr int kSubGridMin = 64;      // ... and at least
 constexpr int kSubKeysPerWg = 12;    // the grid is sized for about this many keys per workgroup
 constexpr int kSubSplit = 4;          // the second pass covers S .. S + 3
 constexpr int kSubTwoPassDepth = 8;   // two passes when maxd >= S + 8 (trees of >= 2^19 nodes)
+constexpr int64_t kTwoPassKeys = 1536;  // ... and the update has at least this many keys (RTH_TREE_PASSES unset)
 static_assert(kSubKeys == kSubThreads, "one key per lane in the rank sort / ownership scan");
 
 struct SubEnt {
@@ -1267,7 +1268,11 @@ int tree_update_impl(rth_sumtree *t, const int64_t *idx, int64_t fifo_start, con
   if (t->maxd >= S && a.pn + a.n > 0) {  // levels S..maxd: one workgroup per group of subtrees,
     // the last one to finish (of the last pass) also runs the top pass; deep trees in two
     // passes split at S1 = S + kSubSplit (RTH_TREE_PASSES=1: one pass, A/B aid)
-    const int passes = env_int("RTH_TREE_PASSES", 1);  // read per call: tests switch it
+    // RTH_TREE_PASSES: 1 / 2 fixed (read per call: tests switch it); unset (0): two passes for
+    // large updates -- Breakout's 2,048-row append is one run of leaves, which a single pass
+    // hands to the one or two workgroups owning its level-S subtrees (alone 56-57 vs 34-35 us)
+    const int passes_env = env_int("RTH_TREE_PASSES", 0);
+    const int passes = passes_env > 0 ? passes_env : (a.pn + a.n >= kTwoPassKeys ? 2 : 1);
     // fewer workgroups for small updates: less dispatch and L2 traffic beside the learner
     // stream (Pong's 768 keys: 64 workgroups, 0.617-0.620 vs 0.618-0.625 ms/step with 256;
     // Breakout's 2,560 keys keep 256).  RTH_TREE_GRID fixes it (A/B aid).

@@ -163,11 +163,11 @@ PY
       summ gpurun_out/c2tsab_*.log ;;
     boab)  # Breakout: the tree update in two passes (RTH_TREE_PASSES=2: the append's run of leaves
       # spread over level-15 subtrees first) vs one pass
-      RTH_TREE_PASSES=2 RTH_TREE_TIMING=1 step tree_phases_2pass 300 python scripts/probe_tree_phases.py
-      for r in 1 2; do
-        step boab_1pass_$r 600 python bench.py --workload breakout --steps 100 --warmup 10 --no-cpu-baseline --no-sweep
-        RTH_TREE_PASSES=2 step boab_2pass_$r 600 python bench.py --workload breakout --steps 100 --warmup 10 \
+      step boab_tests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_scale_gpu.py
+      for r in 1 2 3 4; do
+        RTH_TREE_PASSES=1 step boab_1pass_$r 600 python bench.py --workload breakout --steps 100 --warmup 10 \
             --no-cpu-baseline --no-sweep
+        step boab_2pass_$r 600 python bench.py --workload breakout --steps 100 --warmup 10 --no-cpu-baseline --no-sweep
       done
       summ gpurun_out/boab_*.log ;;
     dp8)  # 8 ranks on one GPU over gloo: bench.py's multi-rank path and its teardown (shutdown())

@@ -34,12 +34,13 @@ def _assert_tree_equal(tree, o):
     assert np.array_equal(m, o.min_), "min"
 
 
-@pytest.mark.parametrize("passes", ["1", "2"])
+@pytest.mark.parametrize("passes", ["1", "2", "0"])
 @pytest.mark.parametrize("cap,n_app,steps", [(1_000_000, 256, 40), (4_000_000, 2048, 40)])
 def test_loop_shaped_tree_vs_oracle(dev, orc, cap, n_app, steps, passes, monkeypatch):
     """prefill to near capacity, then per step one merged launch: the previous learner
     update's 512 priorities (deferred, step=True) + n_app appended rows, wrapping the FIFO;
-    passes = 2: the two-pass subtree update of deep trees (RTH_TREE_PASSES)"""
+    passes = 2: the two-pass subtree update of deep trees (RTH_TREE_PASSES), 0: the default rule
+    (two passes from 1,536 keys of one launch)"""
     monkeypatch.setenv("RTH_TREE_PASSES", passes)
     from reth_amd.replay import Column, HbmReplay
 

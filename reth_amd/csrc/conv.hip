@@ -1228,15 +1228,19 @@ static bool find_conv(const rth_conv_shape &s, ConvLaunch *out, int *geom = null
     // LDS: the other stream's workgroups fit beside it -- 0.543-0.544 vs 0.540-0.542 ms/step)
     static const ConvLaunch f32 = [] {
       const char *e = getenv("RTH_CONV2_SCHED");
-      const std::string v = e ? e : (CONV2_NS == 2 ? "ns2" : "static");
+      const std::string v = e ? e : (CONV2_NS == 2 ? "ns2" : "ts8big");
       if (v == "ns2") return conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 2, 0>();
       if (v == "pw2") return conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 2, 1>();
       if (v == "ts2") return conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 1, 0, 2>();
       if (v == "ts4") return conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 1, 0, 4>();
-      if (v == "ts4big") {  // the split form only where whole rounds dominate (the learner's 1,024)
+      // ts4big / ts8big: the split form only for launches of >= 4 / >= 8 whole rounds of tiles.
+      // Default ts8big (r05): Breakout's 2,048-sample actor forwards (10 rounds) split their
+      // last round, 0.885-0.888 vs 0.893-0.898 ms/step with >= 4 rounds; Pong's launches (at
+      // most 1,024 samples, 5 rounds) stay whole -- there the split was neutral to 0.3 % slower
+      if (v == "ts4big" || v == "ts8big") {
         ConvLaunch l = conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 1>();
         l.tsfn = conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 1, 0, 4>().fn;
-        l.tsfn_rounds = 4;
+        l.tsfn_rounds = v == "ts4big" ? 4 : 8;
         return l;
       }
       return conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 1>();

@@ -172,9 +172,9 @@ PY
       summ gpurun_out/boab_*.log ;;
     bots)  # Breakout (actor stream critical, 2,048-sample actor forwards): conv2 split tail (ts4big) vs static
       for r in 1 2 3; do
-        step bots_static_$r 600 python bench.py --workload breakout --steps 100 --warmup 10 --no-cpu-baseline --no-sweep
-        RTH_CONV2_SCHED=ts4big step bots_ts4big_$r 600 python bench.py --workload breakout --steps 100 --warmup 10 \
+        RTH_CONV2_SCHED=static step bots_static_$r 600 python bench.py --workload breakout --steps 100 --warmup 10 \
             --no-cpu-baseline --no-sweep
+        step bots_ts8big_$r 600 python bench.py --workload breakout --steps 100 --warmup 10 --no-cpu-baseline --no-sweep
       done
       summ gpurun_out/bots_*.log ;;
     dp8)  # 8 ranks on one GPU over gloo: bench.py's multi-rank path and its teardown (shutdown())

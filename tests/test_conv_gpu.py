@@ -680,7 +680,7 @@ def test_conv2_schedules_bit_identical(tmp_path, dev):
         torch.cuda.empty_cache()
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     res = {}
-    for sched in ("static", "ns2", "pw2", "ts2", "ts4", "ts4big"):
+    for sched in ("static", "ns2", "pw2", "ts2", "ts4", "ts4big", "ts8big"):
         path = tmp_path / f"{sched}.pt"
         p = subprocess.run([sys.executable, "-c", _C2_CHILD, root, str(path)],
                            env=dict(os.environ, RTH_CONV2_SCHED=sched), capture_output=True, text=True, timeout=120)

@@ -1228,15 +1228,16 @@ static bool find_conv(const rth_conv_shape &s, ConvLaunch *out, int *geom = null
     // LDS: the other stream's workgroups fit beside it -- 0.543-0.544 vs 0.540-0.542 ms/step)
     static const ConvLaunch f32 = [] {
       const char *e = getenv("RTH_CONV2_SCHED");
-      const std::string v = e ? e : (CONV2_NS == 2 ? "ns2" : "ts8big");
+      const std::string v = e ? e : (CONV2_NS == 2 ? "ns2" : "static");
       if (v == "ns2") return conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 2, 0>();
       if (v == "pw2") return conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 2, 1>();
       if (v == "ts2") return conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 1, 0, 2>();
       if (v == "ts4") return conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 1, 0, 4>();
-      // ts4big / ts8big: the split form only for launches of >= 4 / >= 8 whole rounds of tiles.
-      // Default ts8big (r05): Breakout's 2,048-sample actor forwards (10 rounds) split their
-      // last round, 0.885-0.888 vs 0.893-0.898 ms/step with >= 4 rounds; Pong's launches (at
-      // most 1,024 samples, 5 rounds) stay whole -- there the split was neutral to 0.3 % slower
+      // ts4big / ts8big: the split form only for launches of >= 4 / >= 8 whole rounds of tiles
+      // (r05 A/B, profiles/r05/ab_log.txt: alone at 1,024 samples 53.1 vs 57.9 us = 0.65 of the
+      // fp32 peak; in the loop Pong 0.545-0.547 vs 0.543-0.546 ms/step with ts4big, Breakout
+      // 0.885-0.888 vs 0.893-0.898 with ts4big and 0.865-0.874 vs 0.866-0.874 with ts8big --
+      // within the noise, so the whole tiles stay the default)
       if (v == "ts4big" || v == "ts8big") {
         ConvLaunch l = conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 1>();
         l.tsfn = conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 1, 0, 4>().fn;

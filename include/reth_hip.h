@@ -532,6 +532,16 @@ int64_t rth_conv_dgrad_workspace(const rth_conv_shape *shape);
  * rth_conv_dgrad_workspace(shape) > 0. */
 int rth_conv_dgrad_prepacked(const rth_conv_shape *shape, const float *gy_dev, int64_t n, const void *packed_dev,
                              float *gx_dev, void *stream);
+/* rth_conv_dgrad_prepacked for conv3's geometry (rth_conv_dgrad_relu_supported) with the layer
+ * below's ReLU applied in the same launch (r05): gx = the data gradient where y_dev (the layer
+ * below's output, [n, 9, 9, 64] NHWC) > 0, else 0 -- what rth_relu_bias_grad makes of the plain
+ * data gradient -- and that layer's bias-gradient slab partials written to bias_ws_dev (a
+ * rth_relu_bias_grad workspace of C = 64, finished later by a rth_bias_deferred job whose
+ * `slabs` is *slabs_out).  Reference: the backward of dqn_model.py:14-20 (Conv2d + ReLU). */
+int rth_conv_dgrad_relu_supported(const rth_conv_shape *shape);
+int rth_conv_dgrad_relu_prepacked(const rth_conv_shape *shape, const float *gy_dev, int64_t n, const void *packed_dev,
+                                  const float *y_dev, float *gx_dev, void *bias_ws_dev, int64_t *slabs_out,
+                                  void *stream);
 /* FC1 of the dueling heads (the first Linear + ReLU of both branches, dqn_model.py:38-47, as
  * one [N, K] weight) on the exact-split bf16 MFMA: y [M, N] = act(x [M, K] w^T + b), x
  * row-major with row stride ldx, w row-major [N, K] (the Linear weight as stored), act = ReLU
@@ -589,6 +599,8 @@ typedef struct rth_bias_deferred {
   float *db;             /* [C] output */
   int64_t rows;
   int32_t C;
+  int32_t slabs; /* the slab count; 0 = rth_relu_bias_grad's for `rows` (rth_conv_dgrad_relu_prepacked
+                  * reports its own) */
 } rth_bias_deferred;
 int rth_conv_relu_wgrad_ex(const rth_conv_shape *shape, const void *x_dev, const int64_t *rows_dev, int64_t n,
                            const float *g_dev, const float *y_dev, float *gw_dev, float *gb_dev, void *workspace_dev,

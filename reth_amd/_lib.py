@@ -57,7 +57,7 @@ class BiasDeferred(ctypes.Structure):
     """rth_bias_deferred (include/reth_hip.h): a bias gradient whose slabs rth_relu_bias_grad
     wrote with db = NULL, finished by rth_conv_relu_wgrad_ex"""
     _fields_ = [("workspace", ctypes.c_void_p), ("db", ctypes.c_void_p), ("rows", ctypes.c_int64),
-                ("C", ctypes.c_int32)]
+                ("C", ctypes.c_int32), ("slabs", ctypes.c_int32)]
 
 
 CONV_F32_NHWC, CONV_U8_CHW = 0, 1
@@ -184,6 +184,9 @@ SIGNATURES = {
     "rth_fc_f32": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i32, c_vp, c_vp, c_vp]),
     "rth_conv_dgrad_ws": (c_i32, [ctypes.POINTER(ConvShape), c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "rth_conv_dgrad_prepacked": (c_i32, [ctypes.POINTER(ConvShape), c_vp, c_i64, c_vp, c_vp, c_vp]),
+    "rth_conv_dgrad_relu_supported": (c_i32, [ctypes.POINTER(ConvShape)]),
+    "rth_conv_dgrad_relu_prepacked": (c_i32, [ctypes.POINTER(ConvShape), c_vp, c_i64, c_vp, c_vp, c_vp, c_vp,
+                                              ctypes.POINTER(c_i64), c_vp]),
     "rth_atari_create": (c_i32, [c_i32, c_i32, c_i32, c_i32, c_i32, ctypes.POINTER(c_vp)]),
     "rth_atari_destroy": (c_i32, [c_vp]),
     "rth_atari_step": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),

@@ -673,13 +673,24 @@ struct X9Geom {
 // blockIdx.y = class (py, px), its packed kernel at wpk + class * PACKED_U4, and output pixel
 // (jy, jx) of the class goes to pixel (2 jy + py, 2 jx + px) of the [n, 2 HOUT, 2 WOUT, COUT]
 // NHWC gradient.
+// MASK (r05, the data gradient of conv3 only: PAD > 0, no CLS): the output is the gradient of
+// the layer below's ReLU output, passed through that ReLU at once -- y = 0 where ymask (the
+// layer below's output, same NHWC index space) is <= 0, threshold_backward -- and each
+// workgroup writes the layer below's bias-gradient partial sums (slab blockIdx.x: float4 of
+// channels 4q.. per quad q, each lane's float4s in order, then a fixed LDS tree over the lanes of
+// a quad -- k_relu_bias_grad's slab layout, finished by the same deferred bias job).  This
+// replaces rth_relu_bias_grad's launch between the two data gradients.
 template <int KH, int KW, int S, int CIN, int HIN, int WIN, int NSAMP, int ROT, int KS, int PAD = 0, int COUT_ = 64,
-          int CLS = 0>
+          int CLS = 0, int MASK = 0>
 __global__ __launch_bounds__(64 * (COUT_ / 16) * KS) void k_conv_x9(const float *__restrict__ x, int64_t n,
                                                                   const int64_t *__restrict__ n_dev, int nsamp,
                                                                   const u32x4 *__restrict__ wpk,
                                                                   const float *__restrict__ bias,
-                                                                  float *__restrict__ y, int out_nchw) {
+                                                                  float *__restrict__ y, int out_nchw,
+                                                                  const float *__restrict__ ymask,
+                                                                  float *__restrict__ bpart) {
+  static_assert(!MASK || (PAD > 0 && !CLS && (64 * (COUT_ / 16) * KS) % (COUT_ / 4) == 0),
+                "the masked epilogue is the NHWC data gradient's; every lane keeps one channel quad");
   using G = X9Geom<KH, KW, S, CIN, HIN, WIN, NSAMP, ROT, KS, COUT_>;
   if constexpr (CLS) wpk += (size_t)blockIdx.y * G::PACKED_U4;
   constexpr int HS = HIN - 2 * PAD, WS = WIN - 2 * PAD;  // the source image
@@ -892,6 +903,43 @@ __global__ __launch_bounds__(64 * (COUT_ / 16) * KS) void k_conv_x9(const float 
       const int64_t o = (((b0 + s) * (2 * G::HOUT) + 2 * jy + py) * (2 * G::WOUT) + 2 * jx + px) * COUT + 4 * c4;
       *reinterpret_cast<float4 *>(y + o) = Fs[i];
     }
+  } else if constexpr (MASK) {
+    const int total4 = nv * COUT / 4;
+    float4 *yo = reinterpret_cast<float4 *>(y + b0 * (int64_t)(COUT * PIX));
+    const float4 *ym = reinterpret_cast<const float4 *>(ymask + b0 * (int64_t)(COUT * PIX));
+    const float4 *Fs = reinterpret_cast<const float4 *>(F);
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);  // channel quad tid % (COUT / 4), in i order
+    for (int i = tid; i < total4; i += NT) {
+      const float4 g = Fs[i], m = ym[i];
+      float4 o;
+      o.x = m.x > 0.0f ? g.x : 0.0f;  // threshold_backward(g, y, 0)
+      o.y = m.y > 0.0f ? g.y : 0.0f;
+      o.z = m.z > 0.0f ? g.z : 0.0f;
+      o.w = m.w > 0.0f ? g.w : 0.0f;
+      yo[i] = o;
+      acc.x = radd(acc.x, o.x);
+      acc.y = radd(acc.y, o.y);
+      acc.z = radd(acc.z, o.z);
+      acc.w = radd(acc.w, o.w);
+    }
+    __syncthreads();  // every lane is done reading F: its first NT float4 hold the lane sums
+    float4 *red = reinterpret_cast<float4 *>(F);
+    red[tid] = acc;
+    __syncthreads();
+    constexpr int Q = COUT / 4;
+    for (int st = NT / 2; st >= Q; st >>= 1) {  // lanes tid and tid + st share a quad
+      if (tid < st) {
+        float4 a = red[tid];
+        const float4 o = red[tid + st];
+        a.x = radd(a.x, o.x);
+        a.y = radd(a.y, o.y);
+        a.z = radd(a.z, o.z);
+        a.w = radd(a.w, o.w);
+        red[tid] = a;
+      }
+      __syncthreads();
+    }
+    if (tid < Q) reinterpret_cast<float4 *>(bpart)[(int64_t)blockIdx.x * Q + tid] = red[tid];
   } else {
     const int total4 = nv * COUT / 4;  // the run [b0, b0 + ns) of y is contiguous in both layouts
     float4 *yo = reinterpret_cast<float4 *>(y + b0 * (int64_t)(COUT * PIX));
@@ -1946,20 +1994,43 @@ static int64_t dgrad_x9_nsamp(int64_t n, int classes, const void *const *fn, int
 }
 
 static int launch_dgrad_x9(const void *fn, const float *gy, int64_t n, int64_t ns, int classes, int threads,
-                           const u32x4 *wpk, float *gx, hipStream_t st) {
+                           const u32x4 *wpk, float *gx, hipStream_t st, const float *ymask = nullptr,
+                           float *bpart = nullptr) {
   const int nsi = (int)ns;
   const int64_t grid = (n + ns - 1) / ns;
   const int64_t *n_dev = nullptr;
   const float *bias = nullptr;
   int out_nchw = 0;
-  void *args[] = {(void *)&gy, (void *)&n, (void *)&n_dev, (void *)&nsi, (void *)&wpk, (void *)&bias, (void *)&gx,
-                  (void *)&out_nchw};
+  void *args[] = {(void *)&gy,  (void *)&n,  (void *)&n_dev,    (void *)&nsi,   (void *)&wpk,
+                  (void *)&bias, (void *)&gx, (void *)&out_nchw, (void *)&ymask, (void *)&bpart};
   RTH_HIP(hipLaunchKernel(fn, dim3((unsigned)grid, (unsigned)classes), dim3(threads), args, 0, st));
   return RTH_OK;
 }
 
 // w == NULL: user_ws already holds the packed kernel (rth_conv_pack_many's data-gradient job)
-static int conv_dgrad_x9_conv3(const float *gy, int64_t n, const float *w, float *gx, void *user_ws, hipStream_t st) {
+// the samples per workgroup of conv3's data gradient at n samples (= its grid's divisor)
+static int64_t dgrad3_nsamp(int64_t n, bool mask) {
+  const void *fn[4] = {nullptr, reinterpret_cast<const void *>(&k_conv_x9<3, 3, 1, 64, 11, 11, 1, 3, X9_DGRAD3_KS, 2>),
+                       reinterpret_cast<const void *>(&k_conv_x9<3, 3, 1, 64, 11, 11, 2, 3, X9_DGRAD3_KS, 2>),
+                       reinterpret_cast<const void *>(&k_conv_x9<3, 3, 1, 64, 11, 11, 3, 3, X9_DGRAD3_KS, 2>)};
+  const void *fm[4] = {
+      nullptr, reinterpret_cast<const void *>(&k_conv_x9<3, 3, 1, 64, 11, 11, 1, 3, X9_DGRAD3_KS, 2, 64, 0, 1>),
+      reinterpret_cast<const void *>(&k_conv_x9<3, 3, 1, 64, 11, 11, 2, 3, X9_DGRAD3_KS, 2, 64, 0, 1>),
+      reinterpret_cast<const void *>(&k_conv_x9<3, 3, 1, 64, 11, 11, 3, 3, X9_DGRAD3_KS, 2, 64, 0, 1>)};
+  return dgrad_x9_nsamp(n, 1, mask ? fm : fn, X9Dgrad3<1>::NT, (int)x9_wg_per_cu());
+}
+static const void *dgrad3_fn(int64_t ns, bool mask) {
+  const void *fn[4] = {nullptr, reinterpret_cast<const void *>(&k_conv_x9<3, 3, 1, 64, 11, 11, 1, 3, X9_DGRAD3_KS, 2>),
+                       reinterpret_cast<const void *>(&k_conv_x9<3, 3, 1, 64, 11, 11, 2, 3, X9_DGRAD3_KS, 2>),
+                       reinterpret_cast<const void *>(&k_conv_x9<3, 3, 1, 64, 11, 11, 3, 3, X9_DGRAD3_KS, 2>)};
+  const void *fm[4] = {
+      nullptr, reinterpret_cast<const void *>(&k_conv_x9<3, 3, 1, 64, 11, 11, 1, 3, X9_DGRAD3_KS, 2, 64, 0, 1>),
+      reinterpret_cast<const void *>(&k_conv_x9<3, 3, 1, 64, 11, 11, 2, 3, X9_DGRAD3_KS, 2, 64, 0, 1>),
+      reinterpret_cast<const void *>(&k_conv_x9<3, 3, 1, 64, 11, 11, 3, 3, X9_DGRAD3_KS, 2, 64, 0, 1>)};
+  return mask ? fm[ns] : fn[ns];
+}
+static int conv_dgrad_x9_conv3(const float *gy, int64_t n, const float *w, float *gx, void *user_ws, hipStream_t st,
+                               const float *ymask = nullptr, float *bpart = nullptr) {
   static u32x4 *ws[64] = {};
   constexpr int PK = X9Dgrad3<1>::PACKED_U4;
   u32x4 *wpk = static_cast<u32x4 *>(user_ws);
@@ -1971,11 +2042,9 @@ static int conv_dgrad_x9_conv3(const float *gy, int64_t n, const float *w, float
                        dim3(256), 0, st, w, wpk);
     RTH_LAUNCHED();
   }
-  const void *fn[4] = {nullptr, reinterpret_cast<const void *>(&k_conv_x9<3, 3, 1, 64, 11, 11, 1, 3, X9_DGRAD3_KS, 2>),
-                       reinterpret_cast<const void *>(&k_conv_x9<3, 3, 1, 64, 11, 11, 2, 3, X9_DGRAD3_KS, 2>),
-                       reinterpret_cast<const void *>(&k_conv_x9<3, 3, 1, 64, 11, 11, 3, 3, X9_DGRAD3_KS, 2>)};
-  const int64_t ns = dgrad_x9_nsamp(n, 1, fn, X9Dgrad3<1>::NT, (int)x9_wg_per_cu());
-  return launch_dgrad_x9(fn[ns], gy, n, ns, 1, X9Dgrad3<1>::NT, wpk, gx, st);
+  const bool mask = ymask != nullptr;
+  const int64_t ns = dgrad3_nsamp(n, mask);
+  return launch_dgrad_x9(dgrad3_fn(ns, mask), gy, n, ns, 1, X9Dgrad3<1>::NT, wpk, gx, st, ymask, bpart);
 }
 
 // conv2: gy [n, 9, 9, 64] -> gx [n, 20, 20, 32]; each class reads gy padded to 11 x 11 and
@@ -2100,12 +2169,13 @@ int rth_conv_relu_wgrad_ex(const rth_conv_shape *shape, const void *x, const int
   bj.n = ndeferred;
   for (int j = 0; j < ndeferred; ++j) {
     const rth_bias_deferred &d = deferred[j];
-    RTH_REQUIRE(d.workspace && d.db && d.C >= 4 && d.C <= 256 && (d.C & (d.C - 1)) == 0 && d.rows >= 0,
+    RTH_REQUIRE(d.workspace && d.db && d.C >= 4 && d.C <= 256 && (d.C & (d.C - 1)) == 0 && d.rows >= 0 &&
+                    d.slabs >= 0 && d.slabs <= kBiasSlabs,
                 "rth_conv_relu_wgrad_ex: deferred bias gradient %d malformed", j);
     bj.part[j] = static_cast<const float *>(d.workspace);
     bj.db[j] = d.db;
     bj.C[j] = d.C;
-    bj.slabs[j] = (int)bias_grad_slabs(d.rows, d.C);
+    bj.slabs[j] = d.slabs > 0 ? d.slabs : (int)bias_grad_slabs(d.rows, d.C);
   }
   RTH_REQUIRE(is_conv1_u8(shape), "rth_conv_relu_wgrad: only the uint8 conv1 geometry (4x84x84 -> 32, k8 s4) is built");
   float *part = static_cast<float *>(workspace);
@@ -2195,8 +2265,10 @@ static int conv_bias_relu(const rth_conv_shape *shape, const void *x, const int6
     const int ns = (int)nsamp;
     const int64_t grid = (n + nsamp - 1) / nsamp;
     const float *xf = static_cast<const float *>(x);
+    const float *no_mask = nullptr;
+    float *no_part = nullptr;
     void *args[] = {(void *)&xf, (void *)&n, (void *)&n_dev, (void *)&ns, (void *)&w, (void *)&bias, (void *)&y,
-                    (void *)&out_nchw};
+                    (void *)&out_nchw, (void *)&no_mask, (void *)&no_part};
     RTH_HIP(hipLaunchKernel(l.x9fn[nsamp], dim3((unsigned)grid), dim3(l.waves * 64), args, 0, as_stream(stream)));
     return RTH_OK;
   }
@@ -2264,6 +2336,27 @@ int rth_conv_dgrad_prepacked(const rth_conv_shape *shape, const float *gy, int64
   void *ws = const_cast<void *>(packed);
   return d3 ? conv_dgrad_x9_conv3(gy, n, nullptr, gx, ws, as_stream(stream))
             : conv_dgrad_x9_conv2(gy, n, nullptr, gx, ws, as_stream(stream));
+}
+
+int rth_conv_dgrad_relu_supported(const rth_conv_shape *shape) { return shape && is_dgrad3_x9(shape) ? 1 : 0; }
+
+int rth_conv_dgrad_relu_prepacked(const rth_conv_shape *shape, const float *gy, int64_t n, const void *packed,
+                                  const float *y, float *gx, void *bias_ws, int64_t *slabs_out, void *stream) {
+  RTH_REQUIRE(shape && gy && packed && y && gx && bias_ws && slabs_out && n >= 0,
+              "rth_conv_dgrad_relu_prepacked: NULL argument");
+  RTH_REQUIRE(is_dgrad3_x9(shape), "rth_conv_dgrad_relu_prepacked: only conv3's geometry (64x9x9, k3 s1) is built");
+  RTH_REQUIRE(((reinterpret_cast<uintptr_t>(gy) | reinterpret_cast<uintptr_t>(packed) | reinterpret_cast<uintptr_t>(gx) |
+                reinterpret_cast<uintptr_t>(y) | reinterpret_cast<uintptr_t>(bias_ws)) &
+               15) == 0,
+              "rth_conv_dgrad_relu_prepacked: misaligned buffer");
+  *slabs_out = 0;
+  if (n == 0) return RTH_OK;
+  const int64_t slabs = (n + dgrad3_nsamp(n, true) - 1) / dgrad3_nsamp(n, true);
+  RTH_REQUIRE(slabs <= kBiasSlabs, "rth_conv_dgrad_relu_prepacked: %lld samples need %lld bias slabs (at most %d)",
+              (long long)n, (long long)slabs, kBiasSlabs);
+  *slabs_out = slabs;
+  return conv_dgrad_x9_conv3(gy, n, nullptr, gx, const_cast<void *>(packed), as_stream(stream), y,
+                             static_cast<float *>(bias_ws));
 }
 
 int rth_conv_dgrad_ws(const rth_conv_shape *shape, const float *gy, int64_t n, const float *w, float *gx,

@@ -52,6 +52,10 @@ HIP_WGRAD = None if not _wg else ("x9" if _wg == "x9" else "f32")
 # with CONV_PACK_DGRAD jobs; rth_conv_dgrad_prepacked in the backward) instead of one pack
 # launch per data gradient; RTH_DGRAD_PREPACK=0 keeps those (A/B)
 DGRAD_PREPACK = os.environ.get("RTH_DGRAD_PREPACK", "1") != "0"
+# conv3's data gradient applies conv2's ReLU mask and writes conv2's bias-gradient slabs in its
+# own epilogue (rth_conv_dgrad_relu_prepacked): one launch (rth_relu_bias_grad) fewer per
+# update; RTH_DGRAD_MASK=0 keeps the separate launch (A/B)
+DGRAD_MASK = os.environ.get("RTH_DGRAD_MASK", "1") != "0"
 
 
 def _net_workspace(net, kind, shape, device):
@@ -218,6 +222,7 @@ def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None, mid=No
         if getattr(net, "_ws", None) is None or net._ws[0].device != x.device:
             net._ws = [torch.zeros(_lib.lib().rth_relu_bias_grad_workspace(m.out_channels), dtype=torch.uint8,
                                    device=x.device) for m in convs]
+        fused_below = None  # (masked gradient, db) of the layer below, from the fused data gradient
         for li in range(len(convs) - 1, -1, -1):
             conv, y = convs[li], ys[li][:B]
             if li == 0 and u8:  # ReLU mask + weight/bias gradients from the stacks, and the
@@ -234,18 +239,23 @@ def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None, mid=No
                 deferred = []  # consumed
                 break
             nb, c, hh, ww = y.shape
-            gy = torch.empty((nb, c, hh, ww), dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
-            db = torch.empty(c, dtype=torch.float32, device=x.device)
             defer = u8  # finished by conv1's rth_conv_relu_wgrad_ex
-            if li == len(convs) - 1:  # NCHW output: mask + bias partials, gy written channels-last
-                call("rth_relu_bias_grad_nchw", ptr(g), ptr(y), ptr(gy), None if defer else ptr(db), ptr(net._ws[li]),
-                     nb, c, hh * ww, st)
+            if fused_below is not None:  # masked and its bias slabs written by the data gradient above
+                gy, db = fused_below
+                fused_below = None
             else:
-                g = _nhwc(g)
-                call("rth_relu_bias_grad", ptr(g), ptr(y), ptr(gy), None if defer else ptr(db), ptr(net._ws[li]),
-                     nb * hh * ww, c, st)
-            if defer:
-                deferred.append(_lib.BiasDeferred(net._ws[li].data_ptr(), db.data_ptr(), nb * hh * ww, c))
+                gy = torch.empty((nb, c, hh, ww), dtype=torch.float32, device=x.device,
+                                 memory_format=torch.channels_last)
+                db = torch.empty(c, dtype=torch.float32, device=x.device)
+                if li == len(convs) - 1:  # NCHW output: mask + bias partials, gy written channels-last
+                    call("rth_relu_bias_grad_nchw", ptr(g), ptr(y), ptr(gy), None if defer else ptr(db),
+                         ptr(net._ws[li]), nb, c, hh * ww, st)
+                else:
+                    g = _nhwc(g)
+                    call("rth_relu_bias_grad", ptr(g), ptr(y), ptr(gy), None if defer else ptr(db), ptr(net._ws[li]),
+                         nb * hh * ww, c, st)
+                if defer:
+                    deferred.append(_lib.BiasDeferred(net._ws[li].data_ptr(), db.data_ptr(), nb * hh * ww, c, 0))
             xin = ys[li - 1][:B] if li > 0 else x[:B]
             w = _nhwc(conv.weight.detach())
             hip_dgrad = li in HIP_DGRAD and _lib.lib().rth_conv_dgrad_supported(ctypes.byref(shapes[li]))
@@ -263,7 +273,18 @@ def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None, mid=No
                      ptr(_net_workspace(net, HIP_WGRAD, shapes[li], x.device)), st)
             if hip_dgrad:  # data gradient in rth_conv_dgrad (no zero fill)
                 gx = torch.empty(xin.shape, dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
-                if li in dgp:  # packed in the forward's pack launch
+                if li in dgp and li > 0 and defer and DGRAD_MASK and \
+                        _lib.lib().rth_conv_dgrad_relu_supported(ctypes.byref(shapes[li])):
+                    # + the layer below's ReLU mask and bias slabs (its rth_relu_bias_grad launch)
+                    slabs = ctypes.c_int64(0)
+                    call("rth_conv_dgrad_relu_prepacked", ctypes.byref(shapes[li]), ptr(gy), B, ptr(dgp[li]), ptr(xin),
+                         ptr(gx), ptr(net._ws[li - 1]), ctypes.byref(slabs), st)
+                    cb = convs[li - 1].out_channels
+                    db_below = torch.empty(cb, dtype=torch.float32, device=x.device)
+                    deferred.append(_lib.BiasDeferred(net._ws[li - 1].data_ptr(), db_below.data_ptr(),
+                                                      xin.shape[0] * xin.shape[2] * xin.shape[3], cb, slabs.value))
+                    fused_below = (gx, db_below)
+                elif li in dgp:  # packed in the forward's pack launch
                     call("rth_conv_dgrad_prepacked", ctypes.byref(shapes[li]), ptr(gy), B, ptr(dgp[li]), ptr(gx), st)
                 else:
                     call("rth_conv_dgrad_ws", ctypes.byref(shapes[li]), ptr(gy), B, ptr(w), ptr(gx),

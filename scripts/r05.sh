@@ -177,6 +177,14 @@ PY
         step bots_ts8big_$r 600 python bench.py --workload breakout --steps 100 --warmup 10 --no-cpu-baseline --no-sweep
       done
       summ gpurun_out/bots_*.log ;;
+    maskab)  # conv3's data gradient with conv2's ReLU mask + bias slabs in its epilogue vs the separate launch
+      step mask_tests 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_conv_gpu.py \
+          tests/test_fused_learner_gpu.py tests/test_learner_full_gpu.py tests/test_frame_store_gpu.py
+      for r in 1 2 3; do
+        step maskab_on_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        RTH_DGRAD_MASK=0 step maskab_off_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+      done
+      summ gpurun_out/maskab_*.log ;;
     dp8)  # 8 ranks on one GPU over gloo: bench.py's multi-rank path and its teardown (shutdown())
       RTH_SHARE_GPU=1 RTH_DIST_BACKEND=gloo step dp8_gloo_rehearsal 900 python -m torch.distributed.run --nnodes=1 \
           --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 8 --faithful --steps 20 \

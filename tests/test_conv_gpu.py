@@ -410,6 +410,68 @@ def test_conv_dgrad_prepacked(dev, gi):
     assert torch.equal(got, want)
 
 
+@pytest.mark.parametrize("n", [1, 5, 300, 512])
+def test_conv_dgrad_relu_prepacked(dev, n):
+    """conv3's data gradient with conv2's ReLU mask and bias slabs in its epilogue
+    (rth_conv_dgrad_relu_prepacked, r05): the masked gradient bit-identical to
+    rth_conv_dgrad_prepacked + rth_relu_bias_grad, and conv2's bias gradient -- the slabs finished
+    by the deferred job of conv1's reduce launch -- within fp32 summation error of the fp64 sum,
+    run-to-run bit-identical; refused for other geometries"""
+    from reth_amd import _lib
+
+    cin, h, wd, cout, k, s = GEOMS[2]
+    shape = _shape(_lib.CONV_F32_NHWC, *GEOMS[2])
+    if not _lib.lib().rth_conv_dgrad_relu_supported(_lib.ctypes.byref(shape)):
+        pytest.skip("conv3's data gradient is not the x9 kernel (RTH_DGRAD3_F32)")
+    ho = (h - k) // s + 1
+    g = torch.Generator(device=dev).manual_seed(500 + n)
+    gy = torch.randn((n, cout, ho, ho), device=dev, generator=g).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn((cout, cin, k, k), device=dev, generator=g) * 0.05).contiguous(memory_format=torch.channels_last)
+    y2 = torch.randn((n, cin, h, wd), device=dev, generator=g).contiguous(memory_format=torch.channels_last)
+    work = torch.empty(_lib.lib().rth_conv_dgrad_workspace(_lib.ctypes.byref(shape)) // 4, device=dev)
+    plain = torch.empty((n, cin, h, wd), device=dev).contiguous(memory_format=torch.channels_last)
+    _lib.call("rth_conv_dgrad_ws", _lib.ctypes.byref(shape), gy.data_ptr(), n, w.data_ptr(), plain.data_ptr(),
+              work.data_ptr(), _lib.stream_ptr())  # packs the flipped kernel into work, as the learner's pack launch
+    rows = n * h * wd
+    want = torch.empty_like(plain)
+    ws_ref = torch.empty(_lib.lib().rth_relu_bias_grad_workspace(cin), dtype=torch.uint8, device=dev)
+    db_ref = torch.empty(cin, device=dev)
+    _lib.call("rth_relu_bias_grad", plain.data_ptr(), y2.data_ptr(), want.data_ptr(), db_ref.data_ptr(),
+              ws_ref.data_ptr(), rows, cin, _lib.stream_ptr())
+    # conv1's reduce launch finishes the deferred job (a small conv1 problem beside it)
+    c1 = _shape(_lib.CONV_U8_CHW, *GEOMS[0])
+    st = torch.randint(0, 256, (3, 4, 84, 84), dtype=torch.uint8, device=dev, generator=g)
+    gc = torch.randn((3, 20, 20, 32), device=dev, generator=g)
+    yc = torch.randn((3, 20, 20, 32), device=dev, generator=g)
+    wsc = torch.empty(_lib.lib().rth_conv_wgrad_workspace(_lib.ctypes.byref(c1)), dtype=torch.uint8, device=dev)
+    dbs = []
+    for _ in range(2):
+        got = torch.full_like(plain, float("nan"))
+        ws = torch.empty(_lib.lib().rth_relu_bias_grad_workspace(cin), dtype=torch.uint8, device=dev)
+        slabs = _lib.ctypes.c_int64(-1)
+        _lib.call("rth_conv_dgrad_relu_prepacked", _lib.ctypes.byref(shape), gy.data_ptr(), n, work.data_ptr(),
+                  y2.data_ptr(), got.data_ptr(), ws.data_ptr(), _lib.ctypes.byref(slabs), _lib.stream_ptr())
+        assert 1 <= slabs.value <= n
+        db = torch.full((cin,), float("nan"), device=dev)
+        jobs = (_lib.BiasDeferred * 1)(_lib.BiasDeferred(ws.data_ptr(), db.data_ptr(), rows, cin, slabs.value))
+        gw, gb = torch.empty((32, 8, 8, 4), device=dev), torch.empty(32, device=dev)
+        _lib.call("rth_conv_relu_wgrad_ex", _lib.ctypes.byref(c1), st.data_ptr(), None, 3, gc.data_ptr(),
+                  yc.data_ptr(), gw.data_ptr(), gb.data_ptr(), wsc.data_ptr(), jobs, 1, _lib.stream_ptr())
+        torch.cuda.synchronize()
+        assert torch.equal(got, want)
+        dbs.append(db.clone())
+    assert torch.equal(dbs[0], dbs[1])
+    m = want.permute(0, 2, 3, 1).reshape(-1, cin).double().cpu()
+    exact, scale = m.sum(0), m.abs().sum(0)
+    assert ((dbs[0].double().cpu() - exact).abs() <= 1e-6 * scale + 1e-12).all()
+    assert ((db_ref.double().cpu() - exact).abs() <= 1e-6 * scale + 1e-12).all()
+    conv2 = _shape(_lib.CONV_F32_NHWC, *GEOMS[1])
+    assert _lib.lib().rth_conv_dgrad_relu_supported(_lib.ctypes.byref(conv2)) == 0
+    with pytest.raises(_lib.RethHipError, match="only conv3"):
+        _lib.call("rth_conv_dgrad_relu_prepacked", _lib.ctypes.byref(conv2), gy.data_ptr(), n, work.data_ptr(),
+                  y2.data_ptr(), got.data_ptr(), ws.data_ptr(), _lib.ctypes.byref(slabs), _lib.stream_ptr())
+
+
 def test_conv_dgrad_unsupported(dev):
     from reth_amd import _lib
 

@@ -185,6 +185,12 @@ PY
         RTH_DGRAD_MASK=0 step maskab_off_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
       done
       summ gpurun_out/maskab_*.log ;;
+    cfcab)  # Pong: the actors' FC1 over the N acting rows + the device-counted terminal rows (counted FC) vs 2N rows
+      for r in 1 2 3; do
+        step cfcab_dflt_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        RTH_ACTOR_COUNTED_FC=1 step cfcab_cfc_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+      done
+      summ gpurun_out/cfcab_*.log ;;
     dp8)  # 8 ranks on one GPU over gloo: bench.py's multi-rank path and its teardown (shutdown())
       RTH_SHARE_GPU=1 RTH_DIST_BACKEND=gloo step dp8_gloo_rehearsal 900 python -m torch.distributed.run --nnodes=1 \
           --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 8 --faithful --steps 20 \

@@ -191,6 +191,13 @@ PY
         RTH_ACTOR_COUNTED_FC=1 step cfcab_cfc_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
       done
       summ gpurun_out/cfcab_*.log ;;
+    fcx9s)  # Pong: the 512-row FC1 forwards (actors, target pass) on rth_fc_x9 (48 KB of LDS) vs hipBLASLt (80 KB)
+      for r in 1 2 3; do
+        step fcx9s_blas_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        RTH_FC=x9 RTH_FC_MAX_ROWS=512 step fcx9s_x9_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline \
+            --no-sweep
+      done
+      summ gpurun_out/fcx9s_*.log ;;
     dp8)  # 8 ranks on one GPU over gloo: bench.py's multi-rank path and its teardown (shutdown())
       RTH_SHARE_GPU=1 RTH_DIST_BACKEND=gloo step dp8_gloo_rehearsal 900 python -m torch.distributed.run --nnodes=1 \
           --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 8 --faithful --steps 20 \

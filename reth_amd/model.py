@@ -412,12 +412,16 @@ class _MergeHeads(torch.autograd.Function):
         return (None, *grads)
 
 
-# FC1 + bias + ReLU: RTH_FC=f32 -> rth_fc_f32 (fp32 MFMA, no LDS, fixed-order split-K),
-# RTH_FC=x9 (or RTH_FC_X9=1) -> rth_fc_x9 (the exact-split bf16 MFMA), wherever the shape is
-# built; otherwise hipBLASLt's GEMM with the bias+ReLU epilogue.  RTH_FC_MAX_ROWS limits the
-# hand-written kernels to batches of at most that many rows (the rest stay on hipBLASLt)
-_FC_KIND = os.environ.get("RTH_FC", "x9" if os.environ.get("RTH_FC_X9") == "1" else "blas")
-_FC_MAX_ROWS = int(os.environ.get("RTH_FC_MAX_ROWS", "0") or 0)
+# FC1 + bias + ReLU: RTH_FC=x9 -> rth_fc_x9 (the exact-split bf16 MFMA, fixed-order split-K),
+# RTH_FC=f32 -> rth_fc_f32 (fp32 MFMA, no LDS), RTH_FC=blas -> hipBLASLt's GEMM with the
+# bias+ReLU epilogue, for batches of at most RTH_FC_MAX_ROWS rows (0: any) where the shape is
+# built; the rest on hipBLASLt.  Default since r05: x9 up to 512 rows -- the actors' and the
+# target pass's forwards: the same step as hipBLASLt (0.536-0.539 vs 0.536 ms, interleaved) with
+# every product exact (a third of the learner's |td| error came from FC1's fp32 chains, DESIGN
+# (c)); the learner's 1,024-row forward stays on hipBLASLt (x9: 43 vs 30 us alone).
+# RTH_FC_X9=1 (r04's switch): x9 at every row count.
+_FC_KIND = os.environ.get("RTH_FC", "x9")
+_FC_MAX_ROWS = int(os.environ.get("RTH_FC_MAX_ROWS", "0" if os.environ.get("RTH_FC_X9") == "1" else "512") or 0)
 _FC_WS = {}
 
 

@@ -243,9 +243,10 @@ void *rth_replay_column(rth_replay *h, int32_t c);
  * the gather assembles the same uint8 stacks the full rows would hold.  store_out / head_out
  * (nullable): the store ([n_frames, frame_bytes]) and its device head (frames pushed).  The
  * store is a ring: it must hold every frame a live row references -- a row's oldest frame is
- * at most n + 4 actor steps older than the row, and a row lives capacity / N appends -- so
- * n_frames >= capacity x (1 + the reset rate) + (n + 8) x N with N actors (reth_amd.replay
- * sizes it). */
+ * at most n + 4 actor steps older than the row, and a row lives capacity / N appends, and a
+ * step pushes at most 2 N frames -- so n_frames >= 2 capacity + 2 (n + 16) N with N actors
+ * covers every episode-end pattern (reth_amd.apex.ApexDQN.frame_store_frames, "hard").
+ * *head_out = the device word holding the next frame id (a second word after it is internal). */
 int rth_replay_frames_attach(rth_replay *h, int64_t n_frames, int64_t frame_bytes, void **store_out,
                              int64_t **head_out);
 /* One vectorised actor step's frames into the store (VecActors, after the env step):

@@ -460,7 +460,9 @@ int conv_of(int32_t in_dtype, int32_t out_dtype, int32_t planes, int32_t *conv) 
 //   mode 1 (init): actor i's current stack (slot cur_slot[i]) enters as K new frames
 //     head + K i .. head + K i + K - 1.
 // One workgroup per actor copies its frame(s) (7,056 bytes each at Atari size, 16-byte
-// vectors); k_frames_advance then moves the head past the frames of the step.
+// vectors); the launch's last workgroup (a ticket in fhead[1]) then moves the head past the
+// frames of the step -- every workgroup read it at its start, before taking its ticket (r05:
+// was a second launch, k_frames_advance).
 constexpr int kFrameThreads = 256;
 
 __global__ __launch_bounds__(kFrameThreads) void k_frames_push(const uint8_t *__restrict__ ring, int64_t stack_bytes,
@@ -470,10 +472,38 @@ __global__ __launch_bounds__(kFrameThreads) void k_frames_push(const uint8_t *__
                                                                const float *__restrict__ done,
                                                                const int64_t *__restrict__ cur_slot,
                                                                int32_t *__restrict__ sid, uint8_t *__restrict__ store,
-                                                               int64_t fcap, const int64_t *__restrict__ fhead,
-                                                               int64_t n, int mode) {
+                                                               int64_t fcap, int64_t *fhead, int64_t n, int mode) {
+  __shared__ int64_t part[kFrameThreads];
+  __shared__ int last;
   const int64_t i = blockIdx.x;
   const int64_t head = *fhead;
+  // the last workgroup to finish moves the head: N (+ one per done actor in mode 0, K per
+  // actor in mode 1).  Relaxed atomics suffice: no data is handed between the workgroups, only
+  // the order "every read of the head, then its one write" (the next push reads it after the
+  // launch boundary).
+  auto advance = [&]() {
+    __syncthreads();  // every lane's use of head is behind it
+    if (threadIdx.x == 0) {
+      unsigned int *ticket = reinterpret_cast<unsigned int *>(fhead + 1);
+      last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned int)(n - 1);
+    }
+    __syncthreads();
+    if (!last) return;  // workgroup-uniform
+    int64_t c = 0;
+    if (mode == 0)
+      for (int64_t j = threadIdx.x; j < n; j += kFrameThreads) c += done[j] != 0.0f;
+    part[threadIdx.x] = c;
+    __syncthreads();
+    for (int w = kFrameThreads / 2; w > 0; w >>= 1) {
+      if ((int)threadIdx.x < w) part[threadIdx.x] += part[threadIdx.x + w];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      __hip_atomic_store(fhead, head + (mode == 1 ? (int64_t)K * n : n + part[0]), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(reinterpret_cast<unsigned int *>(fhead + 1), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  };
   const int64_t vecs = frame_bytes / 16;
   auto copy = [&](const uint8_t *src, int64_t fid) {
     uint4 *d = reinterpret_cast<uint4 *>(store + (fid % fcap) * frame_bytes);
@@ -484,6 +514,7 @@ __global__ __launch_bounds__(kFrameThreads) void k_frames_push(const uint8_t *__
     const int64_t st = i * ring_slots + cur_slot[i];
     for (int k = 0; k < K; ++k) copy(ring + st * stack_bytes + k * frame_bytes, head + K * i + k);
     if (threadIdx.x < K) sid[st * K + threadIdx.x] = (int32_t)(uint32_t)((head + K * i + threadIdx.x) % fcap);
+    advance();
     return;
   }
   const int64_t h0 = s0_h[i], h1 = s1_h[i];
@@ -498,22 +529,7 @@ __global__ __launch_bounds__(kFrameThreads) void k_frames_push(const uint8_t *__
     copy(ring + rs * stack_bytes, fid);
     if (threadIdx.x < K) sid[rs * K + threadIdx.x] = (int32_t)(uint32_t)(fid % fcap);
   }
-}
-
-// the head past this step's frames: N (+ one per done actor in mode 0, K per actor in mode 1)
-__global__ __launch_bounds__(kFrameThreads) void k_frames_advance(const float *__restrict__ done, int64_t n, int K,
-                                                                  int mode, int64_t *__restrict__ fhead) {
-  __shared__ int64_t part[kFrameThreads];
-  int64_t c = 0;
-  if (mode == 0)
-    for (int64_t j = threadIdx.x; j < n; j += kFrameThreads) c += done[j] != 0.0f;
-  part[threadIdx.x] = c;
-  __syncthreads();
-  for (int w = kFrameThreads / 2; w > 0; w >>= 1) {
-    if ((int)threadIdx.x < w) part[threadIdx.x] += part[threadIdx.x + w];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) *fhead += mode == 1 ? (int64_t)K * n : n + part[0];
+  advance();
 }
 
 }  // namespace rth
@@ -783,13 +799,13 @@ int rth_replay_frames_attach(rth_replay *h, int64_t n_frames, int64_t frame_byte
     set_error("rth_replay_frames_attach: hipMalloc(%lld x %lld) failed", (long long)n_frames, (long long)frame_bytes);
     return RTH_ERR_NOMEM;
   }
-  if (hipMalloc(&h->fhead, 8) != hipSuccess) {
+  if (hipMalloc(&h->fhead, 16) != hipSuccess) {  // [the next frame id, k_frames_push's ticket]
     (void)hipFree(h->fstore);
     h->fstore = nullptr;
     return RTH_ERR_NOMEM;
   }
   RTH_HIP(hipMemset(h->fstore, 0, (size_t)n_frames * frame_bytes));
-  RTH_HIP(hipMemset(h->fhead, 0, 8));
+  RTH_HIP(hipMemset(h->fhead, 0, 16));
   h->fcap = n_frames;
   h->frame_bytes = frame_bytes;
   if (store_out) *store_out = h->fstore;
@@ -810,8 +826,6 @@ int rth_replay_push_frames(rth_replay *h, const uint8_t *ring, int64_t n, int32_
   hipLaunchKernelGGL(k_frames_push, dim3((unsigned)n), dim3(kFrameThreads), 0, s, ring, stack_bytes, h->frame_bytes,
                      (int)stack, (int)ring_slots, s0_h, s1_h, done, cur_slot, sid, h->fstore, h->fcap, h->fhead, n,
                      (int)mode);
-  RTH_LAUNCHED();
-  hipLaunchKernelGGL(k_frames_advance, dim3(1), dim3(kFrameThreads), 0, s, done, n, (int)stack, (int)mode, h->fhead);
   RTH_LAUNCHED();
   return RTH_OK;
 }

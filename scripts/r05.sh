@@ -198,6 +198,13 @@ PY
             --no-sweep
       done
       summ gpurun_out/fcx9s_*.log ;;
+    fadvab)  # the frame head advanced by k_frames_push's last workgroup vs a second launch
+      for r in 1 2 3; do
+        step fadvab_ticket_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        RTH_FRAMES_ADVANCE_LAUNCH=1 step fadvab_launch_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline \
+            --no-sweep
+      done
+      summ gpurun_out/fadvab_*.log ;;
     dp8)  # 8 ranks on one GPU over gloo: bench.py's multi-rank path and its teardown (shutdown())
       RTH_SHARE_GPU=1 RTH_DIST_BACKEND=gloo step dp8_gloo_rehearsal 900 python -m torch.distributed.run --nnodes=1 \
           --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 8 --faithful --steps 20 \

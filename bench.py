@@ -628,7 +628,7 @@ def main():
     ap.add_argument("--cpu-actor-worker", type=float, default=None, help=argparse.SUPPRESS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-iters", type=int, default=72)
-    ap.add_argument("--tag", default="r04", help="profiles/traffic_TAG.json: the PMC pass the traffic fields cite")
+    ap.add_argument("--tag", default="r05", help="profiles/traffic_TAG.json: the PMC pass the traffic fields cite")
     ap.add_argument("--nchw", action="store_true", help="contiguous NCHW Q-net tensors (default channels-last)")
     ap.add_argument("--no-conv-benchmark", action="store_true", help="MIOpen immediate mode instead of find")
     ap.add_argument("--eager", action="store_true", help="no HIP-graph replay (launch every kernel from Python)")

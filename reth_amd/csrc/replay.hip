@@ -940,17 +940,6 @@ static int gather_impl(rth_replay *h, const int64_t *idx, int64_t n, void *const
     const rth_col_desc &d = h->desc[c];
     if (d.in_dtype == RTH_FRAMES) {  // the stack assembled from the frame store
       RTH_REQUIRE(h->fstore, "rth_replay_gather: frame-stack column %d without a frame store", c);
-      // timing-only diagnostic (RTH_DIAG_NO_STACKS=1, WRONG DATA: the batch keeps stale stacks):
-      // the cost of assembling the stacks, by copying 16 bytes per row instead
-      static const bool no_stacks = [] {
-        const char *e = getenv("RTH_DIAG_NO_STACKS");
-        return e && atoi(e) == 1;
-      }();
-      if (no_stacks) {
-        a.col[c] = CopyCol{h->store[c], (uint8_t *)out_cols[c], idx, nullptr, stored_row_bytes(d), d.row_elems, 16,
-                           CONV_COPY, 0};
-        continue;
-      }
       const int64_t ob = d.row_elems;
       CopyCol col{h->store[c], (uint8_t *)out_cols[c], idx, nullptr, stored_row_bytes(d), ob, ob, CONV_STACK,
                   d.out_planes};

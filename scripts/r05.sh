@@ -205,12 +205,8 @@ PY
             --no-sweep
       done
       summ gpurun_out/fadvab_*.log ;;
-    nostk)  # timing only (WRONG DATA): the step without assembling the sampled stacks (the gather's bulk)
-      for r in 1 2 3; do
-        step nostk_dflt_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
-        RTH_DIAG_NO_STACKS=1 step nostk_skip_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
-      done
-      summ gpurun_out/nostk_*.log ;;
+    # nostk (the gather without its stack assembly, RTH_DIAG_NO_STACKS=1, a timing-only build of
+    # commit 'Diagnostic: RTH_DIAG_NO_STACKS=1'): profiles/r05/ab_log.txt
     dp8)  # 8 ranks on one GPU over gloo: bench.py's multi-rank path and its teardown (shutdown())
       RTH_SHARE_GPU=1 RTH_DIST_BACKEND=gloo step dp8_gloo_rehearsal 900 python -m torch.distributed.run --nnodes=1 \
           --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 8 --faithful --steps 20 \

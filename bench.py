@@ -69,11 +69,14 @@ WORKLOADS = {
 WORKLOADS["pong-node"] = WORKLOADS["pong"]
 
 
-def gather_bytes_per_row(frames_u8=False):
+def gather_bytes_per_row(frames_u8=False, frame_ids=False):
     """algorithmic bytes of one sampled apex row in rth_replay_gather: read s0/s1 uint8
     stacks + a(8) r(4) done(4); write s0/s1 as float32 channels-last stacks, or -- with the
     HIP conv torso, which reads uint8 stacks itself -- as the uint8 stacks; a r done; 5
-    index reads"""
+    index reads.  frame_ids (frames in place): s0/s1 are the rows' 2 x 4 int32 frame ids,
+    read and written as they are"""
+    if frame_ids:
+        return 2 * (2 * 16 + 8 + 4 + 4) + 5 * 8
     read = 2 * STACK + 8 + 4 + 4
     write = 2 * STACK * (1 if frames_u8 else 4) + 8 + 4 + 4
     return read + write + 5 * 8
@@ -106,9 +109,11 @@ def conv1_roofline(ax, slot_cols, reps=30):
     around direct launches on the current stream"""
     from reth_amd import _lib
     from reth_amd.fused_learner import _pair
+    from reth_amd.replay import FrameStacks
 
     net = ax.solver.q_network
-    x = _pair(slot_cols[0], slot_cols[3])
+    frames = isinstance(slot_cols[0], FrameStacks)  # frames in place: conv1 reads the store by frame ids
+    x = (FrameStacks.pair if frames else _pair)(slot_cols[0], slot_cols[3])
     n = x.shape[0]
     shape = net._torso_shapes(tuple(x.shape[1:]), True)[0][1]
     pk = net._packed_for(net.pack_convs(), 0, True)
@@ -119,14 +124,19 @@ def conv1_roofline(ax, slot_cols, reps=30):
     for _ in range(reps):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        _lib.call("rth_conv_bias_relu", _lib.ctypes.byref(shape), x.data_ptr(), None, n, pk.data_ptr(),
-                  bias.data_ptr(), y.data_ptr(), _lib.stream_ptr())
+        if frames:
+            _lib.call("rth_conv1_frames_bias_relu", _lib.ctypes.byref(shape), x.store.data_ptr(), x.ids.data_ptr(), n,
+                      pk.data_ptr(), bias.data_ptr(), y.data_ptr(), _lib.stream_ptr())
+        else:
+            _lib.call("rth_conv_bias_relu", _lib.ctypes.byref(shape), x.data_ptr(), None, n, pk.data_ptr(),
+                      bias.data_ptr(), y.data_ptr(), _lib.stream_ptr())
         e1.record()
         ev.append((e0, e1))
     torch.cuda.synchronize()
     t = float(np.median([a.elapsed_time(b) for a, b in ev[5:]])) / 1e3
     flops = 2.0 * n * ho * ho * shape.cout * shape.cin * shape.kh * shape.kw
-    return {"kernel": f"k_conv1_u8_bf16x3 (uint8 stacks, {n} samples = the learner's [s0; s1])",
+    src = "frames in place, by frame ids" if frames else "uint8 stacks"
+    return {"kernel": f"k_conv1_u8_share ({src}, {n} samples = the learner's [s0; s1])",
             "bound": "mfma", "achieved": round(3 * flops / t / 1e12, 2), "peak": BF16_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": round(3 * flops / t / 1e12 / BF16_PEAK_TFLOPS, 4),
             "achieved_fp32_equiv": round(flops / t / 1e12, 2), "flops_per_launch": flops,
@@ -469,7 +479,8 @@ def hbm_bytes(cfg, n_rows_per_append):
         "k_tree_sample": B * (D * 16 + 8 + 8 + 8),
         # read + write of every sampled row (uint8 stacks, the HIP torso reads them as they are)
         # + the 5 index reads
-        "k_copy_rows (gather)": B * (2 * row + 5 * 8 + (2 * 4 * 4 if cfg.frame_store else 0)),
+        "k_copy_rows (gather)": B * (gather_bytes_per_row(True, True) if cfg.frame_store and cfg.frame_ids else
+                                     2 * row + 5 * 8 + (2 * 4 * 4 if cfg.frame_store else 0)),
         # the append's rows: each column row read from the actors' ring and written to its slot
         # (frame store: the two stacks' frame ids instead of the stacks)
         "k_copy_rows (insert)": N * (2 * ((2 * 4 * 4 + 16) if cfg.frame_store else row) + 5 * 8),
@@ -680,7 +691,8 @@ def main():
                      actor_steps_per_update=args.actor_steps_per_update, seed=0,
                      channels_last=not args.nchw, conv_benchmark=not args.no_conv_benchmark,
                      hip_graph=not args.eager, hip_conv=hip_conv, env=args.env, frame_store=args.frame_store,
-                     frame_store_bound=args.frame_store_bound, extra={"learner_priority": int(os.environ.get("RTH_LEARNER_PRIORITY", "0")),
+                     frame_store_bound=args.frame_store_bound,
+                     frame_ids=args.frame_store and os.environ.get("RTH_FRAME_IDS", "0") == "1", extra={"learner_priority": int(os.environ.get("RTH_LEARNER_PRIORITY", "0")),
                             "probe_conv2": probe})
     ax = ApexDQN(cfg, device=dev, rank=rank, world=world)
     ax.prefill(cfg.capacity)
@@ -858,8 +870,9 @@ def main():
         replicas = all(torch.equal(allh[0], h) for h in allh[1:])
     gather_ms = [a.elapsed_time(b) for a, b in ktimer.pairs["gather"]]
     mean_gather_s = float(np.mean(gather_ms)) / 1e3
-    bytes_launch = (gather_bytes_per_row(cfg.hip_conv and cfg.channels_last) + (32 if cfg.frame_store else 0)) \
-        * cfg.batch_size  # frame store: + the rows' 2 x 4 frame ids
+    fids = bool(cfg.frame_store and cfg.frame_ids and cfg.hip_conv and cfg.channels_last)
+    bytes_launch = (gather_bytes_per_row(cfg.hip_conv and cfg.channels_last, fids) +
+                    (32 if cfg.frame_store and not fids else 0)) * cfg.batch_size  # frame store: + the ids read
     achieved = bytes_launch / mean_gather_s / 1e9
     # the same gather alone on the GPU (in the timed region it shares the GPU with the
     # concurrently running learner block): context for the in-loop figure, not `achieved`
@@ -900,7 +913,8 @@ def main():
     c3_traffic, c3_src = load_traffic(args.tag, "conv3_learner_hbm_bytes_per_launch")
     roofline_gather = {
         "kernel": "rth_replay_gather (k_copy_rows: PER-sampled rows, frames %s)"
-                  % ("uint8 stacks" if cfg.hip_conv and cfg.channels_last else "u8->f32 NHWC"),
+                  % ("as frame ids (conv1 reads the store)" if fids else
+                     "uint8 stacks" if cfg.hip_conv and cfg.channels_last else "u8->f32 NHWC"),
         "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
         "bytes_per_launch": bytes_launch, "mean_launch_us": round(mean_gather_s * 1e6, 2),

@@ -260,6 +260,11 @@ int rth_replay_frames_attach(rth_replay *h, int64_t n_frames, int64_t frame_byte
 int rth_replay_push_frames(rth_replay *h, const uint8_t *ring_dev, int64_t n, int32_t ring_slots, int32_t stack,
                            const int64_t *s0_h_dev, const int64_t *s1_h_dev, const float *done_dev,
                            const int64_t *cur_slot_dev, int32_t *sid_dev, int32_t mode, void *stream);
+/* Frames in place (r05): on = 1 makes the gathers (rth_replay_gather / _sample with out_cols)
+ * write each frame-stack column's stored id tuple (int32 [n][4], 16-byte aligned output)
+ * instead of the assembled stack; rth_conv1_frames_* read the frames from the store by
+ * them.  4-frame stacks only.  on = 0 restores the stacks. */
+int rth_replay_frames_ids_out(rth_replay *h, int32_t on);
 
 /* ------------------------------------------------------------------------------------
  * Row copy / gather with optional uint8 -> float32 widening (the loaders' pinned copy +
@@ -606,6 +611,18 @@ typedef struct rth_bias_deferred {
 int rth_conv_relu_wgrad_ex(const rth_conv_shape *shape, const void *x_dev, const int64_t *rows_dev, int64_t n,
                            const float *g_dev, const float *y_dev, float *gw_dev, float *gb_dev, void *workspace_dev,
                            const rth_bias_deferred *deferred, int32_t ndeferred, void *stream);
+/* Frames in place (r05): conv1 (4x84x84 uint8 -> 32, k8 s4) forward and weight gradient
+ * reading each sample's 4 frames straight from a replay's frame store (the
+ * rth_replay_frames_attach store, 84*84-byte frames) by the int32 [n][4] frame ids a
+ * rth_replay_frames_ids_out gather wrote (16-byte aligned), instead of from gathered stacks:
+ * results bit-identical to rth_conv_bias_relu / rth_conv_relu_wgrad_ex on the stacks
+ * rth_replay_gather would have assembled from the same ids, without that copy. */
+int rth_conv1_frames_bias_relu(const rth_conv_shape *shape, const uint8_t *store_dev, const int32_t *ids_dev,
+                               int64_t n, const float *packed_dev, const float *bias_dev, float *y_dev, void *stream);
+int rth_conv1_frames_relu_wgrad_ex(const rth_conv_shape *shape, const uint8_t *store_dev, const int32_t *ids_dev,
+                                   int64_t n, const float *g_dev, const float *y_dev, float *gw_dev, float *gb_dev,
+                                   void *workspace_dev, const rth_bias_deferred *deferred, int32_t ndeferred,
+                                   void *stream);
 
 /* ------------------------------------------------------------------------------------
  * Atari observation preprocessing (reth/reth/env/util.py:121-209, 281-297): per actor, the

@@ -116,6 +116,7 @@ SIGNATURES = {
     "rth_replay_column": (c_vp, [c_vp, c_i32]),
     "rth_replay_frames_attach": (c_i32, [c_vp, c_i64, c_i64, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp)]),
     "rth_replay_push_frames": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp]),
+    "rth_replay_frames_ids_out": (c_i32, [c_vp, c_i32]),
     "rth_copy_rows": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i32, c_i32, c_vp]),
     # actors
     "rth_eps_greedy": (c_i32, [c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_u64, c_u64, c_vp, c_vp, c_vp]),
@@ -169,9 +170,12 @@ SIGNATURES = {
                                     c_vp]),
     "rth_conv_relu_wgrad_ex": (c_i32, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
                                        c_vp, c_i32, c_vp]),
+    "rth_conv1_frames_relu_wgrad_ex": (c_i32, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp,
+                                               c_vp, c_vp, c_i32, c_vp]),
     "rth_conv_pack_many": (c_i32, [c_i32, ctypes.POINTER(ConvShape), ctypes.POINTER(c_vp), ctypes.POINTER(c_vp),
                                    c_vp]),
     "rth_conv_bias_relu": (c_i32, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "rth_conv1_frames_bias_relu": (c_i32, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "rth_conv_bias_relu_upto": (c_i32, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "rth_conv_dgrad_supported": (c_i32, [ctypes.POINTER(ConvShape)]),
     "rth_conv_dgrad": (c_i32, [ctypes.POINTER(ConvShape), c_vp, c_i64, c_vp, c_vp, c_vp]),

@@ -103,6 +103,7 @@ class ApexConfig:
     env: str = "synthetic"         # actors' observations: synthetic | atari | atari-h2d (VecActors)
     frame_store: bool = False      # frame de-duplicated replay: each frame stored once, rows as frame ids
     frame_store_bound: str = "hard"  # store size: "hard" (worst case, 2 frames per actor step) | "expected" (p_done)
+    frame_ids: bool = False        # frame store: batches hold frame ids, conv1 reads the frames in place (no stacks)
     extra: dict = field(default_factory=dict)
 
 
@@ -154,6 +155,8 @@ class ApexDQN:
         self.replay = self.svc.replay
         if cfg.frame_store:
             self.actors.attach_frame_store(self.replay)
+            if cfg.frame_ids and u8:  # the sampled batches are FrameStacks (fused_learner reads them in place)
+                self.replay.set_frame_ids(True)
         self.loader = TorchCudaLoader(self.addr, buffer_size=2, prefetch=1)
         self.env_steps = 0
         self.updates = 0

@@ -511,10 +511,16 @@ __device__ __forceinline__ uint32_t from_next_lane(uint32_t v) {  // lane i <- l
 
 __device__ unsigned char g_conv1_sink[64 * 128];  // stores of lanes without an output (never read)
 
+// FRM (r05): x is a replay's frame store (84 x 84-byte frames) and fids[b] the 4 frame ids of
+// sample b's stack (the sampled rows' id tuples, rth_replay_sample_frame_ids): each run
+// (ci, kh) is read from frame fids[b][ci] -- the bytes the gather would have assembled, so the
+// outputs are bit-identical, without the batch copy of the stacks
+constexpr int64_t kC1FrameBytes = 84 * 84;
+template <bool FRM = false>
 __global__ __launch_bounds__(256) void k_conv1_u8_share(const void *__restrict__ x, const int64_t *__restrict__ rows,
                                                       int64_t n, const int64_t *__restrict__ n_dev,
                                                       const float *__restrict__ w, const float *__restrict__ bias,
-                                                      float *__restrict__ y) {
+                                                      float *__restrict__ y, const int32_t *__restrict__ fids) {
   constexpr int HIN = 84, WIN = 84, WOUT = 20, PIX = 400, S = 4, COUT = 32;
   constexpr int VPS = WOUT * kC1VPix;  // 420 virtual pixels per sample
   constexpr int64_t STACK = 4 * HIN * WIN;
@@ -563,9 +569,23 @@ __global__ __launch_bounds__(256) void k_conv1_u8_share(const void *__restrict__
   constexpr int NB = kC1BufShare;
   uint32_t raw[NB][kC1Chunks];  // the first halves of the runs, a ring of tiles in flight
   auto load = [&](uint32_t (&dst)[kC1Chunks], int t) {
-    const uint8_t *p = window(t);
+    if constexpr (FRM) {
+      int b, oy, ox;
+      vpix(t, b, oy, ox);
+      const int4 id = reinterpret_cast<const int4 *>(fids)[b];
+      const int off = (S * oy) * WIN + S * ox;
+      const uint8_t *fb[4] = {xb + (int64_t)id.x * kC1FrameBytes + off, xb + (int64_t)id.y * kC1FrameBytes + off,
+                              xb + (int64_t)id.z * kC1FrameBytes + off, xb + (int64_t)id.w * kC1FrameBytes + off};
 #pragma unroll
-    for (int c = 0; c < kC1Chunks; ++c) dst[c] = *reinterpret_cast<const uint32_t *>(p + run_off(c));
+      for (int c = 0; c < kC1Chunks; ++c) {
+        const int rho = 2 * c + h;  // run (ci, kh) = (rho / 8, rho % 8): h picks the odd / even runs
+        dst[c] = *reinterpret_cast<const uint32_t *>(fb[(2 * c) >> 3] + (rho & 7) * WIN);
+      }
+    } else {
+      const uint8_t *p = window(t);
+#pragma unroll
+      for (int c = 0; c < kC1Chunks; ++c) dst[c] = *reinterpret_cast<const uint32_t *>(p + run_off(c));
+    }
   };
   auto compute = [&](const uint32_t (&src)[kC1Chunks], int t) {
     f32x16 acc;
@@ -1176,7 +1196,7 @@ static ConvLaunch conv1_bf16x3_launch() {
     return e && atoi(e) != 0;
   }();
   ConvLaunch l{noshare ? reinterpret_cast<const void *>(&k_conv1_u8_bf16x3)
-                       : reinterpret_cast<const void *>(&k_conv1_u8_share),
+                       : reinterpret_cast<const void *>(&k_conv1_u8_share<false>),
                reinterpret_cast<const void *>(&k_conv1_pack_bf16x3), 4, kC1PackedBytes, 0, 32, noshare ? 1 : 2, 0, 0,
                {}, nullptr, 0, 0};
   int blocks = 0;
@@ -1637,7 +1657,9 @@ __device__ __forceinline__ void split3_trunc(float a, uint32_t &t0, uint32_t &t1
   t2 = __float_as_uint(rsub(r1, __uint_as_float(t1)));  // <= 8 significand bits: exact in bf16
 }
 
-template <bool ROWS>
+// MODE 0: x holds the n stacks; 1: rows[b] indexes x's stacks; 2 (r05): x is a replay's frame
+// store and rows the int32 [n][4] frame ids of the stacks (k_conv1_u8_share<true>'s input)
+template <int MODE>
 __global__ __launch_bounds__(kWgWaves * 64) void k_conv1_wgrad_bf16x3(const uint8_t *__restrict__ x,
                                                                      const int64_t *__restrict__ rows, int64_t n,
                                                                      const float *__restrict__ g,
@@ -1666,11 +1688,17 @@ __global__ __launch_bounds__(kWgWaves * 64) void k_conv1_wgrad_bf16x3(const uint
     const int64_t gi = live ? gq : g_end - 1;
     const int64_t s0 = 2 * gi, s1 = s0 + 1 < NS ? s0 + 1 : NS - 1;  // wave-uniform
     const int64_t b0 = s0 / SLOTS, b1 = s1 / SLOTS;
-    const int64_t rw0 = ROWS ? rows[b0] : b0, rw1 = ROWS ? rows[b1] : b1;
+    const int64_t rw0 = MODE == 1 ? rows[b0] : b0, rw1 = MODE == 1 ? rows[b1] : b1;
     const int64_t sl = h ? s1 : s0, b = h ? b1 : b0, row = h ? rw1 : rw0;
     const int rem = (int)(sl - b * SLOTS), oy = rem / 3, seg = rem % 3;
     rw.nv = live && 2 * gi + h < NS ? (seg == 2 ? 4 : 8) : 0;
-    const uint8_t *src = x + row * (int64_t)STACK + row_off + (S * oy) * WIN + S * 8 * seg;
+    const uint8_t *src;
+    if constexpr (MODE == 2) {  // run (ci, kh) = (o / KH, o % KH) from frame ids[b][ci]
+      const int64_t fid = reinterpret_cast<const int32_t *>(rows)[b * 4 + o / KH];
+      src = x + fid * (int64_t)(HIN * WIN) + (o % KH) * WIN + (S * oy) * WIN + S * 8 * seg;
+    } else {
+      src = x + row * (int64_t)STACK + row_off + (S * oy) * WIN + S * 8 * seg;
+    }
     const u32x4 v0 = *reinterpret_cast<const u32x4 *>(src);
     const uint32_t v4 = *reinterpret_cast<const uint32_t *>(src + 16);
     // the last slot's span ends the row: its unused upper part re-reads the lower
@@ -2159,9 +2187,27 @@ int64_t rth_conv_wgrad_workspace(const rth_conv_shape *shape) {
   return is_conv1_u8(shape) ? (int64_t)kWgBlocks * (32 * 256 + 32) * 4 : 0;
 }
 
+static int conv1_relu_wgrad(const rth_conv_shape *shape, const void *x, const int64_t *rows, const int32_t *fids,
+                            int64_t n, const float *g, const float *y, float *gw, float *gb, void *workspace,
+                            const rth_bias_deferred *deferred, int32_t ndeferred, void *stream);
+
 int rth_conv_relu_wgrad_ex(const rth_conv_shape *shape, const void *x, const int64_t *rows, int64_t n, const float *g,
                            const float *y, float *gw, float *gb, void *workspace, const rth_bias_deferred *deferred,
                            int32_t ndeferred, void *stream) {
+  return conv1_relu_wgrad(shape, x, rows, nullptr, n, g, y, gw, gb, workspace, deferred, ndeferred, stream);
+}
+
+int rth_conv1_frames_relu_wgrad_ex(const rth_conv_shape *shape, const uint8_t *store, const int32_t *ids, int64_t n,
+                                   const float *g, const float *y, float *gw, float *gb, void *workspace,
+                                   const rth_bias_deferred *deferred, int32_t ndeferred, void *stream) {
+  RTH_REQUIRE(store && ids && (reinterpret_cast<uintptr_t>(ids) & 15) == 0,
+              "rth_conv1_frames_relu_wgrad_ex: NULL / misaligned frame store or ids");
+  return conv1_relu_wgrad(shape, store, nullptr, ids, n, g, y, gw, gb, workspace, deferred, ndeferred, stream);
+}
+
+static int conv1_relu_wgrad(const rth_conv_shape *shape, const void *x, const int64_t *rows, const int32_t *fids,
+                            int64_t n, const float *g, const float *y, float *gw, float *gb, void *workspace,
+                            const rth_bias_deferred *deferred, int32_t ndeferred, void *stream) {
   RTH_REQUIRE(shape && x && g && y && gw && gb && workspace && n >= 0, "rth_conv_relu_wgrad: NULL argument");
   RTH_REQUIRE(ndeferred >= 0 && ndeferred <= kBiasJobsMax && (ndeferred == 0 || deferred),
               "rth_conv_relu_wgrad_ex: %d deferred bias gradients (at most %d)", ndeferred, kBiasJobsMax);
@@ -2191,12 +2237,14 @@ int rth_conv_relu_wgrad_ex(const rth_conv_shape *shape, const void *x, const int
     const char *e = getenv("RTH_CONV1_F32");
     return e && atoi(e) != 0;
   }();
+  RTH_REQUIRE(!(f32 && fids), "rth_conv1_frames_relu_wgrad_ex: not built for the fp32-MFMA kernel (RTH_CONV1_F32)");
   if (f32)
     hipLaunchKernelGGL((k_conv_wgrad_u8<8, 8, 4, 4, 32, 84, 84>), dim3(kWgBlocks), dim3(kWgWaves * 64), 0,
                        as_stream(stream), static_cast<const uint8_t *>(x), rows, n, g, y, part);
   else
-    hipLaunchKernelGGL(rows ? k_conv1_wgrad_bf16x3<true> : k_conv1_wgrad_bf16x3<false>, dim3(kWgBlocks),
-                       dim3(kWgWaves * 64), 0, as_stream(stream), static_cast<const uint8_t *>(x), rows, n, g, y, part);
+    hipLaunchKernelGGL(fids ? k_conv1_wgrad_bf16x3<2> : (rows ? k_conv1_wgrad_bf16x3<1> : k_conv1_wgrad_bf16x3<0>),
+                       dim3(kWgBlocks), dim3(kWgWaves * 64), 0, as_stream(stream), static_cast<const uint8_t *>(x),
+                       fids ? reinterpret_cast<const int64_t *>(fids) : rows, n, g, y, part);
   RTH_LAUNCHED();
   static const bool wide = [] {  // opt-in: 0.565-0.566 vs 0.563-0.564 ms/step in the loop (r04)
     const char *e = getenv("RTH_WGRED_WIDE");
@@ -2241,7 +2289,8 @@ static void select_launch(ConvLaunch *l, int64_t n, int64_t *w_off, int64_t *nsa
 }
 
 static int conv_bias_relu(const rth_conv_shape *shape, const void *x, const int64_t *rows, int64_t n,
-                          const int64_t *n_dev, const float *w, const float *bias, float *y, void *stream) {
+                          const int64_t *n_dev, const float *w, const float *bias, float *y, void *stream,
+                          const int32_t *fids = nullptr) {
   RTH_REQUIRE(shape && x && w && bias && y && n >= 0, "rth_conv_bias_relu: NULL argument");
   ConvLaunch l;
   RTH_REQUIRE(find_conv(*shape, &l),
@@ -2288,11 +2337,13 @@ static int conv_bias_relu(const rth_conv_shape *shape, const void *x, const int6
     grid = grid / ns * ns;
     if (grid < ns) grid = ns;
   }
+  RTH_REQUIRE(!fids || (l.bf16x3 == 2 && !rows), "rth_conv1_frames_bias_relu: needs k_conv1_u8_share (not RTH_CONV1_NOSHARE)");
   void *args[] = {(void *)&x, (void *)&rows, (void *)&n, (void *)&n_dev, (void *)&w, (void *)&bias, (void *)&y,
-                  (void *)&out_nchw};  // (k_conv1_u8_bf16x3 takes the first seven)
+                  l.bf16x3 == 2 ? (void *)&fids : (void *)&out_nchw};  // (k_conv1_u8_bf16x3 takes the first seven)
   // whole rounds of pixel tiles over one wave slot per SIMD (the kernel's own split rule)
   const bool ts = l.tsfn && l.waves % 4 == 0 && tiles / (grid * 4) >= l.tsfn_rounds;
-  RTH_HIP(hipLaunchKernel(ts ? l.tsfn : l.fn, dim3((unsigned)grid), dim3(l.waves * 64), args, 0, as_stream(stream)));
+  const void *fn = fids ? reinterpret_cast<const void *>(&k_conv1_u8_share<true>) : (ts ? l.tsfn : l.fn);
+  RTH_HIP(hipLaunchKernel(fn, dim3((unsigned)grid), dim3(l.waves * 64), args, 0, as_stream(stream)));
   return RTH_OK;
 }
 
@@ -2402,6 +2453,15 @@ int rth_conv_dgrad_ws(const rth_conv_shape *shape, const float *gy, int64_t n, c
 int rth_conv_bias_relu(const rth_conv_shape *shape, const void *x, const int64_t *rows, int64_t n, const float *w,
                        const float *bias, float *y, void *stream) {
   return conv_bias_relu(shape, x, rows, n, nullptr, w, bias, y, stream);
+}
+
+int rth_conv1_frames_bias_relu(const rth_conv_shape *shape, const uint8_t *store, const int32_t *ids, int64_t n,
+                               const float *w, const float *bias, float *y, void *stream) {
+  RTH_REQUIRE(store && ids && (reinterpret_cast<uintptr_t>(ids) & 15) == 0,
+              "rth_conv1_frames_bias_relu: NULL / misaligned frame store or ids");
+  RTH_REQUIRE(shape && is_conv1_u8(shape) && !(shape->input & RTH_CONV_OUT_NCHW),
+              "rth_conv1_frames_bias_relu: only the uint8 conv1 geometry (4x84x84 -> 32, k8 s4) is built");
+  return conv_bias_relu(shape, store, nullptr, n, nullptr, w, bias, y, stream, ids);
 }
 
 int rth_conv_bias_relu_upto(const rth_conv_shape *shape, const void *x, const int64_t *rows, int64_t n_max,

@@ -590,6 +590,9 @@ struct rth_replay {
   uint8_t *fstore;
   int64_t fcap, frame_bytes;
   int64_t *fhead;  // device: frames pushed so far (the next frame id)
+  // rth_replay_frames_ids_out: gathers write the frame-stack columns' stored id tuples (int32
+  // [n][stack]) instead of assembling the stacks; the conv1 kernels read the frames in place
+  int32_t ids_out;
   // rth_replay_set_timing: one-shot events recorded around the next launches of each kind
   hipEvent_t timing[RTH_TIMING_SLOTS];
   int32_t timing_fired;  // bit k: slot k's event was recorded since the last arm
@@ -832,6 +835,16 @@ int rth_replay_frames_attach(rth_replay *h, int64_t n_frames, int64_t frame_byte
   return RTH_OK;
 }
 
+int rth_replay_frames_ids_out(rth_replay *h, int32_t on) {
+  RTH_REQUIRE(h && h->fstore, "rth_replay_frames_ids_out: no frame store attached");
+  bool stacks4 = true;
+  for (int c = 0; c < h->ncols; ++c)
+    if (h->desc[c].in_dtype == RTH_FRAMES) stacks4 = stacks4 && h->desc[c].out_planes == 4;
+  RTH_REQUIRE(!on || stacks4, "rth_replay_frames_ids_out: id tuples are read as int4 (4-frame stacks only)");
+  h->ids_out = on ? 1 : 0;
+  return RTH_OK;
+}
+
 int rth_replay_push_frames(rth_replay *h, const uint8_t *ring, int64_t n, int32_t ring_slots, int32_t stack,
                            const int64_t *s0_h, const int64_t *s1_h, const float *done, const int64_t *cur_slot,
                            int32_t *sid, int32_t mode, void *stream) {
@@ -938,6 +951,13 @@ static int gather_impl(rth_replay *h, const int64_t *idx, int64_t n, void *const
   for (int c = 0; n > 0 && c < h->ncols; ++c) {
     RTH_REQUIRE(out_cols[c], "rth_replay_gather: output column %d is NULL", c);
     const rth_col_desc &d = h->desc[c];
+    if (d.in_dtype == RTH_FRAMES && h->ids_out) {  // the stored id tuples (one lane per 4-byte word)
+      RTH_REQUIRE((reinterpret_cast<uintptr_t>(out_cols[c]) & 15) == 0, "rth_replay_gather: frame-id column %d not "
+                  "16-byte aligned", c);
+      const int64_t sb = stored_row_bytes(d);
+      a.col[c] = CopyCol{h->store[c], (uint8_t *)out_cols[c], idx, nullptr, sb, sb, sb, CONV_COPY, 0};
+      continue;
+    }
     if (d.in_dtype == RTH_FRAMES) {  // the stack assembled from the frame store
       RTH_REQUIRE(h->fstore, "rth_replay_gather: frame-stack column %d without a frame store", c);
       const int64_t ob = d.row_elems;

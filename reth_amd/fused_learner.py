@@ -30,6 +30,7 @@ import torch
 from . import _lib
 from ._lib import call, ctypes, ptr, stream_ptr
 from .model import fc1_relu, nchw_out
+from .replay import FrameStacks
 
 
 TD_HB_MAX = 16384  # rth_td_heads_backward keeps B * (A + 1) TD gradient rows in LDS
@@ -79,6 +80,10 @@ def eligible(net, s0, s1):
     rth_conv_bias_relu, on uint8 stacks or f32 channels-last observations"""
     if not (getattr(net, "dueling", False) and getattr(net, "hwc_features", False) and getattr(net, "hip_conv", False)):
         return False
+    frames = isinstance(s0, FrameStacks), isinstance(s1, FrameStacks)
+    if any(frames):  # frames in place: conv1 reads the frame store by the batch's frame ids
+        return all(frames) and s0.shape == s1.shape and all(
+            sh is not None for _, sh in net._torso_shapes(tuple(s0.shape[1:]), True))
     if not (torch.is_tensor(s0) and torch.is_tensor(s1) and s0.is_cuda and s1.is_cuda and s0.dtype == s1.dtype):
         return False
     if s0.dtype not in (torch.uint8, torch.float32) or s0.shape != s1.shape or s0.dim() != 4:
@@ -125,8 +130,12 @@ def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None, mid=No
     net = solver.q_network
     B = s0.shape[0]
     u8 = s0.dtype == torch.uint8
+    frames = isinstance(s0, FrameStacks)  # conv1 (forward, weight gradient) reads the frame store
     pair = bool(solver.double_q)
-    x = _pair(s0, s1) if pair else (s0 if u8 else _nhwc(s0))
+    if frames:
+        x = FrameStacks.pair(s0, s1) if pair else s0
+    else:
+        x = _pair(s0, s1) if pair else (s0 if u8 else _nhwc(s0))
     n = x.shape[0]
     convs = net._convs()
     shapes = [sh for _, sh in net._torso_shapes(tuple(s0.shape[1:]), u8)]
@@ -159,7 +168,12 @@ def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None, mid=No
                             memory_format=torch.contiguous_format if last else torch.channels_last)
             def launch(shape=nchw_out(shape) if last else shape, h=h, pk=net._packed_for(packed, li, u8),
                        b=conv.bias, y=y):
-                call("rth_conv_bias_relu", ctypes.byref(shape), ptr(h), None, n, ptr(pk), ptr(b), ptr(y), stream_ptr())
+                if isinstance(h, FrameStacks):
+                    call("rth_conv1_frames_bias_relu", ctypes.byref(shape), ptr(h.store), ptr(h.ids), n, ptr(pk),
+                         ptr(b), ptr(y), stream_ptr())
+                else:
+                    call("rth_conv_bias_relu", ctypes.byref(shape), ptr(h), None, n, ptr(pk), ptr(b), ptr(y),
+                         stream_ptr())
 
             if probe is not None and li in (1, 2):
                 probed.append((f"conv{li + 1}", launch))
@@ -232,9 +246,13 @@ def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None, mid=No
                 db = torch.empty(conv.out_channels, dtype=torch.float32, device=x.device)
                 assert len(deferred) <= 4, "rth_conv_relu_wgrad_ex finishes at most 4 deferred bias gradients"
                 jobs = (_lib.BiasDeferred * max(len(deferred), 1))(*deferred)
-                call("rth_conv_relu_wgrad_ex", ctypes.byref(shapes[0]), ptr(x), None, B, ptr(_nhwc(g)), ptr(y),
-                     ptr(gw), ptr(db), ptr(_net_workspace(net, "conv1", shapes[0], x.device)), jobs, len(deferred),
-                     st)
+                ws1 = _net_workspace(net, "conv1", shapes[0], x.device)
+                if frames:
+                    call("rth_conv1_frames_relu_wgrad_ex", ctypes.byref(shapes[0]), ptr(x.store), ptr(x.ids), B,
+                         ptr(_nhwc(g)), ptr(y), ptr(gw), ptr(db), ptr(ws1), jobs, len(deferred), st)
+                else:
+                    call("rth_conv_relu_wgrad_ex", ctypes.byref(shapes[0]), ptr(x), None, B, ptr(_nhwc(g)), ptr(y),
+                         ptr(gw), ptr(db), ptr(ws1), jobs, len(deferred), st)
                 grads[conv.weight], grads[conv.bias] = gw, db
                 deferred = []  # consumed
                 break

@@ -314,7 +314,11 @@ class DQNNetwork(nn.Module):
         output NCHW (FC1 reads the reference's (C, H, W) flatten order); backward:
         rth_relu_bias_grad(_nchw) and MIOpen's data/weight gradients"""
         from . import _lib
+        from .replay import FrameStacks
 
+        if isinstance(x, FrameStacks) and (rows is not None or n_dev is not None or (
+                torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()))):
+            x = x.stacks()  # (frames in place is inference / the explicit learner pass only)
         u8 = x.dtype == torch.uint8
         if not u8 and not x.is_contiguous(memory_format=torch.channels_last):
             x = x.contiguous(memory_format=torch.channels_last)
@@ -347,6 +351,18 @@ class DQNNetwork(nn.Module):
             return x
         for li, (conv, ws) in enumerate(zip(convs, self._ws)):
             shape = shapes[li][1]
+            if isinstance(x, FrameStacks):  # conv1 from the frame store (no autograd: checked above)
+                from ._lib import call, ptr, stream_ptr
+
+                if shape is None:
+                    raise ValueError("frame-id batches need rth_conv_bias_relu's conv1 geometry")
+                y = torch.empty((x.shape[0], shape.cout, (shape.hin - shape.kh) // shape.stride + 1,
+                                 (shape.win - shape.kw) // shape.stride + 1), dtype=torch.float32, device=x.device,
+                                memory_format=torch.channels_last)
+                call("rth_conv1_frames_bias_relu", _lib.ctypes.byref(shape), ptr(x.store), ptr(x.ids), x.shape[0],
+                     ptr(self._packed_for(packed, li, u8)), ptr(conv.bias), ptr(y), stream_ptr())
+                x = y
+                continue
             if shape is not None:
                 pk = self._packed_for(packed, li, u8)
                 last = li == len(convs) - 1 and li > 0  # the last conv writes NCHW (FC1's flatten order)

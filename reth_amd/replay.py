@@ -222,6 +222,50 @@ class FrameColumn(Column):
         return ColDesc(self.row_elems, _lib.RTH_FRAMES, _lib.RTH_U8, self.out_planes, 0)
 
 
+class FrameStacks:
+    """a batch of uint8 frame stacks [n, K, H, W] held as their int32 [n, K] frame ids into a
+    replay's frame store (HbmReplay.set_frame_ids: the gather copies the ids, not the stacks);
+    conv1 reads the frames in place (rth_conv1_frames_bias_relu / _relu_wgrad_ex), with
+    results bit-identical to the same launches on the stacks() the gather would have written"""
+
+    dtype = torch.uint8
+    is_cuda = True
+
+    def __init__(self, ids, store):
+        self.ids, self.store = ids, store  # store: the replay's frames [F, H, W] (uint8)
+        self.shape = torch.Size((ids.shape[0], ids.shape[1], *store.shape[1:]))
+
+    @property
+    def device(self):
+        return self.ids.device
+
+    def data_ptr(self):
+        return self.ids.data_ptr()
+
+    def dim(self):
+        return 4
+
+    def __len__(self):
+        return self.shape[0]
+
+    def __getitem__(self, rows):
+        if not isinstance(rows, slice):
+            raise TypeError("FrameStacks rows are taken by slice")
+        return FrameStacks(self.ids[rows], self.store)
+
+    def stacks(self):
+        """the uint8 stacks themselves [n, K, H, W] (a torch gather; not on the hot path)"""
+        return self.store[self.ids.long()]
+
+    @staticmethod
+    def pair(a, b):
+        """[a; b]: a view when b's ids sit right behind a's (HbmReplay.new_batch), else a copy"""
+        if a.store is b.store and a.ids.is_contiguous() and b.ids.is_contiguous() and \
+                b.ids.data_ptr() == a.ids.data_ptr() + a.ids.numel() * 4:
+            return FrameStacks(torch.as_strided(a.ids, (2 * a.ids.shape[0], a.ids.shape[1]), a.ids.stride()), a.store)
+        return FrameStacks(torch.cat([a.ids, b.ids]), a.store)
+
+
 SAMPLERS = {"per": _lib.SAMPLER_PER, "uniform": _lib.SAMPLER_UNIFORM, "fifo": _lib.SAMPLER_FIFO}
 
 
@@ -408,16 +452,28 @@ class HbmReplay:
         call("rth_replay_gather", self._h, ptr(idx_out), batch_size, arr, s)
         ev1.record()
 
+    def set_frame_ids(self, on=True):
+        """frames in place: gathers write the frame-stack columns' frame ids (FrameStacks
+        batches from new_batch) instead of the assembled stacks (rth_replay_frames_ids_out)"""
+        call("rth_replay_frames_ids_out", self._h, 1 if on else 0)
+        self.frame_ids = bool(on)
+
     def new_batch(self, batch_size):
         """empty (cols, idx, isw) batch buffers.  Columns of identical row shape and sampled
         dtype share one allocation, back to back in column order (s1 directly behind s0), so
-        a learner can run one forward over [s0; s1] without a copy (fused_learner._pair)"""
+        a learner can run one forward over [s0; s1] without a copy (fused_learner._pair);
+        with set_frame_ids, frame-stack columns are FrameStacks over one id allocation"""
         groups = {}
         for i, c in enumerate(self.columns):
             groups.setdefault((c.shape, c.out_dtype, c.channels_last), []).append(i)
         cols = [None] * len(self.columns)
         for members in groups.values():
             c = self.columns[members[0]]
+            if getattr(self, "frame_ids", False) and getattr(c, "frames", False):
+                ids = torch.empty((len(members) * batch_size, c.shape[0]), dtype=torch.int32, device=self.device)
+                for k, i in enumerate(members):
+                    cols[i] = FrameStacks(ids[k * batch_size:(k + 1) * batch_size], self.frames)
+                continue
             buf = c.empty_out(len(members) * batch_size, self.device)
             for k, i in enumerate(members):
                 cols[i] = buf[k * batch_size:(k + 1) * batch_size]
@@ -433,7 +489,8 @@ class HbmReplay:
     def gather(self, indices, out_cols=None):
         idx = as_device(indices, torch.int64, self.device)
         if out_cols is None:
-            out_cols = [c.empty_out(idx.numel(), self.device) for c in self.columns]
+            out_cols = (self.new_batch(idx.numel())[0] if getattr(self, "frame_ids", False)
+                        else [c.empty_out(idx.numel(), self.device) for c in self.columns])
         arr = (c_vp * len(out_cols))(*[ptr(t) for t in out_cols])
         call("rth_replay_gather", self._h, ptr(idx), idx.numel(), arr, stream_ptr())
         return out_cols

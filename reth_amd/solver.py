@@ -19,6 +19,7 @@ from . import _lib, fused_learner
 from ._lib import call, ptr, stream_ptr
 from .model import default_models
 from .optim import ClipAdam
+from .replay import FrameStacks
 from .schedule import Interval
 
 
@@ -211,7 +212,8 @@ class DQNSolver(Algorithm):
 
     def _u8_frames(self, x):
         net = self.q_network
-        return (torch.is_tensor(x) and x.dtype == torch.uint8 and x.is_cuda and self._heads
+        return ((torch.is_tensor(x) or isinstance(x, FrameStacks)) and x.dtype == torch.uint8 and x.is_cuda
+                and self._heads
                 and getattr(net, "hwc_features", False) and getattr(net, "hip_conv", False))
 
     def target_heads(self, s1):

@@ -205,6 +205,12 @@ PY
             --no-sweep
       done
       summ gpurun_out/fadvab_*.log ;;
+    fidab)  # frames in place (batches as frame ids, conv1 reads the store) vs the gather's stacks
+      for r in 1 2 3; do
+        step fidab_stacks_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        RTH_FRAME_IDS=1 step fidab_ids_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+      done
+      summ gpurun_out/fidab_*.log ;;
     # nostk (the gather without its stack assembly, RTH_DIAG_NO_STACKS=1, a timing-only build of
     # commit 'Diagnostic: RTH_DIAG_NO_STACKS=1'): profiles/r05/ab_log.txt
     dp8)  # 8 ranks on one GPU over gloo: bench.py's multi-rank path and its teardown (shutdown())

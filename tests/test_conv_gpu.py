@@ -759,3 +759,53 @@ def test_conv2_schedules_bit_identical(tmp_path, dev):
     for sched, r in res.items():
         for k in base:
             assert torch.equal(torch.nan_to_num(r[k], nan=-1.0), torch.nan_to_num(base[k], nan=-1.0)), (sched, k)
+
+
+@pytest.mark.parametrize("n", [1, 7, 512, 1024])
+def test_conv1_frames_in_place_bit_identical(dev, n):
+    """frames in place (rth_conv1_frames_bias_relu / rth_conv1_frames_relu_wgrad_ex): conv1
+    reading each sample's 4 frames from a frame store by int32 [n][4] frame ids gives the same
+    bits as rth_conv_bias_relu / rth_conv_relu_wgrad_ex on the stacks the gather would have
+    assembled from those ids (repeated and out-of-order ids, the store's last frame included)"""
+    from reth_amd import _lib
+
+    g = torch.Generator().manual_seed(300 + n)
+    F_ = 97
+    store = torch.randint(0, 256, (F_, 84, 84), dtype=torch.uint8, generator=g).to(dev)
+    ids = torch.randint(0, F_, (n, 4), dtype=torch.int32, generator=g)
+    ids[0] = torch.tensor([F_ - 1, 0, F_ - 1, 5], dtype=torch.int32)
+    ids = ids.to(dev)
+    stacks = store[ids.long()].contiguous()  # [n, 4, 84, 84]: the gather's output
+    w = (torch.rand((32, 4, 8, 8), generator=g) * 2 - 1) / 16
+    b = ((torch.rand(32, generator=g) * 2 - 1) * 0.1).to(dev)
+    shape = _shape(_lib.CONV_U8_CHW, *GEOMS[0])
+    pk = torch.empty(_lib.lib().rth_conv_packed_bytes(_lib.ctypes.byref(shape)) // 4, device=dev)
+    _lib.call("rth_conv_pack", _lib.ctypes.byref(shape), w.to(dev).contiguous(memory_format=torch.channels_last)
+              .data_ptr(), pk.data_ptr(), _lib.stream_ptr())
+    y_st = torch.full((n, 20, 20, 32), float("nan"), device=dev)
+    y_fr = torch.full((n, 20, 20, 32), float("nan"), device=dev)
+    _lib.call("rth_conv_bias_relu", _lib.ctypes.byref(shape), stacks.data_ptr(), None, n, pk.data_ptr(), b.data_ptr(),
+              y_st.data_ptr(), _lib.stream_ptr())
+    _lib.call("rth_conv1_frames_bias_relu", _lib.ctypes.byref(shape), store.data_ptr(), ids.data_ptr(), n,
+              pk.data_ptr(), b.data_ptr(), y_fr.data_ptr(), _lib.stream_ptr())
+    assert not torch.isnan(y_fr).any()
+    assert torch.equal(y_st, y_fr)
+    torch.testing.assert_close(y_fr.permute(0, 3, 1, 2).cpu().double(), _ref(stacks.cpu().double(), w, b.cpu(), 4),
+                               rtol=1e-5, atol=5e-4)
+    # the weight / bias gradients (ReLU mask from y) from the frames == from the stacks
+    up = torch.randn((n, 20, 20, 32), generator=g).to(dev)
+    ws = torch.empty(_lib.lib().rth_conv_wgrad_workspace(_lib.ctypes.byref(shape)) // 4, device=dev)
+    out = []
+    for fn, x, ix in (("rth_conv_relu_wgrad_ex", stacks, None), ("rth_conv1_frames_relu_wgrad_ex", store, ids)):
+        gw = torch.full((32, 8, 8, 4), float("nan"), device=dev)
+        gb = torch.full((32,), float("nan"), device=dev)
+        args = [x.data_ptr(), None] if ix is None else [x.data_ptr(), ix.data_ptr()]
+        _lib.call(fn, _lib.ctypes.byref(shape), *args, n, up.data_ptr(), y_st.data_ptr(), gw.data_ptr(), gb.data_ptr(),
+                  ws.data_ptr(), None, 0, _lib.stream_ptr())
+        out.append((gw, gb))
+    assert not torch.isnan(out[1][0]).any()
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+    # misaligned ids are refused
+    with pytest.raises(RuntimeError):
+        _lib.call("rth_conv1_frames_bias_relu", _lib.ctypes.byref(shape), store.data_ptr(), ids.data_ptr() + 4, 1,
+                  pk.data_ptr(), b.data_ptr(), y_fr.data_ptr(), _lib.stream_ptr())

@@ -24,12 +24,13 @@ def _deterministic_learner(monkeypatch):
     monkeypatch.setattr(fused_learner, "HIP_WGRAD", "x9")
 
 
-def _run(dev, frame_store, graph, iters=150, env="synthetic", bound="hard"):
+def _run(dev, frame_store, graph, iters=150, env="synthetic", bound="hard", frame_ids=False):
     from reth_amd.apex import ApexConfig, ApexDQN
+    from reth_amd.replay import FrameStacks
 
     cfg = ApexConfig(n_actors=16, capacity=1024, batch_size=32, sample_start=64, p_done=0.25, seed=6,
                      hip_graph=graph, send_weights_interval=3, recv_weights_interval=4, update_target_interval=5,
-                     frame_store=frame_store, env=env, frame_store_bound=bound)
+                     frame_store=frame_store, env=env, frame_store_bound=bound, frame_ids=frame_ids)
     ax = ApexDQN(cfg, device=dev)
     for _ in range(iters):
         ax.iteration()
@@ -39,6 +40,8 @@ def _run(dev, frame_store, graph, iters=150, env="synthetic", bound="hard"):
     size = rep.info()[0]
     s, m, v = rep.tree.export()
     cols = rep.gather(torch.arange(size, device=dev))
+    assert all(isinstance(c, FrameStacks) == (frame_ids and k in (0, 3)) for k, c in enumerate(cols))
+    cols = [c.stacks() if isinstance(c, FrameStacks) else c for c in cols]
     params = torch.cat([p.detach().flatten() for p in ax.solver._params]).cpu()
     out = dict(tree=[s.cpu(), m.cpu(), v.cpu()], cols=[c.cpu() for c in cols], params=params, info=rep.info(),
                frames=ax.actors.frames.cpu(), updates=ax.updates)
@@ -68,6 +71,19 @@ def test_frame_store_loop_bit_identical_to_full_rows(dev, graph, bound):
     assert torch.equal(full["params"], fs["params"])  # the learner saw the same batches
     done = fs["cols"][4].numpy() != 0
     assert done.any() and (~done).any()
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_frame_ids_loop_bit_identical(dev, graph):
+    """frames in place (ApexConfig.frame_ids): the learner's batches are frame ids and conv1
+    (forward, weight gradient, the target network's forward) reads the frames from the store --
+    every update bit-identical to the loop whose gather assembles the stacks"""
+    fs = _run(dev, True, graph, iters=150)
+    fi = _run(dev, True, graph, iters=150, frame_ids=True)
+    assert fs["info"] == fi["info"] and fs["updates"] == fi["updates"] > 50
+    for x, y in zip(fs["cols"], fi["cols"]):
+        assert torch.equal(x, y)
+    assert torch.equal(fs["params"], fi["params"])
 
 
 def test_frame_store_atari_env(dev):

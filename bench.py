@@ -479,7 +479,8 @@ def hbm_bytes(cfg, n_rows_per_append):
         "k_tree_sample": B * (D * 16 + 8 + 8 + 8),
         # read + write of every sampled row (uint8 stacks, the HIP torso reads them as they are)
         # + the 5 index reads
-        "k_copy_rows (gather)": B * (gather_bytes_per_row(True, True) if cfg.frame_store and cfg.frame_ids else
+        "k_copy_rows (gather)": B * (gather_bytes_per_row(True, True) if cfg.frame_store and cfg.frame_ids and
+                                     cfg.hip_conv and cfg.channels_last else
                                      2 * row + 5 * 8 + (2 * 4 * 4 if cfg.frame_store else 0)),
         # the append's rows: each column row read from the actors' ring and written to its slot
         # (frame store: the two stacks' frame ids instead of the stacks)
@@ -626,7 +627,8 @@ def main():
     ap.add_argument("--frame-store", action="store_true", default=True,
                     help="frame de-duplicated replay (SURVEY §8(d) C3; the default since r04): each actor frame "
                          "stored once in an HBM frame store, rows keep their stacks as frame ids, the gather "
-                         "assembles them -- bit-identical rows and updates (tests/test_frame_store_gpu.py), Pong's 1 M "
+                         "copies the ids and conv1 reads the frames in place (RTH_FRAME_IDS=0: the gather assembles "
+                         "the stacks) -- bit-identical rows and updates (tests/test_frame_store_gpu.py), Pong's 1 M "
                          "rows in 14.1 GB instead of 56.5 (hard bound), Breakout's 4 M in 56.7 instead of 225.9, and no "
                          "56 KB stack copies per inserted row (Pong 0.563-0.564 vs 0.571-0.574 ms/step interleaved)")
     ap.add_argument("--frame-store-bound", choices=["hard", "expected"], default="hard",
@@ -692,7 +694,7 @@ def main():
                      channels_last=not args.nchw, conv_benchmark=not args.no_conv_benchmark,
                      hip_graph=not args.eager, hip_conv=hip_conv, env=args.env, frame_store=args.frame_store,
                      frame_store_bound=args.frame_store_bound,
-                     frame_ids=args.frame_store and os.environ.get("RTH_FRAME_IDS", "0") == "1", extra={"learner_priority": int(os.environ.get("RTH_LEARNER_PRIORITY", "0")),
+                     frame_ids=args.frame_store and os.environ.get("RTH_FRAME_IDS", "1") == "1", extra={"learner_priority": int(os.environ.get("RTH_LEARNER_PRIORITY", "0")),
                             "probe_conv2": probe})
     ax = ApexDQN(cfg, device=dev, rank=rank, world=world)
     ax.prefill(cfg.capacity)

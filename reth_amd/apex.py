@@ -103,7 +103,7 @@ class ApexConfig:
     env: str = "synthetic"         # actors' observations: synthetic | atari | atari-h2d (VecActors)
     frame_store: bool = False      # frame de-duplicated replay: each frame stored once, rows as frame ids
     frame_store_bound: str = "hard"  # store size: "hard" (worst case, 2 frames per actor step) | "expected" (p_done)
-    frame_ids: bool = False        # frame store: batches hold frame ids, conv1 reads the frames in place (no stacks)
+    frame_ids: bool = True         # frame store: batches hold frame ids, conv1 reads the frames in place (no stacks)
     extra: dict = field(default_factory=dict)
 
 

@@ -572,7 +572,15 @@ __global__ __launch_bounds__(256) void k_conv1_u8_share(const void *__restrict__
     if constexpr (FRM) {
       int b, oy, ox;
       vpix(t, b, oy, ox);
-      const int4 id = reinterpret_cast<const int4 *>(fids)[b];
+      // a tile's 32 virtual pixels span at most two samples (420 per sample): their id tuples
+      // are wave-uniform scalar loads (lgkmcnt: a vector load here would be the newest in the
+      // vmcnt queue, and waiting for it would drain the ring of tiles in flight)
+      const int tu = __builtin_amdgcn_readfirstlane(t);
+      const int v0 = tu * kC1VPerTile, v1 = v0 + kC1VPerTile - 1 < VP ? v0 + kC1VPerTile - 1 : VP - 1;
+      const int b0 = (int)((unsigned)v0 / (unsigned)VPS), b1 = (int)((unsigned)v1 / (unsigned)VPS);
+      const int4 i0 = reinterpret_cast<const int4 *>(fids)[b0], i1 = reinterpret_cast<const int4 *>(fids)[b1];
+      const bool second = b != b0;
+      const int4 id = {second ? i1.x : i0.x, second ? i1.y : i0.y, second ? i1.z : i0.z, second ? i1.w : i0.w};
       const int off = (S * oy) * WIN + S * ox;
       const uint8_t *fb[4] = {xb + (int64_t)id.x * kC1FrameBytes + off, xb + (int64_t)id.y * kC1FrameBytes + off,
                               xb + (int64_t)id.z * kC1FrameBytes + off, xb + (int64_t)id.w * kC1FrameBytes + off};
@@ -1694,7 +1702,11 @@ __global__ __launch_bounds__(kWgWaves * 64) void k_conv1_wgrad_bf16x3(const uint
     rw.nv = live && 2 * gi + h < NS ? (seg == 2 ? 4 : 8) : 0;
     const uint8_t *src;
     if constexpr (MODE == 2) {  // run (ci, kh) = (o / KH, o % KH) from frame ids[b][ci]
-      const int64_t fid = reinterpret_cast<const int32_t *>(rows)[b * 4 + o / KH];
+      // the two slots' id tuples as wave-uniform scalar loads (not in the vmcnt queue)
+      const int4 i0 = reinterpret_cast<const int4 *>(rows)[b0], i1 = reinterpret_cast<const int4 *>(rows)[b1];
+      const int4 iv = h ? i1 : i0;
+      const int ci = o / KH;
+      const int64_t fid = ci == 0 ? iv.x : ci == 1 ? iv.y : ci == 2 ? iv.z : iv.w;
       src = x + fid * (int64_t)(HIN * WIN) + (o % KH) * WIN + (S * oy) * WIN + S * 8 * seg;
     } else {
       src = x + row * (int64_t)STACK + row_off + (S * oy) * WIN + S * 8 * seg;

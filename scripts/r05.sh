@@ -207,7 +207,7 @@ PY
       summ gpurun_out/fadvab_*.log ;;
     fidab)  # frames in place (batches as frame ids, conv1 reads the store) vs the gather's stacks
       for r in 1 2 3; do
-        step fidab_stacks_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        RTH_FRAME_IDS=0 step fidab_stacks_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
         RTH_FRAME_IDS=1 step fidab_ids_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
       done
       summ gpurun_out/fidab_*.log ;;

@@ -114,6 +114,7 @@ def test_frame_store_prefill_and_footprint(dev):
     assert np.array_equal(ids[:, 0], base + np.arange(cfg.capacity))
     rows = torch.tensor([0, 1, 777, cfg.capacity - 1], device=dev)
     s0, _, _, s1, _ = rep.gather(rows)
+    s0, s1 = s0.stacks(), s1.stacks()  # frame_ids (the default): the gather wrote the rows' frame ids
     store = rep.frames
     for k, j in enumerate(rows.tolist()):
         assert torch.equal(s0[k], store[base + j:base + j + 4])

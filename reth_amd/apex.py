@@ -287,7 +287,7 @@ class ApexDQN:
         """one Ape-X iteration, enqueued on this object's own stream (the stream the graphs
         are captured from); callers synchronise with torch.cuda.synchronize()"""
         if not hasattr(self, "_stream"):
-            self._stream = torch.cuda.Stream(self.device)
+            self._stream = torch.cuda.Stream(self.device, priority=self.cfg.extra.get("actor_priority", 0))
             self._stream.wait_stream(torch.cuda.current_stream(self.device))  # init + prefill
         with torch.cuda.stream(self._stream):
             self._iteration()

@@ -211,6 +211,13 @@ PY
         RTH_FRAME_IDS=1 step fidab_ids_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
       done
       summ gpurun_out/fidab_*.log ;;
+    prioab)  # stream priorities: the actor stream high (RTH_ACTOR_PRIORITY=-1) vs both normal
+      for r in 1 2 3; do
+        step prioab_dflt_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        RTH_ACTOR_PRIORITY=-1 step prioab_actor_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline \
+            --no-sweep
+      done
+      summ gpurun_out/prioab_*.log ;;
     # nostk (the gather without its stack assembly, RTH_DIAG_NO_STACKS=1, a timing-only build of
     # commit 'Diagnostic: RTH_DIAG_NO_STACKS=1'): profiles/r05/ab_log.txt
     dp8)  # 8 ranks on one GPU over gloo: bench.py's multi-rank path and its teardown (shutdown())

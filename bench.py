@@ -663,6 +663,8 @@ def main():
     from reth_amd.apex import ApexConfig, ApexDQN
     from reth_amd.dist import init_from_env, shutdown
 
+    if os.environ.get("RTH_CUDNN_DET") == "1":  # A/B aid: MIOpen's deterministic solvers (no atomic wrw + fills)
+        torch.backends.cudnn.deterministic = True
     if os.environ.get("RTH_BLAS"):  # A/B aid: torch's GEMM backend ("cublas" = rocBLAS, "cublaslt" = hipBLASLt)
         torch.backends.cuda.preferred_blas_library(os.environ["RTH_BLAS"])
 

@@ -193,7 +193,7 @@ PY
       summ gpurun_out/cfcab_*.log ;;
     fcx9s)  # Pong: the 512-row FC1 forwards (actors, target pass) on rth_fc_x9 (48 KB of LDS) vs hipBLASLt (80 KB)
       for r in 1 2 3; do
-        step fcx9s_blas_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        RTH_FC=blas step fcx9s_blas_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
         RTH_FC=x9 RTH_FC_MAX_ROWS=512 step fcx9s_x9_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline \
             --no-sweep
       done
@@ -218,6 +218,14 @@ PY
             --no-sweep
       done
       summ gpurun_out/prioab_*.log ;;
+    wgab)  # conv2 / conv3 weight gradients: MIOpen (default) vs its deterministic solvers vs rth_conv_wgrad_x9 / _f32
+      for r in 1 2; do
+        step wgab_dflt_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        RTH_CUDNN_DET=1 step wgab_det_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        RTH_HIP_WGRAD=x9 step wgab_x9_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        RTH_HIP_WGRAD=f32 step wgab_f32_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+      done
+      summ gpurun_out/wgab_*.log ;;
     # nostk (the gather without its stack assembly, RTH_DIAG_NO_STACKS=1, a timing-only build of
     # commit 'Diagnostic: RTH_DIAG_NO_STACKS=1'): profiles/r05/ab_log.txt
     dp8)  # 8 ranks on one GPU over gloo: bench.py's multi-rank path and its teardown (shutdown())

@@ -698,7 +698,6 @@ def main():
                      frame_store_bound=args.frame_store_bound,
                      frame_ids=args.frame_store and os.environ.get("RTH_FRAME_IDS", "1") == "1", extra={"learner_priority": int(os.environ.get("RTH_LEARNER_PRIORITY", "0")),
                             "actor_priority": int(os.environ.get("RTH_ACTOR_PRIORITY", "0")),
-                            "learner_cu_reserve": int(os.environ.get("RTH_LEARNER_CU_RESERVE", "0")),
                             "probe_conv2": probe})
     ax = ApexDQN(cfg, device=dev, rank=rank, world=world)
     ax.prefill(cfg.capacity)

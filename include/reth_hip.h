@@ -68,10 +68,6 @@ int rth_graph_upload(void *graph_exec, void *stream);
  * of a capture and until something is captured), or -1 when the stream is not capturing:
  * ApexDQN's graph cuts skip a part that would be empty (two boundaries back to back). */
 int rth_stream_capture_deps(void *stream);
-/* A/B aid (r05): a stream whose launches may use every CU but the last `reserve` bits of the
- * device's CU mask (hipExtStreamCreateWithCUMask; priority unused), and its destruction. */
-int rth_stream_create_cu_masked(int32_t reserve, int32_t priority, void **stream_out);
-int rth_stream_destroy(void *stream);
 
 /* ------------------------------------------------------------------------------------
  * In-order heap sum-tree, fp64, resident in HBM.

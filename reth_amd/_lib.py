@@ -82,8 +82,6 @@ SIGNATURES = {
     "rth_build_id": (ctypes.c_char_p, []),
     "rth_graph_upload": (c_i32, [c_vp, c_vp]),
     "rth_stream_capture_deps": (c_i32, [c_vp]),
-    "rth_stream_create_cu_masked": (c_i32, [c_i32, c_i32, ctypes.POINTER(c_vp)]),
-    "rth_stream_destroy": (c_i32, [c_vp]),
     # sum-tree
     "rth_sumtree_create": (c_i32, [c_i64, c_i32, ctypes.POINTER(c_vp)]),
     "rth_sumtree_destroy": (c_i32, [c_vp]),

@@ -24,7 +24,6 @@ of the gather are exactly those of the eager schedule.  All per-step scalars the
 need (FIFO tail, Philox counters, beta schedule step, env step) live in device memory, so
 the captured launches are valid on every replay.
 """
-import ctypes
 from dataclasses import dataclass, field
 from typing import Optional
 
@@ -594,17 +593,7 @@ class ApexDQN:
         if not hasattr(self, "_stream_b"):
             # both streams at normal priority: a high-priority learner stream (-1) gives the same
             # step time and a slower in-loop gather (40 vs 33-35 us)
-            reserve = int(self.cfg.extra.get("learner_cu_reserve", 0))
-            if reserve > 0:  # A/B aid: the learner stream kept off `reserve` CUs (the actor stream's alone)
-                from ._lib import c_vp, call
-
-                h = c_vp()
-                with torch.cuda.device(self.device):
-                    call("rth_stream_create_cu_masked", reserve, 0, ctypes.byref(h))
-                self._stream_b = torch.cuda.ExternalStream(h.value, device=self.device)
-                self._stream_b_handle = h.value  # (lives as long as the process: graphs replay on it)
-            else:
-                self._stream_b = torch.cuda.Stream(self.device, priority=self.cfg.extra.get("learner_priority", 0))
+            self._stream_b = torch.cuda.Stream(self.device, priority=self.cfg.extra.get("learner_priority", 0))
             self._ev_learn = torch.cuda.Event()
             self._ev_sample = torch.cuda.Event()
             self._ev_sample.record(A)  # batch k was sampled on A before the first overlapped step

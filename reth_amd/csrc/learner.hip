@@ -88,26 +88,6 @@ int rth_stream_capture_deps(void *stream) {
   return st == hipStreamCaptureStatusActive ? (int)n : -1;
 }
 
-int rth_stream_create_cu_masked(int32_t reserve, int32_t priority, void **stream_out) {
-  int dev = 0, cus = 0;
-  RTH_HIP(hipGetDevice(&dev));
-  RTH_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  RTH_REQUIRE(stream_out && reserve >= 0 && reserve < cus && cus <= 1024,
-              "rth_stream_create_cu_masked: reserve %d of %d CUs", reserve, cus);
-  uint32_t mask[32] = {};
-  for (int c = 0; c < cus - reserve; ++c) mask[c / 32] |= 1u << (c % 32);  // the last `reserve` CU bits cleared
-  hipStream_t s = nullptr;
-  RTH_HIP(hipExtStreamCreateWithCUMask(&s, (uint32_t)((cus + 31) / 32), mask));
-  (void)priority;  // (a CU-masked stream has the default priority)
-  *stream_out = s;
-  return RTH_OK;
-}
-
-int rth_stream_destroy(void *stream) {
-  RTH_HIP(hipStreamDestroy(as_stream(stream)));
-  return RTH_OK;
-}
-
 int rth_td_huber(const float *q0, const float *q1o, const float *q1t, const int64_t *a, const float *r,
                  const float *done, const double *isw, int64_t B, int64_t A, float gamma_n, int32_t double_q,
                  int32_t dueling, float *td_out, float *td_abs_out, float *loss_elem, float *loss_out, float *dq,

@@ -233,14 +233,7 @@ PY
         RTH_CONV2_X9_MAX=600 step c2x9ab_600_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
       done
       summ gpurun_out/c2x9ab_*.log ;;
-    cumab)  # the learner stream kept off the last 8 / 16 CU-mask bits (RTH_LEARNER_CU_RESERVE) vs unmasked
-      for r in 1 2; do
-        step cumab_dflt_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
-        RTH_LEARNER_CU_RESERVE=8 step cumab_8_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
-        RTH_LEARNER_CU_RESERVE=16 step cumab_16_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline \
-            --no-sweep
-      done
-      summ gpurun_out/cumab_*.log ;;
+    # cumab (the learner stream on a CU-masked queue, a knob since removed): profiles/r05/ab_log.txt
     # nostk (the gather without its stack assembly, RTH_DIAG_NO_STACKS=1, a timing-only build of
     # commit 'Diagnostic: RTH_DIAG_NO_STACKS=1'): profiles/r05/ab_log.txt
     dp8)  # 8 ranks on one GPU over gloo: bench.py's multi-rank path and its teardown (shutdown())

@@ -99,12 +99,15 @@ class VecActors:
         self._base = torch.arange(N, device=dev, dtype=torch.int64) * ring
         self.qrows = None
         # dedup forwards with the counted FC: FC1 as a GEMM over the N acting rows only, the
-        # terminal stacks behind them device-counted, instead of one GEMM over all 2N rows.  By
-        # default above 512 actors: at Breakout (2,048 actors, the actor stream critical) 0.905
-        # vs 0.954 ms/step (r04); at Pong no faster (the 256-row GEMM takes as long as the 512-row
-        # one: one round of K-deep tiles either way).  RTH_ACTOR_COUNTED_FC=0 / 1 forces it.
+        # terminal stacks behind them device-counted, instead of one GEMM over all 2N rows.  Above
+        # 512 actors (Breakout: 2,048 actors, the actor stream critical) 0.905 vs 0.954 ms/step
+        # (r04); at Pong since the N-row FC1 runs on rth_fc_x9 (late r05: the hipBLASLt 256-row
+        # GEMM took as long as the 512-row one, the x9 kernel's time follows the rows) 0.534 vs
+        # 0.542-0.544 ms/step.  RTH_ACTOR_COUNTED_FC=0 / 1 forces it.
+        from .model import fc1_on_hip
+
         cfc = os.environ.get("RTH_ACTOR_COUNTED_FC")
-        self._counted_fc = (cfc == "1") if cfc in ("0", "1") else N > 512
+        self._counted_fc = (cfc == "1") if cfc in ("0", "1") else (N > 512 or fc1_on_hip(N))
         # RTH_ACTOR_FC2_CACHE=0: the second layer over all 2N rows and the cache scatter as a
         # launch of its own (the r03 form, for A/B runs)
         self._fc2_cache = os.environ.get("RTH_ACTOR_FC2_CACHE", "1") != "0"

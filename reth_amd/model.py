@@ -441,6 +441,11 @@ _FC_MAX_ROWS = int(os.environ.get("RTH_FC_MAX_ROWS", "0" if os.environ.get("RTH_
 _FC_WS = {}
 
 
+def fc1_on_hip(rows):
+    """whether an FC1 forward of `rows` rows runs on the hand-written rth_fc_{x9,f32} (fc1_relu)"""
+    return _FC_KIND in ("f32", "x9") and (_FC_MAX_ROWS <= 0 or rows <= _FC_MAX_ROWS)
+
+
 def fc1_relu(x, w, b, out=None):
     """relu(x @ w.T + b) (FC1 of both dueling branches): rth_fc_f32 / rth_fc_x9 when selected
     (RTH_FC) and built for the shape, else one hipBLASLt GEMM with the bias+ReLU epilogue.  The

@@ -553,12 +553,9 @@ int rth_conv_dgrad_relu_prepacked(const rth_conv_shape *shape, const float *gy_d
  * row-major with row stride ldx, w row-major [N, K] (the Linear weight as stored), act = ReLU
  * when relu != 0, bias may be NULL; M % 64 == 0, N % 128 == 0, K % 32 == 0
  * (rth_fc_x9_supported).  Fixed-order split-K partials in `workspace` (rth_fc_x9_workspace
- * bytes, NULL when that is 0; ZERO-FILLED before its first use -- its tail holds one ticket per
- * output tile, through which the last split of a tile sums the partials in split order in the
- * same launch, and every call leaves them zero; one workspace per stream): run-to-run
- * deterministic.  Replaces the hipBLASLt GEMM + bias + ReLU epilogue (torch._addmm_activation)
- * of the 512-row forwards (the actors', the target pass's) by default, every FC1 with
- * RTH_FC_X9=1. */
+ * bytes, NULL when that is 0): run-to-run deterministic.  Replaces the hipBLASLt GEMM +
+ * bias + ReLU epilogue (torch._addmm_activation) of the actors', the target pass's and the
+ * learner's forward when enabled (RTH_FC_X9=1). */
 int rth_fc_x9_supported(int64_t M, int64_t N, int64_t K);
 int64_t rth_fc_x9_workspace(int64_t M, int64_t N, int64_t K);
 int rth_fc_x9(const float *x_dev, int64_t ldx, int64_t M, const float *w_dev, int64_t N, int64_t K,

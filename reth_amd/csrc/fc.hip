@@ -36,16 +36,11 @@ __device__ __forceinline__ void static_for(std::integer_sequence<int, I...>, F &
 
 // PF: chunks whose global loads are in flight ahead of the one being computed (register ring of
 // PF + 1 sets; the LDS weight tile stays double-buffered)
-// tickets (splits > 1, r05; nullable -> k_fc_reduce follows): per output tile, the split that
-// finishes last sums the tile's partials in split order (k_fc_reduce's order: bit-identical)
-// and writes y; the partials are agent-scope stores counted in before the ticket, the last
-// split reads them after an agent-scope acquire, and re-arms its tile's ticket
 template <int PF>
 __global__ __launch_bounds__(kFcThreads) void k_fc_x9(const float *__restrict__ x, int64_t ldx, int M,
                                                       const float *__restrict__ w, int N, int K, int splits,
                                                       const float *__restrict__ bias, int relu,
-                                                      float *__restrict__ out, float *__restrict__ y, int64_t ldy,
-                                                      unsigned *__restrict__ tickets) {
+                                                      float *__restrict__ out) {
   __shared__ uint4 bl[2][kFcBUnits];
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, r = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -146,55 +141,12 @@ __global__ __launch_bounds__(kFcThreads) void k_fc_x9(const float *__restrict__ 
         out[(int64_t)(mrow + i) * N + n] = relu ? fc_relu(v) : v;
       }
     }
-  } else if (!tickets) {
-    float *part = out + (int64_t)split * M * N;
-#pragma unroll
-    for (int nb = 0; nb < 8; ++nb)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) part[(int64_t)(mrow + i) * N + n0 + 16 * nb + r] = acc[nb][i];
   } else {
     float *part = out + (int64_t)split * M * N;
 #pragma unroll
     for (int nb = 0; nb < 8; ++nb)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        __hip_atomic_store(part + (int64_t)(mrow + i) * N + n0 + 16 * nb + r, acc[nb][i], __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    __shared__ int last;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this lane's partials have landed
-    __syncthreads();
-    if (tid == 0) {
-      last = __hip_atomic_fetch_add(tickets + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-             (unsigned)(splits - 1);
-      if (last) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-    }
-    __syncthreads();
-    if (!last) return;  // workgroup-uniform
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    // the tile's 64 x 128 outputs as 2,048 float4, 8 per thread; k_fc_reduce's sums
-    const int64_t MN = (int64_t)M * N;
-    for (int q = tid; q < kFcTm * kFcTn / 4; q += kFcThreads) {
-      const int row = m0 + q / (kFcTn / 4), col = n0 + 4 * (q % (kFcTn / 4));
-      const int64_t e = (int64_t)row * N + col;
-      f32x4 sm;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) sm[j] = __hip_atomic_load(out + e + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      for (int k = 1; k < splits; ++k)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          sm[j] = radd(sm[j], __hip_atomic_load(out + k * MN + e + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      f32x4 o;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float v = radd(sm[j], bias ? bias[col + j] : 0.0f);
-        o[j] = relu ? fc_relu(v) : v;
-      }
-      *reinterpret_cast<f32x4 *>(y + (int64_t)row * ldy + col) = o;
-    }
-    if (tid == 0) __hip_atomic_store(tickets + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int i = 0; i < 4; ++i) part[(int64_t)(mrow + i) * N + n0 + 16 * nb + r] = acc[nb][i];
   }
 }
 
@@ -377,23 +329,10 @@ int rth_fc_x9_supported(int64_t M, int64_t N, int64_t K) {
              : 0;
 }
 
-// the split-K reduce in the x9 launch's last split per tile (tickets) unless RTH_FC_REDUCE=1
-// (the separate k_fc_reduce launch, r05's first form: A/B)
-static bool fc_fused_reduce() {
-  static const bool v = [] {
-    const char *e = getenv("RTH_FC_REDUCE");
-    return !(e && atoi(e) == 1);
-  }();
-  return v;
-}
-
-// [splits x M x N partials | one ticket per output tile (zero before the first call; every
-// call leaves them zero)]
 int64_t rth_fc_x9_workspace(int64_t M, int64_t N, int64_t K) {
   if (!rth_fc_x9_supported(M, N, K)) return 0;
   const int s = fc_splits((int)M, (int)N, (int)K);
-  const int64_t tiles = (M / kFcTm) * (N / kFcTn);
-  return s > 1 ? (int64_t)s * M * N * 4 + (tiles * 4 + 255) / 256 * 256 : 0;
+  return s > 1 ? (int64_t)s * M * N * 4 : 0;
 }
 
 int rth_fc_x9(const float *x, int64_t ldx, int64_t M, const float *w, int64_t N, int64_t K, const float *bias,
@@ -415,17 +354,14 @@ int rth_fc_x9(const float *x, int64_t ldx, int64_t M, const float *w, int64_t N,
     const char *e = getenv("RTH_FC_PF");
     return e && atoi(e) == 1 ? 1 : 2;
   }();
-  const bool fused = splits > 1 && fc_fused_reduce();
-  unsigned *tickets = fused ? reinterpret_cast<unsigned *>(static_cast<float *>(workspace) + (int64_t)splits * M * N)
-                            : nullptr;
   if (pf == 1)
     hipLaunchKernelGGL(k_fc_x9<1>, dim3((unsigned)(tiles * splits)), dim3(kFcThreads), 0, s, x, ldx, (int)M, w,
-                       (int)N, (int)K, splits, bias, (int)relu, out, y, N, tickets);
+                       (int)N, (int)K, splits, bias, (int)relu, out);
   else
     hipLaunchKernelGGL(k_fc_x9<2>, dim3((unsigned)(tiles * splits)), dim3(kFcThreads), 0, s, x, ldx, (int)M, w,
-                       (int)N, (int)K, splits, bias, (int)relu, out, y, N, tickets);
+                       (int)N, (int)K, splits, bias, (int)relu, out);
   RTH_LAUNCHED();
-  if (splits > 1 && !fused) {
+  if (splits > 1) {
     const int64_t MN = M * N;
     hipLaunchKernelGGL(k_fc_reduce, dim3((unsigned)((MN / 4 + 255) / 256)), dim3(256), 0, s,
                        static_cast<const float *>(workspace), splits, MN, (int)N, bias, (int)relu, y, N);

@@ -463,8 +463,7 @@ def fc1_relu(x, w, b, out=None):
             key = (x.device, w.data_ptr(), M, N, K, fn)
             ws = _FC_WS.get(key)
             if ws is None:
-                # zero-filled: rth_fc_x9's per-tile tickets live at its end
-                ws = _FC_WS[key] = torch.zeros(max(getattr(lib(), fn + "_workspace")(M, N, K), 16) // 4,
+                ws = _FC_WS[key] = torch.empty(max(getattr(lib(), fn + "_workspace")(M, N, K), 16) // 4,
                                                dtype=torch.float32, device=x.device)
             call(fn, ptr(x), x.stride(0), M, ptr(w), N, K, ptr(b), 1, ptr(y), ptr(ws), stream_ptr())
             return y

@@ -22,7 +22,7 @@ for M in [int(v) for v in os.environ.get("FC_MS", "256,512,1024,2048").split(","
         name = "rth_fc_" + kind
         if not getattr(_lib.lib(), name + "_supported")(M, N, K):
             continue
-        ws = torch.zeros(max(getattr(_lib.lib(), name + "_workspace")(M, N, K), 16) // 4, device=dev)
+        ws = torch.empty(max(getattr(_lib.lib(), name + "_workspace")(M, N, K), 16) // 4, device=dev)
         fns[name] = (lambda nm=name, wsp=ws: _lib.call(nm, x.data_ptr(), K, M, w.data_ptr(), N, K, b.data_ptr(), 1,
                                                         y.data_ptr(), wsp.data_ptr(), _lib.stream_ptr()))
     ref = torch.relu(x.double() @ w.double().t() + b.double())

@@ -234,12 +234,6 @@ PY
       done
       summ gpurun_out/c2x9ab_*.log ;;
     # cumab (the learner stream on a CU-masked queue, a knob since removed): profiles/r05/ab_log.txt
-    fcrab)  # rth_fc_x9's split-K reduce in the launch's last split per tile (default) vs the k_fc_reduce launch
-      for r in 1 2 3; do
-        step fcrab_fused_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
-        RTH_FC_REDUCE=1 step fcrab_launch_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
-      done
-      summ gpurun_out/fcrab_*.log ;;
     # nostk (the gather without its stack assembly, RTH_DIAG_NO_STACKS=1, a timing-only build of
     # commit 'Diagnostic: RTH_DIAG_NO_STACKS=1'): profiles/r05/ab_log.txt
     dp8)  # 8 ranks on one GPU over gloo: bench.py's multi-rank path and its teardown (shutdown())

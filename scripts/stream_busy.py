@@ -18,9 +18,8 @@ for r in rows:
     names[r["Stream_Id"]][r["Kernel_Name"][:70]] += d
 n_it = iters * 0.3 * (span / span)  # window = last 30% of rows ~ 30% of iterations
 per = span / (busy.total() and 1) if False else None
-steps = sum(1 for r in rows if "k_tree_sample" in r["Kernel_Name"])  # one PER sample per step
-print(f"window {span:.0f} us, {steps} steps ({span / max(steps, 1):.1f} us per profiled step)")
+print(f"window {span:.0f} us")
 for s, b in busy.most_common():
-    print(f"stream {s}: busy {b:.0f} us = {b / span:.1%} of the window = {b / max(steps, 1):.1f} us per step")
-    for k, v in names[s].most_common(24):
-        print(f"   {v / span * 100:6.2f}%  {v / max(steps, 1):7.1f} us/step  {k}")
+    print(f"stream {s}: busy {b:.0f} us = {b / span:.1%} of the window")
+    for k, v in names[s].most_common(14):
+        print(f"   {v / span * 100:6.2f}%  {k}")

@@ -560,6 +560,13 @@ int rth_fc_x9_supported(int64_t M, int64_t N, int64_t K);
 int64_t rth_fc_x9_workspace(int64_t M, int64_t N, int64_t K);
 int rth_fc_x9(const float *x_dev, int64_t ldx, int64_t M, const float *w_dev, int64_t N, int64_t K,
               const float *bias_dev, int32_t relu, float *y_dev, void *workspace_dev, void *stream);
+/* The actors' counted FC1 (r05): y [n_max, N] rows [0, M) = rth_fc_x9 (ReLU, M % 64 == 0) and
+ * rows [M, min(*n_dev, n_max)) = rth_linear_relu_rows_upto (the device-counted terminal stacks),
+ * the split-K reduce and the counted rows in one launch; y row stride N; the same bits as
+ * those two calls. */
+int rth_fc_x9_rows_upto(const float *x_dev, int64_t ldx, int64_t M, int64_t n_max, const int64_t *n_dev,
+                        const float *w_dev, int64_t N, int64_t K, const float *bias_dev, float *y_dev,
+                        void *workspace_dev, void *stream);
 /* The same FC1 on the fp32 MFMA with no LDS (r05): the arguments, the workspace protocol and
  * the determinism of rth_fc_x9; any M >= 1 (ragged actor batches), N % 128 == 0, K % 32 == 0
  * (rth_fc_f32_supported).  Selected for the FC1 forwards by RTH_FC=f32. */

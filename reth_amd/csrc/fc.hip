@@ -20,6 +20,7 @@
 #include <utility>
 
 #include "common.hpp"
+#include "fc_rows.hpp"
 
 namespace rth {
 
@@ -266,10 +267,10 @@ __global__ __launch_bounds__(kFfThreads) void k_fc_f32(const float *__restrict__
 }
 
 // y = act(b + sum of the splits' partials, in split order), 4 outputs per thread
-__global__ __launch_bounds__(256) void k_fc_reduce(const float *__restrict__ part, int splits, int64_t MN, int N,
-                                                   const float *__restrict__ bias, int relu, float *__restrict__ y,
-                                                   int64_t ldy) {
-  const int64_t e4 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+__device__ __forceinline__ void fc_reduce_wg(int blk, const float *__restrict__ part, int splits, int64_t MN, int N,
+                                             const float *__restrict__ bias, int relu, float *__restrict__ y,
+                                             int64_t ldy) {
+  const int64_t e4 = ((int64_t)blk * 256 + threadIdx.x) * 4;
   if (e4 >= MN) return;
   f32x4 s = *reinterpret_cast<const f32x4 *>(part + e4);
   for (int k = 1; k < splits; ++k) {
@@ -286,6 +287,28 @@ __global__ __launch_bounds__(256) void k_fc_reduce(const float *__restrict__ par
     o[j] = relu ? fc_relu(v) : v;
   }
   *reinterpret_cast<f32x4 *>(y + m * ldy + n) = o;
+}
+
+__global__ __launch_bounds__(256) void k_fc_reduce(const float *__restrict__ part, int splits, int64_t MN, int N,
+                                                   const float *__restrict__ bias, int relu, float *__restrict__ y,
+                                                   int64_t ldy) {
+  fc_reduce_wg((int)blockIdx.x, part, splits, MN, N, bias, relu, y, ldy);
+}
+
+// r05: k_fc_reduce's workgroups (blocks [0, nred)) + the device-counted tail rows behind the M
+// fixed rows (k_linear_relu_rows' workgroups, blocks [nred, ...)) in one launch -- the actors'
+// counted FC1 (their terminal stacks: none in most steps) without a launch of its own
+static_assert(kLrThreads == 256, "k_fc_reduce_rows runs k_linear_relu_rows' workgroups at 256 lanes");
+__global__ __launch_bounds__(256) void k_fc_reduce_rows(const float *__restrict__ part, int splits, int64_t MN, int N,
+                                                        const float *__restrict__ bias, float *__restrict__ y,
+                                                        int64_t ldy, int nred, const float *__restrict__ x,
+                                                        int64_t ldx, int64_t r0, int64_t n_max,
+                                                        const int64_t *__restrict__ n_dev,
+                                                        const float *__restrict__ w, int K) {
+  if ((int)blockIdx.x < nred)
+    fc_reduce_wg((int)blockIdx.x, part, splits, MN, N, bias, 1, y, ldy);
+  else
+    linear_relu_rows_wg((int)blockIdx.x - nred, x, ldx, r0, n_max, n_dev, w, bias, K, N, y, ldy);
 }
 
 // k splits: about one workgroup per CU (256) over the output tiles, at most 16 and at most the
@@ -367,6 +390,37 @@ int rth_fc_x9(const float *x, int64_t ldx, int64_t M, const float *w, int64_t N,
                        static_cast<const float *>(workspace), splits, MN, (int)N, bias, (int)relu, y, N);
     RTH_LAUNCHED();
   }
+  return RTH_OK;
+}
+
+int rth_fc_x9_rows_upto(const float *x, int64_t ldx, int64_t M, int64_t n_max, const int64_t *n_dev, const float *w,
+                        int64_t N, int64_t K, const float *bias, float *y, void *workspace, void *stream) {
+  RTH_REQUIRE(x && w && y && bias && n_dev, "rth_fc_x9_rows_upto: NULL argument");
+  RTH_REQUIRE(rth_fc_x9_supported(M, N, K) && n_max >= M,
+              "rth_fc_x9_rows_upto: shape %lld (+ %lld counted) x %lld x %lld not built (M %% 64, N %% 128, K %% 32)",
+              (long long)M, (long long)(n_max - M), (long long)N, (long long)K);
+  RTH_REQUIRE(ldx >= K && ldx % 4 == 0 &&
+                  ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(y)) &
+                   15) == 0,
+              "rth_fc_x9_rows_upto: row stride %lld or misaligned buffer", (long long)ldx);
+  const int splits = fc_splits((int)M, (int)N, (int)K);
+  if (splits == 1) {  // no reduce launch to share: the two launches
+    int rc = rth_fc_x9(x, ldx, M, w, N, K, bias, 1, y, workspace, stream);
+    return rc ? rc : rth_linear_relu_rows_upto(x, ldx, M, n_max, n_dev, w, bias, K, N, y, N, stream);
+  }
+  RTH_REQUIRE(workspace && (reinterpret_cast<uintptr_t>(workspace) & 15) == 0,
+              "rth_fc_x9_rows_upto: %d splits need the workspace (rth_fc_x9_workspace)", splits);
+  hipStream_t s = as_stream(stream);
+  const int tiles = (int)(M / kFcTm) * (int)(N / kFcTn);
+  float *part = static_cast<float *>(workspace);
+  hipLaunchKernelGGL(k_fc_x9<2>, dim3((unsigned)(tiles * splits)), dim3(kFcThreads), 0, s, x, ldx, (int)M, w,
+                     (int)N, (int)K, splits, bias, 1, part);
+  RTH_LAUNCHED();
+  const int64_t MN = M * N;
+  const int nred = (int)((MN / 4 + 255) / 256), nrows = n_max > M ? (int)((N + kLrCols - 1) / kLrCols) : 0;
+  hipLaunchKernelGGL(k_fc_reduce_rows, dim3((unsigned)(nred + nrows)), dim3(256), 0, s, part, splits, MN, (int)N,
+                     bias, y, (int64_t)N, nred, x, ldx, M, n_max, n_dev, w, (int)K);
+  RTH_LAUNCHED();
   return RTH_OK;
 }
 

@@ -223,7 +223,7 @@ class DQNNetwork(nn.Module):
         a GEMM over the n_fixed live rows and rth_linear_relu_rows_upto over the counted rows
         behind them (usually none); then the second layer (+ the heads-cache scatter) over the
         counted rows only"""
-        from ._lib import c_vp, call, ptr, stream_ptr
+        from ._lib import c_vp, call, lib, ptr, stream_ptr
 
         n, F = h.shape
         O = w1.shape[0]
@@ -234,9 +234,16 @@ class DQNNetwork(nn.Module):
             if not (0 < n_fixed <= n) or not h.is_contiguous():
                 raise ValueError(f"forward_heads: n_fixed {n_fixed} outside (0, {n}] or features not contiguous")
             h1 = torch.empty((n, O), dtype=torch.float32, device=h.device)
-            fc1_relu(h[:n_fixed], w1, b1, out=h1[:n_fixed])
-            call("rth_linear_relu_rows_upto", ptr(h), F, n_fixed, n, ptr(n_dev), ptr(w1), ptr(b1), F, O, ptr(h1), O,
-                 stream_ptr())
+            if _FC_ROWS_FUSED and _FC_KIND == "x9" and fc1_on_hip(n_fixed) and w1.is_contiguous() and \
+                    lib().rth_fc_x9_supported(n_fixed, O, F):
+                # the x9 GEMM over the fixed rows, then its split-K reduce and the counted rows in one launch
+                ws = _fc_workspace("rth_fc_x9", h.device, w1, n_fixed, O, F)
+                call("rth_fc_x9_rows_upto", ptr(h), F, n_fixed, n, ptr(n_dev), ptr(w1), O, F, ptr(b1), ptr(h1), ptr(ws),
+                     stream_ptr())
+            else:
+                fc1_relu(h[:n_fixed], w1, b1, out=h1[:n_fixed])
+                call("rth_linear_relu_rows_upto", ptr(h), F, n_fixed, n, ptr(n_dev), ptr(w1), ptr(b1), F, O, ptr(h1),
+                     O, stream_ptr())
         ps = self._head_params()[4:]
         A, H = ps[0].shape
         out = torch.empty((n, A + 1), dtype=torch.float32, device=h.device)
@@ -439,6 +446,21 @@ class _MergeHeads(torch.autograd.Function):
 _FC_KIND = os.environ.get("RTH_FC", "x9")
 _FC_MAX_ROWS = int(os.environ.get("RTH_FC_MAX_ROWS", "0" if os.environ.get("RTH_FC_X9") == "1" else "512") or 0)
 _FC_WS = {}
+# the actors' counted FC1 on x9: the split-K reduce and the counted rows in one launch
+# (rth_fc_x9_rows_upto); RTH_FC_ROWS_FUSED=0: rth_fc_x9 + rth_linear_relu_rows_upto (A/B)
+_FC_ROWS_FUSED = os.environ.get("RTH_FC_ROWS_FUSED", "1") != "0"
+
+
+def _fc_workspace(fn, device, w, M, N, K):
+    """the split-K workspace of fn for (M, N, K), keyed by the weight storage (one per network)"""
+    from ._lib import lib
+
+    key = (device, w.data_ptr(), M, N, K, fn)
+    ws = _FC_WS.get(key)
+    if ws is None:
+        ws = _FC_WS[key] = torch.empty(max(getattr(lib(), fn + "_workspace")(M, N, K), 16) // 4, dtype=torch.float32,
+                                       device=device)
+    return ws
 
 
 def fc1_on_hip(rows):
@@ -460,11 +482,7 @@ def fc1_relu(x, w, b, out=None):
         fn = "rth_fc_" + _FC_KIND
         if getattr(lib(), fn + "_supported")(M, N, K):
             y = out if out is not None else torch.empty((M, N), dtype=torch.float32, device=x.device)
-            key = (x.device, w.data_ptr(), M, N, K, fn)
-            ws = _FC_WS.get(key)
-            if ws is None:
-                ws = _FC_WS[key] = torch.empty(max(getattr(lib(), fn + "_workspace")(M, N, K), 16) // 4,
-                                               dtype=torch.float32, device=x.device)
+            ws = _fc_workspace(fn, x.device, w, M, N, K)
             call(fn, ptr(x), x.stride(0), M, ptr(w), N, K, ptr(b), 1, ptr(y), ptr(ws), stream_ptr())
             return y
     if out is not None:

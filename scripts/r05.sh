@@ -234,6 +234,13 @@ PY
       done
       summ gpurun_out/c2x9ab_*.log ;;
     # cumab (the learner stream on a CU-masked queue, a knob since removed): profiles/r05/ab_log.txt
+    fcrowsab)  # the actors' counted FC1: reduce + counted rows in one launch (default) vs two launches
+      for r in 1 2 3; do
+        step fcrowsab_fused_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        RTH_FC_ROWS_FUSED=0 step fcrowsab_two_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline \
+            --no-sweep
+      done
+      summ gpurun_out/fcrowsab_*.log ;;
     # nostk (the gather without its stack assembly, RTH_DIAG_NO_STACKS=1, a timing-only build of
     # commit 'Diagnostic: RTH_DIAG_NO_STACKS=1'): profiles/r05/ab_log.txt
     dp8)  # 8 ranks on one GPU over gloo: bench.py's multi-rank path and its teardown (shutdown())

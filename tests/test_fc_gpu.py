@@ -105,3 +105,36 @@ def test_fc_unsupported(dev, kind):
     with pytest.raises(_lib.RethHipError, match="not built"):
         _lib.call(fn, t.data_ptr(), 3136, 100, t.data_ptr(), 500, 3136, None, 1, t.data_ptr(), None,
                   _lib.stream_ptr())
+
+
+@pytest.mark.parametrize("count", [256, 259, 300, 512])
+def test_fc_x9_rows_upto_matches_two_launches(dev, count):
+    """rth_fc_x9_rows_upto (the actors' counted FC1: the x9 GEMM over the 256 fixed rows, then
+    its split-K reduce and the device-counted rows behind them in one launch) == rth_fc_x9 +
+    rth_linear_relu_rows_upto, bit for bit; rows past the count untouched"""
+    from reth_amd import _lib
+
+    M, n_max, N, K = 256, 512, 512, 3136
+    g = torch.Generator(device=dev).manual_seed(count)
+    x = torch.rand((n_max, K), device=dev, generator=g) * 3
+    w = (torch.rand((N, K), device=dev, generator=g) * 2 - 1) / 56
+    b = (torch.rand(N, device=dev, generator=g) * 2 - 1) * 0.1
+    n_dev = torch.tensor([count], dtype=torch.int64, device=dev)
+    ws = torch.empty(_lib.lib().rth_fc_x9_workspace(M, N, K) // 4, device=dev)
+    ys = []
+    for fused in (True, False):
+        y = torch.full((n_max, N), float("nan"), device=dev)
+        if fused:
+            _lib.call("rth_fc_x9_rows_upto", x.data_ptr(), K, M, n_max, n_dev.data_ptr(), w.data_ptr(), N, K,
+                      b.data_ptr(), y.data_ptr(), ws.data_ptr(), _lib.stream_ptr())
+        else:
+            _lib.call("rth_fc_x9", x.data_ptr(), K, M, w.data_ptr(), N, K, b.data_ptr(), 1, y.data_ptr(), ws.data_ptr(),
+                      _lib.stream_ptr())
+            _lib.call("rth_linear_relu_rows_upto", x.data_ptr(), K, M, n_max, n_dev.data_ptr(), w.data_ptr(),
+                      b.data_ptr(), K, N, y.data_ptr(), N, _lib.stream_ptr())
+        ys.append(y)
+    live = min(count, n_max)
+    assert torch.equal(ys[0][:live], ys[1][:live])
+    assert not torch.isnan(ys[0][:live]).any() and torch.isnan(ys[0][live:]).all()
+    want = torch.relu(x[:live].double() @ w.double().t() + b.double())
+    assert (ys[0][:live].double() - want).abs().max().item() < 1e-4

@@ -151,6 +151,146 @@ __global__ __launch_bounds__(kFcThreads) void k_fc_x9(const float *__restrict__ 
   }
 }
 
+// The 128 x 128 form (r05; from 1,024 rows, fc_plan): in the 64 x 128 form every 72 MFMAs of a
+// wave read 24 split weight fragments from LDS and the wave splits its own 16 activation rows,
+// and each weight chunk is split for 64 rows only.  Here BOTH operands of a 32-deep chunk are
+// split once per workgroup into LDS fragments (A: 128 rows of x, B: 128 rows of w; 3 bf16 terms
+// each, 48 KB per buffer, double-buffered: 96 KB, one barrier per chunk) and each wave owns a
+// 64 x (512 / WAVES) block of the tile: 4 x NB output blocks per 12 + 3 NB fragment reads, 36 NB
+// MFMAs.  The MFMAs run term-major -- term k of every block before term k + 1 -- so consecutive
+// MFMAs never depend on each other; each output's chain is still the 9 terms in the fixed order
+// per chunk, chunks in order, splits reduced in order.  Global loads of the next PF chunks are
+// in flight in registers while a chunk's MFMAs run.  Measured (r05, profiles/r05/ab_log.txt): 8
+// waves beat 4 (2 per SIMD), a ring of 2 chunks in flight and coalesced 8-lanes-per-row staging
+// loads do not help; at 512 rows alone the MFMA pipes are 26 % busy (23 us for 5.9 us of bf16
+// MFMA work): the waves wait on their loads and the LDS fragments, not on the MFMAs.
+constexpr int kFbTile = 128;
+// the 9 (A term, B term) pairs, smallest first: (3,3) (3,2) (2,3) (3,1) (2,2) (1,3) (2,1) (1,2) (1,1)
+__host__ __device__ constexpr int fc_ta(int k) { return (int)((0x221210100ull >> (4 * (8 - k))) & 15); }
+__host__ __device__ constexpr int fc_tb(int k) { return (int)((0x212012010ull >> (4 * (8 - k))) & 15); }
+static_assert(fc_ta(0) == 2 && fc_tb(0) == 2 && fc_ta(3) == 2 && fc_tb(3) == 0 && fc_ta(5) == 0 && fc_tb(5) == 2 &&
+                  fc_ta(8) == 0 && fc_tb(8) == 0 && fc_ta(6) == 1 && fc_tb(6) == 0,
+              "term order");
+constexpr int kFbUnits = 8 * 3 * 64;  // 16-byte units of one operand's split chunk (8 blocks x 3 terms)
+template <int WAVES, int PF>
+__global__ __launch_bounds__(WAVES * 64) void k_fc_x9t(const float *__restrict__ x, int64_t ldx, int M,
+                                                      const float *__restrict__ w, int N, int K, int splits,
+                                                      const float *__restrict__ bias, int relu,
+                                                      float *__restrict__ out) {
+  constexpr int T = WAVES * 64, WN = WAVES / 2, NB = 8 / WN;  // waves: 2 along M x WN along N
+  constexpr int RH = 2 * 2 * kFbTile / T;                    // row-halves (16 values) staged per thread
+  constexpr int NR = PF + 1;                                 // register sets of the load ring
+  static_assert(WAVES == 4 || WAVES == 8, "4 or 8 waves");
+  __shared__ uint4 sl[2][2][kFbUnits];  // [buffer][A = x, B = w]
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, r = lane & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), wm = wave & 1, wn = wave >> 1;
+  const int tiles_n = N / kFbTile;
+  const int tile = (int)blockIdx.x / splits, split = (int)blockIdx.x % splits;
+  const int m0 = (tile / tiles_n) * kFbTile, n0 = (tile % tiles_n) * kFbTile;
+  const int chunks = K / 32;
+  const int c0 = chunks * split / splits, c1 = chunks * (split + 1) / splits;
+  // staging role j: row-half u = tid + j T -> operand u >> 8, row u & 127, values 16 ((u >> 7) & 1) ..
+  const float *src[RH];
+#pragma unroll
+  for (int j = 0; j < RH; ++j) {
+    const int u = tid + j * T, op = u >> 8, rr = u & 127, h = (u >> 7) & 1;
+    src[j] = op == 0 ? x + (int64_t)(m0 + rr) * ldx + 16 * h : w + (int64_t)(n0 + rr) * K + 16 * h;
+  }
+  f32x4 ring[NR][RH][4];
+  auto load = [&](int c, f32x4 (&v)[RH][4]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < RH; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[j][q] = *reinterpret_cast<const f32x4 *>(src[j] + 32 * c + 4 * q);
+  };
+  auto stage = [&](const f32x4 (&v)[RH][4], uint4 (*buf)[kFbUnits]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < RH; ++j) {
+      const int u = tid + j * T, op = u >> 8, rr = u & 127, h = (u >> 7) & 1;
+      const int blk = rr >> 4, rw = rr & 15;
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const float vv[8] = {v[j][2 * hh][0], v[j][2 * hh][1], v[j][2 * hh][2], v[j][2 * hh][3],
+                             v[j][2 * hh + 1][0], v[j][2 * hh + 1][1], v[j][2 * hh + 1][2], v[j][2 * hh + 1][3]};
+        bf16x8 tr[3];
+        split3_pk8(vv, tr);
+#pragma unroll
+        for (int t = 0; t < 3; ++t) buf[op][(blk * 3 + t) * 64 + rw + 16 * (2 * h + hh)] = __builtin_bit_cast(uint4, tr[t]);
+      }
+    }
+  };
+  f32x4 acc[4][NB];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) acc[mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto compute = [&](uint4 (*buf)[kFbUnits]) __attribute__((always_inline)) {
+    bf16x8 af[4][3], bfr[NB][3];
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+      for (int t = 0; t < 3; ++t) af[mb][t] = __builtin_bit_cast(bf16x8, buf[0][((4 * wm + mb) * 3 + t) * 64 + lane]);
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+      for (int t = 0; t < 3; ++t)
+        bfr[nb][t] = __builtin_bit_cast(bf16x8, buf[1][((NB * wn + nb) * 3 + t) * 64 + lane]);
+#pragma unroll
+    for (int k = 0; k < 9; ++k)
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb)
+          acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mb][fc_ta(k)], bfr[nb][fc_tb(k)], acc[mb][nb], 0, 0, 0);
+  };
+  // chunk j lives in ring set (j - c0) % NR from its load until it is staged (one iteration
+  // before its MFMAs); past c1 - 1 the loads repeat the range's last chunk (in bounds, unused)
+  auto clampc = [&](int c) { return c < c1 ? c : c1 - 1; };
+#pragma unroll
+  for (int q = 0; q < NR; ++q) load(clampc(c0 + q), ring[q]);
+  stage(ring[0], sl[0]);
+  load(clampc(c0 + NR), ring[0]);
+  __syncthreads();
+  // iteration i (chunk c0 + i): MFMAs from buffer i & 1; chunk i + 1 staged from its ring set
+  // into the other buffer, then chunk i + 1 + NR loaded into that set
+  auto iter = [&](int i, auto ic) __attribute__((always_inline)) {
+    constexpr int s = decltype(ic)::value;  // i mod 2 NR
+    compute(sl[s & 1]);
+    stage(ring[(s + 1) % NR], sl[(s + 1) & 1]);
+    load(clampc(c0 + i + 1 + NR), ring[(s + 1) % NR]);
+    __syncthreads();
+  };
+  const int n_it = c1 - c0;
+  constexpr int U = 2 * NR;
+  int i = 0;
+  for (; i + U <= n_it; i += U)
+    static_for(std::make_integer_sequence<int, U>{}, [&](auto ic) __attribute__((always_inline)) {
+      iter(i + decltype(ic)::value, ic);
+    });
+  static_for(std::make_integer_sequence<int, U>{}, [&](auto ic) __attribute__((always_inline)) {
+    if (i + decltype(ic)::value < n_it) iter(i + decltype(ic)::value, ic);
+  });
+  // D: lane holds rows 4 g + i of each 16-row block, column r of each 16-column block
+  float *dst = splits == 1 ? out : out + (int64_t)split * M * N;
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      const int n = n0 + 16 * (NB * wn + nb) + r;
+      const float bn = splits == 1 && bias ? bias[n] : 0.0f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int m = m0 + 64 * wm + 16 * mb + 4 * g + e;
+        float v = acc[mb][nb][e];
+        if (splits == 1) {
+          v = radd(v, bn);
+          v = relu ? fc_relu(v) : v;
+        }
+        dst[(int64_t)m * N + n] = v;
+      }
+    }
+}
+
 // FC1 on the fp32 MFMA (v_mfma_f32_16x16x4_f32, the GEMM's own arithmetic) with no LDS (r05,
 // hipBLASLt's 512-row tile MT64x16x256 holds 80 KB of LDS per workgroup and runs
 // 48 us per launch in the loop against 21-26 alone).  Workgroup = 4 waves over a 64 x 128
@@ -324,6 +464,52 @@ static int fc_splits(int M, int N, int K) {
   return s < chunks ? s : chunks;
 }
 
+// which x9 form runs a shape: the 128 x 128 tile (k_fc_x9t) from 1,024 rows (M and N multiples of
+// 128), the 64 x 128 k_fc_x9 below that -- alone (scripts/bench_fc.py, r05) the 128 tile is
+// faster from 1,024 rows (37.4 vs 44.1 us; 2,048: 55.1 vs 73.1) and slower below (512: 30.8 vs
+// 29.1; 256: 24.8 vs 21.9); RTH_FC_TILE=64 / 128 forces one.  k splits of the 128 tile: about one
+// workgroup per CU, at most 16 (RTH_FCT_SPLITS overrides, at most 32), never more than the chunks
+struct FcPlan {
+  int big, splits;
+};
+static FcPlan fc_plan(int M, int N, int K) {
+  static const int tile = [] {
+    const char *e = getenv("RTH_FC_TILE");
+    return e ? atoi(e) : 0;
+  }();
+  static const int env = [] {
+    const char *e = getenv("RTH_FCT_SPLITS");
+    return e ? atoi(e) : 0;
+  }();
+  if (tile == 64 || M % kFbTile || N % kFbTile || (tile != 128 && M < 1024)) return FcPlan{0, fc_splits(M, N, K)};
+  const int tiles = (M / kFbTile) * (N / kFbTile), chunks = K / 32;
+  int s = env > 0 ? (env > 32 ? 32 : env) : (256 + tiles - 1) / tiles;
+  if (env <= 0 && s > 16) s = 16;
+  s = s < 1 ? 1 : s;
+  return FcPlan{1, s < chunks ? s : chunks};
+}
+
+// one x9 GEMM launch by plan p into out (y when p.splits == 1, else the partials)
+static void fc_x9_launch(const FcPlan &p, const float *x, int64_t ldx, int M, const float *w, int N, int K,
+                         const float *bias, int relu, float *out, hipStream_t s) {
+  if (!p.big) {
+    const int tiles = (M / kFcTm) * (N / kFcTn);
+    static const int pf = [] {  // RTH_FC_PF: chunks of loads in flight (1 or 2)
+      const char *e = getenv("RTH_FC_PF");
+      return e && atoi(e) == 1 ? 1 : 2;
+    }();
+    if (pf == 1)
+      hipLaunchKernelGGL(k_fc_x9<1>, dim3((unsigned)(tiles * p.splits)), dim3(kFcThreads), 0, s, x, ldx, M, w, N, K,
+                         p.splits, bias, relu, out);
+    else
+      hipLaunchKernelGGL(k_fc_x9<2>, dim3((unsigned)(tiles * p.splits)), dim3(kFcThreads), 0, s, x, ldx, M, w, N, K,
+                         p.splits, bias, relu, out);
+    return;
+  }
+  const dim3 grid((unsigned)((M / kFbTile) * (N / kFbTile) * p.splits));
+  hipLaunchKernelGGL((k_fc_x9t<8, 1>), grid, dim3(512), 0, s, x, ldx, M, w, N, K, p.splits, bias, relu, out);
+}
+
 // k_fc_f32's k splits: 8 (one K slice per XCD) while that gives at most 512 workgroups, else
 // fewer; RTH_FCF_SPLITS overrides (A/B); never more than the chunk count
 static int fcf_splits(int M, int N, int K) {
@@ -354,7 +540,7 @@ int rth_fc_x9_supported(int64_t M, int64_t N, int64_t K) {
 
 int64_t rth_fc_x9_workspace(int64_t M, int64_t N, int64_t K) {
   if (!rth_fc_x9_supported(M, N, K)) return 0;
-  const int s = fc_splits((int)M, (int)N, (int)K);
+  const int s = fc_plan((int)M, (int)N, (int)K).splits;
   return s > 1 ? (int64_t)s * M * N * 4 : 0;
 }
 
@@ -367,22 +553,13 @@ int rth_fc_x9(const float *x, int64_t ldx, int64_t M, const float *w, int64_t N,
   RTH_REQUIRE(((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(y)) &
                15) == 0,
               "rth_fc_x9: misaligned buffer");
-  const int splits = fc_splits((int)M, (int)N, (int)K);
+  const FcPlan p = fc_plan((int)M, (int)N, (int)K);
+  const int splits = p.splits;
   RTH_REQUIRE(splits == 1 || (workspace && (reinterpret_cast<uintptr_t>(workspace) & 15) == 0),
               "rth_fc_x9: %d splits need the workspace (rth_fc_x9_workspace)", splits);
   hipStream_t s = as_stream(stream);
-  const int tiles = (int)(M / kFcTm) * (int)(N / kFcTn);
   float *out = splits == 1 ? y : static_cast<float *>(workspace);
-  static const int pf = [] {  // RTH_FC_PF: chunks of loads in flight (1 or 2)
-    const char *e = getenv("RTH_FC_PF");
-    return e && atoi(e) == 1 ? 1 : 2;
-  }();
-  if (pf == 1)
-    hipLaunchKernelGGL(k_fc_x9<1>, dim3((unsigned)(tiles * splits)), dim3(kFcThreads), 0, s, x, ldx, (int)M, w,
-                       (int)N, (int)K, splits, bias, (int)relu, out);
-  else
-    hipLaunchKernelGGL(k_fc_x9<2>, dim3((unsigned)(tiles * splits)), dim3(kFcThreads), 0, s, x, ldx, (int)M, w,
-                       (int)N, (int)K, splits, bias, (int)relu, out);
+  fc_x9_launch(p, x, ldx, (int)M, w, (int)N, (int)K, bias, (int)relu, out, s);
   RTH_LAUNCHED();
   if (splits > 1) {
     const int64_t MN = M * N;
@@ -403,7 +580,8 @@ int rth_fc_x9_rows_upto(const float *x, int64_t ldx, int64_t M, int64_t n_max, c
                   ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(y)) &
                    15) == 0,
               "rth_fc_x9_rows_upto: row stride %lld or misaligned buffer", (long long)ldx);
-  const int splits = fc_splits((int)M, (int)N, (int)K);
+  const FcPlan p = fc_plan((int)M, (int)N, (int)K);
+  const int splits = p.splits;
   if (splits == 1) {  // no reduce launch to share: the two launches
     int rc = rth_fc_x9(x, ldx, M, w, N, K, bias, 1, y, workspace, stream);
     return rc ? rc : rth_linear_relu_rows_upto(x, ldx, M, n_max, n_dev, w, bias, K, N, y, N, stream);
@@ -411,10 +589,8 @@ int rth_fc_x9_rows_upto(const float *x, int64_t ldx, int64_t M, int64_t n_max, c
   RTH_REQUIRE(workspace && (reinterpret_cast<uintptr_t>(workspace) & 15) == 0,
               "rth_fc_x9_rows_upto: %d splits need the workspace (rth_fc_x9_workspace)", splits);
   hipStream_t s = as_stream(stream);
-  const int tiles = (int)(M / kFcTm) * (int)(N / kFcTn);
   float *part = static_cast<float *>(workspace);
-  hipLaunchKernelGGL(k_fc_x9<2>, dim3((unsigned)(tiles * splits)), dim3(kFcThreads), 0, s, x, ldx, (int)M, w,
-                     (int)N, (int)K, splits, bias, 1, part);
+  fc_x9_launch(p, x, ldx, (int)M, w, (int)N, (int)K, bias, 1, part, s);
   RTH_LAUNCHED();
   const int64_t MN = M * N;
   const int nred = (int)((MN / 4 + 255) / 256), nrows = n_max > M ? (int)((N + kLrCols - 1) / kLrCols) : 0;

@@ -243,6 +243,54 @@ PY
       summ gpurun_out/fcrowsab_*.log ;;
     # nostk (the gather without its stack assembly, RTH_DIAG_NO_STACKS=1, a timing-only build of
     # commit 'Diagnostic: RTH_DIAG_NO_STACKS=1'): profiles/r05/ab_log.txt
+    fct)  # FC1 x9 on the 128 x 128 tile (both operands split once per workgroup): tests, alone per form
+      step fct_tests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_fc_gpu.py
+      RTH_FC_TILE=64 step fct_micro_t64 120 python scripts/bench_fc.py
+      RTH_FC_TILE=128 step fct_micro_t128 120 python scripts/bench_fc.py
+      grep -h "M=" gpurun_out/fct_micro_*.log ;;
+    fcpmc)  # per-kernel durations (x9 GEMM vs reduce) and SQ counters of the FC1 x9 forms at FC_M rows
+      fcsum() {  # fcsum DIR: median duration and counters per kernel
+        python - "$1" <<'PY'
+import collections, csv, os, statistics as st, sys
+d = sys.argv[1]
+for f in ("run_kernel_trace.csv", "run_counter_collection.csv"):
+    p = os.path.join(d, f)
+    if not os.path.exists(p):
+        continue
+    v = collections.defaultdict(lambda: collections.defaultdict(list))
+    for r in csv.DictReader(open(p)):
+        k = r["Kernel_Name"].split("(")[0].replace("void ", "")[:40]
+        if "fc" not in k:
+            continue
+        v[k]["us"].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+        if "Counter_Name" in r:
+            v[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    for k, c in v.items():
+        print(d.split("/")[-1], k, {n: round(st.median(x), 2) for n, x in c.items()})
+PY
+      }
+      for form in t64 t128; do  # (r05: also 4 waves, 2 chunks in flight, coalesced staging loads -- removed)
+        case $form in t64) e="RTH_FC_TILE=64";; t128) e="RTH_FC_TILE=128";; esac
+        env $e timeout -s KILL 120 rocprofv3 --kernel-trace --output-format csv -d "$PWD/gpurun_out/fct_$form" -o run \
+            -- python scripts/fc_pmc.py > gpurun_out/fct_$form.log 2>&1 || exit 1
+        fcsum gpurun_out/fct_$form
+      done
+      for form in t64 t128; do
+        case $form in t64) e="RTH_FC_TILE=64";; t128) e="RTH_FC_TILE=128";; esac
+        env $e timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+            SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT --kernel-trace \
+            --output-format csv -d "$PWD/gpurun_out/fcp_$form" -o run -- python scripts/fc_pmc.py \
+            > gpurun_out/fcp_$form.log 2>&1 || exit 1
+        fcsum gpurun_out/fcp_$form
+      done ;;
+    fctab)  # in the loop: FC1 <= 512 rows on the x9 128 tile (RTH_FC_TILE=128) / every FC1 on x9 (RTH_FC_MAX_ROWS=0,
+      # the learner's 1,024 rows on the 128 tile) vs the default (<= 512 rows on the 64 x 128 tile, 1,024 on hipBLASLt)
+      for r in 1 2; do
+        RTH_FC_TILE=128 step fctab_t128_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        RTH_FC_MAX_ROWS=0 step fctab_all_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        step fctab_t64_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+      done
+      summ gpurun_out/fctab_*.log ;;
     dp8)  # 8 ranks on one GPU over gloo: bench.py's multi-rank path and its teardown (shutdown())
       RTH_SHARE_GPU=1 RTH_DIST_BACKEND=gloo step dp8_gloo_rehearsal 900 python -m torch.distributed.run --nnodes=1 \
           --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 8 --faithful --steps 20 \

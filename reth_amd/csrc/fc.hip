@@ -151,7 +151,7 @@ __global__ __launch_bounds__(kFcThreads) void k_fc_x9(const float *__restrict__ 
   }
 }
 
-// The 128 x 128 form (r05; from 1,024 rows, fc_plan): in the 64 x 128 form every 72 MFMAs of a
+// The 128 x 128 form (r05; the default where M % 128 == 0, fc_plan): in the 64 x 128 form every 72 MFMAs of a
 // wave read 24 split weight fragments from LDS and the wave splits its own 16 activation rows,
 // and each weight chunk is split for 64 rows only.  Here BOTH operands of a 32-deep chunk are
 // split once per workgroup into LDS fragments (A: 128 rows of x, B: 128 rows of w; 3 bf16 terms
@@ -464,11 +464,16 @@ static int fc_splits(int M, int N, int K) {
   return s < chunks ? s : chunks;
 }
 
-// which x9 form runs a shape: the 128 x 128 tile (k_fc_x9t) from 1,024 rows (M and N multiples of
-// 128), the 64 x 128 k_fc_x9 below that -- alone (scripts/bench_fc.py, r05) the 128 tile is
-// faster from 1,024 rows (37.4 vs 44.1 us; 2,048: 55.1 vs 73.1) and slower below (512: 30.8 vs
-// 29.1; 256: 24.8 vs 21.9); RTH_FC_TILE=64 / 128 forces one.  k splits of the 128 tile: about one
-// workgroup per CU, at most 16 (RTH_FCT_SPLITS overrides, at most 32), never more than the chunks
+// which x9 form runs a shape: the 128 x 128 tile (k_fc_x9t) where M and N are multiples of 128,
+// else the 64 x 128 k_fc_x9 (RTH_FC_TILE=64 forces it).  Alone (scripts/bench_fc.py, r05) the 128
+// tile is faster from 1,024 rows (37.5 vs 44.1 us; 2,048: 54 vs 72) and slower below (512: 30.6
+// vs 28.9; 256: 24.6 vs 21.8), but in the loop it is the better one at 512 / 256 rows too:
+// 0.521-0.525 vs 0.531-0.533 ms/step (profiles/r05/ab_log.txt) -- one 96 KB workgroup per CU,
+// a single round of at most 256 workgroups, where the 64 x 128 form's 256 workgroups of 48 KB
+// share CUs with the other stream's kernels.  k splits: about one workgroup per CU, at most
+// RTH_FCT_MAXSPLITS (default 16: at 512 rows 256 workgroups; 24 / 32 splits -- two rounds of
+// workgroups -- 0.533-0.539, 8 splits 0.531-0.534); RTH_FCT_SPLITS overrides (at most 32); never
+// more than the chunk count
 struct FcPlan {
   int big, splits;
 };
@@ -481,10 +486,15 @@ static FcPlan fc_plan(int M, int N, int K) {
     const char *e = getenv("RTH_FCT_SPLITS");
     return e ? atoi(e) : 0;
   }();
-  if (tile == 64 || M % kFbTile || N % kFbTile || (tile != 128 && M < 1024)) return FcPlan{0, fc_splits(M, N, K)};
+  static const int cap = [] {
+    const char *e = getenv("RTH_FCT_MAXSPLITS");
+    const int v = e ? atoi(e) : 16;
+    return v < 1 ? 1 : (v > 32 ? 32 : v);
+  }();
+  if (tile == 64 || M % kFbTile || N % kFbTile) return FcPlan{0, fc_splits(M, N, K)};
   const int tiles = (M / kFbTile) * (N / kFbTile), chunks = K / 32;
   int s = env > 0 ? (env > 32 ? 32 : env) : (256 + tiles - 1) / tiles;
-  if (env <= 0 && s > 16) s = 16;
+  if (env <= 0 && s > cap) s = cap;
   s = s < 1 ? 1 : s;
   return FcPlan{1, s < chunks ? s : chunks};
 }

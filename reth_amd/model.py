@@ -437,14 +437,17 @@ class _MergeHeads(torch.autograd.Function):
 
 # FC1 + bias + ReLU: RTH_FC=x9 -> rth_fc_x9 (the exact-split bf16 MFMA, fixed-order split-K),
 # RTH_FC=f32 -> rth_fc_f32 (fp32 MFMA, no LDS), RTH_FC=blas -> hipBLASLt's GEMM with the
-# bias+ReLU epilogue, for batches of at most RTH_FC_MAX_ROWS rows (0: any) where the shape is
-# built; the rest on hipBLASLt.  Default since r05: x9 up to 512 rows -- the actors' and the
-# target pass's forwards: the same step as hipBLASLt (0.536-0.539 vs 0.536 ms, interleaved) with
-# every product exact (a third of the learner's |td| error came from FC1's fp32 chains, DESIGN
-# (c)); the learner's 1,024-row forward stays on hipBLASLt (x9: 43 vs 30 us alone).
-# RTH_FC_X9=1 (r04's switch): x9 at every row count.
+# bias+ReLU epilogue, for batches of at most RTH_FC_MAX_ROWS rows (0, the default: any) where the
+# shape is built; the rest on hipBLASLt.  Since late r05 every FC1 forward but the learner's runs
+# on x9 -- the actors' (256 rows at Pong, 2,048 at Breakout) and the target pass's (512): with the
+# 128 x 128 tile 0.522-0.525 vs 0.532 ms/step at Pong and 0.833 vs 0.851-0.855 at Breakout (the
+# actors' 2,048 rows had been on hipBLASLt), every product exact (a third of the learner's |td|
+# error came from FC1's fp32 chains, DESIGN (c)).  The learner's 1,024-row forward
+# (fc1_relu(learner=True)) stays on hipBLASLt: on x9 0.534-0.539 vs 0.522-0.523 ms/step;
+# RTH_FC_LEARNER=x9 or RTH_FC_X9=1 (r04's switch) put it on x9 too.
 _FC_KIND = os.environ.get("RTH_FC", "x9")
-_FC_MAX_ROWS = int(os.environ.get("RTH_FC_MAX_ROWS", "0" if os.environ.get("RTH_FC_X9") == "1" else "512") or 0)
+_FC_MAX_ROWS = int(os.environ.get("RTH_FC_MAX_ROWS", "0") or 0)
+_FC_LEARNER_X9 = os.environ.get("RTH_FC_X9") == "1" or os.environ.get("RTH_FC_LEARNER", "blas") == "x9"
 _FC_WS = {}
 # the actors' counted FC1 on x9: the split-K reduce and the counted rows in one launch
 # (rth_fc_x9_rows_upto); RTH_FC_ROWS_FUSED=0: rth_fc_x9 + rth_linear_relu_rows_upto (A/B)
@@ -468,15 +471,16 @@ def fc1_on_hip(rows):
     return _FC_KIND in ("f32", "x9") and (_FC_MAX_ROWS <= 0 or rows <= _FC_MAX_ROWS)
 
 
-def fc1_relu(x, w, b, out=None):
+def fc1_relu(x, w, b, out=None, learner=False):
     """relu(x @ w.T + b) (FC1 of both dueling branches): rth_fc_f32 / rth_fc_x9 when selected
-    (RTH_FC) and built for the shape, else one hipBLASLt GEMM with the bias+ReLU epilogue.  The
+    (RTH_FC) and built for the shape, else one hipBLASLt GEMM with the bias+ReLU epilogue
+    (learner=True: the captured learner's forward, on hipBLASLt unless RTH_FC_LEARNER=x9).  The
     split-K workspace is keyed by the weight storage, so two networks (the actors', the
     target's, the learner's -- on different streams) never share one"""
     M, K = x.shape
     N = w.shape[0]
     if _FC_KIND in ("f32", "x9") and x.is_cuda and x.stride(1) == 1 and w.is_contiguous() and \
-            (_FC_MAX_ROWS <= 0 or M <= _FC_MAX_ROWS):
+            (_FC_MAX_ROWS <= 0 or M <= _FC_MAX_ROWS) and (not learner or _FC_LEARNER_X9):
         from ._lib import call, lib, ptr, stream_ptr
 
         fn = "rth_fc_" + _FC_KIND

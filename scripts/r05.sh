@@ -248,6 +248,47 @@ PY
       RTH_FC_TILE=64 step fct_micro_t64 120 python scripts/bench_fc.py
       RTH_FC_TILE=128 step fct_micro_t128 120 python scripts/bench_fc.py
       grep -h "M=" gpurun_out/fct_micro_*.log ;;
+    fctab2)  # in the loop: the <= 512-row FC1 forwards on the 128 tile at 16 (default) / 8 / 4 k splits vs the 64 x 128 tile
+      for r in 1 2 3; do
+        RTH_FC_TILE=128 step fct2_t128_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        RTH_FC_TILE=128 RTH_FCT_SPLITS=8 step fct2_s8_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        RTH_FC_TILE=128 RTH_FCT_SPLITS=4 step fct2_s4_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        RTH_FC_TILE=64 step fct2_t64_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+      done
+      summ gpurun_out/fct2_*.log ;;
+    fctab3)  # in the loop: 128 tile at 16 (default) / 24 / 32 k splits; every FC1 on x9 at 16 splits (the learner's 1,024 rows too)
+      for r in 1 2 3; do
+        RTH_FC_TILE=128 step fct3_s16_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        RTH_FC_TILE=128 RTH_FCT_SPLITS=24 step fct3_s24_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        RTH_FC_TILE=128 RTH_FCT_SPLITS=32 step fct3_s32_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        RTH_FC_TILE=128 RTH_FCT_SPLITS=16 RTH_FC_MAX_ROWS=0 step fct3_all16_$r 300 python bench.py --steps 300 --warmup 5 \
+            --no-cpu-baseline --no-sweep
+      done
+      summ gpurun_out/fct3_*.log ;;
+    fctab4)  # in the loop: the 128 tile by default (16 k splits at most) vs at most 32 (the actors' 256 rows: 256 workgroups) vs 64 x 128
+      for r in 1 2 3; do
+        step fct4_dflt_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        RTH_FCT_MAXSPLITS=32 step fct4_m32_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        RTH_FC_TILE=64 step fct4_t64_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+      done
+      summ gpurun_out/fct4_*.log ;;
+    fctbo)  # Breakout: the 512-row FC1 (target pass) on the 128 tile (default) vs 64 x 128; + the actors' 2,048 rows on x9
+      for r in 1 2; do
+        step fctbo_dflt_$r 300 python bench.py --workload breakout --steps 100 --warmup 10 --no-cpu-baseline --no-sweep
+        RTH_FC_TILE=64 step fctbo_t64_$r 300 python bench.py --workload breakout --steps 100 --warmup 10 --no-cpu-baseline --no-sweep
+        RTH_FC_MAX_ROWS=2048 step fctbo_a2k_$r 300 python bench.py --workload breakout --steps 100 --warmup 10 --no-cpu-baseline \
+            --no-sweep
+      done
+      summ gpurun_out/fctbo_*.log ;;
+    fctab5)  # the late-r05 FC1 rule (every forward but the learner's on x9) vs at most 512 rows on x9 (the earlier rule), Pong + Breakout
+      for r in 1 2; do
+        step fct5_po_dflt_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        RTH_FC_MAX_ROWS=512 step fct5_po_m512_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        step fct5_bo_dflt_$r 300 python bench.py --workload breakout --steps 100 --warmup 10 --no-cpu-baseline --no-sweep
+        RTH_FC_MAX_ROWS=512 step fct5_bo_m512_$r 300 python bench.py --workload breakout --steps 100 --warmup 10 \
+            --no-cpu-baseline --no-sweep
+      done
+      summ gpurun_out/fct5_*.log ;;
     fcpmc)  # per-kernel durations (x9 GEMM vs reduce) and SQ counters of the FC1 x9 forms at FC_M rows
       fcsum() {  # fcsum DIR: median duration and counters per kernel
         python - "$1" <<'PY'

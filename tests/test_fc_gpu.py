@@ -82,8 +82,8 @@ def test_fc_strided_big_tile(dev, kind):
 
 
 def test_fc_x9_forms_agree(dev):
-    """the x9 forms at 512 rows -- the default (64 x 128 tile), the 128 x 128 tile (RTH_FC_TILE=128)
-    at 16 / 1 / 4 / 32 k splits, the 64 x 128 tile forced -- each within fp32 summation error of the
+    """the x9 forms at 512 rows -- the default (128 x 128 tile, 16 k splits), the same tile at 1 / 4 /
+    32 k splits, the 64 x 128 tile (RTH_FC_TILE=64) -- each within fp32 summation error of the
     float64 result and of each other, each bit-identical run to run (child processes: the knobs
     are read once per process)"""
     import os
@@ -100,9 +100,8 @@ def test_fc_x9_forms_agree(dev):
             "assert torch.equal(y, y2) and not torch.isnan(y).any(); np.save(sys.argv[1], y.cpu().numpy());"
             "np.save(sys.argv[1] + '.ref.npy', torch.relu(x.double() @ w.double().t() + b.double()).cpu().numpy())")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    forms = [{}, {"RTH_FC_TILE": "128"}, {"RTH_FC_TILE": "128", "RTH_FCT_SPLITS": "1"},
-             {"RTH_FC_TILE": "128", "RTH_FCT_SPLITS": "4"}, {"RTH_FC_TILE": "128", "RTH_FCT_SPLITS": "32"},
-             {"RTH_FC_TILE": "64"}]
+    forms = [{}, {"RTH_FCT_SPLITS": "1"}, {"RTH_FCT_SPLITS": "4"}, {"RTH_FCT_SPLITS": "32"},
+             {"RTH_FCT_MAXSPLITS": "32"}, {"RTH_FC_TILE": "64"}]
     outs, ref = [], None
     for i, f in enumerate(forms):
         path = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"fcx9_form_{i}_{os.getpid()}.npy")

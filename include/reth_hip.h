@@ -553,9 +553,11 @@ int rth_conv_dgrad_relu_prepacked(const rth_conv_shape *shape, const float *gy_d
  * row-major with row stride ldx, w row-major [N, K] (the Linear weight as stored), act = ReLU
  * when relu != 0, bias may be NULL; M % 64 == 0, N % 128 == 0, K % 32 == 0
  * (rth_fc_x9_supported).  Fixed-order split-K partials in `workspace` (rth_fc_x9_workspace
- * bytes, NULL when that is 0): run-to-run deterministic.  Replaces the hipBLASLt GEMM +
- * bias + ReLU epilogue (torch._addmm_activation) of the actors', the target pass's and the
- * learner's forward when enabled (RTH_FC_X9=1). */
+ * bytes, NULL when that is 0): run-to-run deterministic.  M and N multiples of 128 run on a
+ * 128 x 128 workgroup tile (late r05), others on a 64 x 128 tile; the workspace size follows
+ * the form (the same process-wide RTH_FC_TILE / RTH_FCT_SPLITS / RTH_FCT_MAXSPLITS knobs).
+ * Replaces the hipBLASLt GEMM + bias + ReLU epilogue (torch._addmm_activation) of the actors'
+ * and the target pass's forward by default, and of the learner's with RTH_FC_LEARNER=x9. */
 int rth_fc_x9_supported(int64_t M, int64_t N, int64_t K);
 int64_t rth_fc_x9_workspace(int64_t M, int64_t N, int64_t K);
 int rth_fc_x9(const float *x_dev, int64_t ldx, int64_t M, const float *w_dev, int64_t N, int64_t K,

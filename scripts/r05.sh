@@ -289,6 +289,15 @@ PY
             --no-cpu-baseline --no-sweep
       done
       summ gpurun_out/fct5_*.log ;;
+    ldsab)  # CU-exclusive launches by padded LDS (RTH_LDS_MIN_<CLASS> bytes per workgroup; a knob of a build since removed)
+      for r in 1 2; do
+        step lds_dflt_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        RTH_LDS_MIN_C1=98304 step lds_c1_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        RTH_LDS_MIN_X9=98304 step lds_x9_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        RTH_LDS_MIN_DG=98304 step lds_dg_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        RTH_LDS_MIN_W1=98304 step lds_w1_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+      done
+      summ gpurun_out/lds_*.log ;;
     fcpmc)  # per-kernel durations (x9 GEMM vs reduce) and SQ counters of the FC1 x9 forms at FC_M rows
       fcsum() {  # fcsum DIR: median duration and counters per kernel
         python - "$1" <<'PY'

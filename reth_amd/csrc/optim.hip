@@ -88,14 +88,23 @@ __device__ __forceinline__ int seg_of(const OptArgs &a, int64_t b) {
   return s;
 }
 
-// the norm, the clip coefficient and the bias corrections from the per-workgroup partials
-// (summed in workgroup order: deterministic).  Every Adam workgroup computes them itself --
-// the same values in the same order -- so no workgroup waits for another; the step count was
-// advanced by k_grad_sqsum's first workgroup (a kernel boundary before any read).
-__device__ OptScalars opt_scalars(const double *__restrict__ part, int nparts, double *red, int clip, float max_norm,
-                                  double lr, double beta1, double beta2, int64_t t) {
-  double acc = 0.0;
-  for (int k = threadIdx.x; k < nparts; k += kOptThreads) acc = radd(acc, part[k]);
+// the bias corrections of step t (python-float scalars of adam.py, cast to f32 where they meet
+// the f32 tensors): lr / (1 - beta1^t), sqrt(1 - beta2^t)
+struct BiasCorr {
+  float step_size, bc2_sqrt;
+};
+__device__ __forceinline__ BiasCorr bias_corr(double lr, double beta1, double beta2, int64_t t) {
+  const double bc1 = 1.0 - pow(beta1, (double)t);
+  const double bc2 = 1.0 - pow(beta2, (double)t);
+  return BiasCorr{(float)(lr / bc1), (float)sqrt(bc2)};
+}
+
+// the norm and the clip coefficient from the per-workgroup partials (summed in workgroup
+// order: deterministic), `acc` = this lane's in-order sum of partials tid, tid + T, ...  Every
+// Adam workgroup computes them itself -- the same values in the same order -- so no workgroup
+// waits for another; the step count and the bias corrections were written by k_grad_sqsum's
+// first workgroup (a kernel boundary before any read).
+__device__ OptScalars opt_scalars(double acc, double *red, int clip, float max_norm, BiasCorr bc) {
   red[threadIdx.x] = acc;
   __syncthreads();
   for (int s = kOptThreads / 2; s > 0; s >>= 1) {
@@ -108,10 +117,7 @@ __device__ OptScalars opt_scalars(const double *__restrict__ part, int nparts, d
     const float c = max_norm / radd(total, 1e-6f);
     coef = c < 1.0f ? c : 1.0f;
   }
-  // python-float scalars of adam.py, cast to f32 where they meet the f32 tensors
-  const double bc1 = 1.0 - pow(beta1, (double)t);
-  const double bc2 = 1.0 - pow(beta2, (double)t);
-  return OptScalars{coef, (float)(lr / bc1), (float)sqrt(bc2), total};
+  return OptScalars{coef, bc.step_size, bc.bc2_sqrt, total};
 }
 
 struct ScalarArgs {
@@ -121,11 +127,12 @@ struct ScalarArgs {
   int64_t *step;
   OptScalars *out;
   float *total_out;
+  BiasCorr *bc;  // written by k_grad_sqsum's workgroup 0, read by every k_adam workgroup
 };
 
 // per-workgroup sums of squares of the gradients (fp64 partials); workgroup 0 advances the
-// device step count
-__global__ __launch_bounds__(kOptThreads) void k_grad_sqsum(OptArgs a, double *__restrict__ part, int64_t *step) {
+// device step count and writes the new step's bias corrections
+__global__ __launch_bounds__(kOptThreads) void k_grad_sqsum(OptArgs a, double *__restrict__ part, ScalarArgs sa) {
   __shared__ double red[kOptThreads];
   const int64_t b = blockIdx.x;
   const OptSeg &sg = a.seg[seg_of(a, b)];
@@ -156,7 +163,11 @@ __global__ __launch_bounds__(kOptThreads) void k_grad_sqsum(OptArgs a, double *_
   }
   if (threadIdx.x == 0) {
     part[b] = red[0];
-    if (b == 0) *step += 1;
+    if (b == 0) {
+      const int64_t t = *sa.step + 1;
+      *sa.step = t;
+      *sa.bc = bias_corr(sa.lr, sa.beta1, sa.beta2, t);
+    }
   }
 }
 
@@ -166,7 +177,28 @@ __global__ __launch_bounds__(kOptThreads) void k_adam(OptArgs a, const double *_
   const int64_t b = blockIdx.x;
   const OptSeg &sg = a.seg[seg_of(a, b)];
   const int64_t base = (b - sg.blk0) * kOptChunk;
-  // this chunk's loads first, then the global norm from the partials (overlapping them)
+  // the partials and the bias corrections are loaded first and the chunk's loads issued behind
+  // them, so the norm's reduction runs while the chunk is in flight (the load counter is in
+  // order: waiting for the partials does not wait for the chunk)
+  double pacc = 0.0, pl[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {  // unconditional loads (a clamped index): none waits under a branch
+    const int k = threadIdx.x + u * kOptThreads;
+    pl[u] = part[k < nparts ? k : nparts - 1];
+  }
+  const BiasCorr bc = *sa.bc;
+  // the partials' in-order sum, in each load path right after its loads are issued (at a merge
+  // of the two paths the compiler would wait for every load before it)
+  auto sum_parts = [&]() __attribute__((always_inline)) {
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) asm volatile("" : "+v"(pl[u]));  // keeps the sum behind the loads
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (threadIdx.x + u * kOptThreads < nparts) pacc = radd(pacc, pl[u]);
+    for (int k = threadIdx.x + 4 * kOptThreads; k < nparts; k += kOptThreads) pacc = radd(pacc, part[k]);
+  };
+  __builtin_amdgcn_sched_barrier(0);
   float4 gv[kOptV], mv[kOptV], vv[kOptV], pv[kOptV];
   if (sg.vec) {
     const __amdgpu_buffer_rsrc_t rg = seg_rsrc(sg.grad, sg.n), rm = seg_rsrc(sg.m, sg.n), rv = seg_rsrc(sg.v, sg.n),
@@ -179,6 +211,7 @@ __global__ __launch_bounds__(kOptThreads) void k_adam(OptArgs a, const double *_
       vv[k] = ld4b(rv, e);
       pv[k] = ld4b(rp, e);
     }
+    sum_parts();
   } else {
 #pragma unroll
     for (int k = 0; k < kOptV; ++k) {
@@ -188,8 +221,9 @@ __global__ __launch_bounds__(kOptThreads) void k_adam(OptArgs a, const double *_
       vv[k] = ld4(sg.v, e, sg.n, 0);
       pv[k] = ld4(sg.param, e, sg.n, 0);
     }
+    sum_parts();
   }
-  const OptScalars sc = opt_scalars(part, nparts, red, sa.clip, sa.max_norm, sa.lr, sa.beta1, sa.beta2, *sa.step);
+  const OptScalars sc = opt_scalars(pacc, red, sa.clip, sa.max_norm, bc);
   if (b == 0 && threadIdx.x == 0) {
     *sa.out = sc;
     if (sa.total_out) *sa.total_out = sc.total_norm;
@@ -414,7 +448,8 @@ using namespace rth;
 extern "C" {
 
 // [partials: kMaxPartials doubles (the one-launch form: its tagged granules)][OptScalars (the
-// last update's scalars)][FusedWs: call counter, timeout word]
+// last update's scalars, 16 B)][BiasCorr (k_grad_sqsum -> k_adam, 8 B)][FusedWs at +32: call
+// counter, timeout word]
 int64_t rth_clip_adam_workspace(void) { return (int64_t)kMaxPartials * 8 + 64; }
 
 // the one-launch form's timeout word (nonzero: a grid barrier timed out and that call left
@@ -451,7 +486,8 @@ int rth_clip_adam(const rth_param_tensor *tensors, int32_t n_tensors, double lr,
   auto *sc = reinterpret_cast<OptScalars *>(static_cast<uint8_t *>(workspace_dev) + (int64_t)kMaxPartials * 8);
   const int clip = max_norm >= 0.0;
   hipStream_t s = as_stream(stream);
-  const ScalarArgs sa{clip, (float)max_norm, lr, beta1, beta2, step_dev, sc, total_norm_out};
+  auto *bcw = reinterpret_cast<BiasCorr *>(static_cast<uint8_t *>(workspace_dev) + (int64_t)kMaxPartials * 8 + 16);
+  const ScalarArgs sa{clip, (float)max_norm, lr, beta1, beta2, step_dev, sc, total_norm_out, bcw};
   // RTH_ADAM_ONE_PASS=1: one launch when every segment is 16-byte aligned and the chunks fit the
   // resident grid.  Opt-in: alone it is the faster form (16.8 us kernel time for the Q-net), but
   // in the loop its 256 all-resident workgroups wait for CUs the actor stream's convolutions hold
@@ -494,7 +530,7 @@ int rth_clip_adam(const rth_param_tensor *tensors, int32_t n_tensors, double lr,
     RTH_LAUNCHED();
     return RTH_OK;
   }
-  hipLaunchKernelGGL(k_grad_sqsum, dim3((unsigned)blocks), dim3(kOptThreads), 0, s, a, part, step_dev);
+  hipLaunchKernelGGL(k_grad_sqsum, dim3((unsigned)blocks), dim3(kOptThreads), 0, s, a, part, sa);
   RTH_LAUNCHED();
   // 1 - beta1 and 1 - beta2 are python floats in adam.py, rounded to f32 once
   hipLaunchKernelGGL(k_adam, dim3((unsigned)blocks), dim3(kOptThreads), 0, s, a, part, (int)blocks, sa,

@@ -298,6 +298,18 @@ PY
         RTH_LDS_MIN_W1=98304 step lds_w1_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
       done
       summ gpurun_out/lds_*.log ;;
+    adam2)  # clip+Adam: partials + bias corrections read ahead of the chunk (the norm reduced while it is in flight) vs r05's
+      # earlier k_adam (reth_amd/libreth_hip_adamprev.so: the chunk first, every workgroup evaluating the fp64 pow)
+      step adam2_tests 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_optim_gpu.py
+      step adam2_alone_new 120 python scripts/bench_adam.py
+      RTH_LIB_PATH=reth_amd/libreth_hip_adamprev.so step adam2_alone_prev 120 python scripts/bench_adam.py
+      for r in 1 2 3; do
+        step adam2_new_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        RTH_LIB_PATH=reth_amd/libreth_hip_adamprev.so step adam2_prev_$r 300 python bench.py --steps 300 --warmup 5 \
+            --no-cpu-baseline --no-sweep
+      done
+      grep -h clip_adam gpurun_out/adam2_alone_*.log
+      summ gpurun_out/adam2_new_*.log gpurun_out/adam2_prev_*.log ;;
     fcpmc)  # per-kernel durations (x9 GEMM vs reduce) and SQ counters of the FC1 x9 forms at FC_M rows
       fcsum() {  # fcsum DIR: median duration and counters per kernel
         python - "$1" <<'PY'

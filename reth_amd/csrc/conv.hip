@@ -1301,10 +1301,12 @@ static bool find_conv(const rth_conv_shape &s, ConvLaunch *out, int *geom = null
     // (r04: 16 waves and 16-channel tiles measured slower; dropped)
     // RTH_CONV2_SCHED (r05 A/B): static = r04's round-robin tiles; ns2 = 16 x 32-channel half
     // tiles, round-robin; pw2 = half tiles with the channel part fixed per workgroup (half the
-    // LDS: the other stream's workgroups fit beside it -- 0.543-0.544 vs 0.540-0.542 ms/step)
+    // LDS: the other stream's workgroups fit beside it -- 0.543-0.544 vs 0.540-0.542 ms/step);
+    // ts4big (the default since late r05): the ragged last round split into quarter-width units
+    // for launches of >= 4 whole rounds (the learner's 1,024 samples), whole tiles below
     static const ConvLaunch f32 = [] {
       const char *e = getenv("RTH_CONV2_SCHED");
-      const std::string v = e ? e : (CONV2_NS == 2 ? "ns2" : "static");
+      const std::string v = e ? e : (CONV2_NS == 2 ? "ns2" : "ts4big");
       if (v == "ns2") return conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 2, 0>();
       if (v == "pw2") return conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 2, 1>();
       if (v == "ts2") return conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 1, 0, 2>();
@@ -1312,8 +1314,9 @@ static bool find_conv(const rth_conv_shape &s, ConvLaunch *out, int *geom = null
       // ts4big / ts8big: the split form only for launches of >= 4 / >= 8 whole rounds of tiles
       // (r05 A/B, profiles/r05/ab_log.txt: alone at 1,024 samples 53.1 vs 57.9 us = 0.65 of the
       // fp32 peak; in the loop Pong 0.545-0.547 vs 0.543-0.546 ms/step with ts4big, Breakout
-      // 0.885-0.888 vs 0.893-0.898 with ts4big and 0.865-0.874 vs 0.866-0.874 with ts8big --
-      // within the noise, so the whole tiles stay the default)
+      // 0.885-0.888 vs 0.893-0.898 with ts4big and 0.865-0.874 vs 0.866-0.874 with ts8big; on
+      // the late-r05 tree the learner's conv2 57.2-58.1 vs 58.7-59.5 us live and the step equal,
+      // 0.521-0.523 vs 0.521-0.522 ms: ts4big became the default -- the same outputs, bit for bit)
       if (v == "ts4big" || v == "ts8big") {
         ConvLaunch l = conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 1>();
         l.tsfn = conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 1, 0, 4>().fn;

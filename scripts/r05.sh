@@ -310,6 +310,23 @@ PY
       done
       grep -h clip_adam gpurun_out/adam2_alone_*.log
       summ gpurun_out/adam2_new_*.log gpurun_out/adam2_prev_*.log ;;
+    fcrd)  # 128-tile x9 FC1: fragments read term-major (the MFMAs' consumption order) vs mb-major (libreth_hip_fcprev.so)
+      FC_MS=256,512,2048 step fcrd_alone_new 120 python scripts/bench_fc.py
+      RTH_LIB_PATH=reth_amd/libreth_hip_fcprev.so FC_MS=256,512,2048 step fcrd_alone_prev 120 python scripts/bench_fc.py
+      for r in 1 2 3; do
+        step fcrd_new_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        RTH_LIB_PATH=reth_amd/libreth_hip_fcprev.so step fcrd_prev_$r 300 python bench.py --steps 300 --warmup 5 \
+            --no-cpu-baseline --no-sweep
+      done
+      grep -h "M=" gpurun_out/fcrd_alone_*.log | sed "s/rth_fc_f32.*//"
+      summ gpurun_out/fcrd_new_*.log gpurun_out/fcrd_prev_*.log ;;
+    knobab)  # on the late-r05 tree: conv workgroups per CU 1 (RTH_CONV_WG_PER_CU=1) and conv2's split tail for the learner's launch (ts4big) vs default
+      for r in 1 2 3; do
+        step knob_dflt_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        RTH_CONV_WG_PER_CU=1 step knob_wg1_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        RTH_CONV2_SCHED=ts4big step knob_ts4_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+      done
+      summ gpurun_out/knob_*.log ;;
     fcpmc)  # per-kernel durations (x9 GEMM vs reduce) and SQ counters of the FC1 x9 forms at FC_M rows
       fcsum() {  # fcsum DIR: median duration and counters per kernel
         python - "$1" <<'PY'

@@ -406,39 +406,49 @@ __global__ __launch_bounds__(kFfThreads) void k_fc_f32(const float *__restrict__
     }
 }
 
-// y = act(b + sum of the splits' partials, in split order), 4 outputs per thread
+// y = act(b + sum of the splits' partials, in split order), 4 outputs per thread.  Every partial
+// is loaded before the first add (MAXS >= splits loads, unrolled; indices past splits - 1 repeat
+// the last partial and are not added): the runtime-count loop waited for each load in turn, 16
+// dependent round trips for 16 splits (9.6 / 12.1 us per launch in the loop, r05)
+template <int MAXS>
 __device__ __forceinline__ void fc_reduce_wg(int blk, const float *__restrict__ part, int splits, int64_t MN, int N,
                                              const float *__restrict__ bias, int relu, float *__restrict__ y,
                                              int64_t ldy) {
   const int64_t e4 = ((int64_t)blk * 256 + threadIdx.x) * 4;
   if (e4 >= MN) return;
-  f32x4 s = *reinterpret_cast<const f32x4 *>(part + e4);
-  for (int k = 1; k < splits; ++k) {
-    const f32x4 v = *reinterpret_cast<const f32x4 *>(part + (int64_t)k * MN + e4);
+  f32x4 v[MAXS];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) s[j] = radd(s[j], v[j]);
-  }
+  for (int k = 0; k < MAXS; ++k) v[k] = *reinterpret_cast<const f32x4 *>(part + (int64_t)(k < splits ? k : splits - 1) * MN + e4);
+  f32x4 s = v[0];
+#pragma unroll
+  for (int k = 1; k < MAXS; ++k)
+    if (k < splits) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) s[j] = radd(s[j], v[k][j]);
+    }
   const int64_t m = e4 / N;
   const int n = (int)(e4 - m * N);
   f32x4 o;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const float v = radd(s[j], bias ? bias[n + j] : 0.0f);
-    o[j] = relu ? fc_relu(v) : v;
+    const float t = radd(s[j], bias ? bias[n + j] : 0.0f);
+    o[j] = relu ? fc_relu(t) : t;
   }
   *reinterpret_cast<f32x4 *>(y + m * ldy + n) = o;
 }
 
+template <int MAXS>
 __global__ __launch_bounds__(256) void k_fc_reduce(const float *__restrict__ part, int splits, int64_t MN, int N,
                                                    const float *__restrict__ bias, int relu, float *__restrict__ y,
                                                    int64_t ldy) {
-  fc_reduce_wg((int)blockIdx.x, part, splits, MN, N, bias, relu, y, ldy);
+  fc_reduce_wg<MAXS>((int)blockIdx.x, part, splits, MN, N, bias, relu, y, ldy);
 }
 
 // r05: k_fc_reduce's workgroups (blocks [0, nred)) + the device-counted tail rows behind the M
 // fixed rows (k_linear_relu_rows' workgroups, blocks [nred, ...)) in one launch -- the actors'
 // counted FC1 (their terminal stacks: none in most steps) without a launch of its own
 static_assert(kLrThreads == 256, "k_fc_reduce_rows runs k_linear_relu_rows' workgroups at 256 lanes");
+template <int MAXS>
 __global__ __launch_bounds__(256) void k_fc_reduce_rows(const float *__restrict__ part, int splits, int64_t MN, int N,
                                                         const float *__restrict__ bias, float *__restrict__ y,
                                                         int64_t ldy, int nred, const float *__restrict__ x,
@@ -446,9 +456,29 @@ __global__ __launch_bounds__(256) void k_fc_reduce_rows(const float *__restrict_
                                                         const int64_t *__restrict__ n_dev,
                                                         const float *__restrict__ w, int K) {
   if ((int)blockIdx.x < nred)
-    fc_reduce_wg((int)blockIdx.x, part, splits, MN, N, bias, 1, y, ldy);
+    fc_reduce_wg<MAXS>((int)blockIdx.x, part, splits, MN, N, bias, 1, y, ldy);
   else
     linear_relu_rows_wg((int)blockIdx.x - nred, x, ldx, r0, n_max, n_dev, w, bias, K, N, y, ldy);
+}
+
+// the reduce launch of `splits` partials: the smallest unrolled instance that holds them
+static const void *fc_reduce_fn(int splits, bool rows) {
+  if (rows)
+    return splits <= 4    ? reinterpret_cast<const void *>(&k_fc_reduce_rows<4>)
+           : splits <= 8  ? reinterpret_cast<const void *>(&k_fc_reduce_rows<8>)
+           : splits <= 16 ? reinterpret_cast<const void *>(&k_fc_reduce_rows<16>)
+                          : reinterpret_cast<const void *>(&k_fc_reduce_rows<32>);
+  return splits <= 4    ? reinterpret_cast<const void *>(&k_fc_reduce<4>)
+         : splits <= 8  ? reinterpret_cast<const void *>(&k_fc_reduce<8>)
+         : splits <= 16 ? reinterpret_cast<const void *>(&k_fc_reduce<16>)
+                        : reinterpret_cast<const void *>(&k_fc_reduce<32>);
+}
+static int launch_fc_reduce(const float *part, int splits, int64_t MN, int N, const float *bias, int relu, float *y,
+                            int64_t ldy, hipStream_t s) {
+  RTH_REQUIRE(splits >= 1 && splits <= 32, "fc reduce: %d splits", splits);
+  void *args[] = {&part, &splits, &MN, &N, &bias, &relu, &y, &ldy};
+  RTH_HIP(hipLaunchKernel(fc_reduce_fn(splits, false), dim3((unsigned)((MN / 4 + 255) / 256)), dim3(256), args, 0, s));
+  return RTH_OK;
 }
 
 // k splits: about one workgroup per CU (256) over the output tiles, at most 16 and at most the
@@ -573,9 +603,8 @@ int rth_fc_x9(const float *x, int64_t ldx, int64_t M, const float *w, int64_t N,
   RTH_LAUNCHED();
   if (splits > 1) {
     const int64_t MN = M * N;
-    hipLaunchKernelGGL(k_fc_reduce, dim3((unsigned)((MN / 4 + 255) / 256)), dim3(256), 0, s,
-                       static_cast<const float *>(workspace), splits, MN, (int)N, bias, (int)relu, y, N);
-    RTH_LAUNCHED();
+    const int rc = launch_fc_reduce(static_cast<const float *>(workspace), splits, MN, (int)N, bias, (int)relu, y, N, s);
+    if (rc) return rc;
   }
   return RTH_OK;
 }
@@ -604,9 +633,15 @@ int rth_fc_x9_rows_upto(const float *x, int64_t ldx, int64_t M, int64_t n_max, c
   RTH_LAUNCHED();
   const int64_t MN = M * N;
   const int nred = (int)((MN / 4 + 255) / 256), nrows = n_max > M ? (int)((N + kLrCols - 1) / kLrCols) : 0;
-  hipLaunchKernelGGL(k_fc_reduce_rows, dim3((unsigned)(nred + nrows)), dim3(256), 0, s, part, splits, MN, (int)N,
-                     bias, y, (int64_t)N, nred, x, ldx, M, n_max, n_dev, w, (int)K);
-  RTH_LAUNCHED();
+  RTH_REQUIRE(splits <= 32, "rth_fc_x9_rows_upto: %d splits", splits);
+  {
+    const float *cpart = part;
+    int Ni = (int)N, Ki = (int)K;
+    int64_t ldy = N, r0 = M;
+    void *args[] = {&cpart, const_cast<int *>(&splits), const_cast<int64_t *>(&MN), &Ni, &bias, &y, &ldy,
+                    const_cast<int *>(&nred), &x, &ldx, &r0, &n_max, &n_dev, &w, &Ki};
+    RTH_HIP(hipLaunchKernel(fc_reduce_fn(splits, true), dim3((unsigned)(nred + nrows)), dim3(256), args, 0, s));
+  }
   return RTH_OK;
 }
 
@@ -652,9 +687,8 @@ int rth_fc_f32(const float *x, int64_t ldx, int64_t M, const float *w, int64_t N
   RTH_HIP(hipLaunchKernel(fn, dim3((unsigned)(tiles * splits)), dim3(kFfThreads), args, 0, s));
   if (splits > 1) {
     const int64_t MN = M * N;
-    hipLaunchKernelGGL(k_fc_reduce, dim3((unsigned)((MN / 4 + 255) / 256)), dim3(256), 0, s,
-                       static_cast<const float *>(workspace), splits, MN, (int)N, bias, (int)relu, y, N);
-    RTH_LAUNCHED();
+    const int rc = launch_fc_reduce(static_cast<const float *>(workspace), splits, MN, (int)N, bias, (int)relu, y, N, s);
+    if (rc) return rc;
   }
   return RTH_OK;
 }

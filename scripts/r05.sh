@@ -327,6 +327,19 @@ PY
         RTH_CONV2_SCHED=ts4big step knob_ts4_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
       done
       summ gpurun_out/knob_*.log ;;
+    redab)  # FC1 split-K reduce with every partial loaded ahead (unrolled) vs the runtime-count loop (libreth_hip_redprev.so)
+      step red_tests 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_fc_gpu.py
+      RTH_FC_TILE=128 FC_M=256,512 step red_kt_new 120 rocprofv3 --kernel-trace --stats --output-format csv \
+          -d "$PWD/gpurun_out/red_new" -o run -- python scripts/fc_pmc.py
+      RTH_LIB_PATH=reth_amd/libreth_hip_redprev.so FC_M=256,512 step red_kt_prev 120 rocprofv3 --kernel-trace --stats \
+          --output-format csv -d "$PWD/gpurun_out/red_prev" -o run -- python scripts/fc_pmc.py
+      grep -h "reduce" gpurun_out/red_new/run_kernel_stats.csv gpurun_out/red_prev/run_kernel_stats.csv | cut -c1-160
+      for r in 1 2 3; do
+        step red_new_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        RTH_LIB_PATH=reth_amd/libreth_hip_redprev.so step red_prev_$r 300 python bench.py --steps 300 --warmup 5 \
+            --no-cpu-baseline --no-sweep
+      done
+      summ gpurun_out/red_new_*.log gpurun_out/red_prev_*.log ;;
     fcpmc)  # per-kernel durations (x9 GEMM vs reduce) and SQ counters of the FC1 x9 forms at FC_M rows
       fcsum() {  # fcsum DIR: median duration and counters per kernel
         python - "$1" <<'PY'

@@ -340,6 +340,14 @@ PY
             --no-cpu-baseline --no-sweep
       done
       summ gpurun_out/red_new_*.log gpurun_out/red_prev_*.log ;;
+    boprio)  # Breakout (actor stream critical): the actor stream at high priority; conv2 whole tiles (static) vs the ts4big default
+      for r in 1 2; do
+        step boprio_dflt_$r 300 python bench.py --workload breakout --steps 100 --warmup 10 --no-cpu-baseline --no-sweep
+        RTH_ACTOR_PRIORITY=-1 step boprio_hi_$r 300 python bench.py --workload breakout --steps 100 --warmup 10 --no-cpu-baseline --no-sweep
+        RTH_CONV2_SCHED=static step boprio_static_$r 300 python bench.py --workload breakout --steps 100 --warmup 10 \
+            --no-cpu-baseline --no-sweep
+      done
+      summ gpurun_out/boprio_*.log ;;
     fcpmc)  # per-kernel durations (x9 GEMM vs reduce) and SQ counters of the FC1 x9 forms at FC_M rows
       fcsum() {  # fcsum DIR: median duration and counters per kernel
         python - "$1" <<'PY'

@@ -937,18 +937,31 @@ __global__ __launch_bounds__(64 * (COUT_ / 16) * KS) void k_conv_x9(const float 
     const float4 *ym = reinterpret_cast<const float4 *>(ymask + b0 * (int64_t)(COUT * PIX));
     const float4 *Fs = reinterpret_cast<const float4 *>(F);
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);  // channel quad tid % (COUT / 4), in i order
-    for (int i = tid; i < total4; i += NT) {
-      const float4 g = Fs[i], m = ym[i];
-      float4 o;
-      o.x = m.x > 0.0f ? g.x : 0.0f;  // threshold_backward(g, y, 0)
-      o.y = m.y > 0.0f ? g.y : 0.0f;
-      o.z = m.z > 0.0f ? g.z : 0.0f;
-      o.w = m.w > 0.0f ? g.w : 0.0f;
-      yo[i] = o;
-      acc.x = radd(acc.x, o.x);
-      acc.y = radd(acc.y, o.y);
-      acc.z = radd(acc.z, o.z);
-      acc.w = radd(acc.w, o.w);
+    // every mask load of the lane issued before the first use (clamped indices, no load under a
+    // branch): the one-at-a-time loop waited for each in turn, ~5 round trips per workgroup
+    constexpr int UM = (NSAMP * PIX * (COUT / 4) + NT - 1) / NT;
+    float4 mk[UM];
+#pragma unroll
+    for (int u = 0; u < UM; ++u) {
+      const int i = tid + u * NT;
+      mk[u] = ym[i < total4 ? i : 0];
+    }
+#pragma unroll
+    for (int u = 0; u < UM; ++u) {
+      const int i = tid + u * NT;
+      if (i < total4) {
+        const float4 g = Fs[i], m = mk[u];
+        float4 o;
+        o.x = m.x > 0.0f ? g.x : 0.0f;  // threshold_backward(g, y, 0)
+        o.y = m.y > 0.0f ? g.y : 0.0f;
+        o.z = m.z > 0.0f ? g.z : 0.0f;
+        o.w = m.w > 0.0f ? g.w : 0.0f;
+        yo[i] = o;
+        acc.x = radd(acc.x, o.x);
+        acc.y = radd(acc.y, o.y);
+        acc.z = radd(acc.z, o.z);
+        acc.w = radd(acc.w, o.w);
+      }
     }
     __syncthreads();  // every lane is done reading F: its first NT float4 hold the lane sums
     float4 *red = reinterpret_cast<float4 *>(F);

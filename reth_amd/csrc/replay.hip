@@ -507,10 +507,17 @@ __global__ __launch_bounds__(kFrameThreads) void k_frames_push(const uint8_t *__
     }
   };
   const int64_t vecs = frame_bytes / 16;
+  // a frame's vectors, two per lane per round: both loads issued before either store (the
+  // one-at-a-time loop waited for each load in turn); the second index clamped, not branched
   auto copy = [&](const uint8_t *src, int64_t fid) {
     uint4 *d = reinterpret_cast<uint4 *>(store + (fid % fcap) * frame_bytes);
     const uint4 *sv = reinterpret_cast<const uint4 *>(src);
-    for (int64_t v = threadIdx.x; v < vecs; v += kFrameThreads) d[v] = sv[v];
+    for (int64_t v = threadIdx.x; v < vecs; v += 2 * kFrameThreads) {
+      const int64_t v2 = v + kFrameThreads;
+      const uint4 x0 = sv[v], x1 = sv[v2 < vecs ? v2 : v];
+      d[v] = x0;
+      if (v2 < vecs) d[v2] = x1;
+    }
   };
   if (mode == 1) {
     const int64_t st = i * ring_slots + cur_slot[i];

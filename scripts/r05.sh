@@ -348,6 +348,16 @@ PY
             --no-cpu-baseline --no-sweep
       done
       summ gpurun_out/boprio_*.log ;;
+    ldab)  # serialized-load loops made batched: conv3 dgrad's masked epilogue (mask loads ahead), the frame push copy (2 loads
+      # ahead) vs HEAD before them (libreth_hip_ldprev.so)
+      step ld_tests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_conv_gpu.py \
+          tests/test_frame_store_gpu.py
+      for r in 1 2 3; do
+        step ld_new_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        RTH_LIB_PATH=reth_amd/libreth_hip_ldprev.so step ld_prev_$r 300 python bench.py --steps 300 --warmup 5 \
+            --no-cpu-baseline --no-sweep
+      done
+      summ gpurun_out/ld_new_*.log gpurun_out/ld_prev_*.log ;;
     fcpmc)  # per-kernel durations (x9 GEMM vs reduce) and SQ counters of the FC1 x9 forms at FC_M rows
       fcsum() {  # fcsum DIR: median duration and counters per kernel
         python - "$1" <<'PY'

@@ -358,6 +358,23 @@ PY
             --no-cpu-baseline --no-sweep
       done
       summ gpurun_out/ld_new_*.log gpurun_out/ld_prev_*.log ;;
+    deepab)  # tree sample: 512 / 1,024-lane workgroups (one or half a workgroup for B = 512: one staged top) vs 256
+      RTH_LIB_PATH=reth_amd/libreth_hip_deep512.so step deep_tests 300 python -u -m pytest -x -q --timeout 200 \
+          --timeout-method thread tests/test_sumtree_gpu.py tests/test_replay_gpu.py
+      for r in 1 2 3; do
+        step deep_256_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        RTH_LIB_PATH=reth_amd/libreth_hip_deep512.so step deep_512_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        RTH_LIB_PATH=reth_amd/libreth_hip_deep1024.so step deep_1024_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+      done
+      summ gpurun_out/deep_*_[0-9].log ;;
+    deepab2)  # tree sample: 128-lane workgroups (4 for B = 512) vs 256
+      RTH_LIB_PATH=reth_amd/libreth_hip_deep128.so step deep2_tests 300 python -u -m pytest -x -q --timeout 200 \
+          --timeout-method thread tests/test_sumtree_gpu.py tests/test_replay_gpu.py
+      for r in 1 2 3; do
+        step deep2_256_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+        RTH_LIB_PATH=reth_amd/libreth_hip_deep128.so step deep2_128_$r 300 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-sweep
+      done
+      summ gpurun_out/deep2_*_[0-9].log ;;
     fcpmc)  # per-kernel durations (x9 GEMM vs reduce) and SQ counters of the FC1 x9 forms at FC_M rows
       fcsum() {  # fcsum DIR: median duration and counters per kernel
         python - "$1" <<'PY'

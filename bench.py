@@ -193,16 +193,43 @@ def conv_iteration_alone(ax, sizes, reps=20):
     return out
 
 
-def load_traffic(tag, key):
-    """HBM bytes per launch of a kernel from the committed PMC summary of a tagged rocprofv3
-    pass (scripts/summarize_profile.py TAG: separate --pmc FETCH_SIZE / WRITE_SIZE runs,
-    gfx950-corrected) -> (bytes or None, source)"""
+def traffic_signature(world, cfg, frame_ids):
+    """the run configuration a PMC pass's per-launch byte counts belong to: they are quoted in a
+    bench line only when the line's own run has the same signature (a launch's bytes depend on
+    the batch, the actors, the replay form and the world size)"""
+    return {"world": int(world), "num_actions": int(cfg.num_actions), "batch_size": int(cfg.batch_size),
+            "n_actors": int(cfg.n_actors), "capacity": int(cfg.capacity), "frame_store": bool(cfg.frame_store),
+            "frame_ids": bool(frame_ids), "env": cfg.env, "actor_steps_per_update": int(cfg.actor_steps_per_update)}
+
+
+def load_traffic_file(tag, signature):
+    """the committed PMC summary of a tagged rocprofv3 pass (scripts/summarize_profile.py TAG:
+    separate --pmc FETCH_SIZE / WRITE_SIZE runs, gfx950-corrected) -> (dict, source, reason).
+    dict is {} -- every traffic field of the line null -- when the file is absent, records no
+    `measured_on`, or was measured on a different configuration than `signature`; reason says
+    which."""
     p = os.path.join("profiles", f"traffic_{tag}.json")
     full = os.path.join(ROOT, p)
-    if os.path.exists(full):
-        with open(full) as f:
-            return json.load(f).get(key), p
-    return None, None
+    if not os.path.exists(full):
+        return {}, None, f"no PMC pass {p}"
+    with open(full) as f:
+        prof = json.load(f)
+    on = prof.get("measured_on")
+    if on is None:
+        return {}, p, f"{p} does not record the configuration it was measured on"
+    diff = sorted(k for k in set(on) | set(signature) if on.get(k) != signature.get(k))
+    if diff:
+        return {}, p, (f"{p} was measured on a different configuration ("
+                       + ", ".join(f"{k} {on.get(k)!r} vs {signature.get(k)!r} here" for k in diff) + ")")
+    return prof, p, None
+
+
+def traffic_field(prof, src, reason, key):
+    """(bytes or None, source, null_reason) of one traffic field"""
+    v = prof.get(key)
+    if v is None:
+        return None, None, reason or (f"{src} has no {key}" if src else "no PMC pass")
+    return v, src, None
 
 
 def cpu_model():
@@ -493,7 +520,7 @@ def hbm_bytes(cfg, n_rows_per_append):
     }
 
 
-def hbm_rooflines(ax, timer, probe_ms, tag):
+def hbm_rooflines(ax, timer, probe_ms, tprof, tsrc, treason):
     """roofline_hbm: the HBM-bound kernels north_star names (tree insert / sample / priority
     update, n-step + env (k_actor_tail), TD, gather, clip+Adam) -- algorithmic bytes per launch /
     in-loop launch duration, every duration measured live in the probe window: HIP events
@@ -501,7 +528,8 @@ def hbm_rooflines(ax, timer, probe_ms, tag):
     probe graph copies issue between their parts (the actor tail on the actor stream, the
     TD/heads backward and rth_clip_adam on the learner stream).  `traffic` (HBM bytes per
     launch) is PMC data from a separate rocprofv3 pass of the same command, read from
-    profiles/traffic_TAG.json and labelled as such."""
+    profiles/traffic_TAG.json and labelled as such -- null (with the reason) when that pass ran
+    another configuration (load_traffic_file)."""
     cfg = ax.cfg
     nparams = sum(p.numel() for p in ax.solver._params)
     rows = cfg.n_actors  # one append of N rows per actor step (fused actor: the previous step's rows)
@@ -514,11 +542,7 @@ def hbm_rooflines(ax, timer, probe_ms, tag):
     live = {"k_tree_update_sub": "tree_update", "k_tree_sample": "sample", "k_copy_rows (gather)": "gather",
             "k_copy_rows (insert)": "insert"}
     probed = {"k_actor_tail": "actor_tail", "k_td_heads_backward": "td_heads_backward", clip_name: "clip_adam"}
-    prof = {}
-    full = os.path.join(ROOT, "profiles", f"traffic_{tag}.json")
-    if os.path.exists(full):
-        with open(full) as f:
-            prof = json.load(f)
+    hbm = tprof.get("hbm_bytes_per_launch", {})
     out = []
     for name, nbytes in by.items():
         us, n, src = None, 0, None
@@ -529,11 +553,13 @@ def hbm_rooflines(ax, timer, probe_ms, tag):
             ms = probe_ms[probed[name]]
             us, n = float(np.mean(ms)) * 1e3, len(ms)
             src = f"live HIP events around the probe graphs' eager launch in the probe window, {n} launches"
-        traffic = prof.get("hbm_bytes_per_launch", {}).get(name)
+        traffic = hbm.get(name)
         ent = {"kernel": name, "bound": "hbm", "bytes_per_launch": int(nbytes), "mean_launch_us": None,
                "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None, "traffic": traffic,
                "traffic_ratio": round(traffic / nbytes, 3) if traffic else None, "time_source": src,
-               "traffic_source": f"profiles/traffic_{tag}.json (PMC pass)" if traffic else None}
+               "traffic_source": f"{tsrc} (PMC pass)" if traffic else None}
+        if not traffic:
+            ent["traffic_null_reason"] = treason or f"{tsrc} has no entry for {name}"
         if us:
             gbs = nbytes / (us * 1e-6) / 1e9
             ent.update(mean_launch_us=round(us, 2), achieved=round(gbs, 1), frac=round(gbs / HBM_PEAK_GBS, 4))
@@ -913,16 +939,18 @@ def main():
     flops_actor = cfg.n_actors * f * args.actor_steps_per_update
     flops_step = flops_update + flops_actor
     step_s = dt / args.steps
-    traffic, traffic_src = load_traffic(args.tag, "gather_hbm_bytes_per_launch")
-    c2_traffic, c2_src = load_traffic(args.tag, "conv2_learner_hbm_bytes_per_launch")
-    c3_traffic, c3_src = load_traffic(args.tag, "conv3_learner_hbm_bytes_per_launch")
+    tsig = traffic_signature(world, cfg, fids)
+    tprof, tsrc, treason = load_traffic_file(args.tag, tsig)
+    traffic, traffic_src, traffic_null = traffic_field(tprof, tsrc, treason, "gather_hbm_bytes_per_launch")
+    c2_traffic, c2_src, c2_null = traffic_field(tprof, tsrc, treason, "conv2_learner_hbm_bytes_per_launch")
+    c3_traffic, c3_src, c3_null = traffic_field(tprof, tsrc, treason, "conv3_learner_hbm_bytes_per_launch")
     roofline_gather = {
         "kernel": "rth_replay_gather (k_copy_rows: PER-sampled rows, frames %s)"
                   % ("as frame ids (conv1 reads the store)" if fids else
                      "uint8 stacks" if cfg.hip_conv and cfg.channels_last else "u8->f32 NHWC"),
         "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
-        "bytes_per_launch": bytes_launch, "mean_launch_us": round(mean_gather_s * 1e6, 2),
+        "traffic_null_reason": traffic_null, "bytes_per_launch": bytes_launch, "mean_launch_us": round(mean_gather_s * 1e6, 2),
         "launches_timed": len(gather_ms), "isolated_launch_us": round(iso_s * 1e6, 2),
         "isolated_frac": round(bytes_launch / iso_s / 1e9 / HBM_PEAK_GBS, 4),
         "note": "timed in the probe window; the gather overlaps the learner block on a second stream"}
@@ -931,7 +959,7 @@ def main():
 
     torso = [sh for _, sh in ax.solver.q_network._torso_shapes((4, 84, 84), True)]
 
-    def conv_roofline(ms, name, cin, hin, cout, hout, k, stride, flops, traffic, src):
+    def conv_roofline(ms, name, cin, hin, cout, hout, k, stride, flops, traffic, src, null_reason):
         s_ = float(np.mean(ms)) / 1e3
         label, issue, unit_peak = conv_impl(torso[int(name[-1]) - 1], n2)
         r = {
@@ -939,7 +967,7 @@ def main():
                       f"learner's [s0; s1] forward, {n2} samples per launch",
             "bound": "mfma", "achieved": round(flops / s_ / 1e12, 2), "peak": FP32_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": round(flops / s_ / 1e12 / FP32_PEAK_TFLOPS, 4),
-            "traffic": traffic, "traffic_source": src, "flops_per_launch": flops,
+            "traffic": traffic, "traffic_source": src, "traffic_null_reason": null_reason, "flops_per_launch": flops,
             "algorithmic_bytes_per_launch": n2 * (hin * hin * cin + hout * hout * cout) * 4 + cout * k * k * cin * 4 + cout * 4,
             "mean_launch_us": round(s_ * 1e6, 2), "median_launch_us": round(float(np.median(ms)) * 1e3, 2),
             "launches_timed": len(ms),
@@ -956,12 +984,12 @@ def main():
     roofline_conv2 = None
     if conv2_ms:
         roofline_conv2 = conv_roofline(conv2_ms, "conv2", 32, 20, 64, 9, 4, 2, 2.0 * n2 * 9 * 9 * 64 * 32 * 4 * 4,
-                                       c2_traffic, c2_src)
+                                       c2_traffic, c2_src, c2_null)
         roofline = roofline_conv2
     roofline_conv3 = None
     if conv3_ms:
         roofline_conv3 = conv_roofline(conv3_ms, "conv3", 64, 9, 64, 7, 3, 1, 2.0 * n2 * 7 * 7 * 64 * 64 * 3 * 3,
-                                       c3_traffic, c3_src)
+                                       c3_traffic, c3_src, c3_null)
     # `roofline` = the conv kernel with the most time per iteration (its three launches -- learner,
     # target pass, actors -- timed alone at their batch sizes)
     if roofline_conv2 and roofline_conv3:
@@ -1025,7 +1053,8 @@ def main():
                       "achieved_tflops": round(flops_step / step_s / 1e12, 2),
                       "peak_fp32_tflops": FP32_PEAK_TFLOPS},
         "roofline_conv1": conv1,
-        "roofline_hbm": hbm_rooflines(ax, ktimer, conv_ms, args.tag),
+        "roofline_hbm": hbm_rooflines(ax, ktimer, conv_ms, tprof, tsrc, treason),
+        "traffic_measured_on": tprof.get("measured_on") if tprof else None,
         "decoupled_actors": decoupled,
         "cpu_baseline": cpu,
     }

@@ -49,6 +49,11 @@ const char *rth_last_error(void);
 /* development aid: wall-clock ticks (100 MHz) at the phase boundaries of the last tree
  * update launch (start, prefetch, sort, priorities written, levels done) */
 int rth_debug_tree_timing(long long *out9);
+/* how many tree-update top passes timed out waiting for their subtree workgroups since the
+ * library was loaded (the concurrent top workgroup's bounded wait; a timed-out pass leaves the
+ * levels above the subtree roots unwritten rather than maintaining them from stale sums).
+ * Expected 0; the tests assert it. */
+int rth_tree_update_timeouts(int64_t *out);
 /* development aid (a library built with -DRTH_CLOCK_STAMPS only; the product build returns an
  * error): per workgroup of the last fp32-MFMA conv launch (k_conv_bias_relu), the shader-clock
  * and 100 MHz wall-clock ticks around wave 0's work -- out[2 i], out[2 i + 1] for workgroups

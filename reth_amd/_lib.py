@@ -201,6 +201,7 @@ SIGNATURES = {
     "rth_clip_adam_workspace": (c_i64, []),
     "rth_clip_adam_timed_out": (c_i32, [c_vp]),
     "rth_debug_tree_timing": (c_i32, [c_vp]),
+    "rth_tree_update_timeouts": (c_i32, [ctypes.POINTER(c_i64)]),
     "rth_debug_conv_clock": (c_i32, [c_vp, c_i32]),
     "rth_clip_adam": (c_i32, [c_vp, c_i32, c_f64, c_f64, c_f64, c_f64, c_f64, c_vp, c_vp, c_vp, c_vp]),
     # learner -> actor weights slot (perwez PUB/SUB CONFLATE)

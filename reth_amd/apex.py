@@ -171,13 +171,19 @@ class ApexDQN:
         references.  A row lives capacity / N actor steps after its append and its oldest
         frame is at most n + 4 steps older than the append.  Each step adds N frames plus one
         per ended episode, so at most 2 N: "hard" sizes for that worst case -- 2 capacity +
-        2 (n + 16) N, no frame a live row references is ever overwritten, whatever the episode
-        lengths (Pong 1 M rows: 14.1 GB of frames; Breakout 4 M: 56.5 GB).  "expected" sizes for
+        2 (n + 16 + 2 a) N with a = actor_steps_per_update, no frame a live row references is
+        ever overwritten, whatever the episode lengths (Pong 1 M rows: 14.1 GB of frames;
+        Breakout 4 M: 56.5 GB).  With frame ids (cfg.frame_ids) the learner reads a sampled
+        row's frames at learner time, not at gather time: the batch is sampled one iteration
+        ahead (sample-ahead), so up to 2 a actor steps run between a row's sampling -- when it is
+        still live, possibly the oldest -- and conv1's read of its frames, and the 2 a term keeps
+        those frames in the store over that window (12 steps of slack beyond it, the n + 16 vs
+        n + 4).  "expected" sizes for
         the i.i.d. episode-end rate p_done instead -- capacity (1 + 2 p_done), at least
         capacity / 64 of headroom, + (n + 16) N: half the bytes, but a burst of episode ends
         beyond that rate would overwrite frames that old rows still name."""
         if cfg.frame_store_bound == "hard":
-            return 2 * cfg.capacity + 2 * (cfg.n_step + 16) * cfg.n_actors + 16
+            return 2 * cfg.capacity + 2 * (cfg.n_step + 16 + 2 * cfg.actor_steps_per_update) * cfg.n_actors + 16
         if cfg.frame_store_bound != "expected":
             raise ValueError(f"frame_store_bound {cfg.frame_store_bound!r}: 'hard' or 'expected'")
         reset = max(cfg.capacity // 64, int(2 * cfg.capacity * cfg.p_done) + 1)

@@ -294,6 +294,7 @@ __device__ __forceinline__ double priority_of(const UpdArgs &a, double alpha, in
 // loads, [2] top pass start, [3] top pass after its loads and key scan, [4] top pass end,
 // [5] the subtree pass's last workgroup end (a running max: reset by the reader)
 __device__ long long g_upd_clock[10];
+__device__ unsigned long long g_upd_timeouts;  // top-pass waits that timed out (rth_tree_update_timeouts)
 
 // a workgroup barrier that orders LDS only (outstanding global stores are not waited for)
 __device__ __forceinline__ void lds_barrier() {
@@ -902,8 +903,12 @@ __device__ __forceinline__ void tree_top(const UpdArgs &a, int S, TopLds &L, uns
     if (wu >= 0) uv[t] = priority_of(a, alpha, wu);
   }
   __syncthreads();
+  // a timed-out wait (never seen: the extra workgroup is dispatched after every subtree
+  // workgroup) leaves the levels above S unwritten -- maintaining them from level-S sums not
+  // yet written would corrupt them silently -- and is counted (rth_tree_update_timeouts)
+  __shared__ int tmo;
+  if (t == 0) tmo = 0;
   if (nsub) {  // wait for the subtree workgroups (bounded: a timeout is recorded, not hung on)
-    __shared__ int tmo;
     if (t == 0) {
       unsigned *const done = reinterpret_cast<unsigned *>(&a.nd[0].pad);
       unsigned spins = 0;
@@ -914,16 +919,19 @@ __device__ __forceinline__ void tree_top(const UpdArgs &a, int S, TopLds &L, uns
       tmo = spins >= (1u << 24);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (tmo) atomicAdd(reinterpret_cast<unsigned long long *>(&g_upd_clock[9]), 1ull);
+      // re-arm by subtracting this launch's count (not a store of 0): after a timeout the late
+      // workgroups' increments still land and bring the word back to 0
+      __hip_atomic_fetch_sub(done, nsub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (tmo) atomicAdd(&g_upd_timeouts, 1ull);
     }
     __syncthreads();
     load_children();
   }
+  const bool write_top = tmo == 0;  // uniform
   if (a.timing && t == 0) g_upd_clock[6] = wall_clock64();
   // ---- the lane-local levels S-1, S-2, S-3
   TopVal cur{0.0, 0.0, 0};
-  if (lane) {
+  if (lane && write_top) {
     TopVal v1[4], v2[2];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -942,7 +950,7 @@ __device__ __forceinline__ void tree_top(const UpdArgs &a, int S, TopLds &L, uns
   // ---- levels S-4 .. 0 (slot h = S-3-k): left child on this lane, right child 2^(h-1) lanes up
 #pragma unroll
   for (int h = 1; h <= kTopS - 3; ++h) {
-    if (h <= S - 3) {  // uniform
+    if (h <= S - 3 && write_top) {  // uniform
       const int k = S - 3 - h;
       const int d = 1 << (h - 1);
       TopVal R;
@@ -1378,6 +1386,14 @@ int64_t rth_sumtree_capacity(const rth_sumtree *t) { return t ? t->cap : -1; }
 int rth_sumtree_clear(rth_sumtree *t, void *stream) {
   RTH_REQUIRE(t, "rth_sumtree_clear: NULL tree");
   RTH_HIP(hipMemsetAsync(t->nodes, 0, (size_t)(t->cap + 2) * sizeof(Node), as_stream(stream)));
+  return RTH_OK;
+}
+
+int rth_tree_update_timeouts(int64_t *out) {
+  RTH_REQUIRE(out, "rth_tree_update_timeouts: NULL");
+  unsigned long long v = 0;
+  RTH_HIP(hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_upd_timeouts), sizeof(v)));
+  *out = (int64_t)v;
   return RTH_OK;
 }
 

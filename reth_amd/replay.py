@@ -52,6 +52,14 @@ def _prio_tensor(w, device, raw=False):
     return t, (_lib.RTH_F64 if is64 else _lib.RTH_F32)
 
 
+def tree_update_timeouts():
+    """tree-update top passes whose bounded wait for their subtree workgroups timed out since
+    the library was loaded (rth_tree_update_timeouts; expected 0 -- the tests assert it)"""
+    v = ctypes.c_int64(0)
+    call("rth_tree_update_timeouts", ctypes.byref(v))
+    return int(v.value)
+
+
 class SumTree:
     """Device in-order heap sum-tree with NumbaSumTree's interface (fp64, bit-exact)."""
 
@@ -256,6 +264,11 @@ class FrameStacks:
     def stacks(self):
         """the uint8 stacks themselves [n, K, H, W] (a torch gather; not on the hot path)"""
         return self.store[self.ids.long()]
+
+    def cpu(self):
+        """the stacks on the host (host-side consumers -- NumpyLoader, evaluation clients --
+        treat a frame-id column like any other uint8 column)"""
+        return self.stacks().cpu()
 
     @staticmethod
     def pair(a, b):

@@ -76,10 +76,11 @@ class ReplayService:
 
         self.inbox = queue.Queue(maxsize=int(hwm))
         adv = advertise or (host if host not in ("0.0.0.0", "") else "127.0.0.1")
-        self.append_ep = zmtp.Endpoint(b"PULL", lambda f: self.inbox.put(("append", f)), host)
-        self.update_ep = zmtp.Endpoint(b"PULL", lambda f: self.inbox.put(("update", f)), host)
+        mx = dict(max_msg_size=max_msg_size)  # per-message cap on the unauthenticated sockets
+        self.append_ep = zmtp.Endpoint(b"PULL", lambda f: self.inbox.put(("append", f)), host, **mx)
+        self.update_ep = zmtp.Endpoint(b"PULL", lambda f: self.inbox.put(("update", f)), host, **mx)
         reply = []
-        self.meta_ep = zmtp.Endpoint(b"REP", lambda frames: reply, host, port)  # port 0: an unused one
+        self.meta_ep = zmtp.Endpoint(b"REP", lambda frames: reply, host, port, **mx)  # port 0: an unused one
         meta_addr = self.meta_ep.addr(adv)
         self.config = {"capacity": self.capacity, "batch_size": self.batch_size, "lmdb_path": None,
                        "meta_addr": meta_addr, "append_addr": self.append_ep.addr(adv),

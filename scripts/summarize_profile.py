@@ -166,7 +166,14 @@ def main():
                         f"WRITE_KiB={wv:12.1f} hbm_MB={(2 * fv + wv) * 1024 / 1e6:10.2f}\n")
         out = {"correction": "hbm bytes = (2 x FETCH_SIZE + WRITE_SIZE) x 1024 (gfx950 half-counts FETCH_SIZE "
                              "on wide coalesced reads), median over the dispatches of each pass",
-               "passes": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE, separate runs of bench.py"}
+               "passes": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE, separate runs of bench.py",
+               # bench.py traffic_signature of the profiled command: bench quotes these bytes only
+               # in a line whose own run has the same signature (defaults = the default command)
+               "measured_on": {"world": arg("--world", 1), "num_actions": arg("--actions", 6),
+                               "batch_size": arg("--batch", 512), "n_actors": arg("--actors", 256),
+                               "capacity": arg("--capacity", 1_000_000), "frame_store": bool(arg("--frame-store", 1)),
+                               "frame_ids": bool(arg("--frame-ids", 1)), "env": "synthetic",
+                               "actor_steps_per_update": arg("--actor-steps", 1)}}
         key = ("rth::k_copy_rows", LEARNER_GATHER_GRID)
         if key in fe and key in wr:
             out.update({"gather_kernel": "rth::k_copy_rows (learner gather, B=512, 5 columns)",

@@ -12,17 +12,23 @@ def _cfg(**kw):
     return ApexConfig(frame_store=True, **kw)
 
 
-@pytest.mark.parametrize("n_actors,capacity", [(16, 1024), (256, 1_000_000), (2048, 4_000_000), (32, 125_000)])
-def test_hard_bound_covers_worst_case(n_actors, capacity):
+@pytest.mark.parametrize("n_actors,capacity,aps", [(16, 1024, 1), (256, 1_000_000, 1), (2048, 4_000_000, 1),
+                                                  (32, 125_000, 8), (64, 250_000, 4)])
+def test_hard_bound_covers_worst_case(n_actors, capacity, aps):
+    """(32, 125 000, 8): the sharded Pong workload's rank at 8 GPUs (8 actor steps per update)"""
     from reth_amd.apex import ApexDQN
 
-    cfg = _cfg(n_actors=n_actors, capacity=capacity)
+    cfg = _cfg(n_actors=n_actors, capacity=capacity, actor_steps_per_update=aps)
     F = ApexDQN.frame_store_frames(cfg)
     steps_alive = -(-capacity // n_actors)  # FIFO: a row is overwritten capacity / N appends later
     # worst case: every actor ends its episode every step (N tops + N reset frames per step)
-    # over the row's life plus the n + 4 steps before its append that its oldest frame may date from
-    worst = 2 * n_actors * (steps_alive + cfg.n_step + 4)
+    # over the row's life plus the n + 4 steps before its append that its oldest frame may date
+    # from, plus -- frames in place: conv1 reads them at learner time -- the 2 aps actor steps
+    # that may run between the row's sampling (sample-ahead) and the learner's read
+    worst = 2 * n_actors * (steps_alive + cfg.n_step + 4 + 2 * aps)
     assert F >= worst, (F, worst)
+    # and the slack beyond that window is about 12 steps of worst-case pushes
+    assert F - worst >= 2 * n_actors * 11
 
 
 def test_bounds_and_validation():
@@ -30,7 +36,7 @@ def test_bounds_and_validation():
 
     hard = ApexDQN.frame_store_frames(_cfg(n_actors=256, capacity=1_000_000))
     exp = ApexDQN.frame_store_frames(_cfg(n_actors=256, capacity=1_000_000, frame_store_bound="expected"))
-    assert hard == 2 * 1_000_000 + 2 * (3 + 16) * 256 + 16
+    assert hard == 2 * 1_000_000 + 2 * (3 + 16 + 2) * 256 + 16
     assert exp < hard and exp >= 1_000_000  # the expected-rate store: about capacity (1 + 2 p_done)
     with pytest.raises(ValueError):
         ApexDQN.frame_store_frames(_cfg(n_actors=16, capacity=1024, frame_store_bound="tight"))

@@ -21,6 +21,18 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _no_top_pass_timeouts():
+    """every tree update's concurrent top pass found its subtree workgroups done within its
+    bounded wait (a timeout would leave the levels above S stale: ADVICE r05)"""
+    from reth_amd.replay import tree_update_timeouts
+
+    before = tree_update_timeouts()
+    yield
+    torch.cuda.synchronize()
+    assert tree_update_timeouts() == before, "tree-update top pass timed out"
+
+
 def _export(tree):
     s, m, v = tree.export()
     torch.cuda.synchronize()

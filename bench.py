@@ -535,10 +535,9 @@ def hbm_rooflines(ax, timer, probe_ms, tprof, tsrc, treason):
     rows = cfg.n_actors  # one append of N rows per actor step (fused actor: the previous step's rows)
     by = hbm_bytes(cfg, rows)
     # rth_clip_adam = k_grad_sqsum (reads g) + k_adam (reads p, g, m, v; writes p, m, v): 32 B per
-    # fp32 parameter; RTH_ADAM_ONE_PASS=1: k_clip_adam_fused, each once = 28 B
-    clip_name = ("rth_clip_adam (k_clip_adam_fused)" if os.environ.get("RTH_ADAM_ONE_PASS", "0") != "0"
-                 else "rth_clip_adam (k_grad_sqsum + k_adam)")
-    by[clip_name] = nparams * (28 if clip_name.endswith("fused)") else 32)
+    # fp32 parameter
+    clip_name = "rth_clip_adam (k_grad_sqsum + k_adam)"
+    by[clip_name] = nparams * 32
     live = {"k_tree_update_sub": "tree_update", "k_tree_sample": "sample", "k_copy_rows (gather)": "gather",
             "k_copy_rows (insert)": "insert"}
     probed = {"k_actor_tail": "actor_tail", "k_td_heads_backward": "td_heads_backward", clip_name: "clip_adam"}

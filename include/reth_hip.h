@@ -46,9 +46,6 @@ extern "C" {
 #define RTH_FRAMES 8
 
 const char *rth_last_error(void);
-/* development aid: wall-clock ticks (100 MHz) at the phase boundaries of the last tree
- * update launch (start, prefetch, sort, priorities written, levels done) */
-int rth_debug_tree_timing(long long *out9);
 /* how many tree-update top passes timed out waiting for their subtree workgroups since the
  * library was loaded (the concurrent top workgroup's bounded wait; a timed-out pass leaves the
  * levels above the subtree roots unwritten rather than maintaining them from stale sums).
@@ -676,18 +673,11 @@ int rth_atari_synth_reset(uint8_t *reset_raw_dev, int64_t n, int64_t frame_bytes
 /* ------------------------------------------------------------------------------------
  * Learner optimizer step (reth/reth/algorithm/dqn/dqn_solver.py:118-121):
  * torch.nn.utils.clip_grad_norm_(params, max_norm) then torch.optim.Adam.step() over up to
- * RTH_MAX_PARAM_TENSORS fp32 tensors in two launches (norm partials, then the update), or with
- * RTH_ADAM_ONE_PASS=1 in ONE launch (r05: a resident grid of at most one workgroup per CU
- * issues every load, publishes its squared-norm partial as tagged granules, sweeps them all --
- * the grid barrier -- and updates from registers; the gradients are read once) when every
- * tensor is 16-byte aligned and they fit 256 x 8 x 2,048 elements.  max_norm < 0
- * skips clipping.  step_dev (int64, device) is Adam's step count, incremented on the device;
- * workspace_dev holds rth_clip_adam_workspace() bytes, zero-filled once before the first call
- * (it keeps the one-launch form's call counter, which tags that call's granules); one
- * workspace per optimizer.  total_norm_out_dev (nullable) receives the pre-clip 2-norm
- * (clip_grad_norm_'s return).  rth_clip_adam_timed_out: 1 if a one-launch call's grid barrier
- * ever timed out (that call left the parameters unchanged), 0 if not, -1 on error
- * (host-synchronous; tests).
+ * RTH_MAX_PARAM_TENSORS fp32 tensors in two launches (norm partials, then the update).
+ * max_norm < 0 skips clipping.  step_dev (int64, device) is Adam's step count, incremented on
+ * the device; workspace_dev holds rth_clip_adam_workspace() bytes, zero-filled once before the
+ * first call; one workspace per optimizer.  total_norm_out_dev (nullable) receives the pre-clip
+ * 2-norm (clip_grad_norm_'s return).
  * ---------------------------------------------------------------------------------- */
 #define RTH_MAX_PARAM_TENSORS 32
 typedef struct rth_param_tensor {
@@ -698,7 +688,6 @@ typedef struct rth_param_tensor {
   int64_t n;
 } rth_param_tensor;
 int64_t rth_clip_adam_workspace(void);
-int rth_clip_adam_timed_out(const void *workspace_dev);
 int rth_clip_adam(const rth_param_tensor *tensors, int32_t n_tensors, double lr, double beta1, double beta2,
                   double eps, double max_norm, int64_t *step_dev, void *workspace_dev, float *total_norm_out_dev,
                   void *stream);

@@ -199,8 +199,6 @@ SIGNATURES = {
     "rth_atari_synth_raw": (c_i32, [c_vp, c_i64, c_u64, c_vp, c_vp]),
     "rth_atari_synth_reset": (c_i32, [c_vp, c_i64, c_i64, c_u64, c_vp, c_vp, c_vp]),
     "rth_clip_adam_workspace": (c_i64, []),
-    "rth_clip_adam_timed_out": (c_i32, [c_vp]),
-    "rth_debug_tree_timing": (c_i32, [c_vp]),
     "rth_tree_update_timeouts": (c_i32, [ctypes.POINTER(c_i64)]),
     "rth_debug_conv_clock": (c_i32, [c_vp, c_i32]),
     "rth_clip_adam": (c_i32, [c_vp, c_i32, c_f64, c_f64, c_f64, c_f64, c_f64, c_vp, c_vp, c_vp, c_vp]),

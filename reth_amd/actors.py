@@ -22,7 +22,6 @@ Here all N actors of a GPU step together, entirely in HBM:
            inserts (|td| + 1e-6)^alpha into the tree.
 No host synchronisation anywhere in the loop.
 """
-import os
 
 import numpy as np
 import torch
@@ -103,14 +102,8 @@ class VecActors:
         # 512 actors (Breakout: 2,048 actors, the actor stream critical) 0.905 vs 0.954 ms/step
         # (r04); at Pong since the N-row FC1 runs on rth_fc_x9 (late r05: the hipBLASLt 256-row
         # GEMM took as long as the 512-row one, the x9 kernel's time follows the rows) 0.534 vs
-        # 0.542-0.544 ms/step.  RTH_ACTOR_COUNTED_FC=0 / 1 forces it.
-        from .model import fc1_on_hip
-
-        cfc = os.environ.get("RTH_ACTOR_COUNTED_FC")
-        self._counted_fc = (cfc == "1") if cfc in ("0", "1") else (N > 512 or fc1_on_hip(N))
-        # RTH_ACTOR_FC2_CACHE=0: the second layer over all 2N rows and the cache scatter as a
-        # launch of its own (the r03 form, for A/B runs)
-        self._fc2_cache = os.environ.get("RTH_ACTOR_FC2_CACHE", "1") != "0"
+        # 0.542-0.544 ms/step.  The second layer covers the counted rows only and writes the
+        # per-stack heads cache in the same launch (rth_heads_fc2_upto).
         self.fresh = 0       # steps since the actor network's weights last changed
         self.t = 0           # env steps taken (per actor): host mirror of t_dev
         self.t_dev = torch.zeros(1, dtype=torch.int64, device=dev)  # what the kernels read
@@ -298,9 +291,9 @@ class VecActors:
         if hip:  # step counter + acting rows (= cur_slot + _base) in one launch
             call("rth_actor_prologue", ptr(self.t_dev), ptr(self.cur_slot), N, self.ring, ptr(self.hx), s)
             if dedup:  # acting + terminal stacks (device count); the rows' heads are in the cache
-                if self._fc2_cache and q_net._fc2_inplace():  # the second layer over the counted rows, the cache in its launch
-                    q = q_net.forward_heads(self.frames, rows=self.hx[:2 * N], n_dev=self.n_ext,
-                                            n_fixed=N if self._counted_fc else None, cache=(self.qcache, self.hx))
+                if q_net._fc2_inplace():  # the second layer over the counted rows, the cache in its launch
+                    q = q_net.forward_heads(self.frames, rows=self.hx[:2 * N], n_dev=self.n_ext, n_fixed=N,
+                                            cache=(self.qcache, self.hx))
                 else:
                     q = q_net.forward_heads(self.frames, rows=self.hx[:2 * N], n_dev=self.n_ext)
                     self._scatter_heads(q, self.hx, 2 * N)

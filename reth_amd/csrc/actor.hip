@@ -424,14 +424,6 @@ int rth_actor_prologue(int64_t *t_dev, const int64_t *cur_slot, int64_t n, int64
   return RTH_OK;
 }
 
-static bool actor_tail_reg() {  // RTH_ACTOR_TAIL_REG=0: the pointer-form rows (A/B)
-  static const bool v = [] {
-    const char *e = getenv("RTH_ACTOR_TAIL_REG");
-    return !(e && e[0] == '0');
-  }();
-  return v;
-}
-
 int rth_actor_tail(rth_nstep *h, const rth_actor_tail_args *x, int32_t *emit, int64_t *s0_out, int64_t *a_out,
                    float *r_out, int64_t *s1_out, float *done_out, void *stream) {
   RTH_REQUIRE(h && x && emit && s0_out && a_out && r_out && s1_out && done_out, "rth_actor_tail: NULL argument");
@@ -446,7 +438,7 @@ int rth_actor_tail(rth_nstep *h, const rth_actor_tail_args *x, int32_t *emit, in
               x->prev_r, x->prev_done, x->gamma_n, x->td_abs, x->frames, x->ring, x->cur_slot, x->p_reward,
               x->p_done, x->r_out, x->done_out, x->s0_h, x->s1_h, h->st, h->n, h->gamma, h->mode, emit,
               s0_out, a_out, s1_out, r_out, done_out, x->A, x->ext_frames};
-  if (x->A + 1 <= 8 && actor_tail_reg())  // Atari's minimal action sets (Pong 6, Breakout 4)
+  if (x->A + 1 <= 8)  // Atari's minimal action sets (Pong 6, Breakout 4)
     hipLaunchKernelGGL(k_actor_tail<8>, dim3((unsigned)x->N), dim3(kEnvThreads), 0, as_stream(stream), a);
   else
     hipLaunchKernelGGL(k_actor_tail<0>, dim3((unsigned)x->N), dim3(kEnvThreads), 0, as_stream(stream), a);

@@ -1210,15 +1210,11 @@ static ConvLaunch conv_launch() {
   return l;
 }
 
-// RTH_CONV1_NOSHARE=1: r04's kernel (every lane converts its whole window; A/B)
+// conv1 on the uint8 stacks: k_conv1_u8_share (r05: each lane converts half of its window and
+// takes the other half from its neighbour by DPP; bit-identical to r04's k_conv1_u8_bf16x3)
 static ConvLaunch conv1_bf16x3_launch() {
-  static const bool noshare = [] {
-    const char *e = getenv("RTH_CONV1_NOSHARE");
-    return e && atoi(e) != 0;
-  }();
-  ConvLaunch l{noshare ? reinterpret_cast<const void *>(&k_conv1_u8_bf16x3)
-                       : reinterpret_cast<const void *>(&k_conv1_u8_share<false>),
-               reinterpret_cast<const void *>(&k_conv1_pack_bf16x3), 4, kC1PackedBytes, 0, 32, noshare ? 1 : 2, 0, 0,
+  ConvLaunch l{reinterpret_cast<const void *>(&k_conv1_u8_share<false>),
+               reinterpret_cast<const void *>(&k_conv1_pack_bf16x3), 4, kC1PackedBytes, 0, 32, 2, 0, 0,
                {}, nullptr, 0, 0};
   int blocks = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, l.fn, 256, 0) != hipSuccess || blocks < 1) blocks = 1;
@@ -1251,38 +1247,13 @@ static ConvLaunch conv1_bf16x3_launch() {
 #ifndef CONV3_X9_MIN
 #define CONV3_X9_MIN 0
 #endif
-static int64_t env_i64(const char *name, int64_t dflt) {
-  const char *e = getenv(name);
-  return e && *e ? (int64_t)atoll(e) : dflt;
-}
-// hybrid switch points (samples): conv2 runs x9 up to RTH_CONV2_X9_MAX, conv3 runs x9 above
-// RTH_CONV3_X9_MIN (env overrides for A/B sweeps; defaults from the microbench)
-static int64_t conv2_x9_max() {
-  static const int64_t v = env_i64("RTH_CONV2_X9_MAX", CONV2_X9_MAX);
-  return v;
-}
-static int64_t conv3_x9_min() {
-  static const int64_t v = env_i64("RTH_CONV3_X9_MIN", CONV3_X9_MIN);
-  return v;
-}
-// x9 samples per workgroup = n / (CUs * RTH_X9_WG_PER_CU), rounded down to a built instantiation
-static int64_t x9_wg_per_cu() {
-  static const int64_t v = [] {
-    const int64_t x = env_i64("RTH_X9_WG_PER_CU", 1);
-    return x < 1 ? (int64_t)1 : x;
-  }();
-  return v;
-}
-
-// RTH_CONV_F32MFMA=1: conv2 / conv3 forward on the fp32-MFMA kernels instead of the exact
-// bf16x9 split (A/B and parity cross-checks)
-static bool conv_f32mfma() {
-  static const bool v = [] {
-    const char *e = getenv("RTH_CONV_F32MFMA");
-    return e && atoi(e) != 0;
-  }();
-  return v;
-}
+// hybrid switch points (samples; build-time options of variant libraries): conv2 runs x9 up to
+// CONV2_X9_MAX samples (0: never -- its 77-154 KB of LDS per workgroup crowds the other stream's
+// kernels out of the CUs in the loop), conv3 runs x9 above CONV3_X9_MIN (0: always)
+constexpr int64_t conv2_x9_max() { return CONV2_X9_MAX; }
+constexpr int64_t conv3_x9_min() { return CONV3_X9_MIN; }
+// x9 samples per workgroup = n / CUs, rounded down to a built instantiation
+constexpr int64_t x9_wg_per_cu() { return 1; }
 
 // the supported geometries (the Nature-DQN torso on 4 x 84 x 84 stacks)
 static bool find_conv(const rth_conv_shape &s, ConvLaunch *out, int *geom = nullptr) {
@@ -1291,13 +1262,7 @@ static bool find_conv(const rth_conv_shape &s, ConvLaunch *out, int *geom = null
            s.kw == kw && s.stride == st;
   };
   if (is(RTH_CONV_U8_CHW, 4, 84, 84, 32, 8, 8, 4)) {
-    // RTH_CONV1_F32=1: the fp32-MFMA kernel (A/B and parity cross-checks)
-    static const bool f32 = [] {
-      const char *e = getenv("RTH_CONV1_F32");
-      return e && atoi(e) != 0;
-    }();
-    static const ConvLaunch l = f32 ? conv_launch<RTH_CONV_U8_CHW, 8, 8, 4, 4, 32, 84, 84, 4, CONV1_MB>()
-                                    : conv1_bf16x3_launch();
+    static const ConvLaunch l = conv1_bf16x3_launch();
     *out = l;
     if (geom) *geom = 0;
   } else if (is(RTH_CONV_F32_NHWC, 4, 84, 84, 32, 8, 8, 4)) {
@@ -1309,37 +1274,18 @@ static bool find_conv(const rth_conv_shape &s, ConvLaunch *out, int *geom = null
     // standalone the x9 kernel wins below ~400 samples (16 vs 22 us at 256), but in the Ape-X
     // loop its 77-154 KB of LDS per workgroup crowds the concurrent stream's kernels out of the
     // CUs, and the loop ran 0.5-1 % slower with it
-    // RTH_CONV2_NS = 1 / 2 / 4: wave tiles of 16 pixels x 64 / 32 / 16 channels (finer tiles
-    // even out the last round of tiles over the SIMDs)
-    // (r04: 16 waves and 16-channel tiles measured slower; dropped)
-    // RTH_CONV2_SCHED (r05 A/B): static = r04's round-robin tiles; ns2 = 16 x 32-channel half
-    // tiles, round-robin; pw2 = half tiles with the channel part fixed per workgroup (half the
-    // LDS: the other stream's workgroups fit beside it -- 0.543-0.544 vs 0.540-0.542 ms/step);
-    // ts4big (the default since late r05): the ragged last round split into quarter-width units
-    // for launches of >= 4 whole rounds (the learner's 1,024 samples), whole tiles below
+    // the tile schedule (r05 A/B, profiles/r05/ab_log.txt): 16-pixel x 64-channel wave tiles
+    // round-robin, the ragged last round split into quarter-width units for launches of >= 4
+    // whole rounds of tiles (the learner's 1,024 samples: 53.1 vs 57.9 us alone; whole tiles
+    // below) -- the same outputs, bit for bit
     static const ConvLaunch f32 = [] {
-      const char *e = getenv("RTH_CONV2_SCHED");
-      const std::string v = e ? e : (CONV2_NS == 2 ? "ns2" : "ts4big");
-      if (v == "ns2") return conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 2, 0>();
-      if (v == "pw2") return conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 2, 1>();
-      if (v == "ts2") return conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 1, 0, 2>();
-      if (v == "ts4") return conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 1, 0, 4>();
-      // ts4big / ts8big: the split form only for launches of >= 4 / >= 8 whole rounds of tiles
-      // (r05 A/B, profiles/r05/ab_log.txt: alone at 1,024 samples 53.1 vs 57.9 us = 0.65 of the
-      // fp32 peak; in the loop Pong 0.545-0.547 vs 0.543-0.546 ms/step with ts4big, Breakout
-      // 0.885-0.888 vs 0.893-0.898 with ts4big and 0.865-0.874 vs 0.866-0.874 with ts8big; on
-      // the late-r05 tree the learner's conv2 57.2-58.1 vs 58.7-59.5 us live and the step equal,
-      // 0.521-0.523 vs 0.521-0.522 ms: ts4big became the default -- the same outputs, bit for bit)
-      if (v == "ts4big" || v == "ts8big") {
-        ConvLaunch l = conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 1>();
-        l.tsfn = conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 1, 0, 4>().fn;
-        l.tsfn_rounds = v == "ts4big" ? 4 : 8;
-        return l;
-      }
-      return conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 1>();
+      ConvLaunch l = conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 1>();
+      l.tsfn = conv_launch<RTH_CONV_F32_NHWC, 4, 4, 2, 32, 64, 20, 20, 8, CONV2_MB, 1, 0, 4>().fn;
+      l.tsfn_rounds = 4;
+      return l;
     }();
     static const ConvLaunch l = [] {
-      if (conv_f32mfma() || conv2_x9_max() <= 0) return f32;
+      if (conv2_x9_max() <= 0) return f32;
       ConvLaunch h = x9_launch<X9_CONV2>();
       h.big = &f32;
       h.big_above = conv2_x9_max();
@@ -1355,7 +1301,6 @@ static bool find_conv(const rth_conv_shape &s, ConvLaunch *out, int *geom = null
     static const ConvLaunch x9 = x9_launch<X9_CONV3>();
     static const ConvLaunch l = [] {
       ConvLaunch f = conv_launch<RTH_CONV_F32_NHWC, 3, 3, 1, 64, 64, 9, 9, CONV3_WAVES, CONV3_MB, CONV3_NS>();
-      if (conv_f32mfma()) return f;
       if (conv3_x9_min() <= 0) return x9;
       f.big = &x9;
       f.big_above = conv3_x9_min();
@@ -1517,10 +1462,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_dgrad(const float *__restri
   }
 }
 
-static int dgrad_xcd() {  // RTH_DGRAD_XCD=0: the plain class interleave (A/B)
-  static const int v = (int)env_i64("RTH_DGRAD_XCD", 1) != 0;
-  return v;
-}
+constexpr int dgrad_xcd() { return 1; }  // the XCD-aware class interleave (neutral, r03)
 
 struct DgradLaunch {
   const void *fn;
@@ -1968,14 +1910,7 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const float *__restrict__ 
   gw[((oi * KH + kh) * KW + kw) * CIN + ci] = v;
 }
 
-static int wg_per_cu() {  // RTH_CONV_WG_PER_CU (tuning), default 2
-  static int v = [] {
-    const char *e = getenv("RTH_CONV_WG_PER_CU");
-    const int x = e ? atoi(e) : 2;
-    return x >= 1 && x <= 8 ? x : 2;
-  }();
-  return v;
-}
+constexpr int wg_per_cu() { return 2; }
 
 }  // namespace rth
 
@@ -1983,24 +1918,14 @@ using namespace rth;
 
 // conv3's and conv2's data gradients on the exact-split bf16 MFMA (k_conv_x9 with PAD = K - 1
 // and no epilogue; conv2 as its 4 stride-parity classes, one launch, blockIdx.y = class), the
-// flipped kernels packed into a per-device workspace each launch; RTH_DGRAD3_F32=1 /
-// RTH_DGRAD2_F32=1: the fp32-MFMA k_conv_dgrad instead (A/B and parity cross-checks)
+// flipped kernels packed into a per-device workspace each launch (the fp32-MFMA k_conv_dgrad
+// serves the other geometries)
 template <int NS>
 using X9Dgrad3 = X9Geom<3, 3, 1, 64, 11, 11, NS, 3, X9_DGRAD3_KS>;
 template <int NS>
 using X9Dgrad2 = X9Geom<2, 2, 1, 64, 11, 11, NS, 3, X9_DGRAD2_KS, 32>;
-static bool env_set(const char *name) {
-  const char *e = getenv(name);
-  return e && atoi(e) != 0;
-}
-static bool dgrad3_x9() {
-  static const bool v = !env_set("RTH_DGRAD3_F32");
-  return v;
-}
-static bool dgrad2_x9() {  // 37.8 vs 43 us alone, 0.571-0.573 vs 0.574-0.575 ms/step in the loop (r04)
-  static const bool v = !env_set("RTH_DGRAD2_F32");
-  return v;
-}
+constexpr bool dgrad3_x9() { return true; }
+constexpr bool dgrad2_x9() { return true; }  // 37.8 vs 43 us alone, 0.571-0.573 vs 0.574-0.575 ms/step (r04)
 
 static bool is_dgrad3_x9(const rth_conv_shape *shape) {
   return dgrad3_x9() && shape->input == RTH_CONV_F32_NHWC && shape->cin == 64 && shape->hin == 9 && shape->win == 9 &&
@@ -2260,29 +2185,11 @@ static int conv1_relu_wgrad(const rth_conv_shape *shape, const void *x, const in
       RTH_HIP(hipMemsetAsync(deferred[j].db, 0, deferred[j].C * 4, as_stream(stream)));
     return RTH_OK;
   }
-  // RTH_CONV1_F32=1: the fp32-MFMA kernel (A/B and parity cross-checks)
-  static const bool f32 = [] {
-    const char *e = getenv("RTH_CONV1_F32");
-    return e && atoi(e) != 0;
-  }();
-  RTH_REQUIRE(!(f32 && fids), "rth_conv1_frames_relu_wgrad_ex: not built for the fp32-MFMA kernel (RTH_CONV1_F32)");
-  if (f32)
-    hipLaunchKernelGGL((k_conv_wgrad_u8<8, 8, 4, 4, 32, 84, 84>), dim3(kWgBlocks), dim3(kWgWaves * 64), 0,
-                       as_stream(stream), static_cast<const uint8_t *>(x), rows, n, g, y, part);
-  else
-    hipLaunchKernelGGL(fids ? k_conv1_wgrad_bf16x3<2> : (rows ? k_conv1_wgrad_bf16x3<1> : k_conv1_wgrad_bf16x3<0>),
-                       dim3(kWgBlocks), dim3(kWgWaves * 64), 0, as_stream(stream), static_cast<const uint8_t *>(x),
-                       fids ? reinterpret_cast<const int64_t *>(fids) : rows, n, g, y, part);
+  hipLaunchKernelGGL(fids ? k_conv1_wgrad_bf16x3<2> : (rows ? k_conv1_wgrad_bf16x3<1> : k_conv1_wgrad_bf16x3<0>),
+                     dim3(kWgBlocks), dim3(kWgWaves * 64), 0, as_stream(stream), static_cast<const uint8_t *>(x),
+                     fids ? reinterpret_cast<const int64_t *>(fids) : rows, n, g, y, part);
   RTH_LAUNCHED();
-  static const bool wide = [] {  // opt-in: 0.565-0.566 vs 0.563-0.564 ms/step in the loop (r04)
-    const char *e = getenv("RTH_WGRED_WIDE");
-    return e && atoi(e) != 0;
-  }();
-  if (wide)
-    hipLaunchKernelGGL((k_wgrad_reduce16<8, 8, 4, 32>), dim3((32 * 256 + 32 + 15) / 16 + ndeferred), dim3(256), 0,
-                       as_stream(stream), part, kWgBlocks, gw, gb, bj);
-  else
-    hipLaunchKernelGGL((k_wgrad_reduce<8, 8, 4, 32>), dim3((32 * 256 + 32 + 63) / 64 + ndeferred), dim3(256), 0,
+  hipLaunchKernelGGL((k_wgrad_reduce<8, 8, 4, 32>), dim3((32 * 256 + 32 + 63) / 64 + ndeferred), dim3(256), 0,
                      as_stream(stream), part, kWgBlocks, gw, gb, bj);
   RTH_LAUNCHED();
   return RTH_OK;

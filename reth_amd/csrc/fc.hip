@@ -481,69 +481,45 @@ static int launch_fc_reduce(const float *part, int splits, int64_t MN, int N, co
   return RTH_OK;
 }
 
-// k splits: about one workgroup per CU (256) over the output tiles, at most 16 and at most the
-// chunk count; RTH_FC_SPLITS overrides (A/B)
+// k splits of the 64 x 128 tile: about one workgroup per CU (256) over the output tiles, at
+// most 32 and at most the chunk count
 static int fc_splits(int M, int N, int K) {
-  static const int env = [] {
-    const char *e = getenv("RTH_FC_SPLITS");
-    return e ? atoi(e) : 0;
-  }();
   const int tiles = (M / kFcTm) * (N / kFcTn), chunks = K / 32;
-  int s = env > 0 ? env : (256 + tiles - 1) / tiles;
+  int s = (256 + tiles - 1) / tiles;
   s = s < 1 ? 1 : (s > 32 ? 32 : s);
   return s < chunks ? s : chunks;
 }
 
 // which x9 form runs a shape: the 128 x 128 tile (k_fc_x9t) where M and N are multiples of 128,
-// else the 64 x 128 k_fc_x9 (RTH_FC_TILE=64 forces it).  Alone (scripts/bench_fc.py, r05) the 128
-// tile is faster from 1,024 rows (37.5 vs 44.1 us; 2,048: 54 vs 72) and slower below (512: 30.6
-// vs 28.9; 256: 24.6 vs 21.8), but in the loop it is the better one at 512 / 256 rows too:
-// 0.521-0.525 vs 0.531-0.533 ms/step (profiles/r05/ab_log.txt) -- one 96 KB workgroup per CU,
-// a single round of at most 256 workgroups, where the 64 x 128 form's 256 workgroups of 48 KB
-// share CUs with the other stream's kernels.  k splits: about one workgroup per CU, at most
-// RTH_FCT_MAXSPLITS (default 16: at 512 rows 256 workgroups; 24 / 32 splits -- two rounds of
-// workgroups -- 0.533-0.539, 8 splits 0.531-0.534); RTH_FCT_SPLITS overrides (at most 32); never
-// more than the chunk count
+// else the 64 x 128 k_fc_x9.  Alone (scripts/bench_fc.py, r05) the 128 tile is faster from 1,024
+// rows (37.5 vs 44.1 us; 2,048: 54 vs 72) and slower below (512: 30.6 vs 28.9; 256: 24.6 vs
+// 21.8), but in the loop it is the better one at 512 / 256 rows too: 0.521-0.525 vs 0.531-0.533
+// ms/step (profiles/r05/ab_log.txt) -- one 96 KB workgroup per CU, a single round of at most 256
+// workgroups, where the 64 x 128 form's 256 workgroups of 48 KB share CUs with the other
+// stream's kernels.  k splits: about one workgroup per CU, at most 16 (at 512 rows 256
+// workgroups; 24 / 32 splits -- two rounds of workgroups -- 0.533-0.539, 8 splits 0.531-0.534),
+// never more than the chunk count.  r06: a three-deep LDS ring with the MFMA fragments read one
+// chunk ahead (k_fc_x9p, 144 KB per workgroup) was bit-identical and no faster alone (40.4 vs
+// 39.3 us at 1,024 rows) and slower in the loop (0.529 vs 0.520 ms/step): removed.
 struct FcPlan {
   int big, splits;
 };
+constexpr int kFcMaxSplits = 16;
 static FcPlan fc_plan(int M, int N, int K) {
-  static const int tile = [] {
-    const char *e = getenv("RTH_FC_TILE");
-    return e ? atoi(e) : 0;
-  }();
-  static const int env = [] {
-    const char *e = getenv("RTH_FCT_SPLITS");
-    return e ? atoi(e) : 0;
-  }();
-  static const int cap = [] {
-    const char *e = getenv("RTH_FCT_MAXSPLITS");
-    const int v = e ? atoi(e) : 16;
-    return v < 1 ? 1 : (v > 32 ? 32 : v);
-  }();
-  if (tile == 64 || M % kFbTile || N % kFbTile) return FcPlan{0, fc_splits(M, N, K)};
+  if (M % kFbTile || N % kFbTile) return FcPlan{0, fc_splits(M, N, K)};
   const int tiles = (M / kFbTile) * (N / kFbTile), chunks = K / 32;
-  int s = env > 0 ? (env > 32 ? 32 : env) : (256 + tiles - 1) / tiles;
-  if (env <= 0 && s > cap) s = cap;
-  s = s < 1 ? 1 : s;
+  int s = (256 + tiles - 1) / tiles;
+  s = s > kFcMaxSplits ? kFcMaxSplits : (s < 1 ? 1 : s);
   return FcPlan{1, s < chunks ? s : chunks};
 }
 
 // one x9 GEMM launch by plan p into out (y when p.splits == 1, else the partials)
 static void fc_x9_launch(const FcPlan &p, const float *x, int64_t ldx, int M, const float *w, int N, int K,
                          const float *bias, int relu, float *out, hipStream_t s) {
-  if (!p.big) {
+  if (!p.big) {  // two chunks of loads in flight (r04: ahead of one)
     const int tiles = (M / kFcTm) * (N / kFcTn);
-    static const int pf = [] {  // RTH_FC_PF: chunks of loads in flight (1 or 2)
-      const char *e = getenv("RTH_FC_PF");
-      return e && atoi(e) == 1 ? 1 : 2;
-    }();
-    if (pf == 1)
-      hipLaunchKernelGGL(k_fc_x9<1>, dim3((unsigned)(tiles * p.splits)), dim3(kFcThreads), 0, s, x, ldx, M, w, N, K,
-                         p.splits, bias, relu, out);
-    else
-      hipLaunchKernelGGL(k_fc_x9<2>, dim3((unsigned)(tiles * p.splits)), dim3(kFcThreads), 0, s, x, ldx, M, w, N, K,
-                         p.splits, bias, relu, out);
+    hipLaunchKernelGGL(k_fc_x9<2>, dim3((unsigned)(tiles * p.splits)), dim3(kFcThreads), 0, s, x, ldx, M, w, N, K,
+                       p.splits, bias, relu, out);
     return;
   }
   const dim3 grid((unsigned)((M / kFbTile) * (N / kFbTile) * p.splits));
@@ -551,17 +527,11 @@ static void fc_x9_launch(const FcPlan &p, const float *x, int64_t ldx, int M, co
 }
 
 // k_fc_f32's k splits: 8 (one K slice per XCD) while that gives at most 512 workgroups, else
-// fewer; RTH_FCF_SPLITS overrides (A/B); never more than the chunk count
+// fewer; never more than the chunk count
 static int fcf_splits(int M, int N, int K) {
-  static const int env = [] {
-    const char *e = getenv("RTH_FCF_SPLITS");
-    return e ? atoi(e) : 0;
-  }();
   const int tiles = ((M + kFfTm - 1) / kFfTm) * (N / kFfTn), chunks = K / 32;
-  int s = env > 0 ? env : 8;
-  if (env <= 0)
-    while (s > 1 && tiles * s > 512) s /= 2;
-  s = s < 1 ? 1 : (s > 32 ? 32 : s);
+  int s = 8;
+  while (s > 1 && tiles * s > 512) s /= 2;
   return s < chunks ? s : chunks;
 }
 
@@ -674,14 +644,7 @@ int rth_fc_f32(const float *x, int64_t ldx, int64_t M, const float *w, int64_t N
   hipStream_t s = as_stream(stream);
   const int tiles = (int)((M + kFfTm - 1) / kFfTm) * (int)(N / kFfTn);
   float *out = splits == 1 ? y : static_cast<float *>(workspace);
-  static const int nst = [] {  // RTH_FCF_NST: chunks in flight (2, 3 or 4)
-    const char *e = getenv("RTH_FCF_NST");
-    const int v = e ? atoi(e) : 3;
-    return v == 2 || v == 4 ? v : 3;
-  }();
-  const void *fn = nst == 2   ? reinterpret_cast<const void *>(&k_fc_f32<2>)
-                   : nst == 4 ? reinterpret_cast<const void *>(&k_fc_f32<4>)
-                              : reinterpret_cast<const void *>(&k_fc_f32<3>);
+  const void *fn = reinterpret_cast<const void *>(&k_fc_f32<3>);  // 3 chunks in flight (2 / 4: equal or slower, r05)
   int Mi = (int)M, Ni = (int)N, Ki = (int)K, re = (int)relu;
   void *args[] = {&x, &ldx, &Mi, &w, &Ni, &Ki, const_cast<int *>(&splits), &bias, &re, &out};
   RTH_HIP(hipLaunchKernel(fn, dim3((unsigned)(tiles * splits)), dim3(kFfThreads), args, 0, s));

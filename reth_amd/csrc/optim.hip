@@ -251,217 +251,15 @@ __global__ __launch_bounds__(kOptThreads) void k_adam(OptArgs a, const double *_
   }
 }
 
-// ---------------------------------------------------------------------------------------
-// One-launch form (r05): the two launches above read the 6.7 MB of gradients twice (norm
-// partials, then Adam) and pay a kernel boundary between them.  Here a grid of at most one
-// workgroup per CU (all resident: grid <= CUs, 512 threads, ~100 VGPRs) issues EVERY load of its
-// chunks -- gradient, exp_avg, exp_avg_sq, param -- at once, sums its gradient squares, and
-// publishes the fp64 partial as two tagged 8-byte granules (cdna_hip_programming.md Guideline
-// 16, R2: the data is the flag; {tag = epoch, 32 value bits}, relaxed agent-scope atomic stores
-// = write-through).  One wave of every workgroup sweeps all granules until every tag equals
-// this call's epoch -- the grid barrier and the norm's data in one -- then every workgroup sums
-// the partials in workgroup order (deterministic, the same value everywhere) and updates its
-// chunks from the registers the loads landed in.  HBM traffic: the algorithmic 28 B per
-// parameter, once.  epoch = a call counter kept in the workspace (read by every workgroup at
-// entry, advanced by workgroup 0 after its sweep, when every workgroup has read it), so tags
-// left by an earlier call never match; the spin is bounded and a timeout leaves the
-// parameters untouched and sets the workspace's error word.
-constexpr int kFT = 512;                 // threads per workgroup
-constexpr int kFChunk = kFT * 4;         // elements per chunk (one float4 per lane)
-constexpr int kFMaxJ = 8;                // chunks per workgroup at most (template J: 2, 4, 8)
-constexpr int kFMaxGrid = 256;           // workgroups at most (2 granules each; <= the CUs)
-typedef __attribute__((address_space(1))) unsigned long long gu64;
-typedef __attribute__((address_space(1))) unsigned int gu32;
-
-struct FusedWs {  // after the partials block of the workspace (rth_clip_adam_workspace)
-  unsigned int epoch;    // calls completed
-  unsigned int timeout;  // nonzero: a call's grid barrier timed out (parameters not updated)
-};
-
-struct FusedArgs {
-  OptArgs a;
-  int64_t nchunks;
-  ScalarArgs sa;
-  float w1, beta2, w2, eps;
-  unsigned long long *gran;  // [2 * grid] tagged granules
-  FusedWs *fw;
-};
-
-template <int J>
-__global__ __launch_bounds__(kFT) void k_clip_adam_fused(FusedArgs fa) {
-  __shared__ double red[kFT / 64];
-  __shared__ double total_sh;
-  __shared__ int ok_sh;
-  const OptArgs &a = fa.a;
-  gu64 *const gran = (gu64 *)fa.gran;  // agent-scope accesses on global pointers, never flat
-  const int G = gridDim.x, wave = threadIdx.x / 64, lane = threadIdx.x % 64;
-  const unsigned int epoch = *reinterpret_cast<volatile unsigned int *>(&fa.fw->epoch) + 1u;
-  const int64_t t = *reinterpret_cast<volatile int64_t *>(fa.sa.step) + 1;  // Adam's step, advanced below
-  // t is first used after the grid barrier, but workgroup 0 rewrites *step right after it: the
-  // load must have completed before this workgroup publishes (the epoch is in the tags itself)
-  asm volatile("" ::"v"((unsigned int)t), "v"((unsigned int)(t >> 32)) : "memory");
-  float4 gv[J], mv[J], vv[J], pv[J];
-  int segj[J];
-  int64_t basej[J];
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    const int64_t c = blockIdx.x + (int64_t)j * G;
-    const int64_t cc = c < fa.nchunks ? c : fa.nchunks - 1;
-    const int s = seg_of(a, cc);
-    const OptSeg &sg = a.seg[s];
-    segj[j] = s;
-    // a chunk past the last one reads past its segment's end: the range check returns zeros
-    basej[j] = (cc - sg.blk0) * kFChunk + (c < fa.nchunks ? 0 : (int64_t)1 << 40);
-    const int64_t e = basej[j] + 4 * threadIdx.x;
-    // every segment is 16-byte aligned here (the launcher checks): one unconditional dwordx4
-    // per array, the dwords past the segment read zero; the offset fits 32 bits
-    const int64_t eb = e < sg.n ? e : sg.n;
-    gv[j] = ld4b(seg_rsrc(sg.grad, sg.n), eb);
-    mv[j] = ld4b(seg_rsrc(sg.m, sg.n), eb);
-    vv[j] = ld4b(seg_rsrc(sg.v, sg.n), eb);
-    pv[j] = ld4b(seg_rsrc(sg.param, sg.n), eb);
-  }
-  // this workgroup's sum of squares (fp64; lane order, then the waves in order)
-  double acc = 0.0;
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    const double x = gv[j].x, y = gv[j].y, z = gv[j].z, w = gv[j].w;
-    acc = radd(acc, rmul(x, x));
-    acc = radd(acc, rmul(y, y));
-    acc = radd(acc, rmul(z, z));
-    acc = radd(acc, rmul(w, w));
-  }
-  for (int o = 32; o > 0; o >>= 1) acc = radd(acc, __shfl_down(acc, o, 64));
-  if (lane == 0) red[wave] = acc;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double wsum = 0.0;
-    for (int w = 0; w < kFT / 64; ++w) wsum = radd(wsum, red[w]);
-    const unsigned long long bits = __double_as_longlong(wsum);
-    __hip_atomic_store(gran + 2 * blockIdx.x, ((unsigned long long)epoch << 32) | (unsigned int)bits,
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(gran + 2 * blockIdx.x + 1, ((unsigned long long)epoch << 32) | (unsigned int)(bits >> 32),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  // wave 0 sweeps every granule until all carry this epoch; its values are the partials
-  if (wave == 0) {
-    constexpr int PER = kFMaxGrid * 2 / 64;  // granules per lane at the largest grid
-    unsigned int lo[PER / 2], hi[PER / 2];
-    bool ok = false;
-    for (unsigned int spins = 0; spins < (1u << 22); ++spins) {
-      bool mine = true;
-      unsigned long long x0[PER / 2], x1[PER / 2];
-#pragma unroll
-      for (int k = 0; k < PER / 2; ++k) {  // every load of the pass in flight at once (lanes past
-        const int b = lane + 64 * k;       // the grid re-read the last workgroup's granules)
-        const int bc = b < G ? b : G - 1;
-        x0[k] = __hip_atomic_load(gran + 2 * bc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        x1[k] = __hip_atomic_load(gran + 2 * bc + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-#pragma unroll
-      for (int k = 0; k < PER / 2; ++k) {
-        lo[k] = (unsigned int)x0[k];
-        hi[k] = (unsigned int)x1[k];
-        mine = mine && (lane + 64 * k >= G || ((unsigned int)(x0[k] >> 32) == epoch &&
-                                                (unsigned int)(x1[k] >> 32) == epoch));
-      }
-      if (__all(mine)) {
-        ok = true;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-    // the partials in workgroup order: lane l holds workgroups l, l + 64, ...; sum k-major per
-    // lane, then across lanes in a fixed tree -- the same order in every workgroup
-    double part = 0.0;
-#pragma unroll
-    for (int k = 0; k < PER / 2; ++k) {
-      const int b = lane + 64 * k;
-      if (b < G) part = radd(part, __longlong_as_double(((long long)hi[k] << 32) | lo[k]));
-    }
-    for (int o = 32; o > 0; o >>= 1) part = radd(part, __shfl_down(part, o, 64));
-    if (lane == 0) {
-      total_sh = part;
-      ok_sh = ok ? 1 : 0;
-      if (!ok) __hip_atomic_store((gu32 *)(&fa.fw->timeout), 1u, __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  __syncthreads();
-  if (!ok_sh) return;  // the barrier timed out: leave the parameters as they are
-  const float total = (float)sqrt(total_sh);
-  const int clip = fa.sa.clip;
-  float coef = 1.0f;
-  if (clip) {
-    const float c = fa.sa.max_norm / radd(total, 1e-6f);
-    coef = c < 1.0f ? c : 1.0f;
-  }
-  const double bc1 = 1.0 - pow(fa.sa.beta1, (double)t);
-  const double bc2 = 1.0 - pow(fa.sa.beta2, (double)t);
-  const float step_size = (float)(fa.sa.lr / bc1), bc2_sqrt = (float)sqrt(bc2);
-  if (blockIdx.x == 0 && threadIdx.x == 0) {  // every workgroup has read epoch and step by now
-    *fa.sa.step = t;
-    fa.fw->epoch = epoch;
-    *fa.sa.out = OptScalars{coef, step_size, bc2_sqrt, total};
-    if (fa.sa.total_out) *fa.sa.total_out = total;
-  }
-  const float w1 = fa.w1, beta2 = fa.beta2, w2 = fa.w2, eps = fa.eps;
-  auto adam1 = [&](float g, float &m, float &v, float &p) {
-    if (clip) g = rmul(g, coef);
-    m = radd(m, rmul(w1, rsub(g, m)));
-    v = radd(rmul(v, beta2), rmul(rmul(w2, g), g));
-    const float denom = radd(sqrtf(v) / bc2_sqrt, eps);
-    p = radd(p, rmul(-step_size, m) / denom);
-  };
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    const int64_t c = blockIdx.x + (int64_t)j * G;
-    if (c >= fa.nchunks) break;
-    const OptSeg &sg = a.seg[segj[j]];
-    const int64_t e = basej[j] + 4 * threadIdx.x;
-    if (e >= sg.n) continue;
-    adam1(gv[j].x, mv[j].x, vv[j].x, pv[j].x);
-    adam1(gv[j].y, mv[j].y, vv[j].y, pv[j].y);
-    adam1(gv[j].z, mv[j].z, vv[j].z, pv[j].z);
-    adam1(gv[j].w, mv[j].w, vv[j].w, pv[j].w);
-    st4(sg.param, e, sg.n, sg.vec, pv[j]);
-    st4(sg.m, e, sg.n, sg.vec, mv[j]);
-    st4(sg.v, e, sg.n, sg.vec, vv[j]);
-  }
-}
-
-static int cu_count_opt() {
-  static int n = 0;
-  if (!n) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
-                                                 hipSuccess || n < 1)
-      n = 1;
-  }
-  return n;
-}
-
 }  // namespace rth
 
 using namespace rth;
 
 extern "C" {
 
-// [partials: kMaxPartials doubles (the one-launch form: its tagged granules)][OptScalars (the
-// last update's scalars, 16 B)][BiasCorr (k_grad_sqsum -> k_adam, 8 B)][FusedWs at +32: call
-// counter, timeout word]
+// [partials: kMaxPartials doubles][OptScalars (the last update's scalars, 16 B)][BiasCorr
+// (k_grad_sqsum -> k_adam, 8 B)]
 int64_t rth_clip_adam_workspace(void) { return (int64_t)kMaxPartials * 8 + 64; }
-
-// the one-launch form's timeout word (nonzero: a grid barrier timed out and that call left
-// the parameters as they were); a debug / test read, host-synchronous
-int rth_clip_adam_timed_out(const void *workspace_dev) {
-  unsigned int w[2] = {0, 0};
-  if (!workspace_dev) return -1;
-  if (hipMemcpy(w, static_cast<const uint8_t *>(workspace_dev) + (int64_t)kMaxPartials * 8 + 32, 8,
-                hipMemcpyDeviceToHost) != hipSuccess)
-    return -1;
-  return w[1] ? 1 : 0;
-}
 
 int rth_clip_adam(const rth_param_tensor *tensors, int32_t n_tensors, double lr, double beta1, double beta2,
                   double eps, double max_norm, int64_t *step_dev, void *workspace_dev, float *total_norm_out,
@@ -488,48 +286,9 @@ int rth_clip_adam(const rth_param_tensor *tensors, int32_t n_tensors, double lr,
   hipStream_t s = as_stream(stream);
   auto *bcw = reinterpret_cast<BiasCorr *>(static_cast<uint8_t *>(workspace_dev) + (int64_t)kMaxPartials * 8 + 16);
   const ScalarArgs sa{clip, (float)max_norm, lr, beta1, beta2, step_dev, sc, total_norm_out, bcw};
-  // RTH_ADAM_ONE_PASS=1: one launch when every segment is 16-byte aligned and the chunks fit the
-  // resident grid.  Opt-in: alone it is the faster form (16.8 us kernel time for the Q-net), but
-  // in the loop its 256 all-resident workgroups wait for CUs the actor stream's convolutions hold
-  // and the grid barrier waits for the last of them: 37-40 us per call against 31 for the two
-  // launches, and no step-time difference (r05 A/B)
-  int64_t nchunks = 0;
-  for (int i = 0; i < n_tensors; ++i) nchunks += (tensors[i].n + kFChunk - 1) / kFChunk;
-  const int grid = cu_count_opt() < kFMaxGrid ? cu_count_opt() : kFMaxGrid;
-  static const bool two_pass = [] {
-    const char *e = getenv("RTH_ADAM_ONE_PASS");
-    return !(e && atoi(e) != 0);
-  }();
-  bool aligned = true;
-  for (int i = 0; i < n_tensors; ++i) aligned = aligned && a.seg[i].vec;
-  if (!two_pass && aligned && nchunks <= (int64_t)grid * kFMaxJ) {
-    FusedArgs fa{};
-    fa.a = a;
-    int64_t b0 = 0;
-    for (int i = 0; i < n_tensors; ++i) {  // re-chunked at kFChunk
-      fa.a.seg[i].blk0 = b0;
-      b0 += (tensors[i].n + kFChunk - 1) / kFChunk;
-    }
-    fa.nchunks = nchunks;
-    fa.sa = sa;
-    fa.w1 = (float)(1.0 - beta1);
-    fa.beta2 = (float)beta2;
-    fa.w2 = (float)(1.0 - beta2);
-    fa.eps = (float)eps;
-    // workspace: [partials / granules][OptScalars (16 B)][FusedWs (8 B)]
-    fa.gran = static_cast<unsigned long long *>(workspace_dev);
-    fa.fw = reinterpret_cast<FusedWs *>(static_cast<uint8_t *>(workspace_dev) + (int64_t)kMaxPartials * 8 + 32);
-    const int g = nchunks < grid ? (int)nchunks : grid;
-    const int64_t per = (nchunks + g - 1) / g;  // chunks per workgroup
-    if (per <= 2)
-      hipLaunchKernelGGL(k_clip_adam_fused<2>, dim3((unsigned)g), dim3(kFT), 0, s, fa);
-    else if (per <= 4)
-      hipLaunchKernelGGL(k_clip_adam_fused<4>, dim3((unsigned)g), dim3(kFT), 0, s, fa);
-    else
-      hipLaunchKernelGGL(k_clip_adam_fused<8>, dim3((unsigned)g), dim3(kFT), 0, s, fa);
-    RTH_LAUNCHED();
-    return RTH_OK;
-  }
+  // r05 tried one launch with a grid barrier through tagged granules (every load issued once):
+  // faster alone (16.8 us) but 37-40 us per call in the loop, where its all-resident grid waits
+  // for CUs the actor stream's convolutions hold -- removed in r06 (profiles/r05)
   hipLaunchKernelGGL(k_grad_sqsum, dim3((unsigned)blocks), dim3(kOptThreads), 0, s, a, part, sa);
   RTH_LAUNCHED();
   // 1 - beta1 and 1 - beta2 are python floats in adam.py, rounded to f32 once

@@ -786,13 +786,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
   }
 }
 
-static bool fc2_lean() {  // k_heads_fc2_lean for A + 1 <= 8 (RTH_FC2_LEAN=0: the LDS-staged form)
-  static const bool v = [] {
-    const char *e = getenv("RTH_FC2_LEAN");
-    return !(e && e[0] == '0');
-  }();
-  return v;
-}
 
 // rows [r0, min(*n_dev, n_max)) of y = relu(x w^T + b), x [*, F] row stride ldx, w [O, F],
 // y row stride ldy: the device-counted tail of a batch whose first r0 rows a library GEMM
@@ -941,14 +934,6 @@ static int heads_backward_impl(const float *dq, const float *h, int64_t ldh, con
   return RTH_OK;
 }
 
-// RTH_HB_BATCHED=0: the heads-backward reductions one quantity per tree (r03, A/B); the same sums
-static bool hb_batched() {
-  static const bool v = [] {
-    const char *e = getenv("RTH_HB_BATCHED");
-    return !(e && atoi(e) == 0);
-  }();
-  return v;
-}
 
 static int td_heads_backward_impl(const float *q0, const float *q1o, const float *q1t, const int64_t *a,
                                   const float *r, const float *done, const double *isw, int64_t B, int64_t A,
@@ -963,7 +948,7 @@ static int td_heads_backward_impl(const float *q0, const float *q1o, const float
               H2, kTdHbMaxElems);
   const dim3 grid((unsigned)(H2 / kHbCols + 1)), block(kHbThreads);
   const size_t lds = (size_t)B * (A + 1) * 4;
-  if (A + 1 <= 8 && hb_batched())
+  if (A + 1 <= 8)
     hipLaunchKernelGGL((k_td_heads_backward<8, 4>), grid, block, lds, as_stream(stream), q0, q1o, q1t, a, r, done, isw,
                        B, (int)A, gamma_n, double_q, h, ldh, f, H2, td_abs, loss_out, gh, gb1, td_acc);
   else if (A + 1 <= 8)
@@ -1042,7 +1027,7 @@ static int heads_fc2_impl(const float *h, int64_t ldh, int64_t n, int32_t H, int
               "rth_heads_fc2: built for H <= %d, a multiple of 64 (A=%d H=%d)", kFc2MaxH, A, H);
   const dim3 grid((unsigned)((n + 15) / 16)), block(256);
   const size_t lds = (size_t)(A + 1) * H * 4 + 16;  // + the spare slot of the staging writes
-  if (A + 1 <= 8 && fc2_lean())
+  if (A + 1 <= 8)
     hipLaunchKernelGGL((k_heads_fc2_lean<8>), grid, block, 0, as_stream(stream), h, ldh, n, (int)H, (int)A,
                        fc2_params[0], fc2_params[1], fc2_params[2], fc2_params[3], heads, n_dev, cache, cache_rows);
   else if (A + 1 <= 8)

@@ -375,15 +375,6 @@ __global__ void k_uniform_indices(int64_t size, int64_t batch, const double *uni
   idx_out[i] = j < size ? j : size - 1;
 }
 
-// pixels per HWC chunk = 1024 * M (M in 1, 2, 4, 8); RTH_COPY_HWC_M overrides (tuning aid)
-static int hwc_chunk_m() {
-  static const int m = [] {
-    const char *e = getenv("RTH_COPY_HWC_M");
-    const int v = e ? atoi(e) : 1;
-    return (v == 1 || v == 2 || v == 4 || v == 8) ? v : 1;
-  }();
-  return m;
-}
 
 // lay the columns out on the flat grid (see k_copy_rows)
 int launch_copy(CopyArgs &a, hipStream_t s) {
@@ -411,7 +402,7 @@ int launch_copy(CopyArgs &a, hipStream_t s) {
     }
     if (col.conv == CONV_U8_F32_HWC) {
       const int64_t P = nb / col.planes;
-      col.chunk_px = 4 * kCopyThreads * hwc_chunk_m();
+      col.chunk_px = 4 * kCopyThreads;  // 1,024 pixels per HWC chunk
       col.chunk_in = col.chunk_px * col.planes;
       col.chunks = (P + col.chunk_px - 1) / col.chunk_px;
       col.vec = (al % 16 == 0) && P % 4 == 0;
@@ -483,7 +474,7 @@ __global__ __launch_bounds__(kFrameThreads) void k_frames_push(const uint8_t *__
   // the order "every read of the head, then its one write" (the next push reads it after the
   // launch boundary).
   auto advance = [&]() {
-    if (!ticket) return;  // k_frames_advance follows (A/B)
+    if (!ticket) return;
     __syncthreads();  // every lane's use of head is behind it
     if (threadIdx.x == 0) {
       unsigned int *ticket = reinterpret_cast<unsigned int *>(fhead + 1);
@@ -539,23 +530,6 @@ __global__ __launch_bounds__(kFrameThreads) void k_frames_push(const uint8_t *__
     if (threadIdx.x < K) sid[rs * K + threadIdx.x] = (int32_t)(uint32_t)(fid % fcap);
   }
   advance();
-}
-
-// the head past this step's frames in a launch of its own (RTH_FRAMES_ADVANCE_LAUNCH=1: r04's
-// form, A/B aid)
-__global__ __launch_bounds__(kFrameThreads) void k_frames_advance(const float *__restrict__ done, int64_t n, int K,
-                                                                  int mode, int64_t *__restrict__ fhead) {
-  __shared__ int64_t part[kFrameThreads];
-  int64_t c = 0;
-  if (mode == 0)
-    for (int64_t j = threadIdx.x; j < n; j += kFrameThreads) c += done[j] != 0.0f;
-  part[threadIdx.x] = c;
-  __syncthreads();
-  for (int w = kFrameThreads / 2; w > 0; w >>= 1) {
-    if ((int)threadIdx.x < w) part[threadIdx.x] += part[threadIdx.x + w];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) *fhead += mode == 1 ? (int64_t)K * n : n + part[0];
 }
 
 }  // namespace rth
@@ -862,18 +836,11 @@ int rth_replay_push_frames(rth_replay *h, const uint8_t *ring, int64_t n, int32_
   if (n == 0) return RTH_OK;
   const int64_t stack_bytes = (int64_t)stack * h->frame_bytes;
   hipStream_t s = as_stream(stream);
-  static const bool sep_advance = [] {
-    const char *e = getenv("RTH_FRAMES_ADVANCE_LAUNCH");
-    return e && atoi(e) == 1;
-  }();
+  // the head advance (N + the done count) runs in the push launch's last workgroup
   hipLaunchKernelGGL(k_frames_push, dim3((unsigned)n), dim3(kFrameThreads), 0, s, ring, stack_bytes, h->frame_bytes,
                      (int)stack, (int)ring_slots, s0_h, s1_h, done, cur_slot, sid, h->fstore, h->fcap, h->fhead, n,
-                     (int)mode, sep_advance ? 0 : 1);
+                     (int)mode, 1);
   RTH_LAUNCHED();
-  if (sep_advance) {
-    hipLaunchKernelGGL(k_frames_advance, dim3(1), dim3(kFrameThreads), 0, s, done, n, (int)stack, (int)mode, h->fhead);
-    RTH_LAUNCHED();
-  }
   return RTH_OK;
 }
 

@@ -165,12 +165,9 @@ __device__ __forceinline__ int64_t tree_find_group(const Node *__restrict__ nd, 
   }
 }
 
-// levels per round trip of the grouped walk: 0 = one lane per target (tree_find)
-static int find_group_k() {  // read per call: tests switch it
-  const char *e = getenv("RTH_FIND_GROUP");
-  const int v = e ? atoi(e) : 4;
-  return (v == 0 || v == 3 || v == 5) ? v : 4;
-}
+// rth_sumtree_find's walk: lane groups of 2^kFindGroupK lanes taking that many levels per
+// round trip (one pair per lane); one-lane walks take kFindK levels per round trip
+constexpr int kFindGroupK = 4, kFindK = 2, kFindThreads = 64;
 
 __device__ __forceinline__ int64_t tree_find_grouped(const Node *__restrict__ nd, int64_t cap, double w, int gk,
                                                      int base, int sub, int64_t cur = 0, double cval = -1.0) {
@@ -182,14 +179,11 @@ __device__ __forceinline__ int64_t tree_find_grouped(const Node *__restrict__ nd
 }
 
 // The hot top of the tree staged in LDS (north_star: "LDS-staged segment scans for the tree"):
-// every sample workgroup copies {sum, val} of the nodes of the first kTopLevels levels (the
-// nodes every target's walk passes through) with one coalesced pass, then each target walks
-// those levels in LDS -- the same find_step comparisons and subtractions -- and only the levels
-// below go to HBM (the grouped walk, resumed at the node reached).  Returns true when the walk
-// must continue below the staged levels (cur / cval / w hold its state), false when `cur` is
-// already the answer.
-constexpr int kTopLevels = 10;
-constexpr int kTopStaged = (1 << kTopLevels) - 1;  // 1,023 nodes, 16 KB of LDS
+// every sample workgroup copies {sum, val} of the nodes of the first TL levels (the nodes every
+// target's walk passes through; k_tree_sample_deep), then each target walks those levels in
+// LDS -- the same find_step comparisons and subtractions -- and only the levels below go to HBM.
+// Returns true when the walk must continue below the staged levels (cur / cval / w hold its
+// state), false when `cur` is already the answer.
 __device__ __forceinline__ bool lds_top_walk(const double2 *__restrict__ top, int64_t cap, int64_t nstaged,
                                              int64_t &cur, double &cval, double &w) {
   cur = 0;
@@ -202,21 +196,10 @@ __device__ __forceinline__ bool lds_top_walk(const double2 *__restrict__ top, in
   }
 }
 
-// tuning aids: levels per round trip and sample workgroup size (RTH_FIND_K, RTH_SAMPLE_BS)
+// RTH_TREE_PASSES (read per call): the tree update's subtree passes (tree_update_impl)
 static int env_int(const char *name, int dflt) {
   const char *e = getenv(name);
   return e ? atoi(e) : dflt;
-}
-static int find_k() {
-  static const int k = env_int("RTH_FIND_K", 2);
-  return k;
-}
-static int sample_bs() {  // a multiple of 64: a lane group never straddles two waves
-  static const int b = [] {
-    const int v = env_int("RTH_SAMPLE_BS", 64);
-    return v >= 64 && v <= 1024 && v % 64 == 0 ? v : 64;
-  }();
-  return b;
 }
 
 __device__ __forceinline__ double tree_min(const Node *nd) {  // NumbaSumTree.min :109-110
@@ -245,7 +228,6 @@ struct UpdArgs {
   int32_t pre_step;   // st->sched_step += 1 before alpha is read (its step=True on_step)
   int64_t pn;
   int32_t post_tail;  // st->tail += n after every read of it (the append's FIFO advance)
-  int32_t timing;     // record phase timestamps in g_upd_clock (RTH_TREE_TIMING=1)
   int32_t fuse_top;   // 1: the subtree pass's last workgroup runs the top pass; 2: an extra
                       // workgroup of the last subtree launch runs it concurrently (r05); 0: its own launch
   // nullable: the subtree pass stages the top pass's key information here (set when it runs):
@@ -289,11 +271,6 @@ __device__ __forceinline__ double priority_of(const UpdArgs &a, double alpha, in
   return prio_value(a.td_abs, a.td_dtype, alpha, g);
 }
 
-// phase timestamps of the last update (wall clock ticks, 100 MHz; development aid, read by
-// rth_debug_tree_timing): [0] subtree pass start (workgroup 0), [1] workgroup 0 after its
-// loads, [2] top pass start, [3] top pass after its loads and key scan, [4] top pass end,
-// [5] the subtree pass's last workgroup end (a running max: reset by the reader)
-__device__ long long g_upd_clock[10];
 __device__ unsigned long long g_upd_timeouts;  // top-pass waits that timed out (rth_tree_update_timeouts)
 
 // a workgroup barrier that orders LDS only (outstanding global stores are not waited for)
@@ -386,7 +363,6 @@ __global__ __launch_bounds__(kSubThreads) void k_tree_update_sub(UpdArgs a, int 
   const int tid = threadIdx.x;
   const int maxd = a.maxd;
   const int64_t cap = a.cap;
-  if (a.timing && tid == 0 && blockIdx.x == 0) g_upd_clock[0] = wall_clock64();
   int64_t fifo_start;
   double alpha;
   upd_prologue(a, &fifo_start, &alpha);
@@ -584,7 +560,6 @@ __global__ __launch_bounds__(kSubThreads) void k_tree_update_sub(UpdArgs a, int 
       }
     }
     lds_barrier();
-    if (a.timing && tid == 0 && blockIdx.x == 0) g_upd_clock[1] = wall_clock64();
     // ---- levels, deepest first (_numba_maintain_node on every touched node, once)
     for (int L = D; L >= S; --L) {
       if (L >= lt_j && L <= de_j) {
@@ -644,7 +619,6 @@ __global__ __launch_bounds__(kSubThreads) void k_tree_update_sub(UpdArgs a, int 
     scan = pos;
     R = kSubKeys;
   }
-  if (a.timing && tid == 0) atomicMax(&g_upd_clock[5], wall_clock64());  // the last workgroup's end
   unsigned *const ticket = reinterpret_cast<unsigned *>(&a.nd[0].pad);
   if (early) {  // count this workgroup done once its level-S sums (write-through) have landed
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -757,7 +731,6 @@ __device__ __forceinline__ void tree_top(const UpdArgs &a, int S, TopLds &L, uns
   int *const xt = L.xt, *const ukey = L.ukey;
   const int t = threadIdx.x;
   const int64_t cap = a.cap;
-  if (a.timing && t == 0) g_upd_clock[2] = wall_clock64();
   int64_t fifo_start;
   double alpha;
   upd_prologue(a, &fifo_start, &alpha);
@@ -871,7 +844,6 @@ __device__ __forceinline__ void tree_top(const UpdArgs &a, int S, TopLds &L, uns
     if (lane && b < (1 << S)) mb |= ((bot[b >> 5] >> (b & 31)) & 1u) << c;
   }
   }
-  if (a.timing && t == 0) g_upd_clock[3] = wall_clock64();
   // ---- new priorities of this lane's key nodes (before the level loop: it issues no loads,
   // so its stores are never waited for)
   int key1 = 0, key2 = 0, keyr = 0;
@@ -907,7 +879,6 @@ __device__ __forceinline__ void tree_top(const UpdArgs &a, int S, TopLds &L, uns
   // workgroup) leaves the levels above S unwritten -- maintaining them from level-S sums not
   // yet written would corrupt them silently -- and is counted (rth_tree_update_timeouts)
   __shared__ int tmo;
-  if (t == 0) tmo = 0;
   if (nsub) {  // wait for the subtree workgroups (bounded: a timeout is recorded, not hung on)
     if (t == 0) {
       unsigned *const done = reinterpret_cast<unsigned *>(&a.nd[0].pad);
@@ -927,8 +898,7 @@ __device__ __forceinline__ void tree_top(const UpdArgs &a, int S, TopLds &L, uns
     __syncthreads();
     load_children();
   }
-  const bool write_top = tmo == 0;  // uniform
-  if (a.timing && t == 0) g_upd_clock[6] = wall_clock64();
+  const bool write_top = nsub == 0 || tmo == 0;  // uniform (tmo written before the barrier above)
   // ---- the lane-local levels S-1, S-2, S-3
   TopVal cur{0.0, 0.0, 0};
   if (lane && write_top) {
@@ -946,7 +916,6 @@ __device__ __forceinline__ void tree_top(const UpdArgs &a, int S, TopLds &L, uns
     const int64_t i3 = (int64_t)n3 - 1 + t;
     if (i3 < cap) cur = top_node(a, i3, rr[0], keyr & 1, v2[0], v2[1]);
   }
-  if (a.timing && t == 0) g_upd_clock[7] = wall_clock64();
   // ---- levels S-4 .. 0 (slot h = S-3-k): left child on this lane, right child 2^(h-1) lanes up
 #pragma unroll
   for (int h = 1; h <= kTopS - 3; ++h) {
@@ -985,7 +954,6 @@ __device__ __forceinline__ void tree_top(const UpdArgs &a, int S, TopLds &L, uns
       }
     }
   }
-  if (a.timing && t == 0) g_upd_clock[8] = wall_clock64();
   if (staged) {  // re-arm what this lane read (its values are consumed: no load is pending)
     auto clear = [&](int64_t i) {
       __hip_atomic_store(&a.stage[kStageFlags + i], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1008,7 +976,6 @@ __device__ __forceinline__ void tree_top(const UpdArgs &a, int S, TopLds &L, uns
       if (a.pre_step) a.st->sched_step += 1;
       if (a.post_tail) a.st->tail = (fifo_start + a.n) % cap;  // every read of tail is done
     }
-    if (a.timing) g_upd_clock[4] = wall_clock64();
   }
 }
 
@@ -1042,50 +1009,6 @@ __global__ void k_tree_find(const Node *__restrict__ nd, int64_t cap, const doub
   if (fl.sub) return;
   if (idx_out) idx_out[i] = k;
   if (val_out) val_out[i] = nd[k + 1].val;
-}
-
-// _numba_sample (sumtree.py:70-79) and, with is_weights, PERSampler.sample (:24-28)
-// top > 0: the first kTopLevels levels are staged in LDS (lds_top_walk), the walk resumed below
-// them by the grouped walk (gk > 0) or the one-lane walk with kspec levels per round trip
-__global__ void k_tree_sample(const Node *__restrict__ nd, int64_t cap, int64_t batch,
-                              const double *__restrict__ uniforms, uint64_t seed, uint64_t counter,
-                              int is_weights, double beta, const ReplayState *st, rth_schedule beta_s,
-                              int64_t *__restrict__ idx_out, double *__restrict__ out, int kspec, int gk, int top) {
-  __shared__ double2 topl[kTopStaged];
-  const FindLane fl = find_lane(gk);
-  const int64_t i = fl.i;
-  const int64_t nst = top ? (cap < kTopStaged ? cap : kTopStaged) : 0;
-  if (top) {  // every lane takes part in the staging, before any of them may leave
-    for (int64_t j = threadIdx.x; j < nst; j += blockDim.x)
-      topl[j] = *reinterpret_cast<const double2 *>(&nd[j + 1]);  // {sum, val}
-    __syncthreads();
-  }
-  if (i >= batch) return;  // uniform over a group
-  if (st) {  // a replay shard's device state: call counter and beta_s(sched_step)
-    counter = (uint64_t)st->calls;
-    beta = sched_value(beta_s, st->sched_step);
-  }
-  const double total = top ? topl[0].x : nd[1].sum;
-  const double seg = total / (double)batch;
-  const double u = uniforms ? uniforms[i] : philox_uniform(seed, counter, (uint32_t)i, STREAM_SAMPLE);
-  double t = rmul(radd((double)i, u), seg);
-  int64_t k;
-  if (top) {
-    int64_t cur;
-    double cval;
-    if (!lds_top_walk(topl, cap, nst, cur, cval, t)) k = cur;
-    else k = gk ? tree_find_grouped(nd, cap, t, gk, fl.base, fl.sub, cur, cval) : tree_find(nd, cap, t, kspec, cur, cval);
-  } else {
-    k = gk ? tree_find_grouped(nd, cap, t, gk, fl.base, fl.sub) : tree_find(nd, cap, t, kspec);
-  }
-  if (fl.sub) return;
-  const double p = nd[k + 1].val;
-  idx_out[i] = k;
-  if (is_weights) {
-    out[i] = pow(p / tree_min(nd), -beta);
-  } else if (out) {
-    out[i] = p;
-  }
 }
 
 // r05: the sample at its latency floor.  Every workgroup stages the top TL levels of the tree
@@ -1262,34 +1185,26 @@ int tree_update_impl(rth_sumtree *t, const int64_t *idx, int64_t fifo_start, con
     a.pre_step = pend->step ? 1 : 0;
   }
   a.post_tail = post_tail;
-  static const int timing = env_int("RTH_TREE_TIMING", 0);
-  a.timing = timing;
-  // RTH_TREE_FUSE_TOP: 2 = the top pass as a concurrent extra workgroup (r05 default: the key
-  // scan and the records above level S overlap the subtree pass -- Pong 41-42 vs 51-52 us per
-  // launch in the loop, 0.538 vs 0.543 ms/step; it is dispatched last, after every subtree
-  // workgroup, so its bounded wait never holds a slot they need), 1 = run by the subtree
-  // pass's last workgroup (r02-r04), 0 = its own launch (A/B)
-  static const int fuse = env_int("RTH_TREE_FUSE_TOP", 2);
-  a.fuse_top = fuse;
+  // the top pass runs as one more workgroup of the subtree launch (fuse_top 2, r05): its key scan
+  // and its loads of the records above level S overlap the subtree pass (Pong 41-42 vs 51-52 us
+  // per launch in the loop against the r02-r04 form run by the subtree pass's last workgroup);
+  // it is dispatched last, after every subtree workgroup, so its bounded wait never holds a slot
+  // they need.  Trees too shallow for a subtree pass run k_tree_update_top alone.
+  a.fuse_top = 2;
   RTH_REQUIRE(a.pn + a.n < (int64_t(1) << 31), "tree update: at most 2^31 - 1 keys per call");
   const int S = t->maxd + 1 < kTopMinS ? kTopMinS : (t->maxd + 1 < kTopS ? t->maxd + 1 : kTopS);
   if (t->maxd >= S && a.pn + a.n > 0) {  // levels S..maxd: one workgroup per group of subtrees,
-    // the last one to finish (of the last pass) also runs the top pass; deep trees in two
-    // passes split at S1 = S + kSubSplit (RTH_TREE_PASSES=1: one pass, A/B aid)
-    // RTH_TREE_PASSES: 1 / 2 fixed (read per call: tests switch it); unset (0): two passes for
-    // large updates -- Breakout's 2,048-row append is one run of leaves, which a single pass
-    // hands to the one or two workgroups owning its level-S subtrees (alone 56-57 vs 34-35 us)
+    // deep trees in two passes split at S1 = S + kSubSplit.  RTH_TREE_PASSES: 1 / 2 fixed (read
+    // per call: tests drive both shipped forms at every size); unset (0): two passes for large
+    // updates -- Breakout's 2,048-row append is one run of leaves, which a single pass hands to
+    // the one or two workgroups owning its level-S subtrees (alone 56-57 vs 34-35 us)
     const int passes_env = env_int("RTH_TREE_PASSES", 0);
     const int passes = passes_env > 0 ? passes_env : (a.pn + a.n >= kTwoPassKeys ? 2 : 1);
     // fewer workgroups for small updates: less dispatch and L2 traffic beside the learner
     // stream (Pong's 768 keys: 64 workgroups, 0.617-0.620 vs 0.618-0.625 ms/step with 256;
-    // Breakout's 2,560 keys keep 256).  RTH_TREE_GRID fixes it (A/B aid).
-    static const int grid_env = env_int("RTH_TREE_GRID", 0);
-    int grid = grid_env;
-    if (grid <= 0) {
-      grid = kSubGridMin;
-      while (grid < kSubGrid && (int64_t)grid * kSubKeysPerWg < a.pn + a.n) grid *= 2;
-    }
+    // Breakout's 2,560 keys keep 256)
+    int grid = kSubGridMin;
+    while (grid < kSubGrid && (int64_t)grid * kSubKeysPerWg < a.pn + a.n) grid *= 2;
     const int S1 = S + kSubSplit;
     const bool two = passes >= 2 && t->maxd >= S + kSubTwoPassDepth;
     if (two) {
@@ -1300,13 +1215,11 @@ int tree_update_impl(rth_sumtree *t, const int64_t *idx, int64_t fifo_start, con
     }
     const int64_t nsub = int64_t(1) << S;
     const unsigned g_last = (unsigned)(nsub < grid ? nsub : grid);
-    // fuse_top 1: the last pass stages the top pass's keys for its last workgroup; 2: the top
-    // pass is one more workgroup of the launch and scans the keys itself
-    a.stage = a.fuse_top == 2 ? nullptr : t->stage;
-    hipLaunchKernelGGL(k_tree_update_sub, dim3(g_last + (a.fuse_top == 2 ? 1u : 0u)), dim3(kSubThreads), 0, s, a, S,
-                       two ? S1 - 1 : t->maxd, 1);
+    // the top pass is the launch's extra last workgroup and scans the keys itself
+    a.stage = nullptr;
+    hipLaunchKernelGGL(k_tree_update_sub, dim3(g_last + 1u), dim3(kSubThreads), 0, s, a, S, two ? S1 - 1 : t->maxd, 1);
     RTH_LAUNCHED();
-    if (a.fuse_top) return RTH_OK;
+    return RTH_OK;
   }
   hipLaunchKernelGGL(k_tree_update_top, dim3(1), dim3(kTopThreads), 0, s, a, S);
   RTH_LAUNCHED();
@@ -1316,37 +1229,15 @@ int tree_sample_impl(rth_sumtree *t, int64_t batch, const double *uniforms, uint
                      uint64_t counter, int is_weights, double beta, int64_t *idx_out, double *out,
                      hipStream_t s, const ReplayState *st, const rth_schedule *beta_s) {
   if (batch <= 0) return RTH_OK;
-  // RTH_TREE_LDS_TOP=0: no LDS-staged top (the r03 form, A/B); staged, the workgroups are 256
-  // lanes: fewer copies of the staged levels.  Below the staged top the default is the
-  // one-lane walk, one child pair per level (RTH_FIND_K=1): 0.66 MB of HBM per Pong launch
-  // against 1.47 with the 16-lane grouped walk (the r03 default, 1.33 without the top) and
-  // 0.570-0.573 vs 0.573-0.580 ms/step in the loop (r04, interleaved); RTH_FIND_GROUP /
-  // RTH_FIND_K select the others
-  const int top = env_int("RTH_TREE_LDS_TOP", 1) ? 1 : 0;  // read per call: tests switch it
-  // r05 default: k_tree_sample_deep (10 staged levels, RTH_DEEP_K = 2 levels per round trip below);
-  // RTH_TREE_SAMPLE_DEEP=0 gives r04's kernel (and its RTH_TREE_LDS_TOP / RTH_FIND_* forms)
-  if (env_int("RTH_TREE_SAMPLE_DEEP", 1) && top && !getenv("RTH_FIND_GROUP") && !getenv("RTH_FIND_K")) {
-    const int dk = env_int("RTH_DEEP_K", 2);
-    const void *fn = dk == 2 ? reinterpret_cast<const void *>(&k_tree_sample_deep<10, 2>)
-                     : dk == 3 ? reinterpret_cast<const void *>(&k_tree_sample_deep<10, 3>)
-                               : reinterpret_cast<const void *>(&k_tree_sample_deep<10, 4>);
-    const Node *nd = t->nodes;
-    int64_t cap = t->cap;
-    rth_schedule bs_ = beta_s ? *beta_s : rth_schedule{};
-    void *args[] = {(void *)&nd, (void *)&cap, (void *)&batch, (void *)&uniforms, (void *)&seed, (void *)&counter,
-                    (void *)&is_weights, (void *)&beta, (void *)&st, (void *)&bs_, (void *)&idx_out, (void *)&out};
-    RTH_HIP(hipLaunchKernel(fn, dim3((unsigned)((batch + kDeepThreads - 1) / kDeepThreads)), dim3(kDeepThreads), args,
-                            0, s));
-    return RTH_OK;
-  }
-  const int gk = (top && !getenv("RTH_FIND_GROUP")) ? 0 : find_group_k();
-  const int kspec = (top && !getenv("RTH_FIND_K")) ? 1 : find_k();
-  const int bs = top ? 256 : sample_bs();
-  const int64_t lanes = batch << gk;
-  hipLaunchKernelGGL(k_tree_sample, dim3((unsigned)((lanes + bs - 1) / bs)), dim3(bs), 0, s, t->nodes,
-                     t->cap, batch, uniforms, seed, counter, is_weights, beta, st,
-                     beta_s ? *beta_s : rth_schedule{}, idx_out, out, kspec, gk, top);
-  RTH_LAUNCHED();
+  // k_tree_sample_deep (r05): the top 10 levels staged per 256-lane workgroup, then 2 levels per
+  // HBM round trip below (r04's one-level walk, k_tree_sample: 27-33 vs 17-19 us per Pong launch)
+  const Node *nd = t->nodes;
+  int64_t cap = t->cap;
+  rth_schedule bs_ = beta_s ? *beta_s : rth_schedule{};
+  void *args[] = {(void *)&nd, (void *)&cap, (void *)&batch, (void *)&uniforms, (void *)&seed, (void *)&counter,
+                  (void *)&is_weights, (void *)&beta, (void *)&st, (void *)&bs_, (void *)&idx_out, (void *)&out};
+  RTH_HIP(hipLaunchKernel(reinterpret_cast<const void *>(&k_tree_sample_deep<10, 2>),
+                          dim3((unsigned)((batch + kDeepThreads - 1) / kDeepThreads)), dim3(kDeepThreads), args, 0, s));
   return RTH_OK;
 }
 }  // namespace rth
@@ -1397,14 +1288,6 @@ int rth_tree_update_timeouts(int64_t *out) {
   return RTH_OK;
 }
 
-int rth_debug_tree_timing(long long *out9) {
-  RTH_REQUIRE(out9, "rth_debug_tree_timing: NULL");
-  RTH_HIP(hipMemcpyFromSymbol(out9, HIP_SYMBOL(g_upd_clock), 9 * sizeof(long long)));
-  static const long long zero[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  RTH_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_upd_clock), zero, sizeof(zero)));
-  return RTH_OK;
-}
-
 int rth_sumtree_update(rth_sumtree *t, const int64_t *idx, const double *w, int64_t n, void *stream) {
   RTH_REQUIRE(t && (n == 0 || (idx && w)), "rth_sumtree_update: bad arguments");
   return tree_update_impl(t, idx, 0, w, nullptr, RTH_F64, 0.0, n, as_stream(stream), nullptr, nullptr, nullptr, 0);
@@ -1414,10 +1297,9 @@ int rth_sumtree_find(rth_sumtree *t, const double *tg, int64_t n, int64_t *idx_o
                      void *stream) {
   RTH_REQUIRE(t && (n == 0 || tg), "rth_sumtree_find: bad arguments");
   if (n == 0) return RTH_OK;
-  const int bs = sample_bs(), gk = find_group_k();
-  const int64_t lanes = n << gk;
-  hipLaunchKernelGGL(k_tree_find, dim3((unsigned)((lanes + bs - 1) / bs)), dim3(bs), 0, as_stream(stream),
-                     t->nodes, t->cap, tg, n, idx_out, val_out, find_k(), gk);
+  const int64_t lanes = n << kFindGroupK;
+  hipLaunchKernelGGL(k_tree_find, dim3((unsigned)((lanes + kFindThreads - 1) / kFindThreads)), dim3(kFindThreads), 0,
+                     as_stream(stream), t->nodes, t->cap, tg, n, idx_out, val_out, kFindK, kFindGroupK);
   RTH_LAUNCHED();
   return RTH_OK;
 }

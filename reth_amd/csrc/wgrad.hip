@@ -421,14 +421,9 @@ static bool find_wgx(const rth_conv_shape &s, WgxLaunch *out) {
   return true;
 }
 
-// splits per kernel row: about one workgroup per CU over the KH rows (RTH_WGX_SPLITS: A/B),
-// at most kWgfRedMax
+// splits per kernel row: about one workgroup per CU over the KH rows, at most kWgfRedMax
 static int wgx_splits(const WgxLaunch &l) {
-  static const int env = [] {
-    const char *e = getenv("RTH_WGX_SPLITS");
-    return e ? atoi(e) : 0;
-  }();
-  int x = env > 0 ? env : 256 / l.groups;
+  int x = 256 / l.groups;
   return x < 1 ? 1 : (x > kWgfRedMax ? kWgfRedMax : x);
 }
 

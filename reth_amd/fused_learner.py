@@ -23,8 +23,6 @@ path of solver.py (compute_grads with torch.autograd), without the autograd engi
 Only the first B rows of the 2B forward are differentiated: they are contiguous views
 (NHWC, batch-major), so the backward reads them in place.
 """
-import os
-
 import torch
 
 from . import _lib
@@ -34,29 +32,22 @@ from .replay import FrameStacks
 
 
 TD_HB_MAX = 16384  # rth_td_heads_backward keeps B * (A + 1) TD gradient rows in LDS
-# data gradients in rth_conv_dgrad instead of MIOpen (no zero fill): conv2's by default (49
-# vs 61 us alone; 0.615 vs 0.630 ms/step in the loop, where the learner stream is the critical
-# path), conv3's opt-in (RTH_HIP_DGRAD3=1, A/B aid); RTH_MIOPEN_DGRAD=1 restores MIOpen's
-HIP_DGRAD = {1} if os.environ.get("RTH_MIOPEN_DGRAD") is None else set()
-# conv3's on the exact-split bf16 MFMA (rth_conv_dgrad -> k_conv_x9 over the zero-padded gy with
-# the flipped kernel) by default since r04; RTH_MIOPEN_DGRAD3=1 restores MIOpen's
-if os.environ.get("RTH_MIOPEN_DGRAD3") is None and os.environ.get("RTH_MIOPEN_DGRAD") is None:
-    HIP_DGRAD.add(2)
-# conv2 / conv3 weight gradients in a hand-written kernel (deterministic, no zero fill) instead
-# of MIOpen's: RTH_HIP_WGRAD=x9 (rth_conv_wgrad_x9, bf16 MFMA with the exact 3 x 3-term split)
-# or =f32 / =1 (rth_conv_wgrad_f32, fp32 MFMA: 44-47 vs 38 us alone for conv2)
-_wg = os.environ.get("RTH_HIP_WGRAD")
-HIP_WGRAD = None if not _wg else ("x9" if _wg == "x9" else "f32")
-
-
-# the data gradients' flipped kernels packed in the forward's pack launch (rth_conv_pack_many
-# with CONV_PACK_DGRAD jobs; rth_conv_dgrad_prepacked in the backward) instead of one pack
-# launch per data gradient; RTH_DGRAD_PREPACK=0 keeps those (A/B)
-DGRAD_PREPACK = os.environ.get("RTH_DGRAD_PREPACK", "1") != "0"
-# conv3's data gradient applies conv2's ReLU mask and writes conv2's bias-gradient slabs in its
-# own epilogue (rth_conv_dgrad_relu_prepacked): one launch (rth_relu_bias_grad) fewer per
-# update; RTH_DGRAD_MASK=0 keeps the separate launch (A/B)
-DGRAD_MASK = os.environ.get("RTH_DGRAD_MASK", "1") != "0"
+# Module constants (tests patch them to run the alternative kernels; no environment switches):
+# HIP_DGRAD -- the layers whose data gradient runs on rth_conv_dgrad (the exact-split bf16 MFMA,
+# no zero fill) instead of MIOpen: conv2's (4 stride-parity classes in one launch) and conv3's
+# (0.570-0.574 vs 0.575-0.580 ms/step with MIOpen's, r04).
+HIP_DGRAD = {1, 2}
+# HIP_WGRAD -- the conv2 / conv3 weight gradients in a hand-written kernel instead of MIOpen's:
+# None = MIOpen (the default: its find picks are faster in the loop), "x9" = rth_conv_wgrad_x9
+# (bf16 MFMA with the exact 3 x 3-term split, run-to-run deterministic: the frame-store and
+# data-parallel parity tests use it), "f32" = rth_conv_wgrad_f32 (fp32 MFMA)
+HIP_WGRAD = None
+# DGRAD_PREPACK -- the data gradients' flipped kernels packed in the forward's pack launch
+# (rth_conv_pack_many with CONV_PACK_DGRAD jobs) instead of one pack launch per data gradient
+DGRAD_PREPACK = True
+# DGRAD_MASK -- conv3's data gradient applies conv2's ReLU mask and writes conv2's bias-gradient
+# slabs in its own epilogue (rth_conv_dgrad_relu_prepacked): one launch fewer per update
+DGRAD_MASK = True
 
 
 def _net_workspace(net, kind, shape, device):
@@ -184,7 +175,7 @@ def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None, mid=No
             ys.append(y)
             h = y
         feat = h.view(n, -1)  # the (C, H, W) flatten of the NCHW output: a view
-        h1 = fc1_relu(feat, w1, b1, learner=True)
+        h1 = fc1_relu(feat, w1, b1)
         heads = net._heads_fc2(h1) if w2 is None else torch.addmm(b2, h1, w2.t())
         if q1t is None:
             q1t = solver.target_heads(s1)

@@ -6,7 +6,6 @@ reth/reth/algorithm/dqn/dqn_model.py:6-71, so
     with the reference's, and
   * under the same torch.manual_seed the default initialisation is identical.
 """
-import os
 
 import torch
 from torch import nn
@@ -234,8 +233,7 @@ class DQNNetwork(nn.Module):
             if not (0 < n_fixed <= n) or not h.is_contiguous():
                 raise ValueError(f"forward_heads: n_fixed {n_fixed} outside (0, {n}] or features not contiguous")
             h1 = torch.empty((n, O), dtype=torch.float32, device=h.device)
-            if _FC_ROWS_FUSED and _FC_KIND == "x9" and fc1_on_hip(n_fixed) and w1.is_contiguous() and \
-                    lib().rth_fc_x9_supported(n_fixed, O, F):
+            if w1.is_contiguous() and lib().rth_fc_x9_supported(n_fixed, O, F):
                 # the x9 GEMM over the fixed rows, then its split-K reduce and the counted rows in one launch
                 ws = _fc_workspace("rth_fc_x9", h.device, w1, n_fixed, O, F)
                 call("rth_fc_x9_rows_upto", ptr(h), F, n_fixed, n, ptr(n_dev), ptr(w1), O, F, ptr(b1), ptr(h1), ptr(ws),
@@ -435,23 +433,16 @@ class _MergeHeads(torch.autograd.Function):
         return (None, *grads)
 
 
-# FC1 + bias + ReLU: RTH_FC=x9 -> rth_fc_x9 (the exact-split bf16 MFMA, fixed-order split-K),
-# RTH_FC=f32 -> rth_fc_f32 (fp32 MFMA, no LDS), RTH_FC=blas -> hipBLASLt's GEMM with the
-# bias+ReLU epilogue, for batches of at most RTH_FC_MAX_ROWS rows (0, the default: any) where the
-# shape is built; the rest on hipBLASLt.  Since late r05 every FC1 forward but the learner's runs
-# on x9 -- the actors' (256 rows at Pong, 2,048 at Breakout) and the target pass's (512): with the
-# 128 x 128 tile 0.522-0.525 vs 0.532 ms/step at Pong and 0.833 vs 0.851-0.855 at Breakout (the
-# actors' 2,048 rows had been on hipBLASLt), every product exact (a third of the learner's |td|
-# error came from FC1's fp32 chains, DESIGN (c)).  The learner's 1,024-row forward
-# (fc1_relu(learner=True)) stays on hipBLASLt: on x9 0.534-0.539 vs 0.522-0.523 ms/step;
-# RTH_FC_LEARNER=x9 or RTH_FC_X9=1 (r04's switch) put it on x9 too.
-_FC_KIND = os.environ.get("RTH_FC", "x9")
-_FC_MAX_ROWS = int(os.environ.get("RTH_FC_MAX_ROWS", "0") or 0)
-_FC_LEARNER_X9 = os.environ.get("RTH_FC_X9") == "1" or os.environ.get("RTH_FC_LEARNER", "blas") == "x9"
+# FC1 + bias + ReLU of every forward -- the actors' (256 rows at Pong, 2,048 at Breakout), the
+# target pass's (512) and, since r06, the learner's [s0; s1] (1,024) -- runs on rth_fc_x9 (the
+# exact-split bf16 MFMA: every product exact, fixed-order split-K) where the shape is built
+# (rows % 64, N % 128, K % 32), else on hipBLASLt's GEMM with the bias+ReLU epilogue.  The
+# learner's forward moved off hipBLASLt for accuracy: its MT32x64x64 kernel
+# sums each output as one 3,136-term fp32 chain, 4.4x the reference CPU GEMM's local error,
+# which made the end-to-end |td| 2.1x the reference fp32 run's distance from the exact |td|; on
+# x9 it is 1.1x.  Cost in the loop: 0.516 -> 0.520 ms/step (interleaved, 3 rounds,
+# profiles/r06/ab_log.txt).
 _FC_WS = {}
-# the actors' counted FC1 on x9: the split-K reduce and the counted rows in one launch
-# (rth_fc_x9_rows_upto); RTH_FC_ROWS_FUSED=0: rth_fc_x9 + rth_linear_relu_rows_upto (A/B)
-_FC_ROWS_FUSED = os.environ.get("RTH_FC_ROWS_FUSED", "1") != "0"
 
 
 def _fc_workspace(fn, device, w, M, N, K):
@@ -466,28 +457,20 @@ def _fc_workspace(fn, device, w, M, N, K):
     return ws
 
 
-def fc1_on_hip(rows):
-    """whether an FC1 forward of `rows` rows runs on the hand-written rth_fc_{x9,f32} (fc1_relu)"""
-    return _FC_KIND in ("f32", "x9") and (_FC_MAX_ROWS <= 0 or rows <= _FC_MAX_ROWS)
-
-
-def fc1_relu(x, w, b, out=None, learner=False):
-    """relu(x @ w.T + b) (FC1 of both dueling branches): rth_fc_f32 / rth_fc_x9 when selected
-    (RTH_FC) and built for the shape, else one hipBLASLt GEMM with the bias+ReLU epilogue
-    (learner=True: the captured learner's forward, on hipBLASLt unless RTH_FC_LEARNER=x9).  The
-    split-K workspace is keyed by the weight storage, so two networks (the actors', the
-    target's, the learner's -- on different streams) never share one"""
+def fc1_relu(x, w, b, out=None):
+    """relu(x @ w.T + b) (FC1 of both dueling branches): rth_fc_x9 where built for the shape,
+    else one hipBLASLt GEMM with the bias+ReLU epilogue.  The split-K workspace is keyed by the
+    weight storage, so two networks (the actors', the target's, the learner's -- on different
+    streams) never share one"""
     M, K = x.shape
     N = w.shape[0]
-    if _FC_KIND in ("f32", "x9") and x.is_cuda and x.stride(1) == 1 and w.is_contiguous() and \
-            (_FC_MAX_ROWS <= 0 or M <= _FC_MAX_ROWS) and (not learner or _FC_LEARNER_X9):
+    if x.is_cuda and x.stride(1) == 1 and w.is_contiguous():
         from ._lib import call, lib, ptr, stream_ptr
 
-        fn = "rth_fc_" + _FC_KIND
-        if getattr(lib(), fn + "_supported")(M, N, K):
+        if lib().rth_fc_x9_supported(M, N, K):
             y = out if out is not None else torch.empty((M, N), dtype=torch.float32, device=x.device)
-            ws = _fc_workspace(fn, x.device, w, M, N, K)
-            call(fn, ptr(x), x.stride(0), M, ptr(w), N, K, ptr(b), 1, ptr(y), ptr(ws), stream_ptr())
+            ws = _fc_workspace("rth_fc_x9", x.device, w, M, N, K)
+            call("rth_fc_x9", ptr(x), x.stride(0), M, ptr(w), N, K, ptr(b), 1, ptr(y), ptr(ws), stream_ptr())
             return y
     if out is not None:
         return torch._addmm_activation(b, x, w.t(), out=out)
@@ -495,9 +478,9 @@ def fc1_relu(x, w, b, out=None, learner=False):
 
 
 class _LinearReLU(torch.autograd.Function):
-    """relu(x @ w.T + b) as ONE hipBLASLt GEMM with a bias+ReLU epilogue
-    (torch._addmm_activation, which has no autograd formula of its own); the backward is
-    the one autograd derives for linear -> relu (threshold on the output, addmm grads)."""
+    """relu(x @ w.T + b) as one fc1_relu launch (rth_fc_x9, or hipBLASLt's GEMM with a bias+ReLU
+    epilogue: torch._addmm_activation has no autograd formula of its own); the backward is the
+    one autograd derives for linear -> relu (threshold on the output, addmm grads)."""
 
     @staticmethod
     def forward(ctx, x, w, b):

@@ -114,13 +114,8 @@ def test_conv_empty_and_unsupported(dev):
     bad = _shape(_lib.CONV_F32_NHWC, 3, 84, 84, 32, 8, 4)
     assert _lib.lib().rth_conv_supported(_lib.ctypes.byref(bad)) == 0
     assert _lib.lib().rth_conv_packed_bytes(_lib.ctypes.byref(bad)) == 0
-    import os
-
-    # conv2's packed weights: by default one fp32 copy; with the opt-in x9 kernel for small
-    # batches (RTH_CONV2_X9_MAX > 0) the three bf16 terms of the exact split, then the fp32 copy
-    x9 = int(os.environ.get("RTH_CONV2_X9_MAX", "0") or 0) > 0 and not os.environ.get("RTH_CONV_F32MFMA")
-    per = 3 * 2 + 4 if x9 else 4
-    assert _lib.lib().rth_conv_packed_bytes(_lib.ctypes.byref(shape)) == 64 * 32 * 16 * per
+    # conv2's packed weights: one fp32 copy (the fp32-MFMA kernel)
+    assert _lib.lib().rth_conv_packed_bytes(_lib.ctypes.byref(shape)) == 64 * 32 * 16 * 4
     with pytest.raises(_lib.RethHipError, match="not built"):
         _lib.call("rth_conv_bias_relu", _lib.ctypes.byref(bad), x.data_ptr(), None, 1, w.data_ptr(), w.data_ptr(),
                   y.data_ptr(), _lib.stream_ptr())
@@ -324,11 +319,10 @@ def test_conv_dgrad(dev, gi, n):
     got = gx.cpu()
     assert not torch.isnan(got).any()
     torch.testing.assert_close(got.double(), want, rtol=1e-5, atol=1e-5)
-    if not os.environ.get("RTH_DGRAD2_F32" if gi == 1 else "RTH_DGRAD3_F32"):
-        # the exact-split bf16 MFMA (k_conv_x9: every product exact, fp32 sums): within a few
-        # fp32 roundings of the 256- / 576-term sums
-        err = (got.double() - want).abs().max().item()
-        assert err <= 2e-6 * max(1.0, want.abs().max().item()), err
+    # the exact-split bf16 MFMA (k_conv_x9: every product exact, fp32 sums): within a few fp32
+    # roundings of the 256- / 576-term sums
+    err = (got.double() - want).abs().max().item()
+    assert err <= 2e-6 * max(1.0, want.abs().max().item()), err
 
 
 @pytest.mark.parametrize("gi", [1, 2])
@@ -379,8 +373,7 @@ def test_conv_dgrad_prepacked(dev, gi):
     cin, h, wd, cout, k, s = GEOMS[gi]
     shape = _shape(_lib.CONV_F32_NHWC, *GEOMS[gi])
     nbytes = _lib.lib().rth_conv_dgrad_workspace(_lib.ctypes.byref(shape))
-    if nbytes <= 0:
-        pytest.skip("the fp32-MFMA data gradient (RTH_DGRAD*_F32) packs nothing")
+    assert nbytes > 0
     n, ho = 300, (h - k) // s + 1
     g = torch.Generator(device=dev).manual_seed(11 + gi)
     gy = torch.randn((n, cout, ho, ho), device=dev, generator=g).contiguous(memory_format=torch.channels_last)
@@ -421,8 +414,7 @@ def test_conv_dgrad_relu_prepacked(dev, n):
 
     cin, h, wd, cout, k, s = GEOMS[2]
     shape = _shape(_lib.CONV_F32_NHWC, *GEOMS[2])
-    if not _lib.lib().rth_conv_dgrad_relu_supported(_lib.ctypes.byref(shape)):
-        pytest.skip("conv3's data gradient is not the x9 kernel (RTH_DGRAD3_F32)")
+    assert _lib.lib().rth_conv_dgrad_relu_supported(_lib.ctypes.byref(shape))
     ho = (h - k) // s + 1
     g = torch.Generator(device=dev).manual_seed(500 + n)
     gy = torch.randn((n, cout, ho, ho), device=dev, generator=g).contiguous(memory_format=torch.channels_last)
@@ -613,7 +605,7 @@ def test_conv_fp32_grade_accuracy(dev, gi, n):
 
 def test_conv_impl_selection(dev):
     """rth_conv_impl names the kernel a launch runs: conv1 on uint8 stacks the bf16x3 kernel,
-    conv2 the fp32-MFMA kernel (x9 opt-in below RTH_CONV2_X9_MAX), conv3 the x9 kernel with the
+    conv2 the fp32-MFMA kernel, conv3 the x9 kernel with the
     samples per workgroup of the cost model (one round of at most 4-sample workgroups on 256
     CUs when the batch allows)"""
     import ctypes
@@ -621,8 +613,6 @@ def test_conv_impl_selection(dev):
 
     from reth_amd import _lib
 
-    if os.environ.get("RTH_CONV_F32MFMA") or os.environ.get("RTH_CONV2_X9_MAX") or os.environ.get("RTH_CONV3_X9_MIN"):
-        pytest.skip("non-default conv selection in the environment")
     ns = ctypes.c_int32(-1)
     impl = lambda sh, n: (_lib.lib().rth_conv_impl(ctypes.byref(sh), n, ctypes.byref(ns)), ns.value)
     u8 = _shape(_lib.CONV_U8_CHW, *GEOMS[0])
@@ -630,7 +620,7 @@ def test_conv_impl_selection(dev):
     assert impl(_shape(_lib.CONV_F32_NHWC, *GEOMS[1]), 256) == (_lib.CONV_IMPL_F32, 0)
     c3 = _shape(_lib.CONV_F32_NHWC | _lib.CONV_OUT_NCHW, *GEOMS[2])
     cus = torch.cuda.get_device_properties(dev).multi_processor_count
-    slots = cus * max(1, int(os.environ.get("RTH_X9_WG_PER_CU") or 1))  # workgroups per round (the model's)
+    slots = cus  # workgroups per round (the model's: one x9 workgroup per CU)
     for n in (1, cus // 2, cus, 2 * cus, 3 * cus, 4 * cus, 6 * cus):
         kind, s = impl(c3, n)
         assert kind == _lib.CONV_IMPL_X9 and 1 <= s <= 4, (n, kind, s)
@@ -638,127 +628,6 @@ def test_conv_impl_selection(dev):
         # the chosen instantiation's estimated time is the least of the built ones
         assert all(rounds(s) * (s + 0.5) <= rounds(q) * (q + 0.5) for q in (1, 2, 3, 4)), (n, s)
     assert impl(c3, 0)[0] == 0 and impl(_shape(_lib.CONV_F32_NHWC, 3, 84, 84, 32, 8, 4), 8)[0] == 0
-
-
-_C1_CHILD = r'''
-import sys, torch
-sys.path.insert(0, sys.argv[1])
-from reth_amd import _lib
-dev = torch.device("cuda")
-g = torch.Generator(device=dev).manual_seed(11)
-shape = _lib.ConvShape(_lib.CONV_U8_CHW, 4, 84, 84, 32, 8, 8, 4)
-wt = (torch.randn((32, 4, 8, 8), device=dev, generator=g) * 0.05).contiguous(memory_format=torch.channels_last)
-b = torch.randn(32, device=dev, generator=g) * 0.1
-pk = torch.empty(_lib.lib().rth_conv_packed_bytes(_lib.ctypes.byref(shape)) // 4, device=dev)
-_lib.call("rth_conv_pack", _lib.ctypes.byref(shape), wt.data_ptr(), pk.data_ptr(), _lib.stream_ptr())
-out = {}
-for n in (1, 2, 3, 7, 31, 64, 513):
-    x = torch.randint(0, 256, (n + 5, 4, 84, 84), dtype=torch.uint8, device=dev, generator=g)
-    rows = torch.randperm(n + 5, device=dev, generator=g)[:n].contiguous()
-    for tag, r in (("plain", None), ("rows", rows)):
-        y = torch.full((n, 20, 20, 32), float("nan"), device=dev)
-        _lib.call("rth_conv_bias_relu", _lib.ctypes.byref(shape), x.data_ptr(), None if r is None else r.data_ptr(), n,
-                  pk.data_ptr(), b.data_ptr(), y.data_ptr(), _lib.stream_ptr())
-        out[f"{tag}{n}"] = y.cpu()
-    cnt = torch.tensor([max(n - 2, 0)], dtype=torch.int64, device=dev)  # a device count below n
-    y = torch.full((n, 20, 20, 32), float("nan"), device=dev)
-    _lib.call("rth_conv_bias_relu_upto", _lib.ctypes.byref(shape), x.data_ptr(), rows.data_ptr(), n, cnt.data_ptr(),
-              pk.data_ptr(), b.data_ptr(), y.data_ptr(), _lib.stream_ptr())
-    out[f"upto{n}"] = y.cpu()
-torch.save(out, sys.argv[2])
-'''
-
-
-def test_conv1_shared_conversion_bit_identical(tmp_path, dev):
-    """k_conv1_u8_share (each byte converted once per horizontal window pair, the second half
-    of a window from the next lane) against r04's k_conv1_u8_bf16x3 (RTH_CONV1_NOSHARE=1): the
-    same products in the same order, so every output bit-identical -- ragged tiles (n = 1 .. 513
-    samples: 420 virtual pixels per sample, 31 per tile), row-indexed stacks, a device count below
-    n (rows past it untouched: NaN)"""
-    import subprocess
-    import sys
-
-    if torch.cuda.is_initialized():
-        torch.cuda.synchronize()
-        torch.cuda.empty_cache()
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    res = {}
-    for mode in ("share", "noshare"):
-        env = dict(os.environ, RTH_CONV1_NOSHARE="1" if mode == "noshare" else "0")
-        path = tmp_path / f"{mode}.pt"
-        p = subprocess.run([sys.executable, "-c", _C1_CHILD, root, str(path)], env=env, capture_output=True, text=True,
-                           timeout=120)
-        assert p.returncode == 0, p.stderr[-2000:]
-        res[mode] = torch.load(path, weights_only=True)
-    assert res["share"].keys() == res["noshare"].keys()
-    for k in res["share"]:
-        a, b = res["share"][k], res["noshare"][k]
-        assert torch.equal(a.isnan(), b.isnan()), k
-        assert torch.equal(torch.nan_to_num(a), torch.nan_to_num(b)), k
-        if k.startswith("upto"):
-            n = int(k[4:])
-            assert not a[:max(n - 2, 0)].isnan().any() and a[max(n - 2, 0):].isnan().all()
-        else:
-            assert not a.isnan().any()
-
-
-_C2_CHILD = r'''
-import sys, torch
-sys.path.insert(0, sys.argv[1])
-from reth_amd import _lib
-dev = torch.device("cuda")
-g = torch.Generator(device=dev).manual_seed(12)
-shape = _lib.ConvShape(_lib.CONV_F32_NHWC, 32, 20, 20, 64, 4, 4, 2)
-wt = (torch.randn((64, 32, 4, 4), device=dev, generator=g) * 0.05).contiguous(memory_format=torch.channels_last)
-b = torch.randn(64, device=dev, generator=g) * 0.1
-pk = torch.empty(_lib.lib().rth_conv_packed_bytes(_lib.ctypes.byref(shape)) // 4, device=dev)
-_lib.call("rth_conv_pack", _lib.ctypes.byref(shape), wt.data_ptr(), pk.data_ptr(), _lib.stream_ptr())
-out = {}
-for n in (1, 3, 64, 700, 1024):
-    x = torch.rand((n, 20, 20, 32), device=dev, generator=g)
-    for rep in range(2):  # the same buffers again
-        y = torch.full((n, 9, 9, 64), float("nan"), device=dev)
-        _lib.call("rth_conv_bias_relu", _lib.ctypes.byref(shape), x.data_ptr(), None, n, pk.data_ptr(), b.data_ptr(),
-                  y.data_ptr(), _lib.stream_ptr())
-        out[f"n{n}_{rep}"] = y.cpu()
-    cnt = torch.tensor([max(n // 2, 1)], dtype=torch.int64, device=dev)
-    y = torch.full((n, 9, 9, 64), float("nan"), device=dev)
-    _lib.call("rth_conv_bias_relu_upto", _lib.ctypes.byref(shape), x.data_ptr(), None, n, cnt.data_ptr(), pk.data_ptr(),
-              b.data_ptr(), y.data_ptr(), _lib.stream_ptr())
-    out[f"upto{n}"] = y.cpu()
-torch.save(out, sys.argv[2])
-'''
-
-
-def test_conv2_schedules_bit_identical(tmp_path, dev):
-    """conv2's fp32-MFMA forward under every tile schedule (RTH_CONV2_SCHED: static round-robin,
-    half tiles, the channel part per workgroup) gives the same bits: each output's MFMA chain is
-    the same whichever wave computes it"""
-    import subprocess
-    import sys
-
-    if torch.cuda.is_initialized():
-        torch.cuda.synchronize()
-        torch.cuda.empty_cache()
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    res = {}
-    for sched in ("static", "ns2", "pw2", "ts2", "ts4", "ts4big", "ts8big"):
-        path = tmp_path / f"{sched}.pt"
-        p = subprocess.run([sys.executable, "-c", _C2_CHILD, root, str(path)],
-                           env=dict(os.environ, RTH_CONV2_SCHED=sched), capture_output=True, text=True, timeout=120)
-        assert p.returncode == 0, (sched, p.stderr[-2000:])
-        res[sched] = torch.load(path, weights_only=True)
-    base = res["static"]
-    for k, v in base.items():
-        if k.startswith("upto"):
-            n = int(k[4:])
-            m = max(n // 2, 1)
-            assert not v[:m].isnan().any() and v[m:].isnan().all(), k
-        else:
-            assert not v.isnan().any(), k
-    for sched, r in res.items():
-        for k in base:
-            assert torch.equal(torch.nan_to_num(r[k], nan=-1.0), torch.nan_to_num(base[k], nan=-1.0)), (sched, k)
 
 
 @pytest.mark.parametrize("n", [1, 7, 512, 1024])

@@ -102,7 +102,7 @@ def test_frame_store_prefill_and_footprint(dev):
     from reth_amd.apex import ApexConfig, ApexDQN
 
     hard = ApexDQN.frame_store_frames(ApexConfig(n_actors=16, capacity=2048, frame_store=True))
-    assert hard == 2 * 2048 + 2 * (3 + 16) * 16 + 16
+    assert hard == 2 * 2048 + 2 * (3 + 16 + 2) * 16 + 16  # + 2 actor_steps_per_update: the sample-ahead window
     cfg = ApexConfig(n_actors=16, capacity=2048, batch_size=32, seed=2, hip_graph=False, frame_store=True,
                      frame_store_bound="expected")
     ax = ApexDQN(cfg, device=dev)

@@ -7,14 +7,17 @@ config's BeamRider, config.yaml:8), each two DQNSolver.update calls of the refer
 after each (tests/golden/make_golden.py gen_dqn_full).
 
 What runs here is exactly what the bench replays: an ApexDQN (HIP graphs, uint8 batch
-slots, the explicit gradient pass -- HIP conv forward, bf16x3 conv1 weight gradient from the
-stacks, HIP conv2 data gradient, deferred bias gradients, hipBLASLt FC1 on the committed
-TunableOp solutions, rth_clip_adam) is built with the reference's seed, run until its graphs
-are captured, then reset to the initial weights / zero Adam state; the golden batch is
+slots, the explicit gradient pass of fused_learner.py -- the HIP conv forwards (conv1 bf16x3,
+conv2 fp32 MFMA, conv3 x9), FC1's forward on the exact-split rth_fc_x9, the fused TD / Huber /
+FC2 backward, FC1's two backward GEMMs and conv2 / conv3 weight gradients on hipBLASLt /
+MIOpen, the x9 data gradients, conv1's bf16x3 weight gradient from the stacks with the
+deferred bias gradients, rth_clip_adam) is built with the reference's seed, run until its
+graphs are captured, then reset to the initial weights / zero Adam state; the golden batch is
 written into a learner batch slot and the captured learner graph is replayed twice.
 Tolerances: the first update's |td| within the north-star 1e-5 of the reference's fp32 run
 (same weights, same batch), relative to the magnitude of td's operands Q(s0, a) and the TD
-target (both ~17 on Pong's unnormalised frames; the fixture holds the float64 target).  The parameters are compared with the EXACT update (the same
+target (both ~17 on Pong's unnormalised frames; the fixture holds the float64 target), and in
+absolute terms no farther from the exact |td| than 1.5x the reference fp32 run's own distance.  The parameters are compared with the EXACT update (the same
 reference code run in float64, stored beside the fp32 run): the reference's own fp32 CPU
 update is up to 1.6e-5 away from it on conv1's weight after two updates (Adam's eps = 1.5e-4
 turns the fp32 rounding of near-zero gradients into parameter differences), so every tensor
@@ -162,12 +165,12 @@ def test_apex_learner_graph_vs_reference(golden, dev, name):
             scale = np.maximum(1.0, td64 + np.abs(gd[f"upd{k}_target64"]))
             rel = np.abs(td - td32) / scale
             assert rel.max() <= 1e-5, (k, rel.max(), int(rel.argmax()))
-            # ... and in absolute terms: within 1e-5 of the reference fp32 |td| beyond twice that
-            # run's own largest distance from the exact |td| (measured r04: ours 2.0e-5 from the
-            # reference fp32 run and 2.3e-5 from the exact |td|, the reference fp32 run 1.0e-5 from
-            # it -- ~10 fp32 ulp at |td| ~ 17)
-            bound = 1e-5 + 2 * np.abs(td32 - td64).max()
-            assert np.abs(td - td32).max() <= bound, (k, float(np.abs(td - td32).max()), bound)
+            # ... and in absolute terms at least nearly as accurate as the reference's own fp32
+            # arithmetic: the largest distance from the exact |td| within 1.5x the reference fp32
+            # run's (with FC1's 3,136-term single chains on hipBLASLt it was
+            # 2.1x, with every FC1 forward on the exact-split GEMM 1.1x)
+            e_ours, e_ref = float(np.abs(td - td64).max()), float(np.abs(td32 - td64).max())
+            assert e_ours <= 1.5 * e_ref, (k, e_ours, e_ref, e_ours / e_ref)
         ref_td = np.abs(td32 - td64).max()
         assert np.abs(td - td64).max() <= 2 * ref_td + 1e-5, (k, np.abs(td - td64).max(), ref_td)
     for k, name, e_ours, e_ref in report:

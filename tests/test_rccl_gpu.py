@@ -22,10 +22,11 @@ import json, os, sys
 sys.path.insert(0, sys.argv[1])
 # a run-to-run deterministic learner (the weight gradients on rth_conv_wgrad_x9: MIOpen's
 # solvers differ in the last bits run to run), so the hooked and the plain run can be compared
-os.environ["RTH_HIP_WGRAD"] = "x9"
 import torch
 import torch.distributed as dist
+from reth_amd import fused_learner
 from reth_amd.apex import ApexConfig, ApexDQN
+fused_learner.HIP_WGRAD = "x9"
 
 def say(**kw):
     print("STAGE " + json.dumps(kw), flush=True)

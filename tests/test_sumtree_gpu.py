@@ -216,21 +216,12 @@ def test_per_distribution(dev):
     check(w)
 
 
-@pytest.mark.parametrize("top", ["0", "1"])
-@pytest.mark.parametrize("gk", ["", "0", "3", "4", "5"])
-def test_find_lane_groups(dev, orc, golden, monkeypatch, gk, top):
-    """the walk with one lane per target (RTH_FIND_GROUP=0) and with lane groups of 2^3 /
-    2^4 / 2^5 (several levels per round trip, one pair per lane), the sampler's with and
-    without the LDS-staged top levels ("" = the default: staged top, one-lane walk below),
-    returns the oracle's indices: ragged trees, zeros, targets at and past the total, the
-    golden small trees"""
+def test_find_and_sample_ragged(dev, orc, golden):
+    """rth_sumtree_find (lane groups of 2^4 lanes, 4 levels per round trip) and the sampler
+    (k_tree_sample_deep: 10 levels staged in LDS, 2 per round trip below) return the oracle's
+    indices: ragged trees, zeros, targets at and past the total, the golden small trees"""
     from reth_amd.replay import SumTree
 
-    if gk:
-        monkeypatch.setenv("RTH_FIND_GROUP", gk)
-    else:
-        monkeypatch.delenv("RTH_FIND_GROUP", raising=False)
-    monkeypatch.setenv("RTH_TREE_LDS_TOP", top)
     rng = np.random.default_rng(77)
     for cap in (1, 2, 3, 7, 31, 33, 1000, 65537, 300000):
         t = SumTree(cap, dev)
@@ -256,23 +247,3 @@ def test_find_lane_groups(dev, orc, golden, monkeypatch, gk, top):
         assert np.array_equal(idx.cpu().numpy(), g[f"{tag}/find"]), tag
         idx, val = t.sample(len(g[f"{tag}/sample_u"]), uniforms=g[f"{tag}/sample_u"])
         assert np.array_equal(idx.cpu().numpy(), g[f"{tag}/sample_idx"]), tag
-
-
-@pytest.mark.parametrize("fuse", ["0", "1"])
-def test_top_pass_forms_against_oracle(fuse):
-    """the tree update's other top-pass forms (RTH_TREE_FUSE_TOP, read once per process: a child
-    pytest): 1 = run by the subtree pass's last workgroup on keys it staged (r02-r04), 0 = its
-    own launch -- the same trees as the default concurrent extra workgroup (2), bit for bit
-    against the oracle and the reference's large golden state"""
-    import os
-    import subprocess
-    import sys
-
-    if torch.cuda.is_initialized():
-        torch.cuda.synchronize()
-    here = os.path.dirname(os.path.abspath(__file__))
-    p = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider", os.path.abspath(__file__),
-                        "-k", "random_against_oracle or golden_large or bulk_update"],
-                       cwd=os.path.dirname(here), env=dict(os.environ, RTH_TREE_FUSE_TOP=fuse), capture_output=True,
-                       text=True, timeout=280)
-    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-2000:]

@@ -391,13 +391,20 @@ class ApexDQN:
             act.fresh = fresh
             # the target network's output on each slot's s1, computed on the actor stream ahead
             # of the update (target_heads); "pre" learner graphs consume it, "full" ones
-            # compute it themselves (after a target sync, and before any was precomputed)
+            # compute it themselves (after a target sync, and before any was precomputed).
+            # Captured from a stream of its own: FC1's split-K workspace is keyed by the
+            # capturing stream (model._fc_workspace), and the learner's "full" variant runs the
+            # same target pass concurrently on the learner stream -- one shared workspace would
+            # mix the two launches' partials
+            side_tgt = torch.cuda.Stream(self.device)
+            side_tgt.wait_stream(side)
             for p in range(2):
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, stream=side, capture_error_mode=_CAPTURE_MODE):
+                with torch.cuda.graph(g, stream=side_tgt, capture_error_mode=_CAPTURE_MODE):
                     q1t = solver.target_heads(slots[p][0][3])
                 G["tgt"].append(g)
                 G["q1t"].append(q1t)
+            side.wait_stream(side_tgt)
             for pr, variant, p in [(pr, variant, p) for pr in psets for variant in ("full", "pre") for p in range(2)]:
                     v = ("probe", variant, p) if pr else (variant, p)
                     parts, bounds = [torch.cuda.CUDAGraph()], []

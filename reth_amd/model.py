@@ -446,10 +446,14 @@ _FC_WS = {}
 
 
 def _fc_workspace(fn, device, w, M, N, K):
-    """the split-K workspace of fn for (M, N, K), keyed by the weight storage (one per network)"""
-    from ._lib import lib
+    """the split-K workspace of fn for (M, N, K), keyed by the weight storage (one per network)
+    AND the launching stream: the same network may run the same shape on two streams at once
+    (the target network's B-row pass: the learner's own after a target sync on the learner
+    stream, the next batch's on the actor stream), and a shared workspace would mix the two
+    launches' split-K partials"""
+    from ._lib import lib, stream_ptr
 
-    key = (device, w.data_ptr(), M, N, K, fn)
+    key = (device, w.data_ptr(), M, N, K, fn, stream_ptr())
     ws = _FC_WS.get(key)
     if ws is None:
         ws = _FC_WS[key] = torch.empty(max(getattr(lib(), fn + "_workspace")(M, N, K), 16) // 4, dtype=torch.float32,

@@ -709,7 +709,7 @@ struct X9Geom {
   // same side (R0 or R1): then the 16 units of every group are on 16 distinct bank quads, for
   // every tap (it adds the same offset to all lanes).  Padding rows repeat a pixel of their own
   // side (a broadcast).  Entry = the pixel of (tile, row), or -1 - that pixel for padding rows.
-  struct TMap {
+  struct alignas(16) TMap {
     int16_t v[TILES * 16];
   };
   static constexpr int origin(int p) {
@@ -918,6 +918,16 @@ __global__ __launch_bounds__(64 * (COUT_ / 16) * KS) void k_conv_x9(const float 
 #pragma unroll
     for (int t = 0; t < 3; ++t) l2[(t * NG * PLANE + unit) * 2 + (c4 & 1)] = tr[t];
   };
+  // the tile map goes to LDS with the staging: its global loads issued ahead of phase A's (the
+  // load counter is in order, so committing phase A waits for them too, and nothing later waits
+  // behind phase B's loads for them); the prologue and the epilogue read it from LDS
+  constexpr int TMU = G::PERM ? (int)(sizeof(typename G::TMap) / 16) : 1;  // 16-byte units
+  __shared__ uint4 tm_lds[TMU];
+  uint4 tmv = make_uint4(0u, 0u, 0u, 0u);
+  if constexpr (G::PERM) {
+    static_assert(TMU <= NT, "one 16-byte unit of the tile map per lane at most");
+    if (tid < TMU) tmv = reinterpret_cast<const uint4 *>(&x9_tmap<G>)[tid];
+  }
   {
     float4 va[UA];
 #pragma unroll
@@ -926,6 +936,10 @@ __global__ __launch_bounds__(64 * (COUT_ / 16) * KS) void k_conv_x9(const float 
     for (int u = 0; u < UA; ++u)
       if (tid + u * NT < SA) commit(va[u], tid + u * NT, 0, RA);
   }
+  if constexpr (G::PERM) {
+    if (tid < TMU) tm_lds[tid] = tmv;
+  }
+  const int16_t *const tmap = reinterpret_cast<const int16_t *>(tm_lds);
   float4 vb[UB];
   if constexpr (SB > 0) {
 #pragma unroll
@@ -937,7 +951,6 @@ __global__ __launch_bounds__(64 * (COUT_ / 16) * KS) void k_conv_x9(const float 
   // per chunk of this wave's K half (wave-uniform): the tap's pixel offset and the ci group's
   // plane offset; per tile (per lane): the window origin's staged pixel
   int toff[NCH2], coff[NCH2], rbv[G::TILES];
-  uint32_t vmask = 0;  // the tile map: bit t = this lane's row of tile t is a live output pixel
 #pragma unroll
   for (int c = 0; c < NCH2; ++c) {
     const int k0 = (half * NCH2 + c) * 32, tap = k0 / CIN;
@@ -945,18 +958,12 @@ __global__ __launch_bounds__(64 * (COUT_ / 16) * KS) void k_conv_x9(const float 
     coff[c] = ((k0 % CIN) / 8) * PLANE;
   }
   const int g = lane >> 4;
-  int16_t tm[G::PERM ? G::TILES : 1];
-  if constexpr (G::PERM) {  // every entry of this lane's row loaded at once
-#pragma unroll
-    for (int tile = 0; tile < G::TILES; ++tile) tm[tile] = x9_tmap<G>.v[tile * 16 + (lane & 15)];
-  }
 #pragma unroll
   for (int tile = 0; tile < G::TILES; ++tile) {
     int p;
     if constexpr (G::PERM) {  // the tile map: padding rows repeat a pixel of their side
-      const int v = tm[tile];
+      const int v = tmap[tile * 16 + (lane & 15)];
       p = v >= 0 ? v : -1 - v;
-      vmask |= (uint32_t)(v >= 0 && p < nv) << tile;
       if (p >= nv) p = 0;  // a sample past ns (the last workgroup): any staged pixel, output dropped
     } else {
       p = tile * 16 + (lane & 15);
@@ -1026,20 +1033,20 @@ __global__ __launch_bounds__(64 * (COUT_ / 16) * KS) void k_conv_x9(const float 
     const int s = p / PIX;
     return out_nchw ? (s * COUT + co) * PIX + (p - s * PIX) : p * COUT + co;
   };
-  // the output pixel of D row (tile, row), or -1 (a padding row, or a sample past ns): with the
-  // tile map, the A row's pixel -- held by lane `row`, recovered from its window origin -- and
-  // validity bit come over by lane shuffles (no table reads in the epilogue)
-  int vrow[4] = {};  // the validity bits of D rows 4 g + i (lane-invariant over the tiles)
+  // the output pixel of D row (tile, row), or -1 (a padding row, or a sample past ns); with the
+  // tile map, this lane's rows 4 g .. 4 g + 3 of every tile read from LDS at once (one 8-byte
+  // read per tile, all in flight before the first use)
+  uint2 drow[G::PERM ? G::TILES : 1];
   if constexpr (G::PERM) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) vrow[i] = __shfl((int)vmask, 4 * g + i, 64);
+    for (int tile = 0; tile < G::TILES; ++tile)
+      drow[tile] = *reinterpret_cast<const uint2 *>(tmap + tile * 16 + 4 * g);
   }
   auto row_pixel = [&](int tile, int row) -> int {  // row = 4 g + i
     if constexpr (G::PERM) {
-      const int r = rbv[tile], s = r / (HIN * WIN), rem = r - s * (HIN * WIN), oy = rem / WIN;
-      const int mine = s * PIX + oy * G::WOUT + (rem - oy * WIN);  // S == 1
-      const int p = __shfl(mine, row, 64);
-      return ((vrow[row & 3] >> tile) & 1) ? p : -1;
+      const uint32_t w = (row & 2) ? drow[tile].y : drow[tile].x;
+      const int v = (int)(int16_t)(uint16_t)((row & 1) ? (w >> 16) : (w & 0xffffu));
+      return v >= 0 && v < nv ? v : -1;
     } else {
       const int p = tile * 16 + row;
       return p < nv ? p : -1;

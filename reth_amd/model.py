@@ -238,10 +238,9 @@ class DQNNetwork(nn.Module):
                 ws = _fc_workspace("rth_fc_x9", h.device, w1, n_fixed, O, F)
                 call("rth_fc_x9_rows_upto", ptr(h), F, n_fixed, n, ptr(n_dev), ptr(w1), O, F, ptr(b1), ptr(h1), ptr(ws),
                      stream_ptr())
-            else:
-                fc1_relu(h[:n_fixed], w1, b1, out=h1[:n_fixed])
-                call("rth_linear_relu_rows_upto", ptr(h), F, n_fixed, n, ptr(n_dev), ptr(w1), ptr(b1), F, O, ptr(h1),
-                     O, stream_ptr())
+            else:  # (fixed rows not a multiple of 64: tiny actor counts) every counted row in HIP
+                call("rth_linear_relu_rows_upto", ptr(h), F, 0, n, ptr(n_dev), ptr(w1), ptr(b1), F, O, ptr(h1), O,
+                     stream_ptr())
         ps = self._head_params()[4:]
         A, H = ps[0].shape
         out = torch.empty((n, A + 1), dtype=torch.float32, device=h.device)

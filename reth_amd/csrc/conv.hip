@@ -680,11 +680,8 @@ struct X9Geom {
   // ((r + (r >> shift) * rotation) & 15) of its plane (shift 0 = 5), planes padded by `pad`
   // units (0 = the r03 rule: 1 at rotation 10) -- scripts/x9_lds_sim.py searches these
   static constexpr int ROTV = ROT & 15, SHV = ((ROT >> 4) & 15) ? ((ROT >> 4) & 15) : 5;
-  // stride 1: the tile map below (dense image, PLANE = 8 mod 16); stride 2: the row rotation
-  static constexpr bool PERM = S == 1;
-  static constexpr int PADV = PERM ? 8 : (ROT >> 8) ? (ROT >> 8) : (ROT == 10 ? 1 : 0);
+  static constexpr int PADV = (ROT >> 8) ? (ROT >> 8) : (ROT == 10 ? 1 : 0);
   static constexpr int PLANE = (ROWS + 15) / 16 * 16 + PADV;  // 16-B units per (term, cg)
-  static_assert(!PERM || PLANE % 16 == 8, "the tile map's two ci groups of a read group sit 8 bank quads apart");
   static_assert(SHV >= 4, "the rotation must be constant over each aligned 16-row block (a permutation)");
   static constexpr int LDS_U4 = 3 * NG * PLANE;                          // LDS in 16-B units
   static constexpr int OUT_F = NSAMP * COUT * PIX;                       // output staging floats
@@ -694,125 +691,8 @@ struct X9Geom {
   static_assert(COUT % 16 == 0 && NT <= 1024, "16-channel blocks, at most 16 waves");
   static_assert(OUT_F * 4 <= LDS_U4 * 16, "output staging must fit the input image");
   static_assert(LDS_U4 * 16 <= 163840, "LDS image too large");
-  __device__ static int swz(int r) { return PERM ? r : (r & ~15) | ((r + (r >> SHV) * ROTV) & 15); }
-
-  // ---- the tile map (r06; stride-1 geometries: conv3 forward, both data gradients).  The A
-  // fragment of a 16-pixel tile is read by ds_read_b128 in four 16-lane groups, each group =
-  // rows R0 = {0-3, 12-15} of one ci group g and rows R1 = {4-11} of g ^ 1 (MI355X_MICROARCH.md
-  // LDS table); a lane's 16-byte unit is g PLANE + origin(pixel) + tap offset, its banks
-  // (unit mod 16).  With the raster tiles (16 consecutive output pixels) and the row rotation
-  // two lanes of a group met on one bank in half the LDS cycles.  Here the
-  // image is stored densely (no swizzle), PLANE = 8 mod 16, and each tile is chosen so that its
-  // pixels' window origins are distinct mod 16 -- greedily, every tile takes one pixel from each
-  // of the (up to) 16 residue classes with the most pixels left, phase A's tiles from phase A's
-  // samples only -- and its rows are ordered so that origins r and r + 8 (mod 16) sit on the
-  // same side (R0 or R1): then the 16 units of every group are on 16 distinct bank quads, for
-  // every tap (it adds the same offset to all lanes).  Padding rows repeat a pixel of their own
-  // side (a broadcast).  Entry = the pixel of (tile, row), or -1 - that pixel for padding rows.
-  struct alignas(16) TMap {
-    int16_t v[TILES * 16];
-  };
-  static constexpr int origin(int p) {
-    return (p / PIX) * (HIN * WIN) + S * ((p % PIX) / WOUT) * WIN + S * ((p % PIX) % WOUT);
-  }
-  // tiles [t0, t1) from the pixels marked in `avail` (1 = not yet placed); returns the count left
-  static constexpr int fill(TMap &m, int8_t (&avail)[NSAMP * PIX], int pend, int t0, int t1) {
-    for (int t = t0; t < t1; ++t) {
-      int cnt[16] = {}, first[16] = {};
-      for (int c = 0; c < 16; ++c) first[c] = -1;
-      for (int p = 0; p < pend; ++p)
-        if (avail[p]) {
-          const int c = origin(p) & 15;
-          if (cnt[c]++ == 0) first[c] = p;
-        }
-      int px[16] = {}, np = 0;
-      bool taken[16] = {};
-      for (int k = 0; k < 16; ++k) {  // classes by pixels left (most first), then by residue
-        int best = -1;
-        for (int c = 0; c < 16; ++c)
-          if (!taken[c] && cnt[c] > 0 && (best < 0 || cnt[c] > cnt[best])) best = c;
-        if (best < 0) break;
-        taken[best] = true;
-        px[np++] = first[best];
-        avail[first[best]] = 0;
-      }
-      // sides: residue pairs {c, c + 8} together, pairs first (alternating), then singles
-      int side[16] = {}, nx = 0, ny = 0;
-      for (int pass = 0; pass < 2; ++pass)
-        for (int q = 0; q < 8; ++q) {
-          int a = -1, b = -1;
-          for (int i = 0; i < np; ++i) {
-            if ((origin(px[i]) & 15) == q) a = i;
-            if ((origin(px[i]) & 15) == q + 8) b = i;
-          }
-          const int sz = (a >= 0) + (b >= 0);
-          if (sz != 2 - pass) continue;
-          const bool toX = pass == 0 ? nx <= ny : ((nx < ny && nx < 8) || ny >= 8);
-          if (a >= 0) side[a] = toX ? 0 : 1;
-          if (b >= 0) side[b] = toX ? 0 : 1;
-          (toX ? nx : ny) += sz;
-        }
-      constexpr int R0[8] = {0, 1, 2, 3, 12, 13, 14, 15}, R1[8] = {4, 5, 6, 7, 8, 9, 10, 11};
-      int ix = 0, iy = 0, fx = -1, fy = -1;
-      for (int i = 0; i < np; ++i) {
-        if (side[i] == 0) {
-          m.v[t * 16 + R0[ix++]] = (int16_t)px[i];
-          fx = fx < 0 ? px[i] : fx;
-        } else {
-          m.v[t * 16 + R1[iy++]] = (int16_t)px[i];
-          fy = fy < 0 ? px[i] : fy;
-        }
-      }
-      const int padx = fx >= 0 ? fx : fy, pady = fy >= 0 ? fy : fx;
-      for (; ix < 8; ++ix) m.v[t * 16 + R0[ix]] = (int16_t)(-1 - (padx >= 0 ? padx : 0));
-      for (; iy < 8; ++iy) m.v[t * 16 + R1[iy]] = (int16_t)(-1 - (pady >= 0 ? pady : 0));
-    }
-    int left = 0;
-    for (int p = 0; p < pend; ++p) left += avail[p];
-    return left;
-  }
-  static constexpr int NA_ = NSAMP > 1 ? NSAMP / 2 : NSAMP;
-  static constexpr int TA_ = NSAMP > 1 ? (NA_ * PIX) / 16 : TILES;
-  static constexpr TMap make_tmap() {
-    TMap m{};
-    int8_t avail[NSAMP * PIX] = {};
-    for (int p = 0; p < NSAMP * PIX; ++p) avail[p] = 1;
-    if (NSAMP > 1) {
-      fill(m, avail, NA_ * PIX, 0, TA_);  // phase A: its own samples only
-      fill(m, avail, NSAMP * PIX, TA_, TILES);
-    } else {
-      fill(m, avail, NSAMP * PIX, 0, TILES);
-    }
-    return m;
-  }
-  // the map's promises: every pixel exactly once, origins distinct mod 16 within a tile, and no
-  // two rows of opposite sides with origins 8 apart mod 16 (checked at compile time)
-  static constexpr bool tmap_ok() {
-    if (!PERM) return true;
-    const TMap m = make_tmap();
-    int seen[NSAMP * PIX] = {};
-    for (int t = 0; t < TILES; ++t)
-      for (int r = 0; r < 16; ++r) {
-        const int v = m.v[t * 16 + r];
-        if (v >= 0) {
-          if (v >= NSAMP * PIX || seen[v]++) return false;
-          if (NSAMP > 1 && t < TA_ && v >= NA_ * PIX) return false;
-          for (int r2 = 0; r2 < 16; ++r2) {
-            const int w = m.v[t * 16 + r2];
-            if (r2 == r || w < 0) continue;
-            const bool side = (r >= 4 && r < 12), side2 = (r2 >= 4 && r2 < 12);
-            const int d = (origin(v) - origin(w)) & 15;
-            if (d == 0 || (side != side2 && d == 8)) return false;
-          }
-        }
-      }
-    for (int p = 0; p < NSAMP * PIX; ++p)
-      if (seen[p] != 1) return false;
-    return true;
-  }
+  __device__ static int swz(int r) { return (r & ~15) | ((r + (r >> SHV) * ROTV) & 15); }
 };
-template <class G>
-__constant__ typename G::TMap x9_tmap = G::make_tmap();
 
 // PAD > 0 (the data gradient, rth_conv_dgrad): the staged HIN x WIN image is the input
 // zero-padded by PAD on every side -- x is [n, HIN - 2 PAD, WIN - 2 PAD, CIN], the border reads
@@ -840,7 +720,6 @@ __global__ __launch_bounds__(64 * (COUT_ / 16) * KS) void k_conv_x9(const float 
   static_assert(!MASK || (PAD > 0 && !CLS && (64 * (COUT_ / 16) * KS) % (COUT_ / 4) == 0),
                 "the masked epilogue is the NHWC data gradient's; every lane keeps one channel quad");
   using G = X9Geom<KH, KW, S, CIN, HIN, WIN, NSAMP, ROT, KS, COUT_>;
-  static_assert(G::tmap_ok(), "the tile map must place every pixel once on distinct bank quads");
   if constexpr (CLS) wpk += (size_t)blockIdx.y * G::PACKED_U4;
   constexpr int HS = HIN - 2 * PAD, WS = WIN - 2 * PAD;  // the source image
   constexpr int PIX = G::PIX, NCH2 = G::NCHP, NG = G::NG, PLANE = G::PLANE, COUT = G::COUT, NT = G::NT;
@@ -918,16 +797,6 @@ __global__ __launch_bounds__(64 * (COUT_ / 16) * KS) void k_conv_x9(const float 
 #pragma unroll
     for (int t = 0; t < 3; ++t) l2[(t * NG * PLANE + unit) * 2 + (c4 & 1)] = tr[t];
   };
-  // the tile map goes to LDS with the staging: its global loads issued ahead of phase A's (the
-  // load counter is in order, so committing phase A waits for them too, and nothing later waits
-  // behind phase B's loads for them); the prologue and the epilogue read it from LDS
-  constexpr int TMU = G::PERM ? (int)(sizeof(typename G::TMap) / 16) : 1;  // 16-byte units
-  __shared__ uint4 tm_lds[TMU];
-  uint4 tmv = make_uint4(0u, 0u, 0u, 0u);
-  if constexpr (G::PERM) {
-    static_assert(TMU <= NT, "one 16-byte unit of the tile map per lane at most");
-    if (tid < TMU) tmv = reinterpret_cast<const uint4 *>(&x9_tmap<G>)[tid];
-  }
   {
     float4 va[UA];
 #pragma unroll
@@ -936,10 +805,6 @@ __global__ __launch_bounds__(64 * (COUT_ / 16) * KS) void k_conv_x9(const float 
     for (int u = 0; u < UA; ++u)
       if (tid + u * NT < SA) commit(va[u], tid + u * NT, 0, RA);
   }
-  if constexpr (G::PERM) {
-    if (tid < TMU) tm_lds[tid] = tmv;
-  }
-  const int16_t *const tmap = reinterpret_cast<const int16_t *>(tm_lds);
   float4 vb[UB];
   if constexpr (SB > 0) {
 #pragma unroll
@@ -960,15 +825,8 @@ __global__ __launch_bounds__(64 * (COUT_ / 16) * KS) void k_conv_x9(const float 
   const int g = lane >> 4;
 #pragma unroll
   for (int tile = 0; tile < G::TILES; ++tile) {
-    int p;
-    if constexpr (G::PERM) {  // the tile map: padding rows repeat a pixel of their side
-      const int v = tmap[tile * 16 + (lane & 15)];
-      p = v >= 0 ? v : -1 - v;
-      if (p >= nv) p = 0;  // a sample past ns (the last workgroup): any staged pixel, output dropped
-    } else {
-      p = tile * 16 + (lane & 15);
-      if (p >= nv) p = nv - 1;
-    }
+    int p = tile * 16 + (lane & 15);
+    if (p >= nv) p = nv - 1;
     const int s = p / PIX, pp = p - s * PIX, oy = pp / G::WOUT, ox = pp - oy * G::WOUT;
     rbv[tile] = s * (HIN * WIN) + S * oy * WIN + S * ox;
   }
@@ -1033,25 +891,6 @@ __global__ __launch_bounds__(64 * (COUT_ / 16) * KS) void k_conv_x9(const float 
     const int s = p / PIX;
     return out_nchw ? (s * COUT + co) * PIX + (p - s * PIX) : p * COUT + co;
   };
-  // the output pixel of D row (tile, row), or -1 (a padding row, or a sample past ns); with the
-  // tile map, this lane's rows 4 g .. 4 g + 3 of every tile read from LDS at once (one 8-byte
-  // read per tile, all in flight before the first use)
-  uint2 drow[G::PERM ? G::TILES : 1];
-  if constexpr (G::PERM) {
-#pragma unroll
-    for (int tile = 0; tile < G::TILES; ++tile)
-      drow[tile] = *reinterpret_cast<const uint2 *>(tmap + tile * 16 + 4 * g);
-  }
-  auto row_pixel = [&](int tile, int row) -> int {  // row = 4 g + i
-    if constexpr (G::PERM) {
-      const uint32_t w = (row & 2) ? drow[tile].y : drow[tile].x;
-      const int v = (int)(int16_t)(uint16_t)((row & 1) ? (w >> 16) : (w & 0xffffu));
-      return v >= 0 && v < nv ? v : -1;
-    } else {
-      const int p = tile * 16 + row;
-      return p < nv ? p : -1;
-    }
-  };
   __syncthreads();  // every wave is done reading the input image
   // parts KS-1 .. 1 in turn: the last stores, each earlier one adds its own first
 #pragma unroll
@@ -1061,8 +900,8 @@ __global__ __launch_bounds__(64 * (COUT_ / 16) * KS) void k_conv_x9(const float 
       for (int tile = 0; tile < G::TILES; ++tile)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const int p = row_pixel(tile, 4 * g + i);
-          if (p >= 0) {
+          const int p = tile * 16 + 4 * g + i;
+          if (p < nv) {
             const int f = fidx(p);
             F[f] = pt == KS - 1 ? acc[tile][i] : radd(acc[tile][i], F[f]);
           }
@@ -1075,8 +914,8 @@ __global__ __launch_bounds__(64 * (COUT_ / 16) * KS) void k_conv_x9(const float 
     for (int tile = 0; tile < G::TILES; ++tile)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int p = row_pixel(tile, 4 * g + i);
-        if (p >= 0) {
+        const int p = tile * 16 + 4 * g + i;
+        if (p < nv) {
           const int f = fidx(p);
           F[f] = bias ? relu_c(radd(radd(acc[tile][i], F[f]), bl)) : radd(acc[tile][i], F[f]);
         }

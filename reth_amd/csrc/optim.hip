@@ -18,7 +18,9 @@
 namespace rth {
 
 constexpr int kOptThreads = 256;
-constexpr int kOptChunk = 4096;  // elements per workgroup (16 per lane)
+constexpr int kOptChunk = 4096;   // elements per k_grad_sqsum workgroup (16 per lane)
+constexpr int kAdamChunk = 2048;  // elements per k_adam workgroup (8 per lane): twice the
+                                  // workgroups, so one's stores overlap another's loads (r06)
 constexpr int kMaxPartials = 1 << 15;
 
 struct OptSeg {
@@ -31,7 +33,22 @@ struct OptSeg {
   int vec;       // all four pointers 16-byte aligned: float4 accesses
 };
 
-constexpr int kOptV = kOptChunk / kOptThreads / 4;  // float4 groups per lane
+constexpr int kOptV = kOptChunk / kOptThreads / 4;    // float4 groups per lane (k_grad_sqsum)
+constexpr int kAdamV = kAdamChunk / kOptThreads / 4;  // float4 groups per lane (k_adam)
+
+// the workgroup's sum of one fp64 value per lane in a fixed order (r06: a wavefront shuffle
+// tree, then the 4 waves in order; was an 8-step LDS tree with a barrier per step): every
+// lane returns the same sum
+__device__ __forceinline__ double block_sum(double v, double *red4) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = radd(v, __shfl_down(v, o, 64));
+  if ((threadIdx.x & 63) == 0) red4[threadIdx.x >> 6] = v;
+  __syncthreads();
+  double t = red4[0];
+#pragma unroll
+  for (int w = 1; w < kOptThreads / 64; ++w) t = radd(t, red4[w]);
+  return t;
+}
 
 // lane's k-th float4 group of the chunk at element base: elements base + 4 (k T + tid) + 0..3,
 // zero past n
@@ -105,13 +122,7 @@ __device__ __forceinline__ BiasCorr bias_corr(double lr, double beta1, double be
 // waits for another; the step count and the bias corrections were written by k_grad_sqsum's
 // first workgroup (a kernel boundary before any read).
 __device__ OptScalars opt_scalars(double acc, double *red, int clip, float max_norm, BiasCorr bc) {
-  red[threadIdx.x] = acc;
-  __syncthreads();
-  for (int s = kOptThreads / 2; s > 0; s >>= 1) {
-    if (threadIdx.x < s) red[threadIdx.x] = radd(red[threadIdx.x], red[threadIdx.x + s]);
-    __syncthreads();
-  }
-  const float total = (float)sqrt(red[0]);
+  const float total = (float)sqrt(block_sum(acc, red));
   float coef = 1.0f;
   if (clip) {  // clip_coef = max_norm / (total_norm + 1e-6), clamped to 1 (f32 tensor math)
     const float c = max_norm / radd(total, 1e-6f);
@@ -133,7 +144,7 @@ struct ScalarArgs {
 // per-workgroup sums of squares of the gradients (fp64 partials); workgroup 0 advances the
 // device step count and writes the new step's bias corrections
 __global__ __launch_bounds__(kOptThreads) void k_grad_sqsum(OptArgs a, double *__restrict__ part, ScalarArgs sa) {
-  __shared__ double red[kOptThreads];
+  __shared__ double red[kOptThreads / 64];
   const int64_t b = blockIdx.x;
   const OptSeg &sg = a.seg[seg_of(a, b)];
   const int64_t base = (b - sg.blk0) * kOptChunk;
@@ -155,14 +166,9 @@ __global__ __launch_bounds__(kOptThreads) void k_grad_sqsum(OptArgs a, double *_
     acc = radd(acc, rmul(z, z));
     acc = radd(acc, rmul(w, w));
   }
-  red[threadIdx.x] = acc;
-  __syncthreads();
-  for (int s = kOptThreads / 2; s > 0; s >>= 1) {
-    if (threadIdx.x < s) red[threadIdx.x] = radd(red[threadIdx.x], red[threadIdx.x + s]);
-    __syncthreads();
-  }
+  const double wsum = block_sum(acc, red);
   if (threadIdx.x == 0) {
-    part[b] = red[0];
+    part[b] = wsum;
     if (b == 0) {
       const int64_t t = *sa.step + 1;
       *sa.step = t;
@@ -173,10 +179,10 @@ __global__ __launch_bounds__(kOptThreads) void k_grad_sqsum(OptArgs a, double *_
 
 __global__ __launch_bounds__(kOptThreads) void k_adam(OptArgs a, const double *__restrict__ part, int nparts,
                                                      ScalarArgs sa, float w1, float beta2, float w2, float eps) {
-  __shared__ double red[kOptThreads];
+  __shared__ double red[kOptThreads / 64];
   const int64_t b = blockIdx.x;
-  const OptSeg &sg = a.seg[seg_of(a, b)];
-  const int64_t base = (b - sg.blk0) * kOptChunk;
+  const OptSeg &sg = a.seg[seg_of(a, b)];  // a: the segments at kAdamChunk workgroups
+  const int64_t base = (b - sg.blk0) * kAdamChunk;
   // the partials and the bias corrections are loaded first and the chunk's loads issued behind
   // them, so the norm's reduction runs while the chunk is in flight (the load counter is in
   // order: waiting for the partials does not wait for the chunk)
@@ -199,12 +205,12 @@ __global__ __launch_bounds__(kOptThreads) void k_adam(OptArgs a, const double *_
     for (int k = threadIdx.x + 4 * kOptThreads; k < nparts; k += kOptThreads) pacc = radd(pacc, part[k]);
   };
   __builtin_amdgcn_sched_barrier(0);
-  float4 gv[kOptV], mv[kOptV], vv[kOptV], pv[kOptV];
+  float4 gv[kAdamV], mv[kAdamV], vv[kAdamV], pv[kAdamV];
   if (sg.vec) {
     const __amdgpu_buffer_rsrc_t rg = seg_rsrc(sg.grad, sg.n), rm = seg_rsrc(sg.m, sg.n), rv = seg_rsrc(sg.v, sg.n),
                                  rp = seg_rsrc(sg.param, sg.n);
 #pragma unroll
-    for (int k = 0; k < kOptV; ++k) {
+    for (int k = 0; k < kAdamV; ++k) {
       const int64_t e = base + 4 * (k * kOptThreads + threadIdx.x);
       gv[k] = ld4b(rg, e);
       mv[k] = ld4b(rm, e);
@@ -214,7 +220,7 @@ __global__ __launch_bounds__(kOptThreads) void k_adam(OptArgs a, const double *_
     sum_parts();
   } else {
 #pragma unroll
-    for (int k = 0; k < kOptV; ++k) {
+    for (int k = 0; k < kAdamV; ++k) {
       const int64_t e = base + 4 * (k * kOptThreads + threadIdx.x);
       gv[k] = ld4(sg.grad, e, sg.n, 0);
       mv[k] = ld4(sg.m, e, sg.n, 0);
@@ -238,7 +244,7 @@ __global__ __launch_bounds__(kOptThreads) void k_adam(OptArgs a, const double *_
     p = radd(p, rmul(-step_size, m) / denom);  // addcdiv_(m, denom, -step_size)
   };
 #pragma unroll
-  for (int k = 0; k < kOptV; ++k) {
+  for (int k = 0; k < kAdamV; ++k) {
     const int64_t e = base + 4 * (k * kOptThreads + threadIdx.x);
     if (e >= sg.n) break;
     adam1(gv[k].x, mv[k].x, vv[k].x, pv[k].x);
@@ -280,6 +286,12 @@ int rth_clip_adam(const rth_param_tensor *tensors, int32_t n_tensors, double lr,
   a.nseg = n_tensors;
   RTH_REQUIRE(blocks <= kMaxPartials, "rth_clip_adam: %lld elements exceed the workspace",
               (long long)(blocks * kOptChunk));
+  OptArgs ad = a;  // the same segments at k_adam's chunk size
+  int64_t ablocks = 0;
+  for (int s = 0; s < n_tensors; ++s) {
+    ad.seg[s].blk0 = ablocks;
+    ablocks += (tensors[s].n + kAdamChunk - 1) / kAdamChunk;
+  }
   auto *part = static_cast<double *>(workspace_dev);
   auto *sc = reinterpret_cast<OptScalars *>(static_cast<uint8_t *>(workspace_dev) + (int64_t)kMaxPartials * 8);
   const int clip = max_norm >= 0.0;
@@ -292,7 +304,7 @@ int rth_clip_adam(const rth_param_tensor *tensors, int32_t n_tensors, double lr,
   hipLaunchKernelGGL(k_grad_sqsum, dim3((unsigned)blocks), dim3(kOptThreads), 0, s, a, part, sa);
   RTH_LAUNCHED();
   // 1 - beta1 and 1 - beta2 are python floats in adam.py, rounded to f32 once
-  hipLaunchKernelGGL(k_adam, dim3((unsigned)blocks), dim3(kOptThreads), 0, s, a, part, (int)blocks, sa,
+  hipLaunchKernelGGL(k_adam, dim3((unsigned)ablocks), dim3(kOptThreads), 0, s, ad, part, (int)blocks, sa,
                      (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), (float)eps);
   RTH_LAUNCHED();
   return RTH_OK;

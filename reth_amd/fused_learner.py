@@ -175,7 +175,7 @@ def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None, mid=No
             ys.append(y)
             h = y
         feat = h.view(n, -1)  # the (C, H, W) flatten of the NCHW output: a view
-        h1 = fc1_relu(feat, w1, b1)
+        h1 = fc1_relu(feat, w1, b1, owner=net)
         heads = net._heads_fc2(h1) if w2 is None else torch.addmm(b2, h1, w2.t())
         if q1t is None:
             q1t = solver.target_heads(s1)

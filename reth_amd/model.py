@@ -91,7 +91,7 @@ class DQNNetwork(nn.Module):
 
         new = self.__class__.__new__(self.__class__)
         memo[id(self)] = new
-        skip = ("_w1s", "_b1s", "_frozen", "_frozen_packed", "_ws", "_shape_cache")
+        skip = ("_w1s", "_b1s", "_frozen", "_frozen_packed", "_ws", "_shape_cache", "_fc_ws", "_bwd_ws")
         for k, v in self.__dict__.items():
             if k not in skip:
                 new.__dict__[k] = copy.deepcopy(v, memo)
@@ -212,7 +212,7 @@ class DQNNetwork(nn.Module):
             return self._heads_counted(h, w1, b1, n_dev, n_fixed, cache)
         if cache is not None or n_fixed is not None:
             raise ValueError("forward_heads(cache= / n_fixed=) needs n_dev and the in-place second layer")
-        h = _LinearReLU.apply(h, w1, b1)
+        h = _LinearReLU.apply(h, w1, b1, self)
         if w2 is None:  # the second layer from the branch parameters in place
             return self._heads_fc2(h)
         return torch.addmm(b2, h, w2.t())
@@ -227,7 +227,7 @@ class DQNNetwork(nn.Module):
         n, F = h.shape
         O = w1.shape[0]
         if n_fixed is None:
-            h1 = _LinearReLU.apply(h, w1, b1)
+            h1 = _LinearReLU.apply(h, w1, b1, self)
         else:
             n_fixed = int(n_fixed)
             if not (0 < n_fixed <= n) or not h.is_contiguous():
@@ -235,7 +235,7 @@ class DQNNetwork(nn.Module):
             h1 = torch.empty((n, O), dtype=torch.float32, device=h.device)
             if w1.is_contiguous() and lib().rth_fc_x9_supported(n_fixed, O, F):
                 # the x9 GEMM over the fixed rows, then its split-K reduce and the counted rows in one launch
-                ws = _fc_workspace("rth_fc_x9", h.device, w1, n_fixed, O, F)
+                ws = _fc_workspace("rth_fc_x9", h.device, w1, n_fixed, O, F, self)
                 call("rth_fc_x9_rows_upto", ptr(h), F, n_fixed, n, ptr(n_dev), ptr(w1), O, F, ptr(b1), ptr(h1), ptr(ws),
                      stream_ptr())
             else:  # (fixed rows not a multiple of 64: tiny actor counts) every counted row in HIP
@@ -444,23 +444,26 @@ class _MergeHeads(torch.autograd.Function):
 _FC_WS = {}
 
 
-def _fc_workspace(fn, device, w, M, N, K):
-    """the split-K workspace of fn for (M, N, K), keyed by the weight storage (one per network)
-    AND the launching stream: the same network may run the same shape on two streams at once
-    (the target network's B-row pass: the learner's own after a target sync on the learner
-    stream, the next batch's on the actor stream), and a shared workspace would mix the two
-    launches' split-K partials"""
+def _fc_workspace(fn, device, w, M, N, K, owner=None):
+    """the split-K workspace of fn for (M, N, K), owned by the network that runs it (`owner`: its
+    workspaces live and die with it -- a module-level cache keyed by pointers would hand a later
+    network, allocated at a freed one's addresses, buffers from a released graph pool) and keyed
+    by the launching stream: the same network may run the same shape on two streams at once (the
+    target network's B-row pass: the learner's own after a target sync on the learner stream,
+    the next batch's on the actor stream), and a shared workspace would mix the two launches'
+    split-K partials"""
     from ._lib import lib, stream_ptr
 
+    cache = owner.__dict__.setdefault("_fc_ws", {}) if owner is not None else _FC_WS
     key = (device, w.data_ptr(), M, N, K, fn, stream_ptr())
-    ws = _FC_WS.get(key)
+    ws = cache.get(key)
     if ws is None:
-        ws = _FC_WS[key] = torch.empty(max(getattr(lib(), fn + "_workspace")(M, N, K), 16) // 4, dtype=torch.float32,
-                                       device=device)
+        ws = cache[key] = torch.empty(max(getattr(lib(), fn + "_workspace")(M, N, K), 16) // 4, dtype=torch.float32,
+                                      device=device)
     return ws
 
 
-def fc1_relu(x, w, b, out=None):
+def fc1_relu(x, w, b, out=None, owner=None):
     """relu(x @ w.T + b) (FC1 of both dueling branches): rth_fc_x9 where built for the shape,
     else one hipBLASLt GEMM with the bias+ReLU epilogue.  The split-K workspace is keyed by the
     weight storage, so two networks (the actors', the target's, the learner's -- on different
@@ -472,7 +475,7 @@ def fc1_relu(x, w, b, out=None):
 
         if lib().rth_fc_x9_supported(M, N, K):
             y = out if out is not None else torch.empty((M, N), dtype=torch.float32, device=x.device)
-            ws = _fc_workspace("rth_fc_x9", x.device, w, M, N, K)
+            ws = _fc_workspace("rth_fc_x9", x.device, w, M, N, K, owner)
             call("rth_fc_x9", ptr(x), x.stride(0), M, ptr(w), N, K, ptr(b), 1, ptr(y), ptr(ws), stream_ptr())
             return y
     if out is not None:
@@ -486,8 +489,8 @@ class _LinearReLU(torch.autograd.Function):
     one autograd derives for linear -> relu (threshold on the output, addmm grads)."""
 
     @staticmethod
-    def forward(ctx, x, w, b):
-        out = fc1_relu(x, w, b)
+    def forward(ctx, x, w, b, owner=None):
+        out = fc1_relu(x, w, b, owner=owner)
         ctx.save_for_backward(x, w, out)
         return out
 
@@ -498,7 +501,7 @@ class _LinearReLU(torch.autograd.Function):
         gx = g.mm(w) if ctx.needs_input_grad[0] else None
         gw = g.t().mm(x) if ctx.needs_input_grad[1] else None
         gb = g.sum(0) if ctx.needs_input_grad[2] else None
-        return gx, gw, gb
+        return gx, gw, gb, None
 
 
 class _ConvBiasReLU(torch.autograd.Function):

@@ -13,7 +13,7 @@ from reth_amd.apex import ApexConfig, ApexDQN  # noqa: E402
 
 iters = int(sys.argv[1]) if len(sys.argv) > 1 else 14
 if "blas" in sys.argv:
-    fused_learner.fc1_relu = lambda x, w, b, out=None: torch._addmm_activation(b, x, w.t())
+    fused_learner.fc1_relu = lambda x, w, b, out=None, owner=None: torch._addmm_activation(b, x, w.t())
 dev = torch.device("cuda", 0)
 kw = dict(n_actors=256, num_actions=6, capacity=1_000_000)
 prefill = (1_000_000 - 256 * 10) // 4

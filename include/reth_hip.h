@@ -556,10 +556,10 @@ int rth_conv_dgrad_relu_prepacked(const rth_conv_shape *shape, const float *gy_d
  * when relu != 0, bias may be NULL; M % 64 == 0, N % 128 == 0, K % 32 == 0
  * (rth_fc_x9_supported).  Fixed-order split-K partials in `workspace` (rth_fc_x9_workspace
  * bytes, NULL when that is 0): run-to-run deterministic.  M and N multiples of 128 run on a
- * 128 x 128 workgroup tile (late r05), others on a 64 x 128 tile; the workspace size follows
- * the form (the same process-wide RTH_FC_TILE / RTH_FCT_SPLITS / RTH_FCT_MAXSPLITS knobs).
- * Replaces the hipBLASLt GEMM + bias + ReLU epilogue (torch._addmm_activation) of the actors'
- * and the target pass's forward by default, and of the learner's with RTH_FC_LEARNER=x9. */
+ * 128 x 128 workgroup tile (late r05), others on a 64 x 128 tile; the tile and the k splits
+ * are fixed functions of (M, N, K), so the workspace size is too.  Replaces the hipBLASLt GEMM
+ * + bias + ReLU epilogue (torch._addmm_activation) of every FC1 forward in the loop (r06: the
+ * actors', the target pass's and the learner's). */
 int rth_fc_x9_supported(int64_t M, int64_t N, int64_t K);
 int64_t rth_fc_x9_workspace(int64_t M, int64_t N, int64_t K);
 int rth_fc_x9(const float *x_dev, int64_t ldx, int64_t M, const float *w_dev, int64_t N, int64_t K,
@@ -573,7 +573,8 @@ int rth_fc_x9_rows_upto(const float *x_dev, int64_t ldx, int64_t M, int64_t n_ma
                         void *workspace_dev, void *stream);
 /* The same FC1 on the fp32 MFMA with no LDS (r05): the arguments, the workspace protocol and
  * the determinism of rth_fc_x9; any M >= 1 (ragged actor batches), N % 128 == 0, K % 32 == 0
- * (rth_fc_f32_supported).  Selected for the FC1 forwards by RTH_FC=f32. */
+ * (rth_fc_f32_supported).  Not used by the loop (the x9 form is faster there); kept as the
+ * fp32-MFMA reference form, tested against it. */
 int rth_fc_f32_supported(int64_t M, int64_t N, int64_t K);
 int64_t rth_fc_f32_workspace(int64_t M, int64_t N, int64_t K);
 int rth_fc_f32(const float *x_dev, int64_t ldx, int64_t M, const float *w_dev, int64_t N, int64_t K,

@@ -224,6 +224,14 @@ _lib = None
 _load_error = None
 
 _SRC_EXT = (".hip", ".hpp", ".cpp", ".h")
+# hipcc flags of the library (part of its build id).  The device code is compiled without the
+# packed-FP32 VALU ops (v_pk_{add,mul,fma}_f32): on MI355X a kernel using them returned wrong
+# sums -- single outputs off by one float4's worth of products, 6-60 % of launches -- whenever
+# its waves shared the CUs with k_fc_x9t's bf16-MFMA waves of a concurrent launch on another
+# stream, and exact results with the same source compiled without them (the victim's packed
+# ops, not the other kernel's: scripts/diag_tail_concurrency.py, DESIGN.md "Packed FP32").
+HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17", "-Wall",
+               "-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]
 
 
 def source_files(root=None):
@@ -235,13 +243,14 @@ def source_files(root=None):
 
 
 def source_build_id(root=None):
-    """SHA-1 over "<git blob id> <path>\\n" of every library source (the id compiled into
-    the library as rth_build_id()); from git: `git ls-tree -r HEAD reth_amd/csrc include/reth_hip.h`
-    lists the same blob ids"""
+    """SHA-1 over "<git blob id> <path>\\n" of every library source, then the hipcc flags (the id
+    compiled into the library as rth_build_id()); from git: `git ls-tree -r HEAD reth_amd/csrc
+    include/reth_hip.h` lists the same blob ids"""
     import hashlib
 
     root = root or os.path.dirname(_HERE)
     h = hashlib.sha1()
+    h.update((" ".join(HIPCC_FLAGS) + "\n").encode())
     for rel in source_files(root):
         with open(os.path.join(root, rel), "rb") as f:
             data = f.read()

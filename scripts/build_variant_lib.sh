@@ -7,6 +7,6 @@ cd "$(dirname "$0")/.."
 name=$1; shift
 ID=$(python -c "from reth_amd import _lib; print(_lib.source_build_id())")
 SRCS=$(python -c "import __graft_entry__ as g, os; print(' '.join(os.path.join('reth_amd/csrc', s) for s in g.HIP_SOURCES))")
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -shared -std=c++17 -Wall "$@" \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -shared -std=c++17 -Wall -Xclang -target-feature -Xclang -packed-fp32-ops "$@" \
     -DRTH_BUILD_ID="\"$ID\"" -o "reth_amd/libreth_hip_$name.so" $SRCS
 echo "built reth_amd/libreth_hip_$name.so ($*)"

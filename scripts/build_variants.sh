@@ -8,7 +8,7 @@ out=${VARIANT_DIR:-build_ab}; mkdir -p $out
 srcs=$(python -c "import __graft_entry__ as g; print(' '.join('reth_amd/csrc/' + s for s in g.HIP_SOURCES))")
 pids=()
 while [ $# -ge 2 ]; do
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -shared -std=c++17 $2 -o $out/$1.so $srcs &
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -shared -std=c++17 -Xclang -target-feature -Xclang -packed-fp32-ops $2 -o $out/$1.so $srcs &
   pids+=($!)
   shift 2
 done

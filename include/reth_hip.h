@@ -692,6 +692,26 @@ int64_t rth_clip_adam_workspace(void);
 int rth_clip_adam(const rth_param_tensor *tensors, int32_t n_tensors, double lr, double beta1, double beta2,
                   double eps, double max_norm, int64_t *step_dev, void *workspace_dev, float *total_norm_out_dev,
                   void *stream);
+/* The same step with clip_grad_norm_'s partials produced by the learner's backward (r06, one
+ * rank: the gradients are final there).  rth_conv1_relu_wgrad_norm is rth_conv_relu_wgrad_ex
+ * (rows_dev != NULL: stacks by row; fids_dev != NULL: rth_conv1_frames_relu_wgrad_ex's frame
+ * ids, x_dev the frame store; neither: x_dev the stacks) whose reduce launch also writes the
+ * fp64 sum-of-squares partials clip_grad_norm_ reduces: extra workgroups over the gradients of
+ * `sq` (every parameter but conv1's weight and bias and the deferred bias gradients, which the
+ * launch finishes itself and adds right behind them; only .grad and .n are read), the first of
+ * them advancing step_dev and writing the step's bias corrections as rth_clip_adam's first
+ * launch does, all into adam_workspace_dev (rth_clip_adam_workspace's layout);
+ * *nparts_out = the partial count.  rth_adam_prenormed(..., nparts, ...) is then
+ * rth_clip_adam's second launch alone: the same update, the norm summed in partial order. */
+int rth_conv1_relu_wgrad_norm(const rth_conv_shape *shape, const void *x_dev, const int64_t *rows_dev,
+                              const int32_t *fids_dev, int64_t n, const float *g_dev, const float *y_dev,
+                              float *gw_dev, float *gb_dev, void *workspace_dev, const rth_bias_deferred *deferred,
+                              int32_t ndeferred, const rth_param_tensor *sq, int32_t n_sq, double lr, double beta1,
+                              double beta2, int64_t *step_dev, void *adam_workspace_dev, int32_t *nparts_out,
+                              void *stream);
+int rth_adam_prenormed(const rth_param_tensor *tensors, int32_t n_tensors, double lr, double beta1, double beta2,
+                       double eps, double max_norm, int32_t nparts, int64_t *step_dev, void *workspace_dev,
+                       float *total_norm_out_dev, void *stream);
 
 /* ------------------------------------------------------------------------------------
  * Learner -> actor weights: a device-resident latest-wins slot with a device version.

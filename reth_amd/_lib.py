@@ -202,6 +202,10 @@ SIGNATURES = {
     "rth_tree_update_timeouts": (c_i32, [ctypes.POINTER(c_i64)]),
     "rth_debug_conv_clock": (c_i32, [c_vp, c_i32]),
     "rth_clip_adam": (c_i32, [c_vp, c_i32, c_f64, c_f64, c_f64, c_f64, c_f64, c_vp, c_vp, c_vp, c_vp]),
+    "rth_adam_prenormed": (c_i32, [c_vp, c_i32, c_f64, c_f64, c_f64, c_f64, c_f64, c_i32, c_vp, c_vp, c_vp, c_vp]),
+    "rth_conv1_relu_wgrad_norm": (c_i32, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp,
+                                          c_vp, c_vp, c_i32, c_vp, c_i32, c_f64, c_f64, c_f64, c_vp, c_vp,
+                                          ctypes.POINTER(c_i32), c_vp]),
     # learner -> actor weights slot (perwez PUB/SUB CONFLATE)
     "rth_weights_create": (c_i32, [c_i64, c_i32, ctypes.POINTER(c_vp)]),
     "rth_weights_destroy": (c_i32, [c_vp]),

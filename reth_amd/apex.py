@@ -431,7 +431,8 @@ class ApexDQN:
                     data, idx, isw = slots[p]
                     probe = (lambda items, last=False: cut(("probe", items), last=last)) if pr else None
                     td = solver.compute_grads(data, isw, q1t=G["q1t"][p] if variant == "pre" else None,
-                                              mid=(lambda b: cut(("bucket", b))) if split else None, probe=probe)
+                                              mid=(lambda b: cut(("bucket", b))) if split else None, probe=probe,
+                                              prenorm=not split)
                     self.trainer._track(td)
                     if split and not any(k == "bucket" for k, _ in bounds):  # autograd path: one bucket
                         cut(("bucket", [q.grad for q in solver._params]))

@@ -33,6 +33,7 @@
 #include <type_traits>
 
 #include "common.hpp"
+#include "optim.hpp"
 
 namespace rth {
 
@@ -1777,7 +1778,8 @@ struct BiasJobs {
   int n;
 };
 
-__device__ void bias_job(const BiasJobs &bj, int j) {
+// sq (nullable): the fp64 sum of squares of the finished db (clip_grad_norm_'s partial, r06)
+__device__ void bias_job(const BiasJobs &bj, int j, double *sq = nullptr) {
   __shared__ float red[kBiasVLanes];
   constexpr int Q = kBiasVLanes / 256, U = 16;
   const int C = bj.C[j], G = kBiasVLanes / C, tid = threadIdx.x, slabs = bj.slabs[j];
@@ -1816,61 +1818,29 @@ __device__ void bias_job(const BiasJobs &bj, int j) {
     __syncthreads();
   }
   if (tid < C) bj.db[j][tid] = red[tid];
+  if (sq) {
+    __shared__ double red4[4];
+    const double d = tid < C ? (double)red[tid] : 0.0;
+    const double t = block_sum(rmul(d, d), red4);
+    if (tid == 0) *sq = t;
+  }
 }
 
-// the same sums with one load round trip per thread: a workgroup takes 16 consecutive
-// elements, its 16 lane groups 16 consecutive partial blocks each (all 16 loads in flight), the
-// 16 group sums added in group order -- still a fixed order (another association than the
-// 4 x 64 form below).  Opt-in (RTH_WGRED_WIDE=1): no faster in the loop (r04)
+// workgroup blk of conv1's weight-gradient reduce: 64 of its E outputs, or (blk >= RB) a
+// deferred bias gradient.  sq (nullable): the fp64 sum of squares of what the workgroup
+// finished goes to sq[blk] (r06: clip_grad_norm_'s partials from the backward)
 template <int KH, int KW, int CIN, int COUT>
-__global__ __launch_bounds__(256) void k_wgrad_reduce16(const float *__restrict__ partial, int blocks,
-                                                        float *__restrict__ gw, float *__restrict__ gb, BiasJobs bj) {
-  constexpr int K = CIN * KH * KW, E = COUT * K + COUT, RB = (E + 15) / 16;
-  __shared__ float part[16][16];
-  if ((int)blockIdx.x >= RB) {  // a deferred bias gradient
-    bias_job(bj, blockIdx.x - RB);
-    return;
-  }
-  const int grp = threadIdx.x >> 4, l = threadIdx.x & 15;
-  const int e = blockIdx.x * 16 + l;
-  const int per = (blocks + 15) / 16, w0 = grp * per, w1 = w0 + per < blocks ? w0 + per : blocks;
-  float v = 0.0f;
-  if (e < E) {
-    int w = w0;
-    for (; w + 16 <= w1; w += 16) {
-      float t[16];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) t[u] = partial[(int64_t)(w + u) * E + e];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) v = radd(v, t[u]);
-    }
-    for (; w < w1; ++w) v = radd(v, partial[(int64_t)w * E + e]);
-  }
-  part[grp][l] = v;
-  __syncthreads();
-  if (grp != 0 || e >= E) return;
-  v = part[0][l];
-#pragma unroll
-  for (int q = 1; q < 16; ++q) v = radd(v, part[q][l]);
-  if (e >= COUT * K) {
-    gb[e - COUT * K] = v;
-    return;
-  }
-  const int oi = e / K, kk = e % K, kw = kk / 32, ci = (kk % 32) / KH, kh = kk % KH;
-  gw[((oi * KH + kh) * KW + kw) * CIN + ci] = v;
-}
-
-template <int KH, int KW, int CIN, int COUT>
-__global__ __launch_bounds__(256) void k_wgrad_reduce(const float *__restrict__ partial, int blocks,
-                                                      float *__restrict__ gw, float *__restrict__ gb, BiasJobs bj) {
+__device__ __forceinline__ void wgrad_reduce_wg(int blk, const float *__restrict__ partial, int blocks,
+                                                float *__restrict__ gw, float *__restrict__ gb, const BiasJobs &bj,
+                                                double *__restrict__ sq) {
   constexpr int K = CIN * KH * KW, E = COUT * K + COUT, RB = (E + 63) / 64;
   __shared__ float part[4][64];
-  if ((int)blockIdx.x >= RB) {  // a deferred bias gradient
-    bias_job(bj, blockIdx.x - RB);
+  if (blk >= RB) {  // a deferred bias gradient
+    bias_job(bj, blk - RB, sq ? sq + blk : nullptr);
     return;
   }
   const int grp = threadIdx.x / 64, l = threadIdx.x % 64;
-  const int e = blockIdx.x * 64 + l;
+  const int e = blk * 64 + l;
   const int per = (blocks + 3) / 4, w0 = grp * per, w1 = w0 + per < blocks ? w0 + per : blocks;
   float v = 0.0f;
   if (e < E) {
@@ -1900,14 +1870,44 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const float *__restrict__ 
   }
   part[grp][l] = v;
   __syncthreads();
-  if (grp != 0 || e >= E) return;
+  if (grp != 0) return;  // (wave-uniform)
   v = radd(radd(radd(part[0][l], part[1][l]), part[2][l]), part[3][l]);
+  if (sq) {  // wave 0's 64 outputs, a fixed shuffle tree
+    double d = e < E ? rmul((double)v, (double)v) : 0.0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) d = radd(d, __shfl_down(d, o, 64));
+    if (l == 0) sq[blk] = d;
+  }
+  if (e >= E) return;
   if (e >= COUT * K) {
     gb[e - COUT * K] = v;
     return;
   }
   const int oi = e / K, kk = e % K, kw = kk / 32, ci = (kk % 32) / KH, kh = kk % KH;
   gw[((oi * KH + kh) * KW + kw) * CIN + ci] = v;
+}
+
+template <int KH, int KW, int CIN, int COUT>
+__global__ __launch_bounds__(256) void k_wgrad_reduce(const float *__restrict__ partial, int blocks,
+                                                      float *__restrict__ gw, float *__restrict__ gb, BiasJobs bj) {
+  wgrad_reduce_wg<KH, KW, CIN, COUT>(blockIdx.x, partial, blocks, gw, gb, bj, nullptr);
+}
+
+// the same reduce launch with clip_grad_norm_'s partials (r06, one rank): workgroups [0, nsq)
+// are norm-partial workgroups over the gradients final before it (optim.hpp's grad_sqsum_wg,
+// workgroup 0 advancing Adam's step count), the rest the reduce's, each writing the sum of
+// squares of the gradients it finishes -- conv1's weight and bias, the deferred bias gradients
+// -- right behind them: rth_adam_prenormed then runs the update alone
+template <int KH, int KW, int CIN, int COUT>
+__global__ __launch_bounds__(256) void k_wgrad_reduce_norm(const float *__restrict__ partial, int blocks,
+                                                           float *__restrict__ gw, float *__restrict__ gb, BiasJobs bj,
+                                                           OptArgs na, int nsq, double *__restrict__ npart,
+                                                           SqStep st) {
+  if ((int)blockIdx.x < nsq) {
+    grad_sqsum_wg(na, blockIdx.x, npart, st);
+    return;
+  }
+  wgrad_reduce_wg<KH, KW, CIN, COUT>((int)blockIdx.x - nsq, partial, blocks, gw, gb, bj, npart + nsq);
 }
 
 constexpr int wg_per_cu() { return 2; }
@@ -2140,9 +2140,19 @@ int64_t rth_conv_wgrad_workspace(const rth_conv_shape *shape) {
   return is_conv1_u8(shape) ? (int64_t)kWgBlocks * (32 * 256 + 32) * 4 : 0;
 }
 
+// (norm: clip_grad_norm_'s partials in the reduce launch, rth_conv1_relu_wgrad_norm)
+struct NormJob {
+  const rth_param_tensor *sq;
+  int32_t n_sq;
+  double lr, beta1, beta2;
+  int64_t *step;
+  void *adam_ws;
+  int32_t *nparts_out;
+};
 static int conv1_relu_wgrad(const rth_conv_shape *shape, const void *x, const int64_t *rows, const int32_t *fids,
                             int64_t n, const float *g, const float *y, float *gw, float *gb, void *workspace,
-                            const rth_bias_deferred *deferred, int32_t ndeferred, void *stream);
+                            const rth_bias_deferred *deferred, int32_t ndeferred, void *stream,
+                            const NormJob *norm = nullptr);
 
 int rth_conv_relu_wgrad_ex(const rth_conv_shape *shape, const void *x, const int64_t *rows, int64_t n, const float *g,
                            const float *y, float *gw, float *gb, void *workspace, const rth_bias_deferred *deferred,
@@ -2158,9 +2168,26 @@ int rth_conv1_frames_relu_wgrad_ex(const rth_conv_shape *shape, const uint8_t *s
   return conv1_relu_wgrad(shape, store, nullptr, ids, n, g, y, gw, gb, workspace, deferred, ndeferred, stream);
 }
 
+int rth_conv1_relu_wgrad_norm(const rth_conv_shape *shape, const void *x, const int64_t *rows, const int32_t *fids,
+                              int64_t n, const float *g, const float *y, float *gw, float *gb, void *workspace,
+                              const rth_bias_deferred *deferred, int32_t ndeferred, const rth_param_tensor *sq,
+                              int32_t n_sq, double lr, double beta1, double beta2, int64_t *step_dev,
+                              void *adam_workspace_dev, int32_t *nparts_out, void *stream) {
+  RTH_REQUIRE(!(rows && fids) && sq && n_sq >= 1 && n_sq <= RTH_MAX_PARAM_TENSORS && step_dev && adam_workspace_dev &&
+                  nparts_out && n > 0,
+              "rth_conv1_relu_wgrad_norm: bad arguments (rows and fids, %d tensors, a batch of %lld)", n_sq,
+              (long long)n);
+  for (int i = 0; i < n_sq; ++i)
+    RTH_REQUIRE(sq[i].grad && sq[i].n >= 1, "rth_conv1_relu_wgrad_norm: tensor %d incomplete", i);
+  if (fids)
+    RTH_REQUIRE((reinterpret_cast<uintptr_t>(fids) & 15) == 0, "rth_conv1_relu_wgrad_norm: misaligned frame ids");
+  const NormJob nj{sq, n_sq, lr, beta1, beta2, step_dev, adam_workspace_dev, nparts_out};
+  return conv1_relu_wgrad(shape, x, rows, fids, n, g, y, gw, gb, workspace, deferred, ndeferred, stream, &nj);
+}
+
 static int conv1_relu_wgrad(const rth_conv_shape *shape, const void *x, const int64_t *rows, const int32_t *fids,
                             int64_t n, const float *g, const float *y, float *gw, float *gb, void *workspace,
-                            const rth_bias_deferred *deferred, int32_t ndeferred, void *stream) {
+                            const rth_bias_deferred *deferred, int32_t ndeferred, void *stream, const NormJob *norm) {
   RTH_REQUIRE(shape && x && g && y && gw && gb && workspace && n >= 0, "rth_conv_relu_wgrad: NULL argument");
   RTH_REQUIRE(ndeferred >= 0 && ndeferred <= kBiasJobsMax && (ndeferred == 0 || deferred),
               "rth_conv_relu_wgrad_ex: %d deferred bias gradients (at most %d)", ndeferred, kBiasJobsMax);
@@ -2189,9 +2216,25 @@ static int conv1_relu_wgrad(const rth_conv_shape *shape, const void *x, const in
                      dim3(kWgBlocks), dim3(kWgWaves * 64), 0, as_stream(stream), static_cast<const uint8_t *>(x),
                      fids ? reinterpret_cast<const int64_t *>(fids) : rows, n, g, y, part);
   RTH_LAUNCHED();
-  hipLaunchKernelGGL((k_wgrad_reduce<8, 8, 4, 32>), dim3((32 * 256 + 32 + 63) / 64 + ndeferred), dim3(256), 0,
-                     as_stream(stream), part, kWgBlocks, gw, gb, bj);
+  constexpr int RB = (32 * 256 + 32 + 63) / 64;
+  if (!norm) {
+    hipLaunchKernelGGL((k_wgrad_reduce<8, 8, 4, 32>), dim3(RB + ndeferred), dim3(256), 0, as_stream(stream), part,
+                       kWgBlocks, gw, gb, bj);
+    RTH_LAUNCHED();
+    return RTH_OK;
+  }
+  OptArgs na{};
+  const int64_t nsq = opt_segments(norm->sq, norm->n_sq, kOptChunk, &na);
+  const int64_t nparts = nsq + RB + ndeferred;
+  RTH_REQUIRE(nparts <= kMaxPartials, "rth_conv1_relu_wgrad_norm: %lld norm partials (at most %d)",
+              (long long)nparts, kMaxPartials);
+  auto *npart = static_cast<double *>(norm->adam_ws);  // rth_clip_adam_workspace's layout (optim.hip)
+  auto *bc = reinterpret_cast<BiasCorr *>(static_cast<uint8_t *>(norm->adam_ws) + (int64_t)kMaxPartials * 8 + 16);
+  const SqStep st{norm->step, bc, norm->lr, norm->beta1, norm->beta2};
+  hipLaunchKernelGGL((k_wgrad_reduce_norm<8, 8, 4, 32>), dim3((unsigned)(nsq + RB + ndeferred)), dim3(256), 0,
+                     as_stream(stream), part, kWgBlocks, gw, gb, bj, na, (int)nsq, npart, st);
   RTH_LAUNCHED();
+  *norm->nparts_out = (int32_t)nparts;
   return RTH_OK;
 }
 

@@ -12,84 +12,13 @@
 // The step count t lives on the device (graph replay).  The global norm is a deterministic
 // two-stage reduction (per-workgroup fp64 partials, combined in workgroup order); torch's
 // fused/foreach kernels chunk 65,536 elements per workgroup (~30 workgroups for the 1.69 M
-// Q-net parameters), here every workgroup takes 4,096 elements (~420 workgroups).
-#include "common.hpp"
+// Q-net parameters), here every workgroup takes 2,048 elements (~830 workgroups).  On one rank
+// the partials can come from the learner's backward instead (rth_conv1_relu_wgrad_norm: extra
+// workgroups of conv1's weight-gradient reduce launch), leaving the update alone
+// (rth_adam_prenormed, r06).
+#include "optim.hpp"
 
 namespace rth {
-
-constexpr int kOptThreads = 256;
-constexpr int kOptChunk = 4096;   // elements per k_grad_sqsum workgroup (16 per lane)
-constexpr int kAdamChunk = 2048;  // elements per k_adam workgroup (8 per lane): twice the
-                                  // workgroups, so one's stores overlap another's loads (r06)
-constexpr int kMaxPartials = 1 << 15;
-
-struct OptSeg {
-  float *param;
-  const float *grad;
-  float *m;
-  float *v;
-  int64_t n;
-  int64_t blk0;  // first workgroup of this tensor
-  int vec;       // all four pointers 16-byte aligned: float4 accesses
-};
-
-constexpr int kOptV = kOptChunk / kOptThreads / 4;    // float4 groups per lane (k_grad_sqsum)
-constexpr int kAdamV = kAdamChunk / kOptThreads / 4;  // float4 groups per lane (k_adam)
-
-// the workgroup's sum of one fp64 value per lane in a fixed order (r06: a wavefront shuffle
-// tree, then the 4 waves in order; was an 8-step LDS tree with a barrier per step): every
-// lane returns the same sum
-__device__ __forceinline__ double block_sum(double v, double *red4) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = radd(v, __shfl_down(v, o, 64));
-  if ((threadIdx.x & 63) == 0) red4[threadIdx.x >> 6] = v;
-  __syncthreads();
-  double t = red4[0];
-#pragma unroll
-  for (int w = 1; w < kOptThreads / 64; ++w) t = radd(t, red4[w]);
-  return t;
-}
-
-// lane's k-th float4 group of the chunk at element base: elements base + 4 (k T + tid) + 0..3,
-// zero past n
-__device__ __forceinline__ float4 ld4(const float *__restrict__ p, int64_t e, int64_t n, int vec) {
-  if (vec && e + 3 < n) return *reinterpret_cast<const float4 *>(p + e);
-  float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (e < n) r.x = p[e];
-  if (e + 1 < n) r.y = p[e + 1];
-  if (e + 2 < n) r.z = p[e + 2];
-  if (e + 3 < n) r.w = p[e + 3];
-  return r;
-}
-
-// the same load from a buffer resource over [p, p + n): one unconditional dwordx4 whose dwords
-// past n read zero (the range check), so no load sits under a branch -- the branchy form made
-// the compiler wait for each load before issuing the next.  vec segments only (16-byte aligned).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t seg_rsrc(const float *p, int64_t n) {
-  const uint64_t a = reinterpret_cast<uint64_t>(p);  // wave-uniform (the workgroup's segment)
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-  const int bytes = __builtin_amdgcn_readfirstlane((int)(n * 4));
-  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(((uint64_t)hi << 32) | lo), 0, bytes, 0x00020000);
-}
-__device__ __forceinline__ float4 ld4b(__amdgpu_buffer_rsrc_t r, int64_t e) {
-  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, (uint32_t)(e * 4), 0, 0));
-}
-
-__device__ __forceinline__ void st4(float *__restrict__ p, int64_t e, int64_t n, int vec, float4 v) {
-  if (vec && e + 3 < n) {
-    *reinterpret_cast<float4 *>(p + e) = v;
-    return;
-  }
-  if (e < n) p[e] = v.x;
-  if (e + 1 < n) p[e + 1] = v.y;
-  if (e + 2 < n) p[e + 2] = v.z;
-  if (e + 3 < n) p[e + 3] = v.w;
-}
-
-struct OptArgs {
-  OptSeg seg[RTH_MAX_PARAM_TENSORS];
-  int32_t nseg;
-};
 
 // scalars the combine stage hands to the Adam stage (workspace layout after the partials)
 struct OptScalars {
@@ -98,23 +27,6 @@ struct OptScalars {
   float bc2_sqrt;     // sqrt(1 - beta2^t)
   float total_norm;   // ||g||_2 before clipping (clip_grad_norm_'s return value)
 };
-
-__device__ __forceinline__ int seg_of(const OptArgs &a, int64_t b) {
-  int s = 0;
-  while (s + 1 < a.nseg && b >= a.seg[s + 1].blk0) ++s;
-  return s;
-}
-
-// the bias corrections of step t (python-float scalars of adam.py, cast to f32 where they meet
-// the f32 tensors): lr / (1 - beta1^t), sqrt(1 - beta2^t)
-struct BiasCorr {
-  float step_size, bc2_sqrt;
-};
-__device__ __forceinline__ BiasCorr bias_corr(double lr, double beta1, double beta2, int64_t t) {
-  const double bc1 = 1.0 - pow(beta1, (double)t);
-  const double bc2 = 1.0 - pow(beta2, (double)t);
-  return BiasCorr{(float)(lr / bc1), (float)sqrt(bc2)};
-}
 
 // the norm and the clip coefficient from the per-workgroup partials (summed in workgroup
 // order: deterministic), `acc` = this lane's in-order sum of partials tid, tid + T, ...  Every
@@ -141,40 +53,10 @@ struct ScalarArgs {
   BiasCorr *bc;  // written by k_grad_sqsum's workgroup 0, read by every k_adam workgroup
 };
 
-// per-workgroup sums of squares of the gradients (fp64 partials); workgroup 0 advances the
-// device step count and writes the new step's bias corrections
+// per-workgroup sums of squares of the gradients (fp64 partials, grad_sqsum_wg); workgroup 0
+// advances the device step count and writes the new step's bias corrections
 __global__ __launch_bounds__(kOptThreads) void k_grad_sqsum(OptArgs a, double *__restrict__ part, ScalarArgs sa) {
-  __shared__ double red[kOptThreads / 64];
-  const int64_t b = blockIdx.x;
-  const OptSeg &sg = a.seg[seg_of(a, b)];
-  const int64_t base = (b - sg.blk0) * kOptChunk;
-  float4 gv[kOptV];  // every load of the chunk in flight before the first use
-  if (sg.vec) {
-    const __amdgpu_buffer_rsrc_t rg = seg_rsrc(sg.grad, sg.n);
-#pragma unroll
-    for (int k = 0; k < kOptV; ++k) gv[k] = ld4b(rg, base + 4 * (k * kOptThreads + threadIdx.x));
-  } else {
-#pragma unroll
-    for (int k = 0; k < kOptV; ++k) gv[k] = ld4(sg.grad, base + 4 * (k * kOptThreads + threadIdx.x), sg.n, 0);
-  }
-  double acc = 0.0;
-#pragma unroll
-  for (int k = 0; k < kOptV; ++k) {
-    const double x = gv[k].x, y = gv[k].y, z = gv[k].z, w = gv[k].w;
-    acc = radd(acc, rmul(x, x));
-    acc = radd(acc, rmul(y, y));
-    acc = radd(acc, rmul(z, z));
-    acc = radd(acc, rmul(w, w));
-  }
-  const double wsum = block_sum(acc, red);
-  if (threadIdx.x == 0) {
-    part[b] = wsum;
-    if (b == 0) {
-      const int64_t t = *sa.step + 1;
-      *sa.step = t;
-      *sa.bc = bias_corr(sa.lr, sa.beta1, sa.beta2, t);
-    }
-  }
+  grad_sqsum_wg(a, blockIdx.x, part, SqStep{sa.step, sa.bc, sa.lr, sa.beta1, sa.beta2});
 }
 
 __global__ __launch_bounds__(kOptThreads) void k_adam(OptArgs a, const double *__restrict__ part, int nparts,
@@ -186,9 +68,9 @@ __global__ __launch_bounds__(kOptThreads) void k_adam(OptArgs a, const double *_
   // the partials and the bias corrections are loaded first and the chunk's loads issued behind
   // them, so the norm's reduction runs while the chunk is in flight (the load counter is in
   // order: waiting for the partials does not wait for the chunk)
-  double pacc = 0.0, pl[4];
+  double pacc = 0.0, pl[kPartLoads];
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {  // unconditional loads (a clamped index): none waits under a branch
+  for (int u = 0; u < kPartLoads; ++u) {  // unconditional loads (a clamped index): none waits under a branch
     const int k = threadIdx.x + u * kOptThreads;
     pl[u] = part[k < nparts ? k : nparts - 1];
   }
@@ -198,11 +80,11 @@ __global__ __launch_bounds__(kOptThreads) void k_adam(OptArgs a, const double *_
   auto sum_parts = [&]() __attribute__((always_inline)) {
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) asm volatile("" : "+v"(pl[u]));  // keeps the sum behind the loads
+    for (int u = 0; u < kPartLoads; ++u) asm volatile("" : "+v"(pl[u]));  // keeps the sum behind the loads
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int u = 0; u < kPartLoads; ++u)
       if (threadIdx.x + u * kOptThreads < nparts) pacc = radd(pacc, pl[u]);
-    for (int k = threadIdx.x + 4 * kOptThreads; k < nparts; k += kOptThreads) pacc = radd(pacc, part[k]);
+    for (int k = threadIdx.x + kPartLoads * kOptThreads; k < nparts; k += kOptThreads) pacc = radd(pacc, part[k]);
   };
   __builtin_amdgcn_sched_barrier(0);
   float4 gv[kAdamV], mv[kAdamV], vv[kAdamV], pv[kAdamV];
@@ -267,47 +149,52 @@ extern "C" {
 // (k_grad_sqsum -> k_adam, 8 B)]
 int64_t rth_clip_adam_workspace(void) { return (int64_t)kMaxPartials * 8 + 64; }
 
-int rth_clip_adam(const rth_param_tensor *tensors, int32_t n_tensors, double lr, double beta1, double beta2,
-                  double eps, double max_norm, int64_t *step_dev, void *workspace_dev, float *total_norm_out,
-                  void *stream) {
+static int adam_launch(const rth_param_tensor *tensors, int32_t n_tensors, double lr, double beta1, double beta2,
+                       double eps, double max_norm, int64_t *step_dev, void *workspace_dev, float *total_norm_out,
+                       int nparts, bool sqsum, hipStream_t s) {
   RTH_REQUIRE(tensors && step_dev && workspace_dev, "rth_clip_adam: NULL argument");
   RTH_REQUIRE(n_tensors >= 1 && n_tensors <= RTH_MAX_PARAM_TENSORS, "rth_clip_adam: %d tensors not in [1, %d]",
               n_tensors, RTH_MAX_PARAM_TENSORS);
-  OptArgs a{};
-  int64_t blocks = 0;
-  for (int s = 0; s < n_tensors; ++s) {
-    const rth_param_tensor &t = tensors[s];
-    RTH_REQUIRE(t.param && t.grad && t.exp_avg && t.exp_avg_sq && t.n >= 1, "rth_clip_adam: tensor %d incomplete", s);
-    const uintptr_t al = reinterpret_cast<uintptr_t>(t.param) | reinterpret_cast<uintptr_t>(t.grad) |
-                         reinterpret_cast<uintptr_t>(t.exp_avg) | reinterpret_cast<uintptr_t>(t.exp_avg_sq);
-    a.seg[s] = OptSeg{t.param, t.grad, t.exp_avg, t.exp_avg_sq, t.n, blocks, (al & 15) == 0 ? 1 : 0};
-    blocks += (t.n + kOptChunk - 1) / kOptChunk;
-  }
-  a.nseg = n_tensors;
-  RTH_REQUIRE(blocks <= kMaxPartials, "rth_clip_adam: %lld elements exceed the workspace",
-              (long long)(blocks * kOptChunk));
-  OptArgs ad = a;  // the same segments at k_adam's chunk size
-  int64_t ablocks = 0;
-  for (int s = 0; s < n_tensors; ++s) {
-    ad.seg[s].blk0 = ablocks;
-    ablocks += (tensors[s].n + kAdamChunk - 1) / kAdamChunk;
-  }
+  for (int i = 0; i < n_tensors; ++i)
+    RTH_REQUIRE(tensors[i].param && tensors[i].grad && tensors[i].exp_avg && tensors[i].exp_avg_sq && tensors[i].n >= 1,
+                "rth_clip_adam: tensor %d incomplete", i);
+  OptArgs a{}, ad{};
+  const int64_t blocks = opt_segments(tensors, n_tensors, kOptChunk, &a);
+  const int64_t ablocks = opt_segments(tensors, n_tensors, kAdamChunk, &ad);  // the same segments at k_adam's chunk
+  if (sqsum) nparts = (int)(blocks < kMaxPartials ? blocks : kMaxPartials + 1);
+  RTH_REQUIRE(nparts >= 1 && nparts <= kMaxPartials, "rth_clip_adam: %d norm partials (at most %d)", nparts,
+              kMaxPartials);
   auto *part = static_cast<double *>(workspace_dev);
   auto *sc = reinterpret_cast<OptScalars *>(static_cast<uint8_t *>(workspace_dev) + (int64_t)kMaxPartials * 8);
   const int clip = max_norm >= 0.0;
-  hipStream_t s = as_stream(stream);
   auto *bcw = reinterpret_cast<BiasCorr *>(static_cast<uint8_t *>(workspace_dev) + (int64_t)kMaxPartials * 8 + 16);
   const ScalarArgs sa{clip, (float)max_norm, lr, beta1, beta2, step_dev, sc, total_norm_out, bcw};
   // r05 tried one launch with a grid barrier through tagged granules (every load issued once):
   // faster alone (16.8 us) but 37-40 us per call in the loop, where its all-resident grid waits
   // for CUs the actor stream's convolutions hold -- removed in r06 (profiles/r05)
-  hipLaunchKernelGGL(k_grad_sqsum, dim3((unsigned)blocks), dim3(kOptThreads), 0, s, a, part, sa);
-  RTH_LAUNCHED();
+  if (sqsum) {
+    hipLaunchKernelGGL(k_grad_sqsum, dim3((unsigned)blocks), dim3(kOptThreads), 0, s, a, part, sa);
+    RTH_LAUNCHED();
+  }
   // 1 - beta1 and 1 - beta2 are python floats in adam.py, rounded to f32 once
-  hipLaunchKernelGGL(k_adam, dim3((unsigned)ablocks), dim3(kOptThreads), 0, s, ad, part, (int)blocks, sa,
+  hipLaunchKernelGGL(k_adam, dim3((unsigned)ablocks), dim3(kOptThreads), 0, s, ad, part, nparts, sa,
                      (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), (float)eps);
   RTH_LAUNCHED();
   return RTH_OK;
+}
+
+int rth_clip_adam(const rth_param_tensor *tensors, int32_t n_tensors, double lr, double beta1, double beta2,
+                  double eps, double max_norm, int64_t *step_dev, void *workspace_dev, float *total_norm_out,
+                  void *stream) {
+  return adam_launch(tensors, n_tensors, lr, beta1, beta2, eps, max_norm, step_dev, workspace_dev, total_norm_out, 0,
+                     true, as_stream(stream));
+}
+
+int rth_adam_prenormed(const rth_param_tensor *tensors, int32_t n_tensors, double lr, double beta1, double beta2,
+                       double eps, double max_norm, int32_t nparts, int64_t *step_dev, void *workspace_dev,
+                       float *total_norm_out, void *stream) {
+  return adam_launch(tensors, n_tensors, lr, beta1, beta2, eps, max_norm, step_dev, workspace_dev, total_norm_out,
+                     nparts, false, as_stream(stream));
 }
 
 }  // extern "C"

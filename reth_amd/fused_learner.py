@@ -48,6 +48,10 @@ DGRAD_PREPACK = True
 # DGRAD_MASK -- conv3's data gradient applies conv2's ReLU mask and writes conv2's bias-gradient
 # slabs in its own epilogue (rth_conv_dgrad_relu_prepacked): one launch fewer per update
 DGRAD_MASK = True
+# NORM_IN_BACKWARD -- one rank, ClipAdam: clip_grad_norm_'s partials written by conv1's
+# weight-gradient reduce launch (extra workgroups over the gradients final before it, and the
+# squares of what it finishes itself), so the optimizer step is rth_adam_prenormed alone (r06)
+NORM_IN_BACKWARD = True
 
 
 def _net_workspace(net, kind, shape, device):
@@ -99,7 +103,7 @@ def _nhwc(t):
     return t if t.is_contiguous(memory_format=torch.channels_last) else t.contiguous(memory_format=torch.channels_last)
 
 
-def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None, mid=None, probe=None):
+def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None, mid=None, probe=None, prenorm=False):
     """forward + TD + backward of one learner batch; sets .grad of every online parameter
     and returns (loss [], |td| [B]).  q1t: the target network's heads on s1 if precomputed
     (DQNSolver.target_heads).  td_acc (nullable f32 device scalar): += mean |td|.
@@ -238,7 +242,21 @@ def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None, mid=No
                 assert len(deferred) <= 4, "rth_conv_relu_wgrad_ex finishes at most 4 deferred bias gradients"
                 jobs = (_lib.BiasDeferred * max(len(deferred), 1))(*deferred)
                 ws1 = _net_workspace(net, "conv1", shapes[0], x.device)
-                if frames:
+                opt = solver.optimizer
+                if prenorm and NORM_IN_BACKWARD and mid is None and solver.grad_hook is None and hasattr(opt, "prenorm"):
+                    # every gradient but conv1's weight and bias and the deferred biases (this
+                    # launch finishes those) is final here: the heads' and conv2 / conv3's weights
+                    done = {d.db for d in deferred}
+                    sq = [gr for gr in [gw1[:Hh], gw1[Hh:], gb1[:Hh], gb1[Hh:], *g2]]
+                    sq += [grads[c.weight] for c in convs[1:]] + [grads[c.bias] for c in convs[1:]
+                                                                  if grads[c.bias].data_ptr() not in done]
+                    arr, n_sq = opt.norm_tensors(sq)
+                    nparts = ctypes.c_int32(0)
+                    call("rth_conv1_relu_wgrad_norm", ctypes.byref(shapes[0]), ptr(x.store) if frames else ptr(x), None,
+                         ptr(x.ids) if frames else None, B, ptr(_nhwc(g)), ptr(y), ptr(gw), ptr(db), ptr(ws1), jobs,
+                         len(deferred), arr, n_sq, *opt.prenorm_scalars(), ctypes.byref(nparts), st)
+                    opt.prenorm(nparts.value)
+                elif frames:
                     call("rth_conv1_frames_relu_wgrad_ex", ctypes.byref(shapes[0]), ptr(x.store), ptr(x.ids), B,
                          ptr(_nhwc(g)), ptr(y), ptr(gw), ptr(db), ptr(ws1), jobs, len(deferred), st)
                 else:

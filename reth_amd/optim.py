@@ -39,6 +39,7 @@ class ClipAdam(torch.optim.Optimizer):
         self._step = torch.zeros(1, dtype=torch.int64, device=dev)
         self._ws = torch.zeros(_lib.lib().rth_clip_adam_workspace(), dtype=torch.uint8, device=dev)  # ticket = 0
         self.total_norm = torch.zeros(1, dtype=torch.float32, device=dev)
+        self._prenormed = None  # norm partials of the next step written by the backward (prenorm)
         for p in ps:
             st = self.state[p]
             st["exp_avg"] = torch.zeros_like(p)  # same strides as the parameter
@@ -66,7 +67,30 @@ class ClipAdam(torch.optim.Optimizer):
         if not tensors:
             return loss
         arr = (ParamTensor * len(tensors))(*tensors)
+        nparts, self._prenormed = self._prenormed, None
+        if nparts is not None:  # the norm partials (and the step count) came from the backward
+            call("rth_adam_prenormed", ctypes.cast(arr, _lib.c_vp), len(tensors), float(g["lr"]), float(beta1),
+                 float(beta2), float(g["eps"]), -1.0 if mn is None or mn < 0 else float(mn), nparts, ptr(self._step),
+                 ptr(self._ws), ptr(self.total_norm), stream_ptr())
+            return loss
         call("rth_clip_adam", ctypes.cast(arr, _lib.c_vp), len(tensors), float(g["lr"]), float(beta1), float(beta2),
              float(g["eps"]), -1.0 if mn is None or mn < 0 else float(mn), ptr(self._step), ptr(self._ws),
              ptr(self.total_norm), stream_ptr())
         return loss
+
+    # ---- the norm partials written by the learner's backward (rth_conv1_relu_wgrad_norm, one rank)
+    def norm_tensors(self, grads):
+        """(rth_param_tensor array, count) of the gradients whose squares the backward's launch
+        sums (only .grad and .n are read)"""
+        ts = [ParamTensor(gr.data_ptr(), gr.data_ptr(), gr.data_ptr(), gr.data_ptr(), gr.numel()) for gr in grads]
+        return (ParamTensor * len(ts))(*ts), len(ts)
+
+    def prenorm_scalars(self):
+        """(lr, beta1, beta2, step, workspace) for the launch that advances the step count"""
+        g = self.param_groups[0]
+        beta1, beta2 = g["betas"]
+        return float(g["lr"]), float(beta1), float(beta2), ptr(self._step), ptr(self._ws)
+
+    def prenorm(self, nparts):
+        """the next step() runs the update alone over `nparts` partials the backward wrote"""
+        self._prenormed = int(nparts)

@@ -257,16 +257,19 @@ class DQNSolver(Algorithm):
     def calc_loss(self, batch):
         return self.calc_loss_device(batch).cpu()
 
-    def compute_grads(self, batch, weights=None, q1t=None, mid=None, probe=None):
+    def compute_grads(self, batch, weights=None, q1t=None, mid=None, probe=None, prenorm=False):
         """dqn_solver.py:104-117: forward passes, fused TD/Huber, backward -> |td| (device).
         q1t: the target network's output on this batch's s1 if already computed
         (target_heads), else it is computed here.  mid: gradient-bucket callback of the
-        explicit pass (fused_learner.dueling_grads); the autograd path never calls it"""
+        explicit pass (fused_learner.dueling_grads); the autograd path never calls it.
+        prenorm: the caller runs apply_grads next on these gradients (no all-reduce in
+        between): the explicit pass may write clip_grad_norm_'s partials and advance Adam's
+        step count itself (fused_learner.NORM_IN_BACKWARD)"""
         s0, a, r, s1, done = self._tensors(batch)
         isw = None if weights is None else (weights if torch.is_tensor(weights) else torch.as_tensor(np.asarray(weights)))
         if self.fused_grads and self._heads and fused_learner.eligible(self.q_network, s0, s1):
             loss, td_abs = fused_learner.dueling_grads(self, s0, a, r, s1, done, isw, q1t, td_acc=self.td_mean_acc,
-                                                        mid=mid, probe=probe)
+                                                        mid=mid, probe=probe, prenorm=prenorm)
             if self.td_mean_acc is not None:
                 td_abs._rth_mean_tracked = True
             self.last_loss = loss.detach()
@@ -311,7 +314,7 @@ class DQNSolver(Algorithm):
 
     def update_device(self, batch, weights=None, q1t=None):
         """DQNSolver.update (:104-124) returning |td| as a device tensor (no host sync)."""
-        td_abs = self.compute_grads(batch, weights, q1t)
+        td_abs = self.compute_grads(batch, weights, q1t, prenorm=self.grad_hook is None)
         if self.grad_hook is not None:
             self.grad_hook(self._params)
         self.apply_grads()

@@ -333,3 +333,42 @@ def test_forward_heads_counted_matches_full(dev):
                     assert torch.equal(q[:N + k], full[:N + k])
                 assert torch.equal(cache[crow[:N + k]], q[:N + k])
                 assert bool((cache[:30] == 0).all()) and bool((cache[30 + N + k:] == 0).all())
+
+
+def test_norm_in_backward_matches_clip_adam(dev, monkeypatch):
+    """r06: clip_grad_norm_'s partials written by conv1's weight-gradient reduce launch
+    (rth_conv1_relu_wgrad_norm) + rth_adam_prenormed against rth_clip_adam's two launches: the
+    same gradients, the same step count, the norm and every updated tensor equal up to the
+    norm's summation order (a fixed one: run to run bit-identical)"""
+    from reth_amd import fused_learner
+
+    B = 64
+    g = torch.Generator(device=dev).manual_seed(11)
+    frames = torch.randint(0, 256, (2 * B, 4, 84, 84), dtype=torch.uint8, device=dev, generator=g)
+    batch = [frames[:B], torch.randint(0, 6, (B,), device=dev, generator=g),
+             (torch.rand(B, device=dev, generator=g) < 0.3).float(), frames[B:],
+             (torch.rand(B, device=dev, generator=g) < 0.1).float()]
+    isw = torch.rand(B, device=dev, generator=g, dtype=torch.float64) + 0.5
+    res = {}
+    for on in (True, False, True):
+        monkeypatch.setattr(fused_learner, "NORM_IN_BACKWARD", on)
+        solver = _solver(dev, 3)
+        solver.clip_value = solver.optimizer.max_norm = 1.0  # the clip active (the gradient norm is ~10-100)
+        tds, norms = [], []
+        for _ in range(3):
+            tds.append(solver.update_device(batch, weights=isw).clone())
+            norms.append(float(solver.optimizer.total_norm))
+        assert solver.optimizer._prenormed is None
+        state = [p.detach().clone() for p in solver.q_network.parameters()]
+        state += [solver.optimizer.state[p][k].clone() for p in solver.q_network.parameters()
+                  for k in ("exp_avg", "exp_avg_sq")]
+        res.setdefault(on, []).append((tds, norms, state, int(solver.optimizer._step)))
+    (a,), (b, c) = res[False], res[True]
+    assert b[3] == a[3] == 3
+    for x, y in zip(b[2], c[2]):  # deterministic
+        assert torch.equal(x, y)
+    for k in range(3):
+        assert abs(b[1][k] - a[1][k]) <= 1e-6 * a[1][k], (k, b[1][k], a[1][k])
+        assert a[1][k] > 1.0  # clipped
+    for x, y in zip(b[2], a[2]):
+        torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-7)

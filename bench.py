@@ -670,6 +670,8 @@ def main():
     ap.add_argument("--nchw", action="store_true", help="contiguous NCHW Q-net tensors (default channels-last)")
     ap.add_argument("--no-conv-benchmark", action="store_true", help="MIOpen immediate mode instead of find")
     ap.add_argument("--eager", action="store_true", help="no HIP-graph replay (launch every kernel from Python)")
+    ap.add_argument("--wgrad", choices=["miopen", "f32", "x9"], default=None,
+                    help="conv2 / conv3 weight gradients (default: fused_learner.HIP_WGRAD)")
     ap.add_argument("--miopen-conv", action="store_true", help="conv torso forward in MIOpen (+ rth_bias_relu) "
                     "instead of rth_conv_bias_relu")
     args = ap.parse_args()
@@ -714,6 +716,9 @@ def main():
         if args.batch % world:
             raise SystemExit(f"--faithful: global batch {args.batch} does not split over {world} GPUs")
         per_gpu_batch = args.batch // world
+    if args.wgrad is not None:
+        from reth_amd import fused_learner
+        fused_learner.HIP_WGRAD = None if args.wgrad == "miopen" else args.wgrad
     hip_conv = not args.miopen_conv
     probe = hip_conv and not args.nchw and not args.eager and not args.no_probe
     cfg = ApexConfig(n_actors=args.actors, capacity=args.capacity, batch_size=per_gpu_batch, num_actions=wl["actions"],

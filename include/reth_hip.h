@@ -599,6 +599,17 @@ int rth_conv_wgrad_f32_supported(const rth_conv_shape *shape);
 int64_t rth_conv_wgrad_f32_workspace(const rth_conv_shape *shape);
 int rth_conv_wgrad_f32(const rth_conv_shape *shape, const float *x_dev, int64_t n, const float *gy_dev, float *gw_dev,
                        void *workspace_dev, void *stream);
+/* rth_conv_wgrad_f32's partial launch alone (r06): *job_out describes the fixed-order reduce that
+ * finishes gw_dev -- handed to conv1's weight-gradient reduce launch (rth_conv_relu_wgrad_ex and
+ * its frame-id / norm forms, `wdeferred`), which runs it in its own workgroups; the result is
+ * bit-identical to rth_conv_wgrad_f32's. */
+typedef struct rth_wgrad_deferred {
+  const float *partial; /* the workspace holding the split partials */
+  float *gw;            /* OHWI output */
+  int32_t splits, elems, nb, K;
+} rth_wgrad_deferred;
+int rth_conv_wgrad_f32_partials(const rth_conv_shape *shape, const float *x_dev, int64_t n, const float *gy_dev,
+                                float *gw_dev, void *workspace_dev, rth_wgrad_deferred *job_out, void *stream);
 /* Backward of relu(conv2d(x, w) + b) for the weights and bias, on uint8 stacks (conv1, whose
  * input needs no gradient): gy = (y > 0) ? g : 0, gw = sum over output pixels of gy times the
  * input window (OHWI [cout, kh, kw, cin], the layout of a channels_last weight), gb = sum of
@@ -611,7 +622,8 @@ int rth_conv_relu_wgrad(const rth_conv_shape *shape, const void *x_dev, const in
                         void *stream);
 /* rth_conv_relu_wgrad that also finishes up to 4 deferred bias gradients in its reduce launch
  * (one launch fewer per layer): each a rth_relu_bias_grad called with db = NULL on
- * `workspace`, over `rows` rows of C channels, earlier on the same stream. */
+ * `workspace`, over `rows` rows of C channels, earlier on the same stream; and up to 2 deferred
+ * weight gradients (rth_conv_wgrad_f32_partials jobs, earlier on the same stream). */
 typedef struct rth_bias_deferred {
   const void *workspace; /* the rth_relu_bias_grad workspace holding the slabs */
   float *db;             /* [C] output */
@@ -622,7 +634,8 @@ typedef struct rth_bias_deferred {
 } rth_bias_deferred;
 int rth_conv_relu_wgrad_ex(const rth_conv_shape *shape, const void *x_dev, const int64_t *rows_dev, int64_t n,
                            const float *g_dev, const float *y_dev, float *gw_dev, float *gb_dev, void *workspace_dev,
-                           const rth_bias_deferred *deferred, int32_t ndeferred, void *stream);
+                           const rth_bias_deferred *deferred, int32_t ndeferred,
+                           const rth_wgrad_deferred *wdeferred, int32_t nwdeferred, void *stream);
 /* Frames in place (r05): conv1 (4x84x84 uint8 -> 32, k8 s4) forward and weight gradient
  * reading each sample's 4 frames straight from a replay's frame store (the
  * rth_replay_frames_attach store, 84*84-byte frames) by the int32 [n][4] frame ids a
@@ -634,7 +647,7 @@ int rth_conv1_frames_bias_relu(const rth_conv_shape *shape, const uint8_t *store
 int rth_conv1_frames_relu_wgrad_ex(const rth_conv_shape *shape, const uint8_t *store_dev, const int32_t *ids_dev,
                                    int64_t n, const float *g_dev, const float *y_dev, float *gw_dev, float *gb_dev,
                                    void *workspace_dev, const rth_bias_deferred *deferred, int32_t ndeferred,
-                                   void *stream);
+                                   const rth_wgrad_deferred *wdeferred, int32_t nwdeferred, void *stream);
 
 /* ------------------------------------------------------------------------------------
  * Atari observation preprocessing (reth/reth/env/util.py:121-209, 281-297): per actor, the
@@ -697,8 +710,8 @@ int rth_clip_adam(const rth_param_tensor *tensors, int32_t n_tensors, double lr,
  * (rows_dev != NULL: stacks by row; fids_dev != NULL: rth_conv1_frames_relu_wgrad_ex's frame
  * ids, x_dev the frame store; neither: x_dev the stacks) whose reduce launch also writes the
  * fp64 sum-of-squares partials clip_grad_norm_ reduces: extra workgroups over the gradients of
- * `sq` (every parameter but conv1's weight and bias and the deferred bias gradients, which the
- * launch finishes itself and adds right behind them; only .grad and .n are read), the first of
+ * `sq` (every parameter but conv1's weight and bias and the deferred bias and weight gradients,
+ * which the launch finishes itself and adds right behind them; only .grad and .n are read), the first of
  * them advancing step_dev and writing the step's bias corrections as rth_clip_adam's first
  * launch does, all into adam_workspace_dev (rth_clip_adam_workspace's layout);
  * *nparts_out = the partial count.  rth_adam_prenormed(..., nparts, ...) is then
@@ -706,7 +719,8 @@ int rth_clip_adam(const rth_param_tensor *tensors, int32_t n_tensors, double lr,
 int rth_conv1_relu_wgrad_norm(const rth_conv_shape *shape, const void *x_dev, const int64_t *rows_dev,
                               const int32_t *fids_dev, int64_t n, const float *g_dev, const float *y_dev,
                               float *gw_dev, float *gb_dev, void *workspace_dev, const rth_bias_deferred *deferred,
-                              int32_t ndeferred, const rth_param_tensor *sq, int32_t n_sq, double lr, double beta1,
+                              int32_t ndeferred, const rth_wgrad_deferred *wdeferred, int32_t nwdeferred,
+                              const rth_param_tensor *sq, int32_t n_sq, double lr, double beta1,
                               double beta2, int64_t *step_dev, void *adam_workspace_dev, int32_t *nparts_out,
                               void *stream);
 int rth_adam_prenormed(const rth_param_tensor *tensors, int32_t n_tensors, double lr, double beta1, double beta2,

@@ -53,6 +53,13 @@ class ConvShape(ctypes.Structure):
                 ("kw", c_i32), ("stride", c_i32)]
 
 
+class WgradDeferred(ctypes.Structure):
+    """rth_wgrad_deferred (include/reth_hip.h): a conv2 / conv3 weight gradient whose split
+    partials rth_conv_wgrad_f32_partials wrote, finished by conv1's reduce launch"""
+    _fields_ = [("partial", ctypes.c_void_p), ("gw", ctypes.c_void_p), ("splits", ctypes.c_int32),
+                ("elems", ctypes.c_int32), ("nb", ctypes.c_int32), ("K", ctypes.c_int32)]
+
+
 class BiasDeferred(ctypes.Structure):
     """rth_bias_deferred (include/reth_hip.h): a bias gradient whose slabs rth_relu_bias_grad
     wrote with db = NULL, finished by rth_conv_relu_wgrad_ex"""
@@ -159,6 +166,8 @@ SIGNATURES = {
     "rth_conv_wgrad_f32_supported": (c_i32, [ctypes.POINTER(ConvShape)]),
     "rth_conv_wgrad_f32_workspace": (c_i64, [ctypes.POINTER(ConvShape)]),
     "rth_conv_wgrad_f32": (c_i32, [ctypes.POINTER(ConvShape), c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "rth_conv_wgrad_f32_partials": (c_i32, [ctypes.POINTER(ConvShape), c_vp, c_i64, c_vp, c_vp, c_vp,
+                                            ctypes.POINTER(WgradDeferred), c_vp]),
     "rth_relu_bias_grad": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_vp]),
     "rth_relu_bias_grad_nchw": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_vp]),
     "rth_conv_supported": (c_i32, [ctypes.POINTER(ConvShape)]),
@@ -169,9 +178,9 @@ SIGNATURES = {
     "rth_conv_relu_wgrad": (c_i32, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
                                     c_vp]),
     "rth_conv_relu_wgrad_ex": (c_i32, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
-                                       c_vp, c_i32, c_vp]),
+                                       c_vp, c_i32, c_vp, c_i32, c_vp]),
     "rth_conv1_frames_relu_wgrad_ex": (c_i32, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp,
-                                               c_vp, c_vp, c_i32, c_vp]),
+                                               c_vp, c_vp, c_i32, c_vp, c_i32, c_vp]),
     "rth_conv_pack_many": (c_i32, [c_i32, ctypes.POINTER(ConvShape), ctypes.POINTER(c_vp), ctypes.POINTER(c_vp),
                                    c_vp]),
     "rth_conv_bias_relu": (c_i32, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
@@ -204,7 +213,7 @@ SIGNATURES = {
     "rth_clip_adam": (c_i32, [c_vp, c_i32, c_f64, c_f64, c_f64, c_f64, c_f64, c_vp, c_vp, c_vp, c_vp]),
     "rth_adam_prenormed": (c_i32, [c_vp, c_i32, c_f64, c_f64, c_f64, c_f64, c_f64, c_i32, c_vp, c_vp, c_vp, c_vp]),
     "rth_conv1_relu_wgrad_norm": (c_i32, [ctypes.POINTER(ConvShape), c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp,
-                                          c_vp, c_vp, c_i32, c_vp, c_i32, c_f64, c_f64, c_f64, c_vp, c_vp,
+                                          c_vp, c_vp, c_i32, c_vp, c_i32, c_vp, c_i32, c_f64, c_f64, c_f64, c_vp, c_vp,
                                           ctypes.POINTER(c_i32), c_vp]),
     # learner -> actor weights slot (perwez PUB/SUB CONFLATE)
     "rth_weights_create": (c_i32, [c_i64, c_i32, ctypes.POINTER(c_vp)]),

@@ -34,6 +34,7 @@
 
 #include "common.hpp"
 #include "optim.hpp"
+#include "wgrad.hpp"
 
 namespace rth {
 
@@ -1826,15 +1827,35 @@ __device__ void bias_job(const BiasJobs &bj, int j, double *sq = nullptr) {
   }
 }
 
+// deferred conv2 / conv3 weight gradients (rth_conv_wgrad_f32_partials): their reduce
+// workgroups follow the bias jobs' (r06)
+constexpr int kWgradJobsMax = 2;
+struct WgradJobs {
+  WgfJob j[kWgradJobsMax];
+  int n;
+};
+
 // workgroup blk of conv1's weight-gradient reduce: 64 of its E outputs, or (blk >= RB) a
-// deferred bias gradient.  sq (nullable): the fp64 sum of squares of what the workgroup
-// finished goes to sq[blk] (r06: clip_grad_norm_'s partials from the backward)
+// deferred bias gradient, or (past those) a reduce workgroup of a deferred weight gradient.
+// sq (nullable): the fp64 sum of squares of what the workgroup finished goes to sq[blk] (r06:
+// clip_grad_norm_'s partials from the backward)
 template <int KH, int KW, int CIN, int COUT>
 __device__ __forceinline__ void wgrad_reduce_wg(int blk, const float *__restrict__ partial, int blocks,
                                                 float *__restrict__ gw, float *__restrict__ gb, const BiasJobs &bj,
-                                                double *__restrict__ sq) {
+                                                const WgradJobs &wj, double *__restrict__ sq) {
   constexpr int K = CIN * KH * KW, E = COUT * K + COUT, RB = (E + 63) / 64;
   __shared__ float part[4][64];
+  if (blk >= RB + bj.n) {  // a deferred weight gradient
+    int b = blk - RB - bj.n, j = 0;
+    while (j + 1 < wj.n && b >= wgf_reduce_blocks(wj.j[j])) b -= wgf_reduce_blocks(wj.j[j++]);
+    const float v = wgf_reduce_wg(wj.j[j], b);
+    if (sq) {
+      __shared__ double red4[4];
+      const double t = block_sum(rmul((double)v, (double)v), red4);
+      if (threadIdx.x == 0) sq[blk] = t;
+    }
+    return;
+  }
   if (blk >= RB) {  // a deferred bias gradient
     bias_job(bj, blk - RB, sq ? sq + blk : nullptr);
     return;
@@ -1889,25 +1910,26 @@ __device__ __forceinline__ void wgrad_reduce_wg(int blk, const float *__restrict
 
 template <int KH, int KW, int CIN, int COUT>
 __global__ __launch_bounds__(256) void k_wgrad_reduce(const float *__restrict__ partial, int blocks,
-                                                      float *__restrict__ gw, float *__restrict__ gb, BiasJobs bj) {
-  wgrad_reduce_wg<KH, KW, CIN, COUT>(blockIdx.x, partial, blocks, gw, gb, bj, nullptr);
+                                                      float *__restrict__ gw, float *__restrict__ gb, BiasJobs bj,
+                                                      WgradJobs wj) {
+  wgrad_reduce_wg<KH, KW, CIN, COUT>(blockIdx.x, partial, blocks, gw, gb, bj, wj, nullptr);
 }
 
 // the same reduce launch with clip_grad_norm_'s partials (r06, one rank): workgroups [0, nsq)
 // are norm-partial workgroups over the gradients final before it (optim.hpp's grad_sqsum_wg,
 // workgroup 0 advancing Adam's step count), the rest the reduce's, each writing the sum of
-// squares of the gradients it finishes -- conv1's weight and bias, the deferred bias gradients
-// -- right behind them: rth_adam_prenormed then runs the update alone
+// squares of the gradients it finishes -- conv1's weight and bias, the deferred bias and weight
+// gradients -- right behind them: rth_adam_prenormed then runs the update alone
 template <int KH, int KW, int CIN, int COUT>
 __global__ __launch_bounds__(256) void k_wgrad_reduce_norm(const float *__restrict__ partial, int blocks,
                                                            float *__restrict__ gw, float *__restrict__ gb, BiasJobs bj,
-                                                           OptArgs na, int nsq, double *__restrict__ npart,
+                                                           WgradJobs wj, OptArgs na, int nsq, double *__restrict__ npart,
                                                            SqStep st) {
   if ((int)blockIdx.x < nsq) {
     grad_sqsum_wg(na, blockIdx.x, npart, st);
     return;
   }
-  wgrad_reduce_wg<KH, KW, CIN, COUT>((int)blockIdx.x - nsq, partial, blocks, gw, gb, bj, npart + nsq);
+  wgrad_reduce_wg<KH, KW, CIN, COUT>((int)blockIdx.x - nsq, partial, blocks, gw, gb, bj, wj, npart + nsq);
 }
 
 constexpr int wg_per_cu() { return 2; }
@@ -2151,27 +2173,31 @@ struct NormJob {
 };
 static int conv1_relu_wgrad(const rth_conv_shape *shape, const void *x, const int64_t *rows, const int32_t *fids,
                             int64_t n, const float *g, const float *y, float *gw, float *gb, void *workspace,
-                            const rth_bias_deferred *deferred, int32_t ndeferred, void *stream,
-                            const NormJob *norm = nullptr);
+                            const rth_bias_deferred *deferred, int32_t ndeferred, const rth_wgrad_deferred *wdeferred,
+                            int32_t nwdeferred, void *stream, const NormJob *norm = nullptr);
 
 int rth_conv_relu_wgrad_ex(const rth_conv_shape *shape, const void *x, const int64_t *rows, int64_t n, const float *g,
                            const float *y, float *gw, float *gb, void *workspace, const rth_bias_deferred *deferred,
-                           int32_t ndeferred, void *stream) {
-  return conv1_relu_wgrad(shape, x, rows, nullptr, n, g, y, gw, gb, workspace, deferred, ndeferred, stream);
+                           int32_t ndeferred, const rth_wgrad_deferred *wdeferred, int32_t nwdeferred, void *stream) {
+  return conv1_relu_wgrad(shape, x, rows, nullptr, n, g, y, gw, gb, workspace, deferred, ndeferred, wdeferred,
+                          nwdeferred, stream);
 }
 
 int rth_conv1_frames_relu_wgrad_ex(const rth_conv_shape *shape, const uint8_t *store, const int32_t *ids, int64_t n,
                                    const float *g, const float *y, float *gw, float *gb, void *workspace,
-                                   const rth_bias_deferred *deferred, int32_t ndeferred, void *stream) {
+                                   const rth_bias_deferred *deferred, int32_t ndeferred,
+                                   const rth_wgrad_deferred *wdeferred, int32_t nwdeferred, void *stream) {
   RTH_REQUIRE(store && ids && (reinterpret_cast<uintptr_t>(ids) & 15) == 0,
               "rth_conv1_frames_relu_wgrad_ex: NULL / misaligned frame store or ids");
-  return conv1_relu_wgrad(shape, store, nullptr, ids, n, g, y, gw, gb, workspace, deferred, ndeferred, stream);
+  return conv1_relu_wgrad(shape, store, nullptr, ids, n, g, y, gw, gb, workspace, deferred, ndeferred, wdeferred,
+                          nwdeferred, stream);
 }
 
 int rth_conv1_relu_wgrad_norm(const rth_conv_shape *shape, const void *x, const int64_t *rows, const int32_t *fids,
                               int64_t n, const float *g, const float *y, float *gw, float *gb, void *workspace,
-                              const rth_bias_deferred *deferred, int32_t ndeferred, const rth_param_tensor *sq,
-                              int32_t n_sq, double lr, double beta1, double beta2, int64_t *step_dev,
+                              const rth_bias_deferred *deferred, int32_t ndeferred, const rth_wgrad_deferred *wdeferred,
+                              int32_t nwdeferred, const rth_param_tensor *sq, int32_t n_sq, double lr, double beta1,
+                              double beta2, int64_t *step_dev,
                               void *adam_workspace_dev, int32_t *nparts_out, void *stream) {
   RTH_REQUIRE(!(rows && fids) && sq && n_sq >= 1 && n_sq <= RTH_MAX_PARAM_TENSORS && step_dev && adam_workspace_dev &&
                   nparts_out && n > 0,
@@ -2182,13 +2208,28 @@ int rth_conv1_relu_wgrad_norm(const rth_conv_shape *shape, const void *x, const 
   if (fids)
     RTH_REQUIRE((reinterpret_cast<uintptr_t>(fids) & 15) == 0, "rth_conv1_relu_wgrad_norm: misaligned frame ids");
   const NormJob nj{sq, n_sq, lr, beta1, beta2, step_dev, adam_workspace_dev, nparts_out};
-  return conv1_relu_wgrad(shape, x, rows, fids, n, g, y, gw, gb, workspace, deferred, ndeferred, stream, &nj);
+  return conv1_relu_wgrad(shape, x, rows, fids, n, g, y, gw, gb, workspace, deferred, ndeferred, wdeferred, nwdeferred,
+                          stream, &nj);
 }
 
 static int conv1_relu_wgrad(const rth_conv_shape *shape, const void *x, const int64_t *rows, const int32_t *fids,
                             int64_t n, const float *g, const float *y, float *gw, float *gb, void *workspace,
-                            const rth_bias_deferred *deferred, int32_t ndeferred, void *stream, const NormJob *norm) {
+                            const rth_bias_deferred *deferred, int32_t ndeferred, const rth_wgrad_deferred *wdeferred,
+                            int32_t nwdeferred, void *stream, const NormJob *norm) {
   RTH_REQUIRE(shape && x && g && y && gw && gb && workspace && n >= 0, "rth_conv_relu_wgrad: NULL argument");
+  RTH_REQUIRE(nwdeferred >= 0 && nwdeferred <= kWgradJobsMax && (nwdeferred == 0 || wdeferred),
+              "rth_conv_relu_wgrad_ex: %d deferred weight gradients (at most %d)", nwdeferred, kWgradJobsMax);
+  WgradJobs wj{};
+  wj.n = nwdeferred;
+  int wblocks = 0;
+  for (int j = 0; j < nwdeferred; ++j) {
+    const rth_wgrad_deferred &d = wdeferred[j];
+    RTH_REQUIRE(d.gw && (d.splits == 0 || d.partial) && d.splits >= 0 && d.splits <= kWgfRedMax && d.elems > 0 &&
+                    d.nb >= 0 && d.K > 0,
+                "rth_conv_relu_wgrad_ex: deferred weight gradient %d malformed", j);
+    wj.j[j] = WgfJob{d.partial, d.gw, d.splits, d.elems, d.nb, d.K};
+    wblocks += wgf_reduce_blocks(wj.j[j]);
+  }
   RTH_REQUIRE(ndeferred >= 0 && ndeferred <= kBiasJobsMax && (ndeferred == 0 || deferred),
               "rth_conv_relu_wgrad_ex: %d deferred bias gradients (at most %d)", ndeferred, kBiasJobsMax);
   BiasJobs bj{};
@@ -2210,6 +2251,8 @@ static int conv1_relu_wgrad(const rth_conv_shape *shape, const void *x, const in
     RTH_HIP(hipMemsetAsync(gb, 0, 32 * 4, as_stream(stream)));
     for (int j = 0; j < ndeferred; ++j)  // an empty batch: every layer's slabs are empty too
       RTH_HIP(hipMemsetAsync(deferred[j].db, 0, deferred[j].C * 4, as_stream(stream)));
+    for (int j = 0; j < nwdeferred; ++j)
+      RTH_HIP(hipMemsetAsync(wdeferred[j].gw, 0, (size_t)wdeferred[j].elems * 4, as_stream(stream)));
     return RTH_OK;
   }
   hipLaunchKernelGGL(fids ? k_conv1_wgrad_bf16x3<2> : (rows ? k_conv1_wgrad_bf16x3<1> : k_conv1_wgrad_bf16x3<0>),
@@ -2218,21 +2261,21 @@ static int conv1_relu_wgrad(const rth_conv_shape *shape, const void *x, const in
   RTH_LAUNCHED();
   constexpr int RB = (32 * 256 + 32 + 63) / 64;
   if (!norm) {
-    hipLaunchKernelGGL((k_wgrad_reduce<8, 8, 4, 32>), dim3(RB + ndeferred), dim3(256), 0, as_stream(stream), part,
-                       kWgBlocks, gw, gb, bj);
+    hipLaunchKernelGGL((k_wgrad_reduce<8, 8, 4, 32>), dim3(RB + ndeferred + wblocks), dim3(256), 0, as_stream(stream),
+                       part, kWgBlocks, gw, gb, bj, wj);
     RTH_LAUNCHED();
     return RTH_OK;
   }
   OptArgs na{};
   const int64_t nsq = opt_segments(norm->sq, norm->n_sq, kOptChunk, &na);
-  const int64_t nparts = nsq + RB + ndeferred;
+  const int64_t nparts = nsq + RB + ndeferred + wblocks;
   RTH_REQUIRE(nparts <= kMaxPartials, "rth_conv1_relu_wgrad_norm: %lld norm partials (at most %d)",
               (long long)nparts, kMaxPartials);
   auto *npart = static_cast<double *>(norm->adam_ws);  // rth_clip_adam_workspace's layout (optim.hip)
   auto *bc = reinterpret_cast<BiasCorr *>(static_cast<uint8_t *>(norm->adam_ws) + (int64_t)kMaxPartials * 8 + 16);
   const SqStep st{norm->step, bc, norm->lr, norm->beta1, norm->beta2};
-  hipLaunchKernelGGL((k_wgrad_reduce_norm<8, 8, 4, 32>), dim3((unsigned)(nsq + RB + ndeferred)), dim3(256), 0,
-                     as_stream(stream), part, kWgBlocks, gw, gb, bj, na, (int)nsq, npart, st);
+  hipLaunchKernelGGL((k_wgrad_reduce_norm<8, 8, 4, 32>), dim3((unsigned)nparts), dim3(256), 0, as_stream(stream), part,
+                     kWgBlocks, gw, gb, bj, wj, na, (int)nsq, npart, st);
   RTH_LAUNCHED();
   *norm->nparts_out = (int32_t)nparts;
   return RTH_OK;
@@ -2240,7 +2283,7 @@ static int conv1_relu_wgrad(const rth_conv_shape *shape, const void *x, const in
 
 int rth_conv_relu_wgrad(const rth_conv_shape *shape, const void *x, const int64_t *rows, int64_t n, const float *g,
                         const float *y, float *gw, float *gb, void *workspace, void *stream) {
-  return rth_conv_relu_wgrad_ex(shape, x, rows, n, g, y, gw, gb, workspace, nullptr, 0, stream);
+  return rth_conv_relu_wgrad_ex(shape, x, rows, n, g, y, gw, gb, workspace, nullptr, 0, nullptr, 0, stream);
 }
 
 // the kernel a hybrid geometry runs for n samples (*l becomes it; its packed weights start at

@@ -7,63 +7,111 @@
 //                        gy[p][co] * x[b][S*oy + kh][S*ox + kw][ci]
 //
 // x (the layer's input) and gy (the masked upstream gradient) are channels-last fp32; gw is
-// the OHWI (channels_last) weight gradient.  GEMM view: rows = co (COUT), columns = kk =
-// (kh, kw, ci) in OHWI order (K = KH*KW*CIN), reduction over the pixels.
+// the OHWI (channels_last) weight gradient.  GEMM view: rows = co (64), columns = kk =
+// (kh, kw, ci) in OHWI order (K = KH*KW*CIN), reduction over the output pixels.
 //
-// v_mfma_f32_32x32x2f32: lane (i = lane & 31, h = lane >> 5) supplies A[i][h] = gy[p + h][co]
-// and B[h][i] = x-window[p + h][kk] -- both 32 consecutive channels of one NHWC pixel, one
-// 128-byte segment per half-wave -- so a wave consumes a pair of pixels per MFMA.  A wave
-// holds all COUT = 64 rows (2 blocks) x NB column blocks of 32 (NB*32 consecutive kk, one
-// (kh, kw) run of the window when CIN is a multiple of 32) as 2*NB accumulators, and walks
-// its pixel range with kPf pairs of loads in flight.  The kWaves waves of a workgroup take
-// consecutive pixel sub-ranges of the same column group; their partials are summed in LDS
-// in wave order, and the workgroup's partial goes to the workspace; k_wgrad_f32_reduce adds
-// the partials of a column group in workgroup order.  Every sum has a fixed order.
+// r06 form (register-only main loop, no LDS operand staging: it runs beside the actor stream's
+// LDS-hungry x9 convolutions).  A workgroup owns one kernel row kh -- its NCOL = KW*CIN
+// columns are contiguous in x (one run of KW pixels) -- and a range of pixel pairs (its split);
+// each of its 4 waves a quarter of that range.  v_mfma_f32_32x32x2f32 with the lanes
+// (i = lane & 31, h = lane >> 5) of a wave on the pixels 2q + h of pair q:
+//   A[i][h] = gy[p][2i + c]             (row block c in {0, 1}: one float2 load per lane)
+//   B[h][i] = x-row[p][NB*i + nb]       (column block nb < NB = NCOL/32: NB consecutive floats)
+// so a lane's loads are wide and the wave's 2 x NB accumulators (64 x NCOL outputs) take a pair
+// of pixels per 2 * NB MFMAs; PF pairs of loads are in flight ahead of their MFMAs.  The loads
+// go through buffer resources over the batch: a pixel past it reads zeros (contributes 0).
+// The 4 waves' accumulators are added in LDS in the fixed order (w0 + w1) + (w2 + w3), one
+// 32x32 block at a time (16 KB of LDS), and wave 0 stores the workgroup's partial in the
+// accumulator order; k_conv_wgrad_f32_reduce adds the splits' partials in split order and
+// scatters them to OHWI.  Every sum has a fixed order: run to run bit-identical.
 #include <type_traits>
 
 #include "common.hpp"
+#include "wgrad.hpp"
 
 namespace rth {
 
 using f32x16 = __attribute__((ext_vector_type(16))) float;
 using f32x4 = __attribute__((ext_vector_type(4))) float;
+using f32x3 = __attribute__((ext_vector_type(3))) float;
+using f32x2 = __attribute__((ext_vector_type(2))) float;
 
-constexpr int kWgfWaves = 4;  // waves per workgroup (one per SIMD)
-#ifndef WGF_PF
-#define WGF_PF 4
-#endif
-constexpr int kWgfPf = WGF_PF;  // pixel pairs whose loads are in flight ahead of their MFMAs
-
-template <int KH, int KW, int S, int CIN, int COUT, int HIN, int WIN>
+// column groups: GN = 32 * NB consecutive kk per wave (inside one kernel row), NB in {2, 3, 4, 6}
+template <int KH, int KW, int S, int CIN, int HIN, int WIN, int NB>
 struct WgfGeom {
   static constexpr int HOUT = (HIN - KH) / S + 1, WOUT = (WIN - KW) / S + 1, PIX = HOUT * WOUT;
-  static constexpr int K = KH * KW * CIN;
-  static_assert(COUT == 64 && CIN % 32 == 0, "64 output channels, input channels in runs of 32");
+  static constexpr int COUT = 64, K = KH * KW * CIN, NCOL = KW * CIN, GN = 32 * NB;
+  static constexpr int GROUPS = K / GN;     // column groups
+  static constexpr int BLK = 2 * NB;        // 32x32 accumulator blocks per wave
+  static constexpr int TILE = BLK * 1024;   // floats of one workgroup's partial (= 64 * GN)
+  static_assert(NCOL % GN == 0, "a column group inside one kernel row");
 };
 
-// kk-block kb (32 consecutive kk) -> offset of its first element inside the input window
-template <int KW, int CIN, int WIN>
-__device__ __forceinline__ int kb_off(int kb) {
-  const int kk = kb * 32, khkw = kk / CIN, ci = kk % CIN;
-  return ((khkw / KW) * WIN + khkw % KW) * CIN + ci;
+template <int NB>
+struct XVec;
+template <>
+struct XVec<2> {
+  f32x2 v;
+  __device__ __forceinline__ float operator[](int k) const { return v[k]; }
+};
+template <>
+struct XVec<3> {
+  f32x3 v;
+  __device__ __forceinline__ float operator[](int k) const { return v[k]; }
+};
+template <>
+struct XVec<4> {
+  f32x4 v;
+  __device__ __forceinline__ float operator[](int k) const { return v[k]; }
+};
+template <>
+struct XVec<6> {
+  f32x2 v[3];
+  __device__ __forceinline__ float operator[](int k) const { return v[k >> 1][k & 1]; }
+};
+
+template <int NB>
+__device__ __forceinline__ void load_xvec(XVec<NB> &o, __amdgpu_buffer_rsrc_t r, uint32_t off) {
+  if constexpr (NB == 2) {
+    o.v = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+  } else if constexpr (NB == 3) {
+    o.v = __builtin_bit_cast(f32x3, __builtin_amdgcn_raw_buffer_load_b96(r, off, 0, 0));
+  } else if constexpr (NB == 4) {
+    o.v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+  } else {
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+      o.v[k] = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(r, off + 8 * k, 0, 0));
+  }
 }
 
-template <int KH, int KW, int S, int CIN, int COUT, int HIN, int WIN, int NB>
-__global__ __launch_bounds__(kWgfWaves * 64) void k_conv_wgrad_f32(const float *__restrict__ x,
-                                                                 const float *__restrict__ gy, int64_t n,
-                                                                 int splits, float *__restrict__ part) {
-  using Gm = WgfGeom<KH, KW, S, CIN, COUT, HIN, WIN>;
-  __shared__ float red[2 * NB * 16 * 64];  // one wave's accumulators (lane-major per register)
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 31, h = lane >> 5;
-  const int group = blockIdx.x / splits, split = blockIdx.x % splits;
-  const int64_t P = n * Gm::PIX;
-  // this wave's pixel range: split-major, then wave; pair-aligned
-  const int64_t units = (int64_t)splits * kWgfWaves, u = (int64_t)split * kWgfWaves + wave;
-  const int64_t pairs = (P + 1) / 2;
-  const int64_t q0 = pairs * u / units, q1 = pairs * (u + 1) / units;
-  int koff[NB];
-#pragma unroll
-  for (int nb = 0; nb < NB; ++nb) koff[nb] = kb_off<KW, CIN, WIN>(group * NB + nb) + i;
+// WAVES waves per workgroup take consecutive quarters / eighths of the workgroup's pair range
+// and are summed in the fixed tree ((w0 + w1) + (w2 + w3)) + ((w4 + w5) + (w6 + w7)), one 32x32
+// block at a time, each tree level in its own LDS slots (WAVES - 1 slots of 4 KB: one barrier
+// per level, and a block's slots are free again before the next block writes them)
+template <int KH, int KW, int S, int CIN, int HIN, int WIN, int NB, int WAVES, int PF>
+__global__ __launch_bounds__(WAVES * 64) void k_conv_wgrad_f32(const float *__restrict__ x,
+                                                              const float *__restrict__ gy, int n, int splits,
+                                                              float *__restrict__ part) {
+  using G = WgfGeom<KH, KW, S, CIN, HIN, WIN, NB>;
+  constexpr int PIX = G::PIX, WOUT = G::WOUT, HOUT_ = G::HOUT, LEVELS = WAVES == 8 ? 3 : WAVES == 4 ? 2 : 1;
+  static_assert(WAVES == 2 || WAVES == 4 || WAVES == 8, "2, 4 or 8 waves");
+  __shared__ float red[WAVES - 1][1024];
+  const int lane = threadIdx.x & 63, i = lane & 31, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // workgroup -> (split, column group): the GROUPS workgroups of a split sit on one XCD
+  // (blockIdx % 8 equal) and share its gy pairs through that XCD's L2
+  const int b8 = blockIdx.x & 7, rest = blockIdx.x >> 3;
+  const int grp = rest % G::GROUPS, split = (rest / G::GROUPS) * 8 + b8;
+  const int kk0 = grp * G::GN, kh = kk0 / G::NCOL, col0 = kk0 - kh * G::NCOL;
+  const int P = n * PIX, pairs = (P + 1) >> 1;
+  const int units = splits * WAVES, u = split * WAVES + wave;
+  const int q0 = (int)((int64_t)pairs * u / units), q1 = (int)((int64_t)pairs * (u + 1) / units);
+
+  const __amdgpu_buffer_rsrc_t g_rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(gy), 0, P * G::COUT * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t x_rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(x), 0, n * HIN * WIN * CIN * 4, 0x00020000);
 
   f32x16 acc[2][NB];
 #pragma unroll
@@ -73,121 +121,139 @@ __global__ __launch_bounds__(kWgfWaves * 64) void k_conv_wgrad_f32(const float *
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[c][nb][r] = 0.0f;
 
-  // operands of the pairs in launch order from a cursor at pixel 2q + h: (b, oy, ox) advance by
-  // two pixels per pair with adds only; a pixel past the range reads the range's last pixel
-  // with weight 0
-  const int64_t plast = (2 * q1 - 1 < P ? 2 * q1 - 1 : P - 1);  // the range's last live pixel
-  const int64_t lb = plast / Gm::PIX;
-  const int lpix = (int)(plast - lb * Gm::PIX), loy = lpix / Gm::WOUT, lox = lpix - loy * Gm::WOUT;
-  int64_t cp = 2 * q0 + h;
-  int64_t cb = cp / Gm::PIX;
-  int cpix = (int)(cp - cb * Gm::PIX), coy = cpix / Gm::WOUT, cox = cpix - coy * Gm::WOUT;
-  // branch-free: a dead pixel reads the range's last pixel and is weighted 0 (0 * x = 0 for
-  // finite x), so pairs past q1 may be multiplied in as well
-  auto load = [&](float (&a)[2], float (&b)[NB], bool &lv) {
-    const bool live = cp <= plast;
-    lv = live;
-    const int64_t p = live ? cp : plast, bb = live ? cb : lb;
-    const int oy = live ? coy : loy, ox = live ? cox : lox;
-    const float *g = gy + p * COUT + i;
-    a[0] = g[0];  // weighted 0 at the MFMA when dead (no wait on the load here)
-    a[1] = g[32];
-    const float *xw = x + ((bb * HIN + S * oy) * WIN + S * ox) * CIN;
-#pragma unroll
-    for (int nb = 0; nb < NB; ++nb) b[nb] = xw[koff[nb]];
-    // advance the cursor by one pair (two pixels)
-    cp += 2;
+  f32x2 av[PF];
+  XVec<NB> bv[PF];
+  // a cursor over this lane's pixels 2q + h: (oy, ox) and both byte offsets advance by one pair
+  // per issue with adds and selects only; past the batch both offsets run past the resources'
+  // ranges and read 0
+  constexpr uint32_t XSTEP = 2 * S * CIN * 4;                         // ox += 2
+  constexpr uint32_t XROW = (S * WIN - WOUT * S) * CIN * 4;           // ox wrapped: next output row
+  constexpr uint32_t XIMG = (HIN * WIN - HOUT_ * S * WIN) * CIN * 4;  // oy wrapped: next sample
+  int cox, coy;
+  uint32_t goff, xoff;
+  {
+    const int p = 2 * q0 + h, b = p / PIX, rem = p - b * PIX;
+    coy = rem / WOUT;
+    cox = rem - coy * WOUT;
+    goff = (uint32_t)p * (G::COUT * 4) + (uint32_t)i * 8;
+    xoff = (uint32_t)((((b * HIN + S * coy + kh) * WIN + S * cox) * CIN + col0 + NB * i) * 4);
+  }
+#ifdef WGF_DIAG_NOLOAD
+  int nissued = 0;  // diagnostic build: only the prologue loads (the MFMA loop's own rate)
+#endif
+  auto issue = [&](int d) {
+#ifdef WGF_DIAG_NOLOAD
+    if (nissued++ < PF)
+#endif
+    {
+      av[d] = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(g_rsrc, goff, 0, 0));
+      load_xvec<NB>(bv[d], x_rsrc, xoff);
+    }
+    goff += 2 * G::COUT * 4;
     cox += 2;
-    const bool wrap = cox >= Gm::WOUT;
-    cox = wrap ? cox - Gm::WOUT : cox;
-    coy += wrap ? 1 : 0;
-    const bool wrap2 = coy == Gm::HOUT;
-    coy = wrap2 ? 0 : coy;
-    cb += wrap2 ? 1 : 0;
+    const bool w1 = cox >= WOUT;
+    cox = w1 ? cox - WOUT : cox;
+    coy = w1 ? coy + 1 : coy;
+    const bool w2 = coy == HOUT_;
+    coy = w2 ? 0 : coy;
+    xoff += XSTEP + (w1 ? XROW : 0u) + (w2 ? XIMG : 0u);
   };
-  float av[kWgfPf][2], bv[kWgfPf][NB];
-  bool lv[kWgfPf];
+  auto mfmas = [&](int d) {
 #pragma unroll
-  for (int d = 0; d < kWgfPf; ++d) load(av[d], bv[d], lv[d]);
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb)
+        acc[c][nb] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[d][c], bv[d][nb], acc[c][nb], 0, 0, 0);
+  };
+
+  // the prologue's loads in the loop's order (slot by slot), so the waits the compiler derives
+  // at the loop header count the same loads on both edges (else it waits for nearly all)
+#pragma unroll
+  for (int d = 0; d < PF; ++d) {
+    issue(d);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  int q = q0;
 #pragma unroll 1
-  for (int64_t q = q0; q < q1; q += kWgfPf) {
+  for (; q + PF <= q1; q += PF) {
 #pragma unroll
-    for (int d = 0; d < kWgfPf; ++d) {
+    for (int d = 0; d < PF; ++d) {
+      mfmas(d);
+      // the refill of slot d right behind its MFMAs (the scheduler would sink it to its use
+      // PF pairs later)
+      __builtin_amdgcn_sched_barrier(0);
+      issue(d);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
 #pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const float a = lv[d] ? av[d][c] : 0.0f;
+  for (int d = 0; d < PF - 1; ++d)
+    if (q + d < q1) mfmas(d);  // the last < PF pairs (wave-uniform)
+
+  // the waves' tree sum; wave 0 stores the partial [split][group][block][register][lane]
+  float *out = part + ((int64_t)split * G::GROUPS + grp) * G::TILE;
+#ifdef WGF_DIAG_NOEPI
+  if (wave == 0)
 #pragma unroll
-        for (int nb = 0; nb < NB; ++nb)
-          acc[c][nb] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bv[d][nb], acc[c][nb], 0, 0, 0);
+    for (int blk = 0; blk < G::BLK; ++blk)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) out[(blk * 16 + r) * 64 + lane] = acc[blk / NB][blk % NB][r];
+  return;
+#endif
+#pragma unroll
+  for (int blk = 0; blk < G::BLK; ++blk) {
+    f32x16 &v = acc[blk / NB][blk % NB];
+    int base = 0;
+#pragma unroll
+    for (int lv = 0; lv < LEVELS; ++lv) {
+      const int span = 1 << lv;  // waves w with w % span == 0 hold the level's inputs
+      if (wave % (2 * span) == span) {
+        float *s = red[base + (wave >> (lv + 1))];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[r * 64 + lane] = v[r];
       }
-      // keep the refill of slot d here: the scheduler would otherwise sink these loads down
-      // to their use kWgfPf pairs later and expose their latency
-      __builtin_amdgcn_sched_barrier(0);
-      load(av[d], bv[d], lv[d]);  // the pair kWgfPf ahead (past q1: zero-weighted)
-      __builtin_amdgcn_sched_barrier(0);
+      __syncthreads();
+      if (wave % (2 * span) == 0) {
+        const float *s = red[base + (wave >> (lv + 1))];
+        if (lv == LEVELS - 1) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) out[(blk * 16 + r) * 64 + lane] = radd(v[r], s[r * 64 + lane]);
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) v[r] = radd(v[r], s[r * 64 + lane]);
+        }
+      }
+      base += WAVES >> (lv + 1);
     }
-  }
-  // the workgroup's waves in order: wave 0 stores, waves 1..3 add, the last one writes out
-  for (int w = 0; w < kWgfWaves; ++w) {
-    if (wave == w) {
-#pragma unroll
-      for (int c = 0; c < 2; ++c)
-#pragma unroll
-        for (int nb = 0; nb < NB; ++nb)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            float &slot = red[((c * NB + nb) * 16 + r) * 64 + lane];
-            slot = w == 0 ? acc[c][nb][r] : radd(slot, acc[c][nb][r]);
-          }
-    }
-    __syncthreads();
-  }
-  // partial [split][COUT][K]: D[row][col] of block (c, nb) -> co = 32c + row, kk = (group*NB + nb)*32 + col;
-  // row = (r / 4) * 8 + h' * 4 + r % 4 for the lane (col = l & 31, h' = l >> 5) that held it
-  float *out = part + (int64_t)split * COUT * Gm::K;
-  for (int e = threadIdx.x; e < 2 * NB * 16 * 64; e += kWgfWaves * 64) {
-    const int l = e & 63, r = (e >> 6) & 15, blk = e >> 10, c = blk / NB, nb = blk % NB;
-    const int row = (r >> 2) * 8 + (l >> 5) * 4 + (r & 3), col = l & 31;
-    out[(int64_t)(32 * c + row) * Gm::K + (group * NB + nb) * 32 + col] = red[e];
   }
 }
 
-// gw[e] = sum of the splits' partials (e over COUT * K) in a fixed order: a workgroup takes 64
-// consecutive elements; thread (g, e) sums the splits g, g + 4, g + 8, ... of element e with
-// all of its loads in flight together, then the 4 group sums are added in group order
-constexpr int kWgfRedMax = 128;  // splits per element at most: 32 per thread
-__global__ __launch_bounds__(256) void k_conv_wgrad_f32_reduce(const float *__restrict__ part, int splits,
-                                                              int64_t elems, float *__restrict__ gw) {
-  __shared__ float red[4][64];
-  const int el = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  const int64_t e = (int64_t)blockIdx.x * 64 + el;
-  float v[kWgfRedMax / 4];
-#pragma unroll
-  for (int u = 0; u < kWgfRedMax / 4; ++u) {
-    const int k = grp + 4 * u;
-    v[u] = (k < splits && e < elems) ? part[(int64_t)k * elems + e] : 0.0f;
-  }
-  float s = 0.0f;
-#pragma unroll
-  for (int u = 0; u < kWgfRedMax / 4; ++u)
-    if (grp + 4 * u < splits) s = radd(s, v[u]);
-  red[grp][el] = s;
-  __syncthreads();
-  if (grp == 0 && e < elems) gw[e] = radd(radd(radd(red[0][el], red[1][el]), red[2][el]), red[3][el]);
+// gw = the sum of the splits' partials in split order (wgrad.hpp), scattered to OHWI
+__global__ __launch_bounds__(kWgfRedElems) void k_conv_wgrad_f32_reduce(WgfJob j) {
+  wgf_reduce_wg(j, blockIdx.x);
 }
 
 struct WgfLaunch {
   const void *fn;
-  int groups;  // column groups (K / (NB * 32))
-  int64_t elems;  // COUT * K
+  int groups;  // column groups (K / (32 * NB))
+  int nb;      // column blocks per group
+  int K;       // KH * KW * CIN
+  int elems;   // 64 * K
+  int splits;  // pixel splits (a multiple of 8)
+  int threads; // 64 * waves
 };
 
-template <int KH, int KW, int S, int CIN, int COUT, int HIN, int WIN, int NB>
-static WgfLaunch wgf_launch() {
-  using Gm = WgfGeom<KH, KW, S, CIN, COUT, HIN, WIN>;
-  static_assert(Gm::K % (NB * 32) == 0, "column groups tile K");
-  return WgfLaunch{reinterpret_cast<const void *>(&k_conv_wgrad_f32<KH, KW, S, CIN, COUT, HIN, WIN, NB>),
-                   Gm::K / (NB * 32), (int64_t)COUT * Gm::K};
+template <int KH, int KW, int S, int CIN, int HIN, int WIN, int NB, int WAVES, int PF>
+static WgfLaunch wgf_launch(int splits) {
+  using Gm = WgfGeom<KH, KW, S, CIN, HIN, WIN, NB>;
+  return WgfLaunch{reinterpret_cast<const void *>(&k_conv_wgrad_f32<KH, KW, S, CIN, HIN, WIN, NB, WAVES, PF>),
+                   Gm::GROUPS, NB, Gm::K, Gm::COUT * Gm::K, splits, WAVES * 64};
+}
+
+// pixel splits per column group, a multiple of 8 (RTH_WGF_SPLITS2/3 while tuning)
+static int wgf_env(const char *name, int dflt) {
+  const char *v = getenv(name);
+  return v ? atoi(v) : dflt;
 }
 
 static bool find_wgf(const rth_conv_shape &s, WgfLaunch *out) {
@@ -195,23 +261,35 @@ static bool find_wgf(const rth_conv_shape &s, WgfLaunch *out) {
     return s.input == RTH_CONV_F32_NHWC && s.cin == cin && s.hin == hin && s.win == win && s.cout == cout &&
            s.kh == kh && s.kw == kw && s.stride == st;
   };
-  if (is(32, 20, 20, 64, 4, 4, 2)) {  // conv2: K = 512 -> 4 groups of 128 columns
-    static const WgfLaunch l = wgf_launch<4, 4, 2, 32, 64, 20, 20, 4>();
+  auto fix = [](WgfLaunch l, int sp) {
+    if (sp >= 8 && sp <= kWgfRedMax && sp % 8 == 0) l.splits = sp;
+    return l;
+  };
+  if (is(32, 20, 20, 64, 4, 4, 2)) {  // conv2: 4 kernel rows of 128 columns
+    static const WgfLaunch l = [&] {
+      const int v = wgf_env("RTH_WGF_V2", 0), sp = wgf_env("RTH_WGF_SPLITS2", 0);
+      return fix(v == 1   ? wgf_launch<4, 4, 2, 32, 20, 20, 4, 8, 6>(32)
+                 : v == 2 ? wgf_launch<4, 4, 2, 32, 20, 20, 2, 8, 8>(32)
+                 : v == 3 ? wgf_launch<4, 4, 2, 32, 20, 20, 2, 4, 8>(32)
+                 : v == 4 ? wgf_launch<4, 4, 2, 32, 20, 20, 2, 8, 12>(32)
+                          : wgf_launch<4, 4, 2, 32, 20, 20, 4, 4, 8>(64),
+                 sp);
+    }();
     *out = l;
-  } else if (is(64, 9, 9, 64, 3, 3, 1)) {  // conv3: K = 576 -> 6 groups of 96 columns
-    static const WgfLaunch l = wgf_launch<3, 3, 1, 64, 64, 9, 9, 3>();
+  } else if (is(64, 9, 9, 64, 3, 3, 1)) {  // conv3: 3 kernel rows of 192 columns
+    static const WgfLaunch l = [&] {
+      const int v = wgf_env("RTH_WGF_V3", 0), sp = wgf_env("RTH_WGF_SPLITS3", 0);
+      return fix(v == 1   ? wgf_launch<3, 3, 1, 64, 9, 9, 3, 8, 8>(40)
+                 : v == 2 ? wgf_launch<3, 3, 1, 64, 9, 9, 6, 4, 6>(64)
+                 : v == 3 ? wgf_launch<3, 3, 1, 64, 9, 9, 3, 8, 12>(40)
+                          : wgf_launch<3, 3, 1, 64, 9, 9, 3, 4, 8>(40),
+                 sp);
+    }();
     *out = l;
   } else {
     return false;
   }
   return true;
-}
-
-constexpr int kWgfWorkgroups = 256;  // about one per CU: column groups x pixel splits
-
-static int wgf_splits(const WgfLaunch &l) {
-  const int s = kWgfWorkgroups / l.groups;
-  return s < kWgfRedMax ? s : kWgfRedMax;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -464,8 +542,9 @@ int rth_conv_wgrad_x9(const rth_conv_shape *shape, const float *x, int64_t n, co
   float *part = static_cast<float *>(workspace);
   void *args[] = {(void *)&x, (void *)&gy, (void *)&n, (void *)&splits, (void *)&part};
   RTH_HIP(hipLaunchKernel(l.fn, dim3((unsigned)(l.groups * splits)), dim3(256), args, 0, as_stream(stream)));
-  hipLaunchKernelGGL(k_conv_wgrad_f32_reduce, dim3((unsigned)((l.elems + 63) / 64)), dim3(256), 0, as_stream(stream),
-                     part, splits, l.elems, gw);
+  const WgfJob job{part, gw, splits, (int)l.elems, 0, 0};
+  hipLaunchKernelGGL(k_conv_wgrad_f32_reduce, dim3((unsigned)wgf_reduce_blocks(job)), dim3(kWgfRedElems), 0,
+                     as_stream(stream), job);
   RTH_LAUNCHED();
   return RTH_OK;
 }
@@ -478,26 +557,51 @@ int rth_conv_wgrad_f32_supported(const rth_conv_shape *shape) {
 int64_t rth_conv_wgrad_f32_workspace(const rth_conv_shape *shape) {
   WgfLaunch l;
   if (!shape || !find_wgf(*shape, &l)) return 0;
-  return (int64_t)wgf_splits(l) * l.elems * 4;
+  return (int64_t)l.splits * l.elems * 4;
 }
 
-int rth_conv_wgrad_f32(const rth_conv_shape *shape, const float *x, int64_t n, const float *gy, float *gw,
-                       void *workspace, void *stream) {
+// the partial launch alone; *job = the reduce it needs (rth_conv_wgrad_f32 reduces at once,
+// conv1's reduce launch takes it as a deferred job)
+static int wgf_partials(const rth_conv_shape *shape, const float *x, int64_t n, const float *gy, float *gw,
+                        void *workspace, WgfJob *job, void *stream) {
   RTH_REQUIRE(shape && x && gy && gw && workspace && n >= 0, "rth_conv_wgrad_f32: NULL argument");
   WgfLaunch l;
   RTH_REQUIRE(find_wgf(*shape, &l), "rth_conv_wgrad_f32: geometry (%d x %d x %d -> %d, k %dx%d, stride %d) not built",
               shape->cin, shape->hin, shape->win, shape->cout, shape->kh, shape->kw, shape->stride);
-  if (n == 0) {
-    RTH_HIP(hipMemsetAsync(gw, 0, l.elems * 4, as_stream(stream)));
-    return RTH_OK;
-  }
-  int splits = wgf_splits(l);
+  // byte offsets of both buffer resources are 32-bit
+  RTH_REQUIRE(n * shape->cin * shape->hin * shape->win * 4 < ((int64_t)1 << 31) &&
+                  n * ((shape->hin - shape->kh) / shape->stride + 1) * ((shape->win - shape->kw) / shape->stride + 1) *
+                          shape->cout * 4 < ((int64_t)1 << 31),
+              "rth_conv_wgrad_f32: batch too large");
+  RTH_REQUIRE(((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(gy)) & 15) == 0,
+              "rth_conv_wgrad_f32: misaligned buffer");
+  int ni = (int)n, splits = l.splits;
   float *part = static_cast<float *>(workspace);
-  void *args[] = {(void *)&x, (void *)&gy, (void *)&n, (void *)&splits, (void *)&part};
-  RTH_HIP(hipLaunchKernel(l.fn, dim3((unsigned)(l.groups * splits)), dim3(kWgfWaves * 64), args, 0,
-                          as_stream(stream)));
-  hipLaunchKernelGGL(k_conv_wgrad_f32_reduce, dim3((unsigned)((l.elems + 63) / 64)), dim3(256), 0, as_stream(stream),
-                     part, splits, l.elems, gw);
+  *job = WgfJob{part, gw, n == 0 ? 0 : splits, l.elems, l.nb, l.K};  // no split: the reduce writes zeros
+  if (n == 0) return RTH_OK;
+  void *args[] = {(void *)&x, (void *)&gy, (void *)&ni, (void *)&splits, (void *)&part};
+  RTH_HIP(hipLaunchKernel(l.fn, dim3((unsigned)(l.groups * splits)), dim3(l.threads), args, 0, as_stream(stream)));
+  return RTH_OK;
+}
+
+int rth_conv_wgrad_f32(const rth_conv_shape *shape, const float *x, int64_t n, const float *gy, float *gw,
+                       void *workspace, void *stream) {
+  WgfJob job;
+  const int rc = wgf_partials(shape, x, n, gy, gw, workspace, &job, stream);
+  if (rc != RTH_OK) return rc;
+  hipLaunchKernelGGL(k_conv_wgrad_f32_reduce, dim3((unsigned)wgf_reduce_blocks(job)), dim3(kWgfRedElems), 0,
+                     as_stream(stream), job);
+  RTH_LAUNCHED();
+  return RTH_OK;
+}
+
+int rth_conv_wgrad_f32_partials(const rth_conv_shape *shape, const float *x, int64_t n, const float *gy, float *gw,
+                                void *workspace, rth_wgrad_deferred *job_out, void *stream) {
+  RTH_REQUIRE(job_out, "rth_conv_wgrad_f32_partials: NULL job");
+  WgfJob job;
+  const int rc = wgf_partials(shape, x, n, gy, gw, workspace, &job, stream);
+  if (rc != RTH_OK) return rc;
+  *job_out = rth_wgrad_deferred{job.part, job.gw, job.splits, job.elems, job.nb, job.K};
   RTH_LAUNCHED();
   return RTH_OK;
 }

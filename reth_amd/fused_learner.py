@@ -228,6 +228,7 @@ def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None, mid=No
         g = gfeat.view(ys[-1][:B].shape)  # NCHW, like the last conv's output
         grads = {}
         deferred = []  # bias gradients whose slabs wait for conv1's reduce launch
+        wdeferred = []  # conv2 / conv3 weight gradients whose partials wait for it (HIP_WGRAD "f32")
         if getattr(net, "_ws", None) is None or net._ws[0].device != x.device:
             net._ws = [torch.zeros(_lib.lib().rth_relu_bias_grad_workspace(m.out_channels), dtype=torch.uint8,
                                    device=x.device) for m in convs]
@@ -241,29 +242,32 @@ def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None, mid=No
                 db = torch.empty(conv.out_channels, dtype=torch.float32, device=x.device)
                 assert len(deferred) <= 4, "rth_conv_relu_wgrad_ex finishes at most 4 deferred bias gradients"
                 jobs = (_lib.BiasDeferred * max(len(deferred), 1))(*deferred)
+                wjobs = (_lib.WgradDeferred * max(len(wdeferred), 1))(*wdeferred)
                 ws1 = _net_workspace(net, "conv1", shapes[0], x.device)
                 opt = solver.optimizer
                 if prenorm and NORM_IN_BACKWARD and mid is None and solver.grad_hook is None and hasattr(opt, "prenorm"):
                     # every gradient but conv1's weight and bias and the deferred biases (this
                     # launch finishes those) is final here: the heads' and conv2 / conv3's weights
-                    done = {d.db for d in deferred}
+                    done = {d.db for d in deferred} | {d.gw for d in wdeferred}
                     sq = [gr for gr in [gw1[:Hh], gw1[Hh:], gb1[:Hh], gb1[Hh:], *g2]]
-                    sq += [grads[c.weight] for c in convs[1:]] + [grads[c.bias] for c in convs[1:]
-                                                                  if grads[c.bias].data_ptr() not in done]
+                    sq += [gr for c in convs[1:] for gr in (grads[c.weight], grads[c.bias])
+                           if gr.data_ptr() not in done]
                     arr, n_sq = opt.norm_tensors(sq)
                     nparts = ctypes.c_int32(0)
                     call("rth_conv1_relu_wgrad_norm", ctypes.byref(shapes[0]), ptr(x.store) if frames else ptr(x), None,
                          ptr(x.ids) if frames else None, B, ptr(_nhwc(g)), ptr(y), ptr(gw), ptr(db), ptr(ws1), jobs,
-                         len(deferred), arr, n_sq, *opt.prenorm_scalars(), ctypes.byref(nparts), st)
+                         len(deferred), wjobs, len(wdeferred), arr, n_sq, *opt.prenorm_scalars(),
+                         ctypes.byref(nparts), st)
                     opt.prenorm(nparts.value)
                 elif frames:
                     call("rth_conv1_frames_relu_wgrad_ex", ctypes.byref(shapes[0]), ptr(x.store), ptr(x.ids), B,
-                         ptr(_nhwc(g)), ptr(y), ptr(gw), ptr(db), ptr(ws1), jobs, len(deferred), st)
+                         ptr(_nhwc(g)), ptr(y), ptr(gw), ptr(db), ptr(ws1), jobs, len(deferred), wjobs,
+                         len(wdeferred), st)
                 else:
                     call("rth_conv_relu_wgrad_ex", ctypes.byref(shapes[0]), ptr(x), None, B, ptr(_nhwc(g)), ptr(y),
-                         ptr(gw), ptr(db), ptr(ws1), jobs, len(deferred), st)
+                         ptr(gw), ptr(db), ptr(ws1), jobs, len(deferred), wjobs, len(wdeferred), st)
                 grads[conv.weight], grads[conv.bias] = gw, db
-                deferred = []  # consumed
+                deferred, wdeferred = [], []  # consumed
                 break
             nb, c, hh, ww = y.shape
             defer = u8  # finished by conv1's rth_conv_relu_wgrad_ex
@@ -296,8 +300,15 @@ def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None, mid=No
             if hip_wgrad:  # weight gradient in rth_conv_wgrad_{f32,x9} (deterministic, no zero fill)
                 gw = torch.empty(conv.weight.shape, dtype=torch.float32, device=x.device,
                                  memory_format=torch.channels_last)
-                call(f"rth_conv_wgrad_{HIP_WGRAD}", ctypes.byref(shapes[li]), ptr(xin), B, ptr(gy), ptr(gw),
-                     ptr(_net_workspace(net, HIP_WGRAD, shapes[li], x.device)), st)
+                ws = _net_workspace(net, HIP_WGRAD, shapes[li], x.device)
+                if HIP_WGRAD == "f32" and defer:  # partials now, the reduce in conv1's reduce launch
+                    job = _lib.WgradDeferred()
+                    call("rth_conv_wgrad_f32_partials", ctypes.byref(shapes[li]), ptr(xin), B, ptr(gy), ptr(gw), ptr(ws),
+                         ctypes.byref(job), st)
+                    wdeferred.append(job)
+                else:
+                    call(f"rth_conv_wgrad_{HIP_WGRAD}", ctypes.byref(shapes[li]), ptr(xin), B, ptr(gy), ptr(gw), ptr(ws),
+                         st)
             if hip_dgrad:  # data gradient in rth_conv_dgrad (no zero fill)
                 gx = torch.empty(xin.shape, dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
                 if li in dgp and li > 0 and defer and DGRAD_MASK and \
@@ -320,7 +331,7 @@ def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None, mid=No
             g = gx
         # every deferred bias gradient was finished by conv1's launch (else its db would be
         # uninitialised memory handed to the optimizer)
-        assert not deferred, "deferred bias gradients left unfinished"
+        assert not deferred and not wdeferred, "deferred bias / weight gradients left unfinished"
         if mid is not None:
             mid([t for c in convs for t in (grads[c.weight], grads[c.bias])])
         # the eight branch parameters' gradients: FC1's are row slices of the merged ones (the

@@ -34,7 +34,17 @@ for (cin, h, cout, k, s) in [(32, 20, 64, 4, 2), (64, 9, 64, 3, 1)]:
         torch.ops.aten.convolution_backward(gy, x, w, None, [s, s], [0, 0], [1, 1], False, [0, 0], 1,
                                             [False, True, False])
 
-    for name, fn in (("rth_conv_wgrad_f32", ours), ("rth_conv_wgrad_x9", ours_x9), ("miopen", miopen)):
+    ours()
+    torch.cuda.synchronize()
+    got = gw.clone()
+    want = torch.ops.aten.convolution_backward(gy.double(), x.double(), w.double(), None, [s, s], [0, 0], [1, 1],
+                                               False, [0, 0], 1, [False, True, False])[1]
+    print(f"conv {cin}x{h}: rth_conv_wgrad_f32 max |err| / max |gw| = "
+          f"{((got.double() - want).abs().max() / want.abs().max()).item():.2e}", flush=True)
+    fns = [("rth_conv_wgrad_f32", ours)]
+    if not os.environ.get("WGF_ONLY"):
+        fns += [("rth_conv_wgrad_x9", ours_x9), ("miopen", miopen)]
+    for name, fn in fns:
         for _ in range(5):
             fn()
         torch.cuda.synchronize()

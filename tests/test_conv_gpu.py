@@ -448,7 +448,7 @@ def test_conv_dgrad_relu_prepacked(dev, n):
         jobs = (_lib.BiasDeferred * 1)(_lib.BiasDeferred(ws.data_ptr(), db.data_ptr(), rows, cin, slabs.value))
         gw, gb = torch.empty((32, 8, 8, 4), device=dev), torch.empty(32, device=dev)
         _lib.call("rth_conv_relu_wgrad_ex", _lib.ctypes.byref(c1), st.data_ptr(), None, 3, gc.data_ptr(),
-                  yc.data_ptr(), gw.data_ptr(), gb.data_ptr(), wsc.data_ptr(), jobs, 1, _lib.stream_ptr())
+                  yc.data_ptr(), gw.data_ptr(), gb.data_ptr(), wsc.data_ptr(), jobs, 1, None, 0, _lib.stream_ptr())
         torch.cuda.synchronize()
         assert torch.equal(got, want)
         dbs.append(db.clone())
@@ -510,11 +510,68 @@ def test_deferred_bias_grads_finished_by_conv1_reduce(dev):
         arr = (_lib.BiasDeferred * len(jobs))(*jobs)
         _lib.call("rth_conv_relu_wgrad_ex", _lib.ctypes.byref(shape), st.data_ptr(), None, n, gc.data_ptr(),
                   yc.data_ptr(), gw.data_ptr(), gb.data_ptr(), wsc.data_ptr(), arr if deferred else None,
-                  len(jobs) if deferred else 0, _lib.stream_ptr())
+                  len(jobs) if deferred else 0, None, 0, _lib.stream_ptr())
         res.append((gw.clone(), gb.clone()))
     assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
     for got, ref in zip(outs, want):
         assert torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("n", [0, 1, 37, 512])
+def test_deferred_wgrads_finished_by_conv1_reduce(dev, n):
+    """r06: rth_conv_wgrad_f32_partials leaves conv2's and conv3's split partials;
+    conv1's reduce launch (rth_conv_relu_wgrad_ex's wdeferred jobs) finishes them beside a
+    deferred bias gradient: weight gradients bit-identical to rth_conv_wgrad_f32's (the same
+    per-element split order), conv1's own gradients and the bias unchanged"""
+    from reth_amd import _lib
+
+    g = torch.Generator(device=dev).manual_seed(17 + n)
+    want, jobs, outs, keep = [], [], [], []
+    for gi in (1, 2):
+        cin, h, wd, cout, k, s = GEOMS[gi]
+        ho = (h - k) // s + 1
+        x = torch.randn((n, cin, h, wd), device=dev, generator=g).contiguous(memory_format=torch.channels_last)
+        gy = torch.randn((n, cout, ho, ho), device=dev, generator=g).contiguous(memory_format=torch.channels_last)
+        shape = _shape(_lib.CONV_F32_NHWC, *GEOMS[gi])
+        ws = torch.empty(_lib.lib().rth_conv_wgrad_f32_workspace(_lib.ctypes.byref(shape)) // 4, device=dev)
+        gw = torch.full((cout, cin, k, k), float("nan"), device=dev).contiguous(memory_format=torch.channels_last)
+        _lib.call("rth_conv_wgrad_f32", _lib.ctypes.byref(shape), x.data_ptr(), n, gy.data_ptr(), gw.data_ptr(),
+                  ws.data_ptr(), _lib.stream_ptr())
+        want.append(gw)
+        gw2 = torch.full_like(gw, float("nan"))
+        job = _lib.WgradDeferred()
+        _lib.call("rth_conv_wgrad_f32_partials", _lib.ctypes.byref(shape), x.data_ptr(), n, gy.data_ptr(),
+                  gw2.data_ptr(), ws.data_ptr(), _lib.ctypes.byref(job), _lib.stream_ptr())
+        jobs.append(job)
+        outs.append(gw2)
+        keep += [x, gy, ws]
+    rows, C = 3 * 81, 64
+    gg, yy = torch.randn((rows, C), device=dev, generator=g), torch.randn((rows, C), device=dev, generator=g)
+    wsb = torch.empty(_lib.lib().rth_relu_bias_grad_workspace(C), dtype=torch.uint8, device=dev)
+    gyb, db = torch.empty_like(gg), torch.full((C,), float("nan"), device=dev)
+    _lib.call("rth_relu_bias_grad", gg.data_ptr(), yy.data_ptr(), gyb.data_ptr(), None, wsb.data_ptr(), rows, C,
+              _lib.stream_ptr())
+    shape1 = _shape(_lib.CONV_U8_CHW, *GEOMS[0])
+    m = max(n, 1)
+    st = torch.randint(0, 256, (m, 4, 84, 84), dtype=torch.uint8, device=dev, generator=g)
+    gc = torch.randn((m, 20, 20, 32), device=dev, generator=g)
+    yc = torch.randn((m, 20, 20, 32), device=dev, generator=g)
+    wsc = torch.empty(_lib.lib().rth_conv_wgrad_workspace(_lib.ctypes.byref(shape1)), dtype=torch.uint8, device=dev)
+    res = []
+    for deferred in (False, True):
+        gw1, gb1 = torch.empty((32, 8, 8, 4), device=dev), torch.empty(32, device=dev)
+        barr = (_lib.BiasDeferred * 1)(_lib.BiasDeferred(wsb.data_ptr(), db.data_ptr(), rows, C))
+        warr = (_lib.WgradDeferred * 2)(*jobs)
+        _lib.call("rth_conv_relu_wgrad_ex", _lib.ctypes.byref(shape1), st.data_ptr(), None, m, gc.data_ptr(),
+                  yc.data_ptr(), gw1.data_ptr(), gb1.data_ptr(), wsc.data_ptr(), barr, 1, warr if deferred else None,
+                  2 if deferred else 0, _lib.stream_ptr())
+        res.append((gw1.clone(), gb1.clone(), db.clone()))
+    assert all(torch.equal(a, b) for a, b in zip(res[0], res[1]))
+    for got, ref in zip(outs, want):
+        assert not torch.isnan(got).any()
+        assert torch.equal(got, ref)
+        if n == 0:
+            assert not got.any()
 
 
 @pytest.mark.parametrize("gi,n", [(1, 3), (2, 1), (2, 37), (2, 1024)])
@@ -670,7 +727,7 @@ def test_conv1_frames_in_place_bit_identical(dev, n):
         gb = torch.full((32,), float("nan"), device=dev)
         args = [x.data_ptr(), None] if ix is None else [x.data_ptr(), ix.data_ptr()]
         _lib.call(fn, _lib.ctypes.byref(shape), *args, n, up.data_ptr(), y_st.data_ptr(), gw.data_ptr(), gb.data_ptr(),
-                  ws.data_ptr(), None, 0, _lib.stream_ptr())
+                  ws.data_ptr(), None, 0, None, 0, _lib.stream_ptr())
         out.append((gw, gb))
     assert not torch.isnan(out[1][0]).any()
     assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])

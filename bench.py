@@ -534,10 +534,16 @@ def hbm_rooflines(ax, timer, probe_ms, tprof, tsrc, treason):
     nparams = sum(p.numel() for p in ax.solver._params)
     rows = cfg.n_actors  # one append of N rows per actor step (fused actor: the previous step's rows)
     by = hbm_bytes(cfg, rows)
-    # rth_clip_adam = k_grad_sqsum (reads g) + k_adam (reads p, g, m, v; writes p, m, v): 32 B per
-    # fp32 parameter
-    clip_name = "rth_clip_adam (k_grad_sqsum + k_adam)"
-    by[clip_name] = nparams * 32
+    # one rank: the norm partials come from conv1's weight-gradient reduce launch (fused_learner
+    # NORM_IN_BACKWARD), the step is rth_adam_prenormed = k_adam (reads p, g, m, v; writes p, m, v):
+    # 28 B per fp32 parameter; with a gradient all-reduce: rth_clip_adam = k_grad_sqsum (reads g)
+    # + k_adam, 32 B
+    if getattr(ax.solver, "grad_hook", None) is None:
+        clip_name = "rth_adam_prenormed (k_adam)"
+        by[clip_name] = nparams * 28
+    else:
+        clip_name = "rth_clip_adam (k_grad_sqsum + k_adam)"
+        by[clip_name] = nparams * 32
     live = {"k_tree_update_sub": "tree_update", "k_tree_sample": "sample", "k_copy_rows (gather)": "gather",
             "k_copy_rows (insert)": "insert"}
     probed = {"k_actor_tail": "actor_tail", "k_td_heads_backward": "td_heads_backward", clip_name: "clip_adam"}
@@ -666,7 +672,7 @@ def main():
     ap.add_argument("--cpu-actor-worker", type=float, default=None, help=argparse.SUPPRESS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-iters", type=int, default=72)
-    ap.add_argument("--tag", default="r05", help="profiles/traffic_TAG.json: the PMC pass the traffic fields cite")
+    ap.add_argument("--tag", default="r06", help="profiles/traffic_TAG.json: the PMC pass the traffic fields cite")
     ap.add_argument("--nchw", action="store_true", help="contiguous NCHW Q-net tensors (default channels-last)")
     ap.add_argument("--no-conv-benchmark", action="store_true", help="MIOpen immediate mode instead of find")
     ap.add_argument("--eager", action="store_true", help="no HIP-graph replay (launch every kernel from Python)")

@@ -11,19 +11,20 @@
 // (kh, kw, ci) in OHWI order (K = KH*KW*CIN), reduction over the output pixels.
 //
 // r06 form (register-only main loop, no LDS operand staging: it runs beside the actor stream's
-// LDS-hungry x9 convolutions).  A workgroup owns one kernel row kh -- its NCOL = KW*CIN
-// columns are contiguous in x (one run of KW pixels) -- and a range of pixel pairs (its split);
-// each of its 4 waves a quarter of that range.  v_mfma_f32_32x32x2f32 with the lanes
+// LDS-hungry x9 convolutions).  A workgroup owns one column group -- GN = 32 * NB consecutive
+// kk inside one kernel row kh, contiguous in x -- and a range of pixel pairs (its split); each
+// of its waves a consecutive part of that range.  v_mfma_f32_32x32x2f32 with the lanes
 // (i = lane & 31, h = lane >> 5) of a wave on the pixels 2q + h of pair q:
 //   A[i][h] = gy[p][2i + c]             (row block c in {0, 1}: one float2 load per lane)
-//   B[h][i] = x-row[p][NB*i + nb]       (column block nb < NB = NCOL/32: NB consecutive floats)
-// so a lane's loads are wide and the wave's 2 x NB accumulators (64 x NCOL outputs) take a pair
-// of pixels per 2 * NB MFMAs; PF pairs of loads are in flight ahead of their MFMAs.  The loads
-// go through buffer resources over the batch: a pixel past it reads zeros (contributes 0).
-// The 4 waves' accumulators are added in LDS in the fixed order (w0 + w1) + (w2 + w3), one
-// 32x32 block at a time (16 KB of LDS), and wave 0 stores the workgroup's partial in the
-// accumulator order; k_conv_wgrad_f32_reduce adds the splits' partials in split order and
-// scatters them to OHWI.  Every sum has a fixed order: run to run bit-identical.
+//   B[h][i] = x-row[p][col0 + NB*i + n] (column block n < NB: NB consecutive floats)
+// so a lane's loads are wide and the wave's 2 x NB accumulators (64 x GN outputs) take a pair
+// of pixels per 2 * NB MFMAs; PF pairs of loads are in flight ahead of their MFMAs, addressed by
+// an incremental cursor (adds and selects only).  The loads go through buffer resources over the
+// batch: a pixel past it reads zeros (contributes 0).  The waves' accumulators are added in LDS
+// in a fixed tree, one 32x32 block at a time, and wave 0 stores the workgroup's partial in the
+// accumulator order; the reduce (wgrad.hpp: k_conv_wgrad_f32_reduce here, or conv1's reduce
+// launch for a deferred job) adds the splits' partials in split order and scatters them to
+// OHWI.  Every sum has a fixed order: run to run bit-identical.
 #include <type_traits>
 
 #include "common.hpp"
@@ -138,17 +139,9 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_wgrad_f32(const float *__re
     goff = (uint32_t)p * (G::COUT * 4) + (uint32_t)i * 8;
     xoff = (uint32_t)((((b * HIN + S * coy + kh) * WIN + S * cox) * CIN + col0 + NB * i) * 4);
   }
-#ifdef WGF_DIAG_NOLOAD
-  int nissued = 0;  // diagnostic build: only the prologue loads (the MFMA loop's own rate)
-#endif
   auto issue = [&](int d) {
-#ifdef WGF_DIAG_NOLOAD
-    if (nissued++ < PF)
-#endif
-    {
-      av[d] = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(g_rsrc, goff, 0, 0));
-      load_xvec<NB>(bv[d], x_rsrc, xoff);
-    }
+    av[d] = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(g_rsrc, goff, 0, 0));
+    load_xvec<NB>(bv[d], x_rsrc, xoff);
     goff += 2 * G::COUT * 4;
     cox += 2;
     const bool w1 = cox >= WOUT;
@@ -192,14 +185,6 @@ __global__ __launch_bounds__(WAVES * 64) void k_conv_wgrad_f32(const float *__re
 
   // the waves' tree sum; wave 0 stores the partial [split][group][block][register][lane]
   float *out = part + ((int64_t)split * G::GROUPS + grp) * G::TILE;
-#ifdef WGF_DIAG_NOEPI
-  if (wave == 0)
-#pragma unroll
-    for (int blk = 0; blk < G::BLK; ++blk)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) out[(blk * 16 + r) * 64 + lane] = acc[blk / NB][blk % NB][r];
-  return;
-#endif
 #pragma unroll
   for (int blk = 0; blk < G::BLK; ++blk) {
     f32x16 &v = acc[blk / NB][blk % NB];
@@ -250,41 +235,20 @@ static WgfLaunch wgf_launch(int splits) {
                    Gm::GROUPS, NB, Gm::K, Gm::COUT * Gm::K, splits, WAVES * 64};
 }
 
-// pixel splits per column group, a multiple of 8 (RTH_WGF_SPLITS2/3 while tuning)
-static int wgf_env(const char *name, int dflt) {
-  const char *v = getenv(name);
-  return v ? atoi(v) : dflt;
-}
-
+// the launch per geometry, picked in the loop (r06, interleaved A/Bs of the Pong step,
+// profiles/r06/wgrad_ab.txt): conv2 on 64-column groups, 8 waves (two per SIMD), 48 splits
+// (0.511-0.513 ms/step; 4 waves of 128 columns x 64 splits 0.518-0.520; MIOpen 0.515-0.518);
+// conv3 on 96-column groups, 4 waves, 40 splits (its other forms 0.517-0.521)
 static bool find_wgf(const rth_conv_shape &s, WgfLaunch *out) {
   auto is = [&](int cin, int hin, int win, int cout, int kh, int kw, int st) {
     return s.input == RTH_CONV_F32_NHWC && s.cin == cin && s.hin == hin && s.win == win && s.cout == cout &&
            s.kh == kh && s.kw == kw && s.stride == st;
   };
-  auto fix = [](WgfLaunch l, int sp) {
-    if (sp >= 8 && sp <= kWgfRedMax && sp % 8 == 0) l.splits = sp;
-    return l;
-  };
-  if (is(32, 20, 20, 64, 4, 4, 2)) {  // conv2: 4 kernel rows of 128 columns
-    static const WgfLaunch l = [&] {
-      const int v = wgf_env("RTH_WGF_V2", 0), sp = wgf_env("RTH_WGF_SPLITS2", 0);
-      return fix(v == 1   ? wgf_launch<4, 4, 2, 32, 20, 20, 4, 8, 6>(32)
-                 : v == 2 ? wgf_launch<4, 4, 2, 32, 20, 20, 2, 8, 8>(32)
-                 : v == 3 ? wgf_launch<4, 4, 2, 32, 20, 20, 2, 4, 8>(32)
-                 : v == 4 ? wgf_launch<4, 4, 2, 32, 20, 20, 2, 8, 12>(32)
-                          : wgf_launch<4, 4, 2, 32, 20, 20, 4, 4, 8>(64),
-                 sp);
-    }();
+  if (is(32, 20, 20, 64, 4, 4, 2)) {  // conv2: 8 groups of 64 columns
+    static const WgfLaunch l = wgf_launch<4, 4, 2, 32, 20, 20, 2, 8, 8>(48);
     *out = l;
-  } else if (is(64, 9, 9, 64, 3, 3, 1)) {  // conv3: 3 kernel rows of 192 columns
-    static const WgfLaunch l = [&] {
-      const int v = wgf_env("RTH_WGF_V3", 0), sp = wgf_env("RTH_WGF_SPLITS3", 0);
-      return fix(v == 1   ? wgf_launch<3, 3, 1, 64, 9, 9, 3, 8, 8>(40)
-                 : v == 2 ? wgf_launch<3, 3, 1, 64, 9, 9, 6, 4, 6>(64)
-                 : v == 3 ? wgf_launch<3, 3, 1, 64, 9, 9, 3, 8, 12>(40)
-                          : wgf_launch<3, 3, 1, 64, 9, 9, 3, 4, 8>(40),
-                 sp);
-    }();
+  } else if (is(64, 9, 9, 64, 3, 3, 1)) {  // conv3: 6 groups of 96 columns
+    static const WgfLaunch l = wgf_launch<3, 3, 1, 64, 9, 9, 3, 4, 8>(40);
     *out = l;
   } else {
     return false;
@@ -564,7 +528,7 @@ int64_t rth_conv_wgrad_f32_workspace(const rth_conv_shape *shape) {
 // conv1's reduce launch takes it as a deferred job)
 static int wgf_partials(const rth_conv_shape *shape, const float *x, int64_t n, const float *gy, float *gw,
                         void *workspace, WgfJob *job, void *stream) {
-  RTH_REQUIRE(shape && x && gy && gw && workspace && n >= 0, "rth_conv_wgrad_f32: NULL argument");
+  RTH_REQUIRE(shape && (n == 0 || (x && gy)) && gw && workspace && n >= 0, "rth_conv_wgrad_f32: NULL argument");
   WgfLaunch l;
   RTH_REQUIRE(find_wgf(*shape, &l), "rth_conv_wgrad_f32: geometry (%d x %d x %d -> %d, k %dx%d, stride %d) not built",
               shape->cin, shape->hin, shape->win, shape->cout, shape->kh, shape->kw, shape->stride);

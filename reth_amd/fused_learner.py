@@ -37,11 +37,13 @@ TD_HB_MAX = 16384  # rth_td_heads_backward keeps B * (A + 1) TD gradient rows in
 # no zero fill) instead of MIOpen: conv2's (4 stride-parity classes in one launch) and conv3's
 # (0.570-0.574 vs 0.575-0.580 ms/step with MIOpen's, r04).
 HIP_DGRAD = {1, 2}
-# HIP_WGRAD -- the conv2 / conv3 weight gradients in a hand-written kernel instead of MIOpen's:
-# None = MIOpen (the default: its find picks are faster in the loop), "x9" = rth_conv_wgrad_x9
-# (bf16 MFMA with the exact 3 x 3-term split, run-to-run deterministic: the frame-store and
-# data-parallel parity tests use it), "f32" = rth_conv_wgrad_f32 (fp32 MFMA)
-HIP_WGRAD = None
+# HIP_WGRAD -- the conv2 / conv3 weight gradients: "f32" = rth_conv_wgrad_f32 (the default since
+# r06: fp32 MFMA, register-only, fixed summation order -- run-to-run deterministic, no zero fill;
+# with uint8 input its split partials are reduced by conv1's reduce launch; step equal to
+# MIOpen's, 0.516-0.518 vs 0.515-0.516 ms, whose solvers differ in the last bits run to run and
+# whose find picks differ box to box), "x9" = rth_conv_wgrad_x9 (bf16 MFMA, exact 3 x 3-term
+# split, deterministic), None = MIOpen's solver + zero fill
+HIP_WGRAD = "f32"
 # DGRAD_PREPACK -- the data gradients' flipped kernels packed in the forward's pack launch
 # (rth_conv_pack_many with CONV_PACK_DGRAD jobs) instead of one pack launch per data gradient
 DGRAD_PREPACK = True

@@ -91,6 +91,18 @@ class ClipAdam(torch.optim.Optimizer):
         beta1, beta2 = g["betas"]
         return float(g["lr"]), float(beta1), float(beta2), ptr(self._step), ptr(self._ws)
 
+    def step_launch(self, max_norm=None):
+        """the step() that would run now as a callable that may be issued again (a probe
+        window replays it eagerly after the capture): a pending backward-written norm (prenorm)
+        is bound to it"""
+        nparts, self._prenormed = self._prenormed, None
+
+        def launch():
+            self._prenormed = nparts
+            self.step(max_norm=max_norm)
+
+        return launch
+
     def prenorm(self, nparts):
         """the next step() runs the update alone over `nparts` partials the backward wrote"""
         self._prenormed = int(nparts)

@@ -302,7 +302,7 @@ class DQNSolver(Algorithm):
         if isinstance(self.optimizer, ClipAdam):
             if probe is not None:
                 tail = self.auto_target_update and self._update_target_interval is not None
-                probe([("clip_adam", self.optimizer.step)], last=not tail)
+                probe([("clip_adam", self.optimizer.step_launch())], last=not tail)
             else:
                 self.optimizer.step()  # clips to optimizer.max_norm (= clip_value) itself
         else:

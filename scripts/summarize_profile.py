@@ -208,6 +208,8 @@ def main():
                 hbm[name] = round((2 * st.median(fe[k]) + st.median(wr[k])) * 1024)
         if "k_adam" in hbm and "k_grad_sqsum" in hbm:  # rth_clip_adam = both launches (bench.py roofline_hbm)
             hbm["rth_clip_adam (k_grad_sqsum + k_adam)"] = hbm["k_adam"] + hbm["k_grad_sqsum"]
+        if "k_adam" in hbm:  # one rank: rth_adam_prenormed = k_adam alone (the norm in the backward)
+            hbm["rth_adam_prenormed (k_adam)"] = hbm["k_adam"]
         out["hbm_bytes_per_launch"] = hbm
     if inloop or os.path.exists(pf):
         if not (os.path.exists(pf) and os.path.exists(pw)):

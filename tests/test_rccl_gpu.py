@@ -20,13 +20,13 @@ pytestmark = pytest.mark.gpu
 CHILD = r'''
 import json, os, sys
 sys.path.insert(0, sys.argv[1])
-# a run-to-run deterministic learner (the weight gradients on rth_conv_wgrad_x9: MIOpen's
+# a run-to-run deterministic learner (the default weight gradients, rth_conv_wgrad_f32: MIOpen's
 # solvers differ in the last bits run to run), so the hooked and the plain run can be compared
 import torch
 import torch.distributed as dist
 from reth_amd import fused_learner
 from reth_amd.apex import ApexConfig, ApexDQN
-fused_learner.HIP_WGRAD = "x9"
+assert fused_learner.HIP_WGRAD == "f32"
 
 def say(**kw):
     print("STAGE " + json.dumps(kw), flush=True)

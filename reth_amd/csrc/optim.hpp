@@ -13,7 +13,12 @@ constexpr int kOptThreads = 256;
 // 1,024 22.6-22.7)
 constexpr int kOptChunk = 2048;
 constexpr int kAdamChunk = 2048;
-constexpr int kPartLoads = 4;  // partials each k_adam lane loads up front (all of them up to 1,024)
+#ifndef OPT_PART_LOADS
+#define OPT_PART_LOADS 5
+#endif
+// partials each k_adam lane loads up front (all of them up to 1,280: the one-rank step's ~1,200
+// since the weight gradients' reduce workgroups add theirs, r06)
+constexpr int kPartLoads = OPT_PART_LOADS;
 constexpr int kMaxPartials = 1 << 15;
 
 struct OptSeg {

@@ -678,6 +678,8 @@ def main():
     ap.add_argument("--eager", action="store_true", help="no HIP-graph replay (launch every kernel from Python)")
     ap.add_argument("--wgrad", choices=["miopen", "f32", "x9"], default=None,
                     help="conv2 / conv3 weight gradients (default: fused_learner.HIP_WGRAD)")
+    ap.add_argument("--no-fc1-heads", action="store_true",
+                    help="FC1's reduce and FC2 as two launches (model.FC1_HEADS off; A/B aid)")
     ap.add_argument("--miopen-conv", action="store_true", help="conv torso forward in MIOpen (+ rth_bias_relu) "
                     "instead of rth_conv_bias_relu")
     args = ap.parse_args()
@@ -722,6 +724,9 @@ def main():
         if args.batch % world:
             raise SystemExit(f"--faithful: global batch {args.batch} does not split over {world} GPUs")
         per_gpu_batch = args.batch // world
+    if args.no_fc1_heads:
+        from reth_amd import model
+        model.FC1_HEADS = False
     if args.wgrad is not None:
         from reth_amd import fused_learner
         fused_learner.HIP_WGRAD = None if args.wgrad == "miopen" else args.wgrad

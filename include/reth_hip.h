@@ -571,6 +571,17 @@ int rth_fc_x9(const float *x_dev, int64_t ldx, int64_t M, const float *w_dev, in
 int rth_fc_x9_rows_upto(const float *x_dev, int64_t ldx, int64_t M, int64_t n_max, const int64_t *n_dev,
                         const float *w_dev, int64_t N, int64_t K, const float *bias_dev, float *y_dev,
                         void *workspace_dev, void *stream);
+/* FC1 -> FC2 of the dueling heads in two launches (r06; dqn_model.py:38-47, 59-71 forward
+ * under dqn_solver.py:77-98 _calc_td_error / the target pass): rth_fc_x9's GEMM into its split-K
+ * workspace, then one launch reducing it (+ b1 + ReLU, rth_fc_x9's order) and running the second
+ * layer of both branches from the parameters in place (fc2_params = {adv weight [A, H], value
+ * weight [1, H], adv bias [A], value bias [1]}, rth_heads_fc2's order): heads [M, A + 1] (raw
+ * advantages then value) bit-identical to rth_fc_x9 + rth_heads_fc2; h1_out (nullable) [M, N]
+ * receives relu(FC1).  N = 2H <= 512; workspace = rth_fc_x9_workspace(M, N, K) bytes. */
+int rth_fc1_heads_supported(int64_t M, int64_t N, int64_t K, int32_t A);
+int rth_fc1_heads(const float *x_dev, int64_t ldx, int64_t M, const float *w1_dev, int64_t N, int64_t K,
+                  const float *b1_dev, int32_t A, const float *const *fc2_params, float *heads_dev, float *h1_out_dev,
+                  void *workspace_dev, void *stream);
 /* The same FC1 on the fp32 MFMA with no LDS (r05): the arguments, the workspace protocol and
  * the determinism of rth_fc_x9; any M >= 1 (ragged actor batches), N % 128 == 0, K % 32 == 0
  * (rth_fc_f32_supported).  Not used by the loop (the x9 form is faster there); kept as the

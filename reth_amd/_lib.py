@@ -193,6 +193,9 @@ SIGNATURES = {
     "rth_fc_x9_workspace": (c_i64, [c_i64, c_i64, c_i64]),
     "rth_fc_x9": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i32, c_vp, c_vp, c_vp]),
     "rth_fc_x9_rows_upto": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "rth_fc1_heads_supported": (c_i32, [c_i64, c_i64, c_i64, c_i32]),
+    "rth_fc1_heads": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i32, ctypes.POINTER(c_vp), c_vp, c_vp,
+                              c_vp, c_vp]),
     "rth_fc_f32_supported": (c_i32, [c_i64, c_i64, c_i64]),
     "rth_fc_f32_workspace": (c_i64, [c_i64, c_i64, c_i64]),
     "rth_fc_f32": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i32, c_vp, c_vp, c_vp]),

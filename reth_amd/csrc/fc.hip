@@ -444,6 +444,94 @@ __global__ __launch_bounds__(256) void k_fc_reduce(const float *__restrict__ par
   fc_reduce_wg<MAXS>((int)blockIdx.x, part, splits, MN, N, bias, relu, y, ldy);
 }
 
+// r06: FC1's split-K reduce (+ bias + ReLU, in k_fc_reduce's order) and FC2 of both dueling
+// branches (k_heads_fc2_lean's lanes, terms and order: bit-identical heads) in one launch -- the
+// target pass's and the learner's FC1 -> FC2 without the h1 round trip through a second launch.
+// Workgroup = kRhRows rows: phase 1, every lane reduces float4 groups of the rows' h1 (all of its
+// split loads in flight) into LDS (and h1_out, nullable: the learner's backward reads h1);
+// phase 2, 16 lanes per row run FC2 from LDS.  N = 2H <= kRhMaxN.
+constexpr int kRhRows = 4, kRhMaxN = 512;
+template <int MAXS, int MAXA1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 3))) void k_fc_reduce_heads(const float *__restrict__ part, int splits, int M, int N,
+                                                         const float *__restrict__ b1, int A,
+                                                         const float *__restrict__ wa2, const float *__restrict__ wv2,
+                                                         const float *__restrict__ ba2, const float *__restrict__ bv2,
+                                                         float *__restrict__ heads, float *__restrict__ h1_out) {
+  __shared__ f32x4 hs[kRhRows * kRhMaxN / 4];
+  const int r0 = (int)blockIdx.x * kRhRows, N4 = N / 4;
+  const int64_t MN = (int64_t)M * N;
+  constexpr int PER = kRhRows * kRhMaxN / 4 / 256;  // float4 groups per lane (at N = kRhMaxN)
+  f32x4 v[PER][MAXS];
+  // buffer loads: the lane's element as voffset, the split as the uniform soffset -- no address
+  // registers per load, so all PER x MAXS loads stay in flight together (the host keeps the
+  // partials under 2^31 bytes)
+  const __amdgpu_buffer_rsrc_t pr =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(part), 0, (int)(splits * MN * 4), 0x00020000);
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int i = (int)threadIdx.x + 256 * u, rr = i / N4;
+    const int row = r0 + rr < M ? r0 + rr : M - 1;  // tail rows: a duplicate, not written
+    const uint32_t off = (uint32_t)(((int64_t)row * N + 4 * (i - rr * N4)) * 4);
+#pragma unroll
+    for (int k = 0; k < MAXS; ++k)
+      v[u][k] = __builtin_bit_cast(
+          f32x4, __builtin_amdgcn_raw_buffer_load_b128(pr, off, (int)((k < splits ? k : splits - 1) * MN * 4), 0));
+  }
+  __builtin_amdgcn_sched_barrier(0);  // every split load in flight before the first add
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int i = (int)threadIdx.x + 256 * u, rr = i / N4, c = 4 * (i - rr * N4);
+    if (i >= kRhRows * N4) break;
+    f32x4 sum = v[u][0];
+#pragma unroll
+    for (int k = 1; k < MAXS; ++k)
+      if (k < splits) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sum[j] = radd(sum[j], v[u][k][j]);
+      }
+    f32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = fc_relu(radd(sum[j], b1[c + j]));
+    hs[i] = o;
+    if (h1_out && r0 + rr < M) *reinterpret_cast<f32x4 *>(h1_out + (int64_t)(r0 + rr) * N + c) = o;
+  }
+  __syncthreads();
+  if (threadIdx.x >= 16 * kRhRows) return;  // (whole waves past the first)
+  const int l = threadIdx.x & 15, rr = threadIdx.x >> 4;
+  const int H = N / 2, cq = H / 64, A1 = A + 1;
+  const f32x4 *ha = hs + rr * N4 + l * cq, *hv = hs + rr * N4 + H / 4 + l * cq;
+  float acc[MAXA1];
+#pragma unroll
+  for (int a = 0; a < MAXA1; ++a) acc[a] = 0.0f;
+#pragma unroll 1
+  for (int k = 0; k < cq; ++k) {
+    const f32x4 xa = ha[k], xv = hv[k];
+    float4 w[MAXA1];
+#pragma unroll
+    for (int a = 0; a < MAXA1; ++a) {
+      const int ac = a < A1 ? a : A;  // past A: a duplicate row, unused
+      w[a] = reinterpret_cast<const float4 *>(ac < A ? wa2 + (int64_t)ac * H : wv2)[l * cq + k];
+    }
+#pragma unroll
+    for (int a = 0; a < MAXA1; ++a)
+      if (a < A1) {
+        const f32x4 x = a < A ? xa : xv;
+        const float4 ww = w[a];
+        acc[a] = radd(radd(radd(radd(acc[a], rmul(x[0], ww.x)), rmul(x[1], ww.y)), rmul(x[2], ww.z)), rmul(x[3], ww.w));
+      }
+  }
+#pragma unroll
+  for (int a = 0; a < MAXA1; ++a)
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) acc[a] = radd(acc[a], __shfl_xor(acc[a], o, 64));
+  if (l == 0 && r0 + rr < M) {
+    float *out = heads + (int64_t)(r0 + rr) * A1;
+#pragma unroll
+    for (int a = 0; a < MAXA1; ++a)
+      if (a <= A) out[a] = radd(acc[a], a < A ? ba2[a] : bv2[0]);
+  }
+}
+
 // r05: k_fc_reduce's workgroups (blocks [0, nred)) + the device-counted tail rows behind the M
 // fixed rows (k_linear_relu_rows' workgroups, blocks [nred, ...)) in one launch -- the actors'
 // counted FC1 (their terminal stacks: none in most steps) without a launch of its own
@@ -612,6 +700,42 @@ int rth_fc_x9_rows_upto(const float *x, int64_t ldx, int64_t M, int64_t n_max, c
                     const_cast<int *>(&nred), &x, &ldx, &r0, &n_max, &n_dev, &w, &Ki};
     RTH_HIP(hipLaunchKernel(fc_reduce_fn(splits, true), dim3((unsigned)(nred + nrows)), dim3(256), args, 0, s));
   }
+  return RTH_OK;
+}
+
+int rth_fc1_heads_supported(int64_t M, int64_t N, int64_t K, int32_t A) {
+  if (!rth_fc_x9_supported(M, N, K) || N > kRhMaxN || N % 128 || A < 1 || A + 1 > 8) return 0;
+  const int s = fc_plan((int)M, (int)N, (int)K).splits;
+  return s >= 2 && s <= 16 ? 1 : 0;
+}
+
+int rth_fc1_heads(const float *x, int64_t ldx, int64_t M, const float *w1, int64_t N, int64_t K, const float *b1,
+                  int32_t A, const float *const *fc2_params, float *heads, float *h1_out, void *workspace,
+                  void *stream) {
+  RTH_REQUIRE(x && w1 && b1 && fc2_params && heads && workspace, "rth_fc1_heads: NULL argument");
+  RTH_REQUIRE(rth_fc1_heads_supported(M, N, K, A), "rth_fc1_heads: shape %lld x %lld x %lld, A %d not built",
+              (long long)M, (long long)N, (long long)K, A);
+  RTH_REQUIRE((int64_t)fc_plan((int)M, (int)N, (int)K).splits * M * N * 4 < ((int64_t)1 << 31),
+              "rth_fc1_heads: split-K partials past 2 GiB");
+  for (int i = 0; i < 4; ++i) RTH_REQUIRE(fc2_params[i], "rth_fc1_heads: NULL FC2 parameter %d", i);
+  RTH_REQUIRE(ldx >= K && ldx % 4 == 0 &&
+                  ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w1) |
+                    reinterpret_cast<uintptr_t>(workspace) | reinterpret_cast<uintptr_t>(h1_out)) &
+                   15) == 0,
+              "rth_fc1_heads: row stride %lld or misaligned buffer", (long long)ldx);
+  const FcPlan p = fc_plan((int)M, (int)N, (int)K);
+  hipStream_t s = as_stream(stream);
+  float *part = static_cast<float *>(workspace);
+  fc_x9_launch(p, x, ldx, (int)M, w1, (int)N, (int)K, b1, 1, part, s);
+  RTH_LAUNCHED();
+  const dim3 grid((unsigned)((M + kRhRows - 1) / kRhRows));
+  if (p.splits <= 8)
+    hipLaunchKernelGGL((k_fc_reduce_heads<8, 8>), grid, dim3(256), 0, s, part, p.splits, (int)M, (int)N, b1, (int)A,
+                       fc2_params[0], fc2_params[1], fc2_params[2], fc2_params[3], heads, h1_out);
+  else
+    hipLaunchKernelGGL((k_fc_reduce_heads<16, 8>), grid, dim3(256), 0, s, part, p.splits, (int)M, (int)N, b1, (int)A,
+                       fc2_params[0], fc2_params[1], fc2_params[2], fc2_params[3], heads, h1_out);
+  RTH_LAUNCHED();
   return RTH_OK;
 }
 

@@ -27,6 +27,7 @@ import torch
 
 from . import _lib
 from ._lib import call, ctypes, ptr, stream_ptr
+from . import model
 from .model import fc1_relu, nchw_out
 from .replay import FrameStacks
 
@@ -181,8 +182,13 @@ def dueling_grads(solver, s0, a, r, s1, done, isw, q1t=None, td_acc=None, mid=No
             ys.append(y)
             h = y
         feat = h.view(n, -1)  # the (C, H, W) flatten of the NCHW output: a view
-        h1 = fc1_relu(feat, w1, b1, owner=net)
-        heads = net._heads_fc2(h1) if w2 is None else torch.addmm(b2, h1, w2.t())
+        h1 = heads = None
+        if w2 is None and model.FC1_HEADS:  # FC1's reduce + FC2 in one launch, h1 kept for the backward
+            h1 = torch.empty((feat.shape[0], w1.shape[0]), dtype=torch.float32, device=feat.device)
+            heads = net._fc1_heads(feat, w1, b1, h1_out=h1)
+        if heads is None:
+            h1 = fc1_relu(feat, w1, b1, owner=net)
+            heads = net._heads_fc2(h1) if w2 is None else torch.addmm(b2, h1, w2.t())
         if q1t is None:
             q1t = solver.target_heads(s1)
         q0 = heads[:B]

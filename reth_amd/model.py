@@ -160,6 +160,28 @@ class DQNNetwork(nn.Module):
         call("rth_heads_fc2", ptr(h), h.stride(0), h.shape[0], H, A, arr, ptr(out), stream_ptr())
         return out
 
+    def _fc1_heads(self, h, w1, b1, h1_out=None):
+        """FC1 -> FC2 of both branches in rth_fc1_heads (the x9 GEMM, then its split-K reduce +
+        bias + ReLU and the second layer in one launch, r06; bit-identical to rth_fc_x9 +
+        rth_heads_fc2) where built for the shape, else None.  h1_out (optional [n, 2H]) receives
+        relu(FC1) (the learner's backward reads it)"""
+        from ._lib import c_vp, call, lib, ptr, stream_ptr
+
+        if not (h.is_cuda and h.dim() == 2 and h.stride(1) == 1 and w1.is_contiguous() and self._fc2_inplace()):
+            return None
+        M, K = h.shape
+        N = w1.shape[0]
+        ps = self._head_params()[4:]
+        A, H = ps[0].shape
+        if N != 2 * H or not lib().rth_fc1_heads_supported(M, N, K, A):
+            return None
+        out = torch.empty((M, A + 1), dtype=torch.float32, device=h.device)
+        arr = (c_vp * 4)(*[p.data_ptr() for p in ps])
+        ws = _fc_workspace("rth_fc_x9", h.device, w1, M, N, K, self)
+        call("rth_fc1_heads", ptr(h), h.stride(0), M, ptr(w1), N, K, ptr(b1), A, arr, ptr(out),
+             ptr(h1_out) if h1_out is not None else None, ptr(ws), stream_ptr())
+        return out
+
     @torch.no_grad()
     def freeze_heads(self):
         """(re)build the cached head weights and packed conv weights IN PLACE (stable storage
@@ -212,6 +234,10 @@ class DQNNetwork(nn.Module):
             return self._heads_counted(h, w1, b1, n_dev, n_fixed, cache)
         if cache is not None or n_fixed is not None:
             raise ValueError("forward_heads(cache= / n_fixed=) needs n_dev and the in-place second layer")
+        if w2 is None and FC1_HEADS and not (torch.is_grad_enabled() and (h.requires_grad or w1.requires_grad)):
+            out = self._fc1_heads(h, w1, b1)  # inference: FC1 -> FC2 without the h1 launch boundary
+            if out is not None:
+                return out
         h = _LinearReLU.apply(h, w1, b1, self)
         if w2 is None:  # the second layer from the branch parameters in place
             return self._heads_fc2(h)
@@ -442,6 +468,11 @@ class _MergeHeads(torch.autograd.Function):
 # x9 it is 1.1x.  Cost in the loop: 0.516 -> 0.520 ms/step (interleaved, 3 rounds,
 # profiles/r06/ab_log.txt).
 _FC_WS = {}
+
+
+# FC1_HEADS -- FC1's split-K reduce and FC2 in one launch (rth_fc1_heads) wherever the heads are
+# computed without autograd: the target pass and the learner's forward (r06); tests patch it
+FC1_HEADS = True
 
 
 def _fc_workspace(fn, device, w, M, N, K, owner=None):

@@ -127,3 +127,37 @@ def test_fc_x9_rows_upto_matches_two_launches(dev, count):
     assert not torch.isnan(ys[0][:live]).any() and torch.isnan(ys[0][live:]).all()
     want = torch.relu(x[:live].double() @ w.double().t() + b.double())
     assert (ys[0][:live].double() - want).abs().max().item() < 1e-4
+
+
+@pytest.mark.parametrize("M,A", [(512, 6), (1024, 6), (256, 4), (2048, 7), (512, 1)])
+def test_fc1_heads_matches_two_launches(dev, M, A):
+    """r06 rth_fc1_heads (the x9 GEMM, then its split-K reduce + bias + ReLU and the second layer
+    of both dueling branches in one launch): heads and h1 bit-identical to rth_fc_x9 +
+    rth_heads_fc2; run-to-run identical; shapes it does not build are refused"""
+    from reth_amd import _lib
+
+    N, K, H = 512, 3136, 256
+    g = torch.Generator(device=dev).manual_seed(M + A)
+    x = torch.randn((M, K), device=dev, generator=g)
+    w1 = torch.randn((N, K), device=dev, generator=g) * 0.02
+    b1 = torch.randn(N, device=dev, generator=g) * 0.1
+    ps = [torch.randn((A, H), device=dev, generator=g) * 0.05, torch.randn((1, H), device=dev, generator=g) * 0.05,
+          torch.randn(A, device=dev, generator=g) * 0.1, torch.randn(1, device=dev, generator=g) * 0.1]
+    arr = (_lib.c_vp * 4)(*[p.data_ptr() for p in ps])
+    assert _lib.lib().rth_fc1_heads_supported(M, N, K, A) == 1
+    h1 = _run(dev, x, w1, b1, True)
+    want = torch.full((M, A + 1), float("nan"), device=dev)
+    _lib.call("rth_heads_fc2", h1.data_ptr(), N, M, H, A, arr, want.data_ptr(), _lib.stream_ptr())
+    ws = torch.empty(max(_lib.lib().rth_fc_x9_workspace(M, N, K), 16) // 4, device=dev)
+    outs = []
+    for keep_h1 in (True, False, True):
+        heads = torch.full((M, A + 1), float("nan"), device=dev)
+        h1o = torch.full((M, N), float("nan"), device=dev) if keep_h1 else None
+        _lib.call("rth_fc1_heads", x.data_ptr(), K, M, w1.data_ptr(), N, K, b1.data_ptr(), A, arr, heads.data_ptr(),
+                  h1o.data_ptr() if keep_h1 else None, ws.data_ptr(), _lib.stream_ptr())
+        assert torch.equal(heads, want)
+        if keep_h1:
+            assert torch.equal(h1o, h1)
+        outs.append(heads)
+    assert _lib.lib().rth_fc1_heads_supported(M, N, K, 8) == 0  # A + 1 > 8
+    assert _lib.lib().rth_fc1_heads_supported(M, 1024, K, A) == 0  # N > 512

@@ -33,6 +33,13 @@ for what in "$@"; do
     tests) step gpu_tests 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py ;;
+    dp8)  # 8 ranks on one GPU over gloo: bench.py's multi-rank path and its teardown (shutdown())
+      RTH_SHARE_GPU=1 RTH_DIST_BACKEND=gloo step dp8_gloo_rehearsal 900 python -m torch.distributed.run --nnodes=1 \
+          --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 8 --faithful --steps 20 \
+          --warmup 5 --no-cpu-baseline --no-sweep ;;
+    dp2)  # the driver's N = 2 command shape (weak scaling: 256 actors, 1 M rows, B = 512 per rank), both ranks on one GPU
+      RTH_SHARE_GPU=1 RTH_DIST_BACKEND=gloo step dp2_gloo_rehearsal 900 python -m torch.distributed.run --nnodes=1 \
+          --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29518 bench.py --gpus 2 --steps 20 --warmup 5 ;;
     driver) step bench_driver 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     breakout) step breakout 600 python bench.py --workload breakout ;;
     span) RTH_BENCH_SPAN=1 step span 300 python bench.py --steps 300 --warmup 20 --no-cpu-baseline --no-sweep ;;

@@ -4,9 +4,10 @@ Reference: reth/reth/algorithm/dqn/dqn_solver.py:14-143 (and algorithm/algorithm
 
 The Q-network's forward runs on hand-written HIP kernels (model.py: the conv torso in
 rth_conv_bias_relu, FC1 in rth_fc_x9, FC2 in rth_heads_fc2); the dueling Nature-DQN's learner
-update is the explicit kernel sequence of fused_learner.py (HIP data gradients, conv1's weight
-gradient, the fused TD / FC2 backward; FC1's backward GEMMs and the conv2 / conv3 weight
-gradients on hipBLASLt / MIOpen), other networks go through torch.autograd.  The TD error,
+update is the explicit kernel sequence of fused_learner.py (HIP data gradients, HIP weight
+gradients of every conv layer, the fused TD / FC2 backward, clip + Adam with the norm from the
+backward; only FC1's two backward GEMMs run on hipBLASLt), other networks go through
+torch.autograd.  The TD error,
 double-Q target, Huber loss, IS weighting, mean, |td| and the gradient with respect to Q(s0)
 are ONE HIP kernel (rth_td_huber) wrapped as an autograd Function on the autograd path, so
   * the loss' backward starts from the kernel's d(loss)/d(Q(s0)) -- no chain of small torch

@@ -8,10 +8,11 @@ after each (tests/golden/make_golden.py gen_dqn_full).
 
 What runs here is exactly what the bench replays: an ApexDQN (HIP graphs, uint8 batch
 slots, the explicit gradient pass of fused_learner.py -- the HIP conv forwards (conv1 bf16x3,
-conv2 fp32 MFMA, conv3 x9), FC1's forward on the exact-split rth_fc_x9, the fused TD / Huber /
-FC2 backward, FC1's two backward GEMMs and conv2 / conv3 weight gradients on hipBLASLt /
-MIOpen, the x9 data gradients, conv1's bf16x3 weight gradient from the stacks with the
-deferred bias gradients, rth_clip_adam) is built with the reference's seed, run until its
+conv2 fp32 MFMA, conv3 x9), FC1's forward on the exact-split rth_fc_x9 with FC2 in its reduce
+launch, the fused TD / Huber / FC2 backward, FC1's two backward GEMMs on hipBLASLt, the x9 data
+gradients, the fp32 conv2 / conv3 weight gradients, conv1's bf16x3 weight gradient from the
+stacks whose reduce launch also finishes the deferred bias / weight gradients and the norm
+partials, then Adam) is built with the reference's seed, run until its
 graphs are captured, then reset to the initial weights / zero Adam state; the golden batch is
 written into a learner batch slot and the captured learner graph is replayed twice.
 Tolerances: the first update's |td| within the north-star 1e-5 of the reference's fp32 run
